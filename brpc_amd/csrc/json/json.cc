@@ -1,0 +1,391 @@
+#include "json/json.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+namespace mrpc {
+namespace json {
+
+int64_t Value::as_int() const {
+    switch (_type) {
+    case INT: return _i;
+    case UINT: return (int64_t)_u;
+    case DOUBLE: return (int64_t)_d;
+    case BOOL: return _b;
+    case STRING: return strtoll(_s.c_str(), nullptr, 10);
+    default: return 0;
+    }
+}
+
+uint64_t Value::as_uint() const {
+    switch (_type) {
+    case INT: return (uint64_t)_i;
+    case UINT: return _u;
+    case DOUBLE: return (uint64_t)_d;
+    case BOOL: return _b;
+    case STRING: return strtoull(_s.c_str(), nullptr, 10);
+    default: return 0;
+    }
+}
+
+double Value::as_double() const {
+    switch (_type) {
+    case INT: return (double)_i;
+    case UINT: return (double)_u;
+    case DOUBLE: return _d;
+    case BOOL: return _b;
+    case STRING: return strtod(_s.c_str(), nullptr);
+    default: return 0;
+    }
+}
+
+const Value* Value::find(const std::string& key) const {
+    if (_type != OBJECT) return nullptr;
+    for (auto& kv : _obj) {
+        if (kv.first == key) return &kv.second;
+    }
+    return nullptr;
+}
+
+Value* Value::find(const std::string& key) {
+    if (_type != OBJECT) return nullptr;
+    for (auto& kv : _obj) {
+        if (kv.first == key) return &kv.second;
+    }
+    return nullptr;
+}
+
+Value& Value::set(const std::string& key, Value v) {
+    _type = OBJECT;
+    Value* e = find(key);
+    if (e) {
+        *e = std::move(v);
+        return *e;
+    }
+    _obj.emplace_back(key, std::move(v));
+    return _obj.back().second;
+}
+
+Value& Value::operator[](const std::string& key) {
+    _type = OBJECT;
+    Value* e = find(key);
+    if (e) return *e;
+    _obj.emplace_back(key, Value());
+    return _obj.back().second;
+}
+
+void EscapeString(const std::string& s, std::string* out) {
+    out->push_back('"');
+    for (unsigned char c : s) {
+        switch (c) {
+        case '"': *out += "\\\""; break;
+        case '\\': *out += "\\\\"; break;
+        case '\n': *out += "\\n"; break;
+        case '\r': *out += "\\r"; break;
+        case '\t': *out += "\\t"; break;
+        case '\b': *out += "\\b"; break;
+        case '\f': *out += "\\f"; break;
+        default:
+            if (c < 0x20) {
+                char b[8];
+                snprintf(b, sizeof(b), "\\u%04x", c);
+                *out += b;
+            } else {
+                out->push_back((char)c);
+            }
+        }
+    }
+    out->push_back('"');
+}
+
+void Value::write(std::string* out, bool pretty, int indent) const {
+    char buf[64];
+    auto nl = [&](int ind) {
+        if (!pretty) return;
+        out->push_back('\n');
+        out->append(ind * 2, ' ');
+    };
+    switch (_type) {
+    case NUL: *out += "null"; break;
+    case BOOL: *out += _b ? "true" : "false"; break;
+    case INT: snprintf(buf, sizeof(buf), "%lld", (long long)_i); *out += buf; break;
+    case UINT: snprintf(buf, sizeof(buf), "%llu", (unsigned long long)_u); *out += buf; break;
+    case DOUBLE:
+        if (std::isnan(_d) || std::isinf(_d)) {
+            *out += std::isnan(_d) ? "\"NaN\"" : (_d > 0 ? "\"Infinity\"" : "\"-Infinity\"");
+        } else {
+            snprintf(buf, sizeof(buf), "%.17g", _d);
+            *out += buf;
+        }
+        break;
+    case STRING: EscapeString(_s, out); break;
+    case ARRAY:
+        out->push_back('[');
+        for (size_t i = 0; i < _arr.size(); ++i) {
+            if (i) out->push_back(',');
+            nl(indent + 1);
+            _arr[i].write(out, pretty, indent + 1);
+        }
+        if (!_arr.empty()) nl(indent);
+        out->push_back(']');
+        break;
+    case OBJECT:
+        out->push_back('{');
+        for (size_t i = 0; i < _obj.size(); ++i) {
+            if (i) out->push_back(',');
+            nl(indent + 1);
+            EscapeString(_obj[i].first, out);
+            out->push_back(':');
+            if (pretty) out->push_back(' ');
+            _obj[i].second.write(out, pretty, indent + 1);
+        }
+        if (!_obj.empty()) nl(indent);
+        out->push_back('}');
+        break;
+    }
+}
+
+std::string Value::ToString(bool pretty) const {
+    std::string s;
+    write(&s, pretty, 0);
+    return s;
+}
+
+namespace {
+class Reader {
+public:
+    Reader(const char* p, size_t n) : _p(p), _end(p + n), _begin(p) {}
+    bool parse(Value* v, std::string* err) {
+        skip();
+        if (!value(v, 0)) {
+            if (err) *err = "invalid json at offset " + std::to_string(_p - _begin) + ": " + _err;
+            return false;
+        }
+        skip();
+        if (_p != _end) {
+            if (err) *err = "trailing characters at offset " + std::to_string(_p - _begin);
+            return false;
+        }
+        return true;
+    }
+
+private:
+    void skip() {
+        while (_p < _end && (*_p == ' ' || *_p == '\t' || *_p == '\n' || *_p == '\r')) ++_p;
+    }
+    bool fail(const char* m) {
+        _err = m;
+        return false;
+    }
+    bool value(Value* v, int depth) {
+        if (depth > 200) return fail("nesting too deep");
+        if (_p >= _end) return fail("unexpected end");
+        switch (*_p) {
+        case '{': return object(v, depth);
+        case '[': return array(v, depth);
+        case '"': {
+            std::string s;
+            if (!string(&s)) return false;
+            *v = Value(s);
+            return true;
+        }
+        case 't':
+            if (_end - _p >= 4 && memcmp(_p, "true", 4) == 0) {
+                _p += 4;
+                *v = Value(true);
+                return true;
+            }
+            return fail("bad literal");
+        case 'f':
+            if (_end - _p >= 5 && memcmp(_p, "false", 5) == 0) {
+                _p += 5;
+                *v = Value(false);
+                return true;
+            }
+            return fail("bad literal");
+        case 'n':
+            if (_end - _p >= 4 && memcmp(_p, "null", 4) == 0) {
+                _p += 4;
+                *v = Value();
+                return true;
+            }
+            return fail("bad literal");
+        default: return number(v);
+        }
+    }
+    bool number(Value* v) {
+        const char* b = _p;
+        if (_p < _end && *_p == '-') ++_p;
+        if (_p >= _end || !isdigit((unsigned char)*_p)) return fail("bad number");
+        bool is_float = false;
+        while (_p < _end && (isdigit((unsigned char)*_p) || *_p == '.' || *_p == 'e' || *_p == 'E' ||
+                             ((*_p == '+' || *_p == '-') && (_p[-1] == 'e' || _p[-1] == 'E')))) {
+            if (*_p == '.' || *_p == 'e' || *_p == 'E') is_float = true;
+            ++_p;
+        }
+        std::string s(b, _p - b);
+        if (!is_float) {
+            errno = 0;
+            if (s[0] == '-') {
+                long long x = strtoll(s.c_str(), nullptr, 10);
+                if (errno == 0) {
+                    *v = Value((int64_t)x);
+                    return true;
+                }
+            } else {
+                unsigned long long x = strtoull(s.c_str(), nullptr, 10);
+                if (errno == 0) {
+                    if (x <= (unsigned long long)INT64_MAX) *v = Value((int64_t)x);
+                    else *v = Value((uint64_t)x);
+                    return true;
+                }
+            }
+        }
+        *v = Value(strtod(s.c_str(), nullptr));
+        return true;
+    }
+    static void put_utf8(std::string* s, uint32_t cp) {
+        if (cp < 0x80) {
+            s->push_back((char)cp);
+        } else if (cp < 0x800) {
+            s->push_back((char)(0xC0 | (cp >> 6)));
+            s->push_back((char)(0x80 | (cp & 0x3F)));
+        } else if (cp < 0x10000) {
+            s->push_back((char)(0xE0 | (cp >> 12)));
+            s->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            s->push_back((char)(0x80 | (cp & 0x3F)));
+        } else {
+            s->push_back((char)(0xF0 | (cp >> 18)));
+            s->push_back((char)(0x80 | ((cp >> 12) & 0x3F)));
+            s->push_back((char)(0x80 | ((cp >> 6) & 0x3F)));
+            s->push_back((char)(0x80 | (cp & 0x3F)));
+        }
+    }
+    bool hex4(uint32_t* out) {
+        if (_end - _p < 4) return fail("bad unicode escape");
+        uint32_t v = 0;
+        for (int i = 0; i < 4; ++i) {
+            char c = _p[i];
+            v <<= 4;
+            if (c >= '0' && c <= '9') v |= c - '0';
+            else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+            else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+            else return fail("bad unicode escape");
+        }
+        _p += 4;
+        *out = v;
+        return true;
+    }
+    bool string(std::string* s) {
+        ++_p;  // opening quote
+        while (_p < _end && *_p != '"') {
+            char c = *_p++;
+            if (c != '\\') {
+                s->push_back(c);
+                continue;
+            }
+            if (_p >= _end) return fail("bad escape");
+            char e = *_p++;
+            switch (e) {
+            case '"': s->push_back('"'); break;
+            case '\\': s->push_back('\\'); break;
+            case '/': s->push_back('/'); break;
+            case 'b': s->push_back('\b'); break;
+            case 'f': s->push_back('\f'); break;
+            case 'n': s->push_back('\n'); break;
+            case 'r': s->push_back('\r'); break;
+            case 't': s->push_back('\t'); break;
+            case 'u': {
+                uint32_t cp;
+                if (!hex4(&cp)) return false;
+                if (cp >= 0xD800 && cp < 0xDC00 && _end - _p >= 6 && _p[0] == '\\' && _p[1] == 'u') {
+                    _p += 2;
+                    uint32_t lo;
+                    if (!hex4(&lo)) return false;
+                    cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+                }
+                put_utf8(s, cp);
+                break;
+            }
+            default: return fail("bad escape");
+            }
+        }
+        if (_p >= _end) return fail("unterminated string");
+        ++_p;
+        return true;
+    }
+    bool array(Value* v, int depth) {
+        ++_p;
+        *v = Value::Array();
+        skip();
+        if (_p < _end && *_p == ']') {
+            ++_p;
+            return true;
+        }
+        for (;;) {
+            Value e;
+            skip();
+            if (!value(&e, depth + 1)) return false;
+            v->push_back(std::move(e));
+            skip();
+            if (_p < _end && *_p == ',') {
+                ++_p;
+                continue;
+            }
+            if (_p < _end && *_p == ']') {
+                ++_p;
+                return true;
+            }
+            return fail("expected , or ]");
+        }
+    }
+    bool object(Value* v, int depth) {
+        ++_p;
+        *v = Value::Object();
+        skip();
+        if (_p < _end && *_p == '}') {
+            ++_p;
+            return true;
+        }
+        for (;;) {
+            skip();
+            if (_p >= _end || *_p != '"') return fail("expected key");
+            std::string key;
+            if (!string(&key)) return false;
+            skip();
+            if (_p >= _end || *_p != ':') return fail("expected :");
+            ++_p;
+            skip();
+            Value e;
+            if (!value(&e, depth + 1)) return false;
+            v->set(key, std::move(e));
+            skip();
+            if (_p < _end && *_p == ',') {
+                ++_p;
+                continue;
+            }
+            if (_p < _end && *_p == '}') {
+                ++_p;
+                return true;
+            }
+            return fail("expected , or }");
+        }
+    }
+    const char* _p;
+    const char* _end;
+    const char* _begin;
+    std::string _err;
+};
+}  // namespace
+
+bool Parse(const char* data, size_t n, Value* out, std::string* error) {
+    Reader r(data, n);
+    return r.parse(out, error);
+}
+
+bool Parse(const std::string& text, Value* out, std::string* error) { return Parse(text.data(), text.size(), out, error); }
+
+}  // namespace json
+}  // namespace mrpc

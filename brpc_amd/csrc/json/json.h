@@ -1,0 +1,84 @@
+// Small JSON DOM: parse / serialize (rapidjson is not available; the
+// reference's json2pb builds on rapidjson, src/json2pb). Used by json2pb,
+// naming services and builtin pages.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace mrpc {
+namespace json {
+
+class Value {
+public:
+    enum Type { NUL, BOOL, INT, UINT, DOUBLE, STRING, ARRAY, OBJECT };
+    Value() : _type(NUL) {}
+    explicit Value(bool b) : _type(BOOL), _b(b) {}
+    explicit Value(int64_t i) : _type(INT), _i(i) {}
+    explicit Value(uint64_t u) : _type(UINT), _u(u) {}
+    explicit Value(int i) : _type(INT), _i(i) {}
+    explicit Value(double d) : _type(DOUBLE), _d(d) {}
+    explicit Value(const std::string& s) : _type(STRING), _s(s) {}
+    explicit Value(const char* s) : _type(STRING), _s(s) {}
+    static Value Array() { Value v; v._type = ARRAY; return v; }
+    static Value Object() { Value v; v._type = OBJECT; return v; }
+
+    Type type() const { return _type; }
+    bool is_null() const { return _type == NUL; }
+    bool is_bool() const { return _type == BOOL; }
+    bool is_number() const { return _type == INT || _type == UINT || _type == DOUBLE; }
+    bool is_int() const { return _type == INT || _type == UINT; }
+    bool is_string() const { return _type == STRING; }
+    bool is_array() const { return _type == ARRAY; }
+    bool is_object() const { return _type == OBJECT; }
+
+    bool as_bool() const { return _type == BOOL ? _b : (is_number() && as_double() != 0); }
+    int64_t as_int() const;
+    uint64_t as_uint() const;
+    double as_double() const;
+    const std::string& as_string() const { return _s; }
+    std::string& mutable_string() { return _s; }
+    bool uint_overflows_int() const { return _type == UINT && _u > (uint64_t)INT64_MAX; }
+
+    // arrays
+    const std::vector<Value>& array() const { return _arr; }
+    std::vector<Value>& mutable_array() { _type = ARRAY; return _arr; }
+    Value& push_back(Value v) {
+        _type = ARRAY;
+        _arr.push_back(std::move(v));
+        return _arr.back();
+    }
+    size_t size() const { return _type == ARRAY ? _arr.size() : _obj.size(); }
+
+    // objects (insertion ordered)
+    const std::vector<std::pair<std::string, Value>>& members() const { return _obj; }
+    const Value* find(const std::string& key) const;
+    Value* find(const std::string& key);
+    Value& set(const std::string& key, Value v);
+    Value& operator[](const std::string& key);
+
+    std::string ToString(bool pretty = false) const;
+
+private:
+    void write(std::string* out, bool pretty, int indent) const;
+    Type _type;
+    bool _b = false;
+    int64_t _i = 0;
+    uint64_t _u = 0;
+    double _d = 0;
+    std::string _s;
+    std::vector<Value> _arr;
+    std::vector<std::pair<std::string, Value>> _obj;
+};
+
+// Returns false and sets *error on malformed input.
+bool Parse(const std::string& text, Value* out, std::string* error = nullptr);
+bool Parse(const char* data, size_t n, Value* out, std::string* error = nullptr);
+void EscapeString(const std::string& s, std::string* out);
+
+}  // namespace json
+}  // namespace mrpc

@@ -1,0 +1,143 @@
+#include "net/event_dispatcher.h"
+
+#include <fcntl.h>
+#include <sys/epoll.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <mutex>
+
+#include "base/flags.h"
+#include "base/logging.h"
+#include "fiber/fiber.h"
+
+DEFINE_int32(event_dispatcher_num, 1, "Number of event dispatchers");
+
+namespace mrpc {
+
+EventDispatcher::EventDispatcher() : _epfd(-1), _stop(false), _tid(0) {
+    _wakeup_fds[0] = _wakeup_fds[1] = -1;
+    _epfd = epoll_create1(EPOLL_CLOEXEC);
+    if (_epfd < 0) PLOG(FATAL) << "epoll_create1";
+}
+
+EventDispatcher::~EventDispatcher() {
+    Stop();
+    Join();
+    if (_epfd >= 0) close(_epfd);
+}
+
+int EventDispatcher::Start() {
+    if (_tid) return 0;
+    fiber::Attr attr = fiber::ATTR_NORMAL;
+    // The dispatcher blocks its worker in epoll_wait; run it as a normal
+    // fiber so that start_urgent() hand-offs work as described above.
+    if (fiber::start_background(&_tid, &attr, RunThis, this) != 0) {
+        LOG(FATAL) << "Fail to start EventDispatcher fiber";
+        return -1;
+    }
+    return 0;
+}
+
+bool EventDispatcher::Running() const { return !_stop && _tid != 0; }
+
+void EventDispatcher::Stop() {
+    _stop = true;
+    if (_epfd >= 0 && _wakeup_fds[1] < 0) {
+        if (pipe2(_wakeup_fds, O_CLOEXEC) == 0) {
+            epoll_event evt;
+            evt.events = EPOLLOUT;
+            evt.data.u64 = INVALID_SOCKET_ID;
+            epoll_ctl(_epfd, EPOLL_CTL_ADD, _wakeup_fds[1], &evt);
+        }
+    }
+}
+
+void EventDispatcher::Join() {
+    if (_tid) {
+        fiber::join(_tid);
+        _tid = 0;
+    }
+}
+
+int EventDispatcher::AddConsumer(SocketId socket_id, int fd) {
+    epoll_event evt;
+    evt.events = EPOLLIN | EPOLLET | EPOLLRDHUP;
+    evt.data.u64 = socket_id;
+    return epoll_ctl(_epfd, EPOLL_CTL_ADD, fd, &evt);
+}
+
+int EventDispatcher::RemoveConsumer(int fd) {
+    if (fd < 0) return -1;
+    return epoll_ctl(_epfd, EPOLL_CTL_DEL, fd, nullptr);
+}
+
+int EventDispatcher::AddEpollOut(SocketId socket_id, int fd, bool pollin) {
+    epoll_event evt;
+    evt.data.u64 = socket_id;
+    evt.events = EPOLLOUT | EPOLLET;
+    if (pollin) {
+        evt.events |= EPOLLIN | EPOLLRDHUP;
+        return epoll_ctl(_epfd, EPOLL_CTL_MOD, fd, &evt);
+    }
+    if (epoll_ctl(_epfd, EPOLL_CTL_ADD, fd, &evt) < 0 && errno != EEXIST) return -1;
+    return 0;
+}
+
+int EventDispatcher::RemoveEpollOut(SocketId socket_id, int fd, bool pollin) {
+    if (pollin) {
+        epoll_event evt;
+        evt.data.u64 = socket_id;
+        evt.events = EPOLLIN | EPOLLET | EPOLLRDHUP;
+        return epoll_ctl(_epfd, EPOLL_CTL_MOD, fd, &evt);
+    }
+    return epoll_ctl(_epfd, EPOLL_CTL_DEL, fd, nullptr);
+}
+
+void* EventDispatcher::RunThis(void* arg) {
+    static_cast<EventDispatcher*>(arg)->Run();
+    return nullptr;
+}
+
+void EventDispatcher::Run() {
+    epoll_event e[32];
+    while (!_stop) {
+        const int n = epoll_wait(_epfd, e, 32, -1);
+        if (_stop) break;
+        if (n < 0) {
+            if (errno == EINTR) continue;
+            PLOG(ERROR) << "epoll_wait";
+            break;
+        }
+        for (int i = 0; i < n; ++i) {
+            if (e[i].data.u64 == INVALID_SOCKET_ID) continue;
+            if (e[i].events & (EPOLLIN | EPOLLERR | EPOLLHUP | EPOLLRDHUP)) {
+                Socket::StartInputEvent(e[i].data.u64, e[i].events);
+            }
+        }
+        for (int i = 0; i < n; ++i) {
+            if (e[i].data.u64 == INVALID_SOCKET_ID) continue;
+            if (e[i].events & (EPOLLOUT | EPOLLERR | EPOLLHUP)) Socket::HandleEpollOut(e[i].data.u64);
+        }
+    }
+}
+
+namespace {
+std::once_flag g_disp_once;
+EventDispatcher* g_disps = nullptr;
+int g_ndisp = 1;
+}  // namespace
+
+int GetEventDispatcherNum() { return g_ndisp; }
+
+EventDispatcher& GetGlobalEventDispatcher(int fd) {
+    std::call_once(g_disp_once, [] {
+        g_ndisp = FLAGS_event_dispatcher_num > 0 ? FLAGS_event_dispatcher_num : 1;
+        g_disps = new EventDispatcher[g_ndisp];
+        for (int i = 0; i < g_ndisp; ++i) g_disps[i].Start();
+    });
+    if (g_ndisp == 1) return g_disps[0];
+    return g_disps[(unsigned)fd % (unsigned)g_ndisp];
+}
+
+}  // namespace mrpc

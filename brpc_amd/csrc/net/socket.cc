@@ -1,0 +1,834 @@
+#include "net/socket.h"
+
+#include <fcntl.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdarg>
+#include <vector>
+
+#include "base/flags.h"
+#include "base/logging.h"
+#include "base/pool.h"
+#include "base/time.h"
+#include "base/util.h"
+#include "fiber/butex.h"
+#include "net/event_dispatcher.h"
+#include "rpc/errno.h"
+
+DEFINE_int64(socket_max_unwritten_bytes, 64 * 1024 * 1024,
+             "Max unwritten bytes in each socket; writes beyond fail with EOVERCROWDED");
+DEFINE_int32(connect_timeout_ms_default, 200, "default timeout of lazily connecting sockets");
+DEFINE_int32(socket_recv_buffer_size, -1, "SO_RCVBUF of sockets if positive");
+DEFINE_int32(socket_send_buffer_size, -1, "SO_SNDBUF of sockets if positive");
+DEFINE_int32(max_connection_pool_size, 100, "max pooled connections to one endpoint");
+
+namespace mrpc {
+
+struct Socket::WriteRequest {
+    Buf data;
+    WriteRequest* next = nullptr;
+    fiber::CallId id_wait = fiber::INVALID_CALL_ID;
+    Socket* socket = nullptr;
+};
+
+static Socket::WriteRequest* const UNCONNECTED = (Socket::WriteRequest*)(intptr_t)-1;
+
+struct Socket::SharedPart {
+    std::mutex mu;
+    std::vector<SocketId> pool;  // free pooled sub-sockets
+    std::vector<fiber::CallId> id_wait_list;
+    size_t last_compact = 0;
+    std::vector<std::function<void()>> failure_callbacks;
+};
+
+void Socket::AddFailureCallback(std::function<void()> cb) {
+    std::shared_ptr<SharedPart> sp = _shared;
+    if (Failed() || !sp) {
+        cb();
+        return;
+    }
+    std::lock_guard<std::mutex> g(sp->mu);
+    sp->failure_callbacks.push_back(std::move(cb));
+}
+
+static std::atomic<int64_t> g_nsocket{0};
+
+static inline uint64_t make_vref(uint32_t ver, uint32_t nref) { return ((uint64_t)ver << 32) | nref; }
+static inline uint32_t vref_ver(uint64_t v) { return (uint32_t)(v >> 32); }
+static inline int32_t vref_nref(uint64_t v) { return (int32_t)(uint32_t)v; }
+static inline SocketId make_sid(uint32_t slot, uint32_t ver) { return ((uint64_t)slot << 32) | ver; }
+static inline uint32_t sid_slot(SocketId id) { return (uint32_t)(id >> 32); }
+static inline uint32_t sid_ver(SocketId id) { return (uint32_t)id; }
+
+SocketUniquePtr& SocketUniquePtr::operator=(SocketUniquePtr&& o) noexcept {
+    if (this != &o) {
+        reset(o._s);
+        o._s = nullptr;
+    }
+    return *this;
+}
+
+void SocketUniquePtr::reset(Socket* s) {
+    Socket* old = _s;
+    _s = s;
+    if (old) old->Dereference();
+}
+
+Socket::Socket()
+    : _versioned_ref(0),
+      _this_id(INVALID_SOCKET_ID),
+      _fd(-1),
+      _user(nullptr),
+      _on_edge_triggered_events(nullptr),
+      _health_check_interval_s(-1),
+      _connect_lazily(false),
+      _nevent(0),
+      _write_head(nullptr),
+      _unwritten_bytes(0),
+      _epollout_butex(fiber::butex_create()),
+      _last_active_us(0),
+      _error_code(0),
+      _auth_error(0),
+      _auth_state(0),
+      _auth_butex(fiber::butex_create()),
+      _main_socket_id(INVALID_SOCKET_ID),
+      _recycle_flag(false),
+      _hc_started(false) {}
+
+Socket::~Socket() {}
+
+int64_t Socket::nsocket() { return g_nsocket.load(std::memory_order_relaxed); }
+
+int Socket::ResetFileDescriptor(int fd) {
+    _fd.store(fd, std::memory_order_release);
+    if (fd < 0) return 0;
+    make_non_blocking(fd);
+    make_close_on_exec(fd);
+    if (!_remote_side.is_unix()) make_no_delay(fd);
+    if (FLAGS_socket_send_buffer_size > 0) {
+        int v = FLAGS_socket_send_buffer_size;
+        setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &v, sizeof(v));
+    }
+    if (FLAGS_socket_recv_buffer_size > 0) {
+        int v = FLAGS_socket_recv_buffer_size;
+        setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &v, sizeof(v));
+    }
+    get_local_side(fd, &_local_side);
+    if (_on_edge_triggered_events) {
+        if (GetGlobalEventDispatcher(fd).AddConsumer(_this_id, fd) != 0) {
+            PLOG(ERROR) << "Fail to add consumer fd=" << fd;
+            return -1;
+        }
+    }
+    return 0;
+}
+
+int Socket::Create(const SocketOptions& opt, SocketId* id) {
+    uint32_t slot;
+    Socket* m = get_resource<Socket>(&slot);
+    if (!m) return -1;
+    const uint32_t ver = vref_ver(m->_versioned_ref.load(std::memory_order_relaxed));
+    m->_this_id = make_sid(slot, ver);
+    m->_remote_side = opt.remote_side;
+    m->_local_side = EndPoint();
+    m->_user = opt.user;
+    m->_on_edge_triggered_events = opt.on_edge_triggered_events;
+    m->_conn = opt.conn;
+    m->_health_check_interval_s = opt.health_check_interval_s;
+    m->_connect_lazily = opt.connect_lazily;
+    m->_nevent.store(0, std::memory_order_relaxed);
+    m->_write_head.store(nullptr, std::memory_order_relaxed);
+    m->_unwritten_bytes.store(0, std::memory_order_relaxed);
+    m->_last_active_us.store(monotonic_us(), std::memory_order_relaxed);
+    m->_error_code = 0;
+    m->_error_text.clear();
+    m->_preferred_index = -1;
+    m->_parsing_context = nullptr;
+    m->_parsing_context_deleter = nullptr;
+    m->_avg_msg_size = 0;
+    m->_server_verified.store(false);
+    m->_auth_error.store(0);
+    m->_auth_state.store(0);
+    m->_main_socket_id = INVALID_SOCKET_ID;
+    m->_shared = std::make_shared<SharedPart>();
+    m->_recycle_flag.store(false);
+    m->_hc_started.store(false);
+    m->ninflight_health_check = 0;
+    m->in_bytes = m->out_bytes = m->in_messages = m->out_messages = 0;
+    {
+        std::lock_guard<std::mutex> g(m->_mu);
+        m->_transport.reset();
+    }
+    // One reference held until SetFailed().
+    m->_versioned_ref.store(make_vref(ver, 1), std::memory_order_release);
+    if (m->ResetFileDescriptor(opt.fd) != 0) {
+        const int saved = errno;
+        m->SetFailed(saved, "fail to register fd");
+        return -1;
+    }
+    g_nsocket.fetch_add(1, std::memory_order_relaxed);
+    *id = m->_this_id;
+    return 0;
+}
+
+int Socket::Address(SocketId id, SocketUniquePtr* ptr) {
+    Socket* m = address_resource<Socket>(sid_slot(id));
+    if (!m) return -1;
+    const uint64_t vref1 = m->_versioned_ref.fetch_add(1, std::memory_order_acquire);
+    if (vref_ver(vref1) == sid_ver(id)) {
+        ptr->reset(m);
+        return 0;
+    }
+    const uint64_t vref2 = m->_versioned_ref.fetch_sub(1, std::memory_order_release);
+    const int32_t nref = vref_nref(vref2);
+    if (nref > 1) return -1;
+    if (nref == 1) {
+        const uint32_t ver2 = vref_ver(vref2);
+        if (ver2 & 1) {
+            uint64_t expected = vref2 - 1;
+            if (m->_versioned_ref.compare_exchange_strong(expected, make_vref(ver2 + 1, 0), std::memory_order_acquire)) {
+                m->OnRecycle();
+                return_resource<Socket>(sid_slot(id));
+            }
+        }
+    }
+    return -1;
+}
+
+int Socket::AddressFailedAsWell(SocketId id, SocketUniquePtr* ptr) {
+    Socket* m = address_resource<Socket>(sid_slot(id));
+    if (!m) return -1;
+    const uint64_t vref1 = m->_versioned_ref.fetch_add(1, std::memory_order_acquire);
+    const uint32_t ver1 = vref_ver(vref1);
+    if (ver1 == sid_ver(id) || ver1 == sid_ver(id) + 1) {
+        ptr->reset(m);
+        return ver1 == sid_ver(id) ? 0 : 1;
+    }
+    // Same undo path as Address(): the slot may be recycled or reused.
+    const uint64_t vref2 = m->_versioned_ref.fetch_sub(1, std::memory_order_release);
+    if (vref_nref(vref2) == 1) {
+        const uint32_t ver2 = vref_ver(vref2);
+        if (ver2 & 1) {
+            uint64_t expected = vref2 - 1;
+            if (m->_versioned_ref.compare_exchange_strong(expected, make_vref(ver2 + 1, 0), std::memory_order_acquire)) {
+                m->OnRecycle();
+                return_resource<Socket>(sid_slot(id));
+            }
+        }
+    }
+    return -1;
+}
+
+int Socket::Dereference() {
+    const SocketId id = _this_id;
+    const uint64_t vref = _versioned_ref.fetch_sub(1, std::memory_order_release);
+    const int32_t nref = vref_nref(vref);
+    if (nref > 1) return 0;
+    if (nref == 1) {
+        const uint32_t ver = vref_ver(vref);
+        if (ver & 1) {
+            uint64_t expected = vref - 1;
+            if (_versioned_ref.compare_exchange_strong(expected, make_vref(ver + 1, 0), std::memory_order_acquire)) {
+                OnRecycle();
+                return_resource<Socket>(sid_slot(id));
+                return 1;
+            }
+            return 0;
+        }
+        LOG(FATAL) << "Socket " << id << " dereferenced to 0 without SetFailed";
+    }
+    LOG(FATAL) << "Over dereferenced socket " << id;
+    return -1;
+}
+
+bool Socket::Failed() const {
+    return vref_ver(_versioned_ref.load(std::memory_order_acquire)) != sid_ver(_this_id);
+}
+
+std::string Socket::error_text() const {
+    std::lock_guard<std::mutex> g(_mu);
+    return _error_text;
+}
+
+int Socket::SetFailed(SocketId id) {
+    SocketUniquePtr p;
+    if (Address(id, &p) != 0) return -1;
+    return p->SetFailed();
+}
+
+int Socket::SetFailed() { return SetFailed(EFAILEDSOCKET, "socket closed"); }
+
+int Socket::SetFailed(int error_code, const char* fmt, ...) {
+    if (error_code == 0) error_code = EFAILEDSOCKET;
+    const uint32_t id_ver = sid_ver(_this_id);
+    uint64_t vref = _versioned_ref.load(std::memory_order_relaxed);
+    for (;;) {
+        if (vref_ver(vref) != id_ver) return -1;
+        if (_versioned_ref.compare_exchange_strong(vref, make_vref(id_ver + 1, vref_nref(vref)),
+                                                   std::memory_order_release, std::memory_order_relaxed)) {
+            break;
+        }
+    }
+    std::string text;
+    if (fmt) {
+        va_list ap;
+        va_start(ap, fmt);
+        char buf[512];
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        text = buf;
+    }
+    std::shared_ptr<Transport> tr;
+    {
+        std::lock_guard<std::mutex> g(_mu);
+        _error_code = error_code;
+        _error_text = text.empty() ? ErrorText(error_code) : text;
+        tr = _transport;
+    }
+    const int fd = _fd.load(std::memory_order_acquire);
+    if (fd >= 0) {
+        // Wake peers and our own pending reads; the fd is closed on recycle.
+        if (_on_edge_triggered_events) GetGlobalEventDispatcher(fd).RemoveConsumer(fd);
+        ::shutdown(fd, SHUT_RDWR);
+    }
+    _epollout_butex->fetch_add(1, std::memory_order_release);
+    fiber::butex_wake_all(_epollout_butex);
+    if (tr) tr->OnSocketFailed(this);
+    // Fail every RPC waiting for a response on this socket.
+    std::vector<fiber::CallId> ids;
+    std::vector<std::function<void()>> cbs;
+    {
+        std::lock_guard<std::mutex> g(_shared->mu);
+        ids.swap(_shared->id_wait_list);
+        cbs.swap(_shared->failure_callbacks);
+    }
+    for (fiber::CallId cid : ids) fiber::call_id_error(cid, error_code, _error_text);
+    for (auto& cb : cbs) cb();
+    if (_health_check_interval_s > 0 && !_recycle_flag.load() && !_remote_side.path.size() && !is_pooled()) {
+        StartHealthCheck();
+    } else {
+        Dereference();  // the creator's reference
+    }
+    return 0;
+}
+
+int Socket::ReleaseAdditionalReference() {
+    if (_recycle_flag.exchange(true)) return -1;
+    if (!Failed()) {
+        // SetFailed sees the recycle flag and releases the creator reference.
+        return SetFailed(EFAILEDSOCKET, "released");
+    }
+    // Failed with a health-check loop holding the creator ref: it exits and
+    // releases it on its next iteration.
+    return 0;
+}
+
+void Socket::OnRecycle() {
+    const int fd = _fd.exchange(-1, std::memory_order_acq_rel);
+    if (fd >= 0) {
+        if (_on_edge_triggered_events) GetGlobalEventDispatcher(fd).RemoveConsumer(fd);
+        ::close(fd);
+    }
+    _read_buf.clear();
+    _read_buf.return_cached_blocks();
+    if (_parsing_context && _parsing_context_deleter) _parsing_context_deleter(_parsing_context);
+    _parsing_context = nullptr;
+    _parsing_context_deleter = nullptr;
+    {
+        std::lock_guard<std::mutex> g(_mu);
+        _transport.reset();
+    }
+    _conn.reset();
+    // pooled sub sockets of a main socket are released with it
+    if (_shared) {
+        std::vector<SocketId> pool;
+        {
+            std::lock_guard<std::mutex> g(_shared->mu);
+            pool.swap(_shared->pool);
+        }
+        for (SocketId sid : pool) {
+            SocketUniquePtr p;
+            if (Address(sid, &p) == 0) p->SetFailed(EUNUSED, "main socket recycled");
+        }
+    }
+    _shared.reset();
+    _user = nullptr;
+    _on_edge_triggered_events = nullptr;
+    g_nsocket.fetch_sub(1, std::memory_order_relaxed);
+}
+
+void Socket::reset_parsing_context(void* ctx, void (*deleter)(void*)) {
+    if (_parsing_context && _parsing_context_deleter) _parsing_context_deleter(_parsing_context);
+    _parsing_context = ctx;
+    _parsing_context_deleter = deleter;
+}
+
+std::shared_ptr<Transport> Socket::transport() const {
+    std::lock_guard<std::mutex> g(_mu);
+    return _transport;
+}
+
+void Socket::set_transport(std::shared_ptr<Transport> t) {
+    std::lock_guard<std::mutex> g(_mu);
+    _transport = std::move(t);
+}
+
+// ---------------------------------------------------------------- read
+
+void Socket::StartInputEvent(SocketId id, uint32_t events) {
+    SocketUniquePtr s;
+    if (Address(id, &s) < 0) return;
+    if (s->_nevent.fetch_add(1, std::memory_order_acq_rel) == 0) {
+        Socket* p = s.release();
+        fiber::fiber_t tid;
+        if (fiber::start_urgent(&tid, &fiber::ATTR_NORMAL, ProcessEvent, p) != 0) ProcessEvent(p);
+    }
+}
+
+void* Socket::ProcessEvent(void* arg) {
+    Socket* s = static_cast<Socket*>(arg);
+    if (s->_on_edge_triggered_events) s->_on_edge_triggered_events(s);
+    s->Dereference();
+    return nullptr;
+}
+
+bool Socket::MoreReadEvents(int* progress) {
+    return !_nevent.compare_exchange_strong(*progress, 0, std::memory_order_release, std::memory_order_acquire);
+}
+
+ssize_t Socket::DoRead(size_t size_hint) {
+    const int fd = _fd.load(std::memory_order_acquire);
+    if (fd < 0) {
+        errno = EBADF;
+        return -1;
+    }
+    ssize_t n = _read_buf.append_from_fd(fd, size_hint);
+    if (n > 0) {
+        in_bytes.fetch_add(n, std::memory_order_relaxed);
+        _last_active_us.store(monotonic_us(), std::memory_order_relaxed);
+    }
+    return n;
+}
+
+void Socket::HandleEpollOut(SocketId id) {
+    SocketUniquePtr s;
+    if (AddressFailedAsWell(id, &s) < 0) return;
+    s->_epollout_butex->fetch_add(1, std::memory_order_release);
+    fiber::butex_wake_except(s->_epollout_butex, 0);
+}
+
+int Socket::WaitEpollOut(int fd, bool pollin, const timespec* abstime) {
+    if (Failed()) {
+        errno = EFAILEDSOCKET;
+        return -1;
+    }
+    const int expected = _epollout_butex->load(std::memory_order_acquire);
+    EventDispatcher& d = GetGlobalEventDispatcher(fd);
+    if (d.AddEpollOut(_this_id, fd, pollin) != 0) return -1;
+    int rc = 0;
+    if (fiber::butex_wait(_epollout_butex, expected, abstime) < 0 && errno != EWOULDBLOCK && errno != EINTR) rc = -1;
+    const int saved = errno;
+    d.RemoveEpollOut(_this_id, fd, pollin);
+    errno = saved;
+    return rc;
+}
+
+// ---------------------------------------------------------------- write
+
+int Socket::ConnectIfNot(const timespec* abstime, WriteRequest*) {
+    if (_fd.load(std::memory_order_acquire) >= 0) return 0;
+    if (_conn) return _conn->Connect(this, abstime);
+    // Synchronous (fiber-aware) connect on first write.
+    bool in_progress = false;
+    int fd = tcp_connect_nonblocking(_remote_side, &in_progress);
+    if (fd < 0) return -1;
+    if (in_progress) {
+        timespec ts;
+        if (!abstime) {
+            ts = realtime_after_us((int64_t)FLAGS_connect_timeout_ms_default * 1000);
+            abstime = &ts;
+        }
+        if (fiber::fd_timedwait(fd, EPOLLOUT, abstime) != 0) {
+            const int saved = errno;
+            fiber::close_fd(fd);
+            errno = saved;
+            return -1;
+        }
+        int err = 0;
+        socklen_t len = sizeof(err);
+        getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
+        if (err) {
+            fiber::close_fd(fd);
+            errno = err;
+            return -1;
+        }
+    }
+    // Another writer can't race here: only the head writer connects.
+    if (ResetFileDescriptor(fd) != 0) {
+        const int saved = errno;
+        _fd.store(-1);
+        ::close(fd);
+        errno = saved;
+        return -1;
+    }
+    return 0;
+}
+
+void Socket::ReturnFailedWriteRequest(WriteRequest* req, int error_code, const std::string& error_text) {
+    _unwritten_bytes.fetch_sub((int64_t)req->data.size(), std::memory_order_relaxed);
+    req->data.clear();
+    const fiber::CallId id = req->id_wait;
+    return_object(req);
+    if (id != fiber::INVALID_CALL_ID) fiber::call_id_error(id, error_code, error_text);
+}
+
+void Socket::ReleaseAllFailedWriteRequests(WriteRequest* req) {
+    const int error_code = _error_code ? _error_code : EFAILEDSOCKET;
+    const std::string text = error_text();
+    do {
+        // release all but the last connected request
+        while (req->next != nullptr) {
+            WriteRequest* saved = req;
+            req = req->next;
+            ReturnFailedWriteRequest(saved, error_code, text);
+        }
+        _unwritten_bytes.fetch_sub((int64_t)req->data.size(), std::memory_order_relaxed);
+        req->data.clear();  // MUST: otherwise IsWriteComplete never completes
+    } while (!IsWriteComplete(req, true, nullptr));
+    const fiber::CallId id = req->id_wait;
+    return_object(req);
+    if (id != fiber::INVALID_CALL_ID) fiber::call_id_error(id, error_code, text);
+}
+
+bool Socket::IsWriteComplete(WriteRequest* old_head, bool singular_node, WriteRequest** new_tail) {
+    WriteRequest* new_head = old_head;
+    WriteRequest* desired = nullptr;
+    bool return_when_no_more = true;
+    if (!old_head->data.empty() || !singular_node) {
+        desired = old_head;
+        return_when_no_more = false;
+    }
+    if (_write_head.compare_exchange_strong(new_head, desired, std::memory_order_acquire)) {
+        if (new_tail) *new_tail = old_head;
+        return return_when_no_more;
+    }
+    // New requests were pushed; new_head is the newest. Reverse them and
+    // link after old_head.
+    WriteRequest* tail = nullptr;
+    WriteRequest* p = new_head;
+    do {
+        while (((volatile WriteRequest*)p)->next == UNCONNECTED) sched_yield();
+        WriteRequest* const saved_next = p->next;
+        p->next = tail;
+        tail = p;
+        p = saved_next;
+    } while (p != old_head);
+    old_head->next = tail;
+    if (new_tail) *new_tail = new_head;
+    return false;
+}
+
+int Socket::Write(Buf* data, const WriteOptions* options) {
+    static const WriteOptions kDefault;
+    const WriteOptions& opt = options ? *options : kDefault;
+    if (data->empty()) return 0;
+    if (Failed()) {
+        const int ec = _error_code ? _error_code : EFAILEDSOCKET;
+        if (opt.id_wait != fiber::INVALID_CALL_ID) fiber::call_id_error(opt.id_wait, ec, error_text());
+        errno = ec;
+        return -1;
+    }
+    if (!opt.ignore_eovercrowded && _unwritten_bytes.load(std::memory_order_relaxed) > FLAGS_socket_max_unwritten_bytes) {
+        if (opt.id_wait != fiber::INVALID_CALL_ID) fiber::call_id_error(opt.id_wait, EOVERCROWDED, "socket overcrowded");
+        errno = EOVERCROWDED;
+        return -1;
+    }
+    WriteRequest* req = get_object<WriteRequest>();
+    req->data.swap(*data);
+    req->next = UNCONNECTED;
+    req->id_wait = opt.id_wait;
+    req->socket = this;
+    if (opt.id_wait != fiber::INVALID_CALL_ID) {
+        std::lock_guard<std::mutex> g(_shared->mu);
+        auto& v = _shared->id_wait_list;
+        v.push_back(opt.id_wait);
+        if (v.size() > 256 && v.size() > 2 * _shared->last_compact) {
+            size_t j = 0;
+            for (size_t i = 0; i < v.size(); ++i) {
+                if (fiber::call_id_exists(v[i])) v[j++] = v[i];
+            }
+            v.resize(j);
+            _shared->last_compact = j;
+        }
+    }
+    return StartWrite(req, opt);
+}
+
+int Socket::StartWrite(WriteRequest* req, const WriteOptions& opt) {
+    _unwritten_bytes.fetch_add((int64_t)req->data.size(), std::memory_order_relaxed);
+    out_messages.fetch_add(1, std::memory_order_relaxed);
+    WriteRequest* const prev_head = _write_head.exchange(req, std::memory_order_release);
+    if (prev_head != nullptr) {
+        // Someone is writing; it will pick up this request.
+        req->next = prev_head;
+        return 0;
+    }
+    req->next = nullptr;
+    int saved_errno = 0;
+    ssize_t nw = 0;
+    if (ConnectIfNot(nullptr, req) != 0) {
+        saved_errno = errno;
+        SetFailed(saved_errno ? saved_errno : EFAILEDSOCKET, "fail to connect %s: %s", _remote_side.to_string().c_str(),
+                  ErrorText(saved_errno));
+        ReleaseAllFailedWriteRequests(req);
+        errno = saved_errno;
+        return -1;
+    }
+    if (!opt.write_in_background) {
+        const int fd = _fd.load(std::memory_order_acquire);
+        if (_conn) {
+            Buf* list[1] = {&req->data};
+            nw = _conn->CutMessageIntoFileDescriptor(fd, list, 1);
+        } else {
+            nw = req->data.cut_into_fd(fd);
+        }
+        if (nw < 0) {
+            if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EOVERCROWDED) {
+                saved_errno = errno;
+                SetFailed(saved_errno, "fail to write into fd: %s", ErrorText(saved_errno));
+                ReleaseAllFailedWriteRequests(req);
+                errno = saved_errno;
+                return -1;
+            }
+        } else {
+            _unwritten_bytes.fetch_sub(nw, std::memory_order_relaxed);
+            out_bytes.fetch_add(nw, std::memory_order_relaxed);
+        }
+        if (IsWriteComplete(req, true, nullptr)) {
+            return_object(req);
+            return 0;
+        }
+    }
+    fiber::fiber_t th;
+    if (fiber::start_background(&th, &fiber::ATTR_NORMAL, KeepWrite, req) != 0) KeepWrite(req);
+    return 0;
+}
+
+ssize_t Socket::DoWrite(WriteRequest* req) {
+    Buf* list[Buf::MAX_WRITEV_IOV];
+    size_t n = 0;
+    for (WriteRequest* p = req; p != nullptr && n < (size_t)Buf::MAX_WRITEV_IOV; p = p->next) list[n++] = &p->data;
+    const int fd = _fd.load(std::memory_order_acquire);
+    if (fd < 0) {
+        errno = EBADF;
+        return -1;
+    }
+    ssize_t nw = _conn ? _conn->CutMessageIntoFileDescriptor(fd, list, n) : Buf::cut_multiple_into_fd(fd, list, n);
+    if (nw > 0) out_bytes.fetch_add(nw, std::memory_order_relaxed);
+    return nw;
+}
+
+void* Socket::KeepWrite(void* arg) {
+    WriteRequest* req = static_cast<WriteRequest*>(arg);
+    Socket* s = req->socket;
+    WriteRequest* cur_tail = nullptr;
+    for (;;) {
+        if (req->next != nullptr && req->data.empty()) {
+            WriteRequest* saved = req;
+            req = req->next;
+            return_object(saved);
+        }
+        if (s->Failed()) break;
+        const ssize_t nw = s->DoWrite(req);
+        if (nw < 0) {
+            if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EOVERCROWDED) {
+                const int saved_errno = errno;
+                s->SetFailed(saved_errno, "fail to keep writing: %s", ErrorText(saved_errno));
+                break;
+            }
+            timespec ts = realtime_after_us(50000);
+            const int fd = s->fd();
+            if (fd < 0 || s->WaitEpollOut(fd, s->_on_edge_triggered_events != nullptr, &ts) != 0) {
+                if (errno != ETIMEDOUT && errno != EWOULDBLOCK && errno != EINTR) {
+                    const int saved_errno = errno ? errno : EFAILEDSOCKET;
+                    s->SetFailed(saved_errno, "fail to wait epollout: %s", ErrorText(saved_errno));
+                    break;
+                }
+            }
+        } else {
+            s->_unwritten_bytes.fetch_sub(nw, std::memory_order_relaxed);
+        }
+        while (req->next != nullptr && req->data.empty()) {
+            WriteRequest* saved = req;
+            req = req->next;
+            return_object(saved);
+        }
+        if (cur_tail == nullptr) {
+            for (cur_tail = req; cur_tail->next != nullptr; cur_tail = cur_tail->next) {
+            }
+        }
+        if (s->IsWriteComplete(cur_tail, req == cur_tail, &cur_tail)) {
+            return_object(req);
+            return nullptr;
+        }
+    }
+    s->ReleaseAllFailedWriteRequests(req);
+    return nullptr;
+}
+
+// ---------------------------------------------------------------- pool / short
+
+int Socket::GetPooledSocket(SocketUniquePtr* out) {
+    std::shared_ptr<SharedPart> sp = _shared;
+    if (!sp) return -1;
+    for (;;) {
+        SocketId sid = INVALID_SOCKET_ID;
+        {
+            std::lock_guard<std::mutex> g(sp->mu);
+            if (sp->pool.empty()) break;
+            sid = sp->pool.back();
+            sp->pool.pop_back();
+        }
+        if (Address(sid, out) == 0) return 0;
+    }
+    SocketOptions opt;
+    opt.remote_side = _remote_side;
+    opt.user = _user;
+    opt.on_edge_triggered_events = _on_edge_triggered_events;
+    opt.conn = _conn;
+    opt.connect_lazily = true;
+    SocketId sid;
+    if (Create(opt, &sid) != 0) return -1;
+    if (Address(sid, out) != 0) return -1;
+    (*out)->_main_socket_id = _this_id;
+    return 0;
+}
+
+void Socket::ReturnToPool() {
+    SocketUniquePtr main;
+    if (_main_socket_id == INVALID_SOCKET_ID || Address(_main_socket_id, &main) != 0 || Failed()) {
+        SetFailed(EUNUSED, "pooled socket not returnable");
+        return;
+    }
+    std::shared_ptr<SharedPart> sp = main->_shared;
+    std::lock_guard<std::mutex> g(sp->mu);
+    if ((int)sp->pool.size() >= FLAGS_max_connection_pool_size) {
+        SetFailed(EUNUSED, "connection pool full");
+        return;
+    }
+    sp->pool.push_back(_this_id);
+}
+
+int Socket::GetShortSocket(SocketUniquePtr* out) {
+    SocketOptions opt;
+    opt.remote_side = _remote_side;
+    opt.user = _user;
+    opt.on_edge_triggered_events = _on_edge_triggered_events;
+    opt.conn = _conn;
+    opt.connect_lazily = true;
+    SocketId sid;
+    if (Create(opt, &sid) != 0) return -1;
+    return Address(sid, out);
+}
+
+// ---------------------------------------------------------------- auth
+
+bool Socket::FightAuthentication(int* auth_error) {
+    int expected = 0;
+    if (_auth_state.compare_exchange_strong(expected, 1)) return true;
+    while (_auth_state.load(std::memory_order_acquire) != 2) {
+        fiber::butex_wait(_auth_butex, 0, nullptr);
+    }
+    *auth_error = _auth_error.load();
+    return false;
+}
+
+void Socket::SetAuthentication(int error) {
+    _auth_error.store(error);
+    _auth_state.store(2, std::memory_order_release);
+    _auth_butex->store(1, std::memory_order_release);
+    fiber::butex_wake_all(_auth_butex);
+}
+
+// ---------------------------------------------------------------- health check / revive
+
+int Socket::Revive(int new_fd) {
+    const uint32_t id_ver = sid_ver(_this_id);
+    uint64_t vref = _versioned_ref.load(std::memory_order_relaxed);
+    for (;;) {
+        if (vref_ver(vref) != id_ver + 1) return -1;
+        // reset per-connection state before becoming visible again
+        _read_buf.clear();
+        _nevent.store(0);
+        _preferred_index = -1;
+        if (_parsing_context && _parsing_context_deleter) _parsing_context_deleter(_parsing_context);
+        _parsing_context = nullptr;
+        _auth_state.store(0);
+        const int old = _fd.exchange(-1);
+        if (old >= 0) ::close(old);
+        if (_versioned_ref.compare_exchange_strong(vref, make_vref(id_ver, vref_nref(vref)), std::memory_order_release)) {
+            break;
+        }
+    }
+    {
+        std::lock_guard<std::mutex> g(_mu);
+        _error_code = 0;
+        _error_text.clear();
+    }
+    if (new_fd >= 0) ResetFileDescriptor(new_fd);
+    LOG(INFO) << "Revived " << description();
+    return 0;
+}
+
+void* Socket::HealthCheckThread(void* arg) {
+    Socket* s = static_cast<Socket*>(arg);
+    for (;;) {
+        fiber::usleep((uint64_t)std::max(1, s->_health_check_interval_s) * 1000000);
+        if (s->_recycle_flag.load()) break;
+        int fd = tcp_connect(s->_remote_side, 500);
+        if (fd >= 0) {
+            s->_hc_started.store(false);
+            if (s->_recycle_flag.load()) {
+                ::close(fd);
+                break;
+            }
+            s->Revive(fd);
+            return nullptr;  // keep the creator reference: socket alive again
+        }
+    }
+    s->_hc_started.store(false);
+    s->Dereference();  // release the creator reference
+    return nullptr;
+}
+
+void Socket::StartHealthCheck() {
+    if (_hc_started.exchange(true)) return;
+    fiber::fiber_t th;
+    if (fiber::start_background(&th, &fiber::ATTR_NORMAL, HealthCheckThread, this) != 0) {
+        _hc_started.store(false);
+        Dereference();
+    }
+}
+
+std::string Socket::description() const {
+    return string_printf("Socket{id=%llu fd=%d remote=%s nref=%u%s}", (unsigned long long)_this_id, fd(),
+                         _remote_side.to_string().c_str(), nref(), Failed() ? " failed" : "");
+}
+
+std::string DescribeAllSockets() {
+    std::string out;
+    ResourcePool<Socket>::singleton()->for_each([&out](uint32_t, Socket* s) {
+        const uint64_t v = s->nref();
+        if (v == 0) return;
+        if (s->fd() < 0 && s->Failed()) return;
+        out += s->description();
+        string_appendf(&out, " in=%lld out=%lld\n", (long long)s->in_bytes.load(), (long long)s->out_bytes.load());
+    });
+    return out;
+}
+
+}  // namespace mrpc

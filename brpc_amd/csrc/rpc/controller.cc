@@ -1,0 +1,377 @@
+#include "rpc/controller.h"
+
+#include <cerrno>
+#include <cstdarg>
+
+#include "base/logging.h"
+#include "base/time.h"
+#include "base/util.h"
+#include "cluster/circuit_breaker.h"
+#include "cluster/load_balancer.h"
+#include "fiber/fiber.h"
+#include "http/http_header.h"
+#include "rpc/errno.h"
+#include "rpc/protocol.h"
+#include "rpc/retry_policy.h"
+#include "rpc/server.h"
+#include "rpc/span.h"
+
+namespace mrpc {
+
+Controller::Controller() {}
+
+Controller::~Controller() {
+    ResetNonPods();
+}
+
+void Controller::ResetNonPods() {
+    if (_correlation_id.value) {
+        // A finished RPC already destroyed the id; an unused one must be cancelled.
+        fiber::call_id_cancel(_correlation_id);
+    }
+    if (_timeout_id) fiber::timer_del(_timeout_id);
+    if (_backup_id) fiber::timer_del(_backup_id);
+    delete _accessed;
+    _accessed = nullptr;
+    delete _http_request;
+    _http_request = nullptr;
+    delete _http_response;
+    _http_response = nullptr;
+    if (_session_local_data && _server) _server->ReturnSessionLocalData(_session_local_data);
+    _session_local_data = nullptr;
+    if (_span) {
+        Span::Submit(_span, _end_us ? _end_us : monotonic_us());
+        _span = nullptr;
+    }
+}
+
+void Controller::Reset() {
+    ResetNonPods();
+    _method = nullptr;
+    _response = nullptr;
+    _done = nullptr;
+    _protocol = nullptr;
+    _single_server_id = INVALID_SOCKET_ID;
+    _lb = nullptr;
+    _lb_holder.reset();
+    _auth = nullptr;
+    _request_buf.clear();
+    _request_attachment.clear();
+    _response_attachment.clear();
+    _error_code = 0;
+    _error_text.clear();
+    _timeout_ms = UNSET_MAGIC;
+    _backup_request_ms = UNSET_MAGIC;
+    _max_retry = UNSET_MAGIC;
+    _nretry = 0;
+    _has_backup = false;
+    _retry_policy = nullptr;
+    _connection_type = CONNECTION_TYPE_SINGLE;
+    _request_compress_type = COMPRESS_TYPE_NONE;
+    _response_compress_type = COMPRESS_TYPE_NONE;
+    _log_id = 0;
+    _has_log_id = false;
+    _request_code = 0;
+    _has_request_code = false;
+    _request_id.clear();
+    _correlation_id = fiber::CallId{0};
+    _timeout_id = 0;
+    _backup_id = 0;
+    _begin_us = _begin_real_us = _end_us = 0;
+    _deadline_us = -1;
+    _current_call.Reset();
+    _unfinished_call.Reset();
+    _remote_side = EndPoint();
+    _local_side = EndPoint();
+    _canceled = false;
+    _cancel_callback = nullptr;
+    _span_enabled = false;
+    _trace_id = _span_id = _parent_span_id = 0;
+    _verify_device_payload = false;
+    _read_progressively = false;
+    _progressive_reader = nullptr;
+    _progressive_attachment.reset();
+    _session_kv.clear();
+    _request_stream = _response_stream = 0;
+    _stream_creator.reset();
+    _server = nullptr;
+    _method_status = nullptr;
+    _server_socket_id = INVALID_SOCKET_ID;
+    _server_correlation_id = 0;
+    _close_connection = false;
+    _on_end = nullptr;
+    _received_us = 0;
+}
+
+void Controller::SetFailed(const std::string& reason) {
+    if (_error_code == 0) _error_code = EINTERNAL;
+    if (!_error_text.empty()) _error_text += "; ";
+    _error_text += reason;
+}
+
+void Controller::SetFailed(int error_code, const char* fmt, ...) {
+    if (error_code == 0) error_code = EINTERNAL;
+    _error_code = error_code;
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (!_error_text.empty()) _error_text += "; ";
+    string_appendf(&_error_text, "[E%d]%s", error_code, buf);
+}
+
+fiber::CallId Controller::call_id() {
+    if (_correlation_id.value == 0) {
+        if (fiber::call_id_create(&_correlation_id, this, HandleError) != 0) {
+            LOG(FATAL) << "Fail to create call id";
+        }
+    }
+    return _correlation_id;
+}
+
+void Controller::Join() {
+    if (_correlation_id.value) fiber::call_id_join(_correlation_id);
+}
+
+void Controller::CloseConnection(const char* reason) {
+    _close_connection = true;
+    (void)reason;
+}
+
+bool Controller::IsAskedToQuit() const {
+    if (_server_socket_id == INVALID_SOCKET_ID) return false;
+    SocketUniquePtr s;
+    return Socket::Address(_server_socket_id, &s) != 0;
+}
+
+HttpHeader& Controller::http_request() {
+    if (!_http_request) _http_request = new HttpHeader;
+    return *_http_request;
+}
+
+HttpHeader& Controller::http_response() {
+    if (!_http_response) _http_response = new HttpHeader;
+    return *_http_response;
+}
+
+void Controller::StartCancel() {
+    if (_canceled.exchange(true)) return;
+    if (_correlation_id.value) fiber::call_id_error(_correlation_id, ECANCELED, "canceled");
+    Closure* cb = _cancel_callback;
+    _cancel_callback = nullptr;
+    if (cb) cb->Run();
+}
+
+void StartCancel(fiber::CallId id) { fiber::call_id_error(id, ECANCELED, "canceled"); }
+
+void Controller::NotifyOnCancel(Closure* callback) {
+    if (_canceled.load()) {
+        callback->Run();
+        return;
+    }
+    _cancel_callback = callback;
+}
+
+// ----------------------------------------------------------------- engine
+
+int Controller::HandleError(fiber::CallId id, void* data, int error_code, const std::string& error_text) {
+    Controller* c = static_cast<Controller*>(data);
+    if (error_code == ERPCTIMEDOUT) {
+        c->SetFailed(ERPCTIMEDOUT, "reached timeout=%lldms @%s", (long long)c->_timeout_ms,
+                     c->_remote_side.to_string().c_str());
+        c->EndRPC(c->_current_call.id);
+        return 0;
+    }
+    if (error_code == ECANCELED) {
+        c->SetFailed(ECANCELED, "RPC canceled");
+        c->EndRPC(c->_current_call.id);
+        return 0;
+    }
+    if (error_code == EBACKUPREQUEST) {
+        c->_backup_id = 0;
+        if (c->_nretry >= c->_max_retry || c->_unfinished_call.id.value != 0) {
+            fiber::call_id_unlock(id);
+            return 0;
+        }
+        // Keep the in-flight attempt as "unfinished" and send a duplicate to
+        // another server; the first response wins.
+        c->_unfinished_call.id = c->_current_call.id;
+        c->_unfinished_call.peer_id = c->_current_call.peer_id;
+        c->_unfinished_call.sending_sock = std::move(c->_current_call.sending_sock);
+        c->_unfinished_call.begin_us = c->_current_call.begin_us;
+        c->_unfinished_call.need_feedback = c->_current_call.need_feedback;
+        if (!c->_accessed) c->_accessed = new ExcludedServers;
+        c->_accessed->Add(c->_current_call.peer_id);
+        ++c->_nretry;
+        c->_has_backup = true;
+        c->IssueRPC(realtime_us());
+        return 0;
+    }
+    if (id != c->_current_call.id && id != c->_unfinished_call.id) {
+        fiber::call_id_unlock(id);  // error of an obsolete attempt
+        return 0;
+    }
+    if (id == c->_current_call.id) {
+        c->_error_code = 0;  // replace the error of the attempt
+        c->_error_text.clear();
+        c->SetFailed(error_code, "%s", error_text.c_str());
+    }
+    c->OnVersionedRPCReturned(id, error_code);
+    return 0;
+}
+
+void Controller::OnVersionedRPCReturned(fiber::CallId id, int error_code) {
+    if (id != _current_call.id && id != _unfinished_call.id) {
+        fiber::call_id_unlock(_correlation_id);
+        return;
+    }
+    if (error_code == 0) {
+        EndRPC(id);
+        return;
+    }
+    if (id != _current_call.id) {
+        // The original attempt of a backup request failed; keep waiting.
+        OnCallComplete(&_unfinished_call, error_code, false);
+        _unfinished_call.Reset();
+        fiber::call_id_unlock(_correlation_id);
+        return;
+    }
+    const RetryPolicy* rp = _retry_policy ? _retry_policy : DefaultRetryPolicy();
+    if (_nretry < _max_retry && !_canceled.load() && rp->DoRetry(this)) {
+        OnCallComplete(&_current_call, error_code, false);
+        if (!_accessed) _accessed = new ExcludedServers;
+        _accessed->Add(_current_call.peer_id);
+        ++_nretry;
+        _error_code = 0;
+        _error_text.clear();
+        IssueRPC(realtime_us());
+        return;
+    }
+    EndRPC(id);
+}
+
+void Controller::OnCallComplete(Call* c, int error_code, bool responded) {
+    if (c->id.value == 0) return;
+    if (_enable_circuit_breaker && c->peer_id != INVALID_SOCKET_ID && error_code != ECANCELED) {
+        FeedCircuitBreaker(c->peer_id, error_code, monotonic_us() - c->begin_us);
+    }
+    if (c->need_feedback && _lb) {
+        LoadBalancer::CallInfo info;
+        info.begin_time_us = c->begin_us;
+        info.server_id = c->peer_id;
+        info.error_code = error_code;
+        info.controller = this;
+        _lb->Feedback(info);
+    }
+    if (c->sending_sock) {
+        if (_connection_type == CONNECTION_TYPE_POOLED && responded && error_code == 0) {
+            c->sending_sock->ReturnToPool();
+        } else if (_connection_type == CONNECTION_TYPE_POOLED || _connection_type == CONNECTION_TYPE_SHORT) {
+            c->sending_sock->SetFailed(EUNUSED, "short/pooled connection done");
+        }
+        c->sending_sock.reset();
+    }
+}
+
+void Controller::EndRPC(fiber::CallId id) {
+    if (_timeout_id) {
+        fiber::timer_del(_timeout_id);
+        _timeout_id = 0;
+    }
+    if (_backup_id) {
+        fiber::timer_del(_backup_id);
+        _backup_id = 0;
+    }
+    const bool responded = (_error_code == 0);
+    if (id == _current_call.id) {
+        OnCallComplete(&_current_call, _error_code, responded);
+        OnCallComplete(&_unfinished_call, ECANCELED, false);
+    } else {
+        OnCallComplete(&_unfinished_call, _error_code, responded);
+        OnCallComplete(&_current_call, ECANCELED, false);
+    }
+    _end_us = monotonic_us();
+    if (_span) Span::EndClientSpan(_span, this);
+    if (_on_end) _on_end(this);
+    Closure* done = _done;
+    _done = nullptr;
+    const fiber::CallId cid = _correlation_id;
+    _correlation_id = fiber::CallId{0};
+    // After this, a sync caller may destroy *this.
+    fiber::call_id_unlock_and_destroy(cid);
+    if (done) done->Run();
+}
+
+void Controller::IssueRPC(int64_t start_realtime_us) {
+    (void)start_realtime_us;
+    const fiber::CallId cid = fiber::call_id_with_version(_correlation_id, 1 + _nretry);
+    _current_call.Reset();
+    _current_call.id = cid;
+    _current_call.begin_us = monotonic_us();
+    SocketUniquePtr tmp;
+    if (_single_server_id != INVALID_SOCKET_ID) {
+        if (Socket::Address(_single_server_id, &tmp) != 0) {
+            fiber::call_id_unlock(_correlation_id);
+            fiber::call_id_error(cid, EHOSTDOWN, "server " + _remote_side.to_string() + " is down");
+            return;
+        }
+        _current_call.peer_id = _single_server_id;
+    } else if (_lb) {
+        LoadBalancer::SelectIn in;
+        in.begin_time_us = _current_call.begin_us;
+        in.has_request_code = _has_request_code;
+        in.request_code = _request_code;
+        in.excluded = _accessed;
+        LoadBalancer::SelectOut out;
+        out.ptr = &tmp;
+        const int rc = _lb->SelectServer(in, &out);
+        if (rc != 0 || !tmp) {
+            fiber::call_id_unlock(_correlation_id);
+            fiber::call_id_error(cid, EHOSTDOWN, "no server available");
+            return;
+        }
+        _current_call.need_feedback = out.need_feedback;
+        _current_call.peer_id = tmp->id();
+    } else {
+        fiber::call_id_unlock(_correlation_id);
+        fiber::call_id_error(cid, EINTERNAL, "channel has no server");
+        return;
+    }
+    _remote_side = tmp->remote_side();
+    Socket* sock = tmp.get();
+    if (_connection_type == CONNECTION_TYPE_POOLED) {
+        if (tmp->GetPooledSocket(&_current_call.sending_sock) != 0) {
+            fiber::call_id_unlock(_correlation_id);
+            fiber::call_id_error(cid, EFAILEDSOCKET, "fail to get pooled connection");
+            return;
+        }
+        sock = _current_call.sending_sock.get();
+    } else if (_connection_type == CONNECTION_TYPE_SHORT) {
+        if (tmp->GetShortSocket(&_current_call.sending_sock) != 0) {
+            fiber::call_id_unlock(_correlation_id);
+            fiber::call_id_error(cid, EFAILEDSOCKET, "fail to create short connection");
+            return;
+        }
+        sock = _current_call.sending_sock.get();
+    }
+    Buf packet;
+    _pack_socket = sock;
+    _protocol->pack_request(&packet, cid.value, _method, this, _request_buf, _auth);
+    _pack_socket = nullptr;
+    if (_error_code != 0) {
+        const int ec = _error_code;
+        const std::string et = _error_text;
+        fiber::call_id_unlock(_correlation_id);
+        fiber::call_id_error(cid, ec, et);
+        return;
+    }
+    WriteOptions wopt;
+    wopt.id_wait = cid;
+    // Errors of Write() are delivered through call_id_error(cid), which is
+    // queued while we hold the lock and handled at unlock.
+    sock->Write(&packet, &wopt);
+    fiber::call_id_unlock(cid);
+}
+
+}  // namespace mrpc

@@ -1,3 +1,4 @@
+#include <execinfo.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -38,8 +39,20 @@ static bool match(const std::string& full, const std::string& filters) {
     return false;
 }
 
+static void crash_handler(int sig) {
+    void* frames[64];
+    int n = backtrace(frames, 64);
+    fprintf(stderr, "*** signal %d, backtrace:\n", sig);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 int main(int argc, char** argv) {
     signal(SIGPIPE, SIG_IGN);
+    signal(SIGSEGV, crash_handler);
+    signal(SIGABRT, crash_handler);
+    signal(SIGBUS, crash_handler);
     std::string filter;
     bool list = false;
     std::vector<char*> rest;
