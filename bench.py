@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""Headline benchmark: echo QPS + p99 latency (rpc_press workload, 32 B and
+64 KiB bodies) on 1/2/4/8 MI355X ranks.
+
+One process per GPU (torchrun). Every rank runs an echo Server and an
+rpc_press-style closed-loop client (50 in-flight calls over ONE connection,
+the reference's docs/cn/benchmark.md:92-98 setup) that targets the next rank
+in a ring — rank r -> (r+1) % N, so with N=1 the client talks to its own
+server over loopback. A "step" is a fixed batch of echo calls per rank
+(weak scaling: per-rank work is fixed as N grows).
+
+Timed region: barrier + torch.cuda.synchronize() on both sides of exactly K
+steps, the max elapsed over ranks, value = total successful calls of all
+ranks / that max. The 64 KiB leg and the rpc_press 100-QPS latency sample
+are measured the same way and reported as extra fields.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+   or: python -m torch.distributed.run --nproc-per-node N --master-addr
+       127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_QPS_32B = 215000.0   # echo, single connection, 32 B
+BASELINE_QPS_32KB = 29000.0   # nearest published large-body point (32 KB single conn)
+BASELINE_P99_US = 172.0       # rpc_press -qps=100 sample
+METRIC = "echo QPS + p99 latency (rpc_press, 32B & 64KB body) at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--requests-per-step", type=int, default=0, help="override the 32B step size")
+    ap.add_argument("--concurrency", type=int, default=50)
+    ap.add_argument("--workers", type=int, default=0, help="fiber worker pthreads per rank (0: auto)")
+    ap.add_argument("--skip-64k", action="store_true")
+    ap.add_argument("--device-payload", action="store_true",
+                    help="64 KiB leg with HBM-resident attachments")
+    ap.add_argument("--latency-sample-s", type=float, default=2.0,
+                    help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
+    return ap.parse_args()
+
+
+def auto_workers(local_world):
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 8
+    # a 1-GPU slot gets a 16-CPU share; never oversubscribe the node
+    share = max(4, ncpu // max(1, local_world))
+    return min(16, share)
+
+
+def main():
+    a = parse()
+    import torch  # noqa: E402
+    from brpc_amd import native  # noqa: E402
+    from brpc_amd.models import ECHO_32B, ECHO_64KB, start_echo_server  # noqa: E402
+    from brpc_amd import parallel  # noqa: E402
+
+    topo = parallel.init_distributed()
+    if topo.world_size != a.gpus:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, topo.world_size), file=sys.stderr)
+    workers = a.workers or auto_workers(topo.local_world_size)
+    native.set_flag("fiber_concurrency", str(workers))
+    cuda = torch.cuda.is_available()
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    server = start_echo_server("127.0.0.1:0", num_threads=workers, gpu_device=topo.device)
+    addrs = parallel.exchange_addresses(server.address, topo)
+    peer = addrs[parallel.ring_peer(topo)]
+
+    def timed_leg(wl, steps, warmup):
+        opts = wl.press_options(peer, gpu_device=topo.device)
+        opts["concurrency"] = a.concurrency
+        press = native.Press(opts)
+        n = wl.requests_per_step
+        for _ in range(warmup):
+            press.run_requests(n)
+        press.reset_stats()
+        parallel.barrier(topo)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            press.run_requests(n)
+        parallel.barrier(topo)
+        sync()
+        dt = time.perf_counter() - t0
+        st = press.stats()
+        dt_max = parallel.allreduce_max(dt, topo)
+        ok_total = parallel.allreduce_sum(st["success"], topo)
+        err_total = parallel.allreduce_sum(st["error"], topo)
+        p99_max = parallel.allreduce_max(st["p99_us"], topo)
+        p50_max = parallel.allreduce_max(st["p50_us"], topo)
+        del press
+        return {
+            "qps": ok_total / dt_max if dt_max > 0 else 0.0,
+            "ms_per_step": 1000.0 * dt_max / steps,
+            "p50_us": p50_max,
+            "p99_us": p99_max,
+            "errors": int(err_total),
+            "elapsed_s": dt_max,
+            "last_error": st["last_error"],
+        }
+
+    wl32 = ECHO_32B
+    if a.requests_per_step:
+        wl32.requests_per_step = a.requests_per_step
+    r32 = timed_leg(wl32, a.steps, a.warmup)
+
+    r64 = None
+    if not a.skip_64k:
+        wl64 = ECHO_64KB
+        wl64.device_attachment = bool(a.device_payload and cuda)
+        r64 = timed_leg(wl64, a.steps, a.warmup)
+
+    lat = None
+    if a.latency_sample_s > 0:
+        press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
+                              "connection_type": "single"})
+        parallel.barrier(topo)
+        press.run_for(a.latency_sample_s)
+        st = press.stats()
+        lat = {"p50_us": parallel.allreduce_max(st["p50_us"], topo),
+               "p99_us": parallel.allreduce_max(st["p99_us"], topo),
+               "avg_us": parallel.allreduce_max(st["avg_us"], topo)}
+        del press
+
+    parallel.barrier(topo)
+    server.stop()
+
+    if topo.rank == 0:
+        n = topo.world_size
+        out = {
+            "metric": METRIC,
+            "value": round(r32["qps"], 1),
+            "unit": "requests/s (32B echo, all ranks)",
+            "n_gpus": n,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(r32["ms_per_step"], 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(r32["qps"] / BASELINE_QPS_32B, 4),
+            "dtype": "uint8",
+            "data": "synthetic (random echo payloads)",
+            "config": {
+                "model": "example.EchoService.Echo over baidu_std",
+                "global_batch": a.concurrency * n,
+                "seq_len": 32,
+                "parallelism": "ring%d (rank r -> server of rank r+1), 1 conn/rank" % n,
+                "requests_per_step_per_rank": wl32.requests_per_step,
+                "fiber_workers_per_rank": workers,
+            },
+            "p50_us": r32["p50_us"],
+            "p99_us": r32["p99_us"],
+            "errors": r32["errors"],
+        }
+        if r64:
+            out["qps_64KB"] = round(r64["qps"], 1)
+            out["p99_us_64KB"] = r64["p99_us"]
+            out["gbytes_per_s_64KB"] = round(r64["qps"] * 65536 * 2 / 1e9, 3)
+            out["vs_baseline_64KB"] = round(r64["qps"] / BASELINE_QPS_32KB, 4)
+            out["errors_64KB"] = r64["errors"]
+            out["device_payload_64KB"] = bool(a.device_payload and cuda)
+        if lat:
+            out["p99_us_at_100qps"] = lat["p99_us"]
+            out["p50_us_at_100qps"] = lat["p50_us"]
+            out["vs_baseline_p99_at_100qps"] = round(BASELINE_P99_US / lat["p99_us"], 4) if lat["p99_us"] else None
+        print(json.dumps(out), flush=True)
+    parallel.destroy(topo)
+
+
+if __name__ == "__main__":
+    main()

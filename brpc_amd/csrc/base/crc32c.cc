@@ -89,14 +89,12 @@ uint32_t Extend(uint32_t init_crc, const void* data, size_t n) {
 
 // Multiply a(x) * b(x) mod P(x), reflected representation (bit 31 = x^0).
 uint32_t MultModP(uint32_t a, uint32_t b) {
-    uint32_t m = 1u << 31;
     uint32_t p = 0;
-    for (;;) {
+    for (uint32_t m = 1u << 31; m != 0; m >>= 1) {  // bounded: a == 0 yields 0
         if (a & m) {
             p ^= b;
             if ((a & (m - 1)) == 0) break;
         }
-        m >>= 1;
         b = (b & 1) ? (b >> 1) ^ kPoly : b >> 1;
     }
     return p;

@@ -1,0 +1,82 @@
+// MI355X device runtime for the RPC engine.
+//
+// The reference has no GPU code; this module is what makes the framework
+// MI355X-native (SURVEY.md §2 "GPU" rows, BASELINE.json north star):
+//  * HBM-resident Buf blocks (MemKind::DEVICE) with refcounted ownership so
+//    attachments can stay on the GPU end to end;
+//  * pinned (hipHostMalloc) block allocator so every socket buffer is
+//    DMA-able by the SDMA engines without a bounce;
+//  * a fiber-aware completion poller: a fiber that waits for a hipEvent
+//    parks on a butex and a single poller thread wakes it — GPU work and RPC
+//    handling interleave without ever blocking a worker pthread (the role
+//    bthread's butex plays for sockets, applied to HIP streams);
+//  * small per-device stream pools (GPU_MAX_HW_QUEUES=4 on the box, so we
+//    never create more than 4 streams per device and per process).
+// Everything degrades cleanly on a machine without a GPU: DeviceCount()
+// returns 0 and allocation calls fail with an error string.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+#include "base/buf.h"
+
+typedef struct ihipStream_t* hipStream_t;
+typedef struct ihipEvent_t* hipEvent_t;
+
+namespace mrpc {
+namespace gpu {
+
+// Number of visible devices; 0 when no GPU / runtime unavailable. Does not
+// create a context.
+int DeviceCount();
+bool Available();
+// Initialise the runtime on `device` (-1 = current), install the Buf device
+// copy hook and start the event poller. Idempotent. 0 on success.
+int Init(int device = -1, std::string* error = nullptr);
+int CurrentDevice();
+std::string DeviceName(int device);
+// gfx arch string of the device ("gfx950" on MI355X).
+std::string DeviceArch(int device);
+
+// ---- memory
+void* Malloc(size_t n, int device, std::string* error = nullptr);
+void Free(void* p);
+void* HostMallocPinned(size_t n);
+void HostFreePinned(void* p);
+// Make default Buf blocks pinned host memory (call before heavy traffic).
+int UsePinnedBlocks();
+
+// Copies; stream-ordered on a pool stream, the calling fiber parks until
+// completion (a pthread blocks).
+int CopyHostToDevice(void* dst, const void* src, size_t n, int device);
+int CopyDeviceToHost(void* dst, const void* src, size_t n, int device);
+int CopyDeviceToDevice(void* dst, const void* src, size_t n, int device);
+int Memset(void* dst, int value, size_t n, int device);
+
+// ---- Buf helpers
+// Append [dev, dev+n) as one DEVICE block. deleter(dev, arg) runs when the
+// last reference dies (nullptr = caller keeps ownership).
+int AppendDevice(Buf* b, void* dev, size_t n, int device, void (*deleter)(void*, void*) = nullptr,
+                 void* arg = nullptr);
+// Allocate HBM, upload `data` and append it as a DEVICE block owned by `b`.
+int AppendHostAsDevice(Buf* b, const void* data, size_t n, int device, std::string* error = nullptr);
+// Move every non-host block of `in` to one contiguous HBM allocation
+// appended to *out (host blocks are uploaded). Used by device handlers.
+int GatherToDevice(const Buf& in, Buf* out, int device, std::string* error = nullptr);
+// Copy all of `in` (any kinds) into *out.
+int CopyBufToHost(const Buf& in, std::string* out);
+bool HasDeviceBlocks(const Buf& b);
+
+// ---- streams / events
+hipStream_t PoolStream(int device);  // round-robin over <=4 non-blocking streams
+// Park the calling fiber until `ev` completes (pthread: hipEventSynchronize).
+int WaitEvent(hipEvent_t ev);
+// Record an event on `s` and wait for it fiber-friendly.
+int SyncStream(hipStream_t s);
+// Poller statistics
+int64_t PolledEvents();
+
+}  // namespace gpu
+}  // namespace mrpc

@@ -1,0 +1,51 @@
+// Host-side launch API of the hand-written CDNA4 kernels in kernels.hip.
+// All launches are stream-ordered and asynchronous; pointers are device (or
+// device-accessible pinned) addresses.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "gpu/gpu.h"
+
+namespace mrpc {
+namespace gpu {
+
+struct Segment {
+    const void* src;
+    void* dst;   // used by copies; ignored by crc
+    uint64_t len;
+};
+
+// Maximum number of segments one launch carries inline in its kernel
+// arguments (no descriptor upload); launchers split larger batches.
+constexpr int kInlineSegments = 32;
+// Bytes covered by one workgroup (256 lanes x 64 bytes).
+constexpr uint64_t kChunkBytes = 16384;
+
+// Standard (finalized) CRC32C of every segment into out_dev[i].
+// out_dev must be device memory; it is zeroed by the launch.
+int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s);
+// Copy every segment src -> dst (one launch for many small copies).
+int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s);
+
+// Packed-varint decode (protobuf wire type 0, packed repeated field):
+// `in` holds n bytes of concatenated varints; out receives the values
+// (uint64, zigzag-decoded to int64 when zigzag). count_dev receives the
+// number of values; err_dev gets 1 if the stream is malformed (value longer
+// than 10 bytes or truncated). scratch must hold VarintScratchBytes(n).
+size_t VarintScratchBytes(uint64_t n);
+int LaunchVarintDecode(const uint8_t* in, uint64_t n, uint64_t* out, uint64_t max_out, bool zigzag,
+                       uint64_t* count_dev, int* err_dev, void* scratch, hipStream_t s);
+// Packed-varint encode: values -> bytes. out must hold 10*n bytes; bytes_dev
+// receives the encoded size. scratch must hold VarintScratchBytes(n).
+int LaunchVarintEncode(const uint64_t* in, uint64_t n, bool zigzag, uint8_t* out, uint64_t* bytes_dev,
+                       void* scratch, hipStream_t s);
+
+// ---- synchronous helpers (fiber-friendly waits)
+// CRC32C of device buffers; results to host.
+int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t* out_host, int device);
+int Crc32cOfBuf(const Buf& b, uint32_t* out, int device);  // any block kinds
+
+}  // namespace gpu
+}  // namespace mrpc

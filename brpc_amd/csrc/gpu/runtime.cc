@@ -1,0 +1,395 @@
+#include "gpu/gpu.h"
+
+#include <hip/hip_runtime_api.h>
+#include <pthread.h>
+#include <time.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "base/flags.h"
+#include "base/logging.h"
+#include "fiber/butex.h"
+#include "fiber/fiber.h"
+
+DEFINE_int32(gpu_streams_per_device, 4, "HIP streams per device in the pool (<= GPU_MAX_HW_QUEUES)");
+DEFINE_int32(gpu_poller_spin_us, 20, "event poller busy-polls this long before backing off");
+
+namespace mrpc {
+namespace gpu {
+
+namespace {
+
+const int kMaxDevices = 64;
+
+struct DeviceState {
+    std::once_flag once;
+    int ok = 0;
+    std::vector<hipStream_t> streams;
+    std::atomic<uint32_t> rr{0};
+};
+
+DeviceState g_dev[kMaxDevices];
+std::atomic<int> g_count{-1};
+
+// ---- event pool
+std::mutex g_ev_mu;
+std::vector<hipEvent_t> g_ev_free;
+
+hipEvent_t get_event() {
+    {
+        std::lock_guard<std::mutex> g(g_ev_mu);
+        if (!g_ev_free.empty()) {
+            hipEvent_t e = g_ev_free.back();
+            g_ev_free.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return e;
+}
+
+void put_event(hipEvent_t e) {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    g_ev_free.push_back(e);
+}
+
+// ---- completion poller: fibers park on a butex, one pthread polls events.
+struct Waiter {
+    hipEvent_t ev;
+    std::atomic<int>* butex;
+};
+
+class EventPoller {
+public:
+    void add(const Waiter& w) {
+        std::unique_lock<std::mutex> g(_mu);
+        if (!_started) {
+            _started = true;
+            pthread_create(&_th, nullptr, &EventPoller::run, this);
+        }
+        _incoming.push_back(w);
+        _cv.notify_one();
+    }
+    int64_t polled() const { return _polled.load(std::memory_order_relaxed); }
+
+private:
+    static void* run(void* arg) {
+        pthread_setname_np(pthread_self(), "gpu_poller");
+        static_cast<EventPoller*>(arg)->loop();
+        return nullptr;
+    }
+    void loop() {
+        std::vector<Waiter> active;
+        int64_t last_progress_us = 0;
+        for (;;) {
+            bool progressed = false;
+            {
+                std::unique_lock<std::mutex> g(_mu);
+                if (active.empty()) {
+                    _cv.wait(g, [&] { return !_incoming.empty(); });
+                }
+                progressed = !_incoming.empty();
+                active.insert(active.end(), _incoming.begin(), _incoming.end());
+                _incoming.clear();
+            }
+            const size_t before = active.size();
+            size_t keep = 0;
+            for (size_t i = 0; i < active.size(); ++i) {
+                hipError_t r = hipEventQuery(active[i].ev);
+                if (r == hipErrorNotReady) {
+                    active[keep++] = active[i];
+                    continue;
+                }
+                // done (or failed: wake anyway, the waiter re-queries)
+                active[i].butex->store(1, std::memory_order_release);
+                fiber::butex_wake(active[i].butex);
+                _polled.fetch_add(1, std::memory_order_relaxed);
+            }
+            active.resize(keep);
+            if (keep != before) progressed = true;
+            if (!active.empty()) {
+                timespec now;
+                clock_gettime(CLOCK_MONOTONIC, &now);
+                const int64_t now_us = now.tv_sec * 1000000LL + now.tv_nsec / 1000;
+                if (progressed) last_progress_us = now_us;
+                if (now_us - last_progress_us > FLAGS_gpu_poller_spin_us) {
+                    timespec ts{0, 2000};  // 2us back-off once the spin budget is spent
+                    nanosleep(&ts, nullptr);
+                }
+            }
+        }
+    }
+
+    std::mutex _mu;
+    std::condition_variable _cv;
+    std::vector<Waiter> _incoming;
+    bool _started = false;
+    pthread_t _th;
+    std::atomic<int64_t> _polled{0};
+};
+
+EventPoller* poller() {
+    static EventPoller* p = new EventPoller;
+    return p;
+}
+
+int copy_hook(void* dst, const void* src, size_t n, MemKind kind, int device) {
+    (void)kind;
+    return CopyDeviceToHost(dst, src, n, device);
+}
+
+int check_device(int device) {
+    if (device < 0) device = CurrentDevice();
+    if (device < 0 || device >= kMaxDevices || device >= DeviceCount()) return -1;
+    return device;
+}
+
+}  // namespace
+
+int DeviceCount() {
+    int c = g_count.load(std::memory_order_acquire);
+    if (c >= 0) return c;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    g_count.store(n, std::memory_order_release);
+    return n;
+}
+
+bool Available() { return DeviceCount() > 0; }
+
+int CurrentDevice() {
+    if (!Available()) return -1;
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) return -1;
+    return d;
+}
+
+int Init(int device, std::string* error) {
+    device = check_device(device);
+    if (device < 0) {
+        if (error) *error = "no HIP device available";
+        return -1;
+    }
+    DeviceState& st = g_dev[device];
+    std::call_once(st.once, [&] {
+        int prev = 0;
+        hipGetDevice(&prev);
+        if (hipSetDevice(device) != hipSuccess) return;
+        const int ns = std::max(1, std::min(FLAGS_gpu_streams_per_device, 4));
+        for (int i = 0; i < ns; ++i) {
+            hipStream_t s = nullptr;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) break;
+            st.streams.push_back(s);
+        }
+        hipSetDevice(prev);
+        st.ok = st.streams.empty() ? 0 : 1;
+        SetDeviceCopyHook(copy_hook);
+    });
+    if (!st.ok) {
+        if (error) *error = "fail to initialise HIP device " + std::to_string(device);
+        return -1;
+    }
+    return 0;
+}
+
+std::string DeviceName(int device) {
+    hipDeviceProp_t p;
+    if (check_device(device) < 0 || hipGetDeviceProperties(&p, device) != hipSuccess) return "";
+    return p.name;
+}
+
+std::string DeviceArch(int device) {
+    hipDeviceProp_t p;
+    if (check_device(device) < 0 || hipGetDeviceProperties(&p, device) != hipSuccess) return "";
+    std::string a = p.gcnArchName;
+    const size_t colon = a.find(':');
+    return colon == std::string::npos ? a : a.substr(0, colon);
+}
+
+hipStream_t PoolStream(int device) {
+    device = check_device(device);
+    if (device < 0 || Init(device) != 0) return nullptr;
+    DeviceState& st = g_dev[device];
+    return st.streams[st.rr.fetch_add(1, std::memory_order_relaxed) % st.streams.size()];
+}
+
+int WaitEvent(hipEvent_t ev) {
+    hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return -1;
+    if (fiber::worker_index() < 0) {
+        return hipEventSynchronize(ev) == hipSuccess ? 0 : -1;
+    }
+    std::atomic<int>* b = fiber::butex_create();
+    b->store(0, std::memory_order_relaxed);
+    poller()->add(Waiter{ev, b});
+    while (b->load(std::memory_order_acquire) == 0) fiber::butex_wait(b, 0);
+    fiber::butex_destroy(b);
+    return hipEventQuery(ev) == hipSuccess ? 0 : -1;
+}
+
+int SyncStream(hipStream_t s) {
+    hipEvent_t e = get_event();
+    if (!e) return -1;
+    int rc = -1;
+    if (hipEventRecord(e, s) == hipSuccess) rc = WaitEvent(e);
+    put_event(e);
+    return rc;
+}
+
+int64_t PolledEvents() { return poller()->polled(); }
+
+void* Malloc(size_t n, int device, std::string* error) {
+    device = check_device(device);
+    if (device < 0) {
+        if (error) *error = "no HIP device available";
+        return nullptr;
+    }
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    void* p = nullptr;
+    hipError_t r = hipMalloc(&p, n ? n : 1);
+    if (prev != device) hipSetDevice(prev);
+    if (r != hipSuccess) {
+        if (error) *error = std::string("hipMalloc failed: ") + hipGetErrorString(r);
+        return nullptr;
+    }
+    return p;
+}
+
+void Free(void* p) {
+    if (p) hipFree(p);
+}
+
+void* HostMallocPinned(size_t n) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void HostFreePinned(void* p) {
+    if (p) hipHostFree(p);
+}
+
+static void* pinned_alloc(size_t n) {
+    void* p = HostMallocPinned(n);
+    return p ? p : malloc(n);  // never fail a socket read for lack of pinned memory
+}
+
+static void pinned_dealloc(void* p, size_t) {
+    // hipHostFree on a malloc'ed pointer fails harmlessly; distinguish anyway
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost) {
+        hipHostFree(p);
+    } else {
+        free(p);
+    }
+}
+
+int UsePinnedBlocks() {
+    if (!Available()) return -1;
+    SetBlockMemAllocator(BlockMemAllocator{pinned_alloc, pinned_dealloc, MemKind::PINNED});
+    return 0;
+}
+
+static int copy_impl(void* dst, const void* src, size_t n, hipMemcpyKind kind, int device) {
+    if (n == 0) return 0;
+    hipStream_t s = PoolStream(device);
+    if (!s) return -1;
+    if (hipMemcpyAsync(dst, src, n, kind, s) != hipSuccess) return -1;
+    return SyncStream(s);
+}
+
+int CopyHostToDevice(void* dst, const void* src, size_t n, int device) {
+    return copy_impl(dst, src, n, hipMemcpyHostToDevice, device);
+}
+int CopyDeviceToHost(void* dst, const void* src, size_t n, int device) {
+    return copy_impl(dst, src, n, hipMemcpyDeviceToHost, device);
+}
+int CopyDeviceToDevice(void* dst, const void* src, size_t n, int device) {
+    return copy_impl(dst, src, n, hipMemcpyDeviceToDevice, device);
+}
+
+int Memset(void* dst, int value, size_t n, int device) {
+    hipStream_t s = PoolStream(device);
+    if (!s) return -1;
+    if (hipMemsetAsync(dst, value, n, s) != hipSuccess) return -1;
+    return SyncStream(s);
+}
+
+static void free_device_block(void* p, void*) { Free(p); }
+
+int AppendDevice(Buf* b, void* dev, size_t n, int device, void (*deleter)(void*, void*), void* arg) {
+    if (device < 0) device = CurrentDevice();
+    return b->append_user_data(dev, n, deleter, arg, MemKind::DEVICE, device);
+}
+
+int AppendHostAsDevice(Buf* b, const void* data, size_t n, int device, std::string* error) {
+    if (device < 0) device = CurrentDevice();
+    void* d = Malloc(n, device, error);
+    if (!d) return -1;
+    if (CopyHostToDevice(d, data, n, device) != 0) {
+        Free(d);
+        if (error) *error = "host->device copy failed";
+        return -1;
+    }
+    return b->append_user_data(d, n, free_device_block, nullptr, MemKind::DEVICE, device);
+}
+
+int GatherToDevice(const Buf& in, Buf* out, int device, std::string* error) {
+    if (device < 0) device = CurrentDevice();
+    const size_t n = in.size();
+    if (n == 0) return 0;
+    if (in.backing_block_num() == 1 && in.ref_at(0).block->kind == MemKind::DEVICE &&
+        in.ref_at(0).block->device == device) {
+        out->append(in);
+        return 0;
+    }
+    char* d = static_cast<char*>(Malloc(n, device, error));
+    if (!d) return -1;
+    hipStream_t s = PoolStream(device);
+    size_t off = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BlockRef& r = in.ref_at(i);
+        const hipMemcpyKind k = IsHostAccessible(r.block->kind) ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+        if (hipMemcpyAsync(d + off, r.block->data + r.offset, r.length, k, s) != hipSuccess) {
+            Free(d);
+            if (error) *error = "gather copy failed";
+            return -1;
+        }
+        off += r.length;
+    }
+    if (SyncStream(s) != 0) {
+        Free(d);
+        if (error) *error = "gather sync failed";
+        return -1;
+    }
+    return out->append_user_data(d, n, free_device_block, nullptr, MemKind::DEVICE, device);
+}
+
+bool HasDeviceBlocks(const Buf& b) { return !b.all_host_accessible(); }
+
+int CopyBufToHost(const Buf& in, std::string* out) {
+    out->clear();
+    out->resize(in.size());
+    size_t off = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BlockRef& r = in.ref_at(i);
+        if (IsHostAccessible(r.block->kind)) {
+            memcpy(&(*out)[off], r.block->data + r.offset, r.length);
+        } else if (CopyDeviceToHost(&(*out)[off], r.block->data + r.offset, r.length, r.block->device) != 0) {
+            return -1;
+        }
+        off += r.length;
+    }
+    return 0;
+}
+
+}  // namespace gpu
+}  // namespace mrpc

@@ -1,0 +1,39 @@
+// protobuf <-> JSON conversion over descriptor reflection (role of
+// src/json2pb/json_to_pb.h:54-88, pb_to_json.h:76-90). Works for generated
+// and dynamic messages: rpc_press inputs, http+json bodies, /protobufs.
+#pragma once
+
+#include <string>
+
+#include "base/buf.h"
+#include "json/json.h"
+#include "pb/message.h"
+
+namespace mrpc {
+namespace json2pb {
+
+struct Pb2JsonOptions {
+    bool enum_option_as_string = true;  // else as number
+    bool pretty_json = false;
+    bool bytes_to_base64 = true;
+    bool jsonify_empty_array = false;
+    bool always_print_primitive_fields = false;
+    bool use_json_name = false;  // camelCase keys
+};
+
+struct Json2PbOptions {
+    bool base64_to_bytes = true;
+    bool allow_unknown_fields = true;
+};
+
+bool ProtoMessageToJson(const pb::Message& msg, std::string* json, const Pb2JsonOptions& opt = Pb2JsonOptions(),
+                        std::string* error = nullptr);
+bool ProtoMessageToJsonValue(const pb::Message& msg, json::Value* out, const Pb2JsonOptions& opt, std::string* error);
+bool JsonToProtoMessage(const std::string& json, pb::Message* msg, const Json2PbOptions& opt = Json2PbOptions(),
+                        std::string* error = nullptr);
+bool JsonToProtoMessage(const Buf& json, pb::Message* msg, const Json2PbOptions& opt = Json2PbOptions(),
+                        std::string* error = nullptr);
+bool JsonValueToProtoMessage(const json::Value& v, pb::Message* msg, const Json2PbOptions& opt, std::string* error);
+
+}  // namespace json2pb
+}  // namespace mrpc

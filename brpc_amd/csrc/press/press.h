@@ -1,0 +1,128 @@
+// Load generator behind the rpc_press tool and bench.py (role of the
+// reference's tools/rpc_press/rpc_press_impl.{h,cpp} + info_thread.cpp).
+//
+// Differences from the reference, by design:
+//  * senders are fibers, not pthreads: `concurrency` closed-loop workers (or
+//    paced open-loop senders in qps mode) all live on the M:N runtime, so a
+//    1-GPU box's CPU share is not burnt on idle threads;
+//  * latencies go into an exact log-linear histogram (var::LatencyHistogram)
+//    per worker and are merged at the end, so p99/p99.9 are exact to 1/64;
+//  * RunRequests(n) issues exactly n calls and returns, which is the unit a
+//    benchmark "step" is made of (bench.py times K such steps);
+//  * echo payloads may be device-resident (HBM) attachments that travel the
+//    xGMI transport (ChannelOptions::use_device_transport).
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "var/percentile.h"
+
+namespace mrpc {
+
+class Channel;
+namespace pb {
+class Message;
+class MethodDescriptor;
+class Importer;
+}  // namespace pb
+
+namespace press {
+
+struct PressOptions {
+    std::string server = "127.0.0.1:8002";  // ip:port, or naming-service url when lb_policy set
+    std::string lb_policy;
+    std::string protocol = "baidu_std";
+    std::string connection_type;  // single | pooled | short
+    int timeout_ms = 1000;
+    int connect_timeout_ms = 500;
+    int max_retry = 3;
+    int request_compress_type = 0;
+    int response_compress_type = 0;
+    int concurrency = 50;  // closed-loop workers (or open-loop senders)
+    double qps = 0;        // >0: open loop paced at this rate; 0: closed loop
+    int num_channels = 1;  // independent channels (connections for "single")
+    // echo workload (used when proto_file is empty)
+    int request_size = 32;     // bytes in EchoRequest.message
+    int attachment_size = 0;   // bytes of attachment per request
+    bool device_attachment = false;  // attachment lives in HBM (needs GPU)
+    int gpu_device = -1;
+    bool check_echo = false;   // verify the echoed payload
+    // generic workload (dynamic messages)
+    std::string proto_file;    // .proto path
+    std::string include_paths; // ';' separated
+    std::string method = "example.EchoService.Echo";
+    std::string input;         // file with json requests, or inline json
+};
+
+struct PressCall;
+
+struct Snapshot {
+    int64_t sent = 0;
+    int64_t success = 0;
+    int64_t error = 0;
+    double elapsed_s = 0;
+    double qps = 0;             // successes per second over elapsed_s
+    double avg_us = 0;
+    int64_t p50_us = 0, p70_us = 0, p90_us = 0, p95_us = 0, p97_us = 0;
+    int64_t p99_us = 0, p999_us = 0, p9999_us = 0, max_us = 0, min_us = 0;
+    int64_t bytes = 0;          // request+response payload bytes moved
+    int last_error_code = 0;
+    std::string last_error;
+};
+
+class PressSession {
+public:
+    PressSession();
+    ~PressSession();
+    // Returns 0 on success, else fills *error.
+    int Init(const PressOptions& opt, std::string* error);
+    // Closed loop: issue exactly n calls over `concurrency` workers, return
+    // when all finished. Stats accumulate until ResetStats().
+    int RunRequests(int64_t n);
+    // Run for `seconds` (closed loop, or paced when qps>0); `tick` gets the
+    // per-interval snapshot every second (rpc_press's info thread).
+    int RunFor(double seconds, const std::function<void(const Snapshot& interval, const Snapshot& total)>& tick);
+    Snapshot Stats() const;
+    void ResetStats();
+    const PressOptions& options() const { return _opt; }
+
+    struct Worker;
+    // internal (used by the worker fibers)
+    void issue(Worker* w, int64_t seq, PressCall* call, bool async);
+    void finish(PressCall* call);
+    std::atomic<int64_t>* inflight() { return &_inflight; }
+
+private:
+    void collect(std::vector<std::unique_ptr<Worker>>& ws);
+    Snapshot summarize(const var::LatencyHistogram& h, int64_t sent, int64_t ok, int64_t err, int64_t bytes,
+                       double secs) const;
+
+    PressOptions _opt;
+    std::vector<std::unique_ptr<Channel>> _channels;
+    // generic mode
+    std::unique_ptr<pb::Importer> _importer;
+    const pb::MethodDescriptor* _method = nullptr;
+    std::vector<std::unique_ptr<pb::Message>> _requests;
+    std::string _echo_message;
+    std::string _attachment;
+    void* _device_attachment = nullptr;  // HBM copy of _attachment when device_attachment
+
+    mutable std::mutex _mu;
+    var::LatencyHistogram _hist;
+    int64_t _sent = 0, _ok = 0, _err = 0, _bytes = 0;
+    double _busy_s = 0;
+    int _last_code = 0;
+    std::string _last_error;
+    std::atomic<int64_t> _inflight{0};
+};
+
+// Formats the latency table the way rpc_press prints it.
+std::string FormatLatencyTable(const Snapshot& s);
+
+}  // namespace press
+}  // namespace mrpc

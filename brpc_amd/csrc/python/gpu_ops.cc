@@ -1,0 +1,63 @@
+// Bindings of the device kernels for torch tensors. Python passes raw
+// device pointers (tensor.data_ptr()) and the HIP stream handle
+// (torch.cuda.current_stream().cuda_stream) so the native module never
+// links libtorch; the ops run stream-ordered with torch's own work.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include <vector>
+
+#include "gpu/gpu.h"
+#include "gpu/kernels.h"
+
+namespace py = pybind11;
+using namespace mrpc;
+
+static hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void check(int rc, const char* what) {
+    if (rc != 0) throw std::runtime_error(std::string(what) + " failed: " + hipGetErrorString(hipGetLastError()));
+}
+
+void bind_gpu_ops(py::module_& g) {
+    g.def("crc32c_launch", [](const std::vector<uintptr_t>& ptrs, const std::vector<uint64_t>& lens, uintptr_t out,
+                              uintptr_t stream) {
+        if (ptrs.size() != lens.size()) throw std::invalid_argument("ptrs/lens size mismatch");
+        std::vector<gpu::Segment> segs(ptrs.size());
+        for (size_t i = 0; i < ptrs.size(); ++i) segs[i] = gpu::Segment{(const void*)ptrs[i], nullptr, lens[i]};
+        check(gpu::LaunchCrc32c(segs.data(), (int)segs.size(), (uint32_t*)out, as_stream(stream)), "crc32c");
+    }, py::arg("ptrs"), py::arg("lens"), py::arg("out"), py::arg("stream") = 0);
+    g.def("crc32c_sync", [](uintptr_t ptr, uint64_t len, int device) {
+        uint32_t out = 0;
+        const void* p = (const void*)ptr;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::Crc32cDevice(&p, &len, 1, &out, device);
+        }
+        check(rc, "crc32c_sync");
+        return out;
+    }, py::arg("ptr"), py::arg("len"), py::arg("device") = -1);
+    g.def("batched_copy_launch", [](const std::vector<uintptr_t>& srcs, const std::vector<uintptr_t>& dsts,
+                                    const std::vector<uint64_t>& lens, uintptr_t stream) {
+        if (srcs.size() != lens.size() || dsts.size() != lens.size()) throw std::invalid_argument("size mismatch");
+        std::vector<gpu::Segment> segs(lens.size());
+        for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
+        check(gpu::LaunchBatchedCopy(segs.data(), (int)segs.size(), as_stream(stream)), "batched_copy");
+    }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("stream") = 0);
+    g.def("varint_scratch_bytes", &gpu::VarintScratchBytes);
+    g.def("varint_decode_launch", [](uintptr_t in, uint64_t n, uintptr_t out, uint64_t max_out, bool zigzag,
+                                     uintptr_t count, uintptr_t err, uintptr_t scratch, uintptr_t stream) {
+        check(gpu::LaunchVarintDecode((const uint8_t*)in, n, (uint64_t*)out, max_out, zigzag, (uint64_t*)count,
+                                      (int*)err, (void*)scratch, as_stream(stream)),
+              "varint_decode");
+    });
+    g.def("varint_encode_launch", [](uintptr_t in, uint64_t n, bool zigzag, uintptr_t out, uintptr_t nbytes,
+                                     uintptr_t scratch, uintptr_t stream) {
+        check(gpu::LaunchVarintEncode((const uint64_t*)in, n, zigzag, (uint8_t*)out, (uint64_t*)nbytes,
+                                      (void*)scratch, as_stream(stream)),
+              "varint_encode");
+    });
+}

@@ -1,0 +1,268 @@
+// pybind11 bindings: the Python face of the native runtime (bench.py,
+// tests, and torch-side GPU ops). Every call that can block drops the GIL.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <sstream>
+
+#include "base/crc32c.h"
+#include "base/flags.h"
+#include "base/logging.h"
+#include "fiber/fiber.h"
+#include "gpu/gpu.h"
+#include "mrpc/proto/echo.pb.h"
+#include "press/press.h"
+#include "rpc/channel.h"
+#include "rpc/controller.h"
+#include "rpc/protocol.h"
+#include "rpc/server.h"
+#include "services/echo_service.h"
+#include "var/variable.h"
+
+namespace py = pybind11;
+using namespace mrpc;
+
+void bind_gpu_ops(py::module_& m);  // gpu_ops.cc
+
+namespace {
+
+class PyServer {
+public:
+    PyServer() { GlobalInitializeOrDie(); }
+    ~PyServer() { stop(); }
+    void add_echo_service() {
+        if (!_echo) {
+            _echo.reset(new EchoServiceImpl);
+            if (_server.AddService(_echo.get(), SERVER_DOESNT_OWN_SERVICE) != 0) throw std::runtime_error("AddService failed");
+        }
+    }
+    int start(const std::string& addr, int num_threads, int gpu_device, int idle_timeout_s) {
+        ServerOptions opt;
+        opt.num_threads = num_threads;
+        opt.gpu_device = gpu_device;
+        opt.idle_timeout_sec = idle_timeout_s;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = addr.find(':') == std::string::npos ? _server.Start(std::stoi(addr), &opt)
+                                                     : _server.Start(addr.c_str(), &opt);
+        }
+        if (rc != 0) throw std::runtime_error("fail to start server on " + addr);
+        _running = true;
+        return _server.listen_address().port;
+    }
+    void stop() {
+        if (!_running) return;
+        py::gil_scoped_release nogil;
+        _server.Stop(0);
+        _server.Join();
+        _running = false;
+    }
+    int port() const { return _server.listen_address().port; }
+    std::string address() const { return _server.listen_address().to_string(); }
+    int64_t echo_calls() const { return _echo ? _echo->ncalls() : 0; }
+
+private:
+    Server _server;
+    std::unique_ptr<EchoServiceImpl> _echo;
+    bool _running = false;
+};
+
+class PyChannel {
+public:
+    PyChannel(const std::string& server, const std::string& lb, const std::string& protocol,
+              const std::string& connection_type, int timeout_ms, int max_retry) {
+        GlobalInitializeOrDie();
+        ChannelOptions o;
+        o.protocol = protocol;
+        o.connection_type = connection_type;
+        o.timeout_ms = timeout_ms;
+        o.max_retry = max_retry;
+        const int rc = lb.empty() ? _ch.Init(server.c_str(), &o) : _ch.Init(server.c_str(), lb.c_str(), &o);
+        if (rc != 0) throw std::runtime_error("fail to init channel to " + server);
+    }
+    // Returns (message, attachment, latency_us); raises on RPC failure.
+    py::tuple echo(const std::string& message, py::bytes attachment, int64_t sleep_us) {
+        example::EchoRequest req;
+        example::EchoResponse res;
+        Controller cntl;
+        req.set_message(message);
+        if (sleep_us > 0) req.set_sleep_us(sleep_us);
+        std::string att = attachment;
+        cntl.request_attachment().append(att);
+        {
+            py::gil_scoped_release nogil;
+            example::EchoService_Stub stub(&_ch);
+            stub.Echo(&cntl, &req, &res, nullptr);
+        }
+        if (cntl.Failed()) {
+            throw std::runtime_error("[E" + std::to_string(cntl.ErrorCode()) + "] " + cntl.ErrorText());
+        }
+        return py::make_tuple(res.message(), py::bytes(cntl.response_attachment().to_string()), cntl.latency_us());
+    }
+
+private:
+    Channel _ch;
+};
+
+press::PressOptions press_options(const py::dict& d) {
+    press::PressOptions o;
+    for (auto item : d) {
+        const std::string k = py::str(item.first);
+        py::handle v = item.second;
+        if (k == "server") o.server = v.cast<std::string>();
+        else if (k == "lb_policy") o.lb_policy = v.cast<std::string>();
+        else if (k == "protocol") o.protocol = v.cast<std::string>();
+        else if (k == "connection_type") o.connection_type = v.cast<std::string>();
+        else if (k == "timeout_ms") o.timeout_ms = v.cast<int>();
+        else if (k == "connect_timeout_ms") o.connect_timeout_ms = v.cast<int>();
+        else if (k == "max_retry") o.max_retry = v.cast<int>();
+        else if (k == "request_compress_type") o.request_compress_type = v.cast<int>();
+        else if (k == "response_compress_type") o.response_compress_type = v.cast<int>();
+        else if (k == "concurrency") o.concurrency = v.cast<int>();
+        else if (k == "qps") o.qps = v.cast<double>();
+        else if (k == "num_channels") o.num_channels = v.cast<int>();
+        else if (k == "request_size") o.request_size = v.cast<int>();
+        else if (k == "attachment_size") o.attachment_size = v.cast<int>();
+        else if (k == "device_attachment") o.device_attachment = v.cast<bool>();
+        else if (k == "gpu_device") o.gpu_device = v.cast<int>();
+        else if (k == "check_echo") o.check_echo = v.cast<bool>();
+        else if (k == "proto_file") o.proto_file = v.cast<std::string>();
+        else if (k == "include_paths") o.include_paths = v.cast<std::string>();
+        else if (k == "method") o.method = v.cast<std::string>();
+        else if (k == "input") o.input = v.cast<std::string>();
+        else throw std::invalid_argument("unknown press option: " + k);
+    }
+    return o;
+}
+
+py::dict snapshot_dict(const press::Snapshot& s) {
+    py::dict d;
+    d["sent"] = s.sent;
+    d["success"] = s.success;
+    d["error"] = s.error;
+    d["elapsed_s"] = s.elapsed_s;
+    d["qps"] = s.qps;
+    d["avg_us"] = s.avg_us;
+    d["min_us"] = s.min_us;
+    d["p50_us"] = s.p50_us;
+    d["p70_us"] = s.p70_us;
+    d["p90_us"] = s.p90_us;
+    d["p95_us"] = s.p95_us;
+    d["p97_us"] = s.p97_us;
+    d["p99_us"] = s.p99_us;
+    d["p999_us"] = s.p999_us;
+    d["p9999_us"] = s.p9999_us;
+    d["max_us"] = s.max_us;
+    d["bytes"] = s.bytes;
+    d["last_error_code"] = s.last_error_code;
+    d["last_error"] = s.last_error;
+    return d;
+}
+
+class PyPress {
+public:
+    explicit PyPress(const py::dict& d) {
+        GlobalInitializeOrDie();
+        press::PressOptions o = press_options(d);
+        std::string err;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = _s.Init(o, &err);
+        }
+        if (rc != 0) throw std::runtime_error("press init failed: " + err);
+    }
+    void run_requests(int64_t n) {
+        py::gil_scoped_release nogil;
+        _s.RunRequests(n);
+    }
+    void run_for(double seconds) {
+        py::gil_scoped_release nogil;
+        _s.RunFor(seconds, nullptr);
+    }
+    py::dict stats() const { return snapshot_dict(_s.Stats()); }
+    void reset_stats() { _s.ResetStats(); }
+
+private:
+    press::PressSession _s;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+    m.doc() = "brpc_amd native runtime (fibers, RPC, press, MI355X device ops)";
+    m.def("global_init", [] { GlobalInitializeOrDie(); });
+    m.def("set_concurrency", [](int n) { return fiber::set_concurrency(n); });
+    m.def("get_concurrency", [] { return fiber::get_concurrency(); });
+    m.def("set_flag", [](const std::string& name, const std::string& value) {
+        std::string err;
+        if (!SetFlag(name, value, false, &err)) throw std::invalid_argument("set_flag " + name + ": " + err);
+    });
+    m.def("get_flag", [](const std::string& name) {
+        std::string v;
+        if (!GetFlag(name, &v)) throw std::invalid_argument("no flag " + name);
+        return v;
+    });
+    m.def("list_flags", [] {
+        py::dict d;
+        for (auto& f : ListFlags()) d[py::str(f.name)] = f.current_value;
+        return d;
+    });
+    m.def("dump_vars", [](const std::string& filter) {
+        std::vector<std::pair<std::string, std::string>> out;
+        var::Variable::dump_exposed(&out, filter);
+        py::dict d;
+        for (auto& kv : out) d[py::str(kv.first)] = kv.second;
+        return d;
+    }, py::arg("filter") = "");
+    m.def("dump_prometheus", [] { return var::Variable::dump_prometheus(); });
+    m.def("crc32c", [](py::bytes b) {
+        std::string s = b;
+        return crc32c::Value(s.data(), s.size());
+    });
+    m.def("fiber_stats", [] {
+        py::dict d;
+        d["fibers"] = fiber::fiber_count();
+        d["switches"] = fiber::switch_count();
+        d["steals"] = fiber::steal_count();
+        d["workers"] = fiber::get_concurrency();
+        return d;
+    });
+
+    py::class_<PyServer>(m, "Server")
+        .def(py::init<>())
+        .def("add_echo_service", &PyServer::add_echo_service)
+        .def("start", &PyServer::start, py::arg("addr"), py::arg("num_threads") = -1, py::arg("gpu_device") = -1,
+             py::arg("idle_timeout_s") = -1)
+        .def("stop", &PyServer::stop)
+        .def_property_readonly("port", &PyServer::port)
+        .def_property_readonly("address", &PyServer::address)
+        .def_property_readonly("echo_calls", &PyServer::echo_calls);
+
+    py::class_<PyChannel>(m, "Channel")
+        .def(py::init<const std::string&, const std::string&, const std::string&, const std::string&, int, int>(),
+             py::arg("server"), py::arg("lb") = "", py::arg("protocol") = "baidu_std",
+             py::arg("connection_type") = "", py::arg("timeout_ms") = 1000, py::arg("max_retry") = 3)
+        .def("echo", &PyChannel::echo, py::arg("message"), py::arg("attachment") = py::bytes(),
+             py::arg("sleep_us") = 0);
+
+    py::class_<PyPress>(m, "Press")
+        .def(py::init<const py::dict&>())
+        .def("run_requests", &PyPress::run_requests)
+        .def("run_for", &PyPress::run_for)
+        .def("stats", &PyPress::stats)
+        .def("reset_stats", &PyPress::reset_stats);
+
+    py::module_ g = m.def_submodule("gpu", "MI355X device runtime");
+    g.def("device_count", [] { return gpu::DeviceCount(); });
+    g.def("available", [] { return gpu::Available(); });
+    g.def("init", [](int dev) {
+        std::string err;
+        if (gpu::Init(dev, &err) != 0) throw std::runtime_error(err);
+    }, py::arg("device") = -1);
+    g.def("device_arch", [](int dev) { return gpu::DeviceArch(dev); }, py::arg("device") = 0);
+    g.def("device_name", [](int dev) { return gpu::DeviceName(dev); }, py::arg("device") = 0);
+    g.def("polled_events", [] { return gpu::PolledEvents(); });
+    bind_gpu_ops(g);
+}

@@ -1,0 +1,19 @@
+"""One-launch gather/scatter of many byte ranges (Buf blocks -> HBM)."""
+from ..native import native
+from ._common import nbytes, require_gpu_tensor, stream_handle
+
+
+def batched_copy(srcs, dsts):
+    """dsts[i][:] = srcs[i][:] (byte copies) in one kernel launch per 32 pairs."""
+    if len(srcs) != len(dsts):
+        raise ValueError("srcs/dsts length mismatch")
+    for s, d in zip(srcs, dsts):
+        require_gpu_tensor(s, "src")
+        require_gpu_tensor(d, "dst")
+        if nbytes(d) < nbytes(s):
+            raise ValueError("destination smaller than source")
+    if not srcs:
+        return
+    dev = srcs[0].device
+    native.gpu.batched_copy_launch([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts],
+                                   [nbytes(s) for s in srcs], stream_handle(dev))

@@ -1,0 +1,5 @@
+"""One process per GPU over torch.distributed (backend "nccl" = RCCL on
+ROCm): rank topology, peer address exchange and cross-rank reductions used
+by the benchmarks and by the xGMI device transport's handshake."""
+from .topology import (Topology, init_distributed, exchange_addresses, ring_peer, barrier,  # noqa: F401
+                       allreduce_max, allreduce_sum, destroy)

@@ -1,0 +1,99 @@
+"""Rank topology for one-process-per-GPU jobs.
+
+torchrun exports RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT; with a
+GPU the process group uses RCCL ("nccl"), otherwise gloo (CPU tests).
+Barriers and reductions are tiny control-plane collectives; the RPC data
+itself moves over the framework's own transports (TCP loopback or the
+xGMI device transport), not through RCCL.
+"""
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Topology:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    local_world_size: int = 1
+    device: int = -1          # GPU ordinal, -1 on CPU-only hosts
+    backend: str = ""
+
+    @property
+    def distributed(self):
+        return self.world_size > 1
+
+
+def init_distributed(prefer_gpu=True):
+    """Initialise from torchrun's env; a no-op single-rank topology when
+    WORLD_SIZE is unset or 1."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    lrank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+    use_gpu = prefer_gpu and torch.cuda.is_available()
+    device = -1
+    if use_gpu:
+        device = lrank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+    backend = ""
+    if ws > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if use_gpu else "gloo"
+        kw = {}
+        if use_gpu:
+            kw["device_id"] = torch.device("cuda", device)
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws, **kw)
+    elif dist.is_initialized():
+        backend = dist.get_backend()
+    return Topology(rank, ws, lrank, lws, device, backend)
+
+
+def _tensor(x, topo):
+    dev = torch.device("cuda", topo.device) if topo.backend == "nccl" else torch.device("cpu")
+    return torch.tensor([x], dtype=torch.float64, device=dev)
+
+
+def barrier(topo):
+    if topo.distributed:
+        if topo.backend == "nccl":
+            dist.barrier(device_ids=[topo.device])
+        else:
+            dist.barrier()
+
+
+def allreduce_max(x, topo):
+    if not topo.distributed:
+        return float(x)
+    t = _tensor(x, topo)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(x, topo):
+    if not topo.distributed:
+        return float(x)
+    t = _tensor(x, topo)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def exchange_addresses(addr, topo):
+    """All ranks' server addresses, indexed by rank."""
+    if not topo.distributed:
+        return [addr]
+    out = [None] * topo.world_size
+    dist.all_gather_object(out, addr)
+    return out
+
+
+def ring_peer(topo, hop=1):
+    return (topo.rank + hop) % topo.world_size
+
+
+def destroy(topo):
+    if topo.distributed and dist.is_initialized():
+        dist.destroy_process_group()

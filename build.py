@@ -88,7 +88,7 @@ def main():
 
     cxxflags = (f"-std=c++17 {opt} {san} -fPIC -pthread -march=x86-64-v2 -mpclmul "
                 f"-Wall -Wno-unused-function -Wno-invalid-offsetof -Wno-unused-variable "
-                f"-Wno-sign-compare -Wno-class-memaccess -Wno-unused-but-set-variable "
+                f"-Wno-sign-compare -Wno-class-memaccess -Wno-unused-but-set-variable -Wno-unused-result "
                 f"-D__HIP_PLATFORM_AMD__ -DMRPC_GPU_ARCH=\\\"{ARCH}\\\" "
                 f"-I{rel(CSRC)} -I{rel(GEN)} -isystem {ROCM}/include")
     hipflags = (f"-std=c++17 -O3 -g1 -fPIC --offload-arch={ARCH} -munsafe-fp-atomics "

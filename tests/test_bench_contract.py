@@ -1,0 +1,41 @@
+"""bench.py prints exactly one JSON line with the driver's contract keys;
+the distributed path (ring over ranks) is exercised with gloo on CPU."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+        "scaling", "vs_baseline", "dtype", "data", "config"}
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_bench_single_rank():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--requests-per-step", "2000", "--latency-sample-s", "0.3"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    assert KEYS <= set(j)
+    assert j["n_gpus"] == 1 and j["steps"] == 3 and j["value"] > 0 and j["errors"] == 0
+    assert j["config"]["seq_len"] == 32
+
+
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29517",
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--requests-per-step", "1000", "--latency-sample-s", "0.3", "--workers", "2"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    j = lines[0]
+    assert j["n_gpus"] == 2 and j["value"] > 0 and j["errors"] == 0

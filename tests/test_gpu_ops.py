@@ -1,0 +1,101 @@
+"""Numerics of the gfx950 kernels against host references (CPU crc32c via
+SSE4.2, pure-python varint codec), plus the device-payload echo path."""
+import random
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from brpc_amd import native
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    assert native.gpu.device_count() > 0, "native runtime sees no HIP device"
+    assert native.gpu.device_arch(0) == "gfx950"
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 63, 64, 65, 1000, 16383, 16384, 16385, 65536, 100003, 1 << 20, (1 << 24) + 5])
+def test_crc32c_matches_host(dev, n):
+    from brpc_amd.ops import crc32c, crc32c_host
+    g = torch.Generator().manual_seed(n)
+    host = torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g)
+    assert crc32c(host.to(dev)) == crc32c_host(host.numpy().tobytes())
+
+
+def test_crc32c_known_vector(dev):
+    from brpc_amd.ops import crc32c
+    t = torch.tensor(list(b"123456789"), dtype=torch.uint8, device=dev)
+    assert crc32c(t) == 0xE3069283
+
+
+def test_crc32c_unaligned_views_and_batch(dev):
+    from brpc_amd.ops import crc32c_batch, crc32c_host
+    base = torch.randint(0, 256, (300000,), dtype=torch.uint8, device=dev)
+    views = [base[o:o + l] for o, l in [(1, 5000), (3, 70000), (17, 16384), (0, 1), (5, 0)]] * 10  # 50 > 32 inline
+    got = crc32c_batch(views).tolist()
+    want = [crc32c_host(v.cpu().numpy().tobytes()) for v in views]
+    assert got == want
+
+
+def test_varint_roundtrip(dev):
+    from brpc_amd.ops import varint_decode, varint_encode, varint_encode_host
+    rnd = random.Random(1)
+    vals = [0, 1, 127, 128, 300, 2**31 - 1, -1, -(2**63), 2**63 - 1] + \
+        [rnd.randrange(-(2**63), 2**63) >> rnd.randrange(0, 63) for _ in range(20000)]
+    t = torch.tensor(vals, dtype=torch.int64, device=dev)
+    enc = varint_encode(t)
+    assert enc.cpu().numpy().tobytes() == varint_encode_host(vals)
+    dec = varint_decode(enc)
+    assert dec.cpu().tolist() == vals
+
+
+def test_varint_zigzag(dev):
+    from brpc_amd.ops import varint_decode, varint_encode, varint_encode_host
+    vals = list(range(-5000, 5000, 7))
+    t = torch.tensor(vals, dtype=torch.int64, device=dev)
+    enc = varint_encode(t, zigzag=True)
+    assert enc.cpu().numpy().tobytes() == varint_encode_host(vals, zigzag=True)
+    assert varint_decode(enc, zigzag=True).cpu().tolist() == vals
+
+
+def test_varint_malformed(dev):
+    from brpc_amd.ops import varint_decode
+    bad = torch.tensor([0x80] * 12 + [0x01], dtype=torch.uint8, device=dev)
+    with pytest.raises(ValueError):
+        varint_decode(bad)
+    trunc = torch.tensor([0x05, 0x80], dtype=torch.uint8, device=dev)
+    with pytest.raises(ValueError):
+        varint_decode(trunc)
+
+
+def test_batched_copy(dev):
+    from brpc_amd.ops import batched_copy
+    srcs = [torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev) for n in (1, 15, 16, 4097, 70000, 1 << 20)]
+    dsts = [torch.zeros_like(s) for s in srcs]
+    batched_copy(srcs, dsts)
+    torch.cuda.synchronize()
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(s, d)
+    # unaligned
+    big = torch.randint(0, 256, (10000,), dtype=torch.uint8, device=dev)
+    out = torch.zeros(10000, dtype=torch.uint8, device=dev)
+    batched_copy([big[3:9003]], [out[5:9005]])
+    torch.cuda.synchronize()
+    assert torch.equal(big[3:9003], out[5:9005])
+
+
+def test_device_payload_echo(dev):
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        p = native.Press({"server": s.address, "concurrency": 8, "attachment_size": 65536,
+                          "device_attachment": True, "gpu_device": 0, "check_echo": True})
+        p.run_requests(500)
+        st = p.stats()
+        assert st["success"] == 500 and st["error"] == 0, st
+    finally:
+        s.stop()

@@ -1,0 +1,88 @@
+"""Python-facing RPC surface: Server/Channel/Press over loopback."""
+import pytest
+
+
+def test_echo_roundtrip(native, echo_server):
+    ch = native.Channel(echo_server.address)
+    msg, att, lat = ch.echo("hello", b"\x00\x01payload")
+    assert msg == "hello"
+    assert att == b"\x00\x01payload"
+    assert lat >= 0
+
+
+def test_echo_large_attachment(native, echo_server):
+    ch = native.Channel(echo_server.address)
+    blob = bytes(range(256)) * 4096  # 1 MiB
+    _, att, _ = ch.echo("big", blob)
+    assert att == blob
+
+
+def test_timeout_raises(native, echo_server):
+    ch = native.Channel(echo_server.address, timeout_ms=50, max_retry=0)
+    with pytest.raises(RuntimeError, match="E1008|timed out|Reached timeout"):
+        ch.echo("slow", b"", sleep_us=300000)
+
+
+def test_connection_refused(native):
+    ch = native.Channel("127.0.0.1:1", timeout_ms=200, max_retry=0)
+    with pytest.raises(RuntimeError):
+        ch.echo("x")
+
+
+def test_press_closed_loop(native, echo_server):
+    p = native.Press({"server": echo_server.address, "concurrency": 16, "request_size": 32,
+                      "check_echo": True})
+    p.run_requests(5000)
+    st = p.stats()
+    assert st["success"] == 5000 and st["error"] == 0
+    assert 0 < st["p50_us"] <= st["p99_us"] <= st["max_us"]
+    assert st["qps"] > 1000
+
+
+def test_press_attachment_checked(native, echo_server):
+    p = native.Press({"server": echo_server.address, "concurrency": 4, "attachment_size": 65536,
+                      "check_echo": True})
+    p.run_requests(200)
+    st = p.stats()
+    assert st["success"] == 200, st
+
+
+def test_press_open_loop_qps(native, echo_server):
+    p = native.Press({"server": echo_server.address, "qps": 200.0, "concurrency": 2})
+    p.run_for(1.0)
+    st = p.stats()
+    assert 120 <= st["success"] <= 260, st
+
+
+def test_press_pooled_and_short(native, echo_server):
+    for ct in ("pooled", "short"):
+        p = native.Press({"server": echo_server.address, "concurrency": 8, "connection_type": ct})
+        p.run_requests(400)
+        assert p.stats()["success"] == 400
+
+
+def test_press_generic_proto(native, echo_server, tmp_path):
+    proto = tmp_path / "echo2.proto"
+    proto.write_text('''
+syntax = "proto2";
+package example;
+message EchoRequest { required string message = 1; optional int64 sleep_us = 2; }
+message EchoResponse { required string message = 1; }
+service EchoService { rpc Echo(EchoRequest) returns (EchoResponse); }
+''')
+    p = native.Press({"server": echo_server.address, "concurrency": 4, "proto_file": str(proto),
+                      "method": "example.EchoService.Echo",
+                      "input": '{"message": "a"} {"message": "bb"}'})
+    p.run_requests(100)
+    assert p.stats()["success"] == 100
+
+
+def test_flags_and_vars(native, echo_server):
+    from brpc_amd.utils import dump_vars, get_flag, list_flags, set_flag
+    assert "fiber_concurrency" in list_flags()
+    set_flag("log_unknown_protocol", True)
+    assert get_flag("log_unknown_protocol") == "true"
+    set_flag("log_unknown_protocol", False)
+    v = dump_vars("*")
+    assert len(v) > 10
+    assert "rpc" in native.dump_prometheus() or len(native.dump_prometheus()) > 0
