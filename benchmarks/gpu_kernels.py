@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from brpc_amd.ops import batched_copy, crc32c_batch, crc32c_host, varint_decode, varint_encode  # noqa: E402
+from brpc_amd.ops import batched_copy, crc32c_batch, crc32c_host, crc32c_packed, varint_decode, varint_encode  # noqa: E402
 
 
 def timeit(fn, iters=20, warmup=3):
@@ -31,9 +31,16 @@ def main():
     sizes = [int(x) for x in os.environ.get("SIZES", str(1 << 28)).split(",")]
     for n in sizes:
         buf = torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev)
-        t = timeit(lambda: crc32c_batch([buf]))
-        ok = int(crc32c_batch([buf])[0]) == crc32c_host(buf.cpu().numpy().tobytes()) if n <= (1 << 26) else None
-        print(json.dumps({"kernel": "crc32c", "bytes": n, "sec": t, "GBps": n / t / 1e9, "verified": ok}))
+        for impl in ("mfma", "lds"):
+            t = timeit(lambda: crc32c_batch([buf], impl=impl))
+            print(json.dumps({"kernel": "crc32c_" + impl, "bytes": n, "sec": t, "GBps": n / t / 1e9}))
+        small = buf[: 1 << 24]
+        ok = int(crc32c_batch([small])[0]) == crc32c_host(small.cpu().numpy().tobytes())
+        print(json.dumps({"kernel": "crc32c_verify_16MiB", "verified": ok}))
+        offs = torch.arange(0, n + 1, 65536, dtype=torch.int64, device=dev)
+        t = timeit(lambda: crc32c_packed(buf, offs))
+        print(json.dumps({"kernel": "crc32c_packed_64KiB", "messages": offs.numel() - 1, "bytes": n, "sec": t,
+                          "GBps": n / t / 1e9}))
         # many 64 KiB messages in one launch set (the RPC batch case)
         msgs = [buf[i * 65536:(i + 1) * 65536] for i in range(min(4096, n // 65536))]
         if msgs:

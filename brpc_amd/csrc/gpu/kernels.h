@@ -23,8 +23,16 @@ constexpr int kInlineSegments = 32;
 // Bytes covered by one workgroup (256 lanes x 64 bytes).
 constexpr uint64_t kChunkBytes = 16384;
 
-// Standard (finalized) CRC32C of every segment into out_dev[i].
-// out_dev must be device memory; it is zeroed by the launch.
+// Standard (finalized) CRC32C of every segment into out_dev[i] — the
+// MFMA (GF(2) matmul on v_mfma_i32_32x32x32_i8) kernel. Segment table lives
+// in device memory: starts_dev[i] = address, lens_dev[i] = bytes.
+// total_bytes bounds the sum of lengths (sizes the grid); max_seg_len
+// bounds any one length. scratch: Crc32cScratchBytes(nseg) of device memory.
+size_t Crc32cScratchBytes(int64_t nseg);
+int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, int64_t nseg, uint64_t total_bytes,
+                         uint64_t max_seg_len, uint32_t* out_dev, void* scratch, hipStream_t s);
+// Same result from the LDS slicing-by-8 kernel (segments passed inline;
+// kept as an independent implementation for cross-checks and A/B timing).
 int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s);
 // Copy every segment src -> dst (one launch for many small copies).
 int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s);

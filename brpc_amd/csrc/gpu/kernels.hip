@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "gpu/kernels.h"
 
@@ -174,6 +176,141 @@ __global__ void __launch_bounds__(kThreads) batched_copy_kernel(SegBatch b) {
         }
     } else {
         for (uint64_t off = cbeg + threadIdx.x; off < cend; off += kThreads) dst[off] = src[off];
+    }
+}
+
+// ---------------------------------------------------------------- CRC32C on MFMA
+//
+// CRC32C over GF(2) is linear in the message bits, so the CRC of a 64-byte
+// block is a 32x512 bit-matrix times the block's bits. That product runs on
+// the int8 matrix cores: v_mfma_i32_32x32x32_i8 with
+//   A[r][k] = bit r of the CRC contribution of block-bit k   (constant)
+//   B[k][c] = block-bit k of column c (0/1 bytes expanded from the data)
+//   D[r][c] = number of set bits whose contribution has bit r
+// and the CRC bit is the parity of D. One wave owns a 2 KiB group = 32
+// columns x 64 B per pass (16 MFMAs, K = 512 bits). Lane (c, h) holds column
+// c's bytes [32h, 32h+32), loaded as two 16 B vectors; because A and B share
+// the same k order inside a lane half, the bit->k assignment never needs the
+// exact fragment layout. Columns are folded across the wave-chunk (32
+// groups = 64 KiB) with a Horner step whose constant (x^(8*2048)) is applied
+// through four LDS byte tables, then each lane applies its column shift
+// x^(512*(31-c)) once per chunk and the wave XOR-reduces. Chunks fold into
+// the segment result with one atomicXor (order-free, like the LDS kernel).
+typedef signed char i8x16 __attribute__((ext_vector_type(16)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kGroupBytes = 2048;                       // 32 columns x 64 B
+constexpr int kGroupsPerChunk = 32;
+constexpr uint64_t kMfmaChunk = (uint64_t)kGroupBytes * kGroupsPerChunk;  // 64 KiB per wave
+
+struct CrcMfmaConsts {
+    i8x16 afrag[16][64];     // A fragments, [mfma j][lane]
+    uint32_t t2k[4][256];    // byte tables of "multiply by x^(8*2048)"
+    uint32_t lane_shift[32]; // x^(512*(31-c))
+    uint32_t xl[256];        // x^(8r), r < 256
+    uint32_t xm[256];        // x^(8*256*q), q < 256
+};
+
+__device__ __forceinline__ i8x16 expand16(uint32_t bits) {
+    union {
+        uint32_t u[4];
+        i8x16 v;
+    } r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.u[q] = (((bits >> (4 * q)) & 0xFu) * 0x00204081u) & 0x01010101u;
+    return r.v;
+}
+
+__global__ void __launch_bounds__(kThreads) crc32c_mfma_kernel(
+    const uint64_t* __restrict__ starts, const uint64_t* __restrict__ lens, const uint64_t* __restrict__ chunk_start,
+    int64_t nseg, const CrcMfmaConsts* __restrict__ K, const uint32_t* __restrict__ xc, uint32_t* __restrict__ out) {
+    __shared__ uint32_t t2k[4][256];
+    for (int i = threadIdx.x; i < 1024; i += kThreads) (&t2k[0][0])[i] = (&K->t2k[0][0])[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int c = lane & 31;
+    const int h = lane >> 5;
+    i8x16 a[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = K->afrag[j][lane];
+    const uint32_t lshift = K->lane_shift[c];
+    const uint64_t total = chunk_start[nseg];
+    const uint64_t nwaves = (uint64_t)gridDim.x * (kThreads / 64);
+    for (uint64_t chunk = (uint64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6); chunk < total;
+         chunk += nwaves) {
+        int64_t lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi + 1) >> 1;
+            if (chunk_start[mid] <= chunk) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t seg = lo;
+        const uint64_t len = lens[seg];
+        const uint8_t* base = reinterpret_cast<const uint8_t*>(starts[seg]);
+        const uint64_t nch = chunk_start[seg + 1] - chunk_start[seg];
+        const uint64_t k = chunk - chunk_start[seg];
+        const uint64_t after = nch - 1 - k;
+        const int64_t chunk_end = (int64_t)len - (int64_t)(after * kMfmaChunk);
+        const bool aligned = ((reinterpret_cast<uintptr_t>(base) + len) & 15) == 0;
+        uint32_t acc = 0;
+        for (int g = 0; g < kGroupsPerChunk; ++g) {
+            const int64_t gend = chunk_end - (int64_t)(kGroupsPerChunk - 1 - g) * kGroupBytes;
+            if (gend <= 0) continue;  // wave-uniform: whole group precedes the segment
+            const int64_t lbeg = gend - kGroupBytes + 64 * c + 32 * h;
+            uint32_t w[8];
+            if (lbeg >= 0 && aligned) {
+                const uint4* p = reinterpret_cast<const uint4*>(base + lbeg);
+                const uint4 v0 = p[0], v1 = p[1];
+                w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w;
+                w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
+            } else {
+                // leading partial group or unaligned end: bytes before the
+                // segment read as zero (a zero prefix leaves the CRC unchanged)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w[i] = 0;
+                for (int b = 0; b < 32; ++b) {
+                    const int64_t off = lbeg + b;
+                    if (off >= 0) w[b >> 2] |= (uint32_t)base[off] << (8 * (b & 3));
+                }
+            }
+            i32x16 d = {0};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t bits = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                d = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[j], expand16(bits), d, 0, 0, 0);
+            }
+            // D layout: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+            uint32_t part = 0;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                part |= ((uint32_t)d[reg] & 1u) << row;
+            }
+            const uint32_t crc_c = part | __shfl_xor(part, 32, 64);
+            acc = t2k[0][acc & 0xff] ^ t2k[1][(acc >> 8) & 0xff] ^ t2k[2][(acc >> 16) & 0xff] ^ t2k[3][acc >> 24] ^
+                  crc_c;
+        }
+        uint32_t v = mult_mod_p(lshift, acc);
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+        if (lane == 0) {
+            if (after) v = mult_mod_p(xc[after], v);
+            if (k == 0) {
+                // fold the ~0 initial register and the final inversion
+                const uint32_t x8len = mult_mod_p(mult_mod_p(xc[len / kMfmaChunk], K->xm[(len % kMfmaChunk) >> 8]),
+                                                  K->xl[len & 0xff]);
+                v ^= mult_mod_p(x8len, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+            }
+            atomicXor(out + seg, v);
+        }
+    }
+}
+
+__global__ void crc_chunk_count_kernel(const uint64_t* __restrict__ lens, int64_t nseg, uint64_t* __restrict__ cs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nseg) {
+        const uint64_t n = (lens[i] + kMfmaChunk - 1) / kMfmaChunk;
+        cs[i] = n ? n : 1;
     }
 }
 
@@ -357,21 +494,10 @@ uint32_t host_mult_mod_p(uint32_t a, uint32_t b) {
     return p;
 }
 
-struct DeviceTables {
-    uint32_t* t8 = nullptr;  // device copy of the slicing tables
-    bool ready = false;
-};
-
-DeviceTables g_tables[64];
-
-int ensure_tables() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
-    DeviceTables& dt = g_tables[dev];
-    if (dt.ready) return 0;
+const CrcTables& host_tables() {
     static CrcTables h;
-    static bool built = false;
-    if (!built) {
+    static std::once_flag once;
+    std::call_once(once, [] {
         for (uint32_t i = 0; i < 256; ++i) {
             uint32_t c = i;
             for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
@@ -380,31 +506,121 @@ int ensure_tables() {
         for (int s = 1; s < 8; ++s) {
             for (int i = 0; i < 256; ++i) h.t8[s][i] = (h.t8[s - 1][i] >> 8) ^ h.t8[0][h.t8[s - 1][i] & 0xff];
         }
-        // x2n[k] = x^(2^k) mod P; x^1 reflected = 1<<30
+        // x2n[k] = x^(2^k) mod P (reflected: x^0 = 1<<31, x^1 = 1<<30)
         uint32_t p = 1u << 30;
         for (int k = 0; k < 64; ++k) {
             h.x2n[k] = p;
             p = host_mult_mod_p(p, p);
         }
-        // lane_shift[j] = x^(8*64*j)
-        uint32_t step = 1u << 31;
-        {
-            // x^(512) = product of x2n bits of 512 = 2^9
-            step = h.x2n[9];
-        }
+        // lane_shift[j] = x^(8*64*j) = (x^512)^j
         uint32_t acc = 1u << 31;
         for (int j = 0; j < 256; ++j) {
             h.lane_shift[j] = acc;
-            acc = host_mult_mod_p(step, acc);
+            acc = host_mult_mod_p(h.x2n[9], acc);
         }
-        built = true;
+    });
+    return h;
+}
+
+// x^e mod P for an arbitrary bit exponent e
+uint32_t host_xpow(uint64_t e) {
+    const CrcTables& h = host_tables();
+    uint32_t r = 1u << 31;
+    for (int k = 0; e && k < 64; ++k, e >>= 1) {
+        if (e & 1) r = host_mult_mod_p(h.x2n[k], r);
     }
+    return r;
+}
+
+struct DeviceTables {
+    uint32_t* t8 = nullptr;           // slicing tables (LDS kernel)
+    CrcMfmaConsts* mfma = nullptr;    // MFMA kernel constants
+    uint32_t* xc = nullptr;           // x^(8*64KiB*m), m < xc_len
+    uint64_t xc_len = 0;
+    bool ready = false;
+};
+
+DeviceTables g_tables[64];
+std::mutex g_tables_mu;
+
+int ensure_tables_locked(int dev) {
+    DeviceTables& dt = g_tables[dev];
+    if (dt.ready) return 0;
+    const CrcTables& h = host_tables();
     if (hipMalloc(&dt.t8, sizeof(h.t8)) != hipSuccess) return -1;
     if (hipMemcpy(dt.t8, h.t8, sizeof(h.t8), hipMemcpyHostToDevice) != hipSuccess) return -1;
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_lane_shift), h.lane_shift, sizeof(h.lane_shift)) != hipSuccess) return -1;
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), h.x2n, sizeof(h.x2n)) != hipSuccess) return -1;
+    // ---- MFMA constants
+    static CrcMfmaConsts m;
+    static std::once_flag once;
+    std::call_once(once, [&h] {
+        // contribution of each of the 512 bits of a 64-byte block (zero-init
+        // register, no final inversion) = crc_raw0(block with that bit set)
+        static uint32_t contrib[512];
+        for (int b = 0; b < 512; ++b) {
+            uint8_t blk[64] = {0};
+            blk[b >> 3] = (uint8_t)(1u << (b & 7));
+            uint32_t reg = 0;
+            for (int i = 0; i < 64; ++i) reg = h.t8[0][(reg ^ blk[i]) & 0xff] ^ (reg >> 8);
+            contrib[b] = reg;
+        }
+        for (int j = 0; j < 16; ++j) {
+            for (int lane = 0; lane < 64; ++lane) {
+                const int r = lane & 31, hh = lane >> 5;
+                union {
+                    signed char c[16];
+                    i8x16 v;
+                } u;
+                for (int e = 0; e < 16; ++e) u.c[e] = (signed char)((contrib[256 * hh + 16 * j + e] >> r) & 1u);
+                m.afrag[j][lane] = u.v;
+            }
+        }
+        const uint32_t x2k = h.x2n[14];  // x^(8*2048) = x^(2^14)
+        for (int byte = 0; byte < 4; ++byte) {
+            for (int v = 0; v < 256; ++v) m.t2k[byte][v] = host_mult_mod_p(x2k, (uint32_t)v << (8 * byte));
+        }
+        for (int c = 0; c < 32; ++c) m.lane_shift[c] = host_xpow((uint64_t)512 * (31 - c));
+        for (int r = 0; r < 256; ++r) m.xl[r] = host_xpow((uint64_t)8 * r);
+        for (int q = 0; q < 256; ++q) m.xm[q] = host_xpow((uint64_t)8 * 256 * q);
+    });
+    if (hipMalloc(&dt.mfma, sizeof(m)) != hipSuccess) return -1;
+    if (hipMemcpy(dt.mfma, &m, sizeof(m), hipMemcpyHostToDevice) != hipSuccess) return -1;
     dt.ready = true;
     return 0;
+}
+
+int ensure_tables() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+    std::lock_guard<std::mutex> g(g_tables_mu);
+    return ensure_tables_locked(dev);
+}
+
+// Grow the per-device x^(8*64KiB*m) table to cover m < need. The old table
+// is kept alive (leaked) since in-flight kernels may still read it.
+const uint32_t* ensure_xc(uint64_t need) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(g_tables_mu);
+    if (ensure_tables_locked(dev) != 0) return nullptr;
+    DeviceTables& dt = g_tables[dev];
+    if (dt.xc_len >= need) return dt.xc;
+    uint64_t n = 1024;
+    while (n < need) n <<= 1;
+    std::vector<uint32_t> x(n);
+    const uint32_t step = host_tables().x2n[19];  // x^(8*65536) = x^(2^19)
+    uint32_t acc = 1u << 31;
+    for (uint64_t i = 0; i < n; ++i) {
+        x[i] = acc;
+        acc = host_mult_mod_p(step, acc);
+    }
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, n * sizeof(uint32_t)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, x.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    dt.xc = d;
+    dt.xc_len = n;
+    return d;
 }
 
 // Fill a SegBatch with up to kInlineSegments segments; returns chunk count.
@@ -441,6 +657,30 @@ int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;
+}
+
+size_t Crc32cScratchBytes(int64_t nseg) { return (size_t)(nseg + 1) * sizeof(uint64_t); }
+
+int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, int64_t nseg, uint64_t total_bytes,
+                         uint64_t max_seg_len, uint32_t* out_dev, void* scratch, hipStream_t s) {
+    if (nseg <= 0) return 0;
+    const uint32_t* xc = ensure_xc(max_seg_len / kMfmaChunk + 2);
+    if (!xc) return -1;
+    int dev = 0;
+    hipGetDevice(&dev);
+    uint64_t* cs = static_cast<uint64_t*>(scratch);
+    if (hipMemsetAsync(out_dev, 0, sizeof(uint32_t) * nseg, s) != hipSuccess) return -1;
+    hipLaunchKernelGGL(crc_chunk_count_kernel, dim3((uint32_t)((nseg + 255) / 256)), dim3(256), 0, s, lens_dev, nseg, cs);
+    hipLaunchKernelGGL(scan_tiles_kernel, dim3(1), dim3(1024), 0, s, cs, (uint64_t)nseg, cs + nseg);
+    // every segment has >= 1 chunk; the total is bounded by bytes/64KiB + nseg
+    const uint64_t bound = total_bytes / kMfmaChunk + (uint64_t)nseg;
+    const uint64_t waves_per_wg = kThreads / 64;
+    uint64_t grid = (bound + waves_per_wg - 1) / waves_per_wg;
+    if (grid > 256 * 8) grid = 256 * 8;  // persistent: <= 8 workgroups per CU, waves loop over chunks
+    if (grid == 0) grid = 1;
+    hipLaunchKernelGGL(crc32c_mfma_kernel, dim3((uint32_t)grid), dim3(kThreads), 0, s, starts_dev, lens_dev,
+                       (const uint64_t*)cs, nseg, (const CrcMfmaConsts*)g_tables[dev].mfma, xc, out_dev);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s) {

@@ -16,16 +16,32 @@ int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t*
     int prev = 0;
     hipGetDevice(&prev);
     if (prev != device) hipSetDevice(device);
-    std::vector<Segment> segs(n);
-    for (int i = 0; i < n; ++i) segs[i] = Segment{ptrs[i], nullptr, lens[i]};
-    int rc = -1;
-    uint32_t* out_dev = static_cast<uint32_t*>(Malloc(sizeof(uint32_t) * n, device));
-    hipStream_t s = PoolStream(device);
-    if (out_dev && s && LaunchCrc32c(segs.data(), n, out_dev, s) == 0 &&
-        hipMemcpyAsync(out_host, out_dev, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s) == hipSuccess) {
-        rc = SyncStream(s);
+    // one device allocation: [starts n][lens n][scratch n+1][out n (u32)]
+    std::vector<uint64_t> desc(2 * (size_t)n);
+    uint64_t total = 0, maxlen = 0;
+    for (int i = 0; i < n; ++i) {
+        desc[i] = reinterpret_cast<uint64_t>(ptrs[i]);
+        desc[n + i] = lens[i];
+        total += lens[i];
+        if (lens[i] > maxlen) maxlen = lens[i];
     }
-    Free(out_dev);
+    const size_t desc_bytes = desc.size() * sizeof(uint64_t);
+    const size_t bytes = desc_bytes + Crc32cScratchBytes(n) + sizeof(uint32_t) * n;
+    int rc = -1;
+    char* mem = static_cast<char*>(Malloc(bytes, device));
+    hipStream_t s = PoolStream(device);
+    if (mem && s) {
+        uint64_t* d_starts = reinterpret_cast<uint64_t*>(mem);
+        uint64_t* d_lens = d_starts + n;
+        void* scratch = mem + desc_bytes;
+        uint32_t* out_dev = reinterpret_cast<uint32_t*>(mem + desc_bytes + Crc32cScratchBytes(n));
+        if (hipMemcpyAsync(d_starts, desc.data(), desc_bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+            LaunchCrc32cSegments(d_starts, d_lens, n, total, maxlen, out_dev, scratch, s) == 0 &&
+            hipMemcpyAsync(out_host, out_dev, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, s) == hipSuccess) {
+            rc = SyncStream(s);
+        }
+    }
+    Free(mem);
     if (prev != device) hipSetDevice(prev);
     return rc;
 }

@@ -22,13 +22,20 @@ static void check(int rc, const char* what) {
 }
 
 void bind_gpu_ops(py::module_& g) {
-    g.def("crc32c_launch", [](const std::vector<uintptr_t>& ptrs, const std::vector<uint64_t>& lens, uintptr_t out,
+    g.def("crc32c_lds_launch", [](const std::vector<uintptr_t>& ptrs, const std::vector<uint64_t>& lens, uintptr_t out,
                               uintptr_t stream) {
         if (ptrs.size() != lens.size()) throw std::invalid_argument("ptrs/lens size mismatch");
         std::vector<gpu::Segment> segs(ptrs.size());
         for (size_t i = 0; i < ptrs.size(); ++i) segs[i] = gpu::Segment{(const void*)ptrs[i], nullptr, lens[i]};
         check(gpu::LaunchCrc32c(segs.data(), (int)segs.size(), (uint32_t*)out, as_stream(stream)), "crc32c");
     }, py::arg("ptrs"), py::arg("lens"), py::arg("out"), py::arg("stream") = 0);
+    g.def("crc32c_scratch_bytes", &gpu::Crc32cScratchBytes);
+    g.def("crc32c_segments_launch", [](uintptr_t starts, uintptr_t lens, int64_t nseg, uint64_t total_bytes,
+                                       uint64_t max_seg_len, uintptr_t out, uintptr_t scratch, uintptr_t stream) {
+        check(gpu::LaunchCrc32cSegments((const uint64_t*)starts, (const uint64_t*)lens, nseg, total_bytes, max_seg_len,
+                                        (uint32_t*)out, (void*)scratch, as_stream(stream)),
+              "crc32c_segments");
+    });
     g.def("crc32c_sync", [](uintptr_t ptr, uint64_t len, int device) {
         uint32_t out = 0;
         const void* p = (const void*)ptr;

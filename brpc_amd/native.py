@@ -17,6 +17,13 @@ def _load():
     name = "brpc_amd._native"
     if name in sys.modules:
         return sys.modules[name]
+    # torch ships its own libamdhip64.so.7; load it first so the extension
+    # binds to the SAME HIP runtime (same soname) instead of pulling a second
+    # copy from /opt/rocm — one runtime per process, shared device contexts.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     cands = sorted(glob.glob(os.path.join(_HERE, "_native*.so")))
     if not cands:
         raise ImportError(

@@ -1,6 +1,6 @@
 """Device ops on torch tensors, backed by the hand-written gfx950 kernels in
 ``brpc_amd/csrc/gpu/kernels.hip``. No fallback path: a CPU tensor or a
 missing extension raises."""
-from .crc32c import crc32c, crc32c_batch, crc32c_host  # noqa: F401
+from .crc32c import crc32c, crc32c_batch, crc32c_host, crc32c_packed  # noqa: F401
 from .varint import varint_decode, varint_encode, varint_encode_host, varint_decode_host  # noqa: F401
 from .copy import batched_copy  # noqa: F401

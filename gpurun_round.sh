@@ -7,11 +7,12 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 step() {  # name timeout cmd...
   local name=$1 t=$2; shift 2
-  echo "== $name" | tee -a gpurun_out/steps.log
-  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local out="$GRAFT_REPO_ROOT/gpurun_out"
+  echo "== $name" | tee -a "$out/steps.log"
+  timeout -k 10 "$t" "$@" > "$out/$name.log" 2>&1
   local rc=$?
-  echo "== $name rc=$rc" | tee -a gpurun_out/steps.log
-  tail -5 "gpurun_out/$name.log"
+  echo "== $name rc=$rc" | tee -a "$out/steps.log"
+  tail -5 "$out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }

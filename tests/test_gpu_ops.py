@@ -22,7 +22,37 @@ def test_crc32c_matches_host(dev, n):
     from brpc_amd.ops import crc32c, crc32c_host
     g = torch.Generator().manual_seed(n)
     host = torch.randint(0, 256, (n,), dtype=torch.uint8, generator=g)
-    assert crc32c(host.to(dev)) == crc32c_host(host.numpy().tobytes())
+    want = crc32c_host(host.numpy().tobytes())
+    d = host.to(dev)
+    assert crc32c(d, impl="mfma") == want
+    assert crc32c(d, impl="lds") == want
+
+
+def test_crc32c_single_bits(dev):
+    """Every bit of a 2 KiB group exercises one A-matrix column of the MFMA
+    kernel: a wrong fragment mapping shows up as a mismatch here."""
+    from brpc_amd.ops import crc32c_batch, crc32c_host
+    base = torch.zeros(4096, dtype=torch.uint8)
+    bufs = []
+    for bit in range(0, 4096 * 8, 61):
+        b = base.clone()
+        b[bit // 8] = 1 << (bit % 8)
+        bufs.append(b)
+    got = crc32c_batch([b.to(dev) for b in bufs]).tolist()
+    want = [crc32c_host(b.numpy().tobytes()) for b in bufs]
+    assert got == want
+
+
+def test_crc32c_packed(dev):
+    from brpc_amd.ops import crc32c_host, crc32c_packed
+    sizes = [0, 1, 100, 65536, 65537, 3, 200000, 16]
+    buf = torch.randint(0, 256, (sum(sizes),), dtype=torch.uint8, device=dev)
+    offs = [0]
+    for s in sizes:
+        offs.append(offs[-1] + s)
+    got = crc32c_packed(buf, torch.tensor(offs, dtype=torch.int64, device=dev)).tolist()
+    hb = buf.cpu().numpy().tobytes()
+    assert got == [crc32c_host(hb[offs[i]:offs[i + 1]]) for i in range(len(sizes))]
 
 
 def test_crc32c_known_vector(dev):
@@ -35,9 +65,9 @@ def test_crc32c_unaligned_views_and_batch(dev):
     from brpc_amd.ops import crc32c_batch, crc32c_host
     base = torch.randint(0, 256, (300000,), dtype=torch.uint8, device=dev)
     views = [base[o:o + l] for o, l in [(1, 5000), (3, 70000), (17, 16384), (0, 1), (5, 0)]] * 10  # 50 > 32 inline
-    got = crc32c_batch(views).tolist()
     want = [crc32c_host(v.cpu().numpy().tobytes()) for v in views]
-    assert got == want
+    assert crc32c_batch(views).tolist() == want
+    assert crc32c_batch(views, impl="lds").tolist() == want
 
 
 def test_varint_roundtrip(dev):
