@@ -148,7 +148,6 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
     m->_error_text.clear();
     m->_preferred_index = -1;
     m->_parsing_context = nullptr;
-    m->_parsing_context_deleter = nullptr;
     m->_avg_msg_size = 0;
     m->_server_verified.store(false);
     m->_auth_error.store(0);
@@ -335,9 +334,12 @@ void Socket::OnRecycle() {
     }
     _read_buf.clear();
     _read_buf.return_cached_blocks();
-    if (_parsing_context && _parsing_context_deleter) _parsing_context_deleter(_parsing_context);
+    delete _parsing_context;
     _parsing_context = nullptr;
-    _parsing_context_deleter = nullptr;
+    {
+        std::lock_guard<std::mutex> g(_pipeline_mu);
+        _pipeline_q.clear();
+    }
     {
         std::lock_guard<std::mutex> g(_mu);
         _transport.reset();
@@ -361,10 +363,9 @@ void Socket::OnRecycle() {
     g_nsocket.fetch_sub(1, std::memory_order_relaxed);
 }
 
-void Socket::reset_parsing_context(void* ctx, void (*deleter)(void*)) {
-    if (_parsing_context && _parsing_context_deleter) _parsing_context_deleter(_parsing_context);
+void Socket::reset_parsing_context(ParsingContext* ctx) {
+    delete _parsing_context;
     _parsing_context = ctx;
-    _parsing_context_deleter = deleter;
 }
 
 std::shared_ptr<Transport> Socket::transport() const {
@@ -565,7 +566,38 @@ int Socket::Write(Buf* data, const WriteOptions* options) {
             _shared->last_compact = j;
         }
     }
+    if (opt.pipelined_count > 0) {
+        // the queue order must equal the wire order: enqueue the entry and
+        // the write under one lock (StartWrite's exchange fixes the order)
+        std::lock_guard<std::mutex> g(_pipeline_mu);
+        PipelinedInfo pi;
+        pi.count = opt.pipelined_count;
+        pi.tag = opt.pipelined_tag;
+        pi.id_wait = opt.id_wait;
+        _pipeline_q.push_back(pi);
+        return StartWrite(req, opt);
+    }
     return StartWrite(req, opt);
+}
+
+bool Socket::PopPipelinedInfo(PipelinedInfo* out) {
+    std::lock_guard<std::mutex> g(_pipeline_mu);
+    if (_pipeline_q.empty()) return false;
+    *out = _pipeline_q.front();
+    _pipeline_q.pop_front();
+    return true;
+}
+
+bool Socket::PeekPipelinedInfo(PipelinedInfo* out) {
+    std::lock_guard<std::mutex> g(_pipeline_mu);
+    if (_pipeline_q.empty()) return false;
+    *out = _pipeline_q.front();
+    return true;
+}
+
+void Socket::GivebackPipelinedInfo(const PipelinedInfo& pi) {
+    std::lock_guard<std::mutex> g(_pipeline_mu);
+    _pipeline_q.push_front(pi);
 }
 
 int Socket::StartWrite(WriteRequest* req, const WriteOptions& opt) {
@@ -765,8 +797,12 @@ int Socket::Revive(int new_fd) {
         _read_buf.clear();
         _nevent.store(0);
         _preferred_index = -1;
-        if (_parsing_context && _parsing_context_deleter) _parsing_context_deleter(_parsing_context);
+        delete _parsing_context;
         _parsing_context = nullptr;
+        {
+            std::lock_guard<std::mutex> g(_pipeline_mu);
+            _pipeline_q.clear();
+        }
         _auth_state.store(0);
         const int old = _fd.exchange(-1);
         if (old >= 0) ::close(old);

@@ -19,8 +19,9 @@
 #include <cstdint>
 #include <functional>
 #include <memory>
-#include <vector>
+#include <deque>
 #include <mutex>
+#include <vector>
 #include <string>
 
 #include "base/buf.h"
@@ -61,6 +62,14 @@ private:
     Socket* _s;
 };
 
+// Base of per-connection protocol state kept on a Socket. The type tag
+// lets a protocol's parse() tell its own context from another protocol's.
+class ParsingContext {
+public:
+    virtual ~ParsingContext() {}
+    virtual int protocol_tag() const = 0;
+};
+
 // Hook for non-fd connections (streams multiplexed on a host socket).
 class SocketConnection {
 public:
@@ -93,6 +102,18 @@ struct WriteOptions {
     int abstime_ms = 0;
     bool ignore_eovercrowded = false;
     bool write_in_background = false;
+    // >0: the protocol answers requests in order without correlation ids
+    // (http/1.1, redis, memcache). The socket remembers (count, id_wait) in
+    // write order so the parser can map the next response(s) to the call.
+    int pipelined_count = 0;
+    // protocol-private tag carried with the pipelined entry (e.g. HEAD)
+    uint32_t pipelined_tag = 0;
+};
+
+struct PipelinedInfo {
+    int count = 0;
+    uint32_t tag = 0;
+    fiber::CallId id_wait = fiber::INVALID_CALL_ID;
 };
 
 class Socket {
@@ -134,9 +155,10 @@ public:
     bool MoreReadEvents(int* progress);
     BufPortal _read_buf;
     int _preferred_index = -1;          // protocol index that parsed the last message
-    void* _parsing_context = nullptr;   // protocol private state (h2, http, redis)
-    void (*_parsing_context_deleter)(void*) = nullptr;
-    void reset_parsing_context(void* ctx, void (*deleter)(void*));
+    // Protocol private per-connection state (http parser, h2 context, ...).
+    ParsingContext* parsing_context() const { return _parsing_context; }
+    void reset_parsing_context(ParsingContext* ctx);
+    ParsingContext* _parsing_context = nullptr;
     int64_t _avg_msg_size = 0;
     std::atomic<bool> _server_verified{false};  // server-side authentication done
 
@@ -151,6 +173,12 @@ public:
     bool FightAuthentication(int* auth_error);
     void SetAuthentication(int error);
     int auth_error() const { return _auth_error.load(); }
+
+    // Pipelined protocols: peek/pop the entry of the oldest outstanding write.
+    bool PopPipelinedInfo(PipelinedInfo* out);
+    bool PeekPipelinedInfo(PipelinedInfo* out);
+    // Give back one response slot of a multi-response entry (redis batch).
+    void GivebackPipelinedInfo(const PipelinedInfo& pi);
 
     // Per-socket attached objects
     std::shared_ptr<Transport> transport() const;
@@ -222,6 +250,8 @@ private:
     struct SharedPart;
     std::shared_ptr<SharedPart> _shared;
     std::atomic<bool> _recycle_flag;
+    std::mutex _pipeline_mu;
+    std::deque<PipelinedInfo> _pipeline_q;
     std::atomic<bool> _hc_started;
 };
 

@@ -10,6 +10,8 @@
 #include "cluster/load_balancer.h"
 #include "fiber/fiber.h"
 #include "http/http_header.h"
+#include "http/http_message.h"
+#include "rpc/progressive.h"
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
 #include "rpc/retry_policy.h"
@@ -91,6 +93,9 @@ void Controller::Reset() {
     _read_progressively = false;
     _progressive_reader = nullptr;
     _progressive_attachment.reset();
+    _progressive_sink.reset();
+    _pipelined_count = 0;
+    _pipelined_tag = 0;
     _session_kv.clear();
     _request_stream = _response_stream = 0;
     _stream_creator.reset();
@@ -153,6 +158,24 @@ HttpHeader& Controller::http_request() {
 HttpHeader& Controller::http_response() {
     if (!_http_response) _http_response = new HttpHeader;
     return *_http_response;
+}
+
+std::shared_ptr<ProgressiveAttachment> Controller::CreateProgressiveAttachment() {
+    if (!_progressive_attachment) {
+        const bool http10 = _http_request && _http_request->major_version() == 1 && _http_request->minor_version() == 0;
+        _progressive_attachment = std::make_shared<ProgressiveAttachment>(_server_socket_id, http10);
+    }
+    return _progressive_attachment;
+}
+
+void Controller::ReadProgressiveAttachmentBy(ProgressiveReader* r) {
+    if (!r) return;
+    if (!_progressive_sink) {
+        r->OnEndOfMessage(Status(EINVAL, _read_progressively ? "response has no progressive body"
+                                                             : "call response_will_be_read_progressively() first"));
+        return;
+    }
+    _progressive_sink->SetReader(r);
 }
 
 void Controller::StartCancel() {
@@ -368,6 +391,8 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
     }
     WriteOptions wopt;
     wopt.id_wait = cid;
+    wopt.pipelined_count = _pipelined_count;
+    wopt.pipelined_tag = _pipelined_tag;
     // Errors of Write() are delivered through call_id_error(cid), which is
     // queued while we hold the lock and handled at unlock.
     sock->Write(&packet, &wopt);

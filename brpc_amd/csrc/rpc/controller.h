@@ -35,6 +35,7 @@ class Span;
 class HttpHeader;
 class ProgressiveAttachment;
 class ProgressiveReader;
+class ProgressiveSink;
 class StreamCreator;
 struct Protocol;
 typedef uint64_t StreamId;
@@ -117,8 +118,11 @@ public:
     HttpHeader& http_request();
     HttpHeader& http_response();
     bool has_http_request() const { return _http_request != nullptr; }
-    // Progressive (chunked) response for server push.
-    ProgressiveAttachment* CreateProgressiveAttachment();
+    // Progressive (chunked) response for server push: keep the returned
+    // object and Write() body pieces after done->Run(); dropping the last
+    // reference ends the body.
+    std::shared_ptr<ProgressiveAttachment> CreateProgressiveAttachment();
+    bool has_progressive_attachment() const { return (bool)_progressive_attachment; }
     void ReadProgressiveAttachmentBy(ProgressiveReader* r);
     void response_will_be_read_progressively() { _read_progressively = true; }
     bool is_response_read_progressively() const { return _read_progressively; }
@@ -214,6 +218,10 @@ public:
     bool _read_progressively = false;
     ProgressiveReader* _progressive_reader = nullptr;
     std::shared_ptr<ProgressiveAttachment> _progressive_attachment;
+    std::shared_ptr<ProgressiveSink> _progressive_sink;  // client: streamed response body
+    // set by pack_request of in-order protocols (http/1.1, redis, memcache)
+    int _pipelined_count = 0;
+    uint32_t _pipelined_tag = 0;
     HttpHeader* _http_request = nullptr;
     HttpHeader* _http_response = nullptr;
     std::map<std::string, std::string> _session_kv;

@@ -59,6 +59,7 @@ void GlobalInitializeOrDie() {
         RegisterBuiltinConcurrencyLimiters();
         policy::RegisterBaiduStdProtocol();
         RegisterStreamingProtocol();
+        policy::RegisterHttpProtocol();
         for (ProtocolRegistrar r : extra_registrars()) r();
         // Client-side messenger handles responses of every protocol.
         std::vector<std::pair<ProtocolType, Protocol>> protocols;
