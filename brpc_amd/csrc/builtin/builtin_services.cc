@@ -1,0 +1,598 @@
+// Builtin HTTP pages installed on every server (role of the reference's
+// src/brpc/builtin/*: index, status, vars, flags, connections, rpcz,
+// health, version, list, threads, vlog, bthreads, ids, sockets, protobufs,
+// hotspots, pprof, dir, prometheus metrics; server.cpp:459-555 adds them).
+// Pages answer in plain text (or HTML for /index); every one is a pb
+// service with an empty request/response whose body is the attachment, so
+// they are reachable over http on the same port as RPC traffic.
+#include <dirent.h>
+#include <malloc.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <fstream>
+#include <sstream>
+
+#include "base/flags.h"
+#include "base/logging.h"
+#include "base/time.h"
+#include "base/util.h"
+#include "builtin/cpu_profiler.h"
+#include "fiber/call_id.h"
+#include "fiber/fiber.h"
+#include "fiber/sync.h"
+#include "gpu/gpu.h"
+#include "http/http_header.h"
+#include "mrpc/proto/builtin_service.pb.h"
+#include "net/socket.h"
+#include "rpc/controller.h"
+#include "rpc/errno.h"
+#include "rpc/health_reporter.h"
+#include "rpc/method_status.h"
+#include "rpc/server.h"
+#include "rpc/span.h"
+#include "var/var.h"
+
+DEFINE_bool(enable_dir_service, false, "enable /dir (browse the file system)");
+DEFINE_bool(enable_threads_service, false, "enable /threads (per-thread states)");
+DECLARE_bool(enable_rpcz);
+
+namespace mrpc {
+namespace builtin {
+
+namespace {
+
+const char* kText = "text/plain; charset=utf-8";
+
+Controller* C(RpcController* c) { return static_cast<Controller*>(c); }
+
+void text(Controller* cntl, const std::string& s) {
+    cntl->http_response().set_content_type(kText);
+    cntl->response_attachment().append(s);
+}
+
+const std::string& unresolved(Controller* cntl) { return cntl->http_request().unresolved_path(); }
+
+const std::string* query(Controller* cntl, const char* k) { return cntl->http_request().uri().GetQuery(k); }
+
+std::string fmt_time(int64_t real_us) {
+    time_t t = (time_t)(real_us / 1000000);
+    struct tm tm;
+    localtime_r(&t, &tm);
+    char buf[64];
+    strftime(buf, sizeof(buf), "%Y/%m/%d-%H:%M:%S", &tm);
+    return buf;
+}
+
+// ------------------------------------------------------------------ pages
+class IndexImpl : public index {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const Server* s = cntl->server();
+        std::ostringstream os;
+        os << "<html><head><title>mrpc server</title></head><body><pre>\n";
+        os << "mrpc server on " << s->listen_address() << " (version: " << s->version() << ")\n\n";
+        static const char* pages[][2] = {
+            {"status", "per-method statistics"}, {"vars", "exposed metrics"},       {"flags", "runtime flags"},
+            {"connections", "live connections"}, {"rpcz", "recent RPC spans"},     {"health", "health check"},
+            {"version", "server version"},       {"list", "services and methods"}, {"threads", "thread states"},
+            {"vlog", "verbose log level"},       {"fibers", "fiber runtime"},      {"ids", "call ids"},
+            {"sockets", "socket details"},       {"protobufs", "message types"},   {"hotspots/cpu", "cpu profile"},
+            {"hotspots/contention", "lock contention"}, {"pprof/profile", "pprof cpu profile"},
+            {"brpc_metrics", "prometheus metrics"}, {"memory", "memory usage"},   {"gpu", "MI355X devices"},
+            {"dir", "file browser (opt-in)"}};
+        for (auto& p : pages) os << "<a href=\"/" << p[0] << "\">/" << p[0] << "</a>  " << p[1] << "\n";
+        os << "\nservices:\n";
+        std::vector<const Server::MethodProperty*> mps;
+        s->ListMethodProperties(&mps);
+        for (auto* mp : mps) {
+            if (mp->is_builtin_service) continue;
+            os << "  " << mp->method->full_name << "\n";
+        }
+        os << "</pre></body></html>\n";
+        cntl->http_response().set_content_type("text/html; charset=utf-8");
+        cntl->response_attachment().append(os.str());
+    }
+};
+
+class StatusImpl : public status {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const Server* s = cntl->server();
+        std::ostringstream os;
+        os << "version: " << s->version() << "\n";
+        os << "listen: " << s->listen_address() << "\n";
+        os << "start_time: " << fmt_time(s->start_time_us()) << "\n";
+        os << "uptime_s: " << (realtime_us() - s->start_time_us()) / 1000000 << "\n";
+        os << "concurrency: " << s->concurrency() << " (max " << s->max_concurrency() << ")\n\n";
+        std::vector<const Server::MethodProperty*> mps;
+        s->ListMethodProperties(&mps);
+        for (auto* mp : mps) {
+            if (mp->is_builtin_service) continue;
+            os << mp->method->full_name << "\n";
+            if (mp->status) os << mp->status->Describe() << "\n";
+        }
+        text(cntl, os.str());
+    }
+};
+
+class VarsImpl : public vars {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const std::string& name = unresolved(cntl);
+        std::ostringstream os;
+        if (!name.empty() && name.find_first_of("*?;") == std::string::npos) {
+            if (query(cntl, "series")) {
+                os << var::Variable::series_exposed(name);
+            } else if (var::Variable::describe_exposed(name, os) != 0) {
+                cntl->SetFailed(ENOMETHOD, "no variable named `%s'", name.c_str());
+                return;
+            }
+            os << "\n";
+        } else {
+            std::vector<std::pair<std::string, std::string>> out;
+            var::Variable::dump_exposed(&out, name);
+            for (auto& kv : out) os << kv.first << " : " << kv.second << "\n";
+        }
+        text(cntl, os.str());
+    }
+};
+
+class FlagsImpl : public flags {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const std::string& name = unresolved(cntl);
+        if (const std::string* v = query(cntl, "setvalue")) {
+            if (name.empty()) {
+                cntl->SetFailed(EREQUEST, "/flags/<name>?setvalue=<value>");
+                return;
+            }
+            std::string err;
+            if (!SetFlag(name, *v, /*require_reloadable=*/true, &err)) {
+                cntl->SetFailed(EPERM, "fail to set %s=%s: %s", name.c_str(), v->c_str(), err.c_str());
+                return;
+            }
+            text(cntl, "Set `" + name + "' to " + *v + "\n");
+            return;
+        }
+        std::ostringstream os;
+        for (const FlagInfo& f : ListFlags()) {
+            if (!name.empty() && !wildcard_match(name, f.name)) continue;
+            os << f.name << " = " << f.current_value;
+            if (f.current_value != f.default_value) os << " (default: " << f.default_value << ")";
+            if (f.reloadable) os << " [R]";
+            os << "  # " << f.description << "\n";
+        }
+        text(cntl, os.str());
+    }
+    static bool wildcard_match(const std::string& pat, const std::string& s) {
+        for (const std::string& p : split_string(pat, ';')) {
+            if (p == s || fnmatch_simple(p.c_str(), s.c_str())) return true;
+        }
+        return false;
+    }
+    static bool fnmatch_simple(const char* p, const char* s) {
+        if (!*p) return !*s;
+        if (*p == '*') return fnmatch_simple(p + 1, s) || (*s && fnmatch_simple(p, s + 1));
+        if (*s && (*p == '?' || *p == *s)) return fnmatch_simple(p + 1, s + 1);
+        return false;
+    }
+};
+
+class ConnectionsImpl : public connections {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        text(C(c), DescribeAllSockets());
+    }
+};
+
+class RpczImpl : public rpcz {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        if (query(cntl, "enable")) {
+            SetFlag("enable_rpcz", "true");
+            text(cntl, "rpcz enabled\n");
+            return;
+        }
+        if (query(cntl, "disable")) {
+            SetFlag("enable_rpcz", "false");
+            text(cntl, "rpcz disabled\n");
+            return;
+        }
+        if (!IsRpczEnabled()) {
+            text(cntl, "rpcz is disabled; visit /rpcz?enable to turn it on\n");
+            return;
+        }
+        uint64_t trace = 0;
+        if (const std::string* t = query(cntl, "trace")) trace = strtoull(t->c_str(), nullptr, 16);
+        size_t max = 100;
+        if (const std::string* m = query(cntl, "max")) max = (size_t)atoi(m->c_str());
+        std::ostringstream os;
+        for (const std::string& s : ListRecentSpans(max, trace)) os << s << "\n";
+        text(cntl, os.str());
+    }
+};
+
+class HealthImpl : public health {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        Controller* cntl = C(c);
+        HealthReporter* r = cntl->server()->options().health_reporter;
+        if (r) {
+            r->GenerateReport(cntl, done);
+            return;
+        }
+        ClosureGuard g(done);
+        text(cntl, "OK\n");
+    }
+};
+
+class VersionImpl : public version {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        text(cntl, (cntl->server()->version().empty() ? std::string("unknown") : cntl->server()->version()) + "\n");
+    }
+};
+
+class ListImpl : public list {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        std::vector<Service*> svcs;
+        cntl->server()->ListServices(&svcs);
+        std::ostringstream os;
+        for (Service* s : svcs) {
+            const pb::ServiceDescriptor* sd = s->GetDescriptor();
+            os << "service " << sd->full_name << " {\n";
+            for (int i = 0; i < sd->method_count(); ++i) {
+                const pb::MethodDescriptor* m = sd->method(i);
+                os << "  rpc " << m->name << "(" << (m->input_type ? m->input_type->full_name : m->input_type_name)
+                   << ") returns (" << (m->output_type ? m->output_type->full_name : m->output_type_name) << ");\n";
+            }
+            os << "}\n";
+        }
+        text(cntl, os.str());
+    }
+};
+
+class ThreadsImpl : public threads {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        if (!FLAGS_enable_threads_service) {
+            cntl->SetFailed(EPERM, "/threads is disabled, set -enable_threads_service");
+            return;
+        }
+        std::ostringstream os;
+        DIR* d = opendir("/proc/self/task");
+        if (d) {
+            while (dirent* e = readdir(d)) {
+                if (e->d_name[0] == '.') continue;
+                std::ifstream comm(std::string("/proc/self/task/") + e->d_name + "/comm");
+                std::ifstream stat(std::string("/proc/self/task/") + e->d_name + "/stat");
+                std::string name, st;
+                std::getline(comm, name);
+                std::getline(stat, st);
+                const size_t rp = st.rfind(')');
+                const char state = rp != std::string::npos && rp + 2 < st.size() ? st[rp + 2] : '?';
+                os << e->d_name << "\t" << state << "\t" << name << "\n";
+            }
+            closedir(d);
+        }
+        text(cntl, os.str());
+    }
+};
+
+class VlogImpl : public vlog {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        if (const std::string* v = query(cntl, "setlevel")) SetVerboseLevel(atoi(v->c_str()));
+        text(cntl, "verbose level: " + std::to_string(GetVerboseLevel()) + " (set with /vlog?setlevel=N)\n");
+    }
+};
+
+class FibersImpl : public fibers {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        std::ostringstream os;
+        os << "workers: " << fiber::get_concurrency() << "\n";
+        os << "live fibers: " << fiber::fiber_count() << "\n";
+        os << "context switches: " << fiber::switch_count() << "\n";
+        os << "steals: " << fiber::steal_count() << "\n";
+        os << "worker usage: " << fiber::worker_usage() << "\n";
+        text(C(c), os.str());
+    }
+};
+
+class IdsImpl : public ids {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const std::string& id = unresolved(cntl);
+        if (id.empty()) {
+            text(cntl, "usage: /ids/<call id in decimal>\n");
+            return;
+        }
+        const fiber::CallId cid{strtoull(id.c_str(), nullptr, 10)};
+        text(cntl, std::string("call id ") + id + (fiber::call_id_exists(cid) ? " is alive\n" : " does not exist\n"));
+    }
+};
+
+class SocketsImpl : public sockets {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const std::string& id = unresolved(cntl);
+        if (id.empty()) {
+            text(cntl, DescribeAllSockets());
+            return;
+        }
+        SocketUniquePtr s;
+        if (Socket::AddressFailedAsWell(strtoull(id.c_str(), nullptr, 10), &s) != 0) {
+            cntl->SetFailed(ENOMETHOD, "no socket %s", id.c_str());
+            return;
+        }
+        text(cntl, s->description() + "\n");
+    }
+};
+
+static void print_message(std::ostream& os, const pb::Descriptor* d) {
+    os << "message " << d->full_name << " {\n";
+    for (int i = 0; i < d->field_count(); ++i) {
+        const pb::FieldDescriptor* f = d->field(i);
+        const char* label = f->is_repeated() ? "repeated " : (f->is_required() ? "required " : "optional ");
+        std::string type = f->message_type ? f->message_type->full_name
+                                           : (f->enum_type ? f->enum_type->full_name : pb::FieldTypeName(f->type));
+        os << "  " << label << type << " " << f->name << " = " << f->number;
+        if (f->has_default) os << " [default = " << f->default_str << "]";
+        os << ";\n";
+    }
+    os << "}\n";
+}
+
+class ProtobufsImpl : public protobufs {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        std::vector<Service*> svcs;
+        cntl->server()->ListServices(&svcs);
+        std::map<std::string, const pb::Descriptor*> types;
+        std::function<void(const pb::Descriptor*)> add = [&](const pb::Descriptor* d) {
+            if (!d || types.count(d->full_name)) return;
+            types[d->full_name] = d;
+            for (int i = 0; i < d->field_count(); ++i) add(d->field(i)->message_type);
+        };
+        for (Service* s : svcs) {
+            const pb::ServiceDescriptor* sd = s->GetDescriptor();
+            for (int i = 0; i < sd->method_count(); ++i) {
+                add(sd->method(i)->input_type);
+                add(sd->method(i)->output_type);
+            }
+        }
+        const std::string& name = unresolved(cntl);
+        std::ostringstream os;
+        if (name.empty()) {
+            for (auto& kv : types) os << kv.first << "\n";
+        } else {
+            auto it = types.find(name);
+            if (it == types.end()) {
+                cntl->SetFailed(ENOMETHOD, "no message type %s", name.c_str());
+                return;
+            }
+            print_message(os, it->second);
+        }
+        text(cntl, os.str());
+    }
+};
+
+static double seconds_param(Controller* cntl, double def) {
+    const std::string* s = query(cntl, "seconds");
+    double v = s ? atof(s->c_str()) : def;
+    if (v <= 0) v = def;
+    return std::min(v, 60.0);
+}
+
+class HotspotsImpl : public hotspots {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const std::string& kind = unresolved(cntl);
+        if (kind == "cpu" || kind.empty()) {
+            std::string folded;
+            int64_t n = 0;
+            const int hz = query(cntl, "frequency") ? atoi(query(cntl, "frequency")->c_str()) : 100;
+            if (!profiler::ProfileCpu(seconds_param(cntl, 10), hz, &folded, nullptr, &n)) {
+                cntl->SetFailed(EAGAIN, "another cpu profile is running");
+                return;
+            }
+            text(cntl, "# " + std::to_string(n) + " samples, folded stacks (flamegraph.pl input)\n" + folded);
+        } else if (kind == "contention") {
+            const double secs = seconds_param(cntl, 10);
+            if (!fiber::ContentionProfilerStart(nullptr)) {
+                cntl->SetFailed(EAGAIN, "another contention profile is running");
+                return;
+            }
+            fiber::usleep((int64_t)(secs * 1e6));
+            fiber::ContentionProfilerStop();
+            std::string dump = fiber::ContentionProfilerDump();
+            std::istringstream is(dump);
+            std::ostringstream os;
+            os << "# caller count total_wait_ns\n";
+            std::string line;
+            while (std::getline(is, line)) {
+                unsigned long long addr = strtoull(line.c_str(), nullptr, 16);
+                os << profiler::Symbolize((uintptr_t)addr) << " " << line.substr(line.find(' ') + 1) << "\n";
+            }
+            text(cntl, os.str());
+        } else if (kind == "heap" || kind == "growth") {
+            struct mallinfo2 mi = mallinfo2();
+            std::ostringstream os;
+            os << "heap profiling needs a sampling allocator (not linked); glibc arena summary:\n";
+            os << "arena " << mi.arena << "\nin_use " << mi.uordblks << "\nfree " << mi.fordblks << "\nmmap "
+               << mi.hblkhd << "\n";
+            text(cntl, os.str());
+        } else {
+            cntl->SetFailed(ENOMETHOD, "unknown hotspot kind `%s' (cpu|contention|heap|growth)", kind.c_str());
+        }
+    }
+};
+
+class PprofImpl : public pprof {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        const std::string& kind = unresolved(cntl);
+        if (kind == "profile") {
+            std::string bin;
+            if (!profiler::ProfileCpu(seconds_param(cntl, 10), 100, nullptr, &bin, nullptr)) {
+                cntl->SetFailed(EAGAIN, "another cpu profile is running");
+                return;
+            }
+            cntl->http_response().set_content_type("application/octet-stream");
+            cntl->response_attachment().append(bin);
+        } else if (kind == "symbol") {
+            // GET: report that symbols are available; POST: "0xaddr+0xaddr..."
+            if (cntl->http_request().method() == HTTP_METHOD_GET) {
+                text(cntl, "num_symbols: 1\n");
+                return;
+            }
+            std::string body = cntl->request_attachment().to_string();
+            std::ostringstream os;
+            for (const std::string& a : split_string_any(body, "+ \n")) {
+                const uintptr_t addr = (uintptr_t)strtoull(a.c_str(), nullptr, 16);
+                if (addr) os << a << "\t" << profiler::Symbolize(addr) << "\n";
+            }
+            text(cntl, os.str());
+        } else if (kind == "cmdline") {
+            std::ifstream f("/proc/self/cmdline");
+            std::string s((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+            std::replace(s.begin(), s.end(), '\0', '\n');
+            text(cntl, s);
+        } else if (kind == "heap" || kind == "growth") {
+            cntl->SetFailed(ENOMETHOD, "heap profiles need a sampling allocator, which is not linked");
+        } else {
+            cntl->SetFailed(ENOMETHOD, "unknown pprof endpoint `%s' (profile|symbol|cmdline)", kind.c_str());
+        }
+    }
+};
+
+class DirImpl : public dir {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        if (!FLAGS_enable_dir_service) {
+            cntl->SetFailed(EPERM, "/dir is disabled, set -enable_dir_service");
+            return;
+        }
+        const std::string path = "/" + unresolved(cntl);
+        struct stat st;
+        if (stat(path.c_str(), &st) != 0) {
+            cntl->SetFailed(ENOMETHOD, "no such path %s", path.c_str());
+            return;
+        }
+        if (S_ISDIR(st.st_mode)) {
+            std::ostringstream os;
+            DIR* d = opendir(path.c_str());
+            std::vector<std::string> names;
+            while (d && (true)) {
+                dirent* e = readdir(d);
+                if (!e) break;
+                names.push_back(e->d_name);
+            }
+            if (d) closedir(d);
+            std::sort(names.begin(), names.end());
+            for (auto& n : names) os << n << "\n";
+            text(cntl, os.str());
+        } else {
+            std::ifstream f(path, std::ios::binary);
+            std::string s((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+            text(cntl, s);
+        }
+    }
+};
+
+class MetricsImpl : public brpc_metrics {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = C(c);
+        cntl->http_response().set_content_type("text/plain; version=0.0.4");
+        cntl->response_attachment().append(var::Variable::dump_prometheus());
+    }
+};
+
+class MemoryImpl : public memory {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        struct mallinfo2 mi = mallinfo2();
+        std::ostringstream os;
+        os << "buf_blocks " << Buf::block_count() << "\nbuf_block_memory " << Buf::block_memory()
+           << "\nmalloc_arena " << mi.arena << "\nmalloc_in_use " << mi.uordblks << "\nmalloc_free " << mi.fordblks
+           << "\nmalloc_mmap " << mi.hblkhd << "\n";
+        text(C(c), os.str());
+    }
+};
+
+class GpuImpl : public gpu {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        std::ostringstream os;
+        const int n = mrpc::gpu::DeviceCount();
+        os << "devices: " << n << "\n";
+        for (int i = 0; i < n; ++i) {
+            os << "  [" << i << "] " << mrpc::gpu::DeviceName(i) << " (" << mrpc::gpu::DeviceArch(i) << ")\n";
+        }
+        os << "completion events polled: " << mrpc::gpu::PolledEvents() << "\n";
+        text(C(c), os.str());
+    }
+};
+
+int AddBuiltinServices(Server* server) {
+    Service* svcs[] = {new IndexImpl,   new StatusImpl,   new VarsImpl,     new FlagsImpl,   new ConnectionsImpl,
+                       new RpczImpl,    new HealthImpl,   new VersionImpl,  new ListImpl,    new ThreadsImpl,
+                       new VlogImpl,    new FibersImpl,   new IdsImpl,      new SocketsImpl, new ProtobufsImpl,
+                       new HotspotsImpl, new PprofImpl,   new DirImpl,      new MetricsImpl, new MemoryImpl,
+                       new GpuImpl};
+    for (Service* s : svcs) {
+        if (server->AddBuiltinService(s) != 0) {
+            LOG(ERROR) << "Fail to add builtin service " << s->GetDescriptor()->full_name;
+            return -1;
+        }
+    }
+    return 0;
+}
+
+struct Installer {
+    Installer() { SetAddBuiltinServicesHook(AddBuiltinServices); }
+} g_installer;
+
+}  // namespace
+}  // namespace builtin
+}  // namespace mrpc

@@ -105,6 +105,16 @@ bool set_scalar(Message* m, const FieldDescriptor* f, const json::Value& v, bool
         if (err) *err = "invalid value for field `" + f->name + "': expect " + what;
         return false;
     };
+    // integers may arrive quoted (64-bit values from JavaScript): the whole
+    // string must be a number
+    if (v.is_string() && f->cpp_type() != CppType::STRING && f->cpp_type() != CppType::ENUM &&
+        f->cpp_type() != CppType::FLOAT && f->cpp_type() != CppType::DOUBLE) {
+        const std::string& s = v.as_string();
+        char* end = nullptr;
+        if (s.empty()) return bad("number");
+        (void)strtod(s.c_str(), &end);
+        if (*end != '\0') return bad("number");
+    }
     switch (f->cpp_type()) {
     case CppType::INT32: {
         if (!v.is_number() && !v.is_string()) return bad("int32");

@@ -315,7 +315,11 @@ void ProcessHttpRequest(InputMessageBase* msg_base) {
             cntl->SetFailed(ELOGOFF, "Server is stopping");
             break;
         }
-        std::string path = req_h.uri().path();
+        std::string path;
+        for (char ch : req_h.uri().path()) {  // collapse "//"
+            if (ch == '/' && !path.empty() && path.back() == '/') continue;
+            path.push_back(ch);
+        }
         if (path.empty() || path == "/") path = "/index";
         std::string unresolved;
         mp = server->FindMethodPropertyByURI(path, &unresolved);

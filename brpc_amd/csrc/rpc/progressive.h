@@ -35,6 +35,7 @@ public:
     // Returns 0, or -1 with errno (the connection is gone).
     int Write(const Buf& data);
     int Write(const void* data, size_t n);
+    int Write(const std::string& s) { return Write(s.data(), s.size()); }
     EndPoint remote_side() const;
     // `done` runs when the body is finished or the connection broke.
     void NotifyOnStopped(Closure* done);

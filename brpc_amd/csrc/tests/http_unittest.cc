@@ -1,0 +1,317 @@
+// HTTP protocol + json2pb + builtin pages (spirit of the reference's
+// test/brpc_http_rpc_protocol_unittest.cpp, brpc_http_message_unittest.cpp,
+// test/brpc_builtin_service_unittest.cpp, json2pb unittests).
+#include <unistd.h>
+
+#include <thread>
+
+#include "base/flags.h"
+
+#include "base/time.h"
+#include "fiber/fiber.h"
+#include "http/http_header.h"
+#include "http/http_message.h"
+#include "json/json2pb.h"
+#include "mrpc/proto/echo.pb.h"
+#include "mrpc/proto/test_services.pb.h"
+#include "rpc/channel.h"
+#include "rpc/controller.h"
+#include "rpc/errno.h"
+#include "rpc/progressive.h"
+#include "rpc/server.h"
+#include "services/echo_service.h"
+#include "tests/test.h"
+
+using namespace mrpc;
+
+namespace {
+
+class HttpTestImpl : public test::HttpTest {
+public:
+    void Push(RpcController* c, const test::Empty*, test::Empty*, Closure* done) override {
+        Controller* cntl = static_cast<Controller*>(c);
+        auto pa = cntl->CreateProgressiveAttachment();
+        done->Run();  // header goes out now; the body follows
+        std::thread([pa] {
+            for (int i = 0; i < 5; ++i) {
+                pa->Write("part" + std::to_string(i) + ";");
+                usleep(2000);
+            }
+        }).detach();
+    }
+    void Raw(RpcController* c, const test::Empty*, test::Empty*, Closure* done) override {
+        ClosureGuard g(done);
+        Controller* cntl = static_cast<Controller*>(c);
+        cntl->http_response().set_content_type("application/octet-stream");
+        cntl->http_response().SetHeader("x-echo-method", HttpMethod2Str(cntl->http_request().method()));
+        cntl->response_attachment().append(cntl->request_attachment());
+        const std::string* q = cntl->http_request().uri().GetQuery("q");
+        if (q) cntl->response_attachment().append("|q=" + *q);
+    }
+    void Rich(RpcController*, const test::Rich* req, test::Rich* res, Closure* done) override {
+        ClosureGuard g(done);
+        *res = *req;
+        res->set_i32(req->i32() + 1);
+    }
+};
+
+struct HttpServer {
+    Server server;
+    EchoServiceImpl echo;
+    HttpTestImpl t;
+    int port = 0;
+    HttpServer() {
+        server.AddService(&echo, SERVER_DOESNT_OWN_SERVICE);
+        server.AddService(&t, SERVER_DOESNT_OWN_SERVICE, "/v1/raw/* => Raw");
+        ServerOptions o;
+        if (server.Start("127.0.0.1:0", &o) == 0) port = server.listen_port();
+    }
+    std::string addr() const { return "127.0.0.1:" + std::to_string(port); }
+};
+
+}  // namespace
+
+TEST(Json2pb, roundtrip) {
+    test::Rich r;
+    r.set_i32(-5);
+    r.set_i64(1LL << 40);
+    r.set_u64(~0ULL);
+    r.set_d(2.5);
+    r.set_flag(true);
+    r.set_s("he\"llo\n");
+    r.set_raw(std::string("\x00\x01\xff", 3));
+    r.set_color(test::BLUE);
+    r.mutable_inner()->set_x(7);
+    r.mutable_inner()->add_tags("a");
+    r.add_inners()->set_x(1);
+    r.add_inners()->set_x(2);
+    r.add_nums(3);
+    r.add_nums(4);
+    {
+        test::Rich_CountsEntry* e = r.add_counts();
+        e->set_key("k");
+        e->set_value(9);
+    }
+    r.set_must("m");
+    std::string json, err;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &json, json2pb::Pb2JsonOptions(), &err));
+    EXPECT_TRUE(json.find("\"color\":\"BLUE\"") != std::string::npos);
+    EXPECT_TRUE(json.find("\"raw\":\"AAH/\"") != std::string::npos);
+    test::Rich back;
+    ASSERT_TRUE(json2pb::JsonToProtoMessage(json, &back, json2pb::Json2PbOptions(), &err));
+    EXPECT_EQ(back.i64(), 1LL << 40);
+    EXPECT_EQ(back.u64(), ~0ULL);
+    EXPECT_EQ(back.raw(), std::string("\x00\x01\xff", 3));
+    EXPECT_EQ(back.color(), test::BLUE);
+    EXPECT_EQ(back.inners_size(), 2);
+    EXPECT_EQ(back.inners(1).x(), 2);
+    ASSERT_EQ(back.counts_size(), 1);
+    EXPECT_EQ(back.counts(0).key(), "k");
+    EXPECT_EQ(back.counts(0).value(), 9);
+    EXPECT_EQ(back.s(), "he\"llo\n");
+    // missing required field / bad type
+    test::Rich bad;
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"i32\": 1}", &bad, json2pb::Json2PbOptions(), &err));
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"x\",\"i32\":\"abc\"}", &bad, json2pb::Json2PbOptions(), &err));
+    json2pb::Json2PbOptions strict;
+    strict.allow_unknown_fields = false;
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"x\",\"nope\":1}", &bad, strict, &err));
+}
+
+TEST(HttpParser, chunked_and_pipelined) {
+    Buf b;
+    b.append("POST /a/b?x=1&y=two HTTP/1.1\r\nHost: h\r\nTransfer-Encoding: chunked\r\nContent-Type: text/plain\r\n\r\n"
+             "5\r\nhello\r\n6\r\n world\r\n0\r\n\r\n"
+             "GET /c HTTP/1.0\r\nContent-Length: 3\r\n\r\nabc");
+    HttpParser p(1 << 20);
+    std::string err;
+    ASSERT_EQ((int)p.Consume(&b, false, &err), (int)HttpParser::DONE);
+    std::unique_ptr<HttpMessage> m(p.release());
+    EXPECT_EQ(m->header.method(), HTTP_METHOD_POST);
+    EXPECT_EQ(m->header.uri().path(), "/a/b");
+    EXPECT_EQ(*m->header.uri().GetQuery("y"), "two");
+    EXPECT_EQ(m->header.content_type(), "text/plain");
+    EXPECT_EQ(m->body.to_string(), "hello world");
+    EXPECT_TRUE(m->keep_alive);
+    ASSERT_EQ((int)p.Consume(&b, false, &err), (int)HttpParser::DONE);
+    m.reset(p.release());
+    EXPECT_EQ(m->body.to_string(), "abc");
+    EXPECT_FALSE(m->keep_alive);  // HTTP/1.0 default
+    EXPECT_TRUE(b.empty());
+    // byte-by-byte feeding
+    const std::string resp = "HTTP/1.1 404 Not Found\r\nContent-Length: 4\r\nX-A: 1\r\n\r\nnope";
+    HttpParser p2(1 << 20);
+    Buf in;
+    HttpParser::Result r = HttpParser::NEED_MORE;
+    for (char ch : resp) {
+        in.push_back(ch);
+        r = p2.Consume(&in, false, &err);
+        if (r != HttpParser::NEED_MORE) break;
+    }
+    ASSERT_EQ((int)r, (int)HttpParser::DONE);
+    m.reset(p2.release());
+    EXPECT_TRUE(m->is_response);
+    EXPECT_EQ(m->header.status_code(), 404);
+    EXPECT_EQ(*m->header.GetHeader("x-a"), "1");
+    EXPECT_EQ(m->body.to_string(), "nope");
+    // garbage
+    Buf g;
+    g.append("GET / HTTP/1.1\r\nbad header line\r\n\r\n");
+    HttpParser p3(1 << 20);
+    EXPECT_EQ((int)p3.Consume(&g, false, &err), (int)HttpParser::FAILED);
+}
+
+TEST(Http, pb_over_json_and_proto) {
+    HttpServer s;
+    ASSERT_GT(s.port, 0);
+    Channel ch;
+    ChannelOptions opt;
+    opt.protocol = "http";
+    opt.timeout_ms = 3000;
+    ASSERT_EQ(ch.Init(s.addr().c_str(), &opt), 0);
+    example::EchoService_Stub stub(&ch);
+    for (int i = 0; i < 20; ++i) {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("json " + std::to_string(i));
+        stub.Echo(&cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_EQ(res.message(), "json " + std::to_string(i));
+        EXPECT_EQ(cntl.http_response().status_code(), 200);
+    }
+    Controller cntl;
+    cntl.http_request().set_content_type("application/proto");
+    example::EchoRequest req;
+    example::EchoResponse res;
+    req.set_message("proto");
+    stub.Echo(&cntl, &req, &res, nullptr);
+    ASSERT_FALSE(cntl.Failed());
+    EXPECT_EQ(res.message(), "proto");
+    EXPECT_EQ(cntl.http_response().content_type(), "application/proto");
+    // rich json round trip through a server
+    test::HttpTest_Stub t(&ch);
+    test::Rich rq, rs;
+    rq.set_i32(41);
+    rq.set_must("yes");
+    rq.set_color(test::GREEN);
+    {
+        test::Rich_CountsEntry* e = rq.add_counts();
+        e->set_key("a");
+        e->set_value(1);
+    }
+    Controller c2;
+    t.Rich(&c2, &rq, &rs, nullptr);
+    ASSERT_FALSE(c2.Failed());
+    EXPECT_EQ(rs.i32(), 42);
+    EXPECT_EQ(rs.color(), test::GREEN);
+    ASSERT_EQ(rs.counts_size(), 1);
+    EXPECT_EQ(rs.counts(0).value(), 1);
+}
+
+TEST(Http, plain_calls_builtin_restful_errors) {
+    HttpServer s;
+    Channel ch;
+    ChannelOptions opt;
+    opt.protocol = "http";
+    opt.timeout_ms = 3000;
+    ASSERT_EQ(ch.Init(("http://" + s.addr()).c_str(), &opt), 0);
+    {
+        Controller cntl;
+        cntl.http_request().uri().set_path("/health");
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_EQ(cntl.response_attachment().to_string(), "OK\n");
+    }
+    {
+        Controller cntl;
+        cntl.http_request().uri().SetHttpURL("/v1/raw/anything?q=zz");
+        cntl.http_request().set_method(HTTP_METHOD_PUT);
+        cntl.request_attachment().append("body!");
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_EQ(cntl.response_attachment().to_string(), "body!|q=zz");
+        EXPECT_EQ(*cntl.http_response().GetHeader("x-echo-method"), "PUT");
+    }
+    {
+        Controller cntl;
+        cntl.http_request().uri().set_path("/vars/fiber_count");
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_GT(atoi(cntl.response_attachment().to_string().c_str()), 0);
+    }
+    {
+        Controller cntl;
+        cntl.http_request().uri().set_path("/no/such/method");
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_TRUE(cntl.Failed());
+        EXPECT_EQ(cntl.ErrorCode(), ENOMETHOD);
+        EXPECT_EQ(cntl.http_response().status_code(), 404);
+    }
+    {
+        Controller cntl;  // HEAD: no body even with Content-Length
+        cntl.http_request().uri().set_path("/status");
+        cntl.http_request().set_method(HTTP_METHOD_HEAD);
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_TRUE(cntl.response_attachment().empty());
+    }
+    {
+        Controller cntl;
+        cntl.http_request().uri().set_path("/flags/max_body_size");
+        cntl.http_request().uri().SetQuery("setvalue", "12345678");
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        std::string v;
+        GetFlag("max_body_size", &v);
+        EXPECT_EQ(v, "12345678");
+        SetFlag("max_body_size", "67108864");
+    }
+}
+
+namespace {
+struct CollectReader : public ProgressiveReader {
+    std::string data;
+    std::atomic<int> ended{0};
+    Status st;
+    Status OnReadOnePart(const void* d, size_t n) override {
+        data.append((const char*)d, n);
+        return Status();
+    }
+    void OnEndOfMessage(const Status& s) override {
+        st = s;
+        ended.store(1);
+    }
+};
+}  // namespace
+
+TEST(Http, progressive_attachment_and_reader) {
+    HttpServer s;
+    Channel ch;
+    ChannelOptions opt;
+    opt.protocol = "http";
+    opt.timeout_ms = 3000;
+    ASSERT_EQ(ch.Init(s.addr().c_str(), &opt), 0);
+    // whole body
+    {
+        Controller cntl;
+        cntl.http_request().uri().set_path("/HttpTest/Push");
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_EQ(cntl.response_attachment().to_string(), "part0;part1;part2;part3;part4;");
+    }
+    // progressively
+    {
+        Controller cntl;
+        cntl.http_request().uri().set_path("/HttpTest/Push");
+        cntl.response_will_be_read_progressively();
+        ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        CollectReader r;
+        cntl.ReadProgressiveAttachmentBy(&r);
+        for (int i = 0; i < 300 && !r.ended.load(); ++i) usleep(10000);
+        EXPECT_EQ(r.ended.load(), 1);
+        EXPECT_TRUE(r.st.ok());
+        EXPECT_EQ(r.data, "part0;part1;part2;part3;part4;");
+    }
+}
