@@ -386,54 +386,109 @@ __global__ void __launch_bounds__(1024) scan_tiles_kernel(uint64_t* counts, uint
     if (threadIdx.x == 1023) *total = part[1023];
 }
 
+// Decode: lane owns 16 input bytes (one coalesced 16 B load) and sees the
+// previous lane's 16 bytes through a DPP shuffle (lane 0 of a wave loads
+// them), so every varint ending in its bytes (<= 10 bytes long) is decoded
+// from registers: a terminator mask locates the start, a 128-bit funnel
+// shift brings the bytes into two words and the 7-bit groups are packed
+// with shifts and masks. No data-dependent loops over global memory.
+__device__ __forceinline__ uint32_t term_mask16(uint4 v) {
+    // bit i set <=> byte i has its MSB clear (ends a varint)
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t t = ~w[i] & 0x80808080u;
+        m |= (((t >> 7) & 1u) | ((t >> 14) & 2u) | ((t >> 21) & 4u) | ((t >> 28) & 8u)) << (4 * i);
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint64_t pack7(uint64_t a, uint64_t b) {
+    // bytes a[0..7], b[0..1] -> 70 bits of payload, low 64 kept
+    uint64_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v |= ((a >> (8 * j)) & 0x7full) << (7 * j);
+    v |= (b & 0x7full) << 56;
+    v |= ((b >> 8) & 0x01ull) << 63;
+    return v;
+}
+
 __global__ void __launch_bounds__(kThreads) varint_decode_kernel(const uint8_t* __restrict__ in, uint64_t n,
                                                                  const uint64_t* __restrict__ tile_offsets,
                                                                  uint64_t* __restrict__ out, uint64_t max_out,
                                                                  int zigzag, int* __restrict__ err) {
     __shared__ uint32_t smem[kThreads / 64];
     const uint64_t base = (uint64_t)blockIdx.x * kVTile + threadIdx.x * 16;
-    union {
-        uint4 v;
-        uint8_t b[16];
-    } u;
-    uint8_t* bytes = u.b;
+    const int lane = threadIdx.x & 63;
+    uint4 cur = make_uint4(0, 0, 0, 0);
     int nb = 0;
     if (base < n) {
         nb = (int)(n - base < 16 ? n - base : 16);
         if (nb == 16 && (reinterpret_cast<uintptr_t>(in + base) & 15) == 0) {
-            u.v = *reinterpret_cast<const uint4*>(in + base);
+            cur = *reinterpret_cast<const uint4*>(in + base);
         } else {
-            for (int i = 0; i < nb; ++i) bytes[i] = in[base + i];
+            uint32_t w[4] = {0, 0, 0, 0};
+            for (int i = 0; i < nb; ++i) w[i >> 2] |= (uint32_t)in[base + i] << (8 * (i & 3));
+            cur = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
-    uint32_t c = 0;
-    for (int i = 0; i < nb; ++i) c += (bytes[i] & 0x80) ? 0 : 1;
-    uint32_t total;
-    uint64_t idx = tile_offsets[blockIdx.x] + block_exclusive_scan(c, &total, smem);
-    for (int i = 0; i < nb; ++i) {
-        if (bytes[i] & 0x80) continue;
-        // terminator at base+i: walk back over continuation bytes
-        const uint64_t p = base + i;
-        uint64_t start = p;
-        int len = 1;
-        while (start > 0 && len <= 10 && (in[start - 1] & 0x80)) {
-            --start;
-            ++len;
+    // previous 16 bytes: neighbour lane, or memory for lane 0 (zeros before
+    // the stream start act as terminators)
+    uint4 prev;
+    prev.x = __shfl_up(cur.x, 1, 64);
+    prev.y = __shfl_up(cur.y, 1, 64);
+    prev.z = __shfl_up(cur.z, 1, 64);
+    prev.w = __shfl_up(cur.w, 1, 64);
+    if (lane == 0) {
+        if (base >= 16) {
+            if ((reinterpret_cast<uintptr_t>(in + base - 16) & 15) == 0) {
+                prev = *reinterpret_cast<const uint4*>(in + base - 16);
+            } else {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int i = 0; i < 16; ++i) w[i >> 2] |= (uint32_t)in[base - 16 + i] << (8 * (i & 3));
+                prev = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        } else {
+            prev = make_uint4(0, 0, 0, 0);
         }
-        if (len > 10) {
+    }
+    uint32_t tcur = term_mask16(cur);
+    if (nb < 16) tcur &= (1u << nb) - 1;  // bytes past the end are not terminators
+    const uint32_t window_terms = term_mask16(prev) | (tcur << 16);
+    uint32_t total;
+    uint64_t idx = tile_offsets[blockIdx.x] + block_exclusive_scan(__popc(tcur), &total, smem);
+    const uint64_t W[4] = {((uint64_t)prev.y << 32) | prev.x, ((uint64_t)prev.w << 32) | prev.z,
+                           ((uint64_t)cur.y << 32) | cur.x, ((uint64_t)cur.w << 32) | cur.z};
+    uint32_t t = tcur;
+    while (t) {
+        const int i = __ffs(t) - 1;  // terminator at window position 16+i
+        t &= t - 1;
+        const int end = 16 + i;
+        const uint32_t below = window_terms & ((1u << end) - 1);
+        const int start = below ? 32 - __clz(below) : 0;  // after the previous terminator
+        const int len = end - start + 1;
+        if (len > 10 || (!below && base >= 16)) {
             atomicOr(err, 1);
             ++idx;
             continue;
         }
-        uint64_t v = 0;
-        for (int j = 0; j < len; ++j) v |= (uint64_t)(in[start + j] & 0x7f) << (7 * j);
+        // 16 bytes from window position `start` (start <= 31): funnel shift
+        const int wi = start >> 3, sh = (start & 7) * 8;
+        const uint64_t w0 = W[wi];
+        const uint64_t w1 = wi + 1 < 4 ? W[wi + 1] : 0;
+        const uint64_t w2 = wi + 2 < 4 ? W[wi + 2] : 0;
+        const uint64_t a = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+        const uint64_t b = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+        uint64_t v = pack7(a, b);
+        if (len < 10) v &= (1ull << (7 * len)) - 1;
         if (zigzag) v = (v >> 1) ^ (~(v & 1) + 1);
         if (idx < max_out) out[idx] = v;
         else atomicOr(err, 2);
         ++idx;
     }
     // a trailing continuation byte means truncated input
-    if (base + nb == n && nb > 0 && (bytes[nb - 1] & 0x80)) atomicOr(err, 1);
+    if (nb > 0 && base + nb == n && !((tcur >> (nb - 1)) & 1)) atomicOr(err, 1);
 }
 
 __device__ __forceinline__ uint32_t varint_len(uint64_t v) {
@@ -442,15 +497,34 @@ __device__ __forceinline__ uint32_t varint_len(uint64_t v) {
     return (uint32_t)((bits + 6) / 7);
 }
 
+__device__ __forceinline__ uint64_t zz(uint64_t v, int zigzag) {
+    return zigzag ? (v << 1) ^ (uint64_t)((int64_t)v >> 63) : v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    return x;
+}
+
+// Encode: a tile is 4096 values; wave w owns values [1024w, 1024w+1024) and
+// walks them 64 at a time with coalesced 8 B loads. Pass 1 of the kernel
+// sums the wave's encoded length, the 4 wave totals are scanned in LDS,
+// pass 2 re-reads the (cache-resident) values and writes each varint at
+// tile_offset + wave_prefix + in-wave scan.
 __global__ void __launch_bounds__(kThreads) varint_len_kernel(const uint64_t* __restrict__ in, uint64_t n,
                                                               int zigzag, uint64_t* __restrict__ tile_counts) {
     __shared__ uint32_t smem[kThreads / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kVTile + threadIdx.x * 16;
+    const uint64_t base = (uint64_t)blockIdx.x * kVTile + (threadIdx.x >> 6) * 1024 + (threadIdx.x & 63);
     uint32_t c = 0;
-    for (uint64_t i = base; i < base + 16 && i < n; ++i) {
-        uint64_t v = in[i];
-        if (zigzag) v = (v << 1) ^ (uint64_t)((int64_t)v >> 63);
-        c += varint_len(v);
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = base + (uint64_t)k * 64;
+        if (i < n) c += varint_len(zz(in[i], zigzag));
     }
     uint32_t total;
     block_exclusive_scan(c, &total, smem);
@@ -461,26 +535,33 @@ __global__ void __launch_bounds__(kThreads) varint_encode_kernel(const uint64_t*
                                                                  int zigzag,
                                                                  const uint64_t* __restrict__ tile_offsets,
                                                                  uint8_t* __restrict__ out) {
-    __shared__ uint32_t smem[kThreads / 64];
-    const uint64_t base = (uint64_t)blockIdx.x * kVTile + threadIdx.x * 16;
-    uint64_t vals[16];
+    __shared__ uint32_t wave_tot[kThreads / 64];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * kVTile + (uint64_t)wave * 1024 + lane;
     uint32_t c = 0;
-    int nv = 0;
-    for (uint64_t i = base; i < base + 16 && i < n; ++i) {
-        uint64_t v = in[i];
-        if (zigzag) v = (v << 1) ^ (uint64_t)((int64_t)v >> 63);
-        vals[nv++] = v;
-        c += varint_len(v);
+#pragma unroll 4
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = base + (uint64_t)k * 64;
+        if (i < n) c += varint_len(zz(in[i], zigzag));
     }
-    uint32_t total;
-    uint64_t pos = tile_offsets[blockIdx.x] + block_exclusive_scan(c, &total, smem);
-    for (int k = 0; k < nv; ++k) {
-        uint64_t v = vals[k];
-        while (v >= 0x80) {
-            out[pos++] = (uint8_t)(v | 0x80);
+    const uint32_t wt = wave_incl_scan(c);
+    if (lane == 63) wave_tot[wave] = wt;
+    __syncthreads();
+    uint64_t pos = tile_offsets[blockIdx.x];
+    for (int w = 0; w < wave; ++w) pos += wave_tot[w];
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = base + (uint64_t)k * 64;
+        uint64_t v = i < n ? zz(in[i], zigzag) : 0;
+        const uint32_t L = i < n ? varint_len(v) : 0;
+        const uint32_t incl = wave_incl_scan(L);
+        const uint32_t wsum = __shfl(incl, 63, 64);
+        uint8_t* dst = out + pos + (incl - L);
+        for (uint32_t j = 0; j < L; ++j) {
+            dst[j] = (uint8_t)((v & 0x7f) | (j + 1 < L ? 0x80 : 0));
             v >>= 7;
         }
-        out[pos++] = (uint8_t)v;
+        pos += wsum;
     }
 }
 
