@@ -46,6 +46,7 @@ public:
     bool is_response = false;
     bool keep_alive = true;
     PipelinedInfo pi;                           // client: the call this response answers
+    uint32_t stream_id = 0;                     // h2: stream of this message
     std::shared_ptr<ProgressiveSink> progressive;  // client: body continues through the sink
 };
 

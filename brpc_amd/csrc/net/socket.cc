@@ -147,7 +147,7 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
     m->_error_code = 0;
     m->_error_text.clear();
     m->_preferred_index = -1;
-    m->_parsing_context = nullptr;
+    m->_parsing_context.store(nullptr, std::memory_order_relaxed);
     m->_avg_msg_size = 0;
     m->_server_verified.store(false);
     m->_auth_error.store(0);
@@ -334,8 +334,7 @@ void Socket::OnRecycle() {
     }
     _read_buf.clear();
     _read_buf.return_cached_blocks();
-    delete _parsing_context;
-    _parsing_context = nullptr;
+    delete _parsing_context.exchange(nullptr);
     {
         std::lock_guard<std::mutex> g(_pipeline_mu);
         _pipeline_q.clear();
@@ -363,9 +362,11 @@ void Socket::OnRecycle() {
     g_nsocket.fetch_sub(1, std::memory_order_relaxed);
 }
 
-void Socket::reset_parsing_context(ParsingContext* ctx) {
-    delete _parsing_context;
-    _parsing_context = ctx;
+void Socket::reset_parsing_context(ParsingContext* ctx) { delete _parsing_context.exchange(ctx); }
+
+bool Socket::InstallParsingContext(ParsingContext* ctx) {
+    ParsingContext* expected = nullptr;
+    return _parsing_context.compare_exchange_strong(expected, ctx, std::memory_order_acq_rel);
 }
 
 std::shared_ptr<Transport> Socket::transport() const {
@@ -797,8 +798,7 @@ int Socket::Revive(int new_fd) {
         _read_buf.clear();
         _nevent.store(0);
         _preferred_index = -1;
-        delete _parsing_context;
-        _parsing_context = nullptr;
+        delete _parsing_context.exchange(nullptr);
         {
             std::lock_guard<std::mutex> g(_pipeline_mu);
             _pipeline_q.clear();

@@ -156,9 +156,11 @@ public:
     BufPortal _read_buf;
     int _preferred_index = -1;          // protocol index that parsed the last message
     // Protocol private per-connection state (http parser, h2 context, ...).
-    ParsingContext* parsing_context() const { return _parsing_context; }
+    ParsingContext* parsing_context() const { return _parsing_context.load(std::memory_order_acquire); }
     void reset_parsing_context(ParsingContext* ctx);
-    ParsingContext* _parsing_context = nullptr;
+    // Install ctx if none is set yet; false (ctx untouched) if another won.
+    bool InstallParsingContext(ParsingContext* ctx);
+    std::atomic<ParsingContext*> _parsing_context{nullptr};
     int64_t _avg_msg_size = 0;
     std::atomic<bool> _server_verified{false};  // server-side authentication done
 

@@ -1,0 +1,1021 @@
+// HTTP/2 and gRPC (role of the reference's
+// src/brpc/policy/http2_rpc_protocol.cpp: ParseH2Message :1100,
+// H2Context::Consume :469, OnHeaders/OnData/OnSettings/OnWindowUpdate/
+// OnGoAway :547-1035, PackH2Request :1775; grpc framing from
+// http_rpc_protocol.cpp:243-253 and grpc.cpp).
+//
+// One H2Context per connection (the socket's parsing context) owns the
+// HPACK tables, the stream map and both flow-control windows. The reader
+// fiber consumes frames; any fiber may start a request or send a response.
+// Everything that must follow wire order — stream-id allocation, the HPACK
+// encoder state, writing the frames — happens under the context mutex, so
+// the byte order on the socket always equals the encoder order.
+#include <arpa/inet.h>
+
+#include <cerrno>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <unordered_map>
+
+#include "base/flags.h"
+#include "base/logging.h"
+#include "base/time.h"
+#include "base/util.h"
+#include "fiber/call_id.h"
+#include "http/hpack.h"
+#include "http/http_header.h"
+#include "http/http_message.h"
+#include "json/json2pb.h"
+#include "net/input_messenger.h"
+#include "policy/policies.h"
+#include "rpc/authenticator.h"
+#include "rpc/controller.h"
+#include "rpc/errno.h"
+#include "rpc/grpc.h"
+#include "rpc/method_status.h"
+#include "rpc/protocol.h"
+#include "rpc/server.h"
+
+DECLARE_uint64(max_body_size);
+DEFINE_int32(h2_client_stream_window_size, 256 * 1024, "initial receive window of each h2 stream");
+DEFINE_int32(h2_client_connection_window_size, 1024 * 1024, "receive window of each h2 connection");
+DEFINE_int32(h2_max_concurrent_streams, 100000, "SETTINGS_MAX_CONCURRENT_STREAMS we advertise");
+
+namespace mrpc {
+namespace policy {
+
+namespace {
+
+enum : uint8_t {
+    H2_DATA = 0,
+    H2_HEADERS = 1,
+    H2_PRIORITY = 2,
+    H2_RST_STREAM = 3,
+    H2_SETTINGS = 4,
+    H2_PUSH_PROMISE = 5,
+    H2_PING = 6,
+    H2_GOAWAY = 7,
+    H2_WINDOW_UPDATE = 8,
+    H2_CONTINUATION = 9,
+};
+enum : uint8_t { F_END_STREAM = 1, F_ACK = 1, F_END_HEADERS = 4, F_PADDED = 8, F_PRIORITY = 0x20 };
+enum : uint32_t { H2_NO_ERROR = 0, H2_PROTOCOL_ERROR = 1, H2_INTERNAL_ERROR = 2, H2_FLOW_CONTROL_ERROR = 3,
+                  H2_FRAME_SIZE_ERROR = 6, H2_REFUSED_STREAM = 7, H2_CANCEL = 8, H2_COMPRESSION_ERROR = 9 };
+
+const char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
+const size_t kPrefaceLen = 24;
+const uint32_t kDefaultWindow = 65535;
+const uint32_t kFrameSize = 16384;
+
+struct Settings {
+    uint32_t header_table_size = 4096;
+    uint32_t enable_push = 1;
+    uint32_t max_concurrent_streams = 0xFFFFFFFF;
+    uint32_t initial_window_size = kDefaultWindow;
+    uint32_t max_frame_size = kFrameSize;
+    uint32_t max_header_list_size = 0xFFFFFFFF;
+};
+
+void frame_header(Buf* out, uint32_t len, uint8_t type, uint8_t flags, uint32_t sid) {
+    char h[9];
+    h[0] = (char)(len >> 16);
+    h[1] = (char)(len >> 8);
+    h[2] = (char)len;
+    h[3] = (char)type;
+    h[4] = (char)flags;
+    const uint32_t be = htonl(sid & 0x7FFFFFFF);
+    memcpy(h + 5, &be, 4);
+    out->append(h, 9);
+}
+
+struct Stream {
+    uint32_t id = 0;
+    HttpMessage* msg = nullptr;  // being received
+    std::string header_block;
+    bool got_headers = false;
+    int64_t send_window = kDefaultWindow;
+    int64_t recv_unacked = 0;
+    Buf pending;                 // data blocked by flow control
+    bool pending_end = false;    // END_STREAM after pending (no trailers)
+    std::vector<HPackHeader> pending_trailers;
+    bool has_pending_trailers = false;
+    fiber::CallId cid = fiber::INVALID_CALL_ID;  // client
+    ~Stream() { delete msg; }
+};
+
+}  // namespace
+
+class H2Context : public ParsingContext {
+public:
+    static const int kTag = 0x48324358;  // "H2CX"
+    int protocol_tag() const override { return kTag; }
+
+    H2Context(bool server) : _server(server), _next_stream_id(1) {}
+    ~H2Context() override {
+        for (auto& kv : _streams) {
+            if (kv.second->cid != fiber::INVALID_CALL_ID) {
+                fiber::call_id_error(kv.second->cid, EFAILEDSOCKET, "h2 connection closed");
+            }
+            delete kv.second;
+        }
+    }
+    bool server() const { return _server; }
+
+    // ---------------------------------------------------------------- read
+    ParseResult Consume(Buf* src, Socket* s);
+
+    // ---------------------------------------------------------------- write
+    // Client: open a stream for `cntl` and send HEADERS (+DATA).
+    int StartRequest(Socket* s, fiber::CallId cid, const std::vector<HPackHeader>& headers, Buf* body,
+                     std::string* err);
+    // Server: respond on `sid`; trailers may be null.
+    int SendResponse(Socket* s, uint32_t sid, const std::vector<HPackHeader>& headers, Buf* body,
+                     const std::vector<HPackHeader>* trailers);
+    void CancelStream(Socket* s, uint32_t sid);
+
+private:
+    int on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Buf& payload, HttpMessage** done);
+    int on_headers_complete(Socket* s, Stream* st, bool end_stream, HttpMessage** done);
+    int on_settings(Socket* s, uint8_t flags, Buf& payload);
+    void write_locked(Socket* s, Buf* frames, fiber::CallId id_wait = fiber::INVALID_CALL_ID);
+    void encode_headers_locked(Buf* out, uint32_t sid, const std::vector<HPackHeader>& h, bool end_stream);
+    void flush_stream_locked(Buf* out, Stream* st);
+    void send_local_settings_locked(Buf* out);
+    void maybe_window_update_locked(Buf* out, Stream* st);
+    Stream* find(uint32_t sid) {
+        auto it = _streams.find(sid);
+        return it == _streams.end() ? nullptr : it->second;
+    }
+    void erase(uint32_t sid) {
+        auto it = _streams.find(sid);
+        if (it != _streams.end()) {
+            delete it->second;
+            _streams.erase(it);
+        }
+    }
+    int fail_connection(Socket* s, uint32_t code, const char* why);
+
+    const bool _server;
+    std::mutex _mu;
+    HPackEncoder _enc;
+    HPackDecoder _dec;
+    Settings _remote;
+    bool _preface_done = false;     // server: client preface seen
+    bool _settings_sent = false;
+    uint32_t _next_stream_id;       // client
+    uint32_t _last_peer_stream = 0; // server
+    uint32_t _cont_sid = 0;         // stream with an unfinished header block
+    bool _cont_end_stream = false;  // END_STREAM seen on that block's HEADERS
+    int64_t _conn_send_window = kDefaultWindow;
+    int64_t _conn_recv_unacked = 0;
+    bool _goaway = false;
+    std::unordered_map<uint32_t, Stream*> _streams;
+};
+
+void H2Context::write_locked(Socket* s, Buf* frames, fiber::CallId id_wait) {
+    if (frames->empty()) return;
+    WriteOptions opt;
+    opt.ignore_eovercrowded = true;
+    opt.id_wait = id_wait;
+    s->Write(frames, &opt);
+}
+
+void H2Context::send_local_settings_locked(Buf* out) {
+    if (_settings_sent) return;
+    _settings_sent = true;
+    if (!_server) out->append(kPreface, kPrefaceLen);
+    struct {
+        uint16_t id;
+        uint32_t v;
+    } params[] = {{2, 0},
+                  {3, (uint32_t)FLAGS_h2_max_concurrent_streams},
+                  {4, (uint32_t)FLAGS_h2_client_stream_window_size},
+                  {5, kFrameSize}};
+    const int n = sizeof(params) / sizeof(params[0]);
+    frame_header(out, 6 * n, H2_SETTINGS, 0, 0);
+    for (auto& p : params) {
+        char b[6];
+        const uint16_t id = htons(p.id);
+        const uint32_t v = htonl(p.v);
+        memcpy(b, &id, 2);
+        memcpy(b + 2, &v, 4);
+        out->append(b, 6);
+    }
+    // raise the connection-level receive window beyond the fixed 65535
+    const uint32_t inc = (uint32_t)FLAGS_h2_client_connection_window_size - kDefaultWindow;
+    if ((int64_t)FLAGS_h2_client_connection_window_size > kDefaultWindow) {
+        frame_header(out, 4, H2_WINDOW_UPDATE, 0, 0);
+        const uint32_t be = htonl(inc);
+        out->append(&be, 4);
+    }
+}
+
+void H2Context::encode_headers_locked(Buf* out, uint32_t sid, const std::vector<HPackHeader>& h, bool end_stream) {
+    Buf block;
+    for (const HPackHeader& x : h) {
+        const bool sensitive = strcasecmp(x.name.c_str(), "authorization") == 0;
+        _enc.Encode(&block, x, sensitive ? HPackIndexPolicy::NEVER_INDEXED : HPackIndexPolicy::INCREMENTAL);
+    }
+    const uint32_t maxf = _remote.max_frame_size;
+    bool first = true;
+    do {
+        Buf piece;
+        block.cutn(&piece, std::min<size_t>(block.size(), maxf));
+        const bool last = block.empty();
+        uint8_t flags = last ? F_END_HEADERS : 0;
+        if (first && end_stream) flags |= F_END_STREAM;
+        frame_header(out, (uint32_t)piece.size(), first ? H2_HEADERS : H2_CONTINUATION, flags, sid);
+        out->append(std::move(piece));
+        first = false;
+    } while (!block.empty());
+}
+
+// Moves as much pending data as the windows allow into `out`.
+void H2Context::flush_stream_locked(Buf* out, Stream* st) {
+    while (!st->pending.empty()) {
+        const int64_t allow =
+            std::min<int64_t>({(int64_t)st->pending.size(), st->send_window, _conn_send_window,
+                               (int64_t)_remote.max_frame_size});
+        if (allow <= 0) return;
+        Buf piece;
+        st->pending.cutn(&piece, (size_t)allow);
+        st->send_window -= allow;
+        _conn_send_window -= allow;
+        const bool end = st->pending.empty() && st->pending_end && !st->has_pending_trailers;
+        frame_header(out, (uint32_t)piece.size(), H2_DATA, end ? F_END_STREAM : 0, st->id);
+        out->append(std::move(piece));
+    }
+    if (st->pending.empty()) {
+        if (st->has_pending_trailers) {
+            encode_headers_locked(out, st->id, st->pending_trailers, true);
+            st->has_pending_trailers = false;
+            st->pending_trailers.clear();
+            st->pending_end = false;
+            if (_server) erase(st->id);  // response complete
+            return;
+        }
+        if (st->pending_end) {
+            st->pending_end = false;
+            if (_server) erase(st->id);
+        }
+    }
+}
+
+int H2Context::StartRequest(Socket* s, fiber::CallId cid, const std::vector<HPackHeader>& headers, Buf* body,
+                            std::string* err) {
+    std::lock_guard<std::mutex> g(_mu);
+    if (_goaway) {
+        *err = "h2 connection is going away";
+        return -1;
+    }
+    if (_next_stream_id > 0x7FFFFFFF - 2) {
+        *err = "h2 stream ids exhausted";
+        return -1;
+    }
+    Buf out;
+    send_local_settings_locked(&out);
+    Stream* st = new Stream;
+    st->id = _next_stream_id;
+    _next_stream_id += 2;
+    st->cid = cid;
+    st->send_window = _remote.initial_window_size;
+    _streams[st->id] = st;
+    const bool has_body = body && !body->empty();
+    encode_headers_locked(&out, st->id, headers, !has_body);
+    if (has_body) {
+        st->pending.append(std::move(*body));
+        st->pending_end = true;
+        flush_stream_locked(&out, st);
+    }
+    write_locked(s, &out, cid);
+    return 0;
+}
+
+int H2Context::SendResponse(Socket* s, uint32_t sid, const std::vector<HPackHeader>& headers, Buf* body,
+                            const std::vector<HPackHeader>* trailers) {
+    std::lock_guard<std::mutex> g(_mu);
+    Stream* st = find(sid);
+    if (!st) return -1;  // reset by the client
+    Buf out;
+    const bool has_body = body && !body->empty();
+    encode_headers_locked(&out, sid, headers, !has_body && !trailers);
+    if (has_body || trailers) {
+        if (has_body) st->pending.append(std::move(*body));
+        st->pending_end = true;
+        if (trailers) {
+            st->pending_trailers = *trailers;
+            st->has_pending_trailers = true;
+        }
+        flush_stream_locked(&out, st);
+    } else {
+        erase(sid);
+    }
+    write_locked(s, &out);
+    return 0;
+}
+
+void H2Context::CancelStream(Socket* s, uint32_t sid) {
+    std::lock_guard<std::mutex> g(_mu);
+    if (!find(sid)) return;
+    erase(sid);
+    Buf out;
+    frame_header(&out, 4, H2_RST_STREAM, 0, sid);
+    const uint32_t be = htonl(H2_CANCEL);
+    out.append(&be, 4);
+    write_locked(s, &out);
+}
+
+int H2Context::fail_connection(Socket* s, uint32_t code, const char* why) {
+    {
+        std::lock_guard<std::mutex> g(_mu);
+        Buf out;
+        frame_header(&out, 8, H2_GOAWAY, 0, 0);
+        const uint32_t last = htonl(_last_peer_stream);
+        const uint32_t be = htonl(code);
+        out.append(&last, 4);
+        out.append(&be, 4);
+        write_locked(s, &out);
+        _goaway = true;
+    }
+    LOG_EVERY_SECOND(WARNING) << "h2 connection error on " << s->remote_side() << ": " << why;
+    return -1;
+}
+
+void H2Context::maybe_window_update_locked(Buf* out, Stream* st) {
+    if (_conn_recv_unacked >= FLAGS_h2_client_connection_window_size / 2) {
+        frame_header(out, 4, H2_WINDOW_UPDATE, 0, 0);
+        const uint32_t be = htonl((uint32_t)_conn_recv_unacked);
+        out->append(&be, 4);
+        _conn_recv_unacked = 0;
+    }
+    if (st && st->recv_unacked >= FLAGS_h2_client_stream_window_size / 2) {
+        frame_header(out, 4, H2_WINDOW_UPDATE, 0, st->id);
+        const uint32_t be = htonl((uint32_t)st->recv_unacked);
+        out->append(&be, 4);
+        st->recv_unacked = 0;
+    }
+}
+
+int H2Context::on_settings(Socket* s, uint8_t flags, Buf& payload) {
+    if (flags & F_ACK) return 0;
+    if (payload.size() % 6) return fail_connection(s, H2_FRAME_SIZE_ERROR, "bad SETTINGS length");
+    std::lock_guard<std::mutex> g(_mu);
+    while (!payload.empty()) {
+        unsigned char b[6];
+        payload.cutn(b, 6);
+        const uint16_t id = (uint16_t)((b[0] << 8) | b[1]);
+        const uint32_t v = ((uint32_t)b[2] << 24) | ((uint32_t)b[3] << 16) | ((uint32_t)b[4] << 8) | b[5];
+        switch (id) {
+        case 1:
+            _remote.header_table_size = v;
+            _enc.ResizeTable(v);
+            break;
+        case 2: _remote.enable_push = v; break;
+        case 3: _remote.max_concurrent_streams = v; break;
+        case 4: {
+            if (v > 0x7FFFFFFF) return -1;
+            const int64_t delta = (int64_t)v - (int64_t)_remote.initial_window_size;
+            _remote.initial_window_size = v;
+            for (auto& kv : _streams) kv.second->send_window += delta;
+            break;
+        }
+        case 5:
+            if (v < kFrameSize || v > 16777215) return -1;
+            _remote.max_frame_size = v;
+            break;
+        case 6: _remote.max_header_list_size = v; break;
+        default: break;  // unknown settings are ignored
+        }
+    }
+    Buf out;
+    send_local_settings_locked(&out);
+    frame_header(&out, 0, H2_SETTINGS, F_ACK, 0);
+    for (auto& kv : _streams) flush_stream_locked(&out, kv.second);
+    write_locked(s, &out);
+    return 0;
+}
+
+int H2Context::on_headers_complete(Socket* s, Stream* st, bool end_stream, HttpMessage** done) {
+    std::vector<HPackHeader> hs;
+    if (!_dec.Decode(st->header_block, &hs)) return fail_connection(s, H2_COMPRESSION_ERROR, "bad header block");
+    st->header_block.clear();
+    if (!st->msg) {
+        st->msg = new HttpMessage;
+        st->msg->header.set_version(2, 0);
+        st->msg->is_response = !_server;
+    }
+    HttpHeader& h = st->msg->header;
+    for (HPackHeader& x : hs) {
+        if (x.name.empty()) continue;
+        if (x.name[0] == ':') {
+            if (x.name == ":method") {
+                HttpMethod m;
+                if (Str2HttpMethod(x.value, &m)) h.set_method(m);
+            } else if (x.name == ":path") {
+                h.uri().SetHttpURL(x.value);
+            } else if (x.name == ":authority") {
+                h.SetHeader("host", x.value);
+            } else if (x.name == ":status") {
+                h.set_status_code(atoi(x.value.c_str()));
+            }
+            continue;
+        }
+        if (x.name == "content-type") {
+            h.set_content_type(x.value);
+        } else {
+            h.AppendHeader(x.name, x.value);
+        }
+    }
+    st->got_headers = true;
+    if (end_stream) {
+        *done = st->msg;
+        st->msg = nullptr;
+        (*done)->pi.id_wait = st->cid;
+        if (!_server) erase(st->id);
+    }
+    return 0;
+}
+
+int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Buf& payload, HttpMessage** done) {
+    if (_cont_sid && (type != H2_CONTINUATION || sid != _cont_sid)) {
+        return fail_connection(s, H2_PROTOCOL_ERROR, "expected CONTINUATION");
+    }
+    switch (type) {
+    case H2_SETTINGS:
+        if (sid) return fail_connection(s, H2_PROTOCOL_ERROR, "SETTINGS on a stream");
+        return on_settings(s, flags, payload);
+    case H2_PING: {
+        if (flags & F_ACK) return 0;
+        if (payload.size() != 8) return fail_connection(s, H2_FRAME_SIZE_ERROR, "bad PING");
+        std::lock_guard<std::mutex> g(_mu);
+        Buf out;
+        frame_header(&out, 8, H2_PING, F_ACK, 0);
+        out.append(std::move(payload));
+        write_locked(s, &out);
+        return 0;
+    }
+    case H2_WINDOW_UPDATE: {
+        if (payload.size() != 4) return fail_connection(s, H2_FRAME_SIZE_ERROR, "bad WINDOW_UPDATE");
+        unsigned char b[4];
+        payload.cutn(b, 4);
+        const uint32_t inc = (((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3]) &
+                             0x7FFFFFFF;
+        std::lock_guard<std::mutex> g(_mu);
+        Buf out;
+        if (sid == 0) {
+            _conn_send_window += inc;
+            for (auto& kv : _streams) flush_stream_locked(&out, kv.second);
+        } else if (Stream* st = find(sid)) {
+            st->send_window += inc;
+            flush_stream_locked(&out, st);
+        }
+        write_locked(s, &out);
+        return 0;
+    }
+    case H2_GOAWAY: {
+        std::vector<std::pair<fiber::CallId, uint32_t>> failed;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            _goaway = true;
+            uint32_t last = 0;
+            if (payload.size() >= 4) {
+                unsigned char b[4];
+                payload.copy_to(b, 4);
+                last = (((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3]) & 0x7FFFFFFF;
+            }
+            for (auto it = _streams.begin(); it != _streams.end();) {
+                if (!_server && it->first > last) {
+                    failed.emplace_back(it->second->cid, it->first);
+                    delete it->second;
+                    it = _streams.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+        }
+        for (auto& f : failed) fiber::call_id_error(f.first, EFAILEDSOCKET, "h2 GOAWAY before the stream ran");
+        if (!_server) s->SetFailed(EEOF, "h2 GOAWAY from %s", s->remote_side().to_string().c_str());
+        return 0;
+    }
+    case H2_RST_STREAM: {
+        fiber::CallId cid = fiber::INVALID_CALL_ID;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            if (Stream* st = find(sid)) {
+                cid = st->cid;
+                erase(sid);
+            }
+        }
+        if (cid != fiber::INVALID_CALL_ID) fiber::call_id_error(cid, EREQUEST, "h2 stream reset by the server");
+        return 0;
+    }
+    case H2_PRIORITY:
+    case H2_PUSH_PROMISE:
+        return 0;  // priorities are advisory; we never enable push
+    case H2_HEADERS:
+    case H2_CONTINUATION: {
+        if (sid == 0) return fail_connection(s, H2_PROTOCOL_ERROR, "HEADERS on stream 0");
+        size_t pad = 0;
+        if (type == H2_HEADERS) {
+            if (flags & F_PADDED) {
+                unsigned char p;
+                payload.cutn(&p, 1);
+                pad = p;
+            }
+            if (flags & F_PRIORITY) payload.pop_front(5);
+            if (pad > payload.size()) return fail_connection(s, H2_PROTOCOL_ERROR, "bad padding");
+            payload.pop_back(pad);
+        }
+        Stream* st;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            st = find(sid);
+            if (!st) {
+                if (!_server || type == H2_CONTINUATION) return 0;  // stream already gone
+                if ((sid & 1) == 0 || sid <= _last_peer_stream) {
+                    return fail_connection(s, H2_PROTOCOL_ERROR, "bad client stream id");
+                }
+                _last_peer_stream = sid;
+                st = new Stream;
+                st->id = sid;
+                st->send_window = _remote.initial_window_size;
+                _streams[sid] = st;
+            }
+        }
+        st->header_block.append(payload.to_string());
+        if (!(flags & F_END_HEADERS)) {
+            _cont_sid = sid;
+            if (type == H2_HEADERS) _cont_end_stream = flags & F_END_STREAM;
+            return 0;
+        }
+        const bool end_stream = type == H2_HEADERS ? (flags & F_END_STREAM) : _cont_end_stream;
+        _cont_sid = 0;
+        _cont_end_stream = false;
+        return on_headers_complete(s, st, end_stream, done);
+    }
+    case H2_DATA: {
+        if (sid == 0) return fail_connection(s, H2_PROTOCOL_ERROR, "DATA on stream 0");
+        const size_t flow_len = payload.size();
+        if (flags & F_PADDED) {
+            unsigned char p;
+            payload.cutn(&p, 1);
+            if (p > payload.size()) return fail_connection(s, H2_PROTOCOL_ERROR, "bad padding");
+            payload.pop_back(p);
+        }
+        std::lock_guard<std::mutex> g(_mu);
+        Stream* st = find(sid);
+        _conn_recv_unacked += flow_len;
+        Buf out;
+        if (!st || !st->msg) {
+            maybe_window_update_locked(&out, nullptr);
+            write_locked(s, &out);
+            return 0;
+        }
+        st->recv_unacked += flow_len;
+        if (st->msg->body.size() + payload.size() > FLAGS_max_body_size) {
+            return fail_connection(s, H2_INTERNAL_ERROR, "h2 body exceeds max_body_size");
+        }
+        st->msg->body.append(std::move(payload));
+        if (flags & F_END_STREAM) {
+            *done = st->msg;
+            st->msg = nullptr;
+            (*done)->pi.id_wait = st->cid;
+            if (!_server) erase(sid);
+        } else {
+            maybe_window_update_locked(&out, st);
+        }
+        if (flags & F_END_STREAM) maybe_window_update_locked(&out, nullptr);
+        write_locked(s, &out);
+        return 0;
+    }
+    default:
+        return 0;  // unknown frame types are ignored
+    }
+}
+
+ParseResult H2Context::Consume(Buf* src, Socket* s) {
+    if (_server && !_preface_done) {
+        if (src->size() < kPrefaceLen) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+        char p[kPrefaceLen];
+        src->copy_to(p, kPrefaceLen);
+        if (memcmp(p, kPreface, kPrefaceLen) != 0) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+        src->pop_front(kPrefaceLen);
+        _preface_done = true;
+        std::lock_guard<std::mutex> g(_mu);
+        Buf out;
+        send_local_settings_locked(&out);
+        write_locked(s, &out);
+    }
+    for (;;) {
+        if (src->size() < 9) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+        unsigned char h[9];
+        src->copy_to(h, 9);
+        const uint32_t len = ((uint32_t)h[0] << 16) | ((uint32_t)h[1] << 8) | h[2];
+        if (len > kFrameSize) {
+            fail_connection(s, H2_FRAME_SIZE_ERROR, "frame larger than SETTINGS_MAX_FRAME_SIZE");
+            return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+        }
+        if (src->size() < 9 + (size_t)len) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+        const uint8_t type = h[3], flags = h[4];
+        const uint32_t sid = (((uint32_t)h[5] << 24) | ((uint32_t)h[6] << 16) | ((uint32_t)h[7] << 8) | h[8]) &
+                             0x7FFFFFFF;
+        src->pop_front(9);
+        Buf payload;
+        src->cutn(&payload, len);
+        HttpMessage* done = nullptr;
+        if (on_frame(s, type, flags, sid, payload, &done) != 0) {
+            return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+        }
+        if (done) {
+            done->stream_id = sid;
+            return MakeMessage(done);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ glue
+static bool is_client_socket(Socket* s) { return s->user() == get_client_side_messenger(); }
+
+static bool looks_like_settings(Buf* src) {
+    if (src->size() < 9) return false;
+    unsigned char h[9];
+    src->copy_to(h, 9);
+    const uint32_t len = ((uint32_t)h[0] << 16) | ((uint32_t)h[1] << 8) | h[2];
+    return h[3] == H2_SETTINGS && (h[5] | h[6] | h[7] | h[8]) == 0 && len % 6 == 0 && len <= 60;
+}
+
+static H2Context* client_context(Socket* s) {
+    ParsingContext* ctx = s->parsing_context();
+    if (ctx) return ctx->protocol_tag() == H2Context::kTag ? static_cast<H2Context*>(ctx) : nullptr;
+    H2Context* c = new H2Context(false);
+    if (!s->InstallParsingContext(c)) {
+        delete c;
+        ctx = s->parsing_context();
+        return ctx && ctx->protocol_tag() == H2Context::kTag ? static_cast<H2Context*>(ctx) : nullptr;
+    }
+    return c;
+}
+
+ParseResult ParseH2Message(Buf* source, Socket* socket, bool read_eof, const void* arg) {
+    ParsingContext* ctx = socket->parsing_context();
+    if (ctx && ctx->protocol_tag() != H2Context::kTag) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+    H2Context* h2 = static_cast<H2Context*>(ctx);
+    if (!h2) {
+        if (is_client_socket(socket)) {
+            // a server that speaks first (SETTINGS right after accept)
+            if (!looks_like_settings(source)) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+            h2 = client_context(socket);
+            if (!h2) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+        } else {
+            const size_t n = std::min(source->size(), kPrefaceLen);
+            char p[kPrefaceLen];
+            source->copy_to(p, n);
+            if (memcmp(p, kPreface, n) != 0) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+            if (n < kPrefaceLen) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+            H2Context* c = new H2Context(true);
+            if (!socket->InstallParsingContext(c)) {
+                delete c;
+                return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+            }
+            h2 = c;
+        }
+    }
+    return h2->Consume(source, socket);
+}
+
+static bool is_grpc_content(const std::string& ct) { return starts_with(ct, "application/grpc"); }
+static bool has_fields(const pb::Message* m) { return m && m->GetDescriptor()->field_count() > 0; }
+
+// ------------------------------------------------------------------ client
+void SerializeH2Request(Buf* buf, Controller* cntl, const pb::Message* request) {
+    const bool grpc = cntl->_protocol_param == "grpc";
+    HttpHeader& h = cntl->http_request();
+    if (cntl->_method && request) {
+        if (!request->IsInitialized()) {
+            cntl->SetFailed(EREQUEST, "Missing required fields in request: %s",
+                            request->InitializationErrorString().c_str());
+            return;
+        }
+        if (grpc || h.content_type().find("proto") != std::string::npos) {
+            Buf pbbuf;
+            if (!request->SerializeToBuf(&pbbuf)) {
+                cntl->SetFailed(EREQUEST, "Fail to serialize request");
+                return;
+            }
+            if (grpc) {
+                AddGrpcPrefix(buf, pbbuf, false);
+                h.set_content_type("application/grpc");
+            } else {
+                buf->append(std::move(pbbuf));
+            }
+        } else {
+            std::string json, err;
+            if (!json2pb::ProtoMessageToJson(*request, &json, json2pb::Pb2JsonOptions(), &err)) {
+                cntl->SetFailed(EREQUEST, "Fail to convert request to json: %s", err.c_str());
+                return;
+            }
+            buf->append(json);
+            if (h.content_type().empty()) h.set_content_type("application/json");
+        }
+        h.set_method(HTTP_METHOD_POST);
+        return;
+    }
+    buf->append(cntl->request_attachment());
+}
+
+void PackH2Request(Buf* packet, uint64_t correlation_id, const pb::MethodDescriptor* method, Controller* cntl,
+                   const Buf& request_buf, const Authenticator* auth) {
+    Socket* s = cntl->_pack_socket;
+    H2Context* ctx = s ? client_context(s) : nullptr;
+    if (!ctx) {
+        cntl->SetFailed(EINTERNAL, "connection is not an h2 connection");
+        return;
+    }
+    HttpHeader& h = cntl->http_request();
+    const bool grpc = cntl->_protocol_param == "grpc";
+    std::string path = h.uri().path();
+    if (method && (path.empty() || path == "/")) path = "/" + method->service->full_name + "/" + method->name;
+    if (path.empty()) path = "/";
+    const std::string q = h.uri().query_string();
+    if (!q.empty()) path += "?" + q;
+    std::vector<HPackHeader> hs;
+    hs.push_back({":method", HttpMethod2Str(h.method())});
+    hs.push_back({":scheme", "http"});
+    hs.push_back({":path", path});
+    std::string authority = h.uri().host();
+    if (authority.empty()) authority = cntl->remote_side().to_string();
+    hs.push_back({":authority", authority});
+    if (!h.content_type().empty()) hs.push_back({"content-type", h.content_type()});
+    if (grpc) {
+        hs.push_back({"te", "trailers"});
+        if (cntl->timeout_ms() > 0) hs.push_back({"grpc-timeout", ConvertUSToGrpcTimeout(cntl->timeout_ms() * 1000)});
+    }
+    if (auth) {
+        std::string cred;
+        if (auth->GenerateCredential(&cred) != 0) {
+            cntl->SetFailed(ERPCAUTH, "Fail to generate credential");
+            return;
+        }
+        hs.push_back({"authorization", cred});
+    }
+    for (auto& kv : h.headers()) {
+        std::string name = kv.first;
+        for (char& c : name) c = (char)tolower(c);
+        if (name == "host" || name == "connection" || name == "transfer-encoding" || name == "content-length") {
+            continue;
+        }
+        hs.push_back({name, kv.second});
+    }
+    hs.push_back({"user-agent", "mrpc/1.0"});
+    Buf body(request_buf);
+    std::string err;
+    if (ctx->StartRequest(s, fiber::CallId{correlation_id}, hs, &body, &err) != 0) {
+        cntl->SetFailed(EFAILEDSOCKET, "%s", err.c_str());
+    }
+    // frames are already written in order under the context lock
+    (void)packet;
+}
+
+void ProcessH2Response(InputMessageBase* msg_base) {
+    std::unique_ptr<HttpMessage> msg(static_cast<HttpMessage*>(msg_base));
+    const fiber::CallId cid = msg->pi.id_wait;
+    if (cid == fiber::INVALID_CALL_ID) return;
+    Controller* cntl = nullptr;
+    if (fiber::call_id_lock(cid, (void**)&cntl) != 0) return;
+    if (cid != cntl->current_id() && cid != cntl->_unfinished_call.id) {
+        fiber::call_id_unlock(cid);
+        return;
+    }
+    cntl->http_response() = msg->header;
+    int saved_error = 0;
+    const int status = msg->header.status_code();
+    const bool grpc = is_grpc_content(msg->header.content_type()) || cntl->_protocol_param == "grpc";
+    const std::string* gs = msg->header.GetHeader("grpc-status");
+    if (grpc && gs && atoi(gs->c_str()) != 0) {
+        const std::string* gm = msg->header.GetHeader("grpc-message");
+        saved_error = GrpcStatusToErrorCode(atoi(gs->c_str()));
+        cntl->SetFailed(saved_error, "[grpc-status %s] %s", gs->c_str(), gm ? PercentDecode(*gm).c_str() : "");
+    } else if (status < 200 || status >= 300) {
+        std::string body = msg->body.to_string();
+        if (body.size() > 512) body.resize(512);
+        saved_error = EHTTP;
+        cntl->SetFailed(EHTTP, "[HTTP %d] %s", status, body.c_str());
+    } else if (grpc) {
+        Buf pbbuf;
+        bool compressed = false;
+        const int r = RemoveGrpcPrefix(&msg->body, &pbbuf, &compressed);
+        if (r != 1 || compressed) {
+            saved_error = ERESPONSE;
+            cntl->SetFailed(ERESPONSE, "bad grpc response framing");
+        } else if (cntl->_response && !ParsePbFromBuf(cntl->_response, pbbuf)) {
+            saved_error = ERESPONSE;
+            cntl->SetFailed(ERESPONSE, "Fail to parse grpc response");
+        }
+    } else if (cntl->_response && has_fields(cntl->_response)) {
+        std::string err;
+        const bool ok = msg->header.content_type().find("proto") != std::string::npos
+                            ? ParsePbFromBuf(cntl->_response, msg->body)
+                            : json2pb::JsonToProtoMessage(msg->body, cntl->_response, json2pb::Json2PbOptions(), &err);
+        if (!ok) {
+            saved_error = ERESPONSE;
+            cntl->SetFailed(ERESPONSE, "Fail to parse h2 response body: %s", err.c_str());
+        }
+    } else {
+        cntl->response_attachment().swap(msg->body);
+    }
+    msg.reset();
+    cntl->OnVersionedRPCReturned(cid, saved_error);
+}
+
+// ------------------------------------------------------------------ server
+struct H2ServerCall {
+    Controller* cntl;
+    pb::Message* req;
+    pb::Message* res;
+    Server* server;
+    MethodStatus* ms;
+    int64_t start_us;
+    uint32_t sid;
+    bool grpc;
+    bool json_proto;  // h2 (non-grpc) with a proto content type
+};
+
+static void SendH2Response(H2ServerCall c) {
+    std::unique_ptr<Controller> cntl_guard(c.cntl);
+    std::unique_ptr<pb::Message> req_guard(c.req);
+    std::unique_ptr<pb::Message> res_guard(c.res);
+    ConcurrencyRemover remover(c.ms, c.cntl, c.start_us);
+    if (c.server) c.server->RemoveConcurrency();
+    SocketUniquePtr sock;
+    if (Socket::Address(c.cntl->_server_socket_id, &sock) != 0) return;
+    ParsingContext* pctx = sock->parsing_context();
+    if (!pctx || pctx->protocol_tag() != H2Context::kTag) return;
+    H2Context* ctx = static_cast<H2Context*>(pctx);
+    Controller* cntl = c.cntl;
+    HttpHeader& rh = cntl->http_response();
+    std::vector<HPackHeader> hs;
+    Buf body;
+    if (c.grpc) {
+        hs.push_back({":status", "200"});
+        hs.push_back({"content-type", "application/grpc"});
+        std::vector<HPackHeader> trailers;
+        if (!cntl->Failed() && c.res) {
+            Buf pbbuf;
+            if (!c.res->IsInitialized() || !c.res->SerializeToBuf(&pbbuf)) {
+                cntl->SetFailed(ERESPONSE, "Fail to serialize response");
+            } else {
+                AddGrpcPrefix(&body, pbbuf, false);
+            }
+        }
+        const int st = cntl->Failed() ? ErrorCodeToGrpcStatus(cntl->ErrorCode()) : 0;
+        trailers.push_back({"grpc-status", std::to_string(st)});
+        if (cntl->Failed()) {
+            body.clear();
+            trailers.push_back({"grpc-message", PercentEncode(cntl->ErrorText())});
+        }
+        ctx->SendResponse(sock.get(), c.sid, hs, &body, &trailers);
+        return;
+    }
+    int status = rh.status_code();
+    if (cntl->Failed()) {
+        status = ErrorCodeToStatusCode(cntl->ErrorCode());
+        rh.set_content_type("text/plain");
+        body.append(cntl->ErrorText() + "\n");
+        rh.SetHeader("x-mrpc-error-code", std::to_string(cntl->ErrorCode()));
+    } else if (has_fields(c.res)) {
+        if (c.json_proto) {
+            c.res->SerializeToBuf(&body);
+            rh.set_content_type("application/proto");
+        } else {
+            std::string json, err;
+            json2pb::ProtoMessageToJson(*c.res, &json, json2pb::Pb2JsonOptions(), &err);
+            body.append(json);
+            rh.set_content_type("application/json");
+        }
+    } else {
+        body.swap(cntl->response_attachment());
+    }
+    hs.push_back({":status", std::to_string(status)});
+    if (!rh.content_type().empty()) hs.push_back({"content-type", rh.content_type()});
+    for (auto& kv : rh.headers()) {
+        std::string name = kv.first;
+        for (char& ch : name) ch = (char)tolower(ch);
+        hs.push_back({name, kv.second});
+    }
+    ctx->SendResponse(sock.get(), c.sid, hs, &body, nullptr);
+}
+
+void ProcessH2Request(InputMessageBase* msg_base) {
+    const int64_t start_us = monotonic_us();
+    std::unique_ptr<HttpMessage> msg(static_cast<HttpMessage*>(msg_base));
+    Socket* socket = msg->socket();
+    Server* server = const_cast<Server*>(static_cast<const Server*>(msg->arg()));
+    Controller* cntl = new Controller;
+    cntl->_server = server;
+    cntl->_server_socket_id = socket->id();
+    cntl->_remote_side = socket->remote_side();
+    cntl->_local_side = socket->local_side();
+    cntl->_received_us = msg->received_us();
+    cntl->_begin_us = msg->received_us();
+    cntl->http_request() = msg->header;
+    HttpHeader& req_h = cntl->http_request();
+    const bool grpc = is_grpc_content(req_h.content_type());
+    H2ServerCall call{cntl, nullptr, nullptr, nullptr, nullptr, start_us, msg->stream_id, grpc,
+                      req_h.content_type().find("proto") != std::string::npos};
+    if (grpc) {
+        if (const std::string* t = req_h.GetHeader("grpc-timeout")) {
+            const int64_t us = ConvertGrpcTimeoutToUS(*t);
+            if (us > 0) cntl->_deadline_us = msg->received_us() + us;
+        }
+    }
+    const Server::MethodProperty* mp = nullptr;
+    bool concurrency_added = false;
+    do {
+        if (!server->IsRunning()) {
+            cntl->SetFailed(ELOGOFF, "Server is stopping");
+            break;
+        }
+        std::string unresolved;
+        std::string path = req_h.uri().path();
+        if (path.empty() || path == "/") path = "/index";
+        mp = server->FindMethodPropertyByURI(path, &unresolved);
+        if (!mp) {
+            cntl->SetFailed(ENOMETHOD, "Fail to find method on `%s'", path.c_str());
+            break;
+        }
+        req_h.set_unresolved_path(unresolved);
+        if (!mp->is_builtin_service) {
+            if (!server->AddConcurrency(cntl)) {
+                cntl->SetFailed(ELIMIT, "Reached server's max_concurrency=%d", server->max_concurrency());
+                break;
+            }
+            concurrency_added = true;
+            int rejected = 0;
+            if (!mp->status->OnRequested(&rejected, cntl)) {
+                mp->status->OnResponded(ELIMIT, 0);
+                cntl->SetFailed(ELIMIT, "Reached method's max_concurrency=%d", rejected - 1);
+                break;
+            }
+            call.ms = mp->status.get();
+        }
+        call.req = mp->service->GetRequestPrototype(mp->method).New();
+        call.res = mp->service->GetResponsePrototype(mp->method).New();
+        if (grpc) {
+            Buf pbbuf;
+            bool compressed = false;
+            const int r = RemoveGrpcPrefix(&msg->body, &pbbuf, &compressed);
+            if (r != 1 || compressed) {
+                cntl->SetFailed(EREQUEST, compressed ? "compressed grpc messages are not supported"
+                                                     : "bad grpc message framing");
+                break;
+            }
+            if (!ParsePbFromBuf(call.req, pbbuf)) {
+                cntl->SetFailed(EREQUEST, "Fail to parse grpc request as %s",
+                                call.req->GetDescriptor()->full_name.c_str());
+                break;
+            }
+        } else if (has_fields(call.req)) {
+            std::string err;
+            const bool ok = call.json_proto ? ParsePbFromBuf(call.req, msg->body)
+                            : msg->body.empty()
+                                ? call.req->IsInitialized()
+                                : json2pb::JsonToProtoMessage(msg->body, call.req, json2pb::Json2PbOptions(), &err);
+            if (!ok) {
+                cntl->SetFailed(EREQUEST, "Fail to parse h2 request body %s", err.c_str());
+                break;
+            }
+        } else {
+            cntl->request_attachment().swap(msg->body);
+        }
+    } while (false);
+    msg.reset();
+    if (concurrency_added) call.server = server;
+    if (cntl->Failed()) {
+        SendH2Response(call);
+        return;
+    }
+    Closure* done = NewCallback([call] { SendH2Response(call); });
+    mp->service->CallMethod(mp->method, cntl, call.req, call.res, done);
+}
+
+static const std::string& GetH2MethodName(const pb::MethodDescriptor* method, const Controller*) {
+    static const std::string kCommon = "common_h2_request";
+    return method ? method->full_name : kCommon;
+}
+
+void RegisterH2Protocol() {
+    Protocol p;
+    p.parse = ParseH2Message;
+    p.serialize_request = SerializeH2Request;
+    p.pack_request = PackH2Request;
+    p.process_request = ProcessH2Request;
+    p.process_response = ProcessH2Response;
+    p.get_method_name = GetH2MethodName;
+    p.supported_connection_type = CONNECTION_TYPE_SINGLE;
+    p.name = "h2";
+    RegisterProtocol(PROTOCOL_H2, p);
+}
+
+}  // namespace policy
+}  // namespace mrpc

@@ -184,6 +184,7 @@ void Channel::CallMethod(const pb::MethodDescriptor* method, RpcController* cont
     cntl->_done = done;
     cntl->_protocol = _protocol;
     cntl->_protocol_type = _protocol_type;
+    if (!_protocol_param.empty()) cntl->_protocol_param = _protocol_param;
     cntl->_auth = _options.auth;
     if (cntl->_connection_type == CONNECTION_TYPE_SINGLE) cntl->_connection_type = _connection_type;
     if (!cntl->_retry_policy) cntl->_retry_policy = _options.retry_policy;

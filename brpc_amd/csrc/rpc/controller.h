@@ -222,6 +222,7 @@ public:
     // set by pack_request of in-order protocols (http/1.1, redis, memcache)
     int _pipelined_count = 0;
     uint32_t _pipelined_tag = 0;
+    std::string _protocol_param;  // "grpc" for channels of protocol "h2:grpc"
     HttpHeader* _http_request = nullptr;
     HttpHeader* _http_response = nullptr;
     std::map<std::string, std::string> _session_kv;

@@ -60,6 +60,7 @@ void GlobalInitializeOrDie() {
         policy::RegisterBaiduStdProtocol();
         RegisterStreamingProtocol();
         policy::RegisterHttpProtocol();
+        policy::RegisterH2Protocol();
         for (ProtocolRegistrar r : extra_registrars()) r();
         // Client-side messenger handles responses of every protocol.
         std::vector<std::pair<ProtocolType, Protocol>> protocols;

@@ -10,6 +10,7 @@
 #include "base/time.h"
 #include "fiber/fiber.h"
 #include "http/http_header.h"
+#include "http/hpack.h"
 #include "http/http_message.h"
 #include "json/json2pb.h"
 #include "mrpc/proto/echo.pb.h"
@@ -314,4 +315,95 @@ TEST(Http, progressive_attachment_and_reader) {
         EXPECT_TRUE(r.st.ok());
         EXPECT_EQ(r.data, "part0;part1;part2;part3;part4;");
     }
+}
+
+TEST(Hpack, roundtrip_and_huffman) {
+    HPackEncoder enc;
+    HPackDecoder dec;
+    std::vector<HPackHeader> hs = {{":method", "POST"},
+                                   {":path", "/example.EchoService/Echo"},
+                                   {"content-type", "application/grpc"},
+                                   {"custom-key", "custom-value"},
+                                   {"authorization", "secret"},
+                                   {"x-bin", std::string("\x00\xff\x80 z", 5)}};
+    for (int round = 0; round < 3; ++round) {  // later rounds hit the dynamic table
+        Buf block;
+        for (auto& h : hs) enc.Encode(&block, h, h.name == "authorization" ? HPackIndexPolicy::NEVER_INDEXED
+                                                                              : HPackIndexPolicy::INCREMENTAL);
+        std::vector<HPackHeader> out;
+        ASSERT_TRUE(dec.Decode(block.to_string(), &out));
+        ASSERT_EQ(out.size(), hs.size());
+        for (size_t i = 0; i < hs.size(); ++i) {
+            EXPECT_EQ(out[i].name, hs[i].name);
+            EXPECT_EQ(out[i].value, hs[i].value);
+        }
+    }
+    std::string h;
+    hpack::HuffmanEncode(&h, "www.example.com");
+    std::string hex;
+    for (unsigned char c : h) {
+        char b[3];
+        snprintf(b, 3, "%02x", c);
+        hex += b;
+    }
+    EXPECT_EQ(hex, "f1e3c2e5f23a6ba0ab90f4ff");  // RFC 7541 C.4.1
+    std::string back;
+    ASSERT_TRUE(hpack::HuffmanDecode((const uint8_t*)h.data(), h.size(), &back));
+    EXPECT_EQ(back, "www.example.com");
+    for (int c = 0; c < 256; ++c) {
+        std::string s(3, (char)c), e, d;
+        hpack::HuffmanEncode(&e, s);
+        ASSERT_TRUE(hpack::HuffmanDecode((const uint8_t*)e.data(), e.size(), &d));
+        ASSERT_EQ(d, s);
+    }
+}
+
+TEST(H2, json_and_grpc) {
+    HttpServer s;
+    ASSERT_GT(s.port, 0);
+    for (const char* proto : {"h2", "h2:grpc"}) {
+        Channel ch;
+        ChannelOptions opt;
+        opt.protocol = proto;
+        opt.timeout_ms = 3000;
+        ASSERT_EQ(ch.Init(s.addr().c_str(), &opt), 0);
+        example::EchoService_Stub stub(&ch);
+        // concurrent calls multiplexed on one connection
+        std::vector<std::thread> ths;
+        std::atomic<int> ok{0};
+        for (int t = 0; t < 4; ++t) {
+            ths.emplace_back([&, t] {
+                for (int i = 0; i < 50; ++i) {
+                    Controller cntl;
+                    example::EchoRequest req;
+                    example::EchoResponse res;
+                    req.set_message(std::string(proto) + " " + std::to_string(t * 1000 + i) +
+                                    std::string(i == 7 ? 100000 : 0, 'z'));
+                    stub.Echo(&cntl, &req, &res, nullptr);
+                    if (!cntl.Failed() && res.message() == req.message()) ok.fetch_add(1);
+                    else fprintf(stderr, "%s failed: %s\n", proto, cntl.ErrorText().c_str());
+                }
+            });
+        }
+        for (auto& th : ths) th.join();
+        EXPECT_EQ(ok.load(), 200);
+        // server error maps through grpc-status / http status
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("x");
+        req.set_server_fail(true);
+        stub.Echo(&cntl, &req, &res, nullptr);
+        EXPECT_TRUE(cntl.Failed());
+    }
+    // plain h2 GET of a builtin page
+    Channel ch;
+    ChannelOptions opt;
+    opt.protocol = "h2";
+    ASSERT_EQ(ch.Init(s.addr().c_str(), &opt), 0);
+    Controller cntl;
+    cntl.http_request().uri().set_path("/health");
+    ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
+    ASSERT_FALSE(cntl.Failed());
+    EXPECT_EQ(cntl.response_attachment().to_string(), "OK\n");
 }
