@@ -140,7 +140,8 @@ private:
     int on_settings(Socket* s, uint8_t flags, Buf& payload);
     void write_locked(Socket* s, Buf* frames, fiber::CallId id_wait = fiber::INVALID_CALL_ID);
     void encode_headers_locked(Buf* out, uint32_t sid, const std::vector<HPackHeader>& h, bool end_stream);
-    void flush_stream_locked(Buf* out, Stream* st);
+    bool flush_stream_locked(Buf* out, Stream* st);
+    void flush_all_locked(Buf* out);
     void send_local_settings_locked(Buf* out);
     void maybe_window_update_locked(Buf* out, Stream* st);
     Stream* find(uint32_t sid) {
@@ -231,13 +232,15 @@ void H2Context::encode_headers_locked(Buf* out, uint32_t sid, const std::vector<
     } while (!block.empty());
 }
 
-// Moves as much pending data as the windows allow into `out`.
-void H2Context::flush_stream_locked(Buf* out, Stream* st) {
+// Moves as much pending data as the windows allow into `out`. Returns true
+// when a server stream has sent its last frame (the caller erases it; never
+// erase here, callers may be iterating the stream map).
+bool H2Context::flush_stream_locked(Buf* out, Stream* st) {
     while (!st->pending.empty()) {
         const int64_t allow =
             std::min<int64_t>({(int64_t)st->pending.size(), st->send_window, _conn_send_window,
                                (int64_t)_remote.max_frame_size});
-        if (allow <= 0) return;
+        if (allow <= 0) return false;
         Buf piece;
         st->pending.cutn(&piece, (size_t)allow);
         st->send_window -= allow;
@@ -246,20 +249,26 @@ void H2Context::flush_stream_locked(Buf* out, Stream* st) {
         frame_header(out, (uint32_t)piece.size(), H2_DATA, end ? F_END_STREAM : 0, st->id);
         out->append(std::move(piece));
     }
-    if (st->pending.empty()) {
-        if (st->has_pending_trailers) {
-            encode_headers_locked(out, st->id, st->pending_trailers, true);
-            st->has_pending_trailers = false;
-            st->pending_trailers.clear();
-            st->pending_end = false;
-            if (_server) erase(st->id);  // response complete
-            return;
-        }
-        if (st->pending_end) {
-            st->pending_end = false;
-            if (_server) erase(st->id);
-        }
+    if (st->has_pending_trailers) {
+        encode_headers_locked(out, st->id, st->pending_trailers, true);
+        st->has_pending_trailers = false;
+        st->pending_trailers.clear();
+        st->pending_end = false;
+        return _server;  // response complete
     }
+    if (st->pending_end) {
+        st->pending_end = false;
+        return _server;
+    }
+    return false;
+}
+
+void H2Context::flush_all_locked(Buf* out) {
+    std::vector<uint32_t> finished;
+    for (auto& kv : _streams) {
+        if (flush_stream_locked(out, kv.second)) finished.push_back(kv.first);
+    }
+    for (uint32_t sid : finished) erase(sid);
 }
 
 int H2Context::StartRequest(Socket* s, fiber::CallId cid, const std::vector<HPackHeader>& headers, Buf* body,
@@ -307,7 +316,7 @@ int H2Context::SendResponse(Socket* s, uint32_t sid, const std::vector<HPackHead
             st->pending_trailers = *trailers;
             st->has_pending_trailers = true;
         }
-        flush_stream_locked(&out, st);
+        if (flush_stream_locked(&out, st)) erase(sid);
     } else {
         erase(sid);
     }
@@ -391,7 +400,7 @@ int H2Context::on_settings(Socket* s, uint8_t flags, Buf& payload) {
     Buf out;
     send_local_settings_locked(&out);
     frame_header(&out, 0, H2_SETTINGS, F_ACK, 0);
-    for (auto& kv : _streams) flush_stream_locked(&out, kv.second);
+    flush_all_locked(&out);
     write_locked(s, &out);
     return 0;
 }
@@ -432,7 +441,10 @@ int H2Context::on_headers_complete(Socket* s, Stream* st, bool end_stream, HttpM
         *done = st->msg;
         st->msg = nullptr;
         (*done)->pi.id_wait = st->cid;
-        if (!_server) erase(st->id);
+        if (!_server) {
+            std::lock_guard<std::mutex> g(_mu);  // writers insert concurrently
+            erase(st->id);
+        }
     }
     return 0;
 }
@@ -465,10 +477,10 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
         Buf out;
         if (sid == 0) {
             _conn_send_window += inc;
-            for (auto& kv : _streams) flush_stream_locked(&out, kv.second);
+            flush_all_locked(&out);
         } else if (Stream* st = find(sid)) {
             st->send_window += inc;
-            flush_stream_locked(&out, st);
+            if (flush_stream_locked(&out, st)) erase(sid);
         }
         write_locked(s, &out);
         return 0;

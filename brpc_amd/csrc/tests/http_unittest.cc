@@ -381,7 +381,8 @@ TEST(H2, json_and_grpc) {
                                     std::string(i == 7 ? 100000 : 0, 'z'));
                     stub.Echo(&cntl, &req, &res, nullptr);
                     if (!cntl.Failed() && res.message() == req.message()) ok.fetch_add(1);
-                    else fprintf(stderr, "%s failed: %s\n", proto, cntl.ErrorText().c_str());
+                    else fprintf(stderr, "%s failed (i=%d, %zu bytes): %s\n", proto, i, req.message().size(),
+                                 cntl.ErrorText().c_str());
                 }
             });
         }
