@@ -285,15 +285,6 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
     }
     _amc = _options.max_concurrency;
     _cl.reset(CreateConcurrencyLimiter(_amc));
-    // expose method statuses
-    {
-        std::lock_guard<std::mutex> g(_mu);
-        for (auto& kv : _methods) {
-            if (kv.second.is_builtin_service) continue;
-            std::string name = "rpc_server_" + std::to_string(ep.port) + "_" + kv.first;
-            kv.second.status->Expose(name);
-        }
-    }
     if (_options.session_local_data_factory && !_keytable_pool) _keytable_pool = fiber::keytable_pool_create();
     if (_options.thread_local_data_factory && !_tls_key_created) {
         const DataFactory* f = _options.thread_local_data_factory;
@@ -336,6 +327,15 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
         g_server_count_var = new var::PassiveStatus<int>("rpc_server_count", [] { return g_running_servers.load(); });
     }
     var::start_dump_thread_if_needed();
+    // expose method statuses under the real listening port
+    {
+        std::lock_guard<std::mutex> g(_mu);
+        for (auto& kv : _methods) {
+            if (kv.second.is_builtin_service) continue;
+            std::string name = "rpc_server_" + std::to_string(_listen_addr.port) + "_" + kv.first;
+            kv.second.status->Expose(name);
+        }
+    }
     LOG(INFO) << "Server is serving on " << _listen_addr;
     return 0;
 }

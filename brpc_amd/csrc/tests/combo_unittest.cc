@@ -1,0 +1,280 @@
+// Combo channels: ParallelChannel, PartitionChannel, DynamicPartitionChannel,
+// SelectiveChannel (spirit of the reference's
+// test/brpc_channel_unittest.cpp parallel/selective/partition cases).
+#include <unistd.h>
+
+#include <set>
+#include <thread>
+
+#include "base/time.h"
+#include "fiber/fiber.h"
+#include "mrpc/proto/echo.pb.h"
+#include "rpc/channel.h"
+#include "rpc/combo_channels.h"
+#include "rpc/controller.h"
+#include "rpc/errno.h"
+#include "rpc/server.h"
+#include "tests/test.h"
+
+using namespace mrpc;
+
+namespace {
+
+class TaggedEcho : public example::EchoService {
+public:
+    explicit TaggedEcho(std::string tag) : _tag(std::move(tag)) {}
+    void Echo(RpcController* c, const example::EchoRequest* req, example::EchoResponse* res, Closure* done) override {
+        ClosureGuard g(done);
+        if (req->sleep_us() > 0) fiber::usleep(req->sleep_us());
+        if (delay_us > 0) fiber::usleep(delay_us);
+        if (req->server_fail()) {
+            static_cast<Controller*>(c)->SetFailed(EINTERNAL, "asked to fail by %s", _tag.c_str());
+            return;
+        }
+        res->set_message(req->message() + "@" + _tag);
+    }
+
+    int64_t delay_us = 0;
+
+private:
+    std::string _tag;
+};
+
+struct TaggedServer {
+    Server server;
+    TaggedEcho echo;
+    int port = 0;
+    explicit TaggedServer(const std::string& tag) : echo(tag) {
+        server.AddService(&echo, SERVER_DOESNT_OWN_SERVICE);
+        ServerOptions o;
+        o.has_builtin_services = false;
+        if (server.Start("127.0.0.1:0", &o) == 0) port = server.listen_port();
+    }
+    std::string addr() const { return "127.0.0.1:" + std::to_string(port); }
+};
+
+Channel* make_channel(const std::string& addr, int timeout_ms = 2000) {
+    Channel* ch = new Channel;
+    ChannelOptions o;
+    o.timeout_ms = timeout_ms;
+    o.max_retry = 0;
+    if (ch->Init(addr.c_str(), &o) != 0) {
+        delete ch;
+        return nullptr;
+    }
+    return ch;
+}
+
+class ConcatMerger : public ResponseMerger {
+public:
+    Result Merge(pb::Message* response, const pb::Message* sub) override {
+        auto* r = static_cast<example::EchoResponse*>(response);
+        auto* s = static_cast<const example::EchoResponse*>(sub);
+        r->set_message(r->message().empty() ? s->message() : r->message() + "|" + s->message());
+        return MERGED;
+    }
+};
+
+class SplitMapper : public CallMapper {
+public:
+    SubCall Map(int i, int n, const pb::MethodDescriptor* m, const pb::Message* req, pb::Message* res) override {
+        auto* r = new example::EchoRequest(*static_cast<const example::EchoRequest*>(req));
+        r->set_message(r->message() + "#" + std::to_string(i) + "/" + std::to_string(n));
+        return SubCall(m, r, res->New(), SubCall::DELETE_REQUEST | SubCall::DELETE_RESPONSE);
+    }
+};
+
+std::set<std::string> split(const std::string& s) {
+    std::set<std::string> out;
+    size_t b = 0;
+    while (true) {
+        size_t e = s.find('|', b);
+        out.insert(s.substr(b, e == std::string::npos ? std::string::npos : e - b));
+        if (e == std::string::npos) break;
+        b = e + 1;
+    }
+    return out;
+}
+
+}  // namespace
+
+TEST(ParallelChannel, broadcast_merge_map_and_limits) {
+    TaggedServer a("a"), b("b"), c("c");
+    ParallelChannel pc;
+    ParallelChannelOptions po;
+    po.timeout_ms = 2000;
+    pc.Init(&po);
+    auto merger = std::make_shared<ConcatMerger>();
+    auto mapper = std::make_shared<SplitMapper>();
+    for (TaggedServer* s : {&a, &b, &c}) pc.AddChannel(make_channel(s->addr()), OWNS_CHANNEL, mapper, merger);
+    example::EchoService_Stub stub(&pc);
+    for (int i = 0; i < 20; ++i) {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("m");
+        stub.Echo(&cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_TRUE(split(res.message()) == (std::set<std::string>{"m#0/3@a", "m#1/3@b", "m#2/3@c"}));
+    }
+    // async
+    {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("x");
+        std::atomic<int> fired{0};
+        stub.Echo(&cntl, &req, &res, NewCallback([&] { fired.store(1); }));
+        cntl.Join();
+        EXPECT_EQ(fired.load(), 1);
+        EXPECT_FALSE(cntl.Failed());
+        EXPECT_EQ(split(res.message()).size(), 3u);
+    }
+    // one dead sub channel: default fail_limit tolerates it, fail_limit=1 does not
+    ParallelChannel pc2;
+    pc2.Init(&po);
+    pc2.AddChannel(make_channel(a.addr()), OWNS_CHANNEL, nullptr, merger);
+    pc2.AddChannel(make_channel("127.0.0.1:1", 300), OWNS_CHANNEL, nullptr, merger);
+    example::EchoService_Stub stub2(&pc2);
+    {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("y");
+        stub2.Echo(&cntl, &req, &res, nullptr);
+        EXPECT_FALSE(cntl.Failed());
+        EXPECT_EQ(res.message(), "y@a");
+    }
+    ParallelChannelOptions strict = po;
+    strict.fail_limit = 1;
+    ParallelChannel pc3;
+    pc3.Init(&strict);
+    pc3.AddChannel(make_channel(a.addr()), OWNS_CHANNEL, nullptr, merger);
+    pc3.AddChannel(make_channel("127.0.0.1:1", 300), OWNS_CHANNEL, nullptr, merger);
+    example::EchoService_Stub stub3(&pc3);
+    {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("z");
+        stub3.Echo(&cntl, &req, &res, nullptr);
+        EXPECT_TRUE(cntl.Failed());
+    }
+    // success_limit=1 returns on the first answer
+    ParallelChannelOptions first = po;
+    first.success_limit = 1;
+    ParallelChannel pc4;
+    pc4.Init(&first);
+    pc4.AddChannel(make_channel(a.addr()), OWNS_CHANNEL, nullptr, merger);
+    pc4.AddChannel(make_channel(b.addr()), OWNS_CHANNEL, nullptr, merger);
+    example::EchoService_Stub stub4(&pc4);
+    {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("f");
+        stub4.Echo(&cntl, &req, &res, nullptr);
+        EXPECT_FALSE(cntl.Failed());
+        EXPECT_EQ(split(res.message()).size(), 1u);
+    }
+}
+
+TEST(PartitionChannel, static_and_dynamic) {
+    TaggedServer p0("p0"), p1("p1"), p2("p2"), q0("q0"), q1("q1");
+    auto merger = std::make_shared<ConcatMerger>();
+    PartitionParser parser;
+    PartitionChannelOptions opt;
+    opt.timeout_ms = 2000;
+    opt.response_merger = merger;
+    const std::string url = "list://" + p0.addr() + " 0/3," + p1.addr() + " 1/3," + p2.addr() + " 2/3," +
+                            q0.addr() + " 0/2," + q1.addr() + " 1/2";
+    PartitionChannel pch;
+    ASSERT_EQ(pch.Init(3, &parser, url.c_str(), "rr", &opt), 0);
+    EXPECT_EQ(pch.partition_count(), 3);
+    example::EchoService_Stub stub(&pch);
+    {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("k");
+        stub.Echo(&cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_TRUE(split(res.message()) == (std::set<std::string>{"k@p0", "k@p1", "k@p2"}));
+    }
+    DynamicPartitionChannel dch;
+    ASSERT_EQ(dch.Init(&parser, url.c_str(), "rr", &opt), 0);
+    EXPECT_EQ(dch.scheme_count(), 2);
+    example::EchoService_Stub dstub(&dch);
+    int saw3 = 0, saw2 = 0;
+    for (int i = 0; i < 60; ++i) {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("d");
+        dstub.Echo(&cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        const size_t parts = split(res.message()).size();
+        saw3 += parts == 3;
+        saw2 += parts == 2;
+    }
+    EXPECT_GT(saw3, 0);
+    EXPECT_GT(saw2, 0);
+}
+
+TEST(SelectiveChannel, failover_balance_backup) {
+    TaggedServer a("a"), b("b");
+    SelectiveChannel sc;
+    SelectiveChannelOptions so;
+    so.timeout_ms = 2000;
+    so.max_retry = 2;
+    sc.Init(&so);
+    sc.AddChannel(make_channel(a.addr()));
+    sc.AddChannel(make_channel("127.0.0.1:1", 300));
+    sc.AddChannel(make_channel(b.addr()));
+    example::EchoService_Stub stub(&sc);
+    std::set<std::string> seen;
+    for (int i = 0; i < 30; ++i) {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("s");
+        stub.Echo(&cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        seen.insert(res.message());
+    }
+    EXPECT_TRUE(seen == (std::set<std::string>{"s@a", "s@b"}));
+    // application errors are not retried
+    {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("e");
+        req.set_server_fail(true);
+        stub.Echo(&cntl, &req, &res, nullptr);
+        EXPECT_TRUE(cntl.Failed());
+    }
+    // backup request: a slow first choice is overtaken by the backup
+    TaggedServer slow("slow"), fast("fast");
+    SelectiveChannel bc;
+    SelectiveChannelOptions bo;
+    bo.timeout_ms = 3000;
+    bo.backup_request_ms = 20;
+    bc.Init(&bo);
+    bc.AddChannel(make_channel(slow.addr(), 3000));
+    bc.AddChannel(make_channel(fast.addr(), 3000));
+    example::EchoService_Stub bstub(&bc);
+    slow.echo.delay_us = 300000;
+    int fast_wins = 0;
+    for (int i = 0; i < 4; ++i) {
+        Controller c2;
+        example::EchoResponse r2;
+        example::EchoRequest q2;
+        q2.set_message("b");
+        const int64_t t0 = monotonic_us();
+        bstub.Echo(&c2, &q2, &r2, nullptr);
+        ASSERT_FALSE(c2.Failed());
+        EXPECT_LT(monotonic_us() - t0, 250000);  // never waits for the slow replica
+        fast_wins += r2.message() == "b@fast";
+    }
+    EXPECT_EQ(fast_wins, 4);
+}
