@@ -221,18 +221,30 @@ __device__ __forceinline__ i8x16 expand16(uint32_t bits) {
     return r.v;
 }
 
+// Rare path (leading partial group / unaligned segment end), kept out of
+// line so it does not inflate the hot loop's register allocation.
+__device__ __noinline__ void fetch_bytes_slow(const uint8_t* base, int64_t lbeg, uint32_t* w) {
+    for (int i = 0; i < 8; ++i) w[i] = 0;
+    for (int b = 0; b < 32; ++b) {
+        const int64_t off = lbeg + b;
+        if (off >= 0) w[b >> 2] |= (uint32_t)base[off] << (8 * (b & 3));
+    }
+}
+
 __global__ void __launch_bounds__(kThreads) crc32c_mfma_kernel(
     const uint64_t* __restrict__ starts, const uint64_t* __restrict__ lens, const uint64_t* __restrict__ chunk_start,
     int64_t nseg, const CrcMfmaConsts* __restrict__ K, const uint32_t* __restrict__ xc, uint32_t* __restrict__ out) {
+    // A fragments (16 KiB) and the Horner tables (4 KiB) live in LDS: the
+    // fragments would otherwise pin 64 VGPRs per lane and cap occupancy at
+    // 3 waves/SIMD; ds_read_b128 of consecutive lanes is conflict-free.
+    __shared__ i8x16 sa[16][64];
     __shared__ uint32_t t2k[4][256];
+    for (int i = threadIdx.x; i < 16 * 64; i += kThreads) (&sa[0][0])[i] = (&K->afrag[0][0])[i];
     for (int i = threadIdx.x; i < 1024; i += kThreads) (&t2k[0][0])[i] = (&K->t2k[0][0])[i];
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int c = lane & 31;
     const int h = lane >> 5;
-    i8x16 a[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) a[j] = K->afrag[j][lane];
     const uint32_t lshift = K->lane_shift[c];
     const uint64_t total = chunk_start[nseg];
     const uint64_t nwaves = (uint64_t)gridDim.x * (kThreads / 64);
@@ -252,33 +264,41 @@ __global__ void __launch_bounds__(kThreads) crc32c_mfma_kernel(
         const uint64_t after = nch - 1 - k;
         const int64_t chunk_end = (int64_t)len - (int64_t)(after * kMfmaChunk);
         const bool aligned = ((reinterpret_cast<uintptr_t>(base) + len) & 15) == 0;
-        uint32_t acc = 0;
-        for (int g = 0; g < kGroupsPerChunk; ++g) {
-            const int64_t gend = chunk_end - (int64_t)(kGroupsPerChunk - 1 - g) * kGroupBytes;
-            if (gend <= 0) continue;  // wave-uniform: whole group precedes the segment
+        // lane's 32 bytes of group gg; bytes before the segment read as zero
+        // (a zero prefix leaves the CRC register unchanged)
+        auto fetch = [&](int gg, uint32_t* w) {
+            const int64_t gend = chunk_end - (int64_t)(kGroupsPerChunk - 1 - gg) * kGroupBytes;
             const int64_t lbeg = gend - kGroupBytes + 64 * c + 32 * h;
-            uint32_t w[8];
             if (lbeg >= 0 && aligned) {
                 const uint4* p = reinterpret_cast<const uint4*>(base + lbeg);
                 const uint4 v0 = p[0], v1 = p[1];
                 w[0] = v0.x; w[1] = v0.y; w[2] = v0.z; w[3] = v0.w;
                 w[4] = v1.x; w[5] = v1.y; w[6] = v1.z; w[7] = v1.w;
             } else {
-                // leading partial group or unaligned end: bytes before the
-                // segment read as zero (a zero prefix leaves the CRC unchanged)
-#pragma unroll
-                for (int i = 0; i < 8; ++i) w[i] = 0;
-                for (int b = 0; b < 32; ++b) {
-                    const int64_t off = lbeg + b;
-                    if (off >= 0) w[b >> 2] |= (uint32_t)base[off] << (8 * (b & 3));
-                }
+                fetch_bytes_slow(base, lbeg, w);
             }
+        };
+        // first group that overlaps the segment (wave-uniform)
+        int g0 = 0;
+        while (g0 < kGroupsPerChunk && chunk_end - (int64_t)(kGroupsPerChunk - 1 - g0) * kGroupBytes <= 0) ++g0;
+        uint32_t acc = 0;
+        uint32_t cur[8], nxt[8];
+        if (g0 < kGroupsPerChunk) fetch(g0, cur);
+        for (int g = g0; g < kGroupsPerChunk; ++g) {
+            // issue the next group's loads before this group's MFMA work so a
+            // wave keeps 4 KiB in flight (Little's law at ~2 us HBM latency)
+            if (g + 1 < kGroupsPerChunk) fetch(g + 1, nxt);
             i32x16 d = {0};
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const uint32_t bits = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-                d = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[j], expand16(bits), d, 0, 0, 0);
+                const uint32_t bits = (cur[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                d = __builtin_amdgcn_mfma_i32_32x32x32_i8(sa[j][lane], expand16(bits), d, 0, 0, 0);
+                // keep fragment reads / bit expansion within a window of 4
+                // MFMAs instead of letting the scheduler hoist all 16 (VGPRs)
+                if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
             }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
             // D layout: col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
             uint32_t part = 0;
 #pragma unroll
