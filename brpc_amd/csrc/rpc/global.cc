@@ -61,6 +61,7 @@ void GlobalInitializeOrDie() {
         RegisterStreamingProtocol();
         policy::RegisterHttpProtocol();
         policy::RegisterH2Protocol();
+        policy::RegisterRedisProtocol();
         for (ProtocolRegistrar r : extra_registrars()) r();
         // Client-side messenger handles responses of every protocol.
         std::vector<std::pair<ProtocolType, Protocol>> protocols;
