@@ -62,6 +62,7 @@ void GlobalInitializeOrDie() {
         policy::RegisterHttpProtocol();
         policy::RegisterH2Protocol();
         policy::RegisterRedisProtocol();
+        policy::RegisterMemcacheProtocol();
         for (ProtocolRegistrar r : extra_registrars()) r();
         // Client-side messenger handles responses of every protocol.
         std::vector<std::pair<ProtocolType, Protocol>> protocols;

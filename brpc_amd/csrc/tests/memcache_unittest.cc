@@ -1,0 +1,167 @@
+// Memcache binary client against an in-process fake memcached (blocking
+// sockets on a plain thread) — spirit of test/brpc_memcache_unittest.cpp,
+// which needs a real memcached.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <map>
+#include <thread>
+
+#include "redis/memcache.h"
+#include "rpc/channel.h"
+#include "rpc/controller.h"
+#include "tests/test.h"
+
+using namespace mrpc;
+
+namespace {
+
+struct FakeMemcached {
+    int lfd = -1;
+    int port = 0;
+    std::thread th;
+    std::atomic<bool> stop{false};
+    std::map<std::string, std::pair<std::string, uint32_t>> kv;
+    uint64_t cas = 1;
+
+    FakeMemcached() {
+        lfd = socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        bind(lfd, (sockaddr*)&a, sizeof(a));
+        socklen_t l = sizeof(a);
+        getsockname(lfd, (sockaddr*)&a, &l);
+        port = ntohs(a.sin_port);
+        listen(lfd, 4);
+        th = std::thread([this] { serve(); });
+    }
+    ~FakeMemcached() {
+        stop = true;
+        shutdown(lfd, SHUT_RDWR);
+        close(lfd);
+        th.join();
+    }
+    static bool readn(int fd, void* p, size_t n) {
+        char* c = (char*)p;
+        while (n) {
+            ssize_t r = read(fd, c, n);
+            if (r <= 0) return false;
+            c += r;
+            n -= r;
+        }
+        return true;
+    }
+    static uint64_t be(const unsigned char* p, int n) {
+        uint64_t v = 0;
+        for (int i = 0; i < n; ++i) v = (v << 8) | p[i];
+        return v;
+    }
+    static void put(std::string* s, uint64_t v, int n) {
+        for (int i = n - 1; i >= 0; --i) s->push_back((char)(v >> (8 * i)));
+    }
+    void reply(int fd, uint8_t op, uint16_t status, const std::string& ext, const std::string& value, uint64_t c) {
+        std::string s;
+        s.push_back((char)0x81);
+        s.push_back((char)op);
+        put(&s, 0, 2);
+        s.push_back((char)ext.size());
+        s.push_back(0);
+        put(&s, status, 2);
+        put(&s, ext.size() + value.size(), 4);
+        put(&s, 0, 4);
+        put(&s, c, 8);
+        s += ext + value;
+        (void)!write(fd, s.data(), s.size());
+    }
+    void serve() {
+        while (!stop) {
+            int fd = accept(lfd, nullptr, nullptr);
+            if (fd < 0) return;
+            unsigned char h[24];
+            while (readn(fd, h, 24)) {
+                const uint8_t op = h[1];
+                const uint16_t keylen = (uint16_t)be(h + 2, 2);
+                const uint8_t extlen = h[4];
+                const uint32_t body = (uint32_t)be(h + 8, 4);
+                std::string b(body, '\0');
+                if (body && !readn(fd, &b[0], body)) break;
+                const std::string ext = b.substr(0, extlen), key = b.substr(extlen, keylen),
+                                  val = b.substr(extlen + keylen);
+                if (op == 0x01) {  // set
+                    kv[key] = {val, (uint32_t)be((const unsigned char*)ext.data(), 4)};
+                    reply(fd, op, 0, "", "", ++cas);
+                } else if (op == 0x00) {  // get
+                    auto it = kv.find(key);
+                    if (it == kv.end()) {
+                        reply(fd, op, 1, "", "Not found", 0);
+                    } else {
+                        std::string fl;
+                        put(&fl, it->second.second, 4);
+                        reply(fd, op, 0, fl, it->second.first, cas);
+                    }
+                } else if (op == 0x05) {  // incr
+                    const uint64_t delta = be((const unsigned char*)ext.data(), 8);
+                    const uint64_t init = be((const unsigned char*)ext.data() + 8, 8);
+                    auto it = kv.find(key);
+                    uint64_t v = it == kv.end() ? init : strtoull(it->second.first.c_str(), nullptr, 10) + delta;
+                    kv[key] = {std::to_string(v), 0};
+                    std::string out;
+                    put(&out, v, 8);
+                    reply(fd, op, 0, "", out, ++cas);
+                } else if (op == 0x04) {  // delete
+                    reply(fd, op, kv.erase(key) ? 0 : 1, "", "", 0);
+                } else if (op == 0x0b) {
+                    reply(fd, op, 0, "", "1.6.fake", 0);
+                } else {
+                    reply(fd, op, 0x81, "", "Unknown command", 0);
+                }
+            }
+            close(fd);
+        }
+    }
+};
+
+}  // namespace
+
+TEST(Memcache, pipelined_ops) {
+    FakeMemcached mc;
+    Channel ch;
+    ChannelOptions co;
+    co.protocol = "memcache";
+    co.timeout_ms = 3000;
+    ASSERT_EQ(ch.Init(("127.0.0.1:" + std::to_string(mc.port)).c_str(), &co), 0);
+    MemcacheRequest req;
+    req.Set("hello", "world", 0xdead, 0, 0);
+    req.Get("hello");
+    req.Get("nope");
+    req.Increment("ctr", 5, 100, 0);
+    req.Increment("ctr", 5, 100, 0);
+    req.Delete("hello");
+    req.Version();
+    MemcacheResponse res;
+    Controller cntl;
+    ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+    ASSERT_FALSE(cntl.Failed());
+    uint64_t cas = 0;
+    EXPECT_TRUE(res.PopSet(&cas));
+    EXPECT_GT(cas, 0u);
+    std::string v;
+    uint32_t flags = 0;
+    EXPECT_TRUE(res.PopGet(&v, &flags, nullptr));
+    EXPECT_EQ(v, "world");
+    EXPECT_EQ(flags, 0xdeadu);
+    EXPECT_FALSE(res.PopGet(&v, nullptr, nullptr));
+    uint64_t n = 0;
+    EXPECT_TRUE(res.PopIncrement(&n, nullptr));
+    EXPECT_EQ(n, 100u);
+    EXPECT_TRUE(res.PopIncrement(&n, nullptr));
+    EXPECT_EQ(n, 105u);
+    EXPECT_TRUE(res.PopDelete());
+    std::string ver;
+    EXPECT_TRUE(res.PopVersion(&ver));
+    EXPECT_EQ(ver, "1.6.fake");
+}
