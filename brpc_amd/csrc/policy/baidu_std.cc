@@ -11,6 +11,7 @@
 #include "base/time.h"
 #include "base/util.h"
 #include "fiber/call_id.h"
+#include "gpu/xgmi.h"
 #include "mrpc/proto/rpc_meta.pb.h"
 #include "policy/device_payload.h"
 #include "policy/policies.h"
@@ -115,6 +116,12 @@ void PackRpcRequest(Buf* packet, uint64_t correlation_id, const pb::MethodDescri
     }
     StreamId sid = cntl->_request_stream;
     if (sid) FillStreamSettings(sid, meta.mutable_stream_settings());
+    // xGMI hello: offered on every request until the connection has a
+    // device transport, so each response that could carry device payloads
+    // also carries the server's arena description.
+    if (cntl->_use_device_transport && cntl->_pack_socket && !cntl->_pack_socket->transport()) {
+        gpu::FillXgmiHello(meta.mutable_xgmi_hello());
+    }
     Buf host_attachment;
     if (!SplitDevicePayload(cntl, /*request=*/true, cntl->request_attachment(), &host_attachment, &meta)) return;
     if (host_attachment.size()) meta.set_attachment_size((int32_t)host_attachment.size());
@@ -164,6 +171,7 @@ static void SendRpcResponse(int64_t correlation_id, Controller* cntl, pb::Messag
         }
     }
     meta.set_correlation_id(correlation_id);
+    if (cntl->_reply_xgmi_hello) gpu::FillXgmiHello(meta.mutable_xgmi_hello());
     if (cntl->_response_stream) FillStreamSettings(cntl->_response_stream, meta.mutable_stream_settings());
     Buf packet;
     SerializeRpcHeaderAndMeta(&packet, meta, res_body.size() + host_attachment.size());
@@ -222,6 +230,14 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
             cntl->_span->log_id = (uint64_t)rm.log_id();
             cntl->_trace_id = cntl->_span->trace_id;
             cntl->_span_id = cntl->_span->span_id;
+        }
+    }
+    if (meta.has_xgmi_hello() && gpu::XgmiEnabled()) {
+        std::string err;
+        if (gpu::AttachXgmiPeer(socket, meta.xgmi_hello(), &err) == 0) {
+            cntl->_reply_xgmi_hello = true;
+        } else {
+            LOG_EVERY_SECOND(WARNING) << "xGMI peer " << socket->remote_side() << " not attached: " << err;
         }
     }
     const int64_t corr = meta.correlation_id();
@@ -335,6 +351,12 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         fiber::call_id_unlock(cid);  // response of an obsolete attempt
         msg->Destroy();
         return;
+    }
+    if (meta.has_xgmi_hello() && gpu::XgmiEnabled()) {
+        std::string err;
+        if (gpu::AttachXgmiPeer(msg->socket(), meta.xgmi_hello(), &err) != 0) {
+            LOG_EVERY_SECOND(WARNING) << "xGMI peer " << msg->socket()->remote_side() << " not attached: " << err;
+        }
     }
     int saved_error = 0;
     const RpcResponseMeta& rm = meta.response();

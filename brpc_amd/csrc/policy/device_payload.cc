@@ -62,7 +62,12 @@ bool SplitDevicePayload(Controller* cntl, bool request, const Buf& attachment, B
             d->set_position((int64_t)pos);
             const int rc = g_hooks.send(sock, r.block->data + r.offset, r.length, r.block->device,
                                         cntl->verify_device_payload(), d);
-            if (rc != 0) {
+            if (rc > 0) {  // transport busy (ring full): stage this block inline
+                meta->mutable_device_payload()->RemoveLast();
+                Buf one;
+                one.append_block(r.block, r.offset, r.length);
+                StageDeviceBufToHost(one, host_out);
+            } else if (rc != 0) {
                 cntl->SetFailed(EXGMI, "fail to send %u device bytes over %s", r.length, sock->description().c_str());
                 return false;
             }

@@ -22,7 +22,9 @@ class DevicePayload;
 
 struct DeviceTransportHooks {
     // Copy [dev_ptr, dev_ptr+len) on `device` into the peer ring of `sock`.
-    // Fill desc (ring_offset/length/src_device). 0 on success.
+    // Fill desc (ring_offset/length/src_device). 0 on success, >0 when the
+    // transport cannot take the block right now (sent inline instead), <0 on
+    // error.
     int (*send)(Socket* sock, const void* dev_ptr, size_t len, int device, bool with_crc, policy::DevicePayload* desc) = nullptr;
     // Append a block referencing the received ring region to *out.
     int (*recv)(Socket* sock, const policy::DevicePayload& desc, Buf* out) = nullptr;

@@ -10,6 +10,7 @@
 #include "base/logging.h"
 #include "fiber/fiber.h"
 #include "gpu/gpu.h"
+#include "gpu/xgmi.h"
 #include "mrpc/proto/echo.pb.h"
 #include "press/press.h"
 #include "rpc/channel.h"
@@ -264,5 +265,20 @@ PYBIND11_MODULE(_native, m) {
     g.def("device_arch", [](int dev) { return gpu::DeviceArch(dev); }, py::arg("device") = 0);
     g.def("device_name", [](int dev) { return gpu::DeviceName(dev); }, py::arg("device") = 0);
     g.def("polled_events", [] { return gpu::PolledEvents(); });
+    g.def("enable_xgmi", [](int dev) {
+        std::string err;
+        if (gpu::EnableXgmiTransport(dev, &err) != 0) throw std::runtime_error(err);
+    }, py::arg("device") = 0);
+    g.def("xgmi_stats", [] {
+        const gpu::XgmiStats s = gpu::GetXgmiStats();
+        py::dict d;
+        d["sent_bytes"] = s.sent_bytes;
+        d["recv_bytes"] = s.recv_bytes;
+        d["sent_payloads"] = s.sent_payloads;
+        d["recv_payloads"] = s.recv_payloads;
+        d["ring_full_fallbacks"] = s.ring_full_fallbacks;
+        d["crc_failures"] = s.crc_failures;
+        return d;
+    });
     bind_gpu_ops(g);
 }

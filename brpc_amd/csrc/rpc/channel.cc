@@ -7,6 +7,7 @@
 #include "base/util.h"
 #include "cluster/lb_with_naming.h"
 #include "fiber/fiber.h"
+#include "gpu/xgmi.h"
 #include "net/socket_map.h"
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
@@ -67,6 +68,14 @@ int Channel::InitChannelOptions(const ChannelOptions* options) {
     }
     _map_signature = string_printf("%s|%s|%s|%d", _protocol->name, _options.connection_group.c_str(),
                                    _options.use_ssl ? "ssl" : "", _options.use_device_transport ? _options.gpu_device : -2);
+    if (_options.use_device_transport) {
+        std::string err;
+        if (gpu::EnableXgmiTransport(_options.gpu_device, &err) != 0) {
+            LOG(WARNING) << "xGMI device transport unavailable (" << err
+                         << "); device attachments will be staged through host memory";
+            _options.use_device_transport = false;
+        }
+    }
     return 0;
 }
 
@@ -185,6 +194,7 @@ void Channel::CallMethod(const pb::MethodDescriptor* method, RpcController* cont
     cntl->_protocol = _protocol;
     cntl->_protocol_type = _protocol_type;
     if (!_protocol_param.empty()) cntl->_protocol_param = _protocol_param;
+    cntl->_use_device_transport = _options.use_device_transport;
     cntl->_auth = _options.auth;
     if (cntl->_connection_type == CONNECTION_TYPE_SINGLE) cntl->_connection_type = _connection_type;
     if (!cntl->_retry_policy) cntl->_retry_policy = _options.retry_policy;

@@ -96,6 +96,8 @@ void Controller::Reset() {
     _progressive_sink.reset();
     _pipelined_count = 0;
     _pipelined_tag = 0;
+    _use_device_transport = false;
+    _reply_xgmi_hello = false;
     _session_kv.clear();
     _request_stream = _response_stream = 0;
     _stream_creator.reset();

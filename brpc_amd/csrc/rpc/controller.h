@@ -223,6 +223,8 @@ public:
     int _pipelined_count = 0;
     uint32_t _pipelined_tag = 0;
     std::string _protocol_param;  // "grpc" for channels of protocol "h2:grpc"
+    bool _use_device_transport = false;  // client: offer the xGMI hello on this call
+    bool _reply_xgmi_hello = false;      // server: answer the peer's xGMI hello
     HttpHeader* _http_request = nullptr;
     HttpHeader* _http_response = nullptr;
     std::map<std::string, std::string> _session_kv;

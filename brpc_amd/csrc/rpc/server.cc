@@ -11,6 +11,7 @@
 #include "base/time.h"
 #include "base/util.h"
 #include "fiber/fiber.h"
+#include "gpu/xgmi.h"
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
 #include "var/var.h"
@@ -282,6 +283,13 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
         static std::mutex once_mu;
         std::lock_guard<std::mutex> g(once_mu);
         if (!FindServiceByName("index")) g_builtin_hook(this);
+    }
+    if (_options.gpu_device >= 0) {
+        // Serve device attachments over xGMI to same-node peers that offer it.
+        std::string err;
+        if (gpu::EnableXgmiTransport(_options.gpu_device, &err) != 0) {
+            LOG(WARNING) << "xGMI device transport unavailable on device " << _options.gpu_device << ": " << err;
+        }
     }
     _amc = _options.max_concurrency;
     _cl.reset(CreateConcurrencyLimiter(_amc));

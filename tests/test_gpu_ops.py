@@ -129,3 +129,61 @@ def test_device_payload_echo(dev):
         assert st["success"] == 500 and st["error"] == 0, st
     finally:
         s.stop()
+
+
+def test_device_payload_uses_xgmi_in_process(dev):
+    """Same-process peers: the hello maps the local arena; payloads skip TCP."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        before = native.gpu.xgmi_stats()
+        p = native.Press({"server": s.address, "concurrency": 4, "attachment_size": 1 << 20,
+                          "device_attachment": True, "gpu_device": 0, "check_echo": True})
+        p.run_requests(200)
+        st = p.stats()
+        assert st["success"] == 200 and st["error"] == 0, st
+        after = native.gpu.xgmi_stats()
+        # the first call(s) of a connection are staged through host while the
+        # hello is in flight; everything after moves over the device arena
+        assert after["sent_payloads"] - before["sent_payloads"] >= 100, (before, after)
+        assert after["recv_payloads"] - before["recv_payloads"] >= 100, (before, after)
+        assert after["crc_failures"] == before["crc_failures"]
+    finally:
+        s.stop()
+
+
+_SERVER_SCRIPT = r"""
+import sys, torch
+from brpc_amd.models import start_echo_server
+s = start_echo_server("127.0.0.1:0", gpu_device=0)
+print(s.port, flush=True)
+sys.stdin.read()
+s.stop()
+"""
+
+
+def test_device_payload_xgmi_cross_process(dev):
+    """Two processes on one GPU: IPC-mapped arenas + shm release tables."""
+    import os
+    import subprocess
+    import sys
+    from brpc_amd import native
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=repo + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    srv = subprocess.Popen([sys.executable, "-c", _SERVER_SCRIPT], stdin=subprocess.PIPE,
+                           stdout=subprocess.PIPE, env=env, text=True)
+    try:
+        port = int(srv.stdout.readline())
+        before = native.gpu.xgmi_stats()
+        p = native.Press({"server": "127.0.0.1:%d" % port, "concurrency": 4, "attachment_size": 1 << 20,
+                          "device_attachment": True, "gpu_device": 0, "check_echo": True})
+        p.run_requests(200)
+        st = p.stats()
+        assert st["success"] == 200 and st["error"] == 0, st
+        after = native.gpu.xgmi_stats()
+        assert after["sent_payloads"] - before["sent_payloads"] >= 100, (before, after)
+        assert after["recv_payloads"] - before["recv_payloads"] >= 100, (before, after)
+    finally:
+        srv.stdin.close()
+        srv.wait(timeout=60)
