@@ -574,6 +574,7 @@ int Socket::Write(Buf* data, const WriteOptions* options) {
         PipelinedInfo pi;
         pi.count = opt.pipelined_count;
         pi.tag = opt.pipelined_tag;
+        pi.protocol = opt.pipelined_protocol;
         pi.id_wait = opt.id_wait;
         _pipeline_q.push_back(pi);
         return StartWrite(req, opt);

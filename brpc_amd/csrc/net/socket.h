@@ -108,11 +108,13 @@ struct WriteOptions {
     int pipelined_count = 0;
     // protocol-private tag carried with the pipelined entry (e.g. HEAD)
     uint32_t pipelined_tag = 0;
+    int pipelined_protocol = 0;  // ProtocolType of the request (parsers claim only their own)
 };
 
 struct PipelinedInfo {
     int count = 0;
     uint32_t tag = 0;
+    int protocol = 0;
     fiber::CallId id_wait = fiber::INVALID_CALL_ID;
 };
 

@@ -176,6 +176,11 @@ public:
 
 // Free helpers used by generated code.
 void ClearOneofSiblings(Message* m, const FieldDescriptor* f);
+}  // namespace pb
+// Field-less descriptor for hand-written opaque messages (redis, memcache,
+// nshead, thrift...): such messages carry their own wire encoding.
+const pb::Descriptor* OpaqueDescriptor(const char* full_name);
+namespace pb {
 const Message& DefaultInstanceOf(const Descriptor* d);
 
 }  // namespace pb

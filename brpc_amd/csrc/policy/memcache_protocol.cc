@@ -43,7 +43,7 @@ ParseResult ParseMemcacheMessage(Buf* source, Socket* socket, bool, const void*)
         unsigned char magic;
         source->copy_to(&magic, 1);
         PipelinedInfo peek;
-        if (magic != 0x81 || !socket->PeekPipelinedInfo(&peek)) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+        if (magic != 0x81 || !socket->PeekPipelinedInfo(&peek) || peek.protocol != PROTOCOL_MEMCACHE) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
         ctx = new McContext;
         if (!socket->InstallParsingContext(ctx)) {
             delete ctx;

@@ -130,10 +130,12 @@ ParseResult ParseRedisMessage(Buf* source, Socket* socket, bool read_eof, const 
         } else {
             // only claim the socket if a redis call is waiting on it
             PipelinedInfo peek;
-            if (!socket->PeekPipelinedInfo(&peek)) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+            if (!socket->PeekPipelinedInfo(&peek) || peek.protocol != PROTOCOL_REDIS) {
+                return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+            }
             char c;
             source->copy_to(&c, 1);
-            if (!strchr("+-:$*", c)) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
+            if (c == '\0' || !strchr("+-:$*", c)) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
             ctx = new RedisClientContext;
             if (!socket->InstallParsingContext(ctx)) {
                 delete ctx;

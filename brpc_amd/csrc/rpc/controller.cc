@@ -20,6 +20,11 @@
 
 namespace mrpc {
 
+const IdlNames idl_single_req_single_res = {"req", "res"};
+const IdlNames idl_single_req_multi_res = {"req", ""};
+const IdlNames idl_multi_req_single_res = {"", "res"};
+const IdlNames idl_multi_req_multi_res = {"", ""};
+
 Controller::Controller() {}
 
 Controller::~Controller() {
@@ -96,6 +101,8 @@ void Controller::Reset() {
     _progressive_sink.reset();
     _pipelined_count = 0;
     _pipelined_tag = 0;
+    _idl_names = idl_single_req_single_res;
+    _idl_result = IDL_VOID_RESULT;
     _use_device_transport = false;
     _reply_xgmi_hello = false;
     _session_kv.clear();
@@ -395,6 +402,7 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
     wopt.id_wait = cid;
     wopt.pipelined_count = _pipelined_count;
     wopt.pipelined_tag = _pipelined_tag;
+    wopt.pipelined_protocol = (int)_protocol_type;
     // Errors of Write() are delivered through call_id_error(cid), which is
     // queued while we hold the lock and handled at unlock.
     sock->Write(&packet, &wopt);

@@ -37,6 +37,7 @@ class ProgressiveAttachment;
 class ProgressiveReader;
 class ProgressiveSink;
 class StreamCreator;
+class MongoContext;
 struct Protocol;
 typedef uint64_t StreamId;
 
@@ -47,6 +48,18 @@ public:
     virtual void* CreateData() const = 0;
     virtual void DestroyData(void* d) const = 0;
 };
+
+// Names wrapping the request/response inside ubrpc's params/result_params
+// objects (reference controller.h:86-94).
+struct IdlNames {
+    const char* request_name;   // must be a string constant
+    const char* response_name;
+};
+extern const IdlNames idl_single_req_single_res;  // {"req", "res"} (default)
+extern const IdlNames idl_single_req_multi_res;   // {"req", ""}
+extern const IdlNames idl_multi_req_single_res;   // {"", "res"}
+extern const IdlNames idl_multi_req_multi_res;    // {"", ""}
+static const int64_t IDL_VOID_RESULT = 12345678987654321LL;
 
 class Controller : public RpcController {
 public:
@@ -126,6 +139,16 @@ public:
     void ReadProgressiveAttachmentBy(ProgressiveReader* r);
     void response_will_be_read_progressively() { _read_progressively = true; }
     bool is_response_read_progressively() const { return _read_progressively; }
+
+    // ---------------- ubrpc (mcpack/compack idl) naming and result
+    void set_idl_names(const IdlNames& n) { _idl_names = n; }
+    IdlNames idl_names() const { return _idl_names; }
+    void set_idl_result(int64_t r) { _idl_result = r; }
+    int64_t idl_result() const { return _idl_result; }
+
+    // ---------------- mongo: per-connection context of a mongo server call
+    MongoContext* mongo_session_data() const { return _mongo_session_data.get(); }
+    std::shared_ptr<MongoContext> _mongo_session_data;
 
     // ---------------- kv log for server logging (SessionKV)
     Controller& LogKV(const std::string& k, const std::string& v) {
@@ -223,6 +246,8 @@ public:
     int _pipelined_count = 0;
     uint32_t _pipelined_tag = 0;
     std::string _protocol_param;  // "grpc" for channels of protocol "h2:grpc"
+    IdlNames _idl_names = {"req", "res"};
+    int64_t _idl_result = IDL_VOID_RESULT;
     bool _use_device_transport = false;  // client: offer the xGMI hello on this call
     bool _reply_xgmi_hello = false;      // server: answer the peer's xGMI hello
     HttpHeader* _http_request = nullptr;

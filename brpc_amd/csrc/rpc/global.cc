@@ -63,6 +63,11 @@ void GlobalInitializeOrDie() {
         policy::RegisterH2Protocol();
         policy::RegisterRedisProtocol();
         policy::RegisterMemcacheProtocol();
+        policy::RegisterHuluProtocol();
+        policy::RegisterSofaProtocol();
+        policy::RegisterNsheadProtocols();  // nshead, nova, public_pbrpc, nshead_mcpack, ubrpc_*
+        policy::RegisterEspProtocol();
+        policy::RegisterMongoProtocol();
         for (ProtocolRegistrar r : extra_registrars()) r();
         // Client-side messenger handles responses of every protocol.
         std::vector<std::pair<ProtocolType, Protocol>> protocols;

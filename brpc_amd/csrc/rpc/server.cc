@@ -70,6 +70,7 @@ int Server::AddServiceInternal(Service* s, bool is_builtin, ServiceOwnership own
     sp.restful_mappings = restful;
     _services[sd->full_name] = sp;
     _services_by_short_name[sd->name] = s;
+    if (!is_builtin && !_first_service) _first_service = s;
     for (int i = 0; i < sd->method_count(); ++i) {
         const pb::MethodDescriptor* md = sd->method(i);
         MethodProperty mp;
@@ -111,6 +112,7 @@ int Server::RemoveService(Service* service) {
     if (it == _services.end()) return -1;
     for (int i = 0; i < sd->method_count(); ++i) _methods.erase(sd->full_name + "." + sd->method(i)->name);
     _services_by_short_name.erase(sd->name);
+    if (_first_service == service) _first_service = nullptr;
     if (it->second.ownership == SERVER_OWNS_SERVICE) delete it->second.service;
     _services.erase(it);
     return 0;
@@ -123,6 +125,7 @@ void Server::ClearServices() {
     }
     _services.clear();
     _services_by_short_name.clear();
+    _first_service = nullptr;
     _methods.clear();
     _restful.clear();
 }

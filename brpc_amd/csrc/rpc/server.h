@@ -91,6 +91,8 @@ public:
     // restful lookup: returns property and fills unresolved path
     const MethodProperty* FindMethodPropertyByURI(const std::string& path, std::string* unresolved) const;
     size_t service_count() const;
+    // The first non-builtin service added (nova_pbrpc / nshead adaptors).
+    Service* first_service() const { return _first_service; }
     void ListServices(std::vector<Service*>* out) const;
     void ListMethodProperties(std::vector<const MethodProperty*>* out) const;
 
@@ -140,6 +142,7 @@ private:
     std::unique_ptr<Acceptor> _internal_am;
     std::map<std::string, ServiceProperty> _services;           // full name
     std::map<std::string, Service*> _services_by_short_name;
+    Service* _first_service = nullptr;
     std::unordered_map<std::string, MethodProperty> _methods;  // "svc.Method"
     std::vector<std::pair<std::string, std::string>> _restful;  // prefix -> full method name
     std::atomic<int> _concurrency{0};
