@@ -60,7 +60,7 @@ class NsheadServerContext : public ParsingContext {
 public:
     static const int kTag = 0x4e534856;  // "NSHV"
     int protocol_tag() const override { return kTag; }
-    std::shared_ptr<NsheadResponseSequencer> seq = std::make_shared<NsheadResponseSequencer>();
+    std::shared_ptr<OrderedResponseWriter> seq = std::make_shared<OrderedResponseWriter>();
 };
 
 class NsheadServerMessage : public InputMessageBase {
@@ -68,7 +68,7 @@ public:
     Buf meta;  // the 36-byte head
     Buf payload;
     uint64_t seq = 0;
-    std::shared_ptr<NsheadResponseSequencer> sequencer;
+    std::shared_ptr<OrderedResponseWriter> sequencer;
 };
 
 // 0: complete frame available, else the parse error.

@@ -68,6 +68,7 @@ void GlobalInitializeOrDie() {
         policy::RegisterNsheadProtocols();  // nshead, nova, public_pbrpc, nshead_mcpack, ubrpc_*
         policy::RegisterEspProtocol();
         policy::RegisterMongoProtocol();
+        policy::RegisterThriftProtocol();
         for (ProtocolRegistrar r : extra_registrars()) r();
         // Client-side messenger handles responses of every protocol.
         std::vector<std::pair<ProtocolType, Protocol>> protocols;

@@ -19,6 +19,7 @@
 #include "base/buf.h"
 #include "pb/message.h"
 #include "pb/service.h"
+#include "rpc/ordered_response.h"
 
 namespace mrpc {
 
@@ -86,22 +87,10 @@ public:
     // nshead carries no correlation id: responses of one connection must
     // leave in request order even when handlers finish out of order.
     uint64_t _seq = 0;
-    std::shared_ptr<class NsheadResponseSequencer> _sequencer;
+    std::shared_ptr<OrderedResponseWriter> _sequencer;
 };
 
-// Per-connection reorder buffer: Deliver(seq, packet) writes every packet
-// whose predecessors have all been delivered.
-class NsheadResponseSequencer {
-public:
-    uint64_t NextSeq() { return _next_assign++; }  // parse side (one reader per socket)
-    void Deliver(uint64_t seq, Buf* packet, class Socket* sock);
 
-private:
-    uint64_t _next_assign = 0;
-    std::mutex _mu;
-    uint64_t _next_send = 0;
-    std::map<uint64_t, Buf> _ready;
-};
 
 class NsheadService {
 public:

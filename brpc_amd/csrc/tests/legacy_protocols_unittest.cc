@@ -525,3 +525,105 @@ TEST(Mcpack, object_isoarray_and_lenient_numbers) {
     ASSERT_EQ(r.inners_size(), 3);
     EXPECT_EQ(r.inners(1).x(), 2);
 }
+
+// ---------------------------------------------------------------- thrift
+#include "thrift/thrift.h"
+
+namespace {
+// add(1: i32 a, 2: i32 b) -> i32 ; echo(1: string s) -> string ; boom() -> exception
+class CalcThrift : public ThriftService {
+public:
+    void ProcessThriftFramedRequest(Controller* cntl, ThriftFramedMessage* req, ThriftFramedMessage* res,
+                                    Closure* done) override {
+        ClosureGuard g(done);
+        if (req->method_name == "add") {
+            const thrift::Value* a = req->body.find(1);
+            const thrift::Value* b = req->body.find(2);
+            res->body.field(0) = thrift::Value::I32((int32_t)((a ? a->as_int() : 0) + (b ? b->as_int() : 0)));
+        } else if (req->method_name == "echo") {
+            const thrift::Value* s = req->body.find(1);
+            res->body.field(0) = s ? *s : thrift::Value::String("");
+        } else {
+            cntl->SetFailed(ENOMETHOD, "no method %s", req->method_name.c_str());
+        }
+    }
+};
+}  // namespace
+
+TEST(Thrift, binary_protocol_wire_format) {
+    // CALL "ping" seqid=7 {1: i32 5}: bytes fixed by the TBinaryProtocol spec.
+    thrift::MessageHeader h;
+    h.name = "ping";
+    h.type = thrift::T_CALL;
+    h.seqid = 7;
+    thrift::Value args = thrift::Value::Struct();
+    args.field(1) = thrift::Value::I32(5);
+    std::string out;
+    thrift::WriteMessage(&out, h, args);
+    const unsigned char want[] = {0x80, 0x01, 0x00, 0x01, 0, 0, 0, 4, 'p', 'i', 'n', 'g', 0, 0, 0, 7,
+                                  0x08, 0x00, 0x01, 0, 0, 0, 5, 0x00};
+    ASSERT_EQ(out.size(), sizeof(want));
+    EXPECT_EQ(memcmp(out.data(), want, sizeof(want)), 0);
+    // nested containers round trip
+    thrift::Value v = thrift::Value::Struct();
+    thrift::Value l = thrift::Value::List(thrift::T_STRING);
+    l.elems().push_back(thrift::Value::String("a"));
+    l.elems().push_back(thrift::Value::String("bc"));
+    thrift::Value mp = thrift::Value::Map(thrift::T_I64, thrift::T_DOUBLE);
+    mp.pairs().emplace_back(thrift::Value::I64(-3), thrift::Value::Double(2.5));
+    v.field(1) = l;
+    v.field(2) = mp;
+    v.field(3) = thrift::Value::Bool(true);
+    v.field(-4) = thrift::Value::I16(-9);
+    std::string enc;
+    thrift::WriteValue(&enc, v);
+    thrift::Value back;
+    ASSERT_EQ(thrift::ReadValue(enc.data(), enc.size(), thrift::T_STRUCT, &back), enc.size());
+    EXPECT_TRUE(back == v);
+    EXPECT_EQ(thrift::ReadValue(enc.data(), enc.size() - 1, thrift::T_STRUCT, &back), (size_t)0);
+}
+
+TEST(Thrift, framed_client_server_pipelined) {
+    CalcThrift calc;
+    Server server;
+    ServerOptions o;
+    o.has_builtin_services = false;
+    o.thrift_service = &calc;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &o), 0);
+    Channel ch;
+    ChannelOptions opt;
+    opt.protocol = "thrift";
+    opt.timeout_ms = 3000;
+    opt.max_retry = 0;
+    ASSERT_EQ(ch.Init(("127.0.0.1:" + std::to_string(server.listen_port())).c_str(), &opt), 0);
+    const int N = 32;
+    std::vector<std::unique_ptr<Controller>> cntls(N);
+    std::vector<ThriftFramedMessage> reqs(N), ress(N);
+    for (int i = 0; i < N; ++i) {
+        cntls[i].reset(new Controller);
+        reqs[i].method_name = "add";
+        reqs[i].body.field(1) = thrift::Value::I32(i);
+        reqs[i].body.field(2) = thrift::Value::I32(1000);
+        ch.CallMethod(nullptr, cntls[i].get(), &reqs[i], &ress[i], NewCallback([] {}));
+    }
+    for (int i = 0; i < N; ++i) {
+        cntls[i]->Join();
+        if (cntls[i]->Failed()) fprintf(stderr, "thrift %d: %s\n", i, cntls[i]->ErrorText().c_str());
+        ASSERT_FALSE(cntls[i]->Failed());
+        ASSERT_TRUE(ress[i].success() != nullptr);
+        EXPECT_EQ(ress[i].success()->as_int(), 1000 + i);
+    }
+    Controller c2;
+    ThriftFramedMessage r2, s2;
+    r2.method_name = "echo";
+    r2.body.field(1) = thrift::Value::String(std::string(100000, 'e'));
+    ch.CallMethod(nullptr, &c2, &r2, &s2, nullptr);
+    ASSERT_FALSE(c2.Failed());
+    EXPECT_EQ(s2.success()->as_string().size(), 100000u);
+    Controller c3;
+    ThriftFramedMessage r3, s3;
+    r3.method_name = "nope";
+    ch.CallMethod(nullptr, &c3, &r3, &s3, nullptr);
+    EXPECT_TRUE(c3.Failed());
+    EXPECT_TRUE(c3.ErrorText().find("no method nope") != std::string::npos);
+}
