@@ -61,6 +61,7 @@ void Acceptor::OnNewConnections(Socket* listened) {
         }
         SocketOptions opt;
         opt.fd = fd;
+        opt.ssl_ctx = am->_ssl_ctx;
         get_remote_side(fd, &opt.remote_side);
         SocketId sid;
         if (am->Create(opt, &sid) != 0) {

@@ -22,6 +22,8 @@ public:
     size_t ConnectionCount() const;
     void ListConnections(std::vector<SocketId>* out) const;
     bool accepting() const { return _listened_sid != INVALID_SOCKET_ID; }
+    // Accepted connections detect TLS on their first bytes.
+    void set_ssl_ctx(std::shared_ptr<SslContext> ctx) { _ssl_ctx = std::move(ctx); }
 
 private:
     static void OnNewConnections(Socket* listened);
@@ -33,6 +35,7 @@ private:
     std::set<SocketId> _closing;
     fiber::fiber_t _idle_tid;
     std::atomic<bool> _stop;
+    std::shared_ptr<SslContext> _ssl_ctx;
 };
 
 }  // namespace mrpc

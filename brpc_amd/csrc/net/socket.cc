@@ -138,6 +138,13 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
     m->_user = opt.user;
     m->_on_edge_triggered_events = opt.on_edge_triggered_events;
     m->_conn = opt.conn;
+    m->_ssl_ctx = opt.ssl_ctx;
+    m->_ssl_sni = opt.ssl_sni;
+    {
+        std::lock_guard<std::mutex> g(m->_mu);
+        m->_ssl.reset();
+    }
+    m->_ssl_state.store(!opt.ssl_ctx ? SSL_OFF : (opt.ssl_ctx->is_server() ? SSL_UNKNOWN : SSL_ON));
     m->_health_check_interval_s = opt.health_check_interval_s;
     m->_connect_lazily = opt.connect_lazily;
     m->_nevent.store(0, std::memory_order_relaxed);
@@ -342,8 +349,10 @@ void Socket::OnRecycle() {
     {
         std::lock_guard<std::mutex> g(_mu);
         _transport.reset();
+        _ssl.reset();
     }
     _conn.reset();
+    _ssl_ctx.reset();
     // pooled sub sockets of a main socket are released with it
     if (_shared) {
         std::vector<SocketId> pool;
@@ -408,12 +417,93 @@ ssize_t Socket::DoRead(size_t size_hint) {
         errno = EBADF;
         return -1;
     }
+    if (_ssl_state.load(std::memory_order_acquire) != SSL_OFF) return SslRead(fd, size_hint);
     ssize_t n = _read_buf.append_from_fd(fd, size_hint);
     if (n > 0) {
         in_bytes.fetch_add(n, std::memory_order_relaxed);
         _last_active_us.store(monotonic_us(), std::memory_order_relaxed);
     }
     return n;
+}
+
+ssize_t Socket::WriteList(int fd, Buf** list, size_t n) {
+    if (_conn) return _conn->CutMessageIntoFileDescriptor(fd, list, n);
+    if (_ssl_state.load(std::memory_order_acquire) == SSL_ON) {
+        std::shared_ptr<SslSession> ssl = ssl_session();
+        if (!ssl) {
+            std::lock_guard<std::mutex> g(_mu);
+            if (!_ssl) _ssl = std::make_shared<SslSession>(_ssl_ctx, false, _ssl_sni);
+            ssl = _ssl;
+        }
+        if (!ssl->ok()) {
+            errno = EPROTO;
+            return -1;
+        }
+        return ssl->Write(fd, list, n);
+    }
+    return Buf::cut_multiple_into_fd(fd, list, n);
+}
+
+std::shared_ptr<SslSession> Socket::ssl_session() const {
+    std::lock_guard<std::mutex> g(_mu);
+    return _ssl;
+}
+
+ssize_t Socket::SslRead(int fd, size_t size_hint) {
+    for (;;) {
+        BufPortal raw;
+        const ssize_t n = raw.append_from_fd(fd, size_hint);
+        if (n <= 0) return n;
+        in_bytes.fetch_add(n, std::memory_order_relaxed);
+        _last_active_us.store(monotonic_us(), std::memory_order_relaxed);
+        if (_ssl_state.load(std::memory_order_acquire) == SSL_UNKNOWN) {
+            char head[2];
+            const size_t got = raw.copy_to(head, 2);
+            if (LooksLikeTls(head, got) == 1) {
+                std::lock_guard<std::mutex> g(_mu);
+                _ssl = std::make_shared<SslSession>(_ssl_ctx, true, std::string());
+                _ssl_state.store(SSL_ON, std::memory_order_release);
+            } else {
+                _ssl_state.store(SSL_OFF, std::memory_order_release);  // plaintext client
+                _read_buf.append(std::move(raw));
+                return n;
+            }
+        }
+        std::shared_ptr<SslSession> ssl = ssl_session();
+        if (!ssl) {
+            std::lock_guard<std::mutex> g(_mu);
+            if (!_ssl) _ssl = std::make_shared<SslSession>(_ssl_ctx, false, _ssl_sni);
+            ssl = _ssl;
+        }
+        bool hs_done = false;
+        const ssize_t produced = ssl->Feed(raw, &_read_buf, &hs_done);
+        if (produced < 0) return -1;
+        if (!ssl->Flush(fd)) {
+            // Handshake records did not fit the socket buffer (rare): flush
+            // them from a fiber that waits for EPOLLOUT.
+            AddRef();
+            fiber::fiber_t th;
+            auto flusher = [](void* arg) -> void* {
+                Socket* s = static_cast<Socket*>(arg);
+                std::shared_ptr<SslSession> ss = s->ssl_session();
+                for (int i = 0; ss && i < 200 && !s->Failed(); ++i) {
+                    const int f = s->fd();
+                    if (f < 0 || ss->Flush(f)) break;
+                    timespec ts = realtime_after_us(50000);
+                    s->WaitEpollOut(f, false, &ts);
+                }
+                s->Dereference();
+                return nullptr;
+            };
+            if (fiber::start_background(&th, &fiber::ATTR_NORMAL, flusher, this) != 0) flusher(this);
+        }
+        if (hs_done) {
+            _epollout_butex->fetch_add(1, std::memory_order_release);
+            fiber::butex_wake_all(_epollout_butex);
+        }
+        if (produced > 0) return produced;
+        if (ssl->peer_closed()) return 0;
+    }
 }
 
 void Socket::HandleEpollOut(SocketId id) {
@@ -624,14 +714,14 @@ int Socket::StartWrite(WriteRequest* req, const WriteOptions& opt) {
     }
     if (!opt.write_in_background) {
         const int fd = _fd.load(std::memory_order_acquire);
-        if (_conn) {
+        if (_conn || _ssl_state.load(std::memory_order_relaxed) == SSL_ON) {
             Buf* list[1] = {&req->data};
-            nw = _conn->CutMessageIntoFileDescriptor(fd, list, 1);
+            nw = WriteList(fd, list, 1);
         } else {
             nw = req->data.cut_into_fd(fd);
         }
         if (nw < 0) {
-            if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EOVERCROWDED) {
+            if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EOVERCROWDED && errno != EINPROGRESS) {
                 saved_errno = errno;
                 SetFailed(saved_errno, "fail to write into fd: %s", ErrorText(saved_errno));
                 ReleaseAllFailedWriteRequests(req);
@@ -661,7 +751,7 @@ ssize_t Socket::DoWrite(WriteRequest* req) {
         errno = EBADF;
         return -1;
     }
-    ssize_t nw = _conn ? _conn->CutMessageIntoFileDescriptor(fd, list, n) : Buf::cut_multiple_into_fd(fd, list, n);
+    ssize_t nw = WriteList(fd, list, n);
     if (nw > 0) out_bytes.fetch_add(nw, std::memory_order_relaxed);
     return nw;
 }
@@ -679,6 +769,15 @@ void* Socket::KeepWrite(void* arg) {
         if (s->Failed()) break;
         const ssize_t nw = s->DoWrite(req);
         if (nw < 0) {
+            if (errno == EINPROGRESS) {
+                // TLS handshake in flight: the read side wakes us when done.
+                const int expected = s->_epollout_butex->load(std::memory_order_acquire);
+                if (s->_ssl && !s->_ssl->handshake_done()) {
+                    timespec ts = realtime_after_us(50000);
+                    fiber::butex_wait(s->_epollout_butex, expected, &ts);
+                }
+                continue;
+            }
             if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EOVERCROWDED) {
                 const int saved_errno = errno;
                 s->SetFailed(saved_errno, "fail to keep writing: %s", ErrorText(saved_errno));
@@ -734,6 +833,8 @@ int Socket::GetPooledSocket(SocketUniquePtr* out) {
     opt.user = _user;
     opt.on_edge_triggered_events = _on_edge_triggered_events;
     opt.conn = _conn;
+    opt.ssl_ctx = _ssl_ctx;
+    opt.ssl_sni = _ssl_sni;
     opt.connect_lazily = true;
     SocketId sid;
     if (Create(opt, &sid) != 0) return -1;
@@ -763,6 +864,8 @@ int Socket::GetShortSocket(SocketUniquePtr* out) {
     opt.user = _user;
     opt.on_edge_triggered_events = _on_edge_triggered_events;
     opt.conn = _conn;
+    opt.ssl_ctx = _ssl_ctx;
+    opt.ssl_sni = _ssl_sni;
     opt.connect_lazily = true;
     SocketId sid;
     if (Create(opt, &sid) != 0) return -1;
@@ -799,6 +902,12 @@ int Socket::Revive(int new_fd) {
         _read_buf.clear();
         _nevent.store(0);
         _preferred_index = -1;
+        {
+            // a new connection needs a new TLS session
+            std::lock_guard<std::mutex> g(_mu);
+            _ssl.reset();
+        }
+        if (_ssl_ctx) _ssl_state.store(_ssl_ctx->is_server() ? SSL_UNKNOWN : SSL_ON);
         delete _parsing_context.exchange(nullptr);
         {
             std::lock_guard<std::mutex> g(_pipeline_mu);

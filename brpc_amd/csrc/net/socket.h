@@ -28,6 +28,7 @@
 #include "base/endpoint.h"
 #include "fiber/call_id.h"
 #include "fiber/fiber.h"
+#include "net/ssl.h"
 
 namespace mrpc {
 
@@ -95,6 +96,10 @@ struct SocketOptions {
     int health_check_interval_s = -1;
     std::shared_ptr<SocketConnection> conn;
     bool connect_lazily = false;  // fd < 0: connect to remote_side on first write
+    // TLS: a server context makes the socket detect TLS on its first bytes;
+    // a client context makes it start a TLS session after connecting.
+    std::shared_ptr<SslContext> ssl_ctx;
+    std::string ssl_sni;
 };
 
 struct WriteOptions {
@@ -188,6 +193,9 @@ public:
     std::shared_ptr<Transport> transport() const;
     void set_transport(std::shared_ptr<Transport> t);
     std::shared_ptr<SocketConnection> conn() const { return _conn; }
+    // TLS state (nullptr when the connection is plaintext).
+    std::shared_ptr<SslSession> ssl_session() const;
+    bool is_ssl() const { return _ssl_state.load(std::memory_order_acquire) == SSL_ON; }
 
     // Callbacks run once when the socket fails (streams multiplexed on it).
     void AddFailureCallback(std::function<void()> cb);
@@ -257,6 +265,14 @@ private:
     std::mutex _pipeline_mu;
     std::deque<PipelinedInfo> _pipeline_q;
     std::atomic<bool> _hc_started;
+    // TLS
+    enum { SSL_OFF = 0, SSL_UNKNOWN = 1, SSL_ON = 2 };
+    ssize_t SslRead(int fd, size_t size_hint);
+    ssize_t WriteList(int fd, Buf** list, size_t n);
+    std::shared_ptr<SslContext> _ssl_ctx;
+    std::string _ssl_sni;
+    std::shared_ptr<SslSession> _ssl;
+    std::atomic<int> _ssl_state{SSL_OFF};
 };
 
 // Dump /connections-style info of all live sockets.

@@ -44,6 +44,14 @@ int SocketMapInsert(const SocketMapKey& key, SocketId* id) {
     opt.remote_side = key.peer;
     opt.connect_lazily = true;
     opt.health_check_interval_s = FLAGS_health_check_interval;
+    const size_t ssl_at = key.signature.find("|ssl:");
+    if (ssl_at != std::string::npos) {
+        const size_t b = ssl_at + 5;
+        const size_t e = key.signature.find('|', b);
+        opt.ssl_sni = key.signature.substr(b, e == std::string::npos ? std::string::npos : e - b);
+        opt.ssl_ctx = SslContext::DefaultClient();
+        if (!opt.ssl_ctx) return -1;
+    }
     SocketId sid;
     if (get_client_side_messenger()->Create(opt, &sid) != 0) return -1;
     sm.m[key] = Entry{sid, 1};

@@ -1,0 +1,100 @@
+// TLS for sockets (role of the reference's src/brpc/details/ssl_helper.cpp,
+// ssl_options.h and the SSL state machine in socket.cpp:1852-2035).
+//
+// The TLS engine runs over memory BIOs so it fits the edge-triggered,
+// wait-free socket design unchanged: DoRead feeds raw bytes in and gets
+// plaintext out; writes encrypt plaintext into a per-session ciphertext
+// queue. A write request is only credited once the ciphertext of its bytes
+// reached the kernel, so KeepWrite / partial-write accounting stays exact.
+// Servers detect TLS per connection from the first byte (0x16 = handshake
+// record), so one port serves TLS and plaintext clients alike.
+#pragma once
+
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "base/buf.h"
+
+typedef struct ssl_ctx_st SSL_CTX;
+typedef struct ssl_st SSL;
+typedef struct bio_st BIO;
+
+namespace mrpc {
+
+struct ServerSslOptions {
+    std::string cert_file;      // PEM certificate chain
+    std::string key_file;       // PEM private key
+    std::string ciphers;        // OpenSSL cipher list (empty: default)
+    std::string alpns;          // comma separated, e.g. "h2,http/1.1"
+    bool strict_sni = false;
+};
+
+struct ChannelSslOptions {
+    std::string sni_name;
+    std::string ciphers;
+    std::string ca_file;        // verify the server when set
+    bool verify = false;
+};
+
+class SslContext {
+public:
+    ~SslContext();
+    static std::shared_ptr<SslContext> NewServer(const ServerSslOptions& opt, std::string* err);
+    static std::shared_ptr<SslContext> NewClient(const ChannelSslOptions& opt, std::string* err);
+    // Shared no-verification client context (Channel use_ssl).
+    static std::shared_ptr<SslContext> DefaultClient();
+    SSL_CTX* ctx() const { return _ctx; }
+    bool is_server() const { return _server; }
+
+private:
+    SSL_CTX* _ctx = nullptr;
+    bool _server = false;
+};
+
+class SslSession {
+public:
+    SslSession(const std::shared_ptr<SslContext>& ctx, bool server, const std::string& sni);
+    ~SslSession();
+    bool ok() const { return _ssl != nullptr; }
+    bool handshake_done() const { return _handshake_done; }
+
+    // Read path: raw ciphertext in, plaintext appended to *out. Returns the
+    // plaintext bytes produced, or -1 on a TLS error (errno EPROTO).
+    // *handshake_completed is set when this call finished the handshake
+    // (writers blocked on it should be woken).
+    ssize_t Feed(const Buf& raw, Buf* out, bool* handshake_completed);
+    bool peer_closed() const { return _peer_closed; }
+    // Write path over fd: credits plaintext of data_list whose ciphertext
+    // has been written; returns credited bytes or -1 with errno EAGAIN
+    // (socket buffer full) or EINPROGRESS (waiting for the handshake).
+    ssize_t Write(int fd, Buf** data_list, size_t n);
+    // Flushes pending ciphertext (handshake records); true if empty after.
+    bool Flush(int fd);
+    bool has_pending_output();
+    std::string cipher() const;
+    std::string version() const;
+
+private:
+    void drain_wbio_locked();
+    ssize_t flush_locked(int fd);  // credits plaintext, returns credited bytes
+    std::shared_ptr<SslContext> _ctxref;
+    SSL* _ssl = nullptr;
+    BIO* _rbio = nullptr;
+    BIO* _wbio = nullptr;
+    std::mutex _mu;
+    bool _handshake_done = false;
+    Buf _cipher_out;                            // ciphertext not yet written
+    std::deque<std::pair<size_t, size_t>> _records;  // (cipher bytes, plain bytes) per SSL_write
+    size_t _uncredited_plain = 0;               // encrypted plaintext not yet credited
+    size_t _credited_pending = 0;               // ciphertext bytes of the front record already written
+    size_t _claimable = 0;                      // plaintext credited by reader-side flushes
+    bool _peer_closed = false;
+};
+
+// Is this a TLS ClientHello start? (1 yes, 0 no, -1 need more bytes)
+int LooksLikeTls(const char* p, size_t n);
+
+}  // namespace mrpc

@@ -66,8 +66,10 @@ int Channel::InitChannelOptions(const ChannelOptions* options) {
         _connection_type = (_protocol->supported_connection_type & CONNECTION_TYPE_SINGLE) ? CONNECTION_TYPE_SINGLE
                                                                                           : CONNECTION_TYPE_POOLED;
     }
+    // "ssl:<sni>" in the signature makes SocketMap create TLS client sockets.
     _map_signature = string_printf("%s|%s|%s|%d", _protocol->name, _options.connection_group.c_str(),
-                                   _options.use_ssl ? "ssl" : "", _options.use_device_transport ? _options.gpu_device : -2);
+                                   _options.use_ssl ? ("ssl:" + _options.ssl_sni).c_str() : "",
+                                   _options.use_device_transport ? _options.gpu_device : -2);
     if (_options.use_device_transport) {
         std::string err;
         if (gpu::EnableXgmiTransport(_options.gpu_device, &err) != 0) {

@@ -317,6 +317,22 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
     }
     _listen_addr = actual;
     _am = BuildAcceptor(false);
+    if (_am && !_options.ssl_cert_file.empty()) {
+        ServerSslOptions so;
+        so.cert_file = _options.ssl_cert_file;
+        so.key_file = _options.ssl_key_file;
+        so.ciphers = _options.ssl_ciphers;
+        so.alpns = _options.ssl_alpns;
+        std::string err;
+        std::shared_ptr<SslContext> ctx = SslContext::NewServer(so, &err);
+        if (!ctx) {
+            LOG(ERROR) << "Fail to set up TLS: " << err;
+            ::close(fd);
+            _status = UNINITIALIZED;
+            return -1;
+        }
+        _am->set_ssl_ctx(ctx);  // TLS and plaintext clients share the port
+    }
     if (!_am || _am->StartAccept(fd, _options.idle_timeout_sec) != 0) {
         ::close(fd);
         _status = UNINITIALIZED;

@@ -51,6 +51,8 @@ struct ServerOptions {
     // SSL: certificate + private key (PEM paths); enabled when both set.
     std::string ssl_cert_file;
     std::string ssl_key_file;
+    std::string ssl_ciphers;  // OpenSSL cipher list (empty: library default)
+    std::string ssl_alpns;    // e.g. "h2,http/1.1"
     // MI355X: device ordinal the server's GPU services run on (-1 = none).
     int gpu_device = -1;
 };
