@@ -49,14 +49,31 @@ def parse():
     return ap.parse_args()
 
 
-def auto_workers(local_world):
+def cpu_quota():
+    """CPUs this container may use: the cgroup v2 CFS quota when set (the
+    GPU boxes grant a 16-CPU quota while exposing all host CPUs), else the
+    affinity mask."""
     try:
-        ncpu = len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) / int(period)))
+    except (OSError, ValueError):
+        pass
+    try:
+        return len(os.sched_getaffinity(0))
     except AttributeError:
-        ncpu = os.cpu_count() or 8
-    # a 1-GPU slot gets a 16-CPU share; never oversubscribe the node
-    share = max(4, ncpu // max(1, local_world))
-    return min(16, share)
+        return os.cpu_count() or 8
+
+
+def auto_workers(local_world):
+    # Fiber workers of one rank. Workers plus the dispatcher/timer threads
+    # must stay under the CFS quota, otherwise the whole process is throttled
+    # for the rest of each 100 ms period (measured on the MI355X box with a
+    # 16-CPU quota: 12 workers ~1.0-1.1M QPS, 16 workers 0.4-0.6M;
+    # profiles/bench_r1_worker_sweep.txt).
+    share = cpu_quota() // max(1, local_world)
+    return max(4, min(12, share - 4))
 
 
 def main():

@@ -16,6 +16,7 @@
 #include "base/time.h"
 #include "base/util.h"
 #include "cluster/circuit_breaker.h"
+#include "cluster/cluster_recover_policy.h"
 #include "cluster/load_balancer.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
@@ -90,6 +91,7 @@ protected:
     int pick_from(const ServerList& l, size_t start, const SelectIn& in, SelectOut* out) {
         const size_t n = l.servers.size();
         if (n == 0) return EHOSTDOWN;
+        if (_recover && _recover->StopRecoverIfNecessary() && _recover->DoReject(l.servers)) return EREJECT;
         for (size_t i = 0; i < n; ++i) {
             const ServerId& s = l.servers[(start + i) % n];
             if (in.excluded && in.excluded->IsExcluded(s.id)) continue;
@@ -100,9 +102,21 @@ protected:
             const ServerId& s = l.servers[(start + i) % n];
             if (IsServerAvailable(s.id, out->ptr)) return 0;
         }
+        if (_recover) _recover->StartRecover();
         return EHOSTDOWN;
     }
+    // "min_working_instances=N hold_seconds=S" enables cluster recovery throttling.
+    template <typename T>
+    static LoadBalancer* NewWithRecover(const std::string& params) {
+        T* lb = new T;
+        if (!GetRecoverPolicyByParams(params, &lb->_recover)) {
+            delete lb;
+            return nullptr;
+        }
+        return lb;
+    }
     DoublyBufferedData<ServerList> _db;
+    std::shared_ptr<ClusterRecoverPolicy> _recover;
 };
 
 class RoundRobinLB : public ListLB {
@@ -113,7 +127,7 @@ public:
         static thread_local uint64_t offset = fast_rand();
         return pick_from(*p, (size_t)(offset++), in, out);
     }
-    LoadBalancer* New(const std::string&) const override { return new RoundRobinLB; }
+    LoadBalancer* New(const std::string& params) const override { return NewWithRecover<RoundRobinLB>(params); }
     void Describe(std::ostream& os) const override { os << "rr"; }
 };
 
@@ -124,7 +138,7 @@ public:
         _db.Read(&p);
         return pick_from(*p, (size_t)fast_rand(), in, out);
     }
-    LoadBalancer* New(const std::string&) const override { return new RandomLB; }
+    LoadBalancer* New(const std::string& params) const override { return NewWithRecover<RandomLB>(params); }
     void Describe(std::ostream& os) const override { os << "random"; }
 };
 

@@ -21,6 +21,7 @@
 #include "rpc/server.h"
 #include "rpc/span.h"
 #include "rpc/stream_internal.h"
+#include "rpc/usercode_backup_pool.h"
 
 DECLARE_uint64(max_body_size);
 DEFINE_bool(baidu_protocol_use_fullname, true, "put the full service name in requests");
@@ -315,7 +316,7 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
     Closure* done = NewCallback([corr, cntl, req, res, server, ms, start_parse_us] {
         SendRpcResponse(corr, cntl, req, res, server, ms, start_parse_us);
     });
-    mp->service->CallMethod(mp->method, cntl, req, res, done);
+    CallServiceMethod(mp->service, mp->method, cntl, req, res, done);
 }
 
 bool VerifyRpcRequest(const InputMessageBase* msg_base) {

@@ -36,6 +36,7 @@
 #include "rpc/method_status.h"
 #include "rpc/protocol.h"
 #include "rpc/server.h"
+#include "rpc/usercode_backup_pool.h"
 
 DECLARE_uint64(max_body_size);
 DEFINE_int32(h2_client_stream_window_size, 256 * 1024, "initial receive window of each h2 stream");
@@ -1008,7 +1009,7 @@ void ProcessH2Request(InputMessageBase* msg_base) {
         return;
     }
     Closure* done = NewCallback([call] { SendH2Response(call); });
-    mp->service->CallMethod(mp->method, cntl, call.req, call.res, done);
+    CallServiceMethod(mp->service, mp->method, cntl, call.req, call.res, done);
 }
 
 static const std::string& GetH2MethodName(const pb::MethodDescriptor* method, const Controller*) {

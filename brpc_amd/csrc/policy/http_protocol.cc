@@ -29,6 +29,7 @@
 #include "rpc/protocol.h"
 #include "rpc/server.h"
 #include "rpc/span.h"
+#include "rpc/usercode_backup_pool.h"
 
 DECLARE_uint64(max_body_size);
 DEFINE_bool(http_verbose, false, "print http request/response heads to stderr");
@@ -381,7 +382,7 @@ void ProcessHttpRequest(InputMessageBase* msg_base) {
     Closure* done = NewCallback([cntl, req, res, server, ms, start_us, keep_alive, http10] {
         SendHttpResponse(cntl, req, res, server, ms, start_us, keep_alive, http10);
     });
-    mp->service->CallMethod(mp->method, cntl, req, res, done);
+    CallServiceMethod(mp->service, mp->method, cntl, req, res, done);
 }
 
 bool VerifyHttpRequest(const InputMessageBase* msg_base) {

@@ -14,6 +14,7 @@
 #include "rpc/mongo.h"
 #include "rpc/protocol.h"
 #include "rpc/server.h"
+#include "rpc/usercode_backup_pool.h"
 
 DECLARE_uint64(max_body_size);
 
@@ -177,7 +178,7 @@ void ProcessMongoRequest(InputMessageBase* base) {
         SendMongoResponse(c);
         return;
     }
-    mp->service->CallMethod(mp->method, cntl, &c->req, &c->res, NewCallback([c] { SendMongoResponse(c); }));
+    CallServiceMethod(mp->service, mp->method, cntl, &c->req, &c->res, NewCallback([c] { SendMongoResponse(c); }));
 }
 
 void RegisterMongoProtocol() {

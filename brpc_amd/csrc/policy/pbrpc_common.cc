@@ -9,6 +9,7 @@
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
 #include "rpc/span.h"
+#include "rpc/usercode_backup_pool.h"
 
 namespace mrpc {
 namespace policy {
@@ -197,7 +198,7 @@ void RunPbServerCall(PbServerRequest* r, PbResponsePacker packer) {
     if (cntl->_span) cntl->_span->start_callback_real_us = realtime_us();
     Span::set_tls_parent(cntl->_span);
     Closure* done = NewCallback([st] { SendPbResponse(st); });
-    mp->service->CallMethod(mp->method, cntl, st->req, st->res, done);
+    CallServiceMethod(mp->service, mp->method, cntl, st->req, st->res, done);
 }
 
 void CompleteClientCallWith(fiber::CallId cid, Socket* sock, const std::function<int(Controller*)>& fill) {

@@ -360,7 +360,11 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
         const int rc = _lb->SelectServer(in, &out);
         if (rc != 0 || !tmp) {
             fiber::call_id_unlock(_correlation_id);
-            fiber::call_id_error(cid, EHOSTDOWN, "no server available");
+            if (rc == EREJECT) {
+                fiber::call_id_error(cid, EREJECT, "rejected by the cluster recover policy");
+            } else {
+                fiber::call_id_error(cid, EHOSTDOWN, "no server available");
+            }
             return;
         }
         _current_call.need_feedback = out.need_feedback;

@@ -14,6 +14,7 @@
 #include "rpc/protocol.h"
 #include "rpc/server.h"
 #include "rpc/span.h"
+#include "rpc/usercode_backup_pool.h"
 
 namespace mrpc {
 
@@ -135,7 +136,7 @@ void NsheadPbServiceAdaptor::ProcessNsheadRequest(const Server& server, Controll
         pb_done->Run();
         return;
     }
-    mp->service->CallMethod(mp->method, cntl, req, res, pb_done);
+    CallServiceMethod(mp->service, mp->method, cntl, req, res, pb_done);
 }
 
 // ------------------------------------------------------------ nova_pbrpc
