@@ -88,6 +88,10 @@ def main():
         print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, topo.world_size), file=sys.stderr)
     workers = a.workers or auto_workers(topo.local_world_size)
     native.set_flag("fiber_concurrency", str(workers))
+    # extra runtime flags for experiments: MRPC_FLAGS="--name=value ..."
+    for item in os.environ.get("MRPC_FLAGS", "").split():
+        k, _, v = item.lstrip("-").partition("=")
+        native.set_flag(k, v or "true")
     cuda = torch.cuda.is_available()
 
     def sync():

@@ -232,6 +232,14 @@ int ParseCommandLineFlags(int* argc, char*** argv, bool remove_flags) {
         } else {
             name = body;
         }
+        if (name == "help" || name == "helpfull") {
+            // gflags-like: list every flag with its default and exit
+            for (const FlagInfo& f : ListFlags()) {
+                fprintf(stdout, "  -%s (%s) type: %s default: %s\n", f.name.c_str(), f.description.c_str(),
+                        f.type.c_str(), f.default_value.c_str());
+            }
+            exit(0);
+        }
         FlagInfo info;
         bool known = GetFlagInfo(name, &info);
         if (!known && !has_value && name.compare(0, 2, "no") == 0 && GetFlagInfo(name.substr(2), &info) &&

@@ -164,6 +164,7 @@ public:
     void flush_nosignal_tasks();
     void flush_nosignal_tasks_remote();
     bool steal_task(fiber_t* tid);
+    bool spin_for_task(fiber_t* tid);
     bool wait_task(fiber_t* tid);
 
     void set_remained(void (*fn)(void*), void* arg) {

@@ -9,9 +9,12 @@
 
 #include "base/flags.h"
 #include "base/logging.h"
+#include "base/time.h"
 #include "fiber/fiber.h"
 
 DEFINE_int32(event_dispatcher_num, 1, "Number of event dispatchers");
+DEFINE_int32(event_dispatcher_spin_us, 50,
+             "after handling events, poll epoll without blocking for this long before sleeping (0 disables)");
 
 namespace mrpc {
 
@@ -101,9 +104,24 @@ void* EventDispatcher::RunThis(void* arg) {
 
 void EventDispatcher::Run() {
     epoll_event e[32];
+    int64_t last_event_ns = 0;
     while (!_stop) {
-        const int n = epoll_wait(_epfd, e, 32, -1);
+        int n;
+        if (FLAGS_event_dispatcher_spin_us > 0 &&
+            monotonic_ns() - last_event_ns < (int64_t)FLAGS_event_dispatcher_spin_us * 1000) {
+            // Right after events the reply of what was just sent usually
+            // follows within µs: poll instead of sleeping in the kernel, and
+            // yield between polls so fibers queued on this worker still run.
+            n = epoll_wait(_epfd, e, 32, 0);
+            if (n == 0) {
+                fiber::yield();
+                continue;
+            }
+        } else {
+            n = epoll_wait(_epfd, e, 32, -1);
+        }
         if (_stop) break;
+        if (n > 0) last_event_ns = monotonic_ns();
         if (n < 0) {
             if (errno == EINTR) continue;
             PLOG(ERROR) << "epoll_wait";
