@@ -23,9 +23,11 @@ DEFINE_int32(stack_size_normal, 1048576, "size of normal fiber stacks");
 DEFINE_int32(stack_size_large, 8388608, "size of large fiber stacks");
 DEFINE_int32(guard_page_size, 4096, "size of guard page at the bottom of fiber stacks");
 DEFINE_int32(task_group_runqueue_capacity, 4096, "capacity of each worker's run queue");
-DEFINE_int32(fiber_idle_spin_us, 40,
+// Off by default: on the MI355X box (16-CPU quota) idle spinning cost more
+// throughput than it saved latency (profiles/bench_r1_spin_ab.txt).
+DEFINE_int32(fiber_idle_spin_us, 0,
              "an idle worker polls for new fibers this long before sleeping on its parking lot "
-             "(trades a little CPU for futex-wakeup latency on the RPC round trip; 0 disables)");
+             "(trades CPU for futex-wakeup latency on the RPC round trip; 0 disables)");
 DEFINE_int32(fiber_max_spinning_workers, 2, "at most this many idle workers spin at once");
 
 namespace mrpc {

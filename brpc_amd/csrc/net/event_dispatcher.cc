@@ -13,7 +13,7 @@
 #include "fiber/fiber.h"
 
 DEFINE_int32(event_dispatcher_num, 1, "Number of event dispatchers");
-DEFINE_int32(event_dispatcher_spin_us, 50,
+DEFINE_int32(event_dispatcher_spin_us, 0,
              "after handling events, poll epoll without blocking for this long before sleeping (0 disables)");
 
 namespace mrpc {
