@@ -20,6 +20,7 @@
 #include "rpc/protocol.h"
 #include "rpc/server.h"
 #include "rpc/span.h"
+#include "rpc/rpc_dump.h"
 #include "rpc/stream_internal.h"
 #include "rpc/usercode_backup_pool.h"
 
@@ -240,6 +241,16 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
         } else {
             LOG_EVERY_SECOND(WARNING) << "xGMI peer " << socket->remote_side() << " not attached: " << err;
         }
+    }
+    if (SampledRequest* sample = AskToBeSampled()) {
+        sample->meta.set_service_name(rm.service_name());
+        sample->meta.set_method_name(rm.method_name());
+        sample->meta.set_compress_type((CompressType)meta.compress_type());
+        sample->meta.set_protocol_type(PROTOCOL_BAIDU_STD);
+        sample->meta.set_attachment_size(meta.attachment_size());
+        if (meta.has_authentication_data()) sample->meta.set_authentication_data(meta.authentication_data());
+        sample->request = msg->payload;  // shares the blocks
+        sample->submit();
     }
     const int64_t corr = meta.correlation_id();
     MethodStatus* ms = nullptr;

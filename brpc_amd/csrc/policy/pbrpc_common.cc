@@ -8,6 +8,7 @@
 #include "rpc/controller.h"
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
+#include "rpc/rpc_dump.h"
 #include "rpc/span.h"
 #include "rpc/usercode_backup_pool.h"
 
@@ -146,6 +147,19 @@ void RunPbServerCall(PbServerRequest* r, PbResponsePacker packer) {
             cntl->_span->log_id = r->log_id;
             cntl->_trace_id = cntl->_span->trace_id;
             cntl->_span_id = cntl->_span->span_id;
+        }
+    }
+    if (r->mp) {
+        if (SampledRequest* sample = AskToBeSampled()) {
+            sample->meta.set_service_name(r->mp->service->GetDescriptor()->full_name);
+            sample->meta.set_method_name(r->mp->method->name);
+            sample->meta.set_method_index(r->mp->method->index);
+            sample->meta.set_compress_type(r->compress_type);
+            sample->meta.set_protocol_type(r->protocol);
+            sample->meta.set_attachment_size((int32_t)r->attachment.size());
+            sample->request = r->body;
+            sample->request.append(r->attachment);
+            sample->submit();
         }
     }
     ServerCallState* st = new ServerCallState;

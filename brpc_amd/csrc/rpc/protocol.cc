@@ -10,6 +10,7 @@
 #include "rpc/compress.h"
 #include "rpc/errno.h"
 #include "rpc/retry_policy.h"
+#include "rpc/serialized_request.h"
 
 DEFINE_uint64(max_body_size, 64 * 1024 * 1024, "Maximum size of a single message body in all protocols");
 MRPC_VALIDATE_FLAG(max_body_size, ::mrpc::PassValidator);
@@ -104,6 +105,10 @@ bool ParsePbFromString(pb::Message* msg, const std::string& s) {
 }
 
 bool SerializeAsCompressedData(const pb::Message& msg, Buf* buf, CompressType type) {
+    if (const SerializedRequest* sr = dynamic_cast<const SerializedRequest*>(&msg)) {
+        buf->append(sr->serialized_data());  // already encoded with `type`
+        return true;
+    }
     if (type == COMPRESS_TYPE_NONE) return msg.SerializeToBuf(buf);
     Buf raw;
     if (!msg.SerializeToBuf(&raw)) return false;
