@@ -69,6 +69,7 @@ void GlobalInitializeOrDie() {
         policy::RegisterEspProtocol();
         policy::RegisterMongoProtocol();
         policy::RegisterThriftProtocol();
+        policy::RegisterRtmpProtocol();
         for (ProtocolRegistrar r : extra_registrars()) r();
         // Client-side messenger handles responses of every protocol.
         std::vector<std::pair<ProtocolType, Protocol>> protocols;

@@ -25,6 +25,7 @@ class RedisService;
 class NsheadService;
 class ThriftService;
 class MongoServiceAdaptor;
+class RtmpService;
 
 enum ServiceOwnership { SERVER_OWNS_SERVICE, SERVER_DOESNT_OWN_SERVICE };
 
@@ -46,6 +47,7 @@ struct ServerOptions {
     NsheadService* nshead_service = nullptr;
     ThriftService* thrift_service = nullptr;
     MongoServiceAdaptor* mongo_service_adaptor = nullptr;
+    RtmpService* rtmp_service = nullptr;
     HealthReporter* health_reporter = nullptr;
     std::string pid_file;
     // SSL: certificate + private key (PEM paths); enabled when both set.

@@ -1,0 +1,189 @@
+// RTMP: media streaming over one TCP connection (role of the reference's
+// src/brpc/rtmp.h, policy/rtmp_protocol.cpp and rtmp.cpp).
+//
+// Server: set ServerOptions.rtmp_service; every createStream asks the
+// service for a RtmpServerStream that receives play/publish and media
+// callbacks. Client: RtmpClient owns a connection (handshake + connect),
+// RtmpClientStreams multiplex on it (createStream + play/publish).
+//
+// Wire: simple RTMP handshake (C0/C1/C2 - S0/S1/S2), chunk streams with
+// format 0-3 headers, extended timestamps and negotiated chunk sizes, AMF0
+// commands (connect/createStream/play/publish/deleteStream/onStatus),
+// audio/video/data messages. Incoming messages of a connection are
+// dispatched in order on the connection's read fiber.
+//
+// FlvWriter/FlvReader convert between RTMP messages and FLV tags.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <string>
+
+#include "base/buf.h"
+#include "base/endpoint.h"
+#include "rtmp/amf.h"
+
+namespace mrpc {
+
+namespace rtmp_detail {
+class Connection;
+}
+
+enum RtmpMessageType : uint8_t {
+    RTMP_SET_CHUNK_SIZE = 1,
+    RTMP_ABORT = 2,
+    RTMP_ACK = 3,
+    RTMP_USER_CONTROL = 4,
+    RTMP_WINDOW_ACK_SIZE = 5,
+    RTMP_SET_PEER_BANDWIDTH = 6,
+    RTMP_AUDIO = 8,
+    RTMP_VIDEO = 9,
+    RTMP_DATA_AMF0 = 18,
+    RTMP_COMMAND_AMF0 = 20,
+};
+
+struct RtmpAudioMessage {
+    uint32_t timestamp = 0;
+    uint8_t codec = 10;  // 10 = AAC
+    uint8_t rate = 3;    // 44 kHz
+    uint8_t bits = 1;    // 16 bit
+    uint8_t type = 1;    // stereo
+    Buf data;            // payload after the 1-byte audio header
+};
+
+struct RtmpVideoMessage {
+    uint32_t timestamp = 0;
+    uint8_t frame_type = 1;  // 1 key frame, 2 inter frame
+    uint8_t codec = 7;       // 7 = AVC
+    Buf data;                // payload after the 1-byte video header
+};
+
+struct RtmpMetaData {
+    uint32_t timestamp = 0;
+    rtmp::AMFValue data = rtmp::AMFValue::EcmaArray();
+};
+
+class RtmpStreamBase {
+public:
+    virtual ~RtmpStreamBase();
+    // Media callbacks, called in order on the connection's read fiber.
+    virtual void OnMetaData(RtmpMetaData* md, const std::string& name) {}
+    virtual void OnAudioMessage(RtmpAudioMessage* msg) {}
+    virtual void OnVideoMessage(RtmpVideoMessage* msg) {}
+    // The stream ended (deleteStream, connection closed, Destroy()).
+    virtual void OnStop() {}
+
+    int SendMetaData(const RtmpMetaData& md, const std::string& name = "onMetaData");
+    int SendAudioMessage(const RtmpAudioMessage& msg);
+    int SendVideoMessage(const RtmpVideoMessage& msg);
+
+    uint32_t stream_id() const { return _stream_id; }
+    bool is_stopped() const { return _stopped.load(std::memory_order_acquire); }
+    EndPoint remote_side() const;
+
+    // ---- internal
+    int SendMessage(uint8_t type, uint32_t timestamp, const Buf& body);
+    void CallOnStop();
+    std::shared_ptr<rtmp_detail::Connection> _conn;
+    uint32_t _stream_id = 0;
+    std::atomic<bool> _stopped{false};
+};
+
+struct RtmpPlayOptions {
+    std::string stream_name;
+    double start = -2;
+    double duration = -1;
+    bool reset = true;
+};
+
+struct RtmpConnectRequest {
+    std::string app;
+    std::string tcUrl;
+    std::string flashVer;
+};
+
+class RtmpServerStream : public RtmpStreamBase {
+public:
+    // Accept by leaving *error empty, reject by setting it.
+    virtual void OnPlay(const RtmpPlayOptions& opt, std::string* error) {}
+    virtual void OnPublish(const std::string& name, const std::string& type, std::string* error) {}
+};
+
+class RtmpService {
+public:
+    virtual ~RtmpService() {}
+    // A new stream of a connected client; the framework owns the result and
+    // deletes it after OnStop().
+    virtual RtmpServerStream* NewStream(const RtmpConnectRequest& req) = 0;
+};
+
+struct RtmpClientOptions {
+    std::string app = "live";
+    std::string tcUrl;
+    std::string flashVer = "MRPC 1.0";
+    int timeout_ms = 1000;          // connect / createStream / play / publish
+    uint32_t chunk_size = 60000;    // announced with SetChunkSize
+    uint32_t window_ack_size = 2500000;
+};
+
+class RtmpClient {
+public:
+    RtmpClient();
+    ~RtmpClient();
+    // Connects, handshakes and sends `connect`; 0 when the server accepted.
+    int Init(const char* server_addr_and_port, const RtmpClientOptions& options);
+    bool initialized() const { return (bool)_conn; }
+    const RtmpClientOptions& options() const { return _options; }
+    std::shared_ptr<rtmp_detail::Connection> connection() const { return _conn; }
+
+private:
+    RtmpClientOptions _options;
+    std::shared_ptr<rtmp_detail::Connection> _conn;
+};
+
+struct RtmpClientStreamOptions {
+    std::string play_name;      // set one of play_name / publish_name
+    std::string publish_name;
+    std::string publish_type = "live";
+};
+
+class RtmpClientStream : public RtmpStreamBase {
+public:
+    ~RtmpClientStream() override;
+    // createStream + play/publish; returns 0 once the server accepted.
+    int Init(RtmpClient* client, const RtmpClientStreamOptions& options);
+    // deleteStream and detach (OnStop is called). Idempotent.
+    void Destroy();
+};
+
+// FLV container <-> RTMP messages.
+class FlvWriter {
+public:
+    explicit FlvWriter(Buf* out);  // writes the FLV header on the first tag
+    int Write(const RtmpVideoMessage& msg);
+    int Write(const RtmpAudioMessage& msg);
+    int Write(const RtmpMetaData& md, const std::string& name = "onMetaData");
+
+private:
+    int WriteTag(uint8_t type, uint32_t ts, const Buf& body);
+    Buf* _out;
+    bool _wrote_header = false;
+};
+
+class FlvReader {
+public:
+    explicit FlvReader(Buf* in);
+    // 0 and the type of the next tag (8/9/18); EAGAIN when incomplete.
+    int PeekMessageType(uint8_t* type);
+    int Read(RtmpVideoMessage* msg);
+    int Read(RtmpAudioMessage* msg);
+    int Read(RtmpMetaData* md, std::string* name);
+
+private:
+    int ReadTag(uint8_t want, uint32_t* ts, Buf* body);
+    Buf* _in;
+    bool _read_header = false;
+};
+
+}  // namespace mrpc
