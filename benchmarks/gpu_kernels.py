@@ -66,6 +66,31 @@ def main():
                           "Mvalues_per_s": nv / t / 1e6, "verified": ok}))
         del buf, dst, vals, enc
         torch.cuda.empty_cache()
+    # snappy decompression: 2048 blocks x 64 KiB of mixed (~2:1) data
+    from brpc_amd import native
+    from brpc_amd.ops import snappy_decompress
+    import random
+    rnd = random.Random(5)
+    blk = bytearray()
+    while len(blk) < 65536:
+        blk += bytes(rnd.getrandbits(8) for _ in range(24)) if rnd.random() < 0.5 else blk[-64:][:32] or b"x" * 32
+    blk = bytes(blk[:65536])
+    comps = [native.snappy_compress(blk[i:] + blk[:i]) for i in range(0, 2048 * 13, 13)]
+    packed = b"".join(comps)
+    offs, pos = [], 0
+    for c in comps:
+        offs.append(pos)
+        pos += len(c)
+    d = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(dev)
+    sizes = [len(c) for c in comps]
+    outs = [65536] * len(comps)
+    out = torch.empty(65536 * len(comps), dtype=torch.uint8, device=dev)
+    res = snappy_decompress(d, offs, sizes, outs, out=out)
+    ok = bytes(res[:65536].cpu().numpy().tobytes()) == blk
+    t = timeit(lambda: snappy_decompress(d, offs, sizes, outs, out=out), iters=5)
+    nout = 65536 * len(comps)
+    print(json.dumps({"kernel": "snappy_decompress_64KiB_blocks", "blocks": len(comps), "bytes_in": len(packed),
+                      "bytes_out": nout, "sec": t, "GBps_out": nout / t / 1e9, "verified": ok}))
 
 
 if __name__ == "__main__":

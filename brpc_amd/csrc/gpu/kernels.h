@@ -50,6 +50,19 @@ int LaunchVarintDecode(const uint8_t* in, uint64_t n, uint64_t* out, uint64_t ma
 int LaunchVarintEncode(const uint64_t* in, uint64_t n, bool zigzag, uint8_t* out, uint64_t* bytes_dev,
                        void* scratch, hipStream_t s);
 
+// Batched snappy decompression (gpu/snappy_kernels.hip): every job is an
+// independent raw snappy stream of at most kSnappyMaxBlock uncompressed
+// bytes. jobs_dev is a device array; out_len_dev[i] / err_dev[i] receive
+// the decoded size and 0 (or a nonzero malformed-input code) per job.
+constexpr uint32_t kSnappyMaxBlock = 65536;
+struct SnappyJob {
+    const void* src;    // compressed stream (device)
+    void* dst;          // output (device), dst_cap bytes
+    uint64_t src_len;
+    uint64_t dst_cap;
+};
+int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t* out_len_dev, int* err_dev, hipStream_t s);
+
 // ---- synchronous helpers (fiber-friendly waits)
 // CRC32C of device buffers; results to host.
 int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t* out_host, int device);

@@ -54,6 +54,13 @@ void bind_gpu_ops(py::module_& g) {
         for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
         check(gpu::LaunchBatchedCopy(segs.data(), (int)segs.size(), as_stream(stream)), "batched_copy");
     }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("stream") = 0);
+    g.def("snappy_max_block", [] { return gpu::kSnappyMaxBlock; });
+    // jobs: device array of {src, dst, src_len, dst_cap} (4 x u64 per job)
+    g.def("snappy_decompress_launch", [](uintptr_t jobs, int n, uintptr_t out_len, uintptr_t err, uintptr_t stream) {
+        check(gpu::LaunchSnappyDecompress((const gpu::SnappyJob*)jobs, n, (uint32_t*)out_len, (int*)err,
+                                          as_stream(stream)),
+              "snappy_decompress");
+    });
     g.def("varint_scratch_bytes", &gpu::VarintScratchBytes);
     g.def("varint_decode_launch", [](uintptr_t in, uint64_t n, uintptr_t out, uint64_t max_out, bool zigzag,
                                      uintptr_t count, uintptr_t err, uintptr_t scratch, uintptr_t stream) {

@@ -6,6 +6,7 @@
 #include <sstream>
 
 #include "base/crc32c.h"
+#include "base/snappy.h"
 #include "base/flags.h"
 #include "base/logging.h"
 #include "fiber/fiber.h"
@@ -221,6 +222,17 @@ PYBIND11_MODULE(_native, m) {
     m.def("crc32c", [](py::bytes b) {
         std::string s = b;
         return crc32c::Value(s.data(), s.size());
+    });
+    // Host snappy codec (the CPU half; the GPU decompressor is gpu.snappy_*).
+    m.def("snappy_compress", [](py::bytes b) {
+        std::string s = b, out;
+        snappy::Compress(s.data(), s.size(), &out);
+        return py::bytes(out);
+    });
+    m.def("snappy_uncompress", [](py::bytes b) {
+        std::string s = b, out;
+        if (!snappy::Uncompress(s.data(), s.size(), &out)) throw std::invalid_argument("malformed snappy stream");
+        return py::bytes(out);
     });
     m.def("fiber_stats", [] {
         py::dict d;

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU tests + kernel microbench + rocprof kernel summary.
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 300 python benchmarks/gpu_kernels.py > gpurun_out/kernels.log 2>&1 || exit 1
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_kernels" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/gpu_kernels.py" > "$GRAFT_REPO_ROOT/gpurun_out/rocprof_kernels.log" 2>&1
+echo done

@@ -1,0 +1,80 @@
+"""GPU snappy decompression (gpu/snappy_kernels.hip) against the host codec:
+random, highly repetitive (overlapping copies with offset < length), mixed
+and text-like blocks, many blocks per launch, and malformed input."""
+import random
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from brpc_amd import native
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    assert native.gpu.device_count() > 0
+    return torch.device("cuda", 0)
+
+
+def _corpus(kind, n, seed):
+    rnd = random.Random(seed)
+    if kind == "random":
+        return bytes(rnd.getrandbits(8) for _ in range(n))
+    if kind == "runs":  # long runs -> copies with offset 1..4 < length
+        out = bytearray()
+        while len(out) < n:
+            out += bytes([rnd.getrandbits(8)]) * rnd.randint(1, 300)
+        return bytes(out[:n])
+    if kind == "text":
+        words = [b"rpc", b"channel", b"server", b"mi355x", b"xgmi", b"fiber", b"snappy", b"  ", b"\n"]
+        out = bytearray()
+        while len(out) < n:
+            out += rnd.choice(words)
+        return bytes(out[:n])
+    # mixed: repeats of earlier slices at random distances
+    out = bytearray(rnd.getrandbits(8) for _ in range(64))
+    while len(out) < n:
+        if rnd.random() < 0.5:
+            start = rnd.randrange(len(out))
+            out += out[start:start + rnd.randint(4, 200)]
+        else:
+            out += bytes(rnd.getrandbits(8) for _ in range(rnd.randint(1, 40)))
+    return bytes(out[:n])
+
+
+def _run(dev, data, block=65536):
+    from brpc_amd.ops import snappy_compress_blocks, snappy_decompress
+    comp, lens = snappy_compress_blocks(data, block)
+    packed = b"".join(comp)
+    offs, pos = [], 0
+    for c in comp:
+        offs.append(pos)
+        pos += len(c)
+    d = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(dev) if packed else torch.zeros(1, dtype=torch.uint8, device=dev)
+    out = snappy_decompress(d, offs, [len(c) for c in comp], lens)
+    return bytes(out.cpu().numpy().tobytes()) if lens else b""
+
+
+@pytest.mark.parametrize("kind", ["random", "runs", "text", "mixed"])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 65535, 65536, 65537, 300000])
+def test_snappy_decompress_matches_host(dev, kind, n):
+    data = _corpus(kind, n, n * 7 + len(kind))
+    assert _run(dev, data) == data
+
+
+def test_snappy_many_blocks_one_launch(dev):
+    data = _corpus("mixed", 4 << 20, 1)  # 64 blocks of 64 KiB
+    assert _run(dev, data) == data
+    assert _run(dev, data, block=4096) == data  # 1024 small blocks
+
+
+def test_snappy_rejects_malformed(dev):
+    from brpc_amd import native
+    from brpc_amd.ops import snappy_decompress
+    good = native.snappy_compress(b"hello hello hello hello hello")
+    bad = bytearray(good)
+    bad[-1] = 0xFF  # turn the last element into a copy with a bogus offset
+    d = torch.frombuffer(bytearray(bad), dtype=torch.uint8).to(dev)
+    with pytest.raises(ValueError):
+        snappy_decompress(d, [0], [len(bad)], [29])
