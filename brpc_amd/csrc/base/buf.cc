@@ -126,6 +126,7 @@ void SetBlockMemAllocator(const BlockMemAllocator& a) {
 }
 const BlockMemAllocator& GetBlockMemAllocator() { return g_alloc; }
 void SetDeviceCopyHook(DeviceCopyFn fn) { g_devcopy = fn; }
+DeviceCopyFn GetDeviceCopyHook() { return g_devcopy; }
 
 void BufBlock::dec_ref() {
     if (nshared.fetch_sub(1, std::memory_order_acq_rel) != 1) return;

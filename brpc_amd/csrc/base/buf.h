@@ -50,6 +50,7 @@ const BlockMemAllocator& GetBlockMemAllocator();
 // (dst_host, src_device, n) -> 0 on success.
 using DeviceCopyFn = int (*)(void* dst, const void* src, size_t n, MemKind src_kind, int device);
 void SetDeviceCopyHook(DeviceCopyFn fn);
+DeviceCopyFn GetDeviceCopyHook();
 
 struct BufBlock {
     std::atomic<int32_t> nshared;

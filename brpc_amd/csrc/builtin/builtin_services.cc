@@ -23,6 +23,7 @@
 #include "fiber/fiber.h"
 #include "fiber/sync.h"
 #include "gpu/gpu.h"
+#include "rdma/rdma.h"
 #include "http/http_header.h"
 #include "mrpc/proto/builtin_service.pb.h"
 #include "net/socket.h"
@@ -83,7 +84,7 @@ public:
             {"sockets", "socket details"},       {"protobufs", "message types"},   {"hotspots/cpu", "cpu profile"},
             {"hotspots/contention", "lock contention"}, {"pprof/profile", "pprof cpu profile"},
             {"brpc_metrics", "prometheus metrics"}, {"memory", "memory usage"},   {"gpu", "MI355X devices"},
-            {"dir", "file browser (opt-in)"}};
+            {"rdma", "RDMA provider and block pool"}, {"dir", "file browser (opt-in)"}};
         for (auto& p : pages) os << "<a href=\"/" << p[0] << "\">/" << p[0] << "</a>  " << p[1] << "\n";
         os << "\nservices:\n";
         std::vector<const Server::MethodProperty*> mps;
@@ -574,12 +575,20 @@ public:
     }
 };
 
+class RdmaImpl : public rdma {
+public:
+    void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
+        ClosureGuard g(done);
+        text(C(c), mrpc::rdma::DescribeRdma());
+    }
+};
+
 int AddBuiltinServices(Server* server) {
     Service* svcs[] = {new IndexImpl,   new StatusImpl,   new VarsImpl,     new FlagsImpl,   new ConnectionsImpl,
                        new RpczImpl,    new HealthImpl,   new VersionImpl,  new ListImpl,    new ThreadsImpl,
                        new VlogImpl,    new FibersImpl,   new IdsImpl,      new SocketsImpl, new ProtobufsImpl,
                        new HotspotsImpl, new PprofImpl,   new DirImpl,      new MetricsImpl, new MemoryImpl,
-                       new GpuImpl};
+                       new GpuImpl,     new RdmaImpl};
     for (Service* s : svcs) {
         if (server->AddBuiltinService(s) != 0) {
             LOG(ERROR) << "Fail to add builtin service " << s->GetDescriptor()->full_name;

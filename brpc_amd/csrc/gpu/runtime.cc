@@ -14,6 +14,7 @@
 #include "base/logging.h"
 #include "fiber/butex.h"
 #include "fiber/fiber.h"
+#include "rdma/rdma.h"
 
 DEFINE_int32(gpu_streams_per_device, 4, "HIP streams per device in the pool (<= GPU_MAX_HW_QUEUES)");
 DEFINE_int32(gpu_poller_spin_us, 20, "event poller busy-polls this long before backing off");
@@ -169,6 +170,22 @@ int CurrentDevice() {
     return d;
 }
 
+// GPUDirect RDMA: export an HBM range as a dmabuf fd for ibv_reg_dmabuf_mr.
+int dmabuf_export_hook(void* p, size_t n, int gpu, int* fd, uint64_t* offset) {
+    (void)gpu;
+    const uintptr_t page = 4096;
+    const uintptr_t base = reinterpret_cast<uintptr_t>(p) & ~(page - 1);
+    const size_t len = ((reinterpret_cast<uintptr_t>(p) + n + page - 1) & ~(page - 1)) - base;
+    int h = -1;
+    if (hipMemGetHandleForAddressRange(&h, reinterpret_cast<hipDeviceptr_t>(base), len,
+                                       hipMemRangeHandleTypeDmaBufFd, 0) != hipSuccess) {
+        return -1;
+    }
+    *fd = h;
+    *offset = reinterpret_cast<uintptr_t>(p) - base;
+    return 0;
+}
+
 int Init(int device, std::string* error) {
     device = check_device(device);
     if (device < 0) {
@@ -189,6 +206,7 @@ int Init(int device, std::string* error) {
         hipSetDevice(prev);
         st.ok = st.streams.empty() ? 0 : 1;
         SetDeviceCopyHook(copy_hook);
+        rdma::SetDmabufExportHook(dmabuf_export_hook);
     });
     if (!st.ok) {
         if (error) *error = "fail to initialise HIP device " + std::to_string(device);

@@ -62,6 +62,7 @@ void Acceptor::OnNewConnections(Socket* listened) {
         SocketOptions opt;
         opt.fd = fd;
         opt.ssl_ctx = am->_ssl_ctx;
+        if (am->_rdma) opt.rdma = SocketOptions::RDMA_SERVER;
         get_remote_side(fd, &opt.remote_side);
         SocketId sid;
         if (am->Create(opt, &sid) != 0) {

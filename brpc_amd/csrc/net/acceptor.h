@@ -24,6 +24,8 @@ public:
     bool accepting() const { return _listened_sid != INVALID_SOCKET_ID; }
     // Accepted connections detect TLS on their first bytes.
     void set_ssl_ctx(std::shared_ptr<SslContext> ctx) { _ssl_ctx = std::move(ctx); }
+    // Accepted connections detect an RDMA hello on their first bytes.
+    void set_rdma(bool on) { _rdma = on; }
 
 private:
     static void OnNewConnections(Socket* listened);
@@ -36,6 +38,7 @@ private:
     fiber::fiber_t _idle_tid;
     std::atomic<bool> _stop;
     std::shared_ptr<SslContext> _ssl_ctx;
+    bool _rdma = false;
 };
 
 }  // namespace mrpc

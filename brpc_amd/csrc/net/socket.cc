@@ -1,4 +1,5 @@
 #include "net/socket.h"
+#include "rdma/rdma.h"
 
 #include <fcntl.h>
 #include <netinet/tcp.h>
@@ -145,6 +146,9 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
         m->_ssl.reset();
     }
     m->_ssl_state.store(!opt.ssl_ctx ? SSL_OFF : (opt.ssl_ctx->is_server() ? SSL_UNKNOWN : SSL_ON));
+    m->_rdma_mode = opt.rdma;
+    m->InstallRdmaEndpoint(nullptr);
+    m->_rdma_state.store(opt.rdma == SocketOptions::RDMA_SERVER && !opt.ssl_ctx ? RDMA_UNKNOWN : RDMA_OFF);
     m->_health_check_interval_s = opt.health_check_interval_s;
     m->_connect_lazily = opt.connect_lazily;
     m->_nevent.store(0, std::memory_order_relaxed);
@@ -304,6 +308,7 @@ int Socket::SetFailed(int error_code, const char* fmt, ...) {
     _epollout_butex->fetch_add(1, std::memory_order_release);
     fiber::butex_wake_all(_epollout_butex);
     if (tr) tr->OnSocketFailed(this);
+    if (rdma::Endpoint* ep = rdma_endpoint()) ep->Shutdown();
     // Fail every RPC waiting for a response on this socket.
     std::vector<fiber::CallId> ids;
     std::vector<std::function<void()>> cbs;
@@ -353,6 +358,8 @@ void Socket::OnRecycle() {
     }
     _conn.reset();
     _ssl_ctx.reset();
+    InstallRdmaEndpoint(nullptr);
+    _rdma_state.store(RDMA_OFF);
     // pooled sub sockets of a main socket are released with it
     if (_shared) {
         std::vector<SocketId> pool;
@@ -417,6 +424,7 @@ ssize_t Socket::DoRead(size_t size_hint) {
         errno = EBADF;
         return -1;
     }
+    if (_rdma_state.load(std::memory_order_acquire) != RDMA_OFF) return RdmaRead(fd, size_hint);
     if (_ssl_state.load(std::memory_order_acquire) != SSL_OFF) return SslRead(fd, size_hint);
     ssize_t n = _read_buf.append_from_fd(fd, size_hint);
     if (n > 0) {
@@ -426,7 +434,66 @@ ssize_t Socket::DoRead(size_t size_hint) {
     return n;
 }
 
+void Socket::InstallRdmaEndpoint(std::shared_ptr<rdma::Endpoint> ep) {
+    std::lock_guard<std::mutex> g(_mu);
+    _rdma_ep_raw.store(ep.get(), std::memory_order_release);
+    _rdma_ep = std::move(ep);
+}
+
+ssize_t Socket::RdmaRead(int fd, size_t size_hint) {
+    if (_rdma_state.load(std::memory_order_acquire) == RDMA_UNKNOWN) {
+        // Server side, first bytes: an RDMA hello or a plain TCP client.
+        const ssize_t n = _read_buf.append_from_fd(fd, size_hint);
+        if (n <= 0) return n;
+        in_bytes.fetch_add(n, std::memory_order_relaxed);
+        _last_active_us.store(monotonic_us(), std::memory_order_relaxed);
+        std::shared_ptr<rdma::Endpoint> ep;
+        std::string err;
+        const int rc = rdma::ServerTryHandshake(_this_id, fd, &_read_buf, &ep, &err);
+        if (rc == 0) {
+            errno = EAGAIN;  // hello incomplete: hide it from the parsers
+            return -1;
+        }
+        if (rc < 0) {
+            if (!err.empty()) {
+                LOG(WARNING) << "RDMA handshake with " << _remote_side << " failed: " << err;
+                errno = ERDMA;
+                return -1;
+            }
+            _rdma_state.store(RDMA_OFF, std::memory_order_release);
+            return n;
+        }
+        InstallRdmaEndpoint(std::move(ep));
+        _rdma_state.store(RDMA_ON, std::memory_order_release);
+        errno = EAGAIN;
+        return -1;
+    }
+    rdma::Endpoint* ep = rdma_endpoint();
+    const ssize_t n = ep ? ep->ReadInto(&_read_buf) : -1;
+    if (n > 0) {
+        in_bytes.fetch_add(n, std::memory_order_relaxed);
+        _last_active_us.store(monotonic_us(), std::memory_order_relaxed);
+        return n;
+    }
+    // Nothing from the verbs side: the idle TCP connection tells us whether
+    // the peer went away.
+    char c;
+    const ssize_t r = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+    if (r == 0) return 0;
+    if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return -1;
+    errno = EAGAIN;
+    return -1;
+}
+
 ssize_t Socket::WriteList(int fd, Buf** list, size_t n) {
+    if (_rdma_state.load(std::memory_order_acquire) == RDMA_ON) {
+        rdma::Endpoint* ep = rdma_endpoint();
+        if (!ep) {
+            errno = EPIPE;
+            return -1;
+        }
+        return ep->CutFromBufList(list, n);
+    }
     if (_conn) return _conn->CutMessageIntoFileDescriptor(fd, list, n);
     if (_ssl_state.load(std::memory_order_acquire) == SSL_ON) {
         std::shared_ptr<SslSession> ssl = ssl_session();
@@ -558,6 +625,20 @@ int Socket::ConnectIfNot(const timespec* abstime, WriteRequest*) {
             errno = err;
             return -1;
         }
+    }
+    if (_rdma_mode == SocketOptions::RDMA_CLIENT) {
+        // Hello exchange before the fd joins the dispatcher, so the reply is
+        // read here and not by the input messenger.
+        std::string err;
+        std::shared_ptr<rdma::Endpoint> ep = rdma::ClientHandshake(_this_id, fd, abstime, &err);
+        if (!ep) {
+            LOG(WARNING) << "RDMA handshake with " << _remote_side << " failed: " << err;
+            fiber::close_fd(fd);
+            errno = ERDMA;
+            return -1;
+        }
+        InstallRdmaEndpoint(std::move(ep));
+        _rdma_state.store(RDMA_ON, std::memory_order_release);
     }
     // Another writer can't race here: only the head writer connects.
     if (ResetFileDescriptor(fd) != 0) {
@@ -714,7 +795,8 @@ int Socket::StartWrite(WriteRequest* req, const WriteOptions& opt) {
     }
     if (!opt.write_in_background) {
         const int fd = _fd.load(std::memory_order_acquire);
-        if (_conn || _ssl_state.load(std::memory_order_relaxed) == SSL_ON) {
+        if (_conn || _ssl_state.load(std::memory_order_relaxed) == SSL_ON ||
+            _rdma_state.load(std::memory_order_relaxed) == RDMA_ON) {
             Buf* list[1] = {&req->data};
             nw = WriteList(fd, list, 1);
         } else {
@@ -784,6 +866,15 @@ void* Socket::KeepWrite(void* arg) {
                 break;
             }
             timespec ts = realtime_after_us(50000);
+            if (rdma::Endpoint* ep = s->is_rdma() ? s->rdma_endpoint() : nullptr) {
+                // verbs window / send queue full: park until completions free it
+                if (ep->WaitWritable(&ts) != 0 && errno != ETIMEDOUT) {
+                    const int saved_errno = errno ? errno : EFAILEDSOCKET;
+                    s->SetFailed(saved_errno, "fail to wait rdma window: %s", ErrorText(saved_errno));
+                    break;
+                }
+                continue;
+            }
             const int fd = s->fd();
             if (fd < 0 || s->WaitEpollOut(fd, s->_on_edge_triggered_events != nullptr, &ts) != 0) {
                 if (errno != ETIMEDOUT && errno != EWOULDBLOCK && errno != EINTR) {
@@ -908,6 +999,10 @@ int Socket::Revive(int new_fd) {
             _ssl.reset();
         }
         if (_ssl_ctx) _ssl_state.store(_ssl_ctx->is_server() ? SSL_UNKNOWN : SSL_ON);
+        if (_rdma_mode != SocketOptions::RDMA_NONE) {
+            InstallRdmaEndpoint(nullptr);
+            _rdma_state.store(_rdma_mode == SocketOptions::RDMA_SERVER ? RDMA_UNKNOWN : RDMA_OFF);
+        }
         delete _parsing_context.exchange(nullptr);
         {
             std::lock_guard<std::mutex> g(_pipeline_mu);
@@ -942,6 +1037,11 @@ void* Socket::HealthCheckThread(void* arg) {
                 ::close(fd);
                 break;
             }
+            if (s->_rdma_mode == SocketOptions::RDMA_CLIENT) {
+                // reconnect (with a fresh hello exchange) on the next write
+                ::close(fd);
+                fd = -1;
+            }
             s->Revive(fd);
             return nullptr;  // keep the creator reference: socket alive again
         }
@@ -961,8 +1061,10 @@ void Socket::StartHealthCheck() {
 }
 
 std::string Socket::description() const {
-    return string_printf("Socket{id=%llu fd=%d remote=%s nref=%u%s}", (unsigned long long)_this_id, fd(),
-                         _remote_side.to_string().c_str(), nref(), Failed() ? " failed" : "");
+    return string_printf("Socket{id=%llu fd=%d remote=%s nref=%u%s%s%s}", (unsigned long long)_this_id, fd(),
+                         _remote_side.to_string().c_str(), nref(), Failed() ? " failed" : "",
+                         is_ssl() ? " tls" : "",
+                         is_rdma() && rdma_endpoint() ? (" " + rdma_endpoint()->Describe()).c_str() : "");
 }
 
 std::string DescribeAllSockets() {

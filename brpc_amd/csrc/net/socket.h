@@ -31,6 +31,9 @@
 #include "net/ssl.h"
 
 namespace mrpc {
+namespace rdma {
+class Endpoint;
+}
 
 typedef uint64_t SocketId;
 const SocketId INVALID_SOCKET_ID = (SocketId)-1;
@@ -100,6 +103,11 @@ struct SocketOptions {
     // a client context makes it start a TLS session after connecting.
     std::shared_ptr<SslContext> ssl_ctx;
     std::string ssl_sni;
+    // RDMA (rdma/rdma.h): RDMA_CLIENT exchanges hellos right after connect
+    // and then moves every byte over verbs; RDMA_SERVER detects the hello on
+    // the first bytes of an accepted connection (plain TCP clients still work).
+    enum { RDMA_NONE = 0, RDMA_CLIENT = 1, RDMA_SERVER = 2 };
+    int rdma = RDMA_NONE;
 };
 
 struct WriteOptions {
@@ -196,6 +204,9 @@ public:
     // TLS state (nullptr when the connection is plaintext).
     std::shared_ptr<SslSession> ssl_session() const;
     bool is_ssl() const { return _ssl_state.load(std::memory_order_acquire) == SSL_ON; }
+    // RDMA data plane (nullptr when the connection is plain TCP).
+    bool is_rdma() const { return _rdma_state.load(std::memory_order_acquire) == RDMA_ON; }
+    rdma::Endpoint* rdma_endpoint() const { return _rdma_ep_raw.load(std::memory_order_acquire); }
 
     // Callbacks run once when the socket fails (streams multiplexed on it).
     void AddFailureCallback(std::function<void()> cb);
@@ -273,6 +284,14 @@ private:
     std::string _ssl_sni;
     std::shared_ptr<SslSession> _ssl;
     std::atomic<int> _ssl_state{SSL_OFF};
+    // RDMA
+    enum { RDMA_OFF = 0, RDMA_UNKNOWN = 1, RDMA_ON = 2 };
+    ssize_t RdmaRead(int fd, size_t size_hint);
+    void InstallRdmaEndpoint(std::shared_ptr<rdma::Endpoint> ep);
+    int _rdma_mode = 0;
+    std::atomic<int> _rdma_state{RDMA_OFF};
+    std::shared_ptr<rdma::Endpoint> _rdma_ep;  // guarded by _mu
+    std::atomic<rdma::Endpoint*> _rdma_ep_raw{nullptr};
 };
 
 // Dump /connections-style info of all live sockets.

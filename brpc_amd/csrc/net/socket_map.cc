@@ -52,6 +52,7 @@ int SocketMapInsert(const SocketMapKey& key, SocketId* id) {
         opt.ssl_ctx = SslContext::DefaultClient();
         if (!opt.ssl_ctx) return -1;
     }
+    if (key.signature.find("|rdma") != std::string::npos) opt.rdma = SocketOptions::RDMA_CLIENT;
     SocketId sid;
     if (get_client_side_messenger()->Create(opt, &sid) != 0) return -1;
     sm.m[key] = Entry{sid, 1};

@@ -129,6 +129,7 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
     ChannelOptions copt;
     copt.protocol = _opt.protocol;
     copt.connection_type = _opt.connection_type;
+    copt.use_rdma = _opt.use_rdma;
     copt.timeout_ms = _opt.timeout_ms;
     copt.connect_timeout_ms = _opt.connect_timeout_ms;
     copt.max_retry = _opt.max_retry;

@@ -52,6 +52,7 @@ struct PressOptions {
     bool device_attachment = false;  // attachment lives in HBM (needs GPU)
     int gpu_device = -1;
     bool check_echo = false;   // verify the echoed payload
+    bool use_rdma = false;     // verbs data plane (server needs use_rdma too)
     // generic workload (dynamic messages)
     std::string proto_file;    // .proto path
     std::string include_paths; // ';' separated

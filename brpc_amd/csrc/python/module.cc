@@ -38,11 +38,12 @@ public:
             if (_server.AddService(_echo.get(), SERVER_DOESNT_OWN_SERVICE) != 0) throw std::runtime_error("AddService failed");
         }
     }
-    int start(const std::string& addr, int num_threads, int gpu_device, int idle_timeout_s) {
+    int start(const std::string& addr, int num_threads, int gpu_device, int idle_timeout_s, bool use_rdma) {
         ServerOptions opt;
         opt.num_threads = num_threads;
         opt.gpu_device = gpu_device;
         opt.idle_timeout_sec = idle_timeout_s;
+        opt.use_rdma = use_rdma;
         int rc;
         {
             py::gil_scoped_release nogil;
@@ -129,6 +130,7 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "device_attachment") o.device_attachment = v.cast<bool>();
         else if (k == "gpu_device") o.gpu_device = v.cast<int>();
         else if (k == "check_echo") o.check_echo = v.cast<bool>();
+        else if (k == "use_rdma") o.use_rdma = v.cast<bool>();
         else if (k == "proto_file") o.proto_file = v.cast<std::string>();
         else if (k == "include_paths") o.include_paths = v.cast<std::string>();
         else if (k == "method") o.method = v.cast<std::string>();
@@ -247,7 +249,7 @@ PYBIND11_MODULE(_native, m) {
         .def(py::init<>())
         .def("add_echo_service", &PyServer::add_echo_service)
         .def("start", &PyServer::start, py::arg("addr"), py::arg("num_threads") = -1, py::arg("gpu_device") = -1,
-             py::arg("idle_timeout_s") = -1)
+             py::arg("idle_timeout_s") = -1, py::arg("use_rdma") = false)
         .def("stop", &PyServer::stop)
         .def_property_readonly("port", &PyServer::port)
         .def_property_readonly("address", &PyServer::address)

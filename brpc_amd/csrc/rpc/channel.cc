@@ -8,6 +8,7 @@
 #include "cluster/lb_with_naming.h"
 #include "fiber/fiber.h"
 #include "gpu/xgmi.h"
+#include "rdma/rdma.h"
 #include "net/socket_map.h"
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
@@ -67,9 +68,21 @@ int Channel::InitChannelOptions(const ChannelOptions* options) {
                                                                                           : CONNECTION_TYPE_POOLED;
     }
     // "ssl:<sni>" in the signature makes SocketMap create TLS client sockets.
-    _map_signature = string_printf("%s|%s|%s|%d", _protocol->name, _options.connection_group.c_str(),
+    _map_signature = string_printf("%s|%s|%s|%d%s", _protocol->name, _options.connection_group.c_str(),
                                    _options.use_ssl ? ("ssl:" + _options.ssl_sni).c_str() : "",
-                                   _options.use_device_transport ? _options.gpu_device : -2);
+                                   _options.use_device_transport ? _options.gpu_device : -2,
+                                   _options.use_rdma ? "|rdma" : "");
+    if (_options.use_rdma) {
+        std::string err;
+        if (_options.use_ssl) {
+            LOG(ERROR) << "use_rdma and use_ssl are exclusive";
+            return -1;
+        }
+        if (rdma::GlobalRdmaInitialize(&err) != 0) {
+            LOG(ERROR) << "Fail to initialise RDMA: " << err;
+            return -1;
+        }
+    }
     if (_options.use_device_transport) {
         std::string err;
         if (gpu::EnableXgmiTransport(_options.gpu_device, &err) != 0) {

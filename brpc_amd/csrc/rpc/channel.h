@@ -40,6 +40,9 @@ struct ChannelOptions {
     // SSL: verify nothing, just encrypt when true (ChannelSSLOptions analog)
     bool use_ssl = false;
     std::string ssl_sni;
+    // Move every byte of the connection over RDMA verbs after a TCP hello
+    // exchange (rdma/rdma.h); the server must enable ServerOptions.use_rdma.
+    bool use_rdma = false;
 };
 
 class ChannelBase : public RpcChannel {

@@ -14,6 +14,7 @@
 #include "gpu/xgmi.h"
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
+#include "rdma/rdma.h"
 #include "var/var.h"
 
 DEFINE_bool(reuse_addr, true, "SO_REUSEADDR on listening sockets");
@@ -332,6 +333,16 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
             return -1;
         }
         _am->set_ssl_ctx(ctx);  // TLS and plaintext clients share the port
+    }
+    if (_am && _options.use_rdma) {
+        std::string err;
+        if (!_options.ssl_cert_file.empty() || rdma::GlobalRdmaInitialize(&err) != 0) {
+            LOG(ERROR) << "Fail to enable RDMA: " << (err.empty() ? "exclusive with TLS" : err);
+            ::close(fd);
+            _status = UNINITIALIZED;
+            return -1;
+        }
+        _am->set_rdma(true);
     }
     if (!_am || _am->StartAccept(fd, _options.idle_timeout_sec) != 0) {
         ::close(fd);

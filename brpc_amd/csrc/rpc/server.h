@@ -55,6 +55,9 @@ struct ServerOptions {
     std::string ssl_key_file;
     std::string ssl_ciphers;  // OpenSSL cipher list (empty: library default)
     std::string ssl_alpns;    // e.g. "h2,http/1.1"
+    // Accept RDMA clients (hello detected per connection; TCP clients keep
+    // working on the same port). Exclusive with TLS.
+    bool use_rdma = false;
     // MI355X: device ordinal the server's GPU services run on (-1 = none).
     int gpu_device = -1;
 };

@@ -33,6 +33,7 @@ DEFINE_int32(duration, 0, "seconds to run (0: until killed)");
 DEFINE_double(qps, 0, "target qps (0: closed loop as fast as possible)");
 DEFINE_int32(channels, 1, "independent channels (connections)");
 DEFINE_bool(check, false, "verify echoed payloads");
+DEFINE_bool(use_rdma, false, "move the connection onto RDMA verbs (server needs -use_rdma as well)");
 
 int main(int argc, char** argv) {
     mrpc::ParseCommandLineFlags(&argc, &argv);
@@ -43,6 +44,7 @@ int main(int argc, char** argv) {
     o.lb_policy = FLAGS_lb_policy;
     o.protocol = FLAGS_protocol;
     o.connection_type = FLAGS_connection_type;
+    o.use_rdma = FLAGS_use_rdma;
     o.timeout_ms = FLAGS_timeout_ms;
     o.connect_timeout_ms = FLAGS_connection_timeout_ms;
     o.max_retry = FLAGS_max_retry;

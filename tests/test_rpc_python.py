@@ -1,5 +1,8 @@
 """Python-facing RPC surface: Server/Channel/Press over loopback."""
 import pytest
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_echo_roundtrip(native, echo_server):
@@ -86,3 +89,33 @@ def test_flags_and_vars(native, echo_server):
     v = dump_vars("*")
     assert len(v) > 10
     assert "rpc" in native.dump_prometheus() or len(native.dump_prometheus()) > 0
+
+
+def test_press_over_rdma_soft_provider():
+    """rdma_performance-style closed loop over the RDMA data plane (soft verbs
+    provider: no HCA here). Runs in a child process because enabling RDMA swaps
+    the process-wide Buf block allocator to the registered pool."""
+    import subprocess
+    import sys
+    code = r'''
+import json, sys
+sys.path.insert(0, %r)
+from brpc_amd import native
+s = native.Server(); s.add_echo_service(); s.start("127.0.0.1:0", use_rdma=True)
+out = {}
+for att in (0, 1024, 65536, 1 << 20):
+    p = native.Press({"server": s.address, "concurrency": 8, "attachment_size": att, "use_rdma": True,
+                      "check_echo": True, "timeout_ms": 5000})
+    p.run_requests(400 if att < (1 << 20) else 40)
+    st = p.stats()
+    out[att] = [st["success"], st["error"]]
+s.stop()
+print(json.dumps(out))
+''' % (ROOT,)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    for att, (ok, err) in res.items():
+        assert err == 0, (att, res)
+        assert ok == (400 if int(att) < (1 << 20) else 40), (att, res)
