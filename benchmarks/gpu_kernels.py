@@ -66,32 +66,77 @@ def main():
                           "Mvalues_per_s": nv / t / 1e6, "verified": ok}))
         del buf, dst, vals, enc
         torch.cuda.empty_cache()
-    # snappy decompression: 2048 blocks x 64 KiB of mixed (~2:1) data
+    # snappy: 128 MiB of mixed (~2:1) data as 2048 x 64 KiB and 4096 x 32 KiB
+    # blocks. "sec" is kernel time only (CUDA events around launches with the
+    # job tables already on the device); the python wrappers add host work.
     from brpc_amd import native
-    from brpc_amd.ops import snappy_decompress
+    from brpc_amd.ops import snappy_compress, snappy_decompress
+    from brpc_amd.ops._common import stream_handle
     import random
     rnd = random.Random(5)
-    blk = bytearray()
-    while len(blk) < 65536:
-        blk += bytes(rnd.getrandbits(8) for _ in range(24)) if rnd.random() < 0.5 else blk[-64:][:32] or b"x" * 32
-    blk = bytes(blk[:65536])
-    comps = [native.snappy_compress(blk[i:] + blk[:i]) for i in range(0, 2048 * 13, 13)]
-    packed = b"".join(comps)
-    offs, pos = [], 0
-    for c in comps:
-        offs.append(pos)
-        pos += len(c)
-    d = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(dev)
-    sizes = [len(c) for c in comps]
-    outs = [65536] * len(comps)
-    out = torch.empty(65536 * len(comps), dtype=torch.uint8, device=dev)
-    res = snappy_decompress(d, offs, sizes, outs, out=out)
-    ok = bytes(res[:65536].cpu().numpy().tobytes()) == blk
-    t = timeit(lambda: snappy_decompress(d, offs, sizes, outs, out=out), iters=5)
-    nout = 65536 * len(comps)
-    print(json.dumps({"kernel": "snappy_decompress_64KiB_blocks", "blocks": len(comps), "bytes_in": len(packed),
-                      "bytes_out": nout, "sec": t, "GBps_out": nout / t / 1e9, "verified": ok}))
+    base = bytearray()
+    while len(base) < 65536:
+        base += bytes(rnd.getrandbits(8) for _ in range(24)) if rnd.random() < 0.5 else base[-64:][:32] or b"x" * 32
+    base = bytes(base[:65536])
+    total = 128 << 20
+    raw = b"".join(base[i:] + base[:i] for i in range(0, (total // 65536) * 13, 13))
+    raw_dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
 
+    def kernel_time(fn, iters=10):
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / iters
+
+    for block in (65536, 32768):
+        n = total // block
+        # host codec blocks -> device decompression
+        comps = [native.snappy_compress(raw[i * block:(i + 1) * block]) for i in range(n)]
+        packed = b"".join(comps)
+        offs, pos = [], 0
+        for c in comps:
+            offs.append(pos)
+            pos += len(c)
+        d = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to(dev)
+        out = torch.empty(total, dtype=torch.uint8, device=dev)
+        res = snappy_decompress(d, offs, [len(c) for c in comps], [block] * n, out=out)
+        ok = bool(torch.equal(res, raw_dev))
+        jobs = []
+        for i, c in enumerate(comps):
+            jobs += [d.data_ptr() + offs[i], out.data_ptr() + i * block, len(c), block]
+        jobs_dev = torch.tensor(jobs, dtype=torch.int64, device=dev)
+        meta = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+        st = stream_handle(dev)
+        t = kernel_time(lambda: native.gpu.snappy_decompress_launch(jobs_dev.data_ptr(), n, block, meta.data_ptr(),
+                                                                    meta.data_ptr() + 4 * n, st))
+        print(json.dumps({"kernel": "snappy_decompress", "block": block, "blocks": n, "bytes_in": len(packed),
+                          "bytes_out": total, "sec": t, "GBps_out": total / t / 1e9, "verified": ok}))
+        # device compression -> host + device decompression checks
+        gp, goffs, gsizes, graw = snappy_compress(raw_dev, block=block)
+        host = gp.cpu().numpy().tobytes()
+        ok_host = all(native.snappy_uncompress(host[o:o + s]) == raw[i * block:(i + 1) * block]
+                      for i, (o, s) in enumerate(zip(goffs[:64], gsizes[:64])))
+        back = snappy_decompress(gp, goffs, gsizes, graw)
+        ok_dev = bool(torch.equal(back, raw_dev))
+        cap = (int(native.gpu.snappy_max_compressed_length(block)) + 15) & ~15
+        slots = torch.empty(n * cap, dtype=torch.uint8, device=dev)
+        scratch = torch.empty(n * int(native.gpu.snappy_compress_scratch_per_block()), dtype=torch.uint8, device=dev)
+        cj = []
+        for i in range(n):
+            cj += [raw_dev.data_ptr() + i * block, slots.data_ptr() + i * cap, block, cap]
+        cj_dev = torch.tensor(cj, dtype=torch.int64, device=dev)
+        t = kernel_time(lambda: native.gpu.snappy_compress_launch(cj_dev.data_ptr(), n, scratch.data_ptr(),
+                                                                  meta.data_ptr(), meta.data_ptr() + 4 * n, st))
+        print(json.dumps({"kernel": "snappy_compress", "block": block, "blocks": n, "bytes_in": total,
+                          "bytes_out": int(sum(gsizes)), "host_codec_bytes_out": len(packed), "sec": t,
+                          "GBps_in": total / t / 1e9, "verified_host_decode": ok_host, "verified_gpu_decode": ok_dev}))
+        del d, out, jobs_dev, slots, scratch, cj_dev, gp, back
+        torch.cuda.empty_cache()
 
 if __name__ == "__main__":
     main()

@@ -61,7 +61,19 @@ struct SnappyJob {
     uint64_t src_len;
     uint64_t dst_cap;
 };
-int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t* out_len_dev, int* err_dev, hipStream_t s);
+// max_ulen (>= every job's uncompressed size) sizes the LDS per wave: 32 KiB
+// blocks run 5 waves per CU, 64 KiB blocks 2.
+int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, uint32_t* out_len_dev, int* err_dev,
+                           hipStream_t s);
+// Batched snappy compression: job.src = raw block (<= kSnappyMaxBlock),
+// job.dst = output with job.dst_cap >= SnappyMaxCompressedLength(src_len).
+// scratch: n * SnappyCompressScratchPerBlock() bytes of device memory.
+// out_len_dev[i] = compressed size, err_dev[i] = 0 or an error code.
+constexpr uint32_t SnappyCompressSlot() { return ((kSnappyMaxBlock / 64) + 32 + 63) & ~63u; }
+constexpr uint64_t SnappyCompressScratchPerBlock() { return 64ull * SnappyCompressSlot(); }
+constexpr uint64_t SnappyMaxCompressedLength(uint64_t n) { return 32 + n + n / 6; }
+int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, void* scratch, uint32_t* out_len_dev, int* err_dev,
+                         hipStream_t s);
 
 // ---- synchronous helpers (fiber-friendly waits)
 // CRC32C of device buffers; results to host.

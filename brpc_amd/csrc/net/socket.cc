@@ -34,7 +34,15 @@ struct Socket::WriteRequest {
     WriteRequest* next = nullptr;
     fiber::CallId id_wait = fiber::INVALID_CALL_ID;
     Socket* socket = nullptr;
+    bool shutdown_after = false;  // half-close the connection once written
 };
+
+// A fully written request: honor WriteOptions.shutdown_write_after (the
+// http server's "Connection: close"). Earlier requests were written before.
+static void finish_write_request(Socket::WriteRequest* r, int fd) {
+    if (r->shutdown_after && fd >= 0) ::shutdown(fd, SHUT_WR);
+    return_object(r);
+}
 
 static Socket::WriteRequest* const UNCONNECTED = (Socket::WriteRequest*)(intptr_t)-1;
 
@@ -725,6 +733,7 @@ int Socket::Write(Buf* data, const WriteOptions* options) {
     req->next = UNCONNECTED;
     req->id_wait = opt.id_wait;
     req->socket = this;
+    req->shutdown_after = opt.shutdown_write_after;
     if (opt.id_wait != fiber::INVALID_CALL_ID) {
         std::lock_guard<std::mutex> g(_shared->mu);
         auto& v = _shared->id_wait_list;
@@ -815,7 +824,7 @@ int Socket::StartWrite(WriteRequest* req, const WriteOptions& opt) {
             out_bytes.fetch_add(nw, std::memory_order_relaxed);
         }
         if (IsWriteComplete(req, true, nullptr)) {
-            return_object(req);
+            finish_write_request(req, this->fd());
             return 0;
         }
     }
@@ -846,7 +855,7 @@ void* Socket::KeepWrite(void* arg) {
         if (req->next != nullptr && req->data.empty()) {
             WriteRequest* saved = req;
             req = req->next;
-            return_object(saved);
+            finish_write_request(saved, s->fd());
         }
         if (s->Failed()) break;
         const ssize_t nw = s->DoWrite(req);
@@ -889,14 +898,14 @@ void* Socket::KeepWrite(void* arg) {
         while (req->next != nullptr && req->data.empty()) {
             WriteRequest* saved = req;
             req = req->next;
-            return_object(saved);
+            finish_write_request(saved, s->fd());
         }
         if (cur_tail == nullptr) {
             for (cur_tail = req; cur_tail->next != nullptr; cur_tail = cur_tail->next) {
             }
         }
         if (s->IsWriteComplete(cur_tail, req == cur_tail, &cur_tail)) {
-            return_object(req);
+            finish_write_request(req, s->fd());
             return nullptr;
         }
     }

@@ -115,6 +115,8 @@ struct WriteOptions {
     int abstime_ms = 0;
     bool ignore_eovercrowded = false;
     bool write_in_background = false;
+    // Half-close (shutdown SHUT_WR) once this write is fully on the wire.
+    bool shutdown_write_after = false;
     // >0: the protocol answers requests in order without correlation ids
     // (http/1.1, redis, memcache). The socket remembers (count, id_wait) in
     // write order so the parser can map the next response(s) to the call.

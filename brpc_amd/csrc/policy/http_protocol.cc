@@ -272,6 +272,7 @@ static void SendHttpResponse(Controller* cntl, pb::Message* req, pb::Message* re
     if (cntl->http_request().method() != HTTP_METHOD_HEAD) packet.append(std::move(body));
     WriteOptions wopt;
     wopt.ignore_eovercrowded = true;
+    wopt.shutdown_write_after = !keep_alive;  // "Connection: close" / HTTP/1.0
     sock->Write(&packet, &wopt);
     if (cntl->_progressive_attachment) {
         cntl->_progressive_attachment->MarkRPCAsDone(cntl->Failed());
@@ -324,6 +325,7 @@ void ProcessHttpRequest(InputMessageBase* msg_base) {
         if (path.empty() || path == "/") path = "/index";
         std::string unresolved;
         mp = server->FindMethodPropertyByURI(path, &unresolved);
+        if (!mp && (mp = server->master_method_property()) != nullptr) unresolved = path.substr(1);
         if (!mp) {
             cntl->SetFailed(ENOMETHOD, "Fail to find method on `%s'", req_h.uri().path().c_str());
             break;

@@ -56,10 +56,19 @@ void bind_gpu_ops(py::module_& g) {
     }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("stream") = 0);
     g.def("snappy_max_block", [] { return gpu::kSnappyMaxBlock; });
     // jobs: device array of {src, dst, src_len, dst_cap} (4 x u64 per job)
-    g.def("snappy_decompress_launch", [](uintptr_t jobs, int n, uintptr_t out_len, uintptr_t err, uintptr_t stream) {
-        check(gpu::LaunchSnappyDecompress((const gpu::SnappyJob*)jobs, n, (uint32_t*)out_len, (int*)err,
+    g.def("snappy_decompress_launch", [](uintptr_t jobs, int n, uint32_t max_ulen, uintptr_t out_len, uintptr_t err,
+                                         uintptr_t stream) {
+        check(gpu::LaunchSnappyDecompress((const gpu::SnappyJob*)jobs, n, max_ulen, (uint32_t*)out_len, (int*)err,
                                           as_stream(stream)),
               "snappy_decompress");
+    });
+    g.def("snappy_compress_scratch_per_block", [] { return gpu::SnappyCompressScratchPerBlock(); });
+    g.def("snappy_max_compressed_length", [](uint64_t n) { return gpu::SnappyMaxCompressedLength(n); });
+    g.def("snappy_compress_launch", [](uintptr_t jobs, int n, uintptr_t scratch, uintptr_t out_len, uintptr_t err,
+                                       uintptr_t stream) {
+        check(gpu::LaunchSnappyCompress((const gpu::SnappyJob*)jobs, n, (void*)scratch, (uint32_t*)out_len,
+                                        (int*)err, as_stream(stream)),
+              "snappy_compress");
     });
     g.def("varint_scratch_bytes", &gpu::VarintScratchBytes);
     g.def("varint_decode_launch", [](uintptr_t in, uint64_t n, uintptr_t out, uint64_t max_out, bool zigzag,

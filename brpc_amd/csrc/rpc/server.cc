@@ -15,6 +15,7 @@
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
 #include "rdma/rdma.h"
+#include "rpc/trackme.h"
 #include "var/var.h"
 
 DEFINE_bool(reuse_addr, true, "SO_REUSEADDR on listening sockets");
@@ -295,6 +296,20 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
             LOG(WARNING) << "xGMI device transport unavailable on device " << _options.gpu_device << ": " << err;
         }
     }
+    _master_mp = nullptr;
+    if (Service* master = _options.http_master_service) {
+        // Every http request no service/restful mapping claims goes to the
+        // master service's first method (tools/rpc_view proxies this way).
+        const std::string& sname = master->GetDescriptor()->full_name;
+        if (!FindServiceByFullName(sname) && AddService(master, SERVER_DOESNT_OWN_SERVICE) != 0) {
+            LOG(ERROR) << "Fail to add http_master_service " << sname;
+            _status = UNINITIALIZED;
+            return -1;
+        }
+        if (!master->GetDescriptor()->methods.empty()) {
+            _master_mp = FindMethodPropertyByFullName(sname, master->GetDescriptor()->methods[0].name);
+        }
+    }
     _amc = _options.max_concurrency;
     _cl.reset(CreateConcurrencyLimiter(_amc));
     if (_options.session_local_data_factory && !_keytable_pool) _keytable_pool = fiber::keytable_pool_create();
@@ -375,6 +390,7 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
         }
     }
     LOG(INFO) << "Server is serving on " << _listen_addr;
+    SetTrackMeAddress(_listen_addr);
     return 0;
 }
 

@@ -95,6 +95,8 @@ public:
     const MethodProperty* FindMethodPropertyByFullName(const std::string& service_full_name,
                                                        const std::string& method_name) const;
     const MethodProperty* FindMethodPropertyByFullName(const std::string& full_method_name) const;
+    // ServerOptions.http_master_service's method (nullptr when unset).
+    const MethodProperty* master_method_property() const { return _master_mp; }
     // restful lookup: returns property and fills unresolved path
     const MethodProperty* FindMethodPropertyByURI(const std::string& path, std::string* unresolved) const;
     size_t service_count() const;
@@ -152,6 +154,7 @@ private:
     Service* _first_service = nullptr;
     std::unordered_map<std::string, MethodProperty> _methods;  // "svc.Method"
     std::vector<std::pair<std::string, std::string>> _restful;  // prefix -> full method name
+    const MethodProperty* _master_mp = nullptr;
     std::atomic<int> _concurrency{0};
     std::unique_ptr<ConcurrencyLimiter> _cl;
     AdaptiveMaxConcurrency _amc;

@@ -182,6 +182,9 @@ TEST(Legacy, raw_nshead_pipelined_on_single_connection) {
         ch.CallMethod(nullptr, cntls[i].get(), &reqs[i], &ress[i], NewCallback([&done_n] { done_n.fetch_add(1); }));
     }
     for (int i = 0; i < N; ++i) cntls[i]->Join();
+    // Join() returns once the call id is gone; an async done may still be
+    // running (the reference destroys the id before done->Run as well).
+    for (int spin = 0; spin < 2000 && done_n.load() != N; ++spin) usleep(1000);
     EXPECT_EQ(done_n.load(), N);
     for (int i = 0; i < N; ++i) {
         if (cntls[i]->Failed()) fprintf(stderr, "nshead call %d: %s\n", i, cntls[i]->ErrorText().c_str());

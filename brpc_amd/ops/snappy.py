@@ -1,8 +1,9 @@
-"""Batched snappy decompression on the GPU (``gpu/snappy_kernels.hip``):
-the device half of the snappy body codec. Each input is an independent
-raw snappy stream of at most 64 KiB uncompressed (``snappy_compress_blocks``
-produces exactly that framing on the host); one wave64 workgroup rebuilds
-one block in LDS and streams it to HBM."""
+"""Batched snappy compression and decompression on the GPU
+(``gpu/snappy_kernels.hip``): the device half of the snappy body codec.
+Each block is an independent raw snappy stream of at most 64 KiB
+uncompressed (``snappy_compress_blocks`` produces that framing on the host,
+``snappy_compress`` on the device); one wave64 workgroup owns one block.
+Both directions interoperate with the host codec (``native.snappy_*``)."""
 import torch
 
 from ..native import native
@@ -55,9 +56,10 @@ def snappy_decompress(packed, offsets, sizes, out_sizes, out=None):
         pos += int(u)
     jobs_dev = torch.tensor(jobs, dtype=torch.int64).to(dev)
     meta = torch.zeros(2 * max(n, 1), dtype=torch.int32, device=dev)  # [out_len..., err...]
+    max_ulen = max([int(u) for u in out_sizes] + [1])
     with torch.cuda.device(dev):
-        native.gpu.snappy_decompress_launch(jobs_dev.data_ptr(), n, meta.data_ptr(), meta.data_ptr() + 4 * n,
-                                            stream_handle(dev))
+        native.gpu.snappy_decompress_launch(jobs_dev.data_ptr(), n, max_ulen, meta.data_ptr(),
+                                            meta.data_ptr() + 4 * n, stream_handle(dev))
     m = meta.cpu().tolist()
     errs = m[n:2 * n]
     if any(errs):
@@ -66,3 +68,48 @@ def snappy_decompress(packed, offsets, sizes, out_sizes, out=None):
     if m[:n] != [int(u) for u in out_sizes]:
         raise ValueError("decoded sizes differ from the expected sizes")
     return out[:total]
+
+
+def snappy_compress(data, block=MAX_BLOCK, compact=True):
+    """Compress a uint8 device tensor on the GPU as independent snappy blocks
+    of ``block`` bytes (the last one may be shorter), one launch for all.
+
+    Returns (packed, offsets, comp_sizes, raw_sizes): ``packed`` is a uint8
+    device tensor holding the compressed blocks back to back when ``compact``
+    (else in fixed-stride slots), ready for ``snappy_decompress``; every block
+    also decodes with the host codec."""
+    require_gpu_tensor(data, "data")
+    if data.dtype != torch.uint8:
+        raise TypeError("data must be uint8")
+    if not 0 < block <= MAX_BLOCK:
+        raise ValueError("block must be in (0, %d]" % MAX_BLOCK)
+    dev = data.device
+    total = data.numel()
+    raw = [min(block, total - o) for o in range(0, total, block)]
+    n = len(raw)
+    if n == 0:
+        return torch.zeros(0, dtype=torch.uint8, device=dev), [], [], []
+    cap = (int(native.gpu.snappy_max_compressed_length(block)) + 15) & ~15
+    slots = torch.empty(n * cap, dtype=torch.uint8, device=dev)
+    scratch = torch.empty(n * int(native.gpu.snappy_compress_scratch_per_block()), dtype=torch.uint8, device=dev)
+    base_in, base_out = data.data_ptr(), slots.data_ptr()
+    jobs = []
+    for i, r in enumerate(raw):
+        jobs += [base_in + i * block, base_out + i * cap, r, cap]
+    jobs_dev = torch.tensor(jobs, dtype=torch.int64).to(dev)
+    meta = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        native.gpu.snappy_compress_launch(jobs_dev.data_ptr(), n, scratch.data_ptr(), meta.data_ptr(),
+                                          meta.data_ptr() + 4 * n, stream_handle(dev))
+    m = meta.cpu().tolist()
+    if any(m[n:]):
+        raise RuntimeError("snappy_compress failed for blocks %s" % [i for i, e in enumerate(m[n:]) if e][:8])
+    sizes = m[:n]
+    if not compact:
+        return slots, [i * cap for i in range(n)], sizes, raw
+    packed = torch.cat([slots[i * cap:i * cap + sz] for i, sz in enumerate(sizes)])
+    offs, pos = [], 0
+    for sz in sizes:
+        offs.append(pos)
+        pos += sz
+    return packed, offs, sizes, raw

@@ -78,3 +78,34 @@ def test_snappy_rejects_malformed(dev):
     d = torch.frombuffer(bytearray(bad), dtype=torch.uint8).to(dev)
     with pytest.raises(ValueError):
         snappy_decompress(d, [0], [len(bad)], [29])
+
+
+@pytest.mark.parametrize("kind", ["random", "runs", "text", "mixed"])
+@pytest.mark.parametrize("n", [1, 3, 4, 63, 64, 65, 1000, 65536, 300001])
+def test_gpu_compress_round_trips_through_host_and_gpu(dev, kind, n):
+    from brpc_amd import native
+    from brpc_amd.ops import snappy_compress, snappy_decompress
+    data = _corpus(kind, n, n * 11 + len(kind))
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    packed, offs, sizes, raw = snappy_compress(t)
+    host = packed.cpu().numpy().tobytes()
+    # every device-compressed block is a valid snappy stream for the host codec
+    back = b"".join(native.snappy_uncompress(host[o:o + s]) for o, s in zip(offs, sizes))
+    assert back == data
+    # and for the device decompressor
+    out = snappy_decompress(packed, offs, sizes, raw)
+    assert out.cpu().numpy().tobytes() == data
+    if kind != "random" and n >= 65536:
+        # within 15% of the host codec's output (matches across lane segments work)
+        host_size = sum(len(native.snappy_compress(data[o:o + 65536])) for o in range(0, n, 65536))
+        assert sum(sizes) <= host_size * 1.15, (sum(sizes), host_size)
+
+
+def test_gpu_compress_32k_blocks_and_uncompacted_slots(dev):
+    from brpc_amd.ops import snappy_compress, snappy_decompress
+    data = _corpus("mixed", 3 << 20, 5)
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    slots, offs, sizes, raw = snappy_compress(t, block=32768, compact=False)
+    assert len(sizes) == 96 and all(r == 32768 for r in raw)
+    out = snappy_decompress(slots, offs, sizes, raw)
+    assert out.cpu().numpy().tobytes() == data

@@ -1,0 +1,106 @@
+"""Command-line tools as subprocesses (role of the reference's tools/):
+trackme_server receiving reports from a server started with
+-trackme_server, rpc_view relaying a target's builtin pages, parallel_http
+fetching many urls concurrently."""
+import os
+import socket
+import subprocess
+import time
+import urllib.request
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "build", "bin")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _wait_port(port, timeout=10):
+    end = time.time() + timeout
+    while time.time() < end:
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.2).close()
+            return
+        except OSError:
+            time.sleep(0.05)
+    raise RuntimeError("port %d never opened" % port)
+
+
+@pytest.fixture
+def procs():
+    started = []
+    yield started
+    for p in started:
+        p.terminate()
+        try:
+            p.wait(timeout=5)
+        except subprocess.TimeoutExpired:
+            p.kill()
+
+
+def _spawn(procs, args):
+    p = subprocess.Popen(args, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, cwd="/tmp")
+    procs.append(p)
+    return p
+
+
+def _get(url):
+    with urllib.request.urlopen(url, timeout=5) as r:
+        return r.status, r.read().decode()
+
+
+def test_trackme_reports_and_bug_verdicts(procs, tmp_path):
+    tport, sport = _free_port(), _free_port()
+    bugs = tmp_path / "bugs.txt"
+    bugs.write_text("# versions 10000..19999 have a known bug\n10000 19999 warning upgrade me please\n")
+    tm = _spawn(procs, [os.path.join(BIN, "trackme_server"), "-port=%d" % tport, "-bug_file=%s" % bugs])
+    _wait_port(tport)
+    srv = _spawn(procs, [os.path.join(BIN, "echo_server"), "-port=%d" % sport,
+                         "-trackme_server=127.0.0.1:%d" % tport, "-trackme_interval=1"])
+    _wait_port(sport)
+    time.sleep(2.5)
+    srv.terminate()
+    out_srv = srv.communicate(timeout=10)[0]
+    tm.terminate()
+    out_tm = tm.communicate(timeout=10)[0]
+    assert "new reporter 0.0.0.0:%d" % sport in out_tm, out_tm
+    assert "upgrade me please" in out_srv, out_srv  # the verdict reached the reporting server
+
+
+def test_rpc_view_relays_builtin_pages(procs):
+    sport, vport = _free_port(), _free_port()
+    _spawn(procs, [os.path.join(BIN, "echo_server"), "-port=%d" % sport])
+    _wait_port(sport)
+    _spawn(procs, [os.path.join(BIN, "rpc_view"), "-port=%d" % vport, "-target=127.0.0.1:%d" % sport])
+    _wait_port(vport)
+    st, body = _get("http://127.0.0.1:%d/status" % vport)
+    assert st == 200 and "EchoService" in body, body[:500]
+    st, body = _get("http://127.0.0.1:%d/flags?name=port" % vport)
+    assert st == 200 and "port" in body
+    st, direct = _get("http://127.0.0.1:%d/version" % sport)
+    st2, viewed = _get("http://127.0.0.1:%d/version" % vport)
+    assert st2 == 200 and viewed == direct
+    with pytest.raises(urllib.error.HTTPError):
+        _get("http://127.0.0.1:%d/no_such_page_xyz" % vport)
+
+
+def test_parallel_http(procs, tmp_path):
+    sport = _free_port()
+    _spawn(procs, [os.path.join(BIN, "echo_server"), "-port=%d" % sport])
+    _wait_port(sport)
+    urls = tmp_path / "urls.txt"
+    pages = ["status", "vars", "flags", "version", "health", "connections"]
+    urls.write_text("".join("http://127.0.0.1:%d/%s\n" % (sport, p) for p in pages * 20))
+    r = subprocess.run([os.path.join(BIN, "parallel_http"), "-url_file=%s" % urls, "-thread_num=16"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "fetched 120 urls" in r.stdout and "failed=0" in r.stdout
+    lines = [l for l in r.stdout.splitlines() if l.startswith("200 ")]
+    assert len(lines) == 120
