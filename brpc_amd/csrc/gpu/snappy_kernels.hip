@@ -26,8 +26,7 @@
 // Compression splits a block into 64 contiguous segments, one per lane; each
 // lane runs a greedy hash matcher with snappy's skip heuristic over
 // incompressible runs and emits literal / copy elements into its own scratch
-// slot. Candidates come from two LDS tables of (position, fingerprint)
-// entries: a 128-entry table per lane
+// slot. Candidates come from two LDS tables: a 128-entry u16 table per lane
 // (the most recent position in its own segment: short offsets, copy-1 form)
 // and a block-wide 4096-entry table holding the EARLIEST position of every
 // hash, filled by all lanes with ds_min before matching starts — the
@@ -37,7 +36,10 @@
 // concatenation of the 64 slots (placed by a prefix sum behind the varint
 // header, copied out coalesced) is a valid snappy stream any decoder
 // accepts; its size lands within ~10% of the CPU codec's on repetitive
-// data. 48 KiB of LDS per wave: 3 waves per CU.
+// data. 32 KiB of LDS per wave: 5 waves per CU. (A/B on the MI355X: 32-bit
+// (position, fingerprint) entries that skip most verification loads ran
+// slower — 48 KiB/wave drops to 3 waves per CU; a double-buffered window
+// prefetch in the decompressor also lost to the single re-centred window.)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -91,12 +93,8 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
     const SnappyJob job = jobs[blk];
     gbyte_c* in = as_global(job.src);
     const uint32_t in_len = (uint32_t)job.src_len;
-    // Two 256-byte windows at fixed 256-byte steps: w0 = [wbase, wbase+256),
-    // w1 = the next 256 bytes, loaded one step ahead so its latency hides
-    // behind the elements of w0.
     uint32_t wbase = 0;
     uint32_t win = load_window(in, in_len, 0, lane);
-    uint32_t win1 = load_window(in, in_len, kWindow, lane);
     // uncompressed length (varint, <= 5 bytes; all inside the first window)
     uint32_t ulen = 0, ip = 0;
     int bad = 0;
@@ -112,18 +110,11 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
     if (!bad && (ulen > lds_cap || ulen > job.dst_cap)) bad = 2;
     uint32_t op = 0;
     while (!bad && ip < in_len) {
-        if (ip >= wbase + kWindow) {
-            if (ip < wbase + 2 * kWindow) {
-                wbase += kWindow;
-                win = win1;
-            } else {  // jumped past both windows (long literal)
-                wbase = ip & ~(kWindow - 1);
-                win = load_window(in, in_len, wbase, lane);
-            }
-            win1 = load_window(in, in_len, wbase + kWindow, lane);
+        if (ip + 5 > wbase + kWindow) {  // tag + up to 4 extra bytes must be in the window
+            wbase = ip & ~3u;
+            win = load_window(in, in_len, wbase, lane);
         }
-        // tag + up to 4 extra bytes lie in [wbase, wbase + 2 * kWindow)
-#define WBYTE(q) ((q) < kWindow ? window_byte(win, (q)) : window_byte(win1, (q) - kWindow))
+#define WBYTE(q) window_byte(win, (q))
         const uint32_t tag = window_byte(win, ip - wbase);
         ++ip;
         const uint32_t kind = tag & 3;
@@ -144,15 +135,12 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
                 bad = 4;
                 break;
             }
-            if (ip + len <= wbase + 2 * kWindow) {
-                // short literal: lanes gather bytes from the VGPR windows
+            if (ip + len <= wbase + kWindow) {
+                // short literal: lanes gather bytes from the VGPR window
                 for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
                     const uint32_t j = j0 + (uint32_t)lane;
                     const uint32_t q = ip - wbase + j;
-                    const int src = (int)((q >> 2) & 63) << 2;
-                    const uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)win);
-                    const uint32_t d1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)win1);
-                    const uint32_t d = q < kWindow ? d0 : d1;
+                    const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q >> 2) & 63) << 2, (int)win);
                     if (j < len) buf[op + j] = (uint8_t)(d >> ((q & 3) * 8));
                 }
             } else {
@@ -224,10 +212,7 @@ constexpr int kHashBits = 7;  // per-lane table
 constexpr int kHashEntries = 1 << kHashBits;
 constexpr int kFirstBits = 12;  // block-wide earliest-position table
 constexpr int kFirstEntries = 1 << kFirstBits;
-constexpr uint32_t kNoEntry = 0xFFFFFFFFu;
-// Table entries are (position << 16) | 16-bit fingerprint of the 4 bytes, so
-// most false candidates are rejected without touching HBM.
-__device__ __forceinline__ uint32_t fingerprint(uint32_t v) { return (v ^ (v >> 16)) & 0xFFFF; }
+constexpr uint16_t kNoPos = 0xFFFF;
 __device__ __forceinline__ uint64_t load64(gbyte_c* p) {
     typedef uint64_t __attribute__((aligned(1))) u64_unaligned;
     return *reinterpret_cast<const __attribute__((address_space(1))) u64_unaligned*>(p);
@@ -279,7 +264,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
                                                                 uint8_t* __restrict__ scratch,
                                                                 uint32_t* __restrict__ out_len,
                                                                 int* __restrict__ err) {
-    __shared__ uint32_t table[kWave * kHashEntries];
+    __shared__ uint16_t table[kWave * kHashEntries];
     __shared__ uint32_t first_pos[kFirstEntries];
     __shared__ uint32_t sizes[kWave];
     const int blk = blockIdx.x;
@@ -296,7 +281,8 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         return;
     }
     {
-        for (int i = lane; i < kWave * kHashEntries; i += kWave) table[i] = kNoEntry;
+        uint32_t* t = reinterpret_cast<uint32_t*>(table);
+        for (int i = lane; i < kWave * kHashEntries / 2; i += kWave) t[i] = 0xFFFFFFFFu;
         for (int i = lane; i < kFirstEntries; i += kWave) first_pos[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
@@ -304,27 +290,23 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
     const uint32_t s = min(ulen, seg * (uint32_t)lane);
     const uint32_t e = min(ulen, s + seg);
     for (uint32_t q = s; q < e && q + 4 <= ulen; ++q) {
-        const uint32_t v = load32(in + q);
-        atomicMin(&first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)], (q << 16) | fingerprint(v));
+        atomicMin(&first_pos[(load32(in + q) * 0x1e35a7bdu) >> (32 - kFirstBits)], q);
     }
     __syncthreads();
     gbyte* const slot =
         as_global(scratch + (size_t)blk * SnappyCompressScratchPerBlock() + (size_t)lane * SnappyCompressSlot());
-    uint32_t* ht = table + lane * kHashEntries;
+    uint16_t* ht = table + lane * kHashEntries;
     gbyte* o = slot;
     uint32_t p = s, lit = s;
     while (p + 4 <= e) {
         const uint32_t v = load32(in + p);
         const uint32_t h = (v * 0x1e35a7bdu) >> (32 - kHashBits);
-        const uint32_t fp = fingerprint(v);
-        uint32_t ent = ht[h];
-        ht[h] = (p << 16) | fp;
-        uint32_t cand = ent >> 16;
-        bool hit = ent != kNoEntry && (ent & 0xFFFF) == fp && load32(in + cand) == v;
+        uint32_t cand = ht[h];
+        ht[h] = (uint16_t)p;
+        bool hit = cand != kNoPos && load32(in + cand) == v;
         if (!hit) {
-            ent = first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)];
-            cand = ent >> 16;
-            hit = ent != kNoEntry && cand < p && (ent & 0xFFFF) == fp && load32(in + cand) == v;
+            cand = first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)];
+            hit = cand < p && load32(in + cand) == v;
         }
         if (hit) {
             uint32_t len = 4;
