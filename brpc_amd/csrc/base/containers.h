@@ -5,6 +5,10 @@
 // and an intrusive doubly linked list.
 #pragma once
 
+#include <unordered_map>
+
+#include <list>
+
 #include <algorithm>
 #include <atomic>
 #include <cctype>
@@ -291,6 +295,66 @@ struct LinkNode {
         next->prev = prev;
         prev = next = this;
     }
+};
+
+// Most-recently-used cache with a fixed capacity: Put/Get move the entry
+// to the front, inserting past capacity evicts the least recently used
+// (reference butil/containers/mru_cache.h). Not thread-safe.
+template <typename K, typename V, typename Hash = std::hash<K>>
+class MRUCache {
+public:
+    explicit MRUCache(size_t capacity) : _cap(capacity ? capacity : 1) {}
+    // Insert or overwrite; returns true if an old entry was evicted.
+    bool Put(const K& k, V v, K* evicted_key = nullptr) {
+        auto it = _index.find(k);
+        if (it != _index.end()) {
+            it->second->second = std::move(v);
+            _order.splice(_order.begin(), _order, it->second);
+            return false;
+        }
+        _order.emplace_front(k, std::move(v));
+        _index[k] = _order.begin();
+        if (_order.size() <= _cap) return false;
+        if (evicted_key) *evicted_key = _order.back().first;
+        _index.erase(_order.back().first);
+        _order.pop_back();
+        return true;
+    }
+    // Pointer to the value (refreshes recency), nullptr if absent.
+    V* Get(const K& k) {
+        auto it = _index.find(k);
+        if (it == _index.end()) return nullptr;
+        _order.splice(_order.begin(), _order, it->second);
+        return &it->second->second;
+    }
+    // Lookup without touching recency.
+    const V* Peek(const K& k) const {
+        auto it = _index.find(k);
+        return it == _index.end() ? nullptr : &it->second->second;
+    }
+    bool Erase(const K& k) {
+        auto it = _index.find(k);
+        if (it == _index.end()) return false;
+        _order.erase(it->second);
+        _index.erase(it);
+        return true;
+    }
+    size_t size() const { return _order.size(); }
+    size_t capacity() const { return _cap; }
+    void clear() {
+        _order.clear();
+        _index.clear();
+    }
+    // Iterate from most to least recently used.
+    template <typename Fn>
+    void for_each(Fn fn) const {
+        for (const auto& kv : _order) fn(kv.first, kv.second);
+    }
+
+private:
+    size_t _cap;
+    std::list<std::pair<K, V>> _order;
+    std::unordered_map<K, typename std::list<std::pair<K, V>>::iterator, Hash> _index;
 };
 
 }  // namespace mrpc

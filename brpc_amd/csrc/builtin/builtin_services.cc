@@ -319,7 +319,8 @@ public:
         os << "live fibers: " << fiber::fiber_count() << "\n";
         os << "context switches: " << fiber::switch_count() << "\n";
         os << "steals: " << fiber::steal_count() << "\n";
-        os << "worker usage: " << fiber::worker_usage() << "\n";
+        os << "worker usage: " << fiber::worker_usage() << "\n\n";
+        os << fiber::DescribeFibers(200);
         text(C(c), os.str());
     }
 };

@@ -8,6 +8,8 @@
 // stubs, socket IO and HIP stream completions interleave on few cores.
 #pragma once
 
+#include <string>
+
 #include <time.h>
 
 #include <cstdint>
@@ -108,6 +110,8 @@ int close_fd(int fd);
 
 // ---- stats
 int64_t fiber_count();
+// One line per live fiber: tid, entry, arg, saved sp, stack, age (/fibers, gdb).
+std::string DescribeFibers(size_t max_lines = 200);
 int64_t switch_count();
 int64_t steal_count();
 double worker_usage();  // in worker-equivalents

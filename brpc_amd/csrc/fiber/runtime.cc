@@ -870,6 +870,22 @@ int get_concurrency() {
 static std::atomic<bool> g_about_to_quit{false};
 void about_to_quit() { g_about_to_quit.store(true); }
 
+std::string DescribeFibers(size_t max_lines) {
+    std::string out;
+    size_t n = 0;
+    const int64_t now = monotonic_ns();
+    ResourcePool<TaskMeta>::singleton()->for_each([&](uint32_t, TaskMeta* m) {
+        if (n >= max_lines || !m->version_butex || m->is_main || !m->fn) return;
+        if ((uint32_t)m->version_butex->load(std::memory_order_acquire) != tid_version(m->tid)) return;
+        ++n;
+        char line[160];
+        snprintf(line, sizeof(line), "tid=%llu fn=%p arg=%p sp=%p stack=%p age_ms=%lld\n", (unsigned long long)m->tid,
+                 (void*)m->fn, m->arg, m->sp, (void*)m->stack, (long long)((now - m->start_ns) / 1000000));
+        out += line;
+    });
+    return out;
+}
+
 int64_t fiber_count() {
     TaskControl* c = get_task_control();
     return c ? c->nfibers.load(std::memory_order_relaxed) : 0;
@@ -924,3 +940,12 @@ int timer_del(TimerId id) {
 
 }  // namespace fiber
 }  // namespace mrpc
+
+// For debuggers (tools/gdb_fiber_stack.py): `call mrpc_fiber_dump()` returns
+// the live fibers with their saved stack pointers, which the gdb commands
+// turn back into frames (see fiber/context.cc for the saved layout).
+extern "C" const char* mrpc_fiber_dump() {
+    static std::string* s = new std::string;
+    *s = mrpc::fiber::DescribeFibers(100000);
+    return s->c_str();
+}

@@ -12,6 +12,8 @@
 #include "base/crc32c.h"
 #include "base/endpoint.h"
 #include "base/flags.h"
+#include "base/time.h"
+#include "rpc/periodic_task.h"
 #include "base/pool.h"
 #include "base/util.h"
 #include "tests/test.h"
@@ -237,4 +239,46 @@ TEST(ResourcePool, get_put_address) {
     bool reused = false;
     for (int i = 0; i < 100; ++i) reused |= (ids[i] == id);
     EXPECT_TRUE(reused);
+}
+
+TEST(Base, mru_cache_evicts_least_recent) {
+    mrpc::MRUCache<std::string, int> c(3);
+    c.Put("a", 1);
+    c.Put("b", 2);
+    c.Put("c", 3);
+    ASSERT_TRUE(c.Get("a") != nullptr);  // a becomes most recent
+    std::string ev;
+    EXPECT_TRUE(c.Put("d", 4, &ev));
+    EXPECT_EQ(ev, "b");
+    EXPECT_TRUE(c.Peek("b") == nullptr);
+    EXPECT_EQ(*c.Get("a"), 1);
+    EXPECT_FALSE(c.Put("a", 10));
+    EXPECT_EQ(*c.Peek("a"), 10);
+    std::vector<std::string> order;
+    c.for_each([&](const std::string& k, int) { order.push_back(k); });
+    EXPECT_EQ(order.size(), 3u);
+    EXPECT_EQ(order[0], "a");
+    EXPECT_TRUE(c.Erase("c"));
+    EXPECT_EQ(c.size(), 2u);
+}
+
+namespace {
+struct CountingTask : public mrpc::PeriodicTask {
+    std::atomic<int> runs{0};
+    std::atomic<bool> destroyed{false};
+    bool OnTriggeringTask(timespec* next) override {
+        if (++runs >= 5) return false;
+        *next = mrpc::realtime_after_us(2000);
+        return true;
+    }
+    void OnDestroyingTask() override { destroyed = true; }
+};
+}  // namespace
+
+TEST(Base, periodic_task_runs_until_it_stops) {
+    CountingTask t;
+    mrpc::PeriodicTaskManager::StartTaskAt(&t, mrpc::realtime_after_us(1000));
+    for (int i = 0; i < 500 && !t.destroyed; ++i) usleep(2000);
+    EXPECT_TRUE(t.destroyed.load());
+    EXPECT_EQ(t.runs.load(), 5);
 }

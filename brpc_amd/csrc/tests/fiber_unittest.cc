@@ -303,3 +303,28 @@ TEST(Fiber, scheduling_latency_and_throughput) {
     EXPECT_EQ(done.load(), N);
     printf("  fiber create+run+join: %.1f ns/fiber\n", (double)dt / N);
 }
+
+extern "C" const char* mrpc_fiber_dump();
+
+namespace {
+void* sleepy_fiber(void*) {
+    mrpc::fiber::usleep(300000);
+    return nullptr;
+}
+}  // namespace
+
+TEST(Fiber, describe_lists_suspended_fibers_for_debuggers) {
+    mrpc::fiber::fiber_t t[3];
+    for (auto& x : t) mrpc::fiber::start_background(&x, nullptr, sleepy_fiber, nullptr);
+    mrpc::fiber::usleep(50000);
+    const std::string d = mrpc::fiber::DescribeFibers(1000);
+    char fn[32];
+    snprintf(fn, sizeof(fn), "fn=%p", (void*)sleepy_fiber);
+    size_t n = 0;
+    for (size_t p = d.find(fn); p != std::string::npos; p = d.find(fn, p + 1)) ++n;
+    EXPECT_EQ(n, 3u);
+    EXPECT_TRUE(d.find("sp=0x") != std::string::npos);
+    EXPECT_TRUE(std::string(mrpc_fiber_dump()).find(fn) != std::string::npos);
+    for (auto& x : t) mrpc::fiber::join(x);
+    EXPECT_TRUE(mrpc::fiber::DescribeFibers(1000).find(fn) == std::string::npos);
+}
