@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--workers", type=int, default=0, help="fiber worker pthreads per rank (0: auto)")
     ap.add_argument("--skip-64k", action="store_true")
+    ap.add_argument("--skip-stream", action="store_true",
+                    help="skip the streaming-RPC leg (64 KiB chunks, BASELINE config 3)")
     ap.add_argument("--device-payload", action="store_true",
                     help="64 KiB leg with HBM-resident attachments")
     ap.add_argument("--latency-sample-s", type=float, default=2.0,
@@ -146,6 +148,25 @@ def main():
         wl64.device_attachment = bool(a.device_payload and cuda)
         r64 = timed_leg(wl64, a.steps, a.warmup)
 
+    # Streaming-RPC leg: each rank pushes 64 KiB chunks through one
+    # flow-controlled stream to its ring peer; a step is 32 chunks (2 MiB)
+    # and ends when the peer acknowledged them.
+    rs = None
+    if not a.skip_stream:
+        sp = native.StreamPress({"server": peer, "chunk_size": 65536, "chunks_per_step": 32})
+        sp.run_steps(a.warmup)
+        parallel.barrier(topo)
+        sync()
+        t0 = time.perf_counter()
+        sp.run_steps(a.steps)
+        parallel.barrier(topo)
+        sync()
+        dt = time.perf_counter() - t0
+        dt_max = parallel.allreduce_max(dt, topo)
+        nbytes = parallel.allreduce_sum(a.steps * 32 * 65536, topo)
+        rs = {"gbps": nbytes / dt_max / 1e9 if dt_max > 0 else 0.0, "ms_per_step": 1000.0 * dt_max / a.steps}
+        sp.close()
+
     lat = None
     if a.latency_sample_s > 0:
         press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
@@ -195,6 +216,9 @@ def main():
             out["vs_baseline_64KB"] = round(r64["qps"] / BASELINE_QPS_32KB, 4)
             out["errors_64KB"] = r64["errors"]
             out["device_payload_64KB"] = bool(a.device_payload and cuda)
+        if rs:
+            out["stream_gbytes_per_s_64KB_chunks"] = round(rs["gbps"], 3)
+            out["stream_ms_per_step"] = round(rs["ms_per_step"], 3)
         if lat:
             out["p99_us_at_100qps"] = lat["p99_us"]
             out["p50_us_at_100qps"] = lat["p50_us"]

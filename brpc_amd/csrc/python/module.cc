@@ -14,6 +14,7 @@
 #include "gpu/xgmi.h"
 #include "mrpc/proto/echo.pb.h"
 #include "press/press.h"
+#include "press/stream_press.h"
 #include "rpc/channel.h"
 #include "rpc/controller.h"
 #include "rpc/protocol.h"
@@ -192,6 +193,56 @@ private:
     press::PressSession _s;
 };
 
+// Streaming-RPC throughput driver (press/stream_press.h).
+class PyStreamPress {
+public:
+    explicit PyStreamPress(const py::dict& d) {
+        GlobalInitializeOrDie();
+        press::StreamPressOptions o;
+        for (auto item : d) {
+            const std::string k = py::str(item.first);
+            py::handle v = item.second;
+            if (k == "server") o.server = v.cast<std::string>();
+            else if (k == "chunk_size") o.chunk_size = v.cast<int>();
+            else if (k == "chunks_per_step") o.chunks_per_step = v.cast<int>();
+            else if (k == "timeout_ms") o.timeout_ms = v.cast<int>();
+            else if (k == "max_buf_size") o.max_buf_size = v.cast<int64_t>();
+            else throw std::invalid_argument("unknown stream press option: " + k);
+        }
+        _s.reset(new press::StreamPress);
+        std::string err;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = _s->Init(o, &err);
+        }
+        if (rc != 0) throw std::runtime_error("stream press init failed: " + err);
+    }
+    void run_steps(int steps) {
+        std::string err;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = _s->RunSteps(steps, &err);
+        }
+        if (rc != 0) throw std::runtime_error(err);
+    }
+    py::dict stats() {
+        py::dict d;
+        d["bytes_sent"] = _s->bytes_sent();
+        d["bytes_acked"] = _s->bytes_acked();
+        d["steps"] = _s->steps_done();
+        return d;
+    }
+    void close() {
+        py::gil_scoped_release nogil;
+        _s.reset();
+    }
+
+private:
+    std::unique_ptr<press::StreamPress> _s;
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -261,6 +312,12 @@ PYBIND11_MODULE(_native, m) {
              py::arg("connection_type") = "", py::arg("timeout_ms") = 1000, py::arg("max_retry") = 3)
         .def("echo", &PyChannel::echo, py::arg("message"), py::arg("attachment") = py::bytes(),
              py::arg("sleep_us") = 0);
+
+    py::class_<PyStreamPress>(m, "StreamPress")
+        .def(py::init<const py::dict&>())
+        .def("run_steps", &PyStreamPress::run_steps)
+        .def("stats", &PyStreamPress::stats)
+        .def("close", &PyStreamPress::close);
 
     py::class_<PyPress>(m, "Press")
         .def(py::init<const py::dict&>())

@@ -99,6 +99,8 @@ public:
 
     // ---------------- results
     bool Failed() const override { return _error_code != 0; }
+    // Server side: the request carries a stream the handler may StreamAccept.
+    bool has_remote_stream() const { return _request_stream != 0; }
     int ErrorCode() const { return _error_code; }
     std::string ErrorText() const override { return _error_text; }
     void SetFailed(const std::string& reason) override;

@@ -1,10 +1,41 @@
 #include "services/echo_service.h"
 
+#include <cstdlib>
+#include <cstring>
+
 #include "fiber/fiber.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
+#include "rpc/stream.h"
 
 namespace mrpc {
+
+namespace {
+// Stream sink of the "stream:<round_bytes>" echo mode (streaming_echo /
+// BASELINE config 3): counts received bytes and writes back the cumulative
+// count (8 bytes, little endian) every round_bytes, so a sender can time
+// rounds end to end. Deletes itself when the stream closes.
+class StreamSink : public StreamInputHandler {
+public:
+    explicit StreamSink(int64_t round) : _round(round > 0 ? round : 1) {}
+    int on_received_messages(StreamId id, Buf* const messages[], size_t n) override {
+        for (size_t i = 0; i < n; ++i) _bytes += (int64_t)messages[i]->size();
+        while (_bytes >= _acked + _round) {
+            _acked += _round;
+            Buf ack;
+            ack.append(&_acked, sizeof(_acked));
+            StreamWrite(id, ack);
+        }
+        return 0;
+    }
+    void on_closed(StreamId) override { delete this; }
+
+private:
+    int64_t _round;
+    int64_t _bytes = 0;
+    int64_t _acked = 0;
+};
+}  // namespace
 
 void (*EchoServiceImpl::device_hook)(RpcController* cntl, example::EchoResponse* response) = nullptr;
 
@@ -21,6 +52,17 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
     if (request->close_fd()) {
         cntl->CloseConnection("close_fd requested");
         return;
+    }
+    if (cntl->has_remote_stream() && request->message().compare(0, 7, "stream:") == 0) {
+        StreamSink* sink = new StreamSink(strtoll(request->message().c_str() + 7, nullptr, 10));
+        StreamOptions so;
+        so.handler = sink;
+        StreamId sid;
+        if (StreamAccept(&sid, *cntl, &so) != 0) {
+            delete sink;
+            cntl->SetFailed(EINTERNAL, "fail to accept the stream");
+            return;
+        }
     }
     response->set_message(request->message());
     response->set_device(-1);

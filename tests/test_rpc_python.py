@@ -119,3 +119,12 @@ print(json.dumps(out))
     for att, (ok, err) in res.items():
         assert err == 0, (att, res)
         assert ok == (400 if int(att) < (1 << 20) else 40), (att, res)
+
+
+def test_stream_press_rounds_are_acknowledged(native, echo_server):
+    sp = native.StreamPress({"server": echo_server.address, "chunk_size": 65536, "chunks_per_step": 8})
+    sp.run_steps(5)
+    st = sp.stats()
+    assert st["steps"] == 5
+    assert st["bytes_sent"] == st["bytes_acked"] == 5 * 8 * 65536
+    sp.close()
