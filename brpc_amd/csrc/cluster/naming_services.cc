@@ -120,9 +120,10 @@ public:
 
 class DomainNamingService : public PeriodicNamingService {
 public:
+    explicit DomainNamingService(int default_port = 80) : _default_port(default_port) {}
     int GetServers(const char* name, std::vector<ServerNode>* servers) override {
         std::string host = name;
-        int port = 80;
+        int port = _default_port;
         size_t slash = host.find('/');
         if (slash != std::string::npos) host = host.substr(0, slash);
         size_t colon = host.rfind(':');
@@ -144,8 +145,35 @@ public:
         freeaddrinfo(res);
         return 0;
     }
-    NamingService* New() const override { return new DomainNamingService; }
+    NamingService* New() const override { return new DomainNamingService(_default_port); }
     void Describe(std::ostream& os) const override { os << "dns"; }
+
+private:
+    int _default_port;
+};
+
+// dlist://a.com:80,b.com:8080 — every domain of the list resolved and merged
+// (reference policy/domain_naming_service.cpp DomainListNamingService).
+class DomainListNamingService : public PeriodicNamingService {
+public:
+    int GetServers(const char* name, std::vector<ServerNode>* servers) override {
+        const std::string list = name;
+        size_t b = 0;
+        int resolved = 0;
+        while (b <= list.size()) {
+            size_t e = list.find(',', b);
+            if (e == std::string::npos) e = list.size();
+            const std::string item = trim(list.substr(b, e - b));
+            if (!item.empty()) {
+                DomainNamingService one;
+                if (one.GetServers(item.c_str(), servers) == 0) ++resolved;
+            }
+            b = e + 1;
+        }
+        return resolved > 0 ? 0 : -1;
+    }
+    NamingService* New() const override { return new DomainListNamingService; }
+    void Describe(std::ostream& os) const override { os << "dlist"; }
 };
 
 class RemoteFileNamingService : public PeriodicNamingService {
@@ -277,6 +305,9 @@ void RegisterBuiltinNamingServices() {
         RegisterNamingService("file", new FileNamingService);
         RegisterNamingService("http", new DomainNamingService);
         RegisterNamingService("dns", new DomainNamingService);
+        RegisterNamingService("https", new DomainNamingService(443));
+        RegisterNamingService("redis", new DomainNamingService(6379));
+        RegisterNamingService("dlist", new DomainListNamingService);
         RegisterNamingService("remotefile", new RemoteFileNamingService);
         RegisterNamingService("consul", new ConsulNamingService);
         RegisterNamingService("discovery", new DiscoveryNamingService);

@@ -14,6 +14,7 @@
 #include "cluster/circuit_breaker.h"
 #include "fiber/fiber.h"
 #include "fiber/sync.h"
+#include "cluster/naming_service.h"
 #include "rpc/channel.h"
 #include "rpc/errno.h"
 #include "rpc/server.h"
@@ -353,4 +354,28 @@ TEST(Rpc, circuit_breaker_isolates) {
     const SocketId fake = 0x7777000000000001ull;
     for (int i = 0; i < 4000 && !IsIsolatedByCircuitBreaker(fake); ++i) FeedCircuitBreaker(fake, EINTERNAL, 1000);
     EXPECT_TRUE(IsIsolatedByCircuitBreaker(fake));
+}
+
+TEST(Rpc, domain_list_https_and_redis_naming_services) {
+    for (const char* scheme : {"dns", "https", "redis", "dlist"}) {
+        std::unique_ptr<NamingService> ns(CreateNamingService(scheme));
+        ASSERT_TRUE(ns != nullptr);
+    }
+    auto* dl = static_cast<PeriodicNamingService*>(CreateNamingService("dlist"));
+    std::vector<ServerNode> servers;
+    EXPECT_EQ(dl->GetServers("localhost:8001, 127.0.0.1:8002,localhost:8001", &servers), 0);
+    EXPECT_EQ(servers.size(), 2u);  // localhost:8001 deduplicated
+    delete dl;
+    auto* https = static_cast<PeriodicNamingService*>(CreateNamingService("https"));
+    servers.clear();
+    EXPECT_EQ(https->GetServers("localhost", &servers), 0);
+    ASSERT_FALSE(servers.empty());
+    EXPECT_EQ(servers[0].addr.port, 443);
+    delete https;
+    auto* redis = static_cast<PeriodicNamingService*>(CreateNamingService("redis"));
+    servers.clear();
+    EXPECT_EQ(redis->GetServers("127.0.0.1", &servers), 0);
+    ASSERT_FALSE(servers.empty());
+    EXPECT_EQ(servers[0].addr.port, 6379);
+    delete redis;
 }
