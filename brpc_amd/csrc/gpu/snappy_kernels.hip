@@ -114,8 +114,14 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
             wbase = ip & ~3u;
             win = load_window(in, in_len, wbase, lane);
         }
-#define WBYTE(q) window_byte(win, (q))
-        const uint32_t tag = window_byte(win, ip - wbase);
+        // The tag and the 4 bytes after it in one go: two dword readlanes and
+        // a 64-bit shift (ip + 5 <= wbase + 256 keeps both dwords in range).
+        const uint32_t q = ip - wbase;
+        const uint32_t dlo = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(q >> 2));
+        const uint32_t dhi = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(q >> 2) + 1);
+        const uint64_t x = ((((uint64_t)dhi) << 32) | dlo) >> ((q & 3) * 8);
+        const uint32_t tag = (uint32_t)x & 0xff;
+        const uint32_t ext = (uint32_t)(x >> 8);  // next 4 bytes, little endian
         ++ip;
         const uint32_t kind = tag & 3;
         if (kind == 0) {
@@ -126,10 +132,8 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
                     bad = 3;
                     break;
                 }
-                uint32_t l = 0;
-                for (uint32_t k = 0; k < nb; ++k) l |= WBYTE(ip - wbase + k) << (8 * k);
+                len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
                 ip += nb;
-                len = l + 1;
             }
             if (len > in_len - ip || len > ulen - op) {
                 bad = 4;
@@ -139,9 +143,9 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
                 // short literal: lanes gather bytes from the VGPR window
                 for (uint32_t j0 = 0; j0 < len; j0 += kWave) {
                     const uint32_t j = j0 + (uint32_t)lane;
-                    const uint32_t q = ip - wbase + j;
-                    const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((q >> 2) & 63) << 2, (int)win);
-                    if (j < len) buf[op + j] = (uint8_t)(d >> ((q & 3) * 8));
+                    const uint32_t qq = ip - wbase + j;
+                    const uint32_t d = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((qq >> 2) & 63) << 2, (int)win);
+                    if (j < len) buf[op + j] = (uint8_t)(d >> ((qq & 3) * 8));
                 }
             } else {
                 for (uint32_t j = lane; j < len; j += kWave) buf[op + j] = in[ip + j];
@@ -149,30 +153,30 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
             ip += len;
             op += len;
         } else {
-            uint32_t len, off;
-            const uint32_t need = kind == 1 ? 1 : (kind == 2 ? 2 : 4);
-            if (ip + need > in_len) {
-                bad = 5;
-                break;
-            }
-            const uint32_t q = ip - wbase;
+            uint32_t len, off, need;
             if (kind == 1) {
                 len = ((tag >> 2) & 7) + 4;
-                off = ((tag >> 5) << 8) | WBYTE(q);
+                off = ((tag >> 5) << 8) | (ext & 0xff);
+                need = 1;
             } else if (kind == 2) {
                 len = (tag >> 2) + 1;
-                off = WBYTE(q) | (WBYTE(q + 1) << 8);
+                off = ext & 0xffff;
+                need = 2;
             } else {
                 len = (tag >> 2) + 1;
-                off = WBYTE(q) | (WBYTE(q + 1) << 8) | (WBYTE(q + 2) << 16) | (WBYTE(q + 3) << 24);
+                off = ext;
+                need = 4;
             }
             ip += need;
-            if (off == 0 || off > op || len > ulen - op) {
+            // one unsigned compare covers off == 0 and off > op
+            if (ip > in_len || off - 1 >= op || len > ulen - op) {
                 bad = 6;
                 break;
             }
             const uint32_t from = op - off;
-            if (off >= len) {
+            if (len <= (uint32_t)kWave && off >= len) {
+                if ((uint32_t)lane < len) buf[op + lane] = buf[from + lane];  // the common case: one step
+            } else if (off >= len) {
                 for (uint32_t j = lane; j < len; j += kWave) buf[op + j] = buf[from + j];
             } else {
                 for (uint32_t j = lane; j < len; j += kWave) buf[op + j] = buf[from + j % off];
@@ -180,7 +184,6 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
             op += len;
         }
         __builtin_amdgcn_wave_barrier();
-#undef WBYTE
     }
     if (!bad && op != ulen) bad = 7;
     if (bad) {
