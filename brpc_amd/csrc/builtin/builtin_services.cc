@@ -1,3 +1,4 @@
+#include <dlfcn.h>
 // Builtin HTTP pages installed on every server (role of the reference's
 // src/brpc/builtin/*: index, status, vars, flags, connections, rpcz,
 // health, version, list, threads, vlog, bthreads, ids, sockets, protobufs,
@@ -416,6 +417,56 @@ static double seconds_param(Controller* cntl, double def) {
     return std::min(v, 60.0);
 }
 
+// Heap profiles come from heapprof/heapprof.cc when it is linked into the
+// executable (or LD_PRELOADed): found at run time, like the reference finds
+// tcmalloc's MallocExtension (details/tcmalloc_extension.cpp).
+std::string HeapProfileRaw(bool growth, bool* linked) {
+    typedef char* (*Fn)(int);
+    static Fn fn = reinterpret_cast<Fn>(dlsym(RTLD_DEFAULT, "mrpc_heap_profile_text"));
+    *linked = fn != nullptr;
+    if (!fn) return std::string();
+    char* p = fn(growth ? 1 : 0);
+    std::string out = p ? p : "";
+    free(p);
+    return out;
+}
+
+// Human view of a raw profile: stacks sorted by bytes, symbolized.
+std::string HeapProfileReport(const std::string& raw, bool growth) {
+    struct Row {
+        long long bytes, count;
+        std::string stack;
+    };
+    std::vector<Row> rows;
+    std::istringstream is(raw);
+    std::string line, header;
+    std::getline(is, header);
+    while (std::getline(is, line)) {
+        if (line.empty() || line[0] == 'M') break;
+        const size_t at = line.find('@');
+        if (at == std::string::npos) continue;
+        Row r;
+        r.count = atoll(line.c_str());
+        r.bytes = atoll(line.c_str() + line.find(':') + 1);
+        std::istringstream fs(line.substr(at + 1));
+        std::string a;
+        bool first = true;
+        while (fs >> a) {
+            const std::string sym = profiler::Symbolize((uintptr_t)strtoull(a.c_str(), nullptr, 16));
+            if (sym.find("mrpc_heap") != std::string::npos) continue;
+            r.stack += (first ? "" : " <- ") + sym;
+            first = false;
+        }
+        rows.push_back(r);
+    }
+    std::sort(rows.begin(), rows.end(), [](const Row& x, const Row& y) { return x.bytes > y.bytes; });
+    std::ostringstream os;
+    os << (growth ? "# cumulative sampled allocations (growth)\n" : "# in-use sampled allocations\n") << header
+       << "\n# bytes count stack\n";
+    for (const Row& r : rows) os << r.bytes << " " << r.count << " " << r.stack << "\n";
+    return os.str();
+}
+
 class HotspotsImpl : public hotspots {
 public:
     void default_method(RpcController* c, const BuiltinRequest*, BuiltinResponse*, Closure* done) override {
@@ -450,9 +501,16 @@ public:
             }
             text(cntl, os.str());
         } else if (kind == "heap" || kind == "growth") {
+            bool linked = false;
+            const std::string raw = HeapProfileRaw(kind == "growth", &linked);
+            if (linked) {
+                text(cntl, HeapProfileReport(raw, kind == "growth"));
+                return;
+            }
             struct mallinfo2 mi = mallinfo2();
             std::ostringstream os;
-            os << "heap profiling needs a sampling allocator (not linked); glibc arena summary:\n";
+            os << "heap profiling needs the sampling allocator (link heapprof/heapprof.cc or LD_PRELOAD "
+                  "libmrpc_heapprof.so); glibc arena summary:\n";
             os << "arena " << mi.arena << "\nin_use " << mi.uordblks << "\nfree " << mi.fordblks << "\nmmap "
                << mi.hblkhd << "\n";
             text(cntl, os.str());
@@ -495,7 +553,14 @@ public:
             std::replace(s.begin(), s.end(), '\0', '\n');
             text(cntl, s);
         } else if (kind == "heap" || kind == "growth") {
-            cntl->SetFailed(ENOMETHOD, "heap profiles need a sampling allocator, which is not linked");
+            bool linked = false;
+            const std::string raw = HeapProfileRaw(kind == "growth", &linked);
+            if (!linked) {
+                cntl->SetFailed(ENOMETHOD, "heap profiles need heapprof/heapprof.cc linked or preloaded");
+                return;
+            }
+            cntl->http_response().set_content_type("text/plain");
+            cntl->response_attachment().append(raw);  // pprof reads the legacy text format
         } else {
             cntl->SetFailed(ENOMETHOD, "unknown pprof endpoint `%s' (profile|symbol|cmdline)", kind.c_str());
         }

@@ -33,7 +33,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 # Directories whose sources form the bootstrap library used by mrpc_protoc.
 BOOT_DIRS = ["base", "pb"]
 # Directories excluded from libmrpc.
-NON_LIB_DIRS = {"tools", "python", "tests", "examples"}
+NON_LIB_DIRS = {"tools", "python", "tests", "examples", "heapprof"}
 
 
 def rel(p):
@@ -190,6 +190,17 @@ def main():
             b = os.path.join(BUILD, "bin", name)
             w(f"build {rel(b)}: link {rel(o)} | {rel(libso)}\n  extra = {linkmrpc}\n")
             bins.append(b)
+    # sampling heap profiler: never part of libmrpc (it interposes malloc);
+    # linked into heapprof_demo and shipped as an LD_PRELOAD library
+    hp = os.path.join(CSRC, "heapprof", "heapprof.cc")
+    if os.path.exists(hp):
+        hp_o = cxx(hp)
+        hp_so = os.path.join(PKG, "lib", "libmrpc_heapprof.so")
+        w(f"build {rel(hp_so)}: solink {rel(hp_o)}\n  ldlibs = -ldl -lpthread\n")
+        d_o = cxx(os.path.join(CSRC, "heapprof", "heapprof_demo.cc"), implicit=["gen_headers"])
+        b = os.path.join(BUILD, "bin", "heapprof_demo")
+        w(f"build {rel(b)}: link {rel(d_o)} {rel(hp_o)} | {rel(libso)}\n  extra = {linkmrpc} -rdynamic\n")
+        bins += [hp_so, b]
     w(f"build all: phony {rel(libso)} {rel(pymod)} {' '.join(rel(b) for b in bins)}\n")
     w("default all\n")
     with open(os.path.join(BUILD, "build.ninja"), "w") as f:

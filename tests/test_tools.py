@@ -104,3 +104,12 @@ def test_parallel_http(procs, tmp_path):
     assert "fetched 120 urls" in r.stdout and "failed=0" in r.stdout
     lines = [l for l in r.stdout.splitlines() if l.startswith("200 ")]
     assert len(lines) == 120
+
+
+def test_sampling_heap_profiler():
+    """heapprof/heapprof.cc linked into heapprof_demo: /hotspots/heap,
+    /hotspots/growth and /pprof/heap attribute sampled bytes to the right
+    functions (the demo checks the estimates against the true sizes)."""
+    r = subprocess.run([os.path.join(BIN, "heapprof_demo")], capture_output=True, text=True, timeout=60, cwd="/tmp")
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "KeepLiveBuffers" in r.stdout
