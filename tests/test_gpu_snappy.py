@@ -87,7 +87,7 @@ def test_gpu_compress_round_trips_through_host_and_gpu(dev, kind, n):
     from brpc_amd.ops import snappy_compress, snappy_decompress
     data = _corpus(kind, n, n * 11 + len(kind))
     t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
-    packed, offs, sizes, raw = snappy_compress(t)
+    packed, offs, sizes, raw = snappy_compress(t, block=65536)
     host = packed.cpu().numpy().tobytes()
     # every device-compressed block is a valid snappy stream for the host codec
     back = b"".join(native.snappy_uncompress(host[o:o + s]) for o, s in zip(offs, sizes))
@@ -109,3 +109,14 @@ def test_gpu_compress_32k_blocks_and_uncompacted_slots(dev):
     assert len(sizes) == 96 and all(r == 32768 for r in raw)
     out = snappy_decompress(slots, offs, sizes, raw)
     assert out.cpu().numpy().tobytes() == data
+
+
+def test_default_block_is_32k_and_round_trips(dev):
+    from brpc_amd.ops import snappy_compress, snappy_decompress
+    from brpc_amd.ops.snappy import DEFAULT_BLOCK
+    assert DEFAULT_BLOCK == 32768
+    data = _corpus("text", 200000, 3)
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    packed, offs, sizes, raw = snappy_compress(t)
+    assert raw[:-1] == [32768] * (len(raw) - 1)
+    assert snappy_decompress(packed, offs, sizes, raw).cpu().numpy().tobytes() == data
