@@ -46,7 +46,7 @@ def parse():
                     help="skip the streaming-RPC leg (64 KiB chunks, BASELINE config 3)")
     ap.add_argument("--device-payload", action="store_true",
                     help="64 KiB leg with HBM-resident attachments")
-    ap.add_argument("--latency-sample-s", type=float, default=2.0,
+    ap.add_argument("--latency-sample-s", type=float, default=4.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
 

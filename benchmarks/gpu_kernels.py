@@ -66,6 +66,37 @@ def main():
                           "Mvalues_per_s": nv / t / 1e6, "verified": ok}))
         del buf, dst, vals, enc
         torch.cuda.empty_cache()
+    # protobuf wire scan: 4M RpcMeta-sized messages (tag/varint/len walk)
+    from brpc_amd.ops import pb_scan
+    import random as _r
+    rnd0 = _r.Random(11)
+
+    def _vi(v):
+        out = bytearray()
+        while v >= 0x80:
+            out.append((v & 0x7F) | 0x80)
+            v >>= 7
+        out.append(v)
+        return bytes(out)
+
+    tmpl = []
+    for _ in range(1024):  # RpcMeta-like: request{service,method,log_id}, correlation_id, attachment_size
+        req = b"\x0a" + _vi(20) + b"example.EchoService_" + b"\x12\x04Echo" + b"\x18" + _vi(rnd0.getrandbits(40))
+        tmpl.append(b"\x0a" + _vi(len(req)) + req + b"\x20" + _vi(rnd0.getrandbits(50)) + b"\x28" + _vi(rnd0.randrange(1 << 17)))
+    nmsg = 1 << 22
+    lens = torch.tensor([len(m) for m in tmpl], dtype=torch.int64)
+    t_bytes = torch.frombuffer(bytearray(b"".join(tmpl)), dtype=torch.uint8)
+    reps = nmsg // len(tmpl)
+    pbbuf = t_bytes.repeat(reps).to(dev)
+    pboffs = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(lens.repeat(reps), 0)]).to(dev)
+    fields, nf = pb_scan(pbbuf, pboffs, 8)
+    ok = bool((nf == 3).all().item())
+    t = timeit(lambda: pb_scan(pbbuf, pboffs, 8), iters=10)
+    print(json.dumps({"kernel": "pb_scan", "messages": nmsg, "bytes": pbbuf.numel(), "sec": t,
+                      "Mmsgs_per_s": nmsg / t / 1e6, "GBps_in": pbbuf.numel() / t / 1e9, "verified": ok}))
+    del pbbuf, pboffs, fields, nf
+    torch.cuda.empty_cache()
+
     # snappy: 128 MiB of mixed (~2:1) data as 2048 x 64 KiB and 4096 x 32 KiB
     # blocks. "sec" is kernel time only (CUDA events around launches with the
     # job tables already on the device); the python wrappers add host work.

@@ -75,6 +75,13 @@ constexpr uint64_t SnappyMaxCompressedLength(uint64_t n) { return 32 + n + n / 6
 int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, void* scratch, uint32_t* out_len_dev, int* err_dev,
                          hipStream_t s);
 
+// Batched protobuf wire scan (gpu/pb_kernels.hip): message i is
+// buf[offsets[i], offsets[i+1]); its top-level fields land in
+// fields[i * max_fields * 2 + 2k] = tag, [.. + 1] = value (varint / fixed /
+// (offset << 32) | length); nfields[i] = count or a negative error code.
+int LaunchPbScan(const uint8_t* buf, const int64_t* offsets_dev, int64_t n, uint32_t max_fields, uint64_t* fields,
+                 int32_t* nfields, hipStream_t s);
+
 // ---- synchronous helpers (fiber-friendly waits)
 // CRC32C of device buffers; results to host.
 int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t* out_host, int device);
