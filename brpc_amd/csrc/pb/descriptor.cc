@@ -7,6 +7,10 @@
 namespace mrpc {
 namespace pb {
 
+Descriptor::~Descriptor() {
+    if (owns_prototype) delete prototype;
+}
+
 const char* FieldTypeName(FieldType t) {
     switch (t) {
     case FieldType::DOUBLE: return "double";

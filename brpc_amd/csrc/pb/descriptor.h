@@ -100,6 +100,11 @@ public:
     uint32_t object_size = 0;
     Message* (*factory)() = nullptr;  // generated messages
     const Message* prototype = nullptr;  // default instance (generated or dynamic)
+    bool owns_prototype = false;         // dynamic prototypes die with their descriptor
+    Descriptor() = default;
+    Descriptor(const Descriptor&) = delete;
+    Descriptor& operator=(const Descriptor&) = delete;
+    ~Descriptor();
 
     int field_count() const { return (int)fields.size(); }
     const FieldDescriptor* field(int i) const { return &fields[i]; }
@@ -153,6 +158,11 @@ public:
     std::vector<ServiceDescriptor*> services;
     std::map<std::string, std::string> options;
     std::string source;  // original .proto text, for /protobufs
+    // Storage of descriptors parsed at run time (the lists above only point
+    // into it; generated files keep theirs in static registries instead).
+    std::vector<std::unique_ptr<Descriptor>> owned_messages;
+    std::vector<std::unique_ptr<EnumDescriptor>> owned_enums;
+    std::vector<std::unique_ptr<ServiceDescriptor>> owned_services;
 };
 
 // Global registry of all known descriptors (generated pool + runtime pools).

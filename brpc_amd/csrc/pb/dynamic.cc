@@ -142,7 +142,10 @@ void PrepareDynamicLayout(Descriptor* d) {
     }
     d->object_size = (uint32_t)align_up(off, 8);
     d->BuildIndex();
-    if (!d->prototype) d->prototype = DynamicMessage::Create(d);
+    if (!d->prototype) {
+        d->prototype = DynamicMessage::Create(d);
+        d->owns_prototype = true;
+    }
 }
 
 }  // namespace pb

@@ -176,15 +176,7 @@ public:
 
 private:
     void delete_file() {
-        std::function<void(Descriptor*)> del = [&](Descriptor* d) {
-            for (Descriptor* n : d->nested_types) del(n);
-            for (EnumDescriptor* e : d->enum_types) delete e;
-            delete d;
-        };
-        for (Descriptor* d : _file->message_types) del(d);
-        for (EnumDescriptor* e : _file->enum_types) delete e;
-        for (ServiceDescriptor* s : _file->services) delete s;
-        delete _file;
+        delete _file;  // frees every descriptor parsed so far (owned_*)
         _file = nullptr;
     }
     [[noreturn]] void fail(const std::string& what) {
@@ -347,6 +339,7 @@ private:
 
     EnumDescriptor* parse_enum(const std::string& scope) {
         EnumDescriptor* e = new EnumDescriptor;
+        _file->owned_enums.emplace_back(e);
         e->name = ident();
         e->full_name = scope_prefix(scope) + e->name;
         e->file = _file;
@@ -413,6 +406,7 @@ private:
 
     Descriptor* parse_message(const std::string& scope, Descriptor* parent) {
         Descriptor* d = new Descriptor;
+        _file->owned_messages.emplace_back(d);
         d->name = ident();
         d->full_name = scope_prefix(scope) + d->name;
         d->file = _file;
@@ -483,6 +477,7 @@ private:
                 expect(";");
                 // synthesize the entry type
                 Descriptor* e = new Descriptor;
+                _file->owned_messages.emplace_back(e);
                 std::string camel;
                 bool up = true;
                 for (char c : f.name) {
@@ -533,6 +528,7 @@ private:
 
     ServiceDescriptor* parse_service() {
         ServiceDescriptor* s = new ServiceDescriptor;
+        _file->owned_services.emplace_back(s);
         s->name = ident();
         s->full_name = scope_prefix(_file->package) + s->name;
         s->file = _file;
