@@ -1,4 +1,9 @@
 // Fiber scheduler implementation. See internal.h for the design notes.
+#if defined(__SANITIZE_ADDRESS__)
+#include <pthread.h>
+#include <sanitizer/asan_interface.h>
+#include <sanitizer/common_interface_defs.h>
+#endif
 #include <sys/mman.h>
 
 #include <cerrno>
@@ -213,6 +218,43 @@ void TaskGroup::sched_to(TaskGroup** pg, fiber_t next_tid) {
 
 void TaskGroup::sched_to(TaskGroup** pg, TaskMeta* next) { sched_to_impl(pg, next, false); }
 
+// AddressSanitizer must be told about stack switches, otherwise shadow left
+// by a fiber on a pooled stack (or by the worker's own stack) reads as
+// overflow / use-after-scope once another context runs there.
+#if defined(__SANITIZE_ADDRESS__)
+static void asan_target_stack(const TaskMeta* next, const void** bottom, size_t* size) {
+    if (next->stack) {
+        *bottom = next->stack->base;
+        *size = next->stack->size;
+        return;
+    }
+    static thread_local const void* t_bottom = nullptr;
+    static thread_local size_t t_size = 0;
+    if (!t_bottom) {
+        pthread_attr_t attr;
+        void* addr = nullptr;
+        if (pthread_getattr_np(pthread_self(), &attr) == 0) {
+            pthread_attr_getstack(&attr, &addr, &t_size);
+            pthread_attr_destroy(&attr);
+        }
+        t_bottom = addr;
+    }
+    *bottom = t_bottom;
+    *size = t_size;
+}
+#define MRPC_ASAN_START_SWITCH(fake, next)                 \
+    do {                                                  \
+        const void* _b;                                   \
+        size_t _s;                                        \
+        asan_target_stack(next, &_b, &_s);                \
+        __sanitizer_start_switch_fiber(fake, _b, _s);     \
+    } while (0)
+#define MRPC_ASAN_FINISH_SWITCH(fake) __sanitizer_finish_switch_fiber(fake, nullptr, nullptr)
+#else
+#define MRPC_ASAN_START_SWITCH(fake, next) (void)0
+#define MRPC_ASAN_FINISH_SWITCH(fake) (void)0
+#endif
+
 void TaskGroup::sched_to_impl(TaskGroup** pg, TaskMeta* next, bool handover) {
     TaskGroup* g = *pg;
     TaskMeta* cur = g->_cur_meta;
@@ -222,13 +264,21 @@ void TaskGroup::sched_to_impl(TaskGroup** pg, TaskMeta* next, bool handover) {
             LOG(FATAL) << "Out of fiber stacks";
         }
         next->stack = s;
+#if defined(__SANITIZE_ADDRESS__)
+        // a pooled stack still carries the redzones of the fiber that died on it
+        __asan_unpoison_memory_region(s->base, s->size);
+#endif
         next->sp = make_context(s->base, s->size, TaskGroup::task_runner);
     }
     if (next != cur) {
         ++g->_nswitch;
         g->_cur_meta = next;
         if (!handover) {
+            void* fake_stack = nullptr;
+            (void)fake_stack;
+            MRPC_ASAN_START_SWITCH(&fake_stack, next);
             mrpc_fiber_jump(&cur->sp, next->sp, nullptr);
+            MRPC_ASAN_FINISH_SWITCH(fake_stack);
             g = tls_group();
             *pg = g;
         }
@@ -239,6 +289,7 @@ void TaskGroup::sched_to_impl(TaskGroup** pg, TaskMeta* next, bool handover) {
 }
 
 void TaskGroup::task_runner(void*) {
+    MRPC_ASAN_FINISH_SWITCH(nullptr);  // first entry of a fresh context
     TaskGroup* g = tls_group();
     g->run_remained();
     do {

@@ -613,8 +613,8 @@ int Socket::ConnectIfNot(const timespec* abstime, WriteRequest*) {
     bool in_progress = false;
     int fd = tcp_connect_nonblocking(_remote_side, &in_progress);
     if (fd < 0) return -1;
+    timespec ts;  // function scope: abstime may point here through the RDMA handshake
     if (in_progress) {
-        timespec ts;
         if (!abstime) {
             ts = realtime_after_us((int64_t)FLAGS_connect_timeout_ms_default * 1000);
             abstime = &ts;
