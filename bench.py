@@ -39,13 +39,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--requests-per-step", type=int, default=0, help="override the 32B step size")
+    ap.add_argument("--requests-per-step-64k", type=int, default=0, help="override the 64 KiB step size")
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--workers", type=int, default=0, help="fiber worker pthreads per rank (0: auto)")
     ap.add_argument("--skip-64k", action="store_true")
     ap.add_argument("--skip-stream", action="store_true",
                     help="skip the streaming-RPC leg (64 KiB chunks, BASELINE config 3)")
-    ap.add_argument("--device-payload", action="store_true",
-                    help="64 KiB leg with HBM-resident attachments")
+    ap.add_argument("--host-payload", action="store_true",
+                    help="64 KiB leg with host attachments only (default on a GPU box: HBM-resident "
+                         "attachments over the xGMI transport, plus a host-attachment reference leg)")
+    ap.add_argument("--device-payload", action="store_true", help=argparse.SUPPRESS)  # old flag, now default
     ap.add_argument("--latency-sample-s", type=float, default=4.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
@@ -74,15 +77,18 @@ def auto_workers(local_world):
     # for the rest of each 100 ms period (measured on the MI355X box with a
     # 16-CPU quota: 12 workers ~1.0-1.1M QPS, 16 workers 0.4-0.6M;
     # profiles/bench_r1_worker_sweep.txt).
+    # On a multi-GPU node the ranks share one quota: every rank also runs a
+    # dispatcher, a timer thread, the GPU event poller and the Python main
+    # thread, so those 4 come off each rank's share before the workers.
     share = cpu_quota() // max(1, local_world)
-    return max(4, min(12, share - 4))
+    return max(2, min(12, share - 4))
 
 
 def main():
     a = parse()
     import torch  # noqa: E402
     from brpc_amd import native  # noqa: E402
-    from brpc_amd.models import ECHO_32B, ECHO_64KB, start_echo_server  # noqa: E402
+    from brpc_amd.models import ECHO_32B, ECHO_64KB, EchoWorkload, start_echo_server  # noqa: E402
     from brpc_amd import parallel  # noqa: E402
 
     topo = parallel.init_distributed()
@@ -115,8 +121,11 @@ def main():
         parallel.barrier(topo)
         sync()
         t0 = time.perf_counter()
+        step_s = []
         for _ in range(steps):
+            ts = time.perf_counter()
             press.run_requests(n)
+            step_s.append(time.perf_counter() - ts)
         parallel.barrier(topo)
         sync()
         dt = time.perf_counter() - t0
@@ -127,6 +136,7 @@ def main():
         p99_max = parallel.allreduce_max(st["p99_us"], topo)
         p50_max = parallel.allreduce_max(st["p50_us"], topo)
         del press
+        step_qps = sorted(n / x for x in step_s if x > 0)
         return {
             "qps": ok_total / dt_max if dt_max > 0 else 0.0,
             "ms_per_step": 1000.0 * dt_max / steps,
@@ -135,6 +145,10 @@ def main():
             "errors": int(err_total),
             "elapsed_s": dt_max,
             "last_error": st["last_error"],
+            # this rank's per-step spread (box noise indicator)
+            "step_qps_median": step_qps[len(step_qps) // 2] if step_qps else 0.0,
+            "step_qps_min": step_qps[0] if step_qps else 0.0,
+            "step_qps_max": step_qps[-1] if step_qps else 0.0,
         }
 
     wl32 = ECHO_32B
@@ -142,11 +156,23 @@ def main():
         wl32.requests_per_step = a.requests_per_step
     r32 = timed_leg(wl32, a.steps, a.warmup)
 
-    r64 = None
+    # 64 KiB leg. On a GPU box the attachment lives in HBM and moves over
+    # the xGMI transport (lent zero-copy, pulled once per hop by the batched
+    # copy engine); the host-attachment leg is kept as the TCP reference.
+    r64 = r64h = None
+    use_dev = cuda and not a.host_payload
     if not a.skip_64k:
         wl64 = ECHO_64KB
-        wl64.device_attachment = bool(a.device_payload and cuda)
-        r64 = timed_leg(wl64, a.steps, a.warmup)
+        if a.requests_per_step_64k:
+            wl64.requests_per_step = a.requests_per_step_64k
+        if use_dev:
+            wl64.device_attachment = True
+            r64 = timed_leg(wl64, a.steps, a.warmup)
+        wl64h = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=False,
+                                    requests_per_step=max(1, wl64.requests_per_step // 2)))
+        r64h = timed_leg(wl64h, a.steps, a.warmup)
+        if r64 is None:
+            r64, r64h = r64h, None
 
     # Streaming-RPC leg: each rank pushes 64 KiB chunks through one
     # flow-controlled stream to its ring peer; a step is 32 chunks (2 MiB)
@@ -208,6 +234,10 @@ def main():
             "p50_us": r32["p50_us"],
             "p99_us": r32["p99_us"],
             "errors": r32["errors"],
+            "timed_s_32B": round(r32["elapsed_s"], 3),
+            "step_qps_median_32B": round(r32["step_qps_median"], 1),
+            "step_qps_min_32B": round(r32["step_qps_min"], 1),
+            "step_qps_max_32B": round(r32["step_qps_max"], 1),
         }
         if r64:
             out["qps_64KB"] = round(r64["qps"], 1)
@@ -215,7 +245,12 @@ def main():
             out["gbytes_per_s_64KB"] = round(r64["qps"] * 65536 * 2 / 1e9, 3)
             out["vs_baseline_64KB"] = round(r64["qps"] / BASELINE_QPS_32KB, 4)
             out["errors_64KB"] = r64["errors"]
-            out["device_payload_64KB"] = bool(a.device_payload and cuda)
+            out["timed_s_64KB"] = round(r64["elapsed_s"], 3)
+            out["device_payload_64KB"] = bool(use_dev)
+        if r64h:
+            out["qps_64KB_host_attachment"] = round(r64h["qps"], 1)
+            out["p99_us_64KB_host_attachment"] = r64h["p99_us"]
+            out["gbytes_per_s_64KB_host_attachment"] = round(r64h["qps"] * 65536 * 2 / 1e9, 3)
         if rs:
             out["stream_gbytes_per_s_64KB_chunks"] = round(rs["gbps"], 3)
             out["stream_ms_per_step"] = round(rs["ms_per_step"], 3)

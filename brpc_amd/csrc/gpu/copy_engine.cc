@@ -1,0 +1,138 @@
+#include "gpu/copy_engine.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+#include "base/logging.h"
+#include "fiber/butex.h"
+#include "gpu/gpu.h"
+
+namespace mrpc {
+namespace gpu {
+
+namespace {
+
+const int kMaxDev = 16;
+
+// One launch worth of segments. Every submitter of the batch parks on
+// `butex`; the poller sets it to 1 (or -1) when the batch's event fires.
+struct Batch {
+    std::vector<Segment> segs;
+    std::atomic<int>* butex = nullptr;
+    hipEvent_t ev = nullptr;
+    std::atomic<int> refs{0};
+};
+
+struct Engine {
+    std::mutex mu;
+    Batch* open = nullptr;     // batch accepting submissions
+    bool launching = false;    // a leader is draining `open`
+    std::vector<Batch*> spare; // recycled batches
+};
+
+Engine g_engine[kMaxDev];
+std::atomic<int64_t> g_submits{0}, g_launches{0}, g_segments{0}, g_bytes{0};
+
+Batch* new_batch(Engine& e) {
+    if (!e.spare.empty()) {
+        Batch* b = e.spare.back();
+        e.spare.pop_back();
+        return b;
+    }
+    Batch* b = new Batch;
+    b->butex = fiber::butex_create();
+    return b;
+}
+
+// Issue one batch: kernel + event + poller registration. On failure the
+// batch's waiters are released with an error.
+void launch(Batch* b, int device) {
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    hipStream_t s = PoolStream(device);
+    b->ev = AcquireEvent();
+    int rc = (s && b->ev) ? LaunchBatchedCopy(b->segs.data(), (int)b->segs.size(), s) : -1;
+    if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
+    if (prev != device) hipSetDevice(prev);
+    g_launches.fetch_add(1, std::memory_order_relaxed);
+    if (rc != 0) {
+        LOG_EVERY_SECOND(ERROR) << "batched copy launch of " << b->segs.size() << " segments failed on device " << device;
+        b->butex->store(-1, std::memory_order_release);
+        fiber::butex_wake_all(b->butex);
+        return;
+    }
+    WatchEvent(b->ev, b->butex);
+}
+
+}  // namespace
+
+int BatchedCopy(const Segment* segs, int n, int device) {
+    if (n <= 0) return 0;
+    if (device < 0) device = CurrentDevice();
+    if (device < 0 || device >= kMaxDev || Init(device) != 0) return -1;
+    Engine& e = g_engine[device];
+    g_submits.fetch_add(1, std::memory_order_relaxed);
+    Batch* mine;
+    bool leader = false;
+    {
+        std::lock_guard<std::mutex> g(e.mu);
+        if (!e.open) {
+            e.open = new_batch(e);
+            e.open->butex->store(0, std::memory_order_relaxed);
+        }
+        mine = e.open;
+        mine->segs.insert(mine->segs.end(), segs, segs + n);
+        mine->refs.fetch_add(1, std::memory_order_relaxed);
+        if (!e.launching) {
+            e.launching = true;
+            leader = true;
+        }
+    }
+    if (leader) {
+        // Drain: whatever accumulated while we were launching goes out as
+        // the next batch, until no submission is left open.
+        for (;;) {
+            Batch* cur;
+            {
+                std::lock_guard<std::mutex> g(e.mu);
+                cur = e.open;
+                e.open = nullptr;
+                if (!cur) {
+                    e.launching = false;
+                    break;
+                }
+            }
+            uint64_t bytes = 0;
+            for (const Segment& s : cur->segs) bytes += s.len;
+            g_segments.fetch_add((int64_t)cur->segs.size(), std::memory_order_relaxed);
+            g_bytes.fetch_add((int64_t)bytes, std::memory_order_relaxed);
+            launch(cur, device);
+        }
+    }
+    while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
+    const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
+    if (mine->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        ReleaseEvent(mine->ev);
+        mine->ev = nullptr;
+        mine->segs.clear();
+        std::lock_guard<std::mutex> g(e.mu);
+        e.spare.push_back(mine);
+    }
+    return rc;
+}
+
+CopyEngineStats GetCopyEngineStats() {
+    CopyEngineStats s;
+    s.submits = g_submits.load(std::memory_order_relaxed);
+    s.launches = g_launches.load(std::memory_order_relaxed);
+    s.segments = g_segments.load(std::memory_order_relaxed);
+    s.bytes = g_bytes.load(std::memory_order_relaxed);
+    return s;
+}
+
+}  // namespace gpu
+}  // namespace mrpc

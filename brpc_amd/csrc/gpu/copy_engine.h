@@ -1,0 +1,36 @@
+// Batched device copy engine: the data mover under the xGMI transport.
+//
+// Every fiber that needs device bytes moved (an xGMI pull of a received
+// payload, a gather into HBM, ...) submits its (src, dst, len) segments here
+// and parks. Submissions that arrive while a launch is being issued are
+// combined: the first submitter becomes the leader, closes the open batch,
+// launches ONE batched-copy kernel for all of its segments on a pool stream,
+// records one event and hands it to the completion poller, which wakes every
+// fiber of that batch at once. Under load this turns N payload transfers per
+// tick into one kernel launch + one event, instead of N hipMemcpyAsync + N
+// event round trips (which is what capped the round-1 HBM path below the
+// host TCP path).
+//
+// Sources may be local HBM, peer HBM mapped through hipIpcOpenMemHandle
+// (the kernel then reads across xGMI) or pinned host memory.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+#include "gpu/kernels.h"
+
+namespace mrpc {
+namespace gpu {
+
+// Copy all segments on `device`; returns when the copies completed (fiber
+// parks, pthread blocks). 0 on success.
+int BatchedCopy(const Segment* segs, int n, int device);
+
+struct CopyEngineStats {
+    int64_t submits = 0, launches = 0, segments = 0, bytes = 0;
+};
+CopyEngineStats GetCopyEngineStats();
+
+}  // namespace gpu
+}  // namespace mrpc

@@ -17,6 +17,7 @@
 #pragma once
 
 #include <cstddef>
+#include <atomic>
 #include <cstdint>
 #include <string>
 
@@ -45,8 +46,11 @@ void* Malloc(size_t n, int device, std::string* error = nullptr);
 void Free(void* p);
 void* HostMallocPinned(size_t n);
 void HostFreePinned(void* p);
-// Make default Buf blocks pinned host memory (call before heavy traffic).
+// Make default Buf blocks pinned host memory from the pinned slab pool
+// (gpu/hbm_pool.h). Idempotent; called when a Server or Channel enables a
+// GPU device, before traffic starts.
 int UsePinnedBlocks();
+bool PinnedBlocksInUse();
 
 // Copies; stream-ordered on a pool stream, the calling fiber parks until
 // completion (a pthread blocks).
@@ -75,6 +79,13 @@ hipStream_t PoolStream(int device);  // round-robin over <=4 non-blocking stream
 int WaitEvent(hipEvent_t ev);
 // Record an event on `s` and wait for it fiber-friendly.
 int SyncStream(hipStream_t s);
+// Hand `ev` to the completion poller: when it completes the poller stores 1
+// (or -1 on failure) into *butex and wakes every waiter parked on it. One
+// event can release a whole batch of fibers.
+void WatchEvent(hipEvent_t ev, std::atomic<int>* butex);
+// Pooled events (hipEventDisableTiming).
+hipEvent_t AcquireEvent();
+void ReleaseEvent(hipEvent_t e);
 // Poller statistics
 int64_t PolledEvents();
 

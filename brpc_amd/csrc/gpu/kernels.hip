@@ -164,7 +164,18 @@ __global__ void __launch_bounds__(kThreads) batched_copy_kernel(SegBatch b) {
     const uint64_t cbeg = k * kChunkBytes;
     const uint64_t cend = cbeg + kChunkBytes < len ? cbeg + kChunkBytes : len;
     const bool aligned = (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0);
-    if (aligned) {
+    if (aligned && cend - cbeg == kChunkBytes) {
+        // full 16 KiB chunk: each lane issues all four 16 B loads before any
+        // store (4 KiB stripes, coalesced), so 64 B per lane are in flight —
+        // what a pull across xGMI needs to cover the remote-read latency
+        const uint4* __restrict__ s4 = reinterpret_cast<const uint4*>(src + cbeg) + threadIdx.x;
+        uint4* __restrict__ d4 = reinterpret_cast<uint4*>(dst + cbeg) + threadIdx.x;
+        uint4 v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = s4[i * kThreads];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d4[i * kThreads] = v[i];
+    } else if (aligned) {
         // coalesced: lane i moves 16 B at i*16 within each 4 KiB stripe
         for (uint64_t off = cbeg + threadIdx.x * 16; off < cend; off += kThreads * 16) {
             if (off + 16 <= cend) {

@@ -4,6 +4,7 @@
 #include <vector>
 
 #include "base/crc32c.h"
+#include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
 
 namespace mrpc {
@@ -28,7 +29,8 @@ int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t*
     const size_t desc_bytes = desc.size() * sizeof(uint64_t);
     const size_t bytes = desc_bytes + Crc32cScratchBytes(n) + sizeof(uint32_t) * n;
     int rc = -1;
-    char* mem = static_cast<char*>(Malloc(bytes, device));
+    // pooled scratch: a hipFree here would synchronise the whole device
+    char* mem = static_cast<char*>(HbmAlloc(bytes, device));
     hipStream_t s = PoolStream(device);
     if (mem && s) {
         uint64_t* d_starts = reinterpret_cast<uint64_t*>(mem);
@@ -41,7 +43,8 @@ int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t*
             rc = SyncStream(s);
         }
     }
-    Free(mem);
+    if (mem && rc != 0 && s) SyncStream(s);  // never recycle scratch a launch may still use
+    HbmFree(mem, bytes, device);
     if (prev != device) hipSetDevice(prev);
     return rc;
 }

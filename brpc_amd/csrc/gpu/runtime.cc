@@ -2,6 +2,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <pthread.h>
+#include <sys/prctl.h>
 #include <time.h>
 
 #include <atomic>
@@ -14,10 +15,12 @@
 #include "base/logging.h"
 #include "fiber/butex.h"
 #include "fiber/fiber.h"
+#include "gpu/hbm_pool.h"
 #include "rdma/rdma.h"
 
 DEFINE_int32(gpu_streams_per_device, 4, "HIP streams per device in the pool (<= GPU_MAX_HW_QUEUES)");
-DEFINE_int32(gpu_poller_spin_us, 20, "event poller busy-polls this long before backing off");
+DEFINE_int32(gpu_poller_spin_us, 50, "event poller busy-polls this long after the last completion before backing off");
+DEFINE_int32(gpu_poller_sleep_us, 2, "event poller sleep between polls once the spin budget is spent");
 
 namespace mrpc {
 namespace gpu {
@@ -60,6 +63,8 @@ void put_event(hipEvent_t e) {
 }
 
 // ---- completion poller: fibers park on a butex, one pthread polls events.
+// The poller stores 1 (completed) or -1 (failed) into *butex and wakes
+// every fiber/pthread parked on it, so one event can release a whole batch.
 struct Waiter {
     hipEvent_t ev;
     std::atomic<int>* butex;
@@ -81,6 +86,9 @@ public:
 private:
     static void* run(void* arg) {
         pthread_setname_np(pthread_self(), "gpu_poller");
+        // the back-off sleeps are a few microseconds: without this the
+        // kernel rounds each one up to the default 50 us timer slack
+        prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
         static_cast<EventPoller*>(arg)->loop();
         return nullptr;
     }
@@ -106,9 +114,8 @@ private:
                     active[keep++] = active[i];
                     continue;
                 }
-                // done (or failed: wake anyway, the waiter re-queries)
-                active[i].butex->store(1, std::memory_order_release);
-                fiber::butex_wake(active[i].butex);
+                active[i].butex->store(r == hipSuccess ? 1 : -1, std::memory_order_release);
+                fiber::butex_wake_all(active[i].butex);
                 _polled.fetch_add(1, std::memory_order_relaxed);
             }
             active.resize(keep);
@@ -119,7 +126,7 @@ private:
                 const int64_t now_us = now.tv_sec * 1000000LL + now.tv_nsec / 1000;
                 if (progressed) last_progress_us = now_us;
                 if (now_us - last_progress_us > FLAGS_gpu_poller_spin_us) {
-                    timespec ts{0, 2000};  // 2us back-off once the spin budget is spent
+                    timespec ts{0, 1000L * std::max(1, FLAGS_gpu_poller_sleep_us)};
                     nanosleep(&ts, nullptr);
                 }
             }
@@ -247,8 +254,16 @@ int WaitEvent(hipEvent_t ev) {
     b->store(0, std::memory_order_relaxed);
     poller()->add(Waiter{ev, b});
     while (b->load(std::memory_order_acquire) == 0) fiber::butex_wait(b, 0);
+    const int v = b->load(std::memory_order_acquire);
     fiber::butex_destroy(b);
-    return hipEventQuery(ev) == hipSuccess ? 0 : -1;
+    return v == 1 ? 0 : -1;
+}
+
+void WatchEvent(hipEvent_t ev, std::atomic<int>* butex) { poller()->add(Waiter{ev, butex}); }
+
+hipEvent_t AcquireEvent() { return get_event(); }
+void ReleaseEvent(hipEvent_t e) {
+    if (e) put_event(e);
 }
 
 int SyncStream(hipStream_t s) {
@@ -295,26 +310,19 @@ void HostFreePinned(void* p) {
     if (p) hipHostFree(p);
 }
 
-static void* pinned_alloc(size_t n) {
-    void* p = HostMallocPinned(n);
-    return p ? p : malloc(n);  // never fail a socket read for lack of pinned memory
-}
-
-static void pinned_dealloc(void* p, size_t) {
-    // hipHostFree on a malloc'ed pointer fails harmlessly; distinguish anyway
-    hipPointerAttribute_t attr;
-    if (hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost) {
-        hipHostFree(p);
-    } else {
-        free(p);
-    }
-}
+// Socket blocks come from the pinned slab pool (gpu/hbm_pool.cc); the
+// pool never falls back to pageable memory, so the kind tag stays true.
+static void* pinned_alloc(size_t n) { return PinnedAlloc(n); }
+static void pinned_dealloc(void* p, size_t n) { PinnedFree(p, n); }
 
 int UsePinnedBlocks() {
     if (!Available()) return -1;
-    SetBlockMemAllocator(BlockMemAllocator{pinned_alloc, pinned_dealloc, MemKind::PINNED});
+    static std::once_flag once;
+    std::call_once(once, [] { SetBlockMemAllocator(BlockMemAllocator{pinned_alloc, pinned_dealloc, MemKind::PINNED}); });
     return 0;
 }
+
+bool PinnedBlocksInUse() { return GetBlockMemAllocator().kind == MemKind::PINNED; }
 
 static int copy_impl(void* dst, const void* src, size_t n, hipMemcpyKind kind, int device) {
     if (n == 0) return 0;
@@ -341,8 +349,6 @@ int Memset(void* dst, int value, size_t n, int device) {
     return SyncStream(s);
 }
 
-static void free_device_block(void* p, void*) { Free(p); }
-
 int AppendDevice(Buf* b, void* dev, size_t n, int device, void (*deleter)(void*, void*), void* arg) {
     if (device < 0) device = CurrentDevice();
     return b->append_user_data(dev, n, deleter, arg, MemKind::DEVICE, device);
@@ -350,14 +356,18 @@ int AppendDevice(Buf* b, void* dev, size_t n, int device, void (*deleter)(void*,
 
 int AppendHostAsDevice(Buf* b, const void* data, size_t n, int device, std::string* error) {
     if (device < 0) device = CurrentDevice();
-    void* d = Malloc(n, device, error);
-    if (!d) return -1;
+    Buf tmp;
+    void* d = AppendNewDeviceBlock(&tmp, n, device);
+    if (!d) {
+        if (error) *error = "HBM allocation failed";
+        return -1;
+    }
     if (CopyHostToDevice(d, data, n, device) != 0) {
-        Free(d);
         if (error) *error = "host->device copy failed";
         return -1;
     }
-    return b->append_user_data(d, n, free_device_block, nullptr, MemKind::DEVICE, device);
+    b->append(std::move(tmp));
+    return 0;
 }
 
 int GatherToDevice(const Buf& in, Buf* out, int device, std::string* error) {
@@ -369,26 +379,30 @@ int GatherToDevice(const Buf& in, Buf* out, int device, std::string* error) {
         out->append(in);
         return 0;
     }
-    char* d = static_cast<char*>(Malloc(n, device, error));
-    if (!d) return -1;
+    Buf tmp;
+    char* d = static_cast<char*>(AppendNewDeviceBlock(&tmp, n, device));
+    if (!d) {
+        if (error) *error = "HBM allocation failed";
+        return -1;
+    }
     hipStream_t s = PoolStream(device);
     size_t off = 0;
     for (size_t i = 0; i < in.backing_block_num(); ++i) {
         const BlockRef& r = in.ref_at(i);
         const hipMemcpyKind k = IsHostAccessible(r.block->kind) ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
         if (hipMemcpyAsync(d + off, r.block->data + r.offset, r.length, k, s) != hipSuccess) {
-            Free(d);
             if (error) *error = "gather copy failed";
+            SyncStream(s);  // earlier copies may still target d
             return -1;
         }
         off += r.length;
     }
     if (SyncStream(s) != 0) {
-        Free(d);
         if (error) *error = "gather sync failed";
         return -1;
     }
-    return out->append_user_data(d, n, free_device_block, nullptr, MemKind::DEVICE, device);
+    out->append(std::move(tmp));
+    return 0;
 }
 
 bool HasDeviceBlocks(const Buf& b) { return !b.all_host_accessible(); }

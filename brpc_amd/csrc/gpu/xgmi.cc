@@ -17,28 +17,32 @@
 
 #include "base/flags.h"
 #include "base/logging.h"
+#include "base/time.h"
+#include "gpu/copy_engine.h"
 #include "gpu/gpu.h"
+#include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
 #include "mrpc/proto/rpc_meta.pb.h"
 #include "net/socket.h"
 #include "policy/device_payload.h"
 #include "var/var.h"
 
-DEFINE_int32(xgmi_arena_mb, 256, "HBM arena per device for outgoing device payloads (MiB)");
-DEFINE_int32(xgmi_slots, 65536, "release-table slots per arena (max in-flight payload regions)");
+DEFINE_int32(xgmi_slots, 65536, "release-table slots per process (max payload blocks lent at once)");
+DEFINE_int32(xgmi_dead_peer_reap_ms, 2000,
+             "lent blocks whose connection failed are reclaimed after this long (the peer may still be pulling)");
 
 namespace mrpc {
 namespace gpu {
 
 namespace {
 
-const uint64_t kShmMagic = 0x58474d4952454c31ull;  // "XGMIREL1"
+const uint64_t kShmMagic = 0x58474d4952454c32ull;  // "XGMIREL2"
 
 struct ShmTable {
     uint64_t magic;
     uint32_t nslots;
     uint32_t pad;
-    std::atomic<uint64_t> released[1];  // nslots entries: seq of the released region
+    std::atomic<uint64_t> released[1];  // nslots entries: seq of the released lend
 };
 
 size_t shm_bytes(uint32_t nslots) { return sizeof(ShmTable) + sizeof(uint64_t) * (nslots - 1); }
@@ -55,26 +59,17 @@ std::string boot_id() {
     return id;
 }
 
-std::atomic<int64_t> g_sent_bytes{0}, g_recv_bytes{0}, g_sent_payloads{0}, g_recv_payloads{0}, g_ring_full{0},
-    g_crc_fail{0};
+std::atomic<int64_t> g_sent_bytes{0}, g_recv_bytes{0}, g_sent_payloads{0}, g_recv_payloads{0}, g_busy{0},
+    g_crc_fail{0}, g_copied_in{0}, g_released_unconsumed{0};
 
-// ------------------------------------------------------------------ arena
-class Arena {
+// ------------------------------------------------------------------ lending
+// The process-wide table of blocks lent to peers. A slot holds a Buf that
+// references the lent bytes until the borrower writes the slot's seq into
+// released[slot] (shared memory) — or the connection is gone for good.
+class Lender {
 public:
     int init(int device, std::string* err) {
         _device = device;
-        _size = (size_t)FLAGS_xgmi_arena_mb << 20;
-        _base = static_cast<char*>(Malloc(_size, device, err));
-        if (!_base) return -1;
-        int prev = 0;
-        hipGetDevice(&prev);
-        hipSetDevice(device);
-        const hipError_t r = hipIpcGetMemHandle(&_handle, _base);
-        hipSetDevice(prev);
-        if (r != hipSuccess) {
-            if (err) *err = std::string("hipIpcGetMemHandle: ") + hipGetErrorString(r);
-            return -1;
-        }
         _nslots = (uint32_t)std::max(1024, FLAGS_xgmi_slots);
         _shm_name = "/mrpc_xgmi_" + std::to_string(getpid()) + "_" + std::to_string(device);
         const int fd = shm_open(_shm_name.c_str(), O_CREAT | O_RDWR, 0600);
@@ -98,89 +93,127 @@ public:
         _table->magic = kShmMagic;
         _table->nslots = _nslots;
         for (uint32_t i = 0; i < _nslots; ++i) _table->released[i].store(0, std::memory_order_relaxed);
-        static std::once_flag unlink_once;
-        std::call_once(unlink_once, [] { atexit([] { Arena::unlink_all(); }); });
+        _slots.resize(_nslots);
+        _free.reserve(_nslots);
+        for (uint32_t i = _nslots; i > 0; --i) _free.push_back(i - 1);
+        atexit([] { Lender::unlink_all(); });
         registry().push_back(_shm_name);
         return 0;
     }
 
-    // Reserve `len` bytes; returns false when the ring is full.
-    bool alloc(size_t len, uint64_t* off, uint32_t* slot, uint64_t* seq) {
-        const size_t need = (len + 255) & ~(size_t)255;
-        std::lock_guard<std::mutex> g(_mu);
-        while (!_q.empty() && _table->released[_q.front().slot].load(std::memory_order_acquire) == _q.front().seq) {
-            _q.pop_front();
-        }
-        if (_q.size() >= _nslots || need > _size) return false;
-        size_t at;
-        if (_q.empty()) {
-            at = 0;  // everything released: restart at the bottom
-        } else {
-            const size_t tail = _q.front().off;  // oldest live region
-            if (_head > tail) {
-                // live = [tail, head); free = [head, size) + [0, tail)
-                if (_size - _head >= need) at = _head;
-                else if (tail > need) at = 0;  // wrap; keep head != tail
-                else return false;
-            } else {
-                // wrapped: live = [tail, size) + [0, head); free = [head, tail)
-                if (tail - _head > need) at = _head;
-                else return false;
+    // Lend `hold` (one reference to the bytes) to the peer behind `sock_id`.
+    bool lend(Buf&& hold, SocketId sock_id, uint32_t* slot, uint64_t* seq) {
+        std::vector<Buf> dead;
+        bool ok = false;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            reap_locked(&dead, false);
+            if (_free.empty()) reap_locked(&dead, true);
+            if (!_free.empty()) {
+                const uint32_t s = _free.back();
+                _free.pop_back();
+                Slot& e = _slots[s];
+                e.hold = std::move(hold);
+                e.seq = ++_next_seq;
+                e.sock = sock_id;
+                e.since_us = monotonic_us();
+                _outstanding.push_back(s);
+                *slot = s;
+                *seq = e.seq;
+                ok = true;
             }
         }
-        _head = at + need;
-        Region r{at, need, _next_slot, ++_next_seq};
-        _next_slot = (_next_slot + 1) % _nslots;
-        _q.push_back(r);
-        *off = at;
-        *slot = r.slot;
-        *seq = r.seq;
-        return true;
+        return ok;  // `dead` drops its references outside the lock
     }
 
-    char* base() const { return _base; }
-    size_t size() const { return _size; }
-    int device() const { return _device; }
+    // Sender-side give-back of a lend that never left this process.
+    void cancel(uint32_t slot, uint64_t seq) {
+        if (slot < _nslots) _table->released[slot].store(seq, std::memory_order_release);
+    }
+
+    void reap(bool full) {
+        std::vector<Buf> dead;
+        std::lock_guard<std::mutex> g(_mu);
+        reap_locked(&dead, full);
+    }
+
+    int64_t outstanding() {
+        std::lock_guard<std::mutex> g(_mu);
+        return (int64_t)_outstanding.size();
+    }
+
     ShmTable* table() const { return _table; }
-    void fill(policy::XgmiHello* h) const {
-        h->set_ipc_handle(std::string(reinterpret_cast<const char*>(&_handle), sizeof(_handle)));
-        h->set_device(_device);
-        h->set_arena_size((int64_t)_size);
-        h->set_pid(getpid());
-        h->set_shm_name(_shm_name);
-        h->set_nslots(_nslots);
-        h->set_host_id(boot_id());
+    uint32_t nslots() const { return _nslots; }
+    const std::string& shm_name() const { return _shm_name; }
+    int device() const { return _device; }
+
+private:
+    struct Slot {
+        Buf hold;
+        uint64_t seq = 0;
+        SocketId sock = 0;
+        int64_t since_us = 0;
+    };
+
+    bool released(uint32_t s) const {
+        return _table->released[s].load(std::memory_order_acquire) == _slots[s].seq;
+    }
+    void free_slot(uint32_t s, std::vector<Buf>* dead) {
+        dead->emplace_back(std::move(_slots[s].hold));
+        _slots[s].hold.clear();
+        _free.push_back(s);
+    }
+    // Cheap pass: pop released slots from the front (borrowers release in
+    // roughly FIFO order). Full pass (slots exhausted, the outstanding list
+    // grew large, or every 100 ms while something is stuck at the front):
+    // compact the list, also reclaiming lends of connections that failed
+    // more than xgmi_dead_peer_reap_ms ago.
+    void reap_locked(std::vector<Buf>* dead, bool full) {
+        while (!_outstanding.empty() && released(_outstanding.front())) {
+            free_slot(_outstanding.front(), dead);
+            _outstanding.pop_front();
+        }
+        if (_outstanding.empty()) return;
+        const int64_t now = monotonic_us();
+        if (!full && _outstanding.size() < _next_full_scan && now - _last_full_us < 100000) return;
+        _last_full_us = now;
+        std::deque<uint32_t> keep;
+        for (uint32_t s : _outstanding) {
+            bool drop = released(s);
+            if (!drop && now - _slots[s].since_us > (int64_t)FLAGS_xgmi_dead_peer_reap_ms * 1000) {
+                SocketUniquePtr p;
+                drop = Socket::Address(_slots[s].sock, &p) != 0;
+            }
+            if (drop) free_slot(s, dead);
+            else keep.push_back(s);
+        }
+        _outstanding.swap(keep);
+        _next_full_scan = std::max<size_t>(1024, _outstanding.size() * 2);
+    }
+
+    static std::vector<std::string>& registry() {
+        static std::vector<std::string>* v = new std::vector<std::string>;
+        return *v;
     }
     static void unlink_all() {
         for (const std::string& n : registry()) shm_unlink(n.c_str());
     }
 
-private:
-    static std::vector<std::string>& registry() {
-        static std::vector<std::string>* v = new std::vector<std::string>;
-        return *v;
-    }
-    struct Region {
-        size_t off, len;
-        uint32_t slot;
-        uint64_t seq;
-    };
     int _device = -1;
-    char* _base = nullptr;
-    size_t _size = 0;
-    hipIpcMemHandle_t _handle;
     uint32_t _nslots = 0;
     std::string _shm_name;
     ShmTable* _table = nullptr;
     std::mutex _mu;
-    std::deque<Region> _q;
-    size_t _head = 0;
-    uint32_t _next_slot = 0;
+    std::vector<Slot> _slots;
+    std::vector<uint32_t> _free;
+    std::deque<uint32_t> _outstanding;
     uint64_t _next_seq = 0;
+    size_t _next_full_scan = 1024;
+    int64_t _last_full_us = 0;
 };
 
 std::mutex g_mu;
-Arena* g_arena = nullptr;  // the enabled device's arena
+Lender* g_lender = nullptr;  // the enabled device's lender
 int g_device = -1;
 
 // ------------------------------------------------------------------ peers
@@ -188,6 +221,7 @@ struct PeerMap {
     char* base = nullptr;
     size_t size = 0;
     ShmTable* table = nullptr;
+    uint32_t nslots = 0;  // slots covered by the mapping (from the hello)
     size_t table_bytes = 0;
     bool local = false;
 };
@@ -203,18 +237,20 @@ std::shared_ptr<PeerMap> map_peer(const policy::XgmiHello& h, std::string* err) 
     if (it != g_peers.end()) return it->second;
     auto pm = std::make_shared<PeerMap>();
     if (h.pid() == getpid()) {
-        if (!g_arena || h.device() != g_arena->device()) {
+        const ArenaDesc a = GetArena(g_device);
+        if (!g_lender || h.device() != g_device || !a.base) {
             if (err) *err = "local arena mismatch";
             return nullptr;
         }
-        pm->base = g_arena->base();
-        pm->size = g_arena->size();
-        pm->table = g_arena->table();
+        pm->base = a.base;
+        pm->size = a.size;
+        pm->table = g_lender->table();
+        pm->nslots = g_lender->nslots();
         pm->local = true;
     } else {
         hipIpcMemHandle_t handle;
-        if (h.ipc_handle().size() != sizeof(handle)) {
-            if (err) *err = "bad ipc handle size";
+        if (h.ipc_handle().size() != sizeof(handle) || h.nslots() == 0 || h.arena_size() <= 0) {
+            if (err) *err = "bad xgmi hello";
             return nullptr;
         }
         memcpy(&handle, h.ipc_handle().data(), sizeof(handle));
@@ -235,9 +271,18 @@ std::shared_ptr<PeerMap> map_peer(const policy::XgmiHello& h, std::string* err) 
             return nullptr;
         }
         const size_t bytes = shm_bytes(h.nslots());
+        struct stat st;
+        if (fstat(fd, &st) != 0 || (size_t)st.st_size < bytes) {
+            close(fd);
+            hipIpcCloseMemHandle(p);
+            if (err) *err = "peer release table is smaller than announced";
+            return nullptr;
+        }
         void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
         close(fd);
-        if (m == MAP_FAILED || static_cast<ShmTable*>(m)->magic != kShmMagic) {
+        if (m == MAP_FAILED || static_cast<ShmTable*>(m)->magic != kShmMagic ||
+            static_cast<ShmTable*>(m)->nslots != h.nslots()) {
+            if (m != MAP_FAILED) munmap(m, bytes);
             hipIpcCloseMemHandle(p);
             if (err) *err = "bad peer release table";
             return nullptr;
@@ -245,6 +290,7 @@ std::shared_ptr<PeerMap> map_peer(const policy::XgmiHello& h, std::string* err) 
         pm->base = static_cast<char*>(p);
         pm->size = (size_t)h.arena_size();
         pm->table = static_cast<ShmTable*>(m);
+        pm->nslots = h.nslots();
         pm->table_bytes = bytes;
     }
     g_peers[key] = pm;
@@ -258,39 +304,53 @@ public:
     std::shared_ptr<PeerMap> peer;
 };
 
+PeerMap* peer_of(Socket* sock, std::shared_ptr<Transport>* keep) {
+    *keep = sock ? sock->transport() : nullptr;
+    XgmiEndpoint* ep = dynamic_cast<XgmiEndpoint*>(keep->get());
+    return ep ? ep->peer.get() : nullptr;
+}
+
 // ------------------------------------------------------------------ hooks
-int xgmi_send(Socket* sock, const void* dev_ptr, size_t len, int device, bool with_crc, policy::DevicePayload* d) {
-    Arena* a = g_arena;
-    if (!a) return -1;
-    uint64_t off = 0, seq = 0;
-    uint32_t slot = 0;
-    if (!a->alloc(len, &off, &slot, &seq)) {
-        g_ring_full.fetch_add(1, std::memory_order_relaxed);
-        return 1;  // ring full: the caller stages this block through host memory
-    }
-    // a region that never reaches the peer must still be released, or the
-    // FIFO ring would stall behind it forever
-    auto give_back = [&] { a->table()->released[slot].store(seq, std::memory_order_release); };
-    hipStream_t s = PoolStream(a->device());
-    if (!s || hipMemcpyAsync(a->base() + off, dev_ptr, len, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-        SyncStream(s) != 0) {
-        give_back();
-        return -1;
+int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, bool with_crc, policy::DevicePayload* d) {
+    Lender* l = g_lender;
+    if (!l) return -1;
+    if (block->device != g_device) return 1;  // another GPU's block: stage it
+    const char* src = block->data + offset;
+    int64_t aoff = ArenaOffset(src, g_device);
+    Buf hold;
+    if (aoff < 0) {
+        // not arena memory (a tensor, a user hipMalloc): one copy into a
+        // lendable block, then lend that
+        void* p = AppendNewDeviceBlock(&hold, len, g_device);
+        aoff = p ? ArenaOffset(p, g_device) : -1;
+        if (aoff < 0) {
+            g_busy.fetch_add(1, std::memory_order_relaxed);
+            return 1;
+        }
+        Segment seg{src, p, len};
+        if (BatchedCopy(&seg, 1, g_device) != 0) return -1;
+        g_copied_in.fetch_add(1, std::memory_order_relaxed);
+        src = static_cast<const char*>(p);
+    } else {
+        hold.append_block(block, offset, len);
     }
     if (with_crc) {
-        const void* p = a->base() + off;
-        uint64_t l = len;
+        const void* p = src;
+        uint64_t l64 = len;
         uint32_t crc = 0;
-        if (Crc32cDevice(&p, &l, 1, &crc, a->device()) != 0) {
-            give_back();
-            return -1;
-        }
+        if (Crc32cDevice(&p, &l64, 1, &crc, g_device) != 0) return -1;
         d->set_crc32c(crc);
         d->set_has_crc(true);
     }
-    d->set_ring_offset((int64_t)off);
+    uint32_t slot = 0;
+    uint64_t seq = 0;
+    if (!l->lend(std::move(hold), sock->id(), &slot, &seq)) {
+        g_busy.fetch_add(1, std::memory_order_relaxed);
+        return 1;  // every slot is out: the caller stages this block inline
+    }
+    d->set_ring_offset(aoff);
     d->set_length((int64_t)len);
-    d->set_src_device(device);
+    d->set_src_device(g_device);
     d->set_slot(slot);
     d->set_seq(seq);
     g_sent_bytes.fetch_add((int64_t)len, std::memory_order_relaxed);
@@ -298,122 +358,117 @@ int xgmi_send(Socket* sock, const void* dev_ptr, size_t len, int device, bool wi
     return 0;
 }
 
-void pool_deleter(void* p, void*) { PoolFree(p); }
+void release_in(PeerMap* pm, const policy::DevicePayload& d) {
+    if (pm && d.slot() < pm->nslots) pm->table->released[d.slot()].store(d.seq(), std::memory_order_release);
+}
 
-int xgmi_recv(Socket* sock, const policy::DevicePayload& d, Buf* out) {
-    std::shared_ptr<Transport> t = sock->transport();
-    XgmiEndpoint* ep = dynamic_cast<XgmiEndpoint*>(t.get());
-    if (!ep || !ep->peer) return -1;
-    PeerMap* pm = ep->peer.get();
-    const size_t len = (size_t)d.length();
-    if (d.ring_offset() < 0 || (size_t)d.ring_offset() + len > pm->size || d.slot() >= pm->table->nslots) return -1;
-    void* dst = PoolAlloc(len, g_device);
-    if (!dst) return -1;
-    hipStream_t s = PoolStream(g_device);
-    if (!s || hipMemcpyAsync(dst, pm->base + d.ring_offset(), len, hipMemcpyDeviceToDevice, s) != hipSuccess ||
-        SyncStream(s) != 0) {
-        PoolFree(dst);
+int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Buf* outs) {
+    std::shared_ptr<Transport> keep;
+    PeerMap* pm = peer_of(sock, &keep);
+    if (!pm) return -1;
+    std::vector<Segment> segs;
+    segs.reserve(n);
+    int rc = 0;
+    for (int i = 0; i < n && rc == 0; ++i) {
+        const policy::DevicePayload& d = *descs[i];
+        const int64_t off = d.ring_offset(), len = d.length();
+        if (off < 0 || len < 0 || (uint64_t)off > pm->size || (uint64_t)len > pm->size - (uint64_t)off ||
+            d.slot() >= pm->nslots) {
+            rc = -1;
+            break;
+        }
+        if (len == 0) continue;
+        void* dst = AppendNewDeviceBlock(&outs[i], (size_t)len, g_device);
+        if (!dst) {
+            rc = -1;
+            break;
+        }
+        segs.push_back(Segment{pm->base + off, dst, (uint64_t)len});
+    }
+    if (rc == 0) rc = BatchedCopy(segs.data(), (int)segs.size(), g_device);
+    // the bytes are ours now (or never will be): give every region back
+    for (int i = 0; i < n; ++i) release_in(pm, *descs[i]);
+    if (rc != 0) {
+        for (int i = 0; i < n; ++i) outs[i].clear();
         return -1;
     }
-    // the bytes are ours now: give the region back to the sender
-    pm->table->released[d.slot()].store(d.seq(), std::memory_order_release);
-    if (d.has_crc()) {
-        const void* p = dst;
-        uint64_t l = len;
-        uint32_t crc = 0;
-        if (Crc32cDevice(&p, &l, 1, &crc, g_device) != 0 || crc != d.crc32c()) {
-            g_crc_fail.fetch_add(1, std::memory_order_relaxed);
-            PoolFree(dst);
-            return -1;
+    for (int i = 0; i < n; ++i) {
+        const policy::DevicePayload& d = *descs[i];
+        if (d.has_crc()) {
+            uint32_t crc = 0;
+            if (Crc32cOfBuf(outs[i], &crc, g_device) != 0 || crc != d.crc32c()) {
+                g_crc_fail.fetch_add(1, std::memory_order_relaxed);
+                for (int k = 0; k < n; ++k) outs[k].clear();
+                return -1;
+            }
         }
+        g_recv_bytes.fetch_add(d.length(), std::memory_order_relaxed);
     }
-    out->append_user_data(dst, len, pool_deleter, nullptr, MemKind::DEVICE, g_device);
-    g_recv_bytes.fetch_add((int64_t)len, std::memory_order_relaxed);
-    g_recv_payloads.fetch_add(1, std::memory_order_relaxed);
+    g_recv_payloads.fetch_add(n, std::memory_order_relaxed);
     return 0;
 }
 
-// ------------------------------------------------------------------ pool
-struct PoolState {
-    std::mutex mu;
-    std::map<size_t, std::vector<void*>> free;  // size class -> blocks
-    std::map<void*, std::pair<size_t, int>> live;  // ptr -> (class, device)
-};
-PoolState& pool() {
-    static PoolState* p = new PoolState;
-    return *p;
+void xgmi_release(Socket* sock, const policy::DevicePayload& d) {
+    std::shared_ptr<Transport> keep;
+    PeerMap* pm = peer_of(sock, &keep);
+    if (!pm) return;
+    release_in(pm, d);
+    g_released_unconsumed.fetch_add(1, std::memory_order_relaxed);
 }
 
-size_t size_class(size_t n) {
-    size_t c = 4096;
-    while (c < n) c <<= 1;
-    return c;
+void xgmi_cancel(const policy::DevicePayload& d) {
+    if (g_lender) g_lender->cancel(d.slot(), d.seq());
 }
 
 }  // namespace
 
-void* PoolAlloc(size_t n, int device) {
-    const size_t c = size_class(n);
-    PoolState& ps = pool();
-    {
-        std::lock_guard<std::mutex> g(ps.mu);
-        auto& v = ps.free[c * 64 + (size_t)device];  // classes are multiples of 4096: room for the device
-        if (!v.empty()) {
-            void* p = v.back();
-            v.pop_back();
-            ps.live[p] = {c, device};
-            return p;
-        }
-    }
-    void* p = Malloc(c, device);
-    if (!p) return nullptr;
-    std::lock_guard<std::mutex> g(ps.mu);
-    ps.live[p] = {c, device};
-    return p;
-}
-
-void PoolFree(void* p) {
-    if (!p) return;
-    PoolState& ps = pool();
-    std::lock_guard<std::mutex> g(ps.mu);
-    auto it = ps.live.find(p);
-    if (it == ps.live.end()) return;
-    ps.free[it->second.first * 64 + (size_t)it->second.second].push_back(p);
-    ps.live.erase(it);
-}
-
 int EnableXgmiTransport(int device, std::string* error) {
     std::lock_guard<std::mutex> g(g_mu);
-    if (g_arena) return g_arena->device() == device || device < 0 ? 0 : -1;
+    if (g_lender) return g_lender->device() == device || device < 0 ? 0 : -1;
     if (device < 0) device = CurrentDevice();
-    if (Init(device, error) != 0) return -1;
-    Arena* a = new Arena;
-    if (a->init(device, error) != 0) {
-        delete a;
+    if (Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
+    Lender* l = new Lender;
+    if (l->init(device, error) != 0) {
+        delete l;
         return -1;
     }
+    UsePinnedBlocks();
     g_device = device;
-    g_arena = a;
+    g_lender = l;
     DeviceTransportHooks h;
     h.send = xgmi_send;
     h.recv = xgmi_recv;
+    h.release = xgmi_release;
+    h.cancel = xgmi_cancel;
     SetDeviceTransportHooks(h);
     static var::PassiveStatus<int64_t> v1("xgmi_sent_bytes", [] { return g_sent_bytes.load(); });
     static var::PassiveStatus<int64_t> v2("xgmi_recv_bytes", [] { return g_recv_bytes.load(); });
-    static var::PassiveStatus<int64_t> v3("xgmi_ring_full_fallbacks", [] { return g_ring_full.load(); });
+    static var::PassiveStatus<int64_t> v3("xgmi_busy_fallbacks", [] { return g_busy.load(); });
+    static var::PassiveStatus<int64_t> v4("xgmi_lent_outstanding",
+                                          [] { return g_lender ? g_lender->outstanding() : 0; });
+    static var::PassiveStatus<int64_t> v5("xgmi_copy_launches", [] { return GetCopyEngineStats().launches; });
     return 0;
 }
 
-bool XgmiEnabled() { return g_arena != nullptr; }
+bool XgmiEnabled() { return g_lender != nullptr; }
+int XgmiDevice() { return g_device; }
 
-bool FillXgmiHello(policy::XgmiHello* hello) {
-    if (!g_arena) return false;
-    g_arena->fill(hello);
+bool FillXgmiHello(policy::XgmiHello* h) {
+    if (!g_lender) return false;
+    const ArenaDesc a = GetArena(g_device);
+    if (!a.base) return false;
+    h->set_ipc_handle(a.ipc_handle);
+    h->set_device(g_device);
+    h->set_arena_size((int64_t)a.size);
+    h->set_pid(getpid());
+    h->set_shm_name(g_lender->shm_name());
+    h->set_nslots(g_lender->nslots());
+    h->set_host_id(boot_id());
     return true;
 }
 
 int AttachXgmiPeer(Socket* sock, const policy::XgmiHello& hello, std::string* error) {
-    if (!g_arena) {
+    if (!g_lender) {
         if (error) *error = "xgmi transport is not enabled in this process";
         return -1;
     }
@@ -428,14 +483,21 @@ int AttachXgmiPeer(Socket* sock, const policy::XgmiHello& hello, std::string* er
     return 0;
 }
 
+void ReapLentBlocks() {
+    if (g_lender) g_lender->reap(true);
+}
+
 XgmiStats GetXgmiStats() {
     XgmiStats s;
     s.sent_bytes = g_sent_bytes.load();
     s.recv_bytes = g_recv_bytes.load();
     s.sent_payloads = g_sent_payloads.load();
     s.recv_payloads = g_recv_payloads.load();
-    s.ring_full_fallbacks = g_ring_full.load();
+    s.ring_full_fallbacks = g_busy.load();
     s.crc_failures = g_crc_fail.load();
+    s.lent_outstanding = g_lender ? g_lender->outstanding() : 0;
+    s.copied_into_arena = g_copied_in.load();
+    s.released_unconsumed = g_released_unconsumed.load();
     return s;
 }
 

@@ -1,18 +1,25 @@
 // xGMI device transport: HBM payloads move GPU-to-GPU over xGMI while only
 // the RPC metadata travels on the TCP connection (the MI355X analog of the
-// reference's RDMA endpoint, src/brpc/rdma/rdma_endpoint.cpp +
-// block_pool.cpp, which zero-copies IOBuf blocks over verbs).
+// reference's RDMA endpoint, src/brpc/rdma/rdma_endpoint.cpp:771-895, whose
+// SGEs point straight into registered IOBuf blocks).
 //
-// Each process owns one IPC arena per device: a large HBM region exported
-// with hipIpcGetMemHandle plus a POSIX-shm release table. Sending a DEVICE
-// attachment block = one D2D copy into a ring region of the sender's arena;
-// the descriptor (offset, length, slot, seq) rides in RpcMeta. The receiver
-// mapped the sender's arena during the per-connection hello
-// (RpcMeta.xgmi_hello, both directions), pulls the region peer-to-peer into
-// a pooled HBM block of its own device (xGMI DMA), verifies the optional
-// CRC32C on device (MFMA kernel) and writes the region's sequence number
-// into the sender's release table; the sender reclaims its ring in FIFO
-// order. Nothing is sent over TCP for the payload bytes.
+// Zero-copy send, one pull per hop:
+//  * every HBM block the framework allocates comes from the per-device
+//    IPC-exported arena (gpu/hbm_pool.h), which each peer process maps once
+//    during the per-connection hello (RpcMeta.xgmi_hello, both directions);
+//  * sending a DEVICE attachment block LENDS it: the sender takes a
+//    reference, assigns a release slot and puts (arena offset, length, slot,
+//    seq) into RpcMeta.device_payload — no copy, no device work at all.
+//    Blocks from outside the arena (a torch tensor, a user hipMalloc) are
+//    first copied into an arena block;
+//  * the receiver pulls every payload of a message into fresh blocks of its
+//    own arena with the batched copy engine (gpu/copy_engine.h: one kernel
+//    for the payloads of all concurrently arriving messages, reading across
+//    xGMI when the sender sits on another GPU), then writes the seq into the
+//    sender's POSIX-shm release table. The sender reaps released slots and
+//    drops its references; slots whose connection died are reaped too.
+// Received blocks are arena memory again, so a server that forwards or
+// echoes them lends them onward without another copy.
 #pragma once
 
 #include <cstddef>
@@ -31,20 +38,20 @@ namespace gpu {
 // `device` (idempotent). Returns 0, or -1 when no GPU / IPC is available.
 int EnableXgmiTransport(int device, std::string* error = nullptr);
 bool XgmiEnabled();
+int XgmiDevice();
 // Fill the local hello (arena of the enabled device).
 bool FillXgmiHello(policy::XgmiHello* hello);
 // Map the peer described by `hello` and attach the endpoint to `sock`.
 // Same-process peers use the local arena directly. Returns 0 on success.
 int AttachXgmiPeer(Socket* sock, const policy::XgmiHello& hello, std::string* error = nullptr);
-
-// Pooled HBM blocks (size classes) so received payloads never hit hipMalloc
-// on the hot path.
-void* PoolAlloc(size_t n, int device);
-void PoolFree(void* p);
+// Drop references of every lent block the peers have released. Runs on
+// every send; exposed for tests and idle-time housekeeping.
+void ReapLentBlocks();
 
 struct XgmiStats {
     int64_t sent_bytes = 0, recv_bytes = 0, sent_payloads = 0, recv_payloads = 0;
     int64_t ring_full_fallbacks = 0, crc_failures = 0;
+    int64_t lent_outstanding = 0, copied_into_arena = 0, released_unconsumed = 0;
 };
 XgmiStats GetXgmiStats();
 

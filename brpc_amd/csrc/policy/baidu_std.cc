@@ -257,6 +257,7 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
     pb::Message* req = nullptr;
     pb::Message* res = nullptr;
     bool concurrency_added = false;
+    bool device_payload_taken = false;  // pulled, or released by the merge on failure
     const Server::MethodProperty* mp = nullptr;
     do {
         if (!server->IsRunning()) {
@@ -302,6 +303,7 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
         } else {
             req_buf.swap(msg->payload);
         }
+        device_payload_taken = true;
         if (meta.device_payload_size() > 0 &&
             !MergeDevicePayload(cntl, socket, meta, /*request=*/true, &cntl->request_attachment())) {
             break;
@@ -315,6 +317,9 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
         }
         res = mp->service->GetResponsePrototype(mp->method).New();
     } while (false);
+    // rejected before the attachment was looked at: the sender's lent HBM
+    // blocks must still be given back, or they stay pinned on its side
+    if (!device_payload_taken) ReleaseDevicePayload(socket, meta);
     msg->Destroy();
     destroyer.m = nullptr;
     if (!concurrency_added) server = nullptr;  // nothing to remove
@@ -350,17 +355,20 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         return;
     }
     if (meta.has_stream_settings() && !meta.has_correlation_id()) {
+        ReleaseDevicePayload(msg->socket(), meta);
         msg->Destroy();
         return;
     }
     const fiber::CallId cid{(uint64_t)meta.correlation_id()};
     Controller* cntl = nullptr;
     if (fiber::call_id_lock(cid, (void**)&cntl) != 0) {
+        ReleaseDevicePayload(msg->socket(), meta);
         msg->Destroy();  // timed out / canceled / duplicated response
         return;
     }
     if (cid != cntl->current_id() && cid != cntl->_unfinished_call.id) {
         fiber::call_id_unlock(cid);  // response of an obsolete attempt
+        ReleaseDevicePayload(msg->socket(), meta);
         msg->Destroy();
         return;
     }
@@ -371,6 +379,7 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         }
     }
     int saved_error = 0;
+    bool device_payload_taken = false;
     const RpcResponseMeta& rm = meta.response();
     if (rm.error_code() != 0) {
         cntl->_error_code = 0;
@@ -392,9 +401,11 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         } else {
             res_buf.swap(msg->payload);
         }
-        if (!saved_error && meta.device_payload_size() > 0 &&
-            !MergeDevicePayload(cntl, msg->socket(), meta, /*request=*/false, &cntl->response_attachment())) {
-            saved_error = cntl->ErrorCode();
+        if (!saved_error && meta.device_payload_size() > 0) {
+            device_payload_taken = true;
+            if (!MergeDevicePayload(cntl, msg->socket(), meta, /*request=*/false, &cntl->response_attachment())) {
+                saved_error = cntl->ErrorCode();
+            }
         }
         if (!saved_error && meta.has_stream_settings()) OnResponseStreamSettings(cntl, msg->socket(), meta.stream_settings());
         if (!saved_error && cntl->_response &&
@@ -405,6 +416,7 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         }
         if (!saved_error) cntl->set_response_compress_type((CompressType)meta.compress_type());
     }
+    if (!device_payload_taken) ReleaseDevicePayload(msg->socket(), meta);
     cntl->_local_side = msg->socket()->local_side();
     msg->Destroy();
     cntl->OnVersionedRPCReturned(cid, saved_error);

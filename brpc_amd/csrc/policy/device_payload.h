@@ -1,13 +1,18 @@
 // Device (HBM) attachment handling for baidu_std (MI355X-native).
-// An attachment may contain DEVICE/PEER blocks (Buf::append_user_data with
+// An attachment may contain DEVICE blocks (Buf::append_user_data with
 // MemKind::DEVICE). When the socket has a device transport (the xGMI
-// endpoint in gpu/xgmi_transport.cc) those blocks are written straight into
-// the peer GPU's receive ring and described by RpcMeta.device_payload —
-// they never touch the TCP byte stream. Without a transport the blocks are
-// staged to host memory and sent inline (always correct, just slower).
+// endpoint in gpu/xgmi.cc) those blocks are lent to the peer and described
+// by RpcMeta.device_payload — they never touch the TCP byte stream. Without
+// a transport the blocks are staged to host memory and sent inline (always
+// correct, just slower).
+//
+// Every received descriptor must end in exactly one of: a pull
+// (MergeDevicePayload) or a release (ReleaseDevicePayload) — otherwise the
+// sender keeps the lent block until the connection dies.
 #pragma once
 
 #include <cstddef>
+#include <cstdint>
 
 #include "base/buf.h"
 
@@ -21,13 +26,19 @@ class DevicePayload;
 }  // namespace policy
 
 struct DeviceTransportHooks {
-    // Copy [dev_ptr, dev_ptr+len) on `device` into the peer ring of `sock`.
-    // Fill desc (ring_offset/length/src_device). 0 on success, >0 when the
-    // transport cannot take the block right now (sent inline instead), <0 on
-    // error.
-    int (*send)(Socket* sock, const void* dev_ptr, size_t len, int device, bool with_crc, policy::DevicePayload* desc) = nullptr;
-    // Append a block referencing the received ring region to *out.
-    int (*recv)(Socket* sock, const policy::DevicePayload& desc, Buf* out) = nullptr;
+    // Lend [block->data+offset, +len) to the peer of `sock` and fill desc
+    // (ring_offset/length/slot/seq/src_device). 0 on success, >0 when the
+    // transport cannot take the block right now (sent inline instead), <0
+    // on error.
+    int (*send)(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, bool with_crc,
+                policy::DevicePayload* desc) = nullptr;
+    // Pull the n described payloads into fresh local HBM blocks (outs[i]
+    // receives payload i) and release them to the sender. 0 on success.
+    int (*recv)(Socket* sock, const policy::DevicePayload* const* descs, int n, Buf* outs) = nullptr;
+    // The receiver will not consume `desc`: give it back to the sender.
+    void (*release)(Socket* sock, const policy::DevicePayload& desc) = nullptr;
+    // The sender lent `desc` but the message carrying it is never sent.
+    void (*cancel)(const policy::DevicePayload& desc) = nullptr;
 };
 void SetDeviceTransportHooks(const DeviceTransportHooks& h);
 bool HasDeviceTransport(Socket* sock);
@@ -39,6 +50,12 @@ namespace policy {
 bool SplitDevicePayload(Controller* cntl, bool request, const Buf& attachment, Buf* host_out, RpcMeta* meta,
                         Socket* sock = nullptr);
 bool MergeDevicePayload(Controller* cntl, Socket* sock, const RpcMeta& meta, bool request, Buf* attachment);
+// Give back every device payload of `meta` without pulling it (rejected
+// requests, stale or failed responses).
+void ReleaseDevicePayload(Socket* sock, const RpcMeta& meta);
+// Un-lend the payloads a sender put into `meta` for a message it will not
+// send after all.
+void CancelDevicePayload(const RpcMeta& meta);
 }  // namespace policy
 
 }  // namespace mrpc

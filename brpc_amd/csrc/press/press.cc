@@ -13,6 +13,7 @@
 #include "pb/dynamic.h"
 #include "pb/parser.h"
 #include "gpu/gpu.h"
+#include "gpu/hbm_pool.h"
 #include "rpc/channel.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
@@ -60,7 +61,7 @@ PressSession::PressSession() {}
 
 PressSession::~PressSession() {
     _channels.clear();
-    if (_device_attachment) gpu::Free(_device_attachment);
+    if (_device_attachment) gpu::HbmFree(_device_attachment, _attachment.size(), _opt.gpu_device);
 }
 
 static bool read_file(const std::string& path, std::string* out) {
@@ -202,8 +203,13 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
             }
             if (_opt.device_attachment) {
                 if (gpu::Init(_opt.gpu_device, error) != 0) return -1;
-                _device_attachment = gpu::Malloc(_attachment.size(), _opt.gpu_device, error);
-                if (!_device_attachment) return -1;
+                // arena memory: the xGMI transport lends it to the server
+                // without a copy (gpu/xgmi.h)
+                _device_attachment = gpu::HbmAlloc(_attachment.size(), _opt.gpu_device);
+                if (!_device_attachment) {
+                    *error = "fail to allocate the HBM attachment";
+                    return -1;
+                }
                 if (gpu::CopyHostToDevice(_device_attachment, _attachment.data(), _attachment.size(),
                                           _opt.gpu_device) != 0) {
                     *error = "fail to upload the attachment to HBM";

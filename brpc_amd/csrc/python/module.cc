@@ -11,6 +11,8 @@
 #include "base/logging.h"
 #include "fiber/fiber.h"
 #include "gpu/gpu.h"
+#include "gpu/copy_engine.h"
+#include "gpu/hbm_pool.h"
 #include "gpu/xgmi.h"
 #include "mrpc/proto/echo.pb.h"
 #include "press/press.h"
@@ -39,9 +41,11 @@ public:
             if (_server.AddService(_echo.get(), SERVER_DOESNT_OWN_SERVICE) != 0) throw std::runtime_error("AddService failed");
         }
     }
-    int start(const std::string& addr, int num_threads, int gpu_device, int idle_timeout_s, bool use_rdma) {
+    int start(const std::string& addr, int num_threads, int gpu_device, int idle_timeout_s, bool use_rdma,
+              int max_concurrency) {
         ServerOptions opt;
         opt.num_threads = num_threads;
+        if (max_concurrency > 0) opt.max_concurrency = max_concurrency;
         opt.gpu_device = gpu_device;
         opt.idle_timeout_sec = idle_timeout_s;
         opt.use_rdma = use_rdma;
@@ -300,7 +304,7 @@ PYBIND11_MODULE(_native, m) {
         .def(py::init<>())
         .def("add_echo_service", &PyServer::add_echo_service)
         .def("start", &PyServer::start, py::arg("addr"), py::arg("num_threads") = -1, py::arg("gpu_device") = -1,
-             py::arg("idle_timeout_s") = -1, py::arg("use_rdma") = false)
+             py::arg("idle_timeout_s") = -1, py::arg("use_rdma") = false, py::arg("max_concurrency") = 0)
         .def("stop", &PyServer::stop)
         .def_property_readonly("port", &PyServer::port)
         .def_property_readonly("address", &PyServer::address)
@@ -349,7 +353,28 @@ PYBIND11_MODULE(_native, m) {
         d["recv_payloads"] = s.recv_payloads;
         d["ring_full_fallbacks"] = s.ring_full_fallbacks;
         d["crc_failures"] = s.crc_failures;
+        d["lent_outstanding"] = s.lent_outstanding;
+        d["copied_into_arena"] = s.copied_into_arena;
+        d["released_unconsumed"] = s.released_unconsumed;
+        const gpu::CopyEngineStats c = gpu::GetCopyEngineStats();
+        d["copy_submits"] = c.submits;
+        d["copy_launches"] = c.launches;
+        d["copy_segments"] = c.segments;
+        d["copy_bytes"] = c.bytes;
         return d;
     });
+    g.def("reap_lent", [] { gpu::ReapLentBlocks(); });
+    g.def("hbm_pool_stats", [](int dev) {
+        const gpu::HbmPoolStats s = gpu::GetHbmPoolStats(dev);
+        py::dict d;
+        d["arena_bytes"] = s.arena_bytes;
+        d["carved_bytes"] = s.carved_bytes;
+        d["live_blocks"] = s.live_blocks;
+        d["live_bytes"] = s.live_bytes;
+        d["fallback_allocs"] = s.fallback_allocs;
+        d["pinned_bytes"] = gpu::PinnedBytes();
+        d["pinned_blocks_in_use"] = gpu::PinnedBlocksInUse();
+        return d;
+    }, py::arg("device") = 0);
     bind_gpu_ops(g);
 }

@@ -42,13 +42,13 @@ class EchoWorkload:
 
 
 # 32 B message, no attachment
-ECHO_32B = EchoWorkload("echo_32B", request_size=32, attachment_size=0, requests_per_step=20000)
+ECHO_32B = EchoWorkload("echo_32B", request_size=32, attachment_size=0, requests_per_step=150000)
 # 64 KiB body: tiny message + 64 KiB attachment (zero-copy Buf path)
-ECHO_64KB = EchoWorkload("echo_64KB", request_size=16, attachment_size=65536 - 16, requests_per_step=2000)
+ECHO_64KB = EchoWorkload("echo_64KB", request_size=16, attachment_size=65536 - 16, requests_per_step=20000)
 
 
-def start_echo_server(addr="127.0.0.1:0", num_threads=-1, gpu_device=-1):
+def start_echo_server(addr="127.0.0.1:0", num_threads=-1, gpu_device=-1, max_concurrency=0):
     s = native.Server()
     s.add_echo_service()
-    s.start(addr, num_threads=num_threads, gpu_device=gpu_device)
+    s.start(addr, num_threads=num_threads, gpu_device=gpu_device, max_concurrency=max_concurrency)
     return s

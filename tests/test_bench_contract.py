@@ -16,7 +16,8 @@ def _json_lines(out):
 
 def test_bench_single_rank():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--requests-per-step", "2000", "--latency-sample-s", "0.3"],
+                        "--requests-per-step", "2000", "--requests-per-step-64k", "500",
+                        "--latency-sample-s", "0.3"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -32,7 +33,8 @@ def test_bench_two_ranks_gloo():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29517",
                         os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-                        "--requests-per-step", "1000", "--latency-sample-s", "0.3", "--workers", "2"],
+                        "--requests-per-step", "1000", "--requests-per-step-64k", "300",
+                        "--latency-sample-s", "0.3", "--workers", "2"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)

@@ -187,3 +187,66 @@ def test_device_payload_xgmi_cross_process(dev):
     finally:
         srv.stdin.close()
         srv.wait(timeout=60)
+
+
+def _drain_lent(native, timeout_s=5.0):
+    import time
+    deadline = time.time() + timeout_s
+    while time.time() < deadline:
+        native.gpu.reap_lent()
+        st = native.gpu.xgmi_stats()
+        if st["lent_outstanding"] == 0:
+            return st
+        time.sleep(0.05)
+    return native.gpu.xgmi_stats()
+
+
+def test_device_payload_zero_copy_lending(dev):
+    """Arena-resident attachments are lent (no sender-side copy), pulled once
+    per hop by the batched copy engine, and every lend is released."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        before = native.gpu.xgmi_stats()
+        p = native.Press({"server": s.address, "concurrency": 32, "attachment_size": 65536,
+                          "device_attachment": True, "gpu_device": 0, "check_echo": True})
+        p.run_requests(2000)
+        st = p.stats()
+        assert st["success"] == 2000 and st["error"] == 0, st
+        after = _drain_lent(native)
+        assert after["lent_outstanding"] == 0, after
+        assert after["copied_into_arena"] == before["copied_into_arena"], (before, after)
+        assert after["ring_full_fallbacks"] == before["ring_full_fallbacks"], (before, after)
+        pulls = after["copy_segments"] - before["copy_segments"]
+        launches = after["copy_launches"] - before["copy_launches"]
+        assert pulls >= 3000, (before, after)
+        # concurrent pulls are combined into shared launches
+        assert launches < pulls, (pulls, launches)
+        pool = native.gpu.hbm_pool_stats(0)
+        assert pool["fallback_allocs"] == 0, pool
+        assert pool["pinned_blocks_in_use"], pool
+    finally:
+        s.stop()
+
+
+def test_device_payload_released_on_reject(dev):
+    """ELIMIT rejections happen before the server looks at the attachment:
+    the lent HBM blocks must still come back (baidu_std early
+    reject paths)."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0, max_concurrency=1)
+    try:
+        before = native.gpu.xgmi_stats()
+        p = native.Press({"server": s.address, "concurrency": 16, "attachment_size": 65536,
+                          "device_attachment": True, "gpu_device": 0, "max_retry": 0})
+        p.run_requests(1000)
+        st = p.stats()
+        assert st["error"] > 0, st  # some were rejected with ELIMIT
+        after = _drain_lent(native)
+        assert after["lent_outstanding"] == 0, after
+        assert after["released_unconsumed"] > before["released_unconsumed"], (before, after)
+        assert after["ring_full_fallbacks"] == before["ring_full_fallbacks"], (before, after)
+    finally:
+        s.stop()
