@@ -78,9 +78,10 @@ int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, void* scratch, uint32
 // Batched protobuf wire scan (gpu/pb_kernels.hip): message i is
 // buf[offsets[i], offsets[i+1]); its top-level fields land in
 // fields[i * max_fields * 2 + 2k] = tag, [.. + 1] = value (varint / fixed /
-// (offset << 32) | length); nfields[i] = count or a negative error code.
-int LaunchPbScan(const uint8_t* buf, const int64_t* offsets_dev, int64_t n, uint32_t max_fields, uint64_t* fields,
-                 int32_t* nfields, hipStream_t s);
+// (offset << 32) | length); nfields[i] = count or a negative error code
+// (-5: the offsets of message i leave [0, buf_len) or descend).
+int LaunchPbScan(const uint8_t* buf, uint64_t buf_len, const int64_t* offsets_dev, int64_t n, uint32_t max_fields,
+                 uint64_t* fields, int32_t* nfields, hipStream_t s);
 
 // ---- synchronous helpers (fiber-friendly waits)
 // CRC32C of device buffers; results to host.

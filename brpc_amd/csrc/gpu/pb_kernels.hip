@@ -11,7 +11,8 @@
 // fields (wire 2), which a second pass (or the host) can descend into.
 // nfields[i] = number of fields, or a negative code: -1 truncated/malformed,
 // -2 more than max_fields fields, -3 field number 0, -4 unsupported wire
-// type (proto2 groups).
+// type (proto2 groups), -5 offsets outside the buffer or descending (the
+// message is not read at all).
 //
 // Layout: one lane per message. Messages are tiny and independent, so the
 // serial tag walk of one message costs one lane, not one wave; a lane reads
@@ -40,14 +41,20 @@ __device__ __forceinline__ bool read_varint(gbyte_c* b, uint64_t& p, uint64_t en
 }
 
 __global__ void __launch_bounds__(256) pb_scan_kernel(const uint8_t* __restrict__ buf_,
-                                                      const int64_t* __restrict__ offsets, int64_t n,
-                                                      uint32_t max_fields, uint64_t* __restrict__ fields,
+                                                      uint64_t buf_len, const int64_t* __restrict__ offsets,
+                                                      int64_t n, uint32_t max_fields, uint64_t* __restrict__ fields,
                                                       int32_t* __restrict__ nfields) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     gbyte_c* b = (gbyte_c*)buf_;
-    const uint64_t start = (uint64_t)offsets[i];
-    const uint64_t end = (uint64_t)offsets[i + 1];
+    const int64_t so = offsets[i], eo = offsets[i + 1];
+    // never trust the offset table: a message must lie inside the buffer
+    if (so < 0 || eo < so || (uint64_t)eo > buf_len) {
+        nfields[i] = -5;
+        return;
+    }
+    const uint64_t start = (uint64_t)so;
+    const uint64_t end = (uint64_t)eo;
     uint64_t* row = fields + (uint64_t)i * max_fields * 2;
     uint64_t p = start;
     int32_t k = 0;
@@ -105,13 +112,13 @@ __global__ void __launch_bounds__(256) pb_scan_kernel(const uint8_t* __restrict_
 
 }  // namespace
 
-int LaunchPbScan(const uint8_t* buf, const int64_t* offsets_dev, int64_t n, uint32_t max_fields, uint64_t* fields,
-                 int32_t* nfields, hipStream_t s) {
+int LaunchPbScan(const uint8_t* buf, uint64_t buf_len, const int64_t* offsets_dev, int64_t n, uint32_t max_fields,
+                 uint64_t* fields, int32_t* nfields, hipStream_t s) {
     if (n <= 0) return 0;
     if (max_fields == 0) return -1;
     const int64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(pb_scan_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, offsets_dev, n, max_fields,
-                       fields, nfields);
+    hipLaunchKernelGGL(pb_scan_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, buf_len, offsets_dev, n,
+                       max_fields, fields, nfields);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -134,7 +134,11 @@ void record(void* p, size_t n) {
     int depth = backtrace(frames, kMaxFrames + 2);
     const int skip = depth > 2 ? 2 : 0;  // record() and the malloc wrapper
     const uint32_t sid = intern_stack(frames + skip, depth - skip);
-    const int64_t weight = (int64_t)n < g_mean ? g_mean : (int64_t)n;  // unbiased for the exponential sampler
+    // unbiased weight for exponential-gap sampling: an allocation of n bytes
+    // is sampled with probability 1 - exp(-n/mean), so it stands for
+    // n / (1 - exp(-n/mean)) bytes (tends to max(n, mean) at both ends)
+    const double q = 1.0 - std::exp(-(double)n / (double)g_mean);
+    const int64_t weight = q > 0 ? (int64_t)((double)n / q + 0.5) : g_mean;
     StackRec& sr = g_stacks[sid];
     sr.live_count.fetch_add(1, std::memory_order_relaxed);
     sr.live_bytes.fetch_add(weight, std::memory_order_relaxed);
@@ -190,8 +194,9 @@ void* calloc(size_t a, size_t b) {
     return p;
 }
 void* realloc(void* old, size_t n) {
-    forget(old);
     void* p = __libc_realloc(old, n);
+    // a failed realloc leaves `old` live (and tracked); realloc(p, 0) frees
+    if (p || n == 0) forget(old);
     record(p, n);
     return p;
 }

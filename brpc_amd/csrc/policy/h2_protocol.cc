@@ -370,13 +370,25 @@ void H2Context::maybe_window_update_locked(Buf* out, Stream* st) {
 int H2Context::on_settings(Socket* s, uint8_t flags, Buf& payload) {
     if (flags & F_ACK) return 0;
     if (payload.size() % 6) return fail_connection(s, H2_FRAME_SIZE_ERROR, "bad SETTINGS length");
-    std::lock_guard<std::mutex> g(_mu);
+    // validate every value before applying any (RFC 7540 §6.5.2): errors
+    // are connection errors and go out as GOAWAY, outside _mu
+    std::vector<std::pair<uint16_t, uint32_t>> kvs;
     while (!payload.empty()) {
         unsigned char b[6];
         payload.cutn(b, 6);
         const uint16_t id = (uint16_t)((b[0] << 8) | b[1]);
         const uint32_t v = ((uint32_t)b[2] << 24) | ((uint32_t)b[3] << 16) | ((uint32_t)b[4] << 8) | b[5];
-        switch (id) {
+        if (id == 2 && v > 1) return fail_connection(s, H2_PROTOCOL_ERROR, "bad SETTINGS_ENABLE_PUSH");
+        if (id == 4 && v > 0x7FFFFFFF) return fail_connection(s, H2_FLOW_CONTROL_ERROR, "bad SETTINGS_INITIAL_WINDOW_SIZE");
+        if (id == 5 && (v < kFrameSize || v > 16777215)) {
+            return fail_connection(s, H2_PROTOCOL_ERROR, "bad SETTINGS_MAX_FRAME_SIZE");
+        }
+        kvs.emplace_back(id, v);
+    }
+    std::unique_lock<std::mutex> g(_mu);
+    for (const auto& kv : kvs) {
+        const uint32_t v = kv.second;
+        switch (kv.first) {
         case 1:
             _remote.header_table_size = v;
             _enc.ResizeTable(v);
@@ -384,16 +396,18 @@ int H2Context::on_settings(Socket* s, uint8_t flags, Buf& payload) {
         case 2: _remote.enable_push = v; break;
         case 3: _remote.max_concurrent_streams = v; break;
         case 4: {
-            if (v > 0x7FFFFFFF) return -1;
             const int64_t delta = (int64_t)v - (int64_t)_remote.initial_window_size;
+            for (auto& st : _streams) {
+                if (st.second->send_window + delta > 0x7FFFFFFF) {
+                    g.unlock();
+                    return fail_connection(s, H2_FLOW_CONTROL_ERROR, "SETTINGS_INITIAL_WINDOW_SIZE overflows a window");
+                }
+            }
             _remote.initial_window_size = v;
-            for (auto& kv : _streams) kv.second->send_window += delta;
+            for (auto& st : _streams) st.second->send_window += delta;
             break;
         }
-        case 5:
-            if (v < kFrameSize || v > 16777215) return -1;
-            _remote.max_frame_size = v;
-            break;
+        case 5: _remote.max_frame_size = v; break;
         case 6: _remote.max_header_list_size = v; break;
         default: break;  // unknown settings are ignored
         }
@@ -474,16 +488,39 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
         payload.cutn(b, 4);
         const uint32_t inc = (((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3]) &
                              0x7FFFFFFF;
-        std::lock_guard<std::mutex> g(_mu);
-        Buf out;
-        if (sid == 0) {
-            _conn_send_window += inc;
-            flush_all_locked(&out);
-        } else if (Stream* st = find(sid)) {
-            st->send_window += inc;
-            if (flush_stream_locked(&out, st)) erase(sid);
+        // RFC 7540 §6.9: a zero increment is a PROTOCOL_ERROR and a window
+        // above 2^31-1 a FLOW_CONTROL_ERROR — of the connection for stream
+        // 0, of the stream (RST_STREAM) otherwise
+        if (sid == 0 && inc == 0) return fail_connection(s, H2_PROTOCOL_ERROR, "WINDOW_UPDATE with 0 increment");
+        uint32_t rst_code = 0;
+        fiber::CallId cid = fiber::INVALID_CALL_ID;
+        {
+            std::unique_lock<std::mutex> g(_mu);
+            Buf out;
+            if (sid == 0) {
+                if (_conn_send_window + (int64_t)inc > 0x7FFFFFFF) {
+                    g.unlock();
+                    return fail_connection(s, H2_FLOW_CONTROL_ERROR, "connection window above 2^31-1");
+                }
+                _conn_send_window += inc;
+                flush_all_locked(&out);
+            } else if (Stream* st = find(sid)) {
+                if (inc == 0) rst_code = H2_PROTOCOL_ERROR;
+                else if (st->send_window + (int64_t)inc > 0x7FFFFFFF) rst_code = H2_FLOW_CONTROL_ERROR;
+                if (rst_code) {
+                    cid = st->cid;
+                    erase(sid);
+                    frame_header(&out, 4, H2_RST_STREAM, 0, sid);
+                    const uint32_t be = htonl(rst_code);
+                    out.append(&be, 4);
+                } else {
+                    st->send_window += inc;
+                    if (flush_stream_locked(&out, st)) erase(sid);
+                }
+            }
+            write_locked(s, &out);
         }
-        write_locked(s, &out);
+        if (cid != fiber::INVALID_CALL_ID) fiber::call_id_error(cid, EREQUEST, "h2 stream flow-control error");
         return 0;
     }
     case H2_GOAWAY: {

@@ -54,10 +54,10 @@ void bind_gpu_ops(py::module_& g) {
         for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
         check(gpu::LaunchBatchedCopy(segs.data(), (int)segs.size(), as_stream(stream)), "batched_copy");
     }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("stream") = 0);
-    g.def("pb_scan_launch", [](uintptr_t buf, uintptr_t offsets, int64_t n, uint32_t max_fields, uintptr_t fields,
-                               uintptr_t nfields, uintptr_t stream) {
-        check(gpu::LaunchPbScan((const uint8_t*)buf, (const int64_t*)offsets, n, max_fields, (uint64_t*)fields,
-                                (int32_t*)nfields, as_stream(stream)),
+    g.def("pb_scan_launch", [](uintptr_t buf, uint64_t buf_len, uintptr_t offsets, int64_t n, uint32_t max_fields,
+                               uintptr_t fields, uintptr_t nfields, uintptr_t stream) {
+        check(gpu::LaunchPbScan((const uint8_t*)buf, buf_len, (const int64_t*)offsets, n, max_fields,
+                                (uint64_t*)fields, (int32_t*)nfields, as_stream(stream)),
               "pb_scan");
     });
     g.def("snappy_max_block", [] { return gpu::kSnappyMaxBlock; });

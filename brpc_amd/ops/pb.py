@@ -7,7 +7,8 @@ from ..native import native
 from ._common import require_gpu_tensor, stream_handle
 
 WIRE_VARINT, WIRE_FIXED64, WIRE_LEN, WIRE_FIXED32 = 0, 1, 2, 5
-ERRORS = {-1: "truncated or malformed", -2: "too many fields", -3: "field number 0", -4: "unsupported wire type"}
+ERRORS = {-1: "truncated or malformed", -2: "too many fields", -3: "field number 0", -4: "unsupported wire type",
+          -5: "offsets outside the buffer or descending"}
 
 
 def pb_scan(buf, offsets, max_fields=16):
@@ -21,14 +22,19 @@ def pb_scan(buf, offsets, max_fields=16):
     require_gpu_tensor(offsets, "offsets")
     if buf.dtype != torch.uint8 or offsets.dtype != torch.int64:
         raise TypeError("buf must be uint8 and offsets int64")
+    if offsets.device != buf.device:
+        raise ValueError("offsets must live on the same device as buf (%s vs %s)" % (offsets.device, buf.device))
+    if not buf.is_contiguous() or not offsets.is_contiguous():
+        raise ValueError("buf and offsets must be contiguous")
     n = offsets.numel() - 1
     dev = buf.device
     fields = torch.zeros((max(n, 1), max_fields, 2), dtype=torch.int64, device=dev)
     nfields = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
     if n > 0:
         with torch.cuda.device(dev):
-            native.gpu.pb_scan_launch(buf.data_ptr(), offsets.data_ptr(), n, int(max_fields), fields.data_ptr(),
-                                      nfields.data_ptr(), stream_handle(dev))
+            # the kernel bounds every message by buf.numel() (code -5)
+            native.gpu.pb_scan_launch(buf.data_ptr(), buf.numel(), offsets.data_ptr(), n, int(max_fields),
+                                      fields.data_ptr(), nfields.data_ptr(), stream_handle(dev))
     return fields[:n], nfields[:n]
 
 

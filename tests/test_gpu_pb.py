@@ -85,3 +85,16 @@ def test_pb_scan_error_codes(dev):
     ]
     _, nfields = _run(dev, msgs, max_fields=4)
     assert nfields == [-1, -1, -3, -4, -2, -1, 0, 1]
+
+
+def test_pb_scan_rejects_bad_offsets(dev):
+    """the offset table is never trusted — messages past the end of
+    the buffer or with descending bounds report -5 and are not read."""
+    from brpc_amd.ops import pb_scan
+    data = b"\x08\x01\x10\x02"
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    o = torch.tensor([0, 2, 4, 1 << 40, 3, 2], dtype=torch.int64, device=dev)
+    _, nfields = pb_scan(buf, o, 4)
+    assert nfields.cpu().tolist() == [1, 1, -5, -5, -5]
+    with pytest.raises((ValueError, TypeError)):
+        pb_scan(buf, o.cpu(), 4)  # offsets on another device than buf
