@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--workers", type=int, default=0, help="fiber worker pthreads per rank (0: auto)")
     ap.add_argument("--skip-64k", action="store_true")
+    ap.add_argument("--skip-fanout", action="store_true", help="skip the ParallelChannel fan-out leg (N>1)")
+    ap.add_argument("--requests-per-step-fanout", type=int, default=500)
     ap.add_argument("--skip-stream", action="store_true",
                     help="skip the streaming-RPC leg (64 KiB chunks, BASELINE config 3)")
     ap.add_argument("--host-payload", action="store_true",
@@ -174,12 +176,16 @@ def main():
         if r64 is None:
             r64, r64h = r64h, None
 
-    # Streaming-RPC leg: each rank pushes 64 KiB chunks through one
-    # flow-controlled stream to its ring peer; a step is 32 chunks (2 MiB)
-    # and ends when the peer acknowledged them.
+    # Streaming-RPC leg (BASELINE config 3): 64 KiB chunks through one
+    # flow-controlled stream per peer — rank r to every other rank (to its
+    # own server when alone); a step is 32 chunks per stream and ends when
+    # every peer acknowledged them. On a GPU box the chunk lives in HBM and
+    # the frames lend it over xGMI.
     rs = None
     if not a.skip_stream:
-        sp = native.StreamPress({"server": peer, "chunk_size": 65536, "chunks_per_step": 32})
+        others = [x for i, x in enumerate(addrs) if i != topo.rank] or [peer]
+        sp = native.StreamPress({"server": ",".join(others), "chunk_size": 65536, "chunks_per_step": 32,
+                                 "device_chunks": bool(cuda), "gpu_device": topo.device})
         sp.run_steps(a.warmup)
         parallel.barrier(topo)
         sync()
@@ -189,9 +195,41 @@ def main():
         sync()
         dt = time.perf_counter() - t0
         dt_max = parallel.allreduce_max(dt, topo)
-        nbytes = parallel.allreduce_sum(a.steps * 32 * 65536, topo)
-        rs = {"gbps": nbytes / dt_max / 1e9 if dt_max > 0 else 0.0, "ms_per_step": 1000.0 * dt_max / a.steps}
+        nbytes = parallel.allreduce_sum(a.steps * 32 * 65536 * len(others), topo)
+        rs = {"gbps": nbytes / dt_max / 1e9 if dt_max > 0 else 0.0, "ms_per_step": 1000.0 * dt_max / a.steps,
+              "device": bool(cuda), "fanout": len(others)}
         sp.close()
+
+    # Fan-out leg (BASELINE config 2, the DP analog): every call is broadcast
+    # by a ParallelChannel to the servers of ALL other ranks — one direct
+    # xGMI link each — with a 64 KiB HBM attachment, and the echoes are
+    # gathered. Only meaningful with peers (N > 1).
+    rf = None
+    if topo.world_size > 1 and not a.skip_fanout:
+        others = [x for i, x in enumerate(addrs) if i != topo.rank]
+        fo = ECHO_64KB.press_options(peer, gpu_device=topo.device)
+        fo.update({"fanout_servers": ",".join(others), "concurrency": 16, "device_attachment": bool(cuda)})
+        press = native.Press(fo)
+        nf = max(1, a.requests_per_step_fanout)
+        for _ in range(a.warmup):
+            press.run_requests(nf)
+        press.reset_stats()
+        parallel.barrier(topo)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            press.run_requests(nf)
+        parallel.barrier(topo)
+        sync()
+        dt = time.perf_counter() - t0
+        st = press.stats()
+        dt_max = parallel.allreduce_max(dt, topo)
+        bytes_total = parallel.allreduce_sum(st["bytes"], topo)
+        rf = {"gbps": bytes_total / dt_max / 1e9 if dt_max > 0 else 0.0,
+              "qps": parallel.allreduce_sum(st["success"], topo) / dt_max if dt_max > 0 else 0.0,
+              "errors": int(parallel.allreduce_sum(st["error"], topo)),
+              "p99_us": parallel.allreduce_max(st["p99_us"], topo), "fanout": len(others)}
+        del press
 
     lat = None
     if a.latency_sample_s > 0:
@@ -254,6 +292,14 @@ def main():
         if rs:
             out["stream_gbytes_per_s_64KB_chunks"] = round(rs["gbps"], 3)
             out["stream_ms_per_step"] = round(rs["ms_per_step"], 3)
+            out["stream_device_chunks"] = rs["device"]
+            out["stream_fanout_per_rank"] = rs["fanout"]
+        if rf:
+            out["fanout_gbytes_per_s"] = round(rf["gbps"], 3)
+            out["fanout_calls_per_s"] = round(rf["qps"], 1)
+            out["fanout_p99_us"] = rf["p99_us"]
+            out["fanout_errors"] = rf["errors"]
+            out["fanout_peers_per_rank"] = rf["fanout"]
         if lat:
             out["p99_us_at_100qps"] = lat["p99_us"]
             out["p50_us_at_100qps"] = lat["p50_us"]

@@ -258,6 +258,15 @@ std::shared_ptr<PeerMap> map_peer(const policy::XgmiHello& h, std::string* err) 
         int prev = 0;
         hipGetDevice(&prev);
         hipSetDevice(g_device);
+        // a peer on another GPU of this node: the pull kernel reads its HBM
+        // directly over xGMI, which needs peer access from our device
+        if (h.device() != g_device && h.device() >= 0 && h.device() < DeviceCount()) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, g_device, h.device()) == hipSuccess && can) {
+                const hipError_t pe = hipDeviceEnablePeerAccess(h.device(), 0);
+                if (pe != hipSuccess) (void)hipGetLastError();  // already enabled is fine
+            }
+        }
         const hipError_t r = hipIpcOpenMemHandle(&p, handle, hipIpcMemLazyEnablePeerAccess);
         hipSetDevice(prev);
         if (r != hipSuccess) {

@@ -14,7 +14,12 @@
 #include <cstddef>
 #include <cstdint>
 
+#include <string>
+#include <utility>
+#include <vector>
+
 #include "base/buf.h"
+#include "pb/message.h"
 
 namespace mrpc {
 
@@ -47,6 +52,20 @@ bool HasDeviceTransport(Socket* sock);
 void StageDeviceBufToHost(const Buf& in, Buf* out);
 
 namespace policy {
+using DevicePayloads = pb::RepeatedPtrField<DevicePayload>;
+// Protocol-neutral core (baidu_std metas and STRM frames): lend the device
+// blocks of `in` into *descs (host blocks go to *host_out, positions are
+// relative to `in`); pull `descs` into *attachment, whose current content
+// is the inline host part; release descriptors that will not be pulled.
+int LendDeviceBlocks(Socket* sock, const Buf& in, bool verify, Buf* host_out, DevicePayloads* descs,
+                     std::string* err);
+int PullDeviceBlocks(Socket* sock, const DevicePayloads& descs, Buf* attachment, std::string* err);
+// Several messages of one connection at once (one batched pull launch).
+int PullDeviceBlocksBatch(Socket* sock, const std::vector<std::pair<const DevicePayloads*, Buf*>>& items,
+                          std::string* err);
+void ReleaseDeviceBlocks(Socket* sock, const DevicePayloads& descs);
+void CancelDeviceBlocks(const DevicePayloads& descs);
+
 bool SplitDevicePayload(Controller* cntl, bool request, const Buf& attachment, Buf* host_out, RpcMeta* meta,
                         Socket* sock = nullptr);
 bool MergeDevicePayload(Controller* cntl, Socket* sock, const RpcMeta& meta, bool request, Buf* attachment);

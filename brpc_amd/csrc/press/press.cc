@@ -15,6 +15,7 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "rpc/channel.h"
+#include "rpc/combo_channels.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
 
@@ -136,7 +137,28 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
     copt.max_retry = _opt.max_retry;
     copt.use_device_transport = _opt.device_attachment;
     copt.gpu_device = _opt.gpu_device;
-    for (int i = 0; i < _opt.num_channels; ++i) {
+    std::vector<std::string> fan;
+    for (const std::string& f : split_string(_opt.fanout_servers, ',')) {
+        if (!f.empty()) fan.push_back(f);
+    }
+    for (int i = 0; i < _opt.num_channels && !fan.empty(); ++i) {
+        ParallelChannelOptions po;
+        po.timeout_ms = _opt.timeout_ms;
+        std::unique_ptr<ParallelChannel> pc(new ParallelChannel);
+        pc->Init(&po);
+        copt.connection_group = _opt.num_channels > 1 ? "press" + std::to_string(i) : std::string();
+        for (const std::string& f : fan) {
+            std::unique_ptr<Channel> sub(new Channel);
+            if (sub->Init(f.c_str(), &copt) != 0) {
+                *error = "fail to init channel to " + f;
+                return -1;
+            }
+            pc->AddChannel(sub.release(), OWNS_CHANNEL, nullptr, nullptr);
+        }
+        _channels.push_back(std::move(pc));
+    }
+    _fanout = fan.empty() ? 1 : (int)fan.size();
+    for (int i = 0; i < _opt.num_channels && fan.empty(); ++i) {
         std::unique_ptr<Channel> ch(new Channel);
         // distinct groups => distinct "single" connections per channel
         copt.connection_group = _opt.num_channels > 1 ? "press" + std::to_string(i) : std::string();
@@ -237,7 +259,7 @@ struct PressCall : public Closure {
 };
 
 void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
-    Channel* ch = _channels[w->index % _channels.size()].get();
+    ChannelBase* ch = _channels[w->index % _channels.size()].get();
     Controller& cntl = call->cntl;
     if (_opt.request_compress_type) cntl.set_request_compress_type((CompressType)_opt.request_compress_type);
     if (_opt.response_compress_type) cntl.set_response_compress_type((CompressType)_opt.response_compress_type);
@@ -257,7 +279,7 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     } else if (!_attachment.empty()) {
         cntl.request_attachment().append(_attachment);
     }
-    call->nbytes = 2 * (int64_t)(_echo_message.size() + _attachment.size());
+    call->nbytes = 2 * (int64_t)(_echo_message.size() + _attachment.size()) * _fanout;
     call->check = _opt.check_echo;
     example::EchoService_Stub stub(ch);
     stub.Echo(&cntl, &call->echo_req, &call->echo_res, done);
@@ -272,8 +294,9 @@ void PressSession::finish(PressCall* call) {
             ok = false;
             cntl.SetFailed(ERESPONSE, "echoed message mismatch");
         } else if (!_attachment.empty()) {
-            std::string got;
-            if (gpu::CopyBufToHost(cntl.response_attachment(), &got) != 0 || got != _attachment) {
+            std::string got, want;
+            for (int k = 0; k < _fanout; ++k) want += _attachment;  // gathered in channel order
+            if (gpu::CopyBufToHost(cntl.response_attachment(), &got) != 0 || got != want) {
                 ok = false;
                 cntl.SetFailed(ERESPONSE, "echoed attachment mismatch (%zu bytes)", got.size());
             }

@@ -24,7 +24,7 @@
 
 namespace mrpc {
 
-class Channel;
+class ChannelBase;
 namespace pb {
 class Message;
 class MethodDescriptor;
@@ -53,6 +53,11 @@ struct PressOptions {
     int gpu_device = -1;
     bool check_echo = false;   // verify the echoed payload
     bool use_rdma = false;     // verbs data plane (server needs use_rdma too)
+    // Fan-out (ParallelChannel, the DP analog of SURVEY §2.10): every call is
+    // broadcast to all of these comma-separated servers — on one node the
+    // xGMI-direct channels to the peer GPUs — and the echoed attachments are
+    // gathered. Empty: plain calls to `server`.
+    std::string fanout_servers;
     // generic workload (dynamic messages)
     std::string proto_file;    // .proto path
     std::string include_paths; // ';' separated
@@ -104,7 +109,8 @@ private:
                        double secs) const;
 
     PressOptions _opt;
-    std::vector<std::unique_ptr<Channel>> _channels;
+    std::vector<std::unique_ptr<ChannelBase>> _channels;
+    int _fanout = 1;  // sub calls per call
     // generic mode
     std::unique_ptr<pb::Importer> _importer;
     const pb::MethodDescriptor* _method = nullptr;

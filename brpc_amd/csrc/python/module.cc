@@ -135,6 +135,7 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "device_attachment") o.device_attachment = v.cast<bool>();
         else if (k == "gpu_device") o.gpu_device = v.cast<int>();
         else if (k == "check_echo") o.check_echo = v.cast<bool>();
+        else if (k == "fanout_servers") o.fanout_servers = v.cast<std::string>();
         else if (k == "use_rdma") o.use_rdma = v.cast<bool>();
         else if (k == "proto_file") o.proto_file = v.cast<std::string>();
         else if (k == "include_paths") o.include_paths = v.cast<std::string>();
@@ -211,6 +212,8 @@ public:
             else if (k == "chunks_per_step") o.chunks_per_step = v.cast<int>();
             else if (k == "timeout_ms") o.timeout_ms = v.cast<int>();
             else if (k == "max_buf_size") o.max_buf_size = v.cast<int64_t>();
+            else if (k == "device_chunks") o.device_chunks = v.cast<bool>();
+            else if (k == "gpu_device") o.gpu_device = v.cast<int>();
             else throw std::invalid_argument("unknown stream press option: " + k);
         }
         _s.reset(new press::StreamPress);
@@ -236,6 +239,7 @@ public:
         d["bytes_sent"] = _s->bytes_sent();
         d["bytes_acked"] = _s->bytes_acked();
         d["steps"] = _s->steps_done();
+        d["streams"] = _s->num_streams();
         return d;
     }
     void close() {

@@ -27,6 +27,7 @@ struct SubState {
     SubCall sc;
     Controller cntl;
     bool launched = false;
+    bool succeeded = false;  // set under PCall::mu
 };
 
 struct PCall {
@@ -59,6 +60,14 @@ struct PCall {
 void finish_parent(PCall* pc, int error_code, const std::string& text) {
     Controller* cntl = pc->cntl;
     if (error_code) cntl->SetFailed(error_code, "%s", text.c_str());
+    // gather: the response attachments of the sub calls that succeeded, in
+    // channel order (blocks are shared, HBM blocks stay in HBM)
+    if (!error_code) {
+        std::lock_guard<std::mutex> g(pc->mu);
+        for (auto& s : pc->subs) {
+            if (s->succeeded) cntl->response_attachment().append(s->cntl.response_attachment());
+        }
+    }
     cntl->_end_us = monotonic_us();
     Closure* done = pc->done;
     const fiber::CallId cid = pc->cid;
@@ -100,6 +109,7 @@ void on_sub_done(SubState* s) {
             }
             if (!pc->finished) {
                 if (ok) {
+                    s->succeeded = true;
                     ++pc->nsuccess;
                 } else {
                     ++pc->nfail;
@@ -231,6 +241,9 @@ void ParallelChannel::CallMethod(const pb::MethodDescriptor* method, RpcControll
         s->cntl.set_timeout_ms(timeout_ms);
         if (cntl->log_id()) s->cntl.set_log_id(cntl->log_id());
         if (cntl->has_request_code()) s->cntl.set_request_code(cntl->request_code());
+        // every sub call carries the attachment (shared blocks, no copy;
+        // reference parallel_channel.cpp:683-684)
+        s->cntl.request_attachment().append(cntl->request_attachment());
         to_launch.push_back(s.get());
     }
     const fiber::CallId cid = pc->cid;

@@ -24,7 +24,16 @@ namespace mrpc {
 namespace {
 
 struct StreamObj;
-typedef fiber::ExecutionQueue<Buf> RecvQueue;
+// One received DATA frame. HBM chunks are NOT pulled by the reading fiber:
+// the frame's descriptors ride along and the consumer pulls every chunk of
+// its batch with one launch, in order, so the socket keeps being read while
+// the GPU moves the bytes.
+struct StreamChunk {
+    Buf payload;                           // inline part (everything for host chunks)
+    std::shared_ptr<StreamFrameMeta> dmeta;  // device descriptors, or null
+    SocketUniquePtr sock;                  // the connection the chunks were lent on
+};
+typedef fiber::ExecutionQueue<StreamChunk> RecvQueue;
 
 struct StreamObj {
     std::mutex mu;
@@ -75,6 +84,18 @@ int send_frame(SocketId host, int64_t dest_stream, int64_t src_stream, FrameType
     fm.set_source_stream_id(src_stream);
     fm.set_frame_type(type);
     if (consumed >= 0) fm.mutable_feedback()->set_consumed_size(consumed);
+    // HBM chunks: lent over the connection's xGMI transport and described
+    // in the frame meta (staged through host memory when the connection has
+    // no device transport); only host bytes go inline
+    Buf host_part;
+    if (payload && !payload->all_host_accessible()) {
+        std::string err;
+        if (policy::LendDeviceBlocks(sock.get(), *payload, false, &host_part, fm.mutable_device_payload(), &err) != 0) {
+            LOG_EVERY_SECOND(WARNING) << "stream " << src_stream << ": " << err;
+            return EINVAL;
+        }
+        payload = &host_part;
+    }
     const uint32_t meta_size = (uint32_t)fm.ByteSizeLong();
     const uint32_t payload_size = payload ? (uint32_t)payload->size() : 0;
     Buf frame;
@@ -86,7 +107,13 @@ int send_frame(SocketId host, int64_t dest_stream, int64_t src_stream, FrameType
     if (payload) frame.append(*payload);
     WriteOptions wopt;
     wopt.ignore_eovercrowded = (type != FRAME_TYPE_DATA);
-    return sock->Write(&frame, &wopt) == 0 ? 0 : errno;
+    if (sock->Write(&frame, &wopt) != 0) {
+        const int e = errno;
+        // the frame never left: take the lends back
+        if (fm.device_payload_size()) policy::CancelDeviceBlocks(fm.device_payload());
+        return e;
+    }
+    return 0;
 }
 
 void release_stream(StreamObj* s) {
@@ -199,6 +226,9 @@ int consume(void* meta, RecvQueue::Iterator& it) {
         handler = s->opt.handler;
     }
     if (it.is_queue_stopped()) {
+        for (; it; ++it) {  // chunks nobody will read: give the lends back
+            if (it->dmeta) policy::ReleaseDeviceBlocks(it->sock.get(), it->dmeta->device_payload());
+        }
         bool call = false;
         {
             std::unique_lock<std::mutex> lk;
@@ -215,11 +245,33 @@ int consume(void* meta, RecvQueue::Iterator& it) {
         return 0;
     }
     std::vector<Buf*> msgs;
+    std::vector<std::pair<const policy::DevicePayloads*, Buf*>> pulls;
+    Socket* pull_sock = nullptr;
     int64_t bytes = 0;
     for (; it; ++it) {
-        msgs.push_back(&*it);
-        bytes += (int64_t)it->size();
+        StreamChunk& c = *it;
+        if (c.dmeta) {
+            if (pull_sock && pull_sock != c.sock.get()) {
+                // (never happens: one stream, one host connection)
+                std::string err;
+                if (policy::PullDeviceBlocksBatch(pull_sock, pulls, &err) != 0) {
+                    LOG_EVERY_SECOND(ERROR) << "stream " << id << " lost device chunks: " << err;
+                }
+                pulls.clear();
+            }
+            pull_sock = c.sock.get();
+            pulls.emplace_back(&c.dmeta->device_payload(), &c.payload);
+        }
+        msgs.push_back(&c.payload);
     }
+    if (!pulls.empty()) {
+        std::string err;
+        if (policy::PullDeviceBlocksBatch(pull_sock, pulls, &err) != 0) {
+            LOG_EVERY_SECOND(ERROR) << "stream " << id << " lost device chunks: " << err;
+            for (auto& p : pulls) p.second->clear();
+        }
+    }
+    for (Buf* m : msgs) bytes += (int64_t)m->size();
     if (handler && !msgs.empty()) handler->on_received_messages(id, msgs.data(), msgs.size());
     SocketId host = INVALID_SOCKET_ID;
     int64_t remote = 0, consumed = -1;
@@ -289,6 +341,7 @@ void ProcessStreamFrame(InputMessageBase* base) {
     std::unique_lock<std::mutex> lk;
     StreamObj* s = lock_stream(id, &lk);
     if (!s) {
+        policy::ReleaseDeviceBlocks(msg->socket(), fm.device_payload());
         if (fm.frame_type() == FRAME_TYPE_DATA && fm.source_stream_id()) {
             send_frame(msg->socket()->id(), fm.source_stream_id(), (int64_t)id, FRAME_TYPE_RST, nullptr);
         }
@@ -303,7 +356,18 @@ void ProcessStreamFrame(InputMessageBase* base) {
         }
         auto q = s->queue;
         lk.unlock();
-        if (q) q->execute(std::move(msg->payload));
+        StreamChunk c;
+        c.payload = std::move(msg->payload);
+        if (fm.device_payload_size() > 0) {
+            c.dmeta = std::make_shared<StreamFrameMeta>();
+            c.dmeta->mutable_device_payload()->raw().swap(msg->meta.mutable_device_payload()->raw());
+            msg->socket()->AddRef();
+            c.sock.reset(msg->socket());
+        }
+        std::shared_ptr<StreamFrameMeta> dmeta = c.dmeta;  // survives a failed execute
+        if (!q || q->execute(std::move(c)) != 0) {
+            if (dmeta) policy::ReleaseDeviceBlocks(msg->socket(), dmeta->device_payload());
+        }
         break;
     }
     case FRAME_TYPE_FEEDBACK: {
@@ -406,12 +470,7 @@ int StreamWrite(StreamId id, const Buf& message, const StreamWriteOptions*) {
     const int64_t remote = s->remote_id;
     lk.unlock();
     Buf payload = message;
-    // Device-resident chunks are staged through the host transport.
-    Buf host_payload;
-    if (!payload.all_host_accessible()) {
-        StageDeviceBufToHost(payload, &host_payload);
-        payload.swap(host_payload);
-    }
+    // device-resident chunks are lent over xGMI inside send_frame
     const int rc = send_frame(host, remote, (int64_t)id, FRAME_TYPE_DATA, &payload);
     return rc == 0 ? 0 : EINVAL;
 }

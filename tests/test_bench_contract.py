@@ -34,6 +34,7 @@ def test_bench_two_ranks_gloo():
                         "--master-addr", "127.0.0.1", "--master-port", "29517",
                         os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
                         "--requests-per-step", "1000", "--requests-per-step-64k", "300",
+                        "--requests-per-step-fanout", "100",
                         "--latency-sample-s", "0.3", "--workers", "2"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -41,3 +42,6 @@ def test_bench_two_ranks_gloo():
     assert len(lines) == 1, r.stdout
     j = lines[0]
     assert j["n_gpus"] == 2 and j["value"] > 0 and j["errors"] == 0
+    # multi-rank legs: stream fan-out to the other rank, ParallelChannel fan-out
+    assert j["stream_fanout_per_rank"] == 1 and j["stream_gbytes_per_s_64KB_chunks"] > 0
+    assert j["fanout_peers_per_rank"] == 1 and j["fanout_errors"] == 0 and j["fanout_gbytes_per_s"] > 0

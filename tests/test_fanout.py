@@ -1,0 +1,39 @@
+"""Fan-out workloads of the multi-GPU bench legs (BASELINE configs 2/3),
+exercised on CPU: a ParallelChannel broadcast with attachment forwarding and
+gathering, and one flow-controlled stream per peer server. On a GPU node the
+same code moves HBM payloads over xGMI (tests/test_gpu_ops.py)."""
+from brpc_amd.models import start_echo_server
+
+
+def test_parallel_channel_fanout_with_attachments(native):
+    servers = [start_echo_server("127.0.0.1:0") for _ in range(3)]
+    try:
+        p = native.Press({"server": servers[0].address,
+                          "fanout_servers": ",".join(s.address for s in servers),
+                          "concurrency": 8, "attachment_size": 4096, "check_echo": True})
+        p.run_requests(300)
+        st = p.stats()
+        assert st["success"] == 300 and st["error"] == 0, st
+        # every call reached every server
+        assert [s.echo_calls for s in servers] == [300, 300, 300]
+        # bytes = 2 directions x (message + attachment) x 3 peers
+        assert st["bytes"] == 300 * 2 * (32 + 4096) * 3, st
+    finally:
+        for s in servers:
+            s.stop()
+
+
+def test_stream_press_fans_out_to_every_peer(native):
+    servers = [start_echo_server("127.0.0.1:0") for _ in range(2)]
+    try:
+        sp = native.StreamPress({"server": ",".join(s.address for s in servers), "chunk_size": 65536,
+                                 "chunks_per_step": 8})
+        sp.run_steps(5)
+        st = sp.stats()
+        assert st["streams"] == 2 and st["steps"] == 5, st
+        assert st["bytes_acked"] == 2 * 5 * 8 * 65536, st
+        assert st["bytes_sent"] == st["bytes_acked"], st
+        sp.close()
+    finally:
+        for s in servers:
+            s.stop()

@@ -250,3 +250,46 @@ def test_device_payload_released_on_reject(dev):
         assert after["ring_full_fallbacks"] == before["ring_full_fallbacks"], (before, after)
     finally:
         s.stop()
+
+
+def test_stream_device_chunks_over_xgmi(dev):
+    """Streaming RPC with HBM chunks: frames lend the chunk, the receiver
+    pulls it in frame order; nothing is staged through host memory."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    servers = [start_echo_server("127.0.0.1:0", gpu_device=0) for _ in range(2)]
+    try:
+        before = native.gpu.xgmi_stats()
+        sp = native.StreamPress({"server": ",".join(s.address for s in servers), "chunk_size": 65536,
+                                 "chunks_per_step": 16, "device_chunks": True, "gpu_device": 0})
+        sp.run_steps(10)
+        st = sp.stats()
+        assert st["bytes_acked"] == 2 * 10 * 16 * 65536, st
+        sp.close()
+        after = _drain_lent(native)
+        assert after["recv_payloads"] - before["recv_payloads"] >= 2 * 10 * 16, (before, after)
+        assert after["lent_outstanding"] == 0, after
+        assert after["copied_into_arena"] == before["copied_into_arena"], (before, after)
+    finally:
+        for s in servers:
+            s.stop()
+
+
+def test_fanout_device_attachment(dev):
+    """ParallelChannel broadcast of one HBM attachment: one lend per peer of
+    the same arena block, gathered echoes pulled back."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    servers = [start_echo_server("127.0.0.1:0", gpu_device=0) for _ in range(3)]
+    try:
+        p = native.Press({"server": servers[0].address, "fanout_servers": ",".join(s.address for s in servers),
+                          "concurrency": 8, "attachment_size": 65536, "device_attachment": True,
+                          "gpu_device": 0, "check_echo": True})
+        p.run_requests(300)
+        st = p.stats()
+        assert st["success"] == 300 and st["error"] == 0, st
+        assert [s.echo_calls for s in servers] == [300, 300, 300]
+        assert _drain_lent(native)["lent_outstanding"] == 0
+    finally:
+        for s in servers:
+            s.stop()
