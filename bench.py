@@ -112,9 +112,10 @@ def main():
     addrs = parallel.exchange_addresses(server.address, topo)
     peer = addrs[parallel.ring_peer(topo)]
 
-    def timed_leg(wl, steps, warmup):
-        opts = wl.press_options(peer, gpu_device=topo.device)
-        opts["concurrency"] = a.concurrency
+    def timed_leg(wl, steps, warmup, opts=None):
+        if opts is None:
+            opts = wl.press_options(peer, gpu_device=topo.device)
+            opts["concurrency"] = a.concurrency
         press = native.Press(opts)
         n = wl.requests_per_step
         for _ in range(warmup):
@@ -175,6 +176,20 @@ def main():
         r64h = timed_leg(wl64h, a.steps, a.warmup)
         if r64 is None:
             r64, r64h = r64h, None
+
+    # GPU-handler leg: 64 KiB host attachments that the server
+    # runs through its GPU — gathered from the pinned socket blocks into HBM
+    # by the fused copy+CRC32C kernel (batched across concurrent requests),
+    # answered from HBM (staged back to the client's TCP stream by one
+    # batched launch). Bytes and device CRC are verified in the GPU tests
+    # (tests/test_gpu_ops.py::test_gpu_process_echo_handler), not here.
+    rg = None
+    if cuda and not a.skip_64k:
+        wlg = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=False,
+                                  requests_per_step=max(1, wl64.requests_per_step // 2)))
+        og = wlg.press_options(peer, gpu_device=topo.device)
+        og.update({"concurrency": a.concurrency, "gpu_process": True})
+        rg = timed_leg(wlg, a.steps, a.warmup, og)
 
     # Streaming-RPC leg (BASELINE config 3): 64 KiB chunks through one
     # flow-controlled stream per peer — rank r to every other rank (to its
@@ -289,6 +304,10 @@ def main():
             out["qps_64KB_host_attachment"] = round(r64h["qps"], 1)
             out["p99_us_64KB_host_attachment"] = r64h["p99_us"]
             out["gbytes_per_s_64KB_host_attachment"] = round(r64h["qps"] * 65536 * 2 / 1e9, 3)
+        if rg:
+            out["qps_64KB_gpu_handler"] = round(rg["qps"], 1)
+            out["p99_us_64KB_gpu_handler"] = rg["p99_us"]
+            out["errors_64KB_gpu_handler"] = rg["errors"]
         if rs:
             out["stream_gbytes_per_s_64KB_chunks"] = round(rs["gbps"], 3)
             out["stream_ms_per_step"] = round(rs["ms_per_step"], 3)

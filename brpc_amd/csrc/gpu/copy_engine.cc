@@ -2,13 +2,16 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
 #include "base/logging.h"
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
+#include "gpu/hbm_pool.h"
 
 namespace mrpc {
 namespace gpu {
@@ -21,6 +24,10 @@ const int kMaxDev = 16;
 // `butex`; the poller sets it to 1 (or -1) when the batch's event fires.
 struct Batch {
     std::vector<Segment> segs;
+    bool want_crc = false;          // some submitter asked for checksums
+    uint32_t* crc_dev = nullptr;    // per-segment CRC32C (HBM pool)
+    uint32_t* crc_host = nullptr;   // ... copied back here (pinned)
+    size_t crc_cap = 0;
     std::atomic<int>* butex = nullptr;
     hipEvent_t ev = nullptr;
     std::atomic<int> refs{0};
@@ -55,7 +62,25 @@ void launch(Batch* b, int device) {
     if (prev != device) hipSetDevice(device);
     hipStream_t s = PoolStream(device);
     b->ev = AcquireEvent();
-    int rc = (s && b->ev) ? LaunchBatchedCopy(b->segs.data(), (int)b->segs.size(), s) : -1;
+    int rc = (s && b->ev) ? 0 : -1;
+    const size_t n = b->segs.size();
+    if (rc == 0 && b->want_crc) {
+        // fused pull + checksum, results back to pinned host memory
+        if (b->crc_cap < n) {
+            HbmFree(b->crc_dev, b->crc_cap * sizeof(uint32_t), device);
+            PinnedFree(b->crc_host, b->crc_cap * sizeof(uint32_t));
+            b->crc_cap = std::max<size_t>(n, 64);
+            b->crc_dev = static_cast<uint32_t*>(HbmAlloc(b->crc_cap * sizeof(uint32_t), device));
+            b->crc_host = static_cast<uint32_t*>(PinnedAlloc(b->crc_cap * sizeof(uint32_t)));
+        }
+        if (!b->crc_dev || !b->crc_host ||
+            LaunchBatchedCopyCrc32c(b->segs.data(), (int)n, b->crc_dev, s) != 0 ||
+            hipMemcpyAsync(b->crc_host, b->crc_dev, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) {
+            rc = -1;
+        }
+    } else if (rc == 0) {
+        rc = LaunchBatchedCopy(b->segs.data(), (int)n, s);
+    }
     if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
     if (prev != device) hipSetDevice(prev);
     g_launches.fetch_add(1, std::memory_order_relaxed);
@@ -70,13 +95,14 @@ void launch(Batch* b, int device) {
 
 }  // namespace
 
-int BatchedCopy(const Segment* segs, int n, int device) {
+int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
     if (n <= 0) return 0;
     if (device < 0) device = CurrentDevice();
     if (device < 0 || device >= kMaxDev || Init(device) != 0) return -1;
     Engine& e = g_engine[device];
     g_submits.fetch_add(1, std::memory_order_relaxed);
     Batch* mine;
+    size_t first = 0;  // index of our first segment in the batch
     bool leader = false;
     {
         std::lock_guard<std::mutex> g(e.mu);
@@ -85,7 +111,9 @@ int BatchedCopy(const Segment* segs, int n, int device) {
             e.open->butex->store(0, std::memory_order_relaxed);
         }
         mine = e.open;
+        first = mine->segs.size();
         mine->segs.insert(mine->segs.end(), segs, segs + n);
+        if (crcs) mine->want_crc = true;
         mine->refs.fetch_add(1, std::memory_order_relaxed);
         if (!e.launching) {
             e.launching = true;
@@ -115,10 +143,12 @@ int BatchedCopy(const Segment* segs, int n, int device) {
     }
     while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
     const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
+    if (rc == 0 && crcs) memcpy(crcs, mine->crc_host + first, sizeof(uint32_t) * (size_t)n);
     if (mine->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
         ReleaseEvent(mine->ev);
         mine->ev = nullptr;
         mine->segs.clear();
+        mine->want_crc = false;
         std::lock_guard<std::mutex> g(e.mu);
         e.spare.push_back(mine);
     }

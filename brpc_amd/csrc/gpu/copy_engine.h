@@ -24,8 +24,10 @@ namespace mrpc {
 namespace gpu {
 
 // Copy all segments on `device`; returns when the copies completed (fiber
-// parks, pthread blocks). 0 on success.
-int BatchedCopy(const Segment* segs, int n, int device);
+// parks, pthread blocks). 0 on success. With `crcs`, the batch runs the
+// fused copy+CRC32C kernel and crcs[i] receives the standard CRC32C of
+// segment i (computed from the bytes while they are moved).
+int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs = nullptr);
 
 struct CopyEngineStats {
     int64_t submits = 0, launches = 0, segments = 0, bytes = 0;

@@ -1,0 +1,112 @@
+#include "gpu/device_handler.h"
+
+#include <cstring>
+#include <vector>
+
+#include "base/crc32c.h"
+#include "gpu/copy_engine.h"
+#include "gpu/gpu.h"
+#include "gpu/hbm_pool.h"
+
+namespace mrpc {
+namespace gpu {
+
+namespace {
+void pinned_deleter(void* p, void* arg) { PinnedFree(p, (size_t)reinterpret_cast<uintptr_t>(arg)); }
+}  // namespace
+
+int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
+    if (device < 0) device = CurrentDevice();
+    const size_t n = in.size();
+    *crc = 0;
+    if (n == 0) return 0;
+    Buf dev;
+    char* d = static_cast<char*>(AppendNewDeviceBlock(&dev, n, device));
+    if (!d) return -1;
+    std::vector<Segment> segs;
+    std::vector<uint32_t> lens;
+    segs.reserve(in.backing_block_num());
+    // pageable host blocks are bounced through one pinned buffer first (the
+    // kernel can only read pinned host memory)
+    size_t pageable = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        if (in.ref_at(i).block->kind == MemKind::HOST) pageable += in.ref_at(i).length;
+    }
+    char* bounce = pageable ? static_cast<char*>(PinnedAlloc(pageable)) : nullptr;
+    if (pageable && !bounce) return -1;
+    size_t off = 0, boff = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BlockRef& r = in.ref_at(i);
+        const char* src = r.block->data + r.offset;
+        if (r.block->kind == MemKind::HOST) {
+            memcpy(bounce + boff, src, r.length);
+            src = bounce + boff;
+            boff += r.length;
+        } else if (!IsHostAccessible(r.block->kind) && r.block->device != device &&
+                   ArenaOffset(src, r.block->device) < 0) {
+            // another device's non-arena block: not mapped here
+            if (bounce) PinnedFree(bounce, pageable);
+            return -1;
+        }
+        segs.push_back(Segment{src, d + off, r.length});
+        lens.push_back(r.length);
+        off += r.length;
+    }
+    std::vector<uint32_t> crcs(segs.size());
+    const int rc = BatchedCopy(segs.data(), (int)segs.size(), device, crcs.data());
+    if (bounce) PinnedFree(bounce, pageable);
+    if (rc != 0) return -1;
+    uint32_t c = crcs[0];
+    for (size_t i = 1; i < crcs.size(); ++i) c = crc32c::Combine(c, crcs[i], lens[i]);
+    *crc = c;
+    out->append(std::move(dev));
+    return 0;
+}
+
+int StageToPinnedHost(const Buf& in, Buf* out) {
+    // one pinned region for all device bytes, filled by one batched launch
+    size_t dbytes = 0;
+    int device = -1;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BlockRef& r = in.ref_at(i);
+        if (!IsHostAccessible(r.block->kind)) {
+            dbytes += r.length;
+            if (device < 0) device = r.block->device;
+            if (r.block->device != device) return -1;  // mixed devices: caller stages per block
+        }
+    }
+    if (dbytes == 0) {
+        out->append(in);
+        return 0;
+    }
+    char* h = static_cast<char*>(PinnedAlloc(dbytes));
+    if (!h) return -1;
+    std::vector<Segment> segs;
+    size_t off = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BlockRef& r = in.ref_at(i);
+        if (!IsHostAccessible(r.block->kind)) {
+            segs.push_back(Segment{r.block->data + r.offset, h + off, r.length});
+            off += r.length;
+        }
+    }
+    if (BatchedCopy(segs.data(), (int)segs.size(), device) != 0) {
+        PinnedFree(h, dbytes);
+        return -1;
+    }
+    Buf staged;
+    staged.append_user_data(h, dbytes, pinned_deleter, reinterpret_cast<void*>((uintptr_t)dbytes), MemKind::PINNED);
+    off = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BlockRef& r = in.ref_at(i);
+        if (IsHostAccessible(r.block->kind)) {
+            out->append_block(r.block, r.offset, r.length);
+        } else {
+            staged.cutn(out, r.length);
+        }
+    }
+    return 0;
+}
+
+}  // namespace gpu
+}  // namespace mrpc

@@ -1,0 +1,30 @@
+// GPU-touching service handlers (the minimum MI355X slice):
+// a request attachment is moved into HBM, a kernel runs over it and the
+// response attachment is served from HBM — with the fiber parked on the
+// batch's hipEvent, never blocking a worker pthread.
+//
+// Host-to-device and device-to-host moves go through the batched copy
+// engine (gpu/copy_engine.h): the kernel reads pinned socket blocks directly
+// (or peer/local HBM) and concurrent requests share one launch.
+#pragma once
+
+#include <cstdint>
+
+#include "base/buf.h"
+
+namespace mrpc {
+namespace gpu {
+
+// Gather `in` (any mix of pinned/pageable host, local or peer HBM blocks)
+// into ONE new arena block on `device` appended to *out; *crc receives the
+// standard CRC32C of the bytes, folded by the same kernel that moves them.
+// 0 on success.
+int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device);
+
+// Copy every device block of `in` into pinned host memory (one batched
+// launch); host blocks are shared. Installed as the staging hook of
+// policy/device_payload.h once a device is enabled.
+int StageToPinnedHost(const Buf& in, Buf* out);
+
+}  // namespace gpu
+}  // namespace mrpc

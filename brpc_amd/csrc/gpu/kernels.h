@@ -36,6 +36,9 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
 int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s);
 // Copy every segment src -> dst (one launch for many small copies).
 int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s);
+// Fused: copy every segment AND write its standard CRC32C to out_dev[i]
+// (one read of the bytes; sources may be local/peer HBM or pinned host).
+int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s);
 
 // Packed-varint decode (protobuf wire type 0, packed repeated field):
 // `in` holds n bytes of concatenated varints; out receives the values

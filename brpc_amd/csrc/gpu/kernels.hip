@@ -190,6 +190,75 @@ __global__ void __launch_bounds__(kThreads) batched_copy_kernel(SegBatch b) {
     }
 }
 
+// Fused pull + checksum: the batched copy and the LDS CRC32C in ONE pass
+// over the bytes (the data is read once — from local HBM, a peer GPU's HBM
+// across xGMI, or pinned host memory — stored to dst and folded into the
+// CRC while in registers). Same end-aligned chunk/lane geometry as
+// crc32c_kernel, so every partial CRC is shifted by a table-resident power
+// of x and chunks fold with one atomicXor per workgroup. Misaligned
+// segments (an attachment that starts mid-block after the RPC meta) use
+// unaligned 16 B accesses, which gfx950 serves natively.
+typedef uint32_t u32x4_unaligned __attribute__((ext_vector_type(4), aligned(1)));
+
+__global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const uint32_t* __restrict__ tables,
+                                                               uint32_t* __restrict__ out) {
+    __shared__ uint32_t t[8][256];
+    __shared__ uint32_t wave_acc[kThreads / 64];
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(tables);
+        uint4* dst = reinterpret_cast<uint4*>(&t[0][0]);
+        dst[threadIdx.x] = src[threadIdx.x];
+        dst[threadIdx.x + kThreads] = src[threadIdx.x + kThreads];
+    }
+    const uint32_t chunk = blockIdx.x;
+    const int seg = find_segment(b, chunk);
+    const uint64_t len = b.len[seg];
+    const uint8_t* base = static_cast<const uint8_t*>(b.src[seg]);
+    uint8_t* dbase = static_cast<uint8_t*>(b.dst[seg]);
+    const uint32_t seg_chunks = b.chunk_start[seg + 1] - b.chunk_start[seg];
+    const uint32_t k = chunk - b.chunk_start[seg];
+    const uint32_t after = seg_chunks - 1 - k;
+    const int64_t chunk_end = (int64_t)len - (int64_t)after * (int64_t)kChunkBytes;
+    const int64_t lane_end = chunk_end - (int64_t)(kThreads - 1 - threadIdx.x) * kLaneBytes;
+    const int64_t lane_beg = lane_end - kLaneBytes;
+    __syncthreads();
+
+    uint32_t crc = 0;
+    if (lane_end > 0) {
+        if (lane_beg >= 0) {
+            const u32x4_unaligned* p = reinterpret_cast<const u32x4_unaligned*>(base + lane_beg);
+            u32x4_unaligned* q = reinterpret_cast<u32x4_unaligned*>(dbase + lane_beg);
+            u32x4_unaligned v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = p[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) q[i] = v[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                crc = crc_word8(crc, v[i].x, v[i].y, t);
+                crc = crc_word8(crc, v[i].z, v[i].w, t);
+            }
+        } else {
+            for (int64_t i = 0; i < lane_end; ++i) {
+                const uint8_t c = base[i];
+                dbase[i] = c;
+                crc = t[0][(crc ^ c) & 0xff] ^ (crc >> 8);
+            }
+        }
+        crc = mult_mod_p(c_lane_shift[kThreads - 1 - threadIdx.x], crc);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) crc ^= __shfl_xor(crc, off, 64);
+    if ((threadIdx.x & 63) == 0) wave_acc[threadIdx.x >> 6] = crc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
+        if (after) acc = mult_mod_p(shift_bytes_poly((uint64_t)after * kChunkBytes), acc);
+        if (after == seg_chunks - 1) acc ^= mult_mod_p(shift_bytes_poly(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        atomicXor(out + seg, acc);
+    }
+}
+
 // ---------------------------------------------------------------- CRC32C on MFMA
 //
 // CRC32C over GF(2) is linear in the message bits, so the CRC of a 64-byte
@@ -793,6 +862,22 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
     hipLaunchKernelGGL(crc32c_mfma_kernel, dim3((uint32_t)grid), dim3(kThreads), 0, s, starts_dev, lens_dev,
                        (const uint64_t*)cs, nseg, (const CrcMfmaConsts*)g_tables[dev].mfma, xc, out_dev);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s) {
+    if (nseg <= 0) return 0;
+    if (ensure_tables() != 0) return -1;
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipMemsetAsync(out_dev, 0, sizeof(uint32_t) * nseg, s) != hipSuccess) return -1;
+    for (int i = 0; i < nseg; i += kInlineSegments) {
+        const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;
+        SegBatch b;
+        const uint32_t chunks = fill_batch(&b, segs + i, n);
+        hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, out_dev + i);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    return 0;
 }
 
 int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s) {

@@ -19,6 +19,7 @@
 #include "base/logging.h"
 #include "base/time.h"
 #include "gpu/copy_engine.h"
+#include "gpu/device_handler.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
@@ -394,23 +395,28 @@ int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Bu
         }
         segs.push_back(Segment{pm->base + off, dst, (uint64_t)len});
     }
-    if (rc == 0) rc = BatchedCopy(segs.data(), (int)segs.size(), g_device);
+    // one pull for every payload; when the sender asked for verification
+    // the pull kernel folds CRC32C while the bytes pass through registers
+    bool want_crc = false;
+    for (int i = 0; i < n; ++i) want_crc |= descs[i]->has_crc();
+    std::vector<uint32_t> crcs(want_crc ? segs.size() : 0);
+    if (rc == 0) rc = BatchedCopy(segs.data(), (int)segs.size(), g_device, want_crc ? crcs.data() : nullptr);
     // the bytes are ours now (or never will be): give every region back
     for (int i = 0; i < n; ++i) release_in(pm, *descs[i]);
     if (rc != 0) {
         for (int i = 0; i < n; ++i) outs[i].clear();
         return -1;
     }
+    size_t si = 0;
     for (int i = 0; i < n; ++i) {
         const policy::DevicePayload& d = *descs[i];
-        if (d.has_crc()) {
-            uint32_t crc = 0;
-            if (Crc32cOfBuf(outs[i], &crc, g_device) != 0 || crc != d.crc32c()) {
-                g_crc_fail.fetch_add(1, std::memory_order_relaxed);
-                for (int k = 0; k < n; ++k) outs[k].clear();
-                return -1;
-            }
+        if (d.length() == 0) continue;
+        if (d.has_crc() && crcs[si] != d.crc32c()) {
+            g_crc_fail.fetch_add(1, std::memory_order_relaxed);
+            for (int k = 0; k < n; ++k) outs[k].clear();
+            return -1;
         }
+        ++si;
         g_recv_bytes.fetch_add(d.length(), std::memory_order_relaxed);
     }
     g_recv_payloads.fetch_add(n, std::memory_order_relaxed);
@@ -442,6 +448,7 @@ int EnableXgmiTransport(int device, std::string* error) {
         return -1;
     }
     UsePinnedBlocks();
+    SetStageToHostHook(StageToPinnedHost);
     g_device = device;
     g_lender = l;
     DeviceTransportHooks h;

@@ -13,7 +13,10 @@ namespace mrpc {
 
 namespace {
 DeviceTransportHooks g_hooks;
+int (*g_stage_hook)(const Buf& in, Buf* out) = nullptr;
 }
+
+void SetStageToHostHook(int (*fn)(const Buf& in, Buf* out)) { g_stage_hook = fn; }
 
 void SetDeviceTransportHooks(const DeviceTransportHooks& h) { g_hooks = h; }
 
@@ -22,6 +25,14 @@ bool HasDeviceTransport(Socket* sock) {
 }
 
 void StageDeviceBufToHost(const Buf& in, Buf* out) {
+    // batched path: every device block in one launch into pinned memory
+    if (g_stage_hook) {
+        Buf staged;
+        if (g_stage_hook(in, &staged) == 0) {
+            out->append(std::move(staged));
+            return;
+        }
+    }
     for (size_t i = 0; i < in.backing_block_num(); ++i) {
         const BlockRef& r = in.ref_at(i);
         if (IsHostAccessible(r.block->kind)) {

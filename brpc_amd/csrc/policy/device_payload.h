@@ -50,6 +50,9 @@ bool HasDeviceTransport(Socket* sock);
 
 // Copies every non-host block of `in` to host memory (appends to *out).
 void StageDeviceBufToHost(const Buf& in, Buf* out);
+// Batched staging implementation (gpu/device_handler.h), installed when a
+// device is enabled; returns non-zero to fall back to per-block copies.
+void SetStageToHostHook(int (*fn)(const Buf& in, Buf* out));
 
 namespace policy {
 using DevicePayloads = pb::RepeatedPtrField<DevicePayload>;

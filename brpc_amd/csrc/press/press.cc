@@ -3,6 +3,7 @@
 #include <fstream>
 #include <sstream>
 
+#include "base/crc32c.h"
 #include "base/logging.h"
 #include "base/time.h"
 #include "base/util.h"
@@ -274,6 +275,7 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
         return;
     }
     call->echo_req.set_message(_echo_message);
+    if (_opt.gpu_process) call->echo_req.set_gpu_process(true);
     if (_device_attachment) {
         gpu::AppendDevice(&cntl.request_attachment(), _device_attachment, _attachment.size(), _opt.gpu_device);
     } else if (!_attachment.empty()) {
@@ -299,6 +301,9 @@ void PressSession::finish(PressCall* call) {
             if (gpu::CopyBufToHost(cntl.response_attachment(), &got) != 0 || got != want) {
                 ok = false;
                 cntl.SetFailed(ERESPONSE, "echoed attachment mismatch (%zu bytes)", got.size());
+            } else if (_opt.gpu_process && call->echo_res.crc32c() != crc32c::Value(want.data(), want.size())) {
+                ok = false;
+                cntl.SetFailed(ERESPONSE, "device CRC32C 0x%08x does not match the host's", call->echo_res.crc32c());
             }
         }
     }

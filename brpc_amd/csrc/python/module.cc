@@ -46,6 +46,7 @@ public:
         ServerOptions opt;
         opt.num_threads = num_threads;
         if (max_concurrency > 0) opt.max_concurrency = max_concurrency;
+        if (_echo) _echo->set_gpu_device(gpu_device);
         opt.gpu_device = gpu_device;
         opt.idle_timeout_sec = idle_timeout_s;
         opt.use_rdma = use_rdma;
@@ -69,6 +70,7 @@ public:
     int port() const { return _server.listen_address().port; }
     std::string address() const { return _server.listen_address().to_string(); }
     int64_t echo_calls() const { return _echo ? _echo->ncalls() : 0; }
+    int64_t gpu_calls() const { return _echo ? _echo->gpu_calls() : 0; }
 
 private:
     Server _server;
@@ -136,6 +138,7 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "gpu_device") o.gpu_device = v.cast<int>();
         else if (k == "check_echo") o.check_echo = v.cast<bool>();
         else if (k == "fanout_servers") o.fanout_servers = v.cast<std::string>();
+        else if (k == "gpu_process") o.gpu_process = v.cast<bool>();
         else if (k == "use_rdma") o.use_rdma = v.cast<bool>();
         else if (k == "proto_file") o.proto_file = v.cast<std::string>();
         else if (k == "include_paths") o.include_paths = v.cast<std::string>();
@@ -312,7 +315,8 @@ PYBIND11_MODULE(_native, m) {
         .def("stop", &PyServer::stop)
         .def_property_readonly("port", &PyServer::port)
         .def_property_readonly("address", &PyServer::address)
-        .def_property_readonly("echo_calls", &PyServer::echo_calls);
+        .def_property_readonly("echo_calls", &PyServer::echo_calls)
+        .def_property_readonly("gpu_calls", &PyServer::gpu_calls);
 
     py::class_<PyChannel>(m, "Channel")
         .def(py::init<const std::string&, const std::string&, const std::string&, const std::string&, int, int>(),

@@ -4,6 +4,7 @@
 #include <cstring>
 
 #include "fiber/fiber.h"
+#include "gpu/device_handler.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
 #include "rpc/stream.h"
@@ -37,8 +38,6 @@ private:
 };
 }  // namespace
 
-void (*EchoServiceImpl::device_hook)(RpcController* cntl, example::EchoResponse* response) = nullptr;
-
 void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest* request,
                            example::EchoResponse* response, Closure* done) {
     ClosureGuard done_guard(done);
@@ -66,9 +65,25 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
     }
     response->set_message(request->message());
     response->set_device(-1);
+    if (request->gpu_process()) {
+        if (_gpu_device < 0) {
+            cntl->SetFailed(EREQUEST, "this server has no GPU for gpu_process");
+            return;
+        }
+        uint32_t crc = 0;
+        Buf dev;
+        if (gpu::GatherToDeviceWithCrc(cntl->request_attachment(), &dev, &crc, _gpu_device) != 0) {
+            cntl->SetFailed(EINTERNAL, "device processing of %zu bytes failed", cntl->request_attachment().size());
+            return;
+        }
+        _gpu_calls.fetch_add(1, std::memory_order_relaxed);
+        response->set_device(_gpu_device);
+        response->set_crc32c(crc);
+        cntl->response_attachment().append(std::move(dev));  // served from HBM
+        return;
+    }
     // zero-copy echo of the attachment (host or device blocks alike)
     cntl->response_attachment().append(cntl->request_attachment());
-    if (device_hook && !cntl->request_attachment().empty()) device_hook(cntl, response);
 }
 
 }  // namespace mrpc

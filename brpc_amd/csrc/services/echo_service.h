@@ -14,12 +14,17 @@ public:
     void Echo(RpcController* controller, const example::EchoRequest* request, example::EchoResponse* response,
               Closure* done) override;
     int64_t ncalls() const { return _ncalls.load(); }
-    // Optional device handler: when set (gpu/gpu_echo.cc), attachments are
-    // processed on the GPU (checksum + copy into HBM) before echoing.
-    static void (*device_hook)(RpcController* cntl, example::EchoResponse* response);
+    int64_t gpu_calls() const { return _gpu_calls.load(); }
+    // GPU that serves requests with gpu_process set (-1: none, such
+    // requests fail with EREQUEST). The attachment is gathered into HBM by
+    // a kernel that also checksums it, and echoed from HBM
+    // (gpu/device_handler.h).
+    void set_gpu_device(int device) { _gpu_device = device; }
 
 private:
     std::atomic<int64_t> _ncalls{0};
+    std::atomic<int64_t> _gpu_calls{0};
+    int _gpu_device = -1;
 };
 
 }  // namespace mrpc

@@ -37,3 +37,15 @@ def test_stream_press_fans_out_to_every_peer(native):
     finally:
         for s in servers:
             s.stop()
+
+
+def test_gpu_process_without_gpu_fails_cleanly(native):
+    s = start_echo_server("127.0.0.1:0")
+    try:
+        p = native.Press({"server": s.address, "concurrency": 2, "attachment_size": 100, "gpu_process": True,
+                          "max_retry": 0})
+        p.run_requests(4)
+        st = p.stats()
+        assert st["error"] == 4 and "GPU" in st["last_error"], st
+    finally:
+        s.stop()

@@ -293,3 +293,25 @@ def test_fanout_device_attachment(dev):
     finally:
         for s in servers:
             s.stop()
+
+
+@pytest.mark.parametrize("device_attachment", [False, True])
+def test_gpu_process_echo_handler(dev, device_attachment):
+    """the handler gathers the attachment into HBM with the
+    fused copy+CRC32C kernel and responds from HBM; the client checks the
+    bytes and the device CRC against the host SSE4.2 CRC32C."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        for size in (1, 4095, 65536 - 16, 300000):
+            p = native.Press({"server": s.address, "concurrency": 8, "attachment_size": size,
+                              "device_attachment": device_attachment, "gpu_device": 0,
+                              "gpu_process": True, "check_echo": True})
+            before = s.gpu_calls
+            p.run_requests(200)
+            st = p.stats()
+            assert st["success"] == 200 and st["error"] == 0, (size, st)
+            assert s.gpu_calls - before == 200
+    finally:
+        s.stop()
