@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--workers", type=int, default=0, help="fiber worker pthreads per rank (0: auto)")
     ap.add_argument("--skip-64k", action="store_true")
     ap.add_argument("--skip-fanout", action="store_true", help="skip the ParallelChannel fan-out leg (N>1)")
+    ap.add_argument("--skip-grpc", action="store_true", help="skip the h2:grpc + snappy leg")
+    ap.add_argument("--requests-per-step-grpc", type=int, default=2000)
     ap.add_argument("--requests-per-step-fanout", type=int, default=500)
     ap.add_argument("--skip-stream", action="store_true",
                     help="skip the streaming-RPC leg (64 KiB chunks, BASELINE config 3)")
@@ -191,6 +193,24 @@ def main():
         og.update({"concurrency": a.concurrency, "gpu_process": True})
         rg = timed_leg(wlg, a.steps, a.warmup, og)
 
+    # gRPC + snappy leg (BASELINE config 4): h2:grpc echo of a 64 KiB
+    # protobuf body, snappy-compressed in both directions (grpc-encoding),
+    # once with the CPU codec and once with the codec on the GPU (batched
+    # snappy kernels behind the compress registry, 16 KiB threshold).
+    rz = None
+    if not a.skip_grpc:
+        wlz = EchoWorkload("grpc_snappy_64KB", request_size=65536, attachment_size=0,
+                           requests_per_step=max(1, a.requests_per_step_grpc))
+        oz = wlz.press_options(peer, gpu_device=topo.device)
+        oz.update({"concurrency": a.concurrency, "protocol": "h2:grpc", "request_compress_type": 1})
+        rz = {"cpu": timed_leg(wlz, a.steps, a.warmup, dict(oz))}
+        if cuda:
+            native.gpu.enable_snappy(topo.device, 16384)
+            try:
+                rz["gpu"] = timed_leg(wlz, a.steps, a.warmup, dict(oz))
+            finally:
+                native.gpu.disable_snappy()
+
     # Streaming-RPC leg (BASELINE config 3): 64 KiB chunks through one
     # flow-controlled stream per peer — rank r to every other rank (to its
     # own server when alone); a step is 32 chunks per stream and ends when
@@ -304,6 +324,13 @@ def main():
             out["qps_64KB_host_attachment"] = round(r64h["qps"], 1)
             out["p99_us_64KB_host_attachment"] = r64h["p99_us"]
             out["gbytes_per_s_64KB_host_attachment"] = round(r64h["qps"] * 65536 * 2 / 1e9, 3)
+        if rz:
+            out["grpc_snappy_64KB_qps_cpu_codec"] = round(rz["cpu"]["qps"], 1)
+            out["grpc_snappy_64KB_p99_us_cpu_codec"] = rz["cpu"]["p99_us"]
+            if "gpu" in rz:
+                out["grpc_snappy_64KB_qps_gpu_codec"] = round(rz["gpu"]["qps"], 1)
+                out["grpc_snappy_64KB_p99_us_gpu_codec"] = rz["gpu"]["p99_us"]
+                out["grpc_snappy_errors"] = rz["cpu"]["errors"] + rz["gpu"]["errors"]
         if rg:
             out["qps_64KB_gpu_handler"] = round(rg["qps"], 1)
             out["p99_us_64KB_gpu_handler"] = rg["p99_us"]

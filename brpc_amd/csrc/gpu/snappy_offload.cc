@@ -1,0 +1,345 @@
+// GPU snappy for RPC bodies: the offload behind rpc/compress.h's
+// SetSnappyOffload (reference: src/brpc/policy/snappy_compress.cpp:28-64,
+// src/brpc/compress.cpp:79-92 — ParseFromCompressedData /
+// SerializeAsCompressedData call the registered snappy handler; this is that
+// handler's device half).
+//
+// Wire format is standard raw snappy in both directions, so peers with a
+// CPU codec interoperate:
+//  * compress: the body is staged into HBM (batched copy kernel reading the
+//    pinned socket blocks), cut into 64 KiB blocks that snappy_compress_kernel
+//    encodes one wave each straight into pinned host memory; the stream is
+//    one varint header + the blocks' element runs (a block never references
+//    another, so the concatenation is one valid stream).
+//  * decompress: the host walks the tag stream once to cut it into pieces of
+//    <= 64 KiB uncompressed whose copies stay inside the piece (true for
+//    every fragmenting encoder, ours and google snappy); each piece gets its
+//    own varint header in a pinned staging buffer, snappy_decompress_kernel
+//    decodes all pieces in one launch straight into pinned output. A stream
+//    that cannot be cut that way falls back to the CPU codec.
+// Each direction is one stream-ordered sequence (copy, kernel) and ONE
+// fiber-friendly event wait.
+#include "gpu/snappy_offload.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstring>
+#include <vector>
+
+#include "base/logging.h"
+#include "gpu/gpu.h"
+#include "gpu/hbm_pool.h"
+#include "gpu/kernels.h"
+#include "rpc/compress.h"
+#include "var/var.h"
+
+namespace mrpc {
+namespace gpu {
+
+namespace {
+
+int g_device = -1;
+std::atomic<int64_t> g_comp_calls{0}, g_decomp_calls{0}, g_fallbacks{0};
+
+void pinned_deleter(void* p, void* arg) { PinnedFree(p, (size_t)reinterpret_cast<uintptr_t>(arg)); }
+
+// A pinned host buffer owned by a Buf block (kind PINNED).
+struct PinnedBuf {
+    char* p = nullptr;
+    size_t n = 0;
+    explicit PinnedBuf(size_t bytes) : p(static_cast<char*>(PinnedAlloc(bytes))), n(bytes) {}
+    ~PinnedBuf() {
+        if (p) PinnedFree(p, n);
+    }
+    // hand ownership to *b as one block
+    void give_to(Buf* b) {
+        b->append_user_data(p, n, pinned_deleter, reinterpret_cast<void*>((uintptr_t)n), MemKind::PINNED);
+        p = nullptr;
+    }
+};
+
+struct HbmTmp {
+    void* p = nullptr;
+    size_t n = 0;
+    int dev = -1;
+    HbmTmp(size_t bytes, int d) : p(HbmAlloc(bytes, d)), n(bytes), dev(d) {}
+    ~HbmTmp() {
+        if (p) HbmFree(p, n, dev);
+    }
+};
+
+int varint_len(uint64_t v) {
+    int n = 1;
+    while (v >= 0x80) {
+        v >>= 7;
+        ++n;
+    }
+    return n;
+}
+
+int put_varint(char* out, uint64_t v) {
+    int n = 0;
+    while (v >= 0x80) {
+        out[n++] = (char)((v & 0x7f) | 0x80);
+        v >>= 7;
+    }
+    out[n++] = (char)v;
+    return n;
+}
+
+// Gather segments for `in` into HBM at dst (pageable bytes bounced through
+// `bounce`, which must hold them).
+void gather_segments(const Buf& in, char* dst, char* bounce, std::vector<Segment>* segs) {
+    size_t off = 0, boff = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BlockRef& r = in.ref_at(i);
+        const char* src = r.block->data + r.offset;
+        if (r.block->kind == MemKind::HOST) {
+            memcpy(bounce + boff, src, r.length);
+            src = bounce + boff;
+            boff += r.length;
+        }
+        segs->push_back(Segment{src, dst + off, r.length});
+        off += r.length;
+    }
+}
+
+size_t pageable_bytes(const Buf& in) {
+    size_t n = 0;
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        if (in.ref_at(i).block->kind == MemKind::HOST) n += in.ref_at(i).length;
+    }
+    return n;
+}
+
+bool device_blocks_elsewhere(const Buf& in, int device) {
+    for (size_t i = 0; i < in.backing_block_num(); ++i) {
+        const BufBlock* b = in.ref_at(i).block;
+        if (!IsHostAccessible(b->kind) && b->device != device) return true;
+    }
+    return false;
+}
+
+// Runs `enqueue` on a pool stream of `device`, records an event and parks
+// the calling fiber until it fires.
+template <typename F>
+int run_and_wait(int device, F enqueue) {
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    hipStream_t s = PoolStream(device);
+    int rc = s ? enqueue(s) : -1;
+    if (rc == 0) rc = SyncStream(s);
+    else if (s) SyncStream(s);  // never free buffers a launched kernel may still use
+    if (prev != device) hipSetDevice(prev);
+    return rc;
+}
+
+bool gpu_compress(const Buf& in, Buf* out) {
+    const int dev = g_device;
+    const size_t n = in.size();
+    const size_t nblk = (n + kSnappyMaxBlock - 1) / kSnappyMaxBlock;
+    const size_t cap = (SnappyMaxCompressedLength(kSnappyMaxBlock) + 15) & ~(size_t)15;
+    HbmTmp raw(n, dev), scratch(nblk * SnappyCompressScratchPerBlock(), dev);
+    const size_t pageable = pageable_bytes(in);
+    PinnedBuf bounce(pageable ? pageable : 1), comp(nblk * cap), jobs(nblk * sizeof(SnappyJob)),
+        meta(2 * nblk * sizeof(uint32_t));
+    if (!raw.p || !scratch.p || !bounce.p || !comp.p || !jobs.p || !meta.p) return false;
+    std::vector<Segment> segs;
+    gather_segments(in, static_cast<char*>(raw.p), bounce.p, &segs);
+    SnappyJob* j = reinterpret_cast<SnappyJob*>(jobs.p);
+    for (size_t i = 0; i < nblk; ++i) {
+        const size_t off = i * kSnappyMaxBlock;
+        j[i].src = static_cast<char*>(raw.p) + off;
+        j[i].dst = comp.p + i * cap;
+        j[i].src_len = std::min<size_t>(kSnappyMaxBlock, n - off);
+        j[i].dst_cap = cap;
+    }
+    uint32_t* out_len = reinterpret_cast<uint32_t*>(meta.p);
+    int* err = reinterpret_cast<int*>(out_len + nblk);
+    const int rc = run_and_wait(dev, [&](hipStream_t s) {
+        if (LaunchBatchedCopy(segs.data(), (int)segs.size(), s) != 0) return -1;
+        return LaunchSnappyCompress(j, (int)nblk, scratch.p, out_len, err, s);
+    });
+    if (rc != 0) return false;
+    for (size_t i = 0; i < nblk; ++i) {
+        if (err[i] || out_len[i] > cap) return false;
+    }
+    // one stream: total-length varint + each block's elements (its own
+    // varint header stripped); the compressed bytes stay in the pinned
+    // buffer, referenced zero-copy by the output Buf
+    char hdr[10];
+    out->append(hdr, put_varint(hdr, n));
+    Buf whole;
+    comp.give_to(&whole);
+    size_t pos = 0;
+    for (size_t i = 0; i < nblk; ++i) {
+        const size_t h = (size_t)varint_len(j[i].src_len);
+        whole.pop_front(i * cap + h - pos);
+        whole.cutn(out, out_len[i] - h);
+        pos = i * cap + out_len[i];
+    }
+    return true;
+}
+
+// Cuts a raw snappy stream into pieces of <= kSnappyMaxBlock uncompressed
+// bytes that are self-contained. Returns false when impossible.
+struct Piece {
+    size_t comp_off, comp_len, ulen;
+};
+bool split_stream(const uint8_t* p, size_t n, size_t* total, size_t* hdr_len, std::vector<Piece>* pieces) {
+    uint64_t ulen = 0;
+    size_t i = 0;
+    for (int shift = 0; shift <= 35; shift += 7) {
+        if (i >= n) return false;
+        const uint8_t c = p[i++];
+        ulen |= (uint64_t)(c & 0x7f) << shift;
+        if (!(c & 0x80)) break;
+        if (shift == 35) return false;
+    }
+    *total = ulen;
+    *hdr_len = i;
+    size_t piece_start_comp = i, piece_start_u = 0, upos = 0;
+    while (i < n) {
+        const size_t elem_start = i;
+        const uint8_t tag = p[i++];
+        size_t len = 0, off = 0;
+        bool literal = false;
+        switch (tag & 3) {
+        case 0: {
+            literal = true;
+            size_t l = tag >> 2;
+            if (l >= 60) {
+                const int nb = (int)l - 59;
+                if (i + nb > n) return false;
+                l = 0;
+                for (int k = 0; k < nb; ++k) l |= (size_t)p[i + k] << (8 * k);
+                i += nb;
+            }
+            len = l + 1;
+            if (i + len > n) return false;
+            break;
+        }
+        case 1:
+            if (i + 1 > n) return false;
+            len = 4 + ((tag >> 2) & 7);
+            off = ((size_t)(tag >> 5) << 8) | p[i];
+            i += 1;
+            break;
+        case 2:
+            if (i + 2 > n) return false;
+            len = 1 + (tag >> 2);
+            off = (size_t)p[i] | ((size_t)p[i + 1] << 8);
+            i += 2;
+            break;
+        default:
+            if (i + 4 > n) return false;
+            len = 1 + (tag >> 2);
+            off = (size_t)p[i] | ((size_t)p[i + 1] << 8) | ((size_t)p[i + 2] << 16) | ((size_t)p[i + 3] << 24);
+            i += 4;
+            break;
+        }
+        // start a new piece when this element would overflow the current one
+        if (upos - piece_start_u + len > kSnappyMaxBlock) {
+            if (upos == piece_start_u) return false;  // one element larger than a piece
+            pieces->push_back(Piece{piece_start_comp, elem_start - piece_start_comp, upos - piece_start_u});
+            piece_start_comp = elem_start;
+            piece_start_u = upos;
+        }
+        if (!literal && (off == 0 || off > upos - piece_start_u)) return false;  // crosses the piece start
+        if (literal) i += len;
+        upos += len;
+    }
+    if (upos != ulen) return false;
+    if (upos > piece_start_u) pieces->push_back(Piece{piece_start_comp, n - piece_start_comp, upos - piece_start_u});
+    return true;
+}
+
+bool gpu_decompress(const Buf& in, Buf* out) {
+    const int dev = g_device;
+    std::string flat = in.to_string();  // the tag walk needs contiguous bytes
+    size_t total = 0, hdr = 0;
+    std::vector<Piece> pieces;
+    if (!split_stream(reinterpret_cast<const uint8_t*>(flat.data()), flat.size(), &total, &hdr, &pieces)) {
+        return false;
+    }
+    if (total == 0) return true;
+    // per-piece raw streams (own varint header) back to back, 16 B aligned
+    std::vector<size_t> soff(pieces.size());
+    size_t sbytes = 0;
+    for (size_t k = 0; k < pieces.size(); ++k) {
+        soff[k] = sbytes;
+        sbytes += (varint_len(pieces[k].ulen) + pieces[k].comp_len + 15) & ~(size_t)15;
+    }
+    PinnedBuf staged(sbytes), dst(total), jobs(pieces.size() * sizeof(SnappyJob)), meta(2 * pieces.size() * 4);
+    HbmTmp dstage(sbytes, dev);
+    if (!staged.p || !dst.p || !jobs.p || !meta.p || !dstage.p) return false;
+    SnappyJob* j = reinterpret_cast<SnappyJob*>(jobs.p);
+    size_t upos = 0;
+    uint32_t max_ulen = 1;
+    for (size_t k = 0; k < pieces.size(); ++k) {
+        char* s = staged.p + soff[k];
+        const int h = put_varint(s, pieces[k].ulen);
+        memcpy(s + h, flat.data() + pieces[k].comp_off, pieces[k].comp_len);
+        j[k].src = static_cast<char*>(dstage.p) + soff[k];
+        j[k].dst = dst.p + upos;
+        j[k].src_len = h + pieces[k].comp_len;
+        j[k].dst_cap = pieces[k].ulen;
+        upos += pieces[k].ulen;
+        max_ulen = std::max<uint32_t>(max_ulen, (uint32_t)pieces[k].ulen);
+    }
+    uint32_t* out_len = reinterpret_cast<uint32_t*>(meta.p);
+    int* err = reinterpret_cast<int*>(out_len + pieces.size());
+    Segment seg{staged.p, dstage.p, sbytes};
+    const int rc = run_and_wait(dev, [&](hipStream_t s) {
+        if (LaunchBatchedCopy(&seg, 1, s) != 0) return -1;
+        return LaunchSnappyDecompress(j, (int)pieces.size(), max_ulen, out_len, err, s);
+    });
+    if (rc != 0) return false;
+    for (size_t k = 0; k < pieces.size(); ++k) {
+        if (err[k] || out_len[k] != pieces[k].ulen) return false;
+    }
+    Buf whole;
+    dst.give_to(&whole);
+    out->append(std::move(whole));
+    return true;
+}
+
+bool offload(const Buf& in, Buf* out, bool compress) {
+    if (g_device < 0 || device_blocks_elsewhere(in, g_device)) return false;
+    Buf result;
+    const bool ok = compress ? gpu_compress(in, &result) : gpu_decompress(in, &result);
+    if (!ok) {
+        g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        return false;  // the CPU codec takes over
+    }
+    (compress ? g_comp_calls : g_decomp_calls).fetch_add(1, std::memory_order_relaxed);
+    out->append(std::move(result));
+    return true;
+}
+
+}  // namespace
+
+int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
+    if (Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
+    g_device = device;
+    SetSnappyOffload(offload, min_bytes);
+    static var::PassiveStatus<int64_t> v1("gpu_snappy_compress_calls", [] { return g_comp_calls.load(); });
+    static var::PassiveStatus<int64_t> v2("gpu_snappy_decompress_calls", [] { return g_decomp_calls.load(); });
+    static var::PassiveStatus<int64_t> v3("gpu_snappy_fallbacks", [] { return g_fallbacks.load(); });
+    return 0;
+}
+
+void DisableGpuSnappy() { SetSnappyOffload(nullptr, (size_t)-1); }
+
+GpuSnappyStats GetGpuSnappyStats() {
+    GpuSnappyStats s;
+    s.compress_calls = g_comp_calls.load();
+    s.decompress_calls = g_decomp_calls.load();
+    s.fallbacks = g_fallbacks.load();
+    return s;
+}
+
+}  // namespace gpu
+}  // namespace mrpc

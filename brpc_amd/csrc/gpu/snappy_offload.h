@@ -1,0 +1,24 @@
+// GPU snappy offload for RPC bodies (see snappy_offload.cc): installs the
+// device codec behind rpc/compress.h's snappy handler for bodies of at
+// least min_bytes. Standard raw snappy on the wire; anything the device
+// path cannot take (a stream it cannot cut, HBM blocks of another GPU)
+// falls back to the CPU codec.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace mrpc {
+namespace gpu {
+
+int EnableGpuSnappy(int device, size_t min_bytes, std::string* error = nullptr);
+void DisableGpuSnappy();
+
+struct GpuSnappyStats {
+    int64_t compress_calls = 0, decompress_calls = 0, fallbacks = 0;
+};
+GpuSnappyStats GetGpuSnappyStats();
+
+}  // namespace gpu
+}  // namespace mrpc

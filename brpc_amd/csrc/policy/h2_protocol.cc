@@ -23,6 +23,7 @@
 #include "base/time.h"
 #include "base/util.h"
 #include "fiber/call_id.h"
+#include "fiber/sync.h"
 #include "http/hpack.h"
 #include "http/http_header.h"
 #include "http/http_message.h"
@@ -32,6 +33,7 @@
 #include "rpc/authenticator.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
+#include "rpc/compress.h"
 #include "rpc/grpc.h"
 #include "rpc/method_status.h"
 #include "rpc/protocol.h"
@@ -159,7 +161,7 @@ private:
     int fail_connection(Socket* s, uint32_t code, const char* why);
 
     const bool _server;
-    std::mutex _mu;
+    fiber::Mutex _mu;  // fiber-aware: held across Socket::Write (HPACK order = wire order)
     HPackEncoder _enc;
     HPackDecoder _dec;
     Settings _remote;
@@ -274,7 +276,7 @@ void H2Context::flush_all_locked(Buf* out) {
 
 int H2Context::StartRequest(Socket* s, fiber::CallId cid, const std::vector<HPackHeader>& headers, Buf* body,
                             std::string* err) {
-    std::lock_guard<std::mutex> g(_mu);
+    std::lock_guard<fiber::Mutex> g(_mu);
     if (_goaway) {
         *err = "h2 connection is going away";
         return -1;
@@ -304,7 +306,7 @@ int H2Context::StartRequest(Socket* s, fiber::CallId cid, const std::vector<HPac
 
 int H2Context::SendResponse(Socket* s, uint32_t sid, const std::vector<HPackHeader>& headers, Buf* body,
                             const std::vector<HPackHeader>* trailers) {
-    std::lock_guard<std::mutex> g(_mu);
+    std::lock_guard<fiber::Mutex> g(_mu);
     Stream* st = find(sid);
     if (!st) return -1;  // reset by the client
     Buf out;
@@ -326,7 +328,7 @@ int H2Context::SendResponse(Socket* s, uint32_t sid, const std::vector<HPackHead
 }
 
 void H2Context::CancelStream(Socket* s, uint32_t sid) {
-    std::lock_guard<std::mutex> g(_mu);
+    std::lock_guard<fiber::Mutex> g(_mu);
     if (!find(sid)) return;
     erase(sid);
     Buf out;
@@ -338,7 +340,7 @@ void H2Context::CancelStream(Socket* s, uint32_t sid) {
 
 int H2Context::fail_connection(Socket* s, uint32_t code, const char* why) {
     {
-        std::lock_guard<std::mutex> g(_mu);
+        std::lock_guard<fiber::Mutex> g(_mu);
         Buf out;
         frame_header(&out, 8, H2_GOAWAY, 0, 0);
         const uint32_t last = htonl(_last_peer_stream);
@@ -385,7 +387,7 @@ int H2Context::on_settings(Socket* s, uint8_t flags, Buf& payload) {
         }
         kvs.emplace_back(id, v);
     }
-    std::unique_lock<std::mutex> g(_mu);
+    std::unique_lock<fiber::Mutex> g(_mu);
     for (const auto& kv : kvs) {
         const uint32_t v = kv.second;
         switch (kv.first) {
@@ -457,7 +459,7 @@ int H2Context::on_headers_complete(Socket* s, Stream* st, bool end_stream, HttpM
         st->msg = nullptr;
         (*done)->pi.id_wait = st->cid;
         if (!_server) {
-            std::lock_guard<std::mutex> g(_mu);  // writers insert concurrently
+            std::lock_guard<fiber::Mutex> g(_mu);  // writers insert concurrently
             erase(st->id);
         }
     }
@@ -475,7 +477,7 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
     case H2_PING: {
         if (flags & F_ACK) return 0;
         if (payload.size() != 8) return fail_connection(s, H2_FRAME_SIZE_ERROR, "bad PING");
-        std::lock_guard<std::mutex> g(_mu);
+        std::lock_guard<fiber::Mutex> g(_mu);
         Buf out;
         frame_header(&out, 8, H2_PING, F_ACK, 0);
         out.append(std::move(payload));
@@ -495,7 +497,7 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
         uint32_t rst_code = 0;
         fiber::CallId cid = fiber::INVALID_CALL_ID;
         {
-            std::unique_lock<std::mutex> g(_mu);
+            std::unique_lock<fiber::Mutex> g(_mu);
             Buf out;
             if (sid == 0) {
                 if (_conn_send_window + (int64_t)inc > 0x7FFFFFFF) {
@@ -526,7 +528,7 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
     case H2_GOAWAY: {
         std::vector<std::pair<fiber::CallId, uint32_t>> failed;
         {
-            std::lock_guard<std::mutex> g(_mu);
+            std::lock_guard<fiber::Mutex> g(_mu);
             _goaway = true;
             uint32_t last = 0;
             if (payload.size() >= 4) {
@@ -551,7 +553,7 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
     case H2_RST_STREAM: {
         fiber::CallId cid = fiber::INVALID_CALL_ID;
         {
-            std::lock_guard<std::mutex> g(_mu);
+            std::lock_guard<fiber::Mutex> g(_mu);
             if (Stream* st = find(sid)) {
                 cid = st->cid;
                 erase(sid);
@@ -579,7 +581,7 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
         }
         Stream* st;
         {
-            std::lock_guard<std::mutex> g(_mu);
+            std::lock_guard<fiber::Mutex> g(_mu);
             st = find(sid);
             if (!st) {
                 if (!_server || type == H2_CONTINUATION) return 0;  // stream already gone
@@ -613,7 +615,7 @@ int H2Context::on_frame(Socket* s, uint8_t type, uint8_t flags, uint32_t sid, Bu
             if (p > payload.size()) return fail_connection(s, H2_PROTOCOL_ERROR, "bad padding");
             payload.pop_back(p);
         }
-        std::lock_guard<std::mutex> g(_mu);
+        std::lock_guard<fiber::Mutex> g(_mu);
         Stream* st = find(sid);
         _conn_recv_unacked += flow_len;
         Buf out;
@@ -652,7 +654,7 @@ ParseResult H2Context::Consume(Buf* src, Socket* s) {
         if (memcmp(p, kPreface, kPrefaceLen) != 0) return MakeParseError(PARSE_ERROR_TRY_OTHERS);
         src->pop_front(kPrefaceLen);
         _preface_done = true;
-        std::lock_guard<std::mutex> g(_mu);
+        std::lock_guard<fiber::Mutex> g(_mu);
         Buf out;
         send_local_settings_locked(&out);
         write_locked(s, &out);
@@ -754,7 +756,22 @@ void SerializeH2Request(Buf* buf, Controller* cntl, const pb::Message* request) 
                 return;
             }
             if (grpc) {
-                AddGrpcPrefix(buf, pbbuf, false);
+                // per-message compression (grpc-encoding), through the
+                // compress registry — the snappy handler may run on the GPU
+                const int ct = cntl->request_compress_type();
+                bool compressed = false;
+                if (ct != COMPRESS_TYPE_NONE) {
+                    Buf z;
+                    if (!CompressBuf((CompressType)ct, pbbuf, &z)) {
+                        cntl->SetFailed(EREQUEST, "Fail to compress the grpc request with %s", CompressTypeToCStr((CompressType)ct));
+                        return;
+                    }
+                    pbbuf.swap(z);
+                    compressed = true;
+                    h.SetHeader("grpc-encoding", CompressTypeToGrpcEncoding(ct));
+                }
+                h.SetHeader("grpc-accept-encoding", "identity,gzip,deflate,snappy");
+                AddGrpcPrefix(buf, pbbuf, compressed);
                 h.set_content_type("application/grpc");
             } else {
                 buf->append(std::move(pbbuf));
@@ -855,10 +872,17 @@ void ProcessH2Response(InputMessageBase* msg_base) {
         Buf pbbuf;
         bool compressed = false;
         const int r = RemoveGrpcPrefix(&msg->body, &pbbuf, &compressed);
-        if (r != 1 || compressed) {
+        const std::string* enc = msg->header.GetHeader("grpc-encoding");
+        const int ct = compressed ? GrpcEncodingToCompressType(enc ? *enc : std::string()) : COMPRESS_TYPE_NONE;
+        Buf plain;
+        if (r != 1) {
             saved_error = ERESPONSE;
             cntl->SetFailed(ERESPONSE, "bad grpc response framing");
-        } else if (cntl->_response && !ParsePbFromBuf(cntl->_response, pbbuf)) {
+        } else if (compressed && (ct <= 0 || !DecompressBuf((CompressType)ct, pbbuf, &plain))) {
+            saved_error = ERESPONSE;
+            cntl->SetFailed(ERESPONSE, "Fail to decompress the grpc response (grpc-encoding=%s)",
+                            enc ? enc->c_str() : "<missing>");
+        } else if (cntl->_response && !ParsePbFromBuf(cntl->_response, compressed ? plain : pbbuf)) {
             saved_error = ERESPONSE;
             cntl->SetFailed(ERESPONSE, "Fail to parse grpc response");
         }
@@ -912,8 +936,15 @@ static void SendH2Response(H2ServerCall c) {
         std::vector<HPackHeader> trailers;
         if (!cntl->Failed() && c.res) {
             Buf pbbuf;
+            const int ct = cntl->response_compress_type();
+            Buf z;
             if (!c.res->IsInitialized() || !c.res->SerializeToBuf(&pbbuf)) {
                 cntl->SetFailed(ERESPONSE, "Fail to serialize response");
+            } else if (ct != COMPRESS_TYPE_NONE && !CompressBuf((CompressType)ct, pbbuf, &z)) {
+                cntl->SetFailed(ERESPONSE, "Fail to compress the grpc response");
+            } else if (ct != COMPRESS_TYPE_NONE) {
+                hs.push_back({"grpc-encoding", CompressTypeToGrpcEncoding(ct)});
+                AddGrpcPrefix(&body, z, true);
             } else {
                 AddGrpcPrefix(&body, pbbuf, false);
             }
@@ -1015,10 +1046,23 @@ void ProcessH2Request(InputMessageBase* msg_base) {
             Buf pbbuf;
             bool compressed = false;
             const int r = RemoveGrpcPrefix(&msg->body, &pbbuf, &compressed);
-            if (r != 1 || compressed) {
-                cntl->SetFailed(EREQUEST, compressed ? "compressed grpc messages are not supported"
-                                                     : "bad grpc message framing");
+            if (r != 1) {
+                cntl->SetFailed(EREQUEST, "bad grpc message framing");
                 break;
+            }
+            if (compressed) {
+                const std::string* enc = req_h.GetHeader("grpc-encoding");
+                const int ct = GrpcEncodingToCompressType(enc ? *enc : std::string());
+                Buf plain;
+                if (ct <= 0 || !DecompressBuf((CompressType)ct, pbbuf, &plain)) {
+                    cntl->SetFailed(EREQUEST, "Fail to decompress the grpc request (grpc-encoding=%s)",
+                                    enc ? enc->c_str() : "<missing>");
+                    break;
+                }
+                pbbuf.swap(plain);
+                // answer in the client's encoding unless the service decides otherwise
+                cntl->set_request_compress_type((CompressType)ct);
+                cntl->set_response_compress_type((CompressType)ct);
             }
             if (!ParsePbFromBuf(call.req, pbbuf)) {
                 cntl->SetFailed(EREQUEST, "Fail to parse grpc request as %s",

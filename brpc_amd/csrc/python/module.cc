@@ -12,7 +12,9 @@
 #include "fiber/fiber.h"
 #include "gpu/gpu.h"
 #include "gpu/copy_engine.h"
+#include "rpc/compress.h"
 #include "gpu/hbm_pool.h"
+#include "gpu/snappy_offload.h"
 #include "gpu/xgmi.h"
 #include "mrpc/proto/echo.pb.h"
 #include "press/press.h"
@@ -298,6 +300,30 @@ PYBIND11_MODULE(_native, m) {
         if (!snappy::Uncompress(s.data(), s.size(), &out)) throw std::invalid_argument("malformed snappy stream");
         return py::bytes(out);
     });
+    // The body codec registry (rpc/compress.h) exactly as protocols call it:
+    // a registered offload (GPU snappy) applies here too.
+    m.def("compress", [](int type, py::bytes b) {
+        std::string s = b;
+        Buf in(s), out;
+        bool ok;
+        {
+            py::gil_scoped_release nogil;
+            ok = CompressBuf((CompressType)type, in, &out);
+        }
+        if (!ok) throw std::invalid_argument("compression failed");
+        return py::bytes(out.to_string());
+    });
+    m.def("decompress", [](int type, py::bytes b) {
+        std::string s = b;
+        Buf in(s), out;
+        bool ok;
+        {
+            py::gil_scoped_release nogil;
+            ok = DecompressBuf((CompressType)type, in, &out);
+        }
+        if (!ok) throw std::invalid_argument("decompression failed");
+        return py::bytes(out.to_string());
+    });
     m.def("fiber_stats", [] {
         py::dict d;
         d["fibers"] = fiber::fiber_count();
@@ -372,6 +398,19 @@ PYBIND11_MODULE(_native, m) {
         return d;
     });
     g.def("reap_lent", [] { gpu::ReapLentBlocks(); });
+    g.def("enable_snappy", [](int dev, size_t min_bytes) {
+        std::string err;
+        if (gpu::EnableGpuSnappy(dev, min_bytes, &err) != 0) throw std::runtime_error(err);
+    }, py::arg("device") = 0, py::arg("min_bytes") = 32768);
+    g.def("disable_snappy", [] { gpu::DisableGpuSnappy(); });
+    g.def("snappy_stats", [] {
+        const gpu::GpuSnappyStats s = gpu::GetGpuSnappyStats();
+        py::dict d;
+        d["compress_calls"] = s.compress_calls;
+        d["decompress_calls"] = s.decompress_calls;
+        d["fallbacks"] = s.fallbacks;
+        return d;
+    });
     g.def("hbm_pool_stats", [](int dev) {
         const gpu::HbmPoolStats s = gpu::GetHbmPoolStats(dev);
         py::dict d;

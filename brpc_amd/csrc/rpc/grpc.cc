@@ -1,5 +1,7 @@
 #include "rpc/grpc.h"
 
+#include "rpc/compress.h"
+
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -129,6 +131,23 @@ int RemoveGrpcPrefix(Buf* in, Buf* message, bool* compressed) {
     in->cutn(message, n);
     if (compressed) *compressed = head[0] == 1;
     return 1;
+}
+
+int GrpcEncodingToCompressType(const std::string& name) {
+    if (name.empty() || name == "identity") return COMPRESS_TYPE_NONE;
+    if (name == "gzip") return COMPRESS_TYPE_GZIP;
+    if (name == "deflate") return COMPRESS_TYPE_ZLIB;
+    if (name == "snappy") return COMPRESS_TYPE_SNAPPY;
+    return -1;
+}
+
+const char* CompressTypeToGrpcEncoding(int type) {
+    switch (type) {
+    case COMPRESS_TYPE_GZIP: return "gzip";
+    case COMPRESS_TYPE_ZLIB: return "deflate";
+    case COMPRESS_TYPE_SNAPPY: return "snappy";
+    default: return "identity";
+    }
 }
 
 }  // namespace mrpc

@@ -43,5 +43,9 @@ void AddGrpcPrefix(Buf* out, const Buf& message, bool compressed);
 // Cuts one length-prefixed message from `in`. Returns 1 ok, 0 not enough
 // data, -1 malformed.
 int RemoveGrpcPrefix(Buf* in, Buf* message, bool* compressed);
+// grpc-encoding names <-> compress types ("identity" = none, "gzip",
+// "deflate" = zlib, "snappy"). Unknown names map to -1.
+int GrpcEncodingToCompressType(const std::string& name);
+const char* CompressTypeToGrpcEncoding(int type);
 
 }  // namespace mrpc

@@ -8,7 +8,7 @@ namespace mrpc {
 void OrderedResponseWriter::Deliver(uint64_t seq, Buf* packet, Socket* sock) {
     Buf out;
     {
-        std::lock_guard<std::mutex> g(_mu);
+        std::lock_guard<fiber::Mutex> g(_mu);
         if (seq != _next_send) {
             _ready[seq].swap(*packet);
             return;

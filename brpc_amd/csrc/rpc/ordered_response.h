@@ -10,6 +10,7 @@
 #include <mutex>
 
 #include "base/buf.h"
+#include "fiber/sync.h"
 
 namespace mrpc {
 
@@ -23,7 +24,7 @@ public:
 
 private:
     uint64_t _next_assign = 0;
-    std::mutex _mu;
+    fiber::Mutex _mu;  // fiber-aware: held across Socket::Write
     uint64_t _next_send = 0;
     std::map<uint64_t, Buf> _ready;
 };

@@ -88,7 +88,7 @@ public:
 
     // Chunks one message with the negotiated outgoing chunk size.
     int SendMessage(uint32_t csid, uint8_t type, uint32_t ts, uint32_t stream_id, const Buf& body) {
-        std::lock_guard<std::mutex> g(_write_mu);
+        std::lock_guard<fiber::Mutex> g(_write_mu);
         Buf out;
         std::string h;
         auto basic = [&](uint8_t fmt) {
@@ -211,7 +211,7 @@ public:
         }
     }
     void set_out_chunk_size(uint32_t n) {
-        std::lock_guard<std::mutex> g(_write_mu);
+        std::lock_guard<fiber::Mutex> g(_write_mu);
         _out_chunk_size = n;
     }
     RtmpConnectRequest connect_req;
@@ -231,7 +231,7 @@ private:
     uint32_t _in_chunk_size = kDefaultChunkSize;
     uint32_t _out_chunk_size = kDefaultChunkSize;
     std::map<uint32_t, ChunkState> _chunks;
-    std::mutex _write_mu;
+    fiber::Mutex _write_mu;  // fiber-aware: held across Socket::Write
     std::mutex _mu;
     std::map<uint32_t, StreamEntry> _streams;
     std::map<double, TxCallback> _pending_tx;

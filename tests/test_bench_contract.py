@@ -16,7 +16,7 @@ def _json_lines(out):
 
 def test_bench_single_rank():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--requests-per-step", "2000", "--requests-per-step-64k", "500",
+                        "--requests-per-step", "2000", "--requests-per-step-64k", "500", "--requests-per-step-grpc", "100",
                         "--latency-sample-s", "0.3"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
@@ -34,7 +34,7 @@ def test_bench_two_ranks_gloo():
                         "--master-addr", "127.0.0.1", "--master-port", "29517",
                         os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
                         "--requests-per-step", "1000", "--requests-per-step-64k", "300",
-                        "--requests-per-step-fanout", "100",
+                        "--requests-per-step-fanout", "100", "--requests-per-step-grpc", "50",
                         "--latency-sample-s", "0.3", "--workers", "2"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
