@@ -248,130 +248,227 @@ public:
 };
 
 // ------------------------------------------------------------------ locality aware
-struct LAStat {
-    std::atomic<int64_t> ema_latency_us{0};
-    std::atomic<int64_t> inflight{0};
+// Locality-aware LB (reference src/brpc/policy/locality_aware_load_balancer.h
+// :41-216, docs/cn/lalb.md): a server's weight is proportional to its
+// throughput capacity, kLAWeightScale / avg_latency, and is punished while
+// its in-flight calls are older than its average latency (weight *=
+// avg_latency / inflight_delay), so a server that suddenly stalls sheds
+// traffic before its calls even complete.
+//
+// Selection is O(log n) and lock-free: the weights sit in a Fenwick tree
+// (an implicit complete binary tree of prefix sums) of atomics inside the
+// DoublyBufferedData copy; a select draws r in [0, total) and descends the
+// tree with atomic loads. Feedback and selection re-weight one server and
+// push the difference up its Fenwick path with fetch_add. Each tree copy
+// keeps its own leaf values, so a copy rebuilt concurrently with an update
+// converges at that server's next update instead of drifting. The only lock
+// is a per-server mutex around that server's latency statistics.
+const int64_t kLAWeightScale = (int64_t)1 << 40;
+const int64_t kLAMinWeight = 1000;  // never starve a server completely
+
+struct LAServerStats {
+    std::mutex mu;
+    int64_t avg_latency_us = 0;  // EMA; 0 = no sample yet
+    int64_t inflight = 0;
+    int64_t inflight_begin_sum_us = 0;
+    int64_t samples = 0;
+    std::atomic<int64_t> weight{0};  // last computed weight
     std::atomic<int64_t> errors{0};
+
+    // Weight from the statistics (caller holds mu).
+    int64_t compute_locked(int64_t now_us, int64_t default_latency) const {
+        const int64_t lat = std::max<int64_t>(avg_latency_us > 0 ? avg_latency_us : default_latency, 1);
+        int64_t w = kLAWeightScale / lat;
+        if (inflight > 0) {
+            const int64_t delay = now_us - inflight_begin_sum_us / inflight;
+            if (delay > lat) w = (int64_t)((double)w * (double)lat / (double)delay);
+        }
+        return std::max(w, kLAMinWeight);
+    }
 };
 
-struct LAList {
+struct LATree {
     std::vector<ServerId> servers;
-    std::vector<std::shared_ptr<LAStat>> stats;
+    std::vector<std::shared_ptr<LAServerStats>> stats;
+    std::unique_ptr<std::atomic<int64_t>[]> fen;   // 1-based Fenwick tree
+    std::unique_ptr<std::atomic<int64_t>[]> leaf;  // this copy's value of each leaf
+    std::unordered_map<SocketId, size_t> index;     // server -> leaf (read-only between rebuilds)
+    size_t n = 0;
+
+    void rebuild() {
+        n = servers.size();
+        index.clear();
+        for (size_t i = 0; i < n; ++i) index[servers[i].id] = i;
+        fen.reset(new std::atomic<int64_t>[n + 1]);
+        leaf.reset(new std::atomic<int64_t>[n]);
+        std::vector<int64_t> f(n + 1, 0);
+        for (size_t i = 0; i < n; ++i) {
+            const int64_t w = std::max(stats[i]->weight.load(std::memory_order_relaxed), kLAMinWeight);
+            leaf[i].store(w, std::memory_order_relaxed);
+            f[i + 1] += w;
+            const size_t parent = (i + 1) + ((i + 1) & (~(i + 1) + 1));
+            if (parent <= n) f[parent] += f[i + 1];
+        }
+        for (size_t i = 0; i <= n; ++i) fen[i].store(f[i], std::memory_order_relaxed);
+    }
+    int64_t total() const {
+        int64_t t = 0;
+        for (size_t i = n; i > 0; i -= i & (~i + 1)) t += fen[i].load(std::memory_order_relaxed);
+        return t;
+    }
+    // Set leaf i to w (lock-free; concurrent setters of one leaf serialise
+    // through the exchange).
+    void set(size_t i, int64_t w) const {
+        const int64_t old = leaf[i].exchange(w, std::memory_order_relaxed);
+        const int64_t diff = w - old;
+        if (!diff) return;
+        for (size_t k = i + 1; k <= n; k += k & (~k + 1)) fen[k].fetch_add(diff, std::memory_order_relaxed);
+    }
+    // Index whose cumulative range contains r (0 <= r < total).
+    size_t find(int64_t r) const {
+        size_t pos = 0;
+        size_t step = 1;
+        while (step * 2 <= n) step *= 2;
+        for (; step; step >>= 1) {
+            if (pos + step <= n) {
+                const int64_t v = fen[pos + step].load(std::memory_order_relaxed);
+                if (v <= r) {
+                    pos += step;
+                    r -= v;
+                }
+            }
+        }
+        return pos < n ? pos : n - 1;
+    }
 };
 
 class LocalityAwareLB : public LoadBalancer {
 public:
     bool AddServer(const ServerId& s) override {
-        auto st = get_stat(s.id);
-        return _db.Modify([&](LAList& l) -> size_t {
-            for (auto& x : l.servers) {
+        auto st = std::make_shared<LAServerStats>();
+        // a newcomer starts at the average weight of the cluster, so it is
+        // explored without being flooded
+        st->weight.store(average_weight(), std::memory_order_relaxed);
+        return _db.Modify([&](LATree& t) -> size_t {
+            for (auto& x : t.servers) {
                 if (x.id == s.id) return 0;
             }
-            l.servers.push_back(s);
-            l.stats.push_back(st);
+            t.servers.push_back(s);
+            t.stats.push_back(st);
+            t.rebuild();
             return 1;
         }) > 0;
     }
     bool RemoveServer(const ServerId& s) override {
-        const bool r = _db.Modify([&s](LAList& l) -> size_t {
-            for (size_t i = 0; i < l.servers.size(); ++i) {
-                if (l.servers[i].id == s.id) {
-                    l.servers.erase(l.servers.begin() + i);
-                    l.stats.erase(l.stats.begin() + i);
+        return _db.Modify([&s](LATree& t) -> size_t {
+            for (size_t i = 0; i < t.servers.size(); ++i) {
+                if (t.servers[i].id == s.id) {
+                    t.servers.erase(t.servers.begin() + i);
+                    t.stats.erase(t.stats.begin() + i);
+                    t.rebuild();
                     return 1;
                 }
             }
             return 0;
         }) > 0;
-        return r;
     }
     size_t ServerCount() const override {
-        DoublyBufferedData<LAList>::ScopedPtr p;
-        const_cast<DoublyBufferedData<LAList>&>(_db).Read(&p);
-        return p->servers.size();
+        DoublyBufferedData<LATree>::ScopedPtr p;
+        const_cast<DoublyBufferedData<LATree>&>(_db).Read(&p);
+        return p->n;
     }
     int SelectServer(const SelectIn& in, SelectOut* out) override {
-        DoublyBufferedData<LAList>::ScopedPtr p;
+        DoublyBufferedData<LATree>::ScopedPtr p;
         _db.Read(&p);
-        const size_t n = p->servers.size();
-        if (n == 0) return EHOSTDOWN;
-        // weight = 1e9 / (latency * (inflight + 1)); servers without samples
-        // get the average weight so that they are explored.
-        double total = 0;
-        std::vector<double> w(n);
-        int64_t known = 0, sum_lat = 0;
-        for (size_t i = 0; i < n; ++i) {
-            const int64_t l = p->stats[i]->ema_latency_us.load(std::memory_order_relaxed);
-            if (l > 0) {
-                sum_lat += l;
-                ++known;
-            }
+        const LATree& t = *p;
+        if (t.n == 0) return EHOSTDOWN;
+        const int64_t now = in.begin_time_us ? in.begin_time_us : monotonic_us();
+        // weighted draws first; if they keep hitting excluded or unavailable
+        // servers, scan from a random start for any usable one (excluded
+        // servers last, as the other LBs do)
+        size_t chosen = t.n;
+        for (size_t attempt = 0; attempt < t.n + 2 && chosen == t.n; ++attempt) {
+            const int64_t total = t.total();
+            const size_t i = total > 0 ? t.find((int64_t)fast_rand_less_than((uint64_t)total))
+                                       : (size_t)fast_rand_less_than(t.n);
+            if (in.excluded && in.excluded->IsExcluded(t.servers[i].id)) continue;
+            if (IsServerAvailable(t.servers[i].id, out->ptr)) chosen = i;
         }
-        const int64_t avg = known ? sum_lat / known : 1000;
-        for (size_t i = 0; i < n; ++i) {
-            if (in.excluded && in.excluded->IsExcluded(p->servers[i].id)) {
-                w[i] = 0;
-                continue;
-            }
-            int64_t l = p->stats[i]->ema_latency_us.load(std::memory_order_relaxed);
-            if (l <= 0) l = avg;
-            const int64_t inflight = p->stats[i]->inflight.load(std::memory_order_relaxed);
-            w[i] = 1e9 / ((double)std::max<int64_t>(l, 1) * (double)(inflight + 1));
-            total += w[i];
-        }
-        for (int attempt = 0; attempt < (int)n + 1; ++attempt) {
-            size_t idx;
-            if (total > 0) {
-                double r = fast_rand_double() * total;
-                idx = 0;
-                while (idx + 1 < n && r >= w[idx]) {
-                    r -= w[idx];
-                    ++idx;
+        for (int pass = 0; pass < 2 && chosen == t.n; ++pass) {
+            const size_t start = (size_t)fast_rand_less_than(t.n);
+            for (size_t k = 0; k < t.n; ++k) {
+                const size_t i = (start + k) % t.n;
+                if (pass == 0 && in.excluded && in.excluded->IsExcluded(t.servers[i].id)) continue;
+                if (IsServerAvailable(t.servers[i].id, out->ptr)) {
+                    chosen = i;
+                    break;
                 }
-            } else {
-                idx = fast_rand_less_than(n);
             }
-            if (IsServerAvailable(p->servers[idx].id, out->ptr)) {
-                p->stats[idx]->inflight.fetch_add(1, std::memory_order_relaxed);
-                out->need_feedback = true;
-                return 0;
-            }
-            total -= w[idx];
-            w[idx] = 0;
         }
-        return EHOSTDOWN;
+        if (chosen == t.n) return EHOSTDOWN;
+        LAServerStats& st = *t.stats[chosen];
+        int64_t w;
+        {
+            std::lock_guard<std::mutex> g(st.mu);
+            ++st.inflight;
+            st.inflight_begin_sum_us += now;
+            w = st.compute_locked(now, _default_latency.load(std::memory_order_relaxed));
+        }
+        st.weight.store(w, std::memory_order_relaxed);
+        t.set(chosen, w);
+        out->need_feedback = true;
+        return 0;
     }
     void Feedback(const CallInfo& info) override {
-        auto st = find_stat(info.server_id);
-        if (!st) return;
-        st->inflight.fetch_sub(1, std::memory_order_relaxed);
-        int64_t lat = monotonic_us() - info.begin_time_us;
-        if (info.error_code) {
-            // punish errors: count them as slow calls
-            st->errors.fetch_add(1, std::memory_order_relaxed);
-            lat = std::max<int64_t>(lat, 2 * std::max<int64_t>(st->ema_latency_us.load(), 1000));
+        DoublyBufferedData<LATree>::ScopedPtr p;
+        _db.Read(&p);
+        const LATree& t = *p;
+        auto it = t.index.find(info.server_id);
+        if (it == t.index.end()) return;  // removed meanwhile
+        const size_t i = it->second;
+        LAServerStats& st = *t.stats[i];
+        const int64_t now = monotonic_us();
+        int64_t lat = now - info.begin_time_us;
+        int64_t w;
+        {
+            std::lock_guard<std::mutex> g(st.mu);
+            if (st.inflight > 0) {
+                --st.inflight;
+                st.inflight_begin_sum_us -= info.begin_time_us;
+            }
+            if (info.error_code) {
+                // an error costs like a slow call (reference: punish_error_ratio)
+                st.errors.fetch_add(1, std::memory_order_relaxed);
+                lat = std::max<int64_t>(lat, 2 * std::max<int64_t>(st.avg_latency_us, 1000));
+            }
+            lat = std::max<int64_t>(lat, 1);
+            // EMA that converges fast for the first samples
+            const int64_t k = std::min<int64_t>(st.samples + 1, 8);
+            st.avg_latency_us = st.samples == 0 ? lat : (st.avg_latency_us * (k - 1) + lat) / k;
+            ++st.samples;
+            w = st.compute_locked(now, _default_latency.load(std::memory_order_relaxed));
         }
-        int64_t old = st->ema_latency_us.load(std::memory_order_relaxed);
-        st->ema_latency_us.store(old == 0 ? lat : (old * 7 + lat) / 8, std::memory_order_relaxed);
+        st.weight.store(w, std::memory_order_relaxed);
+        t.set(i, w);
+        int64_t d = _default_latency.load(std::memory_order_relaxed);
+        _default_latency.store(d == 0 ? lat : (d * 15 + lat) / 16, std::memory_order_relaxed);
     }
     LoadBalancer* New(const std::string&) const override { return new LocalityAwareLB; }
-    void Describe(std::ostream& os) const override { os << "la"; }
+    void Describe(std::ostream& os) const override {
+        os << "la";
+        DoublyBufferedData<LATree>::ScopedPtr p;
+        const_cast<DoublyBufferedData<LATree>&>(_db).Read(&p);
+        os << "{n=" << p->n << " total=" << p->total() << "}";
+    }
 
 private:
-    std::shared_ptr<LAStat> get_stat(SocketId id) {
-        std::lock_guard<std::mutex> g(_mu);
-        auto& s = _stats[id];
-        if (!s) s = std::make_shared<LAStat>();
-        return s;
+    int64_t average_weight() {
+        DoublyBufferedData<LATree>::ScopedPtr p;
+        _db.Read(&p);
+        return p->n ? std::max(p->total() / (int64_t)p->n, kLAMinWeight) : kLAWeightScale / 1000;
     }
-    std::shared_ptr<LAStat> find_stat(SocketId id) {
-        std::lock_guard<std::mutex> g(_mu);
-        auto it = _stats.find(id);
-        return it == _stats.end() ? nullptr : it->second;
-    }
-    DoublyBufferedData<LAList> _db;
-    std::mutex _mu;
-    std::unordered_map<SocketId, std::shared_ptr<LAStat>> _stats;
+    DoublyBufferedData<LATree> _db;
+    std::atomic<int64_t> _default_latency{0};
 };
 
 // ------------------------------------------------------------------ consistent hashing

@@ -24,9 +24,22 @@ bool snappy_compress(const Buf& in, Buf* out) {
     return true;
 }
 
+// Uncompressed length from the stream's varint header (0 if malformed).
+size_t snappy_ulen(const Buf& in) {
+    unsigned char h[5];
+    const size_t n = in.copy_to(h, sizeof(h));
+    size_t v = 0;
+    for (size_t i = 0; i < n; ++i) {
+        v |= (size_t)(h[i] & 0x7f) << (7 * i);
+        if (!(h[i] & 0x80)) return v;
+    }
+    return 0;
+}
+
 bool snappy_decompress(const Buf& in, Buf* out) {
     SnappyOffload off = g_snappy_offload.load(std::memory_order_acquire);
-    if (off && in.size() >= g_snappy_offload_min && off(in, out, false)) return true;
+    // offload by the work (the uncompressed size), not the wire size
+    if (off && snappy_ulen(in) >= g_snappy_offload_min && off(in, out, false)) return true;
     std::string src = in.to_string();
     std::string dst;
     if (!snappy::Uncompress(src.data(), src.size(), &dst)) return false;
