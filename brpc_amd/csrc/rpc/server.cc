@@ -464,6 +464,23 @@ int Server::ResetMaxConcurrency(const AdaptiveMaxConcurrency& amc) {
 
 int Server::max_concurrency() const { return _amc.max_concurrency(); }
 
+int Server::SetMaxConcurrencyOf(const std::string& full_method_name, const AdaptiveMaxConcurrency& amc) {
+    const size_t dot = full_method_name.rfind('.');
+    if (dot == std::string::npos) return -1;
+    const MethodProperty* mp =
+        FindMethodPropertyByFullName(full_method_name.substr(0, dot), full_method_name.substr(dot + 1));
+    if (!mp || !mp->status) return -1;
+    return mp->status->SetMaxConcurrency(amc);
+}
+
+AdaptiveMaxConcurrency Server::MaxConcurrencyOf(const std::string& full_method_name) const {
+    const size_t dot = full_method_name.rfind('.');
+    if (dot == std::string::npos) return AdaptiveMaxConcurrency();
+    const MethodProperty* mp = const_cast<Server*>(this)->FindMethodPropertyByFullName(
+        full_method_name.substr(0, dot), full_method_name.substr(dot + 1));
+    return mp && mp->status ? mp->status->max_concurrency() : AdaptiveMaxConcurrency();
+}
+
 bool Server::AddConcurrency(Controller* c) {
     const int cc = _concurrency.fetch_add(1, std::memory_order_relaxed) + 1;
     if (_cl && !_cl->OnRequested(cc, c)) {

@@ -121,6 +121,11 @@ public:
     int listen_port() const { return _listen_addr.port; }
     const ServerOptions& options() const { return _options; }
     int ResetMaxConcurrency(const AdaptiveMaxConcurrency& amc);
+    // Per-method admission (reference Server::MaxConcurrencyOf): "N",
+    // "auto", "timeout" or "unlimited" for "pkg.Service.Method" (or
+    // "Service.Method"). 0 on success, -1 if no such method.
+    int SetMaxConcurrencyOf(const std::string& full_method_name, const AdaptiveMaxConcurrency& amc);
+    AdaptiveMaxConcurrency MaxConcurrencyOf(const std::string& full_method_name) const;
     int max_concurrency() const;
     // server-wide concurrency (AddConcurrency/RemoveConcurrency)
     bool AddConcurrency(Controller* c);
