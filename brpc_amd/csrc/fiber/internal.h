@@ -133,6 +133,7 @@ struct TaskMeta {
     KeyTable* local_storage = nullptr;
     void* span = nullptr;  // rpcz parent span (opaque)
     int64_t start_ns = 0;
+    void* tsan_fiber = nullptr;  // ThreadSanitizer fiber of this context (TSan builds)
     std::mutex version_lock;
 };
 

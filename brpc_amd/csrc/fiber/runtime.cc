@@ -4,6 +4,9 @@
 #include <sanitizer/asan_interface.h>
 #include <sanitizer/common_interface_defs.h>
 #endif
+#if defined(__SANITIZE_THREAD__)
+#include <sanitizer/tsan_interface.h>
+#endif
 #include <sys/mman.h>
 
 #include <cerrno>
@@ -20,6 +23,29 @@
 #include "fiber/internal.h"
 #include "fiber/key_internal.h"
 #include "fiber/timer.h"
+
+// ThreadSanitizer must be told which logical thread (fiber) runs on a stack,
+// or it attributes the accesses of every fiber a worker runs to the worker
+// and reports nonsense: each fiber context gets a TSan fiber,
+// the worker's main context keeps the thread's own, and every stack switch
+// is announced with __tsan_switch_to_fiber right before the jump.
+#if defined(__SANITIZE_THREAD__)
+#define MRPC_TSAN_NEW_CONTEXT(m) ((m)->tsan_fiber = __tsan_create_fiber(0))
+#define MRPC_TSAN_MAIN_CONTEXT(m) ((m)->tsan_fiber = __tsan_get_current_fiber())
+#define MRPC_TSAN_SWITCH(next) __tsan_switch_to_fiber((next)->tsan_fiber, 0)
+#define MRPC_TSAN_DESTROY(m)                   \
+    do {                                       \
+        if ((m)->tsan_fiber && !(m)->is_main) { \
+            __tsan_destroy_fiber((m)->tsan_fiber); \
+        }                                      \
+        (m)->tsan_fiber = nullptr;             \
+    } while (0)
+#else
+#define MRPC_TSAN_NEW_CONTEXT(m) (void)0
+#define MRPC_TSAN_MAIN_CONTEXT(m) (void)0
+#define MRPC_TSAN_SWITCH(next) (void)0
+#define MRPC_TSAN_DESTROY(m) (void)0
+#endif
 
 DEFINE_int32(fiber_concurrency, 8, "Number of fiber worker pthreads");
 DEFINE_int32(fiber_min_concurrency, 0, "Initial number of workers; grows lazily up to fiber_concurrency if > 0");
@@ -186,6 +212,7 @@ int TaskGroup::init(size_t rq_cap) {
     m->stack = nullptr;
     m->attr = ATTR_PTHREAD;
     m->tid = make_tid((uint32_t)m->version_butex->load(std::memory_order_relaxed), slot);
+    MRPC_TSAN_MAIN_CONTEXT(m);
     _main_meta = m;
     _main_tid = m->tid;
     _cur_meta = m;
@@ -269,6 +296,7 @@ void TaskGroup::sched_to_impl(TaskGroup** pg, TaskMeta* next, bool handover) {
         __asan_unpoison_memory_region(s->base, s->size);
 #endif
         next->sp = make_context(s->base, s->size, TaskGroup::task_runner);
+        MRPC_TSAN_NEW_CONTEXT(next);
     }
     if (next != cur) {
         ++g->_nswitch;
@@ -277,6 +305,7 @@ void TaskGroup::sched_to_impl(TaskGroup** pg, TaskMeta* next, bool handover) {
             void* fake_stack = nullptr;
             (void)fake_stack;
             MRPC_ASAN_START_SWITCH(&fake_stack, next);
+            MRPC_TSAN_SWITCH(next);
             mrpc_fiber_jump(&cur->sp, next->sp, nullptr);
             MRPC_ASAN_FINISH_SWITCH(fake_stack);
             g = tls_group();
@@ -313,6 +342,7 @@ void TaskGroup::task_runner(void*) {
         g->_control->nfibers.fetch_sub(1, std::memory_order_relaxed);
         g->set_remained([](void* arg) {
             TaskMeta* dead = (TaskMeta*)arg;
+            MRPC_TSAN_DESTROY(dead);
             if (dead->stack) {
                 return_stack(dead->stack);
                 dead->stack = nullptr;
@@ -335,9 +365,14 @@ void TaskGroup::ending_sched(TaskGroup** pg) {
         (next->attr.stack_type == cur->stack->type ||
          (next->attr.stack_type == STACK_PTHREAD && cur->stack->type == STACK_NORMAL) ||
          (next->attr.stack_type == STACK_UNKNOWN && cur->stack->type == STACK_NORMAL))) {
-        // Hand our stack to the fresh fiber: no context switch needed.
+        // Hand our stack to the fresh fiber: no context switch needed (it
+        // also inherits the TSan fiber of the stack it runs on).
         next->stack = cur->stack;
         cur->stack = nullptr;
+#if defined(__SANITIZE_THREAD__)
+        next->tsan_fiber = cur->tsan_fiber;
+        cur->tsan_fiber = nullptr;
+#endif
         sched_to_impl(pg, next, true);
         return;
     }
@@ -921,18 +956,29 @@ int get_concurrency() {
 static std::atomic<bool> g_about_to_quit{false};
 void about_to_quit() { g_about_to_quit.store(true); }
 
+// Best-effort listing for debuggers (/fibers, gdb helper): it reads the
+// metadata of fibers that keep running, so the values are a racy snapshot
+// by design and ThreadSanitizer is told not to instrument the reads.
+__attribute__((no_sanitize("thread"))) static void describe_one(const TaskMeta* m, int64_t now, std::string* out) {
+    char line[160];
+    snprintf(line, sizeof(line), "tid=%llu fn=%p arg=%p sp=%p stack=%p age_ms=%lld\n", (unsigned long long)m->tid,
+             (void*)m->fn, m->arg, m->sp, (void*)m->stack, (long long)((now - m->start_ns) / 1000000));
+    *out += line;
+}
+
+__attribute__((no_sanitize("thread"))) static bool is_listed(const TaskMeta* m) {
+    return m->version_butex && !m->is_main && m->fn &&
+           (uint32_t)m->version_butex->load(std::memory_order_acquire) == tid_version(m->tid);
+}
+
 std::string DescribeFibers(size_t max_lines) {
     std::string out;
     size_t n = 0;
     const int64_t now = monotonic_ns();
     ResourcePool<TaskMeta>::singleton()->for_each([&](uint32_t, TaskMeta* m) {
-        if (n >= max_lines || !m->version_butex || m->is_main || !m->fn) return;
-        if ((uint32_t)m->version_butex->load(std::memory_order_acquire) != tid_version(m->tid)) return;
+        if (n >= max_lines || !is_listed(m)) return;
         ++n;
-        char line[160];
-        snprintf(line, sizeof(line), "tid=%llu fn=%p arg=%p sp=%p stack=%p age_ms=%lld\n", (unsigned long long)m->tid,
-                 (void*)m->fn, m->arg, m->sp, (void*)m->stack, (long long)((now - m->start_ns) / 1000000));
-        out += line;
+        describe_one(m, now, &out);
     });
     return out;
 }

@@ -702,7 +702,8 @@ bool Socket::IsWriteComplete(WriteRequest* old_head, bool singular_node, WriteRe
     WriteRequest* tail = nullptr;
     WriteRequest* p = new_head;
     do {
-        while (((volatile WriteRequest*)p)->next == UNCONNECTED) sched_yield();
+        // the pusher links `next` right after its exchange (release store)
+        while (__atomic_load_n(&p->next, __ATOMIC_ACQUIRE) == UNCONNECTED) sched_yield();
         WriteRequest* const saved_next = p->next;
         p->next = tail;
         tail = p;
@@ -788,7 +789,7 @@ int Socket::StartWrite(WriteRequest* req, const WriteOptions& opt) {
     WriteRequest* const prev_head = _write_head.exchange(req, std::memory_order_release);
     if (prev_head != nullptr) {
         // Someone is writing; it will pick up this request.
-        req->next = prev_head;
+        __atomic_store_n(&req->next, prev_head, __ATOMIC_RELEASE);  // read by the writer's IsWriteComplete
         return 0;
     }
     req->next = nullptr;

@@ -289,7 +289,7 @@ ssize_t SslSession::Feed(const Buf& raw, Buf* out, bool* handshake_completed) {
     if (!_handshake_done) {
         const int r = SSL_do_handshake(_ssl);
         if (r == 1) {
-            _handshake_done = true;
+            _handshake_done.store(true, std::memory_order_release);
             *handshake_completed = true;
         } else {
             const int e = SSL_get_error(_ssl, r);

@@ -10,6 +10,8 @@
 // record), so one port serves TLS and plaintext clients alike.
 #pragma once
 
+#include <atomic>
+
 #include <cstdint>
 #include <deque>
 #include <memory>
@@ -59,7 +61,8 @@ public:
     SslSession(const std::shared_ptr<SslContext>& ctx, bool server, const std::string& sni);
     ~SslSession();
     bool ok() const { return _ssl != nullptr; }
-    bool handshake_done() const { return _handshake_done; }
+    // read by the writer (KeepWrite) while the reader completes the handshake
+    bool handshake_done() const { return _handshake_done.load(std::memory_order_acquire); }
 
     // Read path: raw ciphertext in, plaintext appended to *out. Returns the
     // plaintext bytes produced, or -1 on a TLS error (errno EPROTO).
@@ -85,7 +88,7 @@ private:
     BIO* _rbio = nullptr;
     BIO* _wbio = nullptr;
     std::mutex _mu;
-    bool _handshake_done = false;
+    std::atomic<bool> _handshake_done{false};
     Buf _cipher_out;                            // ciphertext not yet written
     std::deque<std::pair<size_t, size_t>> _records;  // (cipher bytes, plain bytes) per SSL_write
     size_t _uncredited_plain = 0;               // encrypted plaintext not yet credited

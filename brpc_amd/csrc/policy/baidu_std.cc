@@ -137,8 +137,7 @@ static void SendRpcResponse(int64_t correlation_id, Controller* cntl, pb::Messag
     std::unique_ptr<Controller> cntl_guard(cntl);
     std::unique_ptr<pb::Message> req_guard(req);
     std::unique_ptr<pb::Message> res_guard(res);
-    ConcurrencyRemover remover(method_status, cntl, received_us);
-    if (server) server->RemoveConcurrency();
+    ConcurrencyRemover remover(method_status, cntl, received_us, server);
     SocketUniquePtr sock;
     if (Socket::Address(cntl->_server_socket_id, &sock) != 0) return;  // client gone
     if (cntl->IsCloseConnection()) {

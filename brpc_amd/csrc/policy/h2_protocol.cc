@@ -919,8 +919,7 @@ static void SendH2Response(H2ServerCall c) {
     std::unique_ptr<Controller> cntl_guard(c.cntl);
     std::unique_ptr<pb::Message> req_guard(c.req);
     std::unique_ptr<pb::Message> res_guard(c.res);
-    ConcurrencyRemover remover(c.ms, c.cntl, c.start_us);
-    if (c.server) c.server->RemoveConcurrency();
+    ConcurrencyRemover remover(c.ms, c.cntl, c.start_us, c.server);
     SocketUniquePtr sock;
     if (Socket::Address(c.cntl->_server_socket_id, &sock) != 0) return;
     ParsingContext* pctx = sock->parsing_context();

@@ -219,8 +219,7 @@ static void SendHttpResponse(Controller* cntl, pb::Message* req, pb::Message* re
     std::unique_ptr<Controller> cntl_guard(cntl);
     std::unique_ptr<pb::Message> req_guard(req);
     std::unique_ptr<pb::Message> res_guard(res);
-    ConcurrencyRemover remover(ms, cntl, received_us);
-    if (server) server->RemoveConcurrency();
+    ConcurrencyRemover remover(ms, cntl, received_us, server);
     SocketUniquePtr sock;
     if (Socket::Address(cntl->_server_socket_id, &sock) != 0) {
         if (cntl->_progressive_attachment) cntl->_progressive_attachment->MarkRPCAsDone(true);

@@ -57,8 +57,7 @@ struct MongoCall {
 
 void SendMongoResponse(MongoCall* c) {
     std::unique_ptr<MongoCall> guard(c);
-    ConcurrencyRemover remover(c->status, &c->cntl, c->received_us);
-    if (c->added_concurrency) c->server->RemoveConcurrency();
+    ConcurrencyRemover remover(c->status, &c->cntl, c->received_us, c->added_concurrency ? c->server : nullptr);
     SocketUniquePtr sock;
     if (Socket::Address(c->cntl._server_socket_id, &sock) != 0) return;
     if (c->cntl.IsCloseConnection()) {

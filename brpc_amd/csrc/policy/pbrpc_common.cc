@@ -75,8 +75,7 @@ void SendPbResponse(ServerCallState* st) {
     std::unique_ptr<Controller> cntl(st->cntl);
     std::unique_ptr<pb::Message> req(st->req);
     std::unique_ptr<pb::Message> res(st->res);
-    ConcurrencyRemover remover(st->ms, cntl.get(), st->start_us);
-    if (st->server) st->server->RemoveConcurrency();
+    ConcurrencyRemover remover(st->ms, cntl.get(), st->start_us, st->server);
     SocketUniquePtr sock;
     if (Socket::Address(cntl->_server_socket_id, &sock) != 0) return;
     if (cntl->IsCloseConnection()) {

@@ -67,8 +67,8 @@ struct ThriftCall {
 void SendThriftResponse(ThriftCall* c) {
     std::unique_ptr<ThriftCall> guard(c);
     ThriftService* svc = c->server->options().thrift_service;
-    ConcurrencyRemover remover(svc ? svc->status() : nullptr, &c->cntl, c->received_us);
-    if (c->added_concurrency) c->server->RemoveConcurrency();
+    ConcurrencyRemover remover(svc ? svc->status() : nullptr, &c->cntl, c->received_us,
+                               c->added_concurrency ? c->server : nullptr);
     SocketUniquePtr sock;
     if (Socket::Address(c->cntl._server_socket_id, &sock) != 0) return;
     if (c->cntl.IsCloseConnection()) {

@@ -71,7 +71,7 @@ void finish_parent(PCall* pc, int error_code, const std::string& text) {
     cntl->_end_us = monotonic_us();
     Closure* done = pc->done;
     const fiber::CallId cid = pc->cid;
-    cntl->_correlation_id = fiber::CallId{0};
+    __atomic_store_n(&cntl->_correlation_id.value, 0, __ATOMIC_RELEASE);  // pairs with Controller::Join
     // cancel sub calls still in flight; their done closures only unref
     for (auto& s : pc->subs) {
         if (s->launched) s->cntl.StartCancel();
@@ -721,7 +721,7 @@ void SelectiveChannel::Call::on_attempt_done(Attempt* a) {
         Closure* d = done;
         const fiber::CallId id = cid;
         const bool drop_timer_ref = backup_cancelled;
-        cntl->_correlation_id = fiber::CallId{0};
+        __atomic_store_n(&cntl->_correlation_id.value, 0, __ATOMIC_RELEASE);  // pairs with Controller::Join
         if (fiber::call_id_lock(id, nullptr) == 0) fiber::call_id_unlock_and_destroy(id);
         if (d) d->Run();
         if (drop_timer_ref) unref();
@@ -766,7 +766,7 @@ void SelectiveChannel::CallMethod(const pb::MethodDescriptor* method, RpcControl
     const int idx = select({});
     if (idx < 0) {
         cntl->SetFailed(EHOSTDOWN, "SelectiveChannel has no sub channel");
-        cntl->_correlation_id = fiber::CallId{0};
+        __atomic_store_n(&cntl->_correlation_id.value, 0, __ATOMIC_RELEASE);  // pairs with Controller::Join
         fiber::call_id_unlock_and_destroy(cid);
         c->unref();
         if (done) done->Run();

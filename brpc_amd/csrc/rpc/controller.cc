@@ -145,7 +145,9 @@ fiber::CallId Controller::call_id() {
 }
 
 void Controller::Join() {
-    if (_correlation_id.value) fiber::call_id_join(_correlation_id);
+    // EndRPC may clear the id concurrently (async calls joined by the user)
+    const fiber::CallId cid{__atomic_load_n(&_correlation_id.value, __ATOMIC_ACQUIRE)};
+    if (cid.value) fiber::call_id_join(cid);
 }
 
 void Controller::CloseConnection(const char* reason) {
@@ -189,7 +191,8 @@ void Controller::ReadProgressiveAttachmentBy(ProgressiveReader* r) {
 
 void Controller::StartCancel() {
     if (_canceled.exchange(true)) return;
-    if (_correlation_id.value) fiber::call_id_error(_correlation_id, ECANCELED, "canceled");
+    const fiber::CallId cid{__atomic_load_n(&_correlation_id.value, __ATOMIC_ACQUIRE)};
+    if (cid.value) fiber::call_id_error(cid, ECANCELED, "canceled");
     Closure* cb = _cancel_callback;
     _cancel_callback = nullptr;
     if (cb) cb->Run();
@@ -329,7 +332,7 @@ void Controller::EndRPC(fiber::CallId id) {
     Closure* done = _done;
     _done = nullptr;
     const fiber::CallId cid = _correlation_id;
-    _correlation_id = fiber::CallId{0};
+    __atomic_store_n(&_correlation_id.value, 0, __ATOMIC_RELEASE);  // pairs with Join()
     // After this, a sync caller may destroy *this.
     fiber::call_id_unlock_and_destroy(cid);
     if (done) done->Run();

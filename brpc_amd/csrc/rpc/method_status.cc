@@ -1,5 +1,7 @@
 #include "rpc/method_status.h"
 
+#include "rpc/server.h"
+
 #include "base/time.h"
 #include "base/util.h"
 #include "rpc/controller.h"
@@ -48,6 +50,7 @@ std::string MethodStatus::Describe() const {
 
 ConcurrencyRemover::~ConcurrencyRemover() {
     if (_status) _status->OnResponded(_c ? _c->ErrorCode() : 0, monotonic_us() - _received_us);
+    if (_server) _server->RemoveConcurrency();
 }
 
 }  // namespace mrpc

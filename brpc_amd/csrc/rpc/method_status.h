@@ -13,6 +13,7 @@
 namespace mrpc {
 
 class Controller;
+class Server;
 
 class MethodStatus {
 public:
@@ -43,11 +44,15 @@ private:
 // RAII: calls OnResponded on destruction (used by protocols).
 class ConcurrencyRemover {
 public:
-    ConcurrencyRemover(MethodStatus* s, Controller* c, int64_t received_us)
-        : _status(s), _c(c), _received_us(received_us) {}
+    // `server` (when the request was counted in the server's concurrency)
+    // is decremented LAST, after the method status was updated: Server::Join
+    // waits for that count to drain before the statuses may be destroyed.
+    ConcurrencyRemover(MethodStatus* s, Controller* c, int64_t received_us, Server* server = nullptr)
+        : _status(s), _c(c), _received_us(received_us), _server(server) {}
     ~ConcurrencyRemover();
 private:
     MethodStatus* _status;
+    Server* _server;
     Controller* _c;
     int64_t _received_us;
 };

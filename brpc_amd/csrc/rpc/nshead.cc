@@ -39,8 +39,8 @@ void NsheadClosure::Run() {
     std::unique_ptr<NsheadClosure> self(this);
     Controller* cntl = _cntl.get();
     NsheadService* svc = _server->options().nshead_service;
-    ConcurrencyRemover remover(svc ? svc->status() : nullptr, cntl, _received_us);
-    if (_added_concurrency) _server->RemoveConcurrency();
+    ConcurrencyRemover remover(svc ? svc->status() : nullptr, cntl, _received_us,
+                               _added_concurrency ? _server : nullptr);
     SocketUniquePtr sock;
     if (Socket::Address(cntl->_server_socket_id, &sock) != 0) return;
     if (cntl->IsCloseConnection()) {

@@ -436,7 +436,7 @@ int Server::Stop(int closewait_ms) {
 int Server::Join() {
     if (_status.load() != STOPPING) return 0;
     // wait for in-flight requests to drain
-    for (int i = 0; i < 2000 && _concurrency.load() > 0; ++i) fiber::usleep(1000);
+    for (int i = 0; i < 2000 && _concurrency.load(std::memory_order_acquire) > 0; ++i) fiber::usleep(1000);
     if (_am) _am->Join();
     if (_internal_am) _internal_am->Join();
     _am.reset();
@@ -490,7 +490,7 @@ bool Server::AddConcurrency(Controller* c) {
     return true;
 }
 
-void Server::RemoveConcurrency() { _concurrency.fetch_sub(1, std::memory_order_relaxed); }
+void Server::RemoveConcurrency() { _concurrency.fetch_sub(1, std::memory_order_release); }
 
 void* Server::BorrowSessionLocalData() {
     if (!_options.session_local_data_factory) return nullptr;

@@ -342,9 +342,18 @@ TEST(Rpc, streaming_in_order_with_flow_control) {
             ASSERT_EQ(StreamWait(sid, &ts), 0);
         }
     }
-    for (int i = 0; i < 300 && (int)svc.receiver.got.size() < N; ++i) fiber::usleep(10000);
-    ASSERT_EQ((int)svc.receiver.got.size(), N);
-    for (int i = 0; i < N; ++i) EXPECT_EQ(svc.receiver.got[i].substr(0, 4 + std::to_string(i).size()), "msg-" + std::to_string(i));
+    auto received = [&] {
+        std::lock_guard<std::mutex> g(svc.receiver.mu);
+        return (int)svc.receiver.got.size();
+    };
+    for (int i = 0; i < 300 && received() < N; ++i) fiber::usleep(10000);
+    ASSERT_EQ(received(), N);
+    std::vector<std::string> got;
+    {
+        std::lock_guard<std::mutex> g(svc.receiver.mu);
+        got = svc.receiver.got;
+    }
+    for (int i = 0; i < N; ++i) EXPECT_EQ(got[i].substr(0, 4 + std::to_string(i).size()), "msg-" + std::to_string(i));
     StreamClose(sid);
     for (int i = 0; i < 200 && !svc.receiver.closed; ++i) fiber::usleep(5000);
     EXPECT_TRUE(svc.receiver.closed.load());
