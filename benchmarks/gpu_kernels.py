@@ -49,6 +49,18 @@ def main():
             print(json.dumps({"kernel": "crc32c_batch_64KiB", "messages": len(msgs), "bytes": tot, "sec": t,
                               "GBps": tot / t / 1e9}))
         dst = torch.empty_like(buf)
+        from brpc_amd.ops import batched_copy_crc32c
+        ok = int(batched_copy_crc32c([small], [dst[: small.numel()]])[0]) == crc32c_host(small.cpu().numpy().tobytes())
+        t = timeit(lambda: batched_copy_crc32c([buf], [dst]))
+        print(json.dumps({"kernel": "copy_crc32c_fused", "bytes": n, "sec": t, "GBps_read": n / t / 1e9,
+                          "GBps_rw": 2 * n / t / 1e9, "verified": ok}))
+        # the transport's per-tick pull: 64 x 64 KiB payloads in one launch set
+        nb = min(64, n // 65536)
+        pulls_s = [buf[i * 65536:(i + 1) * 65536] for i in range(nb)]
+        pulls_d = [dst[i * 65536:(i + 1) * 65536] for i in range(nb)]
+        t = timeit(lambda: batched_copy(pulls_s, pulls_d))
+        print(json.dumps({"kernel": "pull_batch_64x64KiB", "bytes": nb * 65536, "sec": t,
+                          "GBps_rw": 2 * nb * 65536 / t / 1e9}))
         t = timeit(lambda: batched_copy([buf], [dst]))
         print(json.dumps({"kernel": "batched_copy", "bytes": n, "sec": t, "GBps": 2 * n / t / 1e9}))
         t = timeit(lambda: dst.copy_(buf))

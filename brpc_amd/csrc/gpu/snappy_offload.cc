@@ -7,18 +7,23 @@
 // Wire format is standard raw snappy in both directions, so peers with a
 // CPU codec interoperate:
 //  * compress: the body is staged into HBM (batched copy kernel reading the
-//    pinned socket blocks), cut into 64 KiB blocks that snappy_compress_kernel
-//    encodes one wave each straight into pinned host memory; the stream is
+//    pinned socket blocks), cut into gpu_snappy_block_kb blocks (16 KiB: one
+//    64 KiB body spreads over 4 waves) that snappy_compress_kernel encodes
+//    one wave each straight into pinned host memory; the stream is
 //    one varint header + the blocks' element runs (a block never references
 //    another, so the concatenation is one valid stream).
 //  * decompress: the host walks the tag stream once to cut it into pieces of
-//    <= 64 KiB uncompressed whose copies stay inside the piece (true for
-//    every fragmenting encoder, ours and google snappy); each piece gets its
+//    <= 16 KiB (device streams), else <= 64 KiB, uncompressed whose copies
+//    stay inside the piece (true for every fragmenting encoder, ours and
+//    google snappy); each piece gets its
 //    own varint header in a pinned staging buffer, snappy_decompress_kernel
 //    decodes all pieces in one launch straight into pinned output. A stream
 //    that cannot be cut that way falls back to the CPU codec.
 // Each direction is one stream-ordered sequence (copy, kernel) and ONE
-// fiber-friendly event wait.
+// fiber-friendly event wait. Measured on MI355X (bench.py gRPC leg) the
+// serial snappy format keeps one wave per block busy for hundreds of
+// microseconds, so per-RPC offload loses to the CPU codec on latency; it is
+// opt-in (EnableGpuSnappy) for bodies that are headed to the GPU anyway.
 #include "gpu/snappy_offload.h"
 
 #include <hip/hip_runtime_api.h>
@@ -33,6 +38,11 @@
 #include "gpu/kernels.h"
 #include "rpc/compress.h"
 #include "var/var.h"
+#include "base/flags.h"
+
+DEFINE_int32(gpu_snappy_block_kb, 16,
+             "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
+             "waves (lower latency) at some cost in ratio; <= 64");
 
 namespace mrpc {
 namespace gpu {
@@ -139,8 +149,9 @@ int run_and_wait(int device, F enqueue) {
 bool gpu_compress(const Buf& in, Buf* out) {
     const int dev = g_device;
     const size_t n = in.size();
-    const size_t nblk = (n + kSnappyMaxBlock - 1) / kSnappyMaxBlock;
-    const size_t cap = (SnappyMaxCompressedLength(kSnappyMaxBlock) + 15) & ~(size_t)15;
+    const size_t blk = (size_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
+    const size_t nblk = (n + blk - 1) / blk;
+    const size_t cap = (SnappyMaxCompressedLength(blk) + 15) & ~(size_t)15;
     HbmTmp raw(n, dev), scratch(nblk * SnappyCompressScratchPerBlock(), dev);
     const size_t pageable = pageable_bytes(in);
     PinnedBuf bounce(pageable ? pageable : 1), comp(nblk * cap), jobs(nblk * sizeof(SnappyJob)),
@@ -150,10 +161,10 @@ bool gpu_compress(const Buf& in, Buf* out) {
     gather_segments(in, static_cast<char*>(raw.p), bounce.p, &segs);
     SnappyJob* j = reinterpret_cast<SnappyJob*>(jobs.p);
     for (size_t i = 0; i < nblk; ++i) {
-        const size_t off = i * kSnappyMaxBlock;
+        const size_t off = i * blk;
         j[i].src = static_cast<char*>(raw.p) + off;
         j[i].dst = comp.p + i * cap;
-        j[i].src_len = std::min<size_t>(kSnappyMaxBlock, n - off);
+        j[i].src_len = std::min<size_t>(blk, n - off);
         j[i].dst_cap = cap;
     }
     uint32_t* out_len = reinterpret_cast<uint32_t*>(meta.p);
@@ -188,7 +199,8 @@ bool gpu_compress(const Buf& in, Buf* out) {
 struct Piece {
     size_t comp_off, comp_len, ulen;
 };
-bool split_stream(const uint8_t* p, size_t n, size_t* total, size_t* hdr_len, std::vector<Piece>* pieces) {
+bool split_stream(const uint8_t* p, size_t n, size_t limit, size_t* total, size_t* hdr_len,
+                  std::vector<Piece>* pieces) {
     uint64_t ulen = 0;
     size_t i = 0;
     for (int shift = 0; shift <= 35; shift += 7) {
@@ -241,7 +253,7 @@ bool split_stream(const uint8_t* p, size_t n, size_t* total, size_t* hdr_len, st
             break;
         }
         // start a new piece when this element would overflow the current one
-        if (upos - piece_start_u + len > kSnappyMaxBlock) {
+        if (upos - piece_start_u + len > limit) {
             if (upos == piece_start_u) return false;  // one element larger than a piece
             pieces->push_back(Piece{piece_start_comp, elem_start - piece_start_comp, upos - piece_start_u});
             piece_start_comp = elem_start;
@@ -261,8 +273,13 @@ bool gpu_decompress(const Buf& in, Buf* out) {
     std::string flat = in.to_string();  // the tag walk needs contiguous bytes
     size_t total = 0, hdr = 0;
     std::vector<Piece> pieces;
-    if (!split_stream(reinterpret_cast<const uint8_t*>(flat.data()), flat.size(), &total, &hdr, &pieces)) {
-        return false;
+    // small pieces first (streams from device encoders: more waves, less
+    // latency), then the 64 KiB fragments every host encoder respects
+    const uint8_t* bytes = reinterpret_cast<const uint8_t*>(flat.data());
+    const size_t small = (size_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
+    if (!split_stream(bytes, flat.size(), small, &total, &hdr, &pieces)) {
+        pieces.clear();
+        if (!split_stream(bytes, flat.size(), kSnappyMaxBlock, &total, &hdr, &pieces)) return false;
     }
     if (total == 0) return true;
     // per-piece raw streams (own varint header) back to back, 16 B aligned

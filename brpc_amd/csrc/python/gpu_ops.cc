@@ -54,6 +54,14 @@ void bind_gpu_ops(py::module_& g) {
         for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
         check(gpu::LaunchBatchedCopy(segs.data(), (int)segs.size(), as_stream(stream)), "batched_copy");
     }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("stream") = 0);
+    g.def("batched_copy_crc32c_launch", [](const std::vector<uintptr_t>& srcs, const std::vector<uintptr_t>& dsts,
+                                           const std::vector<uint64_t>& lens, uintptr_t out, uintptr_t stream) {
+        if (srcs.size() != lens.size() || dsts.size() != lens.size()) throw std::invalid_argument("size mismatch");
+        std::vector<gpu::Segment> segs(lens.size());
+        for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
+        check(gpu::LaunchBatchedCopyCrc32c(segs.data(), (int)segs.size(), (uint32_t*)out, as_stream(stream)),
+              "batched_copy_crc32c");
+    }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("out"), py::arg("stream") = 0);
     g.def("pb_scan_launch", [](uintptr_t buf, uint64_t buf_len, uintptr_t offsets, int64_t n, uint32_t max_fields,
                                uintptr_t fields, uintptr_t nfields, uintptr_t stream) {
         check(gpu::LaunchPbScan((const uint8_t*)buf, buf_len, (const int64_t*)offsets, n, max_fields,

@@ -17,3 +17,24 @@ def batched_copy(srcs, dsts):
     dev = srcs[0].device
     native.gpu.batched_copy_launch([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts],
                                    [nbytes(s) for s in srcs], stream_handle(dev))
+
+
+def batched_copy_crc32c(srcs, dsts):
+    """Fused: dsts[i][:] = srcs[i][:] and returns the standard CRC32C of each
+    source (int64 device tensor) — one read of the bytes (the pull kernel of
+    the xGMI transport's verified receives)."""
+    import torch
+    if len(srcs) != len(dsts):
+        raise ValueError("srcs/dsts length mismatch")
+    for s, d in zip(srcs, dsts):
+        require_gpu_tensor(s, "src")
+        require_gpu_tensor(d, "dst")
+        if nbytes(d) < nbytes(s):
+            raise ValueError("destination smaller than source")
+    if not srcs:
+        return None
+    dev = srcs[0].device
+    out = torch.zeros(len(srcs), dtype=torch.int32, device=dev)
+    native.gpu.batched_copy_crc32c_launch([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts],
+                                          [nbytes(s) for s in srcs], out.data_ptr(), stream_handle(dev))
+    return out.to(torch.int64) & 0xFFFFFFFF

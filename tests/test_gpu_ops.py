@@ -315,3 +315,19 @@ def test_gpu_process_echo_handler(dev, device_attachment):
             assert s.gpu_calls - before == 200
     finally:
         s.stop()
+
+
+def test_batched_copy_crc32c_fused(dev):
+    """The fused pull+checksum kernel: bytes copied exactly and CRC32C equal
+    to the host SSE4.2 value, aligned and misaligned segments alike."""
+    from brpc_amd.ops import batched_copy_crc32c, crc32c_host
+    big = torch.randint(0, 256, (1 << 21,), dtype=torch.uint8, device=dev)
+    cases = [(0, 1), (3, 15), (0, 16), (5, 4099), (1, 65521), (16, 1 << 20), (7, (1 << 20) + 333)]
+    srcs = [big[o:o + n] for o, n in cases]
+    outs = [torch.zeros(n + 32, dtype=torch.uint8, device=dev) for _, n in cases]
+    dsts = [outs[i][3 + i:3 + i + n] for i, (_, n) in enumerate(cases)]
+    crcs = batched_copy_crc32c(srcs, dsts).cpu().tolist()
+    torch.cuda.synchronize()
+    for s, d, c in zip(srcs, dsts, crcs):
+        assert torch.equal(s, d)
+        assert c == crc32c_host(s.cpu().numpy().tobytes())
