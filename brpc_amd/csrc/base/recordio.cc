@@ -68,7 +68,26 @@ size_t Record::ByteSize() const {
     return n;
 }
 
-RecordWriter::RecordWriter(const std::string& path) { _f = fopen(path.c_str(), "ab"); }
+RecordWriter::RecordWriter(const std::string& path) {
+    _f = fopen(path.c_str(), "ab");
+    if (_f) fseek(_f, 0, SEEK_END);  // offset() is meaningful before the first write
+}
+
+uint64_t RecordWriter::offset() const {
+    if (!_f) return 0;
+    const long off = ftell(_f);
+    return off < 0 ? 0 : (uint64_t)off;
+}
+
+bool RecordReader::SeekTo(uint64_t offset) {
+    if (!_f || fseek(_f, (long)offset, SEEK_SET) != 0) return false;
+    _buf.clear();
+    _pos = 0;
+    _base = offset;
+    _eof = false;
+    _err = 0;
+    return true;
+}
 RecordWriter::~RecordWriter() {
     if (_f) fclose(_f);
 }
@@ -106,6 +125,7 @@ RecordReader::~RecordReader() {
 bool RecordReader::fill(size_t n) {
     if (_pos > (1u << 20)) {
         _buf.erase(0, _pos);
+        _base += _pos;
         _pos = 0;
     }
     while (_buf.size() - _pos < n && !_eof) {
@@ -175,6 +195,7 @@ bool RecordReader::ReadNext(Record* out) {
             continue;
         }
         out->_payload.append(p, (size_t)(end - p));
+        _last_offset = _base + _pos;
         _pos += kHead + size;
         return true;
     }

@@ -45,6 +45,8 @@ public:
     bool ok() const { return _f != nullptr; }
     int Write(const Record& r);  // 0 on success
     int Flush();
+    // Byte offset the next record will be written at (RecordReader::SeekTo).
+    uint64_t offset() const;
     size_t written_bytes() const { return _bytes; }
 
 private:
@@ -59,6 +61,11 @@ public:
     bool ok() const { return _f != nullptr; }
     // false at end of file (last_error()==0) or on I/O error.
     bool ReadNext(Record* out);
+    // Position the reader at a record boundary returned by
+    // RecordWriter::offset() (random access for indexed stores).
+    bool SeekTo(uint64_t offset);
+    // File offset of the record ReadNext last returned.
+    uint64_t last_offset() const { return _last_offset; }
     int last_error() const { return _err; }
     size_t skipped_bytes() const { return _skipped; }  // bytes dropped while resyncing
 
@@ -67,6 +74,8 @@ private:
     FILE* _f = nullptr;
     std::string _buf;
     size_t _pos = 0;
+    uint64_t _base = 0;  // file offset of _buf[0]
+    uint64_t _last_offset = 0;
     bool _eof = false;
     int _err = 0;
     size_t _skipped = 0;

@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <ctime>
 #include <fstream>
 #include <sstream>
 
@@ -34,6 +35,7 @@
 #include "rpc/method_status.h"
 #include "rpc/server.h"
 #include "rpc/span.h"
+#include "rpc/span_db.h"
 #include "var/var.h"
 
 DEFINE_bool(enable_dir_service, false, "enable /dir (browse the file system)");
@@ -213,16 +215,45 @@ public:
             text(cntl, "rpcz disabled\n");
             return;
         }
-        if (!IsRpczEnabled()) {
-            text(cntl, "rpcz is disabled; visit /rpcz?enable to turn it on\n");
-            return;
-        }
         uint64_t trace = 0;
+        if (const std::string* t = query(cntl, "trace_id")) trace = strtoull(t->c_str(), nullptr, 16);
         if (const std::string* t = query(cntl, "trace")) trace = strtoull(t->c_str(), nullptr, 16);
         size_t max = 100;
         if (const std::string* m = query(cntl, "max")) max = (size_t)atoi(m->c_str());
+        const std::string* tq = query(cntl, "time");
+        // time=<epoch us> or time=YYYY/MM/DD-HH:MM:SS (local time): spans
+        // that ended at or before it, from the on-disk store
+        int64_t before_us = 0;
+        if (tq) {
+            struct tm tmv = {};
+            if (strptime(tq->c_str(), "%Y/%m/%d-%H:%M:%S", &tmv)) {
+                tmv.tm_isdst = -1;
+                before_us = (int64_t)mktime(&tmv) * 1000000 + 999999;
+            } else {
+                before_us = strtoll(tq->c_str(), nullptr, 10);
+            }
+        }
+        const span_db::Stats st = span_db::GetStats();
+        if (!IsRpczEnabled() && st.indexed == 0) {
+            text(cntl, "rpcz is disabled; visit /rpcz?enable to turn it on\n");
+            return;
+        }
         std::ostringstream os;
-        for (const std::string& s : ListRecentSpans(max, trace)) os << s << "\n";
+        if (query(cntl, "stats")) {
+            os << "dir: " << st.dir << "\nwritten: " << st.written << "\ndropped: " << st.dropped
+               << "\nindexed: " << st.indexed << "\nfiles: " << st.files << "\nbytes: " << st.bytes
+               << "\nreloaded: " << st.reloaded << "\n";
+        } else if (trace) {
+            // whole trace from disk (includes spans evicted from memory and,
+            // with -rpcz_keep_span_db, spans of the previous run)
+            std::vector<std::string> v = span_db::FindTrace(trace, max);
+            if (v.empty()) v = ListRecentSpans(max, trace);
+            for (const std::string& x : v) os << x << "\n";
+        } else if (tq) {
+            for (const std::string& x : span_db::ListBefore(before_us, max)) os << x << "\n";
+        } else {
+            for (const std::string& x : ListRecentSpans(max, 0)) os << x << "\n";
+        }
         text(cntl, os.str());
     }
 };

@@ -18,7 +18,7 @@ int main(int argc, char** argv) {
         demo::LocalServer s(std::string("lim-") + limit, 2000, so);
         mrpc::Channel ch;
         mrpc::ChannelOptions opt;
-        opt.timeout_ms = 3000;
+        opt.timeout_ms = 15000;  // shedding, not timeouts, must bound latency (even on a loaded CI box)
         opt.max_retry = 0;
         opt.connection_type = "pooled";
         if (ch.Init(s.addr().c_str(), &opt) != 0) return 1;

@@ -12,6 +12,9 @@
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
+#include "base/time.h"
+#include "base/util.h"
+#include "rpc/span.h"
 
 namespace mrpc {
 namespace gpu {
@@ -101,6 +104,9 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
     if (device < 0 || device >= kMaxDev || Init(device) != 0) return -1;
     Engine& e = g_engine[device];
     g_submits.fetch_add(1, std::memory_order_relaxed);
+    // rpcz: the call this copy is done for gets the device wait annotated
+    Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
+    const int64_t t0 = span ? monotonic_us() : 0;
     Batch* mine;
     size_t first = 0;  // index of our first segment in the batch
     bool leader = false;
@@ -144,6 +150,13 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
     while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
     const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
     if (rc == 0 && crcs) memcpy(crcs, mine->crc_host + first, sizeof(uint32_t) * (size_t)n);
+    if (span) {
+        uint64_t bytes = 0;
+        for (int i = 0; i < n; ++i) bytes += segs[i].len;
+        span->AnnotateDevice(string_printf("%s %d segs %llu B dev%d%s", crcs ? "copy+crc32c" : "batched copy", n,
+                                           (unsigned long long)bytes, device, rc ? " FAILED" : ""),
+                             (float)(monotonic_us() - t0) / 1000.0f);
+    }
     if (mine->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
         ReleaseEvent(mine->ev);
         mine->ev = nullptr;

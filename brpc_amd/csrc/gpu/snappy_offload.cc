@@ -44,6 +44,9 @@ DEFINE_int32(gpu_snappy_block_kb, 16,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
              "waves (lower latency) at some cost in ratio; <= 64");
 
+#include "base/time.h"
+#include "rpc/span.h"
+
 namespace mrpc {
 namespace gpu {
 
@@ -326,7 +329,14 @@ bool gpu_decompress(const Buf& in, Buf* out) {
 bool offload(const Buf& in, Buf* out, bool compress) {
     if (g_device < 0 || device_blocks_elsewhere(in, g_device)) return false;
     Buf result;
+    Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
+    const int64_t t0 = span ? monotonic_us() : 0;
     const bool ok = compress ? gpu_compress(in, &result) : gpu_decompress(in, &result);
+    if (span) {
+        span->AnnotateDevice(string_printf("snappy %s %zu -> %zu B dev%d%s", compress ? "compress" : "decompress",
+                                           in.size(), result.size(), g_device, ok ? "" : " (fell back to CPU)"),
+                             (float)(monotonic_us() - t0) / 1000.0f);
+    }
     if (!ok) {
         g_fallbacks.fetch_add(1, std::memory_order_relaxed);
         return false;  // the CPU codec takes over

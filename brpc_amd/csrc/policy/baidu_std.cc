@@ -303,9 +303,9 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
             req_buf.swap(msg->payload);
         }
         device_payload_taken = true;
-        if (meta.device_payload_size() > 0 &&
-            !MergeDevicePayload(cntl, socket, meta, /*request=*/true, &cntl->request_attachment())) {
-            break;
+        if (meta.device_payload_size() > 0) {
+            Span::set_tls_parent(cntl->_span);  // rpcz: annotate the xGMI pull
+            if (!MergeDevicePayload(cntl, socket, meta, /*request=*/true, &cntl->request_attachment())) break;
         }
         if (meta.has_stream_settings()) OnRequestStreamSettings(cntl, socket, meta.stream_settings());
         req = mp->service->GetRequestPrototype(mp->method).New();
@@ -402,9 +402,12 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         }
         if (!saved_error && meta.device_payload_size() > 0) {
             device_payload_taken = true;
+            Span* const prev_span = Span::tls_parent();
+            Span::set_tls_parent(cntl->_span);  // rpcz: annotate the xGMI pull
             if (!MergeDevicePayload(cntl, msg->socket(), meta, /*request=*/false, &cntl->response_attachment())) {
                 saved_error = cntl->ErrorCode();
             }
+            Span::set_tls_parent(prev_span);
         }
         if (!saved_error && meta.has_stream_settings()) OnResponseStreamSettings(cntl, msg->socket(), meta.stream_settings());
         if (!saved_error && cntl->_response &&

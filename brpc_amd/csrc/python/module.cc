@@ -23,6 +23,8 @@
 #include "rpc/controller.h"
 #include "rpc/protocol.h"
 #include "rpc/server.h"
+#include "rpc/span.h"
+#include "rpc/span_db.h"
 #include "services/echo_service.h"
 #include "var/variable.h"
 
@@ -271,6 +273,25 @@ PYBIND11_MODULE(_native, m) {
         std::string v;
         if (!GetFlag(name, &v)) throw std::invalid_argument("no flag " + name);
         return v;
+    });
+    // rpcz: recent spans (memory), spans by trace id / end time (disk store)
+    m.def("rpcz_recent", [](size_t max) { return ListRecentSpans(max, 0); }, py::arg("max") = 100);
+    m.def("rpcz_trace", [](uint64_t trace, size_t max) { return span_db::FindTrace(trace, max); },
+          py::arg("trace_id"), py::arg("max") = 100, py::call_guard<py::gil_scoped_release>());
+    m.def("rpcz_before", [](int64_t before_us, size_t max) { return span_db::ListBefore(before_us, max); },
+          py::arg("before_us") = 0, py::arg("max") = 100, py::call_guard<py::gil_scoped_release>());
+    m.def("rpcz_flush", [] { span_db::Flush(); }, py::call_guard<py::gil_scoped_release>());
+    m.def("rpcz_stats", [] {
+        const span_db::Stats st = span_db::GetStats();
+        py::dict d;
+        d["written"] = st.written;
+        d["dropped"] = st.dropped;
+        d["indexed"] = st.indexed;
+        d["files"] = st.files;
+        d["bytes"] = st.bytes;
+        d["reloaded"] = st.reloaded;
+        d["dir"] = st.dir;
+        return d;
     });
     m.def("list_flags", [] {
         py::dict d;

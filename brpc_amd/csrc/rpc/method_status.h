@@ -48,7 +48,7 @@ public:
     // is decremented LAST, after the method status was updated: Server::Join
     // waits for that count to drain before the statuses may be destroyed.
     ConcurrencyRemover(MethodStatus* s, Controller* c, int64_t received_us, Server* server = nullptr)
-        : _status(s), _c(c), _received_us(received_us), _server(server) {}
+        : _status(s), _server(server), _c(c), _received_us(received_us) {}
     ~ConcurrencyRemover();
 private:
     MethodStatus* _status;

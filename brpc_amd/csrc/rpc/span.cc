@@ -7,11 +7,14 @@
 #include "base/util.h"
 #include "fiber/fiber.h"
 #include "fiber/internal.h"
+#include "mrpc/proto/rpcz.pb.h"
 #include "rpc/controller.h"
+#include "rpc/span_db.h"
 
 DEFINE_bool(enable_rpcz, false, "collect rpcz spans (browse at /rpcz)");
 DEFINE_int32(rpcz_max_spans, 10000, "max spans kept in memory");
 DEFINE_int32(rpcz_max_spans_per_second, 5000, "sampling speed limit of spans");
+DEFINE_bool(rpcz_save_to_disk, true, "also append spans to the on-disk store (rpc/span_db.h)");
 MRPC_VALIDATE_FLAG(enable_rpcz, ::mrpc::PassValidator);
 
 namespace mrpc {
@@ -99,6 +102,11 @@ void Span::Submit(Span* s, int64_t) {
         delete s;
         return;
     }
+    if (FLAGS_rpcz_save_to_disk) {
+        SpanRecord* r = new SpanRecord;
+        s->ToRecord(r);
+        span_db::Submit(r);
+    }
     st.spans.push_front(s);
     while ((int)st.spans.size() > FLAGS_rpcz_max_spans) {
         delete st.spans.back();
@@ -125,6 +133,31 @@ void Span::Annotate(const std::string& text) { annotations.emplace_back(realtime
 
 void Span::AnnotateDevice(const std::string& what, float device_ms) {
     annotations.emplace_back(realtime_us(), string_printf("[gpu] %s %.3f ms", what.c_str(), device_ms));
+}
+
+void Span::ToRecord(SpanRecord* r) const {
+    r->set_trace_id(trace_id);
+    r->set_span_id(span_id);
+    r->set_parent_span_id(parent_span_id);
+    r->set_log_id(log_id);
+    r->set_type(type);
+    r->set_remote(remote_side.to_string());
+    r->set_full_method_name(full_method_name);
+    r->set_protocol(protocol);
+    r->set_error_code(error_code);
+    r->set_request_size(request_size);
+    r->set_response_size(response_size);
+    r->set_received_real_us(received_real_us);
+    r->set_start_parse_real_us(start_parse_real_us);
+    r->set_start_callback_real_us(start_callback_real_us);
+    r->set_start_send_real_us(start_send_real_us);
+    r->set_sent_real_us(sent_real_us);
+    for (auto& a : annotations) {
+        SpanAnnotation* x = r->add_annotations();
+        x->set_realtime_us(a.first);
+        x->set_text(a.second);
+    }
+    for (const Span* c : client_spans) c->ToRecord(r->add_client_spans());
 }
 
 std::string Span::Describe() const {

@@ -17,6 +17,7 @@
 namespace mrpc {
 
 class Controller;
+class SpanRecord;
 
 class Span {
 public:
@@ -34,6 +35,7 @@ public:
     void Annotate(const std::string& text);
     void AnnotateDevice(const std::string& what, float device_ms);
     std::string Describe() const;
+    void ToRecord(SpanRecord* r) const;
 
     uint64_t trace_id = 0, span_id = 0, parent_span_id = 0, log_id = 0;
     Type type = CLIENT;

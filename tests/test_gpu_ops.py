@@ -331,3 +331,32 @@ def test_batched_copy_crc32c_fused(dev):
     for s, d, c in zip(srcs, dsts, crcs):
         assert torch.equal(s, d)
         assert c == crc32c_host(s.cpu().numpy().tobytes())
+
+
+def test_rpcz_annotates_device_pulls(dev, tmp_path):
+    """rpcz: the xGMI pull done for a call is annotated in that call's span
+    (server side: request attachment; client side: response attachment)
+    and the spans land in the on-disk store, findable by trace id."""
+    import re
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    native.set_flag("rpcz_database_dir", str(tmp_path))
+    native.set_flag("enable_rpcz", "true")
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        p = native.Press({"server": s.address, "concurrency": 4, "attachment_size": 65536,
+                          "device_attachment": True, "gpu_device": 0, "check_echo": True})
+        p.run_requests(200)
+        assert p.stats()["error"] == 0
+        native.rpcz_flush()
+        spans = native.rpcz_recent(400)
+        gpu = [x for x in spans if "[gpu]" in x and "copy" in x]
+        assert gpu, spans[:3]
+        assert any(x.startswith("S ") for x in gpu), gpu[:3]
+        assert any(x.startswith("C ") for x in gpu), gpu[:3]
+        trace = int(re.search(r"trace=([0-9a-f]{16})", gpu[0]).group(1), 16)
+        stored = native.rpcz_trace(trace)
+        assert stored and any("[gpu]" in x for x in stored), stored
+    finally:
+        native.set_flag("enable_rpcz", "false")
+        s.stop()

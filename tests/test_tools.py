@@ -113,3 +113,38 @@ def test_sampling_heap_profiler():
     r = subprocess.run([os.path.join(BIN, "heapprof_demo")], capture_output=True, text=True, timeout=60, cwd="/tmp")
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "KeepLiveBuffers" in r.stdout
+
+
+def test_rpcz_pages_by_trace_and_time(procs, tmp_path):
+    """/rpcz browsing of the on-disk span store: recent view, ?trace_id=,
+    ?time= (epoch us or YYYY/MM/DD-HH:MM:SS) and ?stats."""
+    import re
+    from brpc_amd import native
+    port = _free_port()
+    _spawn(procs, [os.path.join(BIN, "echo_server"), "-port=%d" % port, "-enable_rpcz=true",
+                   "-rpcz_database_dir=%s" % tmp_path])
+    _wait_port(port)
+    p = native.Press({"server": "127.0.0.1:%d" % port, "concurrency": 2})
+    p.run_requests(20)
+    assert p.stats()["error"] == 0
+    time.sleep(0.3)
+    mid_us = int(time.time() * 1e6)
+    time.sleep(0.3)
+    p.run_requests(5)
+    time.sleep(1.2)
+    st, recent = _get("http://127.0.0.1:%d/rpcz?max=500" % port)
+    assert st == 200 and "EchoService.Echo" in recent, recent[:500]
+    trace = re.search(r"trace=([0-9a-f]{16})", recent).group(1)
+    _, by_trace = _get("http://127.0.0.1:%d/rpcz?trace_id=%s" % (port, trace))
+    assert by_trace.strip() and all(("trace=" + trace) in line for line in by_trace.splitlines()
+                                    if line.startswith(("S ", "C "))), by_trace
+    _, before = _get("http://127.0.0.1:%d/rpcz?time=%d&max=500" % (port, mid_us))
+    _, now = _get("http://127.0.0.1:%d/rpcz?time=%d&max=500" % (port, int(time.time() * 1e6)))
+    n_before = sum(1 for l in before.splitlines() if l.startswith("S "))
+    n_now = sum(1 for l in now.splitlines() if l.startswith("S "))
+    assert n_before == 20 and n_now == 25, (n_before, n_now)
+    _, stats = _get("http://127.0.0.1:%d/rpcz?stats" % port)
+    assert "written: 25" in stats and "dir: %s" % tmp_path in stats, stats
+    stamp = time.strftime("%Y/%m/%d-%H:%M:%S", time.localtime(time.time() + 5))
+    _, by_date = _get("http://127.0.0.1:%d/rpcz?time=%s&max=500" % (port, stamp))
+    assert sum(1 for l in by_date.splitlines() if l.startswith("S ")) == 25
