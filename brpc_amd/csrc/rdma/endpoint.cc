@@ -437,6 +437,11 @@ int Endpoint::Init(std::string* err) {
     }
     _sbuf.resize((size_t)_sq_size);
     _rbuf.assign((size_t)_rq_size, nullptr);
+    if (_qp->Prepare() != 0) {
+        if (err) *err = std::string("fail to move the QP to INIT: ") + strerror(errno);
+        return -1;
+    }
+    // receives are posted in INIT, before the peer can send (no RNR gap)
     for (size_t i = 0; i < _rbuf.size(); ++i) {
         if (PostRecvSlot(i) != 0) {
             if (err) *err = "fail to post receive blocks";

@@ -12,9 +12,11 @@
 //              GPUDirect HCA reads HBM.
 //  * ibverbs — libibverbs loaded with dlopen (the reference's
 //              rdma_helper.cpp:49-74 pattern), RC QPs over the first active
-//              port, ibv_reg_dmabuf_mr for HBM. Only compiled where the
-//              rdma-core headers exist; neither this build container nor the
-//              MI355X boxes have them, so this half is unverified here.
+//              port, ibv_reg_dmabuf_mr for HBM. Always compiled, against the
+//              in-tree ABI declaration rdma/verbs_abi.h; exercised in the
+//              unit tests through a stub verbs library implementing that
+//              ABI (tests/fake_ibverbs.cc). No HCA exists on this pool, so
+//              real-hardware behaviour stays unverified.
 #include <sys/eventfd.h>
 #include <unistd.h>
 
@@ -277,51 +279,80 @@ std::unique_ptr<Provider> CreateSoftProvider() { return std::unique_ptr<Provider
 }  // namespace mrpc
 
 // ------------------------------------------------------------------ ibverbs
-#if __has_include(<infiniband/verbs.h>)
+// Compiled against the in-tree ABI declaration (rdma/verbs_abi.h), library
+// loaded at run time with dlopen (-rdma_verbs_library), so hosts without
+// an HCA or rdma-core simply report the provider unavailable.
+#include <arpa/inet.h>
 #include <dlfcn.h>
-#include <infiniband/verbs.h>
+#include <fcntl.h>
+
+#include "base/flags.h"
+#include "rdma/verbs_abi.h"
+
+DEFINE_string(rdma_verbs_library, "libibverbs.so.1", "verbs library dlopen()ed by the ibverbs RDMA provider");
 
 namespace mrpc {
 namespace rdma {
 namespace {
 
+using namespace verbs;
+
 struct IbvApi {
     void* handle = nullptr;
-    decltype(&ibv_get_device_list) get_device_list;
-    decltype(&ibv_free_device_list) free_device_list;
-    decltype(&ibv_get_device_name) get_device_name;
-    decltype(&ibv_open_device) open_device;
-    decltype(&ibv_alloc_pd) alloc_pd;
-    decltype(&ibv_reg_mr) reg_mr;
-    decltype(&ibv_reg_dmabuf_mr) reg_dmabuf_mr;
-    decltype(&ibv_dereg_mr) dereg_mr;
-    decltype(&ibv_create_comp_channel) create_comp_channel;
-    decltype(&ibv_create_cq) create_cq;
-    decltype(&ibv_destroy_cq) destroy_cq;
-    decltype(&ibv_get_cq_event) get_cq_event;
-    decltype(&ibv_ack_cq_events) ack_cq_events;
-    decltype(&ibv_create_qp) create_qp;
-    decltype(&ibv_destroy_qp) destroy_qp;
-    decltype(&ibv_modify_qp) modify_qp;
-    decltype(&ibv_query_port) query_port;
-    decltype(&ibv_query_gid) query_gid;
+    std::string loaded_from;
+    ibv_get_device_list_fn get_device_list = nullptr;
+    ibv_free_device_list_fn free_device_list = nullptr;
+    ibv_get_device_name_fn get_device_name = nullptr;
+    ibv_open_device_fn open_device = nullptr;
+    ibv_close_device_fn close_device = nullptr;
+    ibv_alloc_pd_fn alloc_pd = nullptr;
+    ibv_dealloc_pd_fn dealloc_pd = nullptr;
+    ibv_reg_mr_fn reg_mr = nullptr;
+    ibv_reg_dmabuf_mr_fn reg_dmabuf_mr = nullptr;
+    ibv_dereg_mr_fn dereg_mr = nullptr;
+    ibv_create_comp_channel_fn create_comp_channel = nullptr;
+    ibv_destroy_comp_channel_fn destroy_comp_channel = nullptr;
+    ibv_create_cq_fn create_cq = nullptr;
+    ibv_destroy_cq_fn destroy_cq = nullptr;
+    ibv_get_cq_event_fn get_cq_event = nullptr;
+    ibv_ack_cq_events_fn ack_cq_events = nullptr;
+    ibv_create_qp_fn create_qp = nullptr;
+    ibv_destroy_qp_fn destroy_qp = nullptr;
+    ibv_modify_qp_fn modify_qp = nullptr;
+    ibv_query_port_fn query_port = nullptr;
+    ibv_query_gid_fn query_gid = nullptr;
+
+    // The symbols are resolved once per library path; a failed load is
+    // retried with the next Open (the flag may have changed).
     bool Load(std::string* why) {
-        handle = dlopen("libibverbs.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!handle) {
-            *why = "libibverbs.so.1 not found";
+        std::lock_guard<std::mutex> g(mu);
+        const std::string lib = FLAGS_rdma_verbs_library;
+        if (handle && lib == loaded_from) return true;
+        void* h = dlopen(lib.c_str(), RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            *why = lib + " not loadable";
             return false;
         }
-#define MRPC_IBV_SYM(f) \
-    if (!(f = (decltype(f))dlsym(handle, "ibv_" #f))) { *why = "missing ibv_" #f; return false; }
+#define MRPC_IBV_SYM(f)                                                         \
+    f = reinterpret_cast<decltype(f)>(dlsym(h, "ibv_" #f));                     \
+    if (!f) {                                                                   \
+        *why = "missing ibv_" #f " in " + lib;                                  \
+        return false;                                                           \
+    }
         MRPC_IBV_SYM(get_device_list) MRPC_IBV_SYM(free_device_list) MRPC_IBV_SYM(get_device_name)
-        MRPC_IBV_SYM(open_device) MRPC_IBV_SYM(alloc_pd) MRPC_IBV_SYM(reg_mr) MRPC_IBV_SYM(dereg_mr)
-        MRPC_IBV_SYM(create_comp_channel) MRPC_IBV_SYM(create_cq) MRPC_IBV_SYM(destroy_cq)
+        MRPC_IBV_SYM(open_device) MRPC_IBV_SYM(close_device) MRPC_IBV_SYM(alloc_pd) MRPC_IBV_SYM(dealloc_pd)
+        MRPC_IBV_SYM(reg_mr) MRPC_IBV_SYM(dereg_mr) MRPC_IBV_SYM(create_comp_channel)
+        MRPC_IBV_SYM(destroy_comp_channel) MRPC_IBV_SYM(create_cq) MRPC_IBV_SYM(destroy_cq)
         MRPC_IBV_SYM(get_cq_event) MRPC_IBV_SYM(ack_cq_events) MRPC_IBV_SYM(create_qp) MRPC_IBV_SYM(destroy_qp)
         MRPC_IBV_SYM(modify_qp) MRPC_IBV_SYM(query_port) MRPC_IBV_SYM(query_gid)
 #undef MRPC_IBV_SYM
-        reg_dmabuf_mr = (decltype(reg_dmabuf_mr))dlsym(handle, "ibv_reg_dmabuf_mr");  // optional
+        // optional: rdma-core >= 34 (GPUDirect through dmabuf)
+        reg_dmabuf_mr = reinterpret_cast<ibv_reg_dmabuf_mr_fn>(dlsym(h, "ibv_reg_dmabuf_mr"));
+        handle = h;  // never dlclose()d: contexts may outlive a provider
+        loaded_from = lib;
         return true;
     }
+    std::mutex mu;
 };
 
 IbvApi& api() {
@@ -333,15 +364,24 @@ class IbvCq : public CompletionQueue {
 public:
     IbvCq(ibv_context* ctx, int depth) {
         _ch = api().create_comp_channel(ctx);
-        if (_ch) _cq = api().create_cq(ctx, depth, nullptr, _ch, 0);
+        if (!_ch) return;
+        // the endpoint waits on the fd with the fiber poller and then
+        // drains events: the channel must not block
+        const int fl = fcntl(_ch->fd, F_GETFL);
+        if (fl < 0 || fcntl(_ch->fd, F_SETFL, fl | O_NONBLOCK) < 0) return;
+        _cq = api().create_cq(ctx, depth, nullptr, _ch, 0);
     }
     ~IbvCq() override {
-        if (_cq) api().destroy_cq(_cq);
+        if (_cq) {
+            if (_unacked) api().ack_cq_events(_cq, _unacked);
+            api().destroy_cq(_cq);
+        }
+        if (_ch) api().destroy_comp_channel(_ch);
     }
     bool ok() const { return _cq != nullptr; }
     int Poll(WorkCompletion* out, int n) override {
         ibv_wc wc[32];
-        const int k = ibv_poll_cq(_cq, std::min(n, 32), wc);
+        const int k = _cq->context->ops.poll_cq(_cq, std::min(n, 32), wc);
         for (int i = 0; i < k; ++i) {
             out[i].wr_id = wc[i].wr_id;
             out[i].opcode = (wc[i].opcode & IBV_WC_RECV) ? WC_RECV : WC_SEND;
@@ -352,31 +392,40 @@ public:
         }
         return k;
     }
-    int Arm() override { return ibv_req_notify_cq(_cq, 0); }
+    int Arm() override { return _cq->context->ops.req_notify_cq(_cq, 0); }
     int notify_fd() const override { return _ch->fd; }
     void AckEvent() override {
+        // the channel fd is non-blocking, so this drains what is pending; acks are batched (ibv_ack_cq_events
+        // takes a mutex in the library)
         ibv_cq* cq;
         void* ctx;
-        while (api().get_cq_event(_ch, &cq, &ctx) == 0) api().ack_cq_events(cq, 1);
+        while (api().get_cq_event(_ch, &cq, &ctx) == 0) {
+            if (++_unacked >= 64) {
+                api().ack_cq_events(_cq, _unacked);
+                _unacked = 0;
+            }
+        }
     }
     ibv_cq* cq() const { return _cq; }
 
 private:
     ibv_comp_channel* _ch = nullptr;
     ibv_cq* _cq = nullptr;
+    unsigned _unacked = 0;
 };
 
 class IbvQp : public QueuePair {
 public:
-    IbvQp(ibv_pd* pd, IbvCq* cq, int sq, int rq, int port, const ibv_port_attr& pa, const ibv_gid& gid, int gid_index)
-        : _port(port), _gid_index(gid_index), _mtu(pa.active_mtu) {
+    IbvQp(ibv_pd* pd, IbvCq* cq, int sq, int rq, int max_sge, int port, const ibv_port_attr& pa, const ibv_gid& gid,
+          int gid_index)
+        : _port(port), _gid_index(gid_index), _max_sge(max_sge), _mtu(pa.active_mtu) {
         ibv_qp_init_attr a;
         memset(&a, 0, sizeof(a));
         a.send_cq = cq->cq();
         a.recv_cq = cq->cq();
         a.cap.max_send_wr = sq;
         a.cap.max_recv_wr = rq;
-        a.cap.max_send_sge = 16;
+        a.cap.max_send_sge = max_sge;
         a.cap.max_recv_sge = 1;
         a.qp_type = IBV_QPT_RC;
         _qp = api().create_qp(pd, &a);
@@ -390,7 +439,8 @@ public:
     }
     bool ok() const { return _qp != nullptr; }
     QpAddress local() const override { return _addr; }
-    int Connect(const QpAddress& r) override {
+    int Prepare() override {
+        if (_inited) return 0;
         ibv_qp_attr a;
         memset(&a, 0, sizeof(a));
         a.qp_state = IBV_QPS_INIT;
@@ -398,6 +448,14 @@ public:
         a.pkey_index = 0;
         a.qp_access_flags = IBV_ACCESS_LOCAL_WRITE;
         if (api().modify_qp(_qp, &a, IBV_QP_STATE | IBV_QP_PKEY_INDEX | IBV_QP_PORT | IBV_QP_ACCESS_FLAGS)) return -1;
+        _inited = true;
+        return 0;
+    }
+    // (RESET -> INIT via Prepare) -> RTR -> RTS (RC, reliable: retries and
+    // infinite RNR retry — the credit window keeps receivers from running dry).
+    int Connect(const QpAddress& r) override {
+        if (Prepare() != 0) return -1;
+        ibv_qp_attr a;
         memset(&a, 0, sizeof(a));
         a.qp_state = IBV_QPS_RTR;
         a.path_mtu = _mtu;
@@ -420,13 +478,14 @@ public:
         a.qp_state = IBV_QPS_RTS;
         a.timeout = 14;
         a.retry_cnt = 7;
-        a.rnr_retry = 7;  // infinite: the credit window never lets receivers run dry
+        a.rnr_retry = 7;
         a.sq_psn = 0;
         a.max_rd_atomic = 1;
         return api().modify_qp(_qp, &a, IBV_QP_STATE | IBV_QP_TIMEOUT | IBV_QP_RETRY_CNT | IBV_QP_RNR_RETRY |
                                              IBV_QP_SQ_PSN | IBV_QP_MAX_QP_RD_ATOMIC);
     }
     int PostSend(uint64_t wr_id, const Sge* sge, int nsge, bool with_imm, uint32_t imm, bool signaled) override {
+        if (nsge > _max_sge || nsge > 16) return EINVAL;
         ibv_sge s[16];
         for (int i = 0; i < nsge; ++i) {
             s[i].addr = sge[i].addr;
@@ -441,7 +500,7 @@ public:
         wr.opcode = with_imm ? IBV_WR_SEND_WITH_IMM : IBV_WR_SEND;
         wr.imm_data = htonl(imm);
         wr.send_flags = signaled ? IBV_SEND_SIGNALED : 0;
-        return ibv_post_send(_qp, &wr, &bad);
+        return _qp->context->ops.post_send(_qp, &wr, &bad);
     }
     int PostRecv(uint64_t wr_id, const Sge& sge) override {
         ibv_sge s;
@@ -453,18 +512,24 @@ public:
         wr.wr_id = wr_id;
         wr.sg_list = &s;
         wr.num_sge = 1;
-        return ibv_post_recv(_qp, &wr, &bad);
+        return _qp->context->ops.post_recv(_qp, &wr, &bad);
     }
 
 private:
     ibv_qp* _qp = nullptr;
-    int _port, _gid_index;
+    bool _inited = false;
+    int _port, _gid_index, _max_sge;
     ibv_mtu _mtu;
     QpAddress _addr;
 };
 
 class IbvProvider : public Provider {
 public:
+    ~IbvProvider() override {
+        for (auto& kv : _mrs) api().dereg_mr(kv.second);
+        if (_pd) api().dealloc_pd(_pd);
+        if (_ctx) api().close_device(_ctx);
+    }
     bool Open(std::string* why) {
         if (!api().Load(why)) return false;
         int n = 0;
@@ -479,7 +544,8 @@ public:
             if (!ctx) continue;
             for (int port = 1; port <= 2; ++port) {
                 ibv_port_attr pa;
-                if (api().query_port(ctx, port, &pa) == 0 && pa.state == IBV_PORT_ACTIVE) {
+                memset(&pa, 0, sizeof(pa));
+                if (api().query_port(ctx, (uint8_t)port, &pa) == 0 && pa.state == IBV_PORT_ACTIVE) {
                     _ctx = ctx;
                     _port = port;
                     _pa = pa;
@@ -487,13 +553,14 @@ public:
                     break;
                 }
             }
+            if (!_ctx) api().close_device(ctx);
         }
         api().free_device_list(list);
         if (!_ctx) {
             *why = "no active RDMA port";
             return false;
         }
-        if (api().query_gid(_ctx, _port, _gid_index, &_gid) != 0) {
+        if (api().query_gid(_ctx, (uint8_t)_port, _gid_index, &_gid) != 0) {
             *why = "ibv_query_gid failed";
             return false;
         }
@@ -508,6 +575,7 @@ public:
         ibv_mr* mr = nullptr;
         const int access = IBV_ACCESS_LOCAL_WRITE;
         if (device) {
+            // GPUDirect: HBM exported as a dmabuf by the HIP runtime
             DmabufExportFn exp = GetDmabufExportHook();
             int fd = -1;
             uint64_t off = 0;
@@ -535,7 +603,8 @@ public:
         return std::unique_ptr<CompletionQueue>(cq.release());
     }
     std::unique_ptr<QueuePair> CreateQp(CompletionQueue* cq, int sq, int rq) override {
-        std::unique_ptr<IbvQp> qp(new IbvQp(_pd, static_cast<IbvCq*>(cq), sq, rq, _port, _pa, _gid, _gid_index));
+        std::unique_ptr<IbvQp> qp(
+            new IbvQp(_pd, static_cast<IbvCq*>(cq), sq, rq, max_sge(), _port, _pa, _gid, _gid_index));
         if (!qp->ok()) return nullptr;
         return std::unique_ptr<QueuePair>(qp.release());
     }
@@ -563,14 +632,3 @@ std::unique_ptr<Provider> CreateIbverbsProvider(std::string* why) {
 
 }  // namespace rdma
 }  // namespace mrpc
-#else
-namespace mrpc {
-namespace rdma {
-bool IbverbsCompiledIn() { return false; }
-std::unique_ptr<Provider> CreateIbverbsProvider(std::string* why) {
-    if (why) *why = "built without rdma-core headers (infiniband/verbs.h)";
-    return nullptr;
-}
-}  // namespace rdma
-}  // namespace mrpc
-#endif

@@ -87,6 +87,9 @@ public:
     virtual QpAddress local() const = 0;
     // INIT -> RTR -> RTS against the remote address.
     virtual int Connect(const QpAddress& remote) = 0;
+    // RESET -> INIT: receives may be posted from here on (verbs refuse them
+    // in RESET), before Connect() makes the QP ready to receive and send.
+    virtual int Prepare() { return 0; }
     virtual int PostSend(uint64_t wr_id, const Sge* sge, int nsge, bool with_imm, uint32_t imm, bool signaled) = 0;
     virtual int PostRecv(uint64_t wr_id, const Sge& sge) = 0;
 };

@@ -172,6 +172,14 @@ def main():
         ut = os.path.join(BUILD, "bin", "mrpc_unittests")
         w(f"build {rel(ut)}: link {' '.join(rel(o) for o in ut_objs)} | {rel(libso)}\n  extra = {linkmrpc}\n")
         bins.append(ut)
+    # stub shared libraries the unit tests dlopen (tests/stub/<name>.cc ->
+    # build/lib/lib<name>.so), e.g. the fake verbs library of RdmaVerbs.*
+    for s in sorted(glob.glob(os.path.join(CSRC, "tests", "stub", "*.cc"))):
+        name = os.path.splitext(os.path.basename(s))[0]
+        o = cxx(s, extra="-fvisibility=hidden")
+        so = os.path.join(BUILD, "lib", "lib%s.so" % name)
+        w(f"build {rel(so)}: solink {rel(o)}\n  ldlibs = -lpthread\n")
+        bins.append(so)
     # tools and examples: every tools/<name>.cc except protoc_main, examples/<name>/*.cc
     for s in sorted(glob.glob(os.path.join(CSRC, "tools", "*.cc"))):
         name = os.path.splitext(os.path.basename(s))[0]
