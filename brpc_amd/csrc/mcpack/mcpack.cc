@@ -1,5 +1,7 @@
 #include "mcpack/mcpack.h"
 
+#include <atomic>
+
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -409,7 +411,7 @@ static uint8_t WireType(const FieldDescriptor* f) {
 }
 
 // Writes an integral/floating value with the field's wire type.
-static void AddNumber(Serializer* sr, const std::string& name, uint8_t t, int64_t iv, uint64_t uv, double dv,
+void AddConverted(Serializer* sr, const std::string& name, uint8_t t, int64_t iv, uint64_t uv, double dv,
                       bool is_float_src, bool is_unsigned_src) {
     const int64_t si = is_float_src ? (int64_t)dv : (is_unsigned_src ? (int64_t)uv : iv);
     const uint64_t ui = is_float_src ? (uint64_t)dv : (is_unsigned_src ? uv : (uint64_t)iv);
@@ -436,35 +438,35 @@ static void AddScalar(Serializer* sr, const std::string& name, const Message& m,
     switch (f->cpp_type()) {
     case CppType::INT32: {
         const int32_t v = rep ? Reflection::GetRepeatedInt32(m, f, idx) : Reflection::GetInt32(m, f);
-        return AddNumber(sr, name, t, v, 0, 0, false, false);
+        return AddConverted(sr, name, t, v, 0, 0, false, false);
     }
     case CppType::ENUM: {
         const int v = rep ? Reflection::GetRepeatedEnumValue(m, f, idx) : Reflection::GetEnumValue(m, f);
-        return AddNumber(sr, name, t, v, 0, 0, false, false);
+        return AddConverted(sr, name, t, v, 0, 0, false, false);
     }
     case CppType::INT64: {
         const int64_t v = rep ? Reflection::GetRepeatedInt64(m, f, idx) : Reflection::GetInt64(m, f);
-        return AddNumber(sr, name, t, v, 0, 0, false, false);
+        return AddConverted(sr, name, t, v, 0, 0, false, false);
     }
     case CppType::UINT32: {
         const uint32_t v = rep ? Reflection::GetRepeatedUInt32(m, f, idx) : Reflection::GetUInt32(m, f);
-        return AddNumber(sr, name, t, 0, v, 0, false, true);
+        return AddConverted(sr, name, t, 0, v, 0, false, true);
     }
     case CppType::UINT64: {
         const uint64_t v = rep ? Reflection::GetRepeatedUInt64(m, f, idx) : Reflection::GetUInt64(m, f);
-        return AddNumber(sr, name, t, 0, v, 0, false, true);
+        return AddConverted(sr, name, t, 0, v, 0, false, true);
     }
     case CppType::BOOL: {
         const bool v = rep ? Reflection::GetRepeatedBool(m, f, idx) : Reflection::GetBool(m, f);
-        return AddNumber(sr, name, t, v ? 1 : 0, 0, 0, false, false);
+        return AddConverted(sr, name, t, v ? 1 : 0, 0, 0, false, false);
     }
     case CppType::FLOAT: {
         const float v = rep ? Reflection::GetRepeatedFloat(m, f, idx) : Reflection::GetFloat(m, f);
-        return AddNumber(sr, name, t, 0, 0, v, true, false);
+        return AddConverted(sr, name, t, 0, 0, v, true, false);
     }
     case CppType::DOUBLE: {
         const double v = rep ? Reflection::GetRepeatedDouble(m, f, idx) : Reflection::GetDouble(m, f);
-        return AddNumber(sr, name, t, 0, 0, v, true, false);
+        return AddConverted(sr, name, t, 0, 0, v, true, false);
     }
     case CppType::STRING: {
         const std::string& v = rep ? Reflection::GetRepeatedString(m, f, idx) : Reflection::GetString(m, f);
@@ -479,7 +481,27 @@ static void AddScalar(Serializer* sr, const std::string& name, const Message& m,
     }
 }
 
+namespace {
+std::atomic<bool> g_generated_enabled{true};
+}  // namespace
+
+void RegisterMessageHandler(const pb::Descriptor* d, const MessageHandler* h) {
+    const_cast<pb::Descriptor*>(d)->mcpack_handler.store(h, std::memory_order_release);
+}
+
+const MessageHandler* FindMessageHandler(const pb::Descriptor* d) {
+    if (!g_generated_enabled.load(std::memory_order_relaxed)) return nullptr;
+    return static_cast<const MessageHandler*>(d->mcpack_handler.load(std::memory_order_acquire));
+}
+
+void SetGeneratedHandlersEnabled(bool on) { g_generated_enabled.store(on, std::memory_order_relaxed); }
+
 bool SerializeFields(const Message& msg, Format fmt, Serializer* sr) {
+    if (const MessageHandler* h = FindMessageHandler(msg.GetDescriptor())) return h->serialize_fields(msg, fmt, sr);
+    return SerializeFieldsByReflection(msg, fmt, sr);
+}
+
+bool SerializeFieldsByReflection(const Message& msg, Format fmt, Serializer* sr) {
     const pb::Descriptor* d = msg.GetDescriptor();
     for (int i = 0; i < d->field_count() && sr->good(); ++i) {
         const FieldDescriptor* f = d->field(i);
@@ -607,7 +629,7 @@ static bool SetFromValue(Message* m, const FieldDescriptor* f, const Value& v) {
 }
 
 // {a=[1,3],b=[2,4]} -> [{a=1,b=2},{a=3,b=4}] for a repeated message field.
-static bool ParseObjectIsoArray(const Value& v, Message* m, const FieldDescriptor* f) {
+bool ParseObjectIsoArrayField(const Value& v, Message* m, const FieldDescriptor* f) {
     std::vector<Item> cols;
     if (!ListItems(v, &cols)) return false;
     std::vector<Message*> rows;
@@ -627,6 +649,11 @@ static bool ParseObjectIsoArray(const Value& v, Message* m, const FieldDescripto
 }
 
 bool ParseFromObject(const Value& obj, Message* msg) {
+    if (const MessageHandler* h = FindMessageHandler(msg->GetDescriptor())) return h->parse_object(obj, msg);
+    return ParseFromObjectByReflection(obj, msg);
+}
+
+bool ParseFromObjectByReflection(const Value& obj, Message* msg) {
     if (obj.type() != FIELD_OBJECT) return false;
     std::vector<Item> items;
     if (!ListItems(obj, &items)) return false;
@@ -638,7 +665,7 @@ bool ParseFromObject(const Value& obj, Message* msg) {
         const uint8_t t = it.value.type();
         if (f->is_repeated()) {
             if (t == FIELD_OBJECTISOARRAY) {
-                if (f->cpp_type() != CppType::MESSAGE || !ParseObjectIsoArray(it.value, msg, f)) return false;
+                if (f->cpp_type() != CppType::MESSAGE || !ParseObjectIsoArrayField(it.value, msg, f)) return false;
                 continue;
             }
             if (t == FIELD_ARRAY || t == FIELD_ISOARRAY) {

@@ -11,10 +11,15 @@
 // an isomorphic array (compack) stores one item-type byte followed by raw
 // primitive values. A message is an anonymous top-level object.
 //
-// Instead of generating per-message code with a protoc plugin, conversion
-// is driven by the runtime descriptors every mrpc message carries (the same
-// reflection json2pb uses); `idl_name` / `idl_type` field options are
-// honoured as in the reference's idl_options.proto.
+// Conversion is driven by the runtime descriptors every mrpc message
+// carries (the same reflection json2pb uses); `idl_name` / `idl_type` field
+// options are honoured as in the reference's idl_options.proto. Like the
+// reference's protoc-gen-mcpack (src/mcpack2pb/generator.cpp), `mrpc_protoc
+// --mcpack_out=DIR` emits specialised per-message serialize/parse functions
+// (no reflection, no name hashing per field) that register themselves as the
+// message's MessageHandler; the entry points below dispatch to them and fall
+// back to the descriptor walk for messages without generated code. Both
+// paths produce identical bytes (tests/legacy_protocols_unittest.cc).
 #pragma once
 
 #include <cstddef>
@@ -25,6 +30,8 @@
 namespace mrpc {
 class Buf;
 namespace pb {
+class Descriptor;
+class FieldDescriptor;
 class Message;
 }
 namespace mcpack {
@@ -147,6 +154,25 @@ struct Item {
 };
 bool ListItems(const Value& group, std::vector<Item>* items);
 
+// Generated per-message codec (see the header comment).
+struct MessageHandler {
+    // fields of msg into the currently open object
+    bool (*serialize_fields)(const pb::Message& msg, Format fmt, Serializer* sr);
+    // msg from an object value
+    bool (*parse_object)(const Value& obj, pb::Message* msg);
+};
+void RegisterMessageHandler(const pb::Descriptor* d, const MessageHandler* h);
+const MessageHandler* FindMessageHandler(const pb::Descriptor* d);
+// Process-wide switch (tests/benchmarks compare the two paths).
+void SetGeneratedHandlersEnabled(bool on);
+
+// Helpers of the generated code: a number written with a wire type other
+// than its natural one (idl_type), and a repeated message field from an
+// object isoarray ({a=[..],b=[..]} columns).
+void AddConverted(Serializer* sr, const std::string& name, uint8_t wire_type, int64_t iv, uint64_t uv, double dv,
+                  bool is_float_src, bool is_unsigned_src);
+bool ParseObjectIsoArrayField(const Value& v, pb::Message* msg, const pb::FieldDescriptor* f);
+
 // pb <-> mcpack. The output is a complete top-level object.
 bool SerializeToString(const pb::Message& msg, Format fmt, std::string* out);
 bool SerializeToBuf(const pb::Message& msg, Format fmt, Buf* out);
@@ -156,6 +182,9 @@ bool ParseFromArray(const char* data, size_t n, pb::Message* msg);
 bool ParseFromBuf(const Buf& buf, pb::Message* msg);
 // Fills msg from an object value (e.g. a nested "params" object).
 bool ParseFromObject(const Value& obj, pb::Message* msg);
+// The descriptor walk only (ignores generated handlers).
+bool SerializeFieldsByReflection(const pb::Message& msg, Format fmt, Serializer* sr);
+bool ParseFromObjectByReflection(const Value& obj, pb::Message* msg);
 
 }  // namespace mcpack
 }  // namespace mrpc

@@ -4,6 +4,8 @@
 // registration, json2pb, rpc_press's DynamicMessageFactory, /protobufs).
 #pragma once
 
+#include <atomic>
+
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -101,6 +103,9 @@ public:
     Message* (*factory)() = nullptr;  // generated messages
     const Message* prototype = nullptr;  // default instance (generated or dynamic)
     bool owns_prototype = false;         // dynamic prototypes die with their descriptor
+    // Generated mcpack codec of this message (mcpack::MessageHandler*,
+    // installed by `mrpc_protoc --mcpack_out` output at static init).
+    std::atomic<const void*> mcpack_handler{nullptr};
     Descriptor() = default;
     Descriptor(const Descriptor&) = delete;
     Descriptor& operator=(const Descriptor&) = delete;

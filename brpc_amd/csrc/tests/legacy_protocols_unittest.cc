@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "base/endpoint.h"
+#include "base/time.h"
 #include "fiber/fiber.h"
 #include "mcpack/mcpack.h"
 #include "mrpc/proto/echo.pb.h"
@@ -629,4 +630,120 @@ TEST(Thrift, framed_client_server_pipelined) {
     ch.CallMethod(nullptr, &c3, &r3, &s3, nullptr);
     EXPECT_TRUE(c3.Failed());
     EXPECT_TRUE(c3.ErrorText().find("no method nope") != std::string::npos);
+}
+
+// Generated per-message codecs (mrpc_protoc --mcpack_out, the role of the
+// reference's protoc-gen-mcpack) against the descriptor walk: same bytes
+// both ways, and each path parses the other's output.
+namespace {
+test::Rich MakeRich() {
+    test::Rich r;
+    r.set_i32(-5);
+    r.set_i64(-1234567890123LL);
+    r.set_u64(18000000000000000000ULL);
+    r.set_d(3.25);
+    r.set_flag(true);
+    r.set_s(std::string(300, 's'));
+    r.set_raw(std::string("\0\1\2", 3));
+    r.set_color(test::BLUE);
+    r.mutable_inner()->set_x(9);
+    r.mutable_inner()->add_tags("a");
+    r.mutable_inner()->add_tags("bb");
+    for (int i = 0; i < 3; ++i) r.add_inners()->set_x(i);
+    for (int i = 0; i < 5; ++i) r.add_nums(i * i);
+    r.set_must("m");
+    return r;
+}
+test::IdlTyped MakeIdl() {
+    test::IdlTyped t;
+    t.set_small(-7);
+    t.set_big(4000000000ULL);
+    t.set_blob(std::string("\0bin", 4));
+    t.add_fs(1.5f);
+    t.add_fs(-2.25f);
+    t.set_b(true);
+    t.add_colors(test::GREEN);
+    t.add_colors(test::BLUE);
+    t.add_inners()->set_x(11);
+    t.set_ratio(41.9);
+    return t;
+}
+}  // namespace
+
+TEST(Mcpack, generated_codec_matches_reflection) {
+    ASSERT_TRUE(mcpack::FindMessageHandler(test::Rich::descriptor()) != nullptr);
+    ASSERT_TRUE(mcpack::FindMessageHandler(test::IdlTyped::descriptor()) != nullptr);
+    ASSERT_TRUE(mcpack::FindMessageHandler(example::EchoRequest::descriptor()) != nullptr);
+    const test::Rich r = MakeRich();
+    const test::IdlTyped t = MakeIdl();
+    for (int k = 0; k < 2; ++k) {
+        const mcpack::Format fmt = k ? mcpack::FORMAT_MCPACK_V2 : mcpack::FORMAT_COMPACK;
+        std::string gen_r, ref_r, gen_t, ref_t;
+        ASSERT_TRUE(mcpack::SerializeToString(r, fmt, &gen_r));
+        ASSERT_TRUE(mcpack::SerializeToString(t, fmt, &gen_t));
+        mcpack::SetGeneratedHandlersEnabled(false);
+        ASSERT_TRUE(mcpack::SerializeToString(r, fmt, &ref_r));
+        ASSERT_TRUE(mcpack::SerializeToString(t, fmt, &ref_t));
+        // reflective parse of the generated bytes
+        test::Rich r_ref;
+        test::IdlTyped t_ref;
+        ASSERT_TRUE(mcpack::ParseFromArray(gen_r.data(), gen_r.size(), &r_ref));
+        ASSERT_TRUE(mcpack::ParseFromArray(gen_t.data(), gen_t.size(), &t_ref));
+        mcpack::SetGeneratedHandlersEnabled(true);
+        EXPECT_TRUE(gen_r == ref_r);
+        EXPECT_TRUE(gen_t == ref_t);
+        // generated parse of the reflective bytes
+        test::Rich r_gen;
+        test::IdlTyped t_gen;
+        ASSERT_TRUE(mcpack::ParseFromArray(ref_r.data(), ref_r.size(), &r_gen));
+        ASSERT_TRUE(mcpack::ParseFromArray(ref_t.data(), ref_t.size(), &t_gen));
+        EXPECT_EQ(r_gen.SerializeAsString(), r.SerializeAsString());
+        EXPECT_EQ(r_ref.SerializeAsString(), r.SerializeAsString());
+        EXPECT_EQ(t_gen.SerializeAsString(), t_ref.SerializeAsString());
+        // idl_type conversions: int8 wire for `small`, uint32 for `big`
+        // (truncated), double for floats, int32 for the double `ratio`
+        EXPECT_EQ(t_gen.small(), -7);
+        EXPECT_EQ(t_gen.big(), (uint64_t)(uint32_t)4000000000ULL);
+        EXPECT_EQ(t_gen.blob(), std::string("\0bin", 4));
+        ASSERT_EQ(t_gen.fs_size(), 2);
+        EXPECT_EQ(t_gen.fs(1), -2.25f);
+        EXPECT_EQ(t_gen.colors(1), test::BLUE);
+        ASSERT_EQ(t_gen.inners_size(), 1);
+        EXPECT_EQ(t_gen.inners(0).x(), 11);
+        EXPECT_EQ(t_gen.ratio(), 41.0);
+        // idl_name renames the wire field
+        std::string name;
+        mcpack::Value top;
+        std::vector<mcpack::Item> items;
+        ASSERT_TRUE(mcpack::DecodeField(gen_t.data(), gen_t.size(), &name, &top) > 0);
+        ASSERT_TRUE(mcpack::ListItems(top, &items));
+        bool saw_big = false, saw_rows = false;
+        for (auto& it : items) {
+            if (it.name == "BigOne") saw_big = it.value.type() == mcpack::FIELD_UINT32;
+            if (it.name == "rows") saw_rows = true;
+            if (it.name == "small") EXPECT_EQ((int)it.value.type(), (int)mcpack::FIELD_INT8);
+        }
+        EXPECT_TRUE(saw_big && saw_rows);
+    }
+}
+
+TEST(Mcpack, generated_codec_is_faster) {
+    const test::Rich r = MakeRich();
+    std::string out;
+    auto run = [&](bool gen) {
+        mcpack::SetGeneratedHandlersEnabled(gen);
+        const int64_t t0 = monotonic_us();
+        for (int i = 0; i < 20000; ++i) {
+            mcpack::SerializeToString(r, mcpack::FORMAT_MCPACK_V2, &out);
+            test::Rich back;
+            mcpack::ParseFromArray(out.data(), out.size(), &back);
+        }
+        return monotonic_us() - t0;
+    };
+    run(true);
+    const int64_t ref = run(false), gen = run(true);
+    mcpack::SetGeneratedHandlersEnabled(true);
+    printf("  mcpack serialize+parse x20000: reflection %lld us, generated %lld us (%.2fx)\n", (long long)ref,
+           (long long)gen, (double)ref / std::max<int64_t>(1, gen));
+    EXPECT_GT(ref, 0);
 }

@@ -6,6 +6,7 @@
 // reference relies on).
 //
 // Usage: mrpc_protoc --cpp_out=DIR --proto_path=DIR [--include_prefix=P] a.proto ...
+//        mrpc_protoc --mcpack_out=DIR --proto_path=DIR a.proto ...   (per-message mcpack codec)
 #include <cstdio>
 #include <fstream>
 #include <functional>
@@ -573,17 +574,249 @@ struct Gen {
     }
 };
 
+
+// ------------------------------------------------------------ --mcpack_out
+// Per-message mcpack codec (role of the reference's protoc-gen-mcpack,
+// src/mcpack2pb/generator.cpp): straight-line serialize/parse functions
+// over the generated accessors, registered as the message's
+// mcpack::MessageHandler. Wire types and names follow the same rules as the
+// descriptor-driven codec (mcpack/mcpack.cc: idl_name / idl_type options).
+std::string mc_option(const FieldDescriptor& f, const char* key) {
+    auto it = f.options.find(std::string("(") + key + ")");
+    if (it == f.options.end()) it = f.options.find(key);
+    if (it == f.options.end()) return std::string();
+    std::string v = it->second;
+    if (v.size() >= 2 && (v[0] == '"' || v[0] == '\'') && v.back() == v[0]) v = v.substr(1, v.size() - 2);
+    return v;
+}
+
+std::string mc_wire_type(const FieldDescriptor& f) {
+    const std::string idl = mc_option(f, "idl_type");
+    static const char* kIdl[][2] = {
+        {"IDL_INT8", "FIELD_INT8"},     {"IDL_INT16", "FIELD_INT16"},   {"IDL_INT32", "FIELD_INT32"},
+        {"IDL_INT64", "FIELD_INT64"},   {"IDL_UINT8", "FIELD_UINT8"},   {"IDL_UINT16", "FIELD_UINT16"},
+        {"IDL_UINT32", "FIELD_UINT32"}, {"IDL_UINT64", "FIELD_UINT64"}, {"IDL_BOOL", "FIELD_BOOL"},
+        {"IDL_FLOAT", "FIELD_FLOAT"},   {"IDL_DOUBLE", "FIELD_DOUBLE"}, {"IDL_BINARY", "FIELD_BINARY"},
+        {"IDL_STRING", "FIELD_STRING"},
+    };
+    for (auto& k : kIdl) {
+        if (idl == k[0]) return k[1];
+    }
+    switch (f.type) {
+    case FieldType::INT32: case FieldType::SINT32: case FieldType::SFIXED32: case FieldType::ENUM: return "FIELD_INT32";
+    case FieldType::INT64: case FieldType::SINT64: case FieldType::SFIXED64: return "FIELD_INT64";
+    case FieldType::UINT32: case FieldType::FIXED32: return "FIELD_UINT32";
+    case FieldType::UINT64: case FieldType::FIXED64: return "FIELD_UINT64";
+    case FieldType::BOOL: return "FIELD_BOOL";
+    case FieldType::FLOAT: return "FIELD_FLOAT";
+    case FieldType::DOUBLE: return "FIELD_DOUBLE";
+    case FieldType::STRING: return "FIELD_STRING";
+    case FieldType::BYTES: return "FIELD_BINARY";
+    default: return "FIELD_OBJECT";
+    }
+}
+
+struct McpackGen {
+    const FileDescriptor* file;
+    std::string prefix;
+    std::vector<const Descriptor*> msgs;
+    std::ostringstream c;
+
+    void collect(const Descriptor* d) {
+        msgs.push_back(d);
+        for (const Descriptor* n : d->nested_types) collect(n);
+    }
+    bool local(const Descriptor* d) const {
+        for (const Descriptor* m : msgs) {
+            if (m == d) return true;
+        }
+        return false;
+    }
+    std::string fn(const Descriptor* d, const char* what) const { return std::string("mc_") + what + "_" + ident_of(d->full_name); }
+    std::string kname(const Descriptor* d, const FieldDescriptor& f) const { return "kMc_" + ident_of(d->full_name) + "_" + f.name; }
+
+    // value expression -> Serializer call with wire type t
+    std::string add_call(const FieldDescriptor& f, const std::string& t, const std::string& name, const std::string& v) const {
+        const CppType ct = f.cpp_type();
+        if (ct == CppType::STRING) {
+            return t == "FIELD_STRING" ? "sr->add_string(" + name + ", " + v + ");"
+                                       : "{ const std::string& s_ = " + v + "; sr->add_binary(" + name + ", s_.data(), s_.size()); }";
+        }
+        struct Nat { CppType ct; const char* t; const char* call; };
+        static const Nat kNat[] = {
+            {CppType::INT32, "FIELD_INT32", "add_int32"}, {CppType::ENUM, "FIELD_INT32", "add_int32"},
+            {CppType::INT64, "FIELD_INT64", "add_int64"}, {CppType::UINT32, "FIELD_UINT32", "add_uint32"},
+            {CppType::UINT64, "FIELD_UINT64", "add_uint64"}, {CppType::BOOL, "FIELD_BOOL", "add_bool"},
+            {CppType::FLOAT, "FIELD_FLOAT", "add_float"}, {CppType::DOUBLE, "FIELD_DOUBLE", "add_double"},
+        };
+        for (auto& n : kNat) {
+            if (n.ct == ct && t == n.t) {
+                const std::string cast = ct == CppType::ENUM ? "(int32_t)" : "";
+                return "sr->" + std::string(n.call) + "(" + name + ", " + cast + v + ");";
+            }
+        }
+        // idl_type asked for another width/kind: same conversion as the reflective codec
+        const bool is_float = ct == CppType::FLOAT || ct == CppType::DOUBLE;
+        const bool is_unsigned = ct == CppType::UINT32 || ct == CppType::UINT64;
+        std::string iv = "0", uv = "0", dv = "0";
+        if (is_float) dv = "(double)" + v;
+        else if (is_unsigned) uv = "(uint64_t)" + v;
+        else iv = "(int64_t)" + v;
+        return "::mrpc::mcpack::AddConverted(sr, " + name + ", ::mrpc::mcpack::" + t + ", " + iv + ", " + uv + ", " + dv +
+               ", " + (is_float ? "true" : "false") + ", " + (is_unsigned ? "true" : "false") + ");";
+    }
+
+    // parse one Value `val` into field f (set or add) of `m`
+    std::string set_code(const Descriptor* d, const FieldDescriptor& f, const std::string& val) const {
+        (void)d;
+        const bool rep = f.is_repeated();
+        const std::string op = rep ? "add_" + f.name : "set_" + f.name;
+        switch (f.cpp_type()) {
+        case CppType::INT32:
+            return "{ int64_t v_; if (!" + val + ".to_int64(&v_)) return false; m->" + op + "((int32_t)v_); }";
+        case CppType::ENUM:
+            return "{ int64_t v_; if (!" + val + ".to_int64(&v_)) return false; m->" + op + "((" + cpp_enum(f.enum_type) +
+                   ")(int)v_); }";
+        case CppType::INT64:
+            return "{ int64_t v_; if (!" + val + ".to_int64(&v_)) return false; m->" + op + "(v_); }";
+        case CppType::UINT32:
+            return "{ uint64_t v_; if (!" + val + ".to_uint64(&v_)) return false; m->" + op + "((uint32_t)v_); }";
+        case CppType::UINT64:
+            return "{ uint64_t v_; if (!" + val + ".to_uint64(&v_)) return false; m->" + op + "(v_); }";
+        case CppType::BOOL:
+            return "{ bool v_; if (!" + val + ".to_bool(&v_)) return false; m->" + op + "(v_); }";
+        case CppType::FLOAT:
+            return "{ double v_; if (!" + val + ".to_double(&v_)) return false; m->" + op + "((float)v_); }";
+        case CppType::DOUBLE:
+            return "{ double v_; if (!" + val + ".to_double(&v_)) return false; m->" + op + "(v_); }";
+        case CppType::STRING:
+            if (rep) return "{ if (!" + val + ".to_string(m->add_" + f.name + "())) return false; }";
+            return "{ if (!" + val + ".to_string(m->mutable_" + f.name + "())) return false; }";
+        case CppType::MESSAGE: {
+            const std::string target = rep ? "m->add_" + f.name + "()" : "m->mutable_" + f.name + "()";
+            const std::string parse = local(f.message_type) ? fn(f.message_type, "parse") + "(" + val + ", " + target + ")"
+                                                            : "::mrpc::mcpack::ParseFromObject(" + val + ", " + target + ")";
+            return "{ if (" + val + ".type() != ::mrpc::mcpack::FIELD_OBJECT || !" + parse + ") return false; }";
+        }
+        }
+        return "";
+    }
+
+    void gen_message(const Descriptor* d) {
+        const std::string cls = cpp_class(d);
+        for (const FieldDescriptor& f : d->fields) {
+            if (f.is_map()) continue;
+            std::string n = mc_option(f, "idl_name");
+            if (n.empty()) n = f.name;
+            c << "const std::string " << kname(d, f) << "(" << cstr_literal(n) << ");\n";
+        }
+        // serialize
+        c << "bool " << fn(d, "ser") << "(const ::mrpc::pb::Message& m_, ::mrpc::mcpack::Format fmt, ::mrpc::mcpack::Serializer* sr) {\n";
+        c << "  const " << cls << "& m = static_cast<const " << cls << "&>(m_);\n  (void)m; (void)fmt;\n";
+        for (const FieldDescriptor& f : d->fields) {
+            if (f.is_map()) continue;
+            const std::string K = kname(d, f), t = mc_wire_type(f);
+            if (f.is_repeated()) {
+                c << "  if (m." << f.name << "_size() > 0) {\n";
+                if (f.cpp_type() == CppType::MESSAGE) {
+                    c << "    sr->begin_array(" << K << ", ::mrpc::mcpack::FIELD_OBJECT, fmt);\n";
+                    c << "    for (int i = 0; i < m." << f.name << "_size(); ++i) {\n      sr->begin_object();\n";
+                    c << "      " << (local(f.message_type) ? fn(f.message_type, "ser") : std::string("::mrpc::mcpack::SerializeFields"))
+                      << "(m." << f.name << "(i), fmt, sr);\n      sr->end_object();\n    }\n";
+                } else {
+                    c << "    sr->begin_array(" << K << ", ::mrpc::mcpack::" << t << ", fmt);\n";
+                    c << "    for (int i = 0; i < m." << f.name << "_size(); ++i) " << add_call(f, t, "kMcEmpty", "m." + f.name + "(i)")
+                      << "\n";
+                }
+                c << "    sr->end_array();\n  }\n";
+                continue;
+            }
+            c << "  if (m.has_" << f.name << "()) {\n";
+            if (f.cpp_type() == CppType::MESSAGE) {
+                c << "    sr->begin_object(" << K << ");\n    "
+                  << (local(f.message_type) ? fn(f.message_type, "ser") : std::string("::mrpc::mcpack::SerializeFields")) << "(m."
+                  << f.name << "(), fmt, sr);\n    sr->end_object();\n";
+            } else {
+                c << "    " << add_call(f, t, K, "m." + f.name + "()") << "\n";
+            }
+            c << "  }\n";
+        }
+        c << "  return sr->good();\n}\n";
+        // parse
+        c << "bool " << fn(d, "parse") << "(const ::mrpc::mcpack::Value& obj, ::mrpc::pb::Message* m_) {\n";
+        c << "  if (obj.type() != ::mrpc::mcpack::FIELD_OBJECT) return false;\n";
+        c << "  " << cls << "* m = static_cast<" << cls << "*>(m_);\n";
+        c << "  std::vector<::mrpc::mcpack::Item> items;\n  if (!::mrpc::mcpack::ListItems(obj, &items)) return false;\n";
+        c << "  for (const ::mrpc::mcpack::Item& it : items) {\n    if (it.value.is_null()) continue;\n";
+        c << "    const uint8_t t_ = it.value.type();\n    (void)t_;\n";
+        bool first = true;
+        for (const FieldDescriptor& f : d->fields) {
+            if (f.is_map()) continue;
+            c << "    " << (first ? "" : "} else ") << "if (it.name == " << kname(d, f) << ") {\n";
+            first = false;
+            if (f.is_repeated()) {
+                if (f.cpp_type() == CppType::MESSAGE) {
+                    c << "      if (t_ == ::mrpc::mcpack::FIELD_OBJECTISOARRAY) {\n"
+                      << "        if (!::mrpc::mcpack::ParseObjectIsoArrayField(it.value, m, " << cls << "::descriptor()->field("
+                      << f.index << "))) return false;\n        continue;\n      }\n";
+                } else {
+                    c << "      if (t_ == ::mrpc::mcpack::FIELD_OBJECTISOARRAY) return false;\n";
+                }
+                c << "      if (t_ == ::mrpc::mcpack::FIELD_ARRAY || t_ == ::mrpc::mcpack::FIELD_ISOARRAY) {\n"
+                  << "        std::vector<::mrpc::mcpack::Item> elems;\n"
+                  << "        if (!::mrpc::mcpack::ListItems(it.value, &elems)) return false;\n"
+                  << "        for (const ::mrpc::mcpack::Item& e : elems) {\n          if (e.value.is_null()) continue;\n"
+                  << "          " << set_code(d, f, "e.value") << "\n        }\n        continue;\n      }\n";
+            }
+            c << "      " << set_code(d, f, "it.value") << "\n";
+        }
+        if (!first) c << "    }\n";
+        c << "  }\n  return true;\n}\n";
+        c << "const ::mrpc::mcpack::MessageHandler " << fn(d, "handler") << " = {&" << fn(d, "ser") << ", &" << fn(d, "parse")
+          << "};\n\n";
+    }
+
+    void run(const std::string& base) {
+        for (const Descriptor* d : file->message_types) collect(d);
+        c << "// Generated by mrpc_protoc --mcpack_out from " << file->name << ". DO NOT EDIT.\n";
+        c << "#include \"" << prefix << base << ".pb.h\"\n#include <string>\n#include <vector>\n";
+        c << "#include \"mcpack/mcpack.h\"\n\nnamespace {\n\nconst std::string kMcEmpty;\n\n";
+        for (const Descriptor* d : msgs) {
+            if (d->map_entry) continue;
+            c << "bool " << fn(d, "ser") << "(const ::mrpc::pb::Message&, ::mrpc::mcpack::Format, ::mrpc::mcpack::Serializer*);\n";
+            c << "bool " << fn(d, "parse") << "(const ::mrpc::mcpack::Value&, ::mrpc::pb::Message*);\n";
+        }
+        c << "\n";
+        for (const Descriptor* d : msgs) {
+            if (!d->map_entry) gen_message(d);
+        }
+        c << "struct McpackRegistrar {\n  McpackRegistrar() {\n";
+        for (const Descriptor* d : msgs) {
+            if (!d->map_entry) {
+                c << "    ::mrpc::mcpack::RegisterMessageHandler(" << cpp_class(d) << "::descriptor(), &" << fn(d, "handler")
+                  << ");\n";
+            }
+        }
+        c << "  }\n} mc_registrar_" << ident_of(base) << ";\n\n}  // namespace\n";
+    }
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
-    std::string out_dir = ".", prefix;
+    std::string out_dir = ".", prefix, mcpack_out;
+    bool cpp_out = false;
     std::vector<std::string> paths, files;
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
-        if (a.compare(0, 10, "--cpp_out=") == 0) out_dir = a.substr(10);
+        if (a.compare(0, 10, "--cpp_out=") == 0) {
+            out_dir = a.substr(10);
+            cpp_out = true;
+        }
         else if (a.compare(0, 13, "--proto_path=") == 0) paths.push_back(a.substr(13));
         else if (a.compare(0, 2, "-I") == 0) paths.push_back(a.substr(2));
         else if (a.compare(0, 17, "--include_prefix=") == 0) prefix = a.substr(17);
+        else if (a.compare(0, 13, "--mcpack_out=") == 0) mcpack_out = a.substr(13);
         else files.push_back(a);
     }
     if (files.empty()) {
@@ -607,10 +840,18 @@ int main(int argc, char** argv) {
             fprintf(stderr, "mrpc_protoc: %s\n", err.c_str());
             return 1;
         }
+        std::string base = basename_noext(rel);
+        if (!mcpack_out.empty()) {
+            McpackGen mg;
+            mg.file = fd;
+            mg.prefix = prefix;
+            mg.run(base);
+            std::ofstream(mcpack_out + "/" + base + ".pb.mcpack.cc") << mg.c.str();
+            if (!cpp_out) continue;  // --mcpack_out alone: no message classes
+        }
         Gen g;
         g.file = fd;
         g.prefix = prefix;
-        std::string base = basename_noext(rel);
         g.run(base);
         std::ofstream(out_dir + "/" + base + ".pb.h") << g.h.str();
         std::ofstream(out_dir + "/" + base + ".pb.cc") << g.c.str();

@@ -32,6 +32,9 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0]
 
 # Directories whose sources form the bootstrap library used by mrpc_protoc.
 BOOT_DIRS = ["base", "pb"]
+# Protos that also get generated mcpack codecs (mrpc_protoc --mcpack_out),
+# compiled into libmrpc: the mcpack/ubrpc/nshead_mcpack services' messages.
+MCPACK_PROTOS = ["echo", "test_services"]
 # Directories excluded from libmrpc.
 NON_LIB_DIRS = {"tools", "python", "tests", "examples", "heapprof"}
 
@@ -136,6 +139,17 @@ def main():
         w(f"build {rel(cc)} {rel(h)}: protoc {rel(p)} | {rel(protoc)}\n"
           f"  protoc = {rel(protoc)}\n  gendir = {rel(os.path.join(GEN, 'mrpc', 'proto'))}\n"
           f"  protodir = {rel(os.path.join(PKG, 'proto'))}\n")
+    w("rule protoc_mcpack\n  command = $protoc --mcpack_out=$gendir --proto_path=$protodir $in\n"
+      "  description = PROTOC-MCPACK $in\n")
+    for p in protos:
+        b = os.path.splitext(os.path.basename(p))[0]
+        if b not in MCPACK_PROTOS:
+            continue
+        mc = os.path.join(GEN, "mrpc", "proto", b + ".pb.mcpack.cc")
+        w(f"build {rel(mc)}: protoc_mcpack {rel(p)} | {rel(protoc)}\n"
+          f"  protoc = {rel(protoc)}\n  gendir = {rel(os.path.join(GEN, 'mrpc', 'proto'))}\n"
+          f"  protodir = {rel(os.path.join(PKG, 'proto'))}\n")
+        gen_ccs.append(mc)
     w(f"build gen_headers: phony {' '.join(rel(h) for h in gen_hs)}\n")
 
     lib_objs = []
