@@ -141,8 +141,10 @@ def main():
         p99_max = parallel.allreduce_max(st["p99_us"], topo)
         p50_max = parallel.allreduce_max(st["p50_us"], topo)
         del press
-        step_qps = sorted(n / x for x in step_s if x > 0)
+        step_seq = [n / x for x in step_s if x > 0]
+        step_qps = sorted(step_seq)
         return {
+            "step_qps_seq": [int(q) for q in step_seq],
             "qps": ok_total / dt_max if dt_max > 0 else 0.0,
             "ms_per_step": 1000.0 * dt_max / steps,
             "p50_us": p50_max,
@@ -311,6 +313,7 @@ def main():
             "step_qps_median_32B": round(r32["step_qps_median"], 1),
             "step_qps_min_32B": round(r32["step_qps_min"], 1),
             "step_qps_max_32B": round(r32["step_qps_max"], 1),
+            "step_qps_seq_32B": r32["step_qps_seq"],
         }
         if r64:
             out["qps_64KB"] = round(r64["qps"], 1)

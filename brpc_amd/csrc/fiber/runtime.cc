@@ -7,11 +7,15 @@
 #if defined(__SANITIZE_THREAD__)
 #include <sanitizer/tsan_interface.h>
 #endif
+#include <dirent.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 
 #include <cerrno>
 #include <cstring>
 #include <functional>
+#include <map>
 
 #include "base/flags.h"
 #include "base/logging.h"
@@ -20,6 +24,7 @@
 #include "base/util.h"
 #include "fiber/butex.h"
 #include "fiber/context.h"
+
 #include "fiber/internal.h"
 #include "fiber/key_internal.h"
 #include "fiber/timer.h"
@@ -54,6 +59,12 @@ DEFINE_int32(stack_size_normal, 1048576, "size of normal fiber stacks");
 DEFINE_int32(stack_size_large, 8388608, "size of large fiber stacks");
 DEFINE_int32(guard_page_size, 4096, "size of guard page at the bottom of fiber stacks");
 DEFINE_int32(task_group_runqueue_capacity, 4096, "capacity of each worker's run queue");
+DEFINE_int32(cpu_l3_domain, -1,
+             "confine the whole process (all threads) to the CPUs sharing the k-th L3 cache of the "
+             "affinity mask (-1: leave the mask alone); one process per GPU passes a rank-derived k");
+DEFINE_int32(fiber_worker_cpu_offset, -1,
+             "pin worker i to the (offset + i)-th CPU of the process affinity mask (-1: no pinning); "
+             "one process per GPU passes local_rank * cpus_per_rank");
 // Off by default: on the MI355X box (16-CPU quota) idle spinning cost more
 // throughput than it saved latency (profiles/bench_r1_spin_ab.txt).
 DEFINE_int32(fiber_idle_spin_us, 0,
@@ -661,6 +672,106 @@ TaskControl::TaskControl() {
     start_ns = monotonic_ns();
 }
 
+namespace {
+
+int read_cpu_int(int cpu, const char* what, int dflt) {
+    char path[160];
+    snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/%s", cpu, what);
+    FILE* f = fopen(path, "r");
+    int x = dflt;
+    if (f) {
+        if (fscanf(f, "%d", &x) != 1) x = dflt;
+        fclose(f);
+    }
+    return x;
+}
+
+// Orders `cpus` so that the first SMT thread of every physical core comes
+// first, then the second threads, ...
+std::vector<int> order_by_core(const std::vector<int>& cpus) {
+    std::map<std::pair<int, int>, std::vector<int>> by_core;  // (package, core) -> cpus
+    for (int cpu : cpus) {
+        by_core[{read_cpu_int(cpu, "topology/physical_package_id", 0), read_cpu_int(cpu, "topology/core_id", cpu)}]
+            .push_back(cpu);
+    }
+    std::vector<int> v;
+    for (size_t round = 0;; ++round) {
+        bool any = false;
+        for (auto& kv : by_core) {
+            if (round < kv.second.size()) {
+                v.push_back(kv.second[round]);
+                any = true;
+            }
+        }
+        if (!any) break;
+    }
+    return v;
+}
+
+std::vector<int> allowed_cpus() {
+    std::vector<int> v;
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return v;
+    for (int cpu = 0; cpu < CPU_SETSIZE; ++cpu) {
+        if (CPU_ISSET(cpu, &allowed)) v.push_back(cpu);
+    }
+    return v;
+}
+
+// The k-th group (mod count) of allowed CPUs sharing an L3 cache, ordered by
+// core. The machines this runs on expose hundreds of CPUs to a container
+// whose CPU-time quota is a small fraction of them: left alone, the
+// scheduler scatters the runtime's threads over many L3 domains (and both
+// sockets), and every cross-domain cache-line transfer on the request path
+// shows up as latency and as large step-to-step throughput swings.
+std::vector<int> l3_domain_cpus(int k) {
+    std::map<int, std::vector<int>> groups;  // lowest cpu sharing the L3 -> cpus
+    for (int cpu : allowed_cpus()) {
+        char path[160];
+        snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+        FILE* f = fopen(path, "r");
+        int first = cpu;
+        if (f) {
+            if (fscanf(f, "%d", &first) != 1) first = cpu;
+            fclose(f);
+        }
+        groups[first].push_back(cpu);
+    }
+    if (groups.empty()) return {};
+    auto it = groups.begin();
+    std::advance(it, (size_t)k % groups.size());
+    return order_by_core(it->second);
+}
+
+void apply_process_affinity() {
+    if (FLAGS_cpu_l3_domain < 0) return;
+    const std::vector<int> cpus = l3_domain_cpus(FLAGS_cpu_l3_domain);
+    if (cpus.empty()) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int c : cpus) CPU_SET(c, &set);
+    // every existing thread (the embedding interpreter, HIP's helpers) and,
+    // through the calling thread's mask, every thread created from now on
+    if (DIR* d = opendir("/proc/self/task")) {
+        while (dirent* e = readdir(d)) {
+            const int tid = atoi(e->d_name);
+            if (tid > 0) sched_setaffinity(tid, sizeof(set), &set);
+        }
+        closedir(d);
+    }
+    sched_setaffinity(0, sizeof(set), &set);
+    LOG(INFO) << "fiber runtime confined to L3 domain " << FLAGS_cpu_l3_domain << " (" << cpus.size() << " CPUs from "
+              << cpus.front() << ")";
+}
+
+}  // namespace
+
+// CPUs of the (possibly confined) affinity mask, physical cores first.
+static const std::vector<int>& cpu_order_by_core() {
+    static std::vector<int>* order = new std::vector<int>(order_by_core(allowed_cpus()));
+    return *order;
+}
+
 void* TaskControl::worker_thread(void* arg) {
     TaskControl* c = (TaskControl*)arg;
     TaskGroup* g = new TaskGroup(c);
@@ -682,6 +793,18 @@ void* TaskControl::worker_thread(void* arg) {
     char name[32];
     snprintf(name, sizeof(name), "mrpc_worker%d", g->_index);
     pthread_setname_np(pthread_self(), name);
+    if (FLAGS_fiber_worker_cpu_offset >= 0) {
+        // a worker that never migrates keeps its run queue, stacks and the
+        // sockets it serves hot in one core's caches; physical cores are
+        // handed out before their SMT siblings
+        const std::vector<int>& order = cpu_order_by_core();
+        if (!order.empty()) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(order[(size_t)(FLAGS_fiber_worker_cpu_offset + g->_index) % order.size()], &one);
+            pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+        }
+    }
     set_tls_group(g);
     g->run_main_task();
     set_tls_group(nullptr);
@@ -689,6 +812,7 @@ void* TaskControl::worker_thread(void* arg) {
 }
 
 int TaskControl::init(int concurrency) {
+    apply_process_affinity();
     if (concurrency <= 0) concurrency = 1;
     if (concurrency > kMaxConcurrency) concurrency = kMaxConcurrency;
     return add_workers(concurrency) > 0 ? 0 : -1;

@@ -1,9 +1,35 @@
 #!/bin/bash
-# Worker-count sweep of the 32B echo bench (3 repeats each) + latency sample.
-cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-cat /sys/fs/cgroup/cpu.max > gpurun_out/sweep_cpu.txt 2>&1; cat /proc/loadavg >> gpurun_out/sweep_cpu.txt
-for w in ${SWEEP_WORKERS:-4 6 8 12 16}; do
-  for r in 1 2 3; do
-    timeout -k 10 120 python bench.py --workers $w --skip-64k --latency-sample-s ${LAT_S:-0} > gpurun_out/sweep_w${w}_r${r}.json 2>/dev/null || exit 1
-  done
+# 32 B headline sweep on the GPU box: fiber workers and idle-spin knobs.
+# Each run prints one JSON line; summary in gpurun_out/sweep.txt.
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+out=gpurun_out/sweep.txt
+: > $out
+run() {  # label, then env assignments / args
+  local label=$1; shift
+  echo "== $label" | tee -a $out
+  local t0=$(grep -E '^(nr_throttled|throttled_usec|usage_usec)' /sys/fs/cgroup/cpu.stat | tr '\n' ' ')
+  timeout -k 10 120 env "$@" > gpurun_out/sweep_run.log 2>&1
+  local rc=$?
+  local t1=$(grep -E '^(nr_throttled|throttled_usec|usage_usec)' /sys/fs/cgroup/cpu.stat | tr '\n' ' ')
+  echo "cpu.stat before: $t0" | tee -a $out
+  echo "cpu.stat after:  $t1" | tee -a $out
+  grep '^{' gpurun_out/sweep_run.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print('value=%.0f p99=%s med=%.0f min=%.0f max=%.0f' % (d['value'], d['p99_us'], d['step_qps_median_32B'], d['step_qps_min_32B'], d['step_qps_max_32B'])); print('steps(k): ' + ' '.join(str(q // 1000) for q in d.get('step_qps_seq_32B', [])))
+" | tee -a $out
+  if [ $rc -ne 0 ]; then echo "rc=$rc" | tee -a $out; tail -5 gpurun_out/sweep_run.log; exit $rc; fi
+}
+B="python3 bench.py --skip-64k --skip-grpc --skip-stream --latency-sample-s 0 --steps 20 --warmup 3"
+nproc; cat /sys/fs/cgroup/cpu.max || true
+for rep in 1 2; do
+  run "rep$rep w8 l3=0" MRPC_FLAGS="--cpu_l3_domain=0" $B --workers 8
+  run "rep$rep w10 l3=0" MRPC_FLAGS="--cpu_l3_domain=0" $B --workers 10
+  run "rep$rep w12 l3=0" MRPC_FLAGS="--cpu_l3_domain=0" $B --workers 12
+  run "rep$rep w8 l3=0 pinned" MRPC_FLAGS="--cpu_l3_domain=0 --fiber_worker_cpu_offset=0" $B --workers 8
+  run "rep$rep w12 l3=0 pinned" MRPC_FLAGS="--cpu_l3_domain=0 --fiber_worker_cpu_offset=0" $B --workers 12
+  run "rep$rep w8 l3=3 pinned" MRPC_FLAGS="--cpu_l3_domain=3 --fiber_worker_cpu_offset=0" $B --workers 8
 done
+echo done
