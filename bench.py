@@ -53,6 +53,9 @@ def parse():
                     help="64 KiB leg with host attachments only (default on a GPU box: HBM-resident "
                          "attachments over the xGMI transport, plus a host-attachment reference leg)")
     ap.add_argument("--device-payload", action="store_true", help=argparse.SUPPRESS)  # old flag, now default
+    ap.add_argument("--cpu-l3-domain", type=int, default=-2,
+                    help="confine the rank to the CPUs of this L3 domain (-2: auto, one domain per local rank "
+                         "spread over the node; -1: no confinement)")
     ap.add_argument("--latency-sample-s", type=float, default=4.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
@@ -73,6 +76,35 @@ def cpu_quota():
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 8
+
+
+def l3_domain_count():
+    """Number of distinct L3 caches among the CPUs this process may run on."""
+    firsts = set()
+    try:
+        cpus = os.sched_getaffinity(0)
+    except AttributeError:
+        return 1
+    for c in cpus:
+        try:
+            with open("/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list" % c) as f:
+                firsts.add(f.read().split(",")[0].split("-")[0].strip())
+        except OSError:
+            firsts.add(str(c))
+    return max(1, len(firsts))
+
+
+def auto_l3_domain(local_rank, local_world):
+    # The GPU boxes expose every CPU of the node (256) under a CPU-time quota
+    # of a few cores per GPU. Unconfined, the scheduler scatters the
+    # runtime's threads over many L3 domains and both sockets; confined to
+    # one L3 domain the 32 B echo runs ~1.1 M QPS with p99 ~70 us and
+    # <5% step-to-step spread instead of 0.4-1.1 M (profiles/r2_cpu_affinity_sweep.txt).
+    # Ranks of one node take domains spread evenly over the node.
+    n = l3_domain_count()
+    if n <= 1:
+        return -1
+    return (local_rank * max(1, n // max(1, local_world))) % n
 
 
 def auto_workers(local_world):
@@ -100,6 +132,9 @@ def main():
         print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, topo.world_size), file=sys.stderr)
     workers = a.workers or auto_workers(topo.local_world_size)
     native.set_flag("fiber_concurrency", str(workers))
+    l3 = a.cpu_l3_domain if a.cpu_l3_domain != -2 else auto_l3_domain(topo.local_rank, topo.local_world_size)
+    if l3 >= 0:
+        native.set_flag("cpu_l3_domain", str(l3))
     # extra runtime flags for experiments: MRPC_FLAGS="--name=value ..."
     for item in os.environ.get("MRPC_FLAGS", "").split():
         k, _, v = item.lstrip("-").partition("=")
@@ -305,6 +340,7 @@ def main():
                 "parallelism": "ring%d (rank r -> server of rank r+1), 1 conn/rank" % n,
                 "requests_per_step_per_rank": wl32.requests_per_step,
                 "fiber_workers_per_rank": workers,
+                "cpu_l3_domain_rank0": l3,
             },
             "p50_us": r32["p50_us"],
             "p99_us": r32["p99_us"],

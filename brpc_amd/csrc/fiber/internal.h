@@ -139,6 +139,37 @@ struct TaskMeta {
 
 class TaskControl;
 
+// Queue of fibers made runnable by threads that are not this worker (event
+// dispatcher, timer, GPU poller, foreign pthreads), guarded by the group's
+// _remote_mu. A power-of-two ring that only grows: no allocation per push
+// once warm (std::deque allocated a node every 64 pushes).
+class RemoteQueue {
+public:
+    RemoteQueue() : _buf(256) {}
+    bool empty() const { return _n == 0; }
+    size_t size() const { return _n; }
+    void push_back(fiber_t t) {
+        if (_n == _buf.size()) grow();
+        _buf[(_head + _n) & (_buf.size() - 1)] = t;
+        ++_n;
+    }
+    fiber_t front() const { return _buf[_head]; }
+    void pop_front() {
+        _head = (_head + 1) & (_buf.size() - 1);
+        --_n;
+    }
+
+private:
+    void grow() {
+        std::vector<fiber_t> b(_buf.size() * 2);
+        for (size_t i = 0; i < _n; ++i) b[i] = _buf[(_head + i) & (_buf.size() - 1)];
+        _buf.swap(b);
+        _head = 0;
+    }
+    std::vector<fiber_t> _buf;
+    size_t _head = 0, _n = 0;
+};
+
 class TaskGroup {
 public:
     explicit TaskGroup(TaskControl* c);
@@ -194,7 +225,7 @@ private:
     fiber_t _main_tid;
     WorkStealingQueue<fiber_t> _rq;
     std::mutex _remote_mu;
-    std::deque<fiber_t> _remote_rq;
+    RemoteQueue _remote_rq;
     std::atomic<int> _remote_size{0};
     void (*_last_fn)(void*) = nullptr;
     void* _last_arg = nullptr;

@@ -103,13 +103,18 @@ size_t stack_size_of(StackType t) {
     }
 }
 
+// Per-worker stack cache: a fiber that ends on a worker leaves its stack
+// there for the next fiber that worker starts (no lock, warm cache lines);
+// overflow goes to the global pools.
+const size_t kTlsStackCacheSize = 32;
+struct TlsStackCache {
+    std::vector<Stack*> v[5];
+};
+thread_local TlsStackCache tls_stack_cache;
+
 Stack* get_stack(StackType t) {
     if (t == STACK_PTHREAD || t == STACK_UNKNOWN) t = STACK_NORMAL;
-    struct TLSCache {
-        std::vector<Stack*> v[5];
-    };
-    static thread_local TLSCache cache;
-    auto& local = cache.v[t];
+    auto& local = tls_stack_cache.v[t];
     if (!local.empty()) {
         Stack* s = local.back();
         local.pop_back();
@@ -145,9 +150,11 @@ Stack* get_stack(StackType t) {
 }
 
 void return_stack(Stack* s) {
-    struct TLSCache {
-        std::vector<Stack*> v[5];
-    };
+    auto& local = tls_stack_cache.v[s->type];
+    if (local.size() < kTlsStackCacheSize) {
+        local.push_back(s);
+        return;
+    }
     StackPool& p = g_stack_pools[s->type];
     std::lock_guard<std::mutex> g(p.mu);
     if (p.free.size() < 1024) {
@@ -437,7 +444,12 @@ int TaskGroup::usleep(TaskGroup** pg, uint64_t us) {
     // The timer may still be running (it just woke us); spin until it ends.
     uint64_t id = m->current_sleep.exchange(0, std::memory_order_acquire);
     if (id) {
-        while (get_global_timer_thread()->unschedule(id) == -1) cpu_relax();
+        // -1: the timer callback that woke us is still returning; it is a
+        // few instructions from done, but never burn a whole time slice
+        for (int spin = 0; get_global_timer_thread()->unschedule(id) == -1; ++spin) {
+            if (spin < 64) cpu_relax();
+            else sched_yield();
+        }
     }
     if (m->interrupted) {
         m->interrupted = false;
