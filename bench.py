@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu-l3-domain", type=int, default=-2,
                     help="confine the rank to the CPUs of this L3 domain (-2: auto, one domain per local rank "
                          "spread over the node; -1: no confinement)")
+    ap.add_argument("--dispatcher-poll-us", type=int, default=1000000,
+                    help="event dispatcher busy-polls epoll for this long after the last event before "
+                         "sleeping (-event_dispatcher_spin_us; 0: always sleep in epoll_wait)")
     ap.add_argument("--latency-sample-s", type=float, default=4.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
@@ -104,7 +107,8 @@ def auto_l3_domain(local_rank, local_world):
     n = l3_domain_count()
     if n <= 1:
         return -1
-    return (local_rank * max(1, n // max(1, local_world))) % n
+    # domain 0 holds CPU 0 (housekeeping, most IRQs): start at 1
+    return (1 + local_rank * max(1, n // max(1, local_world))) % n
 
 
 def auto_workers(local_world):
@@ -135,6 +139,12 @@ def main():
     l3 = a.cpu_l3_domain if a.cpu_l3_domain != -2 else auto_l3_domain(topo.local_rank, topo.local_world_size)
     if l3 >= 0:
         native.set_flag("cpu_l3_domain", str(l3))
+    # Busy-polling dispatcher: one core per rank keeps polling epoll while
+    # traffic flows (it sleeps after --dispatcher-poll-us of silence). On the
+    # box this removes the epoll_wait wake-up from every hop: 32 B echo
+    # 1.11-1.15 M -> 1.21-1.26 M QPS, p99 at 100 QPS 390-455 -> 45-138 us
+    # (profiles/r2_cpu_affinity_sweep.txt).
+    native.set_flag("event_dispatcher_spin_us", str(max(0, a.dispatcher_poll_us)))
     # extra runtime flags for experiments: MRPC_FLAGS="--name=value ..."
     for item in os.environ.get("MRPC_FLAGS", "").split():
         k, _, v = item.lstrip("-").partition("=")
@@ -341,6 +351,7 @@ def main():
                 "requests_per_step_per_rank": wl32.requests_per_step,
                 "fiber_workers_per_rank": workers,
                 "cpu_l3_domain_rank0": l3,
+                "dispatcher_poll_us": max(0, a.dispatcher_poll_us),
             },
             "p50_us": r32["p50_us"],
             "p99_us": r32["p99_us"],

@@ -24,12 +24,28 @@ for l in sys.stdin:
 }
 B="python3 bench.py --skip-64k --skip-grpc --skip-stream --latency-sample-s 0 --steps 20 --warmup 3"
 nproc; cat /sys/fs/cgroup/cpu.max || true
+L="python3 bench.py --skip-64k --skip-grpc --skip-stream --latency-sample-s 4 --steps 2 --warmup 1 --requests-per-step 2000"
+lat() {
+  local label=$1; shift
+  echo "== $label" | tee -a $out
+  timeout -k 10 120 env "$@" > gpurun_out/sweep_run.log 2>&1 || { echo "rc=$?" | tee -a $out; tail -5 gpurun_out/sweep_run.log; exit 1; }
+  grep '^{' gpurun_out/sweep_run.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print('lat100: p50=%s p99=%s' % (d.get('p50_us_at_100qps'), d.get('p99_us_at_100qps')))
+" | tee -a $out
+}
+F="python3 bench.py --skip-64k --skip-grpc --skip-stream --latency-sample-s 4 --steps 20 --warmup 3 --cpu-l3-domain 3"
+full() {
+  run "$@"
+  grep '^{' gpurun_out/sweep_run.log | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); print('lat100: p50=%s p99=%s' % (d.get('p50_us_at_100qps'), d.get('p99_us_at_100qps')))
+" | tee -a $out
+}
 for rep in 1 2; do
-  run "rep$rep w8 l3=0" MRPC_FLAGS="--cpu_l3_domain=0" $B --workers 8
-  run "rep$rep w10 l3=0" MRPC_FLAGS="--cpu_l3_domain=0" $B --workers 10
-  run "rep$rep w12 l3=0" MRPC_FLAGS="--cpu_l3_domain=0" $B --workers 12
-  run "rep$rep w8 l3=0 pinned" MRPC_FLAGS="--cpu_l3_domain=0 --fiber_worker_cpu_offset=0" $B --workers 8
-  run "rep$rep w12 l3=0 pinned" MRPC_FLAGS="--cpu_l3_domain=0 --fiber_worker_cpu_offset=0" $B --workers 12
-  run "rep$rep w8 l3=3 pinned" MRPC_FLAGS="--cpu_l3_domain=3 --fiber_worker_cpu_offset=0" $B --workers 8
+  full "rep$rep base" $F
+  full "rep$rep disp_spin 1s" MRPC_FLAGS="--event_dispatcher_spin_us=1000000" $F
 done
 echo done
