@@ -3,6 +3,7 @@
 // status.h:44), and MultiDimension (labelled families, multi_dimension.h:35).
 #pragma once
 
+
 #include <functional>
 #include <map>
 #include <memory>
@@ -150,55 +151,6 @@ public:
 private:
     mutable std::mutex _mu;
     T _v;
-};
-
-// A labelled family of metrics of type M (e.g. Adder<int64_t>). describe()
-// renders Prometheus lines prefixed with '#' so the Prometheus dumper can
-// forward them verbatim.
-template <typename M>
-class MultiDimension : public Variable {
-public:
-    MultiDimension(const std::string& name, const std::vector<std::string>& labels) : _labels(labels) { expose(name); }
-    ~MultiDimension() { hide(); }
-    M* get_stats(const std::vector<std::string>& label_values) {
-        if (label_values.size() != _labels.size()) return nullptr;
-        std::lock_guard<std::mutex> g(_mu);
-        auto& p = _m[label_values];
-        if (!p) p.reset(new M);
-        return p.get();
-    }
-    bool has_stats(const std::vector<std::string>& lv) const {
-        std::lock_guard<std::mutex> g(_mu);
-        return _m.count(lv) > 0;
-    }
-    void delete_stats(const std::vector<std::string>& lv) {
-        std::lock_guard<std::mutex> g(_mu);
-        _m.erase(lv);
-    }
-    size_t count_stats() const {
-        std::lock_guard<std::mutex> g(_mu);
-        return _m.size();
-    }
-    void describe(std::ostream& os, bool) const override {
-        std::lock_guard<std::mutex> g(_mu);
-        os << "#";
-        for (auto& kv : _m) {
-            os << name() << "{";
-            for (size_t i = 0; i < _labels.size(); ++i) {
-                if (i) os << ",";
-                os << _labels[i] << "=\"" << kv.first[i] << "\"";
-            }
-            double v = 0;
-            kv.second->get_number(&v);
-            os << "} " << v << "\n";
-        }
-    }
-    bool get_number(double*) const override { return false; }
-
-private:
-    std::vector<std::string> _labels;
-    mutable std::mutex _mu;
-    std::map<std::vector<std::string>, std::unique_ptr<M>> _m;
 };
 
 // Registers process-level variables (cpu, memory, fds, io, loadavg, uptime)

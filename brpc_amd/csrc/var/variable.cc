@@ -15,6 +15,7 @@
 #include "base/time.h"
 
 DEFINE_bool(var_dump, false, "periodically dump exposed variables to var_dump_file");
+DEFINE_int64(var_max_multi_dimension_stats_count, 20000, "max label tuples of one MultiDimension family");
 DEFINE_string(var_dump_file, "monitor/mrpc.vars", "file of the periodic dump");
 DEFINE_int32(var_dump_interval, 10, "seconds between dumps");
 DEFINE_string(var_dump_include, "", "only dump variables matching this wildcard list");
