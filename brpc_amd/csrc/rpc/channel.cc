@@ -68,10 +68,13 @@ int Channel::InitChannelOptions(const ChannelOptions* options) {
                                                                                           : CONNECTION_TYPE_POOLED;
     }
     // "ssl:<sni>" in the signature makes SocketMap create TLS client sockets.
-    _map_signature = string_printf("%s|%s|%s|%d%s", _protocol->name, _options.connection_group.c_str(),
+    // Connections are shared only between channels that would talk the same
+    // way: a connection authenticated by one Authenticator must never carry
+    // calls of a channel with another (or none).
+    _map_signature = string_printf("%s|%s|%s|%d%s|auth:%p", _protocol->name, _options.connection_group.c_str(),
                                    _options.use_ssl ? ("ssl:" + _options.ssl_sni).c_str() : "",
                                    _options.use_device_transport ? _options.gpu_device : -2,
-                                   _options.use_rdma ? "|rdma" : "");
+                                   _options.use_rdma ? "|rdma" : "", (const void*)_options.auth);
     if (_options.use_rdma) {
         std::string err;
         if (_options.use_ssl) {
