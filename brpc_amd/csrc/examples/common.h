@@ -4,6 +4,8 @@
 // smoke test). Mirrors the reference's example/* programs.
 #pragma once
 
+#include <execinfo.h>
+#include <signal.h>
 #include <unistd.h>
 
 #include <cstdio>
@@ -54,6 +56,24 @@ struct LocalServer {
     }
     std::string addr() const { return "127.0.0.1:" + std::to_string(server.listen_port()); }
 };
+
+// A crashing demo prints where it crashed (no debugger on the test boxes).
+inline void CrashHandler(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    fprintf(stderr, "*** signal %d, backtrace:\n", sig);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+struct CrashHandlerInstaller {
+    CrashHandlerInstaller() {
+        signal(SIGSEGV, CrashHandler);
+        signal(SIGABRT, CrashHandler);
+        signal(SIGBUS, CrashHandler);
+    }
+};
+static CrashHandlerInstaller g_crash_handler_installer;
 
 inline int Check(bool ok, const char* what) {
     printf("%-48s %s\n", what, ok ? "OK" : "FAILED");

@@ -420,15 +420,20 @@ struct SleepArgs {
 static void ready_to_run_from_timer(void* arg) { ready_to_run_general((fiber_t)(uintptr_t)arg); }
 
 static void add_sleep_event(void* arg) {
-    SleepArgs* e = (SleepArgs*)arg;
+    // `arg` lives on the sleeping fiber's stack: once the timer is armed the
+    // fiber may wake on another worker and return from usleep(), so copy
+    // everything out before scheduling and never touch `arg` afterwards.
+    const SleepArgs e = *(const SleepArgs*)arg;
     TimerThread::TaskId id =
-        get_global_timer_thread()->schedule_after_us(ready_to_run_from_timer, (void*)(uintptr_t)e->tid, e->timeout_us);
+        get_global_timer_thread()->schedule_after_us(ready_to_run_from_timer, (void*)(uintptr_t)e.tid, e.timeout_us);
     if (!id) {
-        tls_group()->ready_to_run(e->tid);
+        tls_group()->ready_to_run(e.tid);
         return;
     }
-    // Publish the timer id so interrupt() can cancel the sleep.
-    e->meta->current_sleep.store(id, std::memory_order_release);
+    // Publish the timer id so interrupt() can cancel the sleep (TaskMeta is
+    // pooled memory, valid even if the fiber already woke; a stale id left
+    // here is harmless: timer ids are versioned).
+    e.meta->current_sleep.store(id, std::memory_order_release);
 }
 
 int TaskGroup::usleep(TaskGroup** pg, uint64_t us) {

@@ -126,6 +126,8 @@ TEST(ParallelChannel, broadcast_merge_map_and_limits) {
         std::atomic<int> fired{0};
         stub.Echo(&cntl, &req, &res, NewCallback([&] { fired.store(1); }));
         cntl.Join();
+        // Join() returns once the call id is gone; done may still be running
+        for (int spin = 0; spin < 2000 && fired.load() == 0; ++spin) usleep(1000);
         EXPECT_EQ(fired.load(), 1);
         EXPECT_FALSE(cntl.Failed());
         EXPECT_EQ(split(res.message()).size(), 3u);
