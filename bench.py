@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--dispatcher-poll-us", type=int, default=1000000,
                     help="event dispatcher busy-polls epoll for this long after the last event before "
                          "sleeping (-event_dispatcher_spin_us; 0: always sleep in epoll_wait)")
+    ap.add_argument("--latency-first", action="store_true",
+                    help="take the 100-QPS latency sample before the throughput legs")
     ap.add_argument("--latency-sample-s", type=float, default=4.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
@@ -203,6 +205,23 @@ def main():
             "step_qps_max": step_qps[-1] if step_qps else 0.0,
         }
 
+    def latency_sample():
+        # rpc_press -qps=100 -thread_num=1 analog: one caller, paced, 32 B
+        if a.latency_sample_s <= 0:
+            return None
+        press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
+                              "connection_type": "single"})
+        parallel.barrier(topo)
+        press.run_for(a.latency_sample_s)
+        st = press.stats()
+        out = {"p50_us": parallel.allreduce_max(st["p50_us"], topo),
+               "p99_us": parallel.allreduce_max(st["p99_us"], topo),
+               "avg_us": parallel.allreduce_max(st["avg_us"], topo)}
+        del press
+        return out
+
+    lat = latency_sample() if a.latency_first else None
+
     wl32 = ECHO_32B
     if a.requests_per_step:
         wl32.requests_per_step = a.requests_per_step
@@ -313,18 +332,8 @@ def main():
               "p99_us": parallel.allreduce_max(st["p99_us"], topo), "fanout": len(others)}
         del press
 
-    lat = None
-    if a.latency_sample_s > 0:
-        press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
-                              "connection_type": "single"})
-        parallel.barrier(topo)
-        press.run_for(a.latency_sample_s)
-        st = press.stats()
-        lat = {"p50_us": parallel.allreduce_max(st["p50_us"], topo),
-               "p99_us": parallel.allreduce_max(st["p99_us"], topo),
-               "avg_us": parallel.allreduce_max(st["avg_us"], topo)}
-        del press
-
+    if not a.latency_first:
+        lat = latency_sample()
     parallel.barrier(topo)
     server.stop()
 

@@ -4,6 +4,7 @@
 #include <sstream>
 
 #include "base/crc32c.h"
+#include "base/flags.h"
 #include "base/logging.h"
 #include "base/time.h"
 #include "base/util.h"
@@ -20,8 +21,28 @@
 #include "rpc/controller.h"
 #include "rpc/errno.h"
 
+DEFINE_int32(press_slow_trace_us, 0,
+             "record start time and latency of calls at least this slow (0: off; SlowCalls() returns them)");
+
 namespace mrpc {
 namespace press {
+
+namespace {
+std::mutex g_slow_mu;
+std::vector<std::pair<int64_t, int64_t>> g_slow;  // (monotonic start us, latency us)
+}  // namespace
+
+void RecordSlowCall(int64_t t0_us, int64_t lat_us) {
+    std::lock_guard<std::mutex> g(g_slow_mu);
+    if (g_slow.size() < 100000) g_slow.emplace_back(t0_us, lat_us);
+}
+
+std::vector<std::pair<int64_t, int64_t>> TakeSlowCalls() {
+    std::lock_guard<std::mutex> g(g_slow_mu);
+    std::vector<std::pair<int64_t, int64_t>> out;
+    out.swap(g_slow);
+    return out;
+}
 
 // Per-worker state. Each worker owns its histograms; the lock is only
 // contended when the 1-second ticker swaps the interval histogram out.
@@ -289,6 +310,7 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
 
 void PressSession::finish(PressCall* call) {
     const int64_t lat = monotonic_us() - call->t0;
+    if (FLAGS_press_slow_trace_us > 0 && lat >= FLAGS_press_slow_trace_us) RecordSlowCall(call->t0, lat);
     Controller& cntl = call->cntl;
     bool ok = !cntl.Failed();
     if (ok && call->check && !_method) {

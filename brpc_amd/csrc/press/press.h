@@ -132,5 +132,10 @@ private:
 // Formats the latency table the way rpc_press prints it.
 std::string FormatLatencyTable(const Snapshot& s);
 
+// Diagnostics: calls slower than -press_slow_trace_us, as (monotonic start
+// us, latency us); taking them clears the list.
+void RecordSlowCall(int64_t t0_us, int64_t lat_us);
+std::vector<std::pair<int64_t, int64_t>> TakeSlowCalls();
+
 }  // namespace press
 }  // namespace mrpc

@@ -17,6 +17,7 @@
 #include "gpu/snappy_offload.h"
 #include "gpu/xgmi.h"
 #include "mrpc/proto/echo.pb.h"
+#include "base/time.h"
 #include "press/press.h"
 #include "press/stream_press.h"
 #include "rpc/channel.h"
@@ -275,6 +276,8 @@ PYBIND11_MODULE(_native, m) {
         return v;
     });
     // rpcz: recent spans (memory), spans by trace id / end time (disk store)
+    m.def("press_slow_calls", [] { return press::TakeSlowCalls(); });
+    m.def("monotonic_us", [] { return monotonic_us(); });
     m.def("rpcz_recent", [](size_t max) { return ListRecentSpans(max, 0); }, py::arg("max") = 100);
     m.def("rpcz_trace", [](uint64_t trace, size_t max) { return span_db::FindTrace(trace, max); },
           py::arg("trace_id"), py::arg("max") = 100, py::call_guard<py::gil_scoped_release>());

@@ -35,7 +35,7 @@ for l in sys.stdin:
     d=json.loads(l); print('lat100: p50=%s p99=%s' % (d.get('p50_us_at_100qps'), d.get('p99_us_at_100qps')))
 " | tee -a $out
 }
-F="python3 bench.py --skip-64k --skip-grpc --skip-stream --latency-sample-s 4 --steps 20 --warmup 3 --cpu-l3-domain 3"
+F="python3 bench.py --skip-64k --skip-grpc --skip-stream --latency-sample-s 6 --steps 20 --warmup 3"
 full() {
   run "$@"
   grep '^{' gpurun_out/sweep_run.log | python3 -c "
@@ -45,7 +45,8 @@ for l in sys.stdin:
 " | tee -a $out
 }
 for rep in 1 2; do
-  full "rep$rep base" $F
-  full "rep$rep disp_spin 1s" MRPC_FLAGS="--event_dispatcher_spin_us=1000000" $F
+  full "rep$rep default" $F
+  full "rep$rep latency-first" $F --latency-first
+  full "rep$rep l3=3" $F --cpu-l3-domain 3
 done
 echo done
