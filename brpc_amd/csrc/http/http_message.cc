@@ -122,7 +122,11 @@ bool HttpParser::parse_head(const std::string& head, std::string* error) {
             if (line.compare(0, 5, "HTTP/") == 0) {
                 // HTTP/1.1 200 OK
                 _msg->is_response = true;
-                if (line.size() < 12 || line[6] != '.' || line[8] != ' ') {
+                // RFC 9112: status-code = 3DIGIT, followed by SP or end of line
+                if (line.size() < 12 || line[6] != '.' || line[8] != ' ' || !isdigit((unsigned char)line[5]) ||
+                    !isdigit((unsigned char)line[7]) || !isdigit((unsigned char)line[9]) ||
+                    !isdigit((unsigned char)line[10]) || !isdigit((unsigned char)line[11]) ||
+                    (line.size() > 12 && line[12] != ' ') || line[9] == '0') {
                     *error = "bad status line: " + line;
                     return false;
                 }
