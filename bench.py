@@ -61,7 +61,7 @@ def parse():
                          "sleeping (-event_dispatcher_spin_us; 0: always sleep in epoll_wait)")
     ap.add_argument("--latency-first", action="store_true",
                     help="take the 100-QPS latency sample before the throughput legs")
-    ap.add_argument("--latency-sample-s", type=float, default=4.0,
+    ap.add_argument("--latency-sample-s", type=float, default=6.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
 
@@ -212,6 +212,8 @@ def main():
         press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
                               "connection_type": "single"})
         parallel.barrier(topo)
+        press.run_for(0.5)  # warm-up: the first calls of a connection pay lazy setup
+        press.reset_stats()
         press.run_for(a.latency_sample_s)
         st = press.stats()
         out = {"p50_us": parallel.allreduce_max(st["p50_us"], topo),
