@@ -334,6 +334,62 @@ def main():
               "p99_us": parallel.allreduce_max(st["p99_us"], topo), "fanout": len(others)}
         del press
 
+    # Scatter leg (TP analog): the 64 KiB HBM attachment is split across the
+    # servers of all other ranks (one slice per peer GPU over xGMI) and the
+    # echoed slices are gathered back in order.
+    rt = None
+    if topo.world_size > 1 and not a.skip_fanout:
+        others = [x for i, x in enumerate(addrs) if i != topo.rank]
+        so = ECHO_64KB.press_options(peer, gpu_device=topo.device)
+        so.update({"fanout_servers": ",".join(others), "scatter": True, "concurrency": 16,
+                   "device_attachment": bool(cuda), "attachment_size": 65536 * len(others)})
+        press = native.Press(so)
+        nf = max(1, a.requests_per_step_fanout)
+        for _ in range(a.warmup):
+            press.run_requests(nf)
+        press.reset_stats()
+        parallel.barrier(topo)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            press.run_requests(nf)
+        parallel.barrier(topo)
+        sync()
+        dt = time.perf_counter() - t0
+        st = press.stats()
+        dt_max = parallel.allreduce_max(dt, topo)
+        rt = {"gbps": parallel.allreduce_sum(st["bytes"], topo) / dt_max / 1e9 if dt_max > 0 else 0.0,
+              "errors": int(parallel.allreduce_sum(st["error"], topo)),
+              "p99_us": parallel.allreduce_max(st["p99_us"], topo)}
+        del press
+
+    # Routing leg (EP analog): every call carries a key; a consistent-hash
+    # balancer over the servers of ALL ranks sends it to the rank owning the
+    # key's shard, with a 64 KiB HBM attachment (xGMI to remote ranks).
+    rr = None
+    if topo.world_size > 1 and not a.skip_fanout:
+        ro = ECHO_64KB.press_options("list://" + ",".join(addrs), gpu_device=topo.device)
+        ro.update({"lb_policy": "c_murmurhash", "concurrency": a.concurrency, "device_attachment": bool(cuda)})
+        press = native.Press(ro)
+        nf = max(1, a.requests_per_step_fanout) * 4
+        for _ in range(a.warmup):
+            press.run_requests(nf)
+        press.reset_stats()
+        parallel.barrier(topo)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            press.run_requests(nf)
+        parallel.barrier(topo)
+        sync()
+        dt = time.perf_counter() - t0
+        st = press.stats()
+        dt_max = parallel.allreduce_max(dt, topo)
+        rr = {"qps": parallel.allreduce_sum(st["success"], topo) / dt_max if dt_max > 0 else 0.0,
+              "errors": int(parallel.allreduce_sum(st["error"], topo)),
+              "p99_us": parallel.allreduce_max(st["p99_us"], topo)}
+        del press
+
     if not a.latency_first:
         lat = latency_sample()
     parallel.barrier(topo)
@@ -407,6 +463,14 @@ def main():
             out["fanout_p99_us"] = rf["p99_us"]
             out["fanout_errors"] = rf["errors"]
             out["fanout_peers_per_rank"] = rf["fanout"]
+        if rr:
+            out["route_calls_per_s"] = round(rr["qps"], 1)
+            out["route_p99_us"] = rr["p99_us"]
+            out["route_errors"] = rr["errors"]
+        if rt:
+            out["scatter_gbytes_per_s"] = round(rt["gbps"], 3)
+            out["scatter_p99_us"] = rt["p99_us"]
+            out["scatter_errors"] = rt["errors"]
         if lat:
             out["p99_us_at_100qps"] = lat["p99_us"]
             out["p50_us_at_100qps"] = lat["p50_us"]

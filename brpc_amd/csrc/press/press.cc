@@ -168,6 +168,8 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
         po.timeout_ms = _opt.timeout_ms;
         std::unique_ptr<ParallelChannel> pc(new ParallelChannel);
         pc->Init(&po);
+        std::shared_ptr<CallMapper> mapper;
+        if (_opt.scatter) mapper = std::make_shared<ScatterAttachmentMapper>();
         copt.connection_group = _opt.num_channels > 1 ? "press" + std::to_string(i) : std::string();
         for (const std::string& f : fan) {
             std::unique_ptr<Channel> sub(new Channel);
@@ -175,7 +177,7 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
                 *error = "fail to init channel to " + f;
                 return -1;
             }
-            pc->AddChannel(sub.release(), OWNS_CHANNEL, nullptr, nullptr);
+            pc->AddChannel(sub.release(), OWNS_CHANNEL, mapper, nullptr);
         }
         _channels.push_back(std::move(pc));
     }
@@ -285,6 +287,9 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     Controller& cntl = call->cntl;
     if (_opt.request_compress_type) cntl.set_request_compress_type((CompressType)_opt.request_compress_type);
     if (_opt.response_compress_type) cntl.set_response_compress_type((CompressType)_opt.response_compress_type);
+    // with a load balancer the sequence number is the routing key
+    // (consistent-hash balancers send a key to the server owning its shard)
+    if (!_opt.lb_policy.empty()) cntl.set_request_code((uint64_t)seq * 0x9E3779B97F4A7C15ull);
     call->s = this;
     call->w = w;
     call->t0 = monotonic_us();
@@ -302,7 +307,8 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     } else if (!_attachment.empty()) {
         cntl.request_attachment().append(_attachment);
     }
-    call->nbytes = 2 * (int64_t)(_echo_message.size() + _attachment.size()) * _fanout;
+    call->nbytes = _opt.scatter ? 2 * (int64_t)(_echo_message.size() * _fanout + _attachment.size())
+                                : 2 * (int64_t)(_echo_message.size() + _attachment.size()) * _fanout;
     call->check = _opt.check_echo;
     example::EchoService_Stub stub(ch);
     stub.Echo(&cntl, &call->echo_req, &call->echo_res, done);
@@ -319,7 +325,11 @@ void PressSession::finish(PressCall* call) {
             cntl.SetFailed(ERESPONSE, "echoed message mismatch");
         } else if (!_attachment.empty()) {
             std::string got, want;
-            for (int k = 0; k < _fanout; ++k) want += _attachment;  // gathered in channel order
+            if (_opt.scatter) {
+                want = _attachment;  // slices gathered back in channel order
+            } else {
+                for (int k = 0; k < _fanout; ++k) want += _attachment;  // gathered in channel order
+            }
             if (gpu::CopyBufToHost(cntl.response_attachment(), &got) != 0 || got != want) {
                 ok = false;
                 cntl.SetFailed(ERESPONSE, "echoed attachment mismatch (%zu bytes)", got.size());

@@ -59,6 +59,10 @@ struct PressOptions {
     // xGMI-direct channels to the peer GPUs — and the echoed attachments are
     // gathered. Empty: plain calls to `server`.
     std::string fanout_servers;
+    // With fanout_servers: scatter instead of broadcast — server i gets the
+    // i-th slice of the attachment (ScatterAttachmentMapper, the TP analog)
+    // and the echoed slices are gathered back in order.
+    bool scatter = false;
     // generic workload (dynamic messages)
     std::string proto_file;    // .proto path
     std::string include_paths; // ';' separated

@@ -143,6 +143,7 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "gpu_device") o.gpu_device = v.cast<int>();
         else if (k == "check_echo") o.check_echo = v.cast<bool>();
         else if (k == "fanout_servers") o.fanout_servers = v.cast<std::string>();
+        else if (k == "scatter") o.scatter = v.cast<bool>();
         else if (k == "gpu_process") o.gpu_process = v.cast<bool>();
         else if (k == "use_rdma") o.use_rdma = v.cast<bool>();
         else if (k == "proto_file") o.proto_file = v.cast<std::string>();

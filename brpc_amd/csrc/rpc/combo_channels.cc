@@ -241,9 +241,14 @@ void ParallelChannel::CallMethod(const pb::MethodDescriptor* method, RpcControll
         s->cntl.set_timeout_ms(timeout_ms);
         if (cntl->log_id()) s->cntl.set_log_id(cntl->log_id());
         if (cntl->has_request_code()) s->cntl.set_request_code(cntl->request_code());
-        // every sub call carries the attachment (shared blocks, no copy;
-        // reference parallel_channel.cpp:683-684)
-        s->cntl.request_attachment().append(cntl->request_attachment());
+        // every sub call carries the attachment, or the mapper's slice of it
+        // (shared blocks, no copy; reference parallel_channel.cpp:683-684)
+        if (_subs[s->index].mapper) {
+            _subs[s->index].mapper->MapAttachment(s->index, (int)_subs.size(), cntl->request_attachment(),
+                                                  &s->cntl.request_attachment());
+        } else {
+            s->cntl.request_attachment().append(cntl->request_attachment());
+        }
         to_launch.push_back(s.get());
     }
     const fiber::CallId cid = pc->cid;

@@ -51,6 +51,35 @@ public:
     virtual ~CallMapper() {}
     virtual SubCall Map(int channel_index, int channel_count, const pb::MethodDescriptor* method,
                         const pb::Message* request, pb::Message* response) = 0;
+    // The part of the parent's request attachment sub call `channel_index`
+    // carries. Default: all of it (broadcast). `out` shares the blocks — a
+    // slice of an HBM attachment is lent to its peer GPU without a copy.
+    virtual void MapAttachment(int channel_index, int channel_count, const Buf& attachment, Buf* out) {
+        (void)channel_index;
+        (void)channel_count;
+        out->append(attachment);
+    }
+};
+
+// Tensor-parallel style scatter (SURVEY §2.10 TP analog): every sub call
+// gets the same request message and the channel_index-th of channel_count
+// near-equal contiguous slices of the attachment; the default merge
+// appends the sub responses' attachments in channel order, so an echo
+// service gathers the original attachment back.
+class ScatterAttachmentMapper : public CallMapper {
+public:
+    SubCall Map(int, int, const pb::MethodDescriptor* method, const pb::Message* request,
+                pb::Message* response) override {
+        return SubCall(method, request, response ? response->New() : nullptr, SubCall::DELETE_RESPONSE);
+    }
+    void MapAttachment(int i, int n, const Buf& attachment, Buf* out) override {
+        const size_t total = attachment.size();
+        const size_t begin = total * (size_t)i / (size_t)n, end = total * (size_t)(i + 1) / (size_t)n;
+        Buf view(attachment);  // shares blocks
+        view.pop_back(total - end);
+        view.pop_front(begin);
+        out->append(std::move(view));
+    }
 };
 
 class ResponseMerger {

@@ -45,3 +45,5 @@ def test_bench_two_ranks_gloo():
     # multi-rank legs: stream fan-out to the other rank, ParallelChannel fan-out
     assert j["stream_fanout_per_rank"] == 1 and j["stream_gbytes_per_s_64KB_chunks"] > 0
     assert j["fanout_peers_per_rank"] == 1 and j["fanout_errors"] == 0 and j["fanout_gbytes_per_s"] > 0
+    assert j["scatter_errors"] == 0 and j["scatter_gbytes_per_s"] > 0
+    assert j["route_errors"] == 0 and j["route_calls_per_s"] > 0

@@ -49,3 +49,39 @@ def test_gpu_process_without_gpu_fails_cleanly(native):
         assert st["error"] == 4 and "GPU" in st["last_error"], st
     finally:
         s.stop()
+
+
+def test_parallel_channel_scatter_gather(native):
+    """TP analog: each server echoes its slice of the attachment; the
+    gathered response is the original attachment (checked by the press)."""
+    servers = [start_echo_server("127.0.0.1:0") for _ in range(3)]
+    try:
+        p = native.Press({"server": servers[0].address,
+                          "fanout_servers": ",".join(s.address for s in servers), "scatter": True,
+                          "concurrency": 8, "attachment_size": 65536, "check_echo": True})
+        p.run_requests(200)
+        st = p.stats()
+        assert st["success"] == 200 and st["error"] == 0, st
+        assert [s.echo_calls for s in servers] == [200, 200, 200]
+        # bytes = 2 directions x (3 messages + one attachment in slices)
+        assert st["bytes"] == 200 * 2 * (32 * 3 + 65536), st
+    finally:
+        for s in servers:
+            s.stop()
+
+
+def test_consistent_hash_routing_spreads_keys(native):
+    """EP analog: every call carries a routing key; c_murmurhash sends each
+    key to the server owning its shard, keys spread over all servers."""
+    servers = [start_echo_server("127.0.0.1:0") for _ in range(4)]
+    try:
+        p = native.Press({"server": "list://" + ",".join(s.address for s in servers), "lb_policy": "c_murmurhash",
+                          "concurrency": 4, "attachment_size": 1024, "check_echo": True})
+        p.run_requests(800)
+        st = p.stats()
+        assert st["success"] == 800 and st["error"] == 0, st
+        calls = [s.echo_calls for s in servers]
+        assert sum(calls) == 800 and min(calls) > 800 // 16, calls
+    finally:
+        for s in servers:
+            s.stop()

@@ -295,6 +295,47 @@ def test_fanout_device_attachment(dev):
             s.stop()
 
 
+def test_scatter_device_attachment(dev):
+    """TP analog over xGMI: each peer is lent only its (unaligned) slice of
+    the HBM attachment and echoes it; the gathered slices are the original."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    servers = [start_echo_server("127.0.0.1:0", gpu_device=0) for _ in range(3)]
+    try:
+        p = native.Press({"server": servers[0].address, "fanout_servers": ",".join(s.address for s in servers),
+                          "scatter": True, "concurrency": 8, "attachment_size": 65536 + 7,
+                          "device_attachment": True, "gpu_device": 0, "check_echo": True})
+        p.run_requests(300)
+        st = p.stats()
+        assert st["success"] == 300 and st["error"] == 0, st
+        assert [s.echo_calls for s in servers] == [300, 300, 300]
+        assert _drain_lent(native)["lent_outstanding"] == 0
+    finally:
+        for s in servers:
+            s.stop()
+
+
+def test_route_device_attachment_by_key(dev):
+    """EP analog: keyed calls routed by c_murmurhash to the owning server,
+    HBM attachments lent over the transport to whichever server owns the key."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    servers = [start_echo_server("127.0.0.1:0", gpu_device=0) for _ in range(4)]
+    try:
+        p = native.Press({"server": "list://" + ",".join(s.address for s in servers), "lb_policy": "c_murmurhash",
+                          "concurrency": 16, "attachment_size": 65536, "device_attachment": True,
+                          "gpu_device": 0, "check_echo": True})
+        p.run_requests(800)
+        st = p.stats()
+        assert st["success"] == 800 and st["error"] == 0, st
+        calls = [s.echo_calls for s in servers]
+        assert sum(calls) == 800 and min(calls) > 0, calls
+        assert _drain_lent(native)["lent_outstanding"] == 0
+    finally:
+        for s in servers:
+            s.stop()
+
+
 @pytest.mark.parametrize("device_attachment", [False, True])
 def test_gpu_process_echo_handler(dev, device_attachment):
     """the handler gathers the attachment into HBM with the
