@@ -18,6 +18,7 @@
 #include "rpc/errno.h"
 #include "rpc/protocol.h"
 #include "rpc/server.h"
+#include "rtmp/handshake.h"
 
 DECLARE_uint64(max_body_size);
 
@@ -34,6 +35,8 @@ static const uint32_t kAudioCsid = 4;
 static const uint32_t kDataCsid = 5;
 static const uint32_t kVideoCsid = 6;
 static const uint32_t kControlCsid = 2;
+
+std::atomic<int64_t> g_complex_handshakes{0}, g_unsigned_c2{0};
 
 static void be24(std::string* o, uint32_t v) {
     o->push_back((char)(v >> 16));
@@ -196,7 +199,12 @@ public:
 
     // Parse: consumes handshake bytes and complete messages, dispatching
     // each in order. Returns false on a protocol error.
-    bool Consume(Buf* source, Socket* sock, const Server* server);
+    bool Consume(Buf* source, Socket* sock, const Server* server) {
+        const size_t before = source->size();
+        const bool ok = ConsumeImpl(source, sock, server);
+        if (ok) OnBytesReceived(before - source->size());
+        return ok;
+    }
 
     // client-side hooks
     typedef std::function<void(const std::vector<AMFValue>& args)> StatusFn;
@@ -215,19 +223,44 @@ public:
         _out_chunk_size = n;
     }
     RtmpConnectRequest connect_req;
+    // handshake: set by the client when it offered a complex C1
+    std::string c1_digest;
+    bool complex_handshake = false;  // both sides signed the handshake
+    int64_t acks_sent = 0, pings_answered = 0;
+    std::function<void()> on_pong;  // guarded by _mu
+    void SetPongCallback(std::function<void()> fn) {
+        std::lock_guard<std::mutex> g(_mu);
+        on_pong = std::move(fn);
+    }
 
 private:
     struct StreamEntry {
         RtmpStreamBase* s;
         bool owned;
     };
+    bool ConsumeImpl(Buf* source, Socket* sock, const Server* server);
     bool OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& body, const Server* server);
+    // Acknowledgement (type 3) after every `peer window` bytes received.
+    void OnBytesReceived(size_t n) {
+        if (!n || _state != ESTABLISHED) return;
+        _bytes_in += n;
+        if (_peer_window && _bytes_in - _last_ack_at >= _peer_window) {
+            _last_ack_at = _bytes_in;
+            std::string p;
+            be32(&p, (uint32_t)_bytes_in);  // sequence number wraps at 2^32
+            SendControl(RTMP_ACK, p);
+            ++acks_sent;
+        }
+    }
     bool OnCommand(uint32_t stream_id, const std::vector<AMFValue>& v, const Server* server);
     void ReplyStatus(uint32_t stream_id, const char* level, const char* code, const std::string& desc);
 
     const bool _server;
     const SocketId _sid;
     State _state;
+    std::string _s1_digest;  // server: digest of the S1 we sent
+    uint64_t _bytes_in = 0, _last_ack_at = 0;
+    uint32_t _peer_window = 0;  // from the peer's Window Acknowledgement Size
     uint32_t _in_chunk_size = kDefaultChunkSize;
     uint32_t _out_chunk_size = kDefaultChunkSize;
     std::map<uint32_t, ChunkState> _chunks;
@@ -241,20 +274,35 @@ private:
     bool _closed = false;
 };
 
-bool Connection::Consume(Buf* source, Socket* sock, const Server* server) {
+bool Connection::ConsumeImpl(Buf* source, Socket* sock, const Server* server) {
     for (;;) {
         if (_state == HS_WAIT_C0C1) {
             if (source->size() < 1 + kHandshakeSize) return true;
             std::string c0c1;
             source->cutn(&c0c1, 1 + kHandshakeSize);
             if (c0c1[0] != 3) return false;
-            // S0 + S1 (time, zero, random) + S2 (echo of C1)
-            std::string s;
-            s.push_back(3);
-            be32(&s, (uint32_t)(monotonic_us() / 1000));
-            be32(&s, 0);
-            for (size_t i = 8; i < kHandshakeSize; ++i) s.push_back((char)fast_rand());
-            s.append(c0c1, 1, kHandshakeSize);
+            const std::string c1 = c0c1.substr(1);
+            std::string s(1, (char)3);
+            std::string c1_digest;
+            rtmp::HandshakeSchema schema = rtmp::kSchemaInvalid;
+            if (rtmp::OffersComplexHandshake(c1)) schema = rtmp::ValidateComplexC1(c1, &c1_digest);
+            if (schema != rtmp::kSchemaInvalid) {
+                // complex: S1 with our digest in the client's schema, S2 keyed by its digest
+                std::string s1, s2;
+                rtmp::MakeComplexS1(schema, &s1);
+                rtmp::ValidateComplexS1(s1, &_s1_digest);
+                rtmp::MakeComplexS2(c1_digest, &s2);
+                s += s1;
+                s += s2;
+                complex_handshake = true;
+                g_complex_handshakes.fetch_add(1, std::memory_order_relaxed);
+            } else {
+                // simple: S1 (time, zero, random) + S2 (echo of C1)
+                be32(&s, (uint32_t)(monotonic_us() / 1000));
+                be32(&s, 0);
+                for (size_t i = 8; i < kHandshakeSize; ++i) s.push_back((char)fast_rand());
+                s.append(c1);
+            }
             Buf out(s);
             if (Write(&out) != 0) return false;
             _state = HS_WAIT_C2;
@@ -262,7 +310,14 @@ bool Connection::Consume(Buf* source, Socket* sock, const Server* server) {
         }
         if (_state == HS_WAIT_C2) {
             if (source->size() < kHandshakeSize) return true;
-            source->pop_front(kHandshakeSize);
+            if (complex_handshake) {
+                std::string c2;
+                source->cutn(&c2, kHandshakeSize);
+                // some encoders echo S1 instead of signing it: accept, but count
+                if (!rtmp::ValidateComplexC2(c2, _s1_digest)) g_unsigned_c2.fetch_add(1, std::memory_order_relaxed);
+            } else {
+                source->pop_front(kHandshakeSize);
+            }
             _state = ESTABLISHED;
             continue;
         }
@@ -271,8 +326,19 @@ bool Connection::Consume(Buf* source, Socket* sock, const Server* server) {
             std::string s0s1s2;
             source->cutn(&s0s1s2, 1 + 2 * kHandshakeSize);
             if (s0s1s2[0] != 3) return false;
-            Buf c2(s0s1s2.substr(1, kHandshakeSize));  // echo S1
-            if (Write(&c2) != 0) return false;
+            const std::string s1 = s0s1s2.substr(1, kHandshakeSize), s2 = s0s1s2.substr(1 + kHandshakeSize);
+            std::string s1_digest, c2;
+            if (!c1_digest.empty() && rtmp::OffersComplexHandshake(s1) &&
+                rtmp::ValidateComplexS1(s1, &s1_digest) != rtmp::kSchemaInvalid) {
+                // the server signed S1 and S2 (our C1 digest): answer with a signed C2
+                complex_handshake = rtmp::ValidateComplexS2(s2, c1_digest);
+                if (!complex_handshake) return false;  // a server that signs S1 must sign S2
+                rtmp::MakeComplexC2(s1_digest, &c2);
+            } else {
+                c2 = s1;  // simple: echo S1
+            }
+            Buf c2buf(c2);
+            if (Write(&c2buf) != 0) return false;
             _state = ESTABLISHED;
             if (on_handshake_done) on_handshake_done();
             continue;
@@ -374,10 +440,42 @@ bool Connection::OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& b
         if (body.copy_to(b, 4) == 4) _chunks.erase(rd32(b));
         return true;
     }
+    case RTMP_WINDOW_ACK_SIZE: {
+        uint8_t b[4];
+        if (body.copy_to(b, 4) == 4) _peer_window = rd32(b);
+        return true;
+    }
+    case RTMP_USER_CONTROL: {
+        uint8_t b[6];
+        if (body.copy_to(b, 6) == 6 && ((b[0] << 8) | b[1]) == 7) {  // PingResponse to our Ping()
+            std::function<void()> fn;
+            {
+                std::lock_guard<std::mutex> g(_mu);
+                fn.swap(on_pong);
+            }
+            if (fn) fn();
+            return true;
+        }
+        if (body.copy_to(b, 6) == 6 && ((b[0] << 8) | b[1]) == 6) {  // PingRequest -> PingResponse
+            std::string p;
+            p.push_back(0);
+            p.push_back(7);
+            p.append((const char*)b + 2, 4);
+            SendControl(RTMP_USER_CONTROL, p);
+            ++pings_answered;
+        }
+        return true;
+    }
     case RTMP_ACK:
-    case RTMP_USER_CONTROL:
-    case RTMP_WINDOW_ACK_SIZE:
     case RTMP_SET_PEER_BANDWIDTH: return true;
+    case RTMP_COMMAND_AMF3:
+    case RTMP_DATA_AMF3: {
+        // AMF3 messages of encoders carry a 0 format byte and AMF0 values
+        uint8_t f = 1;
+        if (body.copy_to(&f, 1) != 1 || f != 0) return true;  // true AMF3 payloads are ignored
+        body.pop_front(1);
+        return OnMessage(type == RTMP_COMMAND_AMF3 ? RTMP_COMMAND_AMF0 : RTMP_DATA_AMF0, ts, stream_id, body, server);
+    }
     case RTMP_COMMAND_AMF0: {
         const std::string s = body.to_string();
         std::vector<AMFValue> v;
@@ -700,11 +798,17 @@ int RtmpClient::Init(const char* server_addr_and_port, const RtmpClientOptions& 
     std::shared_ptr<Waiter> hs = std::make_shared<Waiter>();
     conn->on_handshake_done = [hs] { hs->ev.signal(); };
     // C0 + C1
-    std::string c;
-    c.push_back(3);
-    rtmp_detail::be32(&c, (uint32_t)(monotonic_us() / 1000));
-    rtmp_detail::be32(&c, 0);
-    for (size_t i = 8; i < rtmp_detail::kHandshakeSize; ++i) c.push_back((char)fast_rand());
+    std::string c(1, (char)3);
+    if (_options.complex_handshake) {
+        std::string c1;
+        rtmp::MakeComplexC1(rtmp::kSchema1, &c1);
+        rtmp::ValidateComplexC1(c1, &conn->c1_digest);
+        c += c1;
+    } else {
+        rtmp_detail::be32(&c, (uint32_t)(monotonic_us() / 1000));
+        rtmp_detail::be32(&c, 0);
+        for (size_t i = 8; i < rtmp_detail::kHandshakeSize; ++i) c.push_back((char)fast_rand());
+    }
     Buf out(c);
     if (conn->Write(&out) != 0 || !hs->Wait(_options.timeout_ms)) {
         sock->SetFailed(ETIMEDOUT, "rtmp handshake failed");
@@ -908,4 +1012,34 @@ int FlvReader::Read(RtmpMetaData* md, std::string* name) {
     return 0;
 }
 
+}  // namespace mrpc
+
+namespace mrpc {
+bool RtmpClient::complex_handshake_done() const { return _conn && _conn->complex_handshake; }
+int64_t RtmpClient::acks_sent() const { return _conn ? _conn->acks_sent : 0; }
+
+int64_t RtmpClient::Ping(int timeout_ms) {
+    if (!_conn) return -1;
+    struct Pong {
+        fiber::CountdownEvent ev{1};
+    };
+    std::shared_ptr<Pong> w = std::make_shared<Pong>();
+    _conn->SetPongCallback([w] { w->ev.signal(); });
+    const int64_t t0 = monotonic_us();
+    std::string p;
+    p.push_back(0);
+    p.push_back(6);  // PingRequest
+    rtmp_detail::be32(&p, (uint32_t)(t0 / 1000));
+    if (_conn->SendControl(RTMP_USER_CONTROL, p) != 0) return -1;
+    timespec ts = realtime_after_us((int64_t)timeout_ms * 1000);
+    if (w->ev.timed_wait(&ts) != 0) {
+        _conn->SetPongCallback(nullptr);
+        return -1;
+    }
+    return monotonic_us() - t0;
+}
+namespace rtmp {
+int64_t ComplexHandshakesServed() { return rtmp_detail::g_complex_handshakes.load(std::memory_order_relaxed); }
+int64_t UnsignedC2Count() { return rtmp_detail::g_unsigned_c2.load(std::memory_order_relaxed); }
+}  // namespace rtmp
 }  // namespace mrpc

@@ -6,13 +6,17 @@
 // callbacks. Client: RtmpClient owns a connection (handshake + connect),
 // RtmpClientStreams multiplex on it (createStream + play/publish).
 //
-// Wire: simple RTMP handshake (C0/C1/C2 - S0/S1/S2), chunk streams with
+// Wire: simple or digest ("complex", rtmp/handshake.h) handshake, chunk streams with
 // format 0-3 headers, extended timestamps and negotiated chunk sizes, AMF0
 // commands (connect/createStream/play/publish/deleteStream/onStatus),
 // audio/video/data messages. Incoming messages of a connection are
 // dispatched in order on the connection's read fiber.
 //
 // FlvWriter/FlvReader convert between RTMP messages and FLV tags.
+//
+// Servers also acknowledge received bytes per the peer's window
+// (Acknowledgement after every window-ack-size bytes), answer user-control
+// pings, and accept AMF3-wrapped commands/data (types 17/15).
 #pragma once
 
 #include <atomic>
@@ -39,6 +43,8 @@ enum RtmpMessageType : uint8_t {
     RTMP_SET_PEER_BANDWIDTH = 6,
     RTMP_AUDIO = 8,
     RTMP_VIDEO = 9,
+    RTMP_DATA_AMF3 = 15,
+    RTMP_COMMAND_AMF3 = 17,
     RTMP_DATA_AMF0 = 18,
     RTMP_COMMAND_AMF0 = 20,
 };
@@ -125,6 +131,9 @@ struct RtmpClientOptions {
     int timeout_ms = 1000;          // connect / createStream / play / publish
     uint32_t chunk_size = 60000;    // announced with SetChunkSize
     uint32_t window_ack_size = 2500000;
+    // Offer the digest ("complex") handshake; servers that do not sign
+    // their S1 fall back to the simple one.
+    bool complex_handshake = false;
 };
 
 class RtmpClient {
@@ -136,6 +145,12 @@ public:
     bool initialized() const { return (bool)_conn; }
     const RtmpClientOptions& options() const { return _options; }
     std::shared_ptr<rtmp_detail::Connection> connection() const { return _conn; }
+    // Both sides signed the handshake (complex_handshake offered and accepted).
+    bool complex_handshake_done() const;
+    // User-control PingRequest; the round trip in microseconds, -1 on timeout.
+    int64_t Ping(int timeout_ms = 1000);
+    // Acknowledgements this connection sent for the server's window.
+    int64_t acks_sent() const;
 
 private:
     RtmpClientOptions _options;
@@ -185,5 +200,12 @@ private:
     Buf* _in;
     bool _read_header = false;
 };
+
+namespace rtmp {
+// Server-side handshake counters (tests, /vars): complex handshakes served,
+// and clients whose C2 was not signed.
+int64_t ComplexHandshakesServed();
+int64_t UnsignedC2Count();
+}  // namespace rtmp
 
 }  // namespace mrpc

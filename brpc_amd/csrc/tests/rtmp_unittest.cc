@@ -12,6 +12,7 @@
 
 #include "base/time.h"
 #include "rpc/server.h"
+#include "rtmp/handshake.h"
 #include "rtmp/rtmp.h"
 #include "tests/test.h"
 
@@ -237,4 +238,78 @@ TEST(Rtmp, live_relay_publish_and_play) {
     const int64_t d2 = monotonic_us() + 3000000;
     while (svc.stopped.load() < 3 && monotonic_us() < d2) usleep(2000);
     EXPECT_GE(svc.stopped.load(), 3);
+}
+
+TEST(Rtmp, complex_handshake_digests) {
+    for (rtmp::HandshakeSchema schema : {rtmp::kSchema0, rtmp::kSchema1}) {
+        std::string c1, s1, d1, ds, s2, c2;
+        rtmp::MakeComplexC1(schema, &c1);
+        ASSERT_EQ(c1.size(), rtmp::kRtmpHandshakeSize);
+        EXPECT_TRUE(rtmp::OffersComplexHandshake(c1));
+        EXPECT_EQ(rtmp::ValidateComplexC1(c1, &d1), schema);
+        EXPECT_EQ(d1.size(), 32u);
+        EXPECT_EQ(rtmp::ValidateComplexS1(c1, nullptr), rtmp::kSchemaInvalid);  // player key != server key
+        std::string bad = c1;
+        bad[100] ^= 1;
+        EXPECT_EQ(rtmp::ValidateComplexC1(bad, nullptr), rtmp::kSchemaInvalid);
+        rtmp::MakeComplexS1(schema, &s1);
+        EXPECT_EQ(rtmp::ValidateComplexS1(s1, &ds), schema);
+        rtmp::MakeComplexS2(d1, &s2);
+        EXPECT_TRUE(rtmp::ValidateComplexS2(s2, d1));
+        EXPECT_FALSE(rtmp::ValidateComplexS2(s2, ds));  // bound to the client's digest
+        rtmp::MakeComplexC2(ds, &c2);
+        EXPECT_TRUE(rtmp::ValidateComplexC2(c2, ds));
+        EXPECT_FALSE(rtmp::ValidateComplexC2(c2, d1));
+    }
+    std::string simple(rtmp::kRtmpHandshakeSize, '\0');
+    EXPECT_FALSE(rtmp::OffersComplexHandshake(simple));
+}
+
+TEST(Rtmp, complex_handshake_ping_and_acks) {
+    RelayService svc;
+    Server server;
+    ServerOptions o;
+    o.has_builtin_services = false;
+    o.rtmp_service = &svc;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &o), 0);
+    const std::string addr = "127.0.0.1:" + std::to_string(server.listen_port());
+    const int64_t served0 = rtmp::ComplexHandshakesServed();
+    RtmpClientOptions copt;
+    copt.app = "relay";
+    copt.timeout_ms = 3000;
+    copt.complex_handshake = true;
+    RtmpClient client;
+    ASSERT_EQ(client.Init(addr.c_str(), copt), 0);
+    EXPECT_TRUE(client.complex_handshake_done());
+    EXPECT_EQ(rtmp::ComplexHandshakesServed(), served0 + 1);
+    EXPECT_EQ(rtmp::UnsignedC2Count(), 0);
+    RtmpClient simple;  // simple clients keep working on the same server
+    copt.complex_handshake = false;
+    ASSERT_EQ(simple.Init(addr.c_str(), copt), 0);
+    EXPECT_FALSE(simple.complex_handshake_done());
+    // user-control ping answered by the server
+    const int64_t rtt = client.Ping(2000);
+    EXPECT_GE(rtt, 0);
+    // a player that receives more than the server's window acknowledges it
+    Player player;
+    RtmpClientStreamOptions po;
+    po.play_name = "big";
+    ASSERT_EQ(player.Init(&client, po), 0);
+    RtmpClientStream pub;
+    RtmpClientStreamOptions pubo;
+    pubo.publish_name = "big";
+    ASSERT_EQ(pub.Init(&simple, pubo), 0);
+    const int N = 30;
+    for (int i = 0; i < N; ++i) {
+        RtmpVideoMessage vm;
+        vm.timestamp = (uint32_t)(i * 40);
+        vm.data.append(std::string(200000, (char)('a' + i % 26)));  // 6 MB in total
+        ASSERT_EQ(pub.SendVideoMessage(vm), 0);
+    }
+    const int64_t deadline = monotonic_us() + 5000000;
+    while (player.n.load() < N && monotonic_us() < deadline) usleep(2000);
+    EXPECT_EQ(player.n.load(), N);
+    EXPECT_GE(client.acks_sent(), 1);  // 6 MB over a 2.5 MB window
+    pub.Destroy();
+    player.Destroy();
 }

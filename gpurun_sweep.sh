@@ -35,18 +35,16 @@ for l in sys.stdin:
     d=json.loads(l); print('lat100: p50=%s p99=%s' % (d.get('p50_us_at_100qps'), d.get('p99_us_at_100qps')))
 " | tee -a $out
 }
-F="python3 bench.py --skip-64k --skip-grpc --skip-stream --latency-sample-s 6 --steps 20 --warmup 3"
-full() {
-  run "$@"
+G="python3 bench.py --skip-64k --skip-stream --latency-sample-s 0 --steps 5 --warmup 1 --requests-per-step 20000"
+grpc() {
+  local label=$1; shift
+  echo "== $label" | tee -a $out
+  timeout -k 10 180 env "$@" > gpurun_out/sweep_run.log 2>&1 || { echo "rc=$?" | tee -a $out; tail -5 gpurun_out/sweep_run.log; exit 1; }
   grep '^{' gpurun_out/sweep_run.log | python3 -c "
 import json,sys
 for l in sys.stdin:
-    d=json.loads(l); print('lat100: p50=%s p99=%s' % (d.get('p50_us_at_100qps'), d.get('p99_us_at_100qps')))
+    d=json.loads(l); print('grpc cpu=%s gpu=%s p99 cpu=%s gpu=%s' % (d.get('grpc_snappy_64KB_qps_cpu_codec'), d.get('grpc_snappy_64KB_qps_gpu_codec'), d.get('grpc_snappy_64KB_p99_us_cpu_codec'), d.get('grpc_snappy_64KB_p99_us_gpu_codec')))
 " | tee -a $out
 }
-for rep in 1 2; do
-  full "rep$rep default" $F
-  full "rep$rep latency-first" $F --latency-first
-  full "rep$rep l3=3" $F --cpu-l3-domain 3
-done
+for kb in 4 8 16; do grpc "block_kb=$kb" MRPC_FLAGS="--gpu_snappy_block_kb=$kb" $G; done
 echo done
