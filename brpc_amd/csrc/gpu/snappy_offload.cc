@@ -7,23 +7,25 @@
 // Wire format is standard raw snappy in both directions, so peers with a
 // CPU codec interoperate:
 //  * compress: the body is staged into HBM (batched copy kernel reading the
-//    pinned socket blocks), cut into gpu_snappy_block_kb blocks (16 KiB: one
-//    64 KiB body spreads over 4 waves) that snappy_compress_kernel encodes
+//    pinned socket blocks), cut into gpu_snappy_block_kb blocks (4 KiB: one
+//    64 KiB body spreads over 16 waves) that snappy_compress_kernel encodes
 //    one wave each straight into pinned host memory; the stream is
 //    one varint header + the blocks' element runs (a block never references
 //    another, so the concatenation is one valid stream).
 //  * decompress: the host walks the tag stream once to cut it into pieces of
-//    <= 16 KiB (device streams), else <= 64 KiB, uncompressed whose copies
+//    <= 4 KiB (device streams), else <= 64 KiB, uncompressed whose copies
 //    stay inside the piece (true for every fragmenting encoder, ours and
 //    google snappy); each piece gets its
 //    own varint header in a pinned staging buffer, snappy_decompress_kernel
 //    decodes all pieces in one launch straight into pinned output. A stream
 //    that cannot be cut that way falls back to the CPU codec.
 // Each direction is one stream-ordered sequence (copy, kernel) and ONE
-// fiber-friendly event wait. Measured on MI355X (bench.py gRPC leg) the
-// serial snappy format keeps one wave per block busy for hundreds of
-// microseconds, so per-RPC offload loses to the CPU codec on latency; it is
-// opt-in (EnableGpuSnappy) for bodies that are headed to the GPU anyway.
+// fiber-friendly event wait. Measured on MI355X (bench.py gRPC leg, 64 KiB
+// bodies, 50 in flight): 16 KiB blocks 12.9k QPS, 8 KiB 19.4k, 4 KiB 24.6k,
+// 1-2 KiB 25k (saturated by the per-call launch/wait overhead) vs 53k with
+// the CPU codec — the serial snappy format keeps one wave per block busy, so
+// per-RPC offload loses to the CPU on latency; it is opt-in
+// (EnableGpuSnappy) for bodies that are headed to the GPU anyway.
 #include "gpu/snappy_offload.h"
 
 #include <hip/hip_runtime_api.h>
@@ -40,7 +42,7 @@
 #include "var/var.h"
 #include "base/flags.h"
 
-DEFINE_int32(gpu_snappy_block_kb, 16,
+DEFINE_int32(gpu_snappy_block_kb, 4,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
              "waves (lower latency) at some cost in ratio; <= 64");
 

@@ -46,5 +46,5 @@ for l in sys.stdin:
     d=json.loads(l); print('grpc cpu=%s gpu=%s p99 cpu=%s gpu=%s' % (d.get('grpc_snappy_64KB_qps_cpu_codec'), d.get('grpc_snappy_64KB_qps_gpu_codec'), d.get('grpc_snappy_64KB_p99_us_cpu_codec'), d.get('grpc_snappy_64KB_p99_us_gpu_codec')))
 " | tee -a $out
 }
-for kb in 4 8 16; do grpc "block_kb=$kb" MRPC_FLAGS="--gpu_snappy_block_kb=$kb" $G; done
+for kb in 1 2 4; do grpc "block_kb=$kb" MRPC_FLAGS="--gpu_snappy_block_kb=$kb" $G; done
 echo done
