@@ -303,6 +303,27 @@ def main():
               "device": bool(cuda), "fanout": len(others)}
         sp.close()
 
+    # Pipeline leg (PP analog): one stream per rank through a chain of all
+    # other ranks' servers (r+1 -> r+2 -> ... -> r+N-1): every hop pulls
+    # each HBM chunk over xGMI and lends it on; the tail acknowledges.
+    rp = None
+    if topo.world_size > 2 and not a.skip_stream:
+        chain = [addrs[(topo.rank + k) % topo.world_size] for k in range(1, topo.world_size)]
+        pp = native.StreamPress({"server": chain[0], "relay_chain": ",".join(chain[1:]), "chunk_size": 65536,
+                                 "chunks_per_step": 32, "device_chunks": bool(cuda), "gpu_device": topo.device})
+        pp.run_steps(a.warmup)
+        parallel.barrier(topo)
+        sync()
+        t0 = time.perf_counter()
+        pp.run_steps(a.steps)
+        parallel.barrier(topo)
+        sync()
+        dt = time.perf_counter() - t0
+        dt_max = parallel.allreduce_max(dt, topo)
+        nbytes = parallel.allreduce_sum(a.steps * 32 * 65536, topo)
+        rp = {"gbps": nbytes / dt_max / 1e9 if dt_max > 0 else 0.0, "hops": len(chain)}
+        pp.close()
+
     # Fan-out leg (BASELINE config 2, the DP analog): every call is broadcast
     # by a ParallelChannel to the servers of ALL other ranks — one direct
     # xGMI link each — with a 64 KiB HBM attachment, and the echoes are
@@ -463,6 +484,9 @@ def main():
             out["fanout_p99_us"] = rf["p99_us"]
             out["fanout_errors"] = rf["errors"]
             out["fanout_peers_per_rank"] = rf["fanout"]
+        if rp:
+            out["pipeline_gbytes_per_s"] = round(rp["gbps"], 3)
+            out["pipeline_hops"] = rp["hops"]
         if rr:
             out["route_calls_per_s"] = round(rr["qps"], 1)
             out["route_p99_us"] = rr["p99_us"]

@@ -74,7 +74,8 @@ int StreamPress::Init(const StreamPressOptions& opt, std::string* err) {
         example::EchoService_Stub stub(&p->ch);
         example::EchoRequest req;
         example::EchoResponse res;
-        req.set_message("stream:" + std::to_string((int64_t)opt.chunk_size * opt.chunks_per_step));
+        const std::string round = std::to_string((int64_t)opt.chunk_size * opt.chunks_per_step);
+        req.set_message(opt.relay_chain.empty() ? "stream:" + round : "relay:" + round + ":" + opt.relay_chain);
         stub.Echo(&cntl, &req, &res, nullptr);
         if (cntl.Failed()) {
             *err = "stream handshake with " + server + " failed: " + cntl.ErrorText();

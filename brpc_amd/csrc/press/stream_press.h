@@ -33,6 +33,9 @@ struct StreamPressOptions {
     int64_t max_buf_size = 2 * 1024 * 1024;  // stream window (StreamOptions)
     bool device_chunks = false;              // chunks in HBM, moved over xGMI
     int gpu_device = -1;
+    // Pipeline (PP analog): the servers in `server` relay every chunk on
+    // through these comma-separated hops before the last one acknowledges.
+    std::string relay_chain;
 };
 
 class StreamPress {

@@ -223,6 +223,7 @@ public:
             else if (k == "max_buf_size") o.max_buf_size = v.cast<int64_t>();
             else if (k == "device_chunks") o.device_chunks = v.cast<bool>();
             else if (k == "gpu_device") o.gpu_device = v.cast<int>();
+            else if (k == "relay_chain") o.relay_chain = v.cast<std::string>();
             else throw std::invalid_argument("unknown stream press option: " + k);
         }
         _s.reset(new press::StreamPress);

@@ -3,8 +3,10 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "base/time.h"
 #include "fiber/fiber.h"
 #include "gpu/device_handler.h"
+#include "rpc/channel.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
 #include "rpc/stream.h"
@@ -36,6 +38,112 @@ private:
     int64_t _bytes = 0;
     int64_t _acked = 0;
 };
+
+// Stream relay of the "relay:<round_bytes>:<next>[,<next>...]" mode, the
+// pipeline-parallel analog (SURVEY §2.10 PP: a stream chain across GPUs).
+// The server opens a stream to the next hop (which relays further, or sinks
+// with "stream:" at the end of the chain), forwards every chunk downstream
+// in order — device chunks are re-lent to the next GPU over xGMI, never
+// staged — and forwards the tail's acknowledgements back upstream, so the
+// sender sees end-to-end completion. A full downstream window blocks the
+// upstream consumer, which backpressures the sender through its window.
+struct RelayState {
+    Channel ch;  // to the next hop
+    StreamId up = INVALID_STREAM_ID, down = INVALID_STREAM_ID;
+};
+
+class RelayUp : public StreamInputHandler {
+public:
+    explicit RelayUp(std::shared_ptr<RelayState> st) : _st(std::move(st)) {}
+    int on_received_messages(StreamId, Buf* const messages[], size_t n) override {
+        for (size_t i = 0; i < n; ++i) {
+            for (;;) {
+                const int rc = StreamWrite(_st->down, *messages[i]);
+                if (rc == 0) break;
+                if (rc != EAGAIN) return 0;  // downstream gone: on_closed follows
+                timespec ts = realtime_after_us(10 * 1000000LL);
+                if (StreamWait(_st->down, &ts) != 0) return 0;
+            }
+        }
+        return 0;
+    }
+    void on_closed(StreamId) override {
+        StreamClose(_st->down);
+        delete this;
+    }
+
+private:
+    std::shared_ptr<RelayState> _st;
+};
+
+class RelayDown : public StreamInputHandler {
+public:
+    explicit RelayDown(std::shared_ptr<RelayState> st) : _st(std::move(st)) {}
+    int on_received_messages(StreamId, Buf* const messages[], size_t n) override {
+        for (size_t i = 0; i < n; ++i) StreamWrite(_st->up, *messages[i]);  // acks: tiny
+        return 0;
+    }
+    void on_closed(StreamId) override {
+        StreamClose(_st->up);
+        delete this;
+    }
+
+private:
+    std::shared_ptr<RelayState> _st;
+};
+
+// Sets up the relay for `spec` = "<round>:<next>[,<rest>]"; 0 or -1 + *err.
+int StartRelay(Controller* cntl, const std::string& spec, int gpu_device, std::string* err) {
+    const size_t colon = spec.find(':');
+    if (colon == std::string::npos || colon + 1 >= spec.size()) {
+        *err = "relay spec must be <round>:<next>[,<next>...]";
+        return -1;
+    }
+    const std::string round = spec.substr(0, colon);
+    const std::string hops = spec.substr(colon + 1);
+    const size_t comma = hops.find(',');
+    const std::string next = hops.substr(0, comma);
+    const std::string rest = comma == std::string::npos ? std::string() : hops.substr(comma + 1);
+    auto st = std::make_shared<RelayState>();
+    ChannelOptions co;
+    co.timeout_ms = 10000;
+    co.max_retry = 0;
+    co.use_device_transport = gpu_device >= 0;
+    co.gpu_device = gpu_device;
+    co.connection_group = "relay";
+    if (st->ch.Init(next.c_str(), &co) != 0) {
+        *err = "relay: cannot reach " + next;
+        return -1;
+    }
+    RelayDown* down_h = new RelayDown(st);
+    Controller dc;
+    StreamOptions dso;
+    dso.handler = down_h;
+    if (StreamCreate(&st->down, dc, &dso) != 0) {
+        delete down_h;
+        *err = "relay: StreamCreate failed";
+        return -1;
+    }
+    example::EchoService_Stub stub(&st->ch);
+    example::EchoRequest req;
+    example::EchoResponse res;
+    req.set_message(rest.empty() ? "stream:" + round : "relay:" + round + ":" + rest);
+    stub.Echo(&dc, &req, &res, nullptr);
+    if (dc.Failed()) {
+        *err = "relay: next hop " + next + " refused: " + dc.ErrorText();
+        return -1;  // the failed stream closes and frees down_h
+    }
+    RelayUp* up_h = new RelayUp(st);
+    StreamOptions uso;
+    uso.handler = up_h;
+    if (StreamAccept(&st->up, *cntl, &uso) != 0) {
+        delete up_h;
+        StreamClose(st->down);
+        *err = "relay: fail to accept the upstream";
+        return -1;
+    }
+    return 0;
+}
 }  // namespace
 
 void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest* request,
@@ -60,6 +168,13 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
         if (StreamAccept(&sid, *cntl, &so) != 0) {
             delete sink;
             cntl->SetFailed(EINTERNAL, "fail to accept the stream");
+            return;
+        }
+    }
+    if (cntl->has_remote_stream() && request->message().compare(0, 6, "relay:") == 0) {
+        std::string err;
+        if (StartRelay(cntl, request->message().substr(6), _gpu_device, &err) != 0) {
+            cntl->SetFailed(EINTERNAL, "%s", err.c_str());
             return;
         }
     }

@@ -2,6 +2,8 @@
 the distributed path (ring over ranks) is exercised with gloo on CPU."""
 import json
 import os
+
+import pytest
 import subprocess
 import sys
 
@@ -28,11 +30,12 @@ def test_bench_single_rank():
     assert j["config"]["seq_len"] == 32
 
 
-def test_bench_two_ranks_gloo():
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_bench_multi_rank_gloo(nranks):
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29517",
-                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
+                        "--master-addr", "127.0.0.1", "--master-port", str(29517 + nranks),
+                        os.path.join(ROOT, "bench.py"), "--gpus", str(nranks), "--steps", "2", "--warmup", "1",
                         "--requests-per-step", "1000", "--requests-per-step-64k", "300",
                         "--requests-per-step-fanout", "100", "--requests-per-step-grpc", "50",
                         "--latency-sample-s", "0.3", "--workers", "2"],
@@ -41,9 +44,11 @@ def test_bench_two_ranks_gloo():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout
     j = lines[0]
-    assert j["n_gpus"] == 2 and j["value"] > 0 and j["errors"] == 0
-    # multi-rank legs: stream fan-out to the other rank, ParallelChannel fan-out
-    assert j["stream_fanout_per_rank"] == 1 and j["stream_gbytes_per_s_64KB_chunks"] > 0
-    assert j["fanout_peers_per_rank"] == 1 and j["fanout_errors"] == 0 and j["fanout_gbytes_per_s"] > 0
+    assert j["n_gpus"] == nranks and j["value"] > 0 and j["errors"] == 0
+    # multi-rank legs: stream fan-out to the other ranks, ParallelChannel fan-out
+    assert j["stream_fanout_per_rank"] == nranks - 1 and j["stream_gbytes_per_s_64KB_chunks"] > 0
+    assert j["fanout_peers_per_rank"] == nranks - 1 and j["fanout_errors"] == 0 and j["fanout_gbytes_per_s"] > 0
     assert j["scatter_errors"] == 0 and j["scatter_gbytes_per_s"] > 0
     assert j["route_errors"] == 0 and j["route_calls_per_s"] > 0
+    if nranks > 2:  # a relay chain needs at least two other ranks
+        assert j["pipeline_hops"] == nranks - 1 and j["pipeline_gbytes_per_s"] > 0

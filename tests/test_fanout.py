@@ -85,3 +85,33 @@ def test_consistent_hash_routing_spreads_keys(native):
     finally:
         for s in servers:
             s.stop()
+
+
+def test_stream_relay_chain(native):
+    """PP analog: chunks pushed into server A are relayed A -> B -> C in
+    order; C's acknowledgements travel back, so steps complete end to end."""
+    servers = [start_echo_server("127.0.0.1:0") for _ in range(3)]
+    try:
+        sp = native.StreamPress({"server": servers[0].address, "chunk_size": 65536, "chunks_per_step": 8,
+                                 "relay_chain": ",".join(s.address for s in servers[1:])})
+        sp.run_steps(6)
+        st = sp.stats()
+        assert st["streams"] == 1 and st["steps"] == 6, st
+        assert st["bytes_acked"] == 6 * 8 * 65536, st
+        sp.close()
+        # every hop saw the set-up call: A (from the press), B (from A), C (from B)
+        assert [s.echo_calls for s in servers] == [1, 1, 1]
+    finally:
+        for s in servers:
+            s.stop()
+
+
+def test_stream_relay_to_unreachable_hop_fails(native):
+    import pytest
+    s = start_echo_server("127.0.0.1:0")
+    try:
+        with pytest.raises(Exception):
+            native.StreamPress({"server": s.address, "chunk_size": 4096, "chunks_per_step": 2,
+                                "relay_chain": "127.0.0.1:1"})
+    finally:
+        s.stop()

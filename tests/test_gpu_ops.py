@@ -336,6 +336,30 @@ def test_route_device_attachment_by_key(dev):
             s.stop()
 
 
+def test_stream_relay_chain_device_chunks(dev):
+    """PP analog over xGMI: HBM chunks relayed through three servers, each
+    hop pulling the chunk and lending it on; acks come back from the tail."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    servers = [start_echo_server("127.0.0.1:0", gpu_device=0) for _ in range(3)]
+    try:
+        before = native.gpu.xgmi_stats()
+        sp = native.StreamPress({"server": servers[0].address, "chunk_size": 65536, "chunks_per_step": 16,
+                                 "device_chunks": True, "gpu_device": 0,
+                                 "relay_chain": ",".join(s.address for s in servers[1:])})
+        sp.run_steps(5)
+        st = sp.stats()
+        assert st["steps"] == 5 and st["bytes_acked"] == 5 * 16 * 65536, st
+        sp.close()
+        after = _drain_lent(native)
+        assert after["lent_outstanding"] == 0, after
+        # three hops each pulled every chunk
+        assert after["copy_segments"] - before["copy_segments"] >= 3 * 5 * 16, (before, after)
+    finally:
+        for s in servers:
+            s.stop()
+
+
 @pytest.mark.parametrize("device_attachment", [False, True])
 def test_gpu_process_echo_handler(dev, device_attachment):
     """the handler gathers the attachment into HBM with the
