@@ -86,6 +86,15 @@ int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, void* scratch, uint32
 int LaunchPbScan(const uint8_t* buf, uint64_t buf_len, const int64_t* offsets_dev, int64_t n, uint32_t max_fields,
                  uint64_t* fields, int32_t* nfields, hipStream_t s);
 
+// JSON structural index (gpu/json_kernels.hip): out_pos receives, in order,
+// the byte offsets of every unescaped '"' and of every { } [ ] : , outside
+// strings; count_dev the number found (positions past max_out are dropped
+// and err |= 2); err |= 1 when a string is left open at the end. n < 4 GiB.
+// scratch must hold JsonIndexScratchBytes(n).
+size_t JsonIndexScratchBytes(uint64_t n);
+int LaunchJsonIndex(const uint8_t* in, uint64_t n, uint32_t* out_pos, uint64_t max_out, uint64_t* count_dev,
+                    int* err_dev, void* scratch, hipStream_t s);
+
 // ---- synchronous helpers (fiber-friendly waits)
 // CRC32C of device buffers; results to host.
 int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t* out_host, int device);

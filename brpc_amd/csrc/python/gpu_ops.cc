@@ -97,4 +97,11 @@ void bind_gpu_ops(py::module_& g) {
                                       (void*)scratch, as_stream(stream)),
               "varint_encode");
     });
+    g.def("json_index_scratch_bytes", &gpu::JsonIndexScratchBytes);
+    g.def("json_index_launch", [](uintptr_t in, uint64_t n, uintptr_t out, uint64_t max_out, uintptr_t count,
+                                  uintptr_t err, uintptr_t scratch, uintptr_t stream) {
+        check(gpu::LaunchJsonIndex((const uint8_t*)in, n, (uint32_t*)out, max_out, (uint64_t*)count, (int*)err,
+                                   (void*)scratch, as_stream(stream)),
+              "json_index");
+    });
 }

@@ -6,3 +6,4 @@ from .varint import varint_decode, varint_encode, varint_encode_host, varint_dec
 from .copy import batched_copy, batched_copy_crc32c  # noqa: F401
 from .pb import pb_scan  # noqa: F401
 from .snappy import snappy_compress, snappy_compress_blocks, snappy_decompress  # noqa: F401
+from .json import json_index, json_index_host  # noqa: F401

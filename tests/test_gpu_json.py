@@ -1,0 +1,130 @@
+"""GPU JSON structural index (gpu/json_kernels.hip) against the pure-python
+reference walk of the same bytes: real json.dumps documents (escapes,
+unicode, nesting), adversarial backslash/quote soups whose runs straddle
+64-byte lane and 16 KiB tile boundaries, inputs past 1024 tiles (the tile
+scan's multi-entry path), unaligned views, and the error codes."""
+import json
+import random
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from brpc_amd.ops.json import json_index_host  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from brpc_amd import native
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    assert native.gpu.device_count() > 0
+    return torch.device("cuda", 0)
+
+
+def _doc(rnd, depth=0):
+    k = rnd.random()
+    if depth > 4 or k < 0.3:
+        return rnd.choice([
+            rnd.randint(-10**12, 10**12), rnd.random(), True, None,
+            "".join(rnd.choice('ab"\\/\n\t{}[]:,é中') for _ in range(rnd.randint(0, 20))),
+        ])
+    if k < 0.65:
+        return [_doc(rnd, depth + 1) for _ in range(rnd.randint(0, 6))]
+    return {"k%d\"{" % i: _doc(rnd, depth + 1) for i in range(rnd.randint(0, 6))}
+
+
+def _run(dev, data):
+    from brpc_amd.ops import json_index
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if data else torch.empty(0, dtype=torch.uint8,
+                                                                                                   device=dev)
+    return json_index(buf).cpu().tolist()
+
+
+def test_host_reference_matches_json_structure():
+    # CPU: the reference walk agrees with the structure json.dumps wrote
+    rnd = random.Random(3)
+    for _ in range(50):
+        obj = _doc(rnd)
+        text = json.dumps(obj, ensure_ascii=rnd.random() < 0.5).encode()
+        pos, open_ = json_index_host(text)
+        assert not open_
+        toks = bytes(text[p] for p in pos)
+        assert toks.count(b'"'[0]) % 2 == 0
+        assert toks.count(b"{"[0]) == toks.count(b"}"[0]) and toks.count(b"["[0]) == toks.count(b"]"[0])
+    assert json_index_host(b'{"a\\"b": [1, "x,y"]}') == ([0, 1, 6, 7, 9, 11, 13, 17, 18, 19], False)
+    assert json_index_host(b'"abc')[1]
+
+
+@pytest.mark.gpu
+def test_json_documents(dev):
+    rnd = random.Random(11)
+    for _ in range(40):
+        text = json.dumps([_doc(rnd) for _ in range(rnd.randint(1, 40))], ensure_ascii=rnd.random() < 0.5).encode()
+        assert _run(dev, text) == json_index_host(text)[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("alphabet", ['"\\a', '"\\\\\\a{', '"\\{}[]:,xy '])
+def test_adversarial_escapes(dev, alphabet):
+    # soups of quotes and backslash runs: every lane and tile boundary sees
+    # odd and even runs and open strings; the stream closes its last string
+    rnd = random.Random(hash(alphabet) & 0xFFFF)
+    for n in (1, 63, 64, 65, 4095, 16383, 16384, 16385, 70000):
+        s = "".join(rnd.choice(alphabet) for _ in range(n)).encode()
+        pos, open_ = json_index_host(s)
+        if open_:
+            s += b'"'
+            pos, open_ = json_index_host(s)
+            if open_:  # the added quote was escaped
+                s += b' "'
+                pos, open_ = json_index_host(s)
+        assert not open_
+        assert _run(dev, s) == pos, n
+
+
+@pytest.mark.gpu
+def test_backslash_lanes_and_tiles(dev):
+    # whole lanes (and a whole tile) of backslashes inside a string, both parities
+    for run in (63, 64, 65, 127, 128, 129, 16384, 16385):
+        for lead in (0, 1, 30, 62, 63):
+            s = b" " * lead + b'["' + b"\\" * run + b'x", "y"]'
+            pos, open_ = json_index_host(s)
+            if open_:
+                s += b'"]'
+                pos, open_ = json_index_host(s)
+            assert not open_
+            assert _run(dev, s) == pos, (run, lead)
+
+
+@pytest.mark.gpu
+def test_many_tiles(dev):
+    # > 1024 tiles: the tile scan folds several tiles per thread. The input
+    # repeats an odd-length unit, so the expected index is the unit's index
+    # shifted by k * len(unit)
+    rnd = random.Random(5)
+    unit = (json.dumps({"a\\\\\"": [_doc(rnd) for _ in range(8)], "s": "x\\\"y"}) + ",").encode()
+    if len(unit) % 2 == 0:
+        unit = b" " + unit
+    reps = (20 << 20) // len(unit) + 1
+    upos = torch.tensor(json_index_host(unit)[0], dtype=torch.int64)
+    expect = (upos[None, :] + torch.arange(reps, dtype=torch.int64)[:, None] * len(unit)).reshape(-1)
+    from brpc_amd.ops import json_index
+    buf = torch.frombuffer(bytearray(unit * reps), dtype=torch.uint8).to(dev)
+    got = json_index(buf).cpu()
+    assert got.numel() == expect.numel()
+    assert torch.equal(got, expect)
+
+
+@pytest.mark.gpu
+def test_unaligned_view_and_errors(dev):
+    from brpc_amd.ops import json_index
+    text = json.dumps({"k": ["v\\\"", 1, {"z": [2, 3]}]}).encode() * 300
+    big = torch.frombuffer(bytearray(b"xyz" + text), dtype=torch.uint8).to(dev)
+    assert json_index(big[3:]).cpu().tolist() == json_index_host(text)[0]
+    assert _run(dev, b"") == []
+    with pytest.raises(ValueError, match="unterminated"):
+        _run(dev, b'{"a": "b')
+    with pytest.raises(ValueError, match="structural positions"):
+        json_index(torch.frombuffer(bytearray(b"[1,2,3,4]"), dtype=torch.uint8).to(dev), max_positions=3)
+    with pytest.raises(ValueError):
+        json_index(torch.zeros(4, dtype=torch.uint8))
