@@ -277,50 +277,80 @@ __global__ void __launch_bounds__(kJThreads) json_tile_kernel(const uint8_t* __r
 }
 
 // Pass 2 (one block): tile start states from (carry 0, outside strings),
-// output offsets, total count; err |= 1 for a string open at the end.
-__global__ void __launch_bounds__(1024) json_scan_kernel(Scratch sc, uint64_t ntiles, uint64_t* total, int* err) {
-    __shared__ uint32_t xpart[1024];
-    __shared__ uint64_t cpart[1024];
-    const uint64_t per = (ntiles + 1023) / 1024;
-    const uint64_t b = threadIdx.x * per;
-    const uint64_t e = b + per < ntiles ? b + per : ntiles;
-    uint32_t acc = kXfIdentity;
-    for (uint64_t i = b; i < e; ++i) acc = xf_compose(acc, sc.tile_xfer[i]);
-    xpart[threadIdx.x] = acc;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const uint32_t y = threadIdx.x >= (unsigned)off ? xpart[threadIdx.x - off] : kXfIdentity;
+// output offsets, total count; err |= 1 for a string open at the end. The
+// tile arrays stream through LDS in coalesced chunks of kScanPer tiles per
+// thread; the state and the running offset carry from chunk to chunk.
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = 4;
+constexpr int kScanChunk = kScanThreads * kScanPer;
+
+__global__ void __launch_bounds__(kScanThreads) json_scan_kernel(Scratch sc, uint64_t ntiles, uint64_t* total,
+                                                                 int* err) {
+    __shared__ uint32_t sx[kScanChunk];
+    __shared__ uint64_t scnt[kScanChunk];
+    __shared__ uint32_t xpart[kScanThreads];
+    __shared__ uint64_t cpart[kScanThreads];
+    const int t = threadIdx.x;
+    int k_carry = 0;
+    uint64_t off_carry = 0;
+    for (uint64_t base = 0; base < ntiles; base += kScanChunk) {
+        const uint64_t m = ntiles - base < (uint64_t)kScanChunk ? ntiles - base : (uint64_t)kScanChunk;
+        for (int j = t; j < kScanChunk; j += kScanThreads) {
+            sx[j] = (uint64_t)j < m ? sc.tile_xfer[base + j] : kXfIdentity;
+            scnt[j] = (uint64_t)j < m ? sc.tile_cnt[base + j] : 0;
+        }
         __syncthreads();
-        xpart[threadIdx.x] = xf_compose(y, xpart[threadIdx.x]);
+        uint32_t acc = kXfIdentity;
+#pragma unroll
+        for (int i = 0; i < kScanPer; ++i) acc = xf_compose(acc, sx[t * kScanPer + i]);
+        xpart[t] = acc;
         __syncthreads();
-    }
-    int k = threadIdx.x ? xf_apply(xpart[threadIdx.x - 1], 0) : 0;
-    uint64_t sum = 0;
-    for (uint64_t i = b; i < e; ++i) {
-        const uint32_t x = sc.tile_xfer[i];
-        const uint64_t cnt = (sc.tile_cnt[i] >> (16 * k)) & 0xFFFF;
-        sc.tile_xfer[i] = (uint32_t)k;  // now: the tile's start state
-        sc.tile_cnt[i] = cnt;
-        sum += cnt;
-        k = xf_apply(x, k);
-    }
-    cpart[threadIdx.x] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-        const uint64_t y = threadIdx.x >= (unsigned)off ? cpart[threadIdx.x - off] : 0;
+        for (int off = 1; off < kScanThreads; off <<= 1) {
+            const uint32_t y = t >= off ? xpart[t - off] : kXfIdentity;
+            __syncthreads();
+            xpart[t] = xf_compose(y, xpart[t]);
+            __syncthreads();
+        }
+        int k = xf_apply(t ? xpart[t - 1] : kXfIdentity, k_carry);
+        uint64_t sum = 0;
+#pragma unroll
+        for (int i = 0; i < kScanPer; ++i) {
+            const int j = t * kScanPer + i;
+            const uint32_t x = sx[j];
+            const uint64_t cnt = (scnt[j] >> (16 * k)) & 0xFFFF;
+            sx[j] = (uint32_t)k;  // now: the tile's start state
+            scnt[j] = cnt;
+            sum += cnt;
+            k = xf_apply(x, k);
+        }
+        cpart[t] = sum;
         __syncthreads();
-        cpart[threadIdx.x] += y;
+        for (int off = 1; off < kScanThreads; off <<= 1) {
+            const uint64_t y = t >= off ? cpart[t - off] : 0;
+            __syncthreads();
+            cpart[t] += y;
+            __syncthreads();
+        }
+        uint64_t run = off_carry + (t ? cpart[t - 1] : 0);
+#pragma unroll
+        for (int i = 0; i < kScanPer; ++i) {
+            const int j = t * kScanPer + i;
+            const uint64_t c = scnt[j];
+            scnt[j] = run;
+            run += c;
+        }
         __syncthreads();
+        for (int j = t; (uint64_t)j < m; j += kScanThreads) {
+            sc.tile_xfer[base + j] = sx[j];
+            sc.tile_cnt[base + j] = scnt[j];
+        }
+        k_carry = xf_apply(xpart[kScanThreads - 1], k_carry);
+        off_carry += cpart[kScanThreads - 1];
+        __syncthreads();  // the next chunk reuses the LDS arrays
     }
-    uint64_t run = threadIdx.x ? cpart[threadIdx.x - 1] : 0;
-    for (uint64_t i = b; i < e; ++i) {
-        const uint64_t c = sc.tile_cnt[i];
-        sc.tile_cnt[i] = run;
-        run += c;
-    }
-    if (threadIdx.x == 1023) {
-        *total = cpart[1023];
-        if (xf_flip(xpart[1023], 0)) atomicOr(err, 1);
+    if (t == 0) {
+        *total = off_carry;
+        if (k_carry >> 1) atomicOr(err, 1);
     }
 }
 
@@ -375,7 +405,7 @@ int LaunchJsonIndex(const uint8_t* in, uint64_t n, uint32_t* out_pos, uint64_t m
     const Scratch sc = carve(scratch, tiles);
     const dim3 grid((uint32_t)tiles), block(kJThreads);
     hipLaunchKernelGGL(json_tile_kernel, grid, block, 0, s, in, n, sc, err_dev);
-    hipLaunchKernelGGL(json_scan_kernel, dim3(1), dim3(1024), 0, s, sc, tiles, count_dev, err_dev);
+    hipLaunchKernelGGL(json_scan_kernel, dim3(1), dim3(kScanThreads), 0, s, sc, tiles, count_dev, err_dev);
     hipLaunchKernelGGL(json_emit_kernel, grid, block, 0, s, sc, tiles, (const uint64_t*)count_dev, out_pos, max_out,
                        err_dev);
     return hipGetLastError() == hipSuccess ? 0 : -1;

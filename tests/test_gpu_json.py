@@ -1,8 +1,9 @@
 """GPU JSON structural index (gpu/json_kernels.hip) against the pure-python
 reference walk of the same bytes: real json.dumps documents (escapes,
 unicode, nesting), adversarial backslash/quote soups whose runs straddle
-64-byte lane and 16 KiB tile boundaries, inputs past 1024 tiles (the tile
-scan's multi-entry path), unaligned views, and the error codes."""
+64-byte lane and 16 KiB tile boundaries, inputs past 4096 tiles (the tile
+scan carries state and offsets across LDS chunks), unaligned views and the
+error codes."""
 import json
 import random
 
@@ -98,14 +99,14 @@ def test_backslash_lanes_and_tiles(dev):
 
 @pytest.mark.gpu
 def test_many_tiles(dev):
-    # > 1024 tiles: the tile scan folds several tiles per thread. The input
+    # > 4096 tiles: the tile scan carries state and offsets across LDS chunks. The input
     # repeats an odd-length unit, so the expected index is the unit's index
     # shifted by k * len(unit)
     rnd = random.Random(5)
     unit = (json.dumps({"a\\\\\"": [_doc(rnd) for _ in range(8)], "s": "x\\\"y"}) + ",").encode()
     if len(unit) % 2 == 0:
         unit = b" " + unit
-    reps = (20 << 20) // len(unit) + 1
+    reps = (70 << 20) // len(unit) + 1
     upos = torch.tensor(json_index_host(unit)[0], dtype=torch.int64)
     expect = (upos[None, :] + torch.arange(reps, dtype=torch.int64)[:, None] * len(unit)).reshape(-1)
     from brpc_amd.ops import json_index
