@@ -829,6 +829,10 @@ int Socket::StartWrite(WriteRequest* req, const WriteOptions& opt) {
             return 0;
         }
     }
+    // KeepWrite owns a reference: the caller's may go away while requests
+    // are still queued, and a recycled slot would hand this write queue to
+    // the next connection.
+    AddRef();
     fiber::fiber_t th;
     if (fiber::start_background(&th, &fiber::ATTR_NORMAL, KeepWrite, req) != 0) KeepWrite(req);
     return 0;
@@ -907,10 +911,12 @@ void* Socket::KeepWrite(void* arg) {
         }
         if (s->IsWriteComplete(cur_tail, req == cur_tail, &cur_tail)) {
             finish_write_request(req, s->fd());
+            s->Dereference();
             return nullptr;
         }
     }
     s->ReleaseAllFailedWriteRequests(req);
+    s->Dereference();
     return nullptr;
 }
 
