@@ -38,9 +38,12 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
+#include "pb/message.h"
 #include "rpc/compress.h"
 #include "var/var.h"
 #include "base/flags.h"
+
+DECLARE_uint64(max_body_size);
 
 DEFINE_int32(gpu_snappy_block_kb, 4,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
@@ -78,7 +81,7 @@ struct HbmTmp {
     void* p = nullptr;
     size_t n = 0;
     int dev = -1;
-    HbmTmp(size_t bytes, int d) : p(HbmAlloc(bytes, d)), n(bytes), dev(d) {}
+    HbmTmp(size_t bytes, int d) : p(bytes ? HbmAlloc(bytes, d) : nullptr), n(bytes), dev(d) {}
     ~HbmTmp() {
         if (p) HbmFree(p, n, dev);
     }
@@ -273,7 +276,18 @@ bool split_stream(const uint8_t* p, size_t n, size_t limit, size_t* total, size_
     return true;
 }
 
-bool gpu_decompress(const Buf& in, Buf* out) {
+// Top-level field table of a decompressed message (pb_scan layout).
+constexpr uint32_t kIndexFields = 128;
+struct PbIndex {
+    PinnedBuf table{kIndexFields * 2 * sizeof(uint64_t) + 16};
+    int nfields = -1;  // pb_scan's count or negative code
+    const uint64_t* fields() const { return reinterpret_cast<const uint64_t*>(table.p); }
+};
+
+// Decodes a raw snappy stream on the device into a pinned Buf. With `index`
+// the output is decoded into HBM instead, pb_scan indexes it there, and one
+// copy brings the bytes to pinned memory — still one event wait per call.
+bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     const int dev = g_device;
     std::string flat = in.to_string();  // the tag walk needs contiguous bytes
     size_t total = 0, hdr = 0;
@@ -287,16 +301,23 @@ bool gpu_decompress(const Buf& in, Buf* out) {
         if (!split_stream(bytes, flat.size(), kSnappyMaxBlock, &total, &hdr, &pieces)) return false;
     }
     if (total == 0) return true;
-    // per-piece raw streams (own varint header) back to back, 16 B aligned
+    if (index && (total > FLAGS_max_body_size || total > 0xFFFFFFFFull)) return false;
+    // per-piece raw streams (own varint header) back to back, 16 B aligned;
+    // with an index, the message offset table {0, total} rides at the end
     std::vector<size_t> soff(pieces.size());
     size_t sbytes = 0;
     for (size_t k = 0; k < pieces.size(); ++k) {
         soff[k] = sbytes;
         sbytes += (varint_len(pieces[k].ulen) + pieces[k].comp_len + 15) & ~(size_t)15;
     }
-    PinnedBuf staged(sbytes), dst(total), jobs(pieces.size() * sizeof(SnappyJob)), meta(2 * pieces.size() * 4);
-    HbmTmp dstage(sbytes, dev);
-    if (!staged.p || !dst.p || !jobs.p || !meta.p || !dstage.p) return false;
+    const size_t offsets_at = sbytes;
+    if (index) sbytes += 2 * sizeof(int64_t);
+    PinnedBuf staged(sbytes), dst(total), jobs(pieces.size() * sizeof(SnappyJob)), meta(2 * pieces.size() * 4 + 16);
+    HbmTmp dstage(sbytes, dev), dbody(index ? total : 0, dev);
+    if (!staged.p || !dst.p || !jobs.p || !meta.p || !dstage.p || (index && (!dbody.p || !index->table.p))) {
+        return false;
+    }
+    char* out_base = index ? static_cast<char*>(dbody.p) : dst.p;
     SnappyJob* j = reinterpret_cast<SnappyJob*>(jobs.p);
     size_t upos = 0;
     uint32_t max_ulen = 1;
@@ -305,27 +326,79 @@ bool gpu_decompress(const Buf& in, Buf* out) {
         const int h = put_varint(s, pieces[k].ulen);
         memcpy(s + h, flat.data() + pieces[k].comp_off, pieces[k].comp_len);
         j[k].src = static_cast<char*>(dstage.p) + soff[k];
-        j[k].dst = dst.p + upos;
+        j[k].dst = out_base + upos;
         j[k].src_len = h + pieces[k].comp_len;
         j[k].dst_cap = pieces[k].ulen;
         upos += pieces[k].ulen;
         max_ulen = std::max<uint32_t>(max_ulen, (uint32_t)pieces[k].ulen);
     }
+    if (index) {
+        const int64_t offs[2] = {0, (int64_t)total};
+        memcpy(staged.p + offsets_at, offs, sizeof(offs));
+    }
     uint32_t* out_len = reinterpret_cast<uint32_t*>(meta.p);
     int* err = reinterpret_cast<int*>(out_len + pieces.size());
+    int32_t* nfields = reinterpret_cast<int32_t*>(err + pieces.size());
     Segment seg{staged.p, dstage.p, sbytes};
+    Segment back{dbody.p, dst.p, total};
     const int rc = run_and_wait(dev, [&](hipStream_t s) {
         if (LaunchBatchedCopy(&seg, 1, s) != 0) return -1;
-        return LaunchSnappyDecompress(j, (int)pieces.size(), max_ulen, out_len, err, s);
+        if (LaunchSnappyDecompress(j, (int)pieces.size(), max_ulen, out_len, err, s) != 0) return -1;
+        if (!index) return 0;
+        const int64_t* offs_dev = reinterpret_cast<const int64_t*>(static_cast<char*>(dstage.p) + offsets_at);
+        if (LaunchPbScan(static_cast<const uint8_t*>(dbody.p), total, offs_dev, 1, kIndexFields,
+                         reinterpret_cast<uint64_t*>(index->table.p), nfields, s) != 0) {
+            return -1;
+        }
+        return LaunchBatchedCopy(&back, 1, s);
     });
     if (rc != 0) return false;
     for (size_t k = 0; k < pieces.size(); ++k) {
         if (err[k] || out_len[k] != pieces[k].ulen) return false;
     }
+    if (index) index->nfields = *nfields;
     Buf whole;
     dst.give_to(&whole);
     out->append(std::move(whole));
     return true;
+}
+
+std::atomic<int64_t> g_indexed_parses{0}, g_index_fallbacks{0};
+
+// SetPbParseOffload hook: snappy decode + pb_scan in one device pass; the
+// host merges the top-level fields from the table (bytes fields become one
+// assign each, nested messages parse from their ranges).
+int parse_offload(const Buf& in, CompressType type, pb::Message* msg) {
+    if (type != COMPRESS_TYPE_SNAPPY || g_device < 0 || device_blocks_elsewhere(in, g_device)) return 0;
+    Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
+    const int64_t t0 = span ? monotonic_us() : 0;
+    PbIndex index;
+    Buf raw;
+    if (!gpu_decompress(in, &raw, &index)) {
+        g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        return 0;  // the CPU codec and parser take over
+    }
+    g_decomp_calls.fetch_add(1, std::memory_order_relaxed);
+    bool ok;
+    msg->Clear();
+    const bool contiguous = raw.backing_block_num() <= 1;
+    if (index.nfields >= 0 && contiguous &&
+        msg->MergeFromFieldTable(raw.empty() ? nullptr : reinterpret_cast<const uint8_t*>(raw.block_data(0)),
+                                 raw.size(), index.fields(), index.nfields)) {
+        ok = msg->IsInitialized();
+        g_indexed_parses.fetch_add(1, std::memory_order_relaxed);
+    } else {
+        // too many fields for the table, unknown fields, ...: the bytes are
+        // already decoded, so only the parse runs on the host
+        g_index_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        ok = msg->ParseFromBuf(raw);
+    }
+    if (span) {
+        span->AnnotateDevice(string_printf("snappy decompress + pb_scan %zu -> %zu B, %d fields dev%d", in.size(),
+                                           raw.size(), index.nfields, g_device),
+                             (float)(monotonic_us() - t0) / 1000.0f);
+    }
+    return ok ? 1 : -1;
 }
 
 bool offload(const Buf& in, Buf* out, bool compress) {
@@ -354,19 +427,27 @@ int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
     if (Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
     g_device = device;
     SetSnappyOffload(offload, min_bytes);
+    SetPbParseOffload(parse_offload, min_bytes);
     static var::PassiveStatus<int64_t> v1("gpu_snappy_compress_calls", [] { return g_comp_calls.load(); });
     static var::PassiveStatus<int64_t> v2("gpu_snappy_decompress_calls", [] { return g_decomp_calls.load(); });
     static var::PassiveStatus<int64_t> v3("gpu_snappy_fallbacks", [] { return g_fallbacks.load(); });
+    static var::PassiveStatus<int64_t> v4("gpu_pb_indexed_parses", [] { return g_indexed_parses.load(); });
+    static var::PassiveStatus<int64_t> v5("gpu_pb_index_fallbacks", [] { return g_index_fallbacks.load(); });
     return 0;
 }
 
-void DisableGpuSnappy() { SetSnappyOffload(nullptr, (size_t)-1); }
+void DisableGpuSnappy() {
+    SetSnappyOffload(nullptr, (size_t)-1);
+    SetPbParseOffload(nullptr, (size_t)-1);
+}
 
 GpuSnappyStats GetGpuSnappyStats() {
     GpuSnappyStats s;
     s.compress_calls = g_comp_calls.load();
     s.decompress_calls = g_decomp_calls.load();
     s.fallbacks = g_fallbacks.load();
+    s.indexed_parses = g_indexed_parses.load();
+    s.index_fallbacks = g_index_fallbacks.load();
     return s;
 }
 

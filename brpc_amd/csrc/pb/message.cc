@@ -667,6 +667,53 @@ bool Message::ParseFromBuf(const Buf& in) {
     return ParseFromArray(tmp.data(), tmp.size());
 }
 
+bool Message::MergeFromFieldTable(const uint8_t* data, size_t size, const uint64_t* fields, int nfields) {
+    const Descriptor* d = GetDescriptor();
+    for (int i = 0; i < nfields; ++i) {
+        const uint64_t tag = fields[2 * i], v = fields[2 * i + 1];
+        const WireType wt = (WireType)(tag & 7);
+        const FieldDescriptor* f = d->FindFieldByNumber((int)(tag >> 3));
+        if (!f || f->type == FieldType::GROUP) return false;
+        if (wt != WIRETYPE_LENGTH_DELIMITED) {
+            if (wt != wire_type_of(f->type)) return false;
+            store_number(this, f, v);
+            continue;
+        }
+        const size_t off = (size_t)(v >> 32), len = (size_t)(v & 0xFFFFFFFFu);
+        if (off > size || len > size - off) return false;
+        const uint8_t* p = data + off;
+        if (f->is_repeated() && f->is_packable()) {
+            CodedInput in(p, len);
+            while (!in.at_limit()) {
+                uint64_t x;
+                if (!read_number(&in, f->type, &x)) return false;
+                store_number(this, f, x);
+            }
+            continue;
+        }
+        switch (f->cpp_type()) {
+        case CppType::STRING:
+            if (f->is_repeated()) {
+                ref<std::vector<std::string>>(this, f).emplace_back((const char*)p, len);
+            } else {
+                if (f->oneof_index >= 0) ClearOneofSiblings(this, f);
+                ref<std::string>(this, f).assign((const char*)p, len);
+                set_has(this, f);
+            }
+            break;
+        case CppType::MESSAGE: {
+            Message* sub = f->is_repeated() ? Reflection::AddMessage(this, f) : Reflection::MutableMessage(this, f);
+            CodedInput in(p, len);
+            if (!parse_message(sub, &in) || !in.at_limit()) return false;
+            break;
+        }
+        default:
+            return false;  // a scalar field sent length-delimited but not packable
+        }
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- text format
 static void escape_bytes(const std::string& s, std::string* out) {
     for (unsigned char c : s) {

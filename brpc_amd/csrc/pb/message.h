@@ -52,6 +52,14 @@ public:
     bool ParseFromString(const std::string& s) { return ParseFromArray(s.data(), s.size()); }
     bool MergeFromString(const std::string& s);
     bool ParseFromBuf(const Buf& in);
+    // Merges the top-level fields listed in a wire-scan table (the GPU
+    // pb_scan layout: {tag, value} pairs, value = the number for wires
+    // 0/1/5, (offset << 32) | length into `data` for wire 2) instead of
+    // walking the bytes; nested messages and packed runs are parsed from
+    // their ranges. False for anything the table cannot express (unknown
+    // fields, mismatched wire types, groups, ranges outside data): the
+    // caller then parses the bytes normally.
+    bool MergeFromFieldTable(const uint8_t* data, size_t size, const uint64_t* fields, int nfields);
     std::string DebugString() const;
     std::string ShortDebugString() const;
     std::string GetTypeName() const { return GetDescriptor()->full_name; }

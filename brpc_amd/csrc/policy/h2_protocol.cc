@@ -878,11 +878,22 @@ void ProcessH2Response(InputMessageBase* msg_base) {
         if (r != 1) {
             saved_error = ERESPONSE;
             cntl->SetFailed(ERESPONSE, "bad grpc response framing");
-        } else if (compressed && (ct <= 0 || !DecompressBuf((CompressType)ct, pbbuf, &plain))) {
+        } else if (compressed && ct <= 0) {
             saved_error = ERESPONSE;
             cntl->SetFailed(ERESPONSE, "Fail to decompress the grpc response (grpc-encoding=%s)",
                             enc ? enc->c_str() : "<missing>");
-        } else if (cntl->_response && !ParsePbFromBuf(cntl->_response, compressed ? plain : pbbuf)) {
+        } else if (compressed && cntl->_response) {
+            // decompress + parse in one step (the device path indexes fields on the GPU)
+            if (!ParseFromCompressedData(pbbuf, cntl->_response, (CompressType)ct)) {
+                saved_error = ERESPONSE;
+                cntl->SetFailed(ERESPONSE, "Fail to decompress/parse the grpc response (grpc-encoding=%s)",
+                                enc ? enc->c_str() : "<missing>");
+            }
+        } else if (compressed && !DecompressBuf((CompressType)ct, pbbuf, &plain)) {
+            saved_error = ERESPONSE;
+            cntl->SetFailed(ERESPONSE, "Fail to decompress the grpc response (grpc-encoding=%s)",
+                            enc ? enc->c_str() : "<missing>");
+        } else if (cntl->_response && !ParsePbFromBuf(cntl->_response, pbbuf)) {
             saved_error = ERESPONSE;
             cntl->SetFailed(ERESPONSE, "Fail to parse grpc response");
         }
@@ -1052,18 +1063,16 @@ void ProcessH2Request(InputMessageBase* msg_base) {
             if (compressed) {
                 const std::string* enc = req_h.GetHeader("grpc-encoding");
                 const int ct = GrpcEncodingToCompressType(enc ? *enc : std::string());
-                Buf plain;
-                if (ct <= 0 || !DecompressBuf((CompressType)ct, pbbuf, &plain)) {
-                    cntl->SetFailed(EREQUEST, "Fail to decompress the grpc request (grpc-encoding=%s)",
-                                    enc ? enc->c_str() : "<missing>");
+                // decompress + parse in one step (the device path indexes fields on the GPU)
+                if (ct <= 0 || !ParseFromCompressedData(pbbuf, call.req, (CompressType)ct)) {
+                    cntl->SetFailed(EREQUEST, "Fail to decompress/parse the grpc request (grpc-encoding=%s) as %s",
+                                    enc ? enc->c_str() : "<missing>", call.req->GetDescriptor()->full_name.c_str());
                     break;
                 }
-                pbbuf.swap(plain);
                 // answer in the client's encoding unless the service decides otherwise
                 cntl->set_request_compress_type((CompressType)ct);
                 cntl->set_response_compress_type((CompressType)ct);
-            }
-            if (!ParsePbFromBuf(call.req, pbbuf)) {
+            } else if (!ParsePbFromBuf(call.req, pbbuf)) {
                 cntl->SetFailed(EREQUEST, "Fail to parse grpc request as %s",
                                 call.req->GetDescriptor()->full_name.c_str());
                 break;

@@ -435,6 +435,8 @@ PYBIND11_MODULE(_native, m) {
         d["compress_calls"] = s.compress_calls;
         d["decompress_calls"] = s.decompress_calls;
         d["fallbacks"] = s.fallbacks;
+        d["indexed_parses"] = s.indexed_parses;
+        d["index_fallbacks"] = s.index_fallbacks;
         return d;
     });
     g.def("hbm_pool_stats", [](int dev) {

@@ -165,6 +165,22 @@ bool DecompressBuf(CompressType type, const Buf& in, Buf* out) {
     return h && h->Decompress(in, out);
 }
 
+namespace {
+std::atomic<PbParseOffload> g_pb_offload{nullptr};
+size_t g_pb_offload_min = (size_t)-1;
+}  // namespace
+
+void SetPbParseOffload(PbParseOffload fn, size_t min_bytes) {
+    g_pb_offload_min = min_bytes;
+    g_pb_offload.store(fn, std::memory_order_release);
+}
+
+int TryPbParseOffload(const Buf& compressed, CompressType type, pb::Message* msg) {
+    PbParseOffload off = g_pb_offload.load(std::memory_order_acquire);
+    if (!off || type != COMPRESS_TYPE_SNAPPY || snappy_ulen(compressed) < g_pb_offload_min) return 0;
+    return off(compressed, type, msg);
+}
+
 void SetSnappyOffload(SnappyOffload fn, size_t min_bytes) {
     g_snappy_offload_min = min_bytes;
     g_snappy_offload.store(fn, std::memory_order_release);

@@ -30,4 +30,18 @@ bool DecompressBuf(CompressType type, const Buf& in, Buf* out);
 typedef bool (*SnappyOffload)(const Buf& in, Buf* out, bool compress);
 void SetSnappyOffload(SnappyOffload fn, size_t min_bytes);
 
+// Hook for decompress + parse in one device pass (GPU snappy decode, then
+// the pb wire-scan kernel indexes the message's top-level fields, so the
+// host merges fields from a table instead of walking the bytes). Returns
+// 1 when *msg is parsed, 0 when the hook declines (the CPU path runs), -1
+// when the data is malformed.
+namespace pb {
+class Message;
+}
+typedef int (*PbParseOffload)(const Buf& compressed, CompressType type, pb::Message* msg);
+void SetPbParseOffload(PbParseOffload fn, size_t min_bytes);
+// Runs the hook for `type` if one is installed and the body is large
+// enough; same return codes, 0 without a hook.
+int TryPbParseOffload(const Buf& compressed, CompressType type, pb::Message* msg);
+
 }  // namespace mrpc

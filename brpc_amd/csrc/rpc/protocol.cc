@@ -117,6 +117,10 @@ bool SerializeAsCompressedData(const pb::Message& msg, Buf* buf, CompressType ty
 
 bool ParseFromCompressedData(const Buf& data, pb::Message* msg, CompressType type) {
     if (type == COMPRESS_TYPE_NONE) return ParsePbFromBuf(msg, data);
+    if (data.size() <= FLAGS_max_body_size) {
+        const int rc = TryPbParseOffload(data, type, msg);
+        if (rc != 0) return rc > 0;
+    }
     Buf raw;
     if (!DecompressBuf(type, data, &raw)) return false;
     return ParsePbFromBuf(msg, raw);

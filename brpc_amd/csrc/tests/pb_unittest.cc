@@ -170,3 +170,80 @@ TEST(Pb, service_descriptor) {
     EXPECT_EQ(sd->method(0)->input_type, example::EchoRequest::descriptor());
     EXPECT_TRUE(DescriptorPool::generated_pool()->FindMethodByName("example.EchoService.Echo") != nullptr);
 }
+
+// Host construction of the GPU pb_scan table ({tag, value} pairs; wire 2
+// values are (offset << 32) | length) for MergeFromFieldTable.
+static std::vector<uint64_t> scan_fields(const std::string& wire) {
+    std::vector<uint64_t> t;
+    CodedInput in(wire.data(), wire.size());
+    for (;;) {
+        const uint32_t tag = in.read_tag();
+        if (tag == 0) break;
+        uint64_t v = 0;
+        switch (tag & 7) {
+        case 0: in.read_varint(&v); break;
+        case 1: in.read_fixed64(&v); break;
+        case 5: {
+            uint32_t x = 0;
+            in.read_fixed32(&x);
+            v = x;
+            break;
+        }
+        case 2: {
+            uint64_t len = 0;
+            const uint8_t* d = nullptr;
+            in.read_varint(&len);
+            in.read_bytes((size_t)len, &d);
+            v = ((uint64_t)(d - (const uint8_t*)wire.data()) << 32) | len;
+            break;
+        }
+        }
+        t.push_back(tag);
+        t.push_back(v);
+    }
+    return t;
+}
+
+TEST(Pb, merge_from_field_table) {
+    Importer imp({});
+    std::string err;
+    ASSERT_TRUE(imp.ImportFromString("t.proto", kTestProto, &err) != nullptr);
+    const Descriptor* d = imp.FindMessageTypeByName("t.All");
+    Message* m = d->prototype->New();
+    Reflection::SetDouble(m, d->FindFieldByName("d"), -2.5);
+    Reflection::SetFloat(m, d->FindFieldByName("f"), 0.75f);
+    Reflection::SetInt32(m, d->FindFieldByName("si32"), -100);
+    Reflection::SetInt64(m, d->FindFieldByName("si64"), -1000000000000LL);
+    Reflection::SetUInt32(m, d->FindFieldByName("f32"), 0xDEADBEEF);
+    Reflection::SetInt32(m, d->FindFieldByName("sf32"), -3);
+    Reflection::SetString(m, d->FindFieldByName("by"), std::string(70000, 'z'));
+    for (int i = 0; i < 40; ++i) Reflection::AddInt32(m, d->FindFieldByName("packed_i32"), i * 1000 - 7);
+    Reflection::AddInt32(m, d->FindFieldByName("unpacked_i32"), -9);
+    Message* in = Reflection::AddMessage(m, d->FindFieldByName("inners"));
+    Reflection::SetInt32(in, in->GetDescriptor()->FindFieldByName("a"), 5);
+    Reflection::AddString(in, in->GetDescriptor()->FindFieldByName("tags"), "t1");
+    Reflection::SetString(m, d->FindFieldByName("name"), "oneof-name");
+    const std::string wire = m->SerializeAsString();
+    const std::vector<uint64_t> table = scan_fields(wire);
+    Message* back = d->prototype->New();
+    ASSERT_TRUE(back->MergeFromFieldTable((const uint8_t*)wire.data(), wire.size(), table.data(),
+                                          (int)table.size() / 2));
+    EXPECT_EQ(back->SerializeAsString(), wire);
+    EXPECT_EQ(Reflection::GetInt64(*back, d->FindFieldByName("si64")), -1000000000000LL);
+    EXPECT_EQ(Reflection::GetFloat(*back, d->FindFieldByName("f")), 0.75f);
+    EXPECT_EQ(Reflection::FieldSize(*back, d->FindFieldByName("packed_i32")), 40);
+    // declines what the table cannot express: ranges past the data, unknown fields
+    std::vector<uint64_t> bad = table;
+    for (size_t i = 0; i < bad.size(); i += 2) {
+        if ((bad[i] & 7) == 2) bad[i + 1] = ((uint64_t)wire.size() << 32) | 1;
+    }
+    Message* b2 = d->prototype->New();
+    EXPECT_FALSE(b2->MergeFromFieldTable((const uint8_t*)wire.data(), wire.size(), bad.data(), (int)bad.size() / 2));
+    const uint64_t unknown[2] = {(99u << 3) | 0, 1};
+    Message* b3 = d->prototype->New();
+    EXPECT_FALSE(b3->MergeFromFieldTable((const uint8_t*)wire.data(), wire.size(), unknown, 1));
+    delete m;
+    delete back;
+    delete b2;
+    delete b3;
+}

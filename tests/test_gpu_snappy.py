@@ -160,6 +160,37 @@ def test_grpc_snappy_bodies_on_gpu():
         # request + response, each compressed and decompressed on the GPU
         assert after["compress_calls"] - before["compress_calls"] >= 400, (before, after)
         assert after["decompress_calls"] - before["decompress_calls"] >= 400, (before, after)
+        # ... and parsed from the pb_scan field table of the decoded bytes
+        assert after["indexed_parses"] - before["indexed_parses"] >= 400, (before, after)
+        assert after["index_fallbacks"] == before["index_fallbacks"], (before, after)
+    finally:
+        native.gpu.disable_snappy()
+        s.stop()
+
+
+def test_baidu_std_snappy_bodies_parsed_from_device_index():
+    """baidu_std bodies with compress_type snappy: decode + pb_scan on the
+    device, fields merged from the table on the host (ParseFromCompressedData
+    path); the echo check compares every response byte."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    native.gpu.enable_snappy(0, 16384)
+    try:
+        before = native.gpu.snappy_stats()
+        p = native.Press({"server": s.address, "protocol": "baidu_std", "concurrency": 8, "request_size": 40000,
+                          "request_compress_type": 1, "check_echo": True})
+        p.run_requests(100)
+        st = p.stats()
+        assert st["success"] == 100 and st["error"] == 0, st
+        after = native.gpu.snappy_stats()
+        assert after["indexed_parses"] - before["indexed_parses"] >= 100, (before, after)
+        # small bodies stay on the CPU codec
+        p2 = native.Press({"server": s.address, "protocol": "baidu_std", "concurrency": 4, "request_size": 1000,
+                           "request_compress_type": 1, "check_echo": True})
+        p2.run_requests(50)
+        assert p2.stats()["success"] == 50
+        assert native.gpu.snappy_stats()["indexed_parses"] == after["indexed_parses"]
     finally:
         native.gpu.disable_snappy()
         s.stop()
