@@ -1,0 +1,138 @@
+// Device half of json2pb for large bodies (the reference parses
+// every http+json body on the CPU, src/json2pb/json_to_pb.cpp): the body is
+// staged into HBM through a pinned bounce buffer, LaunchJsonIndex
+// (gpu/json_kernels.hip) finds every structural position, and the positions
+// come back for json::ParseWithIndex. Two stream-ordered waits per body:
+// one for the count, one for the positions (only count * 4 bytes cross the
+// link).
+#include "gpu/json_offload.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <cstring>
+
+#include "base/time.h"
+#include "gpu/gpu.h"
+#include "gpu/hbm_pool.h"
+#include "gpu/kernels.h"
+#include "json/json2pb.h"
+#include "rpc/span.h"
+#include "var/var.h"
+
+namespace mrpc {
+namespace gpu {
+
+namespace {
+
+int g_device = -1;
+std::atomic<int64_t> g_bodies{0}, g_bytes{0}, g_failures{0};
+
+struct Hbm {
+    void* p = nullptr;
+    size_t n = 0;
+    int dev = -1;
+    Hbm(size_t bytes, int d) : p(HbmAlloc(bytes, d)), n(bytes), dev(d) {}
+    ~Hbm() {
+        if (p) HbmFree(p, n, dev);
+    }
+};
+
+struct Pinned {
+    void* p = nullptr;
+    size_t n = 0;
+    explicit Pinned(size_t bytes) : p(PinnedAlloc(bytes)), n(bytes) {}
+    ~Pinned() {
+        if (p) PinnedFree(p, n);
+    }
+};
+
+bool offload(const char* data, size_t n, std::vector<uint32_t>* index) {
+    if (g_device < 0) return false;
+    Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
+    const int64_t t0 = span ? monotonic_us() : 0;
+    const int rc = JsonIndex(data, n, index, g_device);
+    if (rc != 0) {
+        g_failures.fetch_add(1, std::memory_order_relaxed);
+        return false;  // malformed or no device: the CPU parser reports it
+    }
+    g_bodies.fetch_add(1, std::memory_order_relaxed);
+    g_bytes.fetch_add((int64_t)n, std::memory_order_relaxed);
+    if (span) {
+        span->AnnotateDevice(string_printf("json index %zu B -> %zu positions dev%d", n, index->size(), g_device),
+                             (float)(monotonic_us() - t0) / 1000.0f);
+    }
+    return true;
+}
+
+}  // namespace
+
+int JsonIndex(const char* data, size_t n, std::vector<uint32_t>* out, int device) {
+    out->clear();
+    if (n == 0) return 0;
+    if (n > 0xFFFFFFFFull || device < 0) return -1;
+    // every byte could be a position; the count decides what comes back
+    Hbm in(n, device), pos(n * sizeof(uint32_t), device), scratch(JsonIndexScratchBytes(n), device);
+    Pinned bounce(n), meta(16);
+    if (!in.p || !pos.p || !scratch.p || !bounce.p || !meta.p) return -1;
+    memcpy(bounce.p, data, n);
+    uint64_t* count = static_cast<uint64_t*>(meta.p);
+    int* err = reinterpret_cast<int*>(count + 1);
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    hipStream_t s = PoolStream(device);
+    int rc = -1;
+    if (s) {
+        Segment seg{bounce.p, in.p, n};
+        rc = LaunchBatchedCopy(&seg, 1, s);
+        if (rc == 0) {
+            rc = LaunchJsonIndex(static_cast<const uint8_t*>(in.p), n, static_cast<uint32_t*>(pos.p), n, count, err,
+                                 scratch.p, s);
+        }
+        const int wrc = SyncStream(s);  // never free buffers a launched kernel may still use
+        if (rc == 0) rc = wrc;
+        if (rc == 0 && *err != 0) rc = -1;
+        if (rc == 0 && *count > 0) {
+            const size_t bytes = (size_t)*count * sizeof(uint32_t);
+            Pinned back(bytes);
+            if (!back.p) {
+                rc = -1;
+            } else {
+                Segment seg2{pos.p, back.p, bytes};
+                rc = LaunchBatchedCopy(&seg2, 1, s);
+                const int w2 = SyncStream(s);
+                if (rc == 0) rc = w2;
+                if (rc == 0) {
+                    const uint32_t* p = static_cast<const uint32_t*>(back.p);
+                    out->assign(p, p + *count);
+                }
+            }
+        }
+    }
+    if (prev != device) hipSetDevice(prev);
+    return rc == 0 ? 0 : -1;
+}
+
+int EnableGpuJsonIndex(int device, size_t min_bytes, std::string* error) {
+    if (Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
+    g_device = device;
+    json2pb::SetJsonIndexOffload(offload, min_bytes);
+    static var::PassiveStatus<int64_t> v1("gpu_json_indexed_bodies", [] { return g_bodies.load(); });
+    static var::PassiveStatus<int64_t> v2("gpu_json_indexed_bytes", [] { return g_bytes.load(); });
+    static var::PassiveStatus<int64_t> v3("gpu_json_index_failures", [] { return g_failures.load(); });
+    return 0;
+}
+
+void DisableGpuJsonIndex() { json2pb::SetJsonIndexOffload(nullptr, (size_t)-1); }
+
+GpuJsonStats GetGpuJsonStats() {
+    GpuJsonStats s;
+    s.indexed_bodies = g_bodies.load();
+    s.indexed_bytes = g_bytes.load();
+    s.failures = g_failures.load();
+    return s;
+}
+
+}  // namespace gpu
+}  // namespace mrpc

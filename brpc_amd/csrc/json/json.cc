@@ -157,6 +157,15 @@ namespace {
 class Reader {
 public:
     Reader(const char* p, size_t n) : _p(p), _end(p + n), _begin(p) {}
+    // A structural index (offsets of unescaped quotes and of {}[]:, outside
+    // strings, ascending — gpu/json_kernels.hip): strings end at the next
+    // indexed quote instead of a byte scan. An index that disagrees with the
+    // text is ignored from that point on.
+    void set_index(const uint32_t* idx, size_t n) {
+        _idx = idx;
+        _nidx = n;
+        _k = 0;
+    }
     bool parse(Value* v, std::string* err) {
         skip();
         if (!value(v, 0)) {
@@ -278,42 +287,71 @@ private:
         *out = v;
         return true;
     }
+    // Closing quote of the string opening at _p from the index, or nullptr.
+    const char* indexed_close() {
+        if (!_idx) return nullptr;
+        const size_t at = (size_t)(_p - _begin);
+        while (_k < _nidx && _idx[_k] < at) ++_k;
+        if (_k + 1 >= _nidx || _idx[_k] != at || _idx[_k + 1] >= (size_t)(_end - _begin) ||
+            _begin[_idx[_k + 1]] != '"') {
+            _idx = nullptr;  // stale or foreign index: scan from here on
+            return nullptr;
+        }
+        const char* close = _begin + _idx[_k + 1];
+        _k += 2;
+        return close;
+    }
     bool string(std::string* s) {
+        if (const char* close = indexed_close()) {
+            const char* b = _p + 1;
+            // only trusted when the range holds no quote or backslash: then
+            // `close` is certainly this string's end
+            if (!memchr(b, '\\', (size_t)(close - b)) && !memchr(b, '"', (size_t)(close - b))) {
+                s->append(b, (size_t)(close - b));
+                _p = close + 1;
+                return true;
+            }
+        }
         ++_p;  // opening quote
-        while (_p < _end && *_p != '"') {
-            char c = *_p++;
-            if (c != '\\') {
-                s->push_back(c);
-                continue;
-            }
+        for (;;) {  // runs without escapes or quotes go in one append
+            const char* q = _p;
+            while (q < _end && *q != '"' && *q != '\\') ++q;
+            s->append(_p, (size_t)(q - _p));
+            _p = q;
+            if (_p >= _end || *_p == '"') break;
+            ++_p;  // backslash
             if (_p >= _end) return fail("bad escape");
-            char e = *_p++;
-            switch (e) {
-            case '"': s->push_back('"'); break;
-            case '\\': s->push_back('\\'); break;
-            case '/': s->push_back('/'); break;
-            case 'b': s->push_back('\b'); break;
-            case 'f': s->push_back('\f'); break;
-            case 'n': s->push_back('\n'); break;
-            case 'r': s->push_back('\r'); break;
-            case 't': s->push_back('\t'); break;
-            case 'u': {
-                uint32_t cp;
-                if (!hex4(&cp)) return false;
-                if (cp >= 0xD800 && cp < 0xDC00 && _end - _p >= 6 && _p[0] == '\\' && _p[1] == 'u') {
-                    _p += 2;
-                    uint32_t lo;
-                    if (!hex4(&lo)) return false;
-                    cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
-                }
-                put_utf8(s, cp);
-                break;
-            }
-            default: return fail("bad escape");
-            }
+            if (!escape(s)) return false;
         }
         if (_p >= _end) return fail("unterminated string");
         ++_p;
+        return true;
+    }
+    bool escape(std::string* s) {
+        char e = *_p++;
+        switch (e) {
+        case '"': s->push_back('"'); break;
+        case '\\': s->push_back('\\'); break;
+        case '/': s->push_back('/'); break;
+        case 'b': s->push_back('\b'); break;
+        case 'f': s->push_back('\f'); break;
+        case 'n': s->push_back('\n'); break;
+        case 'r': s->push_back('\r'); break;
+        case 't': s->push_back('\t'); break;
+        case 'u': {
+            uint32_t cp;
+            if (!hex4(&cp)) return false;
+            if (cp >= 0xD800 && cp < 0xDC00 && _end - _p >= 6 && _p[0] == '\\' && _p[1] == 'u') {
+                _p += 2;
+                uint32_t lo;
+                if (!hex4(&lo)) return false;
+                cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            }
+            put_utf8(s, cp);
+            break;
+        }
+        default: return fail("bad escape");
+        }
         return true;
     }
     bool array(Value* v, int depth) {
@@ -377,11 +415,20 @@ private:
     const char* _end;
     const char* _begin;
     std::string _err;
+    const uint32_t* _idx = nullptr;
+    size_t _nidx = 0, _k = 0;
 };
 }  // namespace
 
 bool Parse(const char* data, size_t n, Value* out, std::string* error) {
     Reader r(data, n);
+    return r.parse(out, error);
+}
+
+bool ParseWithIndex(const char* data, size_t n, const uint32_t* index, size_t nindex, Value* out,
+                    std::string* error) {
+    Reader r(data, n);
+    r.set_index(index, nindex);
     return r.parse(out, error);
 }
 

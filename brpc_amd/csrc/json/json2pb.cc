@@ -1,5 +1,6 @@
 #include "json/json2pb.h"
 
+#include <atomic>
 #include <cmath>
 
 #include "base/util.h"
@@ -270,9 +271,25 @@ bool JsonValueToProtoMessage(const json::Value& v, pb::Message* msg, const Json2
     return value_to_msg(v, msg, opt, error);
 }
 
+namespace {
+std::atomic<JsonIndexOffload> g_index_offload{nullptr};
+size_t g_index_min = (size_t)-1;
+}  // namespace
+
+void SetJsonIndexOffload(JsonIndexOffload fn, size_t min_bytes) {
+    g_index_min = min_bytes;
+    g_index_offload.store(fn, std::memory_order_release);
+}
+
 bool JsonToProtoMessage(const std::string& text, pb::Message* msg, const Json2PbOptions& opt, std::string* error) {
     json::Value v;
-    if (!json::Parse(text, &v, error)) return false;
+    JsonIndexOffload off = g_index_offload.load(std::memory_order_acquire);
+    std::vector<uint32_t> index;
+    if (off && text.size() >= g_index_min && off(text.data(), text.size(), &index)) {
+        if (!json::ParseWithIndex(text.data(), text.size(), index.data(), index.size(), &v, error)) return false;
+    } else if (!json::Parse(text, &v, error)) {
+        return false;
+    }
     return value_to_msg(v, msg, opt, error);
 }
 

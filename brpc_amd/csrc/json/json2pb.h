@@ -4,6 +4,7 @@
 #pragma once
 
 #include <string>
+#include <vector>
 
 #include "base/buf.h"
 #include "json/json.h"
@@ -34,6 +35,12 @@ bool JsonToProtoMessage(const std::string& json, pb::Message* msg, const Json2Pb
 bool JsonToProtoMessage(const Buf& json, pb::Message* msg, const Json2PbOptions& opt = Json2PbOptions(),
                         std::string* error = nullptr);
 bool JsonValueToProtoMessage(const json::Value& v, pb::Message* msg, const Json2PbOptions& opt, std::string* error);
+
+// Hook for a structural index of large bodies built on the GPU
+// (gpu/json_offload.cc, kernel K6): fills *index for data[0, n) and returns
+// true, or false to parse without one. Bodies of at least min_bytes use it.
+typedef bool (*JsonIndexOffload)(const char* data, size_t n, std::vector<uint32_t>* index);
+void SetJsonIndexOffload(JsonIndexOffload fn, size_t min_bytes);
 
 }  // namespace json2pb
 }  // namespace mrpc

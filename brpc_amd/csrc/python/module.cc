@@ -15,6 +15,9 @@
 #include "rpc/compress.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/snappy_offload.h"
+#include "gpu/json_offload.h"
+#include "json/json2pb.h"
+#include "pb/descriptor.h"
 #include "gpu/xgmi.h"
 #include "mrpc/proto/echo.pb.h"
 #include "base/time.h"
@@ -328,6 +331,23 @@ PYBIND11_MODULE(_native, m) {
     });
     // The body codec registry (rpc/compress.h) exactly as protocols call it:
     // a registered offload (GPU snappy) applies here too.
+    // json2pb round trip through a generated message type: JSON text ->
+    // message (json2pb, with the GPU index when enabled and large enough)
+    // -> JSON text. Raises with the parser's error.
+    m.def("json_to_pb_to_json", [](const std::string& type_name, py::bytes text) {
+        const pb::Descriptor* d = pb::DescriptorPool::generated_pool()->FindMessageTypeByName(type_name);
+        if (!d || !d->prototype) throw std::invalid_argument("unknown message type " + type_name);
+        std::unique_ptr<pb::Message> msg(d->prototype->New());
+        std::string in = text, err, out;
+        bool ok;
+        {
+            py::gil_scoped_release nogil;
+            ok = json2pb::JsonToProtoMessage(in, msg.get(), json2pb::Json2PbOptions(), &err) &&
+                 json2pb::ProtoMessageToJson(*msg, &out, json2pb::Pb2JsonOptions(), &err);
+        }
+        if (!ok) throw std::runtime_error(err);
+        return out;
+    });
     m.def("compress", [](int type, py::bytes b) {
         std::string s = b;
         Buf in(s), out;
@@ -439,6 +459,31 @@ PYBIND11_MODULE(_native, m) {
         d["index_fallbacks"] = s.index_fallbacks;
         return d;
     });
+    g.def("enable_json_index", [](int dev, size_t min_bytes) {
+        std::string err;
+        if (gpu::EnableGpuJsonIndex(dev, min_bytes, &err) != 0) throw std::runtime_error(err);
+    }, py::arg("device") = 0, py::arg("min_bytes") = 65536);
+    g.def("disable_json_index", [] { gpu::DisableGpuJsonIndex(); });
+    g.def("json_stats", [] {
+        const gpu::GpuJsonStats s = gpu::GetGpuJsonStats();
+        py::dict d;
+        d["indexed_bodies"] = s.indexed_bodies;
+        d["indexed_bytes"] = s.indexed_bytes;
+        d["failures"] = s.failures;
+        return d;
+    });
+    // host bytes -> structural positions through the device (tests)
+    g.def("json_index_bytes", [](py::bytes b, int dev) {
+        std::string data = b;
+        std::vector<uint32_t> pos;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::JsonIndex(data.data(), data.size(), &pos, dev);
+        }
+        if (rc != 0) throw std::runtime_error("json index failed (device error or unterminated string)");
+        return pos;
+    }, py::arg("data"), py::arg("device") = 0);
     g.def("hbm_pool_stats", [](int dev) {
         const gpu::HbmPoolStats s = gpu::GetHbmPoolStats(dev);
         py::dict d;

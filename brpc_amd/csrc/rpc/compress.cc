@@ -3,6 +3,7 @@
 #include <zlib.h>
 
 #include <atomic>
+#include <mutex>
 
 #include "base/logging.h"
 #include "base/snappy.h"
@@ -117,6 +118,7 @@ int RegisterCompressHandler(CompressType type, const CompressHandler& h) {
 
 const CompressHandler* FindCompressHandler(CompressType type) {
     if ((int)type <= 0 || (int)type >= 16) return nullptr;
+    RegisterBuiltinCompressHandlers();  // usable before any server or channel exists
     return g_handlers[type].Compress ? &g_handlers[type] : nullptr;
 }
 
@@ -127,24 +129,24 @@ const char* CompressTypeToCStr(CompressType type) {
 }
 
 void RegisterBuiltinCompressHandlers() {
-    static bool done = false;
-    if (done) return;
-    done = true;
-    CompressHandler sh;
-    sh.Compress = snappy_compress;
-    sh.Decompress = snappy_decompress;
-    sh.name = "snappy";
-    RegisterCompressHandler(COMPRESS_TYPE_SNAPPY, sh);
-    CompressHandler gh;
-    gh.Compress = gzip_compress;
-    gh.Decompress = gzip_decompress;
-    gh.name = "gzip";
-    RegisterCompressHandler(COMPRESS_TYPE_GZIP, gh);
-    CompressHandler zh;
-    zh.Compress = zlib_compress;
-    zh.Decompress = zlib_decompress;
-    zh.name = "zlib";
-    RegisterCompressHandler(COMPRESS_TYPE_ZLIB, zh);
+    static std::once_flag once;
+    std::call_once(once, [] {
+        CompressHandler sh;
+        sh.Compress = snappy_compress;
+        sh.Decompress = snappy_decompress;
+        sh.name = "snappy";
+        RegisterCompressHandler(COMPRESS_TYPE_SNAPPY, sh);
+        CompressHandler gh;
+        gh.Compress = gzip_compress;
+        gh.Decompress = gzip_decompress;
+        gh.name = "gzip";
+        RegisterCompressHandler(COMPRESS_TYPE_GZIP, gh);
+        CompressHandler zh;
+        zh.Compress = zlib_compress;
+        zh.Decompress = zlib_decompress;
+        zh.name = "zlib";
+        RegisterCompressHandler(COMPRESS_TYPE_ZLIB, zh);
+    });
 }
 
 bool CompressBuf(CompressType type, const Buf& in, Buf* out) {

@@ -581,6 +581,54 @@ TEST(JsonUnit, malformed_inputs) {
     EXPECT_TRUE(v.is_array());
 }
 
+// Host structural index with the kernel's semantics (gpu/json_kernels.hip).
+static std::vector<uint32_t> json_index_ref(const std::string& t) {
+    std::vector<uint32_t> out;
+    bool in_str = false, esc = false;
+    for (size_t i = 0; i < t.size(); ++i) {
+        const char c = t[i];
+        const bool escaped = esc;
+        esc = c == '\\' && !esc;
+        if (c == '"' && !escaped) {
+            in_str = !in_str;
+            out.push_back((uint32_t)i);
+        } else if (!in_str && strchr("{}[]:,", c) && c) {
+            out.push_back((uint32_t)i);
+        }
+    }
+    return out;
+}
+
+TEST(JsonUnit, parse_with_structural_index) {
+    std::string doc = "{\"k\":[";
+    for (int i = 0; i < 300; ++i) {
+        if (i) doc += ",";
+        doc += "{\"s\":\"" + std::string(i % 50, 'x') + (i % 7 == 0 ? "\\\"q\\\\" : "") + "\",\"n\":" +
+               std::to_string(i * 1.5) + ",\"b\":" + (i % 2 ? "true" : "null") + "}";
+    }
+    doc += "],\"t\":\"tail \\u00e9\"}";
+    json::Value plain, indexed, wrong;
+    std::string err;
+    ASSERT_TRUE(json::Parse(doc, &plain, &err));
+    const std::vector<uint32_t> idx = json_index_ref(doc);
+    ASSERT_TRUE(json::ParseWithIndex(doc.data(), doc.size(), idx.data(), idx.size(), &indexed, &err));
+    EXPECT_EQ(indexed.ToString(), plain.ToString());
+    EXPECT_EQ(indexed.find("k")->size(), 300u);
+    // a wrong index never changes the result: shifted positions, dropped ones
+    std::vector<uint32_t> bad = idx;
+    for (size_t i = 5; i < bad.size(); i += 3) bad[i] += 1;
+    ASSERT_TRUE(json::ParseWithIndex(doc.data(), doc.size(), bad.data(), bad.size(), &wrong, &err));
+    EXPECT_EQ(wrong.ToString(), plain.ToString());
+    std::vector<uint32_t> sparse;
+    for (size_t i = 0; i < idx.size(); i += 2) sparse.push_back(idx[i]);
+    ASSERT_TRUE(json::ParseWithIndex(doc.data(), doc.size(), sparse.data(), sparse.size(), &wrong, &err));
+    EXPECT_EQ(wrong.ToString(), plain.ToString());
+    // malformed input is still reported
+    const std::string broken = doc.substr(0, doc.size() - 3);
+    const std::vector<uint32_t> bidx = json_index_ref(broken);
+    EXPECT_FALSE(json::ParseWithIndex(broken.data(), broken.size(), bidx.data(), bidx.size(), &wrong, &err));
+}
+
 TEST(JsonUnit, object_order_and_escaping) {
     json::Value o = json::Value::Object();
     o.set("z", json::Value(1));

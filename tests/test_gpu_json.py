@@ -129,3 +129,55 @@ def test_unaligned_view_and_errors(dev):
         json_index(torch.frombuffer(bytearray(b"[1,2,3,4]"), dtype=torch.uint8).to(dev), max_positions=3)
     with pytest.raises(ValueError):
         json_index(torch.zeros(4, dtype=torch.uint8))
+
+
+def _echo_doc(n):
+    # an example.EchoRequest as JSON whose message is long and escape-heavy
+    body = ("plain text run " * 40 + 'q"uote \\ back\\slash é 中 ') * n
+    return json.dumps({"message": body, "sleep_us": 7, "server_fail": False}).encode(), body
+
+
+def test_json2pb_round_trip_cpu():
+    from brpc_amd import native
+    text, body = _echo_doc(3)
+    out = json.loads(native.json_to_pb_to_json("example.EchoRequest", text))
+    assert out["message"] == body and out["sleep_us"] == 7
+    with pytest.raises(RuntimeError):
+        native.json_to_pb_to_json("example.EchoRequest", text[:-5])
+
+
+@pytest.mark.gpu
+def test_json_index_bytes_matches_host(dev):
+    from brpc_amd import native
+    rnd = random.Random(9)
+    text = json.dumps([_doc(rnd) for _ in range(300)]).encode()
+    assert native.gpu.json_index_bytes(text, 0) == json_index_host(text)[0]
+    with pytest.raises(RuntimeError):
+        native.gpu.json_index_bytes(b'{"open', 0)
+
+
+@pytest.mark.gpu
+def test_json2pb_uses_device_index_for_large_bodies(dev):
+    """json2pb with the device index installed: bodies at or above the
+    threshold are indexed on the GPU (stats move) and parse to exactly what
+    the CPU-only parser produces; smaller bodies stay on the CPU."""
+    from brpc_amd import native
+    text, body = _echo_doc(400)  # ~400 KiB
+    small, _ = _echo_doc(1)
+    cpu_big = native.json_to_pb_to_json("example.EchoRequest", text)
+    native.gpu.enable_json_index(0, 65536)
+    try:
+        s0 = native.gpu.json_stats()
+        assert native.json_to_pb_to_json("example.EchoRequest", text) == cpu_big
+        s1 = native.gpu.json_stats()
+        assert s1["indexed_bodies"] == s0["indexed_bodies"] + 1 and s1["indexed_bytes"] - s0["indexed_bytes"] == len(text)
+        assert json.loads(cpu_big)["message"] == body
+        native.json_to_pb_to_json("example.EchoRequest", small)
+        assert native.gpu.json_stats()["indexed_bodies"] == s1["indexed_bodies"]
+        # malformed large body (cut inside the message string): the device
+        # reports the open string, the CPU parser reports the error
+        with pytest.raises(RuntimeError):
+            native.json_to_pb_to_json("example.EchoRequest", text[:100000])
+        assert native.gpu.json_stats()["failures"] == s1["failures"] + 1
+    finally:
+        native.gpu.disable_json_index()
