@@ -275,11 +275,14 @@ def main():
         if cuda:
             native.gpu.enable_snappy(topo.device, 16384)
             try:
-                z0 = native.gpu.snappy_stats()
+                z0, b0 = native.gpu.snappy_stats(), native.gpu.codec_batch_stats()
                 rz["gpu"] = timed_leg(wlz, a.steps, a.warmup, dict(oz))
-                z1 = native.gpu.snappy_stats()
+                z1, b1 = native.gpu.snappy_stats(), native.gpu.codec_batch_stats()
                 # bodies decoded + pb_scan-indexed on the GPU, merged from the field table
                 rz["gpu"]["indexed_parses"] = z1["indexed_parses"] - z0["indexed_parses"]
+                # codec requests of concurrent RPCs share launch sequences
+                nl = b1["launches"] - b0["launches"]
+                rz["gpu"]["codec_requests_per_launch"] = round((b1["requests"] - b0["requests"]) / nl, 2) if nl else 0
             finally:
                 native.gpu.disable_snappy()
 
@@ -473,6 +476,7 @@ def main():
                 out["grpc_snappy_64KB_qps_gpu_codec"] = round(rz["gpu"]["qps"], 1)
                 out["grpc_snappy_64KB_p99_us_gpu_codec"] = rz["gpu"]["p99_us"]
                 out["grpc_gpu_codec_indexed_parses"] = rz["gpu"]["indexed_parses"]
+                out["grpc_gpu_codec_requests_per_launch"] = rz["gpu"]["codec_requests_per_launch"]
                 out["grpc_snappy_errors"] = rz["cpu"]["errors"] + rz["gpu"]["errors"]
         if rg:
             out["qps_64KB_gpu_handler"] = round(rg["qps"], 1)

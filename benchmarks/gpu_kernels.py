@@ -109,7 +109,8 @@ def main():
     del pbbuf, pboffs, fields, nf
     torch.cuda.empty_cache()
 
-    # snappy: 128 MiB of mixed (~2:1) data as 2048 x 64 KiB and 4096 x 32 KiB
+    # snappy: 128 MiB of mixed (~2:1) data as 2048 x 64 KiB, 4096 x 32 KiB and
+    # 32768 x 4 KiB (the RPC offload's block)
     # blocks. "sec" is kernel time only (CUDA events around launches with the
     # job tables already on the device); the python wrappers add host work.
     from brpc_amd import native
@@ -136,7 +137,7 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / 1e3 / iters
 
-    for block in (65536, 32768):
+    for block in (65536, 32768, 4096):
         n = total // block
         # host codec blocks -> device decompression
         comps = [native.snappy_compress(raw[i * block:(i + 1) * block]) for i in range(n)]
@@ -173,7 +174,7 @@ def main():
         for i in range(n):
             cj += [raw_dev.data_ptr() + i * block, slots.data_ptr() + i * cap, block, cap]
         cj_dev = torch.tensor(cj, dtype=torch.int64, device=dev)
-        t = kernel_time(lambda: native.gpu.snappy_compress_launch(cj_dev.data_ptr(), n, scratch.data_ptr(),
+        t = kernel_time(lambda: native.gpu.snappy_compress_launch(cj_dev.data_ptr(), n, block, scratch.data_ptr(),
                                                                   meta.data_ptr(), meta.data_ptr() + 4 * n, st))
         print(json.dumps({"kernel": "snappy_compress", "block": block, "blocks": n, "bytes_in": total,
                           "bytes_out": int(sum(gsizes)), "host_codec_bytes_out": len(packed), "sec": t,

@@ -1,0 +1,224 @@
+#include "gpu/codec_batch.h"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+
+#include "base/logging.h"
+#include "fiber/butex.h"
+#include "gpu/gpu.h"
+#include "gpu/hbm_pool.h"
+
+namespace mrpc {
+namespace gpu {
+
+namespace {
+
+const int kMaxDev = 16;
+
+// A pinned host array the kernels read (job tables) or write (results);
+// grows, never shrinks, owned by one batch.
+template <typename T>
+struct PinnedArray {
+    T* p = nullptr;
+    size_t cap = 0;
+    bool reserve(size_t n) {
+        if (n <= cap) return true;
+        if (p) PinnedFree(p, cap * sizeof(T));
+        cap = std::max<size_t>(n, 64);
+        p = static_cast<T*>(PinnedAlloc(cap * sizeof(T)));
+        if (!p) cap = 0;
+        return p != nullptr;
+    }
+};
+
+struct CBatch {
+    std::vector<CodecRequest*> reqs;
+    std::vector<size_t> comp_first, decomp_first, scan_row;
+    PinnedArray<SnappyJob> comp_jobs, decomp_jobs;
+    PinnedArray<uint32_t> comp_len, decomp_len;
+    PinnedArray<int> comp_err, decomp_err;
+    PinnedArray<PbScanJob> scan_jobs;
+    PinnedArray<uint64_t> scan_fields;
+    PinnedArray<int32_t> scan_n;
+    void* scratch = nullptr;  // compress slots of blocks above 16 KiB
+    size_t scratch_bytes = 0;
+    std::atomic<int>* butex = nullptr;
+    hipEvent_t ev = nullptr;
+    std::atomic<int> refs{0};
+};
+
+struct Engine {
+    std::mutex mu;
+    CBatch* open = nullptr;
+    bool launching = false;
+    std::vector<CBatch*> spare;
+};
+
+Engine g_engine[kMaxDev];
+std::atomic<int64_t> g_requests{0}, g_launches{0};
+
+CBatch* new_batch(Engine& e) {
+    if (!e.spare.empty()) {
+        CBatch* b = e.spare.back();
+        e.spare.pop_back();
+        return b;
+    }
+    CBatch* b = new CBatch;
+    b->butex = fiber::butex_create();
+    return b;
+}
+
+// Lay the batch's requests out in its pinned tables and issue one stream
+// sequence; false when nothing could be launched.
+bool launch(CBatch* b, int device) {
+    size_t ncomp = 0, ndecomp = 0, nscan = 0;
+    uint32_t comp_max = 1, decomp_max = 1;
+    std::vector<Segment> h2d, d2h;
+    b->comp_first.clear();
+    b->decomp_first.clear();
+    b->scan_row.clear();
+    for (CodecRequest* r : b->reqs) {
+        b->comp_first.push_back(ncomp);
+        b->decomp_first.push_back(ndecomp);
+        b->scan_row.push_back(r->want_scan ? nscan : (size_t)-1);
+        ncomp += r->comp.size();
+        ndecomp += r->decomp.size();
+        nscan += r->want_scan ? 1 : 0;
+        comp_max = std::max(comp_max, r->comp_max_ulen);
+        decomp_max = std::max(decomp_max, r->decomp_max_ulen);
+        h2d.insert(h2d.end(), r->h2d.begin(), r->h2d.end());
+        d2h.insert(d2h.end(), r->d2h.begin(), r->d2h.end());
+    }
+    if (!b->comp_jobs.reserve(ncomp) || !b->comp_len.reserve(ncomp) || !b->comp_err.reserve(ncomp) ||
+        !b->decomp_jobs.reserve(ndecomp) || !b->decomp_len.reserve(ndecomp) || !b->decomp_err.reserve(ndecomp) ||
+        !b->scan_jobs.reserve(nscan) || !b->scan_fields.reserve(nscan * 2 * kCodecScanFields) ||
+        !b->scan_n.reserve(nscan)) {
+        return false;
+    }
+    for (size_t i = 0; i < b->reqs.size(); ++i) {
+        const CodecRequest* r = b->reqs[i];
+        std::copy(r->comp.begin(), r->comp.end(), b->comp_jobs.p + b->comp_first[i]);
+        std::copy(r->decomp.begin(), r->decomp.end(), b->decomp_jobs.p + b->decomp_first[i]);
+        if (r->want_scan) b->scan_jobs.p[b->scan_row[i]] = r->scan;
+    }
+    if (ncomp && SnappyCompressUsesScratch(comp_max)) {
+        const size_t need = ncomp * SnappyCompressScratchPerBlock();
+        if (need > b->scratch_bytes) {
+            if (b->scratch) HbmFree(b->scratch, b->scratch_bytes, device);
+            b->scratch = HbmAlloc(need, device);
+            b->scratch_bytes = b->scratch ? need : 0;
+        }
+        if (!b->scratch) return false;
+    }
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    hipStream_t s = PoolStream(device);
+    b->ev = AcquireEvent();
+    int rc = (s && b->ev) ? 0 : -1;
+    if (rc == 0 && !h2d.empty()) rc = LaunchBatchedCopy(h2d.data(), (int)h2d.size(), s);
+    if (rc == 0 && ncomp) {
+        rc = LaunchSnappyCompress(b->comp_jobs.p, (int)ncomp, comp_max, b->scratch, b->comp_len.p, b->comp_err.p, s);
+    }
+    if (rc == 0 && ndecomp) {
+        rc = LaunchSnappyDecompress(b->decomp_jobs.p, (int)ndecomp, decomp_max, b->decomp_len.p, b->decomp_err.p, s);
+    }
+    if (rc == 0 && nscan) {
+        rc = LaunchPbScanPtrs(b->scan_jobs.p, (int64_t)nscan, kCodecScanFields, b->scan_fields.p, b->scan_n.p, s);
+    }
+    if (rc == 0 && !d2h.empty()) rc = LaunchBatchedCopy(d2h.data(), (int)d2h.size(), s);
+    if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
+    if (prev != device) hipSetDevice(prev);
+    g_launches.fetch_add(1, std::memory_order_relaxed);
+    if (rc != 0) {
+        // kernels already queued may still read the tables: wait them out
+        // before anyone frees request buffers
+        if (s) SyncStream(s);
+        return false;
+    }
+    WatchEvent(b->ev, b->butex);
+    return true;
+}
+
+}  // namespace
+
+int RunCodecRequest(CodecRequest* r, int device) {
+    if (device < 0 || device >= kMaxDev || Init(device) != 0) return -1;
+    Engine& e = g_engine[device];
+    g_requests.fetch_add(1, std::memory_order_relaxed);
+    CBatch* mine;
+    size_t idx = 0;
+    bool leader = false;
+    {
+        std::lock_guard<std::mutex> g(e.mu);
+        if (!e.open) {
+            e.open = new_batch(e);
+            e.open->butex->store(0, std::memory_order_relaxed);
+        }
+        mine = e.open;
+        idx = mine->reqs.size();
+        mine->reqs.push_back(r);
+        mine->refs.fetch_add(1, std::memory_order_relaxed);
+        if (!e.launching) {
+            e.launching = true;
+            leader = true;
+        }
+    }
+    if (leader) {
+        for (;;) {
+            CBatch* cur;
+            {
+                std::lock_guard<std::mutex> g(e.mu);
+                cur = e.open;
+                e.open = nullptr;
+                if (!cur) {
+                    e.launching = false;
+                    break;
+                }
+            }
+            if (!launch(cur, device)) {
+                LOG_EVERY_SECOND(ERROR) << "codec batch of " << cur->reqs.size() << " requests failed on device "
+                                        << device;
+                cur->butex->store(-1, std::memory_order_release);
+                fiber::butex_wake_all(cur->butex);
+            }
+        }
+    }
+    while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
+    const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
+    if (rc == 0) {
+        const size_t c0 = mine->comp_first[idx], d0 = mine->decomp_first[idx];
+        r->comp_len.assign(mine->comp_len.p + c0, mine->comp_len.p + c0 + r->comp.size());
+        r->comp_err.assign(mine->comp_err.p + c0, mine->comp_err.p + c0 + r->comp.size());
+        r->decomp_len.assign(mine->decomp_len.p + d0, mine->decomp_len.p + d0 + r->decomp.size());
+        r->decomp_err.assign(mine->decomp_err.p + d0, mine->decomp_err.p + d0 + r->decomp.size());
+        if (r->want_scan) {
+            const size_t row = mine->scan_row[idx];
+            const uint64_t* f = mine->scan_fields.p + row * 2 * kCodecScanFields;
+            r->scan_nfields = mine->scan_n.p[row];
+            r->scan_fields.assign(f, f + 2 * kCodecScanFields);
+        }
+    }
+    if (mine->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        if (mine->ev) ReleaseEvent(mine->ev);
+        mine->ev = nullptr;
+        mine->reqs.clear();
+        std::lock_guard<std::mutex> g(e.mu);
+        e.spare.push_back(mine);
+    }
+    return rc;
+}
+
+CodecBatchStats GetCodecBatchStats() {
+    CodecBatchStats s;
+    s.requests = g_requests.load(std::memory_order_relaxed);
+    s.launches = g_launches.load(std::memory_order_relaxed);
+    return s;
+}
+
+}  // namespace gpu
+}  // namespace mrpc

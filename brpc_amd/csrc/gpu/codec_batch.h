@@ -1,0 +1,50 @@
+// Cross-request batching of the device body codecs (snappy compress /
+// decompress, pb_scan) — the same leader-combining scheme as the copy
+// engine (gpu/copy_engine.h): concurrent RPCs submit their codec work, one
+// submitter becomes the leader and issues everything that accumulated as ONE
+// sequence on one stream (staging copies, one compress launch, one
+// decompress launch, one pb_scan launch, copies back) with ONE event; every
+// submitter parks its fiber on that event. At 50 RPCs in flight this turns
+// ~4 launches + 1 event per body into a few per batch of bodies.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "gpu/kernels.h"
+
+namespace mrpc {
+namespace gpu {
+
+struct CodecRequest {
+    // staging copies issued before the codec kernels (host/pinned -> HBM)
+    std::vector<Segment> h2d;
+    // codec jobs; pointers in the jobs are device-accessible
+    std::vector<SnappyJob> comp, decomp;
+    uint32_t comp_max_ulen = 0, decomp_max_ulen = 0;
+    // optional wire scan of one decoded message (kCodecScanFields rows)
+    bool want_scan = false;
+    PbScanJob scan{nullptr, 0};
+    // copies issued after the kernels (HBM -> pinned)
+    std::vector<Segment> d2h;
+
+    // results, filled before RunCodecRequest returns 0
+    std::vector<uint32_t> comp_len, decomp_len;
+    std::vector<int> comp_err, decomp_err;
+    std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields
+    int32_t scan_nfields = -1;
+};
+
+constexpr uint32_t kCodecScanFields = 128;
+
+// Blocks the calling fiber until the batch holding `r` completed; 0 on
+// success (per-job codes in the result vectors), -1 on a device error.
+int RunCodecRequest(CodecRequest* r, int device);
+
+struct CodecBatchStats {
+    int64_t requests = 0, launches = 0;
+};
+CodecBatchStats GetCodecBatchStats();
+
+}  // namespace gpu
+}  // namespace mrpc

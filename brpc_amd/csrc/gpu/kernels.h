@@ -75,8 +75,14 @@ int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, 
 constexpr uint32_t SnappyCompressSlot() { return ((kSnappyMaxBlock / 64) + 32 + 63) & ~63u; }
 constexpr uint64_t SnappyCompressScratchPerBlock() { return 64ull * SnappyCompressSlot(); }
 constexpr uint64_t SnappyMaxCompressedLength(uint64_t n) { return 32 + n + n / 6; }
-int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, void* scratch, uint32_t* out_len_dev, int* err_dev,
-                         hipStream_t s);
+// max_ulen (>= every job's src_len) sizes the LDS: the block is staged in
+// LDS, and blocks up to 16 KiB keep their output slots there too (scratch
+// is then unused).
+int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch, uint32_t* out_len_dev,
+                         int* err_dev, hipStream_t s);
+// Whether a launch with this max_ulen writes the global scratch (blocks
+// above 16 KiB); otherwise scratch may be null.
+constexpr bool SnappyCompressUsesScratch(uint32_t max_ulen) { return max_ulen > 16384; }
 
 // Batched protobuf wire scan (gpu/pb_kernels.hip): message i is
 // buf[offsets[i], offsets[i+1]); its top-level fields land in
@@ -85,6 +91,14 @@ int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, void* scratch, uint32
 // (-5: the offsets of message i leave [0, buf_len) or descend).
 int LaunchPbScan(const uint8_t* buf, uint64_t buf_len, const int64_t* offsets_dev, int64_t n, uint32_t max_fields,
                  uint64_t* fields, int32_t* nfields, hipStream_t s);
+// Same scan for messages in separate buffers: job i is buf[0, len) (device
+// or device-readable pinned table).
+struct PbScanJob {
+    const uint8_t* buf;
+    uint64_t len;
+};
+int LaunchPbScanPtrs(const PbScanJob* jobs, int64_t n, uint32_t max_fields, uint64_t* fields, int32_t* nfields,
+                     hipStream_t s);
 
 // JSON structural index (gpu/json_kernels.hip): out_pos receives, in order,
 // the byte offsets of every unescaped '"' and of every { } [ ] : , outside

@@ -40,22 +40,10 @@ __device__ __forceinline__ bool read_varint(gbyte_c* b, uint64_t& p, uint64_t en
     return false;
 }
 
-__global__ void __launch_bounds__(256) pb_scan_kernel(const uint8_t* __restrict__ buf_,
-                                                      uint64_t buf_len, const int64_t* __restrict__ offsets,
-                                                      int64_t n, uint32_t max_fields, uint64_t* __restrict__ fields,
-                                                      int32_t* __restrict__ nfields) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    gbyte_c* b = (gbyte_c*)buf_;
-    const int64_t so = offsets[i], eo = offsets[i + 1];
-    // never trust the offset table: a message must lie inside the buffer
-    if (so < 0 || eo < so || (uint64_t)eo > buf_len) {
-        nfields[i] = -5;
-        return;
-    }
-    const uint64_t start = (uint64_t)so;
-    const uint64_t end = (uint64_t)eo;
-    uint64_t* row = fields + (uint64_t)i * max_fields * 2;
+// Walks one message b[start, end) into row (max_fields {tag, value} pairs);
+// returns the field count or a negative code.
+__device__ __forceinline__ int32_t scan_message(gbyte_c* b, uint64_t start, uint64_t end, uint64_t* row,
+                                                uint32_t max_fields) {
     uint64_t p = start;
     int32_t k = 0;
     int32_t status = 0;
@@ -107,7 +95,36 @@ __global__ void __launch_bounds__(256) pb_scan_kernel(const uint8_t* __restrict_
         *reinterpret_cast<u64x2*>(row + 2 * k) = v;
         ++k;
     }
-    nfields[i] = status ? status : k;
+    return status ? status : k;
+}
+
+__global__ void __launch_bounds__(256) pb_scan_kernel(const uint8_t* __restrict__ buf_,
+                                                      uint64_t buf_len, const int64_t* __restrict__ offsets,
+                                                      int64_t n, uint32_t max_fields, uint64_t* __restrict__ fields,
+                                                      int32_t* __restrict__ nfields) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    gbyte_c* b = (gbyte_c*)buf_;
+    const int64_t so = offsets[i], eo = offsets[i + 1];
+    // never trust the offset table: a message must lie inside the buffer
+    if (so < 0 || eo < so || (uint64_t)eo > buf_len) {
+        nfields[i] = -5;
+        return;
+    }
+    const uint64_t start = (uint64_t)so;
+    const uint64_t end = (uint64_t)eo;
+    nfields[i] = scan_message(b, start, end, fields + (uint64_t)i * max_fields * 2, max_fields);
+}
+
+// Messages in separate buffers (one per job): the batched codec path, where
+// every request decoded its body into its own HBM block.
+__global__ void __launch_bounds__(256) pb_scan_ptrs_kernel(const PbScanJob* __restrict__ jobs, int64_t n,
+                                                           uint32_t max_fields, uint64_t* __restrict__ fields,
+                                                           int32_t* __restrict__ nfields) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const PbScanJob job = jobs[i];
+    nfields[i] = scan_message((gbyte_c*)job.buf, 0, job.len, fields + (uint64_t)i * max_fields * 2, max_fields);
 }
 
 }  // namespace
@@ -119,6 +136,16 @@ int LaunchPbScan(const uint8_t* buf, uint64_t buf_len, const int64_t* offsets_de
     const int64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(pb_scan_kernel, dim3((unsigned)blocks), dim3(256), 0, s, buf, buf_len, offsets_dev, n,
                        max_fields, fields, nfields);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int LaunchPbScanPtrs(const PbScanJob* jobs, int64_t n, uint32_t max_fields, uint64_t* fields, int32_t* nfields,
+                     hipStream_t s) {
+    if (n <= 0) return 0;
+    if (max_fields == 0) return -1;
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(pb_scan_ptrs_kernel, dim3((unsigned)blocks), dim3(256), 0, s, jobs, n, max_fields, fields,
+                       nfields);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

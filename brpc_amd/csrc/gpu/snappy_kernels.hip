@@ -23,7 +23,9 @@
 // LDS instructions of one wave execute in order, so consecutive elements
 // need no wait between them.
 //
-// Compression splits a block into 64 contiguous segments, one per lane; each
+// Compression first stages the block in LDS (coalesced 16-byte loads), so
+// the lanes' serial match loops probe LDS instead of waiting on HBM for
+// every position, then splits it into 64 contiguous segments, one per lane; each
 // lane runs a greedy hash matcher with snappy's skip heuristic over
 // incompressible runs and emits literal / copy elements into its own scratch
 // slot. Candidates come from two LDS tables: a 128-entry u16 table per lane
@@ -36,7 +38,9 @@
 // concatenation of the 64 slots (placed by a prefix sum behind the varint
 // header, copied out coalesced) is a valid snappy stream any decoder
 // accepts; its size lands within ~10% of the CPU codec's on repetitive
-// data. 32 KiB of LDS per wave: 5 waves per CU. (A/B on the MI355X: 32-bit
+// data. Blocks up to 16 KiB also keep the output slots in LDS (a lane's
+// output never exceeds its segment plus one literal header); 4 KiB blocks
+// take 42 KiB of LDS per wave, 3 waves per CU. (A/B on the MI355X: 32-bit
 // (position, fingerprint) entries that skip most verification loads ran
 // slower — 48 KiB/wave drops to 3 waves per CU; a double-buffered window
 // prefetch in the decompressor also lost to the single re-centred window.)
@@ -221,7 +225,8 @@ __device__ __forceinline__ uint64_t load64(gbyte_c* p) {
     return *reinterpret_cast<const __attribute__((address_space(1))) u64_unaligned*>(p);
 }
 
-__device__ __forceinline__ gbyte* emit_literal(gbyte* o, gbyte_c* src, uint32_t len) {
+template <typename O, typename S>
+__device__ __forceinline__ O emit_literal(O o, S src, uint32_t len) {
     const uint32_t n = len - 1;
     if (n < 60) {
         *o++ = (uint8_t)(n << 2);
@@ -237,7 +242,8 @@ __device__ __forceinline__ gbyte* emit_literal(gbyte* o, gbyte_c* src, uint32_t 
     return o + len;
 }
 
-__device__ __forceinline__ gbyte* emit_copy2(gbyte* o, uint32_t off, uint32_t len) {
+template <typename O>
+__device__ __forceinline__ O emit_copy2(O o, uint32_t off, uint32_t len) {
     o[0] = (uint8_t)(((len - 1) << 2) | 2);
     o[1] = (uint8_t)off;
     o[2] = (uint8_t)(off >> 8);
@@ -246,7 +252,8 @@ __device__ __forceinline__ gbyte* emit_copy2(gbyte* o, uint32_t off, uint32_t le
 
 // Same split as snappy's encoder: 64-byte pieces, a 60 so the tail stays
 // >= 4, and the 2-byte copy-1 form for short, near matches.
-__device__ __forceinline__ gbyte* emit_copy(gbyte* o, uint32_t off, uint32_t len) {
+template <typename O>
+__device__ __forceinline__ O emit_copy(O o, uint32_t off, uint32_t len) {
     while (len >= 68) {
         o = emit_copy2(o, off, 64);
         len -= 64;
@@ -263,27 +270,56 @@ __device__ __forceinline__ gbyte* emit_copy(gbyte* o, uint32_t off, uint32_t len
     return emit_copy2(o, off, len);
 }
 
+typedef __attribute__((address_space(3))) uint8_t lbyte;
+__device__ __forceinline__ uint32_t lload32(const lbyte* p) {
+    typedef uint32_t __attribute__((aligned(1))) u32u;
+    return *reinterpret_cast<const __attribute__((address_space(3))) u32u*>(p);
+}
+__device__ __forceinline__ uint64_t lload64(const lbyte* p) {
+    typedef uint64_t __attribute__((aligned(1))) u64u;
+    return *reinterpret_cast<const __attribute__((address_space(3))) u64u*>(p);
+}
+
+// Dynamic LDS: the block's input (in_cap bytes), then — kOutLds — the 64
+// lanes' output slots of `slot` bytes each; otherwise the slots live in the
+// global scratch (blocks above 32 KiB, whose slots would not fit).
+template <bool kOutLds>
 __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob* __restrict__ jobs, int n,
                                                                 uint8_t* __restrict__ scratch,
                                                                 uint32_t* __restrict__ out_len,
-                                                                int* __restrict__ err) {
+                                                                int* __restrict__ err, uint32_t in_cap,
+                                                                uint32_t slot_bytes) {
     __shared__ uint16_t table[kWave * kHashEntries];
     __shared__ uint32_t first_pos[kFirstEntries];
     __shared__ uint32_t sizes[kWave];
+    extern __shared__ uint8_t dyn_lds[];
     const int blk = blockIdx.x;
     if (blk >= n) return;
     const int lane = threadIdx.x;
     const SnappyJob job = jobs[blk];
-    gbyte_c* in = as_global(job.src);
     const uint32_t ulen = (uint32_t)job.src_len;
-    if (ulen > kSnappyMaxBlock) {
+    if (job.src_len > in_cap) {
         if (lane == 0) {
             err[blk] = 1;
             out_len[blk] = 0;
         }
         return;
     }
+    lbyte* const in = (lbyte*)dyn_lds;
+    // stage the block in LDS: every match probe below is an LDS read, not an
+    // HBM round trip on the lane's serial path
     {
+        gbyte_c* src = as_global(job.src);
+        uint32_t done = 0;
+        if ((reinterpret_cast<uintptr_t>(job.src) & 15) == 0) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            done = ulen & ~15u;
+            for (uint32_t o = lane * 16; o < done; o += kWave * 16) {
+                *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(in + o) =
+                    *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(src + o);
+            }
+        }
+        for (uint32_t o = done + lane; o < ulen; o += kWave) in[o] = src[o];
         uint32_t* t = reinterpret_cast<uint32_t*>(table);
         for (int i = lane; i < kWave * kHashEntries / 2; i += kWave) t[i] = 0xFFFFFFFFu;
         for (int i = lane; i < kFirstEntries; i += kWave) first_pos[i] = 0xFFFFFFFFu;
@@ -293,39 +329,45 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
     const uint32_t s = min(ulen, seg * (uint32_t)lane);
     const uint32_t e = min(ulen, s + seg);
     for (uint32_t q = s; q < e && q + 4 <= ulen; ++q) {
-        atomicMin(&first_pos[(load32(in + q) * 0x1e35a7bdu) >> (32 - kFirstBits)], q);
+        atomicMin(&first_pos[(lload32(in + q) * 0x1e35a7bdu) >> (32 - kFirstBits)], q);
     }
     __syncthreads();
-    gbyte* const slot =
-        as_global(scratch + (size_t)blk * SnappyCompressScratchPerBlock() + (size_t)lane * SnappyCompressSlot());
     uint16_t* ht = table + lane * kHashEntries;
-    gbyte* o = slot;
-    uint32_t p = s, lit = s;
-    while (p + 4 <= e) {
-        const uint32_t v = load32(in + p);
-        const uint32_t h = (v * 0x1e35a7bdu) >> (32 - kHashBits);
-        uint32_t cand = ht[h];
-        ht[h] = (uint16_t)p;
-        bool hit = cand != kNoPos && load32(in + cand) == v;
-        if (!hit) {
-            cand = first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)];
-            hit = cand < p && load32(in + cand) == v;
+    auto match = [&](auto o0) {
+        auto o = o0;
+        uint32_t p = s, lit = s;
+        while (p + 4 <= e) {
+            const uint32_t v = lload32(in + p);
+            const uint32_t h = (v * 0x1e35a7bdu) >> (32 - kHashBits);
+            uint32_t cand = ht[h];
+            ht[h] = (uint16_t)p;
+            bool hit = cand != kNoPos && lload32(in + cand) == v;
+            if (!hit) {
+                cand = first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)];
+                hit = cand < p && lload32(in + cand) == v;
+            }
+            if (hit) {
+                uint32_t len = 4;
+                while (p + len + 8 <= e && lload64(in + cand + len) == lload64(in + p + len)) len += 8;
+                while (p + len < e && in[cand + len] == in[p + len]) ++len;
+                if (p > lit) o = emit_literal(o, in + lit, p - lit);
+                o = emit_copy(o, p - cand, len);
+                p += len;
+                lit = p;
+            } else {
+                p += 1 + ((p - lit) >> 5);
+            }
         }
-        if (hit) {
-            uint32_t len = 4;
-            while (p + len + 8 <= e && load64(in + cand + len) == load64(in + p + len)) len += 8;
-            while (p + len < e && in[cand + len] == in[p + len]) ++len;
-            if (p > lit) o = emit_literal(o, in + lit, p - lit);
-            o = emit_copy(o, p - cand, len);
-            p += len;
-            lit = p;
-        } else {
-            p += 1 + ((p - lit) >> 5);
-        }
+        if (e > lit) o = emit_literal(o, in + lit, e - lit);
+        return (uint32_t)(o - o0);
+    };
+    lbyte* const lds_slots = in + in_cap;
+    uint8_t* const gscratch = scratch + (size_t)blk * SnappyCompressScratchPerBlock();
+    if (kOutLds) {
+        sizes[lane] = match(lds_slots + (size_t)lane * slot_bytes);
+    } else {
+        sizes[lane] = match(as_global(gscratch + (size_t)lane * SnappyCompressSlot()));
     }
-    if (e > lit) o = emit_literal(o, in + lit, e - lit);
-    const uint32_t mine = (uint32_t)(o - slot);
-    sizes[lane] = mine;
     __syncthreads();
     // varint header + exclusive prefix sum of the 64 slot sizes
     uint32_t hdr = 1;
@@ -348,9 +390,13 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
     uint32_t at = hdr;
     for (int k = 0; k < kWave; ++k) {
         const uint32_t sz = sizes[k];
-        gbyte_c* src =
-            as_global(scratch + (size_t)blk * SnappyCompressScratchPerBlock() + (size_t)k * SnappyCompressSlot());
-        for (uint32_t j = lane; j < sz; j += kWave) dst[at + j] = src[j];
+        if (kOutLds) {
+            const lbyte* src = lds_slots + (size_t)k * slot_bytes;
+            for (uint32_t j = lane; j < sz; j += kWave) dst[at + j] = src[j];
+        } else {
+            gbyte_c* src = as_global(gscratch + (size_t)k * SnappyCompressSlot());
+            for (uint32_t j = lane; j < sz; j += kWave) dst[at + j] = src[j];
+        }
         at += sz;
     }
     if (lane == 0) {
@@ -371,11 +417,27 @@ int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, void* scratch, uint32_t* out_len_dev, int* err_dev,
-                         hipStream_t s) {
+int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch, uint32_t* out_len_dev,
+                         int* err_dev, hipStream_t s) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(snappy_compress_kernel, dim3(n), dim3(kWave), 0, s, jobs_dev, n,
-                       static_cast<uint8_t*>(scratch), out_len_dev, err_dev);
+    if (max_ulen == 0) max_ulen = 1;
+    if (max_ulen > kSnappyMaxBlock) return -1;
+    const uint32_t in_cap = (max_ulen + 15) & ~15u;  // larger jobs fail with code 1
+    // a lane's output never exceeds its segment plus one literal header
+    const uint32_t seg = (max_ulen + kWave - 1) / kWave;
+    const uint32_t slot = (seg + 16 + 15) & ~15u;
+    // slots in LDS too while that keeps >= 2 waves per CU (blocks up to
+    // 16 KiB: <= 67 KiB); a 32 KiB block with LDS slots would run alone on its CU
+    static_assert(16384 + kWave * ((16384 / kWave + 16 + 15) & ~15u) + kWave * kHashEntries * 2 + kFirstEntries * 4 +
+                          kWave * 4 <= 80 * 1024,
+                  "16 KiB blocks keep their slots in LDS");
+    if (!SnappyCompressUsesScratch(max_ulen)) {
+        hipLaunchKernelGGL(snappy_compress_kernel<true>, dim3(n), dim3(kWave), in_cap + kWave * slot, s, jobs_dev, n,
+                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot);
+    } else {
+        hipLaunchKernelGGL(snappy_compress_kernel<false>, dim3(n), dim3(kWave), in_cap, s, jobs_dev, n,
+                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

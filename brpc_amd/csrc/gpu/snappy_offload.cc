@@ -20,7 +20,8 @@
 //    decodes all pieces in one launch straight into pinned output. A stream
 //    that cannot be cut that way falls back to the CPU codec.
 // Each direction is one stream-ordered sequence (copy, kernel) and ONE
-// fiber-friendly event wait. Measured on MI355X (bench.py gRPC leg, 64 KiB
+// fiber-friendly event wait, shared with every other RPC's codec work that
+// arrived meanwhile (gpu/codec_batch.h: one launch sequence per batch). Measured on MI355X (bench.py gRPC leg, 64 KiB
 // bodies, 50 in flight): 16 KiB blocks 12.9k QPS, 8 KiB 19.4k, 4 KiB 24.6k,
 // 1-2 KiB 25k (saturated by the per-call launch/wait overhead) vs 53k with
 // the CPU codec — the serial snappy format keeps one wave per block busy, so
@@ -35,6 +36,7 @@
 #include <vector>
 
 #include "base/logging.h"
+#include "gpu/codec_batch.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
@@ -139,51 +141,28 @@ bool device_blocks_elsewhere(const Buf& in, int device) {
     return false;
 }
 
-// Runs `enqueue` on a pool stream of `device`, records an event and parks
-// the calling fiber until it fires.
-template <typename F>
-int run_and_wait(int device, F enqueue) {
-    int prev = 0;
-    hipGetDevice(&prev);
-    if (prev != device) hipSetDevice(device);
-    hipStream_t s = PoolStream(device);
-    int rc = s ? enqueue(s) : -1;
-    if (rc == 0) rc = SyncStream(s);
-    else if (s) SyncStream(s);  // never free buffers a launched kernel may still use
-    if (prev != device) hipSetDevice(prev);
-    return rc;
-}
-
 bool gpu_compress(const Buf& in, Buf* out) {
     const int dev = g_device;
     const size_t n = in.size();
     const size_t blk = (size_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
     const size_t nblk = (n + blk - 1) / blk;
     const size_t cap = (SnappyMaxCompressedLength(blk) + 15) & ~(size_t)15;
-    HbmTmp raw(n, dev), scratch(nblk * SnappyCompressScratchPerBlock(), dev);
+    HbmTmp raw(n, dev);
     const size_t pageable = pageable_bytes(in);
-    PinnedBuf bounce(pageable ? pageable : 1), comp(nblk * cap), jobs(nblk * sizeof(SnappyJob)),
-        meta(2 * nblk * sizeof(uint32_t));
-    if (!raw.p || !scratch.p || !bounce.p || !comp.p || !jobs.p || !meta.p) return false;
-    std::vector<Segment> segs;
-    gather_segments(in, static_cast<char*>(raw.p), bounce.p, &segs);
-    SnappyJob* j = reinterpret_cast<SnappyJob*>(jobs.p);
+    PinnedBuf bounce(pageable ? pageable : 1), comp(nblk * cap);
+    if (!raw.p || !bounce.p || !comp.p) return false;
+    CodecRequest req;
+    gather_segments(in, static_cast<char*>(raw.p), bounce.p, &req.h2d);
+    req.comp.resize(nblk);
     for (size_t i = 0; i < nblk; ++i) {
         const size_t off = i * blk;
-        j[i].src = static_cast<char*>(raw.p) + off;
-        j[i].dst = comp.p + i * cap;
-        j[i].src_len = std::min<size_t>(blk, n - off);
-        j[i].dst_cap = cap;
+        req.comp[i] = SnappyJob{static_cast<char*>(raw.p) + off, comp.p + i * cap, std::min<size_t>(blk, n - off), cap};
     }
-    uint32_t* out_len = reinterpret_cast<uint32_t*>(meta.p);
-    int* err = reinterpret_cast<int*>(out_len + nblk);
-    const int rc = run_and_wait(dev, [&](hipStream_t s) {
-        if (LaunchBatchedCopy(segs.data(), (int)segs.size(), s) != 0) return -1;
-        return LaunchSnappyCompress(j, (int)nblk, scratch.p, out_len, err, s);
-    });
-    if (rc != 0) return false;
+    req.comp_max_ulen = (uint32_t)std::min(blk, n);
+    // batched with the other RPCs' codec work: one launch sequence, one event
+    if (RunCodecRequest(&req, dev) != 0) return false;
     for (size_t i = 0; i < nblk; ++i) {
-        if (err[i] || out_len[i] > cap) return false;
+        if (req.comp_err[i] || req.comp_len[i] > cap) return false;
     }
     // one stream: total-length varint + each block's elements (its own
     // varint header stripped); the compressed bytes stay in the pinned
@@ -194,10 +173,10 @@ bool gpu_compress(const Buf& in, Buf* out) {
     comp.give_to(&whole);
     size_t pos = 0;
     for (size_t i = 0; i < nblk; ++i) {
-        const size_t h = (size_t)varint_len(j[i].src_len);
+        const size_t h = (size_t)varint_len(req.comp[i].src_len);
         whole.pop_front(i * cap + h - pos);
-        whole.cutn(out, out_len[i] - h);
-        pos = i * cap + out_len[i];
+        whole.cutn(out, req.comp_len[i] - h);
+        pos = i * cap + req.comp_len[i];
     }
     return true;
 }
@@ -277,16 +256,15 @@ bool split_stream(const uint8_t* p, size_t n, size_t limit, size_t* total, size_
 }
 
 // Top-level field table of a decompressed message (pb_scan layout).
-constexpr uint32_t kIndexFields = 128;
 struct PbIndex {
-    PinnedBuf table{kIndexFields * 2 * sizeof(uint64_t) + 16};
+    std::vector<uint64_t> fields;
     int nfields = -1;  // pb_scan's count or negative code
-    const uint64_t* fields() const { return reinterpret_cast<const uint64_t*>(table.p); }
 };
 
 // Decodes a raw snappy stream on the device into a pinned Buf. With `index`
 // the output is decoded into HBM instead, pb_scan indexes it there, and one
-// copy brings the bytes to pinned memory — still one event wait per call.
+// copy brings the bytes to pinned memory. The work joins the cross-RPC codec
+// batch (gpu/codec_batch.h): one launch sequence and one event per batch.
 bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     const int dev = g_device;
     std::string flat = in.to_string();  // the tag walk needs contiguous bytes
@@ -302,61 +280,45 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     }
     if (total == 0) return true;
     if (index && (total > FLAGS_max_body_size || total > 0xFFFFFFFFull)) return false;
-    // per-piece raw streams (own varint header) back to back, 16 B aligned;
-    // with an index, the message offset table {0, total} rides at the end
+    // per-piece raw streams (own varint header) back to back, 16 B aligned
     std::vector<size_t> soff(pieces.size());
     size_t sbytes = 0;
     for (size_t k = 0; k < pieces.size(); ++k) {
         soff[k] = sbytes;
         sbytes += (varint_len(pieces[k].ulen) + pieces[k].comp_len + 15) & ~(size_t)15;
     }
-    const size_t offsets_at = sbytes;
-    if (index) sbytes += 2 * sizeof(int64_t);
-    PinnedBuf staged(sbytes), dst(total), jobs(pieces.size() * sizeof(SnappyJob)), meta(2 * pieces.size() * 4 + 16);
+    PinnedBuf staged(sbytes), dst(total);
     HbmTmp dstage(sbytes, dev), dbody(index ? total : 0, dev);
-    if (!staged.p || !dst.p || !jobs.p || !meta.p || !dstage.p || (index && (!dbody.p || !index->table.p))) {
-        return false;
-    }
+    if (!staged.p || !dst.p || !dstage.p || (index && !dbody.p)) return false;
     char* out_base = index ? static_cast<char*>(dbody.p) : dst.p;
-    SnappyJob* j = reinterpret_cast<SnappyJob*>(jobs.p);
+    CodecRequest req;
+    req.decomp.resize(pieces.size());
     size_t upos = 0;
     uint32_t max_ulen = 1;
     for (size_t k = 0; k < pieces.size(); ++k) {
         char* s = staged.p + soff[k];
         const int h = put_varint(s, pieces[k].ulen);
         memcpy(s + h, flat.data() + pieces[k].comp_off, pieces[k].comp_len);
-        j[k].src = static_cast<char*>(dstage.p) + soff[k];
-        j[k].dst = out_base + upos;
-        j[k].src_len = h + pieces[k].comp_len;
-        j[k].dst_cap = pieces[k].ulen;
+        req.decomp[k] = SnappyJob{static_cast<char*>(dstage.p) + soff[k], out_base + upos, h + pieces[k].comp_len,
+                                  pieces[k].ulen};
         upos += pieces[k].ulen;
         max_ulen = std::max<uint32_t>(max_ulen, (uint32_t)pieces[k].ulen);
     }
+    req.decomp_max_ulen = max_ulen;
+    req.h2d.push_back(Segment{staged.p, dstage.p, sbytes});
     if (index) {
-        const int64_t offs[2] = {0, (int64_t)total};
-        memcpy(staged.p + offsets_at, offs, sizeof(offs));
+        req.want_scan = true;
+        req.scan = PbScanJob{static_cast<const uint8_t*>(dbody.p), total};
+        req.d2h.push_back(Segment{dbody.p, dst.p, total});
     }
-    uint32_t* out_len = reinterpret_cast<uint32_t*>(meta.p);
-    int* err = reinterpret_cast<int*>(out_len + pieces.size());
-    int32_t* nfields = reinterpret_cast<int32_t*>(err + pieces.size());
-    Segment seg{staged.p, dstage.p, sbytes};
-    Segment back{dbody.p, dst.p, total};
-    const int rc = run_and_wait(dev, [&](hipStream_t s) {
-        if (LaunchBatchedCopy(&seg, 1, s) != 0) return -1;
-        if (LaunchSnappyDecompress(j, (int)pieces.size(), max_ulen, out_len, err, s) != 0) return -1;
-        if (!index) return 0;
-        const int64_t* offs_dev = reinterpret_cast<const int64_t*>(static_cast<char*>(dstage.p) + offsets_at);
-        if (LaunchPbScan(static_cast<const uint8_t*>(dbody.p), total, offs_dev, 1, kIndexFields,
-                         reinterpret_cast<uint64_t*>(index->table.p), nfields, s) != 0) {
-            return -1;
-        }
-        return LaunchBatchedCopy(&back, 1, s);
-    });
-    if (rc != 0) return false;
+    if (RunCodecRequest(&req, dev) != 0) return false;
     for (size_t k = 0; k < pieces.size(); ++k) {
-        if (err[k] || out_len[k] != pieces[k].ulen) return false;
+        if (req.decomp_err[k] || req.decomp_len[k] != pieces[k].ulen) return false;
     }
-    if (index) index->nfields = *nfields;
+    if (index) {
+        index->nfields = req.scan_nfields;
+        index->fields.swap(req.scan_fields);
+    }
     Buf whole;
     dst.give_to(&whole);
     out->append(std::move(whole));
@@ -384,7 +346,7 @@ int parse_offload(const Buf& in, CompressType type, pb::Message* msg) {
     const bool contiguous = raw.backing_block_num() <= 1;
     if (index.nfields >= 0 && contiguous &&
         msg->MergeFromFieldTable(raw.empty() ? nullptr : reinterpret_cast<const uint8_t*>(raw.block_data(0)),
-                                 raw.size(), index.fields(), index.nfields)) {
+                                 raw.size(), index.fields.data(), index.nfields)) {
         ok = msg->IsInitialized();
         g_indexed_parses.fetch_add(1, std::memory_order_relaxed);
     } else {

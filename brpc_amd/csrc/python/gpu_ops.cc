@@ -78,9 +78,9 @@ void bind_gpu_ops(py::module_& g) {
     });
     g.def("snappy_compress_scratch_per_block", [] { return gpu::SnappyCompressScratchPerBlock(); });
     g.def("snappy_max_compressed_length", [](uint64_t n) { return gpu::SnappyMaxCompressedLength(n); });
-    g.def("snappy_compress_launch", [](uintptr_t jobs, int n, uintptr_t scratch, uintptr_t out_len, uintptr_t err,
-                                       uintptr_t stream) {
-        check(gpu::LaunchSnappyCompress((const gpu::SnappyJob*)jobs, n, (void*)scratch, (uint32_t*)out_len,
+    g.def("snappy_compress_launch", [](uintptr_t jobs, int n, uint32_t max_ulen, uintptr_t scratch, uintptr_t out_len,
+                                       uintptr_t err, uintptr_t stream) {
+        check(gpu::LaunchSnappyCompress((const gpu::SnappyJob*)jobs, n, max_ulen, (void*)scratch, (uint32_t*)out_len,
                                         (int*)err, as_stream(stream)),
               "snappy_compress");
     });

@@ -16,6 +16,7 @@
 #include "gpu/hbm_pool.h"
 #include "gpu/snappy_offload.h"
 #include "gpu/json_offload.h"
+#include "gpu/codec_batch.h"
 #include "json/json2pb.h"
 #include "pb/descriptor.h"
 #include "gpu/xgmi.h"
@@ -457,6 +458,13 @@ PYBIND11_MODULE(_native, m) {
         d["fallbacks"] = s.fallbacks;
         d["indexed_parses"] = s.indexed_parses;
         d["index_fallbacks"] = s.index_fallbacks;
+        return d;
+    });
+    g.def("codec_batch_stats", [] {
+        const gpu::CodecBatchStats s = gpu::GetCodecBatchStats();
+        py::dict d;
+        d["requests"] = s.requests;
+        d["launches"] = s.launches;
         return d;
     });
     g.def("enable_json_index", [](int dev, size_t min_bytes) {

@@ -103,7 +103,7 @@ def snappy_compress(data, block=DEFAULT_BLOCK, compact=True):
     jobs_dev = torch.tensor(jobs, dtype=torch.int64).to(dev)
     meta = torch.zeros(2 * n, dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
-        native.gpu.snappy_compress_launch(jobs_dev.data_ptr(), n, scratch.data_ptr(), meta.data_ptr(),
+        native.gpu.snappy_compress_launch(jobs_dev.data_ptr(), n, max(raw), scratch.data_ptr(), meta.data_ptr(),
                                           meta.data_ptr() + 4 * n, stream_handle(dev))
     m = meta.cpu().tolist()
     if any(m[n:]):
