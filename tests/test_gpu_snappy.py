@@ -194,3 +194,27 @@ def test_baidu_std_snappy_bodies_parsed_from_device_index():
     finally:
         native.gpu.disable_snappy()
         s.stop()
+
+
+def test_concurrent_codec_requests_share_launches():
+    """50 gRPC calls in flight with snappy on the GPU: the codec batcher
+    (gpu/codec_batch.h) puts several RPCs' codec work into one launch
+    sequence, and every echoed body still checks out byte for byte."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    native.gpu.enable_snappy(0, 16384)
+    try:
+        b0 = native.gpu.codec_batch_stats()
+        p = native.Press({"server": s.address, "protocol": "h2:grpc", "concurrency": 50, "request_size": 65536,
+                          "request_compress_type": 1, "check_echo": True})
+        p.run_requests(1000)
+        st = p.stats()
+        assert st["success"] == 1000 and st["error"] == 0, st
+        b1 = native.gpu.codec_batch_stats()
+        reqs, launches = b1["requests"] - b0["requests"], b1["launches"] - b0["launches"]
+        assert reqs >= 4000 and launches > 0, (b0, b1)
+        assert reqs / launches > 1.2, (reqs, launches)
+    finally:
+        native.gpu.disable_snappy()
+        s.stop()
