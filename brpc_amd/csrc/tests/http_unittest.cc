@@ -3,6 +3,7 @@
 // test/brpc_builtin_service_unittest.cpp, json2pb unittests).
 #include <unistd.h>
 
+#include <cmath>
 #include <thread>
 
 #include "base/flags.h"
@@ -117,6 +118,96 @@ TEST(Json2pb, roundtrip) {
     json2pb::Json2PbOptions strict;
     strict.allow_unknown_fields = false;
     EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"x\",\"nope\":1}", &bad, strict, &err));
+}
+
+TEST(Json2pb, scalar_coercions) {
+    // numbers quoted as strings (how int64 travels through javascript),
+    // enums by number, bools from numbers, NaN / Infinity, nulls skipped
+    const std::string in =
+        "{\"must\":\"m\",\"i64\":\"1099511627776\",\"u64\":\"18446744073709551615\",\"i32\":-7,"
+        "\"color\":2,\"flag\":1,\"d\":\"-Infinity\",\"s\":null,\"nums\":[1,\"2\",3]}";
+    test::Rich r;
+    std::string err;
+    ASSERT_TRUE(json2pb::JsonToProtoMessage(in, &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_EQ(r.i64(), 1099511627776LL);
+    EXPECT_EQ(r.u64(), 18446744073709551615ULL);
+    EXPECT_EQ(r.i32(), -7);
+    EXPECT_EQ((int)r.color(), 2);
+    EXPECT_TRUE(r.flag());
+    EXPECT_TRUE(std::isinf(r.d()) && r.d() < 0);
+    EXPECT_FALSE(r.has_s());
+    ASSERT_EQ(r.nums_size(), 3);
+    EXPECT_EQ(r.nums(1), 2);
+    // bytes: base64 by default, raw text when asked
+    test::Rich b1, b2;
+    ASSERT_TRUE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"raw\":\"AAH/\"}", &b1, json2pb::Json2PbOptions(), &err));
+    EXPECT_EQ(b1.raw(), std::string("\x00\x01\xff", 3));
+    json2pb::Json2PbOptions keep;
+    keep.base64_to_bytes = false;
+    ASSERT_TRUE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"raw\":\"AAH/\"}", &b2, keep, &err));
+    EXPECT_EQ(b2.raw(), "AAH/");
+}
+
+TEST(Json2pb, pb2json_options) {
+    test::Rich r;
+    r.set_must("m");
+    r.set_color(test::BLUE);
+    r.set_raw(std::string("\x01\x02", 2));
+    std::string out, err;
+    json2pb::Pb2JsonOptions o;
+    o.enum_option_as_string = false;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &out, o, &err));
+    EXPECT_TRUE(out.find("\"color\":2") != std::string::npos);
+    EXPECT_TRUE(out.find("\"nums\"") == std::string::npos);  // empty repeated omitted
+    o.jsonify_empty_array = true;
+    o.bytes_to_base64 = false;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &out, o, &err));
+    EXPECT_TRUE(out.find("\"nums\":[]") != std::string::npos);
+    EXPECT_TRUE(out.find("\"raw\":\"\\u0001\\u0002\"") != std::string::npos);
+    json2pb::Pb2JsonOptions all;
+    all.always_print_primitive_fields = true;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &out, all, &err));
+    EXPECT_TRUE(out.find("\"i32\":0") != std::string::npos);
+    EXPECT_TRUE(out.find("\"flag\":false") != std::string::npos);
+    json2pb::Pb2JsonOptions pretty;
+    pretty.pretty_json = true;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &out, pretty, &err));
+    EXPECT_TRUE(out.find('\n') != std::string::npos);
+    test::Rich back;
+    ASSERT_TRUE(json2pb::JsonToProtoMessage(out, &back, json2pb::Json2PbOptions(), &err));
+    EXPECT_EQ(back.SerializeAsString(), r.SerializeAsString());
+}
+
+TEST(Json2pb, type_errors_name_the_field) {
+    test::Rich r;
+    std::string err;
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("[1,2]", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_TRUE(err.find("json object") != std::string::npos);
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"nums\":5}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_TRUE(err.find("nums") != std::string::npos);
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"counts\":[1]}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_TRUE(err.find("counts") != std::string::npos);
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"color\":\"PURPLE\"}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"inner\":{\"x\":\"y\"}}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"s\":7}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_FALSE(err.empty());
+}
+
+TEST(Json2pb, large_document_round_trip) {
+    test::Rich r;
+    r.set_must(std::string(100000, 'q') + "\"\\\n\t end");
+    for (int i = 0; i < 3000; ++i) {
+        test::Inner* in = r.add_inners();
+        in->set_x(i * 7 - 1000);
+        in->add_tags("t" + std::to_string(i));
+        r.add_nums(i);
+    }
+    std::string out, err;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &out, json2pb::Pb2JsonOptions(), &err));
+    test::Rich back;
+    ASSERT_TRUE(json2pb::JsonToProtoMessage(out, &back, json2pb::Json2PbOptions(), &err));
+    EXPECT_EQ(back.SerializeAsString(), r.SerializeAsString());
 }
 
 TEST(HttpParser, chunked_and_pipelined) {
