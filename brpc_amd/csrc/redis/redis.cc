@@ -1,5 +1,8 @@
 #include "redis/redis.h"
 
+#include <cctype>
+#include <cerrno>
+
 #include <cstdarg>
 #include <cstring>
 #include <mutex>
@@ -78,6 +81,15 @@ int64_t read_line(const Buf& in, size_t pos, std::string* line) {
     return 0;
 }
 
+// RESP integers: an optional '-' and digits, nothing else.
+bool parse_int(const std::string& s, long long* out) {
+    if (s.empty() || s.size() > 20) return false;
+    char* end = nullptr;
+    errno = 0;
+    *out = strtoll(s.c_str(), &end, 10);
+    return errno == 0 && end && *end == '\0' && (isdigit((unsigned char)s.back()));
+}
+
 // Parses one reply at `pos`; returns the end offset, 0 incomplete, -1 bad.
 int64_t parse_at(const Buf& in, size_t pos, RedisReply* r, int depth) {
     if (depth > 64) return -1;
@@ -90,10 +102,16 @@ int64_t parse_at(const Buf& in, size_t pos, RedisReply* r, int depth) {
     switch (t) {
     case '+': r->SetStatus(rest); return e;
     case '-': r->SetError(rest); return e;
-    case ':': r->SetInteger(strtoll(rest.c_str(), nullptr, 10)); return e;
+    case ':': {
+        long long v;
+        if (!parse_int(rest, &v)) return -1;
+        r->SetInteger(v);
+        return e;
+    }
     case '$': {
-        const long long n = strtoll(rest.c_str(), nullptr, 10);
-        if (n < 0) {
+        long long n;
+        if (!parse_int(rest, &n) || n < -1) return -1;
+        if (n == -1) {
             r->SetNil();
             return e;
         }
@@ -104,8 +122,9 @@ int64_t parse_at(const Buf& in, size_t pos, RedisReply* r, int depth) {
         return e + n + 2;
     }
     case '*': {
-        const long long n = strtoll(rest.c_str(), nullptr, 10);
-        if (n < 0) {
+        long long n;
+        if (!parse_int(rest, &n) || n < -1) return -1;
+        if (n == -1) {
             r->SetNil();
             return e;
         }

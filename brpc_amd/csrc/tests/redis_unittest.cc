@@ -168,3 +168,77 @@ TEST(Redis, client_server_pipeline_multi) {
     ASSERT_TRUE(res.reply(3).is_array());
     EXPECT_EQ(res.reply(3)[1].integer(), 2);
 }
+
+TEST(Redis, command_formatting) {
+    RedisRequest req;
+    const char bin[] = {'a', '\0', '\r', '\n', 'b'};
+    ASSERT_TRUE(req.AddCommand("SET key%d %b", 7, bin, sizeof(bin)));
+    ASSERT_TRUE(req.AddCommand("INCRBY %s %lld", "cnt", -5000000000LL));
+    ASSERT_TRUE(req.AddCommandByComponents({"MSET", "k 1", "v"}));
+    ASSERT_TRUE(req.AddCommand("ECHO 100%%"));
+    EXPECT_EQ(req.command_size(), 4);
+    Buf out;
+    ASSERT_TRUE(req.SerializeTo(&out));
+    const std::string want = std::string("*3\r\n$3\r\nSET\r\n$4\r\nkey7\r\n$5\r\n") + std::string(bin, sizeof(bin)) +
+                             "\r\n*3\r\n$6\r\nINCRBY\r\n$3\r\ncnt\r\n$11\r\n-5000000000\r\n"
+                             "*3\r\n$4\r\nMSET\r\n$3\r\nk 1\r\n$1\r\nv\r\n"
+                             "*2\r\n$4\r\nECHO\r\n$4\r\n100%\r\n";
+    EXPECT_EQ(out.to_string(), want);
+    RedisRequest bad;
+    EXPECT_FALSE(bad.AddCommand("GET %q", 1));
+    EXPECT_TRUE(bad.has_error());
+    Buf b2;
+    EXPECT_FALSE(bad.SerializeTo(&b2));
+    EXPECT_FALSE(bad.AddCommandByComponents({}));
+}
+
+TEST(Redis, reply_serialize_roundtrip_bytewise) {
+    RedisReply r;
+    r.SetArray(4);
+    r[0].SetStatus("OK");
+    r[1].SetInteger(-12);
+    r[2].SetArray(2);
+    r[2][0].SetString(std::string("bin\0\r\nary", 9));
+    r[2][1].SetNil();
+    r[3].SetError("ERR nested");
+    Buf wire;
+    r.SerializeTo(&wire);
+    const std::string bytes = wire.to_string();
+    // feed one byte at a time: incomplete prefixes return 0 and consume nothing
+    Buf in;
+    RedisReply back;
+    int rc = 0;
+    for (size_t i = 0; i < bytes.size(); ++i) {
+        in.append(bytes.data() + i, 1);
+        rc = back.ConsumePartial(&in);
+        if (i + 1 < bytes.size()) {
+            ASSERT_EQ(rc, 0);
+            ASSERT_EQ(in.size(), i + 1);
+        }
+    }
+    ASSERT_EQ(rc, 1);
+    EXPECT_TRUE(in.empty());
+    ASSERT_TRUE(back.is_array());
+    EXPECT_EQ(back[0].data(), "OK");
+    EXPECT_EQ(back[1].integer(), -12);
+    EXPECT_EQ(back[2][0].data(), std::string("bin\0\r\nary", 9));
+    EXPECT_TRUE(back[2][1].is_nil());
+    EXPECT_TRUE(back[3].is_error());
+    EXPECT_EQ(back.ToString(), r.ToString());
+}
+
+TEST(Redis, malformed_replies_rejected) {
+    for (const char* bad : {"?oops\r\n", "*99999999\r\n", "$-7\r\n", "$4x\r\nabcd\r\n", ":12a\r\n", "*\r\n"}) {
+        Buf b;
+        b.append(bad);
+        RedisReply r;
+        const int rc = r.ConsumePartial(&b);
+        EXPECT_LT(rc, 0);
+    }
+    Buf nil;
+    nil.append("$-1\r\n*-1\r\n");
+    RedisResponse res;
+    ASSERT_EQ(res.ConsumePartial(&nil, 2), 1);
+    EXPECT_TRUE(res.reply(0).is_nil());
+    EXPECT_TRUE(res.reply(1).is_nil());
+}
