@@ -61,7 +61,13 @@ void MemcacheRequest::Clear() {
     _nop = 0;
 }
 
+// memcached rejects keys above 250 bytes; the header's body length is 32-bit
+static bool valid_op(const std::string& key, size_t value_size = 0) {
+    return key.size() <= 250 && value_size <= 0xFFFFFFFFull - 300;
+}
+
 bool MemcacheRequest::Get(const std::string& key) {
+    if (!valid_op(key)) return false;
     std::string s;
     header(&s, OP_GET, key.size(), 0, key.size(), 0);
     s += key;
@@ -72,6 +78,7 @@ bool MemcacheRequest::Get(const std::string& key) {
 
 bool MemcacheRequest::store(uint8_t op, const std::string& key, const std::string& value, uint32_t flags,
                             uint32_t exptime, uint64_t cas) {
+    if (!valid_op(key, value.size())) return false;
     const bool extras = op == OP_SET || op == OP_ADD || op == OP_REPLACE;
     std::string s;
     const size_t ext = extras ? 8 : 0;
@@ -104,6 +111,7 @@ bool MemcacheRequest::Prepend(const std::string& k, const std::string& v, uint32
 }
 
 bool MemcacheRequest::Delete(const std::string& key) {
+    if (!valid_op(key)) return false;
     std::string s;
     header(&s, OP_DELETE, key.size(), 0, key.size(), 0);
     s += key;
@@ -122,6 +130,7 @@ bool MemcacheRequest::Flush(uint32_t timeout) {
 }
 
 bool MemcacheRequest::counter(uint8_t op, const std::string& key, uint64_t delta, uint64_t initial, uint32_t exptime) {
+    if (!valid_op(key)) return false;
     std::string s;
     header(&s, op, key.size(), 20, 20 + key.size(), 0);
     put64(&s, delta);
@@ -141,6 +150,7 @@ bool MemcacheRequest::Decrement(const std::string& k, uint64_t d, uint64_t i, ui
 }
 
 bool MemcacheRequest::Touch(const std::string& key, uint32_t exptime) {
+    if (!valid_op(key)) return false;
     std::string s;
     header(&s, OP_TOUCH, key.size(), 4, 4 + key.size(), 0);
     put32(&s, exptime);

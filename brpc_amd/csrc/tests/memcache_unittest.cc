@@ -165,3 +165,80 @@ TEST(Memcache, pipelined_ops) {
     EXPECT_TRUE(res.PopVersion(&ver));
     EXPECT_EQ(ver, "1.6.fake");
 }
+
+static std::string mc_header(uint8_t magic, uint8_t op, uint16_t keylen, uint8_t extlen, uint16_t status,
+                             uint32_t body, uint64_t cas) {
+    std::string s;
+    s.push_back((char)magic);
+    s.push_back((char)op);
+    s.push_back((char)(keylen >> 8));
+    s.push_back((char)keylen);
+    s.push_back((char)extlen);
+    s.push_back(0);
+    s.push_back((char)(status >> 8));
+    s.push_back((char)status);
+    for (int i = 3; i >= 0; --i) s.push_back((char)(body >> (8 * i)));
+    for (int i = 0; i < 4; ++i) s.push_back(0);
+    for (int i = 7; i >= 0; --i) s.push_back((char)(cas >> (8 * i)));
+    return s;
+}
+
+TEST(Memcache, request_wire_format) {
+    MemcacheRequest req;
+    ASSERT_TRUE(req.Set("k", "vv", 0x01020304, 60, 7));
+    ASSERT_TRUE(req.Touch("k", 30));
+    ASSERT_TRUE(req.Decrement("n", 2, 9, 0));
+    ASSERT_TRUE(req.Flush(0));
+    EXPECT_EQ(req.op_count(), 4);
+    const std::string w = req.raw().to_string();
+    // SET: extras = flags(4) + exptime(4); key; value; cas in the header
+    std::string want = mc_header(0x80, 0x01, 1, 8, 0, 8 + 1 + 2, 7);
+    want += std::string("\x01\x02\x03\x04\x00\x00\x00\x3c", 8) + "k" + "vv";
+    // TOUCH: extras = exptime(4)
+    want += mc_header(0x80, 0x1c, 1, 4, 0, 4 + 1, 0) + std::string("\x00\x00\x00\x1e", 4) + "k";
+    // DECR: extras = delta(8) + initial(8) + exptime(4)
+    want += mc_header(0x80, 0x06, 1, 20, 0, 20 + 1, 0) + std::string("\0\0\0\0\0\0\0\x02", 8) +
+            std::string("\0\0\0\0\0\0\0\x09", 8) + std::string("\0\0\0\0", 4) + "n";
+    // FLUSH: extras = expiration(4)
+    want += mc_header(0x80, 0x08, 0, 4, 0, 4, 0) + std::string("\0\0\0\0", 4);
+    ASSERT_EQ(w.size(), want.size());
+    EXPECT_TRUE(w == want);
+    // keys longer than the protocol's 250 bytes are refused
+    EXPECT_FALSE(req.Get(std::string(251, 'x')));
+    EXPECT_EQ(req.op_count(), 4);
+}
+
+TEST(Memcache, response_errors_and_partial_input) {
+    std::string wire = mc_header(0x81, 0x01, 0, 0, 0, 0, 11);                                // SET ok
+    wire += mc_header(0x81, 0x02, 0, 0, MC_STATUS_KEY_EEXISTS, 10, 0) + "Data exists";        // ADD fails
+    wire.erase(wire.size() - 1);  // "Data exist" (body length 10)
+    wire += mc_header(0x81, 0x0b, 0, 0, 0, 5, 0) + "1.6.x";                                  // VERSION
+    MemcacheResponse res;
+    Buf in;
+    for (size_t i = 0; i + 1 < wire.size(); i += 7) {  // arrives in 7-byte pieces
+        in.append(wire.data() + i, std::min<size_t>(7, wire.size() - 1 - i));
+        EXPECT_EQ(res.ConsumePartial(&in, 3), 0);
+    }
+    in.append(wire.data() + wire.size() - 1, 1);
+    ASSERT_EQ(res.ConsumePartial(&in, 3), 1);
+    uint64_t cas = 0;
+    EXPECT_TRUE(res.PopSet(&cas));
+    EXPECT_EQ(cas, 11u);
+    EXPECT_FALSE(res.PopAdd(&cas));
+    EXPECT_FALSE(res.LastError().empty());
+    std::string v;
+    EXPECT_TRUE(res.PopVersion(&v));
+    EXPECT_EQ(v, "1.6.x");
+    EXPECT_EQ(res.result_count(), 0);
+    // popping the wrong kind fails instead of misreading the result
+    MemcacheResponse r2;
+    Buf in2;
+    in2.append(mc_header(0x81, 0x04, 0, 0, 0, 0, 0));
+    ASSERT_EQ(r2.ConsumePartial(&in2, 1), 1);
+    EXPECT_FALSE(r2.PopSet(&cas));
+    // a request magic in a response stream is malformed
+    MemcacheResponse r3;
+    Buf in3;
+    in3.append(mc_header(0x80, 0x01, 0, 0, 0, 0, 0));
+    EXPECT_LT(r3.ConsumePartial(&in3, 1), 0);
+}
