@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--skip-64k", action="store_true")
     ap.add_argument("--skip-fanout", action="store_true", help="skip the ParallelChannel fan-out leg (N>1)")
     ap.add_argument("--skip-grpc", action="store_true", help="skip the h2:grpc + snappy leg")
+    ap.add_argument("--skip-rccl", action="store_true", help="skip the RCCL-plane 64 KiB leg (GPU only)")
     ap.add_argument("--requests-per-step-grpc", type=int, default=2000)
     ap.add_argument("--requests-per-step-fanout", type=int, default=500)
     ap.add_argument("--skip-stream", action="store_true",
@@ -157,6 +158,17 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
+    # RCCL data plane (csrc/gpu/rccl_plane.h): one communicator over all
+    # ranks, joined before any connection exists so every hello carries the
+    # rank. It only carries payloads during the rccl leg (-rccl_min_bytes).
+    rccl_up = False
+    if cuda and not a.skip_rccl:
+        try:
+            rccl_up = parallel.init_rccl_plane(topo)
+        except RuntimeError as e:
+            print("rccl plane unavailable: %s" % e, file=sys.stderr)
+        rccl_up = parallel.allreduce_sum(1 if rccl_up else 0, topo) == topo.world_size
+
     server = start_echo_server("127.0.0.1:0", num_threads=workers, gpu_device=topo.device)
     addrs = parallel.exchange_addresses(server.address, topo)
     peer = addrs[parallel.ring_peer(topo)]
@@ -246,6 +258,25 @@ def main():
         r64h = timed_leg(wl64h, a.steps, a.warmup)
         if r64 is None:
             r64, r64h = r64h, None
+
+    # RCCL leg: the same 64 KiB HBM echo ring, but every payload (request
+    # and response) moves by ncclSend/ncclRecv on the job's communicator,
+    # announced by a per-pair sequence number in the RPC meta.
+    rc = None
+    if rccl_up and not a.skip_64k:
+        wlr = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=True,
+                                  requests_per_step=max(1, wl64.requests_per_step // 2)))
+        s0 = parallel.rccl_stats()
+        parallel.set_rccl_min_bytes(32768)  # the 64 KiB message carries a 65520 B attachment
+        try:
+            rc = timed_leg(wlr, a.steps, a.warmup)
+        finally:
+            parallel.set_rccl_min_bytes(None)
+        s1 = parallel.rccl_stats()
+        rc["payloads"] = parallel.allreduce_sum(s1["recv_payloads"] - s0["recv_payloads"], topo)
+        rc["aborts"] = parallel.allreduce_sum(s1["aborts"] - s0["aborts"], topo)
+        groups = parallel.allreduce_sum(s1["groups"] - s0["groups"], topo)
+        rc["payloads_per_group"] = round(2 * rc["payloads"] / groups, 2) if groups else 0.0
 
     # GPU-handler leg: 64 KiB host attachments that the server
     # runs through its GPU — gathered from the pinned socket blocks into HBM
@@ -478,6 +509,14 @@ def main():
                 out["grpc_gpu_codec_indexed_parses"] = rz["gpu"]["indexed_parses"]
                 out["grpc_gpu_codec_requests_per_launch"] = rz["gpu"]["codec_requests_per_launch"]
                 out["grpc_snappy_errors"] = rz["cpu"]["errors"] + rz["gpu"]["errors"]
+        if rc:
+            out["rccl_64KB_qps"] = round(rc["qps"], 1)
+            out["rccl_64KB_p99_us"] = rc["p99_us"]
+            out["rccl_64KB_gbytes_per_s"] = round(rc["qps"] * 65536 * 2 / 1e9, 3)
+            out["rccl_64KB_errors"] = rc["errors"]
+            out["rccl_payloads"] = int(rc["payloads"])
+            out["rccl_ops_per_group"] = rc["payloads_per_group"]
+            out["rccl_aborts"] = int(rc["aborts"])
         if rg:
             out["qps_64KB_gpu_handler"] = round(rg["qps"], 1)
             out["p99_us_64KB_gpu_handler"] = rg["p99_us"]

@@ -20,6 +20,7 @@
 #include "json/json2pb.h"
 #include "pb/descriptor.h"
 #include "gpu/xgmi.h"
+#include "gpu/rccl_plane.h"
 #include "mrpc/proto/echo.pb.h"
 #include "base/time.h"
 #include "press/press.h"
@@ -445,6 +446,40 @@ PYBIND11_MODULE(_native, m) {
         return d;
     });
     g.def("reap_lent", [] { gpu::ReapLentBlocks(); });
+    // RCCL data plane (gpu/rccl_plane.h): collective init from every rank
+    g.def("rccl_unique_id", [] {
+        std::string err;
+        std::string id = gpu::rccl::UniqueId(&err);
+        if (id.empty()) throw std::runtime_error(err);
+        return py::bytes(id);
+    });
+    g.def("rccl_init", [](int rank, int world, py::bytes uid, int dev) {
+        std::string err, id = uid;
+        int rc;
+        {
+            py::gil_scoped_release nogil;  // blocks until every rank joined
+            rc = gpu::rccl::Init(rank, world, id, dev, &err);
+        }
+        if (rc != 0) throw std::runtime_error(err);
+    }, py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"));
+    g.def("rccl_active", [] { return gpu::rccl::Active(); });
+    g.def("rccl_shutdown", [] {
+        py::gil_scoped_release nogil;
+        gpu::rccl::Shutdown();
+    });
+    g.def("rccl_stats", [] {
+        const gpu::rccl::Stats s = gpu::rccl::GetStats();
+        py::dict d;
+        d["sent_payloads"] = s.sent_payloads;
+        d["sent_bytes"] = s.sent_bytes;
+        d["recv_payloads"] = s.recv_payloads;
+        d["recv_bytes"] = s.recv_bytes;
+        d["discarded"] = s.discarded;
+        d["groups"] = s.groups;
+        d["aborts"] = s.aborts;
+        d["reorder_waits"] = s.reorder_waits;
+        return d;
+    });
     g.def("enable_snappy", [](int dev, size_t min_bytes) {
         std::string err;
         if (gpu::EnableGpuSnappy(dev, min_bytes, &err) != 0) throw std::runtime_error(err);
