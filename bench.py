@@ -38,8 +38,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--requests-per-step", type=int, default=0, help="override the 32B step size")
-    ap.add_argument("--requests-per-step-64k", type=int, default=0, help="override the 64 KiB step size")
+    # step sizes: with the default 20 steps every headline leg is timed for
+    # >= ~3 s on the MI355X box (0.4 s legs were too noisy)
+    ap.add_argument("--requests-per-step", type=int, default=200000, help="32B requests per step and rank")
+    ap.add_argument("--requests-per-step-64k", type=int, default=60000,
+                    help="64 KiB HBM requests per step and rank (host/GPU-handler/RCCL legs use half)")
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--workers", type=int, default=0, help="fiber worker pthreads per rank (0: auto)")
     ap.add_argument("--skip-64k", action="store_true")
