@@ -494,6 +494,13 @@ bool Connection::OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& b
             i = 1;
             name = v[1].str();
         }
+        if (name == "onCuePoint") {
+            RtmpCuePoint cp;
+            cp.timestamp = ts;
+            if (i + 1 < v.size()) cp.data = v[i + 1];
+            st->OnCuePoint(&cp);
+            return true;
+        }
         RtmpMetaData md;
         md.timestamp = ts;
         if (i + 1 < v.size()) md.data = v[i + 1];
@@ -753,6 +760,25 @@ int RtmpStreamBase::SendVideoMessage(const RtmpVideoMessage& msg) {
     return SendMessage(RTMP_VIDEO, msg.timestamp, b);
 }
 
+int RtmpStreamBase::SendCuePoint(const RtmpCuePoint& cp) {
+    std::string s;
+    rtmp::WriteAMF(&s, AMFValue::String("onCuePoint"));
+    rtmp::WriteAMF(&s, cp.data);
+    return SendMessage(RTMP_DATA_AMF0, cp.timestamp, Buf(s));
+}
+
+int RtmpStreamBase::SendAACMessage(const RtmpAACMessage& msg) {
+    RtmpAudioMessage a;
+    msg.ToAudioMessage(&a);
+    return SendAudioMessage(a);
+}
+
+int RtmpStreamBase::SendAVCMessage(const RtmpAVCMessage& msg) {
+    RtmpVideoMessage v;
+    msg.ToVideoMessage(&v);
+    return SendVideoMessage(v);
+}
+
 // ------------------------------------------------------------ client
 
 namespace {
@@ -842,6 +868,8 @@ int RtmpClient::Init(const char* server_addr_and_port, const RtmpClientOptions& 
     _conn = conn;
     return 0;
 }
+
+uint64_t RtmpClient::socket_id() const { return _conn ? (uint64_t)_conn->socket_id() : 0; }
 
 RtmpClientStream::~RtmpClientStream() { Destroy(); }
 

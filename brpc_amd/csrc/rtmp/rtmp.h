@@ -27,6 +27,7 @@
 #include "base/buf.h"
 #include "base/endpoint.h"
 #include "rtmp/amf.h"
+#include "rtmp/media.h"
 
 namespace mrpc {
 
@@ -77,19 +78,24 @@ public:
     virtual void OnMetaData(RtmpMetaData* md, const std::string& name) {}
     virtual void OnAudioMessage(RtmpAudioMessage* msg) {}
     virtual void OnVideoMessage(RtmpVideoMessage* msg) {}
+    // Data messages named "onCuePoint".
+    virtual void OnCuePoint(RtmpCuePoint* cp) {}
     // The stream ended (deleteStream, connection closed, Destroy()).
     virtual void OnStop() {}
 
     int SendMetaData(const RtmpMetaData& md, const std::string& name = "onMetaData");
     int SendAudioMessage(const RtmpAudioMessage& msg);
     int SendVideoMessage(const RtmpVideoMessage& msg);
+    int SendCuePoint(const RtmpCuePoint& cp);
+    int SendAACMessage(const RtmpAACMessage& msg);
+    int SendAVCMessage(const RtmpAVCMessage& msg);
 
     uint32_t stream_id() const { return _stream_id; }
     bool is_stopped() const { return _stopped.load(std::memory_order_acquire); }
     EndPoint remote_side() const;
 
     // ---- internal
-    int SendMessage(uint8_t type, uint32_t timestamp, const Buf& body);
+    virtual int SendMessage(uint8_t type, uint32_t timestamp, const Buf& body);
     void CallOnStop();
     std::shared_ptr<rtmp_detail::Connection> _conn;
     uint32_t _stream_id = 0;
@@ -151,6 +157,8 @@ public:
     int64_t Ping(int timeout_ms = 1000);
     // Acknowledgements this connection sent for the server's window.
     int64_t acks_sent() const;
+    // The connection's socket (0 before Init); failing it drops every stream.
+    uint64_t socket_id() const;
 
 private:
     RtmpClientOptions _options;
@@ -170,6 +178,49 @@ public:
     int Init(RtmpClient* client, const RtmpClientStreamOptions& options);
     // deleteStream and detach (OnStop is called). Idempotent.
     void Destroy();
+};
+
+// A client stream that outlives its connection (the reference's
+// RtmpRetryingClientStream, src/brpc/rtmp.h:880-1050): when the sub stream
+// stops for any reason other than Destroy(), a new client is obtained from
+// the creator and the play/publish is re-issued, first `fast_retry_count`
+// times immediately, then every `retry_interval_ms`, until
+// `max_retry_duration_ms` of failing (-1: forever). Media sent while no sub
+// stream is up fails with EAGAIN; callbacks of every sub stream arrive on
+// this object.
+struct RtmpRetryingClientStreamOptions : public RtmpClientStreamOptions {
+    int retry_interval_ms = 1000;
+    int max_retry_duration_ms = -1;
+    int fast_retry_count = 2;
+};
+
+class RtmpSubStreamCreator {
+public:
+    virtual ~RtmpSubStreamCreator() {}
+    // A connected client for the next sub stream (nullptr: try later).
+    virtual std::shared_ptr<RtmpClient> NewClient() = 0;
+};
+
+class RtmpRetryingClientStream : public RtmpStreamBase {
+public:
+    RtmpRetryingClientStream();
+    ~RtmpRetryingClientStream() override;
+    // Takes ownership of `creator`. 0 when the first sub stream is up;
+    // otherwise retries continue in the background and -1 is returned.
+    int Init(RtmpSubStreamCreator* creator, const RtmpRetryingClientStreamOptions& options);
+    void Destroy();
+    // Sub streams started after the first one.
+    int64_t reconnects() const;
+    bool connected() const;
+    // Called after every successful (re)start of the sub stream.
+    virtual void OnSubStreamStarted() {}
+
+    int SendMessage(uint8_t type, uint32_t timestamp, const Buf& body) override;
+
+    struct Impl;
+
+private:
+    std::shared_ptr<Impl> _impl;
 };
 
 // FLV container <-> RTMP messages.

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "base/time.h"
+#include "net/socket.h"
 #include "rpc/server.h"
 #include "rtmp/handshake.h"
 #include "rtmp/rtmp.h"
@@ -312,4 +313,339 @@ TEST(Rtmp, complex_handshake_ping_and_acks) {
     EXPECT_GE(client.acks_sent(), 1);  // 6 MB over a 2.5 MB window
     pub.Destroy();
     player.Destroy();
+}
+
+// ------------------------------------------------------------ media payloads
+
+namespace {
+// MSB-first bit writer with exp-Golomb codes (builds SPS test vectors)
+struct BitWriter {
+    std::string out;
+    uint32_t acc = 0;
+    int n = 0;
+    void bit(uint32_t b) {
+        acc = (acc << 1) | (b & 1);
+        if (++n == 8) {
+            out.push_back((char)acc);
+            acc = 0;
+            n = 0;
+        }
+    }
+    void bits(uint32_t v, int k) {
+        for (int i = k - 1; i >= 0; --i) bit((v >> i) & 1);
+    }
+    void ue(uint32_t v) {
+        const uint32_t x = v + 1;
+        int len = 0;
+        while ((x >> len) > 1) ++len;
+        bits(0, len);
+        bits(x, len + 1);
+    }
+    void se(int32_t v) { ue(v > 0 ? 2 * v - 1 : -2 * v); }
+    std::string finish() {  // rbsp_stop_one_bit + alignment
+        bit(1);
+        while (n) bit(0);
+        return out;
+    }
+};
+
+// A high-profile SPS for w x h (crop to the exact size) in escaped form.
+std::string make_sps(int w, int h, bool high) {
+    BitWriter bw;
+    bw.bits(high ? 100 : 66, 8);  // profile_idc
+    bw.bits(0, 8);
+    bw.bits(40, 8);  // level 4.0
+    bw.ue(0);        // sps id
+    if (high) {
+        bw.ue(1);   // 4:2:0
+        bw.ue(0);   // bit depth luma - 8
+        bw.ue(0);   // chroma
+        bw.bit(0);  // qpprime
+        bw.bit(1);  // scaling matrix present
+        for (int i = 0; i < 8; ++i) {
+            bw.bit(i == 0 ? 1 : 0);
+            if (i == 0)
+                for (int j = 0; j < 16; ++j) bw.se(j == 0 ? 8 : 0);  // one flat delta list
+        }
+    }
+    bw.ue(0);  // log2_max_frame_num - 4
+    bw.ue(0);  // poc type 0
+    bw.ue(2);  // log2_max_poc_lsb - 4
+    bw.ue(4);  // max_num_ref_frames
+    bw.bit(0);
+    const int wm = (w + 15) / 16, hm = (h + 15) / 16;
+    bw.ue(wm - 1);
+    bw.ue(hm - 1);
+    bw.bit(1);  // frame_mbs_only
+    bw.bit(1);  // direct_8x8
+    const int cr = wm * 16 - w, cb = hm * 16 - h;
+    bw.bit(cr || cb ? 1 : 0);
+    if (cr || cb) {
+        bw.ue(0);
+        bw.ue(cr / 2);
+        bw.ue(0);
+        bw.ue(cb / 2);
+    }
+    bw.bit(0);  // vui
+    const std::string rbsp = bw.finish();
+    // escape 00 00 0x (x <= 3) -> 00 00 03 0x
+    std::string nalu(1, (char)0x67);
+    int zeros = 0;
+    for (char c : rbsp) {
+        if (zeros >= 2 && (uint8_t)c <= 3) {
+            nalu.push_back(3);
+            zeros = 0;
+        }
+        zeros = c == 0 ? zeros + 1 : 0;
+        nalu.push_back(c);
+    }
+    return nalu;
+}
+}  // namespace
+
+TEST(RtmpMedia, aac_config_and_adts) {
+    AudioSpecificConfig asc;
+    const uint8_t lc_44k_stereo[2] = {0x12, 0x10};  // object 2, index 4, 2 channels
+    ASSERT_EQ(asc.Create(lc_44k_stereo, 2), 0);
+    EXPECT_EQ((int)asc.aac_object, 2);
+    EXPECT_EQ(asc.sample_rate, 44100u);
+    EXPECT_EQ((int)asc.channels, 2);
+    EXPECT_EQ(asc.Serialize(), std::string("\x12\x10", 2));
+    uint8_t h[7];
+    ASSERT_EQ(asc.MakeAdtsHeader(100, h), 0);
+    EXPECT_EQ((int)h[0], 0xff);
+    EXPECT_EQ((int)h[1], 0xf1);
+    EXPECT_EQ((int)(h[2] >> 6), 1);          // profile = object - 1
+    EXPECT_EQ((int)((h[2] >> 2) & 0xf), 4);  // 44.1 kHz
+    const int frame = ((h[3] & 3) << 11) | (h[4] << 3) | (h[5] >> 5);
+    EXPECT_EQ(frame, 107);
+    // explicit sampling rate (index 15) round trips through 24 bits
+    AudioSpecificConfig odd;
+    odd.aac_object = 2;
+    odd.sample_rate = 12345;
+    odd.sample_rate_index = 15;
+    odd.channels = 1;
+    const std::string s = odd.Serialize();
+    AudioSpecificConfig back;
+    ASSERT_EQ(back.Create(s.data(), s.size()), 0);
+    EXPECT_EQ(back.sample_rate, 12345u);
+    EXPECT_EQ((int)back.channels, 1);
+    EXPECT_NE(back.MakeAdtsHeader(10, h), 0);  // ADTS cannot carry an explicit rate
+    EXPECT_NE(asc.Create(lc_44k_stereo, 1), 0);  // truncated
+
+    RtmpAACMessage aac;
+    aac.timestamp = 33;
+    aac.packet_type = AAC_PACKET_SEQUENCE_HEADER;
+    aac.data.append(asc.Serialize());
+    RtmpAudioMessage am;
+    aac.ToAudioMessage(&am);
+    EXPECT_EQ((int)am.codec, 10);
+    RtmpAACMessage aac2;
+    ASSERT_EQ(aac2.Create(am), 0);
+    EXPECT_EQ((int)aac2.packet_type, (int)AAC_PACKET_SEQUENCE_HEADER);
+    EXPECT_EQ(aac2.data.to_string(), asc.Serialize());
+    am.codec = 2;  // MP3
+    EXPECT_NE(aac2.Create(am), 0);
+}
+
+TEST(RtmpMedia, sps_dimensions) {
+    struct Case {
+        int w, h;
+        bool high;
+    } cases[] = {{1920, 1080, true}, {1280, 720, false}, {640, 360, true}, {176, 144, false}};
+    for (const Case& c : cases) {
+        AvcSps sps;
+        ASSERT_EQ(sps.Parse(make_sps(c.w, c.h, c.high)), 0);
+        EXPECT_EQ(sps.width, c.w);
+        EXPECT_EQ(sps.height, c.h);
+        EXPECT_EQ((int)sps.profile_idc, c.high ? 100 : 66);
+        EXPECT_EQ((int)sps.max_num_ref_frames, 4);
+    }
+    AvcSps bad;
+    EXPECT_NE(bad.Parse(std::string("\x67\x64", 2)), 0);     // truncated
+    EXPECT_NE(bad.Parse(std::string("\x68\x64\x00\x28", 4)), 0);  // a PPS
+    EXPECT_EQ(AvcUnescapeRbsp("\x00\x00\x03\x01\x00\x00\x03", 7), std::string("\x00\x00\x01\x00\x00", 5));
+}
+
+TEST(RtmpMedia, avc_config_record_and_nalus) {
+    AVCDecoderConfigurationRecord rec;
+    rec.avc_profile = 100;
+    rec.avc_level = 40;
+    rec.length_size_minus1 = 3;
+    rec.sps_list.push_back(make_sps(1920, 1080, true));
+    rec.pps_list.push_back(std::string("\x68\xee\x3c\x80", 4));
+    const std::string bytes = rec.Serialize();
+    AVCDecoderConfigurationRecord back;
+    ASSERT_EQ(back.Create(bytes.data(), bytes.size()), 0);
+    EXPECT_EQ(back.width, 1920);
+    EXPECT_EQ(back.height, 1080);
+    ASSERT_EQ(back.sps_list.size(), 1u);
+    ASSERT_EQ(back.pps_list.size(), 1u);
+    EXPECT_EQ(back.pps_list[0], rec.pps_list[0]);
+    EXPECT_EQ(back.Serialize(), bytes);
+    EXPECT_NE(back.Create(bytes.data(), bytes.size() - 2), 0);  // PPS cut short
+
+    // the record rides in an AVC sequence-header message; composition time is SI24
+    RtmpAVCMessage m;
+    m.timestamp = 1000;
+    m.frame_type = 1;
+    m.packet_type = AVC_PACKET_NALU;
+    m.composition_time = -40;
+    const std::string idr("\x65\x88\x84\x00\x33", 5), sei("\x06\x05\x01\xff", 4);
+    auto put32 = [](Buf* b, uint32_t v) {
+        const char x[4] = {(char)(v >> 24), (char)(v >> 16), (char)(v >> 8), (char)v};
+        b->append(x, 4);
+    };
+    put32(&m.data, (uint32_t)sei.size());
+    m.data.append(sei);
+    put32(&m.data, (uint32_t)idr.size());
+    m.data.append(idr);
+    RtmpVideoMessage vm;
+    m.ToVideoMessage(&vm);
+    RtmpAVCMessage m2;
+    ASSERT_EQ(m2.Create(vm), 0);
+    EXPECT_EQ(m2.composition_time, -40);
+    EXPECT_EQ((int)m2.packet_type, (int)AVC_PACKET_NALU);
+
+    AVCNaluFormat fmt = AVC_NALU_FORMAT_UNKNOWN;
+    AVCNaluIterator it(&m2.data, back.length_size_minus1 + 1, &fmt);
+    std::string nalu;
+    AVCNaluType t;
+    ASSERT_TRUE(it.Next(&nalu, &t));
+    EXPECT_EQ((int)fmt, (int)AVC_NALU_FORMAT_IBMF);
+    EXPECT_EQ((int)t, (int)AVC_NALU_SEI);
+    ASSERT_TRUE(it.Next(&nalu, &t));
+    EXPECT_EQ((int)t, (int)AVC_NALU_IDR);
+    EXPECT_EQ(nalu, idr);
+    EXPECT_FALSE(it.Next(&nalu));
+    EXPECT_FALSE(it.error());
+
+    // Annex B: 4- and 3-byte start codes, trailing zero bytes
+    Buf annexb;
+    annexb.append(std::string("\x00\x00\x00\x01", 4) + rec.sps_list[0] + std::string("\x00\x00\x01", 3) +
+                  rec.pps_list[0] + std::string("\x00\x00\x00\x01", 4) + idr + std::string("\x00\x00", 2));
+    AVCNaluFormat f2 = AVC_NALU_FORMAT_UNKNOWN;
+    AVCNaluIterator it2(&annexb, 4, &f2);
+    std::vector<int> types;
+    while (it2.Next(&nalu, &t)) types.push_back((int)t);
+    EXPECT_EQ((int)f2, (int)AVC_NALU_FORMAT_ANNEXB);
+    EXPECT_FALSE(it2.error());
+    ASSERT_EQ(types.size(), 3u);
+    EXPECT_EQ(types[0], (int)AVC_NALU_SPS);
+    EXPECT_EQ(types[1], (int)AVC_NALU_PPS);
+    EXPECT_EQ(types[2], (int)AVC_NALU_IDR);
+    EXPECT_EQ(nalu, idr);
+
+    // a length prefix running past the packet is a framing error
+    Buf broken;
+    put32(&broken, 100);
+    broken.append("\x65\x01", 2);
+    AVCNaluFormat f3 = AVC_NALU_FORMAT_IBMF;
+    AVCNaluIterator it3(&broken, 4, &f3);
+    EXPECT_FALSE(it3.Next(&nalu));
+    EXPECT_TRUE(it3.error());
+}
+
+namespace {
+class CueSink : public RtmpServerStream {
+public:
+    explicit CueSink(std::atomic<int>* n, std::string* last) : _n(n), _last(last) {}
+    void OnCuePoint(RtmpCuePoint* cp) override {
+        const AMFValue* name = cp->data.Find("name");
+        *_last = (name ? name->str() : "") + "@" + std::to_string(cp->timestamp);
+        _n->fetch_add(1);
+    }
+    void OnVideoMessage(RtmpVideoMessage* m) override {
+        RtmpAVCMessage avc;
+        if (avc.Create(*m) == 0 && avc.composition_time == 80) _n->fetch_add(100);
+    }
+
+private:
+    std::atomic<int>* _n;
+    std::string* _last;
+};
+
+class CueService : public RtmpService {
+public:
+    std::atomic<int> n{0}, streams{0};
+    std::string last;
+    RtmpServerStream* NewStream(const RtmpConnectRequest&) override {
+        streams.fetch_add(1);
+        return new CueSink(&n, &last);
+    }
+};
+
+class FixedCreator : public RtmpSubStreamCreator {
+public:
+    explicit FixedCreator(std::string addr) : _addr(std::move(addr)) {}
+    std::shared_ptr<RtmpClient> NewClient() override {
+        auto c = std::make_shared<RtmpClient>();
+        RtmpClientOptions o;
+        o.timeout_ms = 2000;
+        if (c->Init(_addr.c_str(), o) != 0) return nullptr;
+        std::lock_guard<std::mutex> g(mu);
+        last = c;
+        return c;
+    }
+    std::mutex mu;
+    std::shared_ptr<RtmpClient> last;
+
+private:
+    std::string _addr;
+};
+}  // namespace
+
+TEST(RtmpMedia, cue_points_and_retrying_publisher) {
+    CueService svc;
+    Server server;
+    ServerOptions o;
+    o.has_builtin_services = false;
+    o.rtmp_service = &svc;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &o), 0);
+    const std::string addr = "127.0.0.1:" + std::to_string(server.listen_port());
+
+    FixedCreator* creator = new FixedCreator(addr);
+    RtmpRetryingClientStream pub;
+    RtmpRetryingClientStreamOptions ro;
+    ro.publish_name = "cues";
+    ro.retry_interval_ms = 50;
+    ro.fast_retry_count = 1;
+    ASSERT_EQ(pub.Init(creator, ro), 0);
+    EXPECT_TRUE(pub.connected());
+    RtmpCuePoint cp;
+    cp.timestamp = 777;
+    cp.data.Set("name", AMFValue::String("ad-break"));
+    cp.data.Set("time", AMFValue::Number(7.77));
+    ASSERT_EQ(pub.SendCuePoint(cp), 0);
+    RtmpAVCMessage avc;
+    avc.composition_time = 80;
+    avc.data.append("\x00\x00\x00\x01\x65", 5);
+    ASSERT_EQ(pub.SendAVCMessage(avc), 0);
+    int64_t deadline = monotonic_us() + 3000000;
+    while (svc.n.load() < 101 && monotonic_us() < deadline) usleep(2000);
+    EXPECT_EQ(svc.n.load(), 101);
+    EXPECT_EQ(svc.last, "ad-break@777");
+
+    // kill the publisher's connection: the stream comes back on a new one
+    {
+        std::lock_guard<std::mutex> g(creator->mu);
+        SocketUniquePtr s;
+        ASSERT_EQ(Socket::Address(creator->last->socket_id(), &s), 0);
+        s->SetFailed(ECONNRESET, "test kills the publisher connection");
+    }
+    deadline = monotonic_us() + 5000000;
+    while (pub.reconnects() < 1 && monotonic_us() < deadline) usleep(5000);
+    ASSERT_EQ(pub.reconnects(), 1);
+    deadline = monotonic_us() + 2000000;
+    while (!pub.connected() && monotonic_us() < deadline) usleep(2000);
+    cp.timestamp = 888;
+    ASSERT_EQ(pub.SendCuePoint(cp), 0);
+    deadline = monotonic_us() + 3000000;
+    while (svc.n.load() < 102 && monotonic_us() < deadline) usleep(2000);
+    EXPECT_EQ(svc.n.load(), 102);
+    EXPECT_EQ(svc.last, "ad-break@888");
+    EXPECT_GE(svc.streams.load(), 2);
+    pub.Destroy();
+    EXPECT_FALSE(pub.connected());
+    EXPECT_NE(pub.SendCuePoint(cp), 0);
 }
