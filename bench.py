@@ -328,8 +328,11 @@ def main():
     rs = None
     if not a.skip_stream:
         others = [x for i, x in enumerate(addrs) if i != topo.rank] or [peer]
+        # up to 4 rounds (8 MiB per stream, the window) in flight: the next
+        # round is written while earlier acks travel back
         sp = native.StreamPress({"server": ",".join(others), "chunk_size": 65536, "chunks_per_step": 32,
-                                 "device_chunks": bool(cuda), "gpu_device": topo.device})
+                                 "device_chunks": bool(cuda), "gpu_device": topo.device,
+                                 "pipeline_rounds": 4, "max_buf_size": 8 << 20})
         sp.run_steps(a.warmup)
         parallel.barrier(topo)
         sync()
@@ -351,7 +354,8 @@ def main():
     if topo.world_size > 2 and not a.skip_stream:
         chain = [addrs[(topo.rank + k) % topo.world_size] for k in range(1, topo.world_size)]
         pp = native.StreamPress({"server": chain[0], "relay_chain": ",".join(chain[1:]), "chunk_size": 65536,
-                                 "chunks_per_step": 32, "device_chunks": bool(cuda), "gpu_device": topo.device})
+                                 "chunks_per_step": 32, "device_chunks": bool(cuda), "gpu_device": topo.device,
+                                 "pipeline_rounds": 4, "max_buf_size": 8 << 20})
         pp.run_steps(a.warmup)
         parallel.barrier(topo)
         sync()

@@ -1,5 +1,6 @@
 #include "press/stream_press.h"
 
+#include <algorithm>
 #include <cstring>
 
 #include "base/time.h"
@@ -105,15 +106,11 @@ int StreamPress::write_chunk(Peer* p, std::string* err) {
 
 int StreamPress::RunSteps(int steps, std::string* err) {
     const int64_t round = (int64_t)_opt.chunk_size * _opt.chunks_per_step;
-    for (int s = 0; s < steps; ++s) {
-        for (int c = 0; c < _opt.chunks_per_step; ++c) {
-            for (auto& p : _peers) {
-                if (write_chunk(p.get(), err) != 0) return -1;
-                _sent += _opt.chunk_size;
-            }
-        }
+    const int depth = std::max(1, _opt.pipeline_rounds);
+    // every peer acknowledged `rounds` complete rounds (cumulative acks)
+    auto wait_acked = [&](int64_t rounds) -> int {
+        const int64_t want = rounds * round;
         std::unique_lock<std::mutex> g(_mu);
-        const int64_t want = (_steps + 1) * round;
         const bool ok = _cv.wait_for(g, std::chrono::milliseconds(_opt.timeout_ms), [&] {
             for (auto& p : _peers) {
                 if (p->closed || p->acked < want) return p->closed;
@@ -126,8 +123,22 @@ int StreamPress::RunSteps(int steps, std::string* err) {
                 return -1;
             }
         }
-        ++_steps;
+        return 0;
+    };
+    const int64_t first = _steps;
+    for (int s = 0; s < steps; ++s) {
+        for (int c = 0; c < _opt.chunks_per_step; ++c) {
+            for (auto& p : _peers) {
+                if (write_chunk(p.get(), err) != 0) return -1;
+                _sent += _opt.chunk_size;
+            }
+        }
+        // round first+s+1 is written; keep at most depth-1 rounds unacked
+        const int64_t must = first + s + 1 - (depth - 1);
+        if (must > first && wait_acked(must) != 0) return -1;
     }
+    if (wait_acked(first + steps) != 0) return -1;
+    _steps = first + steps;
     return 0;
 }
 

@@ -31,6 +31,10 @@ struct StreamPressOptions {
     int chunks_per_step = 64;
     int timeout_ms = 10000;
     int64_t max_buf_size = 2 * 1024 * 1024;  // stream window (StreamOptions)
+    // Rounds in flight: the next round is written while up to this many
+    // earlier rounds still wait for their acks (1 = write, wait, repeat).
+    // RunSteps drains every ack before it returns either way.
+    int pipeline_rounds = 1;
     bool device_chunks = false;              // chunks in HBM, moved over xGMI
     int gpu_device = -1;
     // Pipeline (PP analog): the servers in `server` relay every chunk on

@@ -226,6 +226,7 @@ public:
             else if (k == "chunks_per_step") o.chunks_per_step = v.cast<int>();
             else if (k == "timeout_ms") o.timeout_ms = v.cast<int>();
             else if (k == "max_buf_size") o.max_buf_size = v.cast<int64_t>();
+            else if (k == "pipeline_rounds") o.pipeline_rounds = v.cast<int>();
             else if (k == "device_chunks") o.device_chunks = v.cast<bool>();
             else if (k == "gpu_device") o.gpu_device = v.cast<int>();
             else if (k == "relay_chain") o.relay_chain = v.cast<std::string>();
