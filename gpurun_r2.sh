@@ -28,5 +28,6 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp
   step rocprof_dev 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_dev" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --latency-sample-s 0 --skip-stream --steps 5 --warmup 1
+  rm -f "$GRAFT_REPO_ROOT/gpurun_out/prof_dev/run_kernel_trace.csv"  # per-launch rows: too big to copy back
 fi
 echo done
