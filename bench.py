@@ -152,9 +152,8 @@ def main():
     # (profiles/r2_cpu_affinity_sweep.txt).
     native.set_flag("event_dispatcher_spin_us", str(max(0, a.dispatcher_poll_us)))
     # extra runtime flags for experiments: MRPC_FLAGS="--name=value ..."
-    for item in os.environ.get("MRPC_FLAGS", "").split():
-        k, _, v = item.lstrip("-").partition("=")
-        native.set_flag(k, v or "true")
+    from brpc_amd.utils import apply_env_flags  # noqa: E402
+    apply_env_flags("MRPC_FLAGS")
     cuda = torch.cuda.is_available()
 
     def sync():
