@@ -218,7 +218,10 @@ void ParallelChannel::CallMethod(const pb::MethodDescriptor* method, RpcControll
         pc->mergers.push_back(_subs[i].merger);
         pc->subs.push_back(std::move(s));
     }
+    // finish_parent locks the call id itself: release ours first (the
+    // early exits below used to self-deadlock on it)
     if (nbad) {
+        fiber::call_id_unlock(pc->cid);
         finish_parent(pc, EREQUEST, "CallMapper returned Bad() for " + std::to_string(nbad) + " sub calls");
         pc->unref();
         return;
@@ -227,6 +230,7 @@ void ParallelChannel::CallMethod(const pb::MethodDescriptor* method, RpcControll
         if (!s->sc.is_skip()) ++pc->nlaunched;
     }
     if (pc->nlaunched == 0) {
+        fiber::call_id_unlock(pc->cid);
         finish_parent(pc, EREQUEST, "all sub calls are skipped");
         pc->unref();
         return;

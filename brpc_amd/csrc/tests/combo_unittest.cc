@@ -332,3 +332,185 @@ TEST(ParallelChannel, scatter_attachment_slices_and_gather) {
     }
     EXPECT_EQ(covered, whole.size());
 }
+
+// ------------------------------------------------------------ more ParallelChannel semantics
+// (reference test/brpc_channel_unittest.cpp: skip/bad sub calls, merger
+// verdicts, success_limit, parent timeout, health)
+
+namespace {
+
+class OddSkipMapper : public CallMapper {
+public:
+    bool all = false, bad = false;
+    SubCall Map(int i, int n, const pb::MethodDescriptor* m, const pb::Message* req, pb::Message* res) override {
+        if (bad && i == 1) return SubCall::Bad();
+        if (all || i % 2 == 1) return SubCall::Skip();
+        return SubCall(m, req, res->New(), SubCall::DELETE_RESPONSE);
+    }
+};
+
+class VerdictMerger : public ResponseMerger {
+public:
+    explicit VerdictMerger(Result r) : _r(r) {}
+    Result Merge(pb::Message* response, const pb::Message* sub) override {
+        if (_r == MERGED) response->MergeFrom(*sub);
+        return _r;
+    }
+
+private:
+    Result _r;
+};
+
+int call(ChannelBase* ch, const std::string& msg, std::string* out, int64_t sleep_us = 0, int timeout_ms = -1,
+         int64_t* elapsed_us = nullptr) {
+    example::EchoService_Stub stub(ch);
+    Controller cntl;
+    if (timeout_ms > 0) cntl.set_timeout_ms(timeout_ms);
+    example::EchoRequest req;
+    example::EchoResponse res;
+    req.set_message(msg);
+    if (sleep_us) req.set_sleep_us(sleep_us);
+    const int64_t t0 = monotonic_us();
+    stub.Echo(&cntl, &req, &res, nullptr);
+    if (elapsed_us) *elapsed_us = monotonic_us() - t0;
+    if (out) *out = res.message();
+    return cntl.Failed() ? cntl.ErrorCode() : 0;
+}
+
+}  // namespace
+
+TEST(ParallelChannel, skipped_and_bad_sub_calls) {
+    TaggedServer a("a"), b("b"), c("c"), d("d");
+    ParallelChannelOptions po;
+    po.timeout_ms = 2000;
+    ParallelChannel pc;
+    pc.Init(&po);
+    auto mapper = std::make_shared<OddSkipMapper>();
+    auto merger = std::make_shared<ConcatMerger>();
+    for (TaggedServer* s : {&a, &b, &c, &d}) pc.AddChannel(make_channel(s->addr()), OWNS_CHANNEL, mapper, merger);
+    std::string out;
+    ASSERT_EQ(call(&pc, "k", &out), 0);
+    EXPECT_TRUE(split(out) == (std::set<std::string>{"k@a", "k@c"}));  // odd sub calls skipped
+    mapper->all = true;
+    EXPECT_EQ(call(&pc, "k", &out), EREQUEST);  // nothing left to call
+    mapper->all = false;
+    mapper->bad = true;
+    EXPECT_EQ(call(&pc, "k", &out), EREQUEST);  // one Bad() fails the whole call before any I/O
+}
+
+TEST(ParallelChannel, merger_verdicts) {
+    TaggedServer a("a"), b("b"), c("c");
+    ParallelChannelOptions po;
+    po.timeout_ms = 2000;
+    {
+        // one FAIL is one failed sub call: tolerated by the default limit
+        ParallelChannel pc;
+        pc.Init(&po);
+        pc.AddChannel(make_channel(a.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+        pc.AddChannel(make_channel(b.addr()), OWNS_CHANNEL, nullptr,
+                      std::make_shared<VerdictMerger>(ResponseMerger::FAIL));
+        pc.AddChannel(make_channel(c.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+        std::string out;
+        EXPECT_EQ(call(&pc, "v", &out), 0);
+        EXPECT_TRUE(split(out) == (std::set<std::string>{"v@a", "v@c"}));
+    }
+    {
+        ParallelChannelOptions strict = po;
+        strict.fail_limit = 1;
+        ParallelChannel pc;
+        pc.Init(&strict);
+        pc.AddChannel(make_channel(a.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+        pc.AddChannel(make_channel(b.addr()), OWNS_CHANNEL, nullptr,
+                      std::make_shared<VerdictMerger>(ResponseMerger::FAIL));
+        EXPECT_EQ(call(&pc, "v", nullptr), ETOOMANYFAILS);
+    }
+    {
+        ParallelChannel pc;
+        pc.Init(&po);
+        pc.AddChannel(make_channel(a.addr()), OWNS_CHANNEL, nullptr,
+                      std::make_shared<VerdictMerger>(ResponseMerger::FAIL_ALL));
+        pc.AddChannel(make_channel(b.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+        EXPECT_EQ(call(&pc, "v", nullptr), ERESPONSE);
+    }
+}
+
+TEST(ParallelChannel, success_limit_returns_without_the_slow_sub_call) {
+    TaggedServer fast("fast"), slow("slow");
+    slow.echo.delay_us = 400000;
+    ParallelChannelOptions po;
+    po.timeout_ms = 3000;
+    po.success_limit = 1;
+    ParallelChannel pc;
+    pc.Init(&po);
+    pc.AddChannel(make_channel(fast.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+    pc.AddChannel(make_channel(slow.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+    std::string out;
+    int64_t us = 0;
+    ASSERT_EQ(call(&pc, "s", &out, 0, -1, &us), 0);
+    EXPECT_EQ(out, "s@fast");
+    EXPECT_LT(us, 300000);
+    // without the limit the parent waits for both
+    ParallelChannelOptions all = po;
+    all.success_limit = -1;
+    ParallelChannel pc2;
+    pc2.Init(&all);
+    pc2.AddChannel(make_channel(fast.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+    pc2.AddChannel(make_channel(slow.addr()), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+    ASSERT_EQ(call(&pc2, "s", &out, 0, -1, &us), 0);
+    EXPECT_TRUE(split(out) == (std::set<std::string>{"s@fast", "s@slow"}));
+    EXPECT_GE(us, 350000);
+}
+
+TEST(ParallelChannel, parent_timeout_cancels_sub_calls_and_health) {
+    TaggedServer a("a"), b("b");
+    ParallelChannelOptions po;
+    po.timeout_ms = 5000;
+    ParallelChannel pc;
+    pc.Init(&po);
+    pc.AddChannel(make_channel(a.addr(), 5000), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+    pc.AddChannel(make_channel(b.addr(), 5000), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+    int64_t us = 0;
+    // the servers sleep 1 s; the parent's 150 ms deadline ends the call
+    EXPECT_NE(call(&pc, "t", nullptr, 1000000, 150, &us), 0);
+    EXPECT_LT(us, 800000);
+    EXPECT_EQ(pc.CheckHealth(), 0);
+    EXPECT_EQ(pc.channel_count(), 2);
+    // a dead sub channel: healthy while fail_limit tolerates it
+    ParallelChannelOptions lim = po;
+    lim.fail_limit = 1;
+    ParallelChannel pc2;
+    pc2.Init(&lim);
+    pc2.AddChannel(make_channel(a.addr()), OWNS_CHANNEL, nullptr, nullptr);
+    pc2.AddChannel(make_channel("127.0.0.1:1", 200), OWNS_CHANNEL, nullptr, nullptr);
+    EXPECT_NE(call(&pc2, "h", nullptr), 0);  // the dead one fails the call (fail_limit 1)
+    ParallelChannel empty;
+    EXPECT_EQ(empty.CheckHealth(), -1);
+}
+
+TEST(SelectiveChannel, remove_channel_moves_traffic) {
+    TaggedServer a("a"), b("b");
+    SelectiveChannelOptions so;
+    so.timeout_ms = 2000;
+    SelectiveChannel sc;
+    ASSERT_EQ(sc.Init(&so), 0);
+    const int ha = sc.AddChannel(make_channel(a.addr()));
+    const int hb = sc.AddChannel(make_channel(b.addr()));
+    ASSERT_GE(ha, 0);
+    ASSERT_GE(hb, 0);
+    std::set<std::string> seen;
+    std::string out;
+    for (int i = 0; i < 40; ++i) {
+        ASSERT_EQ(call(&sc, "r", &out), 0);
+        seen.insert(out);
+    }
+    EXPECT_EQ(seen.size(), 2u);  // balanced over both
+    sc.RemoveAndDestroyChannel(ha);
+    seen.clear();
+    for (int i = 0; i < 20; ++i) {
+        ASSERT_EQ(call(&sc, "r", &out), 0);
+        seen.insert(out);
+    }
+    EXPECT_TRUE(seen == (std::set<std::string>{"r@b"}));
+    sc.RemoveAndDestroyChannel(hb);
+    EXPECT_EQ(call(&sc, "r", &out), EHOSTDOWN);
+}
