@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <string>
 #include <thread>
@@ -212,4 +213,82 @@ TEST(Rpcz, device_annotation_recorded) {
     EXPECT_TRUE(d.find("[gpu] copy+crc32c 4 segs 262144 B dev0 0.042 ms") != std::string::npos);
     delete s;
     FLAGS_enable_rpcz = false;
+}
+
+namespace {
+// Server A answers by calling server B from inside its handler: the nested
+// client call must join the caller's trace (reference: Span::tls_parent,
+// span.cpp CreateClientSpan with a parent server span).
+class CascadeEcho : public example::EchoService {
+public:
+    Channel* downstream = nullptr;
+    void Echo(RpcController* c, const example::EchoRequest* req, example::EchoResponse* res, Closure* done) override {
+        ClosureGuard g(done);
+        TRACEPRINTF("cascade hop for %s", req->message().c_str());
+        example::EchoService_Stub stub(downstream);
+        Controller sub;
+        example::EchoRequest r2;
+        example::EchoResponse s2;
+        r2.set_message(req->message() + ">B");
+        stub.Echo(&sub, &r2, &s2, nullptr);
+        if (sub.Failed()) {
+            static_cast<Controller*>(c)->SetFailed(sub.ErrorCode(), "%s", sub.ErrorText().c_str());
+            return;
+        }
+        res->set_message(s2.message());
+    }
+};
+}  // namespace
+
+TEST(Rpcz, cascade_calls_share_one_trace) {
+    const std::string dir = make_tmpdir();
+    ASSERT_FALSE(dir.empty());
+    FLAGS_rpcz_database_dir = dir;
+    FLAGS_enable_rpcz = true;
+    EchoServer b;
+    ASSERT_GT(b.port, 0);
+    Channel to_b;
+    ASSERT_EQ(to_b.Init(("127.0.0.1:" + std::to_string(b.port)).c_str(), nullptr), 0);
+    Server a;
+    CascadeEcho cascade;
+    cascade.downstream = &to_b;
+    a.AddService(&cascade, SERVER_DOESNT_OWN_SERVICE);
+    ServerOptions o;
+    o.has_builtin_services = false;
+    ASSERT_EQ(a.Start("127.0.0.1:0", &o), 0);
+    Channel to_a;
+    ASSERT_EQ(to_a.Init(("127.0.0.1:" + std::to_string(a.listen_port())).c_str(), nullptr), 0);
+
+    const uint64_t t = echo_once(&to_a, "hop");
+    ASSERT_TRUE(t != 0);
+    // Records: client->A (C), A's server span (S) and B's server span (S).
+    // As in the reference, a server span shares its span id with the client
+    // span that called it, and the nested A->B client span is kept inside
+    // A's server span (local parent) rather than stored on its own.
+    std::vector<std::string> v = wait_trace(t, 3);
+    ASSERT_EQ(v.size(), 3u);
+    auto field = [](const std::string& x, const char* key) {
+        const size_t at = x.find(key);
+        return at == std::string::npos ? std::string() : x.substr(at + strlen(key), 16);
+    };
+    std::string client_span, a_span, b_parent;
+    int annotated = 0;
+    for (const std::string& x : v) {
+        EXPECT_TRUE(x.find(string_printf("trace=%016llx", (unsigned long long)t)) != std::string::npos);
+        annotated += x.find("cascade hop for hop") != std::string::npos;
+        if (x[0] == 'C') client_span = field(x, "span=");
+        if (x[0] == 'S' && field(x, "parent=") == "0000000000000000") a_span = field(x, "span=");
+        if (x[0] == 'S' && field(x, "parent=") != "0000000000000000") b_parent = field(x, "parent=");
+    }
+    EXPECT_FALSE(client_span.empty());
+    EXPECT_EQ(a_span, client_span);  // the call's two halves share one id
+    EXPECT_EQ(b_parent, a_span);     // B was called from inside A
+    EXPECT_EQ(annotated, 1);         // TRACEPRINTF lands in A's server span only
+    // an unrelated call starts a new trace
+    const uint64_t t2 = echo_once(&to_a, "again");
+    EXPECT_TRUE(t2 != 0 && t2 != t);
+    EXPECT_EQ(wait_trace(t2, 3).size(), 3u);
+    FLAGS_enable_rpcz = false;
+    a.Stop(0);
+    a.Join();
 }
