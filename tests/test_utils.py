@@ -76,3 +76,22 @@ def test_snapshots_and_rates_follow_traffic():
             wait_for_var(name, lambda v: False, timeout=0.05)
     finally:
         s.stop()
+
+
+def test_rccl_plane_api_on_cpu():
+    """Without a GPU the plane is never joined; the threshold flag still
+    round-trips (the bench toggles it around its rccl leg)."""
+    from brpc_amd import parallel
+    topo = parallel.Topology(rank=0, world_size=1, local_rank=0, local_world_size=1, device=-1)
+    assert parallel.init_rccl_plane(topo) is False
+    assert native.gpu.rccl_active() is False
+    before = get_flag("rccl_min_bytes")
+    try:
+        parallel.set_rccl_min_bytes(32768)
+        assert get_flag_typed("rccl_min_bytes") == 32768
+        parallel.set_rccl_min_bytes(None)
+        assert get_flag_typed("rccl_min_bytes") == 1 << 40
+    finally:
+        set_flag("rccl_min_bytes", before)
+    st = parallel.rccl_stats()
+    assert st["sent_payloads"] == 0 and st["aborts"] == 0
