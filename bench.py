@@ -48,7 +48,16 @@ def parse():
     ap.add_argument("--skip-64k", action="store_true")
     ap.add_argument("--skip-fanout", action="store_true", help="skip the ParallelChannel fan-out leg (N>1)")
     ap.add_argument("--skip-grpc", action="store_true", help="skip the h2:grpc + snappy leg")
-    ap.add_argument("--skip-rccl", action="store_true", help="skip the RCCL-plane 64 KiB leg (GPU only)")
+    ap.add_argument("--skip-rccl", action="store_true", help="skip the RCCL-plane legs")
+    ap.add_argument("--rccl-stub", action="store_true",
+                    help="run the RCCL payload plane on the stub library (CPU rehearsal of the multi-rank plane: "
+                         "host payloads, gloo control plane)")
+    ap.add_argument("--skip-1m", action="store_true", help="skip the 1 MiB payload legs (BASELINE config 5 analog)")
+    ap.add_argument("--requests-per-step-1m", type=int, default=2000, help="1 MiB requests per step and rank")
+    ap.add_argument("--skip-sweep", action="store_true",
+                    help="skip the rdma_performance-style size x queue-depth sweep (lending vs RCCL plane)")
+    ap.add_argument("--sweep-seconds", type=float, default=0.4, help="timed seconds per sweep point")
+    ap.add_argument("--stream-min-s", type=float, default=1.0, help="the stream leg is timed for at least this long")
     ap.add_argument("--requests-per-step-grpc", type=int, default=2000)
     ap.add_argument("--requests-per-step-fanout", type=int, default=500)
     ap.add_argument("--skip-stream", action="store_true",
@@ -142,7 +151,16 @@ def main():
         print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, topo.world_size), file=sys.stderr)
     workers = a.workers or auto_workers(topo.local_world_size)
     native.set_flag("fiber_concurrency", str(workers))
-    l3 = a.cpu_l3_domain if a.cpu_l3_domain != -2 else auto_l3_domain(topo.local_rank, topo.local_world_size)
+    placement = {}
+    if a.cpu_l3_domain != -2:
+        l3 = a.cpu_l3_domain
+    elif topo.device >= 0:
+        # on the GPU's NUMA node (csrc/gpu PciBusId -> local_cpulist)
+        from brpc_amd.parallel.placement import choose_l3_domain  # noqa: E402
+        l3, placement = choose_l3_domain(topo.local_rank, topo.local_world_size, topo.device,
+                                         torch.cuda.device_count() if torch.cuda.is_available() else 0)
+    else:
+        l3 = auto_l3_domain(topo.local_rank, topo.local_world_size)
     if l3 >= 0:
         native.set_flag("cpu_l3_domain", str(l3))
     # Busy-polling dispatcher: one core per rank keeps polling epoll while
@@ -164,12 +182,35 @@ def main():
     # ranks, joined before any connection exists so every hello carries the
     # rank. It only carries payloads during the rccl leg (-rccl_min_bytes).
     rccl_up = False
-    if cuda and not a.skip_rccl:
+    if (cuda or a.rccl_stub) and not a.skip_rccl:
         try:
-            rccl_up = parallel.init_rccl_plane(topo)
+            rccl_up = parallel.init_rccl_plane(topo, library=parallel.stub_library() if a.rccl_stub else None)
         except RuntimeError as e:
             print("rccl plane unavailable: %s" % e, file=sys.stderr)
         rccl_up = parallel.allreduce_sum(1 if rccl_up else 0, topo) == topo.world_size
+    dev_payload = cuda and not a.host_payload  # attachments in HBM (else host memory)
+
+    # Per-leg transport mix: which path did the payloads of each leg take?
+    # Summed over ranks (xGMI lends, of them cross-GPU pulls; RCCL plane
+    # payloads, rounds, aborts, credit stalls; staged fallbacks).
+    def transport_snapshot():
+        x = native.gpu.xgmi_stats()
+        r = parallel.rccl_stats()
+        return {"xgmi_lent_payloads": x["sent_payloads"], "xgmi_pulled_payloads": x["recv_payloads"],
+                "xgmi_cross_gpu_payloads": x["cross_device_payloads"],
+                "xgmi_cross_gpu_pull_failures": x["cross_device_pull_failures"],
+                "xgmi_ring_full_fallbacks": x["ring_full_fallbacks"], "xgmi_crc_failures": x["crc_failures"],
+                "xgmi_attach_failures": x["attach_failures"], "xgmi_peer_access_pairs": x["peer_access_enabled"],
+                "copy_launches": x["copy_launches"],
+                "rccl_payloads": r["recv_payloads"], "rccl_rounds": r["rounds"], "rccl_aborts": r["aborts"],
+                "rccl_credit_stalls": r["credit_stalls"], "rccl_recv_timeouts": r["recv_timeouts"]}
+
+    def transport_delta(s0):
+        s1 = transport_snapshot()
+        d = {k: int(parallel.allreduce_sum(s1[k] - s0[k], topo)) for k in sorted(s0)}
+        d = {k: v for k, v in d.items() if v}  # only what moved (or failed)
+        d["rccl_world"] = parallel.rccl_stats()["world"]
+        return d
 
     server = start_echo_server("127.0.0.1:0", num_threads=workers, gpu_device=topo.device)
     addrs = parallel.exchange_addresses(server.address, topo)
@@ -184,6 +225,7 @@ def main():
         for _ in range(warmup):
             press.run_requests(n)
         press.reset_stats()
+        tr0 = transport_snapshot()
         parallel.barrier(topo)
         sync()
         t0 = time.perf_counter()
@@ -202,6 +244,7 @@ def main():
         p99_max = parallel.allreduce_max(st["p99_us"], topo)
         p50_max = parallel.allreduce_max(st["p50_us"], topo)
         del press
+        tr = transport_delta(tr0)
         step_seq = [n / x for x in step_s if x > 0]
         step_qps = sorted(step_seq)
         return {
@@ -217,6 +260,7 @@ def main():
             "step_qps_median": step_qps[len(step_qps) // 2] if step_qps else 0.0,
             "step_qps_min": step_qps[0] if step_qps else 0.0,
             "step_qps_max": step_qps[-1] if step_qps else 0.0,
+            "transport": tr,
         }
 
     def latency_sample():
@@ -228,11 +272,19 @@ def main():
         parallel.barrier(topo)
         press.run_for(0.5)  # warm-up: the first calls of a connection pay lazy setup
         press.reset_stats()
+        import resource  # noqa: E402
+        r0, w0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
         press.run_for(a.latency_sample_s)
+        r1, w1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
         st = press.stats()
+        # the whole rank (client, server, dispatcher, timers) while it serves
+        # 100 QPS: what the latency costs in CPU
+        cpu_pct = 100.0 * ((r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)) / max(1e-9, w1 - w0)
         out = {"p50_us": parallel.allreduce_max(st["p50_us"], topo),
                "p99_us": parallel.allreduce_max(st["p99_us"], topo),
-               "avg_us": parallel.allreduce_max(st["avg_us"], topo)}
+               "p999_us": parallel.allreduce_max(st["p999_us"], topo),
+               "avg_us": parallel.allreduce_max(st["avg_us"], topo),
+               "cpu_pct": parallel.allreduce_max(cpu_pct, topo)}
         del press
         return out
 
@@ -247,7 +299,7 @@ def main():
     # the xGMI transport (lent zero-copy, pulled once per hop by the batched
     # copy engine); the host-attachment leg is kept as the TCP reference.
     r64 = r64h = None
-    use_dev = cuda and not a.host_payload
+    use_dev = dev_payload
     if not a.skip_64k:
         wl64 = ECHO_64KB
         if a.requests_per_step_64k:
@@ -261,24 +313,31 @@ def main():
         if r64 is None:
             r64, r64h = r64h, None
 
-    # RCCL leg: the same 64 KiB HBM echo ring, but every payload (request
-    # and response) moves by ncclSend/ncclRecv on the job's communicator,
-    # announced by a per-pair sequence number in the RPC meta.
-    rc = None
-    if rccl_up and not a.skip_64k:
-        wlr = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=True,
-                                  requests_per_step=max(1, wl64.requests_per_step // 2)))
-        s0 = parallel.rccl_stats()
-        parallel.set_rccl_min_bytes(32768)  # the 64 KiB message carries a 65520 B attachment
+    def plane_leg(wl, steps, warmup):
+        # the same echo ring, but every attachment payload (request and
+        # response) moves over the RCCL payload plane (rounds of grouped
+        # ncclSend/ncclRecv), announced by a sequence number in the meta
+        parallel.set_rccl_min_bytes(32768)
         try:
-            rc = timed_leg(wlr, a.steps, a.warmup)
+            return timed_leg(wl, steps, warmup)
         finally:
             parallel.set_rccl_min_bytes(None)
-        s1 = parallel.rccl_stats()
-        rc["payloads"] = parallel.allreduce_sum(s1["recv_payloads"] - s0["recv_payloads"], topo)
-        rc["aborts"] = parallel.allreduce_sum(s1["aborts"] - s0["aborts"], topo)
-        groups = parallel.allreduce_sum(s1["groups"] - s0["groups"], topo)
-        rc["payloads_per_group"] = round(2 * rc["payloads"] / groups, 2) if groups else 0.0
+
+    rc = None
+    if rccl_up and not a.skip_64k:
+        wlr = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=dev_payload,
+                                  requests_per_step=max(1, wl64.requests_per_step // 2)))
+        rc = plane_leg(wlr, a.steps, a.warmup)
+
+    # 1 MiB legs (BASELINE config 5 analog: rdma_performance with 1 MB
+    # payloads): HBM attachments lent over xGMI, and over the RCCL plane.
+    r1m = r1mr = None
+    if not a.skip_1m:
+        wl1m = EchoWorkload("echo_1MB", request_size=16, attachment_size=1 << 20, device_attachment=dev_payload,
+                            requests_per_step=max(1, a.requests_per_step_1m))
+        r1m = timed_leg(wl1m, a.steps, a.warmup)
+        if rccl_up:
+            r1mr = plane_leg(wl1m, a.steps, a.warmup)
 
     # GPU-handler leg: 64 KiB host attachments that the server
     # runs through its GPU — gathered from the pinned socket blocks into HBM
@@ -319,11 +378,62 @@ def main():
             finally:
                 native.gpu.disable_snappy()
 
+    # Sweep (example/rdma_performance/client.cpp:35-48,221-300 analog):
+    # payload size x queue depth, lending vs the RCCL plane, each point a
+    # closed loop for --sweep-seconds; avg/p90/p99/p99.9 latency, GB/s and
+    # kQPS. The crossover (smallest size where the plane moves at least as
+    # many bytes as lending) is what -rccl_min_bytes should be.
+    sweep = None
+    if not a.skip_sweep and not a.skip_1m:
+        sweep = {"points": []}
+        sizes = [65536, 262144, 1 << 20, 4 << 20, 16 << 20]
+        base = "lend" if dev_payload else "tcp"  # HBM lent over xGMI, or host bytes inline on TCP
+        transports = [base] + (["rccl"] if rccl_up else [])
+        points = [(sz, 16) for sz in sizes] + [(1 << 20, qd) for qd in (1, 4, 64)]
+        if not dev_payload:  # inline bytes: stay under -socket_max_unwritten_bytes
+            points = [(sz, max(1, min(qd, (32 << 20) // sz))) for sz, qd in points]
+        for sz, qd in points:
+            for t in transports:
+                o = {"server": peer, "concurrency": qd, "attachment_size": sz, "request_size": 16,
+                     "device_attachment": dev_payload, "gpu_device": topo.device}
+                press = native.Press(o)
+                if t == "rccl":
+                    parallel.set_rccl_min_bytes(32768)
+                try:
+                    press.run_for(min(0.1, a.sweep_seconds))
+                    press.reset_stats()
+                    parallel.barrier(topo)
+                    t0 = time.perf_counter()
+                    press.run_for(a.sweep_seconds)
+                    dt = parallel.allreduce_max(time.perf_counter() - t0, topo)
+                    parallel.barrier(topo)
+                finally:
+                    if t == "rccl":
+                        parallel.set_rccl_min_bytes(None)
+                st = press.stats()
+                del press
+                ok = parallel.allreduce_sum(st["success"], topo)
+                sweep["points"].append({
+                    "transport": t, "bytes": sz, "queue_depth": qd,
+                    "kqps": round(ok / dt / 1e3, 2) if dt > 0 else 0.0,
+                    "gbytes_per_s": round(ok * sz * 2 / dt / 1e9, 3) if dt > 0 else 0.0,
+                    "avg_us": round(parallel.allreduce_max(st["avg_us"], topo), 1),
+                    "p90_us": parallel.allreduce_max(st["p90_us"], topo),
+                    "p99_us": parallel.allreduce_max(st["p99_us"], topo),
+                    "p999_us": parallel.allreduce_max(st["p999_us"], topo),
+                    "errors": int(parallel.allreduce_sum(st["error"], topo))})
+        if rccl_up:
+            qd_of = {sz: qd for sz, qd in points[:len(sizes)]}
+            by = {(p["transport"], p["bytes"]): p["gbytes_per_s"] for p in sweep["points"]
+                  if p["queue_depth"] == qd_of.get(p["bytes"])}
+            cross = [sz for sz in sizes if by.get(("rccl", sz), 0) >= by.get((base, sz), 1e30)]
+            sweep["rccl_crossover_bytes"] = cross[0] if cross else None
+
     # Streaming-RPC leg (BASELINE config 3): 64 KiB chunks through one
     # flow-controlled stream per peer — rank r to every other rank (to its
     # own server when alone); a step is 32 chunks per stream and ends when
     # every peer acknowledged them. On a GPU box the chunk lives in HBM and
-    # the frames lend it over xGMI.
+    # the frames lend it over xGMI. Timed for at least --stream-min-s.
     rs = None
     if not a.skip_stream:
         others = [x for i, x in enumerate(addrs) if i != topo.rank] or [peer]
@@ -335,15 +445,20 @@ def main():
         sp.run_steps(a.warmup)
         parallel.barrier(topo)
         sync()
+        # at least --steps steps, and steps until --stream-min-s elapsed
         t0 = time.perf_counter()
         sp.run_steps(a.steps)
+        nsteps = a.steps
+        while time.perf_counter() - t0 < a.stream_min_s:
+            sp.run_steps(max(1, a.steps // 2))
+            nsteps += max(1, a.steps // 2)
         parallel.barrier(topo)
         sync()
         dt = time.perf_counter() - t0
         dt_max = parallel.allreduce_max(dt, topo)
-        nbytes = parallel.allreduce_sum(a.steps * 32 * 65536 * len(others), topo)
-        rs = {"gbps": nbytes / dt_max / 1e9 if dt_max > 0 else 0.0, "ms_per_step": 1000.0 * dt_max / a.steps,
-              "device": bool(cuda), "fanout": len(others)}
+        nbytes = parallel.allreduce_sum(nsteps * 32 * 65536 * len(others), topo)
+        rs = {"gbps": nbytes / dt_max / 1e9 if dt_max > 0 else 0.0, "ms_per_step": 1000.0 * dt_max / nsteps,
+              "device": bool(cuda), "fanout": len(others), "steps": nsteps, "timed_s": dt_max}
         sp.close()
 
     # Pipeline leg (PP analog): one stream per rank through a chain of all
@@ -382,6 +497,7 @@ def main():
         for _ in range(a.warmup):
             press.run_requests(nf)
         press.reset_stats()
+        tr0 = transport_snapshot()
         parallel.barrier(topo)
         sync()
         t0 = time.perf_counter()
@@ -396,7 +512,8 @@ def main():
         rf = {"gbps": bytes_total / dt_max / 1e9 if dt_max > 0 else 0.0,
               "qps": parallel.allreduce_sum(st["success"], topo) / dt_max if dt_max > 0 else 0.0,
               "errors": int(parallel.allreduce_sum(st["error"], topo)),
-              "p99_us": parallel.allreduce_max(st["p99_us"], topo), "fanout": len(others)}
+              "p99_us": parallel.allreduce_max(st["p99_us"], topo), "fanout": len(others),
+              "transport": transport_delta(tr0)}
         del press
 
     # Scatter leg (TP analog): the 64 KiB HBM attachment is split across the
@@ -413,6 +530,7 @@ def main():
         for _ in range(a.warmup):
             press.run_requests(nf)
         press.reset_stats()
+        tr0 = transport_snapshot()
         parallel.barrier(topo)
         sync()
         t0 = time.perf_counter()
@@ -425,7 +543,7 @@ def main():
         dt_max = parallel.allreduce_max(dt, topo)
         rt = {"gbps": parallel.allreduce_sum(st["bytes"], topo) / dt_max / 1e9 if dt_max > 0 else 0.0,
               "errors": int(parallel.allreduce_sum(st["error"], topo)),
-              "p99_us": parallel.allreduce_max(st["p99_us"], topo)}
+              "p99_us": parallel.allreduce_max(st["p99_us"], topo), "transport": transport_delta(tr0)}
         del press
 
     # Routing leg (EP analog): every call carries a key; a consistent-hash
@@ -440,6 +558,7 @@ def main():
         for _ in range(a.warmup):
             press.run_requests(nf)
         press.reset_stats()
+        tr0 = transport_snapshot()
         parallel.barrier(topo)
         sync()
         t0 = time.perf_counter()
@@ -452,7 +571,7 @@ def main():
         dt_max = parallel.allreduce_max(dt, topo)
         rr = {"qps": parallel.allreduce_sum(st["success"], topo) / dt_max if dt_max > 0 else 0.0,
               "errors": int(parallel.allreduce_sum(st["error"], topo)),
-              "p99_us": parallel.allreduce_max(st["p99_us"], topo)}
+              "p99_us": parallel.allreduce_max(st["p99_us"], topo), "transport": transport_delta(tr0)}
         del press
 
     if not a.latency_first:
@@ -460,6 +579,7 @@ def main():
     parallel.barrier(topo)
     server.stop()
 
+    plane_aborts = int(parallel.allreduce_sum(parallel.rccl_stats()["aborts"], topo))
     if topo.rank == 0:
         n = topo.world_size
         out = {
@@ -484,6 +604,8 @@ def main():
                 "fiber_workers_per_rank": workers,
                 "cpu_l3_domain_rank0": l3,
                 "dispatcher_poll_us": max(0, a.dispatcher_poll_us),
+                "placement_rank0": placement,
+                "control_plane": topo.backend or "none",
             },
             "p50_us": r32["p50_us"],
             "p99_us": r32["p99_us"],
@@ -520,9 +642,31 @@ def main():
             out["rccl_64KB_p99_us"] = rc["p99_us"]
             out["rccl_64KB_gbytes_per_s"] = round(rc["qps"] * 65536 * 2 / 1e9, 3)
             out["rccl_64KB_errors"] = rc["errors"]
-            out["rccl_payloads"] = int(rc["payloads"])
-            out["rccl_ops_per_group"] = rc["payloads_per_group"]
-            out["rccl_aborts"] = int(rc["aborts"])
+            tr = rc["transport"]
+            out["rccl_payloads"] = tr.get("rccl_payloads", 0)
+            out["rccl_payloads_per_round"] = round(tr.get("rccl_payloads", 0) / max(1, tr.get("rccl_rounds", 0)), 2)
+            out["rccl_aborts"] = plane_aborts
+            out["rccl_world"] = tr["rccl_world"]
+        if r1m:
+            out["qps_1MB"] = round(r1m["qps"], 1)
+            out["gbytes_per_s_1MB"] = round(r1m["qps"] * (1 << 20) * 2 / 1e9, 3)
+            out["p99_us_1MB"] = r1m["p99_us"]
+            out["errors_1MB"] = r1m["errors"]
+            out["timed_s_1MB"] = round(r1m["elapsed_s"], 3)
+        if r1mr:
+            out["rccl_1MB_qps"] = round(r1mr["qps"], 1)
+            out["rccl_1MB_gbytes_per_s"] = round(r1mr["qps"] * (1 << 20) * 2 / 1e9, 3)
+            out["rccl_1MB_p99_us"] = r1mr["p99_us"]
+            out["rccl_1MB_errors"] = r1mr["errors"]
+        if sweep:
+            out["sweep"] = sweep["points"]
+            if "rccl_crossover_bytes" in sweep:
+                out["rccl_crossover_bytes"] = sweep["rccl_crossover_bytes"]
+        # which transport carried each leg's payloads (summed over ranks)
+        out["transport"] = {name: leg["transport"] for name, leg in
+                            (("echo_32B", r32), ("echo_64KB", r64), ("echo_64KB_host", r64h),
+                             ("rccl_64KB", rc), ("echo_1MB", r1m), ("rccl_1MB", r1mr), ("gpu_handler_64KB", rg))
+                            if leg}
         if rg:
             out["qps_64KB_gpu_handler"] = round(rg["qps"], 1)
             out["p99_us_64KB_gpu_handler"] = rg["p99_us"]
@@ -530,6 +674,8 @@ def main():
         if rs:
             out["stream_gbytes_per_s_64KB_chunks"] = round(rs["gbps"], 3)
             out["stream_ms_per_step"] = round(rs["ms_per_step"], 3)
+            out["stream_steps_timed"] = rs["steps"]
+            out["stream_timed_s"] = round(rs["timed_s"], 3)
             out["stream_device_chunks"] = rs["device"]
             out["stream_fanout_per_rank"] = rs["fanout"]
         if rf:
@@ -545,6 +691,9 @@ def main():
             out["route_calls_per_s"] = round(rr["qps"], 1)
             out["route_p99_us"] = rr["p99_us"]
             out["route_errors"] = rr["errors"]
+        for name, leg in (("fanout_64KB", rf), ("scatter_64KB", rt), ("route_64KB", rr)):
+            if leg:
+                out["transport"][name] = leg["transport"]
         if rt:
             out["scatter_gbytes_per_s"] = round(rt["gbps"], 3)
             out["scatter_p99_us"] = rt["p99_us"]
@@ -552,8 +701,13 @@ def main():
         if lat:
             out["p99_us_at_100qps"] = lat["p99_us"]
             out["p50_us_at_100qps"] = lat["p50_us"]
+            out["p999_us_at_100qps"] = lat["p999_us"]
+            out["cpu_pct_at_100qps"] = round(lat["cpu_pct"], 1)
             out["vs_baseline_p99_at_100qps"] = round(BASELINE_P99_US / lat["p99_us"], 4) if lat["p99_us"] else None
         print(json.dumps(out), flush=True)
+    parallel.barrier(topo)
+    if rccl_up:
+        parallel.shutdown_rccl_plane()
     parallel.destroy(topo)
 
 

@@ -40,6 +40,9 @@ int CurrentDevice();
 std::string DeviceName(int device);
 // gfx arch string of the device ("gfx950" on MI355X).
 std::string DeviceArch(int device);
+// PCI address of the device ("0000:75:00.0"), for placing the rank's CPU
+// threads on the GPU's NUMA node (/sys/bus/pci/devices/<bdf>/local_cpulist).
+std::string PciBusId(int device);
 
 // ---- memory
 void* Malloc(size_t n, int device, std::string* error = nullptr);

@@ -1,16 +1,23 @@
 #include "gpu/rccl_plane.h"
 
 #include <dlfcn.h>
+#include <errno.h>
+#include <fcntl.h>
 #include <hip/hip_runtime_api.h>
+#include <linux/futex.h>
 #include <rccl/rccl.h>
+#include <signal.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
-#include <chrono>
-#include <condition_variable>
+#include <climits>
 #include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -21,11 +28,19 @@
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
+#include "mrpc/proto/device_payload.pb.h"
 #include "var/var.h"
 
 DEFINE_int32(rccl_timeout_ms, 10000,
-             "abort the RCCL plane when its oldest group made no progress for this long");
-DEFINE_int32(rccl_max_group_ops, 256, "most sends/receives issued as one ncclGroupStart/End group");
+             "abort the plane when a round made no progress for this long (and fail Recv waits older than this)");
+DEFINE_string(rccl_library, "",
+              "RCCL library the plane dlopens (empty: the librccl.so the process has, else ROCm's); "
+              "the stub build/lib/libfake_rccl.so runs the plane on CPU hosts");
+DEFINE_int64(rccl_window_bytes, int64_t(256) << 20,
+             "receiver credit per source rank: payload bytes a peer may announce beyond what this rank consumed");
+DEFINE_int32(rccl_round_payloads, 64, "most payloads announced to one peer per round");
+DEFINE_int64(rccl_round_bytes, int64_t(64) << 20, "most payload bytes announced to one peer per round");
+DEFINE_int32(rccl_stash_ttl_ms, 30000, "received payloads nobody claims are dropped after this long");
 
 namespace mrpc {
 namespace gpu {
@@ -33,8 +48,7 @@ namespace rccl {
 
 namespace {
 
-// The entry points we use, resolved from the RCCL the process already has
-// (torch's) or from ROCm's.
+// ------------------------------------------------------------------ library
 struct Api {
     decltype(&::ncclGetUniqueId) get_unique_id = nullptr;
     decltype(&::ncclCommInitRank) comm_init_rank = nullptr;
@@ -45,12 +59,24 @@ struct Api {
     decltype(&::ncclGroupStart) group_start = nullptr;
     decltype(&::ncclGroupEnd) group_end = nullptr;
     decltype(&::ncclGetErrorString) error_string = nullptr;
+    // stub only (tests/stub/fake_rccl.cc): stream stand-ins
+    void* (*fake_stream_create)() = nullptr;
+    int (*fake_stream_memcpy)(void*, void*, const void*, size_t) = nullptr;
+    uint64_t (*fake_stream_record)(void*) = nullptr;
+    int (*fake_stream_query)(void*, uint64_t) = nullptr;
+    bool fake() const { return fake_stream_create != nullptr; }
 };
 
 bool load_api(Api* a, std::string* err) {
     static std::once_flag once;
     static void* lib = nullptr;
+    static std::string load_err;
     std::call_once(once, [] {
+        if (!FLAGS_rccl_library.empty()) {
+            lib = dlopen(FLAGS_rccl_library.c_str(), RTLD_NOW | RTLD_LOCAL);
+            if (!lib) load_err = std::string("dlopen ") + FLAGS_rccl_library + ": " + dlerror();
+            return;
+        }
         for (const char* n : {"librccl.so", "librccl.so.1"}) {
             lib = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
             if (lib) return;
@@ -59,15 +85,16 @@ bool load_api(Api* a, std::string* err) {
             lib = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
             if (lib) return;
         }
+        load_err = "librccl.so not found";
     });
     if (!lib) {
-        if (err) *err = "librccl.so not found";
+        if (err) *err = load_err;
         return false;
     }
 #define MRPC_RCCL_SYM(field, name)                                       \
     a->field = reinterpret_cast<decltype(a->field)>(dlsym(lib, name));   \
     if (!a->field) {                                                     \
-        if (err) *err = std::string("librccl.so lacks ") + name;         \
+        if (err) *err = std::string("rccl library lacks ") + name;       \
         return false;                                                    \
     }
     MRPC_RCCL_SYM(get_unique_id, "ncclGetUniqueId");
@@ -80,297 +107,785 @@ bool load_api(Api* a, std::string* err) {
     MRPC_RCCL_SYM(group_end, "ncclGroupEnd");
     MRPC_RCCL_SYM(error_string, "ncclGetErrorString");
 #undef MRPC_RCCL_SYM
+    if (dlsym(lib, "mrpcfake_abi_version")) {
+        a->fake_stream_create = reinterpret_cast<void* (*)()>(dlsym(lib, "mrpcfake_stream_create"));
+        a->fake_stream_memcpy =
+            reinterpret_cast<int (*)(void*, void*, const void*, size_t)>(dlsym(lib, "mrpcfake_stream_memcpy"));
+        a->fake_stream_record = reinterpret_cast<uint64_t (*)(void*)>(dlsym(lib, "mrpcfake_stream_record"));
+        a->fake_stream_query = reinterpret_cast<int (*)(void*, uint64_t)>(dlsym(lib, "mrpcfake_stream_query"));
+        if (!a->fake_stream_create || !a->fake_stream_memcpy || !a->fake_stream_record || !a->fake_stream_query) {
+            if (err) *err = "stub rccl library lacks its mrpcfake_stream_* functions";
+            return false;
+        }
+    }
     return true;
 }
 
-// Fibers receiving several payloads park on one butex: 0 pending, 1 done,
-// -1 failed.
-struct Waiter {
-    std::atomic<int>* butex = nullptr;
-    std::atomic<int> left{0};
-    std::atomic<bool> failed{false};
+// ------------------------------------------------------------------ streams
+// The stream-ordered work of a round: header upload, the group, header
+// download, a completion marker. HIP on MI355X; the stub's executor on CPU.
+class StreamOps {
+public:
+    virtual ~StreamOps() {}
+    virtual int init(int device, size_t hdr_bytes, std::string* err) = 0;
+    virtual void* stream() = 0;
+    // header buffers: host_out -> dev_out before the group, dev_in -> host_in after
+    char* host_out = nullptr;
+    char* host_in = nullptr;
+    char* dev_out = nullptr;
+    char* dev_in = nullptr;
+    virtual int upload(size_t n) = 0;
+    virtual int download(size_t n) = 0;
+    virtual int record(uint64_t* marker) = 0;
+    // 1 complete, 0 pending, -1 failed
+    virtual int query(uint64_t marker) = 0;
+    virtual void release(uint64_t marker) = 0;
+    virtual void* alloc(size_t len, Buf* out) = 0;
+    virtual bool accepts(const BufBlock* b) const = 0;
+    virtual bool host_memory() const = 0;
 };
 
-void finish(Waiter* w, bool ok) {
-    if (!w) return;
-    if (!ok) w->failed.store(true, std::memory_order_relaxed);
-    if (w->left.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-        // the waiter may return (and its Waiter die) as soon as the store
-        // lands; butexes are pooled, so waking through the copy is safe
-        std::atomic<int>* b = w->butex;
-        b->store(w->failed.load(std::memory_order_relaxed) ? -1 : 1, std::memory_order_release);
-        fiber::butex_wake_all(b);
+class HipOps : public StreamOps {
+public:
+    int init(int device, size_t hdr_bytes, std::string* err) override {
+        _device = device;
+        hipSetDevice(device);
+        if (hipStreamCreateWithFlags(&_stream, hipStreamNonBlocking) != hipSuccess) {
+            if (err) *err = "hipStreamCreate failed";
+            return -1;
+        }
+        void* d = nullptr;
+        void* h = nullptr;
+        if (hipMalloc(&d, 2 * hdr_bytes) != hipSuccess || hipHostMalloc(&h, 2 * hdr_bytes, 0) != hipSuccess) {
+            if (err) *err = "header buffers: allocation failed";
+            return -1;
+        }
+        memset(h, 0, 2 * hdr_bytes);
+        dev_out = static_cast<char*>(d);
+        dev_in = dev_out + hdr_bytes;
+        host_out = static_cast<char*>(h);
+        host_in = host_out + hdr_bytes;
+        return 0;
     }
+    void* stream() override { return _stream; }
+    int upload(size_t n) override {
+        return hipMemcpyAsync(dev_out, host_out, n, hipMemcpyHostToDevice, _stream) == hipSuccess ? 0 : -1;
+    }
+    int download(size_t n) override {
+        return hipMemcpyAsync(host_in, dev_in, n, hipMemcpyDeviceToHost, _stream) == hipSuccess ? 0 : -1;
+    }
+    int record(uint64_t* marker) override {
+        hipEvent_t ev = AcquireEvent();
+        if (!ev || hipEventRecord(ev, _stream) != hipSuccess) {
+            if (ev) ReleaseEvent(ev);
+            return -1;
+        }
+        *marker = reinterpret_cast<uint64_t>(ev);
+        return 0;
+    }
+    int query(uint64_t marker) override {
+        const hipError_t q = hipEventQuery(reinterpret_cast<hipEvent_t>(marker));
+        if (q == hipSuccess) return 1;
+        if (q == hipErrorNotReady) return 0;
+        return -1;
+    }
+    void release(uint64_t marker) override { ReleaseEvent(reinterpret_cast<hipEvent_t>(marker)); }
+    void* alloc(size_t len, Buf* out) override { return AppendNewDeviceBlock(out, len, _device); }
+    bool accepts(const BufBlock* b) const override { return b->kind == MemKind::DEVICE && b->device == _device; }
+    bool host_memory() const override { return false; }
+
+private:
+    int _device = -1;
+    hipStream_t _stream = nullptr;
+};
+
+void free_host(void* p, void*) { free(p); }
+
+class StubOps : public StreamOps {
+public:
+    explicit StubOps(const Api& a) : _api(a) {}
+    int init(int, size_t hdr_bytes, std::string* err) override {
+        _stream = _api.fake_stream_create();
+        char* b = static_cast<char*>(calloc(4, hdr_bytes));
+        if (!_stream || !b) {
+            if (err) *err = "stub stream creation failed";
+            return -1;
+        }
+        host_out = b;
+        host_in = b + hdr_bytes;
+        dev_out = b + 2 * hdr_bytes;
+        dev_in = b + 3 * hdr_bytes;
+        return 0;
+    }
+    void* stream() override { return _stream; }
+    int upload(size_t n) override { return _api.fake_stream_memcpy(_stream, dev_out, host_out, n); }
+    int download(size_t n) override { return _api.fake_stream_memcpy(_stream, host_in, dev_in, n); }
+    int record(uint64_t* marker) override {
+        *marker = _api.fake_stream_record(_stream);
+        return 0;
+    }
+    int query(uint64_t marker) override { return _api.fake_stream_query(_stream, marker); }
+    void release(uint64_t) override {}
+    void* alloc(size_t len, Buf* out) override {
+        void* p = malloc(std::max<size_t>(len, 1));
+        if (!p) return nullptr;
+        out->append_user_data(p, len, free_host);
+        return p;
+    }
+    bool accepts(const BufBlock* b) const override { return IsHostAccessible(b->kind); }
+    bool host_memory() const override { return true; }
+
+private:
+    const Api& _api;
+    void* _stream = nullptr;
+};
+
+// ------------------------------------------------------------------ wire
+const uint64_t kHdrMagic = 0x4d5250435244484full;  // "MRPCRDHO"
+const size_t kHdrBytes = 4096;
+const uint32_t kBusy = 1;
+
+struct HdrEntry {
+    uint64_t seq;
+    uint64_t len;
+};
+struct Hdr {
+    uint64_t magic;
+    uint64_t round;
+    uint64_t credit;   // cumulative bytes the receiver (sender of this header) accepts from us
+    uint32_t n;
+    uint32_t flags;
+    uint64_t from;
+    uint64_t reserved[3];
+    HdrEntry e[(kHdrBytes - 64) / sizeof(HdrEntry)];
+};
+static_assert(sizeof(Hdr) == kHdrBytes, "round header must be fixed-size");
+const int kMaxEntries = (int)((kHdrBytes - 64) / sizeof(HdrEntry));
+
+// The node's doorbell: POSIX shm shared by the ranks of the plane (a
+// private allocation for a one-rank plane).
+const uint64_t kBellMagic = 0x4d52504342454c4cull;  // "MRPCBELL"
+const int kMaxRanks = 64;
+struct Doorbell {
+    uint64_t magic;
+    std::atomic<uint64_t> want_round;
+    std::atomic<uint32_t> seq;     // futex word: bumped on every ring / abort
+    std::atomic<uint32_t> claim;   // the first aborting rank claims the reason slot
+    std::atomic<uint32_t> abort;   // 0, or 1 + the rank that aborted first
+    char reason[200];
+    std::atomic<int32_t> pid[kMaxRanks];
+};
+
+long futex(std::atomic<uint32_t>* w, int op, uint32_t val, const timespec* ts) {
+    return syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), op, val, ts, nullptr, 0);
 }
 
-struct Op {
-    bool is_send = false;
-    int peer = 0;
+uint64_t fnv1a(const std::string& s) {
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+    return h | 1;  // never 0: 0 means "no plane" in the hello
+}
+
+// ------------------------------------------------------------------ state
+struct Payload {
     uint64_t seq = 0;
     void* ptr = nullptr;
     size_t len = 0;
-    Buf hold;               // send: the payload; discard: the scratch block
-    Waiter* waiter = nullptr;
-    int64_t queued_us = 0;  // receives: when the reorder buffer took it
+    Buf hold;  // send: the bytes; receive: the landing block
 };
 
-struct Inflight {
-    hipEvent_t ev = nullptr;
-    std::vector<Op> ops;
-    int64_t issued_us = 0;
+struct Waiter {
+    std::atomic<int>* butex = nullptr;
+    int left = 0;  // under Plane::mu
+    bool failed = false;
 };
 
-std::atomic<int64_t> g_sent{0}, g_sent_bytes{0}, g_recv{0}, g_recv_bytes{0}, g_discarded{0}, g_groups{0},
-    g_aborts{0}, g_reorder{0};
+struct WaitSlot {
+    Waiter* w = nullptr;
+    Buf* out = nullptr;
+};
+
+struct Stashed {
+    Buf buf;
+    size_t len = 0;
+    int64_t since_us = 0;
+};
+
+typedef std::pair<int, uint64_t> Key;  // (source rank, sequence)
+
+struct PeerState {
+    std::deque<Payload> queued;       // not announced yet
+    std::vector<Payload> announced;   // announced in the last header: move next round
+    std::vector<Payload> incoming;    // from the peer's last header: receive next round
+    uint64_t next_seq = 0;
+    uint64_t announced_bytes = 0;     // cumulative, to this peer
+    uint64_t credit = 0;              // cumulative, granted by this peer
+    uint64_t consumed = 0;            // cumulative, from this peer (claimed/dropped)
+};
+
+std::atomic<int64_t> g_sent{0}, g_sent_bytes{0}, g_recv{0}, g_recv_bytes{0}, g_discarded{0}, g_rounds{0},
+    g_payload_rounds{0}, g_aborts{0}, g_credit_stalls{0}, g_expired{0}, g_recv_timeouts{0}, g_doorbells{0},
+    g_withdrawn{0};
+
+void finish_locked(Waiter* w, bool ok) {
+    if (!ok) w->failed = true;
+    if (--w->left == 0) {
+        std::atomic<int>* b = w->butex;
+        b->store(w->failed ? -1 : 1, std::memory_order_release);
+        fiber::butex_wake_all(b);
+    }
+}
 
 class Plane {
 public:
     Api api;
     ncclComm_t comm = nullptr;
-    hipStream_t stream = nullptr;
+    std::unique_ptr<StreamOps> ops;
     int device = -1, rank = 0, world = 0;
     uint64_t id = 0;
+    Doorbell* bell = nullptr;
+    std::string bell_name;
 
     std::mutex mu;
-    std::condition_variable cv;
-    std::vector<Op> ready;                       // issue in this order
-    std::vector<uint64_t> next_send, next_recv;  // per peer / per source
-    std::vector<std::map<uint64_t, Op>> held;    // per source: receives waiting for an earlier seq
-    std::map<uint64_t, Op> self_sends;           // self payloads waiting for their receive
-    bool dead = false, stop = false;
+    std::vector<PeerState> peers;
+    std::deque<Payload> self_q;
+    std::map<Key, Stashed> stash;
+    std::map<Key, WaitSlot> waiting;
+    std::map<Key, int64_t> discards;
+    bool idle = false, dead = false, stop = false;
+    bool busy_next = false;        // some rank's round header asked for another round
+    uint64_t completed_round = 0;  // poster only (read under mu by Send)
     std::atomic<bool> dead_flag{false};
-    std::vector<uint64_t> skipped_self;  // cancelled self payloads (never announced)
     std::thread poster;
+    int64_t last_expire_us = 0, last_liveness_us = 0;
 
+    // the round in flight (poster only)
+    std::vector<std::vector<Payload>> moving_send, moving_recv;
+    std::vector<Payload> self_send, self_recv;
+    uint64_t marker = 0;
+    bool marker_live = false;
+    std::vector<Buf> graveyard;  // blocks RCCL may still touch after an abort
+
+    // ---------------------------------------------------------------- API
     int64_t send(int peer, const void* p, size_t len, Buf&& hold) {
         std::lock_guard<std::mutex> g(mu);
-        if (dead || peer < 0 || peer >= world) return -1;
-        Op op;
-        op.is_send = true;
-        op.peer = peer;
-        op.seq = next_send[peer]++;
-        op.ptr = const_cast<void*>(p);
-        op.len = len;
-        op.hold = std::move(hold);
-        const int64_t seq = (int64_t)op.seq;
-        if (peer == rank) {
-            self_sends.emplace(op.seq, std::move(op));
-        } else {
-            ready.push_back(std::move(op));
-            cv.notify_one();
-        }
+        if (dead || stop || peer < 0 || peer >= world) return -1;
+        Payload pl;
+        pl.seq = peers[peer].next_seq++;
+        pl.ptr = const_cast<void*>(p);
+        pl.len = len;
+        pl.hold = std::move(hold);
+        const int64_t seq = (int64_t)pl.seq;
+        if (peer == rank) self_q.push_back(std::move(pl));
+        else peers[peer].queued.push_back(std::move(pl));
+        if (idle) ring_locked();
         return seq;
     }
 
-    // Queue receives (under mu); drains every source into `ready` in order.
-    bool add_recvs(std::vector<Op>* ops) {
-        std::lock_guard<std::mutex> g(mu);
-        if (dead) return false;
-        for (Op& op : *ops) {
-            if (op.seq < next_recv[op.peer] || held[op.peer].count(op.seq)) {
-                // a payload announced twice: the pair is out of sync
-                LOG(ERROR) << "rccl: duplicate receive of seq " << op.seq << " from rank " << op.peer;
-                finish(op.waiter, false);
-                continue;
-            }
-            const int src = op.peer;
-            const uint64_t seq = op.seq;
-            op.queued_us = monotonic_us();
-            held[src].emplace(seq, std::move(op));
-            if (seq != next_recv[src]) g_reorder.fetch_add(1, std::memory_order_relaxed);
-            auto& h = held[src];
-            for (auto it = h.find(next_recv[src]); it != h.end(); it = h.find(next_recv[src])) {
-                if (src == rank) {
-                    auto s = self_sends.find(it->first);
-                    if (s == self_sends.end()) break;  // cannot happen: sends are queued first
-                    ready.push_back(std::move(s->second));
-                    self_sends.erase(s);
-                }
-                ready.push_back(std::move(it->second));
-                h.erase(it);
-                ++next_recv[src];
-                if (src == rank) skip_cancelled_self();
-            }
+    void ring_locked() {
+        uint64_t want = completed_round + 1, cur = bell->want_round.load();
+        while (cur < want && !bell->want_round.compare_exchange_weak(cur, want)) {
         }
-        cv.notify_one();
-        return true;
+        bell->seq.fetch_add(1);
+        futex(&bell->seq, FUTEX_WAKE, INT_MAX, nullptr);
+        idle = false;
+        g_doorbells.fetch_add(1, std::memory_order_relaxed);
     }
 
-    // (mu held) step over self payloads that were queued but never announced
-    void skip_cancelled_self() {
-        for (auto it = std::find(skipped_self.begin(), skipped_self.end(), next_recv[rank]); it != skipped_self.end();
-             it = std::find(skipped_self.begin(), skipped_self.end(), next_recv[rank])) {
-            skipped_self.erase(it);
-            ++next_recv[rank];
-        }
-    }
-
-    void cancel_self(uint64_t seq) {
-        std::vector<Op> drop;
+    int recv(int n, const int* src, const uint64_t* seq, const size_t* len, Buf* outs) {
+        Waiter w;
+        w.butex = fiber::butex_create();
+        w.butex->store(0, std::memory_order_relaxed);
+        std::vector<Key> mine;
         {
             std::lock_guard<std::mutex> g(mu);
-            auto s = self_sends.find(seq);
-            if (s == self_sends.end()) return;
-            drop.push_back(std::move(s->second));
-            self_sends.erase(s);
-            skipped_self.push_back(seq);
-            skip_cancelled_self();
-            // receives that waited behind the cancelled one can go now
-            auto& h = held[rank];
-            for (auto it = h.find(next_recv[rank]); it != h.end(); it = h.find(next_recv[rank])) {
-                auto ss = self_sends.find(it->first);
-                if (ss == self_sends.end()) break;
-                ready.push_back(std::move(ss->second));
-                self_sends.erase(ss);
-                ready.push_back(std::move(it->second));
-                h.erase(it);
-                ++next_recv[rank];
-                skip_cancelled_self();
+            if (dead) {
+                fiber::butex_destroy(w.butex);
+                return -1;
             }
-            cv.notify_one();
-        }
-        fail_ops(&drop);
-    }
-
-    // (mu held) a receive waited in the reorder buffer for too long: the
-    // payload it waits behind was never announced
-    bool reorder_stalled(int64_t now) const {
-        for (const auto& h : held) {
-            for (const auto& kv : h) {
-                if (now - kv.second.queued_us > (int64_t)FLAGS_rccl_timeout_ms * 1000) return true;
-            }
-        }
-        return false;
-    }
-
-    bool any_held() const {
-        for (const auto& h : held)
-            if (!h.empty()) return true;
-        return false;
-    }
-
-    void fail_ops(std::vector<Op>* ops) {
-        for (Op& op : *ops) {
-            op.hold.clear();
-            finish(op.waiter, false);
-        }
-        ops->clear();
-    }
-
-    // Called by the poster with mu NOT held.
-    void abort(std::deque<Inflight>* inflight, const char* why) {
-        LOG(ERROR) << "rccl plane aborted: " << why << " (payloads fall back to xGMI lending)";
-        g_aborts.fetch_add(1, std::memory_order_relaxed);
-        if (comm) api.comm_abort(comm);
-        comm = nullptr;
-        std::vector<Op> pending;
-        {
-            std::lock_guard<std::mutex> g(mu);
-            dead = true;
-            dead_flag.store(true, std::memory_order_release);
-            pending.swap(ready);
-            for (auto& h : held)
-                for (auto& kv : h) pending.push_back(std::move(kv.second));
-            for (auto& kv : self_sends) pending.push_back(std::move(kv.second));
-            held.assign(held.size(), {});
-            self_sends.clear();
-        }
-        fail_ops(&pending);
-        for (Inflight& f : *inflight) {
-            fail_ops(&f.ops);
-            if (f.ev) ReleaseEvent(f.ev);
-        }
-        inflight->clear();
-    }
-
-    void complete(Inflight* f) {
-        for (Op& op : f->ops) {
-            if (op.is_send) {
-                g_sent.fetch_add(1, std::memory_order_relaxed);
-                g_sent_bytes.fetch_add((int64_t)op.len, std::memory_order_relaxed);
-            } else if (op.waiter) {
-                g_recv.fetch_add(1, std::memory_order_relaxed);
-                g_recv_bytes.fetch_add((int64_t)op.len, std::memory_order_relaxed);
-            } else {
-                g_discarded.fetch_add(1, std::memory_order_relaxed);
-            }
-            op.hold.clear();
-            finish(op.waiter, true);
-        }
-        ReleaseEvent(f->ev);
-    }
-
-    void run() {
-        hipSetDevice(device);
-        std::deque<Inflight> inflight;
-        std::vector<Op> batch;
-        for (;;) {
-            bool stalled = false;
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                if (inflight.empty() && !any_held()) {
-                    cv.wait(lk, [&] { return stop || !ready.empty(); });
-                } else if (ready.empty()) {
-                    const auto nap = inflight.empty() ? std::chrono::microseconds(5000) : std::chrono::microseconds(20);
-                    cv.wait_for(lk, nap, [&] { return stop || !ready.empty(); });
-                }
-                if (stop) break;
-                stalled = !dead && reorder_stalled(monotonic_us());
-                const size_t n = std::min(ready.size(), (size_t)std::max(1, FLAGS_rccl_max_group_ops));
-                // never split a self pair (send directly followed by its receive)
-                size_t cut = n;
-                if (cut < ready.size() && cut > 0 && ready[cut - 1].is_send && ready[cut - 1].peer == rank) ++cut;
-                batch.assign(std::make_move_iterator(ready.begin()), std::make_move_iterator(ready.begin() + cut));
-                ready.erase(ready.begin(), ready.begin() + cut);
-            }
-            if (stalled) {
-                abort(&inflight, "a receive waited -rccl_timeout_ms for an earlier payload that never came");
-                continue;
-            }
-            if (!batch.empty() && comm) {
-                ncclResult_t r = api.group_start();
-                for (const Op& op : batch) {
-                    if (r != ncclSuccess) break;
-                    r = op.is_send ? api.send(op.ptr, op.len, ncclUint8, op.peer, comm, stream)
-                                   : api.recv(op.ptr, op.len, ncclUint8, op.peer, comm, stream);
-                }
-                const ncclResult_t e = api.group_end();
-                if (r == ncclSuccess) r = e;
-                Inflight f;
-                f.ev = AcquireEvent();
-                f.ops.swap(batch);
-                f.issued_us = monotonic_us();
-                const bool rec_ok = f.ev && hipEventRecord(f.ev, stream) == hipSuccess;
-                inflight.push_back(std::move(f));
-                g_groups.fetch_add(1, std::memory_order_relaxed);
-                if (r != ncclSuccess || !rec_ok) {
-                    abort(&inflight, r != ncclSuccess ? api.error_string(r) : "event record failed");
+            for (int i = 0; i < n; ++i) {
+                const Key k(src[i], seq[i]);
+                if (src[i] < 0 || src[i] >= world) {
+                    w.failed = true;
                     continue;
                 }
-            } else if (!batch.empty()) {
-                fail_ops(&batch);
-            }
-            while (!inflight.empty()) {
-                const hipError_t q = hipEventQuery(inflight.front().ev);
-                if (q == hipErrorNotReady) break;
-                if (q != hipSuccess) {
-                    abort(&inflight, hipGetErrorString(q));
-                    break;
+                auto s = stash.find(k);
+                if (s != stash.end()) {
+                    if (s->second.len != len[i]) w.failed = true;
+                    outs[i] = std::move(s->second.buf);
+                    consume_locked(src[i], s->second.len);
+                    stash.erase(s);
+                    continue;
                 }
-                complete(&inflight.front());
-                inflight.pop_front();
-            }
-            if (!inflight.empty() && comm) {
-                ncclResult_t ae = ncclSuccess;
-                api.async_error(comm, &ae);
-                if (ae != ncclSuccess && ae != ncclInProgress) {
-                    abort(&inflight, api.error_string(ae));
-                } else if (monotonic_us() - inflight.front().issued_us > (int64_t)FLAGS_rccl_timeout_ms * 1000) {
-                    abort(&inflight, "no progress within -rccl_timeout_ms");
+                if (waiting.count(k)) {
+                    w.failed = true;
+                    continue;
                 }
+                waiting[k] = WaitSlot{&w, &outs[i]};
+                mine.push_back(k);
+                ++w.left;
+            }
+            if (w.left == 0) w.butex->store(w.failed ? -1 : 1, std::memory_order_relaxed);
+        }
+        const int64_t deadline = monotonic_us() + (int64_t)FLAGS_rccl_timeout_ms * 1000;
+        while (w.butex->load(std::memory_order_acquire) == 0) {
+            const int64_t now = monotonic_us();
+            if (now >= deadline) break;
+            timespec ts = abstime_after_us(deadline - now);
+            fiber::butex_wait(w.butex, 0, &ts);
+        }
+        int rc;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            rc = w.butex->load(std::memory_order_acquire);
+            if (rc == 0) {  // timed out: withdraw what is still pending
+                for (const Key& k : mine) {
+                    auto it = waiting.find(k);
+                    if (it != waiting.end() && it->second.w == &w) {
+                        waiting.erase(it);
+                        discards[k] = monotonic_us();
+                    }
+                }
+                g_recv_timeouts.fetch_add(1, std::memory_order_relaxed);
+                rc = -1;
             }
         }
-        abort(&inflight, "shutdown");
+        fiber::butex_destroy(w.butex);
+        if (rc != 1) {
+            for (int i = 0; i < n; ++i) outs[i].clear();
+            return -1;
+        }
+        return 0;
+    }
+
+    static timespec abstime_after_us(int64_t us) {
+        timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        const int64_t ns = ts.tv_nsec + (us % 1000000) * 1000;
+        ts.tv_sec += us / 1000000 + ns / 1000000000;
+        ts.tv_nsec = ns % 1000000000;
+        return ts;
+    }
+
+    void consume_locked(int src, size_t len) { peers[src].consumed += len; }
+
+    void discard(int src, uint64_t seq, size_t len) {
+        (void)len;
+        std::lock_guard<std::mutex> g(mu);
+        if (src < 0 || src >= world) return;
+        const Key k(src, seq);
+        auto s = stash.find(k);
+        if (s != stash.end()) {
+            consume_locked(src, s->second.len);
+            stash.erase(s);
+            g_discarded.fetch_add(1, std::memory_order_relaxed);
+            return;
+        }
+        discards[k] = monotonic_us();
+    }
+
+    void cancelled(int peer, uint64_t seq) {
+        Buf drop;
+        std::lock_guard<std::mutex> g(mu);
+        if (peer < 0 || peer >= world) return;
+        std::deque<Payload>& q = peer == rank ? self_q : peers[peer].queued;
+        for (auto it = q.begin(); it != q.end(); ++it) {
+            if (it->seq == seq) {
+                drop = std::move(it->hold);
+                q.erase(it);
+                g_withdrawn.fetch_add(1, std::memory_order_relaxed);
+                return;
+            }
+        }
+        // already announced: the receiver's stash expires it
+    }
+
+    // ---------------------------------------------------------------- poster
+    void run() {
+        if (!ops->host_memory()) hipSetDevice(device);
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                for (;;) {
+                    if (stop || dead) break;
+                    if (bell->abort.load(std::memory_order_acquire)) break;
+                    const bool local = !self_q.empty() || any_queued_locked();
+                    const uint64_t want = bell->want_round.load(std::memory_order_acquire);
+                    if (busy_next || want > completed_round) break;
+                    if (local) {
+                        ring_locked();  // the other ranks learn about round k+1 from the doorbell
+                        break;
+                    }
+                    idle = true;
+                    const uint32_t s = bell->seq.load(std::memory_order_acquire);
+                    housekeeping_locked();
+                    lk.unlock();
+                    timespec ts{0, 50 * 1000 * 1000};
+                    futex(&bell->seq, FUTEX_WAIT, s, &ts);
+                    lk.lock();
+                    if (check_liveness()) break;
+                }
+                idle = false;
+                if (stop) break;
+            }
+            if (bell->abort.load(std::memory_order_acquire)) {
+                abort(remote_reason(), false, !remote_is_shutdown());
+                break;
+            }
+            if (dead) break;
+            if (run_round(completed_round + 1) != 0) break;
+        }
+        if (!dead) abort("rank shut down", true, /*is_error=*/false);
+    }
+
+    bool any_queued_locked() const {
+        for (const PeerState& p : peers)
+            if (!p.queued.empty()) return true;
+        return false;
+    }
+
+    bool remote_is_shutdown() const { return strcmp(bell->reason, "rank shut down") == 0; }
+
+    std::string remote_reason() const {
+        const uint32_t who = bell->abort.load();
+        return "rank " + std::to_string((int)who - 1) + " aborted the plane: " + std::string(bell->reason);
+    }
+
+    // (mu held) expire unclaimed payloads and stale discard marks
+    void housekeeping_locked() {
+        const int64_t now = monotonic_us();
+        if (now - last_expire_us < 100000) return;
+        last_expire_us = now;
+        const int64_t ttl = (int64_t)FLAGS_rccl_stash_ttl_ms * 1000;
+        for (auto it = stash.begin(); it != stash.end();) {
+            if (now - it->second.since_us > ttl) {
+                consume_locked(it->first.first, it->second.len);
+                g_expired.fetch_add(1, std::memory_order_relaxed);
+                it = stash.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        for (auto it = discards.begin(); it != discards.end();) {
+            if (now - it->second > ttl) it = discards.erase(it);
+            else ++it;
+        }
+    }
+
+    // true when a peer process is gone (the plane is then aborted)
+    bool check_liveness() {
+        if (world <= 1) return false;
+        const int64_t now = monotonic_us();
+        if (now - last_liveness_us < 100000) return false;
+        last_liveness_us = now;
+        for (int q = 0; q < world && q < kMaxRanks; ++q) {
+            const int32_t pid = bell->pid[q].load(std::memory_order_acquire);
+            if (q != rank && pid > 0 && kill(pid, 0) != 0 && errno == ESRCH) {
+                set_remote_abort("rank " + std::to_string(q) + " (pid " + std::to_string(pid) + ") exited");
+                return true;
+            }
+        }
+        return false;
+    }
+
+    void set_remote_abort(const std::string& why) {
+        // the first rank to claim writes the reason, then raises the flag
+        uint32_t zero = 0;
+        if (bell->claim.compare_exchange_strong(zero, 1)) {
+            snprintf(bell->reason, sizeof(bell->reason), "%s", why.c_str());
+            bell->abort.store((uint32_t)rank + 1, std::memory_order_release);
+        }
+        bell->seq.fetch_add(1);
+        futex(&bell->seq, FUTEX_WAKE, INT_MAX, nullptr);
+    }
+
+    // Build, issue and complete round k. 0 on success; -1 after an abort.
+    int run_round(uint64_t k) {
+        bool my_busy = false, stalled = false;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            moving_send.assign(world, {});
+            moving_recv.assign(world, {});
+            for (int p = 0; p < world; ++p) {
+                if (p == rank) continue;
+                PeerState& ps = peers[p];
+                Hdr* h = reinterpret_cast<Hdr*>(ops->host_out + (size_t)p * kHdrBytes);
+                h->magic = kHdrMagic;
+                h->round = k;
+                h->credit = ps.consumed + (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
+                h->from = (uint64_t)rank;
+                h->n = 0;
+                moving_send[p].swap(ps.announced);
+                moving_recv[p].swap(ps.incoming);
+                uint64_t round_bytes = 0;
+                const int max_n = std::max(1, std::min(FLAGS_rccl_round_payloads, kMaxEntries));
+                while (!ps.queued.empty() && (int)h->n < max_n) {
+                    const Payload& q = ps.queued.front();
+                    if (h->n > 0 && round_bytes + q.len > (uint64_t)FLAGS_rccl_round_bytes) break;
+                    // within credit, or the peer consumed everything we announced
+                    const uint64_t granted = ps.credit;
+                    const uint64_t window = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
+                    const bool drained = granted >= window && ps.announced_bytes <= granted - window;
+                    if (ps.announced_bytes + q.len > granted && !drained) {
+                        stalled = true;
+                        break;
+                    }
+                    h->e[h->n].seq = q.seq;
+                    h->e[h->n].len = q.len;
+                    ++h->n;
+                    round_bytes += q.len;
+                    ps.announced_bytes += q.len;
+                    ps.announced.push_back(std::move(ps.queued.front()));
+                    ps.queued.pop_front();
+                }
+                my_busy |= !ps.announced.empty() || !ps.queued.empty();
+            }
+            self_send.clear();
+            self_recv.clear();
+            for (size_t i = 0; i < 256 && !self_q.empty(); ++i) {
+                Payload s = std::move(self_q.front());
+                self_q.pop_front();
+                Payload r;
+                r.seq = s.seq;
+                r.len = s.len;
+                r.ptr = ops->alloc(s.len, &r.hold);
+                if (!r.ptr) {
+                    self_q.push_front(std::move(s));
+                    break;
+                }
+                self_send.push_back(std::move(s));
+                self_recv.push_back(std::move(r));
+            }
+            my_busy |= !self_q.empty();
+            for (int p = 0; p < world; ++p) {
+                if (p == rank) continue;
+                reinterpret_cast<Hdr*>(ops->host_out + (size_t)p * kHdrBytes)->flags = my_busy ? kBusy : 0;
+            }
+        }
+        if (stalled) g_credit_stalls.fetch_add(1, std::memory_order_relaxed);
+        bool payloads = !self_send.empty();
+        for (int p = 0; p < world; ++p) payloads |= !moving_send[p].empty() || !moving_recv[p].empty();
+
+        // issue: headers up, one group, headers down, one marker
+        void* st = ops->stream();
+        const size_t hdr_total = (size_t)world * kHdrBytes;
+        int rc = world > 1 ? ops->upload(hdr_total) : 0;
+        ncclResult_t r = ncclSuccess;
+        if (rc == 0) {
+            r = api.group_start();
+            for (int p = 0; p < world && r == ncclSuccess; ++p) {
+                if (p == rank) continue;
+                r = api.send(ops->dev_out + (size_t)p * kHdrBytes, kHdrBytes, ncclUint8, p, comm, (hipStream_t)st);
+                if (r == ncclSuccess)
+                    r = api.recv(ops->dev_in + (size_t)p * kHdrBytes, kHdrBytes, ncclUint8, p, comm, (hipStream_t)st);
+                for (size_t i = 0; i < moving_send[p].size() && r == ncclSuccess; ++i)
+                    r = api.send(moving_send[p][i].ptr, moving_send[p][i].len, ncclUint8, p, comm, (hipStream_t)st);
+                for (size_t i = 0; i < moving_recv[p].size() && r == ncclSuccess; ++i)
+                    r = api.recv(moving_recv[p][i].ptr, moving_recv[p][i].len, ncclUint8, p, comm, (hipStream_t)st);
+            }
+            for (size_t i = 0; i < self_send.size() && r == ncclSuccess; ++i) {
+                r = api.send(self_send[i].ptr, self_send[i].len, ncclUint8, rank, comm, (hipStream_t)st);
+                if (r == ncclSuccess)
+                    r = api.recv(self_recv[i].ptr, self_recv[i].len, ncclUint8, rank, comm, (hipStream_t)st);
+            }
+            const ncclResult_t e = api.group_end();
+            if (r == ncclSuccess) r = e;
+            if (r == ncclSuccess && world > 1) rc = ops->download(hdr_total);
+            if (r == ncclSuccess && rc == 0) rc = ops->record(&marker);
+            marker_live = r == ncclSuccess && rc == 0;
+        }
+        g_rounds.fetch_add(1, std::memory_order_relaxed);
+        if (payloads) g_payload_rounds.fetch_add(1, std::memory_order_relaxed);
+        if (r != ncclSuccess || rc != 0) {
+            abort(r != ncclSuccess ? std::string("round issue: ") + api.error_string(r) : "round issue: stream op failed",
+                  true);
+            return -1;
+        }
+        // wait: the poster polls (briefly spinning, then napping) and keeps
+        // an eye on the doorbell, the peers and the watchdog
+        const int64_t t0 = monotonic_us();
+        int spins = 0;
+        for (;;) {
+            const int q = ops->query(marker);
+            if (q == 1) break;
+            if (q < 0) {
+                abort("round " + std::to_string(k) + " failed on the stream", true);
+                return -1;
+            }
+            if (bell->abort.load(std::memory_order_acquire)) {
+                abort(remote_reason(), false);
+                return -1;
+            }
+            ncclResult_t ae = ncclSuccess;
+            api.async_error(comm, &ae);
+            if (ae != ncclSuccess && ae != ncclInProgress) {
+                abort(std::string("rccl: ") + api.error_string(ae), true);
+                return -1;
+            }
+            const int64_t now = monotonic_us();
+            if (now - t0 > (int64_t)FLAGS_rccl_timeout_ms * 1000) {
+                abort("round " + std::to_string(k) + " made no progress within -rccl_timeout_ms", true);
+                return -1;
+            }
+            if (check_liveness()) {
+                abort(std::string(bell->reason), false);
+                return -1;
+            }
+            if (++spins < 200) std::this_thread::yield();
+            else usleep(20);
+        }
+        ops->release(marker);
+        marker_live = false;
+        return complete_round(k, my_busy);
+    }
+
+    int complete_round(uint64_t k, bool my_busy) {
+        std::vector<Buf> drop;  // released outside the lock
+        std::lock_guard<std::mutex> g(mu);
+        for (int p = 0; p < world; ++p) {
+            for (Payload& s : moving_send[p]) {
+                g_sent.fetch_add(1, std::memory_order_relaxed);
+                g_sent_bytes.fetch_add((int64_t)s.len, std::memory_order_relaxed);
+                drop.push_back(std::move(s.hold));
+            }
+            for (Payload& r : moving_recv[p]) deliver_locked(p, &r);
+        }
+        for (Payload& s : self_send) {
+            g_sent.fetch_add(1, std::memory_order_relaxed);
+            g_sent_bytes.fetch_add((int64_t)s.len, std::memory_order_relaxed);
+            drop.push_back(std::move(s.hold));
+        }
+        for (Payload& r : self_recv) deliver_locked(rank, &r);
+        moving_send.assign(world, {});
+        moving_recv.assign(world, {});
+        self_send.clear();
+        self_recv.clear();
+        bool busy = my_busy;
+        for (int p = 0; p < world; ++p) {
+            if (p == rank) continue;
+            const Hdr* h = reinterpret_cast<const Hdr*>(ops->host_in + (size_t)p * kHdrBytes);
+            if (h->magic != kHdrMagic || h->round != k || h->from != (uint64_t)p || h->n > (uint32_t)kMaxEntries) {
+                mu.unlock();
+                abort("round " + std::to_string(k) + ": bad header from rank " + std::to_string(p), true);
+                mu.lock();
+                return -1;
+            }
+            PeerState& ps = peers[p];
+            ps.credit = std::max(ps.credit, h->credit);
+            busy |= (h->flags & kBusy) != 0;
+            for (uint32_t i = 0; i < h->n; ++i) {
+                Payload in;
+                in.seq = h->e[i].seq;
+                in.len = (size_t)h->e[i].len;
+                in.ptr = in.len ? ops->alloc(in.len, &in.hold) : nullptr;
+                if (!in.ptr) {
+                    mu.unlock();
+                    abort("no memory to land a " + std::to_string(in.len) + " B payload from rank " +
+                              std::to_string(p),
+                          true);
+                    mu.lock();
+                    return -1;
+                }
+                ps.incoming.push_back(std::move(in));
+            }
+        }
+        busy_next = busy;
+        completed_round = k;
+        housekeeping_locked();
+        return 0;
+    }
+
+    // (mu held) a payload from `src` landed
+    void deliver_locked(int src, Payload* r) {
+        g_recv.fetch_add(1, std::memory_order_relaxed);
+        g_recv_bytes.fetch_add((int64_t)r->len, std::memory_order_relaxed);
+        const Key k(src, r->seq);
+        auto w = waiting.find(k);
+        if (w != waiting.end()) {
+            *w->second.out = std::move(r->hold);
+            consume_locked(src, r->len);
+            Waiter* wt = w->second.w;
+            waiting.erase(w);
+            finish_locked(wt, true);
+            return;
+        }
+        auto d = discards.find(k);
+        if (d != discards.end()) {
+            discards.erase(d);
+            consume_locked(src, r->len);
+            g_discarded.fetch_add(1, std::memory_order_relaxed);
+            r->hold.clear();
+            return;
+        }
+        Stashed& s = stash[k];
+        s.buf = std::move(r->hold);
+        s.len = r->len;
+        s.since_us = monotonic_us();
+    }
+
+    // Poster only. Tell the other ranks (propagate), abort the communicator,
+    // wait (bounded) for the stream so no kernel still reads or writes our
+    // blocks, then fail everything that waits on the plane.
+    void abort(const std::string& why, bool propagate, bool is_error = true) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (dead) return;
+            dead = true;
+            dead_flag.store(true, std::memory_order_release);
+        }
+        if (is_error) {
+            LOG(ERROR) << "rccl plane aborted on rank " << rank << ": " << why
+                       << " (payloads fall back to xGMI lending)";
+            g_aborts.fetch_add(1, std::memory_order_relaxed);
+        } else {
+            LOG(INFO) << "rccl plane closed on rank " << rank << ": " << why;
+        }
+        if (propagate && world > 1) set_remote_abort(why);
+        if (comm) api.comm_abort(comm);
+        bool drained = true;
+        if (marker_live) {
+            drained = false;
+            const int64_t t0 = monotonic_us();
+            while (monotonic_us() - t0 < 2000000) {
+                const int q = ops->query(marker);
+                if (q != 0) {
+                    drained = true;
+                    break;
+                }
+                usleep(100);
+            }
+            if (drained) ops->release(marker);
+            marker_live = false;
+        }
+        std::vector<Buf> bufs;
+        std::lock_guard<std::mutex> g(mu);
+        auto take = [&](std::vector<Payload>& v) {
+            for (Payload& p : v) bufs.push_back(std::move(p.hold));
+            v.clear();
+        };
+        for (auto& v : moving_send) take(v);
+        for (auto& v : moving_recv) take(v);
+        take(self_send);
+        take(self_recv);
+        if (!drained) {
+            LOG(ERROR) << "rccl plane: stream did not drain after the abort; " << bufs.size()
+                       << " in-flight blocks are leaked, not recycled";
+            for (Buf& b : bufs) graveyard.push_back(std::move(b));
+            bufs.clear();
+        }
+        for (PeerState& ps : peers) {
+            for (Payload& p : ps.queued) bufs.push_back(std::move(p.hold));
+            ps.queued.clear();
+            take(ps.announced);
+            take(ps.incoming);
+        }
+        for (Payload& p : self_q) bufs.push_back(std::move(p.hold));
+        self_q.clear();
+        stash.clear();
+        discards.clear();
+        for (auto& kv : waiting) finish_locked(kv.second.w, false);
+        waiting.clear();
+        if (!bell_name.empty()) shm_unlink(bell_name.c_str());
     }
 };
 
@@ -378,10 +893,20 @@ std::mutex g_mu;
 Plane* g_plane = nullptr;
 std::atomic<bool> g_active{false};
 
-uint64_t fnv1a(const std::string& s) {
-    uint64_t h = 1469598103934665603ull;
-    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
-    return h | 1;  // never 0: 0 means "no plane" in the hello
+Doorbell* open_bell(const std::string& name, bool shared) {
+    if (!shared) return new Doorbell();
+    const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return nullptr;
+    if (ftruncate(fd, (off_t)sizeof(Doorbell)) != 0) {
+        close(fd);
+        return nullptr;
+    }
+    void* m = mmap(nullptr, sizeof(Doorbell), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return nullptr;
+    Doorbell* b = static_cast<Doorbell*>(m);
+    b->magic = kBellMagic;  // every rank writes the same value
+    return b;
 }
 
 }  // namespace
@@ -401,74 +926,74 @@ std::string UniqueId(std::string* error) {
 int Init(int rank, int world, const std::string& unique_id, int device, std::string* error) {
     std::lock_guard<std::mutex> g(g_mu);
     if (g_plane) {
-        if (g_plane->id == fnv1a(unique_id) && g_plane->rank == rank) return 0;
-        if (error) *error = "another RCCL plane is active";
+        if (g_plane->id == fnv1a(unique_id) && g_plane->rank == rank && !g_plane->dead_flag.load()) return 0;
+        if (error) *error = "another RCCL plane was set up in this process";
         return -1;
     }
-    if (world <= 0 || rank < 0 || rank >= world || unique_id.size() != sizeof(ncclUniqueId)) {
+    if (world <= 0 || world > kMaxRanks || rank < 0 || rank >= world || unique_id.size() != sizeof(ncclUniqueId)) {
         if (error) *error = "bad rank/world/unique id";
         return -1;
     }
-    if (device < 0) device = CurrentDevice();
-    if (gpu::Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
     std::unique_ptr<Plane> p(new Plane);
     if (!load_api(&p->api, error)) return -1;
+    if (p->api.fake()) {
+        p->ops.reset(new StubOps(p->api));
+    } else {
+        if (device < 0) device = CurrentDevice();
+        if (gpu::Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
+        p->ops.reset(new HipOps);
+    }
     p->device = device;
     p->rank = rank;
     p->world = world;
     p->id = fnv1a(unique_id);
     int prev = 0;
-    hipGetDevice(&prev);
-    hipSetDevice(device);
+    if (!p->api.fake()) hipGetDevice(&prev);
+    if (p->ops->init(device, (size_t)world * kHdrBytes, error) != 0) {
+        if (!p->api.fake()) hipSetDevice(prev);
+        return -1;
+    }
+    char nb[64];
+    snprintf(nb, sizeof(nb), "/mrpc_rccl_bell_%016llx", (unsigned long long)p->id);
+    if (world > 1) p->bell_name = nb;
+    p->bell = open_bell(nb, world > 1);
+    if (!p->bell) {
+        if (error) *error = "doorbell shm unavailable";
+        return -1;
+    }
+    p->bell->pid[rank].store(getpid(), std::memory_order_release);
+    if (!p->api.fake()) hipSetDevice(device);
     ncclUniqueId id;
     memcpy(id.internal, unique_id.data(), sizeof(id.internal));
     ncclResult_t r = p->api.comm_init_rank(&p->comm, world, id, rank);
     if (r != ncclSuccess) {
-        hipSetDevice(prev);
+        if (!p->api.fake()) hipSetDevice(prev);
         if (error) *error = std::string("ncclCommInitRank: ") + p->api.error_string(r);
         return -1;
     }
-    if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
-        p->api.comm_abort(p->comm);
-        hipSetDevice(prev);
-        if (error) *error = "hipStreamCreate failed";
+    p->peers.assign(world, PeerState());
+    for (PeerState& ps : p->peers) ps.credit = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
+    // round 1, collectively and synchronously: connects every pair (RCCL
+    // connects p2p peers lazily inside the first group that uses them)
+    const int rc = world > 1 ? p->run_round(1) : 0;
+    if (!p->api.fake()) hipSetDevice(prev);
+    if (rc != 0) {
+        if (error) *error = "rccl plane: the first round failed";
+        if (!p->bell_name.empty()) shm_unlink(p->bell_name.c_str());
+        p.release();  // its comm is aborted; the stream may still reference it
         return -1;
     }
-    // Connect every pair now (RCCL connects p2p peers lazily inside
-    // ncclGroupEnd, which would block the poster on a peer that has not yet
-    // posted anything to us): one byte to and from every rank, collectively.
-    void* warm = nullptr;
-    if (hipMalloc(&warm, 2 * (size_t)world) != hipSuccess) warm = nullptr;
-    r = warm ? p->api.group_start() : ncclInternalError;
-    for (int q = 0; q < world && r == ncclSuccess; ++q) {
-        r = p->api.send(static_cast<char*>(warm) + q, 1, ncclUint8, q, p->comm, p->stream);
-        if (r == ncclSuccess) r = p->api.recv(static_cast<char*>(warm) + world + q, 1, ncclUint8, q, p->comm, p->stream);
-    }
-    if (warm) {
-        const ncclResult_t e = p->api.group_end();
-        if (r == ncclSuccess) r = e;
-    }
-    const bool synced = warm && r == ncclSuccess && hipStreamSynchronize(p->stream) == hipSuccess;
-    if (warm) hipFree(warm);
-    hipSetDevice(prev);
-    if (!synced) {
-        p->api.comm_abort(p->comm);
-        hipStreamDestroy(p->stream);
-        if (error) *error = std::string("rccl warm-up exchange failed: ") + p->api.error_string(r);
-        return -1;
-    }
-    p->next_send.assign(world, 0);
-    p->next_recv.assign(world, 0);
-    p->held.assign(world, {});
     Plane* raw = p.release();
     raw->poster = std::thread([raw] { raw->run(); });
     g_plane = raw;
     g_active.store(true, std::memory_order_release);
     static var::PassiveStatus<int64_t> v1("rccl_sent_bytes", [] { return g_sent_bytes.load(); });
     static var::PassiveStatus<int64_t> v2("rccl_recv_bytes", [] { return g_recv_bytes.load(); });
-    static var::PassiveStatus<int64_t> v3("rccl_groups", [] { return g_groups.load(); });
+    static var::PassiveStatus<int64_t> v3("rccl_rounds", [] { return g_rounds.load(); });
     static var::PassiveStatus<int64_t> v4("rccl_aborts", [] { return g_aborts.load(); });
-    LOG(INFO) << "rccl plane up: rank " << rank << "/" << world << " on device " << device;
+    static var::PassiveStatus<int64_t> v5("rccl_credit_stalls", [] { return g_credit_stalls.load(); });
+    LOG(INFO) << "rccl plane up: rank " << rank << "/" << world
+              << (raw->api.fake() ? " on the stub library (host memory)" : " on device " + std::to_string(device));
     return 0;
 }
 
@@ -478,6 +1003,8 @@ bool Active() {
 int Rank() { return g_active.load(std::memory_order_acquire) ? g_plane->rank : -1; }
 int World() { return g_active.load(std::memory_order_acquire) ? g_plane->world : 0; }
 uint64_t PlaneId() { return g_active.load(std::memory_order_acquire) ? g_plane->id : 0; }
+bool HostMemory() { return g_active.load(std::memory_order_acquire) && g_plane->ops->host_memory(); }
+bool AcceptsBlock(const BufBlock* b) { return Active() && g_plane->ops->accepts(b); }
 
 void Shutdown() {
     std::lock_guard<std::mutex> g(g_mu);
@@ -485,83 +1012,52 @@ void Shutdown() {
     {
         std::lock_guard<std::mutex> lk(g_plane->mu);
         g_plane->stop = true;
-        g_plane->cv.notify_one();
     }
+    g_plane->bell->seq.fetch_add(1);
+    futex(&g_plane->bell->seq, FUTEX_WAKE, INT_MAX, nullptr);
     if (g_plane->poster.joinable()) g_plane->poster.join();
     // the plane object stays (Active() is false from now on): late callers
     // may still hold a pointer to it
 }
 
+bool FillHello(policy::PlaneHello* h) {
+    if (!Active()) return false;
+    h->set_rank(g_plane->rank);
+    h->set_plane(g_plane->id);
+    h->set_pid(getpid());
+    return true;
+}
+
+int PeerRank(const policy::PlaneHello& h) {
+    if (!Active() || h.plane() != g_plane->id || h.rank() < 0 || h.rank() >= g_plane->world) return -1;
+    return h.rank();
+}
+
 int64_t Send(int peer, const void* p, size_t len, Buf&& hold) {
-    if (!g_active.load(std::memory_order_acquire) || len == 0) return -1;
+    if (!Active() || len == 0) return -1;
     return g_plane->send(peer, p, len, std::move(hold));
 }
 
 int Recv(int n, const int* src, const uint64_t* seq, const size_t* len, Buf* outs) {
     if (n <= 0) return 0;
     if (!g_active.load(std::memory_order_acquire)) return -1;
-    Plane* pl = g_plane;
-    Waiter w;
-    w.butex = fiber::butex_create();
-    w.butex->store(0, std::memory_order_relaxed);
-    w.left.store(n, std::memory_order_relaxed);
-    std::vector<Op> ops(n);
-    bool ok = true;
-    for (int i = 0; i < n; ++i) {
-        ops[i].peer = src[i];
-        ops[i].seq = seq[i];
-        ops[i].len = len[i];
-        ops[i].waiter = &w;
-        if (src[i] < 0 || src[i] >= pl->world || len[i] == 0) ok = false;
-        else if (!(ops[i].ptr = AppendNewDeviceBlock(&outs[i], len[i], pl->device))) ok = false;
-    }
-    if (!ok) {
-        // on a bad descriptor the good ones still drain the peer's sends
-        for (Op& op : ops) {
-            if (op.peer >= 0 && op.peer < pl->world && op.len > 0) Discard(op.peer, op.seq, op.len);
-        }
-        for (int i = 0; i < n; ++i) outs[i].clear();
-        fiber::butex_destroy(w.butex);
-        return -1;
-    }
-    if (!pl->add_recvs(&ops)) {  // plane dead: nothing was queued
-        for (int i = 0; i < n; ++i) outs[i].clear();
-        fiber::butex_destroy(w.butex);
-        return -1;
-    }
-    while (w.butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(w.butex, 0);
-    const int rc = w.butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
-    fiber::butex_destroy(w.butex);
-    if (rc != 0)
-        for (int i = 0; i < n; ++i) outs[i].clear();
-    return rc;
+    return g_plane->recv(n, src, seq, len, outs);
 }
 
 void Discard(int src, uint64_t seq, size_t len) {
     if (!g_active.load(std::memory_order_acquire)) return;
-    Plane* pl = g_plane;
-    if (src < 0 || src >= pl->world || len == 0) return;
-    std::vector<Op> ops(1);
-    ops[0].peer = src;
-    ops[0].seq = seq;
-    ops[0].len = len;
-    ops[0].ptr = AppendNewDeviceBlock(&ops[0].hold, len, pl->device);
-    if (!ops[0].ptr) {
-        LOG(ERROR) << "rccl: no HBM to drain payload " << seq << " from rank " << src;
-        return;  // the watchdog will abort the stalled pair
-    }
-    pl->add_recvs(&ops);
+    g_plane->discard(src, seq, len);
 }
 
 void Cancelled(int peer, uint64_t seq) {
     if (!g_active.load(std::memory_order_acquire)) return;
-    if (peer == g_plane->rank) {
-        g_plane->cancel_self(seq);  // never issued: just skip its number
-        return;
-    }
-    LOG(ERROR) << "rccl: payload " << seq << " to rank " << peer
-               << " was queued but never announced; the pair cannot resynchronise";
-    // the poster's watchdog aborts the plane once the orphaned send stalls
+    g_plane->cancelled(peer, seq);
+}
+
+void AbortForTest(const std::string& why) {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (!g_plane) return;
+    g_plane->set_remote_abort(why);
 }
 
 Stats GetStats() {
@@ -571,9 +1067,16 @@ Stats GetStats() {
     s.recv_payloads = g_recv.load();
     s.recv_bytes = g_recv_bytes.load();
     s.discarded = g_discarded.load();
-    s.groups = g_groups.load();
+    s.rounds = g_rounds.load();
+    s.payload_rounds = g_payload_rounds.load();
     s.aborts = g_aborts.load();
-    s.reorder_waits = g_reorder.load();
+    s.credit_stalls = g_credit_stalls.load();
+    s.stash_expired = g_expired.load();
+    s.recv_timeouts = g_recv_timeouts.load();
+    s.doorbells = g_doorbells.load();
+    s.withdrawn = g_withdrawn.load();
+    s.world = World();
+    s.host_memory = HostMemory();
     return s;
 }
 

@@ -1,32 +1,43 @@
-// RCCL data plane: large HBM payloads of RPCs between ranks of one job move
-// by ncclSend/ncclRecv over xGMI while the RPC meta (a per-pair sequence
-// number and the length) travels on the TCP connection. The xGMI lending
-// transport (gpu/xgmi.h) stays the default for payloads below
-// -rccl_min_bytes; above it, RCCL's pipelined p2p kernels move the bytes
-// (the analog of the reference's RDMA zero-copy SGEs,
-// src/brpc/rdma/rdma_endpoint.cpp:771-895, with RCCL as the fabric).
+// RCCL payload plane: large payloads of RPCs between ranks of one node move
+// by ncclSend/ncclRecv over xGMI while the RPC meta (the payload's per-pair
+// sequence number and length) travels on the TCP connection. The xGMI
+// lending transport (gpu/xgmi.h) stays the default below -rccl_min_bytes.
+// It is the analog of the reference's RDMA data path
+// (src/brpc/rdma/rdma_endpoint.cpp:771-895: zero-copy SGEs, a sliding
+// window, ACK credits in imm_data, window sizes agreed in the handshake at
+// :505-509,613-617), with RCCL as the fabric.
 //
-// One communicator for the whole job, created collectively (every rank calls
-// Init with the unique id rank 0 generated). All RCCL calls of the process
-// are made by ONE poster thread, which issues whatever is ready as one
-// ncclGroupStart/End group on a dedicated stream and completes waiters from
-// the group's event.
+// Why rounds. RCCL send/recv kernels block until their partner runs, every
+// op of one communicator is serialised, and streams beyond
+// GPU_MAX_HW_QUEUES share hardware queues. Issuing sends and receives as
+// RPCs produce them (round 2's plane) lets two ranks each park a send in
+// front of the receive the other one needs: a cross-rank deadlock once the
+// payloads exceed RCCL's p2p buffering. This plane is deadlock-free by
+// construction instead:
+//  * ONE stream per rank, and every rank issues the same numbered rounds;
+//  * round k is ONE ncclGroupStart/End group holding, for every peer, a
+//    fixed-size header send + header recv, the payloads announced in the
+//    headers of round k-1 (both sides know their sizes) and the self
+//    payloads — every op in round k is matched by an op of round k at its
+//    peer, and ops of one group progress together, so round k completes
+//    once every rank issued it;
+//  * a rank issues round k+1 when the round-k headers (seen identically by
+//    every rank) carry a busy bit, or when some rank rang the node's
+//    doorbell (POSIX shm + futex) asking for round k+1 — so every rank
+//    issues every round, by induction.
+// Flow control: the header also carries the receiver's cumulative credit
+// (bytes it consumed from that sender plus -rccl_window_bytes); a sender
+// announces a payload only within credit. Received payloads wait in a
+// stash, keyed by (source, sequence), until the RPC layer claims them
+// (Recv), gives them back (Discard) or -rccl_stash_ttl_ms expires.
+// Failure: any rank that hits an RCCL error, a round older than
+// -rccl_timeout_ms or a dead peer process sets the doorbell's abort flag;
+// every rank then aborts its communicator, waits (bounded) for its stream
+// to drain before recycling payload memory, fails its waiters, and new
+// payloads fall back to xGMI lending.
 //
-// Matching without tags. RCCL pairs a rank's sends to a peer with that
-// peer's receives in issue order, so:
-//  * the sender numbers its payloads per destination and queues the send
-//    BEFORE the meta that announces it is written to the socket;
-//  * the receiver issues receives per source strictly in sequence order (a
-//    reorder buffer holds payloads whose metas overtook earlier ones on
-//    other connections), and a payload the receiver will not consume is
-//    still received, into scratch, and dropped.
-// Because every receive is issued after its matching send was queued, the
-// stream-order wait-for graph is acyclic and the plane cannot deadlock.
-// A send whose meta is never written (connection died in between) would
-// stall the pair: a watchdog aborts the communicator after
-// -rccl_timeout_ms without progress, fails every waiter, and traffic falls
-// back to xGMI lending. Self-sends (a one-rank job, client and server in
-// one process) are paired with their receive in the same group.
+// On hosts without GPUs the plane runs on the stub library
+// tests/stub/fake_rccl.cc (-rccl_library), moving host blocks.
 #pragma once
 
 #include <cstddef>
@@ -36,40 +47,64 @@
 #include "base/buf.h"
 
 namespace mrpc {
+namespace policy {
+class PlaneHello;
+}  // namespace policy
 namespace gpu {
 namespace rccl {
 
 // Generate a unique id (rank 0). Empty string when RCCL is unavailable.
 std::string UniqueId(std::string* error = nullptr);
-// Collective: create the communicator of `world` ranks on `device` and
-// connect every pair (one warm-up exchange). 0 on success.
+// Collective over the ranks of one node: create the communicator of
+// `world` ranks on `device` (ignored on the stub library) and run the
+// first round (connects every pair). 0 on success.
 int Init(int rank, int world, const std::string& unique_id, int device, std::string* error = nullptr);
 bool Active();
 int Rank();
 int World();
-// Identity of the job's plane (hash of the unique id), carried in the xGMI
-// hello so only peers of the same communicator use it.
+// Identity of the job's plane (hash of the unique id), carried in the
+// connection hello so only peers of the same plane use it.
 uint64_t PlaneId();
-// Abort the communicator (idempotent); pending waiters fail.
+// The plane moves host blocks (stub library) rather than HBM blocks.
+bool HostMemory();
+// Whether a payload block of this kind/device can go over the plane.
+bool AcceptsBlock(const BufBlock* b);
+// Leave the plane (not collective: the other ranks fall back to lending).
 void Shutdown();
 
-// Queue a send of [p, p+len) (HBM of the plane's device) to `peer`. `hold`
-// keeps the bytes alive until RCCL is done with them. Returns the payload's
-// sequence number for that destination, or -1.
+// Connection hello (RpcMeta.plane_hello): this rank's identity, and the
+// peer's plane rank from its hello (-1: not a rank of our plane).
+bool FillHello(policy::PlaneHello* h);
+int PeerRank(const policy::PlaneHello& h);
+
+// Queue [p, p+len) for `peer`; `hold` keeps the bytes alive until RCCL is
+// done with them. Returns the payload's sequence number for that
+// destination (announced in the meta), or -1 when the plane is down.
 int64_t Send(int peer, const void* p, size_t len, Buf&& hold);
-// Receive payloads (src[i], seq[i], len[i]) into fresh HBM blocks outs[i];
-// parks the calling fiber until all arrived. 0 on success.
+// Claim payloads (src[i], seq[i], len[i]) into outs[i]; parks the calling
+// fiber until all arrived (at most -rccl_timeout_ms). 0 on success.
 int Recv(int n, const int* src, const uint64_t* seq, const size_t* len, Buf* outs);
-// Payload the receiver will not consume: receive it into scratch and drop it.
+// Payload the receiver will not consume: drop it (now or on arrival).
 void Discard(int src, uint64_t seq, size_t len);
-// The sender queued payload `seq` for `peer` but will never announce it:
-// the pair cannot be resynchronised, so the plane is aborted.
+// The sender queued payload `seq` for `peer` but will never announce it in
+// a meta: withdrawn if not yet announced in a round header, otherwise the
+// receiver's stash expires it.
 void Cancelled(int peer, uint64_t seq);
+
+// Fault injection: raise the node's abort flag as if this rank had failed
+// (every rank's poster aborts its plane).
+void AbortForTest(const std::string& why);
 
 struct Stats {
     int64_t sent_payloads = 0, sent_bytes = 0, recv_payloads = 0, recv_bytes = 0;
-    int64_t discarded = 0, groups = 0, aborts = 0;
-    int64_t reorder_waits = 0;  // receives held back for an earlier sequence
+    int64_t discarded = 0, rounds = 0, payload_rounds = 0, aborts = 0;
+    int64_t credit_stalls = 0;   // rounds where a queued payload waited for credit
+    int64_t stash_expired = 0;   // received payloads nobody claimed in time
+    int64_t recv_timeouts = 0;   // Recv calls that gave up
+    int64_t doorbells = 0;       // idle -> busy transitions this rank rang
+    int64_t withdrawn = 0;       // Cancelled before announcement
+    int world = 0;
+    bool host_memory = false;
 };
 Stats GetStats();
 

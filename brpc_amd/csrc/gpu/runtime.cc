@@ -6,6 +6,7 @@
 #include <time.h>
 
 #include <atomic>
+#include <cctype>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -234,6 +235,14 @@ std::string DeviceArch(int device) {
     std::string a = p.gcnArchName;
     const size_t colon = a.find(':');
     return colon == std::string::npos ? a : a.substr(0, colon);
+}
+
+std::string PciBusId(int device) {
+    char id[64] = {0};
+    if (check_device(device) < 0 || hipDeviceGetPCIBusId(id, sizeof(id) - 1, device) != hipSuccess) return "";
+    std::string s = id;
+    for (char& c : s) c = (char)tolower((unsigned char)c);
+    return s;
 }
 
 hipStream_t PoolStream(int device) {

@@ -23,16 +23,12 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
-#include "gpu/rccl_plane.h"
 #include "mrpc/proto/rpc_meta.pb.h"
 #include "net/socket.h"
 #include "policy/device_payload.h"
 #include "var/var.h"
 
 DEFINE_int32(xgmi_slots, 65536, "release-table slots per process (max payload blocks lent at once)");
-DEFINE_int64(rccl_min_bytes, int64_t(1) << 40,
-             "device payload blocks of at least this many bytes to a peer of the job's RCCL plane move by "
-             "ncclSend/ncclRecv instead of xGMI lending (reloadable; default: never)");
 DEFINE_int32(xgmi_dead_peer_reap_ms, 2000,
              "lent blocks whose connection failed are reclaimed after this long (the peer may still be pulling)");
 
@@ -65,7 +61,8 @@ std::string boot_id() {
 }
 
 std::atomic<int64_t> g_sent_bytes{0}, g_recv_bytes{0}, g_sent_payloads{0}, g_recv_payloads{0}, g_busy{0},
-    g_crc_fail{0}, g_copied_in{0}, g_released_unconsumed{0};
+    g_crc_fail{0}, g_copied_in{0}, g_released_unconsumed{0}, g_cross_bytes{0}, g_cross_payloads{0},
+    g_peer_fail{0}, g_peer_access{0}, g_attach_fail{0}, g_peer_maps{0};
 
 // ------------------------------------------------------------------ lending
 // The process-wide table of blocks lent to peers. A slot holds a Buf that
@@ -229,6 +226,7 @@ struct PeerMap {
     uint32_t nslots = 0;  // slots covered by the mapping (from the hello)
     size_t table_bytes = 0;
     bool local = false;
+    int device = -1;  // the peer's GPU (== ours: HBM-local pulls; else xGMI)
 };
 
 // Peer arenas are mapped once per (pid, device) and shared by sockets.
@@ -241,6 +239,7 @@ std::shared_ptr<PeerMap> map_peer(const policy::XgmiHello& h, std::string* err) 
     auto it = g_peers.find(key);
     if (it != g_peers.end()) return it->second;
     auto pm = std::make_shared<PeerMap>();
+    pm->device = h.device();
     if (h.pid() == getpid()) {
         const ArenaDesc a = GetArena(g_device);
         if (!g_lender || h.device() != g_device || !a.base) {
@@ -269,7 +268,13 @@ std::shared_ptr<PeerMap> map_peer(const policy::XgmiHello& h, std::string* err) 
             int can = 0;
             if (hipDeviceCanAccessPeer(&can, g_device, h.device()) == hipSuccess && can) {
                 const hipError_t pe = hipDeviceEnablePeerAccess(h.device(), 0);
+                if (pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled) {
+                    g_peer_access.fetch_add(1, std::memory_order_relaxed);
+                }
                 if (pe != hipSuccess) (void)hipGetLastError();  // already enabled is fine
+            } else {
+                LOG(WARNING) << "xgmi: device " << g_device << " cannot access peer device " << h.device()
+                             << "; the pull goes through the IPC mapping alone";
             }
         }
         const hipError_t r = hipIpcOpenMemHandle(&p, handle, hipIpcMemLazyEnablePeerAccess);
@@ -308,37 +313,21 @@ std::shared_ptr<PeerMap> map_peer(const policy::XgmiHello& h, std::string* err) 
         pm->table_bytes = bytes;
     }
     g_peers[key] = pm;
+    g_peer_maps.fetch_add(1, std::memory_order_relaxed);
     return pm;
 }
 
 class XgmiEndpoint : public Transport {
 public:
-    XgmiEndpoint(std::shared_ptr<PeerMap> p, int rr) : peer(std::move(p)), rccl_rank(rr) {}
+    explicit XgmiEndpoint(std::shared_ptr<PeerMap> p) : peer(std::move(p)) {}
     const char* name() const override { return "xgmi"; }
     std::shared_ptr<PeerMap> peer;
-    const int rccl_rank;  // the peer's rank in our RCCL plane, -1 if none
 };
 
-PeerMap* peer_of(Socket* sock, std::shared_ptr<Transport>* keep, int* rccl_rank = nullptr) {
+PeerMap* peer_of(Socket* sock, std::shared_ptr<Transport>* keep) {
     *keep = sock ? sock->transport() : nullptr;
     XgmiEndpoint* ep = dynamic_cast<XgmiEndpoint*>(keep->get());
-    if (rccl_rank) *rccl_rank = ep ? ep->rccl_rank : -1;
     return ep ? ep->peer.get() : nullptr;
-}
-
-// Large payloads to a rank of the job's RCCL plane: queue the send now (it
-// must precede the meta on the wire, gpu/rccl_plane.h) and describe it.
-int rccl_send(int peer, BufBlock* block, uint32_t offset, uint32_t len, policy::DevicePayload* d) {
-    Buf hold;
-    hold.append_block(block, offset, len);
-    const int64_t seq = rccl::Send(peer, block->data + offset, len, std::move(hold));
-    if (seq < 0) return 1;  // plane gone: lend instead
-    d->set_length((int64_t)len);
-    d->set_src_device(g_device);
-    d->set_rccl_seq((uint64_t)seq);
-    d->set_rccl_src(rccl::Rank());
-    d->set_rccl_dst(peer);
-    return 0;
 }
 
 // ------------------------------------------------------------------ hooks
@@ -346,12 +335,6 @@ int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, bool
     Lender* l = g_lender;
     if (!l) return -1;
     if (block->device != g_device) return 1;  // another GPU's block: stage it
-    if (!with_crc && (int64_t)len >= FLAGS_rccl_min_bytes) {
-        std::shared_ptr<Transport> keep;
-        int rr = -1;
-        peer_of(sock, &keep, &rr);
-        if (rr >= 0 && rccl::Active() && rccl_send(rr, block, offset, len, d) == 0) return 0;
-    }
     const char* src = block->data + offset;
     int64_t aoff = ArenaOffset(src, g_device);
     Buf hold;
@@ -399,44 +382,18 @@ void release_in(PeerMap* pm, const policy::DevicePayload& d) {
     if (pm && d.slot() < pm->nslots) pm->table->released[d.slot()].store(d.seq(), std::memory_order_release);
 }
 
-void rccl_drain(const policy::DevicePayload& d) {
-    rccl::Discard(d.rccl_src(), d.rccl_seq(), (size_t)std::max<int64_t>(0, d.length()));
-}
-
 int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Buf* outs) {
     std::shared_ptr<Transport> keep;
-    int rr = -1;
-    PeerMap* pm = peer_of(sock, &keep, &rr);
-    // payloads that came over the RCCL plane: received after the lent ones
-    std::vector<int> rsrc;
-    std::vector<uint64_t> rseq;
-    std::vector<size_t> rlen;
-    std::vector<int> ridx;
-    for (int i = 0; i < n; ++i) {
-        if (!descs[i]->has_rccl_seq()) continue;
-        ridx.push_back(i);
-        rsrc.push_back(descs[i]->rccl_src());
-        rseq.push_back(descs[i]->rccl_seq());
-        rlen.push_back((size_t)std::max<int64_t>(0, descs[i]->length()));
-    }
-    auto drain_rccl = [&] {
-        for (int i : ridx) rccl_drain(*descs[i]);
-    };
+    PeerMap* pm = peer_of(sock, &keep);
     if (!pm) {
-        drain_rccl();
+        for (int i = 0; i < n; ++i) outs[i].clear();
         return -1;
-    }
-    bool bad_rccl = false;
-    for (int i : ridx) {
-        const policy::DevicePayload& d = *descs[i];
-        bad_rccl |= d.rccl_src() != rr || d.rccl_dst() != rccl::Rank() || d.length() <= 0;
     }
     std::vector<Segment> segs;
     segs.reserve(n);
-    int rc = bad_rccl ? -1 : 0;
+    int rc = 0;
     for (int i = 0; i < n && rc == 0; ++i) {
         const policy::DevicePayload& d = *descs[i];
-        if (d.has_rccl_seq()) continue;
         const int64_t off = d.ring_offset(), len = d.length();
         if (off < 0 || len < 0 || (uint64_t)off > pm->size || (uint64_t)len > pm->size - (uint64_t)off ||
             d.slot() >= pm->nslots) {
@@ -459,27 +416,16 @@ int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Bu
     if (rc == 0 && !segs.empty())
         rc = BatchedCopy(segs.data(), (int)segs.size(), g_device, want_crc ? crcs.data() : nullptr);
     // the bytes are ours now (or never will be): give every region back
-    for (int i = 0; i < n; ++i)
-        if (!descs[i]->has_rccl_seq()) release_in(pm, *descs[i]);
-    if (rc != 0) {
-        drain_rccl();
-    } else if (!ridx.empty()) {
-        std::vector<Buf> rb(ridx.size());
-        rc = rccl::Recv((int)ridx.size(), rsrc.data(), rseq.data(), rlen.data(), rb.data());
-        for (size_t k = 0; k < ridx.size() && rc == 0; ++k) outs[ridx[k]] = std::move(rb[k]);
-    }
+    for (int i = 0; i < n; ++i) release_in(pm, *descs[i]);
     if (rc != 0) {
         for (int i = 0; i < n; ++i) outs[i].clear();
+        if (pm->device != g_device) g_peer_fail.fetch_add(1, std::memory_order_relaxed);
         return -1;
     }
     size_t si = 0;
     for (int i = 0; i < n; ++i) {
         const policy::DevicePayload& d = *descs[i];
         if (d.length() == 0) continue;
-        if (d.has_rccl_seq()) {
-            g_recv_bytes.fetch_add(d.length(), std::memory_order_relaxed);
-            continue;
-        }
         if (d.has_crc() && crcs[si] != d.crc32c()) {
             g_crc_fail.fetch_add(1, std::memory_order_relaxed);
             for (int k = 0; k < n; ++k) outs[k].clear();
@@ -487,17 +433,14 @@ int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Bu
         }
         ++si;
         g_recv_bytes.fetch_add(d.length(), std::memory_order_relaxed);
+        if (pm->device != g_device) g_cross_bytes.fetch_add(d.length(), std::memory_order_relaxed);
     }
     g_recv_payloads.fetch_add(n, std::memory_order_relaxed);
+    if (pm->device != g_device) g_cross_payloads.fetch_add(n, std::memory_order_relaxed);
     return 0;
 }
 
 void xgmi_release(Socket* sock, const policy::DevicePayload& d) {
-    if (d.has_rccl_seq()) {  // the sender's RCCL send still has to be matched
-        rccl_drain(d);
-        g_released_unconsumed.fetch_add(1, std::memory_order_relaxed);
-        return;
-    }
     std::shared_ptr<Transport> keep;
     PeerMap* pm = peer_of(sock, &keep);
     if (!pm) return;
@@ -506,10 +449,6 @@ void xgmi_release(Socket* sock, const policy::DevicePayload& d) {
 }
 
 void xgmi_cancel(const policy::DevicePayload& d) {
-    if (d.has_rccl_seq()) {
-        rccl::Cancelled(d.rccl_dst(), d.rccl_seq());
-        return;
-    }
     if (g_lender) g_lender->cancel(d.slot(), d.seq());
 }
 
@@ -558,10 +497,6 @@ bool FillXgmiHello(policy::XgmiHello* h) {
     h->set_shm_name(g_lender->shm_name());
     h->set_nslots(g_lender->nslots());
     h->set_host_id(boot_id());
-    if (rccl::Active()) {
-        h->set_rccl_rank(rccl::Rank());
-        h->set_rccl_plane(rccl::PlaneId());
-    }
     return true;
 }
 
@@ -576,10 +511,13 @@ int AttachXgmiPeer(Socket* sock, const policy::XgmiHello& hello, std::string* er
     }
     if (sock->transport()) return 0;
     std::shared_ptr<PeerMap> pm = map_peer(hello, error);
-    if (!pm) return -1;
-    const bool same_plane = hello.has_rccl_rank() && rccl::Active() && hello.rccl_plane() == rccl::PlaneId() &&
-                            hello.rccl_rank() >= 0 && hello.rccl_rank() < rccl::World();
-    sock->set_transport(std::make_shared<XgmiEndpoint>(pm, same_plane ? hello.rccl_rank() : -1));
+    if (!pm) {
+        // counted fallback: the connection stays on TCP, device payloads
+        // are staged through pinned memory
+        g_attach_fail.fetch_add(1, std::memory_order_relaxed);
+        return -1;
+    }
+    sock->set_transport(std::make_shared<XgmiEndpoint>(pm));
     return 0;
 }
 
@@ -598,6 +536,12 @@ XgmiStats GetXgmiStats() {
     s.lent_outstanding = g_lender ? g_lender->outstanding() : 0;
     s.copied_into_arena = g_copied_in.load();
     s.released_unconsumed = g_released_unconsumed.load();
+    s.cross_device_payloads = g_cross_payloads.load();
+    s.cross_device_bytes = g_cross_bytes.load();
+    s.cross_device_pull_failures = g_peer_fail.load();
+    s.peer_access_enabled = g_peer_access.load();
+    s.attach_failures = g_attach_fail.load();
+    s.peer_maps = g_peer_maps.load();
     return s;
 }
 

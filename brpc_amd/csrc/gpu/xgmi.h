@@ -52,6 +52,12 @@ struct XgmiStats {
     int64_t sent_bytes = 0, recv_bytes = 0, sent_payloads = 0, recv_payloads = 0;
     int64_t ring_full_fallbacks = 0, crc_failures = 0;
     int64_t lent_outstanding = 0, copied_into_arena = 0, released_unconsumed = 0;
+    // pulls whose source sat on ANOTHER GPU (true xGMI traffic), as opposed
+    // to HBM-local lends between processes/sockets of one device
+    int64_t cross_device_payloads = 0, cross_device_bytes = 0, cross_device_pull_failures = 0;
+    int64_t peer_access_enabled = 0;  // hipDeviceEnablePeerAccess successes
+    int64_t attach_failures = 0;      // hellos that could not be mapped (fallback: staged over TCP)
+    int64_t peer_maps = 0;            // peer arenas mapped
 };
 XgmiStats GetXgmiStats();
 

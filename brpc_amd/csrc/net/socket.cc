@@ -103,6 +103,7 @@ Socket::Socket()
       _error_code(0),
       _auth_error(0),
       _auth_state(0),
+      _plane_rank(kPlaneUnknown),
       _auth_butex(fiber::butex_create()),
       _main_socket_id(INVALID_SOCKET_ID),
       _recycle_flag(false),
@@ -171,6 +172,7 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
     m->_server_verified.store(false);
     m->_auth_error.store(0);
     m->_auth_state.store(0);
+    m->_plane_rank.store(kPlaneUnknown);
     m->_main_socket_id = INVALID_SOCKET_ID;
     m->_shared = std::make_shared<SharedPart>();
     m->_recycle_flag.store(false);
@@ -1025,6 +1027,7 @@ int Socket::Revive(int new_fd) {
             _pipeline_q.clear();
         }
         _auth_state.store(0);
+        _plane_rank.store(kPlaneUnknown);
         const int old = _fd.exchange(-1);
         if (old >= 0) ::close(old);
         if (_versioned_ref.compare_exchange_strong(vref, make_vref(id_ver, vref_nref(vref)), std::memory_order_release)) {

@@ -202,6 +202,12 @@ public:
     // Per-socket attached objects
     std::shared_ptr<Transport> transport() const;
     void set_transport(std::shared_ptr<Transport> t);
+    // The peer's rank in this process's RCCL payload plane (gpu/rccl_plane.h):
+    // kPlaneUnknown until the hello round trip, -1 when the peer is not a
+    // rank of our plane.
+    static const int kPlaneUnknown = -2;
+    int plane_rank() const { return _plane_rank.load(std::memory_order_acquire); }
+    void set_plane_rank(int r) { _plane_rank.store(r, std::memory_order_release); }
     std::shared_ptr<SocketConnection> conn() const { return _conn; }
     // TLS state (nullptr when the connection is plaintext).
     std::shared_ptr<SslSession> ssl_session() const;
@@ -269,6 +275,7 @@ private:
     std::shared_ptr<Transport> _transport;
     std::atomic<int> _auth_error;
     std::atomic<int> _auth_state;  // 0 none, 1 fighting, 2 done
+    std::atomic<int> _plane_rank;
     std::atomic<int>* _auth_butex;
     // pooled connections: the main socket keeps a free list of sub sockets
     SocketId _main_socket_id;

@@ -11,6 +11,7 @@
 #include "base/time.h"
 #include "base/util.h"
 #include "fiber/call_id.h"
+#include "gpu/rccl_plane.h"
 #include "gpu/xgmi.h"
 #include "mrpc/proto/rpc_meta.pb.h"
 #include "policy/device_payload.h"
@@ -124,6 +125,11 @@ void PackRpcRequest(Buf* packet, uint64_t correlation_id, const pb::MethodDescri
     if (cntl->_use_device_transport && cntl->_pack_socket && !cntl->_pack_socket->transport()) {
         gpu::FillXgmiHello(meta.mutable_xgmi_hello());
     }
+    // RCCL plane hello: offered until a response told us whether the
+    // server is a rank of our plane
+    if (cntl->_pack_socket && cntl->_pack_socket->plane_rank() == Socket::kPlaneUnknown) {
+        gpu::rccl::FillHello(meta.mutable_plane_hello());
+    }
     Buf host_attachment;
     if (!SplitDevicePayload(cntl, /*request=*/true, cntl->request_attachment(), &host_attachment, &meta)) return;
     if (host_attachment.size()) meta.set_attachment_size((int32_t)host_attachment.size());
@@ -173,6 +179,7 @@ static void SendRpcResponse(int64_t correlation_id, Controller* cntl, pb::Messag
     }
     meta.set_correlation_id(correlation_id);
     if (cntl->_reply_xgmi_hello) gpu::FillXgmiHello(meta.mutable_xgmi_hello());
+    if (cntl->_reply_plane_hello) gpu::rccl::FillHello(meta.mutable_plane_hello());
     if (cntl->_response_stream) FillStreamSettings(cntl->_response_stream, meta.mutable_stream_settings());
     Buf packet;
     SerializeRpcHeaderAndMeta(&packet, meta, res_body.size() + host_attachment.size());
@@ -240,6 +247,10 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
         } else {
             LOG_EVERY_SECOND(WARNING) << "xGMI peer " << socket->remote_side() << " not attached: " << err;
         }
+    }
+    if (meta.has_plane_hello()) {
+        socket->set_plane_rank(gpu::rccl::PeerRank(meta.plane_hello()));
+        cntl->_reply_plane_hello = true;
     }
     if (SampledRequest* sample = AskToBeSampled()) {
         sample->meta.set_service_name(rm.service_name());
@@ -376,6 +387,9 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         if (gpu::AttachXgmiPeer(msg->socket(), meta.xgmi_hello(), &err) != 0) {
             LOG_EVERY_SECOND(WARNING) << "xGMI peer " << msg->socket()->remote_side() << " not attached: " << err;
         }
+    }
+    if (msg->socket()->plane_rank() == Socket::kPlaneUnknown) {
+        msg->socket()->set_plane_rank(meta.has_plane_hello() ? gpu::rccl::PeerRank(meta.plane_hello()) : -1);
     }
     int saved_error = 0;
     bool device_payload_taken = false;

@@ -3,11 +3,17 @@
 #include <algorithm>
 #include <vector>
 
+#include "base/flags.h"
 #include "base/logging.h"
+#include "gpu/rccl_plane.h"
 #include "mrpc/proto/rpc_meta.pb.h"
 #include "net/socket.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
+
+DEFINE_int64(rccl_min_bytes, int64_t(1) << 40,
+             "attachment payloads of at least this many bytes to a rank of the job's RCCL plane move by "
+             "ncclSend/ncclRecv (gpu/rccl_plane.h) instead of xGMI lending (reloadable; default: never)");
 
 namespace mrpc {
 
@@ -48,9 +54,65 @@ void StageDeviceBufToHost(const Buf& in, Buf* out) {
 
 namespace policy {
 
+// One descriptor the receiver will not pull: a lent block goes back to the
+// sender's release table, an RCCL payload is dropped from the plane's stash.
+static void ReleaseOne(Socket* sock, const DevicePayload& d) {
+    if (d.has_rccl_seq()) {
+        gpu::rccl::Discard(d.rccl_src(), d.rccl_seq(), (size_t)std::max<int64_t>(0, d.length()));
+        return;
+    }
+    if (g_hooks.release && sock) g_hooks.release(sock, d);
+}
+
+// One descriptor the sender made for a message that is never sent.
+static void CancelOne(const DevicePayload& d) {
+    if (d.has_rccl_seq()) {
+        gpu::rccl::Cancelled(d.rccl_dst(), d.rccl_seq());
+        return;
+    }
+    if (g_hooks.cancel) g_hooks.cancel(d);
+}
+
+namespace {
+
+// Queue one payload on the RCCL plane and describe it. Host-memory planes
+// (the CPU stub) take a run of host blocks, gathered when it spans several.
+bool plane_send(int peer, const Buf& piece, int64_t pos, DevicePayloads* descs) {
+    const size_t len = piece.size();
+    Buf hold;
+    const char* p = nullptr;
+    if (piece.backing_block_num() == 1) {
+        const BlockRef& r = piece.ref_at(0);
+        p = r.block->data + r.offset;
+        hold = piece;
+    } else {
+        char* dst = hold.append_contiguous(len);  // host planes only
+        if (!dst) return false;
+        piece.copy_to(dst, len);
+        p = dst;
+        if (hold.backing_block_num() != 1) return false;
+    }
+    const int64_t seq = gpu::rccl::Send(peer, p, len, std::move(hold));
+    if (seq < 0) return false;
+    DevicePayload* d = descs->Add();
+    d->set_position(pos);
+    d->set_length((int64_t)len);
+    d->set_rccl_seq((uint64_t)seq);
+    d->set_rccl_src(gpu::rccl::Rank());
+    d->set_rccl_dst(peer);
+    return true;
+}
+
+}  // namespace
+
 int LendDeviceBlocks(Socket* sock, const Buf& in, bool verify, Buf* host_out, DevicePayloads* descs,
                      std::string* err) {
-    if (in.all_host_accessible()) {
+    // the RCCL plane takes large payloads to a rank of our plane (never the
+    // verified ones: the integrity check rides on the lending pull)
+    const int prank = (!verify && sock && in.size() >= (size_t)FLAGS_rccl_min_bytes) ? sock->plane_rank() : -1;
+    const bool plane = prank >= 0 && gpu::rccl::Active();
+    const bool host_plane = plane && gpu::rccl::HostMemory();
+    if (in.all_host_accessible() && !host_plane) {
         host_out->append(in);
         return 0;
     }
@@ -59,6 +121,28 @@ int LendDeviceBlocks(Socket* sock, const Buf& in, bool verify, Buf* host_out, De
     size_t pos = 0;
     for (size_t i = 0; i < in.backing_block_num(); ++i) {
         const BlockRef& r = in.ref_at(i);
+        if (host_plane && IsHostAccessible(r.block->kind)) {
+            // the run of host blocks starting here
+            size_t j = i, run = 0;
+            while (j < in.backing_block_num() && IsHostAccessible(in.ref_at(j).block->kind)) run += in.ref_at(j++).length;
+            if (run >= (size_t)FLAGS_rccl_min_bytes) {
+                Buf piece;
+                for (size_t k = i; k < j; ++k) piece.append_block(in.ref_at(k).block, in.ref_at(k).offset, in.ref_at(k).length);
+                if (plane_send(prank, piece, (int64_t)pos, descs)) {
+                    pos += run;
+                    i = j - 1;
+                    continue;
+                }
+            }
+        }
+        if (plane && !host_plane && r.length >= (uint64_t)FLAGS_rccl_min_bytes && gpu::rccl::AcceptsBlock(r.block)) {
+            Buf piece;
+            piece.append_block(r.block, r.offset, r.length);
+            if (plane_send(prank, piece, (int64_t)pos, descs)) {
+                pos += r.length;
+                continue;
+            }
+        }
         if (IsHostAccessible(r.block->kind) || !direct) {
             if (IsHostAccessible(r.block->kind)) {
                 host_out->append_block(r.block, r.offset, r.length);
@@ -79,9 +163,7 @@ int LendDeviceBlocks(Socket* sock, const Buf& in, bool verify, Buf* host_out, De
             } else if (rc != 0) {
                 descs->RemoveLast();
                 // blocks lent for this message so far will never be pulled
-                for (int k = lent_before; k < descs->size(); ++k) {
-                    if (g_hooks.cancel) g_hooks.cancel(descs->Get(k));
-                }
+                for (int k = lent_before; k < descs->size(); ++k) CancelOne(descs->Get(k));
                 while (descs->size() > lent_before) descs->RemoveLast();
                 if (err) *err = "fail to send " + std::to_string(r.length) + " device bytes over " + sock->description();
                 return -1;
@@ -100,11 +182,6 @@ int PullDeviceBlocksBatch(Socket* sock, const std::vector<std::pair<const Device
     auto release_all = [&] {
         for (const auto& it : items) ReleaseDeviceBlocks(sock, *it.first);
     };
-    if (!g_hooks.recv) {
-        release_all();
-        if (err) *err = "received device payload but no device transport is registered";
-        return -1;
-    }
     // per item: descriptors sorted by position, validated against the
     // inline (host) part before anything is pulled, so a bad meta never
     // leaves half-consumed slots
@@ -130,12 +207,61 @@ int PullDeviceBlocksBatch(Socket* sock, const std::vector<std::pair<const Device
         }
         flat.insert(flat.end(), v.begin(), v.end());
     }
-    // one transport call (one batched pull) for every payload of every item
+    // one transport call (one batched pull) for every lent payload of every
+    // item; payloads that travel over the RCCL plane are claimed after it
     std::vector<Buf> pulled(flat.size());
-    if (g_hooks.recv(sock, flat.data(), (int)flat.size(), pulled.data()) != 0) {
-        // the hook released every slot whatever happened
-        if (err) *err = "fail to receive " + std::to_string(flat.size()) + " device payload(s)";
+    std::vector<const DevicePayload*> lent;
+    std::vector<size_t> lent_at, plane_at;
+    for (size_t i = 0; i < flat.size(); ++i) {
+        if (flat[i]->has_rccl_seq()) plane_at.push_back(i);
+        else {
+            lent.push_back(flat[i]);
+            lent_at.push_back(i);
+        }
+    }
+    auto discard_plane = [&] {
+        for (size_t i : plane_at) ReleaseOne(sock, *flat[i]);
+    };
+    bool bad_plane = false;
+    for (size_t i : plane_at) {
+        const DevicePayload& d = *flat[i];
+        bad_plane |= d.rccl_dst() != gpu::rccl::Rank() || d.rccl_src() != sock->plane_rank() || d.length() <= 0;
+    }
+    if (bad_plane) {
+        release_all();
+        if (err) *err = "bad RCCL plane payload descriptor";
         return -1;
+    }
+    if (!lent.empty()) {
+        if (!g_hooks.recv) {
+            release_all();
+            if (err) *err = "received device payload but no device transport is registered";
+            return -1;
+        }
+        std::vector<Buf> got(lent.size());
+        if (g_hooks.recv(sock, lent.data(), (int)lent.size(), got.data()) != 0) {
+            // the hook released every lent slot whatever happened
+            discard_plane();
+            if (err) *err = "fail to receive " + std::to_string(lent.size()) + " device payload(s)";
+            return -1;
+        }
+        for (size_t k = 0; k < lent.size(); ++k) pulled[lent_at[k]] = std::move(got[k]);
+    }
+    if (!plane_at.empty()) {
+        std::vector<int> src;
+        std::vector<uint64_t> seq;
+        std::vector<size_t> len;
+        for (size_t i : plane_at) {
+            src.push_back(flat[i]->rccl_src());
+            seq.push_back(flat[i]->rccl_seq());
+            len.push_back((size_t)flat[i]->length());
+        }
+        std::vector<Buf> got(plane_at.size());
+        if (gpu::rccl::Recv((int)plane_at.size(), src.data(), seq.data(), len.data(), got.data()) != 0) {
+            if (err) *err = "fail to receive " + std::to_string(plane_at.size()) + " RCCL plane payload(s)";
+            return -1;
+        }
+        for (size_t k = 0; k < plane_at.size(); ++k) pulled[plane_at[k]] = std::move(got[k]);
     }
     size_t at = 0;
     for (size_t k = 0; k < items.size(); ++k) {
@@ -160,8 +286,7 @@ int PullDeviceBlocks(Socket* sock, const DevicePayloads& descs, Buf* attachment,
 }
 
 void ReleaseDeviceBlocks(Socket* sock, const DevicePayloads& descs) {
-    if (!g_hooks.release || !sock) return;
-    for (int i = 0; i < descs.size(); ++i) g_hooks.release(sock, descs.Get(i));
+    for (int i = 0; i < descs.size(); ++i) ReleaseOne(sock, descs.Get(i));
 }
 
 bool SplitDevicePayload(Controller* cntl, bool request, const Buf& attachment, Buf* host_out, RpcMeta* meta,
@@ -190,8 +315,7 @@ bool MergeDevicePayload(Controller* cntl, Socket* sock, const RpcMeta& meta, boo
 void ReleaseDevicePayload(Socket* sock, const RpcMeta& meta) { ReleaseDeviceBlocks(sock, meta.device_payload()); }
 
 void CancelDeviceBlocks(const DevicePayloads& descs) {
-    if (!g_hooks.cancel) return;
-    for (int i = 0; i < descs.size(); ++i) g_hooks.cancel(descs.Get(i));
+    for (int i = 0; i < descs.size(); ++i) CancelOne(descs.Get(i));
 }
 
 void CancelDevicePayload(const RpcMeta& meta) { CancelDeviceBlocks(meta.device_payload()); }

@@ -247,6 +247,9 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
                 r ^= r << 17;
                 _attachment[i] = (char)r;
             }
+            char* blk = _attachment_buf.append_contiguous(_attachment.size());
+            if (blk) memcpy(blk, _attachment.data(), _attachment.size());
+            else _attachment_buf.append(_attachment);
             if (_opt.device_attachment) {
                 if (gpu::Init(_opt.gpu_device, error) != 0) return -1;
                 // arena memory: the xGMI transport lends it to the server
@@ -305,7 +308,9 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     if (_device_attachment) {
         gpu::AppendDevice(&cntl.request_attachment(), _device_attachment, _attachment.size(), _opt.gpu_device);
     } else if (!_attachment.empty()) {
-        cntl.request_attachment().append(_attachment);
+        // one shared block, appended by reference like rpc_press's IOBuf
+        // attachment (tools/rpc_press/rpc_press_impl.cpp): no per-call copy
+        cntl.request_attachment().append(_attachment_buf);
     }
     call->nbytes = _opt.scatter ? 2 * (int64_t)(_echo_message.size() * _fanout + _attachment.size())
                                 : 2 * (int64_t)(_echo_message.size() + _attachment.size()) * _fanout;

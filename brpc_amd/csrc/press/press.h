@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "base/buf.h"
 #include "var/percentile.h"
 
 namespace mrpc {
@@ -122,6 +123,7 @@ private:
     std::vector<std::unique_ptr<pb::Message>> _requests;
     std::string _echo_message;
     std::string _attachment;
+    Buf _attachment_buf;                 // _attachment as one shared block
     void* _device_attachment = nullptr;  // HBM copy of _attachment when device_attachment
 
     mutable std::mutex _mu;

@@ -422,6 +422,7 @@ PYBIND11_MODULE(_native, m) {
     }, py::arg("device") = -1);
     g.def("device_arch", [](int dev) { return gpu::DeviceArch(dev); }, py::arg("device") = 0);
     g.def("device_name", [](int dev) { return gpu::DeviceName(dev); }, py::arg("device") = 0);
+    g.def("pci_bus_id", [](int dev) { return gpu::PciBusId(dev); }, py::arg("device") = 0);
     g.def("polled_events", [] { return gpu::PolledEvents(); });
     g.def("enable_xgmi", [](int dev) {
         std::string err;
@@ -439,6 +440,12 @@ PYBIND11_MODULE(_native, m) {
         d["lent_outstanding"] = s.lent_outstanding;
         d["copied_into_arena"] = s.copied_into_arena;
         d["released_unconsumed"] = s.released_unconsumed;
+        d["cross_device_payloads"] = s.cross_device_payloads;
+        d["cross_device_bytes"] = s.cross_device_bytes;
+        d["cross_device_pull_failures"] = s.cross_device_pull_failures;
+        d["peer_access_enabled"] = s.peer_access_enabled;
+        d["attach_failures"] = s.attach_failures;
+        d["peer_maps"] = s.peer_maps;
         const gpu::CopyEngineStats c = gpu::GetCopyEngineStats();
         d["copy_submits"] = c.submits;
         d["copy_launches"] = c.launches;
@@ -464,6 +471,7 @@ PYBIND11_MODULE(_native, m) {
         if (rc != 0) throw std::runtime_error(err);
     }, py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"));
     g.def("rccl_active", [] { return gpu::rccl::Active(); });
+    g.def("rccl_abort_for_test", [](const std::string& why) { gpu::rccl::AbortForTest(why); });
     g.def("rccl_shutdown", [] {
         py::gil_scoped_release nogil;
         gpu::rccl::Shutdown();
@@ -476,9 +484,16 @@ PYBIND11_MODULE(_native, m) {
         d["recv_payloads"] = s.recv_payloads;
         d["recv_bytes"] = s.recv_bytes;
         d["discarded"] = s.discarded;
-        d["groups"] = s.groups;
+        d["rounds"] = s.rounds;
+        d["payload_rounds"] = s.payload_rounds;
         d["aborts"] = s.aborts;
-        d["reorder_waits"] = s.reorder_waits;
+        d["credit_stalls"] = s.credit_stalls;
+        d["stash_expired"] = s.stash_expired;
+        d["recv_timeouts"] = s.recv_timeouts;
+        d["doorbells"] = s.doorbells;
+        d["withdrawn"] = s.withdrawn;
+        d["world"] = s.world;
+        d["host_memory"] = s.host_memory;
         return d;
     });
     g.def("enable_snappy", [](int dev, size_t min_bytes) {

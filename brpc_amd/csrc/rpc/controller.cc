@@ -105,6 +105,7 @@ void Controller::Reset() {
     _idl_result = IDL_VOID_RESULT;
     _use_device_transport = false;
     _reply_xgmi_hello = false;
+    _reply_plane_hello = false;
     _session_kv.clear();
     _request_stream = _response_stream = 0;
     _stream_creator.reset();

@@ -252,6 +252,7 @@ public:
     int64_t _idl_result = IDL_VOID_RESULT;
     bool _use_device_transport = false;  // client: offer the xGMI hello on this call
     bool _reply_xgmi_hello = false;      // server: answer the peer's xGMI hello
+    bool _reply_plane_hello = false;     // server: answer the peer's RCCL plane hello
     HttpHeader* _http_request = nullptr;
     HttpHeader* _http_response = nullptr;
     std::map<std::string, std::string> _session_kv;

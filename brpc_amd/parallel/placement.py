@@ -1,0 +1,112 @@
+"""CPU placement of one rank: the L3 domain its fiber runtime is confined
+to (-cpu_l3_domain, csrc/fiber/runtime.cc), chosen on the NUMA node its GPU
+hangs off.
+
+The MI355X boxes expose every CPU of the node to a container whose CPU-time
+quota is a small fraction of them. Unconfined, the scheduler scatters the
+runtime's threads over many L3 domains and both sockets; confined to one
+L3 domain the 32 B echo is ~2x faster and stable. Pinned socket blocks and
+the staging copies of a rank are DMA'd by its GPU, so the domain should sit
+on that GPU's NUMA node (/sys/bus/pci/devices/<bdf>/local_cpulist); ranks
+whose GPUs share a node take distinct domains of it.
+"""
+import os
+
+
+def parse_cpulist(text):
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        else:
+            cpus.add(int(part))
+    return cpus
+
+
+def allowed_cpus():
+    try:
+        return sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return list(range(os.cpu_count() or 1))
+
+
+def l3_domains(cpus=None):
+    """[(first_cpu, [cpus])] of the allowed CPUs grouped by shared L3, in the
+    order the runtime's -cpu_l3_domain indexes them."""
+    groups = {}
+    for c in (cpus if cpus is not None else allowed_cpus()):
+        first = c
+        try:
+            with open("/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list" % c) as f:
+                first = int(f.read().split(",")[0].split("-")[0])
+        except (OSError, ValueError):
+            pass
+        groups.setdefault(first, []).append(c)
+    return sorted(groups.items())
+
+
+def gpu_numa(device, native=None):
+    """(numa_node, set of local CPUs) of a GPU, or (-1, None) when unknown."""
+    if device is None or device < 0:
+        return -1, None
+    try:
+        if native is None:
+            from .. import native as native_mod
+            native = native_mod
+        bdf = native.gpu.pci_bus_id(device)
+    except Exception:  # noqa: BLE001 - no GPU runtime
+        return -1, None
+    if not bdf:
+        return -1, None
+    base = "/sys/bus/pci/devices/%s" % bdf
+    node, cpus = -1, None
+    try:
+        with open(base + "/numa_node") as f:
+            node = int(f.read().strip())
+    except (OSError, ValueError):
+        pass
+    try:
+        with open(base + "/local_cpulist") as f:
+            cpus = parse_cpulist(f.read())
+    except OSError:
+        pass
+    return node, cpus
+
+
+def choose_l3_domain(local_rank, local_world, device, device_count=0, native=None):
+    """Index (for -cpu_l3_domain) of the L3 domain this rank should use, and
+    a description dict for the bench JSON. -1: leave the rank unconfined."""
+    domains = l3_domains()
+    info = {"l3_domains": len(domains)}
+    if len(domains) <= 1:
+        return -1, info
+    node, local = gpu_numa(device, native)
+    info["gpu_numa_node"] = node
+    cand = list(range(len(domains)))
+    if local:
+        on_node = [i for i, (_, cs) in enumerate(domains) if set(cs) <= local]
+        if on_node:
+            cand = on_node
+    # CPU 0's domain carries housekeeping and most IRQs
+    if len(cand) > 1:
+        cand = [i for i in cand if 0 not in domains[i][1]] or cand
+    # spread the local ranks whose GPUs share this NUMA node over its domains
+    peers = [local_rank]
+    if device_count > 1 and node >= 0:
+        peers = []
+        for r in range(local_world):
+            n, _ = gpu_numa(r % device_count, native)
+            if n == node:
+                peers.append(r)
+        if local_rank not in peers:
+            peers.append(local_rank)
+    slot = sorted(peers).index(local_rank)
+    step = max(1, len(cand) // max(1, len(peers)))
+    idx = cand[(slot * step) % len(cand)]
+    info["l3_domain_first_cpu"] = domains[idx][0]
+    info["ranks_on_gpu_numa_node"] = len(peers)
+    info["numa_local"] = bool(local) and set(domains[idx][1]) <= local
+    return idx, info

@@ -1,25 +1,43 @@
-"""RCCL data plane for RPC payloads (native side: csrc/gpu/rccl_plane.h).
+"""RCCL payload plane for RPC payloads (native side: csrc/gpu/rccl_plane.h).
 
-Every rank of a torchrun job calls :func:`init_rccl_plane` once, before it
-opens connections: rank 0 generates the RCCL unique id, the process group
-broadcasts it, and each rank joins one communicator on its GPU. Connections
-between ranks of the plane then announce their rank in the xGMI hello, and
-device payload blocks of at least ``-rccl_min_bytes`` travel by
-ncclSend/ncclRecv (sequence numbers in the RPC meta) instead of xGMI
-lending. The plane replaces the reference's RDMA zero-copy path
-(src/brpc/rdma/rdma_endpoint.cpp:771-895) for large payloads.
+Every rank of a one-node torchrun job calls :func:`init_rccl_plane` once,
+before it opens connections: rank 0 generates the unique id, the process
+group broadcasts it, and each rank joins the plane (one communicator, one
+stream, numbered rounds). Connections between ranks of the plane then
+exchange a plane hello, and attachment payloads of at least
+``-rccl_min_bytes`` travel by ncclSend/ncclRecv (sequence numbers in the RPC
+meta) instead of xGMI lending. The plane plays the part of the reference's
+RDMA zero-copy path (src/brpc/rdma/rdma_endpoint.cpp:771-895, credits at
+:505-509).
+
+On CPU-only hosts ``library=stub_library()`` runs the same plane on the stub
+RCCL (csrc/tests/stub/fake_rccl.cc: bounded shared-memory FIFOs, one
+in-order queue per process) with host-memory payloads, so multi-rank jobs
+rehearse the plane with gloo.
 """
+import os
+
 import torch.distributed as dist
 
 from .. import native
 
+_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-def init_rccl_plane(topo, min_bytes=None):
-    """Join the job's RCCL plane on ``topo.device``. ``min_bytes`` sets the
-    payload threshold now (None leaves the flag alone: the default never
-    uses the plane). Returns True when the plane is up; a CPU topology has
-    no plane and returns False."""
-    if topo.device < 0:
+
+def stub_library():
+    """Path of the stub RCCL library built by build.py."""
+    return os.path.join(_ROOT, "build", "lib", "libfake_rccl.so")
+
+
+def init_rccl_plane(topo, min_bytes=None, library=None):
+    """Join the job's RCCL plane on ``topo.device`` (or on the stub library
+    when ``library`` is given). ``min_bytes`` sets the payload threshold now
+    (None leaves the flag alone: the default never uses the plane). Returns
+    True when the plane is up; a CPU topology without ``library`` has no
+    plane and returns False."""
+    if library:
+        native.set_flag("rccl_library", library)
+    elif topo.device < 0:
         return False
     if topo.world_size > 1:
         box = [native.gpu.rccl_unique_id() if topo.rank == 0 else None]

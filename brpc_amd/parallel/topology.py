@@ -1,10 +1,18 @@
 """Rank topology for one-process-per-GPU jobs.
 
-torchrun exports RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT; with a
-GPU the process group uses RCCL ("nccl"), otherwise gloo (CPU tests).
-Barriers and reductions are tiny control-plane collectives; the RPC data
-itself moves over the framework's own transports (TCP loopback or the
-xGMI device transport), not through RCCL.
+torchrun exports RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT. The
+torch process group is only the job's CONTROL plane — address exchange,
+the RCCL plane's unique id, barriers and result reductions — and it runs on
+gloo by default, GPU or not. The RPC data moves over the framework's own
+transports: TCP, xGMI lending, and the RCCL payload plane
+(csrc/gpu/rccl_plane.h), which owns its own communicator and stream.
+
+Why not torch's "nccl" backend for the barriers: its collectives are RCCL
+kernels on torch's streams. With GPU_MAX_HW_QUEUES=4 those streams share
+hardware queues with the payload plane's stream, and two blocking RCCL
+kernels queued in opposite orders on two ranks (a barrier behind a plane
+round on one, a plane round behind the barrier on the other) would wait
+for each other forever. Set MRPC_DIST_BACKEND=nccl to use it anyway.
 """
 import os
 from dataclasses import dataclass
@@ -42,9 +50,9 @@ def init_distributed(prefer_gpu=True):
     backend = ""
     if ws > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if use_gpu else "gloo"
+        backend = os.environ.get("MRPC_DIST_BACKEND", "gloo") if use_gpu else "gloo"
         kw = {}
-        if use_gpu:
+        if backend == "nccl":
             kw["device_id"] = torch.device("cuda", device)
         dist.init_process_group(backend=backend, rank=rank, world_size=ws, **kw)
     elif dist.is_initialized():

@@ -38,7 +38,8 @@ def test_bench_multi_rank_gloo(nranks):
                         os.path.join(ROOT, "bench.py"), "--gpus", str(nranks), "--steps", "2", "--warmup", "1",
                         "--requests-per-step", "1000", "--requests-per-step-64k", "300",
                         "--requests-per-step-fanout", "100", "--requests-per-step-grpc", "50",
-                        "--latency-sample-s", "0.3", "--workers", "2"],
+                        "--latency-sample-s", "0.3", "--workers", "2", "--rccl-stub", "--requests-per-step-1m", "20",
+                        "--sweep-seconds", "0.05", "--stream-min-s", "0.2"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -50,5 +51,14 @@ def test_bench_multi_rank_gloo(nranks):
     assert j["fanout_peers_per_rank"] == nranks - 1 and j["fanout_errors"] == 0 and j["fanout_gbytes_per_s"] > 0
     assert j["scatter_errors"] == 0 and j["scatter_gbytes_per_s"] > 0
     assert j["route_errors"] == 0 and j["route_calls_per_s"] > 0
+    # the RCCL payload plane (stub library on the CPU) carried the rccl legs
+    # between all ranks, without aborts, and the JSON says so per leg
+    assert j["rccl_world"] == nranks and j["rccl_aborts"] == 0 and j["rccl_64KB_errors"] == 0
+    assert j["transport"]["rccl_64KB"]["rccl_payloads"] > 0
+    assert j["rccl_1MB_errors"] == 0 and j["transport"]["rccl_1MB"]["rccl_payloads"] > 0
+    assert j["errors_1MB"] == 0 and j["qps_1MB"] > 0
+    assert all(p["errors"] == 0 for p in j["sweep"])
+    assert "rccl_crossover_bytes" in j
+    assert j["stream_timed_s"] >= 0.2
     if nranks > 2:  # a relay chain needs at least two other ranks
         assert j["pipeline_hops"] == nranks - 1 and j["pipeline_gbytes_per_s"] > 0

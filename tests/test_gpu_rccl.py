@@ -48,7 +48,7 @@ def test_echo_payloads_over_rccl(plane):
         # only the calls in flight before the connection's hello completed
         # (at most one per concurrent caller) were lent over xGMI
         assert x["copy_segments"] <= 64, x
-        assert r["groups"] < r["sent_payloads"], r  # concurrent payloads share groups
+        assert r["payload_rounds"] < r["sent_payloads"], r  # concurrent payloads share rounds
     finally:
         s.stop()
 

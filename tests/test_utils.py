@@ -28,12 +28,12 @@ def test_flag_argument_lists():
     assert parse_flag_args("") == []
     with pytest.raises(ValueError):
         parse_flag_args("a=1")
-    before = get_flag("rccl_max_group_ops")
+    before = get_flag("rccl_round_payloads")
     try:
-        assert apply_flag_args("--rccl_max_group_ops=77") == ["rccl_max_group_ops"]
-        assert get_flag_typed("rccl_max_group_ops") == 77
+        assert apply_flag_args("--rccl_round_payloads=77") == ["rccl_round_payloads"]
+        assert get_flag_typed("rccl_round_payloads") == 77
     finally:
-        set_flag("rccl_max_group_ops", before)
+        set_flag("rccl_round_payloads", before)
 
 
 def test_parse_prometheus():
