@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""CPU profile of one echo leg (where do the host cycles of an RPC go?).
+
+Runs a closed-loop press in a Python thread while the in-process sampling
+profiler (csrc/builtin/cpu_profiler.cc, SIGPROF + backtrace) records every
+thread, then prints the hottest frames by self and inclusive samples.
+
+  python benchmarks/profile_leg.py --leg gpu_handler --seconds 3
+"""
+import argparse
+import collections
+import os
+import sys
+import threading
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--leg", default="gpu_handler",
+                    choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps"])
+    ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--concurrency", type=int, default=50)
+    ap.add_argument("--workers", type=int, default=12)
+    ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--folded-out", default="")
+    a = ap.parse_args()
+    import torch
+    from brpc_amd import native, parallel
+    from brpc_amd.models import start_echo_server
+    cuda = torch.cuda.is_available()
+    native.set_flag("fiber_concurrency", str(a.workers))
+    dev = 0 if cuda else -1
+    if cuda:
+        from brpc_amd.parallel.placement import choose_l3_domain
+        l3, _ = choose_l3_domain(0, 1, 0, torch.cuda.device_count())
+        if l3 >= 0:
+            native.set_flag("cpu_l3_domain", str(l3))
+    native.set_flag("event_dispatcher_spin_us", os.environ.get("SPIN_US", "1000000"))
+    topo = parallel.Topology(rank=0, world_size=1, local_rank=0, local_world_size=1, device=dev)
+    if a.leg == "rccl_64k":
+        parallel.init_rccl_plane(topo, min_bytes=32768)
+    s = start_echo_server("127.0.0.1:0", num_threads=a.workers, gpu_device=dev)
+    o = {"server": s.address, "concurrency": a.concurrency, "request_size": 16, "gpu_device": dev}
+    if a.leg in ("gpu_handler", "host_64k", "dev_64k", "rccl_64k"):
+        o["attachment_size"] = 65520
+    if a.leg == "gpu_handler":
+        o["gpu_process"] = True
+    if a.leg in ("dev_64k", "rccl_64k"):
+        o["device_attachment"] = True
+    if a.leg == "echo_32b":
+        o["request_size"] = 32
+    if a.leg == "lat_100qps":
+        o.update({"qps": 100.0, "concurrency": 1, "request_size": 32})
+    p = native.Press(o)
+    p.run_for(0.5)
+    p.reset_stats()
+    th = threading.Thread(target=p.run_for, args=(a.seconds + 0.4,))
+    th.start()
+    folded, n = native.profile_cpu(a.seconds, 999)
+    th.join()
+    st = p.stats()
+    print("leg=%s qps=%.0f p50=%s p99=%s errors=%d samples=%d" % (a.leg, st["qps"], st["p50_us"], st["p99_us"],
+                                                                  st["error"], n))
+    if a.folded_out:
+        with open(a.folded_out, "w") as f:
+            f.write(folded)
+    self_c, incl_c = collections.Counter(), collections.Counter()
+    total = 0
+    for line in folded.splitlines():
+        stack, _, cnt = line.rpartition(" ")
+        try:
+            c = int(cnt)
+        except ValueError:
+            continue
+        frames = stack.split(";")
+        total += c
+        self_c[frames[-1]] += c
+        for f in set(frames):
+            incl_c[f] += c
+    print("--- self (of %d samples)" % total)
+    for f, c in self_c.most_common(a.top):
+        print("%6.2f%%  %s" % (100.0 * c / max(1, total), f[:160]))
+    print("--- inclusive")
+    for f, c in incl_c.most_common(a.top):
+        print("%6.2f%%  %s" % (100.0 * c / max(1, total), f[:160]))
+    s.stop()
+
+
+if __name__ == "__main__":
+    main()

@@ -6,6 +6,7 @@
 #include <sstream>
 
 #include "base/crc32c.h"
+#include "builtin/cpu_profiler.h"
 #include "base/snappy.h"
 #include "base/flags.h"
 #include "base/logging.h"
@@ -285,6 +286,19 @@ PYBIND11_MODULE(_native, m) {
     });
     // rpcz: recent spans (memory), spans by trace id / end time (disk store)
     m.def("press_slow_calls", [] { return press::TakeSlowCalls(); });
+    // sampling CPU profile of the whole process (folded stacks), e.g. while a
+    // press runs in another Python thread
+    m.def("profile_cpu", [](double seconds, int hz) {
+        std::string folded;
+        int64_t n = 0;
+        bool ok;
+        {
+            py::gil_scoped_release nogil;
+            ok = profiler::ProfileCpu(seconds, hz, &folded, nullptr, &n);
+        }
+        if (!ok) throw std::runtime_error("another CPU profile is running");
+        return py::make_tuple(folded, n);
+    }, py::arg("seconds"), py::arg("hz") = 999);
     m.def("monotonic_us", [] { return monotonic_us(); });
     m.def("rpcz_recent", [](size_t max) { return ListRecentSpans(max, 0); }, py::arg("max") = 100);
     m.def("rpcz_trace", [](uint64_t trace, size_t max) { return span_db::FindTrace(trace, max); },
