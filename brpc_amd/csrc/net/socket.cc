@@ -724,11 +724,13 @@ int Socket::Write(Buf* data, const WriteOptions* options) {
         const int ec = _error_code ? _error_code : EFAILEDSOCKET;
         if (opt.id_wait != fiber::INVALID_CALL_ID) fiber::call_id_error(opt.id_wait, ec, error_text());
         errno = ec;
+        if (opt.auth_winner) SetAuthentication(ec);
         return -1;
     }
     if (!opt.ignore_eovercrowded && _unwritten_bytes.load(std::memory_order_relaxed) > FLAGS_socket_max_unwritten_bytes) {
         if (opt.id_wait != fiber::INVALID_CALL_ID) fiber::call_id_error(opt.id_wait, EOVERCROWDED, "socket overcrowded");
         errno = EOVERCROWDED;
+        if (opt.auth_winner) ResetAuthentication();  // the next writer sends the credentials
         return -1;
     }
     WriteRequest* req = get_object<WriteRequest>();
@@ -756,13 +758,18 @@ int Socket::Write(Buf* data, const WriteOptions* options) {
         std::lock_guard<std::mutex> g(_pipeline_mu);
         PipelinedInfo pi;
         pi.count = opt.pipelined_count;
+        pi.auth_replies = opt.auth_replies;
         pi.tag = opt.pipelined_tag;
         pi.protocol = opt.pipelined_protocol;
         pi.id_wait = opt.id_wait;
         _pipeline_q.push_back(pi);
-        return StartWrite(req, opt);
+        const int rc = StartWrite(req, opt);
+        if (opt.auth_winner) SetAuthentication(0);  // later writers follow the credentials on the wire
+        return rc;
     }
-    return StartWrite(req, opt);
+    const int rc = StartWrite(req, opt);
+    if (opt.auth_winner) SetAuthentication(0);
+    return rc;
 }
 
 bool Socket::PopPipelinedInfo(PipelinedInfo* out) {
@@ -984,19 +991,29 @@ int Socket::GetShortSocket(SocketUniquePtr* out) {
 // ---------------------------------------------------------------- auth
 
 bool Socket::FightAuthentication(int* auth_error) {
-    int expected = 0;
-    if (_auth_state.compare_exchange_strong(expected, 1)) return true;
-    while (_auth_state.load(std::memory_order_acquire) != 2) {
-        fiber::butex_wait(_auth_butex, 0, nullptr);
+    for (;;) {
+        int expected = 0;
+        if (_auth_state.compare_exchange_strong(expected, 1)) return true;
+        if (expected == 2) {
+            *auth_error = _auth_error.load();
+            return false;
+        }
+        // someone is authenticating: wait for the outcome (or a reset)
+        const int seq = _auth_butex->load(std::memory_order_acquire);
+        if (_auth_state.load(std::memory_order_acquire) == 1) fiber::butex_wait(_auth_butex, seq, nullptr);
     }
-    *auth_error = _auth_error.load();
-    return false;
 }
 
 void Socket::SetAuthentication(int error) {
     _auth_error.store(error);
     _auth_state.store(2, std::memory_order_release);
-    _auth_butex->store(1, std::memory_order_release);
+    _auth_butex->fetch_add(1, std::memory_order_release);
+    fiber::butex_wake_all(_auth_butex);
+}
+
+void Socket::ResetAuthentication() {
+    _auth_state.store(0, std::memory_order_release);
+    _auth_butex->fetch_add(1, std::memory_order_release);
     fiber::butex_wake_all(_auth_butex);
 }
 

@@ -124,10 +124,17 @@ struct WriteOptions {
     // protocol-private tag carried with the pipelined entry (e.g. HEAD)
     uint32_t pipelined_tag = 0;
     int pipelined_protocol = 0;  // ProtocolType of the request (parsers claim only their own)
+    // The write carries the connection's credentials in front of the
+    // request (redis AUTH/SELECT): the parser first consumes this many
+    // replies; `auth_winner` ends this socket's authentication fight once
+    // the write is queued (FightAuthentication losers wait for that).
+    int auth_replies = 0;
+    bool auth_winner = false;
 };
 
 struct PipelinedInfo {
     int count = 0;
+    int auth_replies = 0;  // replies to credentials sent in front of the request
     uint32_t tag = 0;
     int protocol = 0;
     fiber::CallId id_wait = fiber::INVALID_CALL_ID;
@@ -191,6 +198,8 @@ public:
     // Authentication: the first writer on a socket sends credentials.
     bool FightAuthentication(int* auth_error);
     void SetAuthentication(int error);
+    // The winner could not send its credentials: let the next writer fight.
+    void ResetAuthentication();
     int auth_error() const { return _auth_error.load(); }
 
     // Pipelined protocols: peek/pop the entry of the oldest outstanding write.

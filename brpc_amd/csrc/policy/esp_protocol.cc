@@ -60,7 +60,12 @@ void SerializeEspRequest(Buf* buf, Controller* cntl, const pb::Message* request)
 }
 
 void PackEspRequest(Buf* packet, uint64_t, const pb::MethodDescriptor*, Controller* cntl, const Buf& request_buf,
-                    const Authenticator*) {
+                    const Authenticator* auth) {
+    if (auth) {  // first request of the connection carries the ESP preamble
+        std::string cred;
+        auth->GenerateCredential(&cred);
+        packet->append(cred);
+    }
     packet->append(request_buf);
     cntl->_pipelined_count = 1;
     cntl->_pipelined_tag = kEspTag;

@@ -3,8 +3,10 @@
 // responses map to calls through the socket's pipelined-info queue.
 #include <memory>
 
+#include "base/logging.h"
 #include "fiber/call_id.h"
 #include "net/input_messenger.h"
+#include "policy/authenticators.h"
 #include "policy/policies.h"
 #include "redis/memcache.h"
 #include "rpc/controller.h"
@@ -55,6 +57,22 @@ ParseResult ParseMemcacheMessage(Buf* source, Socket* socket, bool, const void*)
         ctx->has_pi = true;
         ctx->partial.Clear();
     }
+    if (ctx->pi.auth_replies > 0) {
+        // the SASL reply to the bucket credential sent in front of this
+        // request (reference: memcache_binary_protocol.cpp:130-138)
+        unsigned char h[24];
+        if (source->copy_to(h, sizeof(h)) < sizeof(h)) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+        const uint32_t body = ((uint32_t)h[8] << 24) | ((uint32_t)h[9] << 16) | ((uint32_t)h[10] << 8) | h[11];
+        if (source->size() < sizeof(h) + body) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+        const uint16_t status = (uint16_t)((h[6] << 8) | h[7]);
+        if (h[1] != kMemcacheSaslAuth || status != 0) {
+            LOG(ERROR) << "couchbase bucket authentication failed (status " << status << ")";
+            return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+        }
+        source->pop_front(sizeof(h) + body);
+        ctx->pi.auth_replies = 0;
+        if (source->empty()) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+    }
     const int rc = ctx->partial.ConsumePartial(source, ctx->pi.count);
     if (rc < 0) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
     if (rc == 0) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
@@ -76,7 +94,16 @@ void SerializeMemcacheRequest(Buf* buf, Controller* cntl, const pb::Message* req
 }
 
 void PackMemcacheRequest(Buf* packet, uint64_t, const pb::MethodDescriptor*, Controller* cntl, const Buf& request_buf,
-                         const Authenticator*) {
+                         const Authenticator* auth) {
+    if (auth) {  // first request of the connection: SASL credential in front
+        std::string cred;
+        if (auth->GenerateCredential(&cred) != 0) {
+            cntl->SetFailed(ERPCAUTH, "fail to generate memcache credential");
+            return;
+        }
+        packet->append(cred);
+        cntl->_auth_replies = 1;
+    }
     packet->append(request_buf);
     if (cntl->_pipelined_count <= 0) cntl->_pipelined_count = 1;
 }

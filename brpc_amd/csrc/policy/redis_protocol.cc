@@ -8,6 +8,7 @@
 #include "base/util.h"
 #include "fiber/call_id.h"
 #include "net/input_messenger.h"
+#include "policy/authenticators.h"
 #include "policy/policies.h"
 #include "redis/redis.h"
 #include "rpc/controller.h"
@@ -35,6 +36,13 @@ public:
     int protocol_tag() const override { return kTag; }
     RedisCommandHandler* transaction = nullptr;  // inside MULTI
     std::vector<std::vector<std::string>> queued;
+    // incremental command parser: a command's arguments are consumed from
+    // the socket buffer as each one completes, and the state survives
+    // across reads (a large SET spanning many reads is parsed once, not
+    // re-parsed from its first byte on every read)
+    int64_t want_args = -1;   // -1: expecting "*<n>"
+    int64_t bulk_len = -1;    // -1: expecting "$<len>" of the next argument
+    std::vector<std::string> args;
 };
 
 class RedisResponseMessage : public InputMessageBase {
@@ -45,32 +53,80 @@ public:
 
 bool is_client_socket(Socket* s) { return s->user() == get_client_side_messenger(); }
 
-// A command as an array of bulk strings (inline commands also accepted).
-int parse_command(Buf* in, std::vector<std::string>* args) {
-    RedisReply r;
-    char first;
-    if (in->copy_to(&first, 1) != 1) return 0;
-    if (first != '*') {
-        // inline command: "PING\r\n"
+// One CRLF-terminated line from the front of `in`: 1 (consumed into
+// *line), 0 (incomplete), -1 (no CRLF within a sane header length).
+int read_line(Buf* in, std::string* line, size_t max_len) {
+    char buf[128];
+    const size_t n = in->copy_to(buf, std::min(in->size(), std::min(max_len, sizeof(buf))));
+    const char* nl = static_cast<const char*>(memchr(buf, '\n', n));
+    if (!nl) return n >= std::min(max_len, sizeof(buf)) ? -1 : 0;
+    const size_t len = (size_t)(nl - buf);
+    line->assign(buf, len && buf[len - 1] == '\r' ? len - 1 : len);
+    in->pop_front(len + 1);
+    return 1;
+}
+
+bool parse_int(const std::string& s, size_t from, int64_t* out) {
+    if (from >= s.size()) return false;
+    int64_t v = 0;
+    for (size_t i = from; i < s.size(); ++i) {
+        if (s[i] < '0' || s[i] > '9' || v > (int64_t(1) << 40)) return false;
+        v = v * 10 + (s[i] - '0');
+    }
+    *out = v;
+    return true;
+}
+
+const int64_t kMaxArgs = 1 << 20;
+const int64_t kMaxBulk = int64_t(512) << 20;  // redis' proto-max-bulk-len
+
+// Next complete command (array of bulk strings, or an inline command):
+// 1 (in *args), 0 (need more bytes; progress kept in ctx), -1 (malformed).
+int parse_command(RedisServerContext* ctx, Buf* in, std::vector<std::string>* args) {
+    if (ctx->want_args < 0) {
+        char first;
+        if (in->copy_to(&first, 1) != 1) return 0;
         std::string line;
-        char buf[512];
-        const size_t n = in->copy_to(buf, std::min(in->size(), sizeof(buf)));
-        const char* nl = (const char*)memchr(buf, '\n', n);
-        if (!nl) return n == sizeof(buf) ? -1 : 0;
-        line.assign(buf, nl - buf);
-        in->pop_front(nl - buf + 1);
-        if (!line.empty() && line.back() == '\r') line.pop_back();
-        *args = split_string(line, ' ');
-        return args->empty() ? -1 : 1;
+        if (first != '*') {
+            // inline command: "PING\r\n"
+            const int rc = read_line(in, &line, 128);
+            if (rc <= 0) return rc;
+            *args = split_string(line, ' ');
+            return args->empty() ? -1 : 1;
+        }
+        const int rc = read_line(in, &line, 32);
+        if (rc <= 0) return rc;
+        int64_t n = 0;
+        if (!parse_int(line, 1, &n) || n <= 0 || n > kMaxArgs) return -1;
+        ctx->want_args = n;
+        ctx->bulk_len = -1;
+        ctx->args.clear();
+        ctx->args.reserve((size_t)std::min<int64_t>(n, 64));
     }
-    const int rc = r.ConsumePartial(in);
-    if (rc <= 0) return rc;
-    if (!r.is_array() || r.size() == 0) return -1;
-    args->clear();
-    for (size_t i = 0; i < r.size(); ++i) {
-        if (!r[i].is_string()) return -1;
-        args->push_back(r[i].data());
+    while ((int64_t)ctx->args.size() < ctx->want_args) {
+        if (ctx->bulk_len < 0) {
+            std::string line;
+            const int rc = read_line(in, &line, 32);
+            if (rc <= 0) return rc;
+            int64_t len = 0;
+            if (line.empty() || line[0] != '$' || !parse_int(line, 1, &len) || len > kMaxBulk) return -1;
+            ctx->bulk_len = len;
+        }
+        // O(1) until the whole argument is there
+        if (in->size() < (size_t)ctx->bulk_len + 2) return 0;
+        std::string a((size_t)ctx->bulk_len, '\0');
+        if (ctx->bulk_len) in->copy_to(&a[0], (size_t)ctx->bulk_len);
+        char crlf[2];
+        in->pop_front((size_t)ctx->bulk_len);
+        in->copy_to(crlf, 2);
+        if (crlf[0] != '\r' || crlf[1] != '\n') return -1;
+        in->pop_front(2);
+        ctx->args.push_back(std::move(a));
+        ctx->bulk_len = -1;
     }
+    args->swap(ctx->args);
+    ctx->args.clear();
+    ctx->want_args = -1;
     return 1;
 }
 
@@ -147,6 +203,22 @@ ParseResult ParseRedisMessage(Buf* source, Socket* socket, bool read_eof, const 
             ctx->has_pi = true;
             ctx->partial.Clear();
         }
+        if (ctx->pi.auth_replies > 0) {
+            // replies to AUTH/SELECT sent in front of this request: each
+            // must be +OK (reference: redis_protocol.cpp:220-243)
+            const int rc = ctx->partial.ConsumePartial(source, ctx->pi.auth_replies);
+            if (rc < 0) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+            if (rc == 0) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
+            for (int i = 0; i < ctx->partial.reply_size(); ++i) {
+                const RedisReply& r = ctx->partial.reply(i);
+                if (r.type() != REDIS_REPLY_STATUS || r.data() != "OK") {
+                    LOG(ERROR) << "redis authentication failed: " << r.ToString();
+                    return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+                }
+            }
+            ctx->partial.Clear();
+            ctx->pi.auth_replies = 0;
+        }
         const int rc = ctx->partial.ConsumePartial(source, ctx->pi.count);
         if (rc < 0) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
         if (rc == 0) return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
@@ -175,17 +247,20 @@ ParseResult ParseRedisMessage(Buf* source, Socket* socket, bool read_eof, const 
     }
     // execute every complete command now, in order; one write per batch
     Buf out;
+    int rc;
     for (;;) {
         std::vector<std::string> args;
-        const int rc = parse_command(source, &args);
-        if (rc < 0) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
-        if (rc == 0) break;
+        rc = parse_command(ctx, source, &args);
+        if (rc <= 0) break;
         RedisReply reply;
         run_command(const_cast<Server*>(server), ctx, args, &reply);
         reply.SerializeTo(&out);
     }
     if (!out.empty()) socket->Write(&out);
-    return MakeMessage(nullptr);  // consumed inside parse
+    if (rc < 0) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+    // every complete command ran inside parse; what is left is the start
+    // of the next one: read more (reference: redis_protocol.cpp:167-194)
+    return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);
 }
 
 void SerializeRedisRequest(Buf* buf, Controller* cntl, const pb::Message* request) {
@@ -202,8 +277,18 @@ void SerializeRedisRequest(Buf* buf, Controller* cntl, const pb::Message* reques
 }
 
 void PackRedisRequest(Buf* packet, uint64_t correlation_id, const pb::MethodDescriptor*, Controller* cntl,
-                      const Buf& request_buf, const Authenticator*) {
+                      const Buf& request_buf, const Authenticator* auth) {
     (void)correlation_id;
+    if (auth) {  // first request of the connection: AUTH / SELECT in front
+        std::string cred;
+        if (auth->GenerateCredential(&cred) != 0) {
+            cntl->SetFailed(ERPCAUTH, "fail to generate redis credential");
+            return;
+        }
+        packet->append(cred);
+        const RedisAuthenticator* ra = dynamic_cast<const RedisAuthenticator*>(auth);
+        cntl->_auth_replies = ra ? ra->auth_replies() : 1;
+    }
     packet->append(request_buf);
     if (cntl->_pipelined_count <= 0) cntl->_pipelined_count = 1;
 }

@@ -1,5 +1,7 @@
 #include "rpc/channel.h"
 
+#include "policy/authenticators.h"
+
 #include <cerrno>
 
 #include "base/logging.h"
@@ -53,6 +55,8 @@ int Channel::InitChannelOptions(const ChannelOptions* options) {
         LOG(ERROR) << "Channel does not support protocol " << _options.protocol;
         return -1;
     }
+    // esp connections start with the ESP preamble (reference channel.cpp:222-226)
+    if (_protocol_type == PROTOCOL_ESP && !_options.auth) _options.auth = policy::global_esp_authenticator();
     if (!_options.connection_type.empty()) {
         _connection_type = StringToConnectionType(_options.connection_type);
         if (_connection_type == CONNECTION_TYPE_UNKNOWN) {

@@ -100,6 +100,8 @@ void Controller::Reset() {
     _progressive_attachment.reset();
     _progressive_sink.reset();
     _pipelined_count = 0;
+    _auth_replies = 0;
+    _auth_winner = false;
     _pipelined_tag = 0;
     _idl_names = idl_single_req_single_res;
     _idl_result = IDL_VOID_RESULT;
@@ -397,9 +399,30 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
     }
     Buf packet;
     _pack_socket = sock;
-    _protocol->pack_request(&packet, cid.value, _method, this, _request_buf, _auth);
+    _auth_replies = 0;
+    _auth_winner = false;
+    // Credentials ride on the FIRST request of a connection only: the
+    // first writer wins the socket's authentication fight and packs them;
+    // the others wait until its write is queued, so the credentials are
+    // first on the wire (reference: controller.cpp IssueRPC +
+    // socket.cpp:1999-2035).
+    const Authenticator* auth = nullptr;
+    if (_auth) {
+        int auth_error = 0;
+        if (sock->FightAuthentication(&auth_error)) {
+            auth = _auth;
+            _auth_winner = true;
+        } else if (auth_error != 0) {
+            fiber::call_id_unlock(_correlation_id);
+            fiber::call_id_error(cid, ERPCAUTH, "fail to authenticate the connection: " +
+                                                    std::string(::mrpc::ErrorText(auth_error)));
+            return;
+        }
+    }
+    _protocol->pack_request(&packet, cid.value, _method, this, _request_buf, auth);
     _pack_socket = nullptr;
     if (_error_code != 0) {
+        if (_auth_winner) sock->ResetAuthentication();
         const int ec = _error_code;
         const std::string et = _error_text;
         fiber::call_id_unlock(_correlation_id);
@@ -411,6 +434,8 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
     wopt.pipelined_count = _pipelined_count;
     wopt.pipelined_tag = _pipelined_tag;
     wopt.pipelined_protocol = (int)_protocol_type;
+    wopt.auth_replies = _auth_replies;
+    wopt.auth_winner = _auth_winner;
     // Errors of Write() are delivered through call_id_error(cid), which is
     // queued while we hold the lock and handled at unlock.
     sock->Write(&packet, &wopt);

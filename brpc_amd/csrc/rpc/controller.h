@@ -246,6 +246,8 @@ public:
     std::shared_ptr<ProgressiveSink> _progressive_sink;  // client: streamed response body
     // set by pack_request of in-order protocols (http/1.1, redis, memcache)
     int _pipelined_count = 0;
+    int _auth_replies = 0;       // replies to credentials packed in front (redis AUTH/SELECT)
+    bool _auth_winner = false;   // this write carries the connection's credentials
     uint32_t _pipelined_tag = 0;
     std::string _protocol_param;  // "grpc" for channels of protocol "h2:grpc"
     IdlNames _idl_names = {"req", "res"};

@@ -299,6 +299,7 @@ TEST(Legacy, ubrpc_compack_and_mcpack2) {
 namespace {
 // Minimal blocking ESP peer: answers each request with the body uppercased.
 struct EspPeer {
+    std::atomic<bool> bad_preamble{false};
     int lfd = -1;
     int port = 0;
     std::thread th;
@@ -315,6 +316,13 @@ struct EspPeer {
         th = std::thread([this] {
             const int fd = accept(lfd, nullptr, nullptr);
             if (fd < 0) return;
+            // the connection's preamble (EspAuthenticator): magic + port
+            char pre[8];
+            if (!read_full(fd, pre, sizeof(pre)) || memcmp(pre, "\0ESP\x01\x02", 6) != 0) {
+                bad_preamble = true;
+                close(fd);
+                return;
+            }
             for (;;) {
                 EspHead h;
                 if (!read_full(fd, &h, sizeof(h))) break;
@@ -371,6 +379,7 @@ TEST(Legacy, esp_client_pipelined) {
         EXPECT_EQ(ress[i].head.msg_id, (uint64_t)i);
         EXPECT_EQ(ress[i].head.from.port, 8000);
     }
+    EXPECT_FALSE(peer.bad_preamble.load());
 }
 
 namespace {

@@ -10,6 +10,7 @@
 #include <map>
 #include <thread>
 
+#include "policy/authenticators.h"
 #include "redis/memcache.h"
 #include "rpc/channel.h"
 #include "rpc/controller.h"
@@ -26,6 +27,10 @@ struct FakeMemcached {
     std::atomic<bool> stop{false};
     std::map<std::string, std::pair<std::string, uint32_t>> kv;
     uint64_t cas = 1;
+    // couchbase bucket auth: when set, every connection must start with a
+    // SASL PLAIN for it (opcode 0x21), else commands are refused
+    std::string bucket, password;
+    std::atomic<int> sasl_ok{0}, sasl_bad{0}, unauthenticated{0};
 
     FakeMemcached() {
         lfd = socket(AF_INET, SOCK_STREAM, 0);
@@ -82,6 +87,7 @@ struct FakeMemcached {
             int fd = accept(lfd, nullptr, nullptr);
             if (fd < 0) return;
             unsigned char h[24];
+            bool authed = bucket.empty();
             while (readn(fd, h, 24)) {
                 const uint8_t op = h[1];
                 const uint16_t keylen = (uint16_t)be(h + 2, 2);
@@ -91,6 +97,18 @@ struct FakeMemcached {
                 if (body && !readn(fd, &b[0], body)) break;
                 const std::string ext = b.substr(0, extlen), key = b.substr(extlen, keylen),
                                   val = b.substr(extlen + keylen);
+                if (op == 0x21) {  // SASL auth: "PLAIN", "<bucket>\0<bucket>\0<password>"
+                    const std::string want = bucket + std::string(1, '\0') + bucket + std::string(1, '\0') + password;
+                    authed = key == "PLAIN" && val == want;
+                    (authed ? sasl_ok : sasl_bad).fetch_add(1);
+                    reply(fd, op, authed ? 0 : 0x20, "", authed ? "Authenticated" : "Auth failure", 0);
+                    continue;
+                }
+                if (!authed) {
+                    unauthenticated.fetch_add(1);
+                    reply(fd, op, 0x20, "", "Auth required", 0);
+                    continue;
+                }
                 if (op == 0x01) {  // set
                     kv[key] = {val, (uint32_t)be((const unsigned char*)ext.data(), 4)};
                     reply(fd, op, 0, "", "", ++cas);
@@ -241,4 +259,52 @@ TEST(Memcache, response_errors_and_partial_input) {
     Buf in3;
     in3.append(mc_header(0x80, 0x01, 0, 0, 0, 0, 0));
     EXPECT_LT(r3.ConsumePartial(&in3, 1), 0);
+}
+
+TEST(Memcache, couchbase_bucket_sasl_once_per_connection) {
+    FakeMemcached mc;
+    mc.bucket = "travel";
+    mc.password = "pw";
+    policy::CouchbaseAuthenticator auth("travel", "pw");
+    Channel ch;
+    ChannelOptions opt;
+    opt.protocol = "memcache";
+    opt.auth = &auth;
+    opt.timeout_ms = 3000;
+    ASSERT_EQ(ch.Init(("127.0.0.1:" + std::to_string(mc.port)).c_str(), &opt), 0);
+    for (int i = 0; i < 10; ++i) {
+        MemcacheRequest req;
+        MemcacheResponse res;
+        Controller cntl;
+        ASSERT_TRUE(req.Set("k" + std::to_string(i), "v" + std::to_string(i), 0, 0, 0));
+        ASSERT_TRUE(req.Get("k" + std::to_string(i)));
+        ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        std::string v;
+        uint32_t flags = 0;
+        uint64_t c = 0;
+        ASSERT_TRUE(res.PopSet(&c));
+        ASSERT_TRUE(res.PopGet(&v, &flags, &c));
+        EXPECT_EQ(v, "v" + std::to_string(i));
+    }
+    EXPECT_EQ(mc.sasl_ok.load(), 1);  // one connection, one SASL exchange
+    EXPECT_EQ(mc.sasl_bad.load(), 0);
+    EXPECT_EQ(mc.unauthenticated.load(), 0);
+    // wrong bucket password: the connection fails instead of running the ops
+    // (a second fake: the first one serves one connection at a time)
+    FakeMemcached mc2;
+    mc2.bucket = "travel";
+    mc2.password = "pw";
+    policy::CouchbaseAuthenticator bad("travel", "nope");
+    Channel ch2;
+    opt.auth = &bad;
+    opt.max_retry = 0;
+    ASSERT_EQ(ch2.Init(("127.0.0.1:" + std::to_string(mc2.port)).c_str(), &opt), 0);
+    MemcacheRequest req;
+    MemcacheResponse res;
+    Controller cntl;
+    ASSERT_TRUE(req.Get("k1"));
+    ch2.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+    EXPECT_TRUE(cntl.Failed());
+    EXPECT_EQ(mc2.sasl_bad.load(), 1);
 }

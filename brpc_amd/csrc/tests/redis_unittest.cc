@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "base/time.h"
+#include "policy/authenticators.h"
 #include "redis/redis.h"
 #include "rpc/channel.h"
 #include "rpc/controller.h"
@@ -297,7 +298,128 @@ TEST(Redis, concurrent_clients_and_large_values) {
         ASSERT_FALSE(cntl.Failed());
         EXPECT_EQ(res.reply(0).data(), "1600");
     }
-    // NOTE: a SET whose bulk value spans several socket reads (>= ~48 KiB)
-    // currently times out on the server side; tracked in README "What is not
-    // verified here" for the next round.
+    // values spanning many socket reads: the server keeps its parse state
+    // across reads (reference: redis_protocol.cpp:167-194)
+    for (size_t size : {size_t(48) << 10, size_t(1) << 20, size_t(4) << 20}) {
+        std::string big(size, 'v');
+        for (size_t i = 0; i < big.size(); i += 4093) big[i] = (char)('a' + (i / 4093) % 26);
+        RedisRequest req;
+        RedisResponse res;
+        Controller cntl;
+        req.AddCommandByComponents({"SET", "big", big});
+        req.AddCommandByComponents({"GET", "big"});
+        const int64_t t1 = monotonic_us();
+        ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        ASSERT_EQ(res.reply_size(), 2);
+        EXPECT_EQ(res.reply(0).data(), "OK");
+        EXPECT_TRUE(res.reply(1).data() == big);
+        EXPECT_LT(monotonic_us() - t1, 3000000);
+    }
+}
+
+namespace {
+// AUTH/SELECT handlers that record the order commands reach the server
+struct AuthLog {
+    std::mutex mu;
+    std::vector<std::string> seen;
+    void add(const std::string& s) {
+        std::lock_guard<std::mutex> g(mu);
+        seen.push_back(s);
+    }
+};
+class AuthHandler : public RedisCommandHandler {
+public:
+    explicit AuthHandler(AuthLog* log) : _log(log) {}
+    Result Run(const std::vector<std::string>& args, RedisReply* out, bool) override {
+        _log->add(args[0] + " " + (args.size() > 1 ? args[1] : ""));
+        if (args.size() == 2 && args[1] == "s3cret") out->SetStatus("OK");
+        else out->SetError("ERR invalid password");
+        return OK;
+    }
+    AuthLog* _log;
+};
+class SelectHandler : public RedisCommandHandler {
+public:
+    explicit SelectHandler(AuthLog* log) : _log(log) {}
+    Result Run(const std::vector<std::string>& args, RedisReply* out, bool) override {
+        _log->add(args[0] + " " + (args.size() > 1 ? args[1] : ""));
+        out->SetStatus("OK");
+        return OK;
+    }
+    AuthLog* _log;
+};
+class LoggedGet : public RedisCommandHandler {
+public:
+    explicit LoggedGet(AuthLog* log) : _log(log) {}
+    Result Run(const std::vector<std::string>& args, RedisReply* out, bool) override {
+        _log->add(args[0]);
+        out->SetString("value");
+        return OK;
+    }
+    AuthLog* _log;
+};
+}  // namespace
+
+TEST(Redis, auth_and_select_once_per_connection) {
+    AuthLog log;
+    RedisService svc;
+    AuthHandler auth(&log);
+    SelectHandler sel(&log);
+    LoggedGet get(&log);
+    svc.AddCommandHandler("auth", &auth);
+    svc.AddCommandHandler("select", &sel);
+    svc.AddCommandHandler("get", &get);
+    Server server;
+    ServerOptions so;
+    so.redis_service = &svc;
+    so.has_builtin_services = false;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &so), 0);
+    const std::string addr = "127.0.0.1:" + std::to_string(server.listen_port());
+    policy::RedisAuthenticator good("s3cret", 3);
+    Channel ch;
+    ChannelOptions co;
+    co.protocol = "redis";
+    co.auth = &good;
+    ASSERT_EQ(ch.Init(addr.c_str(), &co), 0);
+    // concurrent first calls: exactly one of them carries AUTH + SELECT,
+    // and both go out before any command of the connection
+    std::vector<std::thread> ts;
+    std::atomic<int> errors{0};
+    for (int t = 0; t < 8; ++t) {
+        ts.emplace_back([&] {
+            for (int i = 0; i < 20; ++i) {
+                RedisRequest req;
+                RedisResponse res;
+                Controller cntl;
+                req.AddCommand("GET k");
+                ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+                if (cntl.Failed() || res.reply_size() != 1 || res.reply(0).data() != "value") errors.fetch_add(1);
+            }
+        });
+    }
+    for (auto& t : ts) t.join();
+    EXPECT_EQ(errors.load(), 0);
+    ASSERT_EQ(log.seen.size(), 162u);
+    EXPECT_EQ(log.seen[0], "auth s3cret");
+    EXPECT_EQ(log.seen[1], "select 3");
+    for (size_t i = 2; i < log.seen.size(); ++i) EXPECT_EQ(log.seen[i], "get");
+    // a wrong password fails the calls instead of running them unauthenticated
+    policy::RedisAuthenticator bad("nope");
+    Channel ch2;
+    co.auth = &bad;
+    co.timeout_ms = 2000;
+    co.max_retry = 0;
+    ASSERT_EQ(ch2.Init(addr.c_str(), &co), 0);
+    RedisRequest req;
+    RedisResponse res;
+    Controller cntl;
+    req.AddCommand("GET k");
+    ch2.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+    EXPECT_TRUE(cntl.Failed());
+    // credentials themselves
+    std::string cred;
+    good.GenerateCredential(&cred);
+    EXPECT_EQ(cred, "*2\r\n$4\r\nAUTH\r\n$6\r\ns3cret\r\n*2\r\n$6\r\nSELECT\r\n$1\r\n3\r\n");
+    EXPECT_EQ(good.auth_replies(), 2);
 }
