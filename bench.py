@@ -69,9 +69,10 @@ def parse():
     ap.add_argument("--cpu-l3-domain", type=int, default=-2,
                     help="confine the rank to the CPUs of this L3 domain (-2: auto, one domain per local rank "
                          "spread over the node; -1: no confinement)")
-    ap.add_argument("--dispatcher-poll-us", type=int, default=1000000,
+    ap.add_argument("--dispatcher-poll-us", type=int, default=200,
                     help="event dispatcher busy-polls epoll for this long after the last event before "
-                         "sleeping (-event_dispatcher_spin_us; 0: always sleep in epoll_wait)")
+                         "sleeping (-event_dispatcher_spin_us; 0: always sleep in epoll_wait). The GPU "
+                         "event poller and the RCCL plane poster watch for work as long before sleeping.")
     ap.add_argument("--latency-first", action="store_true",
                     help="take the 100-QPS latency sample before the throughput legs")
     ap.add_argument("--latency-sample-s", type=float, default=6.0,
@@ -163,12 +164,14 @@ def main():
         l3 = auto_l3_domain(topo.local_rank, topo.local_world_size)
     if l3 >= 0:
         native.set_flag("cpu_l3_domain", str(l3))
-    # Busy-polling dispatcher: one core per rank keeps polling epoll while
-    # traffic flows (it sleeps after --dispatcher-poll-us of silence). On the
-    # box this removes the epoll_wait wake-up from every hop: 32 B echo
-    # 1.11-1.15 M -> 1.21-1.26 M QPS, p99 at 100 QPS 390-455 -> 45-138 us
-    # (profiles/r2_cpu_affinity_sweep.txt).
+    # Adaptive polling: the dispatcher keeps polling epoll (and the GPU
+    # poller / plane poster keep watching for work) for --dispatcher-poll-us
+    # after the last event, then sleep. Under load that removes the kernel
+    # wake-up from every hop; at 100 QPS they sleep between requests, and
+    # the JSON reports the rank's CPU% during that sample.
     native.set_flag("event_dispatcher_spin_us", str(max(0, a.dispatcher_poll_us)))
+    native.set_flag("gpu_poller_idle_spin_us", str(max(0, a.dispatcher_poll_us)))
+    native.set_flag("rccl_idle_spin_us", str(max(0, a.dispatcher_poll_us)))
     # extra runtime flags for experiments: MRPC_FLAGS="--name=value ..."
     from brpc_amd.utils import apply_env_flags  # noqa: E402
     apply_env_flags("MRPC_FLAGS")

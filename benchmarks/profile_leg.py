@@ -38,7 +38,8 @@ def main():
         l3, _ = choose_l3_domain(0, 1, 0, torch.cuda.device_count())
         if l3 >= 0:
             native.set_flag("cpu_l3_domain", str(l3))
-    native.set_flag("event_dispatcher_spin_us", os.environ.get("SPIN_US", "1000000"))
+    native.set_flag("event_dispatcher_spin_us", os.environ.get("SPIN_US", "200"))
+    native.set_flag("gpu_poller_idle_spin_us", os.environ.get("POLL_SPIN_US", os.environ.get("SPIN_US", "200")))
     topo = parallel.Topology(rank=0, world_size=1, local_rank=0, local_world_size=1, device=dev)
     if a.leg == "rccl_64k":
         parallel.init_rccl_plane(topo, min_bytes=32768)

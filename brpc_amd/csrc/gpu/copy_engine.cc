@@ -28,8 +28,7 @@ const int kMaxDev = 16;
 struct Batch {
     std::vector<Segment> segs;
     bool want_crc = false;          // some submitter asked for checksums
-    uint32_t* crc_dev = nullptr;    // per-segment CRC32C (HBM pool)
-    uint32_t* crc_host = nullptr;   // ... copied back here (pinned)
+    uint32_t* crc_host = nullptr;   // per-segment CRC32C, stored by the kernel (pinned)
     size_t crc_cap = 0;
     std::atomic<int>* butex = nullptr;
     hipEvent_t ev = nullptr;
@@ -68,19 +67,14 @@ void launch(Batch* b, int device) {
     int rc = (s && b->ev) ? 0 : -1;
     const size_t n = b->segs.size();
     if (rc == 0 && b->want_crc) {
-        // fused pull + checksum, results back to pinned host memory
+        // fused pull + checksum: the kernel stores the CRCs straight into
+        // pinned host memory (one launch, no memset, no D2H copy)
         if (b->crc_cap < n) {
-            HbmFree(b->crc_dev, b->crc_cap * sizeof(uint32_t), device);
             PinnedFree(b->crc_host, b->crc_cap * sizeof(uint32_t));
             b->crc_cap = std::max<size_t>(n, 64);
-            b->crc_dev = static_cast<uint32_t*>(HbmAlloc(b->crc_cap * sizeof(uint32_t), device));
             b->crc_host = static_cast<uint32_t*>(PinnedAlloc(b->crc_cap * sizeof(uint32_t)));
         }
-        if (!b->crc_dev || !b->crc_host ||
-            LaunchBatchedCopyCrc32c(b->segs.data(), (int)n, b->crc_dev, s) != 0 ||
-            hipMemcpyAsync(b->crc_host, b->crc_dev, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess) {
-            rc = -1;
-        }
+        if (!b->crc_host || LaunchBatchedCopyCrc32c(b->segs.data(), (int)n, b->crc_host, s) != 0) rc = -1;
     } else if (rc == 0) {
         rc = LaunchBatchedCopy(b->segs.data(), (int)n, s);
     }

@@ -15,6 +15,13 @@ namespace {
 void pinned_deleter(void* p, void* arg) { PinnedFree(p, (size_t)reinterpret_cast<uintptr_t>(arg)); }
 }  // namespace
 
+namespace {
+
+// One copy+CRC32C pass of `in` into the contiguous destination `d`.
+int copy_with_crc(const Buf& in, char* d, uint32_t* crc, int device);
+
+}  // namespace
+
 int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
     if (device < 0) device = CurrentDevice();
     const size_t n = in.size();
@@ -23,6 +30,30 @@ int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
     Buf dev;
     char* d = static_cast<char*>(AppendNewDeviceBlock(&dev, n, device));
     if (!d) return -1;
+    if (copy_with_crc(in, d, crc, device) != 0) return -1;
+    out->append(std::move(dev));
+    return 0;
+}
+
+int ProcessToPinnedWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
+    if (device < 0) device = CurrentDevice();
+    const size_t n = in.size();
+    *crc = 0;
+    if (n == 0) return 0;
+    char* h = static_cast<char*>(PinnedAlloc(n));
+    if (!h) return -1;
+    if (copy_with_crc(in, h, crc, device) != 0) {
+        PinnedFree(h, n);
+        return -1;
+    }
+    out->append_user_data(h, n, pinned_deleter, reinterpret_cast<void*>((uintptr_t)n), MemKind::PINNED);
+    return 0;
+}
+
+namespace {
+
+int copy_with_crc(const Buf& in, char* d, uint32_t* crc, int device) {
+    const size_t n = in.size();
     std::vector<Segment> segs;
     std::vector<uint32_t> lens;
     segs.reserve(in.backing_block_num());
@@ -59,9 +90,11 @@ int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
     uint32_t c = crcs[0];
     for (size_t i = 1; i < crcs.size(); ++i) c = crc32c::Combine(c, crcs[i], lens[i]);
     *crc = c;
-    out->append(std::move(dev));
+    (void)n;
     return 0;
 }
+
+}  // namespace
 
 int StageToPinnedHost(const Buf& in, Buf* out) {
     // one pinned region for all device bytes, filled by one batched launch

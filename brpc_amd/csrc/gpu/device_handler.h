@@ -21,6 +21,13 @@ namespace gpu {
 // 0 on success.
 int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device);
 
+// Same kernel, but the destination is ONE new pinned host block: the GPU
+// reads the bytes (from pinned socket blocks or HBM), folds their CRC32C and
+// writes them where the socket can send them from. The handler uses it when
+// its response goes back over TCP, where an HBM copy would only have to be
+// staged out again (a second device round trip per request).
+int ProcessToPinnedWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device);
+
 // Copy every device block of `in` into pinned host memory (one batched
 // launch); host blocks are shared. Installed as the staging hook of
 // policy/device_payload.h once a device is enabled.

@@ -33,12 +33,16 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
                          uint64_t max_seg_len, uint32_t* out_dev, void* scratch, hipStream_t s);
 // Same result from the LDS slicing-by-8 kernel (segments passed inline;
 // kept as an independent implementation for cross-checks and A/B timing).
-int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s);
+// `out` needs no initialisation and may be pinned host memory (the kernel
+// stores each finished CRC; read it after the stream's event).
+int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s);
 // Copy every segment src -> dst (one launch for many small copies).
 int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s);
-// Fused: copy every segment AND write its standard CRC32C to out_dev[i]
+// Fused: copy every segment AND write its standard CRC32C to out[i]
 // (one read of the bytes; sources may be local/peer HBM or pinned host).
-int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s);
+// One launch per 32 segments and nothing else: no memset of `out`, which
+// may be pinned host memory read after the stream's event.
+int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s);
 
 // Packed-varint decode (protobuf wire type 0, packed repeated field):
 // `in` holds n bytes of concatenated varints; out receives the values

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -93,8 +94,31 @@ __device__ __forceinline__ uint32_t crc_word8(uint32_t crc, uint32_t lo, uint32_
            t[3][hi & 0xff] ^ t[2][(hi >> 8) & 0xff] ^ t[1][(hi >> 16) & 0xff] ^ t[0][hi >> 24];
 }
 
+// Per-launch-group fold of the chunk CRCs of each segment, with no
+// zero-initialised output (so no memset launch per batch): chunks XOR into
+// a per-stream accumulator slot, count themselves in, and the LAST chunk of
+// a segment takes the accumulator (resetting it for the next launch on the
+// stream) and stores the CRC straight into `out` — device memory, or
+// pinned host memory the CPU reads after the batch's event (no D2H copy).
+__device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch, int seg, uint32_t seg_chunks,
+                                                 uint32_t acc, uint32_t* __restrict__ out) {
+    uint32_t* sacc = scratch;                    // [kInlineSegments]
+    uint32_t* scnt = scratch + kInlineSegments;  // [kInlineSegments]
+    if (seg_chunks == 1) {
+        out[seg] = acc;
+        return;
+    }
+    atomicXor(sacc + seg, acc);
+    __threadfence();
+    if (atomicAdd(scnt + seg, 1u) == seg_chunks - 1) {
+        __threadfence();
+        atomicExch(scnt + seg, 0u);
+        out[seg] = atomicExch(sacc + seg, 0u);
+    }
+}
+
 __global__ void __launch_bounds__(kThreads) crc32c_kernel(SegBatch b, const uint32_t* __restrict__ tables,
-                                                          uint32_t* __restrict__ out) {
+                                                          uint32_t* __restrict__ scratch, uint32_t* __restrict__ out) {
     __shared__ uint32_t t[8][256];
     __shared__ uint32_t wave_acc[kThreads / 64];
     // stage the 8 KiB of tables into LDS: 2048 dwords, 8 per lane, 16 B loads
@@ -150,7 +174,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_kernel(SegBatch b, const uint
             // std = raw0(M) ^ shift(~0, len) ^ ~0
             acc ^= mult_mod_p(shift_bytes_poly(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         }
-        atomicXor(out + seg, acc);
+        fold_segment_crc(scratch, seg, seg_chunks, acc, out);
     }
 }
 
@@ -201,6 +225,7 @@ __global__ void __launch_bounds__(kThreads) batched_copy_kernel(SegBatch b) {
 typedef uint32_t u32x4_unaligned __attribute__((ext_vector_type(4), aligned(1)));
 
 __global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const uint32_t* __restrict__ tables,
+                                                               uint32_t* __restrict__ scratch,
                                                                uint32_t* __restrict__ out) {
     __shared__ uint32_t t[8][256];
     __shared__ uint32_t wave_acc[kThreads / 64];
@@ -255,7 +280,7 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const
         uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
         if (after) acc = mult_mod_p(shift_bytes_poly((uint64_t)after * kChunkBytes), acc);
         if (after == seg_chunks - 1) acc ^= mult_mod_p(shift_bytes_poly(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
-        atomicXor(out + seg, acc);
+        fold_segment_crc(scratch, seg, seg_chunks, acc, out);
     }
 }
 
@@ -804,6 +829,23 @@ const uint32_t* ensure_xc(uint64_t need) {
     return d;
 }
 
+// The fold scratch of a stream (fold_segment_crc): launches on one stream
+// run in order and every launch leaves its slots zeroed, so one zeroed
+// allocation per (device, stream) serves them all.
+uint32_t* stream_scratch(int dev, hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, uint32_t*>* m = new std::map<std::pair<int, hipStream_t>, uint32_t*>;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = m->find({dev, s});
+    if (it != m->end()) return it->second;
+    uint32_t* p = nullptr;
+    const size_t bytes = 2 * kInlineSegments * sizeof(uint32_t);
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, bytes) != hipSuccess) return nullptr;
+    (*m)[{dev, s}] = p;
+    return p;
+}
+
 // Fill a SegBatch with up to kInlineSegments segments; returns chunk count.
 uint32_t fill_batch(SegBatch* b, const Segment* segs, int n) {
     memset(b, 0, sizeof(*b));
@@ -824,17 +866,18 @@ uint32_t fill_batch(SegBatch* b, const Segment* segs, int n) {
 
 }  // namespace
 
-int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s) {
+int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s) {
     if (nseg <= 0) return 0;
     if (ensure_tables() != 0) return -1;
     int dev = 0;
     hipGetDevice(&dev);
-    if (hipMemsetAsync(out_dev, 0, sizeof(uint32_t) * nseg, s) != hipSuccess) return -1;
+    uint32_t* scratch = stream_scratch(dev, s);
+    if (!scratch) return -1;
     for (int i = 0; i < nseg; i += kInlineSegments) {
         const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;
         SegBatch b;
         const uint32_t chunks = fill_batch(&b, segs + i, n);
-        hipLaunchKernelGGL(crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, out_dev + i);
+        hipLaunchKernelGGL(crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch, out + i);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;
@@ -864,17 +907,19 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out_dev, hipStream_t s) {
+int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s) {
     if (nseg <= 0) return 0;
     if (ensure_tables() != 0) return -1;
     int dev = 0;
     hipGetDevice(&dev);
-    if (hipMemsetAsync(out_dev, 0, sizeof(uint32_t) * nseg, s) != hipSuccess) return -1;
+    uint32_t* scratch = stream_scratch(dev, s);
+    if (!scratch) return -1;
     for (int i = 0; i < nseg; i += kInlineSegments) {
         const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;
         SegBatch b;
         const uint32_t chunks = fill_batch(&b, segs + i, n);
-        hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, out_dev + i);
+        hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch,
+                           out + i);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;

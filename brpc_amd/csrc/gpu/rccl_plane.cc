@@ -41,6 +41,7 @@ DEFINE_int64(rccl_window_bytes, int64_t(256) << 20,
 DEFINE_int32(rccl_round_payloads, 64, "most payloads announced to one peer per round");
 DEFINE_int64(rccl_round_bytes, int64_t(64) << 20, "most payload bytes announced to one peer per round");
 DEFINE_int32(rccl_stash_ttl_ms, 30000, "received payloads nobody claims are dropped after this long");
+DEFINE_int32(rccl_idle_spin_us, 0, "an idle plane poster watches its doorbell this long before sleeping");
 
 namespace mrpc {
 namespace gpu {
@@ -520,6 +521,12 @@ public:
                     const uint32_t s = bell->seq.load(std::memory_order_acquire);
                     housekeeping_locked();
                     lk.unlock();
+                    // watch the doorbell a little while before sleeping: the
+                    // next payload of a busy stream is usually close behind
+                    const int64_t until = monotonic_us() + std::max(0, FLAGS_rccl_idle_spin_us);
+                    while (bell->seq.load(std::memory_order_acquire) == s && monotonic_us() < until) {
+                        for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+                    }
                     timespec ts{0, 50 * 1000 * 1000};
                     futex(&bell->seq, FUTEX_WAIT, s, &ts);
                     lk.lock();

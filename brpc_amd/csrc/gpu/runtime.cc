@@ -22,6 +22,9 @@
 DEFINE_int32(gpu_streams_per_device, 4, "HIP streams per device in the pool (<= GPU_MAX_HW_QUEUES)");
 DEFINE_int32(gpu_poller_spin_us, 50, "event poller busy-polls this long after the last completion before backing off");
 DEFINE_int32(gpu_poller_sleep_us, 2, "event poller sleep between polls once the spin budget is spent");
+DEFINE_int32(gpu_poller_idle_spin_us, 0,
+             "with nothing in flight the event poller watches for new events this long before sleeping "
+             "(saves a condvar wake-up per batch on busy RPC streams; costs that much CPU per idle period)");
 
 namespace mrpc {
 namespace gpu {
@@ -74,13 +77,20 @@ struct Waiter {
 class EventPoller {
 public:
     void add(const Waiter& w) {
-        std::unique_lock<std::mutex> g(_mu);
-        if (!_started) {
-            _started = true;
-            pthread_create(&_th, nullptr, &EventPoller::run, this);
+        bool wake;
+        {
+            std::unique_lock<std::mutex> g(_mu);
+            if (!_started) {
+                _started = true;
+                pthread_create(&_th, nullptr, &EventPoller::run, this);
+            }
+            _incoming.push_back(w);
+            _nincoming.store(1, std::memory_order_release);
+            wake = _sleeping;
         }
-        _incoming.push_back(w);
-        _cv.notify_one();
+        // only a sleeping poller needs the futex wake; a polling or
+        // idle-spinning one sees _nincoming
+        if (wake) _cv.notify_one();
     }
     int64_t polled() const { return _polled.load(std::memory_order_relaxed); }
 
@@ -93,19 +103,37 @@ private:
         static_cast<EventPoller*>(arg)->loop();
         return nullptr;
     }
+    static int64_t now_us() {
+        timespec now;
+        clock_gettime(CLOCK_MONOTONIC, &now);
+        return now.tv_sec * 1000000LL + now.tv_nsec / 1000;
+    }
     void loop() {
         std::vector<Waiter> active;
         int64_t last_progress_us = 0;
         for (;;) {
             bool progressed = false;
+            if (active.empty()) {
+                // idle: keep watching for new work a little while before
+                // sleeping — the next batch of a busy RPC stream is usually
+                // microseconds away, and a condvar wake-up costs a kernel
+                // round trip (and a CPU idle exit) per batch
+                const int64_t until = now_us() + std::max(0, FLAGS_gpu_poller_idle_spin_us);
+                while (!_nincoming.load(std::memory_order_acquire) && now_us() < until) {
+                    for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+                }
+            }
             {
                 std::unique_lock<std::mutex> g(_mu);
-                if (active.empty()) {
+                if (active.empty() && _incoming.empty()) {
+                    _sleeping = true;
                     _cv.wait(g, [&] { return !_incoming.empty(); });
+                    _sleeping = false;
                 }
                 progressed = !_incoming.empty();
                 active.insert(active.end(), _incoming.begin(), _incoming.end());
                 _incoming.clear();
+                _nincoming.store(0, std::memory_order_relaxed);
             }
             const size_t before = active.size();
             size_t keep = 0;
@@ -122,11 +150,9 @@ private:
             active.resize(keep);
             if (keep != before) progressed = true;
             if (!active.empty()) {
-                timespec now;
-                clock_gettime(CLOCK_MONOTONIC, &now);
-                const int64_t now_us = now.tv_sec * 1000000LL + now.tv_nsec / 1000;
-                if (progressed) last_progress_us = now_us;
-                if (now_us - last_progress_us > FLAGS_gpu_poller_spin_us) {
+                const int64_t t = now_us();
+                if (progressed) last_progress_us = t;
+                if (t - last_progress_us > FLAGS_gpu_poller_spin_us) {
                     timespec ts{0, 1000L * std::max(1, FLAGS_gpu_poller_sleep_us)};
                     nanosleep(&ts, nullptr);
                 }
@@ -137,6 +163,8 @@ private:
     std::mutex _mu;
     std::condition_variable _cv;
     std::vector<Waiter> _incoming;
+    std::atomic<int> _nincoming{0};
+    bool _sleeping = false;
     bool _started = false;
     pthread_t _th;
     std::atomic<int64_t> _polled{0};

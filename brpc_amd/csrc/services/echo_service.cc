@@ -6,6 +6,8 @@
 #include "base/time.h"
 #include "fiber/fiber.h"
 #include "gpu/device_handler.h"
+#include "net/socket.h"
+#include "policy/device_payload.h"
 #include "rpc/channel.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
@@ -185,16 +187,29 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
             cntl->SetFailed(EREQUEST, "this server has no GPU for gpu_process");
             return;
         }
+        // The kernel reads the request bytes once and folds their CRC32C.
+        // Its output goes where the response travels from: HBM when the
+        // client is on a device transport (lent over xGMI), else pinned
+        // host memory the socket sends from — one device round trip per
+        // batch of requests instead of a gather plus a stage-out.
         uint32_t crc = 0;
-        Buf dev;
-        if (gpu::GatherToDeviceWithCrc(cntl->request_attachment(), &dev, &crc, _gpu_device) != 0) {
+        Buf out;
+        bool device_peer = false;
+        {
+            SocketUniquePtr sock;
+            device_peer = Socket::Address(cntl->_server_socket_id, &sock) == 0 && HasDeviceTransport(sock.get());
+        }
+        const int rc = device_peer
+                           ? gpu::GatherToDeviceWithCrc(cntl->request_attachment(), &out, &crc, _gpu_device)
+                           : gpu::ProcessToPinnedWithCrc(cntl->request_attachment(), &out, &crc, _gpu_device);
+        if (rc != 0) {
             cntl->SetFailed(EINTERNAL, "device processing of %zu bytes failed", cntl->request_attachment().size());
             return;
         }
         _gpu_calls.fetch_add(1, std::memory_order_relaxed);
         response->set_device(_gpu_device);
         response->set_crc32c(crc);
-        cntl->response_attachment().append(std::move(dev));  // served from HBM
+        cntl->response_attachment().append(std::move(out));
         return;
     }
     // zero-copy echo of the attachment (host or device blocks alike)

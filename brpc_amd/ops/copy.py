@@ -34,7 +34,8 @@ def batched_copy_crc32c(srcs, dsts):
     if not srcs:
         return None
     dev = srcs[0].device
-    out = torch.zeros(len(srcs), dtype=torch.int32, device=dev)
+    # no zeroing needed: the kernel stores each finished CRC (fold_segment_crc)
+    out = torch.empty(len(srcs), dtype=torch.int32, device=dev)
     native.gpu.batched_copy_crc32c_launch([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts],
                                           [nbytes(s) for s in srcs], out.data_ptr(), stream_handle(dev))
     return out.to(torch.int64) & 0xFFFFFFFF

@@ -362,9 +362,11 @@ def test_stream_relay_chain_device_chunks(dev):
 
 @pytest.mark.parametrize("device_attachment", [False, True])
 def test_gpu_process_echo_handler(dev, device_attachment):
-    """the handler gathers the attachment into HBM with the
-    fused copy+CRC32C kernel and responds from HBM; the client checks the
-    bytes and the device CRC against the host SSE4.2 CRC32C."""
+    """the handler runs the attachment through the fused
+    copy+CRC32C kernel — into HBM (lent back over xGMI) when the client has
+    a device transport, straight into pinned memory for a TCP client (one
+    device round trip); the client checks the bytes and the device CRC
+    against the host SSE4.2 CRC32C."""
     from brpc_amd import native
     from brpc_amd.models import start_echo_server
     s = start_echo_server("127.0.0.1:0", gpu_device=0)
@@ -425,3 +427,26 @@ def test_rpcz_annotates_device_pulls(dev, tmp_path):
     finally:
         native.set_flag("enable_rpcz", "false")
         s.stop()
+
+
+def test_crc_kernels_need_no_zeroed_output(dev):
+    """The copy+CRC kernel folds chunk CRCs through a per-stream scratch that
+    every launch leaves zeroed, and STORES each result: garbage in the output
+    buffer, repeated launches on one stream and multi-chunk segments give the
+    same, correct CRCs (no memset launch per batch)."""
+    from brpc_amd import native
+    from brpc_amd.ops import crc32c_host
+    from brpc_amd.ops._common import stream_handle
+    sizes = [1, 16384, 16385, 65536, 200000, 1 << 20]
+    srcs = [torch.randint(0, 256, (n,), dtype=torch.uint8, device=dev) for n in sizes]
+    dsts = [torch.empty(n, dtype=torch.uint8, device=dev) for n in sizes]
+    want = [crc32c_host(s.cpu().numpy().tobytes()) for s in srcs]
+    for rep in range(3):
+        out = torch.full((len(sizes),), 0x5A5A5A5A, dtype=torch.int32, device=dev)
+        native.gpu.batched_copy_crc32c_launch([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts], sizes,
+                                              out.data_ptr(), stream_handle(dev))
+        torch.cuda.synchronize()
+        got = [(int(x) & 0xFFFFFFFF) for x in out.cpu().tolist()]
+        assert got == want, rep
+        for s, d in zip(srcs, dsts):
+            assert torch.equal(s, d)
