@@ -11,7 +11,22 @@ import argparse
 import collections
 import os
 import sys
+import resource
 import threading
+import time
+
+
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters (nr_throttled, throttled_usec, ...)."""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -26,6 +41,7 @@ def main():
     ap.add_argument("--workers", type=int, default=12)
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--folded-out", default="")
+    ap.add_argument("--no-profile", action="store_true", help="just run the leg (no SIGPROF sampling)")
     a = ap.parse_args()
     import torch
     from brpc_amd import native, parallel
@@ -59,12 +75,24 @@ def main():
     p.run_for(0.5)
     p.reset_stats()
     th = threading.Thread(target=p.run_for, args=(a.seconds + 0.4,))
+    c0 = cgroup_cpu_stat()
+    t0 = time.perf_counter()
+    r0 = resource.getrusage(resource.RUSAGE_SELF)
     th.start()
-    folded, n = native.profile_cpu(a.seconds, 999)
+    if a.no_profile:
+        time.sleep(a.seconds)
+        folded, n = "", 0
+    else:
+        folded, n = native.profile_cpu(a.seconds, 999)
     th.join()
+    r1 = resource.getrusage(resource.RUSAGE_SELF)
+    wall = time.perf_counter() - t0
+    c1 = cgroup_cpu_stat()
     st = p.stats()
-    print("leg=%s qps=%.0f p50=%s p99=%s errors=%d samples=%d" % (a.leg, st["qps"], st["p50_us"], st["p99_us"],
-                                                                  st["error"], n))
+    cpu = (r1.ru_utime - r0.ru_utime + r1.ru_stime - r0.ru_stime) / wall
+    thr = {k: c1.get(k, 0) - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "nr_periods")}
+    print("leg=%s qps=%.0f p50=%s p99=%s errors=%d samples=%d cpus_used=%.2f cgroup=%s" % (
+        a.leg, st["qps"], st["p50_us"], st["p99_us"], st["error"], n, cpu, thr))
     if a.folded_out:
         with open(a.folded_out, "w") as f:
             f.write(folded)

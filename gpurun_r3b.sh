@@ -27,12 +27,15 @@ case ",$WHAT," in *,prof,*)
     step cpu_$leg 120 python benchmarks/profile_leg.py --leg $leg --seconds 3
   done
   cd /tmp
-  step kt_handler 180 rocprofv3 --kernel-trace --stats -d "$P/kt_handler" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg gpu_handler --seconds 2
-  step kt_dev64k 180 rocprofv3 --kernel-trace --stats -d "$P/kt_dev64k" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg dev_64k --seconds 2
-  step pmc_fetch_handler 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$P/pmc_fetch_handler" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg gpu_handler --seconds 1
-  step pmc_write_handler 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$P/pmc_write_handler" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg gpu_handler --seconds 1
-  step pmc_fetch_dev64k 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$P/pmc_fetch_dev64k" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg dev_64k --seconds 1
-  step pmc_write_dev64k 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$P/pmc_write_dev64k" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg dev_64k --seconds 1
+  step kt_handler 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/kt_handler" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg gpu_handler --seconds 2
+  step kt_dev64k 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/kt_dev64k" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg dev_64k --seconds 2
+  step pmc_fetch_handler 120 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d "$P/pmc_fetch_handler" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg gpu_handler --seconds 1
+  step pmc_write_handler 120 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d "$P/pmc_write_handler" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg gpu_handler --seconds 1
+  step pmc_fetch_dev64k 120 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d "$P/pmc_fetch_dev64k" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg dev_64k --seconds 1
+  step pmc_write_dev64k 120 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d "$P/pmc_write_dev64k" -o run -- python3 "$GRAFT_REPO_ROOT/benchmarks/profile_leg.py" --leg dev_64k --seconds 1
+  cd "$GRAFT_REPO_ROOT"
+  python benchmarks/rocprof_summary.py "$P"/kt_handler "$P"/kt_dev64k "$P"/pmc_fetch_handler "$P"/pmc_write_handler "$P"/pmc_fetch_dev64k "$P"/pmc_write_dev64k --prune > "$P/rocprof_summary.txt" 2>&1
+  du -sh "$P"
   ;;
 esac
 echo done
