@@ -18,8 +18,9 @@ HBM_GBPS = 8000.0
 
 
 def short(name):
-    n = name.split("(")[0]
-    return n.replace("void ", "").strip()[:48]
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    n = n.split("(")[0].strip()
+    return n.split("::")[-1][:48]
 
 
 def main():

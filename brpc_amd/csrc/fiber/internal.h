@@ -120,6 +120,11 @@ struct Stack;
 struct TaskMeta {
     std::atomic<ButexWaiter*> current_waiter{nullptr};
     std::atomic<uint64_t> current_sleep{0};
+    // Guards publishing current_sleep: a timer id is published only while
+    // the sleep that armed it is still the fiber's current one (sleep_gen),
+    // so a late publish of an old sleep can never hide a newer timer.
+    std::mutex sleep_mu;
+    uint64_t sleep_gen = 0;
     bool stop = false;
     bool interrupted = false;
     bool is_main = false;

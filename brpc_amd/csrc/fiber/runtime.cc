@@ -415,6 +415,7 @@ struct SleepArgs {
     fiber_t tid;
     TaskMeta* meta;
     TaskGroup* group;
+    uint64_t gen;  // the sleep's generation (TaskMeta::sleep_gen when armed)
 };
 
 static void ready_to_run_from_timer(void* arg) { ready_to_run_general((fiber_t)(uintptr_t)arg); }
@@ -431,9 +432,11 @@ static void add_sleep_event(void* arg) {
         return;
     }
     // Publish the timer id so interrupt() can cancel the sleep (TaskMeta is
-    // pooled memory, valid even if the fiber already woke; a stale id left
-    // here is harmless: timer ids are versioned).
-    e.meta->current_sleep.store(id, std::memory_order_release);
+    // pooled memory, valid even if the fiber already woke). If this worker
+    // was delayed until the fiber woke, returned and maybe slept again, the
+    // generation no longer matches and the stale id is dropped.
+    std::lock_guard<std::mutex> g(e.meta->sleep_mu);
+    if (e.meta->sleep_gen == e.gen) e.meta->current_sleep.store(id, std::memory_order_release);
 }
 
 int TaskGroup::usleep(TaskGroup** pg, uint64_t us) {
@@ -443,11 +446,24 @@ int TaskGroup::usleep(TaskGroup** pg, uint64_t us) {
     }
     TaskGroup* g = *pg;
     TaskMeta* m = g->_cur_meta;
-    SleepArgs e{us, g->current_tid(), m, g};
+    uint64_t gen;
+    {
+        std::lock_guard<std::mutex> lk(m->sleep_mu);
+        gen = ++m->sleep_gen;
+        m->current_sleep.store(0, std::memory_order_relaxed);
+    }
+    SleepArgs e{us, g->current_tid(), m, g, gen};
     g->set_remained(add_sleep_event, &e);
     sched(pg);
-    // The timer may still be running (it just woke us); spin until it ends.
-    uint64_t id = m->current_sleep.exchange(0, std::memory_order_acquire);
+    // This sleep is over: retire its generation (a publish still in flight
+    // is dropped) and take the id. The timer may still be running (it just
+    // woke us); spin until it ends.
+    uint64_t id;
+    {
+        std::lock_guard<std::mutex> lk(m->sleep_mu);
+        ++m->sleep_gen;
+        id = m->current_sleep.exchange(0, std::memory_order_acquire);
+    }
     if (id) {
         // -1: the timer callback that woke us is still returning; it is a
         // few instructions from done, but never burn a whole time slice

@@ -166,6 +166,7 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
     for (int i = 0; i < _opt.num_channels && !fan.empty(); ++i) {
         ParallelChannelOptions po;
         po.timeout_ms = _opt.timeout_ms;
+        po.gather_response_attachments = true;  // echoes come back in channel order
         std::unique_ptr<ParallelChannel> pc(new ParallelChannel);
         pc->Init(&po);
         std::shared_ptr<CallMapper> mapper;

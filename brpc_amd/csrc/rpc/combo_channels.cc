@@ -40,6 +40,7 @@ struct PCall {
     std::mutex mu;
     int nlaunched = 0, nfail = 0, nsuccess = 0, ndone = 0;
     int fail_limit = 0, success_limit = 0;
+    bool gather = false;  // ParallelChannelOptions::gather_response_attachments
     bool finished = false;
     int first_error = 0;
     std::string first_error_text;
@@ -60,9 +61,9 @@ struct PCall {
 void finish_parent(PCall* pc, int error_code, const std::string& text) {
     Controller* cntl = pc->cntl;
     if (error_code) cntl->SetFailed(error_code, "%s", text.c_str());
-    // gather: the response attachments of the sub calls that succeeded, in
-    // channel order (blocks are shared, HBM blocks stay in HBM)
-    if (!error_code) {
+    // opt-in gather: the response attachments of the sub calls that
+    // succeeded, in channel order (blocks are shared, HBM blocks stay in HBM)
+    if (!error_code && pc->gather) {
         std::lock_guard<std::mutex> g(pc->mu);
         for (auto& s : pc->subs) {
             if (s->succeeded) cntl->response_attachment().append(s->cntl.response_attachment());
@@ -237,6 +238,7 @@ void ParallelChannel::CallMethod(const pb::MethodDescriptor* method, RpcControll
     }
     pc->fail_limit = _options.fail_limit < 0 ? pc->nlaunched : std::max(1, _options.fail_limit);
     pc->success_limit = _options.success_limit < 0 ? pc->nlaunched : std::max(1, _options.success_limit);
+    pc->gather = _options.gather_response_attachments;
     pc->refs.fetch_add(pc->nlaunched);
     std::vector<SubState*> to_launch;
     for (auto& s : pc->subs) {

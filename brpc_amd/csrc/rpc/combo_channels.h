@@ -93,6 +93,14 @@ struct ParallelChannelOptions {
     int32_t timeout_ms = 500;   // -1: none
     int fail_limit = -1;        // finish as failed once this many sub calls failed (-1: all)
     int success_limit = -1;     // finish as ok once this many succeeded (-1: all)
+    // MI355X extension (off by default, like the reference, whose parallel
+    // channel only forwards the REQUEST attachment, parallel_channel.cpp:
+    // 683-684): append the response attachments of the sub calls that
+    // succeeded to the parent's response attachment, in channel order —
+    // the gather half of a scatter/gather over device payloads (blocks are
+    // shared, HBM blocks stay in HBM). With success_limit < n the gathered
+    // set is the sub calls that had succeeded when the call finished.
+    bool gather_response_attachments = false;
 };
 
 class ParallelChannel : public ChannelBase {

@@ -299,6 +299,7 @@ TEST(ParallelChannel, scatter_attachment_slices_and_gather) {
     ParallelChannel pc;
     ParallelChannelOptions po;
     po.timeout_ms = 3000;
+    po.gather_response_attachments = true;
     pc.Init(&po);
     auto mapper = std::make_shared<ScatterAttachmentMapper>();
     for (auto& x : n) pc.AddChannel(make_channel("127.0.0.1:" + std::to_string(x.port)), OWNS_CHANNEL, mapper, nullptr);
@@ -319,6 +320,24 @@ TEST(ParallelChannel, scatter_attachment_slices_and_gather) {
     }
     EXPECT_EQ(n[0].echo.ncalls(), 4);
     EXPECT_EQ(n[2].echo.ncalls(), 4);
+    // without the opt-in the parent's response attachment stays untouched,
+    // as in the reference (parallel_channel.cpp:683-684)
+    {
+        ParallelChannel plain;
+        ParallelChannelOptions pp;
+        pp.timeout_ms = 3000;
+        plain.Init(&pp);
+        for (auto& x : n) plain.AddChannel(make_channel("127.0.0.1:" + std::to_string(x.port)), OWNS_CHANNEL, mapper, nullptr);
+        example::EchoService_Stub s2(&plain);
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("tp");
+        cntl.request_attachment().append(std::string(999, 'q'));
+        s2.Echo(&cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_EQ(cntl.response_attachment().size(), 0u);
+    }
     // slice boundaries: near-equal, contiguous, covering everything
     ScatterAttachmentMapper m;
     Buf whole;
