@@ -76,6 +76,7 @@ def main():
     p.reset_stats()
     th = threading.Thread(target=p.run_for, args=(a.seconds + 0.4,))
     c0 = cgroup_cpu_stat()
+    x0 = native.gpu.xgmi_stats()
     t0 = time.perf_counter()
     r0 = resource.getrusage(resource.RUSAGE_SELF)
     th.start()
@@ -93,6 +94,13 @@ def main():
     thr = {k: c1.get(k, 0) - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "nr_periods")}
     print("leg=%s qps=%.0f p50=%s p99=%s errors=%d samples=%d cpus_used=%.2f cgroup=%s" % (
         a.leg, st["qps"], st["p50_us"], st["p99_us"], st["error"], n, cpu, thr))
+    x1 = native.gpu.xgmi_stats()
+    subs = x1["copy_submits"] - x0["copy_submits"]
+    if subs:
+        print("copy engine per submission: queue %.1f us, launch API %.1f us, GPU+poll %.1f us, wake %.1f us; "
+              "%.2f submissions/launch" % tuple(
+                  [(x1[k] - x0[k]) / subs for k in ("copy_queue_us", "copy_api_us", "copy_gpu_us", "copy_wake_us")] +
+                  [subs / max(1, x1["copy_launches"] - x0["copy_launches"])]))
     if a.folded_out:
         with open(a.folded_out, "w") as f:
             f.write(folded)

@@ -33,6 +33,9 @@ struct Batch {
     std::atomic<int>* butex = nullptr;
     hipEvent_t ev = nullptr;
     std::atomic<int> refs{0};
+    // latency breakdown (monotonic us): first submission, launch issued,
+    // completion seen by the poller
+    int64_t t_open = 0, t_issue_begin = 0, t_issued = 0, t_done = 0;
 };
 
 struct Engine {
@@ -44,6 +47,9 @@ struct Engine {
 
 Engine g_engine[kMaxDev];
 std::atomic<int64_t> g_submits{0}, g_launches{0}, g_segments{0}, g_bytes{0};
+// sums over submissions (us): waiting for the batch to be issued, the
+// launch API calls, launch-to-completion-seen, completion-to-resumed
+std::atomic<int64_t> g_t_queue{0}, g_t_api{0}, g_t_gpu{0}, g_t_wake{0};
 
 Batch* new_batch(Engine& e) {
     if (!e.spare.empty()) {
@@ -79,6 +85,7 @@ void launch(Batch* b, int device) {
         rc = LaunchBatchedCopy(b->segs.data(), (int)n, s);
     }
     if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
+    b->t_issued = monotonic_us();
     if (prev != device) hipSetDevice(prev);
     g_launches.fetch_add(1, std::memory_order_relaxed);
     if (rc != 0) {
@@ -87,7 +94,7 @@ void launch(Batch* b, int device) {
         fiber::butex_wake_all(b->butex);
         return;
     }
-    WatchEvent(b->ev, b->butex);
+    WatchEvent(b->ev, b->butex, &b->t_done);
 }
 
 }  // namespace
@@ -109,6 +116,7 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
         if (!e.open) {
             e.open = new_batch(e);
             e.open->butex->store(0, std::memory_order_relaxed);
+            e.open->t_open = monotonic_us();
         }
         mine = e.open;
         first = mine->segs.size();
@@ -138,11 +146,20 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
             for (const Segment& s : cur->segs) bytes += s.len;
             g_segments.fetch_add((int64_t)cur->segs.size(), std::memory_order_relaxed);
             g_bytes.fetch_add((int64_t)bytes, std::memory_order_relaxed);
+            cur->t_issue_begin = monotonic_us();
             launch(cur, device);
         }
     }
+    const int64_t t_submit = monotonic_us();
     while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
     const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
+    if (rc == 0 && mine->t_done) {
+        const int64_t now = monotonic_us();
+        g_t_queue.fetch_add(std::max<int64_t>(0, mine->t_issue_begin - t_submit), std::memory_order_relaxed);
+        g_t_api.fetch_add(std::max<int64_t>(0, mine->t_issued - mine->t_issue_begin), std::memory_order_relaxed);
+        g_t_gpu.fetch_add(std::max<int64_t>(0, mine->t_done - mine->t_issued), std::memory_order_relaxed);
+        g_t_wake.fetch_add(std::max<int64_t>(0, now - mine->t_done), std::memory_order_relaxed);
+    }
     if (rc == 0 && crcs) memcpy(crcs, mine->crc_host + first, sizeof(uint32_t) * (size_t)n);
     if (span) {
         uint64_t bytes = 0;
@@ -154,6 +171,7 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
     if (mine->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
         ReleaseEvent(mine->ev);
         mine->ev = nullptr;
+        mine->t_done = 0;
         mine->segs.clear();
         mine->want_crc = false;
         std::lock_guard<std::mutex> g(e.mu);
@@ -168,6 +186,10 @@ CopyEngineStats GetCopyEngineStats() {
     s.launches = g_launches.load(std::memory_order_relaxed);
     s.segments = g_segments.load(std::memory_order_relaxed);
     s.bytes = g_bytes.load(std::memory_order_relaxed);
+    s.queue_us = g_t_queue.load(std::memory_order_relaxed);
+    s.api_us = g_t_api.load(std::memory_order_relaxed);
+    s.gpu_us = g_t_gpu.load(std::memory_order_relaxed);
+    s.wake_us = g_t_wake.load(std::memory_order_relaxed);
     return s;
 }
 

@@ -31,6 +31,9 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs = nullptr
 
 struct CopyEngineStats {
     int64_t submits = 0, launches = 0, segments = 0, bytes = 0;
+    // summed over submissions (us): until the batch's launch began, the
+    // launch API calls, launch-to-completion-seen, completion-to-resumed
+    int64_t queue_us = 0, api_us = 0, gpu_us = 0, wake_us = 0;
 };
 CopyEngineStats GetCopyEngineStats();
 

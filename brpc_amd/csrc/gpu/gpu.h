@@ -85,7 +85,8 @@ int SyncStream(hipStream_t s);
 // Hand `ev` to the completion poller: when it completes the poller stores 1
 // (or -1 on failure) into *butex and wakes every waiter parked on it. One
 // event can release a whole batch of fibers.
-void WatchEvent(hipEvent_t ev, std::atomic<int>* butex);
+// `done_us` (optional) receives the monotonic time the poller saw it done.
+void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us = nullptr);
 // Pooled events (hipEventDisableTiming).
 hipEvent_t AcquireEvent();
 void ReleaseEvent(hipEvent_t e);

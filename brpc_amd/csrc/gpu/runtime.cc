@@ -72,6 +72,7 @@ void put_event(hipEvent_t e) {
 struct Waiter {
     hipEvent_t ev;
     std::atomic<int>* butex;
+    int64_t* done_us;  // optional: when the poller saw the event complete
 };
 
 class EventPoller {
@@ -143,6 +144,7 @@ private:
                     active[keep++] = active[i];
                     continue;
                 }
+                if (active[i].done_us) *active[i].done_us = now_us();
                 active[i].butex->store(r == hipSuccess ? 1 : -1, std::memory_order_release);
                 fiber::butex_wake_all(active[i].butex);
                 _polled.fetch_add(1, std::memory_order_relaxed);
@@ -296,7 +298,9 @@ int WaitEvent(hipEvent_t ev) {
     return v == 1 ? 0 : -1;
 }
 
-void WatchEvent(hipEvent_t ev, std::atomic<int>* butex) { poller()->add(Waiter{ev, butex}); }
+void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us) {
+    poller()->add(Waiter{ev, butex, done_us});
+}
 
 hipEvent_t AcquireEvent() { return get_event(); }
 void ReleaseEvent(hipEvent_t e) {

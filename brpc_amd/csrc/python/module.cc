@@ -465,6 +465,10 @@ PYBIND11_MODULE(_native, m) {
         d["copy_launches"] = c.launches;
         d["copy_segments"] = c.segments;
         d["copy_bytes"] = c.bytes;
+        d["copy_queue_us"] = c.queue_us;
+        d["copy_api_us"] = c.api_us;
+        d["copy_gpu_us"] = c.gpu_us;
+        d["copy_wake_us"] = c.wake_us;
         return d;
     });
     g.def("reap_lent", [] { gpu::ReapLentBlocks(); });
