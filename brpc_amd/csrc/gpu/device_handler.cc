@@ -1,12 +1,14 @@
 #include "gpu/device_handler.h"
 
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "base/crc32c.h"
 #include "gpu/copy_engine.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
+#include "fiber/fiber.h"
 
 namespace mrpc {
 namespace gpu {
@@ -48,6 +50,38 @@ int ProcessToPinnedWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
     }
     out->append_user_data(h, n, pinned_deleter, reinterpret_cast<void*>((uintptr_t)n), MemKind::PINNED);
     return 0;
+}
+
+namespace {
+
+struct AsyncJob {
+    Buf in;
+    bool to_device = false;
+    int device = -1;
+    std::function<void(int, Buf, uint32_t)> done;
+};
+
+void* run_async_job(void* arg) {
+    std::unique_ptr<AsyncJob> j(static_cast<AsyncJob*>(arg));
+    Buf out;
+    uint32_t crc = 0;
+    const int rc = j->to_device ? GatherToDeviceWithCrc(j->in, &out, &crc, j->device)
+                                : ProcessToPinnedWithCrc(j->in, &out, &crc, j->device);
+    j->in.clear();
+    j->done(rc, std::move(out), crc);
+    return nullptr;
+}
+
+}  // namespace
+
+void ProcessWithCrcAsync(Buf in, bool to_device, int device, std::function<void(int, Buf, uint32_t)> done) {
+    AsyncJob* j = new AsyncJob;
+    j->in = std::move(in);
+    j->to_device = to_device;
+    j->device = device;
+    j->done = std::move(done);
+    fiber::fiber_t tid;
+    if (fiber::start_background(&tid, &fiber::ATTR_NORMAL, run_async_job, j) != 0) run_async_job(j);
 }
 
 namespace {

@@ -9,6 +9,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 
 #include "base/buf.h"
 
@@ -27,6 +28,17 @@ int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device);
 // its response goes back over TCP, where an HBM copy would only have to be
 // staged out again (a second device round trip per request).
 int ProcessToPinnedWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device);
+
+// Asynchronous form of both (to_device selects GatherToDeviceWithCrc):
+// returns at once and runs done(rc, out, crc) in a fiber when the kernel
+// finished. A handler that uses it never parks the fiber that called it —
+// usually the connection's reader, which the input messenger runs the last
+// request of a read in (reference: input_messenger.cpp:169-190) — so the
+// next requests of the connection are read and submitted while the device
+// works (the GPU round trips of pipelined requests overlap instead of
+// queueing behind each other).
+void ProcessWithCrcAsync(Buf in, bool to_device, int device,
+                         std::function<void(int rc, Buf out, uint32_t crc)> done);
 
 // Copy every device block of `in` into pinned host memory (one batched
 // launch); host blocks are shared. Installed as the staging hook of

@@ -192,24 +192,31 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
         // client is on a device transport (lent over xGMI), else pinned
         // host memory the socket sends from — one device round trip per
         // batch of requests instead of a gather plus a stage-out.
-        uint32_t crc = 0;
-        Buf out;
         bool device_peer = false;
         {
             SocketUniquePtr sock;
             device_peer = Socket::Address(cntl->_server_socket_id, &sock) == 0 && HasDeviceTransport(sock.get());
         }
-        const int rc = device_peer
-                           ? gpu::GatherToDeviceWithCrc(cntl->request_attachment(), &out, &crc, _gpu_device)
-                           : gpu::ProcessToPinnedWithCrc(cntl->request_attachment(), &out, &crc, _gpu_device);
-        if (rc != 0) {
-            cntl->SetFailed(EINTERNAL, "device processing of %zu bytes failed", cntl->request_attachment().size());
-            return;
-        }
-        _gpu_calls.fetch_add(1, std::memory_order_relaxed);
-        response->set_device(_gpu_device);
-        response->set_crc32c(crc);
-        cntl->response_attachment().append(std::move(out));
+        // asynchronous: the response is sent from the completion, so this
+        // fiber (the connection's reader) goes back to reading at once
+        Buf in;
+        in.swap(cntl->request_attachment());
+        const size_t nbytes = in.size();
+        const int dev = _gpu_device;
+        std::atomic<int64_t>* calls = &_gpu_calls;
+        Closure* d = done_guard.release();
+        gpu::ProcessWithCrcAsync(std::move(in), device_peer, dev,
+                                 [cntl, response, d, dev, nbytes, calls](int rc, Buf out, uint32_t crc) {
+                                     ClosureGuard g(d);
+                                     if (rc != 0) {
+                                         cntl->SetFailed(EINTERNAL, "device processing of %zu bytes failed", nbytes);
+                                         return;
+                                     }
+                                     calls->fetch_add(1, std::memory_order_relaxed);
+                                     response->set_device(dev);
+                                     response->set_crc32c(crc);
+                                     cntl->response_attachment().append(std::move(out));
+                                 });
         return;
     }
     // zero-copy echo of the attachment (host or device blocks alike)
