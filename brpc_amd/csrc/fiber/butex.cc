@@ -105,28 +105,35 @@ int butex_wake(std::atomic<int>* v, bool nosignal) {
 
 static int wake_list(LinkNode* head, bool nosignal) {
     int n = 0;
-    std::vector<ButexWaiter*> fibers;
+    // most wake-ups release a handful of fibers: no heap allocation for those
+    ButexWaiter* inline_fibers[16];
+    std::vector<ButexWaiter*> more;
+    size_t nf = 0;
     while (!head->empty()) {
         ButexWaiter* w = static_cast<ButexWaiter*>(head->next);
         w->remove();
         ++n;
         if (w->tid == 0) {
             wakeup_pthread(static_cast<PthreadWaiter*>(w));
+        } else if (nf < 16) {
+            inline_fibers[nf++] = w;
         } else {
-            fibers.push_back(w);
+            more.push_back(w);
         }
     }
-    if (!fibers.empty()) {
+    const size_t total = nf + more.size();
+    if (total) {
         TaskGroup* g = tls_group();
-        for (size_t i = 0; i < fibers.size(); ++i) {
-            bool last = (i + 1 == fibers.size());
+        for (size_t i = 0; i < total; ++i) {
+            ButexWaiter* w = i < nf ? inline_fibers[i] : more[i - nf];
+            const bool last = (i + 1 == total);
             if (g) {
-                g->ready_to_run(fibers[i]->tid, nosignal || !last);
+                g->ready_to_run(w->tid, nosignal || !last);
             } else {
-                ready_to_run_general(fibers[i]->tid, nosignal || !last);
+                ready_to_run_general(w->tid, nosignal || !last);
             }
         }
-        if (!g && !nosignal) flush();
+        if (!g && !nosignal && total > 1) flush();  // several fibers: wake more than one worker
     }
     return n;
 }

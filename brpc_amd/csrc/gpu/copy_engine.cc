@@ -8,6 +8,7 @@
 #include <mutex>
 #include <vector>
 
+#include "base/crc32c.h"
 #include "base/logging.h"
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
@@ -27,6 +28,8 @@ const int kMaxDev = 16;
 // `butex`; the poller sets it to 1 (or -1) when the batch's event fires.
 struct Batch {
     std::vector<Segment> segs;
+    std::vector<int> msg_of;        // CRC message of each segment (want_crc)
+    int nmsg = 0;
     bool want_crc = false;          // some submitter asked for checksums
     uint32_t* crc_host = nullptr;   // per-segment CRC32C, stored by the kernel (pinned)
     size_t crc_cap = 0;
@@ -75,12 +78,15 @@ void launch(Batch* b, int device) {
     if (rc == 0 && b->want_crc) {
         // fused pull + checksum: the kernel stores the CRCs straight into
         // pinned host memory (one launch, no memset, no D2H copy)
-        if (b->crc_cap < n) {
+        if (b->crc_cap < (size_t)b->nmsg) {
             PinnedFree(b->crc_host, b->crc_cap * sizeof(uint32_t));
-            b->crc_cap = std::max<size_t>(n, 64);
+            b->crc_cap = std::max<size_t>((size_t)b->nmsg, 64);
             b->crc_host = static_cast<uint32_t*>(PinnedAlloc(b->crc_cap * sizeof(uint32_t)));
         }
-        if (!b->crc_host || LaunchBatchedCopyCrc32c(b->segs.data(), (int)n, b->crc_host, s) != 0) rc = -1;
+        if (!b->crc_host ||
+            LaunchBatchedCopyCrc32cMessages(b->segs.data(), b->msg_of.data(), (int)n, b->crc_host, s) != 0) {
+            rc = -1;
+        }
     } else if (rc == 0) {
         rc = LaunchBatchedCopy(b->segs.data(), (int)n, s);
     }
@@ -99,7 +105,7 @@ void launch(Batch* b, int device) {
 
 }  // namespace
 
-int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
+int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs, bool fold_crc) {
     if (n <= 0) return 0;
     if (device < 0) device = CurrentDevice();
     if (device < 0 || device >= kMaxDev || Init(device) != 0) return -1;
@@ -110,6 +116,8 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
     const int64_t t0 = span ? monotonic_us() : 0;
     Batch* mine;
     size_t first = 0;  // index of our first segment in the batch
+    int first_msg = 0; // ... and of our first CRC message
+    bool fold = false;
     bool leader = false;
     {
         std::lock_guard<std::mutex> g(e.mu);
@@ -121,6 +129,13 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
         mine = e.open;
         first = mine->segs.size();
         mine->segs.insert(mine->segs.end(), segs, segs + n);
+        // CRC messages: the whole submission as one (folded on the device)
+        // or one per segment. Segments of copy-only submissions get their
+        // own messages too (their CRC is computed but unused).
+        first_msg = mine->nmsg;
+        fold = fold_crc && n <= kInlineSegments;
+        for (int i = 0; i < n; ++i) mine->msg_of.push_back(fold ? mine->nmsg : mine->nmsg + i);
+        mine->nmsg += fold ? 1 : n;
         if (crcs) mine->want_crc = true;
         mine->refs.fetch_add(1, std::memory_order_relaxed);
         if (!e.launching) {
@@ -160,7 +175,18 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
         g_t_gpu.fetch_add(std::max<int64_t>(0, mine->t_done - mine->t_issued), std::memory_order_relaxed);
         g_t_wake.fetch_add(std::max<int64_t>(0, now - mine->t_done), std::memory_order_relaxed);
     }
-    if (rc == 0 && crcs) memcpy(crcs, mine->crc_host + first, sizeof(uint32_t) * (size_t)n);
+    if (rc == 0 && crcs) {
+        if (fold) {
+            crcs[0] = mine->crc_host[first_msg];
+        } else {
+            memcpy(crcs, mine->crc_host + first_msg, sizeof(uint32_t) * (size_t)n);
+            if (fold_crc) {  // too many segments to fold on the device
+                uint32_t c = crcs[0];
+                for (int i = 1; i < n; ++i) c = crc32c::Combine(c, crcs[i], segs[i].len);
+                crcs[0] = c;
+            }
+        }
+    }
     if (span) {
         uint64_t bytes = 0;
         for (int i = 0; i < n; ++i) bytes += segs[i].len;
@@ -173,6 +199,8 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs) {
         mine->ev = nullptr;
         mine->t_done = 0;
         mine->segs.clear();
+        mine->msg_of.clear();
+        mine->nmsg = 0;
         mine->want_crc = false;
         std::lock_guard<std::mutex> g(e.mu);
         e.spare.push_back(mine);

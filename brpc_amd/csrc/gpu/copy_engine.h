@@ -27,7 +27,9 @@ namespace gpu {
 // parks, pthread blocks). 0 on success. With `crcs`, the batch runs the
 // fused copy+CRC32C kernel and crcs[i] receives the standard CRC32C of
 // segment i (computed from the bytes while they are moved).
-int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs = nullptr);
+// With fold_crc, crcs[0] instead receives the CRC32C of all n segments
+// concatenated (one message), folded on the device.
+int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs = nullptr, bool fold_crc = false);
 
 struct CopyEngineStats {
     int64_t submits = 0, launches = 0, segments = 0, bytes = 0;

@@ -117,13 +117,12 @@ int copy_with_crc(const Buf& in, char* d, uint32_t* crc, int device) {
         lens.push_back(r.length);
         off += r.length;
     }
+    // one message: the device folds the segment CRCs into the request's
     std::vector<uint32_t> crcs(segs.size());
-    const int rc = BatchedCopy(segs.data(), (int)segs.size(), device, crcs.data());
+    const int rc = BatchedCopy(segs.data(), (int)segs.size(), device, crcs.data(), /*fold_crc=*/true);
     if (bounce) PinnedFree(bounce, pageable);
     if (rc != 0) return -1;
-    uint32_t c = crcs[0];
-    for (size_t i = 1; i < crcs.size(); ++i) c = crc32c::Combine(c, crcs[i], lens[i]);
-    *crc = c;
+    *crc = crcs[0];
     (void)n;
     return 0;
 }

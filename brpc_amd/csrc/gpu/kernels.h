@@ -43,6 +43,12 @@ int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s);
 // One launch per 32 segments and nothing else: no memset of `out`, which
 // may be pinned host memory read after the stream's event.
 int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s);
+// Same copy, but consecutive segments with equal msg_of[] (non-decreasing,
+// starting anywhere) form a MESSAGE and out[msg_of[i]] receives the CRC32C
+// of the message's bytes (its segments concatenated), folded on the device.
+// A message may have at most kInlineSegments segments (else -2, nothing
+// launched for it).
+int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s);
 
 // Packed-varint decode (protobuf wire type 0, packed repeated field):
 // `in` holds n bytes of concatenated varints; out receives the values

@@ -76,6 +76,14 @@ struct SegBatch {
     void* dst[kInlineSegments];
     uint64_t len[kInlineSegments];
     uint32_t chunk_start[kInlineSegments + 1];  // exclusive prefix of chunk counts
+    // CRC kernels: consecutive segments may form one MESSAGE whose CRC32C is
+    // folded on the device (the concatenation of its segments), so the host
+    // never combines per-segment CRCs
+    uint64_t tail[kInlineSegments];       // bytes after the segment inside its message
+    uint64_t msg_len[kInlineSegments];    // by message slot
+    uint32_t msg_chunks[kInlineSegments]; // by message slot: chunks of all its segments
+    uint8_t msg[kInlineSegments];         // message slot of the segment
+    uint8_t first_of_msg[kInlineSegments];
 };
 
 __device__ __forceinline__ int find_segment(const SegBatch& b, uint32_t chunk) {
@@ -115,6 +123,22 @@ __device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch,
         atomicExch(scnt + seg, 0u);
         out[seg] = atomicExch(sacc + seg, 0u);
     }
+}
+
+// One chunk's raw CRC: shift it by the bytes that follow the chunk inside its
+// MESSAGE (the rest of its segment plus the segments after it), add the ~0
+// init / final inversion once per message (std = raw0(M) ^ shift(~0,
+// len(M)) ^ ~0), and fold it into the message's slot.
+__device__ __forceinline__ void fold_chunk(const SegBatch& b, int seg, uint32_t after, uint32_t seg_chunks,
+                                           uint32_t acc, uint32_t* __restrict__ scratch,
+                                           uint32_t* __restrict__ out) {
+    const uint64_t shift = (uint64_t)after * kChunkBytes + b.tail[seg];
+    if (shift) acc = mult_mod_p(shift_bytes_poly(shift), acc);
+    const int m = b.msg[seg];
+    if (after == seg_chunks - 1 && b.first_of_msg[seg]) {
+        acc ^= mult_mod_p(shift_bytes_poly(b.msg_len[m]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+    }
+    fold_segment_crc(scratch, m, b.msg_chunks[m], acc, out);
 }
 
 __global__ void __launch_bounds__(kThreads) crc32c_kernel(SegBatch b, const uint32_t* __restrict__ tables,
@@ -168,13 +192,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_kernel(SegBatch b, const uint
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
-        if (after) acc = mult_mod_p(shift_bytes_poly((uint64_t)after * kChunkBytes), acc);
-        if (after == seg_chunks - 1) {
-            // first chunk also folds the ~0 init and final inversion:
-            // std = raw0(M) ^ shift(~0, len) ^ ~0
-            acc ^= mult_mod_p(shift_bytes_poly(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
-        }
-        fold_segment_crc(scratch, seg, seg_chunks, acc, out);
+        fold_chunk(b, seg, after, seg_chunks, acc, scratch, out);
     }
 }
 
@@ -278,9 +296,7 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
-        if (after) acc = mult_mod_p(shift_bytes_poly((uint64_t)after * kChunkBytes), acc);
-        if (after == seg_chunks - 1) acc ^= mult_mod_p(shift_bytes_poly(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
-        fold_segment_crc(scratch, seg, seg_chunks, acc, out);
+        fold_chunk(b, seg, after, seg_chunks, acc, scratch, out);
     }
 }
 
@@ -847,10 +863,13 @@ uint32_t* stream_scratch(int dev, hipStream_t s) {
 }
 
 // Fill a SegBatch with up to kInlineSegments segments; returns chunk count.
-uint32_t fill_batch(SegBatch* b, const Segment* segs, int n) {
+// msg_of (optional, non-decreasing): the message each segment belongs to;
+// without it every segment is its own message.
+uint32_t fill_batch(SegBatch* b, const Segment* segs, int n, const int* msg_of = nullptr) {
     memset(b, 0, sizeof(*b));
     b->nseg = n;
     uint32_t c = 0;
+    const int m0 = msg_of ? msg_of[0] : 0;
     for (int i = 0; i < n; ++i) {
         b->src[i] = segs[i].src;
         b->dst[i] = segs[i].dst;
@@ -859,9 +878,36 @@ uint32_t fill_batch(SegBatch* b, const Segment* segs, int n) {
         uint64_t nc = (segs[i].len + kChunkBytes - 1) / kChunkBytes;
         if (nc == 0) nc = 1;  // empty segment still gets a workgroup (writes crc 0)
         c += (uint32_t)nc;
+        const int m = msg_of ? msg_of[i] - m0 : i;
+        b->msg[i] = (uint8_t)m;
+        b->first_of_msg[i] = (uint8_t)(i == 0 || (msg_of ? msg_of[i] != msg_of[i - 1] : true));
+        b->msg_len[m] += segs[i].len;
+        b->msg_chunks[m] += (uint32_t)nc;
     }
     b->chunk_start[n] = c;
+    // bytes after each segment inside its message
+    uint64_t after = 0;
+    for (int i = n - 1; i >= 0; --i) {
+        if (i == n - 1 || b->msg[i] != b->msg[i + 1]) after = 0;
+        b->tail[i] = after;
+        after += segs[i].len;
+    }
     return c;
+}
+
+// Split [0, nseg) into launch groups of <= kInlineSegments segments that
+// never split a message. Returns false when one message alone is larger.
+bool next_group(const int* msg_of, int nseg, int begin, int* end) {
+    int e = begin;
+    while (e < nseg) {
+        int me = e;  // the message starting at e ends at me
+        while (me < nseg && msg_of[me] == msg_of[e]) ++me;
+        if (me - begin > kInlineSegments) break;
+        e = me;
+    }
+    if (e == begin) return false;
+    *end = e;
+    return true;
 }
 
 }  // namespace
@@ -920,6 +966,24 @@ int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStr
         const uint32_t chunks = fill_batch(&b, segs + i, n);
         hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch,
                            out + i);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    return 0;
+}
+
+int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s) {
+    if (nseg <= 0) return 0;
+    if (ensure_tables() != 0) return -1;
+    int dev = 0;
+    hipGetDevice(&dev);
+    uint32_t* scratch = stream_scratch(dev, s);
+    if (!scratch) return -1;
+    for (int i = 0, e = 0; i < nseg; i = e) {
+        if (!next_group(msg_of, nseg, i, &e)) return -2;
+        SegBatch b;
+        const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of + i);
+        hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch,
+                           out + msg_of[i]);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;

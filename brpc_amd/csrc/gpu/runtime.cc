@@ -146,9 +146,12 @@ private:
                 }
                 if (active[i].done_us) *active[i].done_us = now_us();
                 active[i].butex->store(r == hipSuccess ? 1 : -1, std::memory_order_release);
-                fiber::butex_wake_all(active[i].butex);
+                // queue the woken fibers without signalling; one signal for
+                // the whole pass below (fewer futex wake-ups of idle workers)
+                fiber::butex_wake_all(active[i].butex, /*nosignal=*/true);
                 _polled.fetch_add(1, std::memory_order_relaxed);
             }
+            if (keep != before) fiber::flush();
             active.resize(keep);
             if (keep != before) progressed = true;
             if (!active.empty()) {
