@@ -102,26 +102,31 @@ __device__ __forceinline__ uint32_t crc_word8(uint32_t crc, uint32_t lo, uint32_
            t[3][hi & 0xff] ^ t[2][(hi >> 8) & 0xff] ^ t[1][(hi >> 16) & 0xff] ^ t[0][hi >> 24];
 }
 
-// Per-launch-group fold of the chunk CRCs of each segment, with no
-// zero-initialised output (so no memset launch per batch): chunks XOR into
-// a per-stream accumulator slot, count themselves in, and the LAST chunk of
-// a segment takes the accumulator (resetting it for the next launch on the
-// stream) and stores the CRC straight into `out` — device memory, or
-// pinned host memory the CPU reads after the batch's event (no D2H copy).
-__device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch, int seg, uint32_t seg_chunks,
+// Per-launch-group fold of the chunk CRCs of each message, with no
+// zero-initialised output (so no memset launch per batch): every chunk
+// folds into its message's 64-bit slot of a per-stream scratch with ONE
+// compare-and-swap that both XORs its CRC into the low half and counts it
+// in the high half, so the chunk that completes the count holds the final
+// CRC in its own CAS result — no fences, no second read. It resets the slot
+// for the next launch on the stream and stores the CRC straight into `out`
+// (device memory, or pinned host memory the CPU reads after the batch's
+// event: no D2H copy).
+__device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch, int m, uint32_t chunks,
                                                  uint32_t acc, uint32_t* __restrict__ out) {
-    uint32_t* sacc = scratch;                    // [kInlineSegments]
-    uint32_t* scnt = scratch + kInlineSegments;  // [kInlineSegments]
-    if (seg_chunks == 1) {
-        out[seg] = acc;
+    if (chunks == 1) {
+        out[m] = acc;
         return;
     }
-    atomicXor(sacc + seg, acc);
-    __threadfence();
-    if (atomicAdd(scnt + seg, 1u) == seg_chunks - 1) {
-        __threadfence();
-        atomicExch(scnt + seg, 0u);
-        out[seg] = atomicExch(sacc + seg, 0u);
+    unsigned long long* slot = reinterpret_cast<unsigned long long*>(scratch) + m;
+    unsigned long long old = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), assumed, nv;
+    do {
+        assumed = old;
+        nv = (((assumed >> 32) + 1ull) << 32) | (unsigned long long)((uint32_t)assumed ^ acc);
+        old = atomicCAS(slot, assumed, nv);
+    } while (old != assumed);
+    if ((uint32_t)(nv >> 32) == chunks) {
+        atomicExch(slot, 0ull);
+        out[m] = (uint32_t)nv;
     }
 }
 
