@@ -36,6 +36,8 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
 // `out` needs no initialisation and may be pinned host memory (the kernel
 // stores each finished CRC; read it after the stream's event).
 int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s);
+// One wave that sleeps `us` microseconds of GPU wall clock (capped at 10 s).
+int LaunchSleepKernel(uint64_t us, hipStream_t s);
 // Copy every segment src -> dst (one launch for many small copies).
 int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s);
 // Fused: copy every segment AND write its standard CRC32C to out[i]

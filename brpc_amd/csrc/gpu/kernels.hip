@@ -994,6 +994,24 @@ int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int 
     return 0;
 }
 
+// A kernel that just takes time: one wave sleeps until the GPU's constant
+// wall clock has advanced by `ticks` (bounded: it always exits). Used to
+// show that fibers waiting on a long kernel park instead of holding a
+// worker pthread.
+__global__ void sleep_kernel(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+int LaunchSleepKernel(uint64_t us, hipStream_t s) {
+    int dev = 0, khz = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    if (us > 10000000) us = 10000000;  // never more than 10 s
+    hipLaunchKernelGGL(sleep_kernel, dim3(1), dim3(64), 0, s, (uint64_t)khz * us / 1000);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s) {
     for (int i = 0; i < nseg; i += kInlineSegments) {
         const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;

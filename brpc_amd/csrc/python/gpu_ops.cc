@@ -9,6 +9,8 @@
 
 #include <vector>
 
+#include "base/time.h"
+#include "fiber/fiber.h"
 #include "gpu/gpu.h"
 #include "gpu/kernels.h"
 
@@ -21,7 +23,68 @@ static void check(int rc, const char* what) {
     if (rc != 0) throw std::runtime_error(std::string(what) + " failed: " + hipGetErrorString(hipGetLastError()));
 }
 
+namespace {
+struct ParkedWaiters {
+    std::vector<fiber::fiber_t> tids;
+    std::vector<int64_t> waited_us;
+    std::vector<int> rcs;
+    int device = 0;
+    uint64_t us = 0;
+};
+struct ParkArg {
+    ParkedWaiters* p;
+    size_t i;
+};
+void* park_on_kernel(void* arg) {
+    ParkArg* a = static_cast<ParkArg*>(arg);
+    ParkedWaiters* p = a->p;
+    const size_t i = a->i;
+    delete a;
+    hipSetDevice(p->device);
+    hipStream_t s = gpu::PoolStream(p->device);
+    hipEvent_t ev = gpu::AcquireEvent();
+    const int64_t t0 = monotonic_us();
+    int rc = -1;
+    if (s && ev && gpu::LaunchSleepKernel(p->us, s) == 0 && hipEventRecord(ev, s) == hipSuccess) {
+        rc = gpu::WaitEvent(ev);  // parks this fiber, never the worker
+    }
+    p->waited_us[i] = monotonic_us() - t0;
+    p->rcs[i] = rc;
+    if (ev) gpu::ReleaseEvent(ev);
+    return nullptr;
+}
+}  // namespace
+
 void bind_gpu_ops(py::module_& g) {
+    // n fibers each launch a kernel that runs `us` microseconds and wait for
+    // its event; returns a handle for park_join (tests of the fiber-aware
+    // GPU wait: RPCs must keep flowing on the same workers meanwhile)
+    g.def("park_start", [](int n, uint64_t us, int device) {
+        ParkedWaiters* p = new ParkedWaiters;
+        p->device = device;
+        p->us = us;
+        p->tids.resize(n);
+        p->waited_us.assign(n, 0);
+        p->rcs.assign(n, -1);
+        for (int i = 0; i < n; ++i) {
+            if (fiber::start_background(&p->tids[i], &fiber::ATTR_NORMAL, park_on_kernel, new ParkArg{p, (size_t)i}) != 0) {
+                throw std::runtime_error("fiber start failed");
+            }
+        }
+        return reinterpret_cast<uintptr_t>(p);
+    }, py::arg("n"), py::arg("us"), py::arg("device") = 0);
+    g.def("park_join", [](uintptr_t h) {
+        ParkedWaiters* p = reinterpret_cast<ParkedWaiters*>(h);
+        {
+            py::gil_scoped_release nogil;
+            for (fiber::fiber_t t : p->tids) fiber::join(t, nullptr);
+        }
+        py::list waited, rcs;
+        for (int64_t w : p->waited_us) waited.append(w);
+        for (int r : p->rcs) rcs.append(r);
+        delete p;
+        return py::make_tuple(waited, rcs);
+    });
     g.def("crc32c_lds_launch", [](const std::vector<uintptr_t>& ptrs, const std::vector<uint64_t>& lens, uintptr_t out,
                               uintptr_t stream) {
         if (ptrs.size() != lens.size()) throw std::invalid_argument("ptrs/lens size mismatch");

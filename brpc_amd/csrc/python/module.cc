@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include <sstream>
+#include <unistd.h>
 
 #include "base/crc32c.h"
 #include "builtin/cpu_profiler.h"
@@ -22,6 +23,7 @@
 #include "pb/descriptor.h"
 #include "gpu/xgmi.h"
 #include "gpu/rccl_plane.h"
+#include "rdma/rdma.h"
 #include "mrpc/proto/echo.pb.h"
 #include "base/time.h"
 #include "press/press.h"
@@ -36,6 +38,8 @@
 #include "var/variable.h"
 
 namespace py = pybind11;
+
+DECLARE_string(rdma_verbs_library);
 using namespace mrpc;
 
 void bind_gpu_ops(py::module_& m);  // gpu_ops.cc
@@ -488,6 +492,45 @@ PYBIND11_MODULE(_native, m) {
         }
         if (rc != 0) throw std::runtime_error(err);
     }, py::arg("rank"), py::arg("world"), py::arg("unique_id"), py::arg("device"));
+    // GPUDirect RDMA registration of REAL HBM (arena memory) through the HIP
+    // dmabuf export (hipMemGetHandleForAddressRange) and the ibverbs
+    // provider loaded from `verbs_library` (the stub on hosts without an HCA)
+    g.def("dmabuf_register_probe", [](const std::string& verbs_library, size_t nbytes, int dev) {
+        py::dict d;
+        std::string err;
+        if (gpu::Init(dev, &err) != 0 || gpu::InitHbmPool(dev, &err) != 0) throw std::runtime_error(err);
+        Buf hold;
+        void* p = gpu::AppendNewDeviceBlock(&hold, nbytes, dev);
+        if (!p) throw std::runtime_error("no HBM");
+        d["arena_offset"] = gpu::ArenaOffset(p, dev);
+        // the export itself: a dmabuf fd naming the HBM range
+        int fd = -1;
+        uint64_t off = 0;
+        rdma::DmabufExportFn ex = rdma::GetDmabufExportHook();
+        d["export_rc"] = ex ? ex(p, nbytes, dev, &fd, &off) : -100;
+        d["export_offset"] = off;
+        std::string kind;
+        if (fd >= 0) {
+            char link[256] = {0};
+            const std::string path = "/proc/self/fd/" + std::to_string(fd);
+            const ssize_t n = readlink(path.c_str(), link, sizeof(link) - 1);
+            if (n > 0) kind.assign(link, (size_t)n);
+            close(fd);
+        }
+        d["fd_target"] = kind;
+        // registration through the provider (ibv_reg_dmabuf_mr)
+        FLAGS_rdma_verbs_library = verbs_library;
+        std::string why;
+        std::unique_ptr<rdma::Provider> pr = rdma::CreateIbverbsProvider(&why);
+        d["provider"] = pr ? std::string(pr->name()) : "none: " + why;
+        if (pr) {
+            uint32_t lkey = 0;
+            d["register_rc"] = pr->RegisterMemory(p, nbytes, true, dev, &lkey);
+            d["lkey"] = lkey;
+            pr->DeregisterMemory(p);
+        }
+        return d;
+    }, py::arg("verbs_library"), py::arg("nbytes") = 1 << 20, py::arg("device") = 0);
     g.def("rccl_active", [] { return gpu::rccl::Active(); });
     g.def("rccl_abort_for_test", [](const std::string& why) { gpu::rccl::AbortForTest(why); });
     g.def("rccl_shutdown", [] {

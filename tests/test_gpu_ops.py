@@ -2,7 +2,11 @@
 SSE4.2, pure-python varint codec), plus the device-payload echo path."""
 import random
 
+import os
+
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -450,3 +454,39 @@ def test_crc_kernels_need_no_zeroed_output(dev):
         assert got == want, rep
         for s, d in zip(srcs, dsts):
             assert torch.equal(s, d)
+
+
+def test_fibers_park_on_long_kernels_while_rpcs_flow(dev):
+    """SURVEY §7.1 / north star: tasks yield on hipEvent without blocking a
+    pthread. 8 fibers wait on 100 ms kernels on a 2-worker runtime while 32 B
+    echo calls keep completing on those same workers."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_park_probe.py")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert j["rcs"] == [0] * 8, j
+    # every waiter really waited for its kernel...
+    assert min(j["waited_us"]) >= 80000, j
+    # ...and meanwhile the RPCs flowed on the 2 workers, none stalled
+    assert j["errors"] == 0 and j["calls"] >= 500, j
+    assert j["max_us"] < 50000, j
+
+
+def test_dmabuf_export_of_real_hbm_registers_through_verbs(dev):
+    """GPUDirect RDMA path with REAL HBM: an arena block is exported as a
+    dmabuf fd by hipMemGetHandleForAddressRange (gpu/runtime.cc
+    dmabuf_export_hook) and registered through the ibverbs provider's
+    ibv_reg_dmabuf_mr — against the stub verbs library, since this pool has
+    no HCA (the stub checks the fd and access flags, then records the
+    registration)."""
+    from brpc_amd import native
+    lib = os.path.join(ROOT, "build", "lib", "libfake_ibverbs.so")
+    d = native.gpu.dmabuf_register_probe(lib, 1 << 20, 0)
+    assert d["arena_offset"] >= 0, d            # arena (IPC-exportable) memory
+    assert d["export_rc"] == 0, d               # the real HIP export succeeded
+    assert "dmabuf" in d["fd_target"], d        # and produced a dmabuf fd
+    assert d["provider"] == "ibverbs", d
+    assert d["register_rc"] == 0 and d["lkey"] != 0, d
