@@ -100,6 +100,59 @@ void EscapeString(const std::string& s, std::string* out) {
     out->push_back('"');
 }
 
+// Shortest round-tripping decimal form of a double, laid out the way the
+// reference's rapidjson Writer does (Grisu digits + Prettify): integral
+// values keep a ".0" ("2.0"), plain decimals up to 21 integer digits,
+// "0.000ddd" down to 1e-6, exponent form otherwise ("1e22", "1.5e-7").
+// Matches the expected strings of test/brpc_protobuf_json_unittest.cpp.
+void AppendShortestDouble(double d, std::string* out) {
+    if (d == 0) {
+        *out += std::signbit(d) ? "-0.0" : "0.0";
+        return;
+    }
+    char buf[40];
+    int prec = 1;
+    for (; prec <= 17; ++prec) {
+        snprintf(buf, sizeof(buf), "%.*e", prec - 1, d);
+        if (strtod(buf, nullptr) == d) break;
+    }
+    // buf: [-]d[.ddd]e(+|-)XX
+    const char* p = buf;
+    if (*p == '-') {
+        out->push_back('-');
+        ++p;
+    }
+    std::string digits;
+    for (; *p && *p != 'e'; ++p)
+        if (*p != '.') digits.push_back(*p);
+    const int e10 = atoi(p + 1);
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+    const int length = (int)digits.size();
+    const int kk = e10 + 1;      // position of the decimal point
+    const int k = kk - length;   // zeros after the digits
+    if (k >= 0 && kk <= 21) {
+        *out += digits;
+        out->append((size_t)k, '0');
+        *out += ".0";
+    } else if (kk > 0 && kk <= 21) {
+        out->append(digits, 0, (size_t)kk);
+        out->push_back('.');
+        out->append(digits, (size_t)kk, std::string::npos);
+    } else if (kk > -6 && kk <= 0) {
+        *out += "0.";
+        out->append((size_t)(-kk), '0');
+        *out += digits;
+    } else {
+        out->push_back(digits[0]);
+        if (length > 1) {
+            out->push_back('.');
+            out->append(digits, 1, std::string::npos);
+        }
+        out->push_back('e');
+        *out += std::to_string(kk - 1);
+    }
+}
+
 void Value::write(std::string* out, bool pretty, int indent) const {
     char buf[64];
     auto nl = [&](int ind) {
@@ -116,8 +169,7 @@ void Value::write(std::string* out, bool pretty, int indent) const {
         if (std::isnan(_d) || std::isinf(_d)) {
             *out += std::isnan(_d) ? "\"NaN\"" : (_d > 0 ? "\"Infinity\"" : "\"-Infinity\"");
         } else {
-            snprintf(buf, sizeof(buf), "%.17g", _d);
-            *out += buf;
+            AppendShortestDouble(_d, out);
         }
         break;
     case STRING: EscapeString(_s, out); break;

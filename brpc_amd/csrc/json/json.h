@@ -85,6 +85,8 @@ bool Parse(const char* data, size_t n, Value* out, std::string* error = nullptr)
 bool ParseWithIndex(const char* data, size_t n, const uint32_t* index, size_t nindex, Value* out,
                     std::string* error = nullptr);
 void EscapeString(const std::string& s, std::string* out);
+// Shortest round-tripping form of d in the reference rapidjson layout ("2.0", "0.1", "1e22").
+void AppendShortestDouble(double d, std::string* out);
 
 }  // namespace json
 }  // namespace mrpc

@@ -1,7 +1,14 @@
 #include "json/json2pb.h"
 
+#include <strings.h>
+
 #include <atomic>
+#include <cctype>
+#include <cerrno>
+#include <climits>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 #include "base/util.h"
 
@@ -14,6 +21,41 @@ using pb::Message;
 using pb::Reflection;
 
 namespace {
+
+// Fields jsonified as {"key": value}: real map fields, and (like the
+// reference's IsProtobufMap, src/json2pb/protobuf_map.cpp) any repeated
+// message of exactly a string `key` and a `value` field.
+bool json_map(const FieldDescriptor* f) {
+    if (f->is_map()) return true;
+    if (!f->is_repeated() || f->cpp_type() != CppType::MESSAGE || !f->message_type) return false;
+    const pb::Descriptor* e = f->message_type;
+    return e->field_count() == 2 && e->field(0)->name == "key" && !e->field(0)->is_repeated() &&
+           e->field(0)->cpp_type() == CppType::STRING && e->field(1)->name == "value";
+}
+
+// JSON key of a field: proto names cannot hold characters like '@' or '%',
+// so such keys are spelled _Zddd_ (decimal char code) in the .proto; the
+// JSON side sees the decoded name (reference: src/json2pb/encode_decode.cpp).
+const std::string& json_key(const std::string& name, std::string* tmp) {
+    if (name.find("_Z") == std::string::npos) return name;
+    tmp->clear();
+    size_t i = 0;
+    bool changed = false;
+    while (i < name.size()) {
+        if (i + 6 <= name.size() && name[i] == '_' && name[i + 1] == 'Z' && name[i + 5] == '_' && isdigit((unsigned char)name[i + 2]) &&
+            isdigit((unsigned char)name[i + 3]) && isdigit((unsigned char)name[i + 4])) {
+            const int c = (name[i + 2] - '0') * 100 + (name[i + 3] - '0') * 10 + (name[i + 4] - '0');
+            if (c < 256) {
+                tmp->push_back((char)c);
+                i += 6;
+                changed = true;
+                continue;
+            }
+        }
+        tmp->push_back(name[i++]);
+    }
+    return changed ? *tmp : name;
+}
 
 json::Value scalar_to_json(const Message& m, const FieldDescriptor* f, int idx, const Pb2JsonOptions& opt) {
     const bool rep = idx >= 0;
@@ -60,19 +102,29 @@ bool msg_to_value(const Message& m, json::Value* out, const Pb2JsonOptions& opt,
     const pb::Descriptor* d = m.GetDescriptor();
     for (const FieldDescriptor& fd : d->fields) {
         const FieldDescriptor* f = &fd;
-        const std::string& key = opt.use_json_name ? f->json_name : f->name;
-        if (f->is_map()) {
+        std::string tmp;
+        const std::string& key = opt.use_json_name ? f->json_name : json_key(f->name, &tmp);
+        if (json_map(f)) {
             const int n = Reflection::FieldSize(m, f);
             if (n == 0 && !opt.jsonify_empty_array) continue;
             json::Value obj = json::Value::Object();
-            const FieldDescriptor* kf = f->message_type->FindFieldByNumber(1);
-            const FieldDescriptor* vf = f->message_type->FindFieldByNumber(2);
+            const FieldDescriptor* kf = f->message_type->field(0);
+            const FieldDescriptor* vf = f->message_type->field(1);
             for (int i = 0; i < n; ++i) {
                 const Message& e = Reflection::GetRepeatedMessage(m, f, i);
                 json::Value k = scalar_to_json(e, kf, -1, opt);
                 std::string ks = k.is_string() ? k.as_string() : k.ToString();
                 json::Value v;
-                if (!field_value(e, vf, -1, &v, opt, err)) return false;
+                if (vf->is_repeated()) {  // {"key": [values...]}
+                    v = json::Value::Array();
+                    for (int j = 0, nv = Reflection::FieldSize(e, vf); j < nv; ++j) {
+                        json::Value x;
+                        if (!field_value(e, vf, j, &x, opt, err)) return false;
+                        v.push_back(std::move(x));
+                    }
+                } else if (!field_value(e, vf, -1, &v, opt, err)) {
+                    return false;
+                }
                 obj.set(ks, std::move(v));
             }
             out->set(key, std::move(obj));
@@ -91,6 +143,10 @@ bool msg_to_value(const Message& m, json::Value* out, const Pb2JsonOptions& opt,
             continue;
         }
         if (!Reflection::HasField(m, f)) {
+            if (f->is_required()) {  // reference pb_to_json.cpp: a hard error
+                if (err) *err = "Missing required field: " + d->full_name + "." + f->name;
+                return false;
+            }
             if (!opt.always_print_primitive_fields || f->cpp_type() == CppType::MESSAGE) continue;
         }
         json::Value v;
@@ -100,158 +156,257 @@ bool msg_to_value(const Message& m, json::Value* out, const Pb2JsonOptions& opt,
     return true;
 }
 
-bool set_scalar(Message* m, const FieldDescriptor* f, const json::Value& v, bool rep, const Json2PbOptions& opt,
-                std::string* err) {
-    auto bad = [&](const char* what) {
-        if (err) *err = "invalid value for field `" + f->name + "': expect " + what;
-        return false;
-    };
-    // integers may arrive quoted (64-bit values from JavaScript): the whole
-    // string must be a number
-    if (v.is_string() && f->cpp_type() != CppType::STRING && f->cpp_type() != CppType::ENUM &&
-        f->cpp_type() != CppType::FLOAT && f->cpp_type() != CppType::DOUBLE) {
-        const std::string& s = v.as_string();
-        char* end = nullptr;
-        if (s.empty()) return bad("number");
-        (void)strtod(s.c_str(), &end);
-        if (*end != '\0') return bad("number");
-    }
-    switch (f->cpp_type()) {
-    case CppType::INT32: {
-        if (!v.is_number() && !v.is_string()) return bad("int32");
-        int32_t x = (int32_t)v.as_int();
-        rep ? Reflection::AddInt32(m, f, x) : Reflection::SetInt32(m, f, x);
-        return true;
-    }
-    case CppType::INT64: {
-        if (!v.is_number() && !v.is_string()) return bad("int64");
-        int64_t x = v.as_int();
-        rep ? Reflection::AddInt64(m, f, x) : Reflection::SetInt64(m, f, x);
-        return true;
-    }
-    case CppType::UINT32: {
-        if (!v.is_number() && !v.is_string()) return bad("uint32");
-        uint32_t x = (uint32_t)v.as_uint();
-        rep ? Reflection::AddUInt32(m, f, x) : Reflection::SetUInt32(m, f, x);
-        return true;
-    }
-    case CppType::UINT64: {
-        if (!v.is_number() && !v.is_string()) return bad("uint64");
-        uint64_t x = v.as_uint();
-        rep ? Reflection::AddUInt64(m, f, x) : Reflection::SetUInt64(m, f, x);
-        return true;
-    }
-    case CppType::FLOAT:
-    case CppType::DOUBLE: {
-        double x;
-        if (v.is_number()) x = v.as_double();
-        else if (v.is_string() && (v.as_string() == "NaN" || v.as_string() == "Infinity" || v.as_string() == "-Infinity"))
-            x = v.as_string() == "NaN" ? NAN : (v.as_string()[0] == '-' ? -INFINITY : INFINITY);
-        else return bad("number");
-        if (f->cpp_type() == CppType::FLOAT) rep ? Reflection::AddFloat(m, f, (float)x) : Reflection::SetFloat(m, f, (float)x);
-        else rep ? Reflection::AddDouble(m, f, x) : Reflection::SetDouble(m, f, x);
-        return true;
-    }
-    case CppType::BOOL: {
-        if (!v.is_bool() && !v.is_number()) return bad("bool");
-        rep ? Reflection::AddBool(m, f, v.as_bool()) : Reflection::SetBool(m, f, v.as_bool());
-        return true;
-    }
-    case CppType::ENUM: {
-        int x;
-        if (v.is_string()) {
-            const pb::EnumValueDescriptor* ev = f->enum_type ? f->enum_type->FindValueByName(v.as_string()) : nullptr;
-            if (!ev) return bad("enum name");
-            x = ev->number;
-        } else if (v.is_number()) {
-            x = (int)v.as_int();
-        } else {
-            return bad("enum");
-        }
-        rep ? Reflection::AddEnumValue(m, f, x) : Reflection::SetEnumValue(m, f, x);
-        return true;
-    }
-    case CppType::STRING: {
-        if (!v.is_string()) return bad("string");
-        std::string s = v.as_string();
-        if (f->type == pb::FieldType::BYTES && opt.base64_to_bytes) {
-            std::string d;
-            if (base64_decode(s, &d)) s.swap(d);
-        }
-        rep ? Reflection::AddString(m, f, s) : Reflection::SetString(m, f, s);
-        return true;
-    }
-    case CppType::MESSAGE: break;
-    }
-    return false;
-}
+// ---------------------------------------------------------------- json -> pb
+// Conversion rules and error texts follow the reference's json2pb
+// (src/json2pb/json_to_pb.cpp) so callers that log or compare them see the
+// same thing: descriptor fields are visited in declaration order; a value of
+// the wrong kind in an OPTIONAL field is reported ("Invalid value `v' for
+// optional field `pkg.Msg.f' which SHOULD be T") and skipped while the
+// conversion goes on, in a required or repeated field it fails the
+// conversion; every error is appended to *err with ", ".
+class J2P {
+public:
+    J2P(const Json2PbOptions& opt, std::string* err) : _opt(opt), _err(err) {}
 
-bool value_to_msg(const json::Value& v, Message* m, const Json2PbOptions& opt, std::string* err);
-
-bool set_field(Message* m, const FieldDescriptor* f, const json::Value& v, const Json2PbOptions& opt, std::string* err) {
-    if (v.is_null()) return true;
-    if (f->is_map()) {
+    bool message(const json::Value& v, Message* m) {
+        const pb::Descriptor* d = m->GetDescriptor();
         if (!v.is_object()) {
-            if (err) *err = "field `" + f->name + "' expects an object (map)";
+            append("The input is not a json object [" + d->name + "]");
             return false;
         }
-        const FieldDescriptor* kf = f->message_type->FindFieldByNumber(1);
-        const FieldDescriptor* vf = f->message_type->FindFieldByNumber(2);
-        for (auto& kv : v.members()) {
+        if (!_opt.allow_unknown_fields) {
+            for (const auto& kv : v.members()) {
+                if (!find_field(d, kv.first)) {
+                    append("Unknown field `" + kv.first + "' in " + d->full_name);
+                    return false;
+                }
+            }
+        }
+        for (int i = 0; i < d->field_count(); ++i) {
+            const FieldDescriptor* f = d->field(i);
+            std::string tmp;
+            const json::Value* fv = v.find(json_key(f->name, &tmp));
+            if (!fv && !f->json_name.empty() && f->json_name != f->name) fv = v.find(f->json_name);
+            if (!fv) {
+                if (f->is_required()) {
+                    append("Missing required field: " + full_name(f));
+                    return false;
+                }
+                continue;
+            }
+            if (json_map(f) && fv->is_object()) {
+                if (!map(*fv, f, m)) return false;
+            } else if (!field(*fv, f, m)) {
+                return false;
+            }
+        }
+        return true;
+    }
+
+private:
+    static const FieldDescriptor* find_field(const pb::Descriptor* d, const std::string& key) {
+        if (const FieldDescriptor* f = d->FindFieldByName(key)) return f;
+        if (const FieldDescriptor* f = d->FindFieldByJsonName(key)) return f;
+        std::string tmp;
+        for (int i = 0; i < d->field_count(); ++i) {
+            if (json_key(d->field(i)->name, &tmp) == key) return d->field(i);
+        }
+        return nullptr;
+    }
+
+    static std::string full_name(const FieldDescriptor* f) {
+        return f->containing_type ? f->containing_type->full_name + "." + f->name : f->name;
+    }
+
+    void append(const std::string& s) {
+        if (!_err) return;
+        if (!_err->empty()) *_err += ", ";
+        *_err += s;
+    }
+
+    static std::string describe(const json::Value& v) {
+        char b[64];
+        switch (v.type()) {
+        case json::Value::NUL: return "null";
+        case json::Value::BOOL: return v.as_bool() ? "true" : "false";
+        case json::Value::INT: snprintf(b, sizeof(b), "%lld", (long long)v.as_int()); return b;
+        case json::Value::UINT: snprintf(b, sizeof(b), "%llu", (unsigned long long)v.as_uint()); return b;
+        case json::Value::DOUBLE: snprintf(b, sizeof(b), "%f", v.as_double()); return b;
+        case json::Value::STRING: return "\"" + v.as_string() + "\"";
+        case json::Value::ARRAY: return "array";
+        case json::Value::OBJECT: return "object";
+        }
+        return "";
+    }
+
+    // a value of the wrong kind: soft for optional fields, fatal otherwise
+    bool invalid(const FieldDescriptor* f, const char* type, const json::Value& v) {
+        const bool optional = f->label == pb::Label::OPTIONAL;
+        append("Invalid value `" + describe(v) + "' for " + (optional ? "optional " : "") + "field `" + full_name(f) +
+               "' which SHOULD be " + type);
+        return optional;
+    }
+
+    static bool integral(const json::Value& v, int64_t lo, uint64_t hi) {
+        if (v.type() == json::Value::INT) return v.as_int() >= lo && (v.as_int() < 0 || (uint64_t)v.as_int() <= hi);
+        if (v.type() == json::Value::UINT) return v.as_uint() <= hi;
+        return false;
+    }
+
+    static bool parse_int64(const std::string& s, int64_t* out) {
+        if (s.empty()) return false;
+        char* end = nullptr;
+        errno = 0;
+        const long long x = strtoll(s.c_str(), &end, 10);
+        if (errno || *end) return false;
+        *out = x;
+        return true;
+    }
+    static bool parse_uint64(const std::string& s, uint64_t* out) {
+        if (s.empty() || s[0] == '-') return false;
+        char* end = nullptr;
+        errno = 0;
+        const unsigned long long x = strtoull(s.c_str(), &end, 10);
+        if (errno || *end) return false;
+        *out = x;
+        return true;
+    }
+
+    // one value of a scalar (non-message) field
+    bool scalar(const json::Value& v, const FieldDescriptor* f, Message* m, bool rep) {
+        switch (f->cpp_type()) {
+        case CppType::INT32:
+            if (!integral(v, INT32_MIN, (uint64_t)INT32_MAX)) return invalid(f, "INT32", v);
+            rep ? Reflection::AddInt32(m, f, (int32_t)v.as_int()) : Reflection::SetInt32(m, f, (int32_t)v.as_int());
+            return true;
+        case CppType::UINT32:
+            if (!integral(v, 0, UINT32_MAX)) return invalid(f, "UINT32", v);
+            rep ? Reflection::AddUInt32(m, f, (uint32_t)v.as_uint()) : Reflection::SetUInt32(m, f, (uint32_t)v.as_uint());
+            return true;
+        case CppType::BOOL:
+            if (!v.is_bool()) return invalid(f, "BOOL", v);
+            rep ? Reflection::AddBool(m, f, v.as_bool()) : Reflection::SetBool(m, f, v.as_bool());
+            return true;
+        case CppType::INT64: {
+            int64_t x = 0;
+            if (integral(v, INT64_MIN, (uint64_t)INT64_MAX)) x = v.as_int();
+            else if (!(v.is_string() && parse_int64(v.as_string(), &x))) return invalid(f, "INT64", v);
+            rep ? Reflection::AddInt64(m, f, x) : Reflection::SetInt64(m, f, x);
+            return true;
+        }
+        case CppType::UINT64: {
+            uint64_t x = 0;
+            if (integral(v, 0, UINT64_MAX)) x = v.as_uint();
+            else if (!(v.is_string() && parse_uint64(v.as_string(), &x))) return invalid(f, "UINT64", v);
+            rep ? Reflection::AddUInt64(m, f, x) : Reflection::SetUInt64(m, f, x);
+            return true;
+        }
+        case CppType::FLOAT:
+        case CppType::DOUBLE: {
+            const bool is_float = f->cpp_type() == CppType::FLOAT;
+            double x;
+            if (v.is_number()) {
+                x = v.as_double();
+            } else if (v.is_string()) {
+                // only the three special values travel as strings; the
+                // reference names the type by its typeid ("f" / "d") here
+                const char* t = v.as_string().c_str();
+                if (strcasecmp(t, "NaN") == 0) x = NAN;
+                else if (strcasecmp(t, "Infinity") == 0) x = INFINITY;
+                else if (strcasecmp(t, "-Infinity") == 0) x = -INFINITY;
+                else return invalid(f, is_float ? "f" : "d", v);
+            } else {
+                return invalid(f, is_float ? "float" : "double", v);
+            }
+            if (is_float) rep ? Reflection::AddFloat(m, f, (float)x) : Reflection::SetFloat(m, f, (float)x);
+            else rep ? Reflection::AddDouble(m, f, x) : Reflection::SetDouble(m, f, x);
+            return true;
+        }
+        case CppType::ENUM: {
+            const pb::EnumValueDescriptor* ev = nullptr;
+            if (f->enum_type && integral(v, INT32_MIN, (uint64_t)INT32_MAX)) {
+                ev = f->enum_type->FindValueByNumber((int)v.as_int());
+            } else if (f->enum_type && v.is_string()) {
+                ev = f->enum_type->FindValueByName(v.as_string());
+            }
+            if (!ev) return invalid(f, "enum", v);
+            rep ? Reflection::AddEnumValue(m, f, ev->number) : Reflection::SetEnumValue(m, f, ev->number);
+            return true;
+        }
+        case CppType::STRING: {
+            if (!v.is_string()) return invalid(f, "string", v);
+            std::string str = v.as_string();
+            if (f->type == pb::FieldType::BYTES && _opt.base64_to_bytes) {
+                std::string d;
+                if (!base64_decode(str, &d)) {
+                    append("Fail to decode base64 string=" + str + " [" + m->GetDescriptor()->name + "]");
+                    return false;
+                }
+                str.swap(d);
+            }
+            rep ? Reflection::AddString(m, f, str) : Reflection::SetString(m, f, str);
+            return true;
+        }
+        case CppType::MESSAGE:
+            break;
+        }
+        return false;
+    }
+
+    bool field(const json::Value& v, const FieldDescriptor* f, Message* m) {
+        if (v.is_null()) {
+            if (f->is_required()) {
+                append("Missing required field: " + full_name(f));
+                return false;
+            }
+            return true;
+        }
+        if (f->is_repeated()) {
+            if (!v.is_array()) {
+                append("Invalid value for repeated field: " + full_name(f));
+                return false;
+            }
+            for (const json::Value& e : v.array()) {
+                if (f->cpp_type() == CppType::MESSAGE) {
+                    if (!e.is_object()) {
+                        if (!invalid(f, "message", e)) return false;
+                        continue;
+                    }
+                    if (!message(e, Reflection::AddMessage(m, f))) return false;
+                } else if (!scalar(e, f, m, true)) {
+                    return false;
+                }
+            }
+            return true;
+        }
+        if (f->cpp_type() == CppType::MESSAGE) return message(v, Reflection::MutableMessage(m, f));
+        return scalar(v, f, m, false);
+    }
+
+    // {"key": value, ...} into a map field (keys converted to the key type)
+    bool map(const json::Value& v, const FieldDescriptor* f, Message* m) {
+        const FieldDescriptor* kf = f->message_type->field(0);
+        const FieldDescriptor* vf = f->message_type->field(1);
+        for (const auto& kv : v.members()) {
             Message* e = Reflection::AddMessage(m, f);
             json::Value key(kv.first);
             if (kf->cpp_type() != CppType::STRING) {
                 json::Value parsed;
                 if (json::Parse(kv.first, &parsed)) key = parsed;
             }
-            if (!set_scalar(e, kf, key, false, opt, err)) return false;
-            if (vf->cpp_type() == CppType::MESSAGE) {
-                if (!value_to_msg(kv.second, Reflection::MutableMessage(e, vf), opt, err)) return false;
-            } else if (!set_scalar(e, vf, kv.second, false, opt, err)) {
-                return false;
-            }
+            if (!scalar(key, kf, e, false)) return false;
+            if (!field(kv.second, vf, e)) return false;
         }
         return true;
     }
-    if (f->is_repeated()) {
-        if (!v.is_array()) {
-            if (err) *err = "field `" + f->name + "' expects an array";
-            return false;
-        }
-        for (const json::Value& e : v.array()) {
-            if (f->cpp_type() == CppType::MESSAGE) {
-                if (!value_to_msg(e, Reflection::AddMessage(m, f), opt, err)) return false;
-            } else if (!set_scalar(m, f, e, true, opt, err)) {
-                return false;
-            }
-        }
-        return true;
-    }
-    if (f->cpp_type() == CppType::MESSAGE) return value_to_msg(v, Reflection::MutableMessage(m, f), opt, err);
-    return set_scalar(m, f, v, false, opt, err);
-}
+
+    const Json2PbOptions& _opt;
+    std::string* _err;
+};
 
 bool value_to_msg(const json::Value& v, Message* m, const Json2PbOptions& opt, std::string* err) {
-    if (!v.is_object()) {
-        if (err) *err = "expect a json object for " + m->GetDescriptor()->full_name;
-        return false;
-    }
-    const pb::Descriptor* d = m->GetDescriptor();
-    for (auto& kv : v.members()) {
-        const FieldDescriptor* f = d->FindFieldByName(kv.first);
-        if (!f) f = d->FindFieldByJsonName(kv.first);
-        if (!f) {
-            if (opt.allow_unknown_fields) continue;
-            if (err) *err = "unknown field `" + kv.first + "' in " + d->full_name;
-            return false;
-        }
-        if (!set_field(m, f, kv.second, opt, err)) return false;
-    }
-    if (!m->IsInitialized()) {
-        if (err) *err = "missing required fields: " + m->InitializationErrorString();
-        return false;
-    }
-    return true;
+    if (err) err->clear();
+    return J2P(opt, err).message(v, m);
 }
 
 }  // namespace

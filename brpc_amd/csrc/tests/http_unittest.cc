@@ -114,18 +114,22 @@ TEST(Json2pb, roundtrip) {
     // missing required field / bad type
     test::Rich bad;
     EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"i32\": 1}", &bad, json2pb::Json2PbOptions(), &err));
-    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"x\",\"i32\":\"abc\"}", &bad, json2pb::Json2PbOptions(), &err));
+    // a wrong kind in an optional field is reported but not fatal (reference semantics)
+    test::Rich soft;
+    EXPECT_TRUE(json2pb::JsonToProtoMessage("{\"must\":\"x\",\"i32\":\"abc\"}", &soft, json2pb::Json2PbOptions(), &err));
+    EXPECT_TRUE(err.find("SHOULD be INT32") != std::string::npos);
+    EXPECT_FALSE(soft.has_i32());
     json2pb::Json2PbOptions strict;
     strict.allow_unknown_fields = false;
     EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"x\",\"nope\":1}", &bad, strict, &err));
 }
 
 TEST(Json2pb, scalar_coercions) {
-    // numbers quoted as strings (how int64 travels through javascript),
-    // enums by number, bools from numbers, NaN / Infinity, nulls skipped
+    // 64-bit numbers quoted as strings (how int64 travels through
+    // javascript), enums by number, NaN / Infinity, nulls skipped
     const std::string in =
         "{\"must\":\"m\",\"i64\":\"1099511627776\",\"u64\":\"18446744073709551615\",\"i32\":-7,"
-        "\"color\":2,\"flag\":1,\"d\":\"-Infinity\",\"s\":null,\"nums\":[1,\"2\",3]}";
+        "\"color\":2,\"flag\":true,\"d\":\"-Infinity\",\"s\":null,\"nums\":[1,2,3]}";
     test::Rich r;
     std::string err;
     ASSERT_TRUE(json2pb::JsonToProtoMessage(in, &r, json2pb::Json2PbOptions(), &err));
@@ -187,9 +191,16 @@ TEST(Json2pb, type_errors_name_the_field) {
     EXPECT_TRUE(err.find("nums") != std::string::npos);
     EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"counts\":[1]}", &r, json2pb::Json2PbOptions(), &err));
     EXPECT_TRUE(err.find("counts") != std::string::npos);
-    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"color\":\"PURPLE\"}", &r, json2pb::Json2PbOptions(), &err));
-    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"inner\":{\"x\":\"y\"}}", &r, json2pb::Json2PbOptions(), &err));
-    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"s\":7}", &r, json2pb::Json2PbOptions(), &err));
+    // optional fields of the wrong kind: reported, skipped, not fatal
+    EXPECT_TRUE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"color\":\"PURPLE\"}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_TRUE(err.find("field `mrpc.test.Rich.color' which SHOULD be enum") != std::string::npos);
+    EXPECT_TRUE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"inner\":{\"x\":\"y\"}}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_TRUE(err.find("SHOULD be INT32") != std::string::npos);
+    EXPECT_TRUE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"s\":7}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_TRUE(err.find("Invalid value `7'") != std::string::npos);
+    // ... but fatal in required and repeated fields
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":7}", &r, json2pb::Json2PbOptions(), &err));
+    EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":\"m\",\"nums\":[1,\"2\"]}", &r, json2pb::Json2PbOptions(), &err));
     EXPECT_FALSE(json2pb::JsonToProtoMessage("{\"must\":", &r, json2pb::Json2PbOptions(), &err));
     EXPECT_FALSE(err.empty());
 }

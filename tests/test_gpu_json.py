@@ -5,6 +5,7 @@ unicode, nesting), adversarial backslash/quote soups whose runs straddle
 scan carries state and offsets across LDS chunks), unaligned views and the
 error codes."""
 import json
+import os
 import random
 
 import pytest
@@ -181,3 +182,25 @@ def test_json2pb_uses_device_index_for_large_bodies(dev):
         assert native.gpu.json_stats()["failures"] == s1["failures"] + 1
     finally:
         native.gpu.disable_json_index()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.isfile("/root/reference/test/jsonout"), reason="reference fixture not present")
+def test_reference_jsonout_fixture_through_device_index(dev):
+    """The reference's 98 KB test/jsonout document (gss_us_res_t) parsed with
+    the GPU structural index gives exactly the CPU parser's message."""
+    from brpc_amd import native
+    ref = "/root/reference/test"
+    with open(os.path.join(ref, "jsonout"), "rb") as f:
+        text = f.read()
+    cpu = native.json_proto_roundtrip(ref, "message.proto", "gss.message.gss_us_res_t", text, False)
+    native.gpu.enable_json_index(0, 4096)
+    try:
+        s0 = native.gpu.json_stats()
+        gpu = native.json_proto_roundtrip(ref, "message.proto", "gss.message.gss_us_res_t", text, False)
+        s1 = native.gpu.json_stats()
+    finally:
+        native.gpu.disable_json_index()
+    assert s1["indexed_bodies"] == s0["indexed_bodies"] + 1
+    assert gpu == cpu
+    assert json.loads(gpu[0]) == json.loads(text)
