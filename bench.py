@@ -53,7 +53,7 @@ def parse():
                     help="run the RCCL payload plane on the stub library (CPU rehearsal of the multi-rank plane: "
                          "host payloads, gloo control plane)")
     ap.add_argument("--skip-1m", action="store_true", help="skip the 1 MiB payload legs (BASELINE config 5 analog)")
-    ap.add_argument("--requests-per-step-1m", type=int, default=2000, help="1 MiB requests per step and rank")
+    ap.add_argument("--requests-per-step-1m", type=int, default=10000, help="1 MiB requests per step and rank")
     ap.add_argument("--skip-sweep", action="store_true",
                     help="skip the rdma_performance-style size x queue-depth sweep (lending vs RCCL plane)")
     ap.add_argument("--sweep-seconds", type=float, default=0.4, help="timed seconds per sweep point")
@@ -75,7 +75,7 @@ def parse():
                          "event poller and the RCCL plane poster watch for work as long before sleeping.")
     ap.add_argument("--latency-first", action="store_true",
                     help="take the 100-QPS latency sample before the throughput legs")
-    ap.add_argument("--latency-sample-s", type=float, default=6.0,
+    ap.add_argument("--latency-sample-s", type=float, default=10.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
 

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Where does the time of a paced (100 QPS) 32 B echo go?
+
+Runs the bench's latency sample (one caller, 100 QPS, loopback baidu_std)
+with rpcz on, pairs every client span with its server span by trace id and
+splits each call into phases:
+
+  issue     call start -> request handed to the socket (client)
+  req_wire  request written -> request cut by the server's dispatcher
+            (kernel loopback + the server side waking up)
+  server    request cut -> response written (server)
+  resp_wire response written -> response cut on the client
+            (kernel loopback + the client side waking up)
+  queue     response cut -> response processing began (client)
+  done      processing began -> call ended
+
+  python benchmarks/latency_trace.py --seconds 10
+"""
+import argparse
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PHASES = ("issue", "req_wire", "server", "resp_wire", "queue", "done")
+
+
+def pct(v, q):
+    v = sorted(v)
+    return v[min(len(v) - 1, int(q * len(v)))] if v else 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--qps", type=float, default=100.0)
+    ap.add_argument("--workers", type=int, default=12)
+    ap.add_argument("--top", type=int, default=15)
+    a = ap.parse_args()
+    import torch
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    native.set_flag("fiber_concurrency", str(a.workers))
+    if torch.cuda.is_available():
+        from brpc_amd.parallel.placement import choose_l3_domain
+        l3, _ = choose_l3_domain(0, 1, 0, torch.cuda.device_count())
+        if l3 >= 0:
+            native.set_flag("cpu_l3_domain", str(l3))
+    native.set_flag("event_dispatcher_spin_us", os.environ.get("SPIN_US", "200"))
+    if "NAP_US" in os.environ:
+        native.set_flag("event_dispatcher_nap_us", os.environ["NAP_US"])
+    if "WORKER_NAP_US" in os.environ:
+        native.set_flag("fiber_worker_nap_us", os.environ["WORKER_NAP_US"])
+    native.set_flag("rpcz_save_to_disk", "false")
+    native.set_flag("rpcz_max_spans", "100000")
+    native.set_flag("rpcz_max_spans_per_second", "100000")
+    s = start_echo_server("127.0.0.1:0", num_threads=a.workers, gpu_device=-1)
+    p = native.Press({"server": s.address, "qps": a.qps, "concurrency": 1, "request_size": 32,
+                      "connection_type": "single"})
+    p.run_for(0.5)
+    if not os.environ.get("NO_RPCZ"):
+        native.set_flag("enable_rpcz", "true")
+    p.reset_stats()
+    p.run_for(a.seconds)
+    native.set_flag("enable_rpcz", "false")
+    st = p.stats()
+    spans = native.rpcz_recent(1000000)
+    client, server = {}, {}
+    for d in spans:
+        head = d.split("\n", 1)[0]
+        m = re.search(r"trace=([0-9a-f]+)", head)
+        if not m:
+            continue
+        kv = {k: int(v) for k, v in re.findall(r" (\w+)=\+?(-?\d+)(?:us)?(?= |$)", head)}
+        (client if head.startswith("C ") else server)[m.group(1)] = kv
+    rows = []
+    for t, c in client.items():
+        sv = server.get(t)
+        if not sv or "sent" not in c or "cut" not in c:
+            continue
+        start = c["start"]
+        srv_recv, srv_sent = sv["received"], sv["received"] + sv["sent"]
+        ph = {
+            "issue": c["sent"],
+            "req_wire": srv_recv - (start + c["sent"]),
+            "server": srv_sent - srv_recv,
+            "resp_wire": start + c["cut"] - srv_sent,
+            "queue": c["parse"] - c["cut"],
+            "done": c["latency"] - c["parse"],
+        }
+        rows.append((c["latency"], ph))
+    print("press: qps=%.0f p50=%s p99=%s p999=%s; traced calls=%d" % (st["qps"], st["p50_us"], st["p99_us"],
+                                                                     st["p999_us"], len(rows)))
+    lat = [r[0] for r in rows]
+    print("traced latency: p50=%d p90=%d p99=%d max=%d us" % (pct(lat, .5), pct(lat, .9), pct(lat, .99),
+                                                              max(lat) if lat else 0))
+    print("%-10s %6s %6s %6s %6s" % ("phase", "p50", "p90", "p99", "max"))
+    for k in PHASES:
+        v = [r[1][k] for r in rows]
+        print("%-10s %6d %6d %6d %6d" % (k, pct(v, .5), pct(v, .9), pct(v, .99), max(v) if v else 0))
+    print("slowest calls:")
+    for latency, ph in sorted(rows, key=lambda r: -r[0])[:a.top]:
+        print("  %5d us: " % latency + " ".join("%s=%d" % (k, ph[k]) for k in PHASES))
+    s.stop()
+
+
+if __name__ == "__main__":
+    main()

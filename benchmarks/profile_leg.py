@@ -55,6 +55,8 @@ def main():
         if l3 >= 0:
             native.set_flag("cpu_l3_domain", str(l3))
     native.set_flag("event_dispatcher_spin_us", os.environ.get("SPIN_US", "200"))
+    if "NAP_US" in os.environ:
+        native.set_flag("event_dispatcher_nap_us", os.environ["NAP_US"])
     native.set_flag("gpu_poller_idle_spin_us", os.environ.get("POLL_SPIN_US", os.environ.get("SPIN_US", "200")))
     topo = parallel.Topology(rank=0, world_size=1, local_rank=0, local_world_size=1, device=dev)
     if a.leg == "rccl_64k":

@@ -104,6 +104,10 @@ public:
     }
     State get_state() { return State{_pending.load(std::memory_order_acquire)}; }
     void wait(const State& expected) { futex_wait_private(&_pending, expected.val, nullptr); }
+    void wait_for(const State& expected, int64_t timeout_ns) {
+        const timespec ts{(time_t)(timeout_ns / 1000000000), (long)(timeout_ns % 1000000000)};
+        futex_wait_private(&_pending, expected.val, &ts);
+    }
     void stop() {
         _pending.fetch_or(1);
         futex_wake_private(&_pending, 10000);
@@ -240,6 +244,7 @@ private:
     uint64_t _steal_seed;
     size_t _steal_offset;
     std::atomic<int64_t> _idle_ns{0};
+    int64_t _last_task_ns = 0;  // when this worker last found a fiber (0: running one)
 };
 
 class TaskControl {

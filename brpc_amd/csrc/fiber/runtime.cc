@@ -71,6 +71,12 @@ DEFINE_int32(fiber_idle_spin_us, 0,
              "an idle worker polls for new fibers this long before sleeping on its parking lot "
              "(trades CPU for futex-wakeup latency on the RPC round trip; 0 disables)");
 DEFINE_int32(fiber_max_spinning_workers, 2, "at most this many idle workers spin at once");
+DEFINE_int32(fiber_worker_nap_us, 0,
+             "an idle worker that ran a fiber within -fiber_worker_nap_window_ms sleeps on its parking lot with "
+             "this timeout (us) and re-polls, so its core stays in shallow idle states (warm caches, us wakeups) "
+             "instead of the deep state a long sleep lets the governor pick (0 disables)");
+DEFINE_int32(fiber_nap_workers, 2, "at most this many idle workers nap at once (the rest sleep for good)");
+DEFINE_int32(fiber_worker_nap_window_ms, 1000, "how long after its last fiber a worker keeps napping");
 
 namespace mrpc {
 namespace fiber {
@@ -567,6 +573,7 @@ bool TaskGroup::steal_task(fiber_t* tid) {
 }
 
 static std::atomic<int> g_spinning_workers{0};
+static std::atomic<int> g_napping_workers{0};
 
 // Polls for work for up to -fiber_idle_spin_us. Waking a parked worker
 // costs a futex round trip plus the kernel's wakeup latency (tens of µs on
@@ -597,13 +604,37 @@ bool TaskGroup::spin_for_task(fiber_t* tid) {
 }
 
 bool TaskGroup::wait_task(fiber_t* tid) {
-    if (_rq.pop(tid)) return true;
+    if (_rq.pop(tid)) {
+        _last_task_ns = 0;
+        return true;
+    }
     for (;;) {
-        if (steal_task(tid)) return true;
+        if (steal_task(tid)) {
+            _last_task_ns = 0;
+            return true;
+        }
         if (_last_pl_state.stopped()) return false;
-        if (spin_for_task(tid)) return true;
+        if (spin_for_task(tid)) {
+            _last_task_ns = 0;
+            return true;
+        }
         int64_t t0 = monotonic_ns();
-        _pl->wait(_last_pl_state);
+        if (_last_task_ns == 0) _last_task_ns = t0;  // idle since now
+        const int nap_us = FLAGS_fiber_worker_nap_us;
+        bool nap = false;
+        if (nap_us > 0 && t0 - _last_task_ns < (int64_t)FLAGS_fiber_worker_nap_window_ms * 1000000) {
+            nap = g_napping_workers.fetch_add(1, std::memory_order_relaxed) < FLAGS_fiber_nap_workers;
+            if (!nap) g_napping_workers.fetch_sub(1, std::memory_order_relaxed);
+        }
+        if (nap) {
+            // Nap: a short timed sleep keeps this core out of the deep idle
+            // state (its caches stay warm, it answers a signal in a few us);
+            // on the timeout it polls again (benchmarks/latency_trace.py).
+            _pl->wait_for(_last_pl_state, (int64_t)nap_us * 1000);
+            g_napping_workers.fetch_sub(1, std::memory_order_relaxed);
+        } else {
+            _pl->wait(_last_pl_state);
+        }
         _idle_ns.fetch_add(monotonic_ns() - t0, std::memory_order_relaxed);
     }
 }

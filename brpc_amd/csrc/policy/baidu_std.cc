@@ -230,7 +230,8 @@ void ProcessRpcRequest(InputMessageBase* msg_base) {
     if (rm.has_timeout_ms() && rm.timeout_ms() > 0) cntl->_deadline_us = msg->received_us() + (int64_t)rm.timeout_ms() * 1000;
     if (IsRpczEnabled()) {
         cntl->_span = Span::CreateServerSpan((uint64_t)rm.trace_id(), (uint64_t)rm.span_id(), (uint64_t)rm.parent_span_id(),
-                                             rm.service_name() + "." + rm.method_name(), realtime_us());
+                                             rm.service_name() + "." + rm.method_name(),
+                                             realtime_us() - (monotonic_us() - msg->received_us()));
         if (cntl->_span) {
             cntl->_span->remote_side = socket->remote_side();
             cntl->_span->start_parse_real_us = realtime_us();
@@ -381,6 +382,11 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
         ReleaseDevicePayload(msg->socket(), meta);
         msg->Destroy();
         return;
+    }
+    if (cntl->_span) {
+        const int64_t now = realtime_us();
+        cntl->_span->start_parse_real_us = now;
+        cntl->_span->cut_real_us = now - (monotonic_us() - msg->received_us());
     }
     if (meta.has_xgmi_hello() && gpu::XgmiEnabled()) {
         std::string err;

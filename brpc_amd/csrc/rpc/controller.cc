@@ -439,6 +439,7 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
     // Errors of Write() are delivered through call_id_error(cid), which is
     // queued while we hold the lock and handled at unlock.
     sock->Write(&packet, &wopt);
+    if (_span) _span->sent_real_us = realtime_us();
     fiber::call_id_unlock(cid);
 }
 

@@ -172,7 +172,11 @@ std::string Span::Describe() const {
                        (long long)(start_callback_real_us - received_real_us),
                        (long long)(start_send_real_us - received_real_us), (long long)(sent_real_us - received_real_us));
     } else {
-        string_appendf(&out, " latency=%lldus", (long long)(received_real_us - start_send_real_us));
+        string_appendf(&out, " latency=%lldus start=%lld", (long long)(received_real_us - start_send_real_us),
+                       (long long)start_send_real_us);
+        if (sent_real_us) string_appendf(&out, " sent=+%lld", (long long)(sent_real_us - start_send_real_us));
+        if (cut_real_us) string_appendf(&out, " cut=+%lld", (long long)(cut_real_us - start_send_real_us));
+        if (start_parse_real_us) string_appendf(&out, " parse=+%lld", (long long)(start_parse_real_us - start_send_real_us));
     }
     for (auto& a : annotations) string_appendf(&out, "\n    %lld %s", (long long)a.first, a.second.c_str());
     for (const Span* c : client_spans) out += "\n  " + c->Describe();

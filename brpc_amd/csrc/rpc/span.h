@@ -44,8 +44,12 @@ public:
     int protocol = 0;
     int error_code = 0;
     int64_t request_size = 0, response_size = 0;
+    // server: received = request cut from the socket, parse, callback,
+    // send (response), sent. client: start_send = call start, sent = request
+    // handed to the socket, cut = response cut from the socket, parse =
+    // response processing began, received = call ended.
     int64_t received_real_us = 0, start_parse_real_us = 0, start_callback_real_us = 0, start_send_real_us = 0,
-            sent_real_us = 0;
+            sent_real_us = 0, cut_real_us = 0;
     std::vector<std::pair<int64_t, std::string>> annotations;
     std::vector<Span*> client_spans;
     Span* local_parent = nullptr;

@@ -76,7 +76,29 @@ def gpu_numa(device, native=None):
     return node, cpus
 
 
-def choose_l3_domain(local_rank, local_world, device, device_count=0, native=None):
+def cpu_busy(seconds=0.2):
+    """{cpu: busy fraction} over `seconds` from /proc/stat (every process on
+    the host, not just ours), or {} when unreadable."""
+    def snap():
+        d = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    v = line.split()
+                    t = list(map(int, v[1:]))
+                    d[int(v[0][3:])] = (sum(t), t[3] + t[4])  # total, idle + iowait
+        return d
+    try:
+        import time
+        a = snap()
+        time.sleep(seconds)
+        b = snap()
+    except (OSError, ValueError):
+        return {}
+    return {c: 1.0 - (b[c][1] - a[c][1]) / max(1, b[c][0] - a[c][0]) for c in a if c in b}
+
+
+def choose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.2):
     """Index (for -cpu_l3_domain) of the L3 domain this rank should use, and
     a description dict for the bench JSON. -1: leave the rank unconfined."""
     domains = l3_domains()
@@ -104,8 +126,18 @@ def choose_l3_domain(local_rank, local_world, device, device_count=0, native=Non
         if local_rank not in peers:
             peers.append(local_rank)
     slot = sorted(peers).index(local_rank)
-    step = max(1, len(cand) // max(1, len(peers)))
-    idx = cand[(slot * step) % len(cand)]
+    # ranks sharing the node own disjoint slices of its domains; in its slice
+    # a rank takes the domain the rest of the host keeps least busy (other
+    # jobs' threads preempting ours are what the tail latency is made of)
+    mine = cand[slot::len(peers)] if len(cand) >= len(peers) else [cand[slot % len(cand)]]
+    idx = mine[0]
+    if len(mine) > 1 and sample_s > 0:
+        busy = cpu_busy(sample_s)
+        if busy:
+            load = {i: sum(busy.get(c, 0.0) for c in domains[i][1]) / len(domains[i][1]) for i in mine}
+            idx = min(mine, key=lambda i: (round(load[i], 2), i))
+            info["l3_domain_busy_pct"] = round(100.0 * load[idx], 1)
+            info["l3_domain_busy_pct_max"] = round(100.0 * max(load.values()), 1)
     info["l3_domain_first_cpu"] = domains[idx][0]
     info["ranks_on_gpu_numa_node"] = len(peers)
     info["numa_local"] = bool(local) and set(domains[idx][1]) <= local
