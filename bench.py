@@ -199,6 +199,7 @@ def main():
     def transport_snapshot():
         x = native.gpu.xgmi_stats()
         r = parallel.rccl_stats()
+        hbm = native.gpu.hbm_pool_stats(topo.device) if topo.device >= 0 else {"fallback_allocs": 0, "splits": 0}
         return {"xgmi_lent_payloads": x["sent_payloads"], "xgmi_pulled_payloads": x["recv_payloads"],
                 "xgmi_cross_gpu_payloads": x["cross_device_payloads"],
                 "xgmi_cross_gpu_pull_failures": x["cross_device_pull_failures"],
@@ -206,7 +207,8 @@ def main():
                 "xgmi_attach_failures": x["attach_failures"], "xgmi_peer_access_pairs": x["peer_access_enabled"],
                 "copy_launches": x["copy_launches"],
                 "rccl_payloads": r["recv_payloads"], "rccl_rounds": r["rounds"], "rccl_aborts": r["aborts"],
-                "rccl_credit_stalls": r["credit_stalls"], "rccl_recv_timeouts": r["recv_timeouts"]}
+                "rccl_credit_stalls": r["credit_stalls"], "rccl_recv_timeouts": r["recv_timeouts"],
+                "hbm_fallback_allocs": hbm["fallback_allocs"], "hbm_block_splits": hbm["splits"]}
 
     def transport_delta(s0):
         s1 = transport_snapshot()

@@ -38,6 +38,10 @@ def main():
     ap.add_argument("--qps", type=float, default=100.0)
     ap.add_argument("--workers", type=int, default=12)
     ap.add_argument("--top", type=int, default=15)
+    ap.add_argument("--attachment", type=int, default=0, help="attachment bytes per call")
+    ap.add_argument("--device-attachment", action="store_true", help="attachment in HBM (lent over xGMI)")
+    ap.add_argument("--concurrency", type=int, default=1)
+    ap.add_argument("--dump", type=int, default=0, help="print the full spans of this many slowest calls")
     a = ap.parse_args()
     import torch
     from brpc_amd import native
@@ -56,9 +60,13 @@ def main():
     native.set_flag("rpcz_save_to_disk", "false")
     native.set_flag("rpcz_max_spans", "100000")
     native.set_flag("rpcz_max_spans_per_second", "100000")
-    s = start_echo_server("127.0.0.1:0", num_threads=a.workers, gpu_device=-1)
-    p = native.Press({"server": s.address, "qps": a.qps, "concurrency": 1, "request_size": 32,
-                      "connection_type": "single"})
+    dev = 0 if a.device_attachment else -1
+    s = start_echo_server("127.0.0.1:0", num_threads=a.workers, gpu_device=dev)
+    o = {"server": s.address, "qps": a.qps, "concurrency": a.concurrency, "request_size": 32,
+         "connection_type": "single"}
+    if a.attachment:
+        o.update({"attachment_size": a.attachment, "gpu_device": dev, "device_attachment": a.device_attachment})
+    p = native.Press(o)
     p.run_for(0.5)
     if not os.environ.get("NO_RPCZ"):
         native.set_flag("enable_rpcz", "true")
@@ -67,7 +75,7 @@ def main():
     native.set_flag("enable_rpcz", "false")
     st = p.stats()
     spans = native.rpcz_recent(1000000)
-    client, server = {}, {}
+    client, server, raw = {}, {}, {}
     for d in spans:
         head = d.split("\n", 1)[0]
         m = re.search(r"trace=([0-9a-f]+)", head)
@@ -75,6 +83,7 @@ def main():
             continue
         kv = {k: int(v) for k, v in re.findall(r" (\w+)=\+?(-?\d+)(?:us)?(?= |$)", head)}
         (client if head.startswith("C ") else server)[m.group(1)] = kv
+        raw.setdefault(m.group(1), []).append(d)
     rows = []
     for t, c in client.items():
         sv = server.get(t)
@@ -90,7 +99,7 @@ def main():
             "queue": c["parse"] - c["cut"],
             "done": c["latency"] - c["parse"],
         }
-        rows.append((c["latency"], ph))
+        rows.append((c["latency"], ph, t))
     print("press: qps=%.0f p50=%s p99=%s p999=%s; traced calls=%d" % (st["qps"], st["p50_us"], st["p99_us"],
                                                                      st["p999_us"], len(rows)))
     lat = [r[0] for r in rows]
@@ -101,8 +110,13 @@ def main():
         v = [r[1][k] for r in rows]
         print("%-10s %6d %6d %6d %6d" % (k, pct(v, .5), pct(v, .9), pct(v, .99), max(v) if v else 0))
     print("slowest calls:")
-    for latency, ph in sorted(rows, key=lambda r: -r[0])[:a.top]:
+    slowest = sorted(rows, key=lambda r: -r[0])
+    for latency, ph, _ in slowest[:a.top]:
         print("  %5d us: " % latency + " ".join("%s=%d" % (k, ph[k]) for k in PHASES))
+    for _, _, t in slowest[:a.dump]:
+        print("--- trace %s" % t)
+        for d in raw.get(t, []):
+            print(d)
     s.stop()
 
 

@@ -12,7 +12,7 @@
 #include "base/logging.h"
 #include "gpu/gpu.h"
 
-DEFINE_int32(hbm_arena_mb, 4096,
+DEFINE_int32(hbm_arena_mb, 16384,
              "IPC-exportable HBM arena per device for RPC payload blocks (MiB; 288 GB HBM3E per MI355X)");
 DEFINE_int32(pinned_region_mb, 64, "pinned host memory is carved from hipHostMalloc regions of this size (MiB)");
 
@@ -60,7 +60,7 @@ struct Arena {
     hipIpcMemHandle_t handle;
     std::atomic<size_t> bump{0};
     FreeList lists[kNumClass];
-    std::atomic<int64_t> live_blocks{0}, live_bytes{0}, fallbacks{0};
+    std::atomic<int64_t> live_blocks{0}, live_bytes{0}, fallbacks{0}, splits{0};
 };
 
 Arena g_arena[kMaxDev];
@@ -144,6 +144,31 @@ struct PinnedTls {
 thread_local PinnedTls tls_pinned;
 const int kPinnedMaxClass = 22;  // 4 MiB; larger pinned buffers are dedicated allocations
 
+// Arena fully carved: cut the smallest free block of a larger class into
+// blocks of class c (one returned, the rest onto c's free list) rather than
+// falling back to a dedicated hipMalloc (milliseconds, not IPC-lendable,
+// and its hipFree synchronises the device). Blocks are never merged back;
+// a workload that moves from small to large payloads is what the arena's
+// size (-hbm_arena_mb) is for.
+char* split_larger(Arena& a, int c) {
+    for (int k = c + 1; k <= kMaxClass; ++k) {
+        char* big = nullptr;
+        {
+            std::lock_guard<std::mutex> g(a.lists[k].mu);
+            if (a.lists[k].items.empty()) continue;
+            big = a.lists[k].items.back();
+            a.lists[k].items.pop_back();
+        }
+        const size_t sz = (size_t)1 << c;
+        const size_t pieces = (size_t)1 << (k - c);
+        std::lock_guard<std::mutex> g(a.lists[c].mu);
+        for (size_t i = 1; i < pieces; ++i) a.lists[c].items.push_back(big + i * sz);
+        a.splits.fetch_add(1, std::memory_order_relaxed);
+        return big;
+    }
+    return nullptr;
+}
+
 }  // namespace
 
 int InitHbmPool(int device, std::string* error) {
@@ -202,6 +227,7 @@ void* HbmAlloc(size_t n, int device) {
                 }
                 if (off + sz <= a.size) p = a.base + off;
             }
+            if (!p) p = split_larger(a, c);
         }
         if (p) {
             a.live_blocks.fetch_add(1, std::memory_order_relaxed);
@@ -255,6 +281,7 @@ HbmPoolStats GetHbmPoolStats(int device) {
     s.live_blocks = a.live_blocks.load(std::memory_order_relaxed);
     s.live_bytes = a.live_bytes.load(std::memory_order_relaxed);
     s.fallback_allocs = a.fallbacks.load(std::memory_order_relaxed);
+    s.splits = a.splits.load(std::memory_order_relaxed);
     return s;
 }
 

@@ -56,6 +56,7 @@ void* AppendNewDeviceBlock(Buf* b, size_t n, int device);
 
 struct HbmPoolStats {
     int64_t arena_bytes = 0, carved_bytes = 0, live_blocks = 0, live_bytes = 0, fallback_allocs = 0;
+    int64_t splits = 0;  // free blocks of a larger class cut up once the arena was fully carved
 };
 HbmPoolStats GetHbmPoolStats(int device);
 

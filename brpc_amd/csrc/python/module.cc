@@ -677,6 +677,7 @@ PYBIND11_MODULE(_native, m) {
         d["live_blocks"] = s.live_blocks;
         d["live_bytes"] = s.live_bytes;
         d["fallback_allocs"] = s.fallback_allocs;
+        d["splits"] = s.splits;
         d["pinned_bytes"] = gpu::PinnedBytes();
         d["pinned_blocks_in_use"] = gpu::PinnedBlocksInUse();
         return d;

@@ -1,8 +1,9 @@
 """Numerics of the gfx950 kernels against host references (CPU crc32c via
 SSE4.2, pure-python varint codec), plus the device-payload echo path."""
-import random
-
 import os
+import random
+import subprocess
+import sys
 
 import pytest
 
@@ -490,3 +491,39 @@ def test_dmabuf_export_of_real_hbm_registers_through_verbs(dev):
     assert "dmabuf" in d["fd_target"], d        # and produced a dmabuf fd
     assert d["provider"] == "ibverbs", d
     assert d["register_rc"] == 0 and d["lkey"] != 0, d
+
+
+_SPLIT_PROBE = r"""
+import json, sys
+sys.path.insert(0, sys.argv[1])
+from brpc_amd import native
+from brpc_amd.models import start_echo_server
+native.set_flag("hbm_arena_mb", "64")
+s = start_echo_server("127.0.0.1:0", gpu_device=0)
+def press(size, conc, n):
+    p = native.Press({"server": s.address, "concurrency": conc, "attachment_size": size,
+                      "device_attachment": True, "gpu_device": 0, "check_echo": True})
+    p.run_requests(n)
+    st = p.stats()
+    assert st["success"] == n and st["error"] == 0, st
+press(16 << 20, 2, 20)  # carves the whole 64 MiB arena in 16 MiB blocks (and then some)
+a = native.gpu.hbm_pool_stats(0)
+press(65536, 16, 2000)  # must be served by cutting up free 16 MiB blocks
+b = native.gpu.hbm_pool_stats(0)
+s.stop()
+print(json.dumps({"a": a, "b": b}))
+"""
+
+
+def test_hbm_arena_splits_free_blocks_instead_of_falling_back(dev):
+    """Once the arena is fully carved, a payload class with no free block
+    is served by cutting up a free block of a larger class, not by a
+    dedicated hipMalloc (slow, not lendable, synchronising hipFree)."""
+    r = subprocess.run([sys.executable, "-c", _SPLIT_PROBE, ROOT], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    import json
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    a, b = out["a"], out["b"]
+    assert a["carved_bytes"] == 64 << 20, a
+    assert b["splits"] > a["splits"], out
+    assert b["fallback_allocs"] == a["fallback_allocs"], out
