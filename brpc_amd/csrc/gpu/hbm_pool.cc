@@ -64,6 +64,7 @@ struct Arena {
 };
 
 Arena g_arena[kMaxDev];
+std::atomic<void (*)()> g_reclaim{nullptr};
 
 struct HbmTls {
     TlsCache c[kMaxDev];
@@ -171,6 +172,8 @@ char* split_larger(Arena& a, int c) {
 
 }  // namespace
 
+void SetHbmReclaimHook(void (*fn)()) { g_reclaim.store(fn, std::memory_order_release); }
+
 int InitHbmPool(int device, std::string* error) {
     if (device < 0) device = CurrentDevice();
     if (device < 0 || device >= kMaxDev) {
@@ -228,6 +231,22 @@ void* HbmAlloc(size_t n, int device) {
                 if (off + sz <= a.size) p = a.base + off;
             }
             if (!p) p = split_larger(a, c);
+            if (!p) {
+                // before a dedicated allocation: let the transports give
+                // back what their peers already released, then look again
+                void (*reclaim)() = g_reclaim.load(std::memory_order_acquire);
+                if (reclaim) {
+                    reclaim();
+                    {
+                        std::lock_guard<std::mutex> g(a.lists[c].mu);
+                        if (!a.lists[c].items.empty()) {
+                            p = a.lists[c].items.back();
+                            a.lists[c].items.pop_back();
+                        }
+                    }
+                    if (!p) p = split_larger(a, c);
+                }
+            }
         }
         if (p) {
             a.live_blocks.fetch_add(1, std::memory_order_relaxed);

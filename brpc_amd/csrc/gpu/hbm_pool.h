@@ -54,6 +54,11 @@ int64_t ArenaOffset(const void* p, int device);
 // owned by the Buf (returned to the pool when the last reference dies).
 void* AppendNewDeviceBlock(Buf* b, size_t n, int device);
 
+// Called (from the allocating thread) when the arena has no block of the
+// requested class left: frees what can be freed (the xGMI lender reaps
+// lends its peers released) before the pool falls back to hipMalloc.
+void SetHbmReclaimHook(void (*fn)());
+
 struct HbmPoolStats {
     int64_t arena_bytes = 0, carved_bytes = 0, live_blocks = 0, live_bytes = 0, fallback_allocs = 0;
     int64_t splits = 0;  // free blocks of a larger class cut up once the arena was fully carved

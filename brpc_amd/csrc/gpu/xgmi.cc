@@ -29,6 +29,9 @@
 #include "var/var.h"
 
 DEFINE_int32(xgmi_slots, 65536, "release-table slots per process (max payload blocks lent at once)");
+DEFINE_int32(xgmi_reap_scan_mb, 256,
+             "scan every outstanding lend for releases once they hold this many MiB (out-of-order releases "
+             "of large payloads otherwise pin arena blocks until the 100 ms scan)");
 DEFINE_int32(xgmi_dead_peer_reap_ms, 2000,
              "lent blocks whose connection failed are reclaimed after this long (the peer may still be pulling)");
 
@@ -119,6 +122,8 @@ public:
                 e.seq = ++_next_seq;
                 e.sock = sock_id;
                 e.since_us = monotonic_us();
+                e.bytes = e.hold.size();
+                _held_bytes += e.bytes;
                 _outstanding.push_back(s);
                 *slot = s;
                 *seq = e.seq;
@@ -155,6 +160,7 @@ private:
         uint64_t seq = 0;
         SocketId sock = 0;
         int64_t since_us = 0;
+        size_t bytes = 0;
     };
 
     bool released(uint32_t s) const {
@@ -163,13 +169,17 @@ private:
     void free_slot(uint32_t s, std::vector<Buf>* dead) {
         dead->emplace_back(std::move(_slots[s].hold));
         _slots[s].hold.clear();
+        _held_bytes -= _slots[s].bytes;
+        _slots[s].bytes = 0;
         _free.push_back(s);
     }
     // Cheap pass: pop released slots from the front (borrowers release in
     // roughly FIFO order). Full pass (slots exhausted, the outstanding list
-    // grew large, or every 100 ms while something is stuck at the front):
-    // compact the list, also reclaiming lends of connections that failed
-    // more than xgmi_dead_peer_reap_ms ago.
+    // or the bytes it holds grew large, or every 100 ms while something is
+    // stuck at the front): compact the list, also reclaiming lends of
+    // connections that failed more than xgmi_dead_peer_reap_ms ago. The
+    // byte trigger matters for large payloads: sixteen 16 MiB lends
+    // released out of order must not pin the arena for 100 ms.
     void reap_locked(std::vector<Buf>* dead, bool full) {
         while (!_outstanding.empty() && released(_outstanding.front())) {
             free_slot(_outstanding.front(), dead);
@@ -177,7 +187,9 @@ private:
         }
         if (_outstanding.empty()) return;
         const int64_t now = monotonic_us();
-        if (!full && _outstanding.size() < _next_full_scan && now - _last_full_us < 100000) return;
+        if (!full && _outstanding.size() < _next_full_scan && _held_bytes < _next_scan_bytes &&
+            now - _last_full_us < 100000)
+            return;
         _last_full_us = now;
         std::deque<uint32_t> keep;
         for (uint32_t s : _outstanding) {
@@ -191,6 +203,7 @@ private:
         }
         _outstanding.swap(keep);
         _next_full_scan = std::max<size_t>(1024, _outstanding.size() * 2);
+        _next_scan_bytes = std::max<size_t>((size_t)FLAGS_xgmi_reap_scan_mb << 20, _held_bytes * 2);
     }
 
     static std::vector<std::string>& registry() {
@@ -211,6 +224,8 @@ private:
     std::deque<uint32_t> _outstanding;
     uint64_t _next_seq = 0;
     size_t _next_full_scan = 1024;
+    size_t _held_bytes = 0;  // bytes of the outstanding lends
+    size_t _next_scan_bytes = (size_t)256 << 20;
     int64_t _last_full_us = 0;
 };
 
@@ -468,6 +483,7 @@ int EnableXgmiTransport(int device, std::string* error) {
     SetStageToHostHook(StageToPinnedHost);
     g_device = device;
     g_lender = l;
+    SetHbmReclaimHook(ReapLentBlocks);
     DeviceTransportHooks h;
     h.send = xgmi_send;
     h.recv = xgmi_recv;

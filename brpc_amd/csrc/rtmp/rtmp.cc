@@ -1,5 +1,7 @@
 #include "rtmp/rtmp.h"
 
+#include <cmath>
+
 #include <cstring>
 #include <functional>
 #include <map>
@@ -253,7 +255,14 @@ private:
         }
     }
     bool OnCommand(uint32_t stream_id, const std::vector<AMFValue>& v, const Server* server);
+
+public:
+    // onStatus of a stream (transaction 0, null command object, info).
     void ReplyStatus(uint32_t stream_id, const char* level, const char* code, const std::string& desc);
+    // `_error` (transaction 0) of a stream command: level error + code.
+    void ReplyError(uint32_t stream_id, const char* code, const std::string& desc);
+
+private:
 
     const bool _server;
     const SocketId _sid;
@@ -446,7 +455,15 @@ bool Connection::OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& b
         return true;
     }
     case RTMP_USER_CONTROL: {
-        uint8_t b[6];
+        uint8_t b[10];
+        const size_t nb = body.copy_to(b, 10);
+        const int event = nb >= 2 ? ((b[0] << 8) | b[1]) : -1;
+        if (event == 3 && nb >= 10 && _server) {  // SetBufferLength{stream id, ms}
+            RtmpStreamBase* st = FindStream(rd32(b + 2));
+            if (st) static_cast<RtmpServerStream*>(st)->OnSetBufferLength(rd32(b + 6));
+            return true;
+        }
+        if (event == 2) return true;  // StreamDry: nothing to do on our side
         if (body.copy_to(b, 6) == 6 && ((b[0] << 8) | b[1]) == 7) {  // PingResponse to our Ping()
             std::function<void()> fn;
             {
@@ -494,6 +511,7 @@ bool Connection::OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& b
             i = 1;
             name = v[1].str();
         }
+        st->CallOnFirstMessage();
         if (name == "onCuePoint") {
             RtmpCuePoint cp;
             cp.timestamp = ts;
@@ -512,6 +530,7 @@ bool Connection::OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& b
         if (!st || body.empty()) return true;
         char h;
         body.cut1(&h);
+        st->CallOnFirstMessage();
         RtmpAudioMessage a;
         a.timestamp = ts;
         a.codec = (uint8_t)h >> 4;
@@ -527,6 +546,7 @@ bool Connection::OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& b
         if (!st || body.empty()) return true;
         char h;
         body.cut1(&h);
+        st->CallOnFirstMessage();
         RtmpVideoMessage vm;
         vm.timestamp = ts;
         vm.frame_type = (uint8_t)h >> 4;
@@ -542,6 +562,17 @@ bool Connection::OnMessage(uint8_t type, uint32_t ts, uint32_t stream_id, Buf& b
 bool Connection::OnCommand(uint32_t stream_id, const std::vector<AMFValue>& v, const Server* server) {
     const std::string& name = v[0].str();
     const double tx = v.size() > 1 ? v[1].number() : 0;
+    if (name == "_error" && tx == 0 && stream_id != 0) {
+        // a stream command's failure (seek / pause): reported like onStatus
+        StatusFn fn;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            auto it = _status_listeners.find(stream_id);
+            if (it != _status_listeners.end()) fn = it->second;
+        }
+        if (fn) fn(v);
+        return true;
+    }
     if (name == "_result" || name == "_error") {
         TxCallback cb;
         {
@@ -653,7 +684,59 @@ bool Connection::OnCommand(uint32_t stream_id, const std::vector<AMFValue>& v, c
         }
         return true;
     }
+    if (name == "play2") {
+        if (!st || v.size() < 4 || v[3].type() != rtmp::AMF_OBJECT) return true;
+        RtmpPlay2Options o;
+        const AMFValue& obj = v[3];
+        if (const AMFValue* a = obj.Find("len")) o.len = a->number();
+        if (const AMFValue* a = obj.Find("offset")) o.offset = a->number();
+        if (const AMFValue* a = obj.Find("oldStreamName")) o.old_stream_name = a->str();
+        if (const AMFValue* a = obj.Find("start")) o.start = a->number();
+        if (const AMFValue* a = obj.Find("streamName")) o.stream_name = a->str();
+        if (const AMFValue* a = obj.Find("transition")) o.transition = a->str();
+        st->OnPlay2(o);
+        return true;
+    }
+    if (name == "seek") {
+        if (!st || v.size() < 4 || v[3].type() != rtmp::AMF_NUMBER) return true;
+        if (st->OnSeek(v[3].number()) == 0) {
+            ReplyStatus(stream_id, "status", "NetStream.Seek.Notify", "Seek successfully.");
+        } else {
+            ReplyError(stream_id, "NetStream.Seek.Notify", "Fail to seek");
+        }
+        return true;
+    }
+    if (name == "pause") {
+        if (!st || v.size() < 5 || v[3].type() != rtmp::AMF_BOOLEAN) return true;
+        const bool pause = v[3].boolean();
+        const double ms = v[4].type() == rtmp::AMF_NUMBER ? v[4].number() : 0;
+        const char* code = pause ? "NetStream.Pause.Notify" : "NetStream.Unpause.Notify";
+        if (st->_paused == pause) {  // pausing a paused stream (or the reverse)
+            ReplyError(stream_id, code, pause ? "Stream is already paused" : "Stream is not paused");
+            return true;
+        }
+        if (st->OnPause(pause, ms) != 0) {
+            ReplyError(stream_id, code, pause ? "Fail to pause" : "Fail to unpause");
+            return true;
+        }
+        st->_paused = pause;
+        ReplyStatus(stream_id, "status", code, pause ? "Paused stream." : "Unpaused stream.");
+        std::string p;
+        p.push_back(0);
+        p.push_back(pause ? 1 : 0);  // StreamEOF / StreamBegin
+        be32(&p, stream_id);
+        SendControl(RTMP_USER_CONTROL, p);
+        return true;
+    }
     return true;  // other commands (releaseStream, FCPublish, getStreamLength...) are accepted silently
+}
+
+void Connection::ReplyError(uint32_t stream_id, const char* code, const std::string& desc) {
+    AMFValue info = AMFValue::Object();
+    info.Set("level", AMFValue::String("error"));
+    info.Set("code", AMFValue::String(code));
+    info.Set("description", AMFValue::String(desc));
+    SendCommand(stream_id, {AMFValue::String("_error"), AMFValue::Number(0), AMFValue::Null(), info});
 }
 
 // Socket-attached holder.
@@ -779,6 +862,59 @@ int RtmpStreamBase::SendAVCMessage(const RtmpAVCMessage& msg) {
     return SendVideoMessage(v);
 }
 
+int RtmpStreamBase::SendUserMessage(void*) {
+    LOG(ERROR) << "SendUserMessage is not implemented by this stream class";
+    errno = ENOTSUP;
+    return -1;
+}
+
+int RtmpStreamBase::SendStopMessage(const std::string&) {
+    errno = ENOTSUP;
+    return -1;
+}
+
+// ------------------------------------------------------------ server stream
+
+void RtmpServerStream::OnPlay2(const RtmpPlay2Options& opt) {
+    LOG(WARNING) << remote_side() << '[' << stream_id() << "] ignored play2{streamName=" << opt.stream_name
+                 << " oldStreamName=" << opt.old_stream_name << " transition=" << opt.transition << '}';
+}
+
+int RtmpServerStream::OnSeek(double offset_ms) {
+    LOG(WARNING) << remote_side() << '[' << stream_id() << "] ignored seek(" << offset_ms << ")";
+    return -1;
+}
+
+int RtmpServerStream::OnPause(bool pause, double offset_ms) {
+    LOG(WARNING) << remote_side() << '[' << stream_id() << "] ignored " << (pause ? "pause" : "unpause")
+                 << "(offset_ms=" << offset_ms << ")";
+    return -1;
+}
+
+int RtmpServerStream::SendStopMessage(const std::string& error_description) {
+    std::shared_ptr<Connection> conn = _conn;
+    if (!conn || conn->closed()) {
+        errno = EINVAL;
+        return -1;
+    }
+    // players (flash, ffplay, OBS) close the stream on StreamNotFound
+    conn->ReplyStatus(_stream_id, "error", "NetStream.Play.StreamNotFound", error_description);
+    return 0;
+}
+
+int RtmpServerStream::SendStreamDry() {
+    std::shared_ptr<Connection> conn = _conn;
+    if (!conn || conn->closed()) {
+        errno = EINVAL;
+        return -1;
+    }
+    std::string p;
+    p.push_back(0);
+    p.push_back(2);  // StreamDry
+    rtmp_detail::be32(&p, _stream_id);
+    return conn->SendControl(RTMP_USER_CONTROL, p);
+}
+
 // ------------------------------------------------------------ client
 
 namespace {
@@ -866,6 +1002,7 @@ int RtmpClient::Init(const char* server_addr_and_port, const RtmpClientOptions& 
         return -1;
     }
     _conn = conn;
+    _url_prefix = "rtmp://" + std::string(server_addr_and_port) + "/" + _options.app;
     return 0;
 }
 
@@ -887,14 +1024,29 @@ int RtmpClientStream::Init(RtmpClient* client, const RtmpClientStreamOptions& op
     _stream_id = (uint32_t)w->args[3].number();
     _conn = conn;
     conn->AddStream(_stream_id, this, false);
-    // onStatus of this stream completes play/publish
+    // onStatus of this stream completes play/publish; later ones go to
+    // OnStatus() while the stream is alive (the sink is cut in Destroy())
     std::shared_ptr<Waiter> st = std::make_shared<Waiter>();
-    conn->SetStatusListener(_stream_id, [st](const std::vector<AMFValue>& args) {
-        if (st->ev.count() <= 0) return;  // later statuses of the stream
-        const AMFValue* code = args.size() > 3 ? args[3].Find("code") : nullptr;
-        st->ok = code && (code->str() == "NetStream.Play.Start" || code->str() == "NetStream.Publish.Start");
-        st->ev.signal();
+    _sink = std::make_shared<StatusSink>();
+    _sink->stream = this;
+    std::shared_ptr<StatusSink> sink = _sink;
+    conn->SetStatusListener(_stream_id, [st, sink](const std::vector<AMFValue>& args) {
+        const AMFValue* info = args.size() > 3 && args[3].type() == rtmp::AMF_OBJECT ? &args[3] : nullptr;
+        const AMFValue* code = info ? info->Find("code") : nullptr;
+        if (st->ev.count() > 0) {
+            st->ok = code && (code->str() == "NetStream.Play.Start" || code->str() == "NetStream.Publish.Start");
+            st->ev.signal();
+            return;
+        }
+        const AMFValue* level = info ? info->Find("level") : nullptr;
+        const AMFValue* desc = info ? info->Find("description") : nullptr;
+        std::lock_guard<std::mutex> g(sink->mu);
+        if (!sink->stream) return;
+        sink->stream->SetLastStatus(code ? code->str() : "");
+        sink->stream->OnStatus(level ? level->str() : "", code ? code->str() : "", desc ? desc->str() : "");
     });
+    _name = options.publish_name.empty() ? options.play_name : options.publish_name;
+    _url_prefix = client->url_prefix();
     std::vector<AMFValue> cmd;
     if (!options.publish_name.empty()) {
         cmd = {AMFValue::String("publish"), AMFValue::Number(0), AMFValue::Null(),
@@ -904,6 +1056,14 @@ int RtmpClientStream::Init(RtmpClient* client, const RtmpClientStreamOptions& op
                AMFValue::Number(-2)};
     }
     conn->SendCommand(_stream_id, cmd);
+    if (options.publish_name.empty() && options.buffer_length_ms >= 0) {
+        std::string p;
+        p.push_back(0);
+        p.push_back(3);  // SetBufferLength{stream id, ms}
+        rtmp_detail::be32(&p, _stream_id);
+        rtmp_detail::be32(&p, (uint32_t)options.buffer_length_ms);
+        conn->SendControl(RTMP_USER_CONTROL, p);
+    }
     if (!st->Wait(timeout) || !st->ok) {
         conn->RemoveStream(_stream_id);
         _conn.reset();
@@ -912,7 +1072,59 @@ int RtmpClientStream::Init(RtmpClient* client, const RtmpClientStreamOptions& op
     return 0;
 }
 
+int RtmpClientStream::Play2(const RtmpPlay2Options& opt) {
+    std::shared_ptr<Connection> conn = _conn;
+    if (!conn || conn->closed()) {
+        errno = EINVAL;
+        return -1;
+    }
+    AMFValue o = AMFValue::Object();
+    if (!std::isnan(opt.len)) o.Set("len", AMFValue::Number(opt.len));
+    if (!std::isnan(opt.offset)) o.Set("offset", AMFValue::Number(opt.offset));
+    if (!opt.old_stream_name.empty()) o.Set("oldStreamName", AMFValue::String(opt.old_stream_name));
+    if (!std::isnan(opt.start)) o.Set("start", AMFValue::Number(opt.start));
+    if (!opt.stream_name.empty()) o.Set("streamName", AMFValue::String(opt.stream_name));
+    if (!opt.transition.empty()) o.Set("transition", AMFValue::String(opt.transition));
+    return conn->SendCommand(_stream_id, {AMFValue::String("play2"), AMFValue::Number(0), AMFValue::Null(), o});
+}
+
+int RtmpClientStream::Seek(double offset_ms) {
+    std::shared_ptr<Connection> conn = _conn;
+    if (!conn || conn->closed()) {
+        errno = EINVAL;
+        return -1;
+    }
+    return conn->SendCommand(_stream_id,
+                             {AMFValue::String("seek"), AMFValue::Number(0), AMFValue::Null(), AMFValue::Number(offset_ms)});
+}
+
+int RtmpClientStream::Pause(bool pause, double offset_ms) {
+    std::shared_ptr<Connection> conn = _conn;
+    if (!conn || conn->closed()) {
+        errno = EINVAL;
+        return -1;
+    }
+    return conn->SendCommand(_stream_id, {AMFValue::String("pause"), AMFValue::Number(0), AMFValue::Null(),
+                                          AMFValue::Bool(pause), AMFValue::Number(offset_ms)});
+}
+
+void RtmpClientStream::SetLastStatus(const std::string& code) {
+    std::lock_guard<std::mutex> g(_status_mu);
+    _last_status = code;
+}
+
+std::string RtmpClientStream::last_status() const {
+    std::lock_guard<std::mutex> g(_status_mu);
+    return _last_status;
+}
+
+std::string RtmpClientStream::rtmp_url() const { return _url_prefix + "/" + _name; }
+
 void RtmpClientStream::Destroy() {
+    if (_sink) {  // no OnStatus() after this returns
+        std::lock_guard<std::mutex> g(_sink->mu);
+        _sink->stream = nullptr;
+    }
     std::shared_ptr<Connection> conn = _conn;
     if (!conn) return;
     if (!conn->closed()) {

@@ -21,7 +21,9 @@
 
 #include <atomic>
 #include <cstdint>
+#include <limits>
 #include <memory>
+#include <mutex>
 #include <string>
 
 #include "base/buf.h"
@@ -80,6 +82,8 @@ public:
     virtual void OnVideoMessage(RtmpVideoMessage* msg) {}
     // Data messages named "onCuePoint".
     virtual void OnCuePoint(RtmpCuePoint* cp) {}
+    // Called once, before the first media/metadata/cue-point callback.
+    virtual void OnFirstMessage() {}
     // The stream ended (deleteStream, connection closed, Destroy()).
     virtual void OnStop() {}
 
@@ -89,6 +93,13 @@ public:
     int SendCuePoint(const RtmpCuePoint& cp);
     int SendAACMessage(const RtmpAACMessage& msg);
     int SendAVCMessage(const RtmpAVCMessage& msg);
+    // A message of the application's own kind (reference rtmp.h:564): the
+    // stream class that has one overrides this; the base fails (ENOTSUP).
+    // `msg` stays owned by the caller.
+    virtual int SendUserMessage(void* msg);
+    // Ask the peer to stop; what is sent depends on the stream kind (a
+    // server stream sends NetStream.Play.StreamNotFound). 0 when sent.
+    virtual int SendStopMessage(const std::string& error_description);
 
     uint32_t stream_id() const { return _stream_id; }
     bool is_stopped() const { return _stopped.load(std::memory_order_acquire); }
@@ -97,9 +108,16 @@ public:
     // ---- internal
     virtual int SendMessage(uint8_t type, uint32_t timestamp, const Buf& body);
     void CallOnStop();
+    void CallOnFirstMessage() {
+        if (!_has_data_ever) {
+            _has_data_ever = true;
+            OnFirstMessage();
+        }
+    }
     std::shared_ptr<rtmp_detail::Connection> _conn;
     uint32_t _stream_id = 0;
     std::atomic<bool> _stopped{false};
+    bool _has_data_ever = false;  // touched only on the connection's read fiber
 };
 
 struct RtmpPlayOptions {
@@ -107,6 +125,17 @@ struct RtmpPlayOptions {
     double start = -2;
     double duration = -1;
     bool reset = true;
+};
+
+// play2 (switch bitrate / stream, reference rtmp.proto RtmpPlay2Options):
+// NaN numbers and empty strings are left out of the AMF object.
+struct RtmpPlay2Options {
+    double len = std::numeric_limits<double>::quiet_NaN();
+    double offset = std::numeric_limits<double>::quiet_NaN();
+    std::string old_stream_name;
+    double start = std::numeric_limits<double>::quiet_NaN();
+    std::string stream_name;
+    std::string transition;  // "switch", "swap", ...
 };
 
 struct RtmpConnectRequest {
@@ -120,6 +149,22 @@ public:
     // Accept by leaving *error empty, reject by setting it.
     virtual void OnPlay(const RtmpPlayOptions& opt, std::string* error) {}
     virtual void OnPublish(const std::string& name, const std::string& type, std::string* error) {}
+    // play2 from the client (no reply is sent). The default logs and ignores.
+    virtual void OnPlay2(const RtmpPlay2Options& opt);
+    // seek / pause: 0 accepts (the client gets NetStream.Seek.Notify,
+    // NetStream.Pause.Notify + StreamEOF or NetStream.Unpause.Notify +
+    // StreamBegin), -1 rejects (_error). The defaults reject.
+    virtual int OnSeek(double offset_ms);
+    virtual int OnPause(bool pause, double offset_ms);
+    // The client's buffer length (user control SetBufferLength).
+    virtual void OnSetBufferLength(uint32_t buffer_length_ms) {}
+    // NetStream.Play.StreamNotFound (level error) with the description.
+    int SendStopMessage(const std::string& error_description) override;
+    // User control StreamDry: no more data for now.
+    int SendStreamDry();
+    bool paused() const { return _paused; }
+
+    bool _paused = false;  // read fiber only
 };
 
 class RtmpService {
@@ -159,9 +204,12 @@ public:
     int64_t acks_sent() const;
     // The connection's socket (0 before Init); failing it drops every stream.
     uint64_t socket_id() const;
+    // "rtmp://HOST:PORT/APP"
+    const std::string& url_prefix() const { return _url_prefix; }
 
 private:
     RtmpClientOptions _options;
+    std::string _url_prefix;
     std::shared_ptr<rtmp_detail::Connection> _conn;
 };
 
@@ -169,6 +217,8 @@ struct RtmpClientStreamOptions {
     std::string play_name;      // set one of play_name / publish_name
     std::string publish_name;
     std::string publish_type = "live";
+    // Announced with SetBufferLength after play (-1: not sent).
+    int buffer_length_ms = 1000;
 };
 
 class RtmpClientStream : public RtmpStreamBase {
@@ -178,6 +228,31 @@ public:
     int Init(RtmpClient* client, const RtmpClientStreamOptions& options);
     // deleteStream and detach (OnStop is called). Idempotent.
     void Destroy();
+    // Change bitrate / stream of a playing stream (no reply expected).
+    int Play2(const RtmpPlay2Options& opt);
+    // Seek to offset_ms in the media / playlist; pause (true) or resume.
+    // 0 when the command was sent; the server's verdict arrives as
+    // onStatus (see last_status()).
+    int Seek(double offset_ms);
+    int Pause(bool pause, double offset_ms);
+    // Called for every onStatus / _error of this stream after it started.
+    virtual void OnStatus(const std::string& level, const std::string& code, const std::string& description) {}
+    // code of the last onStatus / _error seen for this stream ("" if none)
+    std::string last_status() const;
+    // "rtmp://HOST:PORT/APP/STREAM"
+    std::string rtmp_url() const;
+
+    // ---- internal
+    void SetLastStatus(const std::string& code);
+    struct StatusSink {
+        std::mutex mu;
+        RtmpClientStream* stream = nullptr;
+    };
+    std::shared_ptr<StatusSink> _sink;
+    std::string _url_prefix;
+    std::string _name;
+    mutable std::mutex _status_mu;
+    std::string _last_status;
 };
 
 // A client stream that outlives its connection (the reference's

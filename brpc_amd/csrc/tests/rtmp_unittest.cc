@@ -4,6 +4,8 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
+#include <cmath>
 #include <map>
 #include <mutex>
 #include <set>
@@ -648,4 +650,153 @@ TEST(RtmpMedia, cue_points_and_retrying_publisher) {
     pub.Destroy();
     EXPECT_FALSE(pub.connected());
     EXPECT_NE(pub.SendCuePoint(cp), 0);
+}
+
+namespace {
+// A VOD-like server stream: seeks within [0, 60000] ms, pauses, records
+// play2 / buffer length; the client sees every verdict as onStatus/_error.
+class VodStream : public RtmpServerStream {
+public:
+    std::mutex mu;
+    std::vector<std::string> log;
+    void OnPlay(const RtmpPlayOptions& opt, std::string* error) override { add("play:" + opt.stream_name); }
+    void OnPlay2(const RtmpPlay2Options& o) override {
+        add("play2:" + o.stream_name + ":" + o.old_stream_name + ":" + o.transition + ":" +
+            std::to_string((int)o.offset) + (std::isnan(o.len) ? ":nolen" : ":len"));
+    }
+    int OnSeek(double ms) override {
+        add("seek:" + std::to_string((int)ms));
+        return ms >= 0 && ms <= 60000 ? 0 : -1;
+    }
+    int OnPause(bool pause, double ms) override {
+        add(std::string(pause ? "pause:" : "unpause:") + std::to_string((int)ms));
+        return 0;
+    }
+    void OnSetBufferLength(uint32_t ms) override { add("buffer:" + std::to_string(ms)); }
+    void add(const std::string& s) {
+        std::lock_guard<std::mutex> g(mu);
+        log.push_back(s);
+    }
+    size_t size() {
+        std::lock_guard<std::mutex> g(mu);
+        return log.size();
+    }
+};
+class VodService : public RtmpService {
+public:
+    std::atomic<VodStream*> last{nullptr};
+    RtmpServerStream* NewStream(const RtmpConnectRequest&) override {
+        VodStream* s = new VodStream;
+        last.store(s);
+        return s;
+    }
+};
+class VodPlayer : public RtmpClientStream {
+public:
+    std::mutex mu;
+    std::vector<std::string> statuses;
+    std::atomic<int> first{0}, media{0};
+    void OnStatus(const std::string& level, const std::string& code, const std::string& desc) override {
+        std::lock_guard<std::mutex> g(mu);
+        statuses.push_back(level + ":" + code + ":" + desc);
+    }
+    void OnFirstMessage() override {
+        EXPECT_EQ(media.load(), 0);  // before any media callback
+        first.fetch_add(1);
+    }
+    void OnVideoMessage(RtmpVideoMessage*) override { media.fetch_add(1); }
+    size_t nstatus() {
+        std::lock_guard<std::mutex> g(mu);
+        return statuses.size();
+    }
+};
+template <typename F>
+bool wait_until(F f, int ms = 3000) {
+    const int64_t deadline = monotonic_us() + (int64_t)ms * 1000;
+    while (!f() && monotonic_us() < deadline) usleep(1000);
+    return f();
+}
+}  // namespace
+
+// Reference: rtmp.h:814-819 (Play2/Seek/Pause), :1096-1112 (OnPlay2/OnSeek/
+// OnPause/OnSetBufferLength, SendStopMessage, SendStreamDry), :564-568.
+TEST(Rtmp, play2_seek_pause_and_stop) {
+    VodService svc;
+    Server server;
+    ServerOptions o;
+    o.has_builtin_services = false;
+    o.rtmp_service = &svc;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &o), 0);
+    const std::string addr = "127.0.0.1:" + std::to_string(server.listen_port());
+    RtmpClient client;
+    RtmpClientOptions copt;
+    copt.app = "vod";
+    copt.timeout_ms = 3000;
+    ASSERT_EQ(client.Init(addr.c_str(), copt), 0);
+    VodPlayer player;
+    RtmpClientStreamOptions po;
+    po.play_name = "movie";
+    po.buffer_length_ms = 2500;
+    ASSERT_EQ(player.Init(&client, po), 0);
+    EXPECT_EQ(player.rtmp_url(), "rtmp://" + addr + "/vod/movie");
+    VodStream* vs = svc.last.load();
+    ASSERT_TRUE(vs != nullptr);
+    ASSERT_TRUE(wait_until([&] { return vs->size() >= 2; }));
+
+    RtmpPlay2Options p2;
+    p2.stream_name = "movie_720p";
+    p2.old_stream_name = "movie";
+    p2.transition = "switch";
+    p2.offset = 1500;
+    ASSERT_EQ(player.Play2(p2), 0);
+    ASSERT_EQ(player.Seek(30000), 0);
+    ASSERT_TRUE(wait_until([&] { return player.nstatus() >= 1; }));
+    EXPECT_EQ(player.last_status(), "NetStream.Seek.Notify");
+    ASSERT_EQ(player.Seek(90000), 0);  // out of range: rejected with _error
+    ASSERT_TRUE(wait_until([&] { return player.nstatus() >= 2; }));
+    ASSERT_EQ(player.Pause(true, 31000), 0);
+    ASSERT_TRUE(wait_until([&] { return player.nstatus() >= 3; }));
+    EXPECT_TRUE(vs->paused());
+    ASSERT_EQ(player.Pause(true, 31000), 0);  // already paused: _error, OnPause not called
+    ASSERT_TRUE(wait_until([&] { return player.nstatus() >= 4; }));
+    ASSERT_EQ(player.Pause(false, 31000), 0);
+    ASSERT_TRUE(wait_until([&] { return player.nstatus() >= 5; }));
+    EXPECT_FALSE(vs->paused());
+    {
+        std::lock_guard<std::mutex> g(player.mu);
+        EXPECT_EQ(player.statuses[0], "status:NetStream.Seek.Notify:Seek successfully.");
+        EXPECT_EQ(player.statuses[1], "error:NetStream.Seek.Notify:Fail to seek");
+        EXPECT_EQ(player.statuses[2], "status:NetStream.Pause.Notify:Paused stream.");
+        EXPECT_EQ(player.statuses[3], "error:NetStream.Pause.Notify:Stream is already paused");
+        EXPECT_EQ(player.statuses[4], "status:NetStream.Unpause.Notify:Unpaused stream.");
+    }
+    {
+        std::lock_guard<std::mutex> g(vs->mu);
+        const std::vector<std::string> want = {"play:movie",  "buffer:2500", "play2:movie_720p:movie:switch:1500:nolen",
+                                               "seek:30000",  "seek:90000",  "pause:31000",
+                                               "unpause:31000"};
+        std::string got_all, want_all;
+        for (const std::string& x : vs->log) got_all += x + ";";
+        for (const std::string& x : want) want_all += x + ";";
+        EXPECT_EQ(got_all, want_all);
+    }
+    // media: OnFirstMessage once, before the first callback
+    RtmpVideoMessage vm;
+    vm.data.append("frame");
+    ASSERT_EQ(vs->SendVideoMessage(vm), 0);
+    ASSERT_EQ(vs->SendVideoMessage(vm), 0);
+    ASSERT_TRUE(wait_until([&] { return player.media.load() == 2; }));
+    EXPECT_EQ(player.first.load(), 1);
+    // StreamDry is accepted silently; SendStopMessage reaches the player
+    EXPECT_EQ(vs->SendStreamDry(), 0);
+    EXPECT_EQ(vs->SendStopMessage("gone away"), 0);
+    ASSERT_TRUE(wait_until([&] { return player.nstatus() >= 6; }));
+    EXPECT_EQ(player.last_status(), "NetStream.Play.StreamNotFound");
+    // the base stream class has no user message and no stop message
+    int dummy = 0;
+    EXPECT_EQ(player.SendUserMessage(&dummy), -1);
+    EXPECT_EQ(errno, ENOTSUP);
+    EXPECT_EQ(player.SendStopMessage("x"), -1);
+    player.Destroy();
+    EXPECT_EQ(player.Seek(1), -1);  // not attached any more
 }
