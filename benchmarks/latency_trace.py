@@ -74,6 +74,11 @@ def main():
     p.run_for(a.seconds)
     native.set_flag("enable_rpcz", "false")
     st = p.stats()
+    if a.device_attachment:
+        x = native.gpu.xgmi_stats()
+        print("hbm pool:", native.gpu.hbm_pool_stats(0))
+        print("xgmi:", {k: x[k] for k in ("sent_payloads", "recv_payloads", "copied_into_arena", "ring_full_fallbacks",
+                                          "copy_launches", "copy_segments")})
     spans = native.rpcz_recent(1000000)
     client, server, raw = {}, {}, {}
     for d in spans:
