@@ -21,6 +21,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 import argparse
 import json
 import os
+import resource
 import sys
 import time
 
@@ -233,6 +234,7 @@ def main():
         tr0 = transport_snapshot()
         parallel.barrier(topo)
         sync()
+        ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
         step_s = []
         for _ in range(steps):
@@ -242,7 +244,13 @@ def main():
         parallel.barrier(topo)
         sync()
         dt = time.perf_counter() - t0
+        ru1 = resource.getrusage(resource.RUSAGE_SELF)
         st = press.stats()
+        # CPU time of the whole rank (client + server + runtime threads) per
+        # completed RPC: a device path that wins by burning more host CPU
+        # shows up here
+        cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+        cpu_us_per_rpc = parallel.allreduce_sum(cpu_s, topo) * 1e6 / max(1, parallel.allreduce_sum(st["success"], topo))
         dt_max = parallel.allreduce_max(dt, topo)
         ok_total = parallel.allreduce_sum(st["success"], topo)
         err_total = parallel.allreduce_sum(st["error"], topo)
@@ -266,6 +274,7 @@ def main():
             "step_qps_min": step_qps[0] if step_qps else 0.0,
             "step_qps_max": step_qps[-1] if step_qps else 0.0,
             "transport": tr,
+            "cpu_us_per_rpc": round(cpu_us_per_rpc, 2),
         }
 
     def latency_sample():
@@ -277,7 +286,6 @@ def main():
         parallel.barrier(topo)
         press.run_for(0.5)  # warm-up: the first calls of a connection pay lazy setup
         press.reset_stats()
-        import resource  # noqa: E402
         r0, w0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
         press.run_for(a.latency_sample_s)
         r1, w1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
@@ -350,13 +358,18 @@ def main():
     # answered from HBM (staged back to the client's TCP stream by one
     # batched launch). Bytes and device CRC are verified in the GPU tests
     # (tests/test_gpu_ops.py::test_gpu_process_echo_handler), not here.
-    rg = None
-    if cuda and not a.skip_64k:
+    # Its host-only twin (cpu_handler) computes the same checksum on the
+    # server's CPU: same bytes on the wire, same verification at the client.
+    rg = rgc = None
+    if not a.skip_64k:
         wlg = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=False,
                                   requests_per_step=max(1, wl64.requests_per_step // 2)))
         og = wlg.press_options(peer, gpu_device=topo.device)
-        og.update({"concurrency": a.concurrency, "gpu_process": True})
-        rg = timed_leg(wlg, a.steps, a.warmup, og)
+        # every 64th reply is verified (bytes + checksum against the host's)
+        og.update({"concurrency": a.concurrency, "check_echo": True, "check_every": 64})
+        rgc = timed_leg(wlg, a.steps, a.warmup, dict(og, cpu_process=True))
+        if cuda:
+            rg = timed_leg(wlg, a.steps, a.warmup, dict(og, gpu_process=True))
 
     # gRPC + snappy leg (BASELINE config 4): h2:grpc echo of a 64 KiB
     # protobuf body, snappy-compressed in both directions (grpc-encoding),
@@ -667,11 +680,19 @@ def main():
             out["sweep"] = sweep["points"]
             if "rccl_crossover_bytes" in sweep:
                 out["rccl_crossover_bytes"] = sweep["rccl_crossover_bytes"]
+        legs = (("echo_32B", r32), ("echo_64KB", r64), ("echo_64KB_host", r64h), ("rccl_64KB", rc),
+                ("echo_1MB", r1m), ("rccl_1MB", r1mr), ("cpu_handler_64KB", rgc), ("gpu_handler_64KB", rg))
+        if rz:
+            legs += (("grpc_snappy_cpu_codec", rz["cpu"]), ("grpc_snappy_gpu_codec", rz.get("gpu")))
         # which transport carried each leg's payloads (summed over ranks)
-        out["transport"] = {name: leg["transport"] for name, leg in
-                            (("echo_32B", r32), ("echo_64KB", r64), ("echo_64KB_host", r64h),
-                             ("rccl_64KB", rc), ("echo_1MB", r1m), ("rccl_1MB", r1mr), ("gpu_handler_64KB", rg))
-                            if leg}
+        out["transport"] = {name: leg["transport"] for name, leg in legs if leg and name[:4] != "grpc"}
+        # host CPU microseconds per RPC of each leg (whole rank: client,
+        # server, dispatcher, pollers)
+        out["cpu_us_per_rpc"] = {name: leg["cpu_us_per_rpc"] for name, leg in legs if leg}
+        if rgc:
+            out["qps_64KB_cpu_handler"] = round(rgc["qps"], 1)
+            out["p99_us_64KB_cpu_handler"] = rgc["p99_us"]
+            out["errors_64KB_cpu_handler"] = rgc["errors"]
         if rg:
             out["qps_64KB_gpu_handler"] = round(rg["qps"], 1)
             out["p99_us_64KB_gpu_handler"] = rg["p99_us"]

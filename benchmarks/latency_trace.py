@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--attachment", type=int, default=0, help="attachment bytes per call")
     ap.add_argument("--device-attachment", action="store_true", help="attachment in HBM (lent over xGMI)")
+    ap.add_argument("--gpu-process", action="store_true", help="the server runs the GPU handler over the attachment")
     ap.add_argument("--concurrency", type=int, default=1)
     ap.add_argument("--dump", type=int, default=0, help="print the full spans of this many slowest calls")
     a = ap.parse_args()
@@ -60,12 +61,13 @@ def main():
     native.set_flag("rpcz_save_to_disk", "false")
     native.set_flag("rpcz_max_spans", "100000")
     native.set_flag("rpcz_max_spans_per_second", "100000")
-    dev = 0 if a.device_attachment else -1
+    dev = 0 if (a.device_attachment or a.gpu_process) else -1
     s = start_echo_server("127.0.0.1:0", num_threads=a.workers, gpu_device=dev)
     o = {"server": s.address, "qps": a.qps, "concurrency": a.concurrency, "request_size": 32,
          "connection_type": "single"}
     if a.attachment:
-        o.update({"attachment_size": a.attachment, "gpu_device": dev, "device_attachment": a.device_attachment})
+        o.update({"attachment_size": a.attachment, "gpu_device": dev, "device_attachment": a.device_attachment,
+                  "gpu_process": a.gpu_process})
     p = native.Press(o)
     p.run_for(0.5)
     if not os.environ.get("NO_RPCZ"):
@@ -74,11 +76,12 @@ def main():
     p.run_for(a.seconds)
     native.set_flag("enable_rpcz", "false")
     st = p.stats()
-    if a.device_attachment:
+    if dev >= 0:
         x = native.gpu.xgmi_stats()
         print("hbm pool:", native.gpu.hbm_pool_stats(0))
         print("xgmi:", {k: x[k] for k in ("sent_payloads", "recv_payloads", "copied_into_arena", "ring_full_fallbacks",
-                                          "copy_launches", "copy_segments")})
+                                          "copy_launches", "copy_segments", "copy_submits", "copy_queue_us",
+                                          "copy_api_us", "copy_gpu_us", "copy_wake_us")})
     spans = native.rpcz_recent(1000000)
     client, server, raw = {}, {}, {}
     for d in spans:

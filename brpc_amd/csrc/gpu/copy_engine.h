@@ -28,7 +28,8 @@ namespace gpu {
 // fused copy+CRC32C kernel and crcs[i] receives the standard CRC32C of
 // segment i (computed from the bytes while they are moved).
 // With fold_crc, crcs[0] instead receives the CRC32C of all n segments
-// concatenated (one message), folded on the device.
+// concatenated (one message), folded on the device. With crcs, a segment
+// whose dst is null is only checksummed (nothing is written).
 int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs = nullptr, bool fold_crc = false);
 
 struct CopyEngineStats {

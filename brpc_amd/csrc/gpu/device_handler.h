@@ -29,9 +29,15 @@ int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device);
 // staged out again (a second device round trip per request).
 int ProcessToPinnedWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device);
 
-// Asynchronous form of both (to_device selects GatherToDeviceWithCrc):
-// returns at once and runs done(rc, out, crc) in a fiber when the kernel
-// finished. A handler that uses it never parks the fiber that called it —
+// CRC32C of `in` computed on the device (the kernel reads pinned/HBM blocks
+// in place; pageable blocks are bounced through pinned memory). 0 on success.
+int CrcOnDevice(const Buf& in, uint32_t* crc, int device);
+
+// Asynchronous handler step: to_device gathers `in` into HBM with its CRC
+// (GatherToDeviceWithCrc, the response is lent over xGMI); otherwise the
+// device only checksums `in` and `out` shares its bytes (the response goes
+// back over TCP from the socket blocks it arrived in). Returns at once and
+// runs done(rc, out, crc) in a fiber when the kernel finished. A handler that uses it never parks the fiber that called it —
 // usually the connection's reader, which the input messenger runs the last
 // request of a read in (reference: input_messenger.cpp:169-190) — so the
 // next requests of the connection are read and submitted while the device

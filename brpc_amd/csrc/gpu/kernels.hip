@@ -279,8 +279,10 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const
             u32x4_unaligned v[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = p[i];
+            if (dbase) {  // null destination: checksum only (uniform per segment)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) q[i] = v[i];
+                for (int i = 0; i < 4; ++i) q[i] = v[i];
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 crc = crc_word8(crc, v[i].x, v[i].y, t);
@@ -289,7 +291,7 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const
         } else {
             for (int64_t i = 0; i < lane_end; ++i) {
                 const uint8_t c = base[i];
-                dbase[i] = c;
+                if (dbase) dbase[i] = c;
                 crc = t[0][(crc ^ c) & 0xff] ^ (crc >> 8);
             }
         }

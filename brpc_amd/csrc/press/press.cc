@@ -306,6 +306,7 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     }
     call->echo_req.set_message(_echo_message);
     if (_opt.gpu_process) call->echo_req.set_gpu_process(true);
+    if (_opt.cpu_process) call->echo_req.set_cpu_process(true);
     if (_device_attachment) {
         gpu::AppendDevice(&cntl.request_attachment(), _device_attachment, _attachment.size(), _opt.gpu_device);
     } else if (!_attachment.empty()) {
@@ -315,7 +316,7 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     }
     call->nbytes = _opt.scatter ? 2 * (int64_t)(_echo_message.size() * _fanout + _attachment.size())
                                 : 2 * (int64_t)(_echo_message.size() + _attachment.size()) * _fanout;
-    call->check = _opt.check_echo;
+    call->check = _opt.check_echo && (_opt.check_every <= 1 || seq % _opt.check_every == 0);
     example::EchoService_Stub stub(ch);
     stub.Echo(&cntl, &call->echo_req, &call->echo_res, done);
 }
@@ -339,7 +340,8 @@ void PressSession::finish(PressCall* call) {
             if (gpu::CopyBufToHost(cntl.response_attachment(), &got) != 0 || got != want) {
                 ok = false;
                 cntl.SetFailed(ERESPONSE, "echoed attachment mismatch (%zu bytes)", got.size());
-            } else if (_opt.gpu_process && call->echo_res.crc32c() != crc32c::Value(want.data(), want.size())) {
+            } else if ((_opt.gpu_process || _opt.cpu_process) &&
+                       call->echo_res.crc32c() != crc32c::Value(want.data(), want.size())) {
                 ok = false;
                 cntl.SetFailed(ERESPONSE, "device CRC32C 0x%08x does not match the host's", call->echo_res.crc32c());
             }

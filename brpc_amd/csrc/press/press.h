@@ -53,7 +53,9 @@ struct PressOptions {
     bool device_attachment = false;  // attachment lives in HBM (needs GPU)
     int gpu_device = -1;
     bool check_echo = false;   // verify the echoed payload
+    int check_every = 1;       // ... of every n-th call (bench legs sample; tests check all)
     bool gpu_process = false;  // ask the server to run the attachment through its GPU
+    bool cpu_process = false;  // ask the server to checksum the attachment on its CPU
     bool use_rdma = false;     // verbs data plane (server needs use_rdma too)
     // Fan-out (ParallelChannel, the DP analog of SURVEY §2.10): every call is
     // broadcast to all of these comma-separated servers — on one node the

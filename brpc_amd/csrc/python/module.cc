@@ -156,6 +156,8 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "fanout_servers") o.fanout_servers = v.cast<std::string>();
         else if (k == "scatter") o.scatter = v.cast<bool>();
         else if (k == "gpu_process") o.gpu_process = v.cast<bool>();
+        else if (k == "cpu_process") o.cpu_process = v.cast<bool>();
+        else if (k == "check_every") o.check_every = v.cast<int>();
         else if (k == "use_rdma") o.use_rdma = v.cast<bool>();
         else if (k == "proto_file") o.proto_file = v.cast<std::string>();
         else if (k == "include_paths") o.include_paths = v.cast<std::string>();

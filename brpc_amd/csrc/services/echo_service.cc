@@ -3,6 +3,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "base/crc32c.h"
 #include "base/time.h"
 #include "fiber/fiber.h"
 #include "gpu/device_handler.h"
@@ -218,6 +219,20 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
                                      cntl->response_attachment().append(std::move(out));
                                  });
         return;
+    }
+    if (request->cpu_process()) {
+        // the GPU handler's work on the host: checksum, zero-copy echo
+        const Buf& in = cntl->request_attachment();
+        if (!in.all_host_accessible()) {
+            cntl->SetFailed(EREQUEST, "cpu_process needs a host attachment");
+            return;
+        }
+        uint32_t crc = 0;
+        for (size_t i = 0; i < in.backing_block_num(); ++i) {
+            crc = crc32c::Extend(crc, in.block_data(i), in.block_len(i));
+        }
+        response->set_device(-1);
+        response->set_crc32c(crc);
     }
     // zero-copy echo of the attachment (host or device blocks alike)
     cntl->response_attachment().append(cntl->request_attachment());

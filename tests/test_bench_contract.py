@@ -60,5 +60,8 @@ def test_bench_multi_rank_gloo(nranks):
     assert all(p["errors"] == 0 for p in j["sweep"])
     assert "rccl_crossover_bytes" in j
     assert j["stream_timed_s"] >= 0.2
+    # the host-only handler twin, and the CPU cost of every leg
+    assert j["errors_64KB_cpu_handler"] == 0 and j["qps_64KB_cpu_handler"] > 0
+    assert all(v > 0 for v in j["cpu_us_per_rpc"].values()) and "cpu_handler_64KB" in j["cpu_us_per_rpc"]
     if nranks > 2:  # a relay chain needs at least two other ranks
         assert j["pipeline_hops"] == nranks - 1 and j["pipeline_gbytes_per_s"] > 0
