@@ -55,6 +55,10 @@ def main():
         if l3 >= 0:
             native.set_flag("cpu_l3_domain", str(l3))
     native.set_flag("event_dispatcher_spin_us", os.environ.get("SPIN_US", "200"))
+    if os.environ.get("RESIDENT"):
+        native.set_flag("copy_engine_resident", "true")
+        if os.environ.get("RESIDENT_GROUPS"):
+            native.set_flag("copy_engine_resident_groups", os.environ["RESIDENT_GROUPS"])
     if "NAP_US" in os.environ:
         native.set_flag("event_dispatcher_nap_us", os.environ["NAP_US"])
     native.set_flag("gpu_poller_idle_spin_us", os.environ.get("POLL_SPIN_US", os.environ.get("SPIN_US", "200")))
@@ -97,6 +101,8 @@ def main():
     print("leg=%s qps=%.0f p50=%s p99=%s errors=%d samples=%d cpus_used=%.2f cgroup=%s" % (
         a.leg, st["qps"], st["p50_us"], st["p99_us"], st["error"], n, cpu, thr))
     x1 = native.gpu.xgmi_stats()
+    if os.environ.get("RESIDENT"):
+        print("resident:", native.gpu.resident_stats())
     subs = x1["copy_submits"] - x0["copy_submits"]
     if subs:
         print("copy engine per submission: queue %.1f us, launch API %.1f us, GPU+poll %.1f us, wake %.1f us; "

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "base/crc32c.h"
+#include "base/flags.h"
 #include "base/logging.h"
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
@@ -16,6 +17,15 @@
 #include "base/time.h"
 #include "base/util.h"
 #include "rpc/span.h"
+
+DEFINE_bool(copy_engine_resident, false,
+            "run batches on the resident copy worker (a persistent kernel fed from a pinned ring: no launch or "
+            "event per batch) instead of one kernel launch each");
+DEFINE_int32(copy_engine_resident_idle_us, 200, "a resident instance exits after this long without a batch");
+DEFINE_int32(copy_engine_resident_groups, 16, "workgroups of a resident instance (each polls the ring)");
+DEFINE_int32(copy_engine_resident_max_us, 4000,
+             "a resident instance exits after this long in any case (bounds how long work sharing its hardware "
+             "queue can wait); the next batch relaunches it");
 
 namespace mrpc {
 namespace gpu {
@@ -65,9 +75,43 @@ Batch* new_batch(Engine& e) {
     return b;
 }
 
+// Resident path: publish the batch to the device's ring; the poller reads
+// its done words. false: not available (the caller launches instead).
+bool submit_resident(Batch* b, int device) {
+    if (!FLAGS_copy_engine_resident) return false;
+    ResidentRing* ring = ResidentRingFor(device, (uint32_t)std::max(1, FLAGS_copy_engine_resident_idle_us),
+                                         (uint32_t)std::max(10, FLAGS_copy_engine_resident_max_us),
+                                         (uint32_t)FLAGS_copy_engine_resident_groups);
+    if (!ring) return false;
+    if (b->want_crc && b->crc_cap < (size_t)b->nmsg) {
+        PinnedFree(b->crc_host, b->crc_cap * sizeof(uint32_t));
+        b->crc_cap = std::max<size_t>((size_t)b->nmsg, 64);
+        b->crc_host = static_cast<uint32_t*>(PinnedAlloc(b->crc_cap * sizeof(uint32_t)));
+        if (!b->crc_host) return false;
+    }
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    uint64_t first = 0, last = 0;
+    const int rc = ResidentSubmit(ring, b->segs.data(), b->want_crc ? b->msg_of.data() : nullptr, (int)b->segs.size(),
+                                  b->want_crc ? b->crc_host : nullptr, &first, &last);
+    b->t_issued = monotonic_us();
+    if (prev != device) hipSetDevice(prev);
+    g_launches.fetch_add(1, std::memory_order_relaxed);
+    if (rc != 0) {
+        LOG_EVERY_SECOND(ERROR) << "resident copy worker refused a batch of " << b->segs.size() << " segments";
+        b->butex->store(-1, std::memory_order_release);
+        fiber::butex_wake_all(b->butex);
+        return true;
+    }
+    WatchResident(ring, first, last, b->butex, &b->t_done);
+    return true;
+}
+
 // Issue one batch: kernel + event + poller registration. On failure the
 // batch's waiters are released with an error.
 void launch(Batch* b, int device) {
+    if (submit_resident(b, device)) return;
     int prev = 0;
     hipGetDevice(&prev);
     if (prev != device) hipSetDevice(device);

@@ -87,6 +87,11 @@ int SyncStream(hipStream_t s);
 // event can release a whole batch of fibers.
 // `done_us` (optional) receives the monotonic time the poller saw it done.
 void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us = nullptr);
+// Same for batches [first, last] of a resident copy worker ring (the
+// poller reads their pinned done words instead of querying an event).
+struct ResidentRing;
+void WatchResident(ResidentRing* ring, uint64_t first_seq, uint64_t last_seq, std::atomic<int>* butex,
+                   int64_t* done_us = nullptr);
 // Pooled events (hipEventDisableTiming).
 hipEvent_t AcquireEvent();
 void ReleaseEvent(hipEvent_t e);

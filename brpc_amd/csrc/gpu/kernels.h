@@ -121,6 +121,30 @@ size_t JsonIndexScratchBytes(uint64_t n);
 int LaunchJsonIndex(const uint8_t* in, uint64_t n, uint32_t* out_pos, uint64_t max_out, uint64_t* count_dev,
                     int* err_dev, void* scratch, hipStream_t s);
 
+// ---- resident copy worker (persistent kernel fed from a pinned ring;
+// kernels.hip explains the protocol). Created on first use per device
+// (nullptr: unavailable); instances exit after idle_us without work or
+// max_us of life and are relaunched on demand.
+struct ResidentRing;
+ResidentRing* ResidentRingFor(int device, uint32_t idle_us, uint32_t max_us, uint32_t groups);
+// Publish segs as ring batches (groups of <= kInlineSegments segments that
+// never split a message; msg_of as in LaunchBatchedCopyCrc32cMessages, null:
+// one message per segment). crc_out (pinned host, null: copy only) receives
+// one CRC32C per message; a null segment dst only checksums. [first, last]
+// are the batches' sequence numbers. 0 on success.
+int ResidentSubmit(ResidentRing* r, const Segment* segs, const int* msg_of, int nseg, uint32_t* crc_out,
+                   uint64_t* first_seq, uint64_t* last_seq);
+// Whether every batch of [first, last] is complete (reads pinned memory).
+bool ResidentDone(ResidentRing* r, uint64_t first_seq, uint64_t last_seq);
+// Watchdog: relaunch when no instance is on the device but a batch waits.
+void ResidentKick(ResidentRing* r);
+// Stop every instance and wait for them (process exit).
+void ResidentShutdown();
+struct ResidentStats {
+    int64_t launches = 0, batches = 0, ring_full_waits = 0;
+};
+ResidentStats GetResidentStats();
+
 // ---- synchronous helpers (fiber-friendly waits)
 // CRC32C of device buffers; results to host.
 int Crc32cDevice(const void* const* ptrs, const uint64_t* lens, int n, uint32_t* out_host, int device);

@@ -1055,5 +1055,399 @@ int LaunchVarintEncode(const uint64_t* in, uint64_t n, bool zigzag, uint8_t* out
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+namespace {
+// ================================================================ resident copy worker
+//
+// A launch per batch costs the host ~6-10 us of HIP API time (kernel
+// arguments of ~1.6 KB, an event record) and the batch a launch latency;
+// at 150k+ batches/s that is a CPU core and a bound on the RPC legs. The
+// resident worker instead stays on the GPU and takes batches from a ring in
+// pinned host memory: the host writes a SegBatch into a slot and publishes
+// its sequence number (one release store); workgroups of the running
+// instance claim its chunks through epoch-tagged counters in HBM, copy +
+// checksum them with the same code as copy_crc32c_kernel, and the workgroup
+// that finishes the last chunk stores the sequence into the slot's done word
+// (a system-scope release), which the completion poller reads as plain host
+// memory — no launch, no event, no hipEventQuery per batch.
+//
+// Every instance exits on its own: after `idle_ticks` without a new batch or
+// `max_ticks` of life (so other work sharing its hardware queue waits at
+// most that long), or when the host sets `stop`. Exit races with a publish
+// are closed Dekker-style: a workgroup announces `exiting = instance`, then
+// re-reads the next slot (system-scope seq_cst both ways); the host
+// publishes, then reads `exiting` and launches a new instance when it names
+// the current one. Instances on the ring's stream run one after another;
+// workgroups of overlapping lifetimes only ever cooperate through the
+// counters. Every loop is bounded.
+static_assert(sizeof(SegBatch) % 16 == 0, "SegBatch is staged into LDS in 16 B words");
+constexpr int kResidentSlots = 64;
+
+struct alignas(128) ResidentSlot {
+    SegBatch batch;
+    uint32_t* crc_out;  // per-message CRC32C (pinned host), null: copy only
+    uint32_t chunks;
+    uint32_t pad;
+    uint64_t seq;       // host: published batch number (written last)
+    uint64_t pad0[13];
+    uint64_t done;      // device: batch number once every chunk is written
+    uint64_t pad1[15];
+};
+
+struct alignas(128) ResidentCtl {
+    uint64_t stop;
+    uint64_t pad0[15];
+    uint64_t exiting;   // instance whose workgroup is about to exit
+    uint64_t pad1[15];
+};
+
+__device__ __forceinline__ uint64_t sys_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Epoch-tagged counter (epoch = low 32 bits of the batch number, count in
+// the low half): adds `add` for batch k32 and returns the count before, or
+// -1 when the counter has moved past k32 or the count would pass `limit`.
+__device__ int64_t tagged_add(uint64_t* ctr, uint32_t k32, uint32_t limit, uint32_t add) {
+    uint64_t old = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int it = 0; it < 4096; ++it) {
+        const uint32_t e = (uint32_t)(old >> 32), c = (uint32_t)old;
+        const int32_t d = (int32_t)(e - k32);
+        if (d > 0) return -1;                // already a later batch's counter
+        const uint32_t cur = d < 0 ? 0 : c;  // an older batch's counter: this batch starts at 0
+        if (cur + add > limit) return -1;
+        const uint64_t nv = ((uint64_t)k32 << 32) | (uint64_t)(cur + add);
+        if (__hip_atomic_compare_exchange_strong(ctr, &old, nv, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return cur;
+    }
+    return -1;
+}
+
+// One 16 KiB chunk of a batch held in LDS (the body of copy_crc32c_kernel;
+// a null destination checksums only; crc_out null copies only).
+__device__ void resident_chunk(const SegBatch& b, uint32_t chunk, const uint32_t (*t)[256], uint32_t* wave_acc,
+                               uint32_t* scratch, uint32_t* crc_out) {
+    const int seg = find_segment(b, chunk);
+    const uint64_t len = b.len[seg];
+    const uint8_t* base = static_cast<const uint8_t*>(b.src[seg]);
+    uint8_t* dbase = static_cast<uint8_t*>(b.dst[seg]);
+    const uint32_t seg_chunks = b.chunk_start[seg + 1] - b.chunk_start[seg];
+    const uint32_t k = chunk - b.chunk_start[seg];
+    const uint32_t after = seg_chunks - 1 - k;
+    const int64_t chunk_end = (int64_t)len - (int64_t)after * (int64_t)kChunkBytes;
+    const int64_t lane_end = chunk_end - (int64_t)(kThreads - 1 - threadIdx.x) * kLaneBytes;
+    const int64_t lane_beg = lane_end - kLaneBytes;
+    const bool want_crc = crc_out != nullptr;
+    uint32_t crc = 0;
+    if (lane_end > 0) {
+        if (lane_beg >= 0) {
+            const u32x4_unaligned* p = reinterpret_cast<const u32x4_unaligned*>(base + lane_beg);
+            u32x4_unaligned* q = reinterpret_cast<u32x4_unaligned*>(dbase + lane_beg);
+            u32x4_unaligned v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = p[i];
+            if (dbase) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) q[i] = v[i];
+            }
+            if (want_crc) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    crc = crc_word8(crc, v[i].x, v[i].y, t);
+                    crc = crc_word8(crc, v[i].z, v[i].w, t);
+                }
+            }
+        } else {
+            for (int64_t i = 0; i < lane_end; ++i) {
+                const uint8_t c = base[i];
+                if (dbase) dbase[i] = c;
+                crc = t[0][(crc ^ c) & 0xff] ^ (crc >> 8);
+            }
+        }
+        if (want_crc) crc = mult_mod_p(c_lane_shift[kThreads - 1 - threadIdx.x], crc);
+    }
+    if (want_crc) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) crc ^= __shfl_xor(crc, off, 64);
+        if ((threadIdx.x & 63) == 0) wave_acc[threadIdx.x >> 6] = crc;
+    }
+    __syncthreads();
+    if (want_crc && threadIdx.x == 0) {
+        const uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
+        fold_chunk(b, seg, after, seg_chunks, acc, scratch, crc_out);
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) resident_copy_kernel(ResidentSlot* ring, ResidentCtl* ctl,
+                                                                 uint64_t* claim, uint64_t* fin,
+                                                                 uint32_t* scratch, const uint32_t* tables,
+                                                                 uint64_t start_seq, uint64_t instance,
+                                                                 uint64_t idle_ticks, uint64_t max_ticks) {
+    __shared__ uint32_t t[8][256];
+    __shared__ uint32_t wave_acc[kThreads / 64];
+    __shared__ __attribute__((aligned(16))) SegBatch sb;
+    __shared__ int64_t s_chunk;
+    __shared__ int s_state;  // 0 work, 1 exit
+    __shared__ uint32_t* s_out;
+    __shared__ uint32_t s_chunks;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(tables);
+        uint4* dst = reinterpret_cast<uint4*>(&t[0][0]);
+        dst[threadIdx.x] = src[threadIdx.x];
+        dst[threadIdx.x + kThreads] = src[threadIdx.x + kThreads];
+    }
+    const uint64_t t_start = wall_clock64();
+    uint64_t t_idle = t_start;
+    uint64_t k = start_seq;
+    for (;;) {
+        ResidentSlot* slot = &ring[k % kResidentSlots];
+        // ---- wait for batch k (thread 0 polls; the group follows)
+        if (threadIdx.x == 0) {
+            int state = 1;
+            for (uint32_t polls = 0;; ++polls) {
+                const uint64_t s = sys_load(&slot->seq);
+                if (s == k) {
+                    state = 0;
+                    break;
+                }
+                if ((int64_t)(s - k) > 0) {  // the slot was reused: batch k is long done (we lagged)
+                    state = 2;
+                    break;
+                }
+                if (sys_load(&ctl->stop)) break;
+                const uint64_t now = wall_clock64();
+                if (now - t_idle > idle_ticks || now - t_start > max_ticks || polls >= (1u << 22)) {
+                    __hip_atomic_store(&ctl->exiting, instance, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (__hip_atomic_load(&slot->seq, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM) == k) {
+                        __hip_atomic_store(&ctl->exiting, 0ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+                        state = 0;
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+            s_state = state;
+            if (state == 0) {
+                s_out = slot->crc_out;
+                s_chunks = slot->chunks;
+            }
+        }
+        __syncthreads();
+        if (s_state == 1) return;
+        if (s_state == 2) {
+            ++k;
+            __syncthreads();
+            continue;
+        }
+        const uint32_t k32 = (uint32_t)k;
+        const uint32_t chunks = s_chunks;
+        uint32_t* crc_out = s_out;
+        const uint32_t si = (uint32_t)(k % kResidentSlots);
+        uint32_t* slot_scratch = scratch + (size_t)si * kInlineSegments * 2;
+        // claim before fetching the descriptor: in a small batch most
+        // workgroups find nothing left and move on at the cost of one CAS
+        if (threadIdx.x == 0) s_chunk = tagged_add(&claim[si], k32, chunks, 1);
+        __syncthreads();
+        int64_t c = s_chunk;
+        __syncthreads();
+        if (c >= 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slot was published before its seq
+            {
+                const uint4* src = reinterpret_cast<const uint4*>(&slot->batch);
+                uint4* dst = reinterpret_cast<uint4*>(&sb);
+                constexpr int kWords = (int)(sizeof(SegBatch) / sizeof(uint4));
+                for (int i = threadIdx.x; i < kWords; i += kThreads) dst[i] = src[i];
+            }
+            __syncthreads();
+            uint32_t mine = 0;
+            for (uint32_t guard = 0; c >= 0 && guard <= chunks; ++guard) {
+                resident_chunk(sb, (uint32_t)c, t, wave_acc, slot_scratch, crc_out);
+                ++mine;
+                if (threadIdx.x == 0) s_chunk = tagged_add(&claim[si], k32, chunks, 1);
+                __syncthreads();
+                c = s_chunk;
+                __syncthreads();
+            }
+            // one system-scope release for everything this workgroup wrote
+            // in the batch (the barrier above ordered every lane's stores)
+            if (threadIdx.x == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                const int64_t f = tagged_add(&fin[si], k32, chunks, mine);
+                if (f >= 0 && f + mine == chunks)
+                    __hip_atomic_store(&slot->done, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        t_idle = wall_clock64();
+        ++k;
+    }
+}
+
+}  // namespace
+
+// ---- host side of the resident worker
+struct ResidentRing {
+    int device = -1;
+    ResidentSlot* slots = nullptr;  // pinned, coherent
+    ResidentCtl* ctl = nullptr;
+    uint64_t* claim = nullptr;      // HBM
+    uint64_t* fin = nullptr;
+    uint32_t* scratch = nullptr;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    uint64_t next_seq = 1;
+    uint64_t instance = 0;          // last launched instance id
+    hipEvent_t last_ev = nullptr;   // recorded after the last launched instance
+    uint64_t idle_ticks = 0, max_ticks = 0;
+    uint32_t groups = 16;           // workgroups per instance
+    std::atomic<int64_t> launches{0}, batches{0}, ring_full_waits{0};
+};
+
+namespace {
+std::mutex g_resident_mu;
+ResidentRing* g_resident[64] = {};
+
+// (re)launch an instance starting at the oldest batch not yet done; mu held
+int resident_launch_locked(ResidentRing* r) {
+    uint64_t start = r->next_seq;
+    for (uint64_t s = r->next_seq > kResidentSlots ? r->next_seq - kResidentSlots : 1; s < r->next_seq; ++s) {
+        const ResidentSlot& sl = r->slots[s % kResidentSlots];
+        if (__atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) < s) {
+            start = s;
+            break;
+        }
+    }
+    const uint64_t inst = ++r->instance;
+    hipLaunchKernelGGL(resident_copy_kernel, dim3(r->groups), dim3(kThreads), 0, r->stream, r->slots, r->ctl,
+                       r->claim, r->fin, r->scratch, g_tables[r->device].t8, start, inst, r->idle_ticks,
+                       r->max_ticks);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (!r->last_ev && hipEventCreateWithFlags(&r->last_ev, hipEventDisableTiming) != hipSuccess) return -1;
+    if (hipEventRecord(r->last_ev, r->stream) != hipSuccess) return -1;
+    r->launches.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+}  // namespace
+
+ResidentRing* ResidentRingFor(int device, uint32_t idle_us, uint32_t max_us, uint32_t groups) {
+    if (device < 0 || device >= 64) return nullptr;
+    std::lock_guard<std::mutex> g(g_resident_mu);
+    if (g_resident[device]) return g_resident[device];
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != device) hipSetDevice(device);
+    ResidentRing* r = new ResidentRing;
+    r->device = device;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0) khz = 100000;
+    r->idle_ticks = (uint64_t)khz * idle_us / 1000;
+    r->max_ticks = (uint64_t)khz * max_us / 1000;
+    r->groups = groups < 1 ? 1 : (groups > 256 ? 256 : groups);
+    bool ok = ensure_tables() == 0 &&
+              hipHostMalloc(reinterpret_cast<void**>(&r->slots), sizeof(ResidentSlot) * kResidentSlots,
+                            hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
+              hipHostMalloc(reinterpret_cast<void**>(&r->ctl), sizeof(ResidentCtl),
+                            hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&r->claim), sizeof(uint64_t) * kResidentSlots) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&r->fin), sizeof(uint64_t) * kResidentSlots) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&r->scratch),
+                        sizeof(uint32_t) * 2 * kInlineSegments * kResidentSlots) == hipSuccess &&
+              hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess;
+    if (ok) {
+        memset(r->slots, 0, sizeof(ResidentSlot) * kResidentSlots);
+        memset(r->ctl, 0, sizeof(ResidentCtl));
+        ok = hipMemset(r->claim, 0, sizeof(uint64_t) * kResidentSlots) == hipSuccess &&
+             hipMemset(r->fin, 0, sizeof(uint64_t) * kResidentSlots) == hipSuccess &&
+             hipMemset(r->scratch, 0, sizeof(uint32_t) * 2 * kInlineSegments * kResidentSlots) == hipSuccess &&
+             hipDeviceSynchronize() == hipSuccess;
+    }
+    if (prev != device) hipSetDevice(prev);
+    if (!ok) return nullptr;  // leaks the partial ring; the engine falls back to launches
+    g_resident[device] = r;
+    return r;
+}
+
+int ResidentSubmit(ResidentRing* r, const Segment* segs, const int* msg_of, int nseg, uint32_t* crc_out,
+                   uint64_t* first_seq, uint64_t* last_seq) {
+    if (nseg <= 0) return -1;
+    std::lock_guard<std::mutex> g(r->mu);
+    *first_seq = r->next_seq;
+    for (int i = 0, e = 0; i < nseg; i = e) {
+        if (msg_of) {
+            if (!next_group(msg_of, nseg, i, &e)) return -2;
+        } else {
+            e = nseg - i < kInlineSegments ? nseg : i + kInlineSegments;
+        }
+        const uint64_t k = r->next_seq;
+        ResidentSlot& sl = r->slots[k % kResidentSlots];
+        // the slot is free once its previous batch (k - slots) is done
+        if (k > kResidentSlots) {
+            const uint64_t need = k - kResidentSlots;
+            for (int spins = 0; __atomic_load_n(&sl.done, __ATOMIC_ACQUIRE) < need; ++spins) {
+                if (spins == 0) r->ring_full_waits.fetch_add(1, std::memory_order_relaxed);
+                if (spins > 2000000) return -1;  // ~seconds: the device stopped consuming
+                if ((spins & 1023) == 1023 && hipEventQuery(r->last_ev) == hipSuccess &&
+                    resident_launch_locked(r) != 0)
+                    return -1;
+                __builtin_ia32_pause();
+            }
+        }
+        SegBatch b;
+        const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of ? msg_of + i : nullptr);
+        memcpy(&sl.batch, &b, sizeof(b));
+        sl.crc_out = crc_out ? crc_out + (msg_of ? msg_of[i] : i) : nullptr;
+        sl.chunks = chunks;
+        __atomic_store_n(&sl.seq, k, __ATOMIC_RELEASE);
+        r->next_seq = k + 1;
+        r->batches.fetch_add(1, std::memory_order_relaxed);
+    }
+    *last_seq = r->next_seq - 1;
+    // Dekker with the instances' exit path: publish (above), full fence,
+    // then look whether the current instance announced its exit
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    const uint64_t exiting = __atomic_load_n(&r->ctl->exiting, __ATOMIC_SEQ_CST);
+    if (r->instance == 0 || exiting == r->instance) return resident_launch_locked(r);
+    return 0;
+}
+
+bool ResidentDone(ResidentRing* r, uint64_t first_seq, uint64_t last_seq) {
+    for (uint64_t s = first_seq; s <= last_seq; ++s) {
+        if (__atomic_load_n(&r->slots[s % kResidentSlots].done, __ATOMIC_ACQUIRE) < s) return false;
+    }
+    return true;
+}
+
+void ResidentKick(ResidentRing* r) {
+    std::lock_guard<std::mutex> g(r->mu);
+    if (r->last_ev && hipEventQuery(r->last_ev) != hipSuccess) return;  // an instance is still on the device
+    // nothing running: start one if a published batch is not done
+    for (uint64_t s = r->next_seq > kResidentSlots ? r->next_seq - kResidentSlots : 1; s < r->next_seq; ++s) {
+        if (__atomic_load_n(&r->slots[s % kResidentSlots].done, __ATOMIC_ACQUIRE) < s) {
+            resident_launch_locked(r);
+            return;
+        }
+    }
+}
+
+void ResidentShutdown() {
+    std::lock_guard<std::mutex> g(g_resident_mu);
+    for (ResidentRing* r : g_resident) {
+        if (!r) continue;
+        __atomic_store_n(&r->ctl->stop, 1ull, __ATOMIC_SEQ_CST);
+        hipStreamSynchronize(r->stream);  // every instance exits within its idle bound
+    }
+}
+
+ResidentStats GetResidentStats() {
+    ResidentStats s;
+    std::lock_guard<std::mutex> g(g_resident_mu);
+    for (ResidentRing* r : g_resident) {
+        if (!r) continue;
+        s.launches += r->launches.load(std::memory_order_relaxed);
+        s.batches += r->batches.load(std::memory_order_relaxed);
+        s.ring_full_waits += r->ring_full_waits.load(std::memory_order_relaxed);
+    }
+    return s;
+}
+
 }  // namespace gpu
 }  // namespace mrpc

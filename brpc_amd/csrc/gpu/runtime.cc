@@ -14,9 +14,11 @@
 
 #include "base/flags.h"
 #include "base/logging.h"
+#include "base/time.h"
 #include "fiber/butex.h"
 #include "fiber/fiber.h"
 #include "gpu/hbm_pool.h"
+#include "gpu/kernels.h"
 #include "rdma/rdma.h"
 
 DEFINE_int32(gpu_streams_per_device, 4, "HIP streams per device in the pool (<= GPU_MAX_HW_QUEUES)");
@@ -73,6 +75,10 @@ struct Waiter {
     hipEvent_t ev;
     std::atomic<int>* butex;
     int64_t* done_us;  // optional: when the poller saw the event complete
+    // resident-worker batches [first, last] instead of an event
+    ResidentRing* ring = nullptr;
+    uint64_t first = 0, last = 0;
+    int64_t since_us = 0;
 };
 
 class EventPoller {
@@ -138,8 +144,24 @@ private:
             }
             const size_t before = active.size();
             size_t keep = 0;
+            int64_t now_pass = 0;
             for (size_t i = 0; i < active.size(); ++i) {
-                hipError_t r = hipEventQuery(active[i].ev);
+                hipError_t r;
+                if (active[i].ring) {
+                    // plain reads of the ring's pinned done words
+                    if (!ResidentDone(active[i].ring, active[i].first, active[i].last)) {
+                        if (!now_pass) now_pass = monotonic_us();
+                        if (now_pass - active[i].since_us > 2000) {  // watchdog: no instance consuming?
+                            ResidentKick(active[i].ring);
+                            active[i].since_us = now_pass;
+                        }
+                        active[keep++] = active[i];
+                        continue;
+                    }
+                    r = hipSuccess;
+                } else {
+                    r = hipEventQuery(active[i].ev);
+                }
                 if (r == hipErrorNotReady) {
                     active[keep++] = active[i];
                     continue;
@@ -303,6 +325,16 @@ int WaitEvent(hipEvent_t ev) {
 
 void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us) {
     poller()->add(Waiter{ev, butex, done_us});
+}
+
+void WatchResident(ResidentRing* ring, uint64_t first_seq, uint64_t last_seq, std::atomic<int>* butex,
+                   int64_t* done_us) {
+    Waiter w{nullptr, butex, done_us};
+    w.ring = ring;
+    w.first = first_seq;
+    w.last = last_seq;
+    w.since_us = monotonic_us();
+    poller()->add(w);
 }
 
 hipEvent_t AcquireEvent() { return get_event(); }

@@ -11,6 +11,7 @@
 
 #include "base/time.h"
 #include "fiber/fiber.h"
+#include "gpu/copy_engine.h"
 #include "gpu/gpu.h"
 #include "gpu/kernels.h"
 
@@ -117,6 +118,33 @@ void bind_gpu_ops(py::module_& g) {
         for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
         check(gpu::LaunchBatchedCopy(segs.data(), (int)segs.size(), as_stream(stream)), "batched_copy");
     }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("stream") = 0);
+    // The copy engine itself (gpu/copy_engine.h): blocks until the batch it
+    // joined completed; with_crc returns one CRC32C per segment (or, with
+    // fold, one for the concatenation). A 0 dst only checksums.
+    g.def("engine_copy", [](const std::vector<uintptr_t>& srcs, const std::vector<uintptr_t>& dsts,
+                            const std::vector<uint64_t>& lens, int device, bool with_crc, bool fold) {
+        if (srcs.size() != lens.size() || dsts.size() != lens.size()) throw std::invalid_argument("size mismatch");
+        std::vector<gpu::Segment> segs(lens.size());
+        for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
+        std::vector<uint32_t> crcs(with_crc ? segs.size() : 0);
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::BatchedCopy(segs.data(), (int)segs.size(), device, with_crc ? crcs.data() : nullptr, fold);
+        }
+        check(rc, "engine_copy");
+        if (fold && !crcs.empty()) crcs.resize(1);
+        return crcs;
+    }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("device") = 0, py::arg("with_crc") = false,
+       py::arg("fold") = false);
+    g.def("resident_stats", [] {
+        const gpu::ResidentStats s = gpu::GetResidentStats();
+        py::dict d;
+        d["launches"] = s.launches;
+        d["batches"] = s.batches;
+        d["ring_full_waits"] = s.ring_full_waits;
+        return d;
+    });
     g.def("batched_copy_crc32c_launch", [](const std::vector<uintptr_t>& srcs, const std::vector<uintptr_t>& dsts,
                                            const std::vector<uint64_t>& lens, uintptr_t out, uintptr_t stream) {
         if (srcs.size() != lens.size() || dsts.size() != lens.size()) throw std::invalid_argument("size mismatch");

@@ -1,0 +1,16 @@
+#!/bin/bash
+set -u
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/u
+P="$GRAFT_REPO_ROOT/gpurun_out/u"
+export TMPDIR=/tmp
+run() { local name=$1; shift; env "$@" timeout -k 10 60 python benchmarks/profile_leg.py --no-profile --seconds 3 $LEGARGS > $P/$name.log 2>&1; local rc=$?; echo "$name rc=$rc $(grep -E '^leg|^copy|^resident' $P/$name.log | tr '\n' ' ')"; return $rc; }
+LEGARGS="--leg dev_64k" run dev_launch X=1 &&
+LEGARGS="--leg dev_64k" run dev_resident RESIDENT=1 &&
+LEGARGS="--leg dev_64k" run dev_resident_g8 RESIDENT=1 RESIDENT_GROUPS=8 &&
+LEGARGS="--leg gpu_handler" run h_launch X=1 &&
+LEGARGS="--leg gpu_handler" run h_resident RESIDENT=1 &&
+LEGARGS="--leg dev_64k --concurrency 1" run dev_qd1_launch X=1 &&
+LEGARGS="--leg dev_64k --concurrency 1" run dev_qd1_resident RESIDENT=1 &&
+LEGARGS="--leg gpu_handler --concurrency 1" run h_qd1_launch X=1 &&
+LEGARGS="--leg gpu_handler --concurrency 1" run h_qd1_resident RESIDENT=1
