@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--skip-sweep", action="store_true",
                     help="skip the rdma_performance-style size x queue-depth sweep (lending vs RCCL plane)")
     ap.add_argument("--sweep-seconds", type=float, default=0.4, help="timed seconds per sweep point")
+    ap.add_argument("--verbose-sweep", action="store_true", help="print HBM pool / free memory after each point")
     ap.add_argument("--stream-min-s", type=float, default=1.0, help="the stream leg is timed for at least this long")
     ap.add_argument("--requests-per-step-grpc", type=int, default=2000)
     ap.add_argument("--requests-per-step-fanout", type=int, default=500)
@@ -431,6 +432,17 @@ def main():
                 st = press.stats()
                 del press
                 ok = parallel.allreduce_sum(st["success"], topo)
+                if cuda and a.verbose_sweep:
+                    free_b, total_b = torch.cuda.mem_get_info(topo.device)
+                    hb = native.gpu.hbm_pool_stats(topo.device)
+                    xs = native.gpu.xgmi_stats()
+                    rs = parallel.rccl_stats()
+                    print("sweep %s %d qd%d: ok=%d err=%d last=%s | hbm live=%d fallback=%d | lent_out=%d | rccl %s"
+                          " | gpu_free=%.1f GiB" % (
+                              t, sz, qd, st["success"], st["error"], st["last_error"][:120], hb["live_blocks"],
+                              hb["fallback_allocs"], xs["lent_outstanding"],
+                              {k: v for k, v in rs.items() if v and k != "host_memory"}, free_b / 2**30),
+                          file=sys.stderr, flush=True)
                 sweep["points"].append({
                     "transport": t, "bytes": sz, "queue_depth": qd,
                     "kqps": round(ok / dt / 1e3, 2) if dt > 0 else 0.0,

@@ -14,6 +14,8 @@
 
 DEFINE_int32(hbm_arena_mb, 16384,
              "IPC-exportable HBM arena per device for RPC payload blocks (MiB; 288 GB HBM3E per MI355X)");
+DEFINE_int32(hbm_fallback_max_mb, 8192,
+             "dedicated hipMalloc blocks (arena exhausted) may hold at most this much HBM; beyond it allocations fail");
 DEFINE_int32(pinned_region_mb, 64, "pinned host memory is carved from hipHostMalloc regions of this size (MiB)");
 
 namespace mrpc {
@@ -60,7 +62,7 @@ struct Arena {
     hipIpcMemHandle_t handle;
     std::atomic<size_t> bump{0};
     FreeList lists[kNumClass];
-    std::atomic<int64_t> live_blocks{0}, live_bytes{0}, fallbacks{0}, splits{0};
+    std::atomic<int64_t> live_blocks{0}, live_bytes{0}, fallbacks{0}, splits{0}, fallback_bytes{0};
 };
 
 Arena g_arena[kMaxDev];
@@ -254,15 +256,28 @@ void* HbmAlloc(size_t n, int device) {
             return p;
         }
     }
-    // arena exhausted (or a block above 256 MiB): a dedicated allocation
+    // arena exhausted (or a block above 256 MiB): a dedicated allocation,
+    // bounded so a leak or a burst cannot take the whole GPU
+    const int64_t cap = (int64_t)FLAGS_hbm_fallback_max_mb << 20;
+    if (a.fallback_bytes.fetch_add((int64_t)n, std::memory_order_relaxed) + (int64_t)n > cap) {
+        a.fallback_bytes.fetch_sub((int64_t)n, std::memory_order_relaxed);
+        LOG_EVERY_SECOND(ERROR) << "HBM arena of device " << device << " exhausted and " << FLAGS_hbm_fallback_max_mb
+                                << " MiB of dedicated allocations in use: refusing " << n << " bytes";
+        return nullptr;
+    }
     a.fallbacks.fetch_add(1, std::memory_order_relaxed);
-    return Malloc(n, device);
+    LOG_EVERY_SECOND(WARNING) << "HBM arena of device " << device << " exhausted (" << a.live_bytes.load()
+                              << " bytes live): dedicated allocation of " << n << " bytes";
+    void* p = Malloc(n, device);
+    if (!p) a.fallback_bytes.fetch_sub((int64_t)n, std::memory_order_relaxed);
+    return p;
 }
 
 void HbmFree(void* p, size_t n, int device) {
     if (!p) return;
     if (ArenaOffset(p, device) < 0) {
         Free(p);
+        if (device >= 0 && device < kMaxDev) g_arena[device].fallback_bytes.fetch_sub((int64_t)n, std::memory_order_relaxed);
         return;
     }
     if (n == 0) n = 1;

@@ -322,7 +322,12 @@ struct PeerState {
     uint64_t announced_bytes = 0;     // cumulative, to this peer
     uint64_t credit = 0;              // cumulative, granted by this peer
     uint64_t consumed = 0;            // cumulative, from this peer (claimed/dropped)
+    std::vector<uint64_t> cancels;    // announced to this peer, then cancelled: tell it to drop them
 };
+
+// A header entry with this length cancels an earlier announcement of its
+// sequence (the receiver drops the payload instead of stashing it).
+const uint64_t kCancelLen = ~0ull;
 
 std::atomic<int64_t> g_sent{0}, g_sent_bytes{0}, g_recv{0}, g_recv_bytes{0}, g_discarded{0}, g_rounds{0},
     g_payload_rounds{0}, g_aborts{0}, g_credit_stalls{0}, g_expired{0}, g_recv_timeouts{0}, g_doorbells{0},
@@ -353,6 +358,8 @@ public:
     std::map<Key, Stashed> stash;
     std::map<Key, WaitSlot> waiting;
     std::map<Key, int64_t> discards;
+    std::map<Key, int64_t> lost;   // self payloads that found no memory to land in: their Recv fails
+    uint64_t self_moved = 0;       // cumulative self bytes landed (credit: vs peers[rank].consumed)
     bool idle = false, dead = false, stop = false;
     bool busy_next = false;        // some rank's round header asked for another round
     uint64_t completed_round = 0;  // poster only (read under mu by Send)
@@ -407,6 +414,12 @@ public:
             for (int i = 0; i < n; ++i) {
                 const Key k(src[i], seq[i]);
                 if (src[i] < 0 || src[i] >= world) {
+                    w.failed = true;
+                    continue;
+                }
+                auto l = lost.find(k);
+                if (l != lost.end()) {
+                    lost.erase(l);
                     w.failed = true;
                     continue;
                 }
@@ -472,12 +485,19 @@ public:
 
     void discard(int src, uint64_t seq, size_t len) {
         (void)len;
+        Buf drop;  // released after the lock
         std::lock_guard<std::mutex> g(mu);
+        discard_locked(src, seq, &drop);
+    }
+
+    // (mu held) drop payload (src, seq) now if it landed, else when it does
+    void discard_locked(int src, uint64_t seq, Buf* drop) {
         if (src < 0 || src >= world) return;
         const Key k(src, seq);
         auto s = stash.find(k);
         if (s != stash.end()) {
             consume_locked(src, s->second.len);
+            drop->append(std::move(s->second.buf));
             stash.erase(s);
             g_discarded.fetch_add(1, std::memory_order_relaxed);
             return;
@@ -498,7 +518,16 @@ public:
                 return;
             }
         }
-        // already announced: the receiver's stash expires it
+        // already announced. To ourselves: drop it here (now or when it
+        // lands). To a peer: the next round header tells it to.
+        if (peer == rank) {
+            Buf dropped;
+            discard_locked(rank, seq, &dropped);
+            drop.append(std::move(dropped));
+        } else {
+            peers[peer].cancels.push_back(seq);
+        }
+        g_withdrawn.fetch_add(1, std::memory_order_relaxed);
     }
 
     // ---------------------------------------------------------------- poster
@@ -577,6 +606,10 @@ public:
             if (now - it->second > ttl) it = discards.erase(it);
             else ++it;
         }
+        for (auto it = lost.begin(); it != lost.end();) {
+            if (now - it->second > ttl) it = lost.erase(it);
+            else ++it;
+        }
     }
 
     // true when a peer process is gone (the plane is then aborted)
@@ -645,11 +678,35 @@ public:
                     ps.announced.push_back(std::move(ps.queued.front()));
                     ps.queued.pop_front();
                 }
-                my_busy |= !ps.announced.empty() || !ps.queued.empty();
+                // cancellations of earlier announcements ride in the same entries
+                size_t nc = 0;
+                while (nc < ps.cancels.size() && (int)h->n < kMaxEntries) {
+                    h->e[h->n].seq = ps.cancels[nc++];
+                    h->e[h->n].len = kCancelLen;
+                    ++h->n;
+                }
+                ps.cancels.erase(ps.cancels.begin(), ps.cancels.begin() + (long)nc);
+                my_busy |= !ps.announced.empty() || !ps.queued.empty() || !ps.cancels.empty();
             }
             self_send.clear();
             self_recv.clear();
-            for (size_t i = 0; i < 256 && !self_q.empty(); ++i) {
+            // self pairs: no credit (the stash is ours) but the same per-round
+            // byte bound as a peer's announcements, so a burst of large
+            // payloads does not land all at once
+            uint64_t self_bytes = 0;
+            const int self_max = std::max(1, std::min(FLAGS_rccl_round_payloads, 256));
+            const uint64_t window = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
+            for (int i = 0; i < self_max && !self_q.empty(); ++i) {
+                const uint64_t len = self_q.front().len;
+                if (i > 0 && self_bytes + len > (uint64_t)FLAGS_rccl_round_bytes) break;
+                // the same window a peer grants: landed-but-unclaimed self
+                // bytes stay under -rccl_window_bytes
+                const uint64_t unclaimed = self_moved - peers[rank].consumed;
+                if (unclaimed > 0 && unclaimed + len > window) {
+                    stalled = true;
+                    break;
+                }
+                self_bytes += len;
                 Payload s = std::move(self_q.front());
                 self_q.pop_front();
                 Payload r;
@@ -657,9 +714,22 @@ public:
                 r.len = s.len;
                 r.ptr = ops->alloc(s.len, &r.hold);
                 if (!r.ptr) {
-                    self_q.push_front(std::move(s));
-                    break;
+                    // no memory to land it: the payload is lost (its Recv
+                    // fails at once) rather than retried every round
+                    const Key k(rank, s.seq);
+                    auto w = waiting.find(k);
+                    if (w != waiting.end()) {
+                        Waiter* wt = w->second.w;
+                        waiting.erase(w);
+                        finish_locked(wt, false);
+                    } else {
+                        lost[k] = monotonic_us();
+                    }
+                    g_withdrawn.fetch_add(1, std::memory_order_relaxed);
+                    self_bytes -= len;
+                    continue;
                 }
+                self_moved += len;
                 self_send.push_back(std::move(s));
                 self_recv.push_back(std::move(r));
             }
@@ -743,11 +813,16 @@ public:
         }
         ops->release(marker);
         marker_live = false;
-        return complete_round(k, my_busy);
+        const int rc2 = complete_round(k, my_busy);
+        // nothing could move for want of credit: give the receivers a moment
+        // to consume instead of spinning empty rounds
+        if (rc2 == 0 && stalled && !payloads) usleep(50);
+        return rc2;
     }
 
     int complete_round(uint64_t k, bool my_busy) {
         std::vector<Buf> drop;  // released outside the lock
+        Buf drop_cancelled;
         std::lock_guard<std::mutex> g(mu);
         for (int p = 0; p < world; ++p) {
             for (Payload& s : moving_send[p]) {
@@ -781,6 +856,10 @@ public:
             ps.credit = std::max(ps.credit, h->credit);
             busy |= (h->flags & kBusy) != 0;
             for (uint32_t i = 0; i < h->n; ++i) {
+                if (h->e[i].len == kCancelLen) {  // the sender gave this payload up
+                    discard_locked(p, h->e[i].seq, &drop_cancelled);
+                    continue;
+                }
                 Payload in;
                 in.seq = h->e[i].seq;
                 in.len = (size_t)h->e[i].len;
@@ -1082,6 +1161,14 @@ Stats GetStats() {
     s.recv_timeouts = g_recv_timeouts.load();
     s.doorbells = g_doorbells.load();
     s.withdrawn = g_withdrawn.load();
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        if (g_plane) {
+            std::lock_guard<std::mutex> lk(g_plane->mu);
+            s.stash_payloads = (int64_t)g_plane->stash.size();
+            for (const auto& kv : g_plane->stash) s.stash_bytes += (int64_t)kv.second.len;
+        }
+    }
     s.world = World();
     s.host_memory = HostMemory();
     return s;

@@ -102,7 +102,8 @@ struct Stats {
     int64_t stash_expired = 0;   // received payloads nobody claimed in time
     int64_t recv_timeouts = 0;   // Recv calls that gave up
     int64_t doorbells = 0;       // idle -> busy transitions this rank rang
-    int64_t withdrawn = 0;       // Cancelled before announcement
+    int64_t withdrawn = 0;       // Cancelled (before announcement, or told to the receiver after)
+    int64_t stash_payloads = 0, stash_bytes = 0;  // landed, not yet claimed (now)
     int world = 0;
     bool host_memory = false;
 };

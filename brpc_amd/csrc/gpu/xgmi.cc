@@ -26,9 +26,11 @@
 #include "mrpc/proto/rpc_meta.pb.h"
 #include "net/socket.h"
 #include "policy/device_payload.h"
+#include "rpc/periodic_task.h"
 #include "var/var.h"
 
 DEFINE_int32(xgmi_slots, 65536, "release-table slots per process (max payload blocks lent at once)");
+DEFINE_int32(xgmi_reap_interval_ms, 5, "reap released lends this often while any are outstanding");
 DEFINE_int32(xgmi_reap_scan_mb, 256,
              "scan every outstanding lend for releases once they hold this many MiB (out-of-order releases "
              "of large payloads otherwise pin arena blocks until the 100 ms scan)");
@@ -469,6 +471,21 @@ void xgmi_cancel(const policy::DevicePayload& d) {
 
 }  // namespace
 
+namespace {
+// Reaps the lender every -xgmi_reap_interval_ms while it holds lends, so
+// blocks whose borrowers already released them go back to the arena even
+// when this process stops lending (otherwise they wait for the next lend).
+class LenderReaper : public PeriodicTask {
+public:
+    bool OnTriggeringTask(timespec* next) override {
+        if (g_lender && g_lender->outstanding() > 0) g_lender->reap(true);
+        *next = realtime_after_us((int64_t)std::max(1, FLAGS_xgmi_reap_interval_ms) * 1000);
+        return true;
+    }
+    void OnDestroyingTask() override { delete this; }
+};
+}  // namespace
+
 int EnableXgmiTransport(int device, std::string* error) {
     std::lock_guard<std::mutex> g(g_mu);
     if (g_lender) return g_lender->device() == device || device < 0 ? 0 : -1;
@@ -484,6 +501,7 @@ int EnableXgmiTransport(int device, std::string* error) {
     g_device = device;
     g_lender = l;
     SetHbmReclaimHook(ReapLentBlocks);
+    PeriodicTaskManager::StartTaskAt(new LenderReaper, realtime_after_us(10000));
     DeviceTransportHooks h;
     h.send = xgmi_send;
     h.recv = xgmi_recv;
@@ -540,6 +558,8 @@ int AttachXgmiPeer(Socket* sock, const policy::XgmiHello& hello, std::string* er
 void ReapLentBlocks() {
     if (g_lender) g_lender->reap(true);
 }
+
+
 
 XgmiStats GetXgmiStats() {
     XgmiStats s;

@@ -104,6 +104,7 @@ Socket::Socket()
       _auth_error(0),
       _auth_state(0),
       _plane_rank(kPlaneUnknown),
+      _dev_hello_butex(fiber::butex_create()),
       _auth_butex(fiber::butex_create()),
       _main_socket_id(INVALID_SOCKET_ID),
       _recycle_flag(false),
@@ -173,6 +174,7 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
     m->_auth_error.store(0);
     m->_auth_state.store(0);
     m->_plane_rank.store(kPlaneUnknown);
+    m->_dev_hello.store(0);
     m->_main_socket_id = INVALID_SOCKET_ID;
     m->_shared = std::make_shared<SharedPart>();
     m->_recycle_flag.store(false);
@@ -581,6 +583,39 @@ ssize_t Socket::SslRead(int fd, size_t size_hint) {
         if (produced > 0) return produced;
         if (ssl->peer_closed()) return 0;
     }
+}
+
+bool Socket::FightDeviceHello(int64_t timeout_us) {
+    int st = _dev_hello.load(std::memory_order_acquire);
+    if (st == 2) return false;
+    if (st == 0 && _dev_hello.compare_exchange_strong(st, 1, std::memory_order_acq_rel)) return true;
+    const int64_t deadline = monotonic_us() + timeout_us;
+    for (;;) {
+        const int seq = _dev_hello_butex->load(std::memory_order_acquire);
+        st = _dev_hello.load(std::memory_order_acquire);
+        if (st == 2) return false;
+        if (st == 0) {  // the negotiator gave up: take over
+            if (_dev_hello.compare_exchange_strong(st, 1, std::memory_order_acq_rel)) return true;
+            continue;
+        }
+        const int64_t now = monotonic_us();
+        if (now >= deadline || Failed()) return false;  // go ahead unnegotiated
+        timespec ts = realtime_after_us(deadline - now);
+        fiber::butex_wait(_dev_hello_butex, seq, &ts);
+    }
+}
+
+void Socket::DeviceHelloAnswered() {
+    if (_dev_hello.exchange(2, std::memory_order_acq_rel) == 2) return;
+    _dev_hello_butex->fetch_add(1, std::memory_order_release);
+    fiber::butex_wake_all(_dev_hello_butex);
+}
+
+void Socket::DeviceHelloAbandoned() {
+    int st = 1;
+    if (!_dev_hello.compare_exchange_strong(st, 0, std::memory_order_acq_rel)) return;
+    _dev_hello_butex->fetch_add(1, std::memory_order_release);
+    fiber::butex_wake_all(_dev_hello_butex);
 }
 
 void Socket::HandleEpollOut(SocketId id) {
@@ -1045,6 +1080,7 @@ int Socket::Revive(int new_fd) {
         }
         _auth_state.store(0);
         _plane_rank.store(kPlaneUnknown);
+        _dev_hello.store(0);
         const int old = _fd.exchange(-1);
         if (old >= 0) ::close(old);
         if (_versioned_ref.compare_exchange_strong(vref, make_vref(id_ver, vref_nref(vref)), std::memory_order_release)) {

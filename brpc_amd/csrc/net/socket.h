@@ -217,6 +217,15 @@ public:
     static const int kPlaneUnknown = -2;
     int plane_rank() const { return _plane_rank.load(std::memory_order_acquire); }
     void set_plane_rank(int r) { _plane_rank.store(r, std::memory_order_release); }
+    // Device-transport negotiation of a client connection: the first
+    // request carrying device payloads also carries the hellos (xGMI arena,
+    // RCCL plane rank); the others wait for its answer (at most timeout_us)
+    // so their payloads take the negotiated transport instead of being
+    // staged inline — N large payloads staged at once overcrowd the socket.
+    // Returns true for the request that negotiates.
+    bool FightDeviceHello(int64_t timeout_us);
+    void DeviceHelloAnswered();  // a response carried (or could have carried) the hellos
+    void DeviceHelloAbandoned(); // the negotiating request never went out
     std::shared_ptr<SocketConnection> conn() const { return _conn; }
     // TLS state (nullptr when the connection is plaintext).
     std::shared_ptr<SslSession> ssl_session() const;
@@ -285,6 +294,8 @@ private:
     std::atomic<int> _auth_error;
     std::atomic<int> _auth_state;  // 0 none, 1 fighting, 2 done
     std::atomic<int> _plane_rank;
+    std::atomic<int> _dev_hello{0};  // 0 not started, 1 in flight, 2 answered
+    std::atomic<int>* _dev_hello_butex = nullptr;
     std::atomic<int>* _auth_butex;
     // pooled connections: the main socket keeps a free list of sub sockets
     SocketId _main_socket_id;

@@ -397,6 +397,7 @@ void ProcessRpcResponse(InputMessageBase* msg_base) {
     if (msg->socket()->plane_rank() == Socket::kPlaneUnknown) {
         msg->socket()->set_plane_rank(meta.has_plane_hello() ? gpu::rccl::PeerRank(meta.plane_hello()) : -1);
     }
+    msg->socket()->DeviceHelloAnswered();  // requests waiting to learn the transports go ahead
     int saved_error = 0;
     bool device_payload_taken = false;
     const RpcResponseMeta& rm = meta.response();

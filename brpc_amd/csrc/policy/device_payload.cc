@@ -1,5 +1,7 @@
 #include "policy/device_payload.h"
 
+#include <atomic>
+
 #include <algorithm>
 #include <vector>
 
@@ -30,7 +32,18 @@ bool HasDeviceTransport(Socket* sock) {
     return sock && g_hooks.send && sock->transport() != nullptr;
 }
 
+std::atomic<int64_t> g_staged_payloads{0}, g_staged_bytes{0};
+
+void GetStagedStats(int64_t* payloads, int64_t* bytes) {
+    *payloads = g_staged_payloads.load(std::memory_order_relaxed);
+    *bytes = g_staged_bytes.load(std::memory_order_relaxed);
+}
+
 void StageDeviceBufToHost(const Buf& in, Buf* out) {
+    // device bytes that travel inline on the connection instead (no device
+    // transport to the peer, or the transport refused them)
+    g_staged_payloads.fetch_add(1, std::memory_order_relaxed);
+    g_staged_bytes.fetch_add((int64_t)in.size(), std::memory_order_relaxed);
     // batched path: every device block in one launch into pinned memory
     if (g_stage_hook) {
         Buf staged;
@@ -291,13 +304,22 @@ void ReleaseDeviceBlocks(Socket* sock, const DevicePayloads& descs) {
 
 bool SplitDevicePayload(Controller* cntl, bool request, const Buf& attachment, Buf* host_out, RpcMeta* meta,
                         Socket* sock) {
-    (void)request;
     if (!sock) sock = cntl->_pack_socket;
     std::string err;
     if (LendDeviceBlocks(sock, attachment, cntl->verify_device_payload(), host_out, meta->mutable_device_payload(),
                          &err) != 0) {
         cntl->SetFailed(EXGMI, "%s", err.c_str());
         return false;
+    }
+    if (request) {
+        if (meta->device_payload_size() > 0) {
+            if (!cntl->_packed_payloads) cntl->_packed_payloads.reset(new PackedPayloads);
+            DevicePayloads& d = cntl->_packed_payloads->descs;
+            d.Clear();
+            for (const DevicePayload& x : meta->device_payload()) d.Add()->CopyFrom(x);
+        } else if (cntl->_packed_payloads) {
+            cntl->_packed_payloads->descs.Clear();
+        }
     }
     return true;
 }

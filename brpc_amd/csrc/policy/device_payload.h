@@ -49,6 +49,8 @@ void SetDeviceTransportHooks(const DeviceTransportHooks& h);
 bool HasDeviceTransport(Socket* sock);
 
 // Copies every non-host block of `in` to host memory (appends to *out).
+// Device payloads staged inline on the connection so far (count, bytes).
+void GetStagedStats(int64_t* payloads, int64_t* bytes);
 void StageDeviceBufToHost(const Buf& in, Buf* out);
 // Batched staging implementation (gpu/device_handler.h), installed when a
 // device is enabled; returns non-zero to fall back to per-block copies.
@@ -56,6 +58,12 @@ void SetStageToHostHook(int (*fn)(const Buf& in, Buf* out));
 
 namespace policy {
 using DevicePayloads = pb::RepeatedPtrField<DevicePayload>;
+
+// A request's packed descriptors, kept by its controller until the write
+// is accepted (rpc/controller.h _packed_payloads).
+struct PackedPayloads {
+    DevicePayloads descs;
+};
 // Protocol-neutral core (baidu_std metas and STRM frames): lend the device
 // blocks of `in` into *descs (host blocks go to *host_out, positions are
 // relative to `in`); pull `descs` into *attachment, whose current content

@@ -371,6 +371,9 @@ static void* closed_loop(void* arg) {
         PressCall call;
         s->issue(w, seq++, &call, false);
         s->finish(&call);
+        // a refused write fails at once: back off instead of spinning the
+        // worker (which would starve the fibers that drain the socket)
+        if (call.cntl.ErrorCode() == EOVERCROWDED) fiber::usleep(200);
     }
     return nullptr;
 }

@@ -23,6 +23,7 @@
 #include "pb/descriptor.h"
 #include "pb/parser.h"
 #include "gpu/xgmi.h"
+#include "policy/device_payload.h"
 #include "gpu/rccl_plane.h"
 #include "rdma/rdma.h"
 #include "mrpc/proto/echo.pb.h"
@@ -531,6 +532,10 @@ PYBIND11_MODULE(_native, m) {
         d["peer_access_enabled"] = s.peer_access_enabled;
         d["attach_failures"] = s.attach_failures;
         d["peer_maps"] = s.peer_maps;
+        int64_t staged = 0, staged_bytes = 0;
+        GetStagedStats(&staged, &staged_bytes);
+        d["staged_payloads"] = staged;
+        d["staged_bytes"] = staged_bytes;
         const gpu::CopyEngineStats c = gpu::GetCopyEngineStats();
         d["copy_submits"] = c.submits;
         d["copy_launches"] = c.launches;
@@ -620,6 +625,8 @@ PYBIND11_MODULE(_native, m) {
         d["recv_timeouts"] = s.recv_timeouts;
         d["doorbells"] = s.doorbells;
         d["withdrawn"] = s.withdrawn;
+        d["stash_payloads"] = s.stash_payloads;
+        d["stash_bytes"] = s.stash_bytes;
         d["world"] = s.world;
         d["host_memory"] = s.host_memory;
         return d;

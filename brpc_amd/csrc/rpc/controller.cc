@@ -3,6 +3,7 @@
 #include <cerrno>
 #include <cstdarg>
 
+#include "base/flags.h"
 #include "base/logging.h"
 #include "base/time.h"
 #include "base/util.h"
@@ -17,6 +18,11 @@
 #include "rpc/retry_policy.h"
 #include "rpc/server.h"
 #include "rpc/span.h"
+#include "policy/device_payload.h"
+
+DEFINE_int32(device_hello_wait_ms, 200,
+             "requests with device payloads wait at most this long for the connection's transport negotiation "
+             "(another request's hello round trip) before staging their payloads inline");
 
 namespace mrpc {
 
@@ -419,10 +425,18 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
             return;
         }
     }
+    // Device payloads on a connection whose transports are not negotiated
+    // yet: one request negotiates, the others wait for its answer.
+    bool hello_negotiator = false;
+    if (_use_device_transport && !sock->transport() && sock->plane_rank() == Socket::kPlaneUnknown &&
+        !_request_attachment.all_host_accessible()) {
+        hello_negotiator = sock->FightDeviceHello((int64_t)FLAGS_device_hello_wait_ms * 1000);
+    }
     _protocol->pack_request(&packet, cid.value, _method, this, _request_buf, auth);
     _pack_socket = nullptr;
     if (_error_code != 0) {
         if (_auth_winner) sock->ResetAuthentication();
+        if (hello_negotiator) sock->DeviceHelloAbandoned();
         const int ec = _error_code;
         const std::string et = _error_text;
         fiber::call_id_unlock(_correlation_id);
@@ -438,7 +452,13 @@ void Controller::IssueRPC(int64_t start_realtime_us) {
     wopt.auth_winner = _auth_winner;
     // Errors of Write() are delivered through call_id_error(cid), which is
     // queued while we hold the lock and handled at unlock.
-    sock->Write(&packet, &wopt);
+    if (sock->Write(&packet, &wopt) != 0) {
+        // refused (overcrowded / failed socket): the peer never sees the
+        // meta, so give back the lent blocks and withdraw plane payloads
+        if (_packed_payloads && _packed_payloads->descs.size() > 0) policy::CancelDeviceBlocks(_packed_payloads->descs);
+        if (hello_negotiator) sock->DeviceHelloAbandoned();
+    }
+    if (_packed_payloads) _packed_payloads->descs.Clear();
     if (_span) _span->sent_real_us = realtime_us();
     fiber::call_id_unlock(cid);
 }

@@ -39,6 +39,9 @@ class ProgressiveSink;
 class StreamCreator;
 class MongoContext;
 struct Protocol;
+namespace policy {
+struct PackedPayloads;
+}  // namespace policy
 typedef uint64_t StreamId;
 
 // Server-side per-connection / per-call user data factory hooks.
@@ -240,6 +243,10 @@ public:
     Span* _span = nullptr;
     uint64_t _trace_id = 0, _span_id = 0, _parent_span_id = 0;
     bool _verify_device_payload = false;
+    // device payloads described in the request being written (lent blocks,
+    // RCCL plane sequences): cancelled when the write is refused, since the
+    // receiver will never see their meta
+    std::unique_ptr<policy::PackedPayloads> _packed_payloads;
     bool _read_progressively = false;
     ProgressiveReader* _progressive_reader = nullptr;
     std::shared_ptr<ProgressiveAttachment> _progressive_attachment;

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--window", type=int, default=0, help="-rccl_window_bytes (0: default)")
     ap.add_argument("--out-dir", default="", help="write rank<N>.json here instead of stdout")
+    ap.add_argument("--overcrowd-test", action="store_true",
+                    help="after the legs, refuse most writes (tiny -socket_max_unwritten_bytes): payloads queued "
+                         "for refused requests must be withdrawn or dropped at the receiver, never stashed")
     ap.add_argument("--abort-test", action="store_true",
                     help="after the legs, rank 1 aborts the plane under traffic; every rank must notice "
                          "within a second and keep serving through the fallback")
@@ -52,6 +55,36 @@ def main():
                             "sent_payloads": s1["sent_payloads"] - s0["sent_payloads"],
                             "recv_payloads": s1["recv_payloads"] - s0["recv_payloads"],
                             "credit_stalls": s1["credit_stalls"] - s0["credit_stalls"]})
+        del p
+        parallel.barrier(topo)
+    if a.overcrowd_test:
+        import time
+        p = native.Press({"server": others[0], "fanout_servers": ",".join(others), "concurrency": a.concurrency,
+                          "attachment_size": 1 << 20, "timeout_ms": 5000, "max_retry": 0})
+        p.run_requests(50)  # connections up and their plane hellos answered
+        p.reset_stats()
+        s0 = parallel.rccl_stats()
+        native.set_flag("socket_max_unwritten_bytes", "1")
+        p.run_requests(300)
+        st = p.stats()
+        del p
+        native.set_flag("socket_max_unwritten_bytes", str(64 << 20))
+        parallel.barrier(topo)
+        # the cancellations ride the next rounds; give them a moment
+        deadline = time.perf_counter() + 5
+        while parallel.rccl_stats()["stash_payloads"] and time.perf_counter() < deadline:
+            time.sleep(0.01)
+        s1 = parallel.rccl_stats()
+        out["overcrowd_leg"] = {"success": st["success"], "error": st["error"], "last_error": st["last_error"],
+                                "withdrawn": s1["withdrawn"] - s0["withdrawn"],
+                                "discarded": s1["discarded"] - s0["discarded"],
+                                "stash_payloads": s1["stash_payloads"], "stash_bytes": s1["stash_bytes"]}
+        parallel.barrier(topo)
+        p = native.Press({"server": others[0], "fanout_servers": ",".join(others), "concurrency": a.concurrency,
+                          "attachment_size": 65536, "check_echo": True})
+        p.run_requests(100)
+        st = p.stats()
+        out["after_overcrowd_leg"] = {"success": st["success"], "error": st["error"]}
         del p
         parallel.barrier(topo)
     if a.abort_test:

@@ -80,3 +80,18 @@ def test_plane_abort_propagates_to_every_rank():
         # over the fallback
         assert o["abort_leg"]["success"] > 0 and o["abort_leg"]["error"] <= 3 * 50, o
         assert o["after_abort_leg"]["error"] == 0 and o["after_abort_leg"]["success"] == 100, o
+
+
+def test_plane_refused_writes_leave_nothing_stashed():
+    # with a 1-byte socket budget most requests are refused after their
+    # payloads were queued on the plane: the controller cancels them, the
+    # plane withdraws the unannounced ones and tells receivers to drop the
+    # announced ones, so no receiver hoards payloads nobody will claim
+    outs = _run(2, 29654, "--overcrowd-test", "--sizes", "65536", "--calls", "100")
+    for o in outs:
+        leg = o["overcrowd_leg"]
+        assert leg["error"] > 0, leg
+        assert leg["stash_payloads"] == 0 and leg["stash_bytes"] == 0, leg
+        assert o["after_overcrowd_leg"] == {"success": 100, "error": 0}, o
+        assert o["aborts"] == 0, o
+    assert sum(o["overcrowd_leg"]["withdrawn"] for o in outs) > 0, [o["overcrowd_leg"] for o in outs]
