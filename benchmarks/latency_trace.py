@@ -48,7 +48,9 @@ def main():
     from brpc_amd import native
     from brpc_amd.models import start_echo_server
     native.set_flag("fiber_concurrency", str(a.workers))
-    if torch.cuda.is_available():
+    if "L3_DOMAIN" in os.environ:
+        native.set_flag("cpu_l3_domain", os.environ["L3_DOMAIN"])
+    elif torch.cuda.is_available():
         from brpc_amd.parallel.placement import choose_l3_domain
         l3, _ = choose_l3_domain(0, 1, 0, torch.cuda.device_count())
         if l3 >= 0:

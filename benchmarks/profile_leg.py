@@ -35,7 +35,8 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", default="gpu_handler",
-                    choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps"])
+                    choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps", "grpc_cpu",
+                             "grpc_gpu"])
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--workers", type=int, default=12)
@@ -77,6 +78,11 @@ def main():
         o["request_size"] = 32
     if a.leg == "lat_100qps":
         o.update({"qps": 100.0, "concurrency": 1, "request_size": 32})
+    if a.leg.startswith("grpc"):
+        # the bench's gRPC + snappy leg: 64 KiB protobuf body, snappy both ways
+        o.update({"request_size": 65536, "protocol": "h2:grpc", "request_compress_type": 1})
+        if a.leg == "grpc_gpu":
+            native.gpu.enable_snappy(dev, 16384)
     p = native.Press(o)
     p.run_for(0.5)
     p.reset_stats()

@@ -37,8 +37,12 @@ struct PinnedArray {
 
 struct CBatch {
     std::vector<CodecRequest*> reqs;
-    std::vector<size_t> comp_first, decomp_first, scan_row;
+    std::vector<size_t> comp_first, decomp_first, stream_first, scan_row;
     PinnedArray<SnappyJob> comp_jobs, decomp_jobs;
+    PinnedArray<SnappyStream> stream_jobs;
+    PinnedArray<int> stream_err, piece_err;
+    SnappyPiece* pieces = nullptr;  // HBM: written by the split kernel, read by the piece decoder
+    size_t pieces_cap = 0;
     PinnedArray<uint32_t> comp_len, decomp_len;
     PinnedArray<int> comp_err, decomp_err;
     PinnedArray<PbScanJob> scan_jobs;
@@ -75,15 +79,20 @@ CBatch* new_batch(Engine& e) {
 // Lay the batch's requests out in its pinned tables and issue one stream
 // sequence; false when nothing could be launched.
 bool launch(CBatch* b, int device) {
-    size_t ncomp = 0, ndecomp = 0, nscan = 0;
-    uint32_t comp_max = 1, decomp_max = 1;
+    size_t ncomp = 0, ndecomp = 0, nscan = 0, nstreams = 0, npieces = 0;
+    uint32_t comp_max = 1, decomp_max = 1, piece_limit = 0;
     std::vector<Segment> h2d, d2h;
     b->comp_first.clear();
     b->decomp_first.clear();
+    b->stream_first.clear();
     b->scan_row.clear();
     for (CodecRequest* r : b->reqs) {
         b->comp_first.push_back(ncomp);
         b->decomp_first.push_back(ndecomp);
+        b->stream_first.push_back(nstreams);
+        nstreams += r->streams.size();
+        for (const SnappyStream& st : r->streams) npieces += st.max_pieces;
+        if (!r->streams.empty()) piece_limit = std::max(piece_limit, r->stream_piece_limit);
         b->scan_row.push_back(r->want_scan ? nscan : (size_t)-1);
         ncomp += r->comp.size();
         ndecomp += r->decomp.size();
@@ -96,14 +105,30 @@ bool launch(CBatch* b, int device) {
     if (!b->comp_jobs.reserve(ncomp) || !b->comp_len.reserve(ncomp) || !b->comp_err.reserve(ncomp) ||
         !b->decomp_jobs.reserve(ndecomp) || !b->decomp_len.reserve(ndecomp) || !b->decomp_err.reserve(ndecomp) ||
         !b->scan_jobs.reserve(nscan) || !b->scan_fields.reserve(nscan * 2 * kCodecScanFields) ||
-        !b->scan_n.reserve(nscan)) {
+        !b->scan_n.reserve(nscan) || !b->stream_jobs.reserve(nstreams) || !b->stream_err.reserve(nstreams) ||
+        !b->piece_err.reserve(npieces)) {
         return false;
+    }
+    if (npieces > b->pieces_cap) {
+        if (b->pieces) HbmFree(b->pieces, b->pieces_cap * sizeof(SnappyPiece), device);
+        const size_t cap = std::max<size_t>(npieces, 256);
+        b->pieces = static_cast<SnappyPiece*>(HbmAlloc(cap * sizeof(SnappyPiece), device));
+        b->pieces_cap = b->pieces ? cap : 0;
+        if (!b->pieces) return false;
     }
     for (size_t i = 0; i < b->reqs.size(); ++i) {
         const CodecRequest* r = b->reqs[i];
         std::copy(r->comp.begin(), r->comp.end(), b->comp_jobs.p + b->comp_first[i]);
         std::copy(r->decomp.begin(), r->decomp.end(), b->decomp_jobs.p + b->decomp_first[i]);
         if (r->want_scan) b->scan_jobs.p[b->scan_row[i]] = r->scan;
+    }
+    for (size_t i = 0, g = 0, first = 0; i < b->reqs.size(); ++i) {
+        for (const SnappyStream& st : b->reqs[i]->streams) {
+            SnappyStream& d = b->stream_jobs.p[g++];
+            d = st;
+            d.first = (uint32_t)first;
+            first += st.max_pieces;
+        }
     }
     if (ncomp && SnappyCompressUsesScratch(comp_max)) {
         const size_t need = ncomp * SnappyCompressScratchPerBlock();
@@ -126,6 +151,16 @@ bool launch(CBatch* b, int device) {
     }
     if (rc == 0 && ndecomp) {
         rc = LaunchSnappyDecompress(b->decomp_jobs.p, (int)ndecomp, decomp_max, b->decomp_len.p, b->decomp_err.p, s);
+    }
+    if (rc == 0 && nstreams) {
+        // cut on the device, then small pieces (many waves per CU) and the
+        // 64 KiB fragments of CPU encoders in a second launch
+        const uint32_t small = std::min(piece_limit, kSnappyMaxBlock);
+        rc = LaunchSnappySplit(b->stream_jobs.p, (int)nstreams, small, b->pieces, b->stream_err.p, s);
+        if (rc == 0) rc = LaunchSnappyDecompressPieces(b->pieces, (int)npieces, 0, small, b->piece_err.p, s);
+        if (rc == 0 && small < kSnappyMaxBlock) {
+            rc = LaunchSnappyDecompressPieces(b->pieces, (int)npieces, small, kSnappyMaxBlock, b->piece_err.p, s);
+        }
     }
     if (rc == 0 && nscan) {
         rc = LaunchPbScanPtrs(b->scan_jobs.p, (int64_t)nscan, kCodecScanFields, b->scan_fields.p, b->scan_n.p, s);
@@ -196,6 +231,14 @@ int RunCodecRequest(CodecRequest* r, int device) {
         r->comp_err.assign(mine->comp_err.p + c0, mine->comp_err.p + c0 + r->comp.size());
         r->decomp_len.assign(mine->decomp_len.p + d0, mine->decomp_len.p + d0 + r->decomp.size());
         r->decomp_err.assign(mine->decomp_err.p + d0, mine->decomp_err.p + d0 + r->decomp.size());
+        r->stream_err.assign(r->streams.size(), 0);
+        for (size_t j = 0; j < r->streams.size(); ++j) {
+            const size_t g = mine->stream_first[idx] + j;
+            int code = mine->stream_err.p[g];
+            const SnappyStream& st = mine->stream_jobs.p[g];
+            for (uint32_t k = 0; code == 0 && k < st.max_pieces; ++k) code = mine->piece_err.p[st.first + k];
+            r->stream_err[j] = code;
+        }
         if (r->want_scan) {
             const size_t row = mine->scan_row[idx];
             const uint64_t* f = mine->scan_fields.p + row * 2 * kCodecScanFields;

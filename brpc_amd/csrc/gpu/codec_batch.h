@@ -3,7 +3,8 @@
 // engine (gpu/copy_engine.h): concurrent RPCs submit their codec work, one
 // submitter becomes the leader and issues everything that accumulated as ONE
 // sequence on one stream (staging copies, one compress launch, one
-// decompress launch, one pb_scan launch, copies back) with ONE event; every
+// stream-split launch, the decompress launches, one pb_scan launch, copies
+// back) with ONE event; every
 // submitter parks its fiber on that event. At 50 RPCs in flight this turns
 // ~4 launches + 1 event per body into a few per batch of bodies.
 #pragma once
@@ -22,6 +23,11 @@ struct CodecRequest {
     // codec jobs; pointers in the jobs are device-accessible
     std::vector<SnappyJob> comp, decomp;
     uint32_t comp_max_ulen = 0, decomp_max_ulen = 0;
+    // whole compressed streams cut into pieces on the device
+    // (snappy_split_kernel) and decoded piecewise, no host tag walk;
+    // SnappyStream::first is relative to this request (the batch rebases it)
+    std::vector<SnappyStream> streams;
+    uint32_t stream_piece_limit = 4096;
     // optional wire scan of one decoded message (kCodecScanFields rows)
     bool want_scan = false;
     PbScanJob scan{nullptr, 0};
@@ -31,6 +37,7 @@ struct CodecRequest {
     // results, filled before RunCodecRequest returns 0
     std::vector<uint32_t> comp_len, decomp_len;
     std::vector<int> comp_err, decomp_err;
+    std::vector<int> stream_err;  // 0, or the split / piece decode code
     std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields
     int32_t scan_nfields = -1;
 };

@@ -80,6 +80,39 @@ struct SnappyJob {
 // blocks run 5 waves per CU, 64 KiB blocks 2.
 int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, uint32_t* out_len_dev, int* err_dev,
                            hipStream_t s);
+// Whole raw streams of any length, cut on the device (no host tag walk):
+// one wave per stream walks its element headers and cuts it into pieces of
+// at most piece_limit uncompressed bytes whose copies stay inside the piece
+// (every fragmenting encoder's output: ours cuts at -gpu_snappy_block_kb,
+// CPU encoders at 64 KiB; a stream that does not cut at piece_limit is
+// retried at kSnappyMaxBlock). Pieces land in pieces[first, first +
+// max_pieces) (unused slots get ulen 0); stream_err[i] = 0 or a code
+// (malformed, longer than dst_cap, not cuttable). A piece is headerless: its
+// ulen is known, its src points into the stream.
+struct SnappyStream {
+    const void* src;  // whole compressed stream (device)
+    void* dst;        // output, dst_cap bytes (device-accessible)
+    uint32_t src_len, dst_cap;
+    uint32_t first, max_pieces;
+};
+struct SnappyPiece {
+    const void* src;
+    void* dst;
+    uint32_t src_len, ulen;
+};
+// Slots a stream of ulen bytes can need: consecutive pieces sum to more
+// than the limit, so there are at most 2*ceil(ulen/limit) of them.
+constexpr uint32_t SnappyMaxPieces(uint64_t ulen, uint32_t limit) {
+    return (uint32_t)(2 * ((ulen + limit - 1) / limit) + 1);
+}
+int LaunchSnappySplit(const SnappyStream* streams_dev, int n, uint32_t piece_limit, SnappyPiece* pieces_dev,
+                      int* stream_err_dev, hipStream_t s);
+// Decodes the pieces with lo < ulen <= hi (LDS per wave = hi, so small
+// pieces run many waves per CU; a second launch takes the large ones) and
+// writes their err (0 or a code); the launch with lo == 0 also writes 0 for
+// empty slots.
+int LaunchSnappyDecompressPieces(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
+                                 hipStream_t s);
 // Batched snappy compression: job.src = raw block (<= kSnappyMaxBlock),
 // job.dst = output with job.dst_cap >= SnappyMaxCompressedLength(src_len).
 // scratch: n * SnappyCompressScratchPerBlock() bytes of device memory.

@@ -87,31 +87,11 @@ __device__ __forceinline__ uint32_t window_byte(uint32_t win, uint32_t q) {
     return (d >> ((q & 3) * 8)) & 0xff;
 }
 
-__global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJob* __restrict__ jobs, int n,
-                                                                  uint32_t lds_cap, uint32_t* __restrict__ out_len,
-                                                                  int* __restrict__ err) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t buf[];
-    const int blk = blockIdx.x;
-    if (blk >= n) return;
-    const int lane = threadIdx.x;
-    const SnappyJob job = jobs[blk];
-    gbyte_c* in = as_global(job.src);
-    const uint32_t in_len = (uint32_t)job.src_len;
-    uint32_t wbase = 0;
-    uint32_t win = load_window(in, in_len, 0, lane);
-    // uncompressed length (varint, <= 5 bytes; all inside the first window)
-    uint32_t ulen = 0, ip = 0;
+// Decodes the elements of in[ip, in_len) into LDS buf[0, ulen) and streams
+// the result to dst; `win` holds the window at `wbase`. Returns 0 or a code.
+__device__ __forceinline__ int decode_elements(gbyte_c* in, uint32_t in_len, uint32_t ip, uint32_t wbase,
+                                               uint32_t win, uint32_t ulen, uint8_t* buf, void* dstp, int lane) {
     int bad = 0;
-    for (int shift = 0;; shift += 7) {
-        if (ip >= in_len || shift >= 35) {
-            bad = 1;
-            break;
-        }
-        const uint32_t c = window_byte(win, ip++);
-        ulen |= (c & 0x7f) << shift;
-        if (!(c & 0x80)) break;
-    }
-    if (!bad && (ulen > lds_cap || ulen > job.dst_cap)) bad = 2;
     uint32_t op = 0;
     while (!bad && ip < in_len) {
         if (ip + 5 > wbase + kWindow) {  // tag + up to 4 extra bytes must be in the window
@@ -190,27 +170,189 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJo
         __builtin_amdgcn_wave_barrier();
     }
     if (!bad && op != ulen) bad = 7;
-    if (bad) {
-        if (lane == 0) {
-            err[blk] = bad;
-            out_len[blk] = 0;
-        }
-        return;
-    }
+    if (bad) return bad;
     __syncthreads();
     // LDS -> HBM, 16 B per lane per step (1 KiB per wave instruction)
-    gbyte* dst = as_global(job.dst);
-    const bool aligned = ((uintptr_t)job.dst & 15) == 0;
+    gbyte* dst = as_global(dstp);
+    const bool aligned = ((uintptr_t)dstp & 15) == 0;
     const uint32_t vec_end = aligned ? (ulen & ~15u) : 0;
     for (uint32_t o = lane * 16; o < vec_end; o += kWave * 16) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         *reinterpret_cast<__attribute__((address_space(1))) u32x4*>(dst + o) = *reinterpret_cast<const u32x4*>(buf + o);
     }
     for (uint32_t o = vec_end + lane; o < ulen; o += kWave) dst[o] = buf[o];
-    if (lane == 0) {
-        out_len[blk] = ulen;
-        err[blk] = 0;
+    return 0;
+}
+
+__global__ void __launch_bounds__(kWave) snappy_decompress_kernel(const SnappyJob* __restrict__ jobs, int n,
+                                                                  uint32_t lds_cap, uint32_t* __restrict__ out_len,
+                                                                  int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t buf[];
+    const int blk = blockIdx.x;
+    if (blk >= n) return;
+    const int lane = threadIdx.x;
+    const SnappyJob job = jobs[blk];
+    gbyte_c* in = as_global(job.src);
+    const uint32_t in_len = (uint32_t)job.src_len;
+    uint32_t win = load_window(in, in_len, 0, lane);
+    // uncompressed length (varint, <= 5 bytes; all inside the first window)
+    uint32_t ulen = 0, ip = 0;
+    int bad = 0;
+    for (int shift = 0;; shift += 7) {
+        if (ip >= in_len || shift >= 35) {
+            bad = 1;
+            break;
+        }
+        const uint32_t c = window_byte(win, ip++);
+        ulen |= (c & 0x7f) << shift;
+        if (!(c & 0x80)) break;
     }
+    if (!bad && (ulen > lds_cap || ulen > job.dst_cap)) bad = 2;
+    if (!bad) bad = decode_elements(in, in_len, ip, 0, win, ulen, buf, job.dst, lane);
+    if (lane == 0) {
+        err[blk] = bad;
+        out_len[blk] = bad ? 0 : ulen;
+    }
+}
+
+// Headerless pieces cut by snappy_split_kernel; this launch takes the ones
+// with lo < ulen <= hi (hi = its LDS per wave).
+__global__ void __launch_bounds__(kWave) snappy_decompress_pieces_kernel(const SnappyPiece* __restrict__ pieces,
+                                                                         int n, uint32_t lo, uint32_t hi,
+                                                                         int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t buf[];
+    const int blk = blockIdx.x;
+    if (blk >= n) return;
+    const int lane = threadIdx.x;
+    const SnappyPiece pc = pieces[blk];
+    if (pc.ulen == 0) {
+        if (lo == 0 && lane == 0) err[blk] = 0;
+        return;
+    }
+    if (pc.ulen <= lo || pc.ulen > hi) return;
+    gbyte_c* in = as_global(pc.src);
+    const uint32_t win = load_window(in, pc.src_len, 0, lane);
+    const int bad = decode_elements(in, pc.src_len, 0, 0, win, pc.ulen, buf, pc.dst, lane);
+    if (lane == 0) err[blk] = bad;
+}
+
+// One wave per whole stream: walks the element headers only (literal bytes
+// are skipped, never loaded) and cuts the stream where the next element
+// would overflow the piece. A copy reaching before its piece's start fails
+// the cut; the walk is then redone at kSnappyMaxBlock (the fragment size of
+// CPU encoders). Every value is wave-uniform (readlane), lane 0 writes.
+__global__ void __launch_bounds__(kWave) snappy_split_kernel(const SnappyStream* __restrict__ streams, int n,
+                                                             uint32_t piece_limit, SnappyPiece* __restrict__ pieces,
+                                                             int* __restrict__ stream_err) {
+    const int sid = blockIdx.x;
+    if (sid >= n) return;
+    const int lane = threadIdx.x;
+    const SnappyStream st = streams[sid];
+    gbyte_c* in = as_global(st.src);
+    const uint32_t in_len = st.src_len;
+    SnappyPiece* const slots = pieces + st.first;
+    uint32_t win = load_window(in, in_len, 0, lane);
+    uint32_t ulen = 0, hdr = 0;
+    int bad = 0;
+    for (int shift = 0;; shift += 7) {
+        if (hdr >= in_len || shift >= 35) {
+            bad = 1;
+            break;
+        }
+        const uint32_t c = window_byte(win, hdr++);
+        ulen |= (c & 0x7f) << shift;
+        if (!(c & 0x80)) break;
+    }
+    if (!bad && ulen > st.dst_cap) bad = 2;
+    uint32_t np = 0;
+    for (int pass = 0; pass < 2 && !bad; ++pass) {
+        const uint32_t limit = pass == 0 ? min(piece_limit, kSnappyMaxBlock) : kSnappyMaxBlock;
+        if (pass == 1 && min(piece_limit, kSnappyMaxBlock) == kSnappyMaxBlock) {  // nothing larger to retry at
+            bad = 8;
+            break;
+        }
+        uint32_t ip = hdr, wbase = 0, upos = 0, pu = 0, pc = hdr;
+        if (pass == 1) win = load_window(in, in_len, 0, lane);
+        np = 0;
+        int cut_bad = 0;
+        while (ip < in_len) {
+            if (ip + 5 > wbase + kWindow) {
+                wbase = ip & ~3u;
+                win = load_window(in, in_len, wbase, lane);
+            }
+            const uint32_t q = ip - wbase;
+            const uint32_t dlo = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(q >> 2));
+            const uint32_t dhi = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(q >> 2) + 1);
+            const uint64_t x = ((((uint64_t)dhi) << 32) | dlo) >> ((q & 3) * 8);
+            const uint32_t tag = (uint32_t)x & 0xff;
+            const uint32_t ext = (uint32_t)(x >> 8);
+            const uint32_t elem = ip++;
+            uint32_t len, off = 0, skip;
+            const uint32_t kind = tag & 3;
+            if (kind == 0) {
+                len = (tag >> 2) + 1;
+                uint32_t nb = 0;
+                if (len > 60) {
+                    nb = len - 60;
+                    len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
+                }
+                skip = nb + len;
+            } else if (kind == 1) {
+                len = ((tag >> 2) & 7) + 4;
+                off = ((tag >> 5) << 8) | (ext & 0xff);
+                skip = 1;
+            } else {
+                len = (tag >> 2) + 1;
+                off = kind == 2 ? (ext & 0xffff) : ext;
+                skip = kind == 2 ? 2 : 4;
+            }
+            if (skip > in_len - ip || len > ulen - upos) {  // truncated element / longer than declared
+                bad = 3;
+                break;
+            }
+            if (upos - pu + len > limit) {
+                if (upos == pu || np >= st.max_pieces) {  // one element larger than a piece / out of slots
+                    cut_bad = 1;
+                    break;
+                }
+                if (lane == 0) slots[np] = SnappyPiece{(const uint8_t*)st.src + pc, (uint8_t*)st.dst + pu, elem - pc, upos - pu};
+                ++np;
+                pc = elem;
+                pu = upos;
+            }
+            if (kind != 0 && off - 1 >= upos - pu) {  // offset 0, or reaches before the piece
+                if (off - 1 >= upos) {
+                    bad = 6;  // before the stream: malformed at any limit
+                    break;
+                }
+                cut_bad = 1;
+                break;
+            }
+            ip += skip;
+            upos += len;
+        }
+        if (bad) break;
+        if (cut_bad) {
+            if (pass == 1) bad = 8;
+            continue;
+        }
+        if (upos != ulen) {
+            bad = 7;
+            break;
+        }
+        if (upos > pu) {
+            if (np >= st.max_pieces) {
+                bad = 9;
+                break;
+            }
+            if (lane == 0) slots[np] = SnappyPiece{(const uint8_t*)st.src + pc, (uint8_t*)st.dst + pu, in_len - pc, upos - pu};
+            ++np;
+        }
+        break;
+    }
+    if (bad) np = 0;
+    for (uint32_t k = np + lane; k < st.max_pieces; k += kWave) slots[k] = SnappyPiece{nullptr, nullptr, 0, 0};
+    if (lane == 0) stream_err[sid] = bad;
 }
 
 // ------------------------------------------------------------- compression
@@ -414,6 +556,24 @@ int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, 
     if (max_ulen > kSnappyMaxBlock) return -1;
     const uint32_t lds = (max_ulen + 4095) & ~4095u;  // LDS per wave; blocks larger than this fail with code 2
     hipLaunchKernelGGL(snappy_decompress_kernel, dim3(n), dim3(kWave), lds, s, jobs_dev, n, lds, out_len_dev, err_dev);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int LaunchSnappySplit(const SnappyStream* streams_dev, int n, uint32_t piece_limit, SnappyPiece* pieces_dev,
+                      int* stream_err_dev, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (piece_limit == 0) return -1;
+    hipLaunchKernelGGL(snappy_split_kernel, dim3(n), dim3(kWave), 0, s, streams_dev, n, piece_limit, pieces_dev,
+                       stream_err_dev);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int LaunchSnappyDecompressPieces(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
+                                 hipStream_t s) {
+    if (n <= 0) return 0;
+    if (hi == 0 || hi > kSnappyMaxBlock || lo >= hi) return -1;
+    const uint32_t lds = (hi + 4095) & ~4095u;
+    hipLaunchKernelGGL(snappy_decompress_pieces_kernel, dim3(n), dim3(kWave), lds, s, pieces_dev, n, lo, hi, err_dev);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -12,21 +12,22 @@
 //    one wave each straight into pinned host memory; the stream is
 //    one varint header + the blocks' element runs (a block never references
 //    another, so the concatenation is one valid stream).
-//  * decompress: the host walks the tag stream once to cut it into pieces of
-//    <= 4 KiB (device streams), else <= 64 KiB, uncompressed whose copies
-//    stay inside the piece (true for every fragmenting encoder, ours and
-//    google snappy); each piece gets its
-//    own varint header in a pinned staging buffer, snappy_decompress_kernel
-//    decodes all pieces in one launch straight into pinned output. A stream
-//    that cannot be cut that way falls back to the CPU codec.
+//  * decompress: the compressed blocks are copied to HBM as they are (no
+//    flattening); snappy_split_kernel walks the element headers on the
+//    device (one wave per stream) and cuts the stream into pieces of
+//    <= 4 KiB (device encoders), else <= 64 KiB (CPU encoders) uncompressed
+//    whose copies stay inside the piece, and the piece decoder rebuilds
+//    every piece in LDS, all in the same stream sequence. A stream that
+//    cannot be cut that way (or is malformed) falls back to the CPU codec.
 // Each direction is one stream-ordered sequence (copy, kernel) and ONE
 // fiber-friendly event wait, shared with every other RPC's codec work that
-// arrived meanwhile (gpu/codec_batch.h: one launch sequence per batch). Measured on MI355X (bench.py gRPC leg, 64 KiB
-// bodies, 50 in flight): 16 KiB blocks 12.9k QPS, 8 KiB 19.4k, 4 KiB 24.6k,
-// 1-2 KiB 25k (saturated by the per-call launch/wait overhead) vs 53k with
-// the CPU codec — the serial snappy format keeps one wave per block busy, so
-// per-RPC offload loses to the CPU on latency; it is opt-in
-// (EnableGpuSnappy) for bodies that are headed to the GPU anyway.
+// arrived meanwhile (gpu/codec_batch.h: one launch sequence per batch).
+// History on MI355X (bench.py gRPC leg, 64 KiB bodies, 50 in flight): one
+// launch + wait per call lost to the CPU codec (25k vs 53k QPS); with
+// cross-RPC batching the GPU codec wins (63k vs 46k QPS at 152 vs 261 host
+// CPU us per RPC, profiles/r3_bench_run7_checkpoint.json). It stays opt-in
+// (EnableGpuSnappy) with a body-size threshold: small bodies are faster on
+// the CPU than any launch.
 #include "gpu/snappy_offload.h"
 
 #include <hip/hip_runtime_api.h>
@@ -181,78 +182,20 @@ bool gpu_compress(const Buf& in, Buf* out) {
     return true;
 }
 
-// Cuts a raw snappy stream into pieces of <= kSnappyMaxBlock uncompressed
-// bytes that are self-contained. Returns false when impossible.
-struct Piece {
-    size_t comp_off, comp_len, ulen;
-};
-bool split_stream(const uint8_t* p, size_t n, size_t limit, size_t* total, size_t* hdr_len,
-                  std::vector<Piece>* pieces) {
-    uint64_t ulen = 0;
-    size_t i = 0;
-    for (int shift = 0; shift <= 35; shift += 7) {
-        if (i >= n) return false;
-        const uint8_t c = p[i++];
-        ulen |= (uint64_t)(c & 0x7f) << shift;
-        if (!(c & 0x80)) break;
-        if (shift == 35) return false;
+// Uncompressed length from the stream's varint preamble (the first <= 5
+// bytes, wherever the Buf's blocks are); false when malformed.
+bool read_preamble(const Buf& in, uint64_t* ulen) {
+    uint8_t h[5];
+    const size_t n = in.copy_to(h, std::min<size_t>(sizeof(h), in.size()));
+    uint64_t v = 0;
+    for (size_t i = 0; i < n; ++i) {
+        v |= (uint64_t)(h[i] & 0x7f) << (7 * i);
+        if (!(h[i] & 0x80)) {
+            *ulen = v;
+            return true;
+        }
     }
-    *total = ulen;
-    *hdr_len = i;
-    size_t piece_start_comp = i, piece_start_u = 0, upos = 0;
-    while (i < n) {
-        const size_t elem_start = i;
-        const uint8_t tag = p[i++];
-        size_t len = 0, off = 0;
-        bool literal = false;
-        switch (tag & 3) {
-        case 0: {
-            literal = true;
-            size_t l = tag >> 2;
-            if (l >= 60) {
-                const int nb = (int)l - 59;
-                if (i + nb > n) return false;
-                l = 0;
-                for (int k = 0; k < nb; ++k) l |= (size_t)p[i + k] << (8 * k);
-                i += nb;
-            }
-            len = l + 1;
-            if (i + len > n) return false;
-            break;
-        }
-        case 1:
-            if (i + 1 > n) return false;
-            len = 4 + ((tag >> 2) & 7);
-            off = ((size_t)(tag >> 5) << 8) | p[i];
-            i += 1;
-            break;
-        case 2:
-            if (i + 2 > n) return false;
-            len = 1 + (tag >> 2);
-            off = (size_t)p[i] | ((size_t)p[i + 1] << 8);
-            i += 2;
-            break;
-        default:
-            if (i + 4 > n) return false;
-            len = 1 + (tag >> 2);
-            off = (size_t)p[i] | ((size_t)p[i + 1] << 8) | ((size_t)p[i + 2] << 16) | ((size_t)p[i + 3] << 24);
-            i += 4;
-            break;
-        }
-        // start a new piece when this element would overflow the current one
-        if (upos - piece_start_u + len > limit) {
-            if (upos == piece_start_u) return false;  // one element larger than a piece
-            pieces->push_back(Piece{piece_start_comp, elem_start - piece_start_comp, upos - piece_start_u});
-            piece_start_comp = elem_start;
-            piece_start_u = upos;
-        }
-        if (!literal && (off == 0 || off > upos - piece_start_u)) return false;  // crosses the piece start
-        if (literal) i += len;
-        upos += len;
-    }
-    if (upos != ulen) return false;
-    if (upos > piece_start_u) pieces->push_back(Piece{piece_start_comp, n - piece_start_comp, upos - piece_start_u});
-    return true;
+    return false;
 }
 
 // Top-level field table of a decompressed message (pb_scan layout).
@@ -267,54 +210,30 @@ struct PbIndex {
 // batch (gpu/codec_batch.h): one launch sequence and one event per batch.
 bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     const int dev = g_device;
-    std::string flat = in.to_string();  // the tag walk needs contiguous bytes
-    size_t total = 0, hdr = 0;
-    std::vector<Piece> pieces;
-    // small pieces first (streams from device encoders: more waves, less
-    // latency), then the 64 KiB fragments every host encoder respects
-    const uint8_t* bytes = reinterpret_cast<const uint8_t*>(flat.data());
-    const size_t small = (size_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
-    if (!split_stream(bytes, flat.size(), small, &total, &hdr, &pieces)) {
-        pieces.clear();
-        if (!split_stream(bytes, flat.size(), kSnappyMaxBlock, &total, &hdr, &pieces)) return false;
-    }
-    if (total == 0) return true;
-    if (index && (total > FLAGS_max_body_size || total > 0xFFFFFFFFull)) return false;
-    // per-piece raw streams (own varint header) back to back, 16 B aligned
-    std::vector<size_t> soff(pieces.size());
-    size_t sbytes = 0;
-    for (size_t k = 0; k < pieces.size(); ++k) {
-        soff[k] = sbytes;
-        sbytes += (varint_len(pieces[k].ulen) + pieces[k].comp_len + 15) & ~(size_t)15;
-    }
-    PinnedBuf staged(sbytes), dst(total);
-    HbmTmp dstage(sbytes, dev), dbody(index ? total : 0, dev);
-    if (!staged.p || !dst.p || !dstage.p || (index && !dbody.p)) return false;
+    uint64_t total = 0;
+    if (!read_preamble(in, &total) || total > 0xFFFFFFFFull || in.size() > 0xFFFFFFFFull) return false;
+    if (total == 0) return in.size() == 1;
+    if (index && total > FLAGS_max_body_size) return false;
+    // the compressed blocks go to HBM as they are (pinned socket blocks read
+    // by the copy kernel, pageable ones bounced); the device cuts the stream
+    // into pieces and decodes them — the host never looks at a tag
+    const uint32_t limit = (uint32_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
+    const size_t pageable = pageable_bytes(in);
+    PinnedBuf bounce(pageable ? pageable : 1), dst(total);
+    HbmTmp dcomp(in.size(), dev), dbody(index ? total : 0, dev);
+    if (!bounce.p || !dst.p || !dcomp.p || (index && !dbody.p)) return false;
     char* out_base = index ? static_cast<char*>(dbody.p) : dst.p;
     CodecRequest req;
-    req.decomp.resize(pieces.size());
-    size_t upos = 0;
-    uint32_t max_ulen = 1;
-    for (size_t k = 0; k < pieces.size(); ++k) {
-        char* s = staged.p + soff[k];
-        const int h = put_varint(s, pieces[k].ulen);
-        memcpy(s + h, flat.data() + pieces[k].comp_off, pieces[k].comp_len);
-        req.decomp[k] = SnappyJob{static_cast<char*>(dstage.p) + soff[k], out_base + upos, h + pieces[k].comp_len,
-                                  pieces[k].ulen};
-        upos += pieces[k].ulen;
-        max_ulen = std::max<uint32_t>(max_ulen, (uint32_t)pieces[k].ulen);
-    }
-    req.decomp_max_ulen = max_ulen;
-    req.h2d.push_back(Segment{staged.p, dstage.p, sbytes});
+    gather_segments(in, static_cast<char*>(dcomp.p), bounce.p, &req.h2d);
+    req.streams.push_back(SnappyStream{dcomp.p, out_base, (uint32_t)in.size(), (uint32_t)total, 0,
+                                       SnappyMaxPieces(total, limit)});
+    req.stream_piece_limit = limit;
     if (index) {
         req.want_scan = true;
         req.scan = PbScanJob{static_cast<const uint8_t*>(dbody.p), total};
         req.d2h.push_back(Segment{dbody.p, dst.p, total});
     }
-    if (RunCodecRequest(&req, dev) != 0) return false;
-    for (size_t k = 0; k < pieces.size(); ++k) {
-        if (req.decomp_err[k] || req.decomp_len[k] != pieces[k].ulen) return false;
-    }
+    if (RunCodecRequest(&req, dev) != 0 || req.stream_err[0] != 0) return false;
     if (index) {
         index->nfields = req.scan_nfields;
         index->fields.swap(req.scan_fields);

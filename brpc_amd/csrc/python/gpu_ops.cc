@@ -167,6 +167,21 @@ void bind_gpu_ops(py::module_& g) {
                                           as_stream(stream)),
               "snappy_decompress");
     });
+    // streams: {src, dst, src_len|dst_cap<<32, first|max_pieces<<32}; pieces: 24 B each (device)
+    g.def("snappy_max_pieces", [](uint64_t ulen, uint32_t limit) { return gpu::SnappyMaxPieces(ulen, limit); });
+    g.def("snappy_piece_bytes", [] { return sizeof(gpu::SnappyPiece); });
+    g.def("snappy_split_launch", [](uintptr_t streams, int n, uint32_t limit, uintptr_t pieces, uintptr_t err,
+                                    uintptr_t stream) {
+        check(gpu::LaunchSnappySplit((const gpu::SnappyStream*)streams, n, limit, (gpu::SnappyPiece*)pieces, (int*)err,
+                                     as_stream(stream)),
+              "snappy_split");
+    });
+    g.def("snappy_decompress_pieces_launch", [](uintptr_t pieces, int n, uint32_t lo, uint32_t hi, uintptr_t err,
+                                                uintptr_t stream) {
+        check(gpu::LaunchSnappyDecompressPieces((const gpu::SnappyPiece*)pieces, n, lo, hi, (int*)err,
+                                                as_stream(stream)),
+              "snappy_decompress_pieces");
+    });
     g.def("snappy_compress_scratch_per_block", [] { return gpu::SnappyCompressScratchPerBlock(); });
     g.def("snappy_max_compressed_length", [](uint64_t n) { return gpu::SnappyMaxCompressedLength(n); });
     g.def("snappy_compress_launch", [](uintptr_t jobs, int n, uint32_t max_ulen, uintptr_t scratch, uintptr_t out_len,

@@ -74,6 +74,60 @@ def snappy_decompress(packed, offsets, sizes, out_sizes, out=None):
     return out[:total]
 
 
+def snappy_decompress_streams(packed, offsets, sizes, out_sizes, piece_limit=4096, out=None):
+    """Decompress whole raw snappy streams of any length: the device cuts
+    each stream into self-contained pieces (``snappy_split_kernel``, one wave
+    walking the element headers; <= piece_limit uncompressed bytes, else the
+    64 KiB fragments of CPU encoders) and decodes the pieces in parallel; no
+    host tag walk. Same arguments as ``snappy_decompress`` minus the 64 KiB
+    limit. Raises ValueError naming the streams the device refused."""
+    require_gpu_tensor(packed, "packed")
+    if packed.dtype != torch.uint8:
+        raise TypeError("packed must be uint8")
+    n = len(offsets)
+    if not (len(sizes) == n == len(out_sizes)):
+        raise ValueError("offsets/sizes/out_sizes length mismatch")
+    dev = packed.device
+    total = int(sum(out_sizes))
+    if out is None:
+        out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    elif out.numel() < total:
+        raise ValueError("out too small")
+    if n == 0:
+        return out[:0]
+    base_in, base_out = packed.data_ptr(), out.data_ptr()
+    rows, pos, first = [], 0, 0
+    for o, s, u in zip(offsets, sizes, out_sizes):
+        if o + s > packed.numel() or s >= 1 << 32 or u >= 1 << 32:
+            raise ValueError("stream out of range")
+        mp = int(native.gpu.snappy_max_pieces(int(u), piece_limit))
+        rows += [base_in + int(o), base_out + pos, int(s) | (int(u) << 32), first | (mp << 32)]
+        pos += int(u)
+        first += mp
+    streams_dev = torch.tensor(rows, dtype=torch.int64).to(dev)
+    pieces = torch.empty(first * int(native.gpu.snappy_piece_bytes()), dtype=torch.uint8, device=dev)
+    errs = torch.full((n + first,), -1, dtype=torch.int32, device=dev)  # [stream codes..., piece codes...]
+    small = min(piece_limit, MAX_BLOCK)
+    with torch.cuda.device(dev):
+        h = stream_handle(dev)
+        native.gpu.snappy_split_launch(streams_dev.data_ptr(), n, small, pieces.data_ptr(), errs.data_ptr(), h)
+        native.gpu.snappy_decompress_pieces_launch(pieces.data_ptr(), first, 0, small, errs.data_ptr() + 4 * n, h)
+        if small < MAX_BLOCK:
+            native.gpu.snappy_decompress_pieces_launch(pieces.data_ptr(), first, small, MAX_BLOCK,
+                                                       errs.data_ptr() + 4 * n, h)
+    e = errs.cpu().tolist()
+    bad, first = [], 0
+    for i, u in enumerate(out_sizes):
+        mp = int(native.gpu.snappy_max_pieces(int(u), piece_limit))
+        code = e[i] or next((c for c in e[n + first:n + first + mp] if c), 0)
+        if code:
+            bad.append((i, code))
+        first += mp
+    if bad:
+        raise ValueError("malformed or uncuttable snappy stream(s) %s" % bad[:8])
+    return out[:total]
+
+
 def snappy_compress(data, block=DEFAULT_BLOCK, compact=True):
     """Compress a uint8 device tensor on the GPU as independent snappy blocks
     of ``block`` bytes (the last one may be shorter), one launch for all.

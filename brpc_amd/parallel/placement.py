@@ -48,6 +48,24 @@ def l3_domains(cpus=None):
     return sorted(groups.items())
 
 
+def numa_nodes():
+    """{node: set of CPUs} from /sys/devices/system/node, or {} when unreadable."""
+    out = {}
+    base = "/sys/devices/system/node"
+    try:
+        names = os.listdir(base)
+    except OSError:
+        return out
+    for n in names:
+        if n.startswith("node") and n[4:].isdigit():
+            try:
+                with open("%s/%s/cpulist" % (base, n)) as f:
+                    out[int(n[4:])] = parse_cpulist(f.read())
+            except OSError:
+                pass
+    return out
+
+
 def gpu_numa(device, native=None):
     """(numa_node, set of local CPUs) of a GPU, or (-1, None) when unknown."""
     if device is None or device < 0:

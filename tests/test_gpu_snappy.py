@@ -101,6 +101,75 @@ def test_gpu_compress_round_trips_through_host_and_gpu(dev, kind, n):
         assert sum(sizes) <= host_size * 1.15, (sum(sizes), host_size)
 
 
+def _streams(dev, datas, comp):
+    from brpc_amd.ops import snappy_decompress_streams
+    packed = b"".join(comp)
+    offs, pos = [], 0
+    for c in comp:
+        offs.append(pos)
+        pos += len(c)
+    d = torch.frombuffer(bytearray(packed + b"\0"), dtype=torch.uint8).to(dev)
+    return snappy_decompress_streams(d, offs, [len(c) for c in comp], [len(x) for x in datas])
+
+
+@pytest.mark.parametrize("kind", ["random", "runs", "text", "mixed"])
+def test_device_split_decodes_whole_host_streams(dev, kind):
+    """Whole streams from the host encoder (64 KiB fragments, copies anywhere
+    inside a fragment): the 4 KiB cut fails and the device re-cuts at 64 KiB;
+    streams of any length, many per launch."""
+    from brpc_amd import native
+    sizes = [0, 1, 100, 4096, 4097, 65536, 65540, 200000, 1 << 20]
+    datas = [_corpus(kind, n, n + 3 * len(kind)) for n in sizes]
+    comp = [native.snappy_compress(x) for x in datas]
+    out = _streams(dev, datas, comp)
+    assert out.cpu().numpy().tobytes() == b"".join(datas)
+
+
+def test_device_split_cuts_device_streams_at_4k(dev):
+    """The RPC offload's own framing (independent 4 KiB blocks behind one
+    preamble) cuts at 4 KiB: pieces decode with 4 KiB of LDS per wave."""
+    from brpc_amd import native
+    from brpc_amd.ops import snappy_compress
+    datas = [_corpus("mixed", n, n) for n in (70000, 4096 * 16, 5000)]
+    comp = []
+    for x in datas:
+        t = torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev)
+        packed, offs, sizes, raw = snappy_compress(t, block=4096)
+        host = packed.cpu().numpy().tobytes()
+        body = b""
+        for o, sz, r in zip(offs, sizes, raw):  # strip each block's own preamble
+            h = 1 + (r >= 128) + (r >= 16384)
+            body += host[o + h:o + sz]
+        n, pre = len(x), bytearray()
+        while True:
+            pre.append((n & 0x7F) | (0x80 if n >= 0x80 else 0))
+            n >>= 7
+            if not n:
+                break
+        comp.append(bytes(pre) + body)
+        assert native.snappy_uncompress(comp[-1]) == x
+    assert _streams(dev, datas, comp).cpu().numpy().tobytes() == b"".join(datas)
+
+
+def test_device_split_rejects_bad_streams(dev):
+    from brpc_amd import native
+    good = native.snappy_compress(_corpus("text", 20000, 9))
+    bad_offset = bytearray(good)
+    bad_offset[-1] = 0xFF
+    cases = [
+        (bytes(bad_offset), 20000),
+        (good[:-3], 20000),  # truncated
+        (good, 19999),  # declared length larger than the output room
+        (b"\x05\x01\x00", 5),  # a copy first
+    ]
+    for comp, room in cases:
+        with pytest.raises(ValueError):
+            _streams(dev, [b"x" * room], [comp])
+    # a good stream next to a bad one still decodes when alone
+    assert _streams(dev, [b"x" * 0 + _corpus("text", 20000, 9)], [good]).cpu().numpy().tobytes() == \
+        _corpus("text", 20000, 9)
+
+
 def test_gpu_compress_32k_blocks_and_uncompacted_slots(dev):
     from brpc_amd.ops import snappy_compress, snappy_decompress
     data = _corpus("mixed", 3 << 20, 5)
@@ -136,10 +205,13 @@ def test_gpu_snappy_offload_is_standard_snappy():
             before = native.gpu.snappy_stats()
             c = native.compress(1, data)
             assert native.snappy_uncompress(c) == data
+            # the device's own 4 KiB-block stream, cut on the device at 4 KiB
+            assert native.decompress(1, c) == data
             assert native.decompress(1, native.snappy_compress(data)) == data
             after = native.gpu.snappy_stats()
             assert after["compress_calls"] == before["compress_calls"] + 1, (before, after)
-            assert after["decompress_calls"] == before["decompress_calls"] + 1, (before, after)
+            assert after["decompress_calls"] == before["decompress_calls"] + 2, (before, after)
+            assert after["fallbacks"] == before["fallbacks"], (before, after)
     finally:
         native.gpu.disable_snappy()
 

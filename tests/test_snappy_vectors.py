@@ -197,3 +197,46 @@ def test_gpu_decoder_rejects_illegal_streams(name, comp):
     d = torch.frombuffer(bytearray(comp), dtype=torch.uint8).to("cuda:0")
     with pytest.raises(ValueError):
         snappy_decompress(d, [0], [len(comp)], [max(ulen, 1)])
+
+
+@pytest.mark.gpu
+def test_gpu_device_split_known_answers_and_rejects():
+    """The same vectors through the device splitter + piece decoder (whole
+    streams, no host tag walk). The 2 MiB preamble example is one unbroken
+    chain of offset-16 copies: no 64 KiB fragment boundary can cut it, so
+    the device refuses it (the RPC codec then decodes on the CPU)."""
+    torch = pytest.importorskip("torch")
+    from brpc_amd.ops import snappy_decompress_streams
+    n = 2097150
+    big = [lit(b"0123456789abcdef")]
+    left = n - 16
+    while left:
+        k = min(64, left)
+        big.append(copy2(k, 16))
+        left -= k
+    comps = [c for _, c, _ in VALID]
+    raws = [r for _, _, r in VALID]
+    packed = b"".join(comps)
+    offs, pos = [], 0
+    for c in comps:
+        offs.append(pos)
+        pos += len(c)
+    d = torch.frombuffer(bytearray(packed), dtype=torch.uint8).to("cuda:0")
+    out = snappy_decompress_streams(d, offs, [len(c) for c in comps], [len(r) for r in raws])
+    assert bytes(out.cpu().numpy().tobytes()) == b"".join(raws)
+    chain = stream(n, *big)
+    d = torch.frombuffer(bytearray(chain), dtype=torch.uint8).to("cuda:0")
+    with pytest.raises(ValueError):
+        snappy_decompress_streams(d, [0], [len(chain)], [n])
+    for name, comp in INVALID:
+        ulen, shift, pos = 0, 0, 0
+        while True:
+            b = comp[pos]
+            pos += 1
+            ulen |= (b & 0x7F) << shift
+            shift += 7
+            if not b & 0x80:
+                break
+        d = torch.frombuffer(bytearray(comp), dtype=torch.uint8).to("cuda:0")
+        with pytest.raises(ValueError):
+            snappy_decompress_streams(d, [0], [len(comp)], [max(ulen, 1)])
