@@ -77,6 +77,8 @@ def parse():
                          "event poller and the RCCL plane poster watch for work as long before sleeping.")
     ap.add_argument("--latency-first", action="store_true",
                     help="take the 100-QPS latency sample before the throughput legs")
+    ap.add_argument("--no-latency-replace", action="store_true",
+                    help="keep the rank's L3 domain for the 100-QPS sample (default: re-probe and move)")
     ap.add_argument("--latency-sample-s", type=float, default=10.0,
                     help="seconds of the 100-QPS rpc_press latency sample (0: skip)")
     return ap.parse_args()
@@ -282,6 +284,14 @@ def main():
         # rpc_press -qps=100 -thread_num=1 analog: one caller, paced, 32 B
         if a.latency_sample_s <= 0:
             return None
+        moved = {}
+        if a.cpu_l3_domain == -2 and topo.device >= 0 and not a.no_latency_replace:
+            # other tenants' load on the host shifts over the minutes the
+            # legs take: probe the rank's domains again and move the rank
+            # to the one whose CPUs wake sleepers promptly
+            from brpc_amd.parallel.placement import rechoose_l3_domain  # noqa: E402
+            moved = rechoose_l3_domain(topo.local_rank, topo.local_world_size, topo.device,
+                                       torch.cuda.device_count() if torch.cuda.is_available() else 0)
         press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
                               "connection_type": "single"})
         parallel.barrier(topo)
@@ -298,7 +308,7 @@ def main():
                "p99_us": parallel.allreduce_max(st["p99_us"], topo),
                "p999_us": parallel.allreduce_max(st["p999_us"], topo),
                "avg_us": parallel.allreduce_max(st["avg_us"], topo),
-               "cpu_pct": parallel.allreduce_max(cpu_pct, topo)}
+               "cpu_pct": parallel.allreduce_max(cpu_pct, topo), "placement": moved}
         del press
         return out
 
@@ -741,6 +751,7 @@ def main():
             out["p50_us_at_100qps"] = lat["p50_us"]
             out["p999_us_at_100qps"] = lat["p999_us"]
             out["cpu_pct_at_100qps"] = round(lat["cpu_pct"], 1)
+            out["placement_at_100qps_rank0"] = lat["placement"]
             out["vs_baseline_p99_at_100qps"] = round(BASELINE_P99_US / lat["p99_us"], 4) if lat["p99_us"] else None
         print(json.dumps(out), flush=True)
     parallel.barrier(topo)

@@ -32,6 +32,44 @@ def pct(v, q):
     return v[min(len(v) - 1, int(q * len(v)))] if v else 0
 
 
+def thread_sched():
+    """{tid: (name, run_ns, runqueue_wait_ns, involuntary switches, cpu)} of this process."""
+    out = {}
+    base = "/proc/self/task"
+    for tid in os.listdir(base):
+        try:
+            with open("%s/%s/schedstat" % (base, tid)) as f:
+                run, wait, _ = (int(x) for x in f.read().split())
+            with open("%s/%s/comm" % (base, tid)) as f:
+                name = f.read().strip()
+            nonvol = 0
+            with open("%s/%s/status" % (base, tid)) as f:
+                for line in f:
+                    if line.startswith("nonvoluntary_ctxt_switches"):
+                        nonvol = int(line.split()[1])
+            with open("%s/%s/stat" % (base, tid)) as f:
+                cpu = int(f.read().rsplit(")", 1)[1].split()[36])
+            out[tid] = (name, run, wait, nonvol, cpu)
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
+def cpu_irq_ticks():
+    """{cpu: (irq + softirq ticks, total ticks)} from /proc/stat."""
+    out = {}
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    v = line.split()
+                    t = list(map(int, v[1:]))
+                    out[int(v[0][3:])] = (t[5] + t[6], sum(t))
+    except OSError:
+        pass
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=10.0)
@@ -75,7 +113,9 @@ def main():
     if not os.environ.get("NO_RPCZ"):
         native.set_flag("enable_rpcz", "true")
     p.reset_stats()
+    t0, q0 = thread_sched(), cpu_irq_ticks()
     p.run_for(a.seconds)
+    t1, q1 = thread_sched(), cpu_irq_ticks()
     native.set_flag("enable_rpcz", "false")
     st = p.stats()
     if dev >= 0:
@@ -119,6 +159,21 @@ def main():
     for k in PHASES:
         v = [r[1][k] for r in rows]
         print("%-10s %6d %6d %6d %6d" % (k, pct(v, .5), pct(v, .9), pct(v, .99), max(v) if v else 0))
+    # were our threads runnable but not running (preempted by other tasks),
+    # and how much of their CPUs went to interrupts?
+    rows_t = []
+    for tid, (name, run, wait, nonvol, cpu) in t1.items():
+        b = t0.get(tid)
+        if b:
+            rows_t.append((wait - b[2], run - b[1], nonvol - b[3], name, cpu))
+    rows_t.sort(reverse=True)
+    print("sched: runqueue wait %.2f ms, run %.2f ms, involuntary switches %d over %d threads; worst: %s" % (
+        sum(r[0] for r in rows_t) / 1e6, sum(r[1] for r in rows_t) / 1e6, sum(r[2] for r in rows_t), len(rows_t),
+        ", ".join("%s@%d wait=%.2fms nonvol=%d" % (r[3], r[4], r[0] / 1e6, r[2]) for r in rows_t[:4])))
+    cpus = sorted(os.sched_getaffinity(0))
+    irq = [(q1[c][0] - q0[c][0]) / max(1, q1[c][1] - q0[c][1]) for c in cpus if c in q0 and c in q1]
+    print("irq+softirq share of our CPUs: mean %.2f%% max %.2f%%" % (100 * sum(irq) / max(1, len(irq)),
+                                                                   100 * max(irq + [0])))
     print("slowest calls:")
     slowest = sorted(rows, key=lambda r: -r[0])
     for latency, ph, _ in slowest[:a.top]:

@@ -9,6 +9,7 @@
 #pragma once
 
 #include <string>
+#include <vector>
 
 #include <time.h>
 
@@ -77,6 +78,22 @@ int set_concurrency(int n);  // can only grow
 int get_concurrency();
 // Start the runtime (idempotent). Called lazily by any start_*.
 int init_runtime();
+
+// Placement on shared hosts (fiber/cpu_probe.cc, fiber/runtime.cc).
+struct CpuWakeProbe {
+    int cpu = -1;
+    int64_t wakes = 0;  // -1: the CPU is not in our allowed set
+    int64_t late_p50_us = 0, late_p99_us = 0, late_max_us = 0;
+    int64_t late_over = 0;     // wake-ups later than the threshold
+    int64_t run_delay_us = 0;  // runnable but not running
+    int64_t nivcsw = 0;        // involuntary context switches
+};
+// One pinned thread per CPU sleeps period_us at a time for duration_ms.
+std::vector<CpuWakeProbe> ProbeCpuWake(const std::vector<int>& cpus, int duration_ms, int period_us,
+                                       int late_threshold_us);
+// Re-confines every thread of the process to L3 domain k (the same
+// indexing as -cpu_l3_domain) and records k in that flag; 0 on success.
+int RebindL3Domain(int k);
 // Tell runtime the process is about to quit (skip waiting for fibers).
 void about_to_quit();
 

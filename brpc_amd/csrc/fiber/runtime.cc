@@ -11,6 +11,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <unistd.h>
 
 #include <cerrno>
 #include <cstring>
@@ -807,28 +808,84 @@ std::vector<int> l3_domain_cpus(int k) {
     return order_by_core(it->second);
 }
 
-void apply_process_affinity() {
-    if (FLAGS_cpu_l3_domain < 0) return;
-    const std::vector<int> cpus = l3_domain_cpus(FLAGS_cpu_l3_domain);
-    if (cpus.empty()) return;
+// Confines every existing thread (the embedding interpreter, HIP's helpers,
+// our workers) and, through the calling thread's mask, every thread created
+// from now on to `cpus`; with -fiber_worker_cpu_offset, worker i goes back
+// to its own core of the new set.
+void confine_process(const std::vector<int>& cpus) {
     cpu_set_t set;
     CPU_ZERO(&set);
     for (int c : cpus) CPU_SET(c, &set);
-    // every existing thread (the embedding interpreter, HIP's helpers) and,
-    // through the calling thread's mask, every thread created from now on
+    const std::vector<int> order = order_by_core(cpus);
     if (DIR* d = opendir("/proc/self/task")) {
         while (dirent* e = readdir(d)) {
             const int tid = atoi(e->d_name);
-            if (tid > 0) sched_setaffinity(tid, sizeof(set), &set);
+            if (tid <= 0) continue;
+            int worker = -1;
+            if (FLAGS_fiber_worker_cpu_offset >= 0 && !order.empty()) {
+                char path[64], name[32] = {0};
+                snprintf(path, sizeof(path), "/proc/self/task/%d/comm", tid);
+                if (FILE* f = fopen(path, "r")) {
+                    if (fscanf(f, "mrpc_worker%d", &worker) != 1) worker = -1;
+                    fclose(f);
+                }
+                (void)name;
+            }
+            if (worker >= 0) {
+                cpu_set_t one;
+                CPU_ZERO(&one);
+                CPU_SET(order[(size_t)(FLAGS_fiber_worker_cpu_offset + worker) % order.size()], &one);
+                sched_setaffinity(tid, sizeof(one), &one);
+            } else {
+                sched_setaffinity(tid, sizeof(set), &set);
+            }
         }
         closedir(d);
     }
     sched_setaffinity(0, sizeof(set), &set);
+}
+
+void apply_process_affinity() {
+    if (FLAGS_cpu_l3_domain < 0) return;
+    const std::vector<int> cpus = l3_domain_cpus(FLAGS_cpu_l3_domain);
+    if (cpus.empty()) return;
+    confine_process(cpus);
     LOG(INFO) << "fiber runtime confined to L3 domain " << FLAGS_cpu_l3_domain << " (" << cpus.size() << " CPUs from "
               << cpus.front() << ")";
 }
 
 }  // namespace
+
+int RebindL3Domain(int k) {
+    // the domains are indexed over the process's allowed CPUs, which the
+    // first confinement narrowed to one domain: index the host's CPUs
+    // (the cgroup's cpuset) instead
+    cpu_set_t all;
+    CPU_ZERO(&all);
+    if (FILE* f = fopen("/sys/fs/cgroup/cpuset.cpus.effective", "r")) {
+        char buf[4096];
+        if (fgets(buf, sizeof(buf), f)) {
+            for (char* tok = strtok(buf, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+                int a = 0, b = 0;
+                const int n = sscanf(tok, "%d-%d", &a, &b);
+                if (n == 1) b = a;
+                for (int c = a; n >= 1 && c <= b && c < CPU_SETSIZE; ++c) CPU_SET(c, &all);
+            }
+        }
+        fclose(f);
+    }
+    if (CPU_COUNT(&all) == 0) {
+        for (int c = 0; c < std::min<int>(CPU_SETSIZE, (int)sysconf(_SC_NPROCESSORS_CONF)); ++c) CPU_SET(c, &all);
+    }
+    if (sched_setaffinity(0, sizeof(all), &all) != 0) return -1;
+    const std::vector<int> cpus = l3_domain_cpus(k);
+    if (cpus.empty()) return -1;
+    confine_process(cpus);
+    FLAGS_cpu_l3_domain = k;
+    LOG(INFO) << "fiber runtime re-confined to L3 domain " << k << " (" << cpus.size() << " CPUs from "
+              << cpus.front() << ")";
+    return 0;
+}
 
 // CPUs of the (possibly confined) affinity mask, physical cores first.
 static const std::vector<int>& cpu_order_by_core() {

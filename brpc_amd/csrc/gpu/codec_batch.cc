@@ -37,7 +37,9 @@ struct PinnedArray {
 
 struct CBatch {
     std::vector<CodecRequest*> reqs;
-    std::vector<size_t> comp_first, decomp_first, stream_first, scan_row;
+    std::vector<size_t> comp_first, decomp_first, stream_first, piece_first, scan_row;
+    PinnedArray<SnappyPiece> piece_jobs;
+    PinnedArray<int> piece_job_err;
     PinnedArray<SnappyJob> comp_jobs, decomp_jobs;
     PinnedArray<SnappyStream> stream_jobs;
     PinnedArray<int> stream_err, piece_err;
@@ -79,17 +81,21 @@ CBatch* new_batch(Engine& e) {
 // Lay the batch's requests out in its pinned tables and issue one stream
 // sequence; false when nothing could be launched.
 bool launch(CBatch* b, int device) {
-    size_t ncomp = 0, ndecomp = 0, nscan = 0, nstreams = 0, npieces = 0;
-    uint32_t comp_max = 1, decomp_max = 1, piece_limit = 0;
+    size_t ncomp = 0, ndecomp = 0, nscan = 0, nstreams = 0, npieces = 0, nhpieces = 0;
+    uint32_t comp_max = 1, decomp_max = 1, piece_limit = 0, hpiece_max = 1;
     std::vector<Segment> h2d, d2h;
     b->comp_first.clear();
     b->decomp_first.clear();
     b->stream_first.clear();
+    b->piece_first.clear();
     b->scan_row.clear();
     for (CodecRequest* r : b->reqs) {
         b->comp_first.push_back(ncomp);
         b->decomp_first.push_back(ndecomp);
         b->stream_first.push_back(nstreams);
+        b->piece_first.push_back(nhpieces);
+        nhpieces += r->pieces.size();
+        hpiece_max = std::max(hpiece_max, r->pieces_max_ulen);
         nstreams += r->streams.size();
         for (const SnappyStream& st : r->streams) npieces += st.max_pieces;
         if (!r->streams.empty()) piece_limit = std::max(piece_limit, r->stream_piece_limit);
@@ -106,7 +112,7 @@ bool launch(CBatch* b, int device) {
         !b->decomp_jobs.reserve(ndecomp) || !b->decomp_len.reserve(ndecomp) || !b->decomp_err.reserve(ndecomp) ||
         !b->scan_jobs.reserve(nscan) || !b->scan_fields.reserve(nscan * 2 * kCodecScanFields) ||
         !b->scan_n.reserve(nscan) || !b->stream_jobs.reserve(nstreams) || !b->stream_err.reserve(nstreams) ||
-        !b->piece_err.reserve(npieces)) {
+        !b->piece_err.reserve(npieces) || !b->piece_jobs.reserve(nhpieces) || !b->piece_job_err.reserve(nhpieces)) {
         return false;
     }
     if (npieces > b->pieces_cap) {
@@ -121,6 +127,7 @@ bool launch(CBatch* b, int device) {
         std::copy(r->comp.begin(), r->comp.end(), b->comp_jobs.p + b->comp_first[i]);
         std::copy(r->decomp.begin(), r->decomp.end(), b->decomp_jobs.p + b->decomp_first[i]);
         if (r->want_scan) b->scan_jobs.p[b->scan_row[i]] = r->scan;
+        std::copy(r->pieces.begin(), r->pieces.end(), b->piece_jobs.p + b->piece_first[i]);
     }
     for (size_t i = 0, g = 0, first = 0; i < b->reqs.size(); ++i) {
         for (const SnappyStream& st : b->reqs[i]->streams) {
@@ -151,6 +158,10 @@ bool launch(CBatch* b, int device) {
     }
     if (rc == 0 && ndecomp) {
         rc = LaunchSnappyDecompress(b->decomp_jobs.p, (int)ndecomp, decomp_max, b->decomp_len.p, b->decomp_err.p, s);
+    }
+    if (rc == 0 && nhpieces) {
+        rc = LaunchSnappyDecompressPieces(b->piece_jobs.p, (int)nhpieces, 0, std::min(hpiece_max, kSnappyMaxBlock),
+                                          b->piece_job_err.p, s);
     }
     if (rc == 0 && nstreams) {
         // cut on the device, then small pieces (many waves per CU) and the
@@ -231,6 +242,8 @@ int RunCodecRequest(CodecRequest* r, int device) {
         r->comp_err.assign(mine->comp_err.p + c0, mine->comp_err.p + c0 + r->comp.size());
         r->decomp_len.assign(mine->decomp_len.p + d0, mine->decomp_len.p + d0 + r->decomp.size());
         r->decomp_err.assign(mine->decomp_err.p + d0, mine->decomp_err.p + d0 + r->decomp.size());
+        const size_t p0 = mine->piece_first[idx];
+        r->piece_err.assign(mine->piece_job_err.p + p0, mine->piece_job_err.p + p0 + r->pieces.size());
         r->stream_err.assign(r->streams.size(), 0);
         for (size_t j = 0; j < r->streams.size(); ++j) {
             const size_t g = mine->stream_first[idx] + j;

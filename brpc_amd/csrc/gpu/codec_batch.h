@@ -28,6 +28,9 @@ struct CodecRequest {
     // SnappyStream::first is relative to this request (the batch rebases it)
     std::vector<SnappyStream> streams;
     uint32_t stream_piece_limit = 4096;
+    // headerless pieces cut on the host (pointers device-accessible)
+    std::vector<SnappyPiece> pieces;
+    uint32_t pieces_max_ulen = 0;
     // optional wire scan of one decoded message (kCodecScanFields rows)
     bool want_scan = false;
     PbScanJob scan{nullptr, 0};
@@ -38,6 +41,7 @@ struct CodecRequest {
     std::vector<uint32_t> comp_len, decomp_len;
     std::vector<int> comp_err, decomp_err;
     std::vector<int> stream_err;  // 0, or the split / piece decode code
+    std::vector<int> piece_err;
     std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields
     int32_t scan_nfields = -1;
 };

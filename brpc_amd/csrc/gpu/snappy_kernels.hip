@@ -236,14 +236,29 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_kernel(const S
     if (lane == 0) err[blk] = bad;
 }
 
-// One wave per whole stream: walks the element headers only (literal bytes
-// are skipped, never loaded) and cuts the stream where the next element
-// would overflow the piece. A copy reaching before its piece's start fails
-// the cut; the walk is then redone at kSnappyMaxBlock (the fragment size of
-// CPU encoders). Every value is wave-uniform (readlane), lane 0 writes.
+// One wave per whole stream, cut at exact multiples of the piece limit: a
+// fragmenting encoder (ours at -gpu_snappy_block_kb, CPU encoders at 64 KiB)
+// never lets an element span such a multiple or a copy reach back across
+// one, so every multiple is an element start and the pieces between them
+// decode independently. Both limits (piece_limit and 64 KiB) are checked in
+// the same walk.
+//
+// The walk is parallel where it can be: with `ip` at an element start, lane
+// j speculatively parses the element header at ip + j (bytes from a 256 B
+// VGPR window via ds_bpermute). Only the chain ip -> ip + size(ip) -> ... is
+// serial, and each step is one v_readlane of the precomputed sizes. Marked
+// lanes (the true element starts) then get their output position from a
+// wave prefix sum and run every check at once: truncation, offsets before
+// the stream, lengths past the declared size, elements spanning a cut,
+// copies reaching before their piece. Piece starts go to LDS; the slots are
+// written at the end.
+constexpr int kSplitMaxSmall = 4096;  // pieces at piece_limit (16 MiB at 4 KiB)
+constexpr int kSplitMaxBig = 1024;    // 64 KiB pieces (64 MiB)
 __global__ void __launch_bounds__(kWave) snappy_split_kernel(const SnappyStream* __restrict__ streams, int n,
                                                              uint32_t piece_limit, SnappyPiece* __restrict__ pieces,
                                                              int* __restrict__ stream_err) {
+    __shared__ uint32_t starts_small[kSplitMaxSmall];
+    __shared__ uint32_t starts_big[kSplitMaxBig];
     const int sid = blockIdx.x;
     if (sid >= n) return;
     const int lane = threadIdx.x;
@@ -251,106 +266,115 @@ __global__ void __launch_bounds__(kWave) snappy_split_kernel(const SnappyStream*
     gbyte_c* in = as_global(st.src);
     const uint32_t in_len = st.src_len;
     SnappyPiece* const slots = pieces + st.first;
+    const uint32_t L0 = min(max(piece_limit, 1u), kSnappyMaxBlock), L1 = kSnappyMaxBlock;
+    uint32_t wbase = 0;
     uint32_t win = load_window(in, in_len, 0, lane);
-    uint32_t ulen = 0, hdr = 0;
+    uint32_t total = 0, ip = 0;
     int bad = 0;
     for (int shift = 0;; shift += 7) {
-        if (hdr >= in_len || shift >= 35) {
+        if (ip >= in_len || shift >= 35) {
             bad = 1;
             break;
         }
-        const uint32_t c = window_byte(win, hdr++);
-        ulen |= (c & 0x7f) << shift;
+        const uint32_t c = window_byte(win, ip++);
+        total |= (c & 0x7f) << shift;
         if (!(c & 0x80)) break;
     }
-    if (!bad && ulen > st.dst_cap) bad = 2;
-    uint32_t np = 0;
-    for (int pass = 0; pass < 2 && !bad; ++pass) {
-        const uint32_t limit = pass == 0 ? min(piece_limit, kSnappyMaxBlock) : kSnappyMaxBlock;
-        if (pass == 1 && min(piece_limit, kSnappyMaxBlock) == kSnappyMaxBlock) {  // nothing larger to retry at
-            bad = 8;
+    if (!bad && total > st.dst_cap) bad = 2;
+    const uint32_t np0 = (total + L0 - 1) / L0, np1 = (total + L1 - 1) / L1;
+    int cut0 = np0 > (uint32_t)kSplitMaxSmall || np0 > st.max_pieces;  // this limit cannot be used
+    int cut1 = np1 > (uint32_t)kSplitMaxBig || np1 > st.max_pieces;
+    uint64_t upos = 0;  // output position of the element at ip
+    while (!bad && ip < in_len) {
+        if (ip + 69 > wbase + kWindow) {  // headers at ip .. ip+63 (+5 bytes each) inside the window
+            wbase = ip & ~3u;
+            win = load_window(in, in_len, wbase, lane);
+        }
+        // speculative header parse at q = ip + lane
+        const uint32_t q = ip + (uint32_t)lane;
+        const uint32_t r = q - wbase;
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((r >> 2) & 63) << 2), (int)win);
+        const uint32_t d1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((((r >> 2) + 1) & 63) << 2), (int)win);
+        const uint64_t x = ((((uint64_t)d1) << 32) | d0) >> ((r & 3) * 8);
+        const uint32_t tag = (uint32_t)x & 0xff;
+        const uint32_t ext = (uint32_t)(x >> 8);
+        const uint32_t kind = tag & 3;
+        uint32_t len, off = 0;
+        uint64_t csize;
+        if (kind == 0) {
+            len = (tag >> 2) + 1;
+            uint32_t nb = 0;
+            if (len > 60) {
+                nb = len - 60;
+                len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
+            }
+            csize = 1ull + nb + len;
+        } else if (kind == 1) {
+            len = ((tag >> 2) & 7) + 4;
+            off = ((tag >> 5) << 8) | (ext & 0xff);
+            csize = 2;
+        } else {
+            len = (tag >> 2) + 1;
+            off = kind == 2 ? (ext & 0xffff) : ext;
+            csize = kind == 2 ? 3 : 5;
+        }
+        // the chain: serial, one readlane per element
+        const uint32_t step = (uint32_t)min(csize, (uint64_t)0x7FFFFFFF);
+        uint64_t mask = 0;
+        uint32_t p = 0;
+        while (p < (uint32_t)kWave && ip + p < in_len) {
+            mask |= 1ull << p;
+            p += (uint32_t)__builtin_amdgcn_readlane((int)step, (int)p);
+        }
+        const bool marked = (mask >> lane) & 1;
+        // output positions of the marked elements: exclusive wave scan
+        uint64_t v = marked ? (uint64_t)len : 0;
+        for (int o = 1; o < kWave; o <<= 1) {
+            const uint64_t t = __shfl_up(v, (unsigned)o, kWave);
+            if (lane >= o) v += t;
+        }
+        const uint64_t u0 = upos + v - (marked ? len : 0);  // this element's output start
+        const uint64_t u1 = u0 + len;
+        int e = 0, c0 = 0, c1 = 0;
+        if (marked) {
+            if ((uint64_t)q + csize > in_len) e = 3;               // truncated
+            else if (u1 > total) e = 4;                            // past the declared length
+            else if (kind != 0 && (off == 0 || off > u0)) e = 6;   // before the stream
+            if (!e) {
+                const uint32_t a = (uint32_t)u0, z = (uint32_t)u1 - 1;
+                c0 = a / L0 != z / L0 || (kind != 0 && off > a % L0);
+                c1 = a / L1 != z / L1 || (kind != 0 && off > a % L1);
+                if (a % L0 == 0 && a / L0 < (uint32_t)kSplitMaxSmall) starts_small[a / L0] = q;
+                if (a % L1 == 0 && a / L1 < (uint32_t)kSplitMaxBig) starts_big[a / L1] = q;
+            }
+        }
+        // wave-uniform verdicts
+        const uint64_t eb = __ballot(e != 0);
+        if (eb) {
+            bad = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(eb));
             break;
         }
-        uint32_t ip = hdr, wbase = 0, upos = 0, pu = 0, pc = hdr;
-        if (pass == 1) win = load_window(in, in_len, 0, lane);
-        np = 0;
-        int cut_bad = 0;
-        while (ip < in_len) {
-            if (ip + 5 > wbase + kWindow) {
-                wbase = ip & ~3u;
-                win = load_window(in, in_len, wbase, lane);
-            }
-            const uint32_t q = ip - wbase;
-            const uint32_t dlo = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(q >> 2));
-            const uint32_t dhi = (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(q >> 2) + 1);
-            const uint64_t x = ((((uint64_t)dhi) << 32) | dlo) >> ((q & 3) * 8);
-            const uint32_t tag = (uint32_t)x & 0xff;
-            const uint32_t ext = (uint32_t)(x >> 8);
-            const uint32_t elem = ip++;
-            uint32_t len, off = 0, skip;
-            const uint32_t kind = tag & 3;
-            if (kind == 0) {
-                len = (tag >> 2) + 1;
-                uint32_t nb = 0;
-                if (len > 60) {
-                    nb = len - 60;
-                    len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
-                }
-                skip = nb + len;
-            } else if (kind == 1) {
-                len = ((tag >> 2) & 7) + 4;
-                off = ((tag >> 5) << 8) | (ext & 0xff);
-                skip = 1;
-            } else {
-                len = (tag >> 2) + 1;
-                off = kind == 2 ? (ext & 0xffff) : ext;
-                skip = kind == 2 ? 2 : 4;
-            }
-            if (skip > in_len - ip || len > ulen - upos) {  // truncated element / longer than declared
-                bad = 3;
-                break;
-            }
-            if (upos - pu + len > limit) {
-                if (upos == pu || np >= st.max_pieces) {  // one element larger than a piece / out of slots
-                    cut_bad = 1;
-                    break;
-                }
-                if (lane == 0) slots[np] = SnappyPiece{(const uint8_t*)st.src + pc, (uint8_t*)st.dst + pu, elem - pc, upos - pu};
-                ++np;
-                pc = elem;
-                pu = upos;
-            }
-            if (kind != 0 && off - 1 >= upos - pu) {  // offset 0, or reaches before the piece
-                if (off - 1 >= upos) {
-                    bad = 6;  // before the stream: malformed at any limit
-                    break;
-                }
-                cut_bad = 1;
-                break;
-            }
-            ip += skip;
-            upos += len;
-        }
-        if (bad) break;
-        if (cut_bad) {
-            if (pass == 1) bad = 8;
-            continue;
-        }
-        if (upos != ulen) {
-            bad = 7;
-            break;
-        }
-        if (upos > pu) {
-            if (np >= st.max_pieces) {
-                bad = 9;
-                break;
-            }
-            if (lane == 0) slots[np] = SnappyPiece{(const uint8_t*)st.src + pc, (uint8_t*)st.dst + pu, in_len - pc, upos - pu};
-            ++np;
-        }
-        break;
+        cut0 |= __ballot(c0) != 0;
+        cut1 |= __ballot(c1) != 0;
+        upos = __shfl(u1, (int)(63 - __builtin_clzll(mask)), kWave);  // after the last marked element
+        ip += p;
     }
-    if (bad) np = 0;
+    if (!bad && ip != in_len) bad = 3;
+    if (!bad && upos != total) bad = 7;
+    if (!bad && cut0 && cut1) bad = 8;  // not cuttable: the host decodes it
+    __syncthreads();
+    uint32_t np = 0;
+    if (!bad) {
+        const bool small = !cut0;
+        const uint32_t L = small ? L0 : L1;
+        const uint32_t* starts = small ? starts_small : starts_big;
+        np = small ? np0 : np1;
+        for (uint32_t k = lane; k < np; k += kWave) {
+            const uint32_t s0 = starts[k], s1 = k + 1 < np ? starts[k + 1] : in_len;
+            slots[k] = SnappyPiece{(const uint8_t*)st.src + s0, (uint8_t*)st.dst + (size_t)k * L, s1 - s0,
+                                   min(L, total - k * L)};
+        }
+    }
     for (uint32_t k = np + lane; k < st.max_pieces; k += kWave) slots[k] = SnappyPiece{nullptr, nullptr, 0, 0};
     if (lane == 0) stream_err[sid] = bad;
 }

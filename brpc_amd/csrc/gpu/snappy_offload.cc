@@ -13,12 +13,15 @@
 //    one varint header + the blocks' element runs (a block never references
 //    another, so the concatenation is one valid stream).
 //  * decompress: the compressed blocks are copied to HBM as they are (no
-//    flattening); snappy_split_kernel walks the element headers on the
-//    device (one wave per stream) and cuts the stream into pieces of
+//    flattening, no per-piece staging); the stream is cut into pieces of
 //    <= 4 KiB (device encoders), else <= 64 KiB (CPU encoders) uncompressed
-//    whose copies stay inside the piece, and the piece decoder rebuilds
-//    every piece in LDS, all in the same stream sequence. A stream that
-//    cannot be cut that way (or is malformed) falls back to the CPU codec.
+//    whose copies stay inside the piece, and the headerless piece decoder
+//    rebuilds every piece in LDS. The cut is one host walk over the blocks
+//    in place (~3 us per 64 KiB body), or with -gpu_snappy_device_split
+//    snappy_split_kernel on the device: the walk is a serial chain, and one
+//    wave takes ~95 us for the same body (MI355X, kernel trace), so the host
+//    walk is the default. A stream that cannot be cut (or is malformed)
+//    falls back to the CPU codec.
 // Each direction is one stream-ordered sequence (copy, kernel) and ONE
 // fiber-friendly event wait, shared with every other RPC's codec work that
 // arrived meanwhile (gpu/codec_batch.h: one launch sequence per batch).
@@ -48,6 +51,10 @@
 
 DECLARE_uint64(max_body_size);
 
+DEFINE_bool(gpu_snappy_device_split, false,
+            "cut received snappy streams on the device (snappy_split_kernel) instead of walking the tags on the "
+            "host; measured slower on MI355X: the walk is serial, ~95 us of one wave per 64 KiB body vs ~3 us of "
+            "host CPU (profiles/r3_snappy_device_split.txt)");
 DEFINE_int32(gpu_snappy_block_kb, 4,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
              "waves (lower latency) at some cost in ratio; <= 64");
@@ -182,6 +189,66 @@ bool gpu_compress(const Buf& in, Buf* out) {
     return true;
 }
 
+// Cuts a raw snappy stream (walked in place over the Buf's blocks: no
+// flattening) into pieces of <= limit uncompressed bytes whose copies stay
+// inside the piece. False when malformed or not cuttable at this limit.
+struct Piece {
+    size_t comp_off, comp_len, ulen;
+};
+bool split_stream(const Buf& in, size_t limit, size_t* total, std::vector<Piece>* pieces) {
+    BufBytesIterator it(in);
+    const size_t n = in.size();
+    auto pos = [&] { return n - it.bytes_left(); };
+    uint64_t ulen = 0;
+    for (int shift = 0;; shift += 7) {
+        if (it.done() || shift > 35) return false;
+        const uint8_t c = (uint8_t)*it;
+        ++it;
+        ulen |= (uint64_t)(c & 0x7f) << shift;
+        if (!(c & 0x80)) break;
+    }
+    *total = ulen;
+    size_t piece_start_comp = pos(), piece_start_u = 0, upos = 0;
+    while (!it.done()) {
+        const size_t elem_start = pos();
+        const uint8_t tag = (uint8_t)*it;
+        ++it;
+        uint8_t ext[4] = {0, 0, 0, 0};
+        size_t len = 0, off = 0, need;
+        const int kind = tag & 3;
+        if (kind == 0) {
+            len = (size_t)(tag >> 2) + 1;
+            need = len > 60 ? len - 60 : 0;
+        } else {
+            need = kind == 1 ? 1 : kind == 2 ? 2 : 4;
+        }
+        if (need && it.copy_and_forward(ext, need) != need) return false;
+        if (kind == 0) {
+            if (need) len = ((size_t)ext[0] | (size_t)ext[1] << 8 | (size_t)ext[2] << 16 | (size_t)ext[3] << 24) + 1;
+        } else if (kind == 1) {
+            len = 4 + ((tag >> 2) & 7);
+            off = ((size_t)(tag >> 5) << 8) | ext[0];
+        } else {
+            len = 1 + (tag >> 2);
+            off = (size_t)ext[0] | ((size_t)ext[1] << 8) | ((size_t)ext[2] << 16) | ((size_t)ext[3] << 24);
+        }
+        if (upos + len > ulen) return false;
+        // start a new piece when this element would overflow the current one
+        if (upos - piece_start_u + len > limit) {
+            if (upos == piece_start_u) return false;  // one element larger than a piece
+            pieces->push_back(Piece{piece_start_comp, elem_start - piece_start_comp, upos - piece_start_u});
+            piece_start_comp = elem_start;
+            piece_start_u = upos;
+        }
+        if (kind != 0 && (off == 0 || off > upos - piece_start_u)) return false;  // crosses the piece start
+        if (kind == 0 && it.forward(len) != len) return false;
+        upos += len;
+    }
+    if (upos != ulen) return false;
+    if (upos > piece_start_u) pieces->push_back(Piece{piece_start_comp, n - piece_start_comp, upos - piece_start_u});
+    return true;
+}
+
 // Uncompressed length from the stream's varint preamble (the first <= 5
 // bytes, wherever the Buf's blocks are); false when malformed.
 bool read_preamble(const Buf& in, uint64_t* ulen) {
@@ -215,9 +282,20 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     if (total == 0) return in.size() == 1;
     if (index && total > FLAGS_max_body_size) return false;
     // the compressed blocks go to HBM as they are (pinned socket blocks read
-    // by the copy kernel, pageable ones bounced); the device cuts the stream
-    // into pieces and decodes them — the host never looks at a tag
+    // by the copy kernel, pageable ones bounced), cut into pieces either by
+    // one host walk over the blocks in place or on the device
     const uint32_t limit = (uint32_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
+    std::vector<Piece> cuts;
+    const bool host_cut = !FLAGS_gpu_snappy_device_split;
+    if (host_cut) {
+        // small pieces first (streams from device encoders: more waves, less
+        // latency), then the 64 KiB fragments every host encoder respects
+        size_t t = 0;
+        if (!split_stream(in, limit, &t, &cuts)) {
+            cuts.clear();
+            if (!split_stream(in, kSnappyMaxBlock, &t, &cuts)) return false;
+        }
+    }
     const size_t pageable = pageable_bytes(in);
     PinnedBuf bounce(pageable ? pageable : 1), dst(total);
     HbmTmp dcomp(in.size(), dev), dbody(index ? total : 0, dev);
@@ -225,15 +303,31 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     char* out_base = index ? static_cast<char*>(dbody.p) : dst.p;
     CodecRequest req;
     gather_segments(in, static_cast<char*>(dcomp.p), bounce.p, &req.h2d);
-    req.streams.push_back(SnappyStream{dcomp.p, out_base, (uint32_t)in.size(), (uint32_t)total, 0,
-                                       SnappyMaxPieces(total, limit)});
-    req.stream_piece_limit = limit;
+    if (host_cut) {
+        size_t upos = 0;
+        for (const Piece& c : cuts) {
+            req.pieces.push_back(SnappyPiece{static_cast<const char*>(dcomp.p) + c.comp_off, out_base + upos,
+                                             (uint32_t)c.comp_len, (uint32_t)c.ulen});
+            req.pieces_max_ulen = std::max(req.pieces_max_ulen, (uint32_t)c.ulen);
+            upos += c.ulen;
+        }
+    } else {
+        req.streams.push_back(SnappyStream{dcomp.p, out_base, (uint32_t)in.size(), (uint32_t)total, 0,
+                                           SnappyMaxPieces(total, limit)});
+        req.stream_piece_limit = limit;
+    }
     if (index) {
         req.want_scan = true;
         req.scan = PbScanJob{static_cast<const uint8_t*>(dbody.p), total};
         req.d2h.push_back(Segment{dbody.p, dst.p, total});
     }
-    if (RunCodecRequest(&req, dev) != 0 || req.stream_err[0] != 0) return false;
+    if (RunCodecRequest(&req, dev) != 0) return false;
+    for (int e : req.stream_err) {
+        if (e) return false;
+    }
+    for (int e : req.piece_err) {
+        if (e) return false;
+    }
     if (index) {
         index->nfields = req.scan_nfields;
         index->fields.swap(req.scan_fields);

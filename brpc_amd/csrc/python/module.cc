@@ -287,6 +287,29 @@ PYBIND11_MODULE(_native, m) {
         std::string err;
         if (!SetFlag(name, value, false, &err)) throw std::invalid_argument("set_flag " + name + ": " + err);
     });
+    // placement on shared hosts: wake-up lateness per CPU, re-confinement
+    m.def("probe_cpu_wake", [](const std::vector<int>& cpus, int duration_ms, int period_us, int threshold_us) {
+        std::vector<fiber::CpuWakeProbe> r;
+        {
+            py::gil_scoped_release nogil;
+            r = fiber::ProbeCpuWake(cpus, duration_ms, period_us, threshold_us);
+        }
+        py::list out;
+        for (const auto& p : r) {
+            py::dict d;
+            d["cpu"] = p.cpu;
+            d["wakes"] = p.wakes;
+            d["late_p50_us"] = p.late_p50_us;
+            d["late_p99_us"] = p.late_p99_us;
+            d["late_max_us"] = p.late_max_us;
+            d["late_over"] = p.late_over;
+            d["run_delay_us"] = p.run_delay_us;
+            d["nivcsw"] = p.nivcsw;
+            out.append(d);
+        }
+        return out;
+    }, py::arg("cpus"), py::arg("duration_ms") = 500, py::arg("period_us") = 1000, py::arg("threshold_us") = 150);
+    m.def("rebind_l3_domain", [](int k) { return fiber::RebindL3Domain(k); });
     m.def("get_flag", [](const std::string& name) {
         std::string v;
         if (!GetFlag(name, &v)) throw std::invalid_argument("no flag " + name);

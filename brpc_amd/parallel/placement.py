@@ -116,10 +116,71 @@ def cpu_busy(seconds=0.2):
     return {c: 1.0 - (b[c][1] - a[c][1]) / max(1, b[c][0] - a[c][0]) for c in a if c in b}
 
 
-def choose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.2):
+def host_cpus():
+    """CPUs of the container's cpuset (what the domains are indexed over,
+    also after the runtime confined this process to one of them)."""
+    try:
+        with open("/sys/fs/cgroup/cpuset.cpus.effective") as f:
+            cpus = sorted(parse_cpulist(f.read()))
+        if cpus:
+            return cpus
+    except OSError:
+        pass
+    return allowed_cpus()
+
+
+def probe_domains(idxs, domains, seconds=0.5, native=None):
+    """{domain index: {"late": wake-ups >150 us late, "run_delay_ms": ...,
+    "nivcsw": ...}} from one pinned sleeper per CPU of every listed domain,
+    all at once (fiber/cpu_probe.cc). {} without the native module."""
+    if native is None:
+        try:
+            from .. import native as native_mod
+            native = native_mod
+        except Exception:  # noqa: BLE001
+            return {}
+    cpus = [c for i in idxs for c in domains[i][1]]
+    try:
+        res = native.probe_cpu_wake(cpus, int(seconds * 1000), 1000, 150)
+    except Exception:  # noqa: BLE001
+        return {}
+    by_cpu = {r["cpu"]: r for r in res if r["wakes"] >= 0}
+    out = {}
+    for i in idxs:
+        rs = [by_cpu[c] for c in domains[i][1] if c in by_cpu]
+        if not rs:
+            continue
+        out[i] = {"late": sum(r["late_over"] for r in rs),
+                  "run_delay_ms": round(sum(r["run_delay_us"] for r in rs) / 1000.0, 2),
+                  "nivcsw": sum(r["nivcsw"] for r in rs),
+                  "late_p99_us": max(r["late_p99_us"] for r in rs)}
+    return out
+
+
+def _quietest(mine, domains, sample_s, native, info):
+    """Index of the domain in `mine` other tenants disturb least: fewest
+    late wake-ups of pinned sleepers, then least runqueue delay; the busy
+    share of /proc/stat when the probe is unavailable."""
+    probe = probe_domains(mine, domains, sample_s, native)
+    if probe:
+        idx = min(probe, key=lambda i: (probe[i]["late"], probe[i]["nivcsw"], probe[i]["run_delay_ms"], i))
+        info["l3_domain_probe"] = probe[idx]
+        info["l3_domain_probe_worst_late"] = max(v["late"] for v in probe.values())
+        return idx
+    busy = cpu_busy(min(sample_s, 0.2))
+    if not busy:
+        return mine[0]
+    load = {i: sum(busy.get(c, 0.0) for c in domains[i][1]) / len(domains[i][1]) for i in mine}
+    idx = min(mine, key=lambda i: (round(load[i], 2), i))
+    info["l3_domain_busy_pct"] = round(100.0 * load[idx], 1)
+    info["l3_domain_busy_pct_max"] = round(100.0 * max(load.values()), 1)
+    return idx
+
+
+def choose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.5):
     """Index (for -cpu_l3_domain) of the L3 domain this rank should use, and
     a description dict for the bench JSON. -1: leave the rank unconfined."""
-    domains = l3_domains()
+    domains = l3_domains(host_cpus())
     info = {"l3_domains": len(domains)}
     if len(domains) <= 1:
         return -1, info
@@ -145,18 +206,37 @@ def choose_l3_domain(local_rank, local_world, device, device_count=0, native=Non
             peers.append(local_rank)
     slot = sorted(peers).index(local_rank)
     # ranks sharing the node own disjoint slices of its domains; in its slice
-    # a rank takes the domain the rest of the host keeps least busy (other
+    # a rank takes the domain the rest of the host disturbs least (other
     # jobs' threads preempting ours are what the tail latency is made of)
     mine = cand[slot::len(peers)] if len(cand) >= len(peers) else [cand[slot % len(cand)]]
     idx = mine[0]
     if len(mine) > 1 and sample_s > 0:
-        busy = cpu_busy(sample_s)
-        if busy:
-            load = {i: sum(busy.get(c, 0.0) for c in domains[i][1]) / len(domains[i][1]) for i in mine}
-            idx = min(mine, key=lambda i: (round(load[i], 2), i))
-            info["l3_domain_busy_pct"] = round(100.0 * load[idx], 1)
-            info["l3_domain_busy_pct_max"] = round(100.0 * max(load.values()), 1)
+        idx = _quietest(mine, domains, sample_s, native, info)
+    info["l3_domain_candidates"] = len(mine)
     info["l3_domain_first_cpu"] = domains[idx][0]
     info["ranks_on_gpu_numa_node"] = len(peers)
     info["numa_local"] = bool(local) and set(domains[idx][1]) <= local
     return idx, info
+
+
+def rechoose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.5):
+    """Probe the rank's slice again and move the running process to its
+    quietest domain (fiber::RebindL3Domain). Run right before a latency
+    measurement: other tenants' load shifts over minutes. Returns the new
+    placement dict ({} when nothing could be chosen)."""
+    idx, info = choose_l3_domain(local_rank, local_world, device, device_count, native, sample_s)
+    if idx < 0:
+        return {}
+    if native is None:
+        from .. import native as native_mod
+        native = native_mod
+    try:
+        cur = int(native.get_flag("cpu_l3_domain"))
+    except Exception:  # noqa: BLE001
+        cur = -1
+    info["l3_domain"] = idx
+    info["moved"] = idx != cur
+    if idx != cur and native.rebind_l3_domain(idx) != 0:
+        info["moved"] = False
+        info["error"] = "rebind failed"
+    return info

@@ -154,10 +154,11 @@ def test_device_split_cuts_device_streams_at_4k(dev):
 def test_device_split_rejects_bad_streams(dev):
     from brpc_amd import native
     good = native.snappy_compress(_corpus("text", 20000, 9))
-    bad_offset = bytearray(good)
-    bad_offset[-1] = 0xFF
+    hello = native.snappy_compress(b"hello hello hello hello hello")  # ends with a copy
+    bad_offset = bytearray(hello)
+    bad_offset[-1] = 0xFF  # its offset now reaches before the stream
     cases = [
-        (bytes(bad_offset), 20000),
+        (bytes(bad_offset), 29),
         (good[:-3], 20000),  # truncated
         (good, 19999),  # declared length larger than the output room
         (b"\x05\x01\x00", 5),  # a copy first
@@ -191,12 +192,15 @@ def test_default_block_is_32k_and_round_trips(dev):
     assert snappy_decompress(packed, offs, sizes, raw).cpu().numpy().tobytes() == data
 
 
-def test_gpu_snappy_offload_is_standard_snappy():
+@pytest.mark.parametrize("device_split", [False, True])
+def test_gpu_snappy_offload_is_standard_snappy(device_split):
     """The RPC body codec with the GPU offload installed: device-compressed
     streams decode with the host codec and host streams decode on the
-    device — bit-exact both ways (rpc/compress.h registry path)."""
+    device — bit-exact both ways (rpc/compress.h registry path), with the
+    stream cut by the host walk or by snappy_split_kernel."""
     import os
     from brpc_amd import native
+    native.set_flag("gpu_snappy_device_split", "true" if device_split else "false")
     native.gpu.enable_snappy(0, 1024)
     try:
         rnd = os.urandom(200000)
@@ -214,6 +218,7 @@ def test_gpu_snappy_offload_is_standard_snappy():
             assert after["fallbacks"] == before["fallbacks"], (before, after)
     finally:
         native.gpu.disable_snappy()
+        native.set_flag("gpu_snappy_device_split", "false")
 
 
 def test_grpc_snappy_bodies_on_gpu():
