@@ -407,6 +407,36 @@ def main():
             finally:
                 native.gpu.disable_snappy()
 
+    # The other device codec paths, CPU vs GPU on the same 64 KiB body:
+    # baidu_std + snappy (the headline's protocol; the body is decoded and
+    # pb_scan-indexed on the device) and http + json (json2pb over the GPU
+    # structural index, gpu/json_offload.h).
+    rx = {}
+    if not a.skip_grpc:
+        codec_legs = (
+            ("baidu_std_snappy_64KB", {"protocol": "baidu_std", "request_compress_type": 1},
+             lambda: native.gpu.enable_snappy(topo.device, 16384), lambda: native.gpu.disable_snappy(),
+             lambda: native.gpu.snappy_stats()["indexed_parses"]),
+            ("http_json_64KB", {"protocol": "http", "connection_type": "pooled"},
+             lambda: native.gpu.enable_json_index(topo.device, 16384), lambda: native.gpu.disable_json_index(),
+             lambda: native.gpu.json_stats()["indexed_bodies"]),
+        )
+        for name, extra, enable, disable, count in codec_legs:
+            wlx = EchoWorkload(name, request_size=65536, attachment_size=0,
+                               requests_per_step=max(1, a.requests_per_step_grpc))
+            ox = wlx.press_options(peer, gpu_device=topo.device)
+            ox.update({"concurrency": a.concurrency})
+            ox.update(extra)
+            rx[name] = {"cpu": timed_leg(wlx, a.steps, a.warmup, dict(ox))}
+            if cuda:
+                enable()
+                try:
+                    c0 = count()
+                    rx[name]["gpu"] = timed_leg(wlx, a.steps, a.warmup, dict(ox))
+                    rx[name]["gpu"]["device_bodies"] = count() - c0
+                finally:
+                    disable()
+
     # Sweep (example/rdma_performance/client.cpp:35-48,221-300 analog):
     # payload size x queue depth, lending vs the RCCL plane, each point a
     # closed loop for --sweep-seconds; avg/p90/p99/p99.9 latency, GB/s and
@@ -677,6 +707,16 @@ def main():
                 out["grpc_gpu_codec_indexed_parses"] = rz["gpu"]["indexed_parses"]
                 out["grpc_gpu_codec_requests_per_launch"] = rz["gpu"]["codec_requests_per_launch"]
                 out["grpc_snappy_errors"] = rz["cpu"]["errors"] + rz["gpu"]["errors"]
+        for name, r in rx.items():
+            out[name + "_qps_cpu"] = round(r["cpu"]["qps"], 1)
+            out[name + "_p99_us_cpu"] = r["cpu"]["p99_us"]
+            errs = r["cpu"]["errors"]
+            if "gpu" in r:
+                out[name + "_qps_gpu"] = round(r["gpu"]["qps"], 1)
+                out[name + "_p99_us_gpu"] = r["gpu"]["p99_us"]
+                out[name + "_device_bodies"] = r["gpu"]["device_bodies"]
+                errs += r["gpu"]["errors"]
+            out[name + "_errors"] = errs
         if rc:
             out["rccl_64KB_qps"] = round(rc["qps"], 1)
             out["rccl_64KB_p99_us"] = rc["p99_us"]
@@ -706,6 +746,8 @@ def main():
                 ("echo_1MB", r1m), ("rccl_1MB", r1mr), ("cpu_handler_64KB", rgc), ("gpu_handler_64KB", rg))
         if rz:
             legs += (("grpc_snappy_cpu_codec", rz["cpu"]), ("grpc_snappy_gpu_codec", rz.get("gpu")))
+        for name, r in rx.items():
+            legs += ((name + "_cpu", r["cpu"]), (name + "_gpu", r.get("gpu")))
         # which transport carried each leg's payloads (summed over ranks)
         out["transport"] = {name: leg["transport"] for name, leg in legs if leg and name[:4] != "grpc"}
         # host CPU microseconds per RPC of each leg (whole rank: client,

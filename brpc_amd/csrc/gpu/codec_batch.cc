@@ -5,12 +5,18 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <deque>
 #include <mutex>
 
+#include "base/flags.h"
 #include "base/logging.h"
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
+
+DEFINE_int32(codec_batch_max_inflight, 6,
+             "codec batches in flight per device before the next one waits for the oldest (0: no limit); while "
+             "it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches");
 
 namespace mrpc {
 namespace gpu {
@@ -62,7 +68,46 @@ struct Engine {
     CBatch* open = nullptr;
     bool launching = false;
     std::vector<CBatch*> spare;
+    std::deque<CBatch*> flying;  // launched, each holding one ref until the leader retires it
 };
+
+void release(Engine& e, CBatch* b) {
+    if (b->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        if (b->ev) ReleaseEvent(b->ev);
+        b->ev = nullptr;
+        b->reqs.clear();
+        std::lock_guard<std::mutex> g(e.mu);
+        e.spare.push_back(b);
+    }
+}
+
+// Leader only: retire completed batches; with the limit reached, wait for
+// the oldest (the open batch keeps collecting requests meanwhile).
+void throttle(Engine& e) {
+    const int limit = FLAGS_codec_batch_max_inflight;
+    for (;;) {
+        CBatch* oldest = nullptr;
+        bool wait = false;
+        {
+            std::lock_guard<std::mutex> g(e.mu);
+            if (e.flying.empty()) return;
+            oldest = e.flying.front();
+            if (oldest->butex->load(std::memory_order_acquire) != 0) {
+                e.flying.pop_front();
+            } else if (limit > 0 && (int)e.flying.size() >= limit) {
+                wait = true;
+            } else {
+                return;
+            }
+        }
+        if (wait) {
+            while (oldest->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(oldest->butex, 0);
+            std::lock_guard<std::mutex> g(e.mu);
+            e.flying.pop_front();
+        }
+        release(e, oldest);
+    }
+}
 
 Engine g_engine[kMaxDev];
 std::atomic<int64_t> g_requests{0}, g_launches{0};
@@ -216,6 +261,7 @@ int RunCodecRequest(CodecRequest* r, int device) {
     }
     if (leader) {
         for (;;) {
+            throttle(e);
             CBatch* cur;
             {
                 std::lock_guard<std::mutex> g(e.mu);
@@ -231,6 +277,10 @@ int RunCodecRequest(CodecRequest* r, int device) {
                                         << device;
                 cur->butex->store(-1, std::memory_order_release);
                 fiber::butex_wake_all(cur->butex);
+            } else {
+                cur->refs.fetch_add(1, std::memory_order_relaxed);
+                std::lock_guard<std::mutex> g(e.mu);
+                e.flying.push_back(cur);
             }
         }
     }
@@ -259,13 +309,7 @@ int RunCodecRequest(CodecRequest* r, int device) {
             r->scan_fields.assign(f, f + 2 * kCodecScanFields);
         }
     }
-    if (mine->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
-        if (mine->ev) ReleaseEvent(mine->ev);
-        mine->ev = nullptr;
-        mine->reqs.clear();
-        std::lock_guard<std::mutex> g(e.mu);
-        e.spare.push_back(mine);
-    }
+    release(e, mine);
     return rc;
 }
 

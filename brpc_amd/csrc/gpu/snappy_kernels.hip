@@ -230,9 +230,13 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_kernel(const S
         return;
     }
     if (pc.ulen <= lo || pc.ulen > hi) return;
-    gbyte_c* in = as_global(pc.src);
-    const uint32_t win = load_window(in, pc.src_len, 0, lane);
-    const int bad = decode_elements(in, pc.src_len, 0, 0, win, pc.ulen, buf, pc.dst, lane);
+    // a piece starts anywhere in its stream: walk it from the dword below,
+    // so every window load is an aligned dword per lane
+    const uint32_t mis = (uint32_t)((uintptr_t)pc.src & 3);
+    gbyte_c* in = as_global(static_cast<const uint8_t*>(pc.src) - mis);
+    const uint32_t in_len = pc.src_len + mis;
+    const uint32_t win = load_window(in, in_len, 0, lane);
+    const int bad = decode_elements(in, in_len, mis, 0, win, pc.ulen, buf, pc.dst, lane);
     if (lane == 0) err[blk] = bad;
 }
 

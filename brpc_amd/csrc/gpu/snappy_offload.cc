@@ -55,6 +55,9 @@ DEFINE_bool(gpu_snappy_device_split, false,
             "cut received snappy streams on the device (snappy_split_kernel) instead of walking the tags on the "
             "host; measured slower on MI355X: the walk is serial, ~95 us of one wave per 64 KiB body vs ~3 us of "
             "host CPU (profiles/r3_snappy_device_split.txt)");
+DEFINE_bool(gpu_snappy_direct_host, true,
+            "codec kernels read their host input and write their host output in pinned memory directly (no "
+            "staging copy kernels around them): two kernels fewer per decode, one per encode");
 DEFINE_int32(gpu_snappy_block_kb, 4,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
              "waves (lower latency) at some cost in ratio; <= 64");
@@ -155,16 +158,30 @@ bool gpu_compress(const Buf& in, Buf* out) {
     const size_t blk = (size_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
     const size_t nblk = (n + blk - 1) / blk;
     const size_t cap = (SnappyMaxCompressedLength(blk) + 15) & ~(size_t)15;
-    HbmTmp raw(n, dev);
-    const size_t pageable = pageable_bytes(in);
-    PinnedBuf bounce(pageable ? pageable : 1), comp(nblk * cap);
-    if (!raw.p || !bounce.p || !comp.p) return false;
+    // direct: the kernel stages its blocks into LDS straight from pinned
+    // host memory (the body's own pinned block, or one flat pinned copy);
+    // otherwise the body is gathered into HBM first
+    const bool direct = FLAGS_gpu_snappy_direct_host && in.all_host_accessible();
+    const bool one_pinned = in.backing_block_num() == 1 && in.ref_at(0).block->kind == MemKind::PINNED;
+    const size_t pageable = direct ? 0 : pageable_bytes(in);
+    HbmTmp raw(direct ? 0 : n, dev);
+    PinnedBuf flat(direct && !one_pinned ? n : 1), bounce(pageable ? pageable : 1), comp(nblk * cap);
+    if ((!direct && !raw.p) || !flat.p || !bounce.p || !comp.p) return false;
     CodecRequest req;
-    gather_segments(in, static_cast<char*>(raw.p), bounce.p, &req.h2d);
+    const char* src;
+    if (!direct) {
+        gather_segments(in, static_cast<char*>(raw.p), bounce.p, &req.h2d);
+        src = static_cast<const char*>(raw.p);
+    } else if (one_pinned) {
+        src = in.block_data(0);
+    } else {
+        in.copy_to(flat.p, n);
+        src = flat.p;
+    }
     req.comp.resize(nblk);
     for (size_t i = 0; i < nblk; ++i) {
         const size_t off = i * blk;
-        req.comp[i] = SnappyJob{static_cast<char*>(raw.p) + off, comp.p + i * cap, std::min<size_t>(blk, n - off), cap};
+        req.comp[i] = SnappyJob{src + off, comp.p + i * cap, std::min<size_t>(blk, n - off), cap};
     }
     req.comp_max_ulen = (uint32_t)std::min(blk, n);
     // batched with the other RPCs' codec work: one launch sequence, one event
@@ -189,48 +206,62 @@ bool gpu_compress(const Buf& in, Buf* out) {
     return true;
 }
 
-// Cuts a raw snappy stream (walked in place over the Buf's blocks: no
-// flattening) into pieces of <= limit uncompressed bytes whose copies stay
-// inside the piece. False when malformed or not cuttable at this limit.
+// Cuts a raw snappy stream into pieces of <= limit uncompressed bytes whose
+// copies stay inside the piece. False when malformed or not cuttable at
+// this limit.
 struct Piece {
     size_t comp_off, comp_len, ulen;
 };
-bool split_stream(const Buf& in, size_t limit, size_t* total, std::vector<Piece>* pieces) {
-    BufBytesIterator it(in);
-    const size_t n = in.size();
-    auto pos = [&] { return n - it.bytes_left(); };
+bool split_stream(const uint8_t* p, size_t n, size_t limit, size_t* total, std::vector<Piece>* pieces) {
     uint64_t ulen = 0;
-    for (int shift = 0;; shift += 7) {
-        if (it.done() || shift > 35) return false;
-        const uint8_t c = (uint8_t)*it;
-        ++it;
+    size_t i = 0;
+    for (int shift = 0; shift <= 35; shift += 7) {
+        if (i >= n) return false;
+        const uint8_t c = p[i++];
         ulen |= (uint64_t)(c & 0x7f) << shift;
         if (!(c & 0x80)) break;
+        if (shift == 35) return false;
     }
     *total = ulen;
-    size_t piece_start_comp = pos(), piece_start_u = 0, upos = 0;
-    while (!it.done()) {
-        const size_t elem_start = pos();
-        const uint8_t tag = (uint8_t)*it;
-        ++it;
-        uint8_t ext[4] = {0, 0, 0, 0};
-        size_t len = 0, off = 0, need;
-        const int kind = tag & 3;
-        if (kind == 0) {
-            len = (size_t)(tag >> 2) + 1;
-            need = len > 60 ? len - 60 : 0;
-        } else {
-            need = kind == 1 ? 1 : kind == 2 ? 2 : 4;
+    size_t piece_start_comp = i, piece_start_u = 0, upos = 0;
+    while (i < n) {
+        const size_t elem_start = i;
+        const uint8_t tag = p[i++];
+        size_t len = 0, off = 0;
+        bool literal = false;
+        switch (tag & 3) {
+        case 0: {
+            literal = true;
+            size_t l = tag >> 2;
+            if (l >= 60) {
+                const int nb = (int)l - 59;
+                if (i + nb > n) return false;
+                l = 0;
+                for (int k = 0; k < nb; ++k) l |= (size_t)p[i + k] << (8 * k);
+                i += nb;
+            }
+            len = l + 1;
+            if (len > n - i) return false;
+            break;
         }
-        if (need && it.copy_and_forward(ext, need) != need) return false;
-        if (kind == 0) {
-            if (need) len = ((size_t)ext[0] | (size_t)ext[1] << 8 | (size_t)ext[2] << 16 | (size_t)ext[3] << 24) + 1;
-        } else if (kind == 1) {
+        case 1:
+            if (i + 1 > n) return false;
             len = 4 + ((tag >> 2) & 7);
-            off = ((size_t)(tag >> 5) << 8) | ext[0];
-        } else {
+            off = ((size_t)(tag >> 5) << 8) | p[i];
+            i += 1;
+            break;
+        case 2:
+            if (i + 2 > n) return false;
             len = 1 + (tag >> 2);
-            off = (size_t)ext[0] | ((size_t)ext[1] << 8) | ((size_t)ext[2] << 16) | ((size_t)ext[3] << 24);
+            off = (size_t)p[i] | ((size_t)p[i + 1] << 8);
+            i += 2;
+            break;
+        default:
+            if (i + 4 > n) return false;
+            len = 1 + (tag >> 2);
+            off = (size_t)p[i] | ((size_t)p[i + 1] << 8) | ((size_t)p[i + 2] << 16) | ((size_t)p[i + 3] << 24);
+            i += 4;
+            break;
         }
         if (upos + len > ulen) return false;
         // start a new piece when this element would overflow the current one
@@ -240,8 +271,8 @@ bool split_stream(const Buf& in, size_t limit, size_t* total, std::vector<Piece>
             piece_start_comp = elem_start;
             piece_start_u = upos;
         }
-        if (kind != 0 && (off == 0 || off > upos - piece_start_u)) return false;  // crosses the piece start
-        if (kind == 0 && it.forward(len) != len) return false;
+        if (!literal && (off == 0 || off > upos - piece_start_u)) return false;  // crosses the piece start
+        if (literal) i += len;
         upos += len;
     }
     if (upos != ulen) return false;
@@ -286,27 +317,53 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     // one host walk over the blocks in place or on the device
     const uint32_t limit = (uint32_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
     std::vector<Piece> cuts;
-    const bool host_cut = !FLAGS_gpu_snappy_device_split;
+    // compressed bytes already in HBM are cut on the device
+    const bool host_cut = !FLAGS_gpu_snappy_device_split && in.all_host_accessible();
     if (host_cut) {
+        // the walk needs contiguous bytes: the block itself, or a flat copy
+        // of a stream spread over several blocks (host memory, only read)
+        std::string flat;
+        const uint8_t* bytes;
+        if (in.backing_block_num() == 1) {
+            bytes = reinterpret_cast<const uint8_t*>(in.block_data(0));
+        } else {
+            flat = in.to_string();
+            bytes = reinterpret_cast<const uint8_t*>(flat.data());
+        }
         // small pieces first (streams from device encoders: more waves, less
         // latency), then the 64 KiB fragments every host encoder respects
         size_t t = 0;
-        if (!split_stream(in, limit, &t, &cuts)) {
+        if (!split_stream(bytes, in.size(), limit, &t, &cuts)) {
             cuts.clear();
-            if (!split_stream(in, kSnappyMaxBlock, &t, &cuts)) return false;
+            if (!split_stream(bytes, in.size(), kSnappyMaxBlock, &t, &cuts)) return false;
         }
     }
-    const size_t pageable = pageable_bytes(in);
-    PinnedBuf bounce(pageable ? pageable : 1), dst(total);
-    HbmTmp dcomp(in.size(), dev), dbody(index ? total : 0, dev);
-    if (!bounce.p || !dst.p || !dcomp.p || (index && !dbody.p)) return false;
-    char* out_base = index ? static_cast<char*>(dbody.p) : dst.p;
+    // direct (host cut only): pieces are read from the pinned block (or one
+    // flat pinned copy) and decoded straight into the pinned output, which
+    // pb_scan reads in place; otherwise compressed bytes go to HBM and the
+    // body comes back with a copy after the scan
+    const bool direct = host_cut && FLAGS_gpu_snappy_direct_host;
+    const bool one_pinned = in.backing_block_num() == 1 && in.ref_at(0).block->kind == MemKind::PINNED;
+    const size_t pageable = direct ? 0 : pageable_bytes(in);
+    PinnedBuf bounce(pageable ? pageable : 1), dst(total), cflat(direct && !one_pinned ? in.size() : 1);
+    HbmTmp dcomp(direct ? 0 : in.size(), dev), dbody(index && !direct ? total : 0, dev);
+    if (!bounce.p || !dst.p || !cflat.p || (!direct && !dcomp.p) || (index && !direct && !dbody.p)) return false;
+    char* out_base = index && !direct ? static_cast<char*>(dbody.p) : dst.p;
     CodecRequest req;
-    gather_segments(in, static_cast<char*>(dcomp.p), bounce.p, &req.h2d);
+    const char* comp_base;
+    if (!direct) {
+        gather_segments(in, static_cast<char*>(dcomp.p), bounce.p, &req.h2d);
+        comp_base = static_cast<const char*>(dcomp.p);
+    } else if (one_pinned) {
+        comp_base = in.block_data(0);
+    } else {
+        in.copy_to(cflat.p, in.size());
+        comp_base = cflat.p;
+    }
     if (host_cut) {
         size_t upos = 0;
         for (const Piece& c : cuts) {
-            req.pieces.push_back(SnappyPiece{static_cast<const char*>(dcomp.p) + c.comp_off, out_base + upos,
+            req.pieces.push_back(SnappyPiece{comp_base + c.comp_off, out_base + upos,
                                              (uint32_t)c.comp_len, (uint32_t)c.ulen});
             req.pieces_max_ulen = std::max(req.pieces_max_ulen, (uint32_t)c.ulen);
             upos += c.ulen;
@@ -318,8 +375,8 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     }
     if (index) {
         req.want_scan = true;
-        req.scan = PbScanJob{static_cast<const uint8_t*>(dbody.p), total};
-        req.d2h.push_back(Segment{dbody.p, dst.p, total});
+        req.scan = PbScanJob{reinterpret_cast<const uint8_t*>(out_base), total};
+        if (out_base != dst.p) req.d2h.push_back(Segment{dbody.p, dst.p, total});
     }
     if (RunCodecRequest(&req, dev) != 0) return false;
     for (int e : req.stream_err) {

@@ -63,5 +63,8 @@ def test_bench_multi_rank_gloo(nranks):
     # the host-only handler twin, and the CPU cost of every leg
     assert j["errors_64KB_cpu_handler"] == 0 and j["qps_64KB_cpu_handler"] > 0
     assert all(v > 0 for v in j["cpu_us_per_rpc"].values()) and "cpu_handler_64KB" in j["cpu_us_per_rpc"]
+    # the other codec paths (baidu_std + snappy, http + json), CPU side here
+    for leg in ("baidu_std_snappy_64KB", "http_json_64KB"):
+        assert j[leg + "_errors"] == 0 and j[leg + "_qps_cpu"] > 0 and leg + "_cpu" in j["cpu_us_per_rpc"]
     if nranks > 2:  # a relay chain needs at least two other ranks
         assert j["pipeline_hops"] == nranks - 1 and j["pipeline_gbytes_per_s"] > 0

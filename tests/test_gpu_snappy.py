@@ -192,15 +192,17 @@ def test_default_block_is_32k_and_round_trips(dev):
     assert snappy_decompress(packed, offs, sizes, raw).cpu().numpy().tobytes() == data
 
 
-@pytest.mark.parametrize("device_split", [False, True])
-def test_gpu_snappy_offload_is_standard_snappy(device_split):
+@pytest.mark.parametrize("mode", ["direct", "staged", "device_split"])
+def test_gpu_snappy_offload_is_standard_snappy(mode):
     """The RPC body codec with the GPU offload installed: device-compressed
     streams decode with the host codec and host streams decode on the
     device — bit-exact both ways (rpc/compress.h registry path), with the
-    stream cut by the host walk or by snappy_split_kernel."""
+    stream cut by the host walk or by snappy_split_kernel, and the kernels
+    reading/writing pinned host memory directly or through HBM staging."""
     import os
     from brpc_amd import native
-    native.set_flag("gpu_snappy_device_split", "true" if device_split else "false")
+    native.set_flag("gpu_snappy_device_split", "true" if mode == "device_split" else "false")
+    native.set_flag("gpu_snappy_direct_host", "false" if mode == "staged" else "true")
     native.gpu.enable_snappy(0, 1024)
     try:
         rnd = os.urandom(200000)
@@ -219,6 +221,7 @@ def test_gpu_snappy_offload_is_standard_snappy(device_split):
     finally:
         native.gpu.disable_snappy()
         native.set_flag("gpu_snappy_device_split", "false")
+        native.set_flag("gpu_snappy_direct_host", "true")
 
 
 def test_grpc_snappy_bodies_on_gpu():
