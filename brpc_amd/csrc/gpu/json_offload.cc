@@ -1,10 +1,11 @@
 // Device half of json2pb for large bodies (the reference parses
 // every http+json body on the CPU, src/json2pb/json_to_pb.cpp): the body is
-// staged into HBM through a pinned bounce buffer, LaunchJsonIndex
-// (gpu/json_kernels.hip) finds every structural position, and the positions
-// come back for json::ParseWithIndex. Two stream-ordered waits per body:
-// one for the count, one for the positions (only count * 4 bytes cross the
-// link).
+// copied into a pinned buffer, LaunchJsonIndex (gpu/json_kernels.hip) reads
+// it there and writes every structural position straight into pinned
+// memory, and json::ParseWithIndex walks the positions: one launch and one
+// fiber-friendly wait per body. (-json_index_direct_host=false keeps the
+// older staging through HBM: a copy kernel in, the index, a second wait for
+// the count, a copy of count * 4 bytes back.)
 #include "gpu/json_offload.h"
 
 #include <hip/hip_runtime_api.h>
@@ -12,6 +13,7 @@
 #include <atomic>
 #include <cstring>
 
+#include "base/flags.h"
 #include "base/time.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
@@ -19,6 +21,9 @@
 #include "json/json2pb.h"
 #include "rpc/span.h"
 #include "var/var.h"
+
+DEFINE_bool(json_index_direct_host, true,
+            "the JSON index kernel reads the pinned body and writes positions to pinned memory directly");
 
 namespace mrpc {
 namespace gpu {
@@ -71,6 +76,27 @@ int JsonIndex(const char* data, size_t n, std::vector<uint32_t>* out, int device
     out->clear();
     if (n == 0) return 0;
     if (n > 0xFFFFFFFFull || device < 0) return -1;
+    if (FLAGS_json_index_direct_host) {
+        Pinned body(n), pos(n * sizeof(uint32_t)), meta(16);  // every byte could be a position
+        Hbm scratch(JsonIndexScratchBytes(n), device);
+        if (!body.p || !pos.p || !meta.p || !scratch.p) return -1;
+        memcpy(body.p, data, n);
+        uint64_t* count = static_cast<uint64_t*>(meta.p);
+        int* err = reinterpret_cast<int*>(count + 1);
+        int prev = 0;
+        hipGetDevice(&prev);
+        if (prev != device) hipSetDevice(device);
+        hipStream_t s = PoolStream(device);
+        int rc = s ? LaunchJsonIndex(static_cast<const uint8_t*>(body.p), n, static_cast<uint32_t*>(pos.p), n, count,
+                                     err, scratch.p, s)
+                   : -1;
+        const int wrc = s ? SyncStream(s) : -1;  // never free buffers a launched kernel may still use
+        if (prev != device) hipSetDevice(prev);
+        if (rc != 0 || wrc != 0 || *err != 0 || *count > n) return -1;
+        const uint32_t* p = static_cast<const uint32_t*>(pos.p);
+        out->assign(p, p + *count);
+        return 0;
+    }
     // every byte could be a position; the count decides what comes back
     Hbm in(n, device), pos(n * sizeof(uint32_t), device), scratch(JsonIndexScratchBytes(n), device);
     Pinned bounce(n), meta(16);

@@ -4,7 +4,7 @@ P=gpurun_out/z7
 rm -rf $P; mkdir -p $P
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_snappy.py tests/test_gpu_json.py > $P/pytest.log 2>&1; rc=$?; tail -1 $P/pytest.log; [ $rc -eq 0 ] || exit $rc
-for k in 2 3 4 6; do
+for k in 6 8; do
 MRPC_FLAGS="--codec_batch_max_inflight=$k" timeout -k 10 300 python bench.py --steps 5 --warmup 1 --skip-64k --skip-rccl --skip-1m --skip-sweep --skip-stream --latency-sample-s 1 > $P/bench_k$k.log 2>&1 || exit $?
 python - $k <<'PY'
 import json, sys

@@ -148,13 +148,27 @@ def test_json2pb_round_trip_cpu():
 
 
 @pytest.mark.gpu
-def test_json_index_bytes_matches_host(dev):
+@pytest.mark.parametrize("direct", [True, False])
+def test_json_index_bytes_matches_host(dev, direct):
+    """Through the offload entry: pinned in/out read and written by the
+    kernel directly, or staged through HBM."""
     from brpc_amd import native
-    rnd = random.Random(9)
-    text = json.dumps([_doc(rnd) for _ in range(300)]).encode()
-    assert native.gpu.json_index_bytes(text, 0) == json_index_host(text)[0]
-    with pytest.raises(RuntimeError):
-        native.gpu.json_index_bytes(b'{"open', 0)
+    native.set_flag("json_index_direct_host", "true" if direct else "false")
+    try:
+        rnd = random.Random(9)
+        text = json.dumps([_doc(rnd) for _ in range(300)]).encode()
+        assert native.gpu.json_index_bytes(text, 0) == json_index_host(text)[0]
+        for k in (1, 63, 64, 65, 4097):  # prefixes: tails in every lane position, some inside a string
+            want, still_open = json_index_host(text[:k])
+            if still_open:
+                with pytest.raises(RuntimeError):
+                    native.gpu.json_index_bytes(text[:k], 0)
+            else:
+                assert native.gpu.json_index_bytes(text[:k], 0) == want
+        with pytest.raises(RuntimeError):
+            native.gpu.json_index_bytes(b'{"open', 0)
+    finally:
+        native.set_flag("json_index_direct_host", "true")
 
 
 @pytest.mark.gpu
