@@ -116,7 +116,8 @@ public:
     uint32_t read_tag() {
         if (_p >= _limit) return 0;
         uint64_t t;
-        if (!read_varint(&t) || t > 0xFFFFFFFFu) return 0xFFFFFFFFu;  // malformed
+        // a zero tag (field number 0) is malformed, not an end marker
+        if (!read_varint(&t) || t > 0xFFFFFFFFu || t == 0) return 0xFFFFFFFFu;
         return (uint32_t)t;
     }
     bool skip_field(uint32_t tag, std::string* unknown);
