@@ -2,6 +2,7 @@
 // reference's test/recordio_unittest.cpp and the rpc_dump/rpc_replay pair).
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -118,6 +119,63 @@ TEST(RpcDump, sample_and_replay_byte_for_byte) {
     }
     EXPECT_EQ(nrec, 20);  // below the speed limit every request is sampled
     EXPECT_EQ(echo.ncalls(), before + nrec);
+    for (const std::string& fn : files) unlink((dir + "/" + fn).c_str());
+    rmdir(dir.c_str());
+}
+
+TEST(RpcDump, files_rotate_and_old_ones_are_removed) {
+    // 5 requests per file, at most 3 files: 23 sampled requests leave the
+    // newest 3 files (the last one partial) and nothing older
+    const std::string dir = "/tmp/mrpc_dump_rot_" + std::to_string(getpid());
+    SetFlag("rpc_dump_dir", dir);
+    SetFlag("rpc_dump_max_requests_in_one_file", "5");
+    SetFlag("rpc_dump_max_files", "3");
+    SetFlag("rpc_dump", "true");
+    Server server;
+    EchoServiceImpl echo;
+    server.AddService(&echo, SERVER_DOESNT_OWN_SERVICE);
+    ServerOptions o;
+    o.has_builtin_services = false;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &o), 0);
+    const std::string addr = "127.0.0.1:" + std::to_string(server.listen_port());
+    Channel ch;
+    ASSERT_EQ(ch.Init(addr.c_str(), nullptr), 0);
+    example::EchoService_Stub stub(&ch);
+    for (int i = 0; i < 23; ++i) {
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("rot-" + std::to_string(i));
+        stub.Echo(&cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        if (i % 5 == 4) FlushRpcDump();  // let the collector see the requests in order
+    }
+    SetFlag("rpc_dump", "false");
+    FlushRpcDump();
+    std::vector<std::string> files = ListRpcDumpFiles(dir);
+    EXPECT_LE(files.size(), 3u);
+    ASSERT_GE(files.size(), 1u);
+    std::vector<int> seen;
+    for (const std::string& fn : files) {
+        RecordReader rd(dir + "/" + fn);
+        Record r;
+        int in_file = 0;
+        while (rd.ReadNext(&r)) {
+            ++in_file;
+            Buf payload = r.Payload();
+            example::EchoRequest req;
+            ASSERT_TRUE(req.ParseFromBuf(payload));
+            seen.push_back(atoi(req.message().c_str() + 4));
+        }
+        EXPECT_LE(in_file, 5);
+    }
+    // the newest requests survive, the oldest files were removed
+    ASSERT_FALSE(seen.empty());
+    EXPECT_EQ(*std::max_element(seen.begin(), seen.end()), 22);
+    EXPECT_GT(*std::min_element(seen.begin(), seen.end()), 0);
+    EXPECT_LE(seen.size(), 15u);
+    SetFlag("rpc_dump_max_requests_in_one_file", "1000");
+    SetFlag("rpc_dump_max_files", "32");
     for (const std::string& fn : files) unlink((dir + "/" + fn).c_str());
     rmdir(dir.c_str());
 }
