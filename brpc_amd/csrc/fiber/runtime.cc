@@ -1109,6 +1109,7 @@ void flush() {
 
 int join(fiber_t tid, void** ret) {
     if (ret) *ret = nullptr;
+    if (tid == INVALID_FIBER) return EINVAL;
     TaskMeta* m = address_meta(tid);
     if (!m || !m->version_butex) return EINVAL;
     TaskGroup* g = tls_group();

@@ -1,5 +1,7 @@
 #include "fiber/timer.h"
 
+#include <sys/prctl.h>
+
 #include <algorithm>
 #include <climits>
 #include <vector>
@@ -118,6 +120,9 @@ int TimerThread::unschedule(TaskId id) {
 
 void TimerThread::run() {
     pthread_setname_np(pthread_self(), "mrpc_timer");
+    // deadlines are kept to the microsecond: without this the kernel may
+    // defer every timed futex wait by the default 50 us timer slack
+    prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);
     struct Cmp {
         bool operator()(const Task* a, const Task* b) const { return a->run_us > b->run_us; }
     };
