@@ -395,7 +395,9 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     return true;
 }
 
-std::atomic<int64_t> g_indexed_parses{0}, g_index_fallbacks{0};
+std::atomic<int64_t> g_indexed_parses{0}, g_index_fallbacks{0}, g_packs{0};
+
+
 
 // SetPbParseOffload hook: snappy decode + pb_scan in one device pass; the
 // host merges the top-level fields from the table (bytes fields become one
@@ -453,6 +455,27 @@ bool offload(const Buf& in, Buf* out, bool compress) {
     return true;
 }
 
+// SetSnappyPackOffload hook: the message is serialized once, straight into
+// a pinned block the compress kernel reads in place (no serialize-then-copy)
+bool pack_offload(const pb::Message& msg, size_t n, Buf* out) {
+    if (g_device < 0 || n == 0 || !FLAGS_gpu_snappy_direct_host) return false;
+    PinnedBuf body(n);
+    if (!body.p) return false;
+    uint8_t* e = msg.SerializeWithCachedSizesToArray(reinterpret_cast<uint8_t*>(body.p));
+    if ((size_t)(e - reinterpret_cast<uint8_t*>(body.p)) != n) return false;
+    Buf raw;
+    body.give_to(&raw);
+    // serialize-only from here: a failed device compress falls back to the CPU codec on the same bytes
+    Buf result;
+    if (!offload(raw, &result, true)) {
+        if (!CompressBuf(COMPRESS_TYPE_SNAPPY, raw, out)) return false;
+        return true;
+    }
+    g_packs.fetch_add(1, std::memory_order_relaxed);
+    out->append(std::move(result));
+    return true;
+}
+
 }  // namespace
 
 int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
@@ -460,6 +483,8 @@ int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
     g_device = device;
     SetSnappyOffload(offload, min_bytes);
     SetPbParseOffload(parse_offload, min_bytes);
+    SetSnappyPackOffload(pack_offload, min_bytes);
+    static var::PassiveStatus<int64_t> v6("gpu_snappy_packs", [] { return g_packs.load(); });
     static var::PassiveStatus<int64_t> v1("gpu_snappy_compress_calls", [] { return g_comp_calls.load(); });
     static var::PassiveStatus<int64_t> v2("gpu_snappy_decompress_calls", [] { return g_decomp_calls.load(); });
     static var::PassiveStatus<int64_t> v3("gpu_snappy_fallbacks", [] { return g_fallbacks.load(); });
@@ -471,6 +496,7 @@ int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
 void DisableGpuSnappy() {
     SetSnappyOffload(nullptr, (size_t)-1);
     SetPbParseOffload(nullptr, (size_t)-1);
+    SetSnappyPackOffload(nullptr, (size_t)-1);
 }
 
 GpuSnappyStats GetGpuSnappyStats() {
@@ -480,6 +506,7 @@ GpuSnappyStats GetGpuSnappyStats() {
     s.fallbacks = g_fallbacks.load();
     s.indexed_parses = g_indexed_parses.load();
     s.index_fallbacks = g_index_fallbacks.load();
+    s.packs = g_packs.load();
     return s;
 }
 

@@ -18,6 +18,7 @@ void DisableGpuSnappy();
 struct GpuSnappyStats {
     int64_t compress_calls = 0, decompress_calls = 0, fallbacks = 0;
     int64_t indexed_parses = 0, index_fallbacks = 0;  // decompress + pb_scan parses
+    int64_t packs = 0;  // bodies serialized straight into pinned memory and compressed there
 };
 GpuSnappyStats GetGpuSnappyStats();
 

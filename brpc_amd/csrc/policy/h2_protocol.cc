@@ -750,8 +750,12 @@ void SerializeH2Request(Buf* buf, Controller* cntl, const pb::Message* request) 
             return;
         }
         if (grpc || h.content_type().find("proto") != std::string::npos) {
-            Buf pbbuf;
-            if (!request->SerializeToBuf(&pbbuf)) {
+            Buf pbbuf, z;
+            // a device snappy codec serializes straight into memory its
+            // kernel reads and compresses from there (rpc/compress.h)
+            const bool packed = grpc && cntl->request_compress_type() == COMPRESS_TYPE_SNAPPY &&
+                                TrySnappyPackOffload(*request, &z);
+            if (!packed && !request->SerializeToBuf(&pbbuf)) {
                 cntl->SetFailed(EREQUEST, "Fail to serialize request");
                 return;
             }
@@ -761,8 +765,7 @@ void SerializeH2Request(Buf* buf, Controller* cntl, const pb::Message* request) 
                 const int ct = cntl->request_compress_type();
                 bool compressed = false;
                 if (ct != COMPRESS_TYPE_NONE) {
-                    Buf z;
-                    if (!CompressBuf((CompressType)ct, pbbuf, &z)) {
+                    if (!packed && !CompressBuf((CompressType)ct, pbbuf, &z)) {
                         cntl->SetFailed(EREQUEST, "Fail to compress the grpc request with %s", CompressTypeToCStr((CompressType)ct));
                         return;
                     }
@@ -948,9 +951,11 @@ static void SendH2Response(H2ServerCall c) {
             Buf pbbuf;
             const int ct = cntl->response_compress_type();
             Buf z;
-            if (!c.res->IsInitialized() || !c.res->SerializeToBuf(&pbbuf)) {
+            const bool init = c.res->IsInitialized();
+            const bool packed = init && ct == COMPRESS_TYPE_SNAPPY && TrySnappyPackOffload(*c.res, &z);
+            if (!init || (!packed && !c.res->SerializeToBuf(&pbbuf))) {
                 cntl->SetFailed(ERESPONSE, "Fail to serialize response");
-            } else if (ct != COMPRESS_TYPE_NONE && !CompressBuf((CompressType)ct, pbbuf, &z)) {
+            } else if (ct != COMPRESS_TYPE_NONE && !packed && !CompressBuf((CompressType)ct, pbbuf, &z)) {
                 cntl->SetFailed(ERESPONSE, "Fail to compress the grpc response");
             } else if (ct != COMPRESS_TYPE_NONE) {
                 hs.push_back({"grpc-encoding", CompressTypeToGrpcEncoding(ct)});

@@ -667,6 +667,7 @@ PYBIND11_MODULE(_native, m) {
         d["fallbacks"] = s.fallbacks;
         d["indexed_parses"] = s.indexed_parses;
         d["index_fallbacks"] = s.index_fallbacks;
+        d["packs"] = s.packs;
         return d;
     });
     g.def("codec_batch_stats", [] {

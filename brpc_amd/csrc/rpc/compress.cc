@@ -7,6 +7,7 @@
 
 #include "base/logging.h"
 #include "base/snappy.h"
+#include "pb/message.h"
 
 namespace mrpc {
 
@@ -181,6 +182,23 @@ int TryPbParseOffload(const Buf& compressed, CompressType type, pb::Message* msg
     PbParseOffload off = g_pb_offload.load(std::memory_order_acquire);
     if (!off || type != COMPRESS_TYPE_SNAPPY || snappy_ulen(compressed) < g_pb_offload_min) return 0;
     return off(compressed, type, msg);
+}
+
+namespace {
+std::atomic<SnappyPackOffload> g_pack_offload{nullptr};
+size_t g_pack_offload_min = (size_t)-1;
+}  // namespace
+
+void SetSnappyPackOffload(SnappyPackOffload fn, size_t min_bytes) {
+    g_pack_offload_min = min_bytes;
+    g_pack_offload.store(fn, std::memory_order_release);
+}
+
+bool TrySnappyPackOffload(const pb::Message& msg, Buf* out) {
+    SnappyPackOffload off = g_pack_offload.load(std::memory_order_acquire);
+    if (!off) return false;
+    const size_t n = msg.ByteSizeLong();  // caches the sizes the serializer uses
+    return n >= g_pack_offload_min && off(msg, n, out);
 }
 
 void SetSnappyOffload(SnappyOffload fn, size_t min_bytes) {

@@ -38,6 +38,15 @@ void SetSnappyOffload(SnappyOffload fn, size_t min_bytes);
 namespace pb {
 class Message;
 }
+// Serialize-and-compress offload for snappy bodies of at least min_bytes
+// (serialized size): the device codec serializes the message straight into
+// memory its kernel reads (pinned) and compresses from there, so the body
+// is written once on the host instead of serialized and then copied.
+// Returns false to fall back to serialize + CompressBuf.
+typedef bool (*SnappyPackOffload)(const pb::Message& msg, size_t serialized_size, Buf* out);
+void SetSnappyPackOffload(SnappyPackOffload fn, size_t min_bytes);
+bool TrySnappyPackOffload(const pb::Message& msg, Buf* out);
+
 typedef int (*PbParseOffload)(const Buf& compressed, CompressType type, pb::Message* msg);
 void SetPbParseOffload(PbParseOffload fn, size_t min_bytes);
 // Runs the hook for `type` if one is installed and the body is large

@@ -110,6 +110,7 @@ bool SerializeAsCompressedData(const pb::Message& msg, Buf* buf, CompressType ty
         return true;
     }
     if (type == COMPRESS_TYPE_NONE) return msg.SerializeToBuf(buf);
+    if (type == COMPRESS_TYPE_SNAPPY && TrySnappyPackOffload(msg, buf)) return true;
     Buf raw;
     if (!msg.SerializeToBuf(&raw)) return false;
     return CompressBuf(type, raw, buf);

@@ -243,6 +243,8 @@ def test_grpc_snappy_bodies_on_gpu():
         # ... and parsed from the pb_scan field table of the decoded bytes
         assert after["indexed_parses"] - before["indexed_parses"] >= 400, (before, after)
         assert after["index_fallbacks"] == before["index_fallbacks"], (before, after)
+        # every body was serialized straight into pinned memory for the kernel
+        assert after["packs"] - before["packs"] >= 400, (before, after)
     finally:
         native.gpu.disable_snappy()
         s.stop()
