@@ -417,9 +417,22 @@ def main():
             ("baidu_std_snappy_64KB", {"protocol": "baidu_std", "request_compress_type": 1},
              lambda: native.gpu.enable_snappy(topo.device, 16384), lambda: native.gpu.disable_snappy(),
              lambda: native.gpu.snappy_stats()["indexed_parses"]),
+            # 16k packed int64 ids per request and response (~70 KiB bodies):
+            # with the GPU codec the device encodes the ids into the body in
+            # the compress batch; device_bodies counts those runs
+            ("baidu_std_snappy_ids16k", {"protocol": "baidu_std", "request_compress_type": 1, "request_size": 16,
+                                         "packed_ids": 16384},
+             lambda: native.gpu.enable_snappy(topo.device, 16384), lambda: native.gpu.disable_snappy(),
+             lambda: native.gpu.snappy_stats()["pack_runs"]),
             ("http_json_64KB", {"protocol": "http", "connection_type": "pooled"},
              lambda: native.gpu.enable_json_index(topo.device, 16384), lambda: native.gpu.disable_json_index(),
              lambda: native.gpu.json_stats()["indexed_bodies"]),
+            # the same 16k ids over http + json: pb2json prints the arrays on
+            # the device; device_bodies counts printed arrays
+            ("http_json_ids16k", {"protocol": "http", "connection_type": "pooled", "request_size": 16,
+                                  "packed_ids": 16384},
+             lambda: native.gpu.enable_json_index(topo.device, 16384), lambda: native.gpu.disable_json_index(),
+             lambda: native.gpu.json_stats()["pb2json_arrays"]),
         )
         for name, extra, enable, disable, count in codec_legs:
             wlx = EchoWorkload(name, request_size=65536, attachment_size=0,

@@ -43,7 +43,9 @@ struct PinnedArray {
 
 struct CBatch {
     std::vector<CodecRequest*> reqs;
-    std::vector<size_t> comp_first, decomp_first, stream_first, piece_first, scan_row;
+    std::vector<size_t> comp_first, decomp_first, stream_first, piece_first, scan_row, run_first;
+    PinnedArray<PbRunChunk> run_jobs;
+    PinnedArray<int32_t> run_err;
     PinnedArray<SnappyPiece> piece_jobs;
     PinnedArray<int> piece_job_err;
     PinnedArray<SnappyJob> comp_jobs, decomp_jobs;
@@ -110,7 +112,7 @@ void throttle(Engine& e) {
 }
 
 Engine g_engine[kMaxDev];
-std::atomic<int64_t> g_requests{0}, g_launches{0};
+std::atomic<int64_t> g_requests{0}, g_launches{0}, g_run_chunks{0};
 
 CBatch* new_batch(Engine& e) {
     if (!e.spare.empty()) {
@@ -126,7 +128,7 @@ CBatch* new_batch(Engine& e) {
 // Lay the batch's requests out in its pinned tables and issue one stream
 // sequence; false when nothing could be launched.
 bool launch(CBatch* b, int device) {
-    size_t ncomp = 0, ndecomp = 0, nscan = 0, nstreams = 0, npieces = 0, nhpieces = 0;
+    size_t ncomp = 0, ndecomp = 0, nscan = 0, nstreams = 0, npieces = 0, nhpieces = 0, nruns = 0;
     uint32_t comp_max = 1, decomp_max = 1, piece_limit = 0, hpiece_max = 1;
     std::vector<Segment> h2d, d2h;
     b->comp_first.clear();
@@ -134,7 +136,10 @@ bool launch(CBatch* b, int device) {
     b->stream_first.clear();
     b->piece_first.clear();
     b->scan_row.clear();
+    b->run_first.clear();
     for (CodecRequest* r : b->reqs) {
+        b->run_first.push_back(nruns);
+        nruns += r->runs.size();
         b->comp_first.push_back(ncomp);
         b->decomp_first.push_back(ndecomp);
         b->stream_first.push_back(nstreams);
@@ -157,7 +162,8 @@ bool launch(CBatch* b, int device) {
         !b->decomp_jobs.reserve(ndecomp) || !b->decomp_len.reserve(ndecomp) || !b->decomp_err.reserve(ndecomp) ||
         !b->scan_jobs.reserve(nscan) || !b->scan_fields.reserve(nscan * 2 * kCodecScanFields) ||
         !b->scan_n.reserve(nscan) || !b->stream_jobs.reserve(nstreams) || !b->stream_err.reserve(nstreams) ||
-        !b->piece_err.reserve(npieces) || !b->piece_jobs.reserve(nhpieces) || !b->piece_job_err.reserve(nhpieces)) {
+        !b->piece_err.reserve(npieces) || !b->piece_jobs.reserve(nhpieces) || !b->piece_job_err.reserve(nhpieces) ||
+        !b->run_jobs.reserve(nruns) || !b->run_err.reserve(nruns)) {
         return false;
     }
     if (npieces > b->pieces_cap) {
@@ -173,6 +179,7 @@ bool launch(CBatch* b, int device) {
         std::copy(r->decomp.begin(), r->decomp.end(), b->decomp_jobs.p + b->decomp_first[i]);
         if (r->want_scan) b->scan_jobs.p[b->scan_row[i]] = r->scan;
         std::copy(r->pieces.begin(), r->pieces.end(), b->piece_jobs.p + b->piece_first[i]);
+        std::copy(r->runs.begin(), r->runs.end(), b->run_jobs.p + b->run_first[i]);
     }
     for (size_t i = 0, g = 0, first = 0; i < b->reqs.size(); ++i) {
         for (const SnappyStream& st : b->reqs[i]->streams) {
@@ -197,6 +204,8 @@ bool launch(CBatch* b, int device) {
     hipStream_t s = PoolStream(device);
     b->ev = AcquireEvent();
     int rc = (s && b->ev) ? 0 : -1;
+    if (rc == 0 && nruns) rc = LaunchPbRunEncode(b->run_jobs.p, (int)nruns, b->run_err.p, s);
+    g_run_chunks.fetch_add((int64_t)nruns, std::memory_order_relaxed);
     if (rc == 0 && !h2d.empty()) rc = LaunchBatchedCopy(h2d.data(), (int)h2d.size(), s);
     if (rc == 0 && ncomp) {
         rc = LaunchSnappyCompress(b->comp_jobs.p, (int)ncomp, comp_max, b->scratch, b->comp_len.p, b->comp_err.p, s);
@@ -292,6 +301,8 @@ int RunCodecRequest(CodecRequest* r, int device) {
         r->comp_err.assign(mine->comp_err.p + c0, mine->comp_err.p + c0 + r->comp.size());
         r->decomp_len.assign(mine->decomp_len.p + d0, mine->decomp_len.p + d0 + r->decomp.size());
         r->decomp_err.assign(mine->decomp_err.p + d0, mine->decomp_err.p + d0 + r->decomp.size());
+        const size_t r0 = mine->run_first[idx];
+        r->run_err.assign(mine->run_err.p + r0, mine->run_err.p + r0 + r->runs.size());
         const size_t p0 = mine->piece_first[idx];
         r->piece_err.assign(mine->piece_job_err.p + p0, mine->piece_job_err.p + p0 + r->pieces.size());
         r->stream_err.assign(r->streams.size(), 0);
@@ -317,6 +328,7 @@ CodecBatchStats GetCodecBatchStats() {
     CodecBatchStats s;
     s.requests = g_requests.load(std::memory_order_relaxed);
     s.launches = g_launches.load(std::memory_order_relaxed);
+    s.run_chunks = g_run_chunks.load(std::memory_order_relaxed);
     return s;
 }
 

@@ -18,6 +18,9 @@ namespace mrpc {
 namespace gpu {
 
 struct CodecRequest {
+    // numeric runs encoded first (K2 packed fields / K6 JSON arrays), into
+    // buffers the later stages may read (the body the compressor takes)
+    std::vector<PbRunChunk> runs;
     // staging copies issued before the codec kernels (host/pinned -> HBM)
     std::vector<Segment> h2d;
     // codec jobs; pointers in the jobs are device-accessible
@@ -42,6 +45,7 @@ struct CodecRequest {
     std::vector<int> comp_err, decomp_err;
     std::vector<int> stream_err;  // 0, or the split / piece decode code
     std::vector<int> piece_err;
+    std::vector<int32_t> run_err;  // per chunk: 0, or 1 when the device size disagreed (nothing written)
     std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields
     int32_t scan_nfields = -1;
 };
@@ -53,7 +57,7 @@ constexpr uint32_t kCodecScanFields = 128;
 int RunCodecRequest(CodecRequest* r, int device);
 
 struct CodecBatchStats {
-    int64_t requests = 0, launches = 0;
+    int64_t requests = 0, launches = 0, run_chunks = 0;
 };
 CodecBatchStats GetCodecBatchStats();
 

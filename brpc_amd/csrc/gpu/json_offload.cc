@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 
@@ -18,10 +19,14 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
+#include "gpu/snappy_offload.h"
 #include "json/json2pb.h"
 #include "rpc/span.h"
 #include "var/var.h"
 
+DEFINE_int32(gpu_pb2json_min_elems, 4096,
+             "repeated integer/bool fields with at least this many elements are printed by the device in pb2json "
+             "(pb_run_encode_kernel, decimal format) while the GPU JSON path is enabled");
 DEFINE_bool(json_index_direct_host, true,
             "the JSON index kernel reads the pinned body and writes positions to pinned memory directly");
 
@@ -140,23 +145,52 @@ int JsonIndex(const char* data, size_t n, std::vector<uint32_t>* out, int device
     return rc == 0 ? 0 : -1;
 }
 
+namespace {
+
+std::atomic<int64_t> g_arrays{0}, g_array_elems{0}, g_array_failures{0};
+
+// pb2json number arrays: pb_run_encode_kernel prints the
+// field's values in the codec batch (gpu/snappy_offload.h
+// EncodeRunOnDevice), the host only sizes them and wraps the brackets.
+bool array_offload(const void* values, size_t n, uint32_t kind, std::string* text) {
+    const int dev = g_device;
+    if (dev < 0) return false;
+    if (EncodeRunOnDevice(values, n, kind, PB_RUN_DECIMAL, text, dev) != 0) {
+        g_array_failures.fetch_add(1, std::memory_order_relaxed);
+        return false;
+    }
+    g_arrays.fetch_add(1, std::memory_order_relaxed);
+    g_array_elems.fetch_add((int64_t)n, std::memory_order_relaxed);
+    return true;
+}
+
+}  // namespace
+
 int EnableGpuJsonIndex(int device, size_t min_bytes, std::string* error) {
     if (Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
     g_device = device;
     json2pb::SetJsonIndexOffload(offload, min_bytes);
+    json2pb::SetPb2JsonArrayOffload(array_offload, (size_t)std::max(1, FLAGS_gpu_pb2json_min_elems));
+    static var::PassiveStatus<int64_t> v4("gpu_pb2json_arrays", [] { return g_arrays.load(); });
     static var::PassiveStatus<int64_t> v1("gpu_json_indexed_bodies", [] { return g_bodies.load(); });
     static var::PassiveStatus<int64_t> v2("gpu_json_indexed_bytes", [] { return g_bytes.load(); });
     static var::PassiveStatus<int64_t> v3("gpu_json_index_failures", [] { return g_failures.load(); });
     return 0;
 }
 
-void DisableGpuJsonIndex() { json2pb::SetJsonIndexOffload(nullptr, (size_t)-1); }
+void DisableGpuJsonIndex() {
+    json2pb::SetJsonIndexOffload(nullptr, (size_t)-1);
+    json2pb::SetPb2JsonArrayOffload(nullptr, (size_t)-1);
+}
 
 GpuJsonStats GetGpuJsonStats() {
     GpuJsonStats s;
     s.indexed_bodies = g_bodies.load();
     s.indexed_bytes = g_bytes.load();
     s.failures = g_failures.load();
+    s.pb2json_arrays = g_arrays.load();
+    s.pb2json_elems = g_array_elems.load();
+    s.pb2json_failures = g_array_failures.load();
     return s;
 }
 

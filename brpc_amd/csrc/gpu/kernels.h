@@ -145,6 +145,40 @@ struct PbScanJob {
 int LaunchPbScanPtrs(const PbScanJob* jobs, int64_t n, uint32_t max_fields, uint64_t* fields, int32_t* nfields,
                      hipStream_t s);
 
+// Batched encoder of repeated numeric runs (SURVEY K2, and the number
+// arrays of pb2json, K6): one workgroup per chunk of <= kPbRunChunkElems
+// elements, read in the std::vector layout of the field (1/4/8 bytes per
+// element), written as protobuf varints (the payload of a packed field) or
+// as comma-separated JSON numbers. The host knows every chunk's output size
+// (its size pass) and so its destination: chunks of many runs of many
+// messages go into one launch with no device-side scan across chunks.
+constexpr uint32_t kPbRunChunkElems = 2048;
+enum PbRunKind : uint32_t {
+    PB_RUN_INT32 = 0,   // int32/enum: sign-extended to 64 bits (negative -> 10 bytes)
+    PB_RUN_UINT32 = 1,
+    PB_RUN_SINT32 = 2,  // zigzag32
+    PB_RUN_INT64 = 3,
+    PB_RUN_UINT64 = 4,
+    PB_RUN_SINT64 = 5,  // zigzag64
+    PB_RUN_BOOL = 6,    // one byte per element
+};
+enum PbRunFormat : uint32_t {
+    PB_RUN_VARINT = 0,
+    PB_RUN_DECIMAL = 1,  // JSON: "v,v,...,v" (true/false for bools); no trailing comma on a run's last chunk
+};
+struct PbRunChunk {
+    const void* src;  // this chunk's first element (device-readable)
+    uint8_t* dst;     // this chunk's first output byte (device-writable)
+    uint32_t count;   // elements, 1..kPbRunChunkElems
+    uint32_t kind;    // PbRunKind
+    uint32_t format;  // PbRunFormat
+    uint32_t last;    // 1: the run's last chunk (decimal: no trailing comma)
+    uint32_t bytes;   // output size the host computed; a mismatch is reported and nothing is written
+    uint32_t pad;
+};
+// err[i] is set to 0 (ok) or 1 (size mismatch) for every chunk.
+int LaunchPbRunEncode(const PbRunChunk* chunks, int n, int32_t* err, hipStream_t s);
+
 // JSON structural index (gpu/json_kernels.hip): out_pos receives, in order,
 // the byte offsets of every unescaped '"' and of every { } [ ] : , outside
 // strings; count_dev the number found (positions past max_out are dropped

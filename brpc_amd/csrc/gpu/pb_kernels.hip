@@ -127,7 +127,155 @@ __global__ void __launch_bounds__(256) pb_scan_ptrs_kernel(const PbScanJob* __re
     nfields[i] = scan_message((gbyte_c*)job.buf, 0, job.len, fields + (uint64_t)i * max_fields * 2, max_fields);
 }
 
+// ------------------------------------------------------------ run encoder
+// One workgroup (4 waves) per PbRunChunk. The chunk is walked in 8 rounds
+// of 256 consecutive elements: lane t of round r takes element 256r + t
+// (a coalesced 1/4/8-byte load from the source, pinned host or HBM), the
+// encoded lengths are block-scanned (wave shuffles + 4 wave totals in LDS)
+// and every lane writes its bytes into the chunk's output image in LDS
+// (<= 21 B per element: 43 KiB). The image then leaves with byte stores
+// that are contiguous across the lanes of each instruction, so a host
+// destination sees full-line PCIe writes instead of one small write per
+// varint.
+constexpr int kRunThreads = 256;
+constexpr uint32_t kRunMaxElemBytes = 21;  // "-9223372036854775808" + ','
+
+__device__ __forceinline__ uint64_t run_value(const void* src, uint32_t i, uint32_t kind) {
+    switch (kind) {
+    case PB_RUN_INT32: return (uint64_t)(int64_t)static_cast<const int32_t*>(src)[i];
+    case PB_RUN_UINT32: return static_cast<const uint32_t*>(src)[i];
+    case PB_RUN_SINT32: {
+        const int32_t v = static_cast<const int32_t*>(src)[i];
+        return (uint32_t)(((uint32_t)v << 1) ^ (uint32_t)(v >> 31));
+    }
+    case PB_RUN_SINT64: {
+        const int64_t v = static_cast<const int64_t*>(src)[i];
+        return ((uint64_t)v << 1) ^ (uint64_t)(v >> 63);
+    }
+    case PB_RUN_BOOL: return static_cast<const uint8_t*>(src)[i] ? 1 : 0;
+    default: return static_cast<const uint64_t*>(src)[i];
+    }
+}
+
+// For decimal output the value is printed as its field type says: signed
+// kinds as two's complement of their width (zigzag undone: the JSON shows
+// the number, not its wire form).
+__device__ __forceinline__ bool run_negative(const void* src, uint32_t i, uint32_t kind, uint64_t* mag) {
+    int64_t s;
+    switch (kind) {
+    case PB_RUN_INT32:
+    case PB_RUN_SINT32: s = static_cast<const int32_t*>(src)[i]; break;
+    case PB_RUN_INT64:
+    case PB_RUN_SINT64: s = static_cast<const int64_t*>(src)[i]; break;
+    case PB_RUN_UINT32: *mag = static_cast<const uint32_t*>(src)[i]; return false;
+    case PB_RUN_BOOL: *mag = static_cast<const uint8_t*>(src)[i] ? 1 : 0; return false;
+    default: *mag = static_cast<const uint64_t*>(src)[i]; return false;
+    }
+    *mag = s < 0 ? (uint64_t)0 - (uint64_t)s : (uint64_t)s;
+    return s < 0;
+}
+
+__device__ __forceinline__ uint32_t run_varint_len(uint64_t v) {
+    const int bits = v ? 64 - __clzll(v) : 1;
+    return (uint32_t)((bits + 6) / 7);
+}
+
+__device__ __forceinline__ uint32_t run_digits(uint64_t v) {
+    uint32_t d = 1;
+    uint64_t p = 10;
+    while (d < 20 && v >= p) {
+        ++d;
+        p *= 10;
+    }
+    return d;
+}
+
+__global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunChunk* __restrict__ chunks,
+                                                                    int32_t* __restrict__ err) {
+    __shared__ uint8_t image[kPbRunChunkElems * kRunMaxElemBytes];
+    __shared__ uint32_t wave_tot[kRunThreads / 64];
+    __shared__ uint32_t round_base;
+    const PbRunChunk c = chunks[blockIdx.x];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const bool decimal = c.format == PB_RUN_DECIMAL;
+    if (t == 0) round_base = 0;
+    __syncthreads();
+    const uint32_t count = c.count < kPbRunChunkElems ? c.count : kPbRunChunkElems;
+    for (uint32_t r0 = 0; r0 < count; r0 += kRunThreads) {
+        const uint32_t i = r0 + t;
+        uint32_t len = 0;
+        uint64_t v = 0;
+        bool neg = false;
+        if (i < count) {
+            if (!decimal) {
+                v = run_value(c.src, i, c.kind);
+                len = run_varint_len(v);
+            } else if (c.kind == PB_RUN_BOOL) {
+                run_negative(c.src, i, c.kind, &v);
+                len = v ? 4 : 5;
+            } else {
+                neg = run_negative(c.src, i, c.kind, &v);
+                len = run_digits(v) + (neg ? 1 : 0);
+            }
+            if (decimal && !(c.last && i + 1 == count)) len += 1;  // ','
+        }
+        // block exclusive scan of len in element order
+        uint32_t incl = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wave_tot[wave] = incl;
+        __syncthreads();
+        uint32_t pos = round_base + incl - len;
+        for (int w = 0; w < wave; ++w) pos += wave_tot[w];
+        const uint32_t round_total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+        if (i < count) {
+            uint8_t* o = image + pos;
+            if (!decimal) {
+                for (uint32_t j = 0; j < len; ++j) {
+                    o[j] = (uint8_t)((v & 0x7f) | (j + 1 < len ? 0x80 : 0));
+                    v >>= 7;
+                }
+            } else if (c.kind == PB_RUN_BOOL) {
+                const char* s = v ? "true" : "false";
+                const uint32_t n = v ? 4 : 5;
+                for (uint32_t j = 0; j < n; ++j) o[j] = (uint8_t)s[j];
+                if (len > n) o[n] = ',';
+            } else {
+                const uint32_t nd = run_digits(v);
+                uint32_t k = 0;
+                if (neg) o[k++] = '-';
+                for (uint32_t j = 0; j < nd; ++j) {
+                    const uint64_t q = v / 10;
+                    o[k + nd - 1 - j] = (uint8_t)('0' + (uint32_t)(v - q * 10));
+                    v = q;
+                }
+                k += nd;
+                if (len > k) o[k] = ',';
+            }
+        }
+        __syncthreads();  // wave_tot is rewritten by the next round
+        if (t == 0) round_base += round_total;
+        __syncthreads();
+    }
+    const uint32_t total = round_base;
+    if (total != c.bytes) {
+        if (t == 0) err[blockIdx.x] = 1;
+        return;
+    }
+    for (uint32_t j = t; j < total; j += kRunThreads) c.dst[j] = image[j];
+    if (t == 0) err[blockIdx.x] = 0;
+}
+
 }  // namespace
+
+int LaunchPbRunEncode(const PbRunChunk* chunks, int n, int32_t* err, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(pb_run_encode_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int LaunchPbScan(const uint8_t* buf, uint64_t buf_len, const int64_t* offsets_dev, int64_t n, uint32_t max_fields,
                  uint64_t* fields, int32_t* nfields, hipStream_t s) {

@@ -58,6 +58,10 @@ DEFINE_bool(gpu_snappy_device_split, false,
 DEFINE_bool(gpu_snappy_direct_host, true,
             "codec kernels read their host input and write their host output in pinned memory directly (no "
             "staging copy kernels around them): two kernels fewer per decode, one per encode");
+DEFINE_int32(gpu_pb_pack_min_elems, 4096,
+             "packed varint fields with at least this many elements are encoded on the device (pb_run_encode_kernel) "
+             "when their message goes through the GPU snappy codec, in the same batch as the compress kernel; 0: "
+             "never");
 DEFINE_int32(gpu_snappy_block_kb, 4,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
              "waves (lower latency) at some cost in ratio; <= 64");
@@ -152,7 +156,59 @@ bool device_blocks_elsewhere(const Buf& in, int device) {
     return false;
 }
 
-bool gpu_compress(const Buf& in, Buf* out) {
+static_assert(kPbRunChunkElems == pb::kPackedRunChunkElems, "serializer and kernel chunking differ");
+
+uint32_t run_kind(pb::FieldType t) {
+    switch (t) {
+    case pb::FieldType::INT32:
+    case pb::FieldType::ENUM: return PB_RUN_INT32;
+    case pb::FieldType::UINT32: return PB_RUN_UINT32;
+    case pb::FieldType::SINT32: return PB_RUN_SINT32;
+    case pb::FieldType::INT64: return PB_RUN_INT64;
+    case pb::FieldType::UINT64: return PB_RUN_UINT64;
+    case pb::FieldType::SINT64: return PB_RUN_SINT64;
+    default: return PB_RUN_BOOL;
+    }
+}
+
+// Collects the packed runs the serializer skipped (pb::PackedRunSink).
+struct RunCollector : public pb::PackedRunSink {
+    std::vector<pb::PackedRun> runs;
+    size_t value_bytes = 0;
+    size_t min_elems() const override { return (size_t)std::max(1, FLAGS_gpu_pb_pack_min_elems); }
+    void Take(pb::PackedRun&& r) override {
+        value_bytes += r.n * r.elem_bytes;
+        runs.push_back(std::move(r));
+    }
+};
+
+// The runs' values copied into one pinned buffer (the kernel cannot read
+// pageable vectors) and cut into device chunks.
+bool stage_runs(const RunCollector& col, PinnedBuf* stage, std::vector<PbRunChunk>* chunks) {
+    size_t off = 0;
+    for (const pb::PackedRun& r : col.runs) {
+        char* v = stage->p + off;
+        memcpy(v, r.values, r.n * r.elem_bytes);
+        uint8_t* d = r.dst;
+        for (size_t c = 0, k = 0; c < r.n; c += kPbRunChunkElems, ++k) {
+            PbRunChunk ch;
+            ch.src = v + c * r.elem_bytes;
+            ch.dst = d;
+            ch.count = (uint32_t)std::min<size_t>(kPbRunChunkElems, r.n - c);
+            ch.kind = run_kind(r.type);
+            ch.format = PB_RUN_VARINT;
+            ch.last = c + kPbRunChunkElems >= r.n ? 1 : 0;
+            ch.bytes = r.chunk_bytes[k];
+            ch.pad = 0;
+            chunks->push_back(ch);
+            d += r.chunk_bytes[k];
+        }
+        off += (r.n * r.elem_bytes + 15) & ~(size_t)15;
+    }
+    return true;
+}
+
+bool gpu_compress(const Buf& in, Buf* out, const std::vector<PbRunChunk>* runs = nullptr) {
     const int dev = g_device;
     const size_t n = in.size();
     const size_t blk = (size_t)std::max(1, std::min(64, FLAGS_gpu_snappy_block_kb)) << 10;
@@ -184,8 +240,14 @@ bool gpu_compress(const Buf& in, Buf* out) {
         req.comp[i] = SnappyJob{src + off, comp.p + i * cap, std::min<size_t>(blk, n - off), cap};
     }
     req.comp_max_ulen = (uint32_t)std::min(blk, n);
+    // packed runs of the body are encoded into it first, in the same stream
+    // sequence (the compress kernel reads what the run kernel wrote)
+    if (runs) req.runs = *runs;
     // batched with the other RPCs' codec work: one launch sequence, one event
     if (RunCodecRequest(&req, dev) != 0) return false;
+    for (int32_t e : req.run_err) {
+        if (e) return false;
+    }
     for (size_t i = 0; i < nblk; ++i) {
         if (req.comp_err[i] || req.comp_len[i] > cap) return false;
     }
@@ -395,7 +457,7 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     return true;
 }
 
-std::atomic<int64_t> g_indexed_parses{0}, g_index_fallbacks{0}, g_packs{0};
+std::atomic<int64_t> g_indexed_parses{0}, g_index_fallbacks{0}, g_packs{0}, g_pack_runs{0}, g_pack_run_chunks{0};
 
 
 
@@ -457,19 +519,54 @@ bool offload(const Buf& in, Buf* out, bool compress) {
 
 // SetSnappyPackOffload hook: the message is serialized once, straight into
 // a pinned block the compress kernel reads in place (no serialize-then-copy)
+// Large packed varint fields are not encoded by the host at all: the
+// serializer leaves their payload to pb_run_encode_kernel, which writes it
+// into the pinned body in the same codec batch, right before the compress
+// kernel reads the body (SURVEY K2 on the path).
 bool pack_offload(const pb::Message& msg, size_t n, Buf* out) {
     if (g_device < 0 || n == 0 || !FLAGS_gpu_snappy_direct_host) return false;
     PinnedBuf body(n);
     if (!body.p) return false;
+    RunCollector col;
+    pb::PackedRunSink* prev = pb::SetThreadPackedRunSink(FLAGS_gpu_pb_pack_min_elems > 0 ? &col : nullptr);
     uint8_t* e = msg.SerializeWithCachedSizesToArray(reinterpret_cast<uint8_t*>(body.p));
+    pb::SetThreadPackedRunSink(prev);
     if ((size_t)(e - reinterpret_cast<uint8_t*>(body.p)) != n) return false;
+    std::vector<PbRunChunk> chunks;
+    PinnedBuf stage(col.value_bytes + 16 * col.runs.size() + 1);
+    bool device_runs = !col.runs.empty();
+    if (device_runs && (!stage.p || !stage_runs(col, &stage, &chunks))) {
+        for (const pb::PackedRun& r : col.runs) pb::EncodePackedRunOnHost(r);
+        device_runs = false;
+    }
     Buf raw;
     body.give_to(&raw);
-    // serialize-only from here: a failed device compress falls back to the CPU codec on the same bytes
     Buf result;
-    if (!offload(raw, &result, true)) {
-        if (!CompressBuf(COMPRESS_TYPE_SNAPPY, raw, out)) return false;
-        return true;
+    bool ok;
+    {
+        Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
+        const int64_t t0 = span ? monotonic_us() : 0;
+        ok = gpu_compress(raw, &result, device_runs ? &chunks : nullptr);
+        if (span) {
+            span->AnnotateDevice(string_printf("pb pack (%zu packed runs, %zu chunks) + snappy compress %zu -> %zu B dev%d%s",
+                                               col.runs.size(), chunks.size(), n, result.size(), g_device,
+                                               ok ? "" : " (fell back to CPU)"),
+                                 (float)(monotonic_us() - t0) / 1000.0f);
+        }
+    }
+    if (!ok) {
+        // the device did not finish: the host encodes what it skipped and
+        // the CPU codec compresses the same bytes
+        g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        if (device_runs) {
+            for (const pb::PackedRun& r : col.runs) pb::EncodePackedRunOnHost(r);
+        }
+        return CompressBuf(COMPRESS_TYPE_SNAPPY, raw, out);
+    }
+    g_comp_calls.fetch_add(1, std::memory_order_relaxed);
+    if (device_runs) {
+        g_pack_runs.fetch_add((int64_t)col.runs.size(), std::memory_order_relaxed);
+        g_pack_run_chunks.fetch_add((int64_t)chunks.size(), std::memory_order_relaxed);
     }
     g_packs.fetch_add(1, std::memory_order_relaxed);
     out->append(std::move(result));
@@ -478,6 +575,93 @@ bool pack_offload(const pb::Message& msg, size_t n, Buf* out) {
 
 }  // namespace
 
+namespace {
+
+size_t run_elem_bytes(uint32_t kind) {
+    switch (kind) {
+    case PB_RUN_BOOL: return 1;
+    case PB_RUN_INT32:
+    case PB_RUN_UINT32:
+    case PB_RUN_SINT32: return 4;
+    default: return 8;
+    }
+}
+
+// Output bytes of element p under kind/format (the host size pass; the
+// kernel checks it chunk by chunk).
+size_t run_elem_len(const char* p, uint32_t kind, uint32_t format) {
+    int64_t sv = 0;
+    uint64_t uv = 0;
+    bool is_signed = false;
+    switch (kind) {
+    case PB_RUN_BOOL: return format == PB_RUN_VARINT ? 1 : (*(const uint8_t*)p ? 4 : 5);
+    case PB_RUN_INT32: sv = *(const int32_t*)p; is_signed = true; break;
+    case PB_RUN_SINT32: sv = *(const int32_t*)p; is_signed = true; break;
+    case PB_RUN_UINT32: uv = *(const uint32_t*)p; break;
+    case PB_RUN_INT64:
+    case PB_RUN_SINT64: sv = *(const int64_t*)p; is_signed = true; break;
+    default: uv = *(const uint64_t*)p; break;
+    }
+    if (format == PB_RUN_VARINT) {
+        uint64_t w;
+        if (kind == PB_RUN_SINT32) w = (uint32_t)(((uint32_t)sv << 1) ^ (uint32_t)((int32_t)sv >> 31));
+        else if (kind == PB_RUN_SINT64) w = ((uint64_t)sv << 1) ^ (uint64_t)(sv >> 63);
+        else w = is_signed ? (uint64_t)sv : uv;
+        return (size_t)varint_len(w);
+    }
+    const bool neg = is_signed && sv < 0;
+    const uint64_t mag = is_signed ? (neg ? (uint64_t)0 - (uint64_t)sv : (uint64_t)sv) : uv;
+    size_t d = 1;
+    for (uint64_t p = 10; d < 20 && mag >= p; p *= 10) ++d;
+    return d + (neg ? 1 : 0);
+}
+
+}  // namespace
+
+int EncodeRunOnDevice(const void* values, size_t n, uint32_t kind, uint32_t format, std::string* out, int device) {
+    out->clear();
+    if (n == 0) return 0;
+    if (kind > PB_RUN_BOOL || format > PB_RUN_DECIMAL || device < 0) return -1;
+    if (Init(device) != 0) return -1;
+    const size_t eb = run_elem_bytes(kind);
+    const char* v = static_cast<const char*>(values);
+    std::vector<PbRunChunk> chunks;
+    size_t total = 0;
+    for (size_t c = 0; c < n; c += kPbRunChunkElems) {
+        const size_t e = std::min(n, c + kPbRunChunkElems);
+        size_t cb = 0;
+        for (size_t i = c; i < e; ++i) cb += run_elem_len(v + i * eb, kind, format) + (format == PB_RUN_DECIMAL && i + 1 < n);
+        PbRunChunk ch;
+        ch.src = nullptr;
+        ch.dst = nullptr;
+        ch.count = (uint32_t)(e - c);
+        ch.kind = kind;
+        ch.format = format;
+        ch.last = e == n ? 1 : 0;
+        ch.bytes = (uint32_t)cb;
+        ch.pad = 0;
+        chunks.push_back(ch);
+        total += cb;
+    }
+    PinnedBuf stage(n * eb), dst(total ? total : 1);
+    if (!stage.p || !dst.p) return -1;
+    memcpy(stage.p, values, n * eb);
+    size_t off = 0;
+    for (size_t k = 0; k < chunks.size(); ++k) {
+        chunks[k].src = stage.p + k * kPbRunChunkElems * eb;
+        chunks[k].dst = reinterpret_cast<uint8_t*>(dst.p) + off;
+        off += chunks[k].bytes;
+    }
+    CodecRequest req;
+    req.runs = chunks;
+    if (RunCodecRequest(&req, device) != 0) return -1;
+    for (int32_t e : req.run_err) {
+        if (e) return -1;
+    }
+    out->assign(dst.p, total);
+    return 0;
+}
+
 int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
     if (Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
     g_device = device;
@@ -485,6 +669,7 @@ int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
     SetPbParseOffload(parse_offload, min_bytes);
     SetSnappyPackOffload(pack_offload, min_bytes);
     static var::PassiveStatus<int64_t> v6("gpu_snappy_packs", [] { return g_packs.load(); });
+    static var::PassiveStatus<int64_t> v7("gpu_pb_pack_runs", [] { return g_pack_runs.load(); });
     static var::PassiveStatus<int64_t> v1("gpu_snappy_compress_calls", [] { return g_comp_calls.load(); });
     static var::PassiveStatus<int64_t> v2("gpu_snappy_decompress_calls", [] { return g_decomp_calls.load(); });
     static var::PassiveStatus<int64_t> v3("gpu_snappy_fallbacks", [] { return g_fallbacks.load(); });
@@ -507,6 +692,8 @@ GpuSnappyStats GetGpuSnappyStats() {
     s.indexed_parses = g_indexed_parses.load();
     s.index_fallbacks = g_index_fallbacks.load();
     s.packs = g_packs.load();
+    s.pack_runs = g_pack_runs.load();
+    s.pack_run_chunks = g_pack_run_chunks.load();
     return s;
 }
 

@@ -19,8 +19,14 @@ struct GpuSnappyStats {
     int64_t compress_calls = 0, decompress_calls = 0, fallbacks = 0;
     int64_t indexed_parses = 0, index_fallbacks = 0;  // decompress + pb_scan parses
     int64_t packs = 0;  // bodies serialized straight into pinned memory and compressed there
+    int64_t pack_runs = 0, pack_run_chunks = 0;  // packed fields those bodies left to pb_run_encode_kernel
 };
 GpuSnappyStats GetGpuSnappyStats();
+
+// One numeric run through pb_run_encode_kernel (gpu/kernels.h PbRunKind /
+// PbRunFormat) via the codec batch: `values` in the field's vector layout,
+// `out` the varint payload or the JSON number list. 0 on success.
+int EncodeRunOnDevice(const void* values, size_t n, uint32_t kind, uint32_t format, std::string* out, int device);
 
 }  // namespace gpu
 }  // namespace mrpc

@@ -173,6 +173,7 @@ void Value::write(std::string* out, bool pretty, int indent) const {
         }
         break;
     case STRING: EscapeString(_s, out); break;
+    case RAW: *out += _s; break;
     case ARRAY:
         out->push_back('[');
         for (size_t i = 0; i < _arr.size(); ++i) {

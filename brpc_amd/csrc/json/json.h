@@ -15,7 +15,9 @@ namespace json {
 
 class Value {
 public:
-    enum Type { NUL, BOOL, INT, UINT, DOUBLE, STRING, ARRAY, OBJECT };
+    // RAW: pre-rendered JSON text written verbatim (an array of numbers
+    // printed by the device, json2pb's SetPb2JsonArrayOffload)
+    enum Type { NUL, BOOL, INT, UINT, DOUBLE, STRING, ARRAY, OBJECT, RAW };
     Value() : _type(NUL) {}
     explicit Value(bool b) : _type(BOOL), _b(b) {}
     explicit Value(int64_t i) : _type(INT), _i(i) {}
@@ -26,6 +28,7 @@ public:
     explicit Value(const char* s) : _type(STRING), _s(s) {}
     static Value Array() { Value v; v._type = ARRAY; return v; }
     static Value Object() { Value v; v._type = OBJECT; return v; }
+    static Value Raw(std::string text) { Value v; v._type = RAW; v._s = std::move(text); return v; }
 
     Type type() const { return _type; }
     bool is_null() const { return _type == NUL; }

@@ -2,6 +2,7 @@
 
 #include <strings.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cctype>
 #include <cerrno>
@@ -97,6 +98,33 @@ bool field_value(const Message& m, const FieldDescriptor* f, int idx, json::Valu
     return true;
 }
 
+std::atomic<Pb2JsonArrayOffload> g_array_offload{nullptr};
+std::atomic<size_t> g_array_offload_min{(size_t)-1};
+
+// Run kinds of gpu/kernels.h PbRunKind (decimal output prints the value,
+// so sint fields use their signed kinds).
+bool array_kind(const FieldDescriptor* f, const Pb2JsonOptions& opt, uint32_t* kind) {
+    switch (f->cpp_type()) {
+    case CppType::INT32: *kind = 0; return true;
+    case CppType::UINT32: *kind = 1; return true;
+    case CppType::INT64: *kind = 3; return true;
+    case CppType::UINT64: *kind = 4; return true;
+    case CppType::BOOL: *kind = 6; return true;
+    case CppType::ENUM: *kind = 0; return !(opt.enum_option_as_string && f->enum_type);
+    default: return false;
+    }
+}
+
+bool array_offload(const Message& m, const FieldDescriptor* f, const Pb2JsonOptions& opt, std::string* text) {
+    Pb2JsonArrayOffload fn = g_array_offload.load(std::memory_order_acquire);
+    uint32_t kind;
+    if (!fn || opt.pretty_json || !array_kind(f, opt, &kind)) return false;
+    size_t n = 0, eb = 0;
+    const void* data = Reflection::RepeatedScalarData(m, f, &n, &eb);
+    if (!data || n < g_array_offload_min.load(std::memory_order_relaxed)) return false;
+    return fn(data, n, kind, text);
+}
+
 bool msg_to_value(const Message& m, json::Value* out, const Pb2JsonOptions& opt, std::string* err) {
     *out = json::Value::Object();
     const pb::Descriptor* d = m.GetDescriptor();
@@ -133,6 +161,13 @@ bool msg_to_value(const Message& m, json::Value* out, const Pb2JsonOptions& opt,
         if (f->is_repeated()) {
             const int n = Reflection::FieldSize(m, f);
             if (n == 0 && !opt.jsonify_empty_array) continue;
+            std::string printed;
+            if (n > 0 && array_offload(m, f, opt, &printed)) {
+                printed.insert(printed.begin(), '[');
+                printed.push_back(']');
+                out->set(key, json::Value::Raw(std::move(printed)));
+                continue;
+            }
             json::Value arr = json::Value::Array();
             for (int i = 0; i < n; ++i) {
                 json::Value v;
@@ -235,6 +270,7 @@ private:
         case json::Value::STRING: return "\"" + v.as_string() + "\"";
         case json::Value::ARRAY: return "array";
         case json::Value::OBJECT: return "object";
+        case json::Value::RAW: return v.as_string();
         }
         return "";
     }
@@ -430,6 +466,11 @@ namespace {
 std::atomic<JsonIndexOffload> g_index_offload{nullptr};
 size_t g_index_min = (size_t)-1;
 }  // namespace
+
+void SetPb2JsonArrayOffload(Pb2JsonArrayOffload fn, size_t min_elems) {
+    g_array_offload_min.store(fn ? std::max<size_t>(1, min_elems) : (size_t)-1, std::memory_order_relaxed);
+    g_array_offload.store(fn, std::memory_order_release);
+}
 
 void SetJsonIndexOffload(JsonIndexOffload fn, size_t min_bytes) {
     g_index_min = min_bytes;

@@ -39,6 +39,13 @@ bool JsonValueToProtoMessage(const json::Value& v, pb::Message* msg, const Json2
 // Hook for a structural index of large bodies built on the GPU
 // (gpu/json_offload.cc, kernel K6): fills *index for data[0, n) and returns
 // true, or false to parse without one. Bodies of at least min_bytes use it.
+// pb2json of large repeated integer/bool fields: the offload
+// prints the numbers of one field — values in the field's vector layout,
+// kind a gpu PbRunKind — as "v,v,...,v" into *text (false: the host prints
+// them). Only for compact output (not pretty_json) and fields of at least
+// min_elems elements; enums printed as names stay on the host.
+typedef bool (*Pb2JsonArrayOffload)(const void* values, size_t n, uint32_t kind, std::string* text);
+void SetPb2JsonArrayOffload(Pb2JsonArrayOffload fn, size_t min_elems);
 typedef bool (*JsonIndexOffload)(const char* data, size_t n, std::vector<uint32_t>* index);
 void SetJsonIndexOffload(JsonIndexOffload fn, size_t min_bytes);
 

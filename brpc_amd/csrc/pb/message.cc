@@ -1,5 +1,6 @@
 #include "pb/message.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <sstream>
@@ -429,6 +430,44 @@ size_t Message::ByteSizeLong() const {
     return total;
 }
 
+const void* Reflection::RepeatedScalarData(const Message& m, const FieldDescriptor* f, size_t* n, size_t* eb) {
+    *n = 0;
+    *eb = 0;
+    if (!f->is_repeated() || f->cpp_type() == CppType::STRING || f->cpp_type() == CppType::MESSAGE) return nullptr;
+    RawVec rv = raw_repeated(m, f);
+    *n = rv.n;
+    *eb = elem_bytes(f->type);
+    return rv.data;
+}
+
+static thread_local PackedRunSink* tls_run_sink = nullptr;
+
+PackedRunSink* SetThreadPackedRunSink(PackedRunSink* sink) {
+    PackedRunSink* prev = tls_run_sink;
+    tls_run_sink = sink;
+    return prev;
+}
+
+bool IsVarintFieldType(FieldType t) {
+    switch (t) {
+    case FieldType::INT32:
+    case FieldType::ENUM:
+    case FieldType::SINT32:
+    case FieldType::UINT32:
+    case FieldType::INT64:
+    case FieldType::SINT64:
+    case FieldType::UINT64:
+    case FieldType::BOOL: return true;
+    default: return false;
+    }
+}
+
+void EncodePackedRunOnHost(const PackedRun& run) {
+    uint8_t* o = run.dst;
+    const char* v = static_cast<const char*>(run.values);
+    for (size_t i = 0; i < run.n; ++i) o = write_scalar(o, run.type, v + i * run.elem_bytes);
+}
+
 uint8_t* Message::SerializeWithCachedSizesToArray(uint8_t* o) const {
     const Descriptor* d = GetDescriptor();
     for (const FieldDescriptor& fd : d->fields) {
@@ -458,7 +497,29 @@ uint8_t* Message::SerializeWithCachedSizesToArray(uint8_t* o) const {
                 RawVec rv = raw_repeated(*this, f);
                 if (rv.n == 0) break;
                 const size_t eb = elem_bytes(f->type);
-                if (f->packed) {
+                PackedRunSink* sink = tls_run_sink;
+                if (f->packed && sink && rv.n >= sink->min_elems() && IsVarintFieldType(f->type)) {
+                    PackedRun run;
+                    run.values = rv.data;
+                    run.n = rv.n;
+                    run.elem_bytes = eb;
+                    run.type = f->type;
+                    run.chunk_bytes.reserve((rv.n + kPackedRunChunkElems - 1) / kPackedRunChunkElems);
+                    size_t data = 0;
+                    for (size_t c = 0; c < rv.n; c += kPackedRunChunkElems) {
+                        const size_t e = std::min(rv.n, c + kPackedRunChunkElems);
+                        size_t cb = 0;
+                        for (size_t i = c; i < e; ++i) cb += scalar_size(f->type, rv.data + i * eb);
+                        run.chunk_bytes.push_back((uint32_t)cb);
+                        data += cb;
+                    }
+                    o = write_tag(o, f->number, WIRETYPE_LENGTH_DELIMITED);
+                    o = write_varint(o, data);
+                    run.dst = o;
+                    run.bytes = data;
+                    o += data;
+                    sink->Take(std::move(run));
+                } else if (f->packed) {
                     size_t data = 0;
                     for (size_t i = 0; i < rv.n; ++i) data += scalar_size(f->type, rv.data + i * eb);
                     o = write_tag(o, f->number, WIRETYPE_LENGTH_DELIMITED);

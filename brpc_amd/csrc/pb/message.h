@@ -169,6 +169,9 @@ public:
     static int GetRepeatedEnumValue(const Message& m, const FieldDescriptor* f, int i);
     static const std::string& GetRepeatedString(const Message& m, const FieldDescriptor* f, int i);
     static const Message& GetRepeatedMessage(const Message& m, const FieldDescriptor* f, int i);
+    // The element array of a repeated scalar field (its std::vector's data;
+    // *elem_bytes 1/4/8) and its size; nullptr for strings and messages.
+    static const void* RepeatedScalarData(const Message& m, const FieldDescriptor* f, size_t* n, size_t* elem_bytes);
 
     static void AddInt32(Message* m, const FieldDescriptor* f, int32_t v);
     static void AddInt64(Message* m, const FieldDescriptor* f, int64_t v);
@@ -184,6 +187,37 @@ public:
 
 // Free helpers used by generated code.
 void ClearOneofSiblings(Message* m, const FieldDescriptor* f);
+
+// Device encoding of large packed varint runs (the body-encode
+// half of the batched device codec). While a sink is installed on the
+// calling thread, SerializeWithCachedSizesToArray writes the tag and the
+// length of every packed varint-typed field with >= min_elems() elements,
+// skips its payload and hands the run to the sink, which must fill
+// [dst, dst + bytes) before the output is used (gpu/snappy_offload.cc does
+// it in the codec batch, ahead of the compress kernel reading the body).
+// Element layout is the field's vector: 1 (bool), 4 (32-bit) or 8 bytes.
+constexpr size_t kPackedRunChunkElems = 2048;  // = gpu kPbRunChunkElems
+struct PackedRun {
+    uint8_t* dst = nullptr;
+    const void* values = nullptr;
+    size_t n = 0;
+    size_t elem_bytes = 0;
+    FieldType type = FieldType::INT32;
+    size_t bytes = 0;
+    std::vector<uint32_t> chunk_bytes;  // output bytes of each kPackedRunChunkElems elements
+};
+class PackedRunSink {
+public:
+    virtual ~PackedRunSink() {}
+    virtual size_t min_elems() const = 0;
+    virtual void Take(PackedRun&& run) = 0;
+};
+// Installs `sink` for this thread (nullptr: none); returns the previous one.
+PackedRunSink* SetThreadPackedRunSink(PackedRunSink* sink);
+// The host encoding of a run (what the serializer would have written):
+// the fallback when the device could not encode it.
+void EncodePackedRunOnHost(const PackedRun& run);
+bool IsVarintFieldType(FieldType t);
 }  // namespace pb
 // Field-less descriptor for hand-written opaque messages (redis, memcache,
 // nshead, thrift...): such messages carry their own wire encoding.

@@ -239,6 +239,16 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
         }
     } else {
         _echo_message.assign(std::max(0, _opt.request_size), 'x');
+        // ids of every varint length (1..10 bytes, a few negative)
+        uint64_t q = 0xD1B54A32D192ED03ull;
+        _ids.resize((size_t)std::max(0, _opt.packed_ids));
+        for (int64_t& id : _ids) {
+            q ^= q << 13;
+            q ^= q >> 7;
+            q ^= q << 17;
+            id = (int64_t)(q >> (q % 57));
+            if ((q & 0xff) == 0) id = -id;
+        }
         if (_opt.attachment_size > 0) {
             _attachment.resize(_opt.attachment_size);
             uint64_t r = 0x9E3779B97F4A7C15ull;
@@ -307,6 +317,7 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     call->echo_req.set_message(_echo_message);
     if (_opt.gpu_process) call->echo_req.set_gpu_process(true);
     if (_opt.cpu_process) call->echo_req.set_cpu_process(true);
+    if (call->echo_req.ids_size() != (int)_ids.size()) *call->echo_req.mutable_ids() = _ids;
     if (_device_attachment) {
         gpu::AppendDevice(&cntl.request_attachment(), _device_attachment, _attachment.size(), _opt.gpu_device);
     } else if (!_attachment.empty()) {
@@ -316,6 +327,7 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     }
     call->nbytes = _opt.scatter ? 2 * (int64_t)(_echo_message.size() * _fanout + _attachment.size())
                                 : 2 * (int64_t)(_echo_message.size() + _attachment.size()) * _fanout;
+    call->nbytes += 2 * (int64_t)(_ids.size() * sizeof(int64_t));
     call->check = _opt.check_echo && (_opt.check_every <= 1 || seq % _opt.check_every == 0);
     example::EchoService_Stub stub(ch);
     stub.Echo(&cntl, &call->echo_req, &call->echo_res, done);
@@ -330,6 +342,9 @@ void PressSession::finish(PressCall* call) {
         if (call->echo_res.message() != _echo_message) {
             ok = false;
             cntl.SetFailed(ERESPONSE, "echoed message mismatch");
+        } else if (call->echo_res.ids() != _ids) {
+            ok = false;
+            cntl.SetFailed(ERESPONSE, "echoed ids mismatch (%d of %zu)", call->echo_res.ids_size(), _ids.size());
         } else if (!_attachment.empty()) {
             std::string got, want;
             if (_opt.scatter) {

@@ -50,6 +50,7 @@ struct PressOptions {
     // echo workload (used when proto_file is empty)
     int request_size = 32;     // bytes in EchoRequest.message
     int attachment_size = 0;   // bytes of attachment per request
+    int packed_ids = 0;        // int64 ids per request (EchoRequest.ids, a packed varint run), echoed back
     bool device_attachment = false;  // attachment lives in HBM (needs GPU)
     int gpu_device = -1;
     bool check_echo = false;   // verify the echoed payload
@@ -125,6 +126,7 @@ private:
     std::vector<std::unique_ptr<pb::Message>> _requests;
     std::string _echo_message;
     std::string _attachment;
+    std::vector<int64_t> _ids;  // EchoRequest.ids of every call
     Buf _attachment_buf;                 // _attachment as one shared block
     void* _device_attachment = nullptr;  // HBM copy of _attachment when device_attachment
 

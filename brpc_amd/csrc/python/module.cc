@@ -151,6 +151,7 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "num_channels") o.num_channels = v.cast<int>();
         else if (k == "request_size") o.request_size = v.cast<int>();
         else if (k == "attachment_size") o.attachment_size = v.cast<int>();
+        else if (k == "packed_ids") o.packed_ids = v.cast<int>();
         else if (k == "device_attachment") o.device_attachment = v.cast<bool>();
         else if (k == "gpu_device") o.gpu_device = v.cast<int>();
         else if (k == "check_echo") o.check_echo = v.cast<bool>();
@@ -668,6 +669,8 @@ PYBIND11_MODULE(_native, m) {
         d["indexed_parses"] = s.indexed_parses;
         d["index_fallbacks"] = s.index_fallbacks;
         d["packs"] = s.packs;
+        d["pack_runs"] = s.pack_runs;
+        d["pack_run_chunks"] = s.pack_run_chunks;
         return d;
     });
     g.def("codec_batch_stats", [] {
@@ -675,8 +678,21 @@ PYBIND11_MODULE(_native, m) {
         py::dict d;
         d["requests"] = s.requests;
         d["launches"] = s.launches;
+        d["run_chunks"] = s.run_chunks;
         return d;
     });
+    // numeric run (vector layout bytes) -> varints / JSON numbers on the device (tests)
+    g.def("pb_run_encode", [](py::bytes values, size_t n, uint32_t kind, uint32_t format, int dev) {
+        std::string v = values;
+        std::string out;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::EncodeRunOnDevice(v.data(), n, kind, format, &out, dev);
+        }
+        if (rc != 0) throw std::runtime_error("pb_run_encode failed");
+        return py::bytes(out);
+    }, py::arg("values"), py::arg("n"), py::arg("kind"), py::arg("format") = 0, py::arg("device") = 0);
     g.def("enable_json_index", [](int dev, size_t min_bytes) {
         std::string err;
         if (gpu::EnableGpuJsonIndex(dev, min_bytes, &err) != 0) throw std::runtime_error(err);
@@ -688,6 +704,9 @@ PYBIND11_MODULE(_native, m) {
         d["indexed_bodies"] = s.indexed_bodies;
         d["indexed_bytes"] = s.indexed_bytes;
         d["failures"] = s.failures;
+        d["pb2json_arrays"] = s.pb2json_arrays;
+        d["pb2json_elems"] = s.pb2json_elems;
+        d["pb2json_failures"] = s.pb2json_failures;
         return d;
     });
     // host bytes -> structural positions through the device (tests)

@@ -182,6 +182,7 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
         }
     }
     response->set_message(request->message());
+    if (request->ids_size()) *response->mutable_ids() = request->ids();
     response->set_device(-1);
     if (request->gpu_process()) {
         if (_gpu_device < 0) {

@@ -221,6 +221,62 @@ TEST(Json2pb, large_document_round_trip) {
     EXPECT_EQ(back.SerializeAsString(), r.SerializeAsString());
 }
 
+// pb2json number-array offload (the device prints large repeated integer
+// fields, gpu/json_offload.cc): a host stand-in with the same contract
+// gives output identical to the DOM path; pretty output, enums printed as
+// names and short fields stay on the DOM path.
+namespace {
+int g_fake_array_calls = 0;
+bool fake_array_offload(const void* values, size_t n, uint32_t kind, std::string* text) {
+    ++g_fake_array_calls;
+    text->clear();
+    for (size_t i = 0; i < n; ++i) {
+        if (i) text->push_back(',');
+        if (kind == 0) text->append(std::to_string(static_cast<const int32_t*>(values)[i]));
+        else if (kind == 3) text->append(std::to_string(static_cast<const int64_t*>(values)[i]));
+        else return false;
+    }
+    return true;
+}
+}  // namespace
+
+TEST(Json2pb, pb2json_array_offload_matches_dom_output) {
+    test::Rich r;
+    r.set_must("m");
+    for (int i = 0; i < 5000; ++i) r.add_nums(i * 977 - 2000000);
+    example::EchoResponse e;
+    e.set_message("x");
+    for (int i = 0; i < 5000; ++i) e.add_ids(((int64_t)i << 40) * ((i & 1) ? -1 : 1));
+    std::string want_r, want_e, got_r, got_e, pretty_want, pretty_got, err;
+    json2pb::Pb2JsonOptions opt;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &want_r, opt, &err));
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(e, &want_e, opt, &err));
+    json2pb::Pb2JsonOptions popt;
+    popt.pretty_json = true;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &pretty_want, popt, &err));
+    json2pb::SetPb2JsonArrayOffload(fake_array_offload, 4096);
+    g_fake_array_calls = 0;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &got_r, opt, &err));
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(e, &got_e, opt, &err));
+    EXPECT_EQ(g_fake_array_calls, 2);
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(r, &pretty_got, popt, &err));
+    EXPECT_EQ(g_fake_array_calls, 2);  // pretty output stays on the DOM path
+    test::Rich small;
+    small.set_must("m");
+    for (int i = 0; i < 100; ++i) small.add_nums(i);
+    std::string s1;
+    ASSERT_TRUE(json2pb::ProtoMessageToJson(small, &s1, opt, &err));
+    EXPECT_EQ(g_fake_array_calls, 2);  // below min_elems
+    json2pb::SetPb2JsonArrayOffload(nullptr, 0);
+    EXPECT_EQ(got_r, want_r);
+    EXPECT_EQ(got_e, want_e);
+    EXPECT_EQ(pretty_got, pretty_want);
+    // and the output parses back to the same message
+    test::Rich back;
+    ASSERT_TRUE(json2pb::JsonToProtoMessage(got_r, &back, json2pb::Json2PbOptions(), &err));
+    EXPECT_EQ(back.SerializeAsString(), r.SerializeAsString());
+}
+
 TEST(HttpParser, chunked_and_pipelined) {
     Buf b;
     b.append("POST /a/b?x=1&y=two HTTP/1.1\r\nHost: h\r\nTransfer-Encoding: chunked\r\nContent-Type: text/plain\r\n\r\n"

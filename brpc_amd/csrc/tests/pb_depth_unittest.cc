@@ -4,6 +4,8 @@
 // reference's brpc_protobuf_json_unittest / brpc_proto_unittest exercise
 // the same codec through google protobuf; here the codec is our own).
 #include <cstring>
+#include <memory>
+#include <vector>
 #include <string>
 
 #include "mrpc/proto/echo.pb.h"
@@ -320,4 +322,108 @@ TEST(PbDepth, generated_and_dynamic_agree) {
     EXPECT_EQ(dyn->SerializeAsString(), gw);
     EXPECT_EQ(dyn->ByteSizeLong(), gw.size());
     delete dyn;
+}
+
+// The device-pack contract: with a PackedRunSink installed the
+// serializer writes tag + length of large packed varint runs, skips their
+// payload and hands the runs over; filling them (here with the host
+// encoder the device path falls back to) gives the ordinary encoding.
+namespace {
+struct CollectRuns : public PackedRunSink {
+    size_t min = 1;
+    std::vector<PackedRun> runs;
+    size_t min_elems() const override { return min; }
+    void Take(PackedRun&& r) override { runs.push_back(std::move(r)); }
+};
+}  // namespace
+
+TEST(PbDepth, packed_run_sink_skips_and_host_fill_matches) {
+    example::EchoRequest req;
+    req.set_message("hdr");
+    const int64_t vals[] = {0, 1, 127, 128, -1, (int64_t)1 << 62, -((int64_t)1 << 40), 300};
+    for (int rep = 0; rep < 700; ++rep) {
+        for (int64_t v : vals) req.add_ids(v * (rep + 1));
+    }
+    const std::string want = req.SerializeAsString();
+    const size_t n = req.ByteSizeLong();
+    ASSERT_TRUE(n == want.size());
+    std::string got(n, '\xAA');
+    CollectRuns sink;
+    sink.min = 4096;
+    PackedRunSink* prev = SetThreadPackedRunSink(&sink);
+    uint8_t* e = req.SerializeWithCachedSizesToArray(reinterpret_cast<uint8_t*>(&got[0]));
+    SetThreadPackedRunSink(prev);
+    EXPECT_EQ((size_t)(e - reinterpret_cast<uint8_t*>(&got[0])), n);
+    ASSERT_TRUE(sink.runs.size() == 1u);
+    const PackedRun& r = sink.runs[0];
+    EXPECT_EQ(r.n, (size_t)5600);
+    EXPECT_EQ(r.elem_bytes, (size_t)8);
+    EXPECT_EQ(r.chunk_bytes.size(), (size_t)3);  // 2048 + 2048 + 1504 elements
+    size_t sum = 0;
+    for (uint32_t c : r.chunk_bytes) sum += c;
+    EXPECT_EQ(sum, r.bytes);
+    // the payload was skipped (still the fill pattern), the rest is final
+    const size_t off = (size_t)(r.dst - reinterpret_cast<uint8_t*>(&got[0]));
+    EXPECT_EQ(got.substr(0, off), want.substr(0, off));
+    EXPECT_EQ(got.substr(off, 4), std::string(4, '\xAA'));
+    EXPECT_EQ(got.substr(off + r.bytes), want.substr(off + r.bytes));
+    EncodePackedRunOnHost(r);
+    EXPECT_EQ(got, want);
+    // below the threshold nothing is handed over
+    CollectRuns high;
+    high.min = 100000;
+    prev = SetThreadPackedRunSink(&high);
+    std::string plain(n, '\0');
+    req.SerializeWithCachedSizesToArray(reinterpret_cast<uint8_t*>(&plain[0]));
+    SetThreadPackedRunSink(prev);
+    EXPECT_TRUE(high.runs.empty());
+    EXPECT_EQ(plain, want);
+}
+
+TEST(PbDepth, packed_run_sink_every_varint_type) {
+    // dynamic message with one packed field per varint type: the host fill
+    // reproduces the ordinary bytes for each (negative int32 -> 10 bytes,
+    // zigzag for sint, 0/1 for bool)
+    const char* proto = R"(
+syntax = "proto2";
+package pr;
+message All {
+  repeated int32 a = 1 [packed = true];
+  repeated uint32 b = 2 [packed = true];
+  repeated sint32 c = 3 [packed = true];
+  repeated int64 d = 4 [packed = true];
+  repeated uint64 e = 5 [packed = true];
+  repeated sint64 f = 6 [packed = true];
+  repeated bool g = 7 [packed = true];
+  repeated fixed32 h = 8 [packed = true];
+}
+)";
+    Importer imp{{}};
+    std::string err;
+    ASSERT_TRUE(imp.ImportFromString("pr.proto", proto, &err) != nullptr);
+    const Descriptor* d = imp.FindMessageTypeByName("pr.All");
+    ASSERT_TRUE(d != nullptr);
+    std::unique_ptr<Message> m(d->prototype->New());
+    for (int i = 0; i < 3000; ++i) {
+        const int64_t x = (int64_t)i * 2654435761LL * ((i & 1) ? -1 : 1);
+        Reflection::AddInt32(m.get(), d->FindFieldByName("a"), (int32_t)x);
+        Reflection::AddUInt32(m.get(), d->FindFieldByName("b"), (uint32_t)x);
+        Reflection::AddInt32(m.get(), d->FindFieldByName("c"), (int32_t)x);
+        Reflection::AddInt64(m.get(), d->FindFieldByName("d"), x << (i % 20));
+        Reflection::AddUInt64(m.get(), d->FindFieldByName("e"), (uint64_t)x << (i % 30));
+        Reflection::AddInt64(m.get(), d->FindFieldByName("f"), x);
+        Reflection::AddBool(m.get(), d->FindFieldByName("g"), (i % 3) == 0);
+        Reflection::AddUInt32(m.get(), d->FindFieldByName("h"), (uint32_t)i);
+    }
+    const std::string want = m->SerializeAsString();
+    std::string got(want.size(), '\0');
+    CollectRuns sink;
+    sink.min = 2000;
+    m->ByteSizeLong();
+    PackedRunSink* prev = SetThreadPackedRunSink(&sink);
+    m->SerializeWithCachedSizesToArray(reinterpret_cast<uint8_t*>(&got[0]));
+    SetThreadPackedRunSink(prev);
+    EXPECT_EQ(sink.runs.size(), (size_t)7);  // every varint type; fixed32 stays on the host
+    for (const PackedRun& r : sink.runs) EncodePackedRunOnHost(r);
+    EXPECT_EQ(got, want);
 }
