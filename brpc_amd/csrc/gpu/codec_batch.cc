@@ -46,6 +46,10 @@ struct CBatch {
     std::vector<size_t> comp_first, decomp_first, stream_first, piece_first, scan_row, run_first;
     PinnedArray<PbRunChunk> run_jobs;
     PinnedArray<int32_t> run_err;
+    std::vector<size_t> dec_first;
+    PinnedArray<PbRunDecodeChunk> dec_jobs;
+    PinnedArray<uint32_t> dec_counts;
+    PinnedArray<int32_t> dec_err;
     PinnedArray<SnappyPiece> piece_jobs;
     PinnedArray<int> piece_job_err;
     PinnedArray<SnappyJob> comp_jobs, decomp_jobs;
@@ -112,7 +116,7 @@ void throttle(Engine& e) {
 }
 
 Engine g_engine[kMaxDev];
-std::atomic<int64_t> g_requests{0}, g_launches{0}, g_run_chunks{0};
+std::atomic<int64_t> g_requests{0}, g_launches{0}, g_run_chunks{0}, g_dec_chunks{0};
 
 CBatch* new_batch(Engine& e) {
     if (!e.spare.empty()) {
@@ -128,7 +132,7 @@ CBatch* new_batch(Engine& e) {
 // Lay the batch's requests out in its pinned tables and issue one stream
 // sequence; false when nothing could be launched.
 bool launch(CBatch* b, int device) {
-    size_t ncomp = 0, ndecomp = 0, nscan = 0, nstreams = 0, npieces = 0, nhpieces = 0, nruns = 0;
+    size_t ncomp = 0, ndecomp = 0, nscan = 0, nstreams = 0, npieces = 0, nhpieces = 0, nruns = 0, ndec = 0;
     uint32_t comp_max = 1, decomp_max = 1, piece_limit = 0, hpiece_max = 1;
     std::vector<Segment> h2d, d2h;
     b->comp_first.clear();
@@ -137,9 +141,12 @@ bool launch(CBatch* b, int device) {
     b->piece_first.clear();
     b->scan_row.clear();
     b->run_first.clear();
+    b->dec_first.clear();
     for (CodecRequest* r : b->reqs) {
         b->run_first.push_back(nruns);
         nruns += r->runs.size();
+        b->dec_first.push_back(ndec);
+        ndec += r->dec_runs.size();
         b->comp_first.push_back(ncomp);
         b->decomp_first.push_back(ndecomp);
         b->stream_first.push_back(nstreams);
@@ -163,7 +170,8 @@ bool launch(CBatch* b, int device) {
         !b->scan_jobs.reserve(nscan) || !b->scan_fields.reserve(nscan * 2 * kCodecScanFields) ||
         !b->scan_n.reserve(nscan) || !b->stream_jobs.reserve(nstreams) || !b->stream_err.reserve(nstreams) ||
         !b->piece_err.reserve(npieces) || !b->piece_jobs.reserve(nhpieces) || !b->piece_job_err.reserve(nhpieces) ||
-        !b->run_jobs.reserve(nruns) || !b->run_err.reserve(nruns)) {
+        !b->run_jobs.reserve(nruns) || !b->run_err.reserve(nruns) || !b->dec_jobs.reserve(ndec) ||
+        !b->dec_counts.reserve(ndec) || !b->dec_err.reserve(ndec)) {
         return false;
     }
     if (npieces > b->pieces_cap) {
@@ -180,6 +188,11 @@ bool launch(CBatch* b, int device) {
         if (r->want_scan) b->scan_jobs.p[b->scan_row[i]] = r->scan;
         std::copy(r->pieces.begin(), r->pieces.end(), b->piece_jobs.p + b->piece_first[i]);
         std::copy(r->runs.begin(), r->runs.end(), b->run_jobs.p + b->run_first[i]);
+        for (size_t k = 0; k < r->dec_runs.size(); ++k) {
+            PbRunDecodeChunk c = r->dec_runs[k];
+            c.first += (uint32_t)b->dec_first[i];
+            b->dec_jobs.p[b->dec_first[i] + k] = c;
+        }
     }
     for (size_t i = 0, g = 0, first = 0; i < b->reqs.size(); ++i) {
         for (const SnappyStream& st : b->reqs[i]->streams) {
@@ -231,6 +244,8 @@ bool launch(CBatch* b, int device) {
         rc = LaunchPbScanPtrs(b->scan_jobs.p, (int64_t)nscan, kCodecScanFields, b->scan_fields.p, b->scan_n.p, s);
     }
     if (rc == 0 && !d2h.empty()) rc = LaunchBatchedCopy(d2h.data(), (int)d2h.size(), s);
+    if (rc == 0 && ndec) rc = LaunchPbRunDecode(b->dec_jobs.p, (int)ndec, b->dec_counts.p, b->dec_err.p, s);
+    g_dec_chunks.fetch_add((int64_t)ndec, std::memory_order_relaxed);
     if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
     if (prev != device) hipSetDevice(prev);
     g_launches.fetch_add(1, std::memory_order_relaxed);
@@ -303,6 +318,9 @@ int RunCodecRequest(CodecRequest* r, int device) {
         r->decomp_err.assign(mine->decomp_err.p + d0, mine->decomp_err.p + d0 + r->decomp.size());
         const size_t r0 = mine->run_first[idx];
         r->run_err.assign(mine->run_err.p + r0, mine->run_err.p + r0 + r->runs.size());
+        const size_t q0 = mine->dec_first[idx];
+        r->dec_counts.assign(mine->dec_counts.p + q0, mine->dec_counts.p + q0 + r->dec_runs.size());
+        r->dec_err.assign(mine->dec_err.p + q0, mine->dec_err.p + q0 + r->dec_runs.size());
         const size_t p0 = mine->piece_first[idx];
         r->piece_err.assign(mine->piece_job_err.p + p0, mine->piece_job_err.p + p0 + r->pieces.size());
         r->stream_err.assign(r->streams.size(), 0);
@@ -329,6 +347,7 @@ CodecBatchStats GetCodecBatchStats() {
     s.requests = g_requests.load(std::memory_order_relaxed);
     s.launches = g_launches.load(std::memory_order_relaxed);
     s.run_chunks = g_run_chunks.load(std::memory_order_relaxed);
+    s.decode_chunks = g_dec_chunks.load(std::memory_order_relaxed);
     return s;
 }
 

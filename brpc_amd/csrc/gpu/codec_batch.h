@@ -39,6 +39,9 @@ struct CodecRequest {
     PbScanJob scan{nullptr, 0};
     // copies issued after the kernels (HBM -> pinned)
     std::vector<Segment> d2h;
+    // packed varint runs decoded last (their bytes are final by then);
+    // PbRunDecodeChunk::first is relative to this request (rebased)
+    std::vector<PbRunDecodeChunk> dec_runs;
 
     // results, filled before RunCodecRequest returns 0
     std::vector<uint32_t> comp_len, decomp_len;
@@ -46,6 +49,8 @@ struct CodecRequest {
     std::vector<int> stream_err;  // 0, or the split / piece decode code
     std::vector<int> piece_err;
     std::vector<int32_t> run_err;  // per chunk: 0, or 1 when the device size disagreed (nothing written)
+    std::vector<uint32_t> dec_counts;  // per decode chunk: varints ending in it
+    std::vector<int32_t> dec_err;      // per decode chunk: 0, or 1 for a malformed varint
     std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields
     int32_t scan_nfields = -1;
 };
@@ -57,7 +62,7 @@ constexpr uint32_t kCodecScanFields = 128;
 int RunCodecRequest(CodecRequest* r, int device);
 
 struct CodecBatchStats {
-    int64_t requests = 0, launches = 0, run_chunks = 0;
+    int64_t requests = 0, launches = 0, run_chunks = 0, decode_chunks = 0;
 };
 CodecBatchStats GetCodecBatchStats();
 

@@ -179,6 +179,26 @@ struct PbRunChunk {
 // err[i] is set to 0 (ok) or 1 (size mismatch) for every chunk.
 int LaunchPbRunEncode(const PbRunChunk* chunks, int n, int32_t* err, hipStream_t s);
 
+// Batched decoder of packed varint runs (the parse half of K2: large packed
+// fields of a body the device already decoded): a run is cut into chunks of
+// <= kPbRunDecodeChunkBytes; pass 1 counts the varints ending in each chunk,
+// pass 2 gives every chunk its first element index (sum of the earlier
+// chunks' counts of the same run) and writes each varint ending in it,
+// converted to the field's vector layout, at dst[index]. A varint belongs
+// to the chunk its last byte is in, so one may start up to 9 bytes into the
+// previous chunk (read from there). Codes in err: 0 ok, 1 a varint longer
+// than 10 bytes (or a 10th byte above 1).
+constexpr uint32_t kPbRunDecodeChunkBytes = 4096;
+struct PbRunDecodeChunk {
+    const uint8_t* run;  // the run's first byte (device-readable)
+    void* dst;           // the run's output array (kind's vector layout)
+    uint32_t offset;     // this chunk's first byte within the run
+    uint32_t len;        // bytes in the chunk, 1..kPbRunDecodeChunkBytes
+    uint32_t first;      // table index of the run's first chunk
+    uint32_t kind;       // PbRunKind
+};
+int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, int32_t* err, hipStream_t s);
+
 // JSON structural index (gpu/json_kernels.hip): out_pos receives, in order,
 // the byte offsets of every unescaped '"' and of every { } [ ] : , outside
 // strings; count_dev the number found (positions past max_out are dropped

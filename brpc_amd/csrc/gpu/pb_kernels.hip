@@ -269,7 +269,131 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunC
     if (t == 0) err[blockIdx.x] = 0;
 }
 
+// ------------------------------------------------------------ run decoder
+// Both passes stage the chunk (plus up to 16 bytes of the run before it)
+// into LDS with byte loads that are contiguous across lanes; lane t then
+// owns chunk bytes [16t, 16t + 16).
+constexpr int kHalo = 16;
+
+__device__ __forceinline__ void stage_chunk(const PbRunDecodeChunk& c, uint8_t* b, uint32_t halo) {
+    const uint8_t* src = c.run + c.offset - halo;
+    for (uint32_t j = threadIdx.x; j < halo + c.len; j += kRunThreads) b[kHalo - halo + j] = src[j];
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t x, uint32_t* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 0) red[wave] = x;
+    __syncthreads();
+    const uint32_t s = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return s;
+}
+
+__global__ void __launch_bounds__(kRunThreads) pb_run_count_kernel(const PbRunDecodeChunk* __restrict__ chunks,
+                                                                   uint32_t* __restrict__ counts) {
+    __shared__ uint8_t b[kHalo + kPbRunDecodeChunkBytes];
+    __shared__ uint32_t red[kRunThreads / 64];
+    const PbRunDecodeChunk c = chunks[blockIdx.x];
+    const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
+    const PbRunDecodeChunk cc = {c.run, c.dst, c.offset, len, c.first, c.kind};
+    stage_chunk(cc, b, 0);
+    __syncthreads();
+    uint32_t n = 0;
+    for (uint32_t j = threadIdx.x * 16; j < threadIdx.x * 16 + 16 && j < len; ++j) n += (b[kHalo + j] & 0x80) ? 0 : 1;
+    n = block_sum(n, red);
+    if (threadIdx.x == 0) counts[blockIdx.x] = n;
+}
+
+__device__ __forceinline__ void store_elem(uint8_t* o, uint32_t kind, uint64_t raw) {
+    switch (kind) {
+    case PB_RUN_INT32:
+    case PB_RUN_UINT32: *reinterpret_cast<uint32_t*>(o) = (uint32_t)raw; break;
+    case PB_RUN_SINT32: {
+        const uint32_t u = (uint32_t)raw;
+        *reinterpret_cast<int32_t*>(o) = (int32_t)(u >> 1) ^ -(int32_t)(u & 1);
+        break;
+    }
+    case PB_RUN_SINT64: *reinterpret_cast<int64_t*>(o) = (int64_t)(raw >> 1) ^ -(int64_t)(raw & 1); break;
+    case PB_RUN_BOOL: *o = raw ? 1 : 0; break;
+    default: *reinterpret_cast<uint64_t*>(o) = raw; break;
+    }
+}
+
+__global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunDecodeChunk* __restrict__ chunks,
+                                                                    const uint32_t* __restrict__ counts,
+                                                                    int32_t* __restrict__ err) {
+    __shared__ uint8_t b[kHalo + kPbRunDecodeChunkBytes];
+    __shared__ __attribute__((aligned(16))) uint8_t image[kPbRunDecodeChunkBytes * 8];
+    __shared__ uint32_t red[kRunThreads / 64];
+    __shared__ uint32_t wave_tot[kRunThreads / 64];
+    __shared__ int bad;
+    const PbRunDecodeChunk c = chunks[blockIdx.x];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
+    const uint32_t halo = c.offset < (uint32_t)kHalo ? c.offset : (uint32_t)kHalo;
+    const PbRunDecodeChunk cc = {c.run, c.dst, c.offset, len, c.first, c.kind};
+    if (t == 0) bad = 0;
+    stage_chunk(cc, b, halo);
+    // first element index: the earlier chunks of the run
+    uint32_t part = 0;
+    for (uint32_t k = c.first + t; k < blockIdx.x; k += kRunThreads) part += counts[k];
+    const uint32_t base = block_sum(part, red);  // (its barriers also order the staging)
+    const uint32_t eb = c.kind == PB_RUN_BOOL ? 1 : (c.kind <= PB_RUN_SINT32 ? 4 : 8);
+    const uint32_t j0 = (uint32_t)t * 16;
+    uint32_t mine = 0;
+    for (uint32_t j = j0; j < j0 + 16 && j < len; ++j) mine += (b[kHalo + j] & 0x80) ? 0 : 1;
+    uint32_t incl = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    if (lane == 63) wave_tot[wave] = incl;
+    __syncthreads();
+    uint32_t rank = incl - mine;
+    for (int w = 0; w < wave; ++w) rank += wave_tot[w];
+    const uint32_t total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+    const int lim = -(int)halo;
+    for (uint32_t j = j0; j < j0 + 16 && j < len; ++j) {
+        const uint8_t last = b[kHalo + j];
+        if (last & 0x80) continue;
+        int s = (int)j;
+        while (s > lim && (b[kHalo + s - 1] & 0x80) && (int)j - s < 9) --s;
+        const bool too_long = (int)j - s == 9 && ((s > lim && (b[kHalo + s - 1] & 0x80)) || last > 1);
+        if (too_long) bad = 1;
+        uint64_t v = 0;
+        for (int k = s; k <= (int)j; ++k) v |= (uint64_t)(b[kHalo + k] & 0x7f) << (7 * (k - s));
+        store_elem(image + (size_t)rank * eb, c.kind, v);
+        ++rank;
+    }
+    __syncthreads();
+    if (bad) {
+        if (t == 0) err[blockIdx.x] = 1;
+        return;
+    }
+    uint8_t* dst = static_cast<uint8_t*>(c.dst) + (size_t)base * eb;
+    const uint32_t nbytes = total * eb;
+    if (eb >= 4) {
+        for (uint32_t w = t; w < nbytes / 4; w += kRunThreads) {
+            reinterpret_cast<uint32_t*>(dst)[w] = reinterpret_cast<const uint32_t*>(image)[w];
+        }
+    } else {
+        for (uint32_t w = t; w < nbytes; w += kRunThreads) dst[w] = image[w];
+    }
+    if (t == 0) err[blockIdx.x] = 0;
+}
+
 }  // namespace
+
+int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, int32_t* err, hipStream_t s) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, counts);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(pb_run_decode_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, counts, err);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int LaunchPbRunEncode(const PbRunChunk* chunks, int n, int32_t* err, hipStream_t s) {
     if (n <= 0) return 0;

@@ -62,6 +62,9 @@ DEFINE_int32(gpu_pb_pack_min_elems, 4096,
              "packed varint fields with at least this many elements are encoded on the device (pb_run_encode_kernel) "
              "when their message goes through the GPU snappy codec, in the same batch as the compress kernel; 0: "
              "never");
+DEFINE_int32(gpu_pb_unpack_min_bytes, 16384,
+             "packed varint fields of at least this many bytes in a body the GPU codec decoded are decoded on the "
+             "device too (pb_run_count/decode kernels, one more codec batch per message); 0: never");
 DEFINE_int32(gpu_snappy_block_kb, 4,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
              "waves (lower latency) at some cost in ratio; <= 64");
@@ -86,6 +89,16 @@ struct PinnedBuf {
     explicit PinnedBuf(size_t bytes) : p(static_cast<char*>(PinnedAlloc(bytes))), n(bytes) {}
     ~PinnedBuf() {
         if (p) PinnedFree(p, n);
+    }
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(PinnedBuf&& o) noexcept {
+        if (this != &o) {
+            if (p) PinnedFree(p, n);
+            p = o.p;
+            n = o.n;
+            o.p = nullptr;
+        }
+        return *this;
     }
     // hand ownership to *b as one block
     void give_to(Buf* b) {
@@ -207,6 +220,76 @@ bool stage_runs(const RunCollector& col, PinnedBuf* stage, std::vector<PbRunChun
     }
     return true;
 }
+
+std::atomic<int64_t> g_unpack_runs{0}, g_unpack_fallbacks{0};
+
+// Decodes packed runs whose bytes are device-readable (pinned) into one
+// pinned array per call: chunks of every run in one codec request.
+// Returns false when nothing could be decoded on the device.
+bool decode_runs(std::vector<pb::PackedRunIn>* runs, PinnedBuf* out, int device) {
+    size_t cap = 0;
+    for (const pb::PackedRunIn& r : *runs) cap += ((r.len * r.elem_bytes) + 15) & ~(size_t)15;
+    *out = PinnedBuf(cap ? cap : 1);
+    if (!out->p) return false;
+    CodecRequest req;
+    std::vector<size_t> first_chunk;
+    size_t off = 0;
+    for (pb::PackedRunIn& r : *runs) {
+        first_chunk.push_back(req.dec_runs.size());
+        // a run must end on a varint's last byte (else it is truncated: the
+        // host parser reports it)
+        if (r.len == 0 || (r.p[r.len - 1] & 0x80) || r.len > 0xFFFFFFFFull) continue;
+        const uint32_t first = (uint32_t)req.dec_runs.size();
+        for (size_t o = 0; o < r.len; o += kPbRunDecodeChunkBytes) {
+            PbRunDecodeChunk c;
+            c.run = r.p;
+            c.dst = out->p + off;
+            c.offset = (uint32_t)o;
+            c.len = (uint32_t)std::min<size_t>(kPbRunDecodeChunkBytes, r.len - o);
+            c.first = first;
+            c.kind = run_kind(r.type);
+            req.dec_runs.push_back(c);
+        }
+        r.values = out->p + off;  // provisional: cleared below on a device error
+        off += ((r.len * r.elem_bytes) + 15) & ~(size_t)15;
+    }
+    first_chunk.push_back(req.dec_runs.size());
+    if (req.dec_runs.empty()) return false;
+    if (RunCodecRequest(&req, device) != 0) {
+        for (pb::PackedRunIn& r : *runs) r.values = nullptr;
+        return false;
+    }
+    for (size_t i = 0; i < runs->size(); ++i) {
+        pb::PackedRunIn& r = (*runs)[i];
+        if (!r.values) continue;
+        size_t count = 0;
+        bool ok = true;
+        for (size_t k = first_chunk[i]; k < first_chunk[i + 1]; ++k) {
+            count += req.dec_counts[k];
+            ok = ok && req.dec_err[k] == 0;
+        }
+        if (!ok) {
+            r.values = nullptr;  // malformed: the host parser reports it
+            continue;
+        }
+        r.count = count;
+    }
+    return true;
+}
+
+struct DeviceRunDecoder : public pb::PackedRunDecoder {
+    PinnedBuf out{1};
+    size_t min_bytes() const override { return (size_t)std::max(1, FLAGS_gpu_pb_unpack_min_bytes); }
+    void Decode(std::vector<pb::PackedRunIn>* runs) override {
+        if (g_device < 0 || !decode_runs(runs, &out, g_device)) {
+            g_unpack_fallbacks.fetch_add(1, std::memory_order_relaxed);
+            return;
+        }
+        for (const pb::PackedRunIn& r : *runs) {
+            if (r.values) g_unpack_runs.fetch_add(1, std::memory_order_relaxed);
+        }
+    }
+};
 
 bool gpu_compress(const Buf& in, Buf* out, const std::vector<PbRunChunk>* runs = nullptr) {
     const int dev = g_device;
@@ -478,9 +561,11 @@ int parse_offload(const Buf& in, CompressType type, pb::Message* msg) {
     bool ok;
     msg->Clear();
     const bool contiguous = raw.backing_block_num() <= 1;
+    DeviceRunDecoder decoder;
     if (index.nfields >= 0 && contiguous &&
         msg->MergeFromFieldTable(raw.empty() ? nullptr : reinterpret_cast<const uint8_t*>(raw.block_data(0)),
-                                 raw.size(), index.fields.data(), index.nfields)) {
+                                 raw.size(), index.fields.data(), index.nfields,
+                                 FLAGS_gpu_pb_unpack_min_bytes > 0 ? &decoder : nullptr)) {
         ok = msg->IsInitialized();
         g_indexed_parses.fetch_add(1, std::memory_order_relaxed);
     } else {
@@ -662,6 +747,28 @@ int EncodeRunOnDevice(const void* values, size_t n, uint32_t kind, uint32_t form
     return 0;
 }
 
+int DecodeRunOnDevice(const void* bytes, size_t len, uint32_t kind, std::string* out, int device) {
+    out->clear();
+    if (kind > PB_RUN_BOOL || device < 0 || Init(device) != 0) return -1;
+    if (len == 0) return 0;
+    PinnedBuf in(len);
+    if (!in.p) return -1;
+    memcpy(in.p, bytes, len);
+    std::vector<pb::PackedRunIn> runs(1);
+    runs[0].p = reinterpret_cast<const uint8_t*>(in.p);
+    runs[0].len = len;
+    runs[0].elem_bytes = run_elem_bytes(kind);
+    // run_kind() maps field types; here the kind is given directly
+    static const pb::FieldType kTypes[] = {pb::FieldType::INT32,  pb::FieldType::UINT32, pb::FieldType::SINT32,
+                                           pb::FieldType::INT64,  pb::FieldType::UINT64, pb::FieldType::SINT64,
+                                           pb::FieldType::BOOL};
+    runs[0].type = kTypes[kind];
+    PinnedBuf dec(1);
+    if (!decode_runs(&runs, &dec, device) || !runs[0].values) return -1;
+    out->assign(static_cast<const char*>(runs[0].values), runs[0].count * runs[0].elem_bytes);
+    return 0;
+}
+
 int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
     if (Init(device, error) != 0 || InitHbmPool(device, error) != 0) return -1;
     g_device = device;
@@ -670,6 +777,7 @@ int EnableGpuSnappy(int device, size_t min_bytes, std::string* error) {
     SetSnappyPackOffload(pack_offload, min_bytes);
     static var::PassiveStatus<int64_t> v6("gpu_snappy_packs", [] { return g_packs.load(); });
     static var::PassiveStatus<int64_t> v7("gpu_pb_pack_runs", [] { return g_pack_runs.load(); });
+    static var::PassiveStatus<int64_t> v8("gpu_pb_unpack_runs", [] { return g_unpack_runs.load(); });
     static var::PassiveStatus<int64_t> v1("gpu_snappy_compress_calls", [] { return g_comp_calls.load(); });
     static var::PassiveStatus<int64_t> v2("gpu_snappy_decompress_calls", [] { return g_decomp_calls.load(); });
     static var::PassiveStatus<int64_t> v3("gpu_snappy_fallbacks", [] { return g_fallbacks.load(); });
@@ -694,6 +802,8 @@ GpuSnappyStats GetGpuSnappyStats() {
     s.packs = g_packs.load();
     s.pack_runs = g_pack_runs.load();
     s.pack_run_chunks = g_pack_run_chunks.load();
+    s.unpack_runs = g_unpack_runs.load();
+    s.unpack_fallbacks = g_unpack_fallbacks.load();
     return s;
 }
 

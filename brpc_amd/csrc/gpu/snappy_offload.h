@@ -20,6 +20,7 @@ struct GpuSnappyStats {
     int64_t indexed_parses = 0, index_fallbacks = 0;  // decompress + pb_scan parses
     int64_t packs = 0;  // bodies serialized straight into pinned memory and compressed there
     int64_t pack_runs = 0, pack_run_chunks = 0;  // packed fields those bodies left to pb_run_encode_kernel
+    int64_t unpack_runs = 0, unpack_fallbacks = 0;  // packed fields of decoded bodies parsed on the device
 };
 GpuSnappyStats GetGpuSnappyStats();
 
@@ -27,6 +28,9 @@ GpuSnappyStats GetGpuSnappyStats();
 // PbRunFormat) via the codec batch: `values` in the field's vector layout,
 // `out` the varint payload or the JSON number list. 0 on success.
 int EncodeRunOnDevice(const void* values, size_t n, uint32_t kind, uint32_t format, std::string* out, int device);
+// A packed varint payload -> elements in the kind's vector layout
+// (pb_run_count/decode kernels). -1 when malformed or on a device error.
+int DecodeRunOnDevice(const void* bytes, size_t len, uint32_t kind, std::string* out, int device);
 
 }  // namespace gpu
 }  // namespace mrpc

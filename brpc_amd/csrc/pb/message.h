@@ -59,7 +59,8 @@ public:
     // their ranges. False for anything the table cannot express (unknown
     // fields, mismatched wire types, groups, ranges outside data): the
     // caller then parses the bytes normally.
-    bool MergeFromFieldTable(const uint8_t* data, size_t size, const uint64_t* fields, int nfields);
+    bool MergeFromFieldTable(const uint8_t* data, size_t size, const uint64_t* fields, int nfields,
+                             class PackedRunDecoder* decoder = nullptr);
     std::string DebugString() const;
     std::string ShortDebugString() const;
     std::string GetTypeName() const { return GetDescriptor()->full_name; }
@@ -211,6 +212,25 @@ public:
     virtual ~PackedRunSink() {}
     virtual size_t min_elems() const = 0;
     virtual void Take(PackedRun&& run) = 0;
+};
+// The parse half: MergeFromFieldTable hands the top-level packed varint
+// runs of >= min_bytes() bytes to a decoder in one call (one device round
+// trip per message) and appends the decoded elements; a run it did not
+// decode (values == nullptr) is parsed on the host.
+struct PackedRunIn {
+    const uint8_t* p = nullptr;  // the run's bytes (inside the decoded body)
+    size_t len = 0;
+    FieldType type = FieldType::INT32;
+    size_t elem_bytes = 0;
+    const void* values = nullptr;  // out: decoded elements in the field's vector layout
+    size_t count = 0;              // out
+};
+class PackedRunDecoder {
+public:
+    virtual ~PackedRunDecoder() {}
+    virtual size_t min_bytes() const = 0;
+    // decoded arrays stay valid until the decoder is destroyed
+    virtual void Decode(std::vector<PackedRunIn>* runs) = 0;
 };
 // Installs `sink` for this thread (nullptr: none); returns the previous one.
 PackedRunSink* SetThreadPackedRunSink(PackedRunSink* sink);

@@ -671,6 +671,8 @@ PYBIND11_MODULE(_native, m) {
         d["packs"] = s.packs;
         d["pack_runs"] = s.pack_runs;
         d["pack_run_chunks"] = s.pack_run_chunks;
+        d["unpack_runs"] = s.unpack_runs;
+        d["unpack_fallbacks"] = s.unpack_fallbacks;
         return d;
     });
     g.def("codec_batch_stats", [] {
@@ -679,6 +681,7 @@ PYBIND11_MODULE(_native, m) {
         d["requests"] = s.requests;
         d["launches"] = s.launches;
         d["run_chunks"] = s.run_chunks;
+        d["decode_chunks"] = s.decode_chunks;
         return d;
     });
     // numeric run (vector layout bytes) -> varints / JSON numbers on the device (tests)
@@ -693,6 +696,17 @@ PYBIND11_MODULE(_native, m) {
         if (rc != 0) throw std::runtime_error("pb_run_encode failed");
         return py::bytes(out);
     }, py::arg("values"), py::arg("n"), py::arg("kind"), py::arg("format") = 0, py::arg("device") = 0);
+    g.def("pb_run_decode", [](py::bytes payload, uint32_t kind, int dev) {
+        std::string v = payload;
+        std::string out;
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::DecodeRunOnDevice(v.data(), v.size(), kind, &out, dev);
+        }
+        if (rc != 0) throw std::runtime_error("pb_run_decode failed (malformed run or device error)");
+        return py::bytes(out);
+    }, py::arg("payload"), py::arg("kind"), py::arg("device") = 0);
     g.def("enable_json_index", [](int dev, size_t min_bytes) {
         std::string err;
         if (gpu::EnableGpuJsonIndex(dev, min_bytes, &err) != 0) throw std::runtime_error(err);

@@ -427,3 +427,104 @@ message All {
     for (const PackedRun& r : sink.runs) EncodePackedRunOnHost(r);
     EXPECT_EQ(got, want);
 }
+
+// The parse half: MergeFromFieldTable hands large packed runs to a decoder
+// in one call and appends what it decoded; runs it leaves (values null)
+// and small runs are parsed on the host. Host stand-in decoder here.
+namespace {
+struct HostRunDecoder : public PackedRunDecoder {
+    size_t min = 64;
+    int calls = 0;
+    size_t runs_seen = 0;
+    bool skip_second = false;
+    std::vector<std::vector<int64_t>> keep;
+    size_t min_bytes() const override { return min; }
+    void Decode(std::vector<PackedRunIn>* runs) override {
+        ++calls;
+        for (size_t k = 0; k < runs->size(); ++k) {
+            PackedRunIn& r = (*runs)[k];
+            ++runs_seen;
+            if (skip_second && k == 1) continue;
+            CodedInput in(r.p, r.len);
+            keep.emplace_back();
+            while (!in.at_limit()) {
+                uint64_t x;
+                if (!in.read_varint(&x)) return;
+                keep.back().push_back((int64_t)x);
+            }
+            r.values = keep.back().data();
+            r.count = keep.back().size();
+        }
+    }
+};
+
+// pb_scan-style table of a wire buffer (host walk)
+std::vector<uint64_t> field_table(const std::string& w) {
+    std::vector<uint64_t> t;
+    CodedInput in(w.data(), w.size());
+    const uint8_t* base = reinterpret_cast<const uint8_t*>(w.data());
+    size_t pos = 0;
+    while (pos < w.size()) {
+        CodedInput c(base + pos, w.size() - pos);
+        const uint32_t tag = c.read_tag();
+        uint64_t v = 0;
+        const size_t hdr = w.size() - pos - c.bytes_left();
+        if ((tag & 7) == 2) {
+            uint64_t len;
+            c.read_varint(&len);
+            const size_t lh = w.size() - pos - c.bytes_left();
+            v = ((uint64_t)(pos + lh) << 32) | len;
+            pos += lh + len;
+        } else {
+            c.read_varint(&v);
+            pos += w.size() - pos - c.bytes_left();
+        }
+        (void)hdr;
+        t.push_back(tag);
+        t.push_back(v);
+    }
+    return t;
+}
+}  // namespace
+
+TEST(PbDepth, field_table_merge_with_run_decoder) {
+    example::EchoRequest req;
+    req.set_message("m");
+    for (int i = 0; i < 3000; ++i) req.add_ids((int64_t)i * 1000003 - 7);
+    const std::string w = req.SerializeAsString();
+    const std::vector<uint64_t> t = field_table(w);
+    example::EchoRequest a, b;
+    HostRunDecoder dec;
+    ASSERT_TRUE(a.MergeFromFieldTable(reinterpret_cast<const uint8_t*>(w.data()), w.size(), t.data(),
+                                      (int)t.size() / 2, &dec));
+    EXPECT_EQ(dec.calls, 1);
+    EXPECT_EQ(dec.runs_seen, (size_t)1);
+    EXPECT_EQ(a.SerializeAsString(), w);
+    // runs below min_bytes never reach the decoder
+    HostRunDecoder big;
+    big.min = 1 << 20;
+    ASSERT_TRUE(b.MergeFromFieldTable(reinterpret_cast<const uint8_t*>(w.data()), w.size(), t.data(),
+                                      (int)t.size() / 2, &big));
+    EXPECT_EQ(big.calls, 0);
+    EXPECT_EQ(b.SerializeAsString(), w);
+    // a wire with the field split in two runs: the decoder declines the
+    // second, the host parses it, order is kept
+    example::EchoRequest h1, h2;
+    for (int i = 0; i < 100; ++i) h1.add_ids(i);
+    for (int i = 0; i < 100; ++i) h2.add_ids(1000 + i);
+    const std::string w2 = h1.SerializeAsString() + h2.SerializeAsString();
+    const std::vector<uint64_t> t2 = field_table(w2);
+    example::EchoRequest c;
+    HostRunDecoder part;
+    part.min = 16;
+    part.skip_second = true;
+    ASSERT_TRUE(c.MergeFromFieldTable(reinterpret_cast<const uint8_t*>(w2.data()), w2.size(), t2.data(),
+                                      (int)t2.size() / 2, &part));
+    EXPECT_EQ(part.calls, 1);
+    EXPECT_EQ(part.runs_seen, (size_t)2);
+    ASSERT_EQ(c.ids_size(), 200);
+    for (int i = 0; i < 100; ++i) {
+        EXPECT_EQ(c.ids(i), (int64_t)i);
+        EXPECT_EQ(c.ids(100 + i), (int64_t)(1000 + i));
+    }
+}

@@ -91,6 +91,37 @@ def test_run_encode_matches_reference(native, kind, fmt, n):
         assert parsed == ([bool(v) for v in vals] if kind == "bool" else vals)
 
 
+@pytest.mark.parametrize("kind", sorted(KINDS))
+@pytest.mark.parametrize("n", [1, 100, 4095, 4096, 5000, 40000])
+def test_run_decode_matches_reference(native, kind, n):
+    """Varint payload -> vector layout on the device (pb_run_count/decode
+    kernels): varints straddling the 4 KiB chunk edges, every length."""
+    code, pk = KINDS[kind]
+    vals = _values(kind, n, seed=n * 17 + code)
+    payload = _ref(kind, vals, 0)
+    got = native.gpu.pb_run_decode(payload, code, 0)
+    want = struct.pack("<%d%s" % (n, pk), *[(1 if v else 0) if kind == "bool" else v for v in vals])
+    assert got == want
+
+
+def test_run_decode_round_trips_the_encoder(native):
+    vals = _values("sint64", 20000, seed=5)
+    raw = struct.pack("<20000q", *vals)
+    enc = native.gpu.pb_run_encode(raw, 20000, 5, 0, 0)
+    assert native.gpu.pb_run_decode(enc, 5, 0) == raw
+
+
+def test_run_decode_rejects_malformed(native):
+    with pytest.raises(RuntimeError):
+        native.gpu.pb_run_decode(b"\x01\x80", 3, 0)  # truncated: ends on a continuation byte
+    with pytest.raises(RuntimeError):
+        native.gpu.pb_run_decode(b"\x01" + b"\xff" * 10 + b"\x01", 3, 0)  # 11-byte varint
+    with pytest.raises(RuntimeError):
+        native.gpu.pb_run_decode(b"\xff" * 9 + b"\x02", 4, 0)  # 10th byte above 1
+    # 10 bytes with a final 0x01 is 2**63 and fine
+    assert native.gpu.pb_run_decode(b"\x80" * 9 + b"\x01", 4, 0) == struct.pack("<Q", 1 << 63)
+
+
 def test_run_encode_rejects_bad_kind(native):
     with pytest.raises(RuntimeError):
         native.gpu.pb_run_encode(b"\0" * 8, 1, 99, 0, 0)
@@ -123,6 +154,10 @@ def test_packed_ids_encoded_on_device_in_the_codec_batch(native, protocol):
         assert b1["pack_runs"] - b0["pack_runs"] >= bodies, (b0, b1)
         assert b1["pack_run_chunks"] - b0["pack_run_chunks"] >= bodies * 8, (b0, b1)
         assert c1["run_chunks"] - c0["run_chunks"] >= bodies * 8, (c0, c1)
+        # the receiving side decodes the ids on the device too (request on
+        # the server always; gRPC responses on the client)
+        assert b1["unpack_runs"] - b0["unpack_runs"] >= bodies, (b0, b1)
+        assert c1["decode_chunks"] - c0["decode_chunks"] > 0, (c0, c1)
         assert b1["fallbacks"] == b0["fallbacks"], (b0, b1)
     finally:
         native.gpu.disable_snappy()
