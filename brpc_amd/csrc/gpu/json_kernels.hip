@@ -386,7 +386,48 @@ __global__ void __launch_bounds__(kJThreads) json_emit_kernel(Scratch sc, uint64
     if (threadIdx.x == 0 && tile_end > max_out && tile_off < tile_end) atomicOr(err, 2);
 }
 
+// One lane per element: elements are short (<= ~21 chars), independent,
+// and their bounds come from the index, so no cooperation is needed; the
+// lanes of a wave read neighbouring elements (adjacent cache lines).
+__global__ void __launch_bounds__(256) json_int_array_kernel(const char* __restrict__ text,
+                                                             const uint32_t* __restrict__ seps, uint32_t n,
+                                                             int64_t* __restrict__ out, int32_t* __restrict__ bad) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t b = seps[i] + 1, e = seps[i + 1];
+    while (b < e && (text[b] == ' ' || text[b] == '\t' || text[b] == '\n' || text[b] == '\r')) ++b;
+    while (e > b && (text[e - 1] == ' ' || text[e - 1] == '\t' || text[e - 1] == '\n' || text[e - 1] == '\r')) --e;
+    bool neg = false;
+    if (b < e && text[b] == '-') {
+        neg = true;
+        ++b;
+    }
+    bool ok = b < e && e - b <= 20;
+    uint64_t v = 0;
+    for (uint32_t k = b; ok && k < e; ++k) {
+        const uint32_t d = (uint32_t)(unsigned char)text[k] - '0';
+        if (d > 9 || v > (0xFFFFFFFFFFFFFFFFull - d) / 10) {
+            ok = false;
+            break;
+        }
+        v = v * 10 + d;
+    }
+    if (ok) ok = neg ? v <= 0x8000000000000000ull : v <= 0x7FFFFFFFFFFFFFFFull;
+    if (!ok) {
+        *bad = 1;
+        return;
+    }
+    out[i] = neg ? (int64_t)((uint64_t)0 - v) : (int64_t)v;
+}
+
 }  // namespace
+
+int LaunchJsonIntArray(const char* text, const uint32_t* seps, uint32_t n, int64_t* out, int32_t* bad,
+                       hipStream_t s) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(json_int_array_kernel, dim3((n + 255) / 256), dim3(256), 0, s, text, seps, n, out, bad);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 size_t JsonIndexScratchBytes(uint64_t n) {
     const uint64_t tiles = (n + kJTile - 1) / kJTile;

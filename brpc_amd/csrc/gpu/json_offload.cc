@@ -26,7 +26,8 @@
 
 DEFINE_int32(gpu_pb2json_min_elems, 4096,
              "repeated integer/bool fields with at least this many elements are printed by the device in pb2json "
-             "(pb_run_encode_kernel, decimal format) while the GPU JSON path is enabled");
+             "(pb_run_encode_kernel, decimal format) and integer arrays of at least as many elements are parsed by "
+             "json_int_array_kernel in json2pb, while the GPU JSON path is enabled");
 DEFINE_bool(json_index_direct_host, true,
             "the JSON index kernel reads the pinned body and writes positions to pinned memory directly");
 
@@ -164,6 +165,51 @@ bool array_offload(const void* values, size_t n, uint32_t kind, std::string* tex
     return true;
 }
 
+std::atomic<int64_t> g_int_arrays{0}, g_int_array_fallbacks{0};
+
+struct PinnedTmp {
+    void* p = nullptr;
+    size_t n = 0;
+    explicit PinnedTmp(size_t bytes) : p(PinnedAlloc(bytes)), n(bytes) {}
+    ~PinnedTmp() {
+        if (p) PinnedFree(p, n);
+    }
+};
+
+// json2pb integer arrays (SURVEY K6 parse half): the array's text and its
+// separators go to pinned memory, json_int_array_kernel parses one element
+// per lane, one fiber-friendly wait.
+bool int_array_offload(const char* base, const uint32_t* seps, size_t nseps, std::vector<int64_t>* out) {
+    const int dev = g_device;
+    if (dev < 0 || nseps < 2) return false;
+    const uint32_t lo = seps[0], hi = seps[nseps - 1];
+    const size_t n = nseps - 1;
+    PinnedTmp text(hi - lo + 1), sep(nseps * sizeof(uint32_t)), vals(n * sizeof(int64_t) + 64);
+    if (!text.p || !sep.p || !vals.p) return false;
+    memcpy(text.p, base + lo, hi - lo + 1);
+    uint32_t* sp = static_cast<uint32_t*>(sep.p);
+    for (size_t i = 0; i < nseps; ++i) sp[i] = seps[i] - lo;
+    int32_t* bad = reinterpret_cast<int32_t*>(static_cast<char*>(vals.p) + n * sizeof(int64_t));
+    *bad = 0;
+    int prev = 0;
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+    hipStream_t s = PoolStream(dev);
+    int rc = s ? LaunchJsonIntArray(static_cast<const char*>(text.p), sp, (uint32_t)n,
+                                    static_cast<int64_t*>(vals.p), bad, s)
+               : -1;
+    const int wrc = s ? SyncStream(s) : -1;  // buffers stay until the kernel is done
+    if (prev != dev) hipSetDevice(prev);
+    if (rc != 0 || wrc != 0 || *bad != 0) {
+        g_int_array_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        return false;
+    }
+    const int64_t* v = static_cast<const int64_t*>(vals.p);
+    out->assign(v, v + n);
+    g_int_arrays.fetch_add(1, std::memory_order_relaxed);
+    return true;
+}
+
 }  // namespace
 
 int EnableGpuJsonIndex(int device, size_t min_bytes, std::string* error) {
@@ -171,6 +217,8 @@ int EnableGpuJsonIndex(int device, size_t min_bytes, std::string* error) {
     g_device = device;
     json2pb::SetJsonIndexOffload(offload, min_bytes);
     json2pb::SetPb2JsonArrayOffload(array_offload, (size_t)std::max(1, FLAGS_gpu_pb2json_min_elems));
+    json::SetIntArrayOffload(int_array_offload, (size_t)std::max(1, FLAGS_gpu_pb2json_min_elems));
+    static var::PassiveStatus<int64_t> v5("gpu_json_int_arrays", [] { return g_int_arrays.load(); });
     static var::PassiveStatus<int64_t> v4("gpu_pb2json_arrays", [] { return g_arrays.load(); });
     static var::PassiveStatus<int64_t> v1("gpu_json_indexed_bodies", [] { return g_bodies.load(); });
     static var::PassiveStatus<int64_t> v2("gpu_json_indexed_bytes", [] { return g_bytes.load(); });
@@ -181,6 +229,7 @@ int EnableGpuJsonIndex(int device, size_t min_bytes, std::string* error) {
 void DisableGpuJsonIndex() {
     json2pb::SetJsonIndexOffload(nullptr, (size_t)-1);
     json2pb::SetPb2JsonArrayOffload(nullptr, (size_t)-1);
+    json::SetIntArrayOffload(nullptr, (size_t)-1);
 }
 
 GpuJsonStats GetGpuJsonStats() {
@@ -191,6 +240,8 @@ GpuJsonStats GetGpuJsonStats() {
     s.pb2json_arrays = g_arrays.load();
     s.pb2json_elems = g_array_elems.load();
     s.pb2json_failures = g_array_failures.load();
+    s.int_arrays = g_int_arrays.load();
+    s.int_array_fallbacks = g_int_array_fallbacks.load();
     return s;
 }
 

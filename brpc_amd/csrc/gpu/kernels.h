@@ -203,6 +203,14 @@ int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, i
 // the byte offsets of every unescaped '"' and of every { } [ ] : , outside
 // strings; count_dev the number found (positions past max_out are dropped
 // and err |= 2); err |= 1 when a string is left open at the end. n < 4 GiB.
+// JSON integer arrays (K6 parse half): element i of an array is the text
+// between separators seps[i] and seps[i+1] (the '[' / ',' / ']' positions of
+// the structural index); one lane per element trims whitespace and parses
+// -?[0-9]+ into out[i] as int64. Any element that is not such an integer
+// (a float, a literal, out of int64 range) sets *bad = 1: the host then
+// parses the array itself. *bad must be 0 before the launch.
+int LaunchJsonIntArray(const char* text, const uint32_t* seps, uint32_t n, int64_t* out, int32_t* bad,
+                       hipStream_t s);
 // scratch must hold JsonIndexScratchBytes(n).
 size_t JsonIndexScratchBytes(uint64_t n);
 int LaunchJsonIndex(const uint8_t* in, uint64_t n, uint32_t* out_pos, uint64_t max_out, uint64_t* count_dev,

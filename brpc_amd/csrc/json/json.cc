@@ -1,5 +1,7 @@
 #include "json/json.h"
 
+#include <atomic>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -175,6 +177,18 @@ void Value::write(std::string* out, bool pretty, int indent) const {
     case STRING: EscapeString(_s, out); break;
     case RAW: *out += _s; break;
     case ARRAY:
+        if (!_ints.empty()) {
+            out->push_back('[');
+            for (size_t i = 0; i < _ints.size(); ++i) {
+                if (i) out->push_back(',');
+                nl(indent + 1);
+                snprintf(buf, sizeof(buf), "%lld", (long long)_ints[i]);
+                *out += buf;
+            }
+            nl(indent);
+            out->push_back(']');
+            break;
+        }
         out->push_back('[');
         for (size_t i = 0; i < _arr.size(); ++i) {
             if (i) out->push_back(',');
@@ -204,6 +218,16 @@ std::string Value::ToString(bool pretty) const {
     std::string s;
     write(&s, pretty, 0);
     return s;
+}
+
+namespace {
+std::atomic<IntArrayOffload> g_int_array_offload{nullptr};
+std::atomic<size_t> g_int_array_min{(size_t)-1};
+}  // namespace
+
+void SetIntArrayOffload(IntArrayOffload fn, size_t min_elems) {
+    g_int_array_min.store(fn ? (min_elems ? min_elems : 1) : (size_t)-1, std::memory_order_relaxed);
+    g_int_array_offload.store(fn, std::memory_order_release);
 }
 
 namespace {
@@ -407,7 +431,29 @@ private:
         }
         return true;
     }
+    // The index shows an array of >= the offload's minimum plain elements
+    // (only ',' between the brackets): one bulk parse instead of a Value
+    // per element; false leaves the array to the element-wise path.
+    bool bulk_int_array(Value* v) {
+        IntArrayOffload fn = g_int_array_offload.load(std::memory_order_acquire);
+        if (!fn || !_idx) return false;
+        const size_t at = (size_t)(_p - _begin);
+        while (_k < _nidx && _idx[_k] < at) ++_k;
+        if (_k >= _nidx || _idx[_k] != at) return false;
+        size_t j = _k + 1;
+        const size_t len = (size_t)(_end - _begin);
+        while (j < _nidx && _idx[j] < len && _begin[_idx[j]] == ',') ++j;
+        if (j >= _nidx || _idx[j] >= len || _begin[_idx[j]] != ']') return false;
+        if (j - _k < g_int_array_min.load(std::memory_order_relaxed)) return false;
+        std::vector<int64_t> ints;
+        if (!fn(_begin, _idx + _k, j - _k + 1, &ints) || ints.size() != j - _k) return false;
+        *v = Value::PackedInts(std::move(ints));
+        _p = _begin + _idx[j] + 1;
+        _k = j + 1;
+        return true;
+    }
     bool array(Value* v, int depth) {
+        if (bulk_int_array(v)) return true;
         ++_p;
         *v = Value::Array();
         skip();

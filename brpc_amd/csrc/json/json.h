@@ -47,15 +47,32 @@ public:
     std::string& mutable_string() { return _s; }
     bool uint_overflows_int() const { return _type == UINT && _u > (uint64_t)INT64_MAX; }
 
-    // arrays
-    const std::vector<Value>& array() const { return _arr; }
-    std::vector<Value>& mutable_array() { _type = ARRAY; return _arr; }
+    // arrays. An array of integers parsed in bulk (the device parser of
+    // SetIntArrayOffload) keeps them packed; array() materializes Values on
+    // first use, packed_ints() lets json2pb take them without that.
+    static Value PackedInts(std::vector<int64_t> v) {
+        Value a;
+        a._type = ARRAY;
+        a._ints = std::move(v);
+        return a;
+    }
+    const std::vector<int64_t>* packed_ints() const { return _ints.empty() ? nullptr : &_ints; }
+    const std::vector<Value>& array() const {
+        materialize();
+        return _arr;
+    }
+    std::vector<Value>& mutable_array() {
+        materialize();
+        _type = ARRAY;
+        return _arr;
+    }
     Value& push_back(Value v) {
+        materialize();
         _type = ARRAY;
         _arr.push_back(std::move(v));
         return _arr.back();
     }
-    size_t size() const { return _type == ARRAY ? _arr.size() : _obj.size(); }
+    size_t size() const { return _type == ARRAY ? (_ints.empty() ? _arr.size() : _ints.size()) : _obj.size(); }
 
     // objects (insertion ordered)
     const std::vector<std::pair<std::string, Value>>& members() const { return _obj; }
@@ -68,15 +85,31 @@ public:
 
 private:
     void write(std::string* out, bool pretty, int indent) const;
+    void materialize() const {
+        if (_ints.empty()) return;
+        _arr.reserve(_ints.size());
+        for (int64_t x : _ints) _arr.emplace_back(x);
+        _ints.clear();
+    }
     Type _type;
     bool _b = false;
     int64_t _i = 0;
     uint64_t _u = 0;
     double _d = 0;
     std::string _s;
-    std::vector<Value> _arr;
+    mutable std::vector<Value> _arr;
+    mutable std::vector<int64_t> _ints;
     std::vector<std::pair<std::string, Value>> _obj;
 };
+
+// Bulk parse of a large integer array (gpu/json_offload.cc): the
+// reader, when it has a structural index, hands an array whose index shows
+// only ',' between its brackets (no strings, objects or nested arrays) and
+// at least min_elems elements to `fn` with the text base and the n + 1
+// separator offsets; fn returns false unless every element is an int64,
+// and the reader then parses the array itself.
+typedef bool (*IntArrayOffload)(const char* base, const uint32_t* seps, size_t nseps, std::vector<int64_t>* out);
+void SetIntArrayOffload(IntArrayOffload fn, size_t min_elems);
 
 // Returns false and sets *error on malformed input.
 bool Parse(const std::string& text, Value* out, std::string* error = nullptr);

@@ -389,6 +389,37 @@ private:
         return false;
     }
 
+    // Integers parsed in bulk (json::SetIntArrayOffload) appended without a
+    // Value per element; false (nothing appended) when a value is out of the
+    // field's range or the type needs the element-wise rules, which then
+    // report it exactly as before.
+    static bool bulk_ints(const std::vector<int64_t>& xs, const FieldDescriptor* f, Message* m) {
+        switch (f->cpp_type()) {
+        case CppType::INT32:
+            for (int64_t x : xs) {
+                if (x < INT32_MIN || x > INT32_MAX) return false;
+            }
+            for (int64_t x : xs) Reflection::AddInt32(m, f, (int32_t)x);
+            return true;
+        case CppType::UINT32:
+            for (int64_t x : xs) {
+                if (x < 0 || x > (int64_t)UINT32_MAX) return false;
+            }
+            for (int64_t x : xs) Reflection::AddUInt32(m, f, (uint32_t)x);
+            return true;
+        case CppType::INT64:
+            for (int64_t x : xs) Reflection::AddInt64(m, f, x);
+            return true;
+        case CppType::UINT64:
+            for (int64_t x : xs) {
+                if (x < 0) return false;
+            }
+            for (int64_t x : xs) Reflection::AddUInt64(m, f, (uint64_t)x);
+            return true;
+        default: return false;
+        }
+    }
+
     bool field(const json::Value& v, const FieldDescriptor* f, Message* m) {
         if (v.is_null()) {
             if (f->is_required()) {
@@ -401,6 +432,9 @@ private:
             if (!v.is_array()) {
                 append("Invalid value for repeated field: " + full_name(f));
                 return false;
+            }
+            if (const std::vector<int64_t>* ints = v.packed_ints()) {
+                if (bulk_ints(*ints, f, m)) return true;
             }
             for (const json::Value& e : v.array()) {
                 if (f->cpp_type() == CppType::MESSAGE) {

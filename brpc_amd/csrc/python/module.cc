@@ -721,6 +721,8 @@ PYBIND11_MODULE(_native, m) {
         d["pb2json_arrays"] = s.pb2json_arrays;
         d["pb2json_elems"] = s.pb2json_elems;
         d["pb2json_failures"] = s.pb2json_failures;
+        d["int_arrays"] = s.int_arrays;
+        d["int_array_fallbacks"] = s.int_array_fallbacks;
         return d;
     });
     // host bytes -> structural positions through the device (tests)

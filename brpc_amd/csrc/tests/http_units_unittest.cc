@@ -270,3 +270,74 @@ TEST(HpackUnit, encoder_decoder_share_dynamic_state) {
     std::vector<HPackHeader> out;
     EXPECT_FALSE(dec.Decode(std::string("\xff\xff\xff\xff\x0f", 5), &out));  // index far past the table
 }
+
+// RFC 7541 Appendix C.3 / C.4: three requests on one connection, without
+// and with Huffman coding; the second and third reference entries the
+// first ones added to the dynamic table (indices 62, 63).
+namespace {
+std::string unhex(const char* h) {
+    std::string s;
+    for (size_t i = 0; h[i] && h[i + 1]; i += 2) {
+        if (h[i] == ' ') {
+            --i;
+            continue;
+        }
+        s.push_back((char)std::stoi(std::string(h + i, 2), nullptr, 16));
+    }
+    return s;
+}
+void expect_headers(const std::vector<HPackHeader>& got, const std::vector<std::pair<std::string, std::string>>& want) {
+    ASSERT_EQ(got.size(), want.size());
+    for (size_t i = 0; i < want.size(); ++i) {
+        EXPECT_EQ(got[i].name, want[i].first);
+        EXPECT_EQ(got[i].value, want[i].second);
+    }
+}
+void run_rfc_requests(const char* r1, const char* r2, const char* r3) {
+    HPackDecoder dec;
+    std::vector<HPackHeader> out;
+    ASSERT_TRUE(dec.Decode(unhex(r1), &out));
+    expect_headers(out, {{":method", "GET"}, {":scheme", "http"}, {":path", "/"}, {":authority", "www.example.com"}});
+    out.clear();
+    ASSERT_TRUE(dec.Decode(unhex(r2), &out));
+    expect_headers(out, {{":method", "GET"}, {":scheme", "http"}, {":path", "/"}, {":authority", "www.example.com"},
+                         {"cache-control", "no-cache"}});
+    out.clear();
+    ASSERT_TRUE(dec.Decode(unhex(r3), &out));
+    expect_headers(out, {{":method", "GET"}, {":scheme", "https"}, {":path", "/index.html"},
+                         {":authority", "www.example.com"}, {"custom-key", "custom-value"}});
+}
+}  // namespace
+
+TEST(HpackUnit, rfc7541_c3_requests_without_huffman) {
+    run_rfc_requests("828684410f7777772e6578616d706c652e636f6d", "828684be58086e6f2d6361636865",
+                     "828785bf400a637573746f6d2d6b65790c637573746f6d2d76616c7565");
+}
+
+TEST(HpackUnit, rfc7541_c4_requests_with_huffman) {
+    run_rfc_requests("828684418cf1e3c2e5f23a6ba0ab90f4ff", "828684be5886a8eb10649cbf",
+                     "828785bf408825a849e95ba97d7f8925a849e95bb8e8b4bf");
+}
+
+TEST(HpackUnit, encoder_output_decodes_in_rfc_order) {
+    // our encoder on the C.3 header lists: whatever it chooses to index,
+    // a fresh decoder reproduces the lists in order across the three blocks
+    HPackEncoder enc;
+    HPackDecoder dec;
+    const std::vector<std::vector<std::pair<std::string, std::string>>> reqs = {
+        {{":method", "GET"}, {":scheme", "http"}, {":path", "/"}, {":authority", "www.example.com"}},
+        {{":method", "GET"}, {":scheme", "http"}, {":path", "/"}, {":authority", "www.example.com"},
+         {"cache-control", "no-cache"}},
+        {{":method", "GET"}, {":scheme", "https"}, {":path", "/index.html"}, {":authority", "www.example.com"},
+         {"custom-key", "custom-value"}}};
+    size_t prev = 0;
+    for (size_t r = 0; r < reqs.size(); ++r) {
+        Buf block;
+        for (const auto& h : reqs[r]) enc.Encode(&block, {h.first, h.second});
+        std::vector<HPackHeader> out;
+        ASSERT_TRUE(dec.Decode(block.to_string(), &out));
+        expect_headers(out, reqs[r]);
+        if (r == 1) EXPECT_LT(block.size(), prev);  // the authority is a table reference now
+        prev = block.size();
+    }
+}

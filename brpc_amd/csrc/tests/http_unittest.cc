@@ -4,6 +4,8 @@
 #include <unistd.h>
 
 #include <cmath>
+#include <cstring>
+#include <cerrno>
 #include <thread>
 
 #include "base/flags.h"
@@ -13,6 +15,7 @@
 #include "http/http_header.h"
 #include "http/hpack.h"
 #include "http/http_message.h"
+#include "json/json.h"
 #include "json/json2pb.h"
 #include "mrpc/proto/echo.pb.h"
 #include "mrpc/proto/test_services.pb.h"
@@ -275,6 +278,96 @@ TEST(Json2pb, pb2json_array_offload_matches_dom_output) {
     test::Rich back;
     ASSERT_TRUE(json2pb::JsonToProtoMessage(got_r, &back, json2pb::Json2PbOptions(), &err));
     EXPECT_EQ(back.SerializeAsString(), r.SerializeAsString());
+}
+
+// json2pb integer arrays parsed in bulk (the device parser's contract,
+// json::SetIntArrayOffload): with a structural index, arrays of plain
+// integers go to the offload in one call and into the message without a
+// Value per element; arrays with anything else (a float, a string, an
+// out-of-range value for the field) take the element-wise path.
+namespace {
+int g_fake_int_calls = 0;
+bool fake_int_array(const char* base, const uint32_t* seps, size_t nseps, std::vector<int64_t>* out) {
+    ++g_fake_int_calls;
+    out->clear();
+    for (size_t i = 0; i + 1 < nseps; ++i) {
+        std::string e(base + seps[i] + 1, seps[i + 1] - seps[i] - 1);
+        char* end = nullptr;
+        errno = 0;
+        const long long x = strtoll(e.c_str(), &end, 10);
+        while (end && (*end == ' ' || *end == '\n')) ++end;
+        if (errno || !end || *end) return false;
+        out->push_back(x);
+    }
+    return true;
+}
+std::vector<uint32_t> host_index(const std::string& t) {
+    std::vector<uint32_t> idx;
+    bool in_str = false;
+    for (size_t i = 0; i < t.size(); ++i) {
+        const char c = t[i];
+        if (in_str) {
+            if (c == '\\') ++i;
+            else if (c == '"') { in_str = false; idx.push_back((uint32_t)i); }
+            continue;
+        }
+        if (c == '"') { in_str = true; idx.push_back((uint32_t)i); }
+        else if (strchr("{}[]:,", c)) idx.push_back((uint32_t)i);
+    }
+    return idx;
+}
+}  // namespace
+
+TEST(Json2pb, bulk_int_arrays_with_index) {
+    example::EchoRequest want;
+    want.set_message("m");
+    std::string text = "{\"message\":\"m\",\"ids\":[";
+    for (int i = 0; i < 6000; ++i) {
+        const int64_t x = ((int64_t)i * 7919) << (i % 40);
+        want.add_ids(i % 3 ? x : -x);
+        if (i) text += (i % 50 == 0) ? ", " : ",";
+        text += std::to_string(i % 3 ? x : -x);
+    }
+    text += "]}";
+    const std::vector<uint32_t> idx = host_index(text);
+    json::SetIntArrayOffload(fake_int_array, 4096);
+    g_fake_int_calls = 0;
+    json::Value v;
+    std::string err;
+    ASSERT_TRUE(json::ParseWithIndex(text.data(), text.size(), idx.data(), idx.size(), &v, &err));
+    EXPECT_EQ(g_fake_int_calls, 1);
+    const json::Value* ids = v.find("ids");
+    ASSERT_TRUE(ids != nullptr && ids->packed_ints() != nullptr);
+    EXPECT_EQ(ids->size(), (size_t)6000);
+    example::EchoRequest got;
+    ASSERT_TRUE(json2pb::JsonValueToProtoMessage(v, &got, json2pb::Json2PbOptions(), &err));
+    EXPECT_EQ(got.SerializeAsString(), want.SerializeAsString());
+    // the packed array prints like the element-wise one
+    json::Value plain;
+    ASSERT_TRUE(json::Parse(text, &plain, &err));
+    EXPECT_EQ(v.ToString(), plain.ToString());
+    EXPECT_EQ(ids->array().size(), (size_t)6000);  // materialized on demand
+    // a float inside: the offload declines, the array parses element-wise
+    std::string t2 = text;
+    t2.insert(t2.find("[") + 1, "1.5,");
+    const std::vector<uint32_t> idx2 = host_index(t2);
+    json::Value v2;
+    ASSERT_TRUE(json::ParseWithIndex(t2.data(), t2.size(), idx2.data(), idx2.size(), &v2, &err));
+    EXPECT_TRUE(v2.find("ids")->packed_ints() == nullptr);
+    EXPECT_EQ(v2.find("ids")->size(), (size_t)6001);
+    // int32 field out of range: the element-wise rules report it
+    test::Rich r;
+    std::string t3 = "{\"must\":\"x\",\"nums\":[";
+    for (int i = 0; i < 5000; ++i) t3 += std::to_string(i) + ",";
+    t3 += "4294967296]}";
+    const std::vector<uint32_t> idx3 = host_index(t3);
+    json::Value v3;
+    ASSERT_TRUE(json::ParseWithIndex(t3.data(), t3.size(), idx3.data(), idx3.size(), &v3, &err));
+    EXPECT_TRUE(v3.find("nums")->packed_ints() != nullptr);
+    std::string err3;
+    EXPECT_FALSE(json2pb::JsonValueToProtoMessage(v3, &r, json2pb::Json2PbOptions(), &err3));
+    EXPECT_TRUE(err3.find("nums") != std::string::npos);
+    json::SetIntArrayOffload(nullptr, 0);
 }
 
 TEST(HttpParser, chunked_and_pipelined) {

@@ -198,6 +198,33 @@ def test_http_json_ids_printed_on_device(native):
         assert j1["pb2json_arrays"] - j0["pb2json_arrays"] >= 200, (j0, j1)
         assert j1["pb2json_elems"] - j0["pb2json_elems"] >= 200 * 16384, (j0, j1)
         assert j1["pb2json_failures"] == j0["pb2json_failures"]
+        # and the receiving json2pb parses the id arrays on the device
+        assert j1["int_arrays"] - j0["int_arrays"] >= 200, (j0, j1)
     finally:
         native.gpu.disable_json_index()
         s.stop()
+
+
+def test_json_int_arrays_parsed_on_device(native):
+    """json2pb of an indexed body: a plain integer array (int64 extremes,
+    whitespace, negative zero) is parsed by json_int_array_kernel; an array
+    holding a float falls back to the element-wise parser, which reports
+    the bad element exactly as before."""
+    ids = [0, -1, 1, (1 << 63) - 1, -(1 << 63)] + [((i * 7919) << (i % 37)) * (-1 if i % 3 == 0 else 1)
+                                                 for i in range(6000)]
+    body = '{"message":"m","ids":[' + ", ".join(str(x) for x in ids[:10]) + "," + \
+        ",".join(str(x) for x in ids[10:]) + ", -0 ]}"
+    native.gpu.enable_json_index(0, 1024)
+    try:
+        j0 = native.gpu.json_stats()
+        out = native.json_to_pb_to_json("example.EchoRequest", body.encode())
+        j1 = native.gpu.json_stats()
+        assert j1["int_arrays"] - j0["int_arrays"] == 1, (j0, j1)
+        assert json.loads(out)["ids"] == ids + [0]
+        bad = body.replace('"ids":[', '"ids":[1.5,', 1)
+        with pytest.raises(RuntimeError):
+            native.json_to_pb_to_json("example.EchoRequest", bad.encode())
+        j2 = native.gpu.json_stats()
+        assert j2["int_array_fallbacks"] - j1["int_array_fallbacks"] == 1, (j1, j2)
+    finally:
+        native.gpu.disable_json_index()
