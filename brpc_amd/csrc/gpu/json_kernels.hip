@@ -386,6 +386,8 @@ __global__ void __launch_bounds__(kJThreads) json_emit_kernel(Scratch sc, uint64
     if (threadIdx.x == 0 && tile_end > max_out && tile_off < tile_end) atomicOr(err, 2);
 }
 
+// json2pb integer arrays (the reference converts them element by element
+// from rapidjson values, src/json2pb/json_to_pb.cpp).
 // One lane per element: elements are short (<= ~21 chars), independent,
 // and their bounds come from the index, so no cooperation is needed; the
 // lanes of a wave read neighbouring elements (adjacent cache lines).

@@ -128,6 +128,10 @@ __global__ void __launch_bounds__(256) pb_scan_ptrs_kernel(const PbScanJob* __re
 }
 
 // ------------------------------------------------------------ run encoder
+// The device half of body encode (the reference serializes every
+// body on the host: SerializeAsCompressedData, src/brpc/compress.cpp:92,
+// called from baidu_rpc_protocol.cpp's response path) and of pb2json's
+// number printing (src/json2pb/pb_to_json.cpp, K6).
 // One workgroup (4 waves) per PbRunChunk. The chunk is walked in 8 rounds
 // of 256 consecutive elements: lane t of round r takes element 256r + t
 // (a coalesced 1/4/8-byte load from the source, pinned host or HBM), the
@@ -270,6 +274,8 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunC
 }
 
 // ------------------------------------------------------------ run decoder
+// Packed fields of a decoded body (the reference's ParsePbFromIOBuf walks
+// them element by element on the host, src/brpc/protocol.cpp).
 // Both passes stage the chunk (plus up to 16 bytes of the run before it)
 // into LDS with byte loads that are contiguous across lanes; lane t then
 // owns chunk bytes [16t, 16t + 16).
