@@ -36,7 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", default="gpu_handler",
                     choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps", "grpc_cpu",
-                             "grpc_gpu"])
+                             "grpc_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu"])
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--workers", type=int, default=12)
@@ -83,6 +83,18 @@ def main():
         o.update({"request_size": 65536, "protocol": "h2:grpc", "request_compress_type": 1})
         if a.leg == "grpc_gpu":
             native.gpu.enable_snappy(dev, 16384)
+    if a.leg.startswith("ids_"):
+        # the bench's 16k packed-ids legs: device pack/unpack with snappy
+        # (baidu_std) or device pb2json/json2pb number arrays (http + json)
+        o.update({"request_size": 16, "packed_ids": 16384})
+        if a.leg.startswith("ids_baidu"):
+            o.update({"protocol": "baidu_std", "request_compress_type": 1})
+            if a.leg.endswith("gpu"):
+                native.gpu.enable_snappy(dev, 16384)
+        else:
+            o.update({"protocol": "http", "connection_type": "pooled"})
+            if a.leg.endswith("gpu"):
+                native.gpu.enable_json_index(dev, 16384)
     p = native.Press(o)
     p.run_for(0.5)
     p.reset_stats()

@@ -113,6 +113,22 @@ struct Fixture {
         opt.timeout_ms = 3000;
         ok = ch.Init(("127.0.0.1:" + std::to_string(server.listen_port())).c_str(), &opt) == 0;
     }
+    // The server-side handlers live in svc: their streams report on_closed
+    // on a consumer fiber, so close them and wait for that before svc goes.
+    ~Fixture() {
+        std::vector<StreamId> ids;
+        std::vector<std::shared_ptr<Recorder>> recs;
+        {
+            std::lock_guard<std::mutex> lk(svc.mu);
+            ids = svc.sids;
+            recs = svc.recorders;
+        }
+        for (StreamId id : ids) StreamClose(id);
+        const int64_t deadline = monotonic_us() + 3000000;
+        for (const auto& r : recs) {
+            while (!r->closed.load() && monotonic_us() < deadline) fiber::usleep(2000);
+        }
+    }
     // Opens a stream in `mode`; the client side reports into `rec`.
     // `window`: the client's write window (a writer is bounded by its own
     // max_buf_size, as in the reference's StreamOptions).
@@ -174,6 +190,9 @@ TEST(StreamingRpc, ping_pong_both_directions) {
     }
     EXPECT_EQ(f.svc.last()->write_errors.load(), 0);
     StreamClose(sid);
+    // the handler lives on this frame: on_closed runs on the stream's
+    // consumer fiber after StreamClose returns, so wait for it
+    EXPECT_TRUE(wait_until([&] { return client.closed.load(); }));
     EXPECT_TRUE(wait_until([&] { return f.svc.last()->closed.load(); }));
 }
 
@@ -208,6 +227,9 @@ TEST(StreamingRpc, writer_blocks_until_the_reader_consumes) {
     ASSERT_TRUE(wait_until([&] { return f.svc.last()->count() == (size_t)total; }));
     EXPECT_TRUE(wait_until([&] { return StreamUnconsumedBytes(sid) == 0; }));
     StreamClose(sid);
+    // the handler lives on this frame: on_closed runs on the stream's
+    // consumer fiber after StreamClose returns, so wait for it
+    EXPECT_TRUE(wait_until([&] { return client.closed.load(); }));
 }
 
 TEST(StreamingRpc, idle_timeout_fires_without_traffic) {
@@ -224,6 +246,9 @@ TEST(StreamingRpc, idle_timeout_fires_without_traffic) {
     EXPECT_TRUE(wait_until([&] { return f.svc.last()->count() == 1; }));
     EXPECT_FALSE(f.svc.last()->closed.load());
     StreamClose(sid);
+    // the handler lives on this frame: on_closed runs on the stream's
+    // consumer fiber after StreamClose returns, so wait for it
+    EXPECT_TRUE(wait_until([&] { return client.closed.load(); }));
 }
 
 TEST(StreamingRpc, server_close_reaches_the_client) {
