@@ -388,26 +388,61 @@ __global__ void __launch_bounds__(kJThreads) json_emit_kernel(Scratch sc, uint64
 
 // json2pb integer arrays (the reference converts them element by element
 // from rapidjson values, src/json2pb/json_to_pb.cpp).
-// One lane per element: elements are short (<= ~21 chars), independent,
-// and their bounds come from the index, so no cooperation is needed; the
-// lanes of a wave read neighbouring elements (adjacent cache lines).
+// One lane per element; a workgroup's 256 elements are one contiguous span
+// of text, staged into LDS with loads that are all issued before any is
+// used (the text is pinned host memory: a lane walking its element byte by
+// byte would pay a PCIe round trip per character). Spans longer than the
+// LDS window (long runs of whitespace) are read from memory directly.
+constexpr uint32_t kIntSpan = 16384;
+
+__device__ __forceinline__ bool json_ws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
 __global__ void __launch_bounds__(256) json_int_array_kernel(const char* __restrict__ text,
                                                              const uint32_t* __restrict__ seps, uint32_t n,
                                                              int64_t* __restrict__ out, int32_t* __restrict__ bad) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ char span[kIntSpan];
+    __shared__ uint32_t lo_s, hi_s;
+    const uint32_t first = blockIdx.x * blockDim.x;
+    const uint32_t i = first + threadIdx.x;
+    const uint32_t last = min(first + blockDim.x, n);  // elements [first, last)
+    uint32_t b = 0, e = 0;
+    if (i < n) {
+        b = seps[i] + 1;
+        e = seps[i + 1];
+    }
+    if (threadIdx.x == 0) lo_s = seps[first] + 1;
+    if (i + 1 == last) hi_s = e;
+    __syncthreads();
+    const uint32_t lo = lo_s, hi = hi_s;
+    const bool staged = hi - lo <= kIntSpan;
+    if (staged) {
+        constexpr int kPer = kIntSpan / 256;
+        char v[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t j = threadIdx.x + (uint32_t)k * 256;
+            v[k] = lo + j < hi ? text[lo + j] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint32_t j = threadIdx.x + (uint32_t)k * 256;
+            if (lo + j < hi) span[j] = v[k];
+        }
+    }
+    __syncthreads();
     if (i >= n) return;
-    uint32_t b = seps[i] + 1, e = seps[i + 1];
-    while (b < e && (text[b] == ' ' || text[b] == '\t' || text[b] == '\n' || text[b] == '\r')) ++b;
-    while (e > b && (text[e - 1] == ' ' || text[e - 1] == '\t' || text[e - 1] == '\n' || text[e - 1] == '\r')) --e;
+    const char* t = staged ? span - lo : text;
+    while (b < e && json_ws(t[b])) ++b;
+    while (e > b && json_ws(t[e - 1])) --e;
     bool neg = false;
-    if (b < e && text[b] == '-') {
+    if (b < e && t[b] == '-') {
         neg = true;
         ++b;
     }
     bool ok = b < e && e - b <= 20;
     uint64_t v = 0;
     for (uint32_t k = b; ok && k < e; ++k) {
-        const uint32_t d = (uint32_t)(unsigned char)text[k] - '0';
+        const uint32_t d = (uint32_t)(unsigned char)t[k] - '0';
         if (d > 9 || v > (0xFFFFFFFFFFFFFFFFull - d) / 10) {
             ok = false;
             break;

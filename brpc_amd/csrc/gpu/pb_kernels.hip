@@ -144,39 +144,38 @@ __global__ void __launch_bounds__(256) pb_scan_ptrs_kernel(const PbScanJob* __re
 constexpr int kRunThreads = 256;
 constexpr uint32_t kRunMaxElemBytes = 21;  // "-9223372036854775808" + ','
 
-__device__ __forceinline__ uint64_t run_value(const void* src, uint32_t i, uint32_t kind) {
+// Raw element bits: signed 32-bit kinds sign-extended, bools as 0/1.
+__device__ __forceinline__ uint64_t run_load(const void* src, uint32_t i, uint32_t kind) {
     switch (kind) {
-    case PB_RUN_INT32: return (uint64_t)(int64_t)static_cast<const int32_t*>(src)[i];
+    case PB_RUN_INT32:
+    case PB_RUN_SINT32: return (uint64_t)(int64_t)static_cast<const int32_t*>(src)[i];
     case PB_RUN_UINT32: return static_cast<const uint32_t*>(src)[i];
-    case PB_RUN_SINT32: {
-        const int32_t v = static_cast<const int32_t*>(src)[i];
-        return (uint32_t)(((uint32_t)v << 1) ^ (uint32_t)(v >> 31));
-    }
-    case PB_RUN_SINT64: {
-        const int64_t v = static_cast<const int64_t*>(src)[i];
-        return ((uint64_t)v << 1) ^ (uint64_t)(v >> 63);
-    }
     case PB_RUN_BOOL: return static_cast<const uint8_t*>(src)[i] ? 1 : 0;
     default: return static_cast<const uint64_t*>(src)[i];
+    }
+}
+
+// Wire value of an element (zigzag for sint kinds).
+__device__ __forceinline__ uint64_t run_value(uint64_t raw, uint32_t kind) {
+    switch (kind) {
+    case PB_RUN_SINT32: {
+        const int32_t v = (int32_t)raw;
+        return (uint32_t)(((uint32_t)v << 1) ^ (uint32_t)(v >> 31));
+    }
+    case PB_RUN_SINT64: return (raw << 1) ^ (uint64_t)((int64_t)raw >> 63);
+    default: return raw;
     }
 }
 
 // For decimal output the value is printed as its field type says: signed
 // kinds as two's complement of their width (zigzag undone: the JSON shows
 // the number, not its wire form).
-__device__ __forceinline__ bool run_negative(const void* src, uint32_t i, uint32_t kind, uint64_t* mag) {
-    int64_t s;
-    switch (kind) {
-    case PB_RUN_INT32:
-    case PB_RUN_SINT32: s = static_cast<const int32_t*>(src)[i]; break;
-    case PB_RUN_INT64:
-    case PB_RUN_SINT64: s = static_cast<const int64_t*>(src)[i]; break;
-    case PB_RUN_UINT32: *mag = static_cast<const uint32_t*>(src)[i]; return false;
-    case PB_RUN_BOOL: *mag = static_cast<const uint8_t*>(src)[i] ? 1 : 0; return false;
-    default: *mag = static_cast<const uint64_t*>(src)[i]; return false;
-    }
-    *mag = s < 0 ? (uint64_t)0 - (uint64_t)s : (uint64_t)s;
-    return s < 0;
+__device__ __forceinline__ bool run_negative(uint64_t raw, uint32_t kind, uint64_t* mag) {
+    const bool is_signed = kind == PB_RUN_INT32 || kind == PB_RUN_SINT32 || kind == PB_RUN_INT64 ||
+                           kind == PB_RUN_SINT64;
+    const bool neg = is_signed && (int64_t)raw < 0;
+    *mag = neg ? (uint64_t)0 - raw : raw;
+    return neg;
 }
 
 __device__ __forceinline__ uint32_t run_varint_len(uint64_t v) {
@@ -205,20 +204,33 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunC
     if (t == 0) round_base = 0;
     __syncthreads();
     const uint32_t count = c.count < kPbRunChunkElems ? c.count : kPbRunChunkElems;
-    for (uint32_t r0 = 0; r0 < count; r0 += kRunThreads) {
+    // every round's element is loaded before any is used: from pinned host
+    // memory each load is a PCIe round trip, so the 8 go out together
+    // instead of one per round behind the scan's barriers
+    constexpr int kRounds = kPbRunChunkElems / kRunThreads;
+    uint64_t raws[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t i = (uint32_t)r * kRunThreads + t;
+        raws[r] = i < count ? run_load(c.src, i, c.kind) : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+        const uint32_t r0 = (uint32_t)r * kRunThreads;
+        if (r0 >= count) break;
         const uint32_t i = r0 + t;
         uint32_t len = 0;
         uint64_t v = 0;
         bool neg = false;
         if (i < count) {
             if (!decimal) {
-                v = run_value(c.src, i, c.kind);
+                v = run_value(raws[r], c.kind);
                 len = run_varint_len(v);
             } else if (c.kind == PB_RUN_BOOL) {
-                run_negative(c.src, i, c.kind, &v);
+                v = raws[r];
                 len = v ? 4 : 5;
             } else {
-                neg = run_negative(c.src, i, c.kind, &v);
+                neg = run_negative(raws[r], c.kind, &v);
                 len = run_digits(v) + (neg ? 1 : 0);
             }
             if (decimal && !(c.last && i + 1 == count)) len += 1;  // ','
@@ -282,8 +294,22 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunC
 constexpr int kHalo = 16;
 
 __device__ __forceinline__ void stage_chunk(const PbRunDecodeChunk& c, uint8_t* b, uint32_t halo) {
+    // all of a lane's loads are issued before its LDS stores (a pinned
+    // source costs one PCIe round trip per dependent load)
+    constexpr int kPer = (kHalo + kPbRunDecodeChunkBytes + kRunThreads - 1) / kRunThreads;
     const uint8_t* src = c.run + c.offset - halo;
-    for (uint32_t j = threadIdx.x; j < halo + c.len; j += kRunThreads) b[kHalo - halo + j] = src[j];
+    const uint32_t n = halo + c.len;
+    uint8_t v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t j = threadIdx.x + (uint32_t)k * kRunThreads;
+        v[k] = j < n ? src[j] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t j = threadIdx.x + (uint32_t)k * kRunThreads;
+        if (j < n) b[kHalo - halo + j] = v[k];
+    }
 }
 
 __device__ __forceinline__ uint32_t block_sum(uint32_t x, uint32_t* red) {
