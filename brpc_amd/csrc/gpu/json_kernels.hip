@@ -431,18 +431,20 @@ __global__ void __launch_bounds__(256) json_int_array_kernel(const char* __restr
     }
     __syncthreads();
     if (i >= n) return;
-    const char* t = staged ? span - lo : text;
-    while (b < e && json_ws(t[b])) ++b;
-    while (e > b && json_ws(t[e - 1])) --e;
+    // positions stay absolute; an LDS pointer must never be offset below the
+    // array (a flat address below the LDS aperture is a global address)
+    auto at = [&](uint32_t k) -> char { return staged ? span[k - lo] : text[k]; };
+    while (b < e && json_ws(at(b))) ++b;
+    while (e > b && json_ws(at(e - 1))) --e;
     bool neg = false;
-    if (b < e && t[b] == '-') {
+    if (b < e && at(b) == '-') {
         neg = true;
         ++b;
     }
     bool ok = b < e && e - b <= 20;
     uint64_t v = 0;
     for (uint32_t k = b; ok && k < e; ++k) {
-        const uint32_t d = (uint32_t)(unsigned char)t[k] - '0';
+        const uint32_t d = (uint32_t)(unsigned char)at(k) - '0';
         if (d > 9 || v > (0xFFFFFFFFFFFFFFFFull - d) / 10) {
             ok = false;
             break;

@@ -193,6 +193,29 @@ __device__ __forceinline__ uint32_t run_digits(uint64_t v) {
     return d;
 }
 
+// Copies an LDS image to dst (any alignment) with 16-byte stores for the
+// aligned middle: over PCIe to pinned host memory a wave's byte stores make
+// 64-byte writes, its 16-byte stores 1 KiB ones.
+__device__ __forceinline__ void copy_out(uint8_t* dst, const uint8_t* image, uint32_t total) {
+    const uint32_t t = threadIdx.x;
+    uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
+    if (head > total) head = total;
+    if (t < head) dst[t] = image[t];
+    const uint32_t nv = (total - head) / 16;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4* body = reinterpret_cast<u32x4*>(dst + head);
+    for (uint32_t w = t; w < nv; w += kRunThreads) {
+        const uint8_t* q = image + head + 16 * w;
+        u32x4 v;
+        v.x = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+        v.y = (uint32_t)q[4] | ((uint32_t)q[5] << 8) | ((uint32_t)q[6] << 16) | ((uint32_t)q[7] << 24);
+        v.z = (uint32_t)q[8] | ((uint32_t)q[9] << 8) | ((uint32_t)q[10] << 16) | ((uint32_t)q[11] << 24);
+        v.w = (uint32_t)q[12] | ((uint32_t)q[13] << 8) | ((uint32_t)q[14] << 16) | ((uint32_t)q[15] << 24);
+        body[w] = v;
+    }
+    for (uint32_t j = head + 16 * nv + t; j < total; j += kRunThreads) dst[j] = image[j];
+}
+
 __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunChunk* __restrict__ chunks,
                                                                     int32_t* __restrict__ err) {
     __shared__ uint8_t image[kPbRunChunkElems * kRunMaxElemBytes];
@@ -281,7 +304,7 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunC
         if (t == 0) err[blockIdx.x] = 1;
         return;
     }
-    for (uint32_t j = t; j < total; j += kRunThreads) c.dst[j] = image[j];
+    copy_out(c.dst, image, total);
     if (t == 0) err[blockIdx.x] = 0;
 }
 
@@ -407,13 +430,7 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunD
     }
     uint8_t* dst = static_cast<uint8_t*>(c.dst) + (size_t)base * eb;
     const uint32_t nbytes = total * eb;
-    if (eb >= 4) {
-        for (uint32_t w = t; w < nbytes / 4; w += kRunThreads) {
-            reinterpret_cast<uint32_t*>(dst)[w] = reinterpret_cast<const uint32_t*>(image)[w];
-        }
-    } else {
-        for (uint32_t w = t; w < nbytes; w += kRunThreads) dst[w] = image[w];
-    }
+    copy_out(dst, image, nbytes);
     if (t == 0) err[blockIdx.x] = 0;
 }
 
