@@ -158,3 +158,27 @@ TEST(VarDepth, window_and_per_second_follow_the_sampler) {
     EXPECT_LE(wm.get_value(), 24);
     EXPECT_TRUE(Variable::series_exposed("depth_window").size() > 2);
 }
+
+TEST(VarDepth, latency_recorder_renders_as_prometheus_summary) {
+    LatencyRecorder lr;
+    lr.expose("depth_summary_rec");
+    for (int i = 1; i <= 1000; ++i) lr << i;
+    const std::string prom = Variable::dump_prometheus();
+    EXPECT_TRUE(prom.find("# TYPE depth_summary_rec summary\n") != std::string::npos);
+    EXPECT_TRUE(prom.find("depth_summary_rec{quantile=\"0.8\"} ") != std::string::npos);
+    EXPECT_TRUE(prom.find("depth_summary_rec{quantile=\"0.9999\"} ") != std::string::npos);
+    EXPECT_TRUE(prom.find("depth_summary_rec{quantile=\"1\"} ") != std::string::npos);
+    EXPECT_TRUE(prom.find("depth_summary_rec_count 1000\n") != std::string::npos);
+    EXPECT_TRUE(prom.find("depth_summary_rec_sum ") != std::string::npos);
+    // members of the summary are not repeated as gauges; qps stays one
+    EXPECT_TRUE(prom.find("# TYPE depth_summary_rec_latency_80 gauge") == std::string::npos);
+    EXPECT_TRUE(prom.find("# TYPE depth_summary_rec_count gauge") == std::string::npos);
+    EXPECT_TRUE(prom.find("# TYPE depth_summary_rec_qps gauge") != std::string::npos);
+    // exactly one summary header
+    const size_t a = prom.find("# TYPE depth_summary_rec summary");
+    EXPECT_EQ(prom.find("# TYPE depth_summary_rec summary", a + 1), std::string::npos);
+    // a plain variable ending in _count is still a gauge
+    Adder<int64_t> c("depth_lonely_count");
+    c << 3;
+    EXPECT_TRUE(Variable::dump_prometheus().find("depth_lonely_count 3\n") != std::string::npos);
+}

@@ -1,5 +1,9 @@
 #include "var/variable.h"
 
+#include <cstring>
+
+#include <set>
+
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -180,32 +184,87 @@ int Variable::dump_exposed(std::vector<std::pair<std::string, std::string>>* out
     return n;
 }
 
+// A LatencyRecorder exposed as P renders as one Prometheus summary P (the
+// reference's prometheus_metrics_service.cpp:103-182 grouping): quantiles
+// 0.8/0.9/0.99/0.999/0.9999 from P_latency_NN, "1" from P_max_latency,
+// "avg" from P_latency, P_sum = avg * count and P_count. Members of a
+// complete group are not repeated as gauges; P_qps stays a gauge.
+namespace {
+const char* const kPctSuffix[] = {"_latency_80", "_latency_90", "_latency_99", "_latency_999", "_latency_9999"};
+const char* const kPctQuantile[] = {"0.8", "0.9", "0.99", "0.999", "0.9999"};
+bool ends_with(const std::string& s, const char* suf, size_t* base_len) {
+    const size_t n = strlen(suf);
+    if (s.size() <= n || s.compare(s.size() - n, n, suf) != 0) return false;
+    *base_len = s.size() - n;
+    return true;
+}
+struct Summary {
+    double pct[5] = {0, 0, 0, 0, 0};
+    int have = 0;  // bit i: percentile i; bit 5: max; bit 6: avg; bit 7: count
+    double max = 0, avg = 0, count = 0;
+    bool complete() const { return have == 0xFF; }
+};
+}  // namespace
+
 std::string Variable::dump_prometheus() {
     Registry& r = reg();
     std::lock_guard<std::mutex> g(r.mu);
-    std::string out;
-    for (auto& kv : r.m) {
-        const std::string& name = kv.first;
-        // latency percentiles are emitted as a summary
-        static const char* kSuffix[] = {"_latency_50", "_latency_90", "_latency_99", "_latency_999", "_latency_9999"};
-        static const char* kQuant[] = {"0.5", "0.9", "0.99", "0.999", "0.9999"};
-        bool handled = false;
+    std::map<std::string, Summary> sums;
+    auto member = [](const std::string& name, std::string* base, int* bit) {
+        size_t bl;
         for (int i = 0; i < 5; ++i) {
-            const std::string suf = kSuffix[i];
-            if (name.size() > suf.size() && name.compare(name.size() - suf.size(), suf.size(), suf) == 0) {
-                double v;
-                if (kv.second.var->get_number(&v)) {
-                    std::string base = name.substr(0, name.size() - suf.size()) + "_latency";
-                    char line[512];
-                    snprintf(line, sizeof(line), "%s{quantile=\"%s\"} %.6g\n", base.c_str(), kQuant[i], v);
-                    out += line;
-                }
-                handled = true;
-                break;
+            if (ends_with(name, kPctSuffix[i], &bl)) {
+                *base = name.substr(0, bl);
+                *bit = i;
+                return true;
             }
         }
-        if (handled) continue;
-        std::string labeled;
+        if (ends_with(name, "_max_latency", &bl)) *bit = 5;
+        else if (ends_with(name, "_latency", &bl)) *bit = 6;
+        else if (ends_with(name, "_count", &bl)) *bit = 7;
+        else return false;
+        *base = name.substr(0, bl);
+        return true;
+    };
+    for (auto& kv : r.m) {
+        std::string base;
+        int bit;
+        double v;
+        if (!member(kv.first, &base, &bit) || !kv.second.var->get_number(&v)) continue;
+        Summary& sm = sums[base];
+        sm.have |= 1 << bit;
+        if (bit < 5) sm.pct[bit] = v;
+        else if (bit == 5) sm.max = v;
+        else if (bit == 6) sm.avg = v;
+        else sm.count = v;
+    }
+    std::string out;
+    std::set<std::string> emitted;
+    char line[512];
+    for (auto& kv : r.m) {
+        const std::string& name = kv.first;
+        std::string base;
+        int bit;
+        if (member(name, &base, &bit)) {
+            auto it = sums.find(base);
+            if (it != sums.end() && it->second.complete()) {
+                if (emitted.insert(base).second) {
+                    const Summary& sm = it->second;
+                    out += "# HELP " + base + "\n# TYPE " + base + " summary\n";
+                    for (int i = 0; i < 5; ++i) {
+                        snprintf(line, sizeof(line), "%s{quantile=\"%s\"} %.10g\n", base.c_str(), kPctQuantile[i],
+                                 sm.pct[i]);
+                        out += line;
+                    }
+                    snprintf(line, sizeof(line),
+                             "%s{quantile=\"1\"} %.10g\n%s{quantile=\"avg\"} %.10g\n%s_sum %.10g\n%s_count %.10g\n",
+                             base.c_str(), sm.max, base.c_str(), sm.avg, base.c_str(), sm.avg * sm.count,
+                             base.c_str(), sm.count);
+                    out += line;
+                }
+                continue;
+            }
+        }
         double v;
         std::ostringstream os;
         kv.second.var->describe(os, false);
@@ -217,7 +276,6 @@ std::string Variable::dump_prometheus() {
             continue;
         }
         if (!kv.second.var->get_number(&v)) continue;
-        char line[512];
         snprintf(line, sizeof(line), "# HELP %s %s\n# TYPE %s gauge\n%s %.10g\n", name.c_str(), name.c_str(),
                  name.c_str(), name.c_str(), v);
         out += line;
