@@ -339,20 +339,71 @@ bool read_number(CodedInput* in, FieldType t, uint64_t* out) {
 
 bool parse_message(Message* m, CodedInput* in);
 
+// Packed payload p[0, len) appended to a repeated scalar field in bulk:
+// fixed-width types are one memcpy, varints are counted first (one pass
+// over the terminator bits, so the vector grows once) and decoded by a
+// typed loop instead of a per-element switch. Same results and the same
+// failures as the element-wise path.
+template <typename T, typename Conv>
+bool bulk_varints(Message* m, const FieldDescriptor* f, const uint8_t* p, size_t len, Conv conv) {
+    size_t n = 0;
+    for (size_t i = 0; i < len; ++i) n += (p[i] >> 7) ^ 1;
+    auto& vec = ref<std::vector<T>>(m, f);
+    const size_t base = vec.size();
+    vec.resize(base + n);
+    T* out = vec.data() + base;
+    CodedInput in(p, len);
+    for (size_t k = 0; k < n; ++k) {
+        uint64_t v;
+        if (!in.read_varint(&v)) {
+            vec.resize(base + k);
+            return false;
+        }
+        out[k] = conv(v);
+    }
+    return in.at_limit();
+}
+
+template <typename T>
+bool bulk_fixed(Message* m, const FieldDescriptor* f, const uint8_t* p, size_t len) {
+    if (len % sizeof(T)) return false;
+    auto& vec = ref<std::vector<T>>(m, f);
+    const size_t base = vec.size();
+    vec.resize(base + len / sizeof(T));
+    memcpy(vec.data() + base, p, len);
+    return true;
+}
+
+bool parse_packed(Message* m, const FieldDescriptor* f, const uint8_t* p, size_t len) {
+    switch (f->type) {
+    case FieldType::INT32:
+    case FieldType::ENUM: return bulk_varints<int32_t>(m, f, p, len, [](uint64_t v) { return (int32_t)v; });
+    case FieldType::SINT32:
+        return bulk_varints<int32_t>(m, f, p, len, [](uint64_t v) { return unzigzag32((uint32_t)v); });
+    case FieldType::UINT32: return bulk_varints<uint32_t>(m, f, p, len, [](uint64_t v) { return (uint32_t)v; });
+    case FieldType::INT64: return bulk_varints<int64_t>(m, f, p, len, [](uint64_t v) { return (int64_t)v; });
+    case FieldType::SINT64: return bulk_varints<int64_t>(m, f, p, len, [](uint64_t v) { return unzigzag64(v); });
+    case FieldType::UINT64: return bulk_varints<uint64_t>(m, f, p, len, [](uint64_t v) { return v; });
+    case FieldType::BOOL: return bulk_varints<uint8_t>(m, f, p, len, [](uint64_t v) { return (uint8_t)(v != 0); });
+    case FieldType::FIXED32:
+    case FieldType::SFIXED32: return f->cpp_type() == CppType::UINT32 ? bulk_fixed<uint32_t>(m, f, p, len)
+                                                                      : bulk_fixed<int32_t>(m, f, p, len);
+    case FieldType::FIXED64: return bulk_fixed<uint64_t>(m, f, p, len);
+    case FieldType::SFIXED64: return bulk_fixed<int64_t>(m, f, p, len);
+    case FieldType::FLOAT: return bulk_fixed<float>(m, f, p, len);
+    case FieldType::DOUBLE: return bulk_fixed<double>(m, f, p, len);
+    default: return false;
+    }
+}
+
 bool parse_field(Message* m, const FieldDescriptor* f, uint32_t tag, CodedInput* in) {
     const WireType wt = (WireType)(tag & 7);
     const WireType expected = wire_type_of(f->type);
     if (f->is_repeated() && f->is_packable() && wt == WIRETYPE_LENGTH_DELIMITED) {
         uint64_t len;
-        const uint8_t* old;
-        if (!in->read_varint(&len) || !in->push_limit((size_t)len, &old)) return false;
-        while (!in->at_limit()) {
-            uint64_t v;
-            if (!read_number(in, f->type, &v)) return false;
-            store_number(m, f, v);
-        }
-        in->pop_limit(old);
-        return true;
+        const uint8_t* p;
+        if (!in->read_varint(&len) || !in->read_bytes((size_t)len, &p)) return false;
+        return parse_packed(m, f, p, (size_t)len);
     }
     if (wt != expected) {
         // Mismatched wire type: keep as unknown field (protobuf semantics).
@@ -835,12 +886,7 @@ bool Message::MergeFromFieldTable(const uint8_t* data, size_t size, const uint64
         if (off > size || len > size - off) return false;
         const uint8_t* p = data + off;
         if (f->is_repeated() && f->is_packable()) {
-            CodedInput in(p, len);
-            while (!in.at_limit()) {
-                uint64_t x;
-                if (!read_number(&in, f->type, &x)) return false;
-                store_number(this, f, x);
-            }
+            if (!parse_packed(this, f, p, len)) return false;
             continue;
         }
         switch (f->cpp_type()) {
