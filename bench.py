@@ -436,7 +436,7 @@ def main():
         )
         # the ids legs' CPU twins are slow (the json DOM path runs ~1.7 k
         # QPS per rank): fewer requests per step keep them around 5 s
-        per_step = {"baidu_std_snappy_ids16k": 2, "http_json_ids16k": 4}
+        per_step = {"baidu_std_snappy_ids16k": 2, "http_json_ids16k": 3}
         for name, extra, enable, disable, count in codec_legs:
             wlx = EchoWorkload(name, request_size=65536, attachment_size=0,
                                requests_per_step=max(1, a.requests_per_step_grpc // per_step.get(name, 1)))
