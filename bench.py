@@ -290,8 +290,11 @@ def main():
             # legs take: probe the rank's domains again and move the rank
             # to the one whose CPUs wake sleepers promptly
             from brpc_amd.parallel.placement import rechoose_l3_domain  # noqa: E402
+            # (the sample is the last leg by default, so a lone rank may even
+            # leave its GPU's NUMA node for a quieter domain)
             moved = rechoose_l3_domain(topo.local_rank, topo.local_world_size, topo.device,
-                                       torch.cuda.device_count() if torch.cuda.is_available() else 0)
+                                       torch.cuda.device_count() if torch.cuda.is_available() else 0,
+                                       widen_late=0 if a.latency_first else 20)
         press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
                               "connection_type": "single"})
         parallel.barrier(topo)

@@ -177,7 +177,8 @@ def _quietest(mine, domains, sample_s, native, info):
     return idx
 
 
-def choose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.5):
+def choose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.5,
+                     widen_late=0):
     """Index (for -cpu_l3_domain) of the L3 domain this rank should use, and
     a description dict for the bench JSON. -1: leave the rank unconfined."""
     domains = l3_domains(host_cpus())
@@ -212,6 +213,21 @@ def choose_l3_domain(local_rank, local_world, device, device_count=0, native=Non
     idx = mine[0]
     if len(mine) > 1 and sample_s > 0:
         idx = _quietest(mine, domains, sample_s, native, info)
+    # a lone rank whose NUMA-local domains are all disturbed (the probe saw
+    # more than widen_late late wake-ups in the best of them) may take a
+    # quieter domain on another node: for small-message latency the host's
+    # other tenants matter more than the GPU's PCIe locality
+    probe = info.get("l3_domain_probe")
+    if widen_late > 0 and local_world == 1 and probe and probe.get("late", 0) > widen_late and sample_s > 0:
+        others = [i for i in range(len(domains)) if i not in mine and 0 not in domains[i][1]]
+        if others:
+            wide = {}
+            idx2 = _quietest(others + [idx], domains, sample_s, native, wide)
+            if idx2 != idx and wide.get("l3_domain_probe", {}).get("late", 1 << 30) < probe.get("late", 0):
+                info["widened_from_probe"] = probe
+                info["l3_domain_probe"] = wide["l3_domain_probe"]
+                idx = idx2
+                mine = mine + others
     info["l3_domain_candidates"] = len(mine)
     info["l3_domain_first_cpu"] = domains[idx][0]
     info["ranks_on_gpu_numa_node"] = len(peers)
@@ -219,12 +235,12 @@ def choose_l3_domain(local_rank, local_world, device, device_count=0, native=Non
     return idx, info
 
 
-def rechoose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.5):
+def rechoose_l3_domain(local_rank, local_world, device, device_count=0, native=None, sample_s=0.5, widen_late=20):
     """Probe the rank's slice again and move the running process to its
     quietest domain (fiber::RebindL3Domain). Run right before a latency
     measurement: other tenants' load shifts over minutes. Returns the new
     placement dict ({} when nothing could be chosen)."""
-    idx, info = choose_l3_domain(local_rank, local_world, device, device_count, native, sample_s)
+    idx, info = choose_l3_domain(local_rank, local_world, device, device_count, native, sample_s, widen_late)
     if idx < 0:
         return {}
     if native is None:
