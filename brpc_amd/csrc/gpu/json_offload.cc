@@ -28,6 +28,9 @@ DEFINE_int32(gpu_pb2json_min_elems, 4096,
              "repeated integer/bool fields with at least this many elements are printed by the device in pb2json "
              "(pb_run_encode_kernel, decimal format) and integer arrays of at least as many elements are parsed by "
              "json_int_array_kernel in json2pb, while the GPU JSON path is enabled");
+DEFINE_int32(json_index_min_density, 8,
+             "structural characters per KiB (sampled in three windows) a JSON body needs before the GPU index is "
+             "used; sparser bodies (long strings) parse faster on the host; 0: always offload");
 DEFINE_bool(json_index_direct_host, true,
             "the JSON index kernel reads the pinned body and writes positions to pinned memory directly");
 
@@ -38,6 +41,7 @@ namespace {
 
 int g_device = -1;
 std::atomic<int64_t> g_bodies{0}, g_bytes{0}, g_failures{0};
+std::atomic<int64_t> g_sparse{0};
 
 struct Hbm {
     void* p = nullptr;
@@ -58,8 +62,29 @@ struct Pinned {
     }
 };
 
+// Structural characters per KiB in three 1 KiB windows (start, middle,
+// end). A body that is mostly one long string (the http_json_64KB leg)
+// has almost none: the host parser crosses it with memchr faster than a
+// device round trip returns its index, so such bodies are not offloaded.
+bool structurally_sparse(const char* data, size_t n) {
+    const int need = FLAGS_json_index_min_density;
+    if (need <= 0 || n < 3 * 1024) return false;
+    int hits = 0;
+    for (size_t w : {(size_t)0, n / 2 - 512, n - 1024}) {
+        for (size_t i = w; i < w + 1024; ++i) {
+            const char c = data[i];
+            hits += c == '"' || c == ',' || c == ':' || c == '{' || c == '[';
+        }
+    }
+    return hits < 3 * need;
+}
+
 bool offload(const char* data, size_t n, std::vector<uint32_t>* index) {
     if (g_device < 0) return false;
+    if (structurally_sparse(data, n)) {
+        g_sparse.fetch_add(1, std::memory_order_relaxed);
+        return false;
+    }
     Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
     const int64_t t0 = span ? monotonic_us() : 0;
     const int rc = JsonIndex(data, n, index, g_device);
@@ -242,6 +267,7 @@ GpuJsonStats GetGpuJsonStats() {
     s.pb2json_failures = g_array_failures.load();
     s.int_arrays = g_int_arrays.load();
     s.int_array_fallbacks = g_int_array_fallbacks.load();
+    s.sparse_skips = g_sparse.load();
     return s;
 }
 

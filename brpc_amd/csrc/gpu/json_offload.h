@@ -24,6 +24,7 @@ struct GpuJsonStats {
     int64_t indexed_bodies = 0, indexed_bytes = 0, failures = 0;
     int64_t pb2json_arrays = 0, pb2json_elems = 0, pb2json_failures = 0;  // number arrays printed on the device
     int64_t int_arrays = 0, int_array_fallbacks = 0;  // json2pb integer arrays parsed on the device
+    int64_t sparse_skips = 0;  // bodies left to the host parser by the density check
 };
 GpuJsonStats GetGpuJsonStats();
 

@@ -723,6 +723,7 @@ PYBIND11_MODULE(_native, m) {
         d["pb2json_failures"] = s.pb2json_failures;
         d["int_arrays"] = s.int_arrays;
         d["int_array_fallbacks"] = s.int_array_fallbacks;
+        d["sparse_skips"] = s.sparse_skips;
         return d;
     });
     // host bytes -> structural positions through the device (tests)

@@ -181,6 +181,7 @@ def test_json2pb_uses_device_index_for_large_bodies(dev):
     small, _ = _echo_doc(1)
     cpu_big = native.json_to_pb_to_json("example.EchoRequest", text)
     native.gpu.enable_json_index(0, 65536)
+    native.set_flag("json_index_min_density", "0")  # this one long string would be left to the host
     try:
         s0 = native.gpu.json_stats()
         assert native.json_to_pb_to_json("example.EchoRequest", text) == cpu_big
@@ -194,6 +195,32 @@ def test_json2pb_uses_device_index_for_large_bodies(dev):
         with pytest.raises(RuntimeError):
             native.json_to_pb_to_json("example.EchoRequest", text[:100000])
         assert native.gpu.json_stats()["failures"] == s1["failures"] + 1
+    finally:
+        native.set_flag("json_index_min_density", "8")
+        native.gpu.disable_json_index()
+
+
+@pytest.mark.gpu
+def test_structurally_sparse_bodies_stay_on_the_host(dev):
+    """A body that is mostly one long string has too few structural
+    characters for the device index to pay (-json_index_min_density): it is
+    parsed by the host parser, with the same result; a dense body of the
+    same size is indexed."""
+    from brpc_amd import native
+    sparse = json.dumps({"message": "x" * 200000, "sleep_us": 1}).encode()
+    dense = json.dumps({"message": "m", "ids": list(range(40000))}).encode()
+    native.gpu.enable_json_index(0, 65536)
+    try:
+        s0 = native.gpu.json_stats()
+        out = native.json_to_pb_to_json("example.EchoRequest", sparse)
+        s1 = native.gpu.json_stats()
+        assert json.loads(out)["message"] == "x" * 200000
+        assert s1["sparse_skips"] == s0["sparse_skips"] + 1
+        assert s1["indexed_bodies"] == s0["indexed_bodies"]
+        out = native.json_to_pb_to_json("example.EchoRequest", dense)
+        s2 = native.gpu.json_stats()
+        assert json.loads(out)["ids"] == list(range(40000))
+        assert s2["indexed_bodies"] == s1["indexed_bodies"] + 1
     finally:
         native.gpu.disable_json_index()
 
