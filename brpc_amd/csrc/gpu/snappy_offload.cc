@@ -86,7 +86,7 @@ void pinned_deleter(void* p, void* arg) { PinnedFree(p, (size_t)reinterpret_cast
 struct PinnedBuf {
     char* p = nullptr;
     size_t n = 0;
-    explicit PinnedBuf(size_t bytes) : p(static_cast<char*>(PinnedAlloc(bytes))), n(bytes) {}
+    explicit PinnedBuf(size_t bytes) : p(bytes ? static_cast<char*>(PinnedAlloc(bytes)) : nullptr), n(bytes) {}
     ~PinnedBuf() {
         if (p) PinnedFree(p, n);
     }
@@ -618,8 +618,9 @@ bool pack_offload(const pb::Message& msg, size_t n, Buf* out) {
     pb::SetThreadPackedRunSink(prev);
     if ((size_t)(e - reinterpret_cast<uint8_t*>(body.p)) != n) return false;
     std::vector<PbRunChunk> chunks;
-    PinnedBuf stage(col.value_bytes + 16 * col.runs.size() + 1);
     bool device_runs = !col.runs.empty();
+    PinnedBuf stage(0);  // values of the runs, only when there are any
+    if (device_runs) stage = PinnedBuf(col.value_bytes + 16 * col.runs.size());
     if (device_runs && (!stage.p || !stage_runs(col, &stage, &chunks))) {
         for (const pb::PackedRun& r : col.runs) pb::EncodePackedRunOnHost(r);
         device_runs = false;
