@@ -528,3 +528,26 @@ TEST(PbDepth, field_table_merge_with_run_decoder) {
         EXPECT_EQ(c.ids(100 + i), (int64_t)(1000 + i));
     }
 }
+
+TEST(PbDepth, repeated_scalar_data_views_the_vectors) {
+    Env e;
+    ASSERT_TRUE(e.node != nullptr);
+    std::unique_ptr<Message> m(e.node->prototype->New());
+    for (int i = 0; i < 5; ++i) Reflection::AddInt32(m.get(), e.f("ints"), i * 3);
+    size_t n = 0, eb = 0;
+    const void* p = Reflection::RepeatedScalarData(*m, e.f("ints"), &n, &eb);
+    ASSERT_TRUE(p != nullptr);
+    EXPECT_EQ(n, (size_t)5);
+    EXPECT_EQ(eb, (size_t)4);
+    EXPECT_EQ(static_cast<const int32_t*>(p)[4], 12);
+    // strings, messages and singular fields have no scalar array
+    EXPECT_TRUE(Reflection::RepeatedScalarData(*m, e.f("leaves"), &n, &eb) == nullptr);
+    EXPECT_EQ(n, (size_t)0);
+    EXPECT_TRUE(Reflection::RepeatedScalarData(*m, e.f("i32"), &n, &eb) == nullptr);
+    // the bulk packed parser fills the same vector the element path would
+    const std::string w = m->SerializeAsString();
+    std::unique_ptr<Message> back(e.node->prototype->New());
+    ASSERT_TRUE(back->ParseFromString(w));
+    EXPECT_EQ(back->SerializeAsString(), w);
+    EXPECT_EQ(Reflection::FieldSize(*back, e.f("ints")), 5);
+}
