@@ -144,6 +144,18 @@ def auto_workers(local_world):
     return max(2, min(12, share - 4))
 
 
+def merge_error_detail(per_rank):
+    """Sum per-rank {code: count} histograms; keep one error text per code
+    (with the rank it came from), so a leg with errors says why."""
+    codes, texts = {}, {}
+    for rank, d in enumerate(per_rank):
+        for k, n in d["codes"].items():
+            codes[k] = codes.get(k, 0) + int(n)
+            if k not in texts and d["texts"].get(k):
+                texts[k] = "rank %d: %s" % (rank, d["texts"][k])
+    return {"codes": codes, "texts": texts} if codes else None
+
+
 def main():
     a = parse()
     import torch  # noqa: E402
@@ -259,6 +271,9 @@ def main():
         err_total = parallel.allreduce_sum(st["error"], topo)
         p99_max = parallel.allreduce_max(st["p99_us"], topo)
         p50_max = parallel.allreduce_max(st["p50_us"], topo)
+        errs_by_rank = parallel.gather_objects(
+            {"codes": {k: v[0] for k, v in st["error_codes"].items()},
+             "texts": {k: v[1] for k, v in st["error_codes"].items()}}, topo)
         del press
         tr = transport_delta(tr0)
         step_seq = [n / x for x in step_s if x > 0]
@@ -272,6 +287,7 @@ def main():
             "errors": int(err_total),
             "elapsed_s": dt_max,
             "last_error": st["last_error"],
+            "error_detail": merge_error_detail(errs_by_rank),
             # this rank's per-step spread (box noise indicator)
             "step_qps_median": step_qps[len(step_qps) // 2] if step_qps else 0.0,
             "step_qps_min": step_qps[0] if step_qps else 0.0,
@@ -816,6 +832,10 @@ def main():
             out["cpu_pct_at_100qps"] = round(lat["cpu_pct"], 1)
             out["placement_at_100qps_rank0"] = lat["placement"]
             out["vs_baseline_p99_at_100qps"] = round(BASELINE_P99_US / lat["p99_us"], 4) if lat["p99_us"] else None
+        # any leg with errors carries its error histogram and texts
+        detail = {name: leg["error_detail"] for name, leg in legs if leg and leg.get("error_detail")}
+        if detail:
+            out["error_detail"] = detail
         print(json.dumps(out), flush=True)
     parallel.barrier(topo)
     if rccl_up:

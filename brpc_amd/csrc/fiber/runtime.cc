@@ -856,6 +856,24 @@ void apply_process_affinity() {
 
 }  // namespace
 
+// CPUs of the (possibly confined) affinity mask, physical cores first, for
+// pinning workers created later (concurrency growth); RebindL3Domain
+// replaces it with the new domain's order.
+static std::mutex g_cpu_order_mu;
+static std::vector<int>* g_cpu_order = nullptr;
+
+static std::vector<int> cpu_order_by_core() {
+    std::lock_guard<std::mutex> g(g_cpu_order_mu);
+    if (!g_cpu_order) g_cpu_order = new std::vector<int>(order_by_core(allowed_cpus()));
+    return *g_cpu_order;
+}
+
+static void set_cpu_order(const std::vector<int>& cpus) {
+    std::lock_guard<std::mutex> g(g_cpu_order_mu);
+    if (!g_cpu_order) g_cpu_order = new std::vector<int>;
+    *g_cpu_order = order_by_core(cpus);
+}
+
 int RebindL3Domain(int k) {
     // the domains are indexed over the process's allowed CPUs, which the
     // first confinement narrowed to one domain: index the host's CPUs
@@ -865,7 +883,8 @@ int RebindL3Domain(int k) {
     if (FILE* f = fopen("/sys/fs/cgroup/cpuset.cpus.effective", "r")) {
         char buf[4096];
         if (fgets(buf, sizeof(buf), f)) {
-            for (char* tok = strtok(buf, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+            char* save = nullptr;
+            for (char* tok = strtok_r(buf, ",\n", &save); tok; tok = strtok_r(nullptr, ",\n", &save)) {
                 int a = 0, b = 0;
                 const int n = sscanf(tok, "%d-%d", &a, &b);
                 if (n == 1) b = a;
@@ -880,17 +899,12 @@ int RebindL3Domain(int k) {
     if (sched_setaffinity(0, sizeof(all), &all) != 0) return -1;
     const std::vector<int> cpus = l3_domain_cpus(k);
     if (cpus.empty()) return -1;
+    set_cpu_order(cpus);
     confine_process(cpus);
     FLAGS_cpu_l3_domain = k;
     LOG(INFO) << "fiber runtime re-confined to L3 domain " << k << " (" << cpus.size() << " CPUs from "
               << cpus.front() << ")";
     return 0;
-}
-
-// CPUs of the (possibly confined) affinity mask, physical cores first.
-static const std::vector<int>& cpu_order_by_core() {
-    static std::vector<int>* order = new std::vector<int>(order_by_core(allowed_cpus()));
-    return *order;
 }
 
 void* TaskControl::worker_thread(void* arg) {
@@ -918,7 +932,7 @@ void* TaskControl::worker_thread(void* arg) {
         // a worker that never migrates keeps its run queue, stacks and the
         // sockets it serves hot in one core's caches; physical cores are
         // handed out before their SMT siblings
-        const std::vector<int>& order = cpu_order_by_core();
+        const std::vector<int> order = cpu_order_by_core();
         if (!order.empty()) {
             cpu_set_t one;
             CPU_ZERO(&one);

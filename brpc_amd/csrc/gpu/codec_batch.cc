@@ -87,30 +87,37 @@ void release(Engine& e, CBatch* b) {
     }
 }
 
+// Retire completed batches from the front of the in-flight list (any
+// thread; non-blocking).
+void retire_done(Engine& e) {
+    for (;;) {
+        CBatch* oldest = nullptr;
+        {
+            std::lock_guard<std::mutex> g(e.mu);
+            if (e.flying.empty()) return;
+            oldest = e.flying.front();
+            if (oldest->butex->load(std::memory_order_acquire) == 0) return;
+            e.flying.pop_front();
+        }
+        release(e, oldest);
+    }
+}
+
 // Leader only: retire completed batches; with the limit reached, wait for
 // the oldest (the open batch keeps collecting requests meanwhile).
 void throttle(Engine& e) {
     const int limit = FLAGS_codec_batch_max_inflight;
     for (;;) {
+        retire_done(e);
         CBatch* oldest = nullptr;
-        bool wait = false;
         {
             std::lock_guard<std::mutex> g(e.mu);
-            if (e.flying.empty()) return;
+            if (limit <= 0 || (int)e.flying.size() < limit) return;
             oldest = e.flying.front();
-            if (oldest->butex->load(std::memory_order_acquire) != 0) {
-                e.flying.pop_front();
-            } else if (limit > 0 && (int)e.flying.size() >= limit) {
-                wait = true;
-            } else {
-                return;
-            }
+            // our own ref: a requester may retire and recycle it meanwhile
+            oldest->refs.fetch_add(1, std::memory_order_relaxed);
         }
-        if (wait) {
-            while (oldest->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(oldest->butex, 0);
-            std::lock_guard<std::mutex> g(e.mu);
-            e.flying.pop_front();
-        }
+        while (oldest->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(oldest->butex, 0);
         release(e, oldest);
     }
 }
@@ -339,6 +346,9 @@ int RunCodecRequest(CodecRequest* r, int device) {
         }
     }
     release(e, mine);
+    // an idle engine must not keep finished batches (their events, pinned
+    // tables and HBM piece buffers) until the next codec request
+    retire_done(e);
     return rc;
 }
 

@@ -32,8 +32,9 @@ int GatherToDeviceWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
     if (n == 0) return 0;
     Buf dev;
     char* d = static_cast<char*>(AppendNewDeviceBlock(&dev, n, device));
-    if (!d) return -1;
-    if (copy_with_crc(in, d, crc, device) != 0) return -1;
+    if (!d) return kNoHbm;
+    const int rc = copy_with_crc(in, d, crc, device);
+    if (rc != 0) return rc;
     out->append(std::move(dev));
     return 0;
 }
@@ -44,10 +45,11 @@ int ProcessToPinnedWithCrc(const Buf& in, Buf* out, uint32_t* crc, int device) {
     *crc = 0;
     if (n == 0) return 0;
     char* h = static_cast<char*>(PinnedAlloc(n));
-    if (!h) return -1;
-    if (copy_with_crc(in, h, crc, device) != 0) {
+    if (!h) return kNoPinnedBounce;
+    const int rc = copy_with_crc(in, h, crc, device);
+    if (rc != 0) {
         PinnedFree(h, n);
-        return -1;
+        return rc;
     }
     out->append_user_data(h, n, pinned_deleter, reinterpret_cast<void*>((uintptr_t)n), MemKind::PINNED);
     return 0;
@@ -114,7 +116,7 @@ int copy_with_crc(const Buf& in, char* d, uint32_t* crc, int device) {
         if (in.ref_at(i).block->kind == MemKind::HOST) pageable += in.ref_at(i).length;
     }
     char* bounce = pageable ? static_cast<char*>(PinnedAlloc(pageable)) : nullptr;
-    if (pageable && !bounce) return -1;
+    if (pageable && !bounce) return kNoPinnedBounce;
     size_t off = 0, boff = 0;
     for (size_t i = 0; i < in.backing_block_num(); ++i) {
         const BlockRef& r = in.ref_at(i);
@@ -127,7 +129,7 @@ int copy_with_crc(const Buf& in, char* d, uint32_t* crc, int device) {
                    ArenaOffset(src, r.block->device) < 0) {
             // another device's non-arena block: not mapped here
             if (bounce) PinnedFree(bounce, pageable);
-            return -1;
+            return kForeignBlock;
         }
         segs.push_back(Segment{src, d ? d + off : nullptr, r.length});
         lens.push_back(r.length);
@@ -137,13 +139,24 @@ int copy_with_crc(const Buf& in, char* d, uint32_t* crc, int device) {
     std::vector<uint32_t> crcs(segs.size());
     const int rc = BatchedCopy(segs.data(), (int)segs.size(), device, crcs.data(), /*fold_crc=*/true);
     if (bounce) PinnedFree(bounce, pageable);
-    if (rc != 0) return -1;
+    if (rc != 0) return kDeviceBatchFailed;
     *crc = crcs[0];
     (void)n;
     return 0;
 }
 
 }  // namespace
+
+const char* DeviceHandlerErrorText(int rc) {
+    switch (rc) {
+    case 0: return "ok";
+    case kNoHbm: return "no HBM block for the gathered bytes";
+    case kNoPinnedBounce: return "no pinned memory for the bounce/output buffer";
+    case kForeignBlock: return "a block of another device is not mapped here";
+    case kDeviceBatchFailed: return "the copy+crc32c batch failed on the device";
+    default: return "unknown device handler error";
+    }
+}
 
 int StageToPinnedHost(const Buf& in, Buf* out) {
     // one pinned region for all device bytes, filled by one batched launch

@@ -16,6 +16,16 @@
 namespace mrpc {
 namespace gpu {
 
+// Failure codes of the handler steps below (0 = success), so the RPC's
+// error text says which step failed (DeviceHandlerErrorText).
+enum DeviceHandlerError {
+    kNoHbm = -1,
+    kNoPinnedBounce = -2,
+    kForeignBlock = -3,
+    kDeviceBatchFailed = -4,
+};
+const char* DeviceHandlerErrorText(int rc);
+
 // Gather `in` (any mix of pinned/pageable host, local or peer HBM blocks)
 // into ONE new arena block on `device` appended to *out; *crc receives the
 // standard CRC32C of the bytes, folded by the same kernel that moves them.

@@ -10,6 +10,21 @@
 namespace mrpc {
 namespace json {
 
+const std::vector<Value>& Value::packed_view() const {
+    std::shared_ptr<const std::vector<Value>> v = std::atomic_load(&_view);
+    if (v) return *v;
+    auto built = std::make_shared<std::vector<Value>>();
+    built->reserve(_ints.size());
+    for (int64_t x : _ints) built->emplace_back(x);
+    std::shared_ptr<const std::vector<Value>> want = built;
+    // first publisher wins; a loser's copy is dropped, every reader gets the
+    // published one
+    std::shared_ptr<const std::vector<Value>> expected;
+    if (std::atomic_compare_exchange_strong(&_view, &expected, want)) return *want;
+    return *expected;
+}
+
+
 int64_t Value::as_int() const {
     switch (_type) {
     case INT: return _i;

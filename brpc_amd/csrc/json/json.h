@@ -19,6 +19,17 @@ public:
     // printed by the device, json2pb's SetPb2JsonArrayOffload)
     enum Type { NUL, BOOL, INT, UINT, DOUBLE, STRING, ARRAY, OBJECT, RAW };
     Value() : _type(NUL) {}
+    // copies never share the packed view (it is rebuilt on demand), so a
+    // copy never reads _view non-atomically while a reader publishes it
+    Value(const Value& o)
+        : _type(o._type), _b(o._b), _i(o._i), _u(o._u), _d(o._d), _s(o._s), _arr(o._arr), _ints(o._ints),
+          _obj(o._obj) {}
+    Value(Value&&) = default;
+    Value& operator=(const Value& o) {
+        if (this != &o) *this = Value(o);
+        return *this;
+    }
+    Value& operator=(Value&&) = default;
     explicit Value(bool b) : _type(BOOL), _b(b) {}
     explicit Value(int64_t i) : _type(INT), _i(i) {}
     explicit Value(uint64_t u) : _type(UINT), _u(u) {}
@@ -48,8 +59,11 @@ public:
     bool uint_overflows_int() const { return _type == UINT && _u > (uint64_t)INT64_MAX; }
 
     // arrays. An array of integers parsed in bulk (the device parser of
-    // SetIntArrayOffload) keeps them packed; array() materializes Values on
-    // first use, packed_ints() lets json2pb take them without that.
+    // SetIntArrayOffload) keeps them packed; packed_ints() lets json2pb take
+    // them as they are. The const array() of a packed array builds a Value
+    // view once (published atomically, so concurrent readers of one parsed
+    // Value are safe; the packed form itself never changes); the mutating
+    // accessors convert the array to Values in place.
     static Value PackedInts(std::vector<int64_t> v) {
         Value a;
         a._type = ARRAY;
@@ -58,8 +72,8 @@ public:
     }
     const std::vector<int64_t>* packed_ints() const { return _ints.empty() ? nullptr : &_ints; }
     const std::vector<Value>& array() const {
-        materialize();
-        return _arr;
+        if (_ints.empty()) return _arr;
+        return packed_view();
     }
     std::vector<Value>& mutable_array() {
         materialize();
@@ -85,20 +99,24 @@ public:
 
 private:
     void write(std::string* out, bool pretty, int indent) const;
-    void materialize() const {
+    void materialize() {
         if (_ints.empty()) return;
         _arr.reserve(_ints.size());
         for (int64_t x : _ints) _arr.emplace_back(x);
         _ints.clear();
+        _view.reset();
     }
+    const std::vector<Value>& packed_view() const;
     Type _type;
     bool _b = false;
     int64_t _i = 0;
     uint64_t _u = 0;
     double _d = 0;
     std::string _s;
-    mutable std::vector<Value> _arr;
-    mutable std::vector<int64_t> _ints;
+    std::vector<Value> _arr;
+    std::vector<int64_t> _ints;
+    // Values of a packed array for const readers (std::atomic_load/store)
+    mutable std::shared_ptr<const std::vector<Value>> _view;
     std::vector<std::pair<std::string, Value>> _obj;
 };
 

@@ -59,6 +59,14 @@ ParseResult InputMessenger::CutInputMessage(Socket* m, size_t* index, bool read_
             return r;
         }
         if (r.error() != PARSE_ERROR_TRY_OTHERS) {
+            // a protocol that installed its parsing context owns the
+            // connection even before its first complete message (the redis
+            // server runs commands inside parse and always asks for more):
+            // later reads go to it first, so a partial value at the front of
+            // the buffer is never offered to the other protocols
+            if (r.error() == PARSE_ERROR_NOT_ENOUGH_DATA && m->parsing_context() != nullptr) {
+                m->_preferred_index = (int)i;
+            }
             *index = i;
             return r;
         }

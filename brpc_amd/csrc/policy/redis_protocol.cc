@@ -56,10 +56,17 @@ bool is_client_socket(Socket* s) { return s->user() == get_client_side_messenger
 // One CRLF-terminated line from the front of `in`: 1 (consumed into
 // *line), 0 (incomplete), -1 (no CRLF within a sane header length).
 int read_line(Buf* in, std::string* line, size_t max_len) {
-    char buf[128];
-    const size_t n = in->copy_to(buf, std::min(in->size(), std::min(max_len, sizeof(buf))));
+    char small[128];
+    std::string big;
+    const size_t window = std::min(in->size(), max_len);
+    char* buf = small;
+    if (window > sizeof(small)) {  // long inline commands: scan a heap window
+        big.resize(window);
+        buf = &big[0];
+    }
+    const size_t n = in->copy_to(buf, window);
     const char* nl = static_cast<const char*>(memchr(buf, '\n', n));
-    if (!nl) return n >= std::min(max_len, sizeof(buf)) ? -1 : 0;
+    if (!nl) return n >= max_len ? -1 : 0;
     const size_t len = (size_t)(nl - buf);
     line->assign(buf, len && buf[len - 1] == '\r' ? len - 1 : len);
     in->pop_front(len + 1);
@@ -78,6 +85,7 @@ bool parse_int(const std::string& s, size_t from, int64_t* out) {
 }
 
 const int64_t kMaxArgs = 1 << 20;
+const size_t kMaxInline = 64 << 10;  // redis' PROTO_INLINE_MAX_SIZE
 const int64_t kMaxBulk = int64_t(512) << 20;  // redis' proto-max-bulk-len
 
 // Next complete command (array of bulk strings, or an inline command):
@@ -88,8 +96,8 @@ int parse_command(RedisServerContext* ctx, Buf* in, std::vector<std::string>* ar
         if (in->copy_to(&first, 1) != 1) return 0;
         std::string line;
         if (first != '*') {
-            // inline command: "PING\r\n"
-            const int rc = read_line(in, &line, 128);
+            // inline command: "PING\r\n", up to redis' 64 KiB inline limit
+            const int rc = read_line(in, &line, kMaxInline);
             if (rc <= 0) return rc;
             *args = split_string(line, ' ');
             return args->empty() ? -1 : 1;

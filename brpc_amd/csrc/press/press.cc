@@ -55,6 +55,7 @@ struct PressSession::Worker {
     int64_t i_sent = 0, i_ok = 0, i_err = 0, i_bytes = 0;
     int last_code = 0;
     std::string last_error;
+    std::map<int, std::pair<int64_t, std::string>> codes;  // error histogram
     std::atomic<int64_t>* remaining = nullptr;  // closed loop with a budget
     std::atomic<bool>* stop = nullptr;          // run-until-stopped
     int64_t pace_us = 0;                        // open loop interval per sender
@@ -76,6 +77,9 @@ struct PressSession::Worker {
             ++i_err;
             last_code = code;
             last_error = etext;
+            auto& c = codes[code];
+            ++c.first;
+            c.second = etext;
         }
     }
 };
@@ -429,6 +433,11 @@ void PressSession::collect(std::vector<std::unique_ptr<Worker>>& ws) {
             _last_code = w->last_code;
             _last_error = w->last_error;
         }
+        for (const auto& kv : w->codes) {
+            auto& c = _error_codes[kv.first];
+            c.first += kv.second.first;
+            c.second = kv.second.second;
+        }
     }
 }
 
@@ -571,6 +580,7 @@ Snapshot PressSession::Stats() const {
     Snapshot s = summarize(_hist, _sent, _ok, _err, _bytes, _busy_s);
     s.last_error_code = _last_code;
     s.last_error = _last_error;
+    s.error_codes = _error_codes;
     return s;
 }
 
@@ -581,6 +591,7 @@ void PressSession::ResetStats() {
     _busy_s = 0;
     _last_code = 0;
     _last_error.clear();
+    _error_codes.clear();
 }
 
 std::string FormatLatencyTable(const Snapshot& s) {

@@ -15,6 +15,7 @@
 
 #include <atomic>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -88,6 +89,10 @@ struct Snapshot {
     int64_t bytes = 0;          // request+response payload bytes moved
     int last_error_code = 0;
     std::string last_error;
+    // failed calls by error code, each with the text of its latest failure
+    // (rpc_press prints error counts next to every latency line:
+    // tools/rpc_press/info_thread.cpp:60-92)
+    std::map<int, std::pair<int64_t, std::string>> error_codes;
 };
 
 class PressSession {
@@ -136,6 +141,7 @@ private:
     double _busy_s = 0;
     int _last_code = 0;
     std::string _last_error;
+    std::map<int, std::pair<int64_t, std::string>> _error_codes;
     std::atomic<int64_t> _inflight{0};
 };
 

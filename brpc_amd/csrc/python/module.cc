@@ -191,6 +191,9 @@ py::dict snapshot_dict(const press::Snapshot& s) {
     d["bytes"] = s.bytes;
     d["last_error_code"] = s.last_error_code;
     d["last_error"] = s.last_error;
+    py::dict codes;
+    for (const auto& kv : s.error_codes) codes[py::str(std::to_string(kv.first))] = py::make_tuple(kv.second.first, kv.second.second);
+    d["error_codes"] = codes;
     return d;
 }
 

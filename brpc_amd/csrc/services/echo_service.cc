@@ -211,7 +211,8 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
                                  [cntl, response, d, dev, nbytes, calls](int rc, Buf out, uint32_t crc) {
                                      ClosureGuard g(d);
                                      if (rc != 0) {
-                                         cntl->SetFailed(EINTERNAL, "device processing of %zu bytes failed", nbytes);
+                                         cntl->SetFailed(EINTERNAL, "device processing of %zu bytes failed (%d: %s)", nbytes, rc,
+                                                         gpu::DeviceHandlerErrorText(rc));
                                          return;
                                      }
                                      calls->fetch_add(1, std::memory_order_relaxed);

@@ -2,6 +2,11 @@
 // test/brpc_redis_unittest.cpp): pipelined commands, reply types, server
 // command handlers and MULTI/EXEC.
 #include <map>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
 #include <atomic>
 #include <mutex>
 #include <thread>
@@ -422,4 +427,83 @@ TEST(Redis, auth_and_select_once_per_connection) {
     good.GenerateCredential(&cred);
     EXPECT_EQ(cred, "*2\r\n$4\r\nAUTH\r\n$6\r\ns3cret\r\n*2\r\n$6\r\nSELECT\r\n$1\r\n3\r\n");
     EXPECT_EQ(good.auth_replies(), 2);
+}
+
+namespace {
+int raw_connect(int port) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons((uint16_t)port);
+    sa.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (connect(fd, (sockaddr*)&sa, sizeof(sa)) != 0) {
+        close(fd);
+        return -1;
+    }
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    return fd;
+}
+bool send_all(int fd, const std::string& s) {
+    size_t off = 0;
+    while (off < s.size()) {
+        const ssize_t n = ::send(fd, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+        if (n <= 0) return false;
+        off += (size_t)n;
+    }
+    return true;
+}
+// read until `want` bytes arrived (or 3 s passed)
+std::string recv_n(int fd, size_t want) {
+    std::string out;
+    const int64_t end = monotonic_us() + 3000000;
+    char buf[4096];
+    while (out.size() < want && monotonic_us() < end) {
+        pollfd p{fd, POLLIN, 0};
+        if (poll(&p, 1, 100) <= 0) continue;
+        const ssize_t n = ::recv(fd, buf, sizeof(buf), 0);
+        if (n <= 0) break;
+        out.append(buf, (size_t)n);
+    }
+    return out;
+}
+}  // namespace
+
+// a SET whose value starts with another protocol's magic
+// ("PRPC" is baidu_std's) arrives split across reads. Once the redis
+// parser installed its context the connection is redis's: the value at the
+// front of the buffer must not be offered to baidu_std.
+TEST(Redis, split_value_with_foreign_magic_stays_redis) {
+    KV kv;
+    RedisService svc;
+    SetHandler set(&kv);
+    GetHandler get(&kv);
+    svc.AddCommandHandler("set", &set);
+    svc.AddCommandHandler("get", &get);
+    Server server;
+    ServerOptions so;
+    so.redis_service = &svc;
+    so.has_builtin_services = false;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &so), 0);
+    const int fd = raw_connect(server.listen_port());
+    ASSERT_GE(fd, 0);
+    const std::string value = "PRPC\x00\x00\x00\x10\x00\x00\x00\x04" + std::string("abcd");
+    const std::string v(value.data(), 16);
+    // header and bulk length first, the value in a later read
+    ASSERT_TRUE(send_all(fd, "*3\r\n$3\r\nSET\r\n$1\r\nk\r\n$16\r\n"));
+    usleep(50000);
+    ASSERT_TRUE(send_all(fd, v.substr(0, 6)));
+    usleep(50000);
+    ASSERT_TRUE(send_all(fd, v.substr(6) + "\r\n"));
+    EXPECT_EQ(recv_n(fd, 5), "+OK\r\n");
+    ASSERT_TRUE(send_all(fd, "*2\r\n$3\r\nGET\r\n$1\r\nk\r\n"));
+    const std::string want = "$16\r\n" + v + "\r\n";
+    EXPECT_EQ(recv_n(fd, want.size()), want);
+    {
+        std::lock_guard<std::mutex> g(kv.mu);
+        EXPECT_EQ(kv.m["k"], v);
+    }
+    close(fd);
+    server.Stop(0);
+    server.Join();
 }

@@ -98,6 +98,15 @@ def exchange_addresses(addr, topo):
     return out
 
 
+def gather_objects(obj, topo):
+    """Every rank's `obj` (picklable), indexed by rank, on every rank."""
+    if not topo.distributed:
+        return [obj]
+    out = [None] * topo.world_size
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def ring_peer(topo, hop=1):
     return (topo.rank + hop) % topo.world_size
 

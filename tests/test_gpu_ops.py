@@ -389,6 +389,29 @@ def test_gpu_process_echo_handler(dev, device_attachment):
         s.stop()
 
 
+@pytest.mark.parametrize("device_attachment", [False, True])
+def test_gpu_process_echo_handler_bench_shape(dev, device_attachment):
+    """The bench's GPU-handler leg shape: 50 in flight on one connection,
+    64 KiB attachments, max_retry 0, every reply checked (bytes + device
+    CRC). Any failure reports its error histogram."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    from brpc_amd.models.echo import ECHO_64KB
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        o = ECHO_64KB.press_options(s.address, gpu_device=0)
+        o.update({"concurrency": 50, "check_echo": True, "check_every": 1, "gpu_process": True,
+                  "device_attachment": device_attachment})
+        p = native.Press(o)
+        p.run_requests(2000)  # warm-up, as the bench does
+        p.reset_stats()
+        p.run_requests(20000)
+        st = p.stats()
+        assert st["success"] == 20000 and st["error"] == 0, (st["error_codes"], st["last_error"])
+    finally:
+        s.stop()
+
+
 def test_batched_copy_crc32c_fused(dev):
     """The fused pull+checksum kernel: bytes copied exactly and CRC32C equal
     to the host SSE4.2 value, aligned and misaligned segments alike."""
