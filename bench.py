@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--verbose-sweep", action="store_true", help="print HBM pool / free memory after each point")
     ap.add_argument("--stream-min-s", type=float, default=1.0, help="the stream leg is timed for at least this long")
     ap.add_argument("--requests-per-step-grpc", type=int, default=2000)
+    ap.add_argument("--bodies", default="text,random",
+                    help="body kinds of the 64 KiB codec legs: text (log records), random, const (one repeated byte)")
     ap.add_argument("--requests-per-step-fanout", type=int, default=500)
     ap.add_argument("--skip-stream", action="store_true",
                     help="skip the streaming-RPC leg (64 KiB chunks, BASELINE config 3)")
@@ -297,38 +299,49 @@ def main():
         }
 
     def latency_sample():
-        # rpc_press -qps=100 -thread_num=1 analog: one caller, paced, 32 B
+        # rpc_press -qps=100 -thread_num=1 analog: one caller, paced, 32 B.
+        # Sampled where the rank runs, then (by default) again after the
+        # rank moved to the L3 domain whose CPUs wake sleepers promptly:
+        # both are reported, so the move's effect is visible.
         if a.latency_sample_s <= 0:
             return None
-        moved = {}
+
+        def sample():
+            press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
+                                  "connection_type": "single"})
+            parallel.barrier(topo)
+            press.run_for(0.5)  # warm-up: the first calls of a connection pay lazy setup
+            press.reset_stats()
+            r0, w0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
+            press.run_for(a.latency_sample_s)
+            r1, w1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
+            st = press.stats()
+            # the whole rank (client, server, dispatcher, timers) while it
+            # serves 100 QPS: what the latency costs in CPU
+            cpu_pct = 100.0 * ((r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)) / max(1e-9, w1 - w0)
+            del press
+            return {"p50_us": parallel.allreduce_max(st["p50_us"], topo),
+                    "p99_us": parallel.allreduce_max(st["p99_us"], topo),
+                    "p999_us": parallel.allreduce_max(st["p999_us"], topo),
+                    "avg_us": parallel.allreduce_max(st["avg_us"], topo),
+                    "errors": int(parallel.allreduce_sum(st["error"], topo)),
+                    "cpu_pct": parallel.allreduce_max(cpu_pct, topo)}
+
+        out = sample()
+        out["placement"] = {}
         if a.cpu_l3_domain == -2 and topo.device >= 0 and not a.no_latency_replace:
             # other tenants' load on the host shifts over the minutes the
             # legs take: probe the rank's domains again and move the rank
-            # to the one whose CPUs wake sleepers promptly
+            # to the quietest (a lone rank may even leave its GPU's NUMA node)
             from brpc_amd.parallel.placement import rechoose_l3_domain  # noqa: E402
-            # (the sample is the last leg by default, so a lone rank may even
-            # leave its GPU's NUMA node for a quieter domain)
             moved = rechoose_l3_domain(topo.local_rank, topo.local_world_size, topo.device,
                                        torch.cuda.device_count() if torch.cuda.is_available() else 0,
                                        widen_late=0 if a.latency_first else 20)
-        press = native.Press({"server": peer, "qps": 100.0, "concurrency": 1, "request_size": 32,
-                              "connection_type": "single"})
-        parallel.barrier(topo)
-        press.run_for(0.5)  # warm-up: the first calls of a connection pay lazy setup
-        press.reset_stats()
-        r0, w0 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
-        press.run_for(a.latency_sample_s)
-        r1, w1 = resource.getrusage(resource.RUSAGE_SELF), time.perf_counter()
-        st = press.stats()
-        # the whole rank (client, server, dispatcher, timers) while it serves
-        # 100 QPS: what the latency costs in CPU
-        cpu_pct = 100.0 * ((r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)) / max(1e-9, w1 - w0)
-        out = {"p50_us": parallel.allreduce_max(st["p50_us"], topo),
-               "p99_us": parallel.allreduce_max(st["p99_us"], topo),
-               "p999_us": parallel.allreduce_max(st["p999_us"], topo),
-               "avg_us": parallel.allreduce_max(st["avg_us"], topo),
-               "cpu_pct": parallel.allreduce_max(cpu_pct, topo), "placement": moved}
-        del press
+            if parallel.allreduce_max(1.0 if moved.get("moved") else 0.0, topo) > 0:
+                before = out
+                out = sample()
+                out["before_move"] = {k: before[k] for k in ("p50_us", "p99_us", "p999_us", "cpu_pct", "errors")}
+            out["placement"] = moved
         return out
 
     lat = latency_sample() if a.latency_first else None
@@ -401,74 +414,66 @@ def main():
         if cuda:
             rg = timed_leg(wlg, a.steps, a.warmup, dict(og, gpu_process=True))
 
-    # gRPC + snappy leg (BASELINE config 4): h2:grpc echo of a 64 KiB
-    # protobuf body, snappy-compressed in both directions (grpc-encoding),
-    # once with the CPU codec and once with the codec on the GPU (batched
-    # snappy kernels behind the compress registry, 16 KiB threshold).
-    rz = None
-    if not a.skip_grpc:
-        wlz = EchoWorkload("grpc_snappy_64KB", request_size=65536, attachment_size=0,
-                           requests_per_step=max(1, a.requests_per_step_grpc))
-        oz = wlz.press_options(peer, gpu_device=topo.device)
-        oz.update({"concurrency": a.concurrency, "protocol": "h2:grpc", "request_compress_type": 1})
-        rz = {"cpu": timed_leg(wlz, a.steps, a.warmup, dict(oz))}
-        if cuda:
-            native.gpu.enable_snappy(topo.device, 16384)
-            try:
-                z0, b0 = native.gpu.snappy_stats(), native.gpu.codec_batch_stats()
-                rz["gpu"] = timed_leg(wlz, a.steps, a.warmup, dict(oz))
-                z1, b1 = native.gpu.snappy_stats(), native.gpu.codec_batch_stats()
-                # bodies decoded + pb_scan-indexed on the GPU, merged from the field table
-                rz["gpu"]["indexed_parses"] = z1["indexed_parses"] - z0["indexed_parses"]
-                # codec requests of concurrent RPCs share launch sequences
-                nl = b1["launches"] - b0["launches"]
-                rz["gpu"]["codec_requests_per_launch"] = round((b1["requests"] - b0["requests"]) / nl, 2) if nl else 0
-            finally:
-                native.gpu.disable_snappy()
-
-    # The other device codec paths, CPU vs GPU on the same 64 KiB body:
-    # baidu_std + snappy (the headline's protocol; the body is decoded and
-    # pb_scan-indexed on the device) and http + json (json2pb over the GPU
-    # structural index, gpu/json_offload.h).
+    # Codec legs, CPU vs GPU codec on the same 64 KiB protobuf body, once per
+    # body kind (--bodies): "text" (log/JSON records, ~3x snappy-compressible)
+    # and "random" (incompressible); "const" (one repeated byte, the best
+    # case for any compressor) only on request.
+    #  * gRPC + snappy (BASELINE config 4): h2:grpc, grpc-encoding snappy both
+    #    ways; the GPU codec is the batched snappy kernels behind the
+    #    compress registry (16 KiB threshold), every body pb_scan-indexed.
+    #  * baidu_std + snappy: the headline's protocol with compressed bodies.
+    #  * baidu_std + snappy with 16k packed int64 ids (~70 KiB bodies): the
+    #    device encodes/decodes the packed run in the codec batch.
+    #  * http + json (text body; JSON needs text), and the same 16k ids over
+    #    http + json, where pb2json/json2pb number arrays run on the device
+    #     against the host parser.
     rx = {}
+    bodies = [b for b in a.bodies.split(",") if b]
     if not a.skip_grpc:
-        codec_legs = (
-            ("baidu_std_snappy_64KB", {"protocol": "baidu_std", "request_compress_type": 1},
-             lambda: native.gpu.enable_snappy(topo.device, 16384), lambda: native.gpu.disable_snappy(),
-             lambda: native.gpu.snappy_stats()["indexed_parses"]),
-            # 16k packed int64 ids per request and response (~70 KiB bodies):
-            # with the GPU codec the device encodes the ids into the body in
-            # the compress batch; device_bodies counts those runs
+        snappy_on = (lambda: native.gpu.enable_snappy(topo.device, 16384), lambda: native.gpu.disable_snappy())
+        json_on = (lambda: native.gpu.enable_json_index(topo.device, 16384), lambda: native.gpu.disable_json_index())
+        codec_legs = []
+        for body in bodies:
+            codec_legs.append(("grpc_snappy_64KB_" + body, {"protocol": "h2:grpc", "request_compress_type": 1,
+                                                            "body": body},
+                               snappy_on, lambda: native.gpu.snappy_stats()["indexed_parses"], 1))
+            codec_legs.append(("baidu_std_snappy_64KB_" + body, {"protocol": "baidu_std", "request_compress_type": 1,
+                                                                 "body": body},
+                               snappy_on, lambda: native.gpu.snappy_stats()["indexed_parses"], 1))
+        codec_legs += [
             ("baidu_std_snappy_ids16k", {"protocol": "baidu_std", "request_compress_type": 1, "request_size": 16,
                                          "packed_ids": 16384},
-             lambda: native.gpu.enable_snappy(topo.device, 16384), lambda: native.gpu.disable_snappy(),
-             lambda: native.gpu.snappy_stats()["pack_runs"]),
-            ("http_json_64KB", {"protocol": "http", "connection_type": "pooled"},
-             lambda: native.gpu.enable_json_index(topo.device, 16384), lambda: native.gpu.disable_json_index(),
-             lambda: native.gpu.json_stats()["indexed_bodies"]),
-            # the same 16k ids over http + json: pb2json prints the arrays on
-            # the device; device_bodies counts printed arrays
+             snappy_on, lambda: native.gpu.snappy_stats()["pack_runs"], 2),
+            ("http_json_64KB_text", {"protocol": "http", "connection_type": "pooled", "body": "text"},
+             json_on, lambda: native.gpu.json_stats()["indexed_bodies"], 1),
             ("http_json_ids16k", {"protocol": "http", "connection_type": "pooled", "request_size": 16,
                                   "packed_ids": 16384},
-             lambda: native.gpu.enable_json_index(topo.device, 16384), lambda: native.gpu.disable_json_index(),
-             lambda: native.gpu.json_stats()["pb2json_arrays"]),
-        )
-        # the ids legs' CPU twins are slow (the json DOM path runs ~1.7 k
-        # QPS per rank): fewer requests per step keep them around 5 s
-        per_step = {"baidu_std_snappy_ids16k": 2, "http_json_ids16k": 3}
-        for name, extra, enable, disable, count in codec_legs:
+             json_on, lambda: native.gpu.json_stats()["pb2json_arrays"], 3),
+        ]
+        # (the ids legs' CPU twins are slow: fewer requests per step)
+        for name, extra, (enable, disable), count, per_step in codec_legs:
             wlx = EchoWorkload(name, request_size=65536, attachment_size=0,
-                               requests_per_step=max(1, a.requests_per_step_grpc // per_step.get(name, 1)))
+                               requests_per_step=max(1, a.requests_per_step_grpc // per_step))
             ox = wlx.press_options(peer, gpu_device=topo.device)
             ox.update({"concurrency": a.concurrency})
             ox.update(extra)
             rx[name] = {"cpu": timed_leg(wlx, a.steps, a.warmup, dict(ox))}
+            if "body" in extra and extra.get("request_compress_type"):
+                # what the compressor sees: the body's snappy ratio on the host
+                raw = native.echo_body(extra["body"], ox["request_size"])
+                rx[name]["body"] = extra["body"]
+                rx[name]["snappy_ratio"] = round(len(raw) / max(1, len(native.snappy_compress(raw))), 3)
             if cuda:
                 enable()
                 try:
-                    c0 = count()
+                    c0, b0 = count(), native.gpu.codec_batch_stats()
                     rx[name]["gpu"] = timed_leg(wlx, a.steps, a.warmup, dict(ox))
+                    b1 = native.gpu.codec_batch_stats()
                     rx[name]["gpu"]["device_bodies"] = count() - c0
+                    # codec requests of concurrent RPCs share launch sequences
+                    nl = b1["launches"] - b0["launches"]
+                    rx[name]["gpu"]["requests_per_launch"] = \
+                        round((b1["requests"] - b0["requests"]) / nl, 2) if nl else 0
                 finally:
                     disable()
 
@@ -699,7 +704,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": round(r32["qps"] / BASELINE_QPS_32B, 4),
             "dtype": "uint8",
-            "data": "synthetic (random echo payloads)",
+            "data": "synthetic: 32 B headline message of 'x' bytes (no compression involved); attachments "
+                    "pseudo-random bytes; codec-leg bodies per --bodies (%s): text = generated log records, "
+                    "random = incompressible bytes (each leg reports its snappy ratio)" % a.bodies,
             "config": {
                 "model": "example.EchoService.Echo over baidu_std",
                 "global_batch": a.concurrency * n,
@@ -725,7 +732,6 @@ def main():
             out["qps_64KB"] = round(r64["qps"], 1)
             out["p99_us_64KB"] = r64["p99_us"]
             out["gbytes_per_s_64KB"] = round(r64["qps"] * 65536 * 2 / 1e9, 3)
-            out["vs_baseline_64KB"] = round(r64["qps"] / BASELINE_QPS_32KB, 4)
             out["errors_64KB"] = r64["errors"]
             out["timed_s_64KB"] = round(r64["elapsed_s"], 3)
             out["device_payload_64KB"] = bool(use_dev)
@@ -733,25 +739,19 @@ def main():
             out["qps_64KB_host_attachment"] = round(r64h["qps"], 1)
             out["p99_us_64KB_host_attachment"] = r64h["p99_us"]
             out["gbytes_per_s_64KB_host_attachment"] = round(r64h["qps"] * 65536 * 2 / 1e9, 3)
-        if rz:
-            out["grpc_snappy_64KB_qps_cpu_codec"] = round(rz["cpu"]["qps"], 1)
-            out["grpc_snappy_64KB_p99_us_cpu_codec"] = rz["cpu"]["p99_us"]
-            if "gpu" in rz:
-                out["grpc_snappy_64KB_qps_gpu_codec"] = round(rz["gpu"]["qps"], 1)
-                out["grpc_snappy_64KB_p99_us_gpu_codec"] = rz["gpu"]["p99_us"]
-                out["grpc_gpu_codec_indexed_parses"] = rz["gpu"]["indexed_parses"]
-                out["grpc_gpu_codec_requests_per_launch"] = rz["gpu"]["codec_requests_per_launch"]
-                out["grpc_snappy_errors"] = rz["cpu"]["errors"] + rz["gpu"]["errors"]
         for name, r in rx.items():
             out[name + "_qps_cpu"] = round(r["cpu"]["qps"], 1)
             out[name + "_timed_s_cpu"] = round(r["cpu"]["elapsed_s"], 3)
             out[name + "_p99_us_cpu"] = r["cpu"]["p99_us"]
+            if "snappy_ratio" in r:
+                out[name + "_snappy_ratio"] = r["snappy_ratio"]
             errs = r["cpu"]["errors"]
             if "gpu" in r:
                 out[name + "_qps_gpu"] = round(r["gpu"]["qps"], 1)
                 out[name + "_timed_s_gpu"] = round(r["gpu"]["elapsed_s"], 3)
                 out[name + "_p99_us_gpu"] = r["gpu"]["p99_us"]
                 out[name + "_device_bodies"] = r["gpu"]["device_bodies"]
+                out[name + "_requests_per_launch"] = r["gpu"]["requests_per_launch"]
                 errs += r["gpu"]["errors"]
             out[name + "_errors"] = errs
         if rc:
@@ -781,8 +781,6 @@ def main():
                 out["rccl_crossover_bytes"] = sweep["rccl_crossover_bytes"]
         legs = (("echo_32B", r32), ("echo_64KB", r64), ("echo_64KB_host", r64h), ("rccl_64KB", rc),
                 ("echo_1MB", r1m), ("rccl_1MB", r1mr), ("cpu_handler_64KB", rgc), ("gpu_handler_64KB", rg))
-        if rz:
-            legs += (("grpc_snappy_cpu_codec", rz["cpu"]), ("grpc_snappy_gpu_codec", rz.get("gpu")))
         for name, r in rx.items():
             legs += ((name + "_cpu", r["cpu"]), (name + "_gpu", r.get("gpu")))
         # which transport carried each leg's payloads (summed over ranks)
@@ -832,6 +830,13 @@ def main():
             out["cpu_pct_at_100qps"] = round(lat["cpu_pct"], 1)
             out["placement_at_100qps_rank0"] = lat["placement"]
             out["vs_baseline_p99_at_100qps"] = round(BASELINE_P99_US / lat["p99_us"], 4) if lat["p99_us"] else None
+            out["errors_at_100qps"] = lat["errors"]
+            # the same sample where the rank ran before the placement move
+            # (equal to the above when the probe kept the rank in place)
+            b = lat.get("before_move", lat)
+            out["p99_us_at_100qps_before_move"] = b["p99_us"]
+            out["p50_us_at_100qps_before_move"] = b["p50_us"]
+            out["p999_us_at_100qps_before_move"] = b["p999_us"]
         # any leg with errors carries its error histogram and texts
         detail = {name: leg["error_detail"] for name, leg in legs if leg and leg.get("error_detail")}
         if detail:

@@ -157,7 +157,7 @@ public:
         }
         void* d = nullptr;
         void* h = nullptr;
-        if (hipMalloc(&d, 2 * hdr_bytes) != hipSuccess || hipHostMalloc(&h, 2 * hdr_bytes, 0) != hipSuccess) {
+        if (hipMalloc(&d, 2 * hdr_bytes) != hipSuccess || hipHostMalloc(&h, 2 * hdr_bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
             if (err) *err = "header buffers: allocation failed";
             return -1;
         }

@@ -376,9 +376,18 @@ void Free(void* p) {
     if (p) hipFree(p);
 }
 
+// Pinned host memory is COHERENT (fine-grained), whatever HIP_HOST_COHERENT
+// says. The pool recycles blocks: a socket block whose earlier bytes a
+// kernel read is refilled by recv() and read by the next kernel. With
+// non-coherent memory the GPU's L2 may still hold the old lines, and
+// kernels on one queue are dispatched with agent-scope acquires that do
+// not invalidate them, so the next kernel reads stale bytes. Measured: the
+// GPU-handler leg returned device CRC32Cs of stale data (226 of ~4.7k
+// checked replies, profiles/r4_bench_handler_crc_mismatch_repro.json) and
+// none with coherent memory, at the same throughput.
 void* HostMallocPinned(size_t n) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
     return p;
 }
 

@@ -1,5 +1,7 @@
 #include "json/json.h"
 
+#include <charconv>
+
 #include <atomic>
 
 #include <cmath>
@@ -316,6 +318,8 @@ private:
         default: return number(v);
         }
     }
+    // Numbers are converted in place from the text (std::from_chars): no
+    // std::string per number, no errno/strtoll round trip.
     bool number(Value* v) {
         const char* b = _p;
         if (_p < _end && *_p == '-') ++_p;
@@ -326,25 +330,61 @@ private:
             if (*_p == '.' || *_p == 'e' || *_p == 'E') is_float = true;
             ++_p;
         }
-        std::string s(b, _p - b);
         if (!is_float) {
-            errno = 0;
-            if (s[0] == '-') {
-                long long x = strtoll(s.c_str(), nullptr, 10);
-                if (errno == 0) {
-                    *v = Value((int64_t)x);
-                    return true;
-                }
-            } else {
-                unsigned long long x = strtoull(s.c_str(), nullptr, 10);
-                if (errno == 0) {
-                    if (x <= (unsigned long long)INT64_MAX) *v = Value((int64_t)x);
-                    else *v = Value((uint64_t)x);
+            int64_t x;
+            if (parse_int64(b, _p, &x) == _p) {
+                *v = Value(x);
+                return true;
+            }
+            if (*b != '-') {
+                uint64_t x;
+                auto r = std::from_chars(b, _p, x);
+                if (r.ec == std::errc() && r.ptr == _p) {
+                    if (x <= (uint64_t)INT64_MAX) *v = Value((int64_t)x);
+                    else *v = Value(x);
                     return true;
                 }
             }
         }
-        *v = Value(strtod(s.c_str(), nullptr));
+        double d = 0;
+        auto r = std::from_chars(b, _p, d);
+        if (r.ec == std::errc::result_out_of_range) {
+            d = strtod(std::string(b, _p - b).c_str(), nullptr);  // +-inf / denormal edge, as before
+        } else if (r.ec != std::errc() || r.ptr != _p) {
+            return fail("bad number");
+        }
+        *v = Value(d);
+        return true;
+    }
+    // A decimal int64 literal at [p, end): the end of its digits, or nullptr
+    // (no digits, more than 19 digits, or out of int64 range: the caller
+    // takes the general path). Up to 19 digits cannot overflow a uint64, so
+    // the loop has no per-digit overflow check.
+    static const char* parse_int64(const char* p, const char* end, int64_t* out) {
+        const bool neg = p < end && *p == '-';
+        if (neg) ++p;
+        const char* b = p;
+        const char* lim = end - p > 19 ? p + 19 : end;
+        uint64_t v = 0;
+        while (p < lim && (unsigned)(*p - '0') < 10u) v = v * 10 + (unsigned)(*p++ - '0');
+        if (p == b || (p < end && (unsigned)(*p - '0') < 10u)) return nullptr;
+        if (neg) {
+            if (v > (uint64_t)INT64_MAX + 1) return nullptr;
+            *out = (int64_t)(0 - v);
+        } else {
+            if (v > (uint64_t)INT64_MAX) return nullptr;
+            *out = (int64_t)v;
+        }
+        return p;
+    }
+    // An integer element of an int array, converted in place: true with *x
+    // when the next value is a plain int64 literal followed by ',' or ']'
+    // (after spaces); false (nothing consumed) otherwise.
+    bool int_element(int64_t* x) {
+        const char* e = parse_int64(_p, _end, x);
+        if (!e) return false;
+        if (e < _end && (*e == '.' || *e == 'e' || *e == 'E')) return false;
+        _p = e;
         return true;
     }
     static void put_utf8(std::string* s, uint32_t cp) {
@@ -476,6 +516,29 @@ private:
             ++_p;
             return true;
         }
+        // Integer arrays stay packed (one int64 per element, no Value per
+        // element; json2pb takes them in bulk, the way rapidjson's in-situ
+        // numbers feed the reference's json_to_pb.cpp). The first element
+        // that is not a plain int64 turns the array into Values.
+        std::vector<int64_t> ints;
+        for (;;) {
+            int64_t x;
+            skip();
+            if (!int_element(&x)) break;
+            ints.push_back(x);
+            skip();
+            if (_p < _end && *_p == ',') {
+                ++_p;
+                continue;
+            }
+            if (_p < _end && *_p == ']') {
+                ++_p;
+                *v = Value::PackedInts(std::move(ints));
+                return true;
+            }
+            return fail("expected , or ]");
+        }
+        for (int64_t x : ints) v->push_back(Value(x));
         for (;;) {
             Value e;
             skip();

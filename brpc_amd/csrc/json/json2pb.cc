@@ -1,5 +1,7 @@
 #include "json/json2pb.h"
 
+#include <charconv>
+
 #include <strings.h>
 
 #include <algorithm>
@@ -125,6 +127,38 @@ bool array_offload(const Message& m, const FieldDescriptor* f, const Pb2JsonOpti
     return fn(data, n, kind, text);
 }
 
+// The host twin of the device printer: the array's elements as decimal
+// text straight from the field's storage (std::to_chars), one string for
+// the whole array instead of a json::Value per element. Same text as
+// Value-by-Value printing.
+bool array_print_host(const Message& m, const FieldDescriptor* f, const Pb2JsonOptions& opt, std::string* text) {
+    uint32_t kind;
+    if (opt.pretty_json || !array_kind(f, opt, &kind)) return false;
+    size_t n = 0, eb = 0;
+    const void* data = Reflection::RepeatedScalarData(m, f, &n, &eb);
+    if (!data || n == 0) return false;
+    text->reserve(n * (kind == 3 || kind == 4 ? 12 : 6) + 2);
+    char buf[24];
+    for (size_t i = 0; i < n; ++i) {
+        if (i) text->push_back(',');
+        char* e = buf;
+        switch (kind) {
+        case 0: e = std::to_chars(buf, buf + sizeof(buf), static_cast<const int32_t*>(data)[i]).ptr; break;
+        case 1: e = std::to_chars(buf, buf + sizeof(buf), static_cast<const uint32_t*>(data)[i]).ptr; break;
+        case 3: e = std::to_chars(buf, buf + sizeof(buf), static_cast<const int64_t*>(data)[i]).ptr; break;
+        case 4: e = std::to_chars(buf, buf + sizeof(buf), static_cast<const uint64_t*>(data)[i]).ptr; break;
+        case 6: {
+            const bool b = eb == 1 ? static_cast<const uint8_t*>(data)[i] != 0 : static_cast<const int32_t*>(data)[i] != 0;
+            text->append(b ? "true" : "false");
+            continue;
+        }
+        default: return false;
+        }
+        text->append(buf, (size_t)(e - buf));
+    }
+    return true;
+}
+
 bool msg_to_value(const Message& m, json::Value* out, const Pb2JsonOptions& opt, std::string* err) {
     *out = json::Value::Object();
     const pb::Descriptor* d = m.GetDescriptor();
@@ -162,7 +196,7 @@ bool msg_to_value(const Message& m, json::Value* out, const Pb2JsonOptions& opt,
             const int n = Reflection::FieldSize(m, f);
             if (n == 0 && !opt.jsonify_empty_array) continue;
             std::string printed;
-            if (n > 0 && array_offload(m, f, opt, &printed)) {
+            if (n > 0 && (array_offload(m, f, opt, &printed) || array_print_host(m, f, opt, &printed))) {
                 printed.insert(printed.begin(), '[');
                 printed.push_back(']');
                 out->set(key, json::Value::Raw(std::move(printed)));

@@ -84,6 +84,56 @@ struct PressSession::Worker {
     }
 };
 
+std::string EchoBody(const std::string& kind, size_t size) {
+    std::string out;
+    if (kind == "const") {
+        out.assign(size, 'x');
+        return out;
+    }
+    uint64_t q = 0x2545F4914F6CDD1Dull;
+    auto next = [&q] {
+        q ^= q << 13;
+        q ^= q >> 7;
+        q ^= q << 17;
+        return q;
+    };
+    if (kind == "random") {
+        out.resize(size);
+        for (size_t i = 0; i < size; i += 8) {
+            const uint64_t r = next();
+            memcpy(&out[i], &r, std::min<size_t>(8, size - i));
+        }
+        return out;
+    }
+    if (kind != "text") return out;
+    // service-log records: a timestamp, a level, small vocabularies, hex
+    // ids and decimal numbers — repeated structure, high-entropy fields
+    static const char* kLevels[] = {"INFO", "INFO", "INFO", "WARN", "DEBUG", "ERROR"};
+    static const char* kPaths[] = {"/api/v1/items", "/api/v1/users", "/api/v2/search", "/healthz", "/api/v1/orders",
+                                   "/static/app.js", "/api/v2/cart", "/login"};
+    static const char* kUsers[] = {"alice", "bob", "carol", "dave", "erin", "frank", "grace", "heidi", "ivan", "judy"};
+    static const char* kAgents[] = {"curl/8.5.0", "Mozilla/5.0 (X11; Linux x86_64)", "python-requests/2.31",
+                                    "grpc-go/1.62.0"};
+    out.reserve(size + 256);
+    uint64_t ts = 1792242500000000ull;
+    char line[384];
+    while (out.size() < size) {
+        ts += next() % 5000;
+        const uint64_t r = next(), id = next();
+        const int n = snprintf(line, sizeof(line),
+                               "{\"ts\":%llu,\"level\":\"%s\",\"rank\":%u,\"req\":\"%016llx\",\"user\":\"%s\","
+                               "\"path\":\"%s/%u\",\"status\":%u,\"latency_us\":%u,\"bytes\":%u,\"agent\":\"%s\"}\n",
+                               (unsigned long long)ts, kLevels[r % 6], (unsigned)((r >> 8) % 8),
+                               (unsigned long long)id, kUsers[(r >> 12) % 10], kPaths[(r >> 16) % 8],
+                               (unsigned)((r >> 20) % 100000), (r >> 40) % 10 ? 200u : 404u,
+                               (unsigned)((r >> 24) % 20000), (unsigned)((id >> 7) % 1000000),
+                               kAgents[(r >> 44) % 4]);
+        out.append(line, (size_t)n);
+    }
+    out.resize(size);
+    return out;
+}
+
 PressSession::PressSession() {}
 
 PressSession::~PressSession() {
@@ -242,7 +292,11 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
             _requests.push_back(std::move(m));
         }
     } else {
-        _echo_message.assign(std::max(0, _opt.request_size), 'x');
+        _echo_message = EchoBody(_opt.body, (size_t)std::max(0, _opt.request_size));
+        if (_opt.request_size > 0 && _echo_message.empty()) {
+            *error = "unknown body kind '" + _opt.body + "' (const, text or random)";
+            return -1;
+        }
         // ids of every varint length (1..10 bytes, a few negative)
         uint64_t q = 0xD1B54A32D192ED03ull;
         _ids.resize((size_t)std::max(0, _opt.packed_ids));

@@ -50,6 +50,10 @@ struct PressOptions {
     int num_channels = 1;  // independent channels (connections for "single")
     // echo workload (used when proto_file is empty)
     int request_size = 32;     // bytes in EchoRequest.message
+    // contents of EchoRequest.message (EchoBody): "const" (one repeated
+    // byte: the best case for any compressor), "text" (log/JSON-like
+    // records, ~2-4x snappy-compressible), "random" (incompressible bytes)
+    std::string body = "const";
     int attachment_size = 0;   // bytes of attachment per request
     int packed_ids = 0;        // int64 ids per request (EchoRequest.ids, a packed varint run), echoed back
     bool device_attachment = false;  // attachment lives in HBM (needs GPU)
@@ -76,6 +80,10 @@ struct PressOptions {
 };
 
 struct PressCall;
+
+// The echo message of `size` bytes for a body kind (see PressOptions::body);
+// deterministic. Empty string for an unknown kind.
+std::string EchoBody(const std::string& kind, size_t size);
 
 struct Snapshot {
     int64_t sent = 0;

@@ -150,6 +150,7 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "qps") o.qps = v.cast<double>();
         else if (k == "num_channels") o.num_channels = v.cast<int>();
         else if (k == "request_size") o.request_size = v.cast<int>();
+        else if (k == "body") o.body = v.cast<std::string>();
         else if (k == "attachment_size") o.attachment_size = v.cast<int>();
         else if (k == "packed_ids") o.packed_ids = v.cast<int>();
         else if (k == "device_attachment") o.device_attachment = v.cast<bool>();
@@ -371,6 +372,7 @@ PYBIND11_MODULE(_native, m) {
         return crc32c::Value(s.data(), s.size());
     });
     // Host snappy codec (the CPU half; the GPU decompressor is gpu.snappy_*).
+    m.def("echo_body", [](const std::string& kind, size_t size) { return py::bytes(press::EchoBody(kind, size)); });
     m.def("snappy_compress", [](py::bytes b) {
         std::string s = b, out;
         snappy::Compress(s.data(), s.size(), &out);

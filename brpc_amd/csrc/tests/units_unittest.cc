@@ -567,6 +567,43 @@ TEST(JsonUnit, parse_types_and_serialize) {
     EXPECT_TRUE(v.find("missing") == nullptr);
 }
 
+// Host int arrays stay packed (no Value per element); anything that is not
+// a plain int64 turns the array into Values with the same contents.
+TEST(JsonUnit, packed_int_arrays_and_fallbacks) {
+    json::Value v;
+    ASSERT_TRUE(json::Parse("[1, -2 ,3,9223372036854775807,-9223372036854775808, 0]", &v));
+    ASSERT_TRUE(v.packed_ints() != nullptr);
+    const std::vector<int64_t> want = {1, -2, 3, INT64_MAX, INT64_MIN, 0};
+    EXPECT_TRUE(*v.packed_ints() == want);
+    EXPECT_EQ(v.size(), 6u);
+    EXPECT_EQ(v.array()[3].as_int(), INT64_MAX);  // the const view
+    EXPECT_EQ(v.ToString(), "[1,-2,3,9223372036854775807,-9223372036854775808,0]");
+    const json::Value copy = v;  // copies do not share the view
+    EXPECT_EQ(copy.array().size(), 6u);
+    // a uint64 beyond int64, a float, a string: element-wise Values
+    ASSERT_TRUE(json::Parse("[1,2,18446744073709551615]", &v));
+    EXPECT_TRUE(v.packed_ints() == nullptr);
+    ASSERT_EQ(v.array().size(), 3u);
+    EXPECT_EQ(v.array()[1].as_int(), 2);
+    EXPECT_TRUE(v.array()[2].uint_overflows_int());
+    ASSERT_TRUE(json::Parse("[1,2.5,\"x\",[3]]", &v));
+    EXPECT_TRUE(v.packed_ints() == nullptr);
+    ASSERT_EQ(v.array().size(), 4u);
+    EXPECT_EQ(v.array()[1].as_double(), 2.5);
+    EXPECT_EQ(v.array()[2].as_string(), "x");
+    EXPECT_TRUE(v.array()[3].packed_ints() != nullptr);
+    ASSERT_TRUE(json::Parse("[1e3, 7]", &v));
+    EXPECT_EQ(v.array()[0].as_double(), 1000.0);
+    // 20 digits: not an int64 literal
+    ASSERT_TRUE(json::Parse("[-92233720368547758080]", &v));
+    EXPECT_TRUE(v.array()[0].type() == json::Value::DOUBLE);
+    // the packed path still rejects what the element path rejects
+    EXPECT_FALSE(json::Parse("[1,2", &v));
+    EXPECT_FALSE(json::Parse("[1 2]", &v));
+    EXPECT_FALSE(json::Parse("[1,]", &v));
+    EXPECT_FALSE(json::Parse("[1.2.3]", &v));
+}
+
 TEST(JsonUnit, malformed_inputs) {
     json::Value v;
     std::string err;

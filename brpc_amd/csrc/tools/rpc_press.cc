@@ -27,6 +27,7 @@ DEFINE_int32(max_retry, 3, "max retries");
 DEFINE_int32(request_compress_type, 0, "0 none, 1 snappy, 2 gzip, 3 zlib");
 DEFINE_int32(response_compress_type, 0, "0 none, 1 snappy, 2 gzip, 3 zlib");
 DEFINE_int32(request_size, 32, "echo message bytes (built-in workload)");
+DEFINE_string(body, "const", "echo message contents: const, text (log records) or random");
 DEFINE_int32(attachment_size, 0, "attachment bytes per request");
 DEFINE_bool(device_attachment, false, "keep the attachment in HBM (MI355X)");
 DEFINE_int32(duration, 0, "seconds to run (0: until killed)");
@@ -54,6 +55,7 @@ int main(int argc, char** argv) {
     o.qps = FLAGS_qps;
     o.num_channels = FLAGS_channels;
     o.request_size = FLAGS_request_size;
+    o.body = FLAGS_body;
     o.attachment_size = FLAGS_attachment_size;
     o.device_attachment = FLAGS_device_attachment;
     o.check_echo = FLAGS_check;

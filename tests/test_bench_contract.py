@@ -63,8 +63,15 @@ def test_bench_multi_rank_gloo(nranks):
     # the host-only handler twin, and the CPU cost of every leg
     assert j["errors_64KB_cpu_handler"] == 0 and j["qps_64KB_cpu_handler"] > 0
     assert all(v > 0 for v in j["cpu_us_per_rpc"].values()) and "cpu_handler_64KB" in j["cpu_us_per_rpc"]
-    # the other codec paths (baidu_std + snappy, http + json), CPU side here
-    for leg in ("baidu_std_snappy_64KB", "http_json_64KB"):
+    # the codec paths per body kind (gRPC/baidu_std + snappy on text and
+    # random bodies, http + json), CPU side here; compressed legs report
+    # their body's snappy ratio
+    for leg in ("grpc_snappy_64KB_text", "grpc_snappy_64KB_random", "baidu_std_snappy_64KB_text",
+                "baidu_std_snappy_64KB_random", "http_json_64KB_text", "baidu_std_snappy_ids16k", "http_json_ids16k"):
         assert j[leg + "_errors"] == 0 and j[leg + "_qps_cpu"] > 0 and leg + "_cpu" in j["cpu_us_per_rpc"]
+    assert 2.0 < j["baidu_std_snappy_64KB_text_snappy_ratio"] < 5.0
+    assert j["grpc_snappy_64KB_random_snappy_ratio"] <= 1.01
+    assert "error_detail" not in j and "vs_baseline_64KB" not in j
+    assert j["p99_us_at_100qps_before_move"] > 0
     if nranks > 2:  # a relay chain needs at least two other ranks
         assert j["pipeline_hops"] == nranks - 1 and j["pipeline_gbytes_per_s"] > 0
