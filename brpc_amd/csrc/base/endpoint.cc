@@ -2,6 +2,7 @@
 
 #include <arpa/inet.h>
 #include <fcntl.h>
+#include <net/if.h>
 #include <netdb.h>
 #include <netinet/tcp.h>
 #include <poll.h>
@@ -33,10 +34,48 @@ int str2ip(const char* s, uint32_t* ip) {
     return 0;
 }
 
-std::string EndPoint::ip_string() const { return is_unix() ? std::string("unix") : ip2str(ip); }
+int str2ip6(const char* s, EndPoint* ep) {
+    while (*s == ' ') ++s;
+    std::string addr(s);
+    uint32_t scope = 0;
+    const size_t pct = addr.find('%');
+    if (pct != std::string::npos) {
+        const std::string zone = addr.substr(pct + 1);
+        addr.resize(pct);
+        char* end = nullptr;
+        const unsigned long z = strtoul(zone.c_str(), &end, 10);
+        scope = (end && *end == 0 && !zone.empty()) ? (uint32_t)z : if_nametoindex(zone.c_str());
+        if (scope == 0) return -1;
+    }
+    in6_addr a;
+    if (inet_pton(AF_INET6, addr.c_str(), &a) != 1) return -1;
+    memcpy(ep->ip6, &a, 16);
+    ep->v6 = true;
+    ep->scope_id = scope;
+    ep->ip = 0;
+    return 0;
+}
+
+static std::string ip6str(const EndPoint& ep) {
+    char buf[INET6_ADDRSTRLEN];
+    inet_ntop(AF_INET6, ep.ip6, buf, sizeof(buf));
+    std::string s = buf;
+    if (ep.scope_id) {
+        char name[IF_NAMESIZE];
+        s += "%";
+        s += if_indextoname(ep.scope_id, name) ? name : std::to_string(ep.scope_id).c_str();
+    }
+    return s;
+}
+
+std::string EndPoint::ip_string() const {
+    if (is_unix()) return "unix";
+    return v6 ? ip6str(*this) : ip2str(ip);
+}
 
 std::string EndPoint::to_string() const {
     if (is_unix()) return "unix:" + path;
+    if (v6) return "[" + ip6str(*this) + "]:" + std::to_string(port);
     return ip2str(ip) + ":" + std::to_string(port);
 }
 
@@ -49,27 +88,45 @@ int str2endpoint(const char* str, EndPoint* ep) {
         ep->path = str + 5;
         return ep->path.empty() ? -1 : 0;
     }
+    while (*str == ' ') ++str;
+    if (*str == '[') {  // "[v6addr]:port"
+        const char* close = strchr(str, ']');
+        if (!close || close[1] != ':') return -1;
+        char* end = nullptr;
+        const long port = strtol(close + 2, &end, 10);
+        if (end == close + 2 || (*end && *end != ' ') || port < 0 || port > 65535) return -1;
+        EndPoint e;
+        if (str2ip6(std::string(str + 1, close - str - 1).c_str(), &e) != 0) return -1;
+        e.port = (int)port;
+        *ep = e;
+        return 0;
+    }
     const char* colon = strrchr(str, ':');
     if (!colon) return -1;
     std::string host(str, colon - str);
+    if (host.find(':') != std::string::npos) return -1;  // bare IPv6 needs brackets
     char* end = nullptr;
     long port = strtol(colon + 1, &end, 10);
     if (end == colon + 1 || (*end && *end != ' ') || port < 0 || port > 65535) return -1;
     uint32_t ip;
     if (str2ip(host.c_str(), &ip) != 0) return -1;
-    ep->ip = ip;
-    ep->port = (int)port;
-    ep->path.clear();
+    *ep = EndPoint(ip, (int)port);
     return 0;
 }
 
 int str2endpoint(const char* ip_str, int port, EndPoint* ep) {
-    uint32_t ip;
-    if (str2ip(ip_str, &ip) != 0) return -1;
     if (port < 0 || port > 65535) return -1;
-    ep->ip = ip;
-    ep->port = port;
-    ep->path.clear();
+    uint32_t ip;
+    if (str2ip(ip_str, &ip) == 0) {
+        *ep = EndPoint(ip, port);
+        return 0;
+    }
+    std::string s(ip_str);
+    if (!s.empty() && s.front() == '[' && s.back() == ']') s = s.substr(1, s.size() - 2);
+    EndPoint e;
+    if (str2ip6(s.c_str(), &e) != 0) return -1;
+    e.port = port;
+    *ep = e;
     return 0;
 }
 
@@ -80,13 +137,31 @@ int hostname2endpoint(const char* host_and_port, EndPoint* ep) {
     int port = colon ? atoi(colon + 1) : 80;
     addrinfo hints;
     memset(&hints, 0, sizeof(hints));
-    hints.ai_family = AF_INET;
+    hints.ai_family = AF_UNSPEC;  // an A record first, else AAAA
     hints.ai_socktype = SOCK_STREAM;
     addrinfo* res = nullptr;
     if (getaddrinfo(host.c_str(), nullptr, &hints, &res) != 0 || !res) return -1;
-    ep->ip = ((sockaddr_in*)res->ai_addr)->sin_addr.s_addr;
-    ep->port = port;
-    ep->path.clear();
+    const addrinfo* pick = res;
+    for (const addrinfo* r = res; r; r = r->ai_next) {
+        if (r->ai_family == AF_INET) {
+            pick = r;
+            break;
+        }
+    }
+    EndPoint e;
+    if (pick->ai_family == AF_INET) {
+        e.ip = ((sockaddr_in*)pick->ai_addr)->sin_addr.s_addr;
+    } else if (pick->ai_family == AF_INET6) {
+        const sockaddr_in6* in6 = (const sockaddr_in6*)pick->ai_addr;
+        e.v6 = true;
+        memcpy(e.ip6, &in6->sin6_addr, 16);
+        e.scope_id = in6->sin6_scope_id;
+    } else {
+        freeaddrinfo(res);
+        return -1;
+    }
+    e.port = port;
+    *ep = e;
     freeaddrinfo(res);
     return 0;
 }
@@ -117,6 +192,14 @@ static socklen_t fill_sockaddr(const EndPoint& ep, sockaddr_storage* ss) {
         strncpy(un->sun_path, ep.path.c_str(), sizeof(un->sun_path) - 1);
         return sizeof(sockaddr_un);
     }
+    if (ep.v6) {
+        sockaddr_in6* in6 = (sockaddr_in6*)ss;
+        in6->sin6_family = AF_INET6;
+        memcpy(&in6->sin6_addr, ep.ip6, 16);
+        in6->sin6_port = htons((uint16_t)ep.port);
+        in6->sin6_scope_id = ep.scope_id;
+        return sizeof(sockaddr_in6);
+    }
     sockaddr_in* in = (sockaddr_in*)ss;
     in->sin_family = AF_INET;
     in->sin_addr.s_addr = ep.ip;
@@ -145,8 +228,10 @@ int make_no_delay(int fd) {
 
 int make_close_on_exec(int fd) { return fcntl(fd, F_SETFD, FD_CLOEXEC); }
 
+static int family_of(const EndPoint& ep) { return ep.is_unix() ? AF_UNIX : ep.v6 ? AF_INET6 : AF_INET; }
+
 int tcp_listen(const EndPoint& ep, bool reuse_port, int backlog) {
-    int fd = socket(ep.is_unix() ? AF_UNIX : AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    int fd = socket(family_of(ep), SOCK_STREAM | SOCK_CLOEXEC, 0);
     if (fd < 0) return -1;
     if (!ep.is_unix()) {
         int one = 1;
@@ -168,7 +253,7 @@ int tcp_listen(const EndPoint& ep, bool reuse_port, int backlog) {
 
 int tcp_connect_nonblocking(const EndPoint& ep, bool* in_progress) {
     *in_progress = false;
-    int fd = socket(ep.is_unix() ? AF_UNIX : AF_INET, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+    int fd = socket(family_of(ep), SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
     if (fd < 0) return -1;
     if (!ep.is_unix()) make_no_delay(fd);
     sockaddr_storage ss;
@@ -217,6 +302,16 @@ static int sockaddr2ep(const sockaddr_storage& ss, EndPoint* ep) {
         ep->ip = in->sin_addr.s_addr;
         ep->port = ntohs(in->sin_port);
         ep->path.clear();
+        return 0;
+    }
+    if (ss.ss_family == AF_INET6) {
+        const sockaddr_in6* in6 = (const sockaddr_in6*)&ss;
+        EndPoint e;
+        e.v6 = true;
+        memcpy(e.ip6, &in6->sin6_addr, 16);
+        e.scope_id = in6->sin6_scope_id;
+        e.port = ntohs(in6->sin6_port);
+        *ep = e;
         return 0;
     }
     if (ss.ss_family == AF_UNIX) {

@@ -1,10 +1,13 @@
 #include "net/ssl.h"
 
 #include <openssl/err.h>
+#include <openssl/pem.h>
 #include <openssl/ssl.h>
+#include <openssl/x509v3.h>
 
 #include <cerrno>
 #include <mutex>
+#include <unordered_map>
 
 #include "base/logging.h"
 #include "base/util.h"
@@ -48,25 +51,146 @@ static int alpn_select_cb(SSL*, const unsigned char** out, unsigned char* outlen
     return SSL_TLSEXT_ERR_NOACK;
 }
 
-std::shared_ptr<SslContext> SslContext::NewServer(const ServerSslOptions& opt, std::string* err) {
-    init_openssl_once();
-    std::shared_ptr<SslContext> c(new SslContext);
-    c->_server = true;
-    c->_ctx = SSL_CTX_new(TLS_server_method());
-    if (!c->_ctx) {
+namespace {
+
+bool is_pem_text(const std::string& s) { return s.compare(0, 10, "-----BEGIN") == 0; }
+
+// certificate chain + key into ctx, from files or PEM text
+bool load_cert(SSL_CTX* ctx, const std::string& cert, const std::string& key, std::string* err) {
+    bool ok;
+    if (is_pem_text(cert)) {
+        BIO* b = BIO_new_mem_buf(cert.data(), (int)cert.size());
+        X509* x = b ? PEM_read_bio_X509(b, nullptr, nullptr, nullptr) : nullptr;
+        ok = x && SSL_CTX_use_certificate(ctx, x) == 1;
+        if (x) X509_free(x);
+        while (ok) {  // the rest of the chain
+            X509* ca = PEM_read_bio_X509(b, nullptr, nullptr, nullptr);
+            if (!ca) {
+                ERR_clear_error();
+                break;
+            }
+            if (SSL_CTX_add_extra_chain_cert(ctx, ca) != 1) {  // takes ownership on success
+                X509_free(ca);
+                ok = false;
+            }
+        }
+        if (b) BIO_free(b);
+    } else {
+        ok = SSL_CTX_use_certificate_chain_file(ctx, cert.c_str()) == 1;
+    }
+    if (ok) {
+        if (is_pem_text(key)) {
+            BIO* b = BIO_new_mem_buf(key.data(), (int)key.size());
+            EVP_PKEY* k = b ? PEM_read_bio_PrivateKey(b, nullptr, nullptr, nullptr) : nullptr;
+            ok = k && SSL_CTX_use_PrivateKey(ctx, k) == 1;
+            if (k) EVP_PKEY_free(k);
+            if (b) BIO_free(b);
+        } else {
+            ok = SSL_CTX_use_PrivateKey_file(ctx, key.c_str(), SSL_FILETYPE_PEM) == 1;
+        }
+    }
+    ok = ok && SSL_CTX_check_private_key(ctx) == 1;
+    if (!ok) {
+        *err = "certificate/key " + (is_pem_text(cert) ? std::string("(PEM text)") : cert) + "/" +
+               (is_pem_text(key) ? std::string("(PEM text)") : key) + ": " + last_ssl_error();
+    }
+    return ok;
+}
+
+X509* read_x509(const std::string& cert) {
+    BIO* b = is_pem_text(cert) ? BIO_new_mem_buf(cert.data(), (int)cert.size()) : BIO_new_file(cert.c_str(), "r");
+    if (!b) return nullptr;
+    X509* x = PEM_read_bio_X509(b, nullptr, nullptr, nullptr);
+    BIO_free(b);
+    return x;
+}
+
+std::string lower(std::string s) {
+    for (char& c : s) c = (char)tolower((unsigned char)c);
+    return s;
+}
+
+}  // namespace
+
+bool SslContext::CertificateNames(const CertInfo& cert, std::vector<std::string>* names, std::string* err) {
+    X509* x = read_x509(cert.certificate);
+    if (!x) {
+        *err = "cannot read certificate: " + last_ssl_error();
+        return false;
+    }
+    char cn[256];
+    if (X509_NAME_get_text_by_NID(X509_get_subject_name(x), NID_commonName, cn, sizeof(cn)) > 0) {
+        names->push_back(lower(cn));
+    }
+    GENERAL_NAMES* sans = static_cast<GENERAL_NAMES*>(X509_get_ext_d2i(x, NID_subject_alt_name, nullptr, nullptr));
+    for (int i = 0; sans && i < sk_GENERAL_NAME_num(sans); ++i) {
+        const GENERAL_NAME* g = sk_GENERAL_NAME_value(sans, i);
+        if (g->type != GEN_DNS) continue;
+        const unsigned char* d = ASN1_STRING_get0_data(g->d.dNSName);
+        names->push_back(lower(std::string((const char*)d, (size_t)ASN1_STRING_length(g->d.dNSName))));
+    }
+    if (sans) GENERAL_NAMES_free(sans);
+    X509_free(x);
+    for (const std::string& f : cert.sni_filters) names->push_back(lower(f));
+    return true;
+}
+
+// hostname -> context; "*.example.com" is stored under "example.com" in
+// `wildcard` and matches exactly one more leading label
+struct SslContext::SniMap {
+    std::unordered_map<std::string, std::shared_ptr<SslContext>> exact, wildcard;
+    std::shared_ptr<SslContext> find(const std::string& host) const {
+        auto it = exact.find(host);
+        if (it != exact.end()) return it->second;
+        const size_t dot = host.find('.');
+        if (dot != std::string::npos) {
+            auto w = wildcard.find(host.substr(dot + 1));
+            if (w != wildcard.end()) return w->second;
+        }
+        return nullptr;
+    }
+};
+
+int sni_callback(SSL* ssl, int* alert, void* arg) {
+    SslContext* self = static_cast<SslContext*>(arg);
+    const char* name = SSL_get_servername(ssl, TLSEXT_NAMETYPE_host_name);
+    const bool strict = self->_opt.strict_sni;
+    if (!name || !*name) {
+        if (!strict) return SSL_TLSEXT_ERR_OK;  // the default certificate
+        *alert = SSL_AD_UNRECOGNIZED_NAME;
+        return SSL_TLSEXT_ERR_ALERT_FATAL;
+    }
+    std::shared_ptr<const SslContext::SniMap> m = std::atomic_load(&self->_sni);
+    std::shared_ptr<SslContext> c = m ? m->find(lower(name)) : nullptr;
+    if (c) {
+        // the SSL holds its own reference to the chosen SSL_CTX
+        if (c.get() != self) SSL_set_SSL_CTX(ssl, c->ctx());
+        return SSL_TLSEXT_ERR_OK;
+    }
+    if (!strict) return SSL_TLSEXT_ERR_OK;
+    *alert = SSL_AD_UNRECOGNIZED_NAME;
+    return SSL_TLSEXT_ERR_ALERT_FATAL;
+}
+
+namespace {
+
+// A server SSL_CTX with the options every certificate shares.
+SSL_CTX* new_server_ctx(const ServerSslOptions& opt, const std::string& cert, const std::string& key,
+                        std::string* err) {
+    SSL_CTX* ctx = SSL_CTX_new(TLS_server_method());
+    if (!ctx) {
         *err = last_ssl_error();
         return nullptr;
     }
-    SSL_CTX_set_min_proto_version(c->_ctx, TLS1_2_VERSION);
-    SSL_CTX_set_mode(c->_ctx, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
-    if (SSL_CTX_use_certificate_chain_file(c->_ctx, opt.cert_file.c_str()) != 1 ||
-        SSL_CTX_use_PrivateKey_file(c->_ctx, opt.key_file.c_str(), SSL_FILETYPE_PEM) != 1 ||
-        SSL_CTX_check_private_key(c->_ctx) != 1) {
-        *err = "certificate/key " + opt.cert_file + "/" + opt.key_file + ": " + last_ssl_error();
+    SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+    SSL_CTX_set_mode(ctx, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
+    if (!load_cert(ctx, cert, key, err)) {
+        SSL_CTX_free(ctx);
         return nullptr;
     }
-    if (!opt.ciphers.empty() && SSL_CTX_set_cipher_list(c->_ctx, opt.ciphers.c_str()) != 1) {
+    if (!opt.ciphers.empty() && SSL_CTX_set_cipher_list(ctx, opt.ciphers.c_str()) != 1) {
         *err = "ciphers: " + last_ssl_error();
+        SSL_CTX_free(ctx);
         return nullptr;
     }
     if (!opt.alpns.empty()) {
@@ -78,11 +202,111 @@ std::shared_ptr<SslContext> SslContext::NewServer(const ServerSslOptions& opt, s
             wire->push_back((char)p.size());
             wire->append(p);
         }
-        SSL_CTX_set_alpn_select_cb(c->_ctx, alpn_select_cb, wire.get());
+        SSL_CTX_set_alpn_select_cb(ctx, alpn_select_cb, wire.get());
         std::lock_guard<std::mutex> g(mu);
         keep.push_back(std::move(wire));
     }
+    return ctx;
+}
+
+}  // namespace
+
+std::shared_ptr<SslContext> SslContext::NewServer(const ServerSslOptions& opt, std::string* err) {
+    init_openssl_once();
+    std::shared_ptr<SslContext> c(new SslContext);
+    c->_server = true;
+    c->_opt = opt;
+    if (c->_opt.default_cert.certificate.empty()) {
+        c->_opt.default_cert.certificate = opt.cert_file;
+        c->_opt.default_cert.private_key = opt.key_file;
+    }
+    const CertInfo& dc = c->_opt.default_cert;
+    c->_ctx = new_server_ctx(opt, dc.certificate, dc.private_key, err);
+    if (!c->_ctx) return nullptr;
+    if (!CertificateNames(dc, &c->_default_names, err)) return nullptr;
+    SSL_CTX_set_tlsext_servername_callback(c->_ctx, sni_callback);
+    SSL_CTX_set_tlsext_servername_arg(c->_ctx, c.get());
+    std::lock_guard<std::mutex> g(c->_cert_mu);
+    for (const CertInfo& ci : opt.certs) {
+        std::shared_ptr<SslContext> x(new SslContext);
+        x->_server = true;
+        x->_ctx = new_server_ctx(opt, ci.certificate, ci.private_key, err);
+        if (!x->_ctx) return nullptr;
+        c->_certs.emplace_back(ci, x);
+    }
+    c->publish_locked();
     return c;
+}
+
+void SslContext::publish_locked() {
+    std::shared_ptr<SniMap> m = std::make_shared<SniMap>();
+    auto add = [&m](const std::string& name, const std::shared_ptr<SslContext>& ctx) {
+        if (name.compare(0, 2, "*.") == 0) m->wildcard.emplace(name.substr(2), ctx);
+        else if (!name.empty()) m->exact.emplace(name, ctx);
+    };
+    // later certificates win over earlier ones for the same name (emplace
+    // keeps the first: walk newest first); the default one serves its own
+    // names unless another certificate claims them
+    for (auto it = _certs.rbegin(); it != _certs.rend(); ++it) {
+        std::vector<std::string> names;
+        std::string err;
+        if (CertificateNames(it->first, &names, &err)) {
+            for (const std::string& n : names) add(n, it->second);
+        }
+    }
+    // the default context is not owned by a shared_ptr here: a non-owning
+    // alias marks "stay on the default" for the callback
+    std::shared_ptr<SslContext> self(std::shared_ptr<SslContext>(), this);
+    for (const std::string& n : _default_names) add(n, self);
+    std::atomic_store(&_sni, std::shared_ptr<const SniMap>(std::move(m)));
+}
+
+int SslContext::AddCertificate(const CertInfo& cert, std::string* err) {
+    if (!_server) return -1;
+    std::vector<std::string> names;
+    if (!CertificateNames(cert, &names, err)) return -1;
+    std::shared_ptr<SslContext> x(new SslContext);
+    x->_server = true;
+    x->_ctx = new_server_ctx(_opt, cert.certificate, cert.private_key, err);
+    if (!x->_ctx) return -1;
+    std::lock_guard<std::mutex> g(_cert_mu);
+    for (auto& e : _certs) {
+        if (e.first.certificate == cert.certificate) {  // replace (new key or filters)
+            e = {cert, x};
+            publish_locked();
+            return 0;
+        }
+    }
+    _certs.emplace_back(cert, x);
+    publish_locked();
+    return 0;
+}
+
+int SslContext::RemoveCertificate(const CertInfo& cert) {
+    std::lock_guard<std::mutex> g(_cert_mu);
+    for (size_t i = 0; i < _certs.size(); ++i) {
+        if (_certs[i].first.certificate == cert.certificate) {
+            _certs.erase(_certs.begin() + (long)i);
+            publish_locked();
+            return 0;
+        }
+    }
+    return -1;
+}
+
+int SslContext::ResetCertificates(const std::vector<CertInfo>& certs, std::string* err) {
+    std::vector<std::pair<CertInfo, std::shared_ptr<SslContext>>> fresh;
+    for (const CertInfo& ci : certs) {
+        std::shared_ptr<SslContext> x(new SslContext);
+        x->_server = true;
+        x->_ctx = new_server_ctx(_opt, ci.certificate, ci.private_key, err);
+        if (!x->_ctx) return -1;
+        fresh.emplace_back(ci, x);
+    }
+    std::lock_guard<std::mutex> g(_cert_mu);
+    _certs.swap(fresh);
+    publish_locked();
+    return 0;
 }
 
 std::shared_ptr<SslContext> SslContext::NewClient(const ChannelSslOptions& opt, std::string* err) {

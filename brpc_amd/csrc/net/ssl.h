@@ -17,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "base/buf.h"
 
@@ -26,11 +27,26 @@ typedef struct bio_st BIO;
 
 namespace mrpc {
 
+// A certificate and its key (reference: src/brpc/ssl_options.h:30-42).
+// Each is a PEM file path, or the PEM text itself ("-----BEGIN ...").
+// The certificate serves its CN and DNS subject-alt-names plus
+// sni_filters; a wildcard may only lead a name ("*.example.com").
+struct CertInfo {
+    std::string certificate;
+    std::string private_key;
+    std::vector<std::string> sni_filters;
+};
+
 struct ServerSslOptions {
-    std::string cert_file;      // PEM certificate chain
+    std::string cert_file;      // PEM certificate chain (default certificate)
     std::string key_file;       // PEM private key
+    CertInfo default_cert;      // alternative to cert_file/key_file (files or PEM text)
+    std::vector<CertInfo> certs;  // more certificates, chosen by the client's SNI name
     std::string ciphers;        // OpenSSL cipher list (empty: default)
     std::string alpns;          // comma separated, e.g. "h2,http/1.1"
+    // Refuse handshakes without an SNI name, or whose name no certificate
+    // (the default one included) serves; otherwise the default certificate
+    // answers them.
     bool strict_sni = false;
 };
 
@@ -45,6 +61,15 @@ class SslContext {
 public:
     ~SslContext();
     static std::shared_ptr<SslContext> NewServer(const ServerSslOptions& opt, std::string* err);
+    // Server contexts: certificates chosen by SNI, changeable while the
+    // server runs (handshakes in progress keep the certificate they chose).
+    // The default certificate is fixed. 0 on success.
+    int AddCertificate(const CertInfo& cert, std::string* err);
+    int RemoveCertificate(const CertInfo& cert);
+    int ResetCertificates(const std::vector<CertInfo>& certs, std::string* err);
+    // The hostnames a certificate serves (CN, DNS SANs, then sni_filters).
+    static bool CertificateNames(const CertInfo& cert, std::vector<std::string>* names, std::string* err);
+    struct SniMap;
     static std::shared_ptr<SslContext> NewClient(const ChannelSslOptions& opt, std::string* err);
     // Shared no-verification client context (Channel use_ssl).
     static std::shared_ptr<SslContext> DefaultClient();
@@ -52,8 +77,17 @@ public:
     bool is_server() const { return _server; }
 
 private:
+    friend int sni_callback(SSL*, int*, void*);
     SSL_CTX* _ctx = nullptr;
     bool _server = false;
+    // SNI: per-certificate contexts by hostname, published as one immutable
+    // map (std::atomic_load in the handshake, rebuilt under _cert_mu)
+    ServerSslOptions _opt;
+    std::mutex _cert_mu;
+    std::vector<std::pair<CertInfo, std::shared_ptr<SslContext>>> _certs;
+    std::vector<std::string> _default_names;
+    std::shared_ptr<const SniMap> _sni;
+    void publish_locked();
 };
 
 class SslSession {

@@ -327,7 +327,7 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
     EndPoint actual;
     if (!ep.is_unix()) {
         get_local_side(fd, &actual);
-        actual.ip = ep.ip;
+        if (!ep.v6) actual.ip = ep.ip;  // keep the asked address (0.0.0.0 stays)
     } else {
         actual = ep;
     }
@@ -339,6 +339,8 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
         so.key_file = _options.ssl_key_file;
         so.ciphers = _options.ssl_ciphers;
         so.alpns = _options.ssl_alpns;
+        so.certs = _options.ssl_certs;
+        so.strict_sni = _options.ssl_strict_sni;
         std::string err;
         std::shared_ptr<SslContext> ctx = SslContext::NewServer(so, &err);
         if (!ctx) {
@@ -348,6 +350,7 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
             return -1;
         }
         _am->set_ssl_ctx(ctx);  // TLS and plaintext clients share the port
+        _ssl_ctx = ctx;
     }
     if (_am && _options.use_rdma) {
         std::string err;
@@ -365,7 +368,8 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
         return -1;
     }
     if (_options.internal_port > 0) {
-        EndPoint iep(ep.ip, _options.internal_port);
+        EndPoint iep = ep;
+        iep.port = _options.internal_port;
         int ifd = tcp_listen(iep, false);
         if (ifd >= 0) {
             _internal_am = BuildAcceptor(true);
@@ -430,6 +434,34 @@ int Server::Stop(int closewait_ms) {
     if (_am) _am->StopAccept(closewait_ms);
     if (_internal_am) _internal_am->StopAccept(0);
     g_running_servers.fetch_sub(1);
+    return 0;
+}
+
+int Server::AddCertificate(const CertInfo& cert) {
+    std::string err;
+    if (!_ssl_ctx) {
+        LOG(ERROR) << "AddCertificate: the server has no default certificate";
+        return -1;
+    }
+    if (_ssl_ctx->AddCertificate(cert, &err) != 0) {
+        LOG(ERROR) << "AddCertificate: " << err;
+        return -1;
+    }
+    return 0;
+}
+
+int Server::RemoveCertificate(const CertInfo& cert) { return _ssl_ctx ? _ssl_ctx->RemoveCertificate(cert) : -1; }
+
+int Server::ResetCertificates(const std::vector<CertInfo>& certs) {
+    std::string err;
+    if (!_ssl_ctx) {
+        LOG(ERROR) << "ResetCertificates: the server has no default certificate";
+        return -1;
+    }
+    if (_ssl_ctx->ResetCertificates(certs, &err) != 0) {
+        LOG(ERROR) << "ResetCertificates: " << err;
+        return -1;
+    }
     return 0;
 }
 

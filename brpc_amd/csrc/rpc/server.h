@@ -12,6 +12,7 @@
 
 #include "base/endpoint.h"
 #include "net/acceptor.h"
+#include "net/ssl.h"
 #include "pb/service.h"
 #include "rpc/authenticator.h"
 #include "rpc/concurrency_limiter.h"
@@ -55,6 +56,11 @@ struct ServerOptions {
     std::string ssl_key_file;
     std::string ssl_ciphers;  // OpenSSL cipher list (empty: library default)
     std::string ssl_alpns;    // e.g. "h2,http/1.1"
+    // More certificates chosen by the client's SNI name, and whether a name
+    // no certificate serves (or no name) is refused (net/ssl.h CertInfo;
+    // reference: src/brpc/ssl_options.h:97-110)
+    std::vector<CertInfo> ssl_certs;
+    bool ssl_strict_sni = false;
     // Accept RDMA clients (hello detected per connection; TCP clients keep
     // working on the same port). Exclusive with TLS.
     bool use_rdma = false;
@@ -111,6 +117,12 @@ public:
     // first free port in [start,end]
     int Start(int port_start, int port_end, const ServerOptions* opt);
     int Stop(int closewait_ms);
+    // Certificates chosen by SNI, changeable while the server runs
+    // (reference: src/brpc/server.h:450-465). The server must have been
+    // started with a default certificate. 0 on success.
+    int AddCertificate(const CertInfo& cert);
+    int RemoveCertificate(const CertInfo& cert);
+    int ResetCertificates(const std::vector<CertInfo>& certs);
     int Join();
     void RunUntilAskedToQuit();
     static bool IsAskedToQuit();
@@ -154,6 +166,7 @@ private:
     EndPoint _listen_addr;
     std::unique_ptr<Acceptor> _am;
     std::unique_ptr<Acceptor> _internal_am;
+    std::shared_ptr<SslContext> _ssl_ctx;  // TLS contexts of the listening port (SNI)
     std::map<std::string, ServiceProperty> _services;           // full name
     std::map<std::string, Service*> _services_by_short_name;
     Service* _first_service = nullptr;

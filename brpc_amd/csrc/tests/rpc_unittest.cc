@@ -388,3 +388,80 @@ TEST(Rpc, domain_list_https_and_redis_naming_services) {
     EXPECT_EQ(servers[0].addr.port, 6379);
     delete redis;
 }
+
+// IPv6 endpoints (reference: butil/details/extended_endpoint.hpp:155-311):
+// parse/print round trips, ordering/hash distinctness, and a server on
+// [::1] answering baidu_std and http clients, with the remote side seen
+// as an IPv6 endpoint.
+TEST(Rpc, ipv6_endpoints_and_loopback_echo) {
+    EndPoint ep;
+    ASSERT_EQ(str2endpoint("[::1]:8000", &ep), 0);
+    EXPECT_TRUE(ep.is_ipv6());
+    EXPECT_EQ(ep.port, 8000);
+    EXPECT_EQ(ep.to_string(), "[::1]:8000");
+    ASSERT_EQ(str2endpoint("[2001:db8::a:1]:65535", &ep), 0);
+    EXPECT_EQ(ep.to_string(), "[2001:db8::a:1]:65535");
+    EXPECT_EQ(ep.ip_string(), "2001:db8::a:1");
+    EXPECT_NE(str2endpoint("::1:80", &ep), 0);      // bare v6 needs brackets
+    EXPECT_NE(str2endpoint("[::1]80", &ep), 0);
+    EXPECT_NE(str2endpoint("[::g]:80", &ep), 0);
+    EXPECT_NE(str2endpoint("[::1]:70000", &ep), 0);
+    ASSERT_EQ(str2endpoint("::", 81, &ep), 0);
+    EXPECT_EQ(ep.to_string(), "[::]:81");
+    ASSERT_EQ(str2endpoint("[::1]", 82, &ep), 0);
+    EXPECT_EQ(ep.to_string(), "[::1]:82");
+    EndPoint a, b, c;
+    ASSERT_EQ(str2endpoint("[::1]:1", &a), 0);
+    ASSERT_EQ(str2endpoint("[::2]:1", &b), 0);
+    ASSERT_EQ(str2endpoint("0.0.0.1:1", &c), 0);
+    EXPECT_TRUE(a != b && a != c && (a < b) != (b < a) && (a < c) != (c < a));
+    EXPECT_NE(EndPointHash()(a), EndPointHash()(b));
+    // IPv4 parsing is unchanged
+    ASSERT_EQ(str2endpoint("127.0.0.1:80", &ep), 0);
+    EXPECT_FALSE(ep.is_ipv6());
+    EXPECT_EQ(ep.to_string(), "127.0.0.1:80");
+
+    Server server;
+    EchoServiceImpl echo;
+    server.AddService(&echo, SERVER_DOESNT_OWN_SERVICE);
+    ServerOptions so;
+    so.has_builtin_services = false;
+    ASSERT_EQ(server.Start("[::1]:0", &so), 0);
+    ASSERT_TRUE(server.listen_address().is_ipv6());
+    const std::string addr = server.listen_address().to_string();
+    EXPECT_EQ(addr.compare(0, 5, "[::1]"), 0);
+    for (const char* proto : {"baidu_std", "http"}) {
+        Channel ch;
+        ChannelOptions opt;
+        opt.timeout_ms = 2000;
+        opt.protocol = proto;
+        ASSERT_EQ(ch.Init(addr.c_str(), &opt), 0);
+        example::EchoService_Stub stub(&ch);
+        for (int i = 0; i < 20; ++i) {
+            Controller cntl;
+            example::EchoRequest req;
+            example::EchoResponse res;
+            req.set_message("v6 " + std::to_string(i));
+            stub.Echo(&cntl, &req, &res, nullptr);
+            ASSERT_FALSE(cntl.Failed());
+            EXPECT_EQ(res.message(), "v6 " + std::to_string(i));
+            EXPECT_TRUE(cntl.remote_side().is_ipv6());
+            EXPECT_EQ(cntl.remote_side(), server.listen_address());
+        }
+    }
+    // a naming-service list of v6 servers through a load balancer
+    Channel lbch;
+    ChannelOptions lo;
+    lo.timeout_ms = 2000;
+    ASSERT_EQ(lbch.Init(("list://" + addr + "," + addr).c_str(), "rr", &lo), 0);
+    example::EchoService_Stub lstub(&lbch);
+    Controller cntl;
+    example::EchoRequest req;
+    example::EchoResponse res;
+    req.set_message("lb");
+    lstub.Echo(&cntl, &req, &res, nullptr);
+    ASSERT_FALSE(cntl.Failed());
+    EXPECT_EQ(res.message(), "lb");
+    server.Stop(0);
+    server.Join();
+}
