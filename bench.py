@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--verbose-sweep", action="store_true", help="print HBM pool / free memory after each point")
     ap.add_argument("--stream-min-s", type=float, default=1.0, help="the stream leg is timed for at least this long")
     ap.add_argument("--requests-per-step-grpc", type=int, default=2000)
+    ap.add_argument("--flag", action="append", default=[], metavar="NAME=VALUE",
+                    help="set a runtime flag before anything starts (repeatable)")
     ap.add_argument("--bodies", default="text,random",
                     help="body kinds of the 64 KiB codec legs: text (log records), random, const (one repeated byte)")
     ap.add_argument("--requests-per-step-fanout", type=int, default=500)
@@ -169,6 +171,9 @@ def main():
     if topo.world_size != a.gpus:
         print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, topo.world_size), file=sys.stderr)
     workers = a.workers or auto_workers(topo.local_world_size)
+    for f in a.flag:
+        k, _, v = f.partition("=")
+        native.set_flag(k, v)
     native.set_flag("fiber_concurrency", str(workers))
     placement = {}
     if a.cpu_l3_domain != -2:

@@ -1,5 +1,9 @@
 #include "fiber/sync.h"
 
+#include <dlfcn.h>
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <cerrno>
 #include <cstdio>
@@ -27,9 +31,17 @@ ContentionState& cstate() {
     return *s;
 }
 std::atomic<bool> g_profiling{false};
+// set while a thread records a sample: the recorder's own locks (which go
+// through the pthread_mutex_lock interposer below) are not sampled
+thread_local bool tls_in_submit = false;
 
 void submit_contention(void* caller, int64_t wait_ns) {
     ContentionState& s = cstate();
+    if (tls_in_submit) return;
+    struct Guard {
+        Guard() { tls_in_submit = true; }
+        ~Guard() { tls_in_submit = false; }
+    } in_submit;
     s.total.fetch_add(1, std::memory_order_relaxed);
     if (!g_profiling.load(std::memory_order_relaxed)) return;
     // Sample proportionally to the wait time: long waits are always kept,
@@ -94,6 +106,51 @@ std::string ContentionProfilerDump() {
 }
 
 int64_t ContentionCount() { return cstate().total.load(std::memory_order_relaxed); }
+
+// ------------------------------------------------------------ pthread mutexes
+// The contention profiler sees pthread mutexes too (std::mutex included):
+// libmrpc defines pthread_mutex_lock, which binds ahead of libc's for every
+// program linked with it (reference: src/bthread/mutex.cpp:367-423). With
+// the profiler off it forwards at once; with it on, a failed try-lock means
+// contention, and the time to acquire is sampled for the caller.
+typedef int (*PthreadMutexOp)(pthread_mutex_t*);
+static PthreadMutexOp g_sys_lock = nullptr;
+static PthreadMutexOp g_sys_trylock = nullptr;
+std::atomic<int64_t> g_pthread_contentions{0};
+
+static void resolve_pthread_mutex() {
+    if (!g_sys_lock) g_sys_lock = (PthreadMutexOp)dlsym(RTLD_NEXT, "pthread_mutex_lock");
+    if (!g_sys_trylock) g_sys_trylock = (PthreadMutexOp)dlsym(RTLD_NEXT, "pthread_mutex_trylock");
+}
+__attribute__((constructor)) static void resolve_pthread_mutex_at_load() { resolve_pthread_mutex(); }
+
+int64_t PthreadContentionCount() { return g_pthread_contentions.load(std::memory_order_relaxed); }
+
+}  // namespace fiber
+}  // namespace mrpc
+
+extern "C" int pthread_mutex_lock(pthread_mutex_t* m) {
+    using namespace mrpc::fiber;
+    if (__builtin_expect(!g_sys_lock, 0)) {
+        resolve_pthread_mutex();
+        if (!g_sys_lock) {  // dlsym not usable yet (very early): spin on try-lock
+            while (pthread_mutex_trylock(m) == EBUSY) sched_yield();
+            return 0;
+        }
+    }
+    if (!g_profiling.load(std::memory_order_relaxed) || tls_in_submit) return g_sys_lock(m);
+    if (g_sys_trylock(m) == 0) return 0;
+    const int64_t t0 = mrpc::monotonic_ns();
+    const int rc = g_sys_lock(m);
+    if (rc == 0) {
+        g_pthread_contentions.fetch_add(1, std::memory_order_relaxed);
+        submit_contention(__builtin_return_address(0), mrpc::monotonic_ns() - t0);
+    }
+    return rc;
+}
+
+namespace mrpc {
+namespace fiber {
 
 // ------------------------------------------------------------ Mutex
 Mutex::Mutex() : _b(butex_create()) { _b->store(0, std::memory_order_relaxed); }

@@ -129,6 +129,8 @@ bool IsContentionProfilerRunning();
 std::string ContentionProfilerDump();
 // Total contended waits observed (also exported as a metric).
 int64_t ContentionCount();
+// contended pthread_mutex_lock calls sampled while the profiler ran
+int64_t PthreadContentionCount();
 
 }  // namespace fiber
 }  // namespace mrpc

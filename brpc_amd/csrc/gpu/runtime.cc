@@ -21,6 +21,9 @@
 #include "gpu/kernels.h"
 #include "rdma/rdma.h"
 
+DEFINE_bool(pinned_coherent, true,
+            "allocate pinned host memory coherent (fine-grained, not cached in the GPU L2); false: non-coherent "
+            "(cached), which is only safe when kernels never re-read recycled pinned blocks");
 DEFINE_int32(gpu_streams_per_device, 4, "HIP streams per device in the pool (<= GPU_MAX_HW_QUEUES)");
 DEFINE_int32(gpu_poller_spin_us, 50, "event poller busy-polls this long after the last completion before backing off");
 DEFINE_int32(gpu_poller_sleep_us, 2, "event poller sleep between polls once the spin budget is spent");
@@ -387,7 +390,9 @@ void Free(void* p) {
 // none with coherent memory, at the same throughput.
 void* HostMallocPinned(size_t n) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, n, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+    const unsigned flags = FLAGS_pinned_coherent ? (hipHostMallocCoherent | hipHostMallocMapped)
+                                                 : (hipHostMallocNonCoherent | hipHostMallocMapped);
+    if (hipHostMalloc(&p, n, flags) != hipSuccess) return nullptr;
     return p;
 }
 

@@ -17,12 +17,19 @@
 #include "base/time.h"
 #include "base/util.h"
 #include "fiber/butex.h"
+#include "http/http_client.h"
 #include "net/event_dispatcher.h"
 #include "rpc/errno.h"
 
 DEFINE_int64(socket_max_unwritten_bytes, 64 * 1024 * 1024,
              "Max unwritten bytes in each socket; writes beyond fail with EOVERCROWDED");
 DEFINE_int32(connect_timeout_ms_default, 200, "default timeout of lazily connecting sockets");
+DEFINE_string(health_check_path, "",
+              "HTTP path of the health check call: a failed socket whose server is connectable again is only "
+              "revived once an HTTP GET of this path succeeds within -health_check_timeout_ms (empty: "
+              "connectable is healthy)");
+DEFINE_int32(health_check_timeout_ms, 500,
+             "timeout of both the health check's connect and its HTTP call to -health_check_path");
 DEFINE_int32(socket_recv_buffer_size, -1, "SO_RCVBUF of sockets if positive");
 DEFINE_int32(socket_send_buffer_size, -1, "SO_SNDBUF of sockets if positive");
 DEFINE_int32(max_connection_pool_size, 100, "max pooled connections to one endpoint");
@@ -1097,12 +1104,35 @@ int Socket::Revive(int new_fd) {
     return 0;
 }
 
+std::atomic<int64_t> g_app_health_checks{0}, g_app_health_check_failures{0};
+
+// The application-level half of the check (reference:
+// src/brpc/details/health_check.cpp:34-39,147-190): the server must answer
+// an HTTP GET of -health_check_path, not merely accept connections. It runs
+// on a connection of its own (servers here take HTTP and the RPC protocols
+// on one port, TLS or not), so the failed socket never carries user
+// traffic before the check passed.
+static bool app_health_check_ok(const EndPoint& remote) {
+    const std::string path = FLAGS_health_check_path;
+    if (path.empty()) return true;
+    g_app_health_checks.fetch_add(1, std::memory_order_relaxed);
+    std::string body;
+    const std::string url = "http://" + remote.to_string() + (path[0] == '/' ? "" : "/") + path;
+    if (HttpGet(url, &body, std::max(1, FLAGS_health_check_timeout_ms)) == 0) return true;
+    g_app_health_check_failures.fetch_add(1, std::memory_order_relaxed);
+    return false;
+}
+
 void* Socket::HealthCheckThread(void* arg) {
     Socket* s = static_cast<Socket*>(arg);
     for (;;) {
         fiber::usleep((uint64_t)std::max(1, s->_health_check_interval_s) * 1000000);
         if (s->_recycle_flag.load()) break;
-        int fd = tcp_connect(s->_remote_side, 500);
+        int fd = tcp_connect(s->_remote_side, std::max(1, FLAGS_health_check_timeout_ms));
+        if (fd >= 0 && !app_health_check_ok(s->_remote_side)) {
+            ::close(fd);  // connectable, not healthy: check again next interval
+            continue;
+        }
         if (fd >= 0) {
             s->_hc_started.store(false);
             if (s->_recycle_flag.load()) {

@@ -21,12 +21,16 @@
 #include "rpc/concurrency_limiter.h"
 #include "rpc/controller.h"
 #include "rpc/errno.h"
+#include "http/http_header.h"
+#include "rpc/health_reporter.h"
 #include "rpc/server.h"
 #include "services/echo_service.h"
 #include "tests/test.h"
 
 DECLARE_int64(socket_max_unwritten_bytes);
 DECLARE_int32(health_check_interval);
+DECLARE_string(health_check_path);
+DECLARE_int32(health_check_timeout_ms);
 DECLARE_int32(auto_cl_sample_window_size_ms);
 DECLARE_int32(auto_cl_min_sample_count);
 DECLARE_int32(auto_cl_max_sample_count);
@@ -225,6 +229,81 @@ TEST(Socket, health_check_revives_the_connection) {
     }
     EXPECT_TRUE(revived);
     FLAGS_health_check_interval = saved;
+}
+
+namespace {
+// /health answers 503 until `healthy` is set
+struct FlipReporter : public HealthReporter {
+    std::atomic<bool> healthy{false};
+    std::atomic<int> reports{0};
+    void GenerateReport(Controller* cntl, Closure* done) override {
+        ClosureGuard g(done);
+        reports.fetch_add(1);
+        if (!healthy.load()) {
+            cntl->http_response().set_status_code(503);
+            cntl->response_attachment().append("not yet\n");
+        } else {
+            cntl->response_attachment().append("OK\n");
+        }
+    }
+};
+}  // namespace
+
+// -health_check_path (reference: src/brpc/details/health_check.cpp:34-39):
+// a connectable server is not healthy until GET path succeeds, so the
+// socket stays failed (calls fail fast) while /health answers 503.
+TEST(Socket, health_check_path_gates_revive) {
+    const int saved = FLAGS_health_check_interval;
+    const std::string saved_path = FLAGS_health_check_path;
+    FLAGS_health_check_interval = 1;
+    FLAGS_health_check_path = "/health";
+    FLAGS_health_check_timeout_ms = 300;
+    EchoServiceImpl echo;
+    std::unique_ptr<Server> s(new Server);
+    s->AddService(&echo, SERVER_DOESNT_OWN_SERVICE);
+    ServerOptions so;
+    ASSERT_EQ(s->Start("127.0.0.1:0", &so), 0);
+    const int port = s->listen_port();
+    Channel ch;
+    ChannelOptions co;
+    co.timeout_ms = 500;
+    co.max_retry = 0;
+    ASSERT_EQ(ch.Init(("127.0.0.1:" + std::to_string(port)).c_str(), &co), 0);
+    example::EchoService_Stub stub(&ch);
+    auto call = [&] {
+        Controller c;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("hc");
+        stub.Echo(&c, &req, &res, nullptr);
+        return !c.Failed();
+    };
+    ASSERT_TRUE(call());
+    s->Stop(0);
+    s->Join();
+    s.reset();
+    EXPECT_FALSE(call());
+    FlipReporter reporter;
+    std::unique_ptr<Server> s2(new Server);
+    s2->AddService(&echo, SERVER_DOESNT_OWN_SERVICE);
+    ServerOptions so2;
+    so2.health_reporter = &reporter;
+    ASSERT_EQ(s2->Start(("127.0.0.1:" + std::to_string(port)).c_str(), &so2), 0);
+    // connectable but unhealthy: checked, and still not revived
+    const int64_t t0 = monotonic_us();
+    while (reporter.reports.load() < 2 && monotonic_us() - t0 < 5000000) usleep(50 * 1000);
+    EXPECT_GE(reporter.reports.load(), 2);
+    EXPECT_FALSE(call());
+    reporter.healthy.store(true);
+    bool revived = false;
+    for (int i = 0; i < 40 && !revived; ++i) {
+        usleep(100 * 1000);
+        revived = call();
+    }
+    EXPECT_TRUE(revived);
+    FLAGS_health_check_interval = saved;
+    FLAGS_health_check_path = saved_path;
+    FLAGS_health_check_timeout_ms = 500;
 }
 
 // ------------------------------------------------------------------ limiters
