@@ -38,6 +38,7 @@ def main():
                     choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps", "grpc_cpu",
                              "grpc_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu"])
     ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--body", default="text", help="echo body kind of the codec legs: text, random, const")
     ap.add_argument("--concurrency", type=int, default=50)
     ap.add_argument("--workers", type=int, default=12)
     ap.add_argument("--top", type=int, default=45)
@@ -95,6 +96,7 @@ def main():
             o.update({"protocol": "http", "connection_type": "pooled"})
             if a.leg.endswith("gpu"):
                 native.gpu.enable_json_index(dev, 16384)
+    o["body"] = a.body
     p = native.Press(o)
     p.run_for(0.5)
     p.reset_stats()

@@ -18,9 +18,33 @@ HBM_GBPS = 8000.0
 
 
 def short(name):
-    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
-    n = n.split("(")[0].strip()
-    return n.split("::")[-1][:48]
+    """Kernel name without return type, namespaces or argument list:
+    'void mrpc::gpu::(anonymous namespace)::copy_crc32c_kernel(SegBatch, ...)'
+    -> 'copy_crc32c_kernel'. Parentheses and '<>' nest, so the argument list
+    is the first '(' at depth 0 after the name (not '(anonymous namespace)')."""
+    n = name.replace("(anonymous namespace)::", "").strip()
+    if n.startswith("void "):
+        n = n[5:]
+    depth, cut = 0, len(n)
+    for i, c in enumerate(n):
+        if c == "<":
+            depth += 1
+        elif c == ">":
+            depth -= 1
+        elif c == "(" and depth == 0:
+            cut = i
+            break
+    n = n[:cut]
+    # last component at template depth 0
+    depth, start = 0, 0
+    for i, c in enumerate(n):
+        if c == "<":
+            depth += 1
+        elif c == ">":
+            depth -= 1
+        elif c == ":" and depth == 0 and i + 1 < len(n) and n[i + 1] == ":":
+            start = i + 2
+    return (n[start:] or name)[:56]
 
 
 def main():
@@ -39,6 +63,34 @@ def main():
                 print("%-48s calls=%-8s total_ms=%-10.3f avg_us=%-9.2f pct=%s" % (
                     short(r.get("Name", "")), r.get("Calls"), float(r.get("TotalDurationNs", 0)) / 1e6,
                     float(r.get("AverageNs", 0)) / 1e3, r.get("Percentage")))
+        # overlap: the union of kernel busy intervals against the sum of
+        # their durations (1.0 = kernels never overlap), and per-queue stats
+        for p in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+            iv, queues = [], collections.Counter()
+            with open(p) as f:
+                for r in csv.DictReader(f):
+                    try:
+                        iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+                    except (KeyError, ValueError):
+                        continue
+                    queues[r.get("Queue_Id", "?")] += 1
+            if not iv:
+                continue
+            iv.sort()
+            busy, cur_s, cur_e = 0, iv[0][0], iv[0][1]
+            for s0, e0 in iv[1:]:
+                if s0 > cur_e:
+                    busy += cur_e - cur_s
+                    cur_s, cur_e = s0, e0
+                else:
+                    cur_e = max(cur_e, e0)
+            busy += cur_e - cur_s
+            total = sum(e0 - s0 for s0, e0 in iv)
+            span = iv[-1][1] - iv[0][0]
+            print("## overlap (%s): %d dispatches over %.1f ms, GPU busy %.1f ms (%.0f%% of the span), "
+                  "sum of durations %.1f ms, mean concurrency when busy %.2f, queues %s" % (
+                      os.path.basename(p), len(iv), span / 1e6, busy / 1e6, 100.0 * busy / max(1, span),
+                      total / 1e6, total / max(1, busy), dict(queues)))
         cc = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
         for p in cc:
             groups = collections.defaultdict(lambda: {"n": set(), "sum": collections.Counter(), "dur": 0.0})
