@@ -32,16 +32,18 @@
 #include "var/var.h"
 
 DEFINE_int32(rccl_timeout_ms, 10000,
-             "abort the plane when a round made no progress for this long (and fail Recv waits older than this)");
+             "abort the plane when a group made no progress for this long (and fail Recv waits older than this)");
 DEFINE_string(rccl_library, "",
               "RCCL library the plane dlopens (empty: the librccl.so the process has, else ROCm's); "
               "the stub build/lib/libfake_rccl.so runs the plane on CPU hosts");
 DEFINE_int64(rccl_window_bytes, int64_t(256) << 20,
-             "receiver credit per source rank: payload bytes a peer may announce beyond what this rank consumed");
-DEFINE_int32(rccl_round_payloads, 64, "most payloads announced to one peer per round");
-DEFINE_int64(rccl_round_bytes, int64_t(64) << 20, "most payload bytes announced to one peer per round");
+             "landing credit per source rank: payload bytes a peer may send beyond what this rank consumed");
+DEFINE_int32(rccl_round_payloads, 64, "most payloads moved to one peer per pair round");
+DEFINE_int64(rccl_round_bytes, int64_t(64) << 20, "most payload bytes moved to one peer per pair round");
 DEFINE_int32(rccl_stash_ttl_ms, 30000, "received payloads nobody claims are dropped after this long");
-DEFINE_int32(rccl_idle_spin_us, 0, "an idle plane poster watches its doorbell this long before sleeping");
+DEFINE_int32(rccl_idle_spin_us, 0, "an idle plane poster watches its wake word this long before sleeping");
+DEFINE_int32(rccl_test_poster_delay_us, 0,
+             "test only: the poster sleeps this long after every group (a slow or preempted rank)");
 
 namespace mrpc {
 namespace gpu {
@@ -62,7 +64,6 @@ struct Api {
     decltype(&::ncclGetErrorString) error_string = nullptr;
     // stub only (tests/stub/fake_rccl.cc): stream stand-ins
     void* (*fake_stream_create)() = nullptr;
-    int (*fake_stream_memcpy)(void*, void*, const void*, size_t) = nullptr;
     uint64_t (*fake_stream_record)(void*) = nullptr;
     int (*fake_stream_query)(void*, uint64_t) = nullptr;
     bool fake() const { return fake_stream_create != nullptr; }
@@ -110,11 +111,9 @@ bool load_api(Api* a, std::string* err) {
 #undef MRPC_RCCL_SYM
     if (dlsym(lib, "mrpcfake_abi_version")) {
         a->fake_stream_create = reinterpret_cast<void* (*)()>(dlsym(lib, "mrpcfake_stream_create"));
-        a->fake_stream_memcpy =
-            reinterpret_cast<int (*)(void*, void*, const void*, size_t)>(dlsym(lib, "mrpcfake_stream_memcpy"));
         a->fake_stream_record = reinterpret_cast<uint64_t (*)(void*)>(dlsym(lib, "mrpcfake_stream_record"));
         a->fake_stream_query = reinterpret_cast<int (*)(void*, uint64_t)>(dlsym(lib, "mrpcfake_stream_query"));
-        if (!a->fake_stream_create || !a->fake_stream_memcpy || !a->fake_stream_record || !a->fake_stream_query) {
+        if (!a->fake_stream_create || !a->fake_stream_record || !a->fake_stream_query) {
             if (err) *err = "stub rccl library lacks its mrpcfake_stream_* functions";
             return false;
         }
@@ -123,20 +122,13 @@ bool load_api(Api* a, std::string* err) {
 }
 
 // ------------------------------------------------------------------ streams
-// The stream-ordered work of a round: header upload, the group, header
-// download, a completion marker. HIP on MI355X; the stub's executor on CPU.
+// The plane's one stream: groups, then a completion marker. A HIP stream
+// and events on MI355X; the stub's executor on CPU hosts.
 class StreamOps {
 public:
     virtual ~StreamOps() {}
-    virtual int init(int device, size_t hdr_bytes, std::string* err) = 0;
+    virtual int init(int device, std::string* err) = 0;
     virtual void* stream() = 0;
-    // header buffers: host_out -> dev_out before the group, dev_in -> host_in after
-    char* host_out = nullptr;
-    char* host_in = nullptr;
-    char* dev_out = nullptr;
-    char* dev_in = nullptr;
-    virtual int upload(size_t n) = 0;
-    virtual int download(size_t n) = 0;
     virtual int record(uint64_t* marker) = 0;
     // 1 complete, 0 pending, -1 failed
     virtual int query(uint64_t marker) = 0;
@@ -148,33 +140,16 @@ public:
 
 class HipOps : public StreamOps {
 public:
-    int init(int device, size_t hdr_bytes, std::string* err) override {
+    int init(int device, std::string* err) override {
         _device = device;
         hipSetDevice(device);
         if (hipStreamCreateWithFlags(&_stream, hipStreamNonBlocking) != hipSuccess) {
             if (err) *err = "hipStreamCreate failed";
             return -1;
         }
-        void* d = nullptr;
-        void* h = nullptr;
-        if (hipMalloc(&d, 2 * hdr_bytes) != hipSuccess || hipHostMalloc(&h, 2 * hdr_bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-            if (err) *err = "header buffers: allocation failed";
-            return -1;
-        }
-        memset(h, 0, 2 * hdr_bytes);
-        dev_out = static_cast<char*>(d);
-        dev_in = dev_out + hdr_bytes;
-        host_out = static_cast<char*>(h);
-        host_in = host_out + hdr_bytes;
         return 0;
     }
     void* stream() override { return _stream; }
-    int upload(size_t n) override {
-        return hipMemcpyAsync(dev_out, host_out, n, hipMemcpyHostToDevice, _stream) == hipSuccess ? 0 : -1;
-    }
-    int download(size_t n) override {
-        return hipMemcpyAsync(host_in, dev_in, n, hipMemcpyDeviceToHost, _stream) == hipSuccess ? 0 : -1;
-    }
     int record(uint64_t* marker) override {
         hipEvent_t ev = AcquireEvent();
         if (!ev || hipEventRecord(ev, _stream) != hipSuccess) {
@@ -205,22 +180,15 @@ void free_host(void* p, void*) { free(p); }
 class StubOps : public StreamOps {
 public:
     explicit StubOps(const Api& a) : _api(a) {}
-    int init(int, size_t hdr_bytes, std::string* err) override {
+    int init(int, std::string* err) override {
         _stream = _api.fake_stream_create();
-        char* b = static_cast<char*>(calloc(4, hdr_bytes));
-        if (!_stream || !b) {
+        if (!_stream) {
             if (err) *err = "stub stream creation failed";
             return -1;
         }
-        host_out = b;
-        host_in = b + hdr_bytes;
-        dev_out = b + 2 * hdr_bytes;
-        dev_in = b + 3 * hdr_bytes;
         return 0;
     }
     void* stream() override { return _stream; }
-    int upload(size_t n) override { return _api.fake_stream_memcpy(_stream, dev_out, host_out, n); }
-    int download(size_t n) override { return _api.fake_stream_memcpy(_stream, host_in, dev_in, n); }
     int record(uint64_t* marker) override {
         *marker = _api.fake_stream_record(_stream);
         return 0;
@@ -241,40 +209,56 @@ private:
     void* _stream = nullptr;
 };
 
-// ------------------------------------------------------------------ wire
-const uint64_t kHdrMagic = 0x4d5250435244484full;  // "MRPCRDHO"
-const size_t kHdrBytes = 4096;
-const uint32_t kBusy = 1;
+// ------------------------------------------------------------------ node shm
+// Everything the ranks of a node tell each other goes through one POSIX shm
+// segment, never through RCCL: per unordered pair of ranks a round word and
+// the two sides' payload lists, landing credit and cancel rings; per rank a
+// futex wake word; the node's abort flag.
+const int kMaxRanks = 16;  // ranks of one node's plane
+const int kListMax = 64;   // payloads one side moves in one pair round
+const int kCancelRing = 64;
 
-struct HdrEntry {
+struct Entry {
     uint64_t seq;
     uint64_t len;
 };
-struct Hdr {
-    uint64_t magic;
-    uint64_t round;
-    uint64_t credit;   // cumulative bytes the receiver (sender of this header) accepts from us
+struct PairList {
     uint32_t n;
-    uint32_t flags;
-    uint64_t from;
-    uint64_t reserved[3];
-    HdrEntry e[(kHdrBytes - 64) / sizeof(HdrEntry)];
+    uint32_t pad;
+    Entry e[kListMax];
 };
-static_assert(sizeof(Hdr) == kHdrBytes, "round header must be fixed-size");
-const int kMaxEntries = (int)((kHdrBytes - 64) / sizeof(HdrEntry));
+struct CancelRing {  // single producer (the sender), single consumer (the receiver)
+    std::atomic<uint64_t> head;
+    std::atomic<uint64_t> tail;
+    uint64_t seq[kCancelRing];
+};
+// A pair's rounds: word = round << 2 | ready(low rank) | ready(high rank) << 1.
+// A side publishes its list for the open round, then sets its ready bit; the
+// side that finds the other bit already set fires the round by moving the
+// word to (round + 1, no bits). Both sides then issue that round's sends and
+// receives. A side clears its bit (withdraws) with a CAS; a failed CAS means
+// the peer fired meanwhile and the round must be issued.
+struct alignas(64) PairSlot {
+    std::atomic<uint64_t> word;
+    char pad0[56];
+    std::atomic<uint64_t> consumed[2];  // [direction]: bytes the receiver consumed (0: low -> high)
+    std::atomic<uint32_t> stalled[2];   // [direction]: the sender waits for credit
+    char pad1[40];
+    PairList list[2][2];                // [round % 2][side]
+    CancelRing cancels[2];              // [direction]: sequences the receiver must drop
+};
+const int kMaxPairs = kMaxRanks * (kMaxRanks - 1) / 2;
 
-// The node's doorbell: POSIX shm shared by the ranks of the plane (a
-// private allocation for a one-rank plane).
-const uint64_t kBellMagic = 0x4d52504342454c4cull;  // "MRPCBELL"
-const int kMaxRanks = 64;
+const uint64_t kBellMagic = 0x4d52504342454c32ull;  // "MRPCBEL2"
 struct Doorbell {
     uint64_t magic;
-    std::atomic<uint64_t> want_round;
-    std::atomic<uint32_t> seq;     // futex word: bumped on every ring / abort
+    std::atomic<uint32_t> seq;     // bumped on abort (futex word of no one in particular)
     std::atomic<uint32_t> claim;   // the first aborting rank claims the reason slot
     std::atomic<uint32_t> abort;   // 0, or 1 + the rank that aborted first
     char reason[200];
     std::atomic<int32_t> pid[kMaxRanks];
+    std::atomic<uint32_t> wake[kMaxRanks];  // futex word per rank: bumped by whoever has news for it
+    PairSlot pairs[kMaxPairs];
 };
 
 long futex(std::atomic<uint32_t>* w, int op, uint32_t val, const timespec* ts) {
@@ -285,6 +269,11 @@ uint64_t fnv1a(const std::string& s) {
     uint64_t h = 1469598103934665603ull;
     for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
     return h | 1;  // never 0: 0 means "no plane" in the hello
+}
+
+int pair_index(int a, int b) {
+    if (a > b) std::swap(a, b);
+    return a * (2 * kMaxRanks - a - 1) / 2 + (b - a - 1);
 }
 
 // ------------------------------------------------------------------ state
@@ -315,23 +304,19 @@ struct Stashed {
 typedef std::pair<int, uint64_t> Key;  // (source rank, sequence)
 
 struct PeerState {
-    std::deque<Payload> queued;       // not announced yet
-    std::vector<Payload> announced;   // announced in the last header: move next round
-    std::vector<Payload> incoming;    // from the peer's last header: receive next round
+    std::deque<Payload> queued;        // not listed yet
+    std::vector<Payload> listed;       // in our list of the pair's open round
     uint64_t next_seq = 0;
-    uint64_t announced_bytes = 0;     // cumulative, to this peer
-    uint64_t credit = 0;              // cumulative, granted by this peer
-    uint64_t consumed = 0;            // cumulative, from this peer (claimed/dropped)
-    std::vector<uint64_t> cancels;    // announced to this peer, then cancelled: tell it to drop them
+    uint64_t announced_bytes = 0;      // cumulative bytes listed to this peer (credit)
+    uint64_t consumed = 0;             // cumulative bytes from this peer claimed/dropped
+    uint64_t round = 0;                // the pair's open round, as this side knows it
+    bool ready = false;                // our ready bit is set for `round`
+    std::vector<uint64_t> cancels;     // moved (or listed) to this peer, then cancelled
 };
-
-// A header entry with this length cancels an earlier announcement of its
-// sequence (the receiver drops the payload instead of stashing it).
-const uint64_t kCancelLen = ~0ull;
 
 std::atomic<int64_t> g_sent{0}, g_sent_bytes{0}, g_recv{0}, g_recv_bytes{0}, g_discarded{0}, g_rounds{0},
     g_payload_rounds{0}, g_aborts{0}, g_credit_stalls{0}, g_expired{0}, g_recv_timeouts{0}, g_doorbells{0},
-    g_withdrawn{0};
+    g_withdrawn{0}, g_pair_rounds{0}, g_withdrawals{0}, g_group_us{0};
 
 void finish_locked(Waiter* w, bool ok) {
     if (!ok) w->failed = true;
@@ -361,18 +346,27 @@ public:
     std::map<Key, int64_t> lost;   // self payloads that found no memory to land in: their Recv fails
     uint64_t self_moved = 0;       // cumulative self bytes landed (credit: vs peers[rank].consumed)
     bool idle = false, dead = false, stop = false;
-    bool busy_next = false;        // some rank's round header asked for another round
-    uint64_t completed_round = 0;  // poster only (read under mu by Send)
     std::atomic<bool> dead_flag{false};
     std::thread poster;
     int64_t last_expire_us = 0, last_liveness_us = 0;
 
-    // the round in flight (poster only)
+    // the group in flight (poster only)
     std::vector<std::vector<Payload>> moving_send, moving_recv;
     std::vector<Payload> self_send, self_recv;
     uint64_t marker = 0;
     bool marker_live = false;
     std::vector<Buf> graveyard;  // blocks RCCL may still touch after an abort
+
+    // ---------------------------------------------------------------- shm
+    PairSlot* slot(int peer) const { return &bell->pairs[pair_index(rank, peer)]; }
+    int side_with(int peer) const { return rank < peer ? 0 : 1; }
+    // direction index of payloads from `src` to `dst`
+    static int dir(int src, int dst) { return src < dst ? 0 : 1; }
+
+    void ring(int r) {
+        bell->wake[r].fetch_add(1, std::memory_order_acq_rel);
+        futex(&bell->wake[r], FUTEX_WAKE, INT_MAX, nullptr);
+    }
 
     // ---------------------------------------------------------------- API
     int64_t send(int peer, const void* p, size_t len, Buf&& hold) {
@@ -386,18 +380,12 @@ public:
         const int64_t seq = (int64_t)pl.seq;
         if (peer == rank) self_q.push_back(std::move(pl));
         else peers[peer].queued.push_back(std::move(pl));
-        if (idle) ring_locked();
-        return seq;
-    }
-
-    void ring_locked() {
-        uint64_t want = completed_round + 1, cur = bell->want_round.load();
-        while (cur < want && !bell->want_round.compare_exchange_weak(cur, want)) {
+        if (idle) {
+            idle = false;
+            g_doorbells.fetch_add(1, std::memory_order_relaxed);
+            ring(rank);
         }
-        bell->seq.fetch_add(1);
-        futex(&bell->seq, FUTEX_WAKE, INT_MAX, nullptr);
-        idle = false;
-        g_doorbells.fetch_add(1, std::memory_order_relaxed);
+        return seq;
     }
 
     int recv(int n, const int* src, const uint64_t* seq, const size_t* len, Buf* outs) {
@@ -481,7 +469,17 @@ public:
         return ts;
     }
 
-    void consume_locked(int src, size_t len) { peers[src].consumed += len; }
+    // (mu held) bytes from `src` were claimed or dropped: return the credit,
+    // and wake the sender if it waits for it
+    void consume_locked(int src, size_t len) {
+        PeerState& ps = peers[src];
+        ps.consumed += len;
+        if (src == rank) return;
+        PairSlot* s = slot(src);
+        const int d = dir(src, rank);
+        s->consumed[d].store(ps.consumed, std::memory_order_release);
+        if (s->stalled[d].load(std::memory_order_acquire) && s->stalled[d].exchange(0)) ring(src);
+    }
 
     void discard(int src, uint64_t seq, size_t len) {
         (void)len;
@@ -518,67 +516,308 @@ public:
                 return;
             }
         }
-        // already announced. To ourselves: drop it here (now or when it
-        // lands). To a peer: the next round header tells it to.
+        // listed or already moved. To ourselves: drop it here (now or when
+        // it lands). To a peer: its cancel ring tells it to.
         if (peer == rank) {
             Buf dropped;
             discard_locked(rank, seq, &dropped);
             drop.append(std::move(dropped));
         } else {
             peers[peer].cancels.push_back(seq);
+            if (idle) ring(rank);
         }
         g_withdrawn.fetch_add(1, std::memory_order_relaxed);
     }
 
     // ---------------------------------------------------------------- poster
+    // One pass: issue nothing that a peer is not also about to issue. A pair
+    // round fires only when both sides are ready for it, and every fired
+    // round this rank takes part in goes into ONE group, the only group the
+    // plane has in flight. A group therefore waits only for peers that
+    // already committed to the matching group, never for a rank that is
+    // busy elsewhere or slow: pairs with traffic move independently, idle
+    // pairs exchange nothing.
     void run() {
         if (!ops->host_memory()) hipSetDevice(device);
         for (;;) {
+            std::vector<int> fired;
+            bool leave = false;
             {
                 std::unique_lock<std::mutex> lk(mu);
                 for (;;) {
-                    if (stop || dead) break;
-                    if (bell->abort.load(std::memory_order_acquire)) break;
-                    const bool local = !self_q.empty() || any_queued_locked();
-                    const uint64_t want = bell->want_round.load(std::memory_order_acquire);
-                    if (busy_next || want > completed_round) break;
-                    if (local) {
-                        ring_locked();  // the other ranks learn about round k+1 from the doorbell
+                    if (dead || bell->abort.load(std::memory_order_acquire)) break;
+                    const uint32_t s = bell->wake[rank].load(std::memory_order_acquire);
+                    drain_cancels_locked();
+                    // a leaving rank offers nothing new, but still issues
+                    // rounds a peer fired with it (else that peer's group
+                    // never completes)
+                    offer_locked(&fired, /*offer_new=*/!stop);
+                    if (stop) {
+                        withdraw_all_locked(&fired);
+                        leave = fired.empty();
                         break;
                     }
+                    if (!fired.empty() || self_ready_locked()) break;
                     idle = true;
-                    const uint32_t s = bell->seq.load(std::memory_order_acquire);
                     housekeeping_locked();
                     lk.unlock();
-                    // watch the doorbell a little while before sleeping: the
+                    // watch the wake word a little while before sleeping: the
                     // next payload of a busy stream is usually close behind
                     const int64_t until = monotonic_us() + std::max(0, FLAGS_rccl_idle_spin_us);
-                    while (bell->seq.load(std::memory_order_acquire) == s && monotonic_us() < until) {
+                    while (bell->wake[rank].load(std::memory_order_acquire) == s && monotonic_us() < until) {
                         for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
                     }
                     timespec ts{0, 50 * 1000 * 1000};
-                    futex(&bell->seq, FUTEX_WAIT, s, &ts);
+                    futex(&bell->wake[rank], FUTEX_WAIT, s, &ts);
                     lk.lock();
+                    idle = false;
                     if (check_liveness()) break;
                 }
                 idle = false;
-                if (stop) break;
+                if (!leave && !dead && !bell->abort.load(std::memory_order_acquire)) {
+                    withdraw_all_locked(&fired);
+                    build_group_locked(fired, /*with_self=*/!stop);
+                }
             }
+            if (leave) break;
             if (bell->abort.load(std::memory_order_acquire)) {
                 abort(remote_reason(), false, !remote_is_shutdown());
                 break;
             }
             if (dead) break;
-            if (run_round(completed_round + 1) != 0) break;
+            if (run_group() != 0) break;
+            if (!stop && FLAGS_rccl_test_poster_delay_us > 0) usleep((useconds_t)FLAGS_rccl_test_poster_delay_us);
         }
         if (!dead) abort("rank shut down", true, /*is_error=*/false);
     }
 
-    bool any_queued_locked() const {
-        for (const PeerState& p : peers)
-            if (!p.queued.empty()) return true;
-        return false;
+    // (mu held) peers' cancel rings: drop what they gave up
+    void drain_cancels_locked() {
+        for (int p = 0; p < world; ++p) {
+            if (p == rank) continue;
+            CancelRing& r = slot(p)->cancels[dir(p, rank)];
+            uint64_t t = r.tail.load(std::memory_order_relaxed);
+            const uint64_t h = r.head.load(std::memory_order_acquire);
+            if (t == h) continue;
+            Buf drop;
+            for (; t < h; ++t) discard_locked(p, r.seq[t % kCancelRing], &drop);
+            r.tail.store(t, std::memory_order_release);
+        }
     }
+
+    // (mu held) our cancels of payloads listed/moved to `p`, into its ring
+    void publish_cancels_locked(int p) {
+        PeerState& ps = peers[p];
+        if (ps.cancels.empty()) return;
+        CancelRing& r = slot(p)->cancels[dir(rank, p)];
+        uint64_t h = r.head.load(std::memory_order_relaxed);
+        const uint64_t t = r.tail.load(std::memory_order_acquire);
+        size_t i = 0;
+        for (; i < ps.cancels.size() && h - t < (uint64_t)kCancelRing; ++i, ++h) r.seq[h % kCancelRing] = ps.cancels[i];
+        r.head.store(h, std::memory_order_release);
+        // a full ring drops the rest: the receiver's stash expires those
+        ps.cancels.clear();
+        ring(p);
+    }
+
+    // (mu held) whether payload `len` fits the landing credit `p` granted
+    bool fits_credit_locked(int p, size_t len) {
+        PeerState& ps = peers[p];
+        PairSlot* s = slot(p);
+        const uint64_t window = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
+        const uint64_t consumed = s->consumed[dir(rank, p)].load(std::memory_order_acquire);
+        // within credit, or the peer consumed everything we sent (a payload
+        // larger than the window then goes alone)
+        return ps.announced_bytes + len <= consumed + window || ps.announced_bytes <= consumed;
+    }
+
+    // (mu held) publish our list for the pair's open round: queued payloads
+    // within credit and the per-round bounds
+    void write_list_locked(int p, bool* stalled) {
+        PeerState& ps = peers[p];
+        PairList& l = slot(p)->list[ps.round % 2][side_with(p)];
+        uint32_t n = 0;
+        uint64_t bytes = 0;
+        const int max_n = std::max(1, std::min(FLAGS_rccl_round_payloads, kListMax));
+        while (!ps.queued.empty() && (int)n < max_n) {
+            const Payload& q = ps.queued.front();
+            if (n > 0 && bytes + q.len > (uint64_t)FLAGS_rccl_round_bytes) break;
+            if (!fits_credit_locked(p, q.len)) {
+                // ask for a wake-up when credit returns, then look once more
+                // (the receiver may have consumed in between)
+                PairSlot* s = slot(p);
+                s->stalled[dir(rank, p)].store(1, std::memory_order_release);
+                if (!fits_credit_locked(p, q.len)) {
+                    *stalled = true;
+                    break;
+                }
+            }
+            l.e[n].seq = q.seq;
+            l.e[n].len = q.len;
+            ++n;
+            bytes += q.len;
+            ps.announced_bytes += q.len;
+            ps.listed.push_back(std::move(ps.queued.front()));
+            ps.queued.pop_front();
+        }
+        l.n = n;
+    }
+
+    // (mu held) the listed payloads go back to the front of the queue
+    void unlist_locked(int p) {
+        PeerState& ps = peers[p];
+        for (auto it = ps.listed.rbegin(); it != ps.listed.rend(); ++it) {
+            ps.announced_bytes -= it->len;
+            ps.queued.push_front(std::move(*it));
+        }
+        ps.listed.clear();
+    }
+
+    // (mu held) every pair: notice fired rounds we were ready for, fire the
+    // ones whose peer is ready, offer the ones with payloads within credit
+    void offer_locked(std::vector<int>* fired, bool offer_new) {
+        bool stalled = false;
+        for (int p = 0; p < world; ++p) {
+            if (p == rank) continue;
+            PeerState& ps = peers[p];
+            PairSlot* s = slot(p);
+            const uint64_t mine = 1ull << side_with(p), other = 1ull << (1 - side_with(p));
+            if (offer_new) publish_cancels_locked(p);
+            uint64_t w = s->word.load(std::memory_order_acquire);
+            if (ps.ready) {
+                if ((w >> 2) != ps.round) fired->push_back(p);  // the peer fired it
+                continue;
+            }
+            if (!offer_new) continue;
+            const bool peer_ready = (w & other) != 0;
+            bool have = !ps.queued.empty() && (fits_credit_locked(p, ps.queued.front().len) || [&] {
+                            s->stalled[dir(rank, p)].store(1, std::memory_order_release);
+                            if (fits_credit_locked(p, ps.queued.front().len)) return true;
+                            stalled = true;
+                            return false;
+                        }());
+            if (!peer_ready && !have) continue;
+            write_list_locked(p, &stalled);
+            for (;;) {
+                if (w & other) {
+                    // both ready: fire (the round moves on, both bits clear)
+                    if (s->word.compare_exchange_weak(w, (ps.round + 1) << 2, std::memory_order_acq_rel)) {
+                        ps.ready = true;
+                        fired->push_back(p);
+                        ring(p);
+                        break;
+                    }
+                } else if (!have) {
+                    break;  // the peer withdrew and we have nothing for it
+                } else if (s->word.compare_exchange_weak(w, w | mine, std::memory_order_acq_rel)) {
+                    ps.ready = true;
+                    ring(p);  // it may be asleep with payloads for us, or none
+                    break;
+                }
+            }
+        }
+        if (stalled) g_credit_stalls.fetch_add(1, std::memory_order_relaxed);
+    }
+
+    // (mu held) clear our ready bit everywhere nothing fired; a failed clear
+    // means the peer fired the round meanwhile, so it joins the group
+    void withdraw_all_locked(std::vector<int>* fired) {
+        for (int p = 0; p < world; ++p) {
+            if (p == rank) continue;
+            PeerState& ps = peers[p];
+            if (!ps.ready || std::find(fired->begin(), fired->end(), p) != fired->end()) continue;
+            PairSlot* s = slot(p);
+            const uint64_t mine = 1ull << side_with(p);
+            uint64_t w = s->word.load(std::memory_order_acquire);
+            for (;;) {
+                if ((w >> 2) != ps.round) {
+                    fired->push_back(p);
+                    break;
+                }
+                if (s->word.compare_exchange_weak(w, w & ~mine, std::memory_order_acq_rel)) {
+                    ps.ready = false;
+                    unlist_locked(p);
+                    g_withdrawals.fetch_add(1, std::memory_order_relaxed);
+                    break;
+                }
+            }
+        }
+    }
+
+    // (mu held) self payloads that may land now (the same window a peer
+    // grants: landed-but-unclaimed self bytes stay under -rccl_window_bytes)
+    bool self_ready_locked() {
+        if (self_q.empty()) return false;
+        const uint64_t window = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
+        const uint64_t unclaimed = self_moved - peers[rank].consumed;
+        return unclaimed == 0 || unclaimed + self_q.front().len <= window;
+    }
+
+    // (mu held) the group: for every fired pair, our listed payloads out and
+    // the peer's listed payloads in; then self payloads
+    void build_group_locked(const std::vector<int>& fired, bool with_self) {
+        moving_send.assign(world, {});
+        moving_recv.assign(world, {});
+        self_send.clear();
+        self_recv.clear();
+        for (int p : fired) {
+            PeerState& ps = peers[p];
+            PairSlot* s = slot(p);
+            const PairList& theirs = s->list[ps.round % 2][1 - side_with(p)];
+            moving_send[p].swap(ps.listed);
+            const uint32_t n = std::min<uint32_t>(theirs.n, kListMax);
+            for (uint32_t i = 0; i < n; ++i) {
+                Payload in;
+                in.seq = theirs.e[i].seq;
+                in.len = (size_t)theirs.e[i].len;
+                in.ptr = in.len ? ops->alloc(in.len, &in.hold) : nullptr;
+                if (in.len && !in.ptr) {
+                    // the landing memory the credit promised is not there:
+                    // the peer's group would wait forever, so fail loudly
+                    dead_reason = "no memory to land a " + std::to_string(in.len) + " B payload from rank " +
+                                  std::to_string(p);
+                    break;
+                }
+                moving_recv[p].push_back(std::move(in));
+            }
+            ps.round += 1;
+            ps.ready = false;
+            g_pair_rounds.fetch_add(1, std::memory_order_relaxed);
+        }
+        uint64_t self_bytes = 0;
+        const int self_max = std::max(1, std::min(FLAGS_rccl_round_payloads, 256));
+        for (int i = 0; with_self && i < self_max && self_ready_locked(); ++i) {
+            const uint64_t len = self_q.front().len;
+            if (i > 0 && self_bytes + len > (uint64_t)FLAGS_rccl_round_bytes) break;
+            self_bytes += len;
+            Payload sp = std::move(self_q.front());
+            self_q.pop_front();
+            Payload r;
+            r.seq = sp.seq;
+            r.len = sp.len;
+            r.ptr = ops->alloc(sp.len, &r.hold);
+            if (!r.ptr) {
+                // no memory to land it: the payload is lost (its Recv
+                // fails at once) rather than retried every group
+                const Key k(rank, sp.seq);
+                auto w = waiting.find(k);
+                if (w != waiting.end()) {
+                    Waiter* wt = w->second.w;
+                    waiting.erase(w);
+                    finish_locked(wt, false);
+                } else {
+                    lost[k] = monotonic_us();
+                }
+                g_withdrawn.fetch_add(1, std::memory_order_relaxed);
+                self_bytes -= len;
+                continue;
+            }
+            self_moved += len;
+            self_send.push_back(std::move(sp));
+            self_recv.push_back(std::move(r));
+        }
+    }
+    std::string dead_reason;
 
     bool remote_is_shutdown() const { return strcmp(bell->reason, "rank shut down") == 0; }
 
@@ -636,157 +875,56 @@ public:
             bell->abort.store((uint32_t)rank + 1, std::memory_order_release);
         }
         bell->seq.fetch_add(1);
-        futex(&bell->seq, FUTEX_WAKE, INT_MAX, nullptr);
+        for (int r = 0; r < world && r < kMaxRanks; ++r) ring(r);
     }
 
-    // Build, issue and complete round k. 0 on success; -1 after an abort.
-    int run_round(uint64_t k) {
-        bool my_busy = false, stalled = false;
-        {
-            std::lock_guard<std::mutex> g(mu);
-            moving_send.assign(world, {});
-            moving_recv.assign(world, {});
-            for (int p = 0; p < world; ++p) {
-                if (p == rank) continue;
-                PeerState& ps = peers[p];
-                Hdr* h = reinterpret_cast<Hdr*>(ops->host_out + (size_t)p * kHdrBytes);
-                h->magic = kHdrMagic;
-                h->round = k;
-                h->credit = ps.consumed + (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
-                h->from = (uint64_t)rank;
-                h->n = 0;
-                moving_send[p].swap(ps.announced);
-                moving_recv[p].swap(ps.incoming);
-                uint64_t round_bytes = 0;
-                const int max_n = std::max(1, std::min(FLAGS_rccl_round_payloads, kMaxEntries));
-                while (!ps.queued.empty() && (int)h->n < max_n) {
-                    const Payload& q = ps.queued.front();
-                    if (h->n > 0 && round_bytes + q.len > (uint64_t)FLAGS_rccl_round_bytes) break;
-                    // within credit, or the peer consumed everything we announced
-                    const uint64_t granted = ps.credit;
-                    const uint64_t window = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
-                    const bool drained = granted >= window && ps.announced_bytes <= granted - window;
-                    if (ps.announced_bytes + q.len > granted && !drained) {
-                        stalled = true;
-                        break;
-                    }
-                    h->e[h->n].seq = q.seq;
-                    h->e[h->n].len = q.len;
-                    ++h->n;
-                    round_bytes += q.len;
-                    ps.announced_bytes += q.len;
-                    ps.announced.push_back(std::move(ps.queued.front()));
-                    ps.queued.pop_front();
-                }
-                // cancellations of earlier announcements ride in the same entries
-                size_t nc = 0;
-                while (nc < ps.cancels.size() && (int)h->n < kMaxEntries) {
-                    h->e[h->n].seq = ps.cancels[nc++];
-                    h->e[h->n].len = kCancelLen;
-                    ++h->n;
-                }
-                ps.cancels.erase(ps.cancels.begin(), ps.cancels.begin() + (long)nc);
-                my_busy |= !ps.announced.empty() || !ps.queued.empty() || !ps.cancels.empty();
-            }
-            self_send.clear();
-            self_recv.clear();
-            // self pairs: no credit (the stash is ours) but the same per-round
-            // byte bound as a peer's announcements, so a burst of large
-            // payloads does not land all at once
-            uint64_t self_bytes = 0;
-            const int self_max = std::max(1, std::min(FLAGS_rccl_round_payloads, 256));
-            const uint64_t window = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
-            for (int i = 0; i < self_max && !self_q.empty(); ++i) {
-                const uint64_t len = self_q.front().len;
-                if (i > 0 && self_bytes + len > (uint64_t)FLAGS_rccl_round_bytes) break;
-                // the same window a peer grants: landed-but-unclaimed self
-                // bytes stay under -rccl_window_bytes
-                const uint64_t unclaimed = self_moved - peers[rank].consumed;
-                if (unclaimed > 0 && unclaimed + len > window) {
-                    stalled = true;
-                    break;
-                }
-                self_bytes += len;
-                Payload s = std::move(self_q.front());
-                self_q.pop_front();
-                Payload r;
-                r.seq = s.seq;
-                r.len = s.len;
-                r.ptr = ops->alloc(s.len, &r.hold);
-                if (!r.ptr) {
-                    // no memory to land it: the payload is lost (its Recv
-                    // fails at once) rather than retried every round
-                    const Key k(rank, s.seq);
-                    auto w = waiting.find(k);
-                    if (w != waiting.end()) {
-                        Waiter* wt = w->second.w;
-                        waiting.erase(w);
-                        finish_locked(wt, false);
-                    } else {
-                        lost[k] = monotonic_us();
-                    }
-                    g_withdrawn.fetch_add(1, std::memory_order_relaxed);
-                    self_bytes -= len;
-                    continue;
-                }
-                self_moved += len;
-                self_send.push_back(std::move(s));
-                self_recv.push_back(std::move(r));
-            }
-            my_busy |= !self_q.empty();
-            for (int p = 0; p < world; ++p) {
-                if (p == rank) continue;
-                reinterpret_cast<Hdr*>(ops->host_out + (size_t)p * kHdrBytes)->flags = my_busy ? kBusy : 0;
-            }
+    // Issue the group built under the lock and wait for it. 0 on success;
+    // -1 after an abort.
+    int run_group() {
+        if (!dead_reason.empty()) {
+            const std::string why = dead_reason;
+            dead_reason.clear();
+            abort(why, true);
+            return -1;
         }
-        if (stalled) g_credit_stalls.fetch_add(1, std::memory_order_relaxed);
         bool payloads = !self_send.empty();
         for (int p = 0; p < world; ++p) payloads |= !moving_send[p].empty() || !moving_recv[p].empty();
-
-        // issue: headers up, one group, headers down, one marker
+        if (!payloads) return 0;  // fired rounds with nothing to move (both lists empty)
         void* st = ops->stream();
-        const size_t hdr_total = (size_t)world * kHdrBytes;
-        int rc = world > 1 ? ops->upload(hdr_total) : 0;
-        ncclResult_t r = ncclSuccess;
-        if (rc == 0) {
-            r = api.group_start();
-            for (int p = 0; p < world && r == ncclSuccess; ++p) {
-                if (p == rank) continue;
-                r = api.send(ops->dev_out + (size_t)p * kHdrBytes, kHdrBytes, ncclUint8, p, comm, (hipStream_t)st);
-                if (r == ncclSuccess)
-                    r = api.recv(ops->dev_in + (size_t)p * kHdrBytes, kHdrBytes, ncclUint8, p, comm, (hipStream_t)st);
-                for (size_t i = 0; i < moving_send[p].size() && r == ncclSuccess; ++i)
-                    r = api.send(moving_send[p][i].ptr, moving_send[p][i].len, ncclUint8, p, comm, (hipStream_t)st);
-                for (size_t i = 0; i < moving_recv[p].size() && r == ncclSuccess; ++i)
-                    r = api.recv(moving_recv[p][i].ptr, moving_recv[p][i].len, ncclUint8, p, comm, (hipStream_t)st);
-            }
-            for (size_t i = 0; i < self_send.size() && r == ncclSuccess; ++i) {
-                r = api.send(self_send[i].ptr, self_send[i].len, ncclUint8, rank, comm, (hipStream_t)st);
-                if (r == ncclSuccess)
-                    r = api.recv(self_recv[i].ptr, self_recv[i].len, ncclUint8, rank, comm, (hipStream_t)st);
-            }
-            const ncclResult_t e = api.group_end();
-            if (r == ncclSuccess) r = e;
-            if (r == ncclSuccess && world > 1) rc = ops->download(hdr_total);
-            if (r == ncclSuccess && rc == 0) rc = ops->record(&marker);
-            marker_live = r == ncclSuccess && rc == 0;
+        const int64_t t0 = monotonic_us();
+        int rc = 0;
+        ncclResult_t r = api.group_start();
+        for (int p = 0; p < world && r == ncclSuccess; ++p) {
+            if (p == rank) continue;
+            for (size_t i = 0; i < moving_send[p].size() && r == ncclSuccess; ++i)
+                r = api.send(moving_send[p][i].ptr, moving_send[p][i].len, ncclUint8, p, comm, (hipStream_t)st);
+            for (size_t i = 0; i < moving_recv[p].size() && r == ncclSuccess; ++i)
+                r = api.recv(moving_recv[p][i].ptr, moving_recv[p][i].len, ncclUint8, p, comm, (hipStream_t)st);
         }
+        for (size_t i = 0; i < self_send.size() && r == ncclSuccess; ++i) {
+            r = api.send(self_send[i].ptr, self_send[i].len, ncclUint8, rank, comm, (hipStream_t)st);
+            if (r == ncclSuccess)
+                r = api.recv(self_recv[i].ptr, self_recv[i].len, ncclUint8, rank, comm, (hipStream_t)st);
+        }
+        const ncclResult_t e = api.group_end();
+        if (r == ncclSuccess) r = e;
+        if (r == ncclSuccess) rc = ops->record(&marker);
+        marker_live = r == ncclSuccess && rc == 0;
         g_rounds.fetch_add(1, std::memory_order_relaxed);
-        if (payloads) g_payload_rounds.fetch_add(1, std::memory_order_relaxed);
+        g_payload_rounds.fetch_add(1, std::memory_order_relaxed);
         if (r != ncclSuccess || rc != 0) {
-            abort(r != ncclSuccess ? std::string("round issue: ") + api.error_string(r) : "round issue: stream op failed",
+            abort(r != ncclSuccess ? std::string("group issue: ") + api.error_string(r) : "group issue: stream op failed",
                   true);
             return -1;
         }
         // wait: the poster polls (briefly spinning, then napping) and keeps
-        // an eye on the doorbell, the peers and the watchdog
-        const int64_t t0 = monotonic_us();
+        // an eye on the abort flag, the peers and the watchdog
         int spins = 0;
         for (;;) {
             const int q = ops->query(marker);
             if (q == 1) break;
             if (q < 0) {
-                abort("round " + std::to_string(k) + " failed on the stream", true);
+                abort("a plane group failed on the stream", true);
                 return -1;
             }
             if (bell->abort.load(std::memory_order_acquire)) {
@@ -801,7 +939,7 @@ public:
             }
             const int64_t now = monotonic_us();
             if (now - t0 > (int64_t)FLAGS_rccl_timeout_ms * 1000) {
-                abort("round " + std::to_string(k) + " made no progress within -rccl_timeout_ms", true);
+                abort("a plane group made no progress within -rccl_timeout_ms", true);
                 return -1;
             }
             if (check_liveness()) {
@@ -813,16 +951,13 @@ public:
         }
         ops->release(marker);
         marker_live = false;
-        const int rc2 = complete_round(k, my_busy);
-        // nothing could move for want of credit: give the receivers a moment
-        // to consume instead of spinning empty rounds
-        if (rc2 == 0 && stalled && !payloads) usleep(50);
-        return rc2;
+        g_group_us.fetch_add(monotonic_us() - t0, std::memory_order_relaxed);
+        complete_group();
+        return 0;
     }
 
-    int complete_round(uint64_t k, bool my_busy) {
+    void complete_group() {
         std::vector<Buf> drop;  // released outside the lock
-        Buf drop_cancelled;
         std::lock_guard<std::mutex> g(mu);
         for (int p = 0; p < world; ++p) {
             for (Payload& s : moving_send[p]) {
@@ -842,43 +977,7 @@ public:
         moving_recv.assign(world, {});
         self_send.clear();
         self_recv.clear();
-        bool busy = my_busy;
-        for (int p = 0; p < world; ++p) {
-            if (p == rank) continue;
-            const Hdr* h = reinterpret_cast<const Hdr*>(ops->host_in + (size_t)p * kHdrBytes);
-            if (h->magic != kHdrMagic || h->round != k || h->from != (uint64_t)p || h->n > (uint32_t)kMaxEntries) {
-                mu.unlock();
-                abort("round " + std::to_string(k) + ": bad header from rank " + std::to_string(p), true);
-                mu.lock();
-                return -1;
-            }
-            PeerState& ps = peers[p];
-            ps.credit = std::max(ps.credit, h->credit);
-            busy |= (h->flags & kBusy) != 0;
-            for (uint32_t i = 0; i < h->n; ++i) {
-                if (h->e[i].len == kCancelLen) {  // the sender gave this payload up
-                    discard_locked(p, h->e[i].seq, &drop_cancelled);
-                    continue;
-                }
-                Payload in;
-                in.seq = h->e[i].seq;
-                in.len = (size_t)h->e[i].len;
-                in.ptr = in.len ? ops->alloc(in.len, &in.hold) : nullptr;
-                if (!in.ptr) {
-                    mu.unlock();
-                    abort("no memory to land a " + std::to_string(in.len) + " B payload from rank " +
-                              std::to_string(p),
-                          true);
-                    mu.lock();
-                    return -1;
-                }
-                ps.incoming.push_back(std::move(in));
-            }
-        }
-        busy_next = busy;
-        completed_round = k;
         housekeeping_locked();
-        return 0;
     }
 
     // (mu held) a payload from `src` landed
@@ -962,8 +1061,7 @@ public:
         for (PeerState& ps : peers) {
             for (Payload& p : ps.queued) bufs.push_back(std::move(p.hold));
             ps.queued.clear();
-            take(ps.announced);
-            take(ps.incoming);
+            take(ps.listed);
         }
         for (Payload& p : self_q) bufs.push_back(std::move(p.hold));
         self_q.clear();
@@ -973,6 +1071,34 @@ public:
         waiting.clear();
         if (!bell_name.empty()) shm_unlink(bell_name.c_str());
     }
+
+    // Collective, at Init: one group in which every rank exchanges 8 bytes
+    // with every peer, so RCCL connects every pair before traffic (it
+    // connects p2p peers lazily inside the first group that uses them).
+    int warm_up() {
+        Buf scratch;
+        char* b = static_cast<char*>(ops->alloc((size_t)16 * world, &scratch));
+        if (!b) return -1;
+        void* st = ops->stream();
+        ncclResult_t r = api.group_start();
+        for (int p = 0; p < world && r == ncclSuccess; ++p) {
+            if (p == rank) continue;
+            r = api.send(b + 16 * p, 8, ncclUint8, p, comm, (hipStream_t)st);
+            if (r == ncclSuccess) r = api.recv(b + 16 * p + 8, 8, ncclUint8, p, comm, (hipStream_t)st);
+        }
+        const ncclResult_t e = api.group_end();
+        if (r == ncclSuccess) r = e;
+        if (r != ncclSuccess || ops->record(&marker) != 0) return -1;
+        const int64_t t0 = monotonic_us();
+        for (;;) {
+            const int q = ops->query(marker);
+            if (q == 1) break;
+            if (q < 0 || monotonic_us() - t0 > (int64_t)FLAGS_rccl_timeout_ms * 1000) return -1;
+            usleep(50);
+        }
+        ops->release(marker);
+        return 0;
+    }
 };
 
 std::mutex g_mu;
@@ -980,7 +1106,13 @@ Plane* g_plane = nullptr;
 std::atomic<bool> g_active{false};
 
 Doorbell* open_bell(const std::string& name, bool shared) {
-    if (!shared) return new Doorbell();
+    if (!shared) {
+        void* m = calloc(1, sizeof(Doorbell));
+        if (!m) return nullptr;
+        Doorbell* b = static_cast<Doorbell*>(m);
+        b->magic = kBellMagic;
+        return b;
+    }
     const int fd = shm_open(name.c_str(), O_CREAT | O_RDWR, 0600);
     if (fd < 0) return nullptr;
     if (ftruncate(fd, (off_t)sizeof(Doorbell)) != 0) {
@@ -1017,7 +1149,7 @@ int Init(int rank, int world, const std::string& unique_id, int device, std::str
         return -1;
     }
     if (world <= 0 || world > kMaxRanks || rank < 0 || rank >= world || unique_id.size() != sizeof(ncclUniqueId)) {
-        if (error) *error = "bad rank/world/unique id";
+        if (error) *error = "bad rank/world/unique id (at most " + std::to_string(kMaxRanks) + " ranks per node)";
         return -1;
     }
     std::unique_ptr<Plane> p(new Plane);
@@ -1035,7 +1167,7 @@ int Init(int rank, int world, const std::string& unique_id, int device, std::str
     p->id = fnv1a(unique_id);
     int prev = 0;
     if (!p->api.fake()) hipGetDevice(&prev);
-    if (p->ops->init(device, (size_t)world * kHdrBytes, error) != 0) {
+    if (p->ops->init(device, error) != 0) {
         if (!p->api.fake()) hipSetDevice(prev);
         return -1;
     }
@@ -1058,15 +1190,14 @@ int Init(int rank, int world, const std::string& unique_id, int device, std::str
         return -1;
     }
     p->peers.assign(world, PeerState());
-    for (PeerState& ps : p->peers) ps.credit = (uint64_t)std::max<int64_t>(FLAGS_rccl_window_bytes, 1);
-    // round 1, collectively and synchronously: connects every pair (RCCL
-    // connects p2p peers lazily inside the first group that uses them)
-    const int rc = world > 1 ? p->run_round(1) : 0;
+    p->moving_send.assign(world, {});
+    p->moving_recv.assign(world, {});
+    const int rc = world > 1 ? p->warm_up() : 0;
     if (!p->api.fake()) hipSetDevice(prev);
     if (rc != 0) {
-        if (error) *error = "rccl plane: the first round failed";
+        if (error) *error = "rccl plane: the warm-up group failed";
         if (!p->bell_name.empty()) shm_unlink(p->bell_name.c_str());
-        p.release();  // its comm is aborted; the stream may still reference it
+        p.release();  // its comm may still be referenced by the stream
         return -1;
     }
     Plane* raw = p.release();
@@ -1078,6 +1209,7 @@ int Init(int rank, int world, const std::string& unique_id, int device, std::str
     static var::PassiveStatus<int64_t> v3("rccl_rounds", [] { return g_rounds.load(); });
     static var::PassiveStatus<int64_t> v4("rccl_aborts", [] { return g_aborts.load(); });
     static var::PassiveStatus<int64_t> v5("rccl_credit_stalls", [] { return g_credit_stalls.load(); });
+    static var::PassiveStatus<int64_t> v6("rccl_pair_rounds", [] { return g_pair_rounds.load(); });
     LOG(INFO) << "rccl plane up: rank " << rank << "/" << world
               << (raw->api.fake() ? " on the stub library (host memory)" : " on device " + std::to_string(device));
     return 0;
@@ -1099,8 +1231,7 @@ void Shutdown() {
         std::lock_guard<std::mutex> lk(g_plane->mu);
         g_plane->stop = true;
     }
-    g_plane->bell->seq.fetch_add(1);
-    futex(&g_plane->bell->seq, FUTEX_WAKE, INT_MAX, nullptr);
+    g_plane->ring(g_plane->rank);
     if (g_plane->poster.joinable()) g_plane->poster.join();
     // the plane object stays (Active() is false from now on): late callers
     // may still hold a pointer to it
@@ -1155,6 +1286,9 @@ Stats GetStats() {
     s.discarded = g_discarded.load();
     s.rounds = g_rounds.load();
     s.payload_rounds = g_payload_rounds.load();
+    s.pair_rounds = g_pair_rounds.load();
+    s.withdrawals = g_withdrawals.load();
+    s.group_us = g_group_us.load();
     s.aborts = g_aborts.load();
     s.credit_stalls = g_credit_stalls.load();
     s.stash_expired = g_expired.load();

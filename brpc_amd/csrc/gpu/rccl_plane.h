@@ -4,34 +4,41 @@
 // lending transport (gpu/xgmi.h) stays the default below -rccl_min_bytes.
 // It is the analog of the reference's RDMA data path
 // (src/brpc/rdma/rdma_endpoint.cpp:771-895: zero-copy SGEs, a sliding
-// window, ACK credits in imm_data, window sizes agreed in the handshake at
-// :505-509,613-617), with RCCL as the fabric.
+// window per connection, ACK credits in imm_data, window sizes agreed in
+// the handshake at :505-509,613-617), with RCCL as the fabric.
 //
-// Why rounds. RCCL send/recv kernels block until their partner runs, every
-// op of one communicator is serialised, and streams beyond
-// GPU_MAX_HW_QUEUES share hardware queues. Issuing sends and receives as
-// RPCs produce them (round 2's plane) lets two ranks each park a send in
-// front of the receive the other one needs: a cross-rank deadlock once the
-// payloads exceed RCCL's p2p buffering. This plane is deadlock-free by
-// construction instead:
-//  * ONE stream per rank, and every rank issues the same numbered rounds;
-//  * round k is ONE ncclGroupStart/End group holding, for every peer, a
-//    fixed-size header send + header recv, the payloads announced in the
-//    headers of round k-1 (both sides know their sizes) and the self
-//    payloads — every op in round k is matched by an op of round k at its
-//    peer, and ops of one group progress together, so round k completes
-//    once every rank issued it;
-//  * a rank issues round k+1 when the round-k headers (seen identically by
-//    every rank) carry a busy bit, or when some rank rang the node's
-//    doorbell (POSIX shm + futex) asking for round k+1 — so every rank
-//    issues every round, by induction.
-// Flow control: the header also carries the receiver's cumulative credit
-// (bytes it consumed from that sender plus -rccl_window_bytes); a sender
-// announces a payload only within credit. Received payloads wait in a
-// stash, keyed by (source, sequence), until the RPC layer claims them
-// (Recv), gives them back (Discard) or -rccl_stash_ttl_ms expires.
-// Failure: any rank that hits an RCCL error, a round older than
-// -rccl_timeout_ms or a dead peer process sets the doorbell's abort flag;
+// Why pair rounds. RCCL send/recv kernels block until their partner runs,
+// every op of one communicator is serialised, and streams beyond
+// GPU_MAX_HW_QUEUES share in-order hardware queues. A plane that issues a
+// send before its peer has committed to the matching receive can park it in
+// front of work another rank needs (a cross-rank deadlock once payloads
+// exceed RCCL's p2p buffering), and a plane that moves every rank in
+// lockstep (round 3's) lets one slow rank stall the node. This plane
+// decouples the pairs instead:
+//  * the control traffic never touches RCCL: per unordered pair of ranks a
+//    shm slot holds a round word, each side's payload list for the open
+//    round, the landing credit each receiver grants and a cancel ring;
+//  * a side with payloads within credit publishes its list and sets its
+//    ready bit; the side that finds the other bit set fires the round (the
+//    word moves to the next round). Idle pairs exchange nothing, and a
+//    payload moves in the round it is listed in — the receiver granted the
+//    landing bytes ahead of time (-rccl_window_bytes, the analog of the
+//    reference's pre-posted receive blocks, rdma_endpoint.cpp:990-1006);
+//  * every round a rank takes part in goes into ONE ncclGroupStart/End
+//    group on its one stream, and the rank clears its ready bit on every
+//    other pair first (a clear that fails means the peer fired it: it joins
+//    the group). So each rank has at most one plane group in flight and
+//    every group's partner ops sit in the partner's only group: no group
+//    can wait behind another, and a group waits only for ranks that
+//    already committed to it, never for an unrelated or slow rank.
+// Flow control: a sender lists a payload only within the receiver's
+// cumulative consumed bytes plus -rccl_window_bytes (or alone, once
+// everything it sent was consumed); the receiver wakes a stalled sender
+// when it consumes. Received payloads wait in a stash, keyed by (source,
+// sequence), until the RPC layer claims them (Recv), gives them back
+// (Discard) or -rccl_stash_ttl_ms expires.
+// Failure: any rank that hits an RCCL error, a group older than
+// -rccl_timeout_ms or a dead peer process sets the node's abort flag;
 // every rank then aborts its communicator, waits (bounded) for its stream
 // to drain before recycling payload memory, fails its waiters, and new
 // payloads fall back to xGMI lending.
@@ -98,10 +105,13 @@ void AbortForTest(const std::string& why);
 struct Stats {
     int64_t sent_payloads = 0, sent_bytes = 0, recv_payloads = 0, recv_bytes = 0;
     int64_t discarded = 0, rounds = 0, payload_rounds = 0, aborts = 0;
+    int64_t pair_rounds = 0;     // pair rounds fired (a group holds one per partner)
+    int64_t withdrawals = 0;     // ready bits cleared because another pair fired first
+    int64_t group_us = 0;        // wall time groups spent on the stream (issue to completion)
     int64_t credit_stalls = 0;   // rounds where a queued payload waited for credit
     int64_t stash_expired = 0;   // received payloads nobody claimed in time
     int64_t recv_timeouts = 0;   // Recv calls that gave up
-    int64_t doorbells = 0;       // idle -> busy transitions this rank rang
+    int64_t doorbells = 0;       // idle -> busy wake-ups of the poster by new payloads
     int64_t withdrawn = 0;       // Cancelled (before announcement, or told to the receiver after)
     int64_t stash_payloads = 0, stash_bytes = 0;  // landed, not yet claimed (now)
     int world = 0;

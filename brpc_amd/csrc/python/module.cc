@@ -648,6 +648,9 @@ PYBIND11_MODULE(_native, m) {
         d["discarded"] = s.discarded;
         d["rounds"] = s.rounds;
         d["payload_rounds"] = s.payload_rounds;
+        d["pair_rounds"] = s.pair_rounds;
+        d["withdrawals"] = s.withdrawals;
+        d["group_us"] = s.group_us;
         d["aborts"] = s.aborts;
         d["credit_stalls"] = s.credit_stalls;
         d["stash_expired"] = s.stash_expired;

@@ -26,6 +26,11 @@ def main():
     ap.add_argument("--overcrowd-test", action="store_true",
                     help="after the legs, refuse most writes (tiny -socket_max_unwritten_bytes): payloads queued "
                          "for refused requests must be withdrawn or dropped at the receiver, never stashed")
+    ap.add_argument("--ring-test", type=float, default=0.0,
+                    help="seconds per phase: every rank presses only rank+1 (ring), first with every poster at "
+                         "full speed, then with --slow-rank's poster sleeping --slow-delay-us after every group")
+    ap.add_argument("--slow-rank", type=int, default=3)
+    ap.add_argument("--slow-delay-us", type=int, default=50000)
     ap.add_argument("--abort-test", action="store_true",
                     help="after the legs, rank 1 aborts the plane under traffic; every rank must notice "
                          "within a second and keep serving through the fallback")
@@ -43,20 +48,58 @@ def main():
     others = [x for i, x in enumerate(addrs) if i != topo.rank]
     parallel.set_rccl_min_bytes(32768)
     out = {"rank": topo.rank, "world": topo.world_size, "plane_up": bool(up), "legs": []}
+    import time
     for size, calls in zip([int(x) for x in a.sizes.split(",")], [int(x) for x in a.calls.split(",")]):
-        s0 = parallel.rccl_stats()
+        if calls <= 0:
+            continue
         p = native.Press({"server": others[0], "fanout_servers": ",".join(others), "concurrency": a.concurrency,
                           "attachment_size": size, "check_echo": True, "timeout_ms": 60000})
+        p.run_requests(min(calls, 20))  # connections and plane hellos up
+        p.reset_stats()
+        parallel.barrier(topo)
+        s0 = parallel.rccl_stats()
+        t0 = time.perf_counter()
         p.run_requests(calls)
+        dt = time.perf_counter() - t0
         st = p.stats()
         s1 = parallel.rccl_stats()
         out["legs"].append({"size": size, "calls": calls, "success": st["success"], "error": st["error"],
-                            "last_error": st["last_error"],
+                            "last_error": st["last_error"], "seconds": dt,
                             "sent_payloads": s1["sent_payloads"] - s0["sent_payloads"],
                             "recv_payloads": s1["recv_payloads"] - s0["recv_payloads"],
+                            "groups": s1["rounds"] - s0["rounds"],
+                            "pair_rounds": s1["pair_rounds"] - s0["pair_rounds"],
+                            "withdrawals": s1["withdrawals"] - s0["withdrawals"],
+                            "group_us": s1["group_us"] - s0["group_us"],
                             "credit_stalls": s1["credit_stalls"] - s0["credit_stalls"]})
         del p
         parallel.barrier(topo)
+    if a.ring_test > 0:
+        nxt = addrs[(topo.rank + 1) % topo.world_size]
+        out["ring"] = []
+        for phase in ("full_speed", "slow_rank"):
+            if phase == "slow_rank" and topo.rank == a.slow_rank:
+                native.set_flag("rccl_test_poster_delay_us", str(a.slow_delay_us))
+            p = native.Press({"server": nxt, "concurrency": a.concurrency, "attachment_size": 65536,
+                              "check_echo": True, "timeout_ms": 60000})
+            p.run_requests(20)
+            p.reset_stats()
+            parallel.barrier(topo)
+            s0 = parallel.rccl_stats()
+            t0 = time.perf_counter()
+            p.run_for(a.ring_test)
+            dt = time.perf_counter() - t0
+            st = p.stats()
+            s1 = parallel.rccl_stats()
+            out["ring"].append({"phase": phase, "qps": st["success"] / dt, "error": st["error"],
+                                "last_error": st["last_error"],
+                                "pair_rounds": s1["pair_rounds"] - s0["pair_rounds"],
+                                "groups": s1["rounds"] - s0["rounds"],
+                                "sent_payloads": s1["sent_payloads"] - s0["sent_payloads"]})
+            del p
+            parallel.barrier(topo)
+            native.set_flag("rccl_test_poster_delay_us", "0")
+            parallel.barrier(topo)
     if a.overcrowd_test:
         import time
         p = native.Press({"server": others[0], "fanout_servers": ",".join(others), "concurrency": a.concurrency,

@@ -95,3 +95,28 @@ def test_plane_refused_writes_leave_nothing_stashed():
         assert o["after_overcrowd_leg"] == {"success": 100, "error": 0}, o
         assert o["aborts"] == 0, o
     assert sum(o["overcrowd_leg"]["withdrawn"] for o in outs) > 0, [o["overcrowd_leg"] for o in outs]
+
+
+def test_plane_slow_rank_stalls_only_its_own_pairs():
+    # ring traffic (rank r calls only rank r+1) on 8 ranks; then rank 3's
+    # poster sleeps 50 ms after every group. Only the pairs that include
+    # rank 3 (2->3 and 3->4) may slow down: every other pair keeps its rate,
+    # because a pair round fires only when both of its ranks are ready and a
+    # group never waits behind another rank's work (round 3's node-wide
+    # lockstep slowed every pair to the slow rank's pace).
+    outs = _run(8, 29656, "--calls", "0,0", "--ring-test", "1.5", "--slow-rank", "3", "--slow-delay-us", "50000")
+    slow_clients = {2, 3}
+    for o in outs:
+        assert o["aborts"] == 0 and o["recv_timeouts"] == 0, o
+        full, slow = o["ring"]
+        assert full["error"] == 0 and slow["error"] == 0, o
+        assert full["qps"] > 0, o
+    rates = {o["rank"]: (o["ring"][0]["qps"], o["ring"][1]["qps"]) for o in outs}
+    # the slow rank's pairs: at most ~20 groups/s on its side
+    for r in slow_clients:
+        assert rates[r][1] < 0.5 * rates[r][0], rates
+    # every other pair keeps at least half its full-speed rate (8 ranks share
+    # this host's CPUs, so rates are noisy)
+    for r, (full, slow) in rates.items():
+        if r not in slow_clients:
+            assert slow > 0.5 * full, (r, rates)
