@@ -113,6 +113,14 @@ int LaunchSnappySplit(const SnappyStream* streams_dev, int n, uint32_t piece_lim
 // empty slots.
 int LaunchSnappyDecompressPieces(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
                                  hipStream_t s);
+// The serial decoder (one element per wave step) for every size: A/B and
+// tests; LaunchSnappyDecompressPieces takes the parallel decoder (source map
+// + pointer jumping) for pieces up to 8 KiB.
+int LaunchSnappyDecompressPiecesSerial(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
+                                       hipStream_t s);
+// With phase stamps (shader clock, block 0) written to stamps[0..4].
+int LaunchSnappyDecompressPiecesStamped(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
+                                        uint64_t* stamps, hipStream_t s);
 // Batched snappy compression: job.src = raw block (<= kSnappyMaxBlock),
 // job.dst = output with job.dst_cap >= SnappyMaxCompressedLength(src_len).
 // scratch: n * SnappyCompressScratchPerBlock() bytes of device memory.

@@ -72,6 +72,8 @@ __device__ __forceinline__ uint32_t load32(gbyte_c* p) {
 
 // 4 bytes per lane of the stream starting at 4-byte-aligned `wbase` (relative
 // to `in`); bytes outside [0, in_len) read as 0 and are never consumed.
+typedef __attribute__((address_space(3))) uint8_t lbyte;
+
 __device__ __forceinline__ uint32_t load_window(gbyte_c* in, uint32_t in_len, uint32_t wbase, int lane) {
     const uint32_t pos = wbase + 4u * (uint32_t)lane;
     if (pos + 4 <= in_len) return load32(in + pos);
@@ -238,6 +240,245 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_kernel(const S
     const uint32_t win = load_window(in, in_len, 0, lane);
     const int bad = decode_elements(in, in_len, mis, 0, win, pc.ulen, buf, pc.dst, lane);
     if (lane == 0) err[blk] = bad;
+}
+
+// ------------------------------------------------- parallel piece decoder
+// Pieces of up to kParMax bytes (the RPC path's 4 KiB device-encoded
+// pieces) decode in three data-parallel phases instead of one element per
+// wave step (the serial decoder above spends ~470 cycles per element on
+// text: every element is a wave-uniform branch tree plus an LDS round trip,
+// 117 us for 4 KiB pieces of log records, benchmarks/snappy_rpc_shapes.py):
+//  1. parse: the compressed piece is staged in LDS with 16-byte loads; lane j
+//     parses the element header at ip + j speculatively, the true element
+//     starts are found by one v_readlane hop each, and a wave prefix sum
+//     gives every element its output position. Each element then writes,
+//     for every output byte it produces, WHERE that byte comes from: a
+//     literal byte of the input (flag bit set) or an earlier output position
+//     (copies) — a source map of u16 entries in LDS;
+//  2. resolve: pointer jumping over the map (src[p] = src[src[p]] until every
+//     entry names a literal byte) — log2(chain depth) rounds of fully
+//     parallel LDS work, overlapping copies included;
+//  3. gather: out[p] = input[src[p]], 8 bytes per lane per step, stored
+//     straight to the destination (HBM or pinned host memory).
+constexpr uint32_t kParMax = 8192;
+constexpr uint16_t kLitFlag = 0x8000;
+
+// Wave64 inclusive prefix sum / max on DPP (row_shr 1,2,4,8 inside rows of
+// 16, then row_bcast:15 and row_bcast:31 across rows): VALU modifiers, no
+// LDS round trip per step as with __shfl_up (ds_bpermute).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Phase stamps (shader clock) of block 0, for benchmarks/snappy_rpc_shapes.py
+__device__ __forceinline__ void stamp(uint64_t* stamps, int blk, int lane, int i) {
+    if (stamps && blk == 0 && lane == 0) stamps[i] = __builtin_amdgcn_s_memtime();
+}
+
+__global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(const SnappyPiece* __restrict__ pieces,
+                                                                             int n, uint32_t lo, uint32_t hi,
+                                                                             uint32_t cin_cap,
+                                                                             int* __restrict__ err,
+                                                                             uint64_t* __restrict__ stamps) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int blk = blockIdx.x;
+    if (blk >= n) return;
+    const int lane = threadIdx.x;
+    const SnappyPiece pc = pieces[blk];
+    if (pc.ulen == 0) {
+        if (lo == 0 && lane == 0) err[blk] = 0;
+        return;
+    }
+    if (pc.ulen <= lo || pc.ulen > hi) return;
+    const uint32_t ulen = pc.ulen;
+    stamp(stamps, blk, lane, 0);
+    // stage: the piece from the 16-byte boundary below it (a 16-byte
+    // aligned chunk never crosses a page, so reading its unused head and
+    // tail stays inside mapped memory)
+    const uint32_t mis = (uint32_t)((uintptr_t)pc.src & 15);
+    const uint32_t end = mis + pc.src_len;  // input is cin[mis, end)
+    if (end + 8 > cin_cap) {
+        if (lane == 0) err[blk] = 9;  // more compressed bytes than a valid piece can have: host codec
+        return;
+    }
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    lbyte* const cin = (lbyte*)lds;
+    __attribute__((address_space(3))) uint16_t* const smap =
+        (__attribute__((address_space(3))) uint16_t*)(lds + cin_cap);
+    {
+        gbyte_c* g = as_global(static_cast<const uint8_t*>(pc.src) - mis);
+        for (uint32_t o = lane * 16; o < end; o += kWave * 16)
+            *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(cin + o) =
+                *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(g + o);
+    }
+    __syncthreads();
+    stamp(stamps, blk, lane, 1);
+    const __attribute__((address_space(3))) uint32_t* cin32 = (const __attribute__((address_space(3))) uint32_t*)cin;
+    // ---- 1. parse + source map
+    uint32_t ip = mis, upos = 0;
+    int bad = 0;
+    uint64_t t_dec = 0, t_chain = 0, t_fill = 0, t_iter = 0;  // phase stamps only
+    while (ip < end) {
+        const uint64_t ta = stamps ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t q = ip + (uint32_t)lane;
+        const uint32_t w = q >> 2;
+        const uint64_t x = ((((uint64_t)cin32[w + 1]) << 32) | cin32[w]) >> ((q & 3) * 8);
+        const uint32_t tag = (uint32_t)x & 0xff;
+        const uint32_t ext = (uint32_t)(x >> 8);
+        const uint32_t kind = tag & 3;
+        uint32_t len, off = 0, hdr;
+        if (kind == 0) {
+            len = (tag >> 2) + 1;
+            hdr = 1;
+            if (len > 60) {
+                const uint32_t nb = len - 60;
+                len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
+                hdr += nb;
+            }
+        } else if (kind == 1) {
+            len = ((tag >> 2) & 7) + 4;
+            off = ((tag >> 5) << 8) | (ext & 0xff);
+            hdr = 2;
+        } else {
+            len = (tag >> 2) + 1;
+            off = kind == 2 ? (ext & 0xffff) : ext;
+            hdr = kind == 2 ? 3 : 5;
+        }
+        const uint64_t csize = (uint64_t)hdr + (kind == 0 ? len : 0);
+        const uint32_t step = (uint32_t)min(csize, (uint64_t)0x7FFFFFFF);
+        const uint64_t tb = stamps ? __builtin_amdgcn_s_memtime() : 0;
+        // the element chain: one readlane per element
+        uint64_t mask = 0;
+        uint32_t p = 0;
+        while (p < (uint32_t)kWave && ip + p < end) {
+            mask |= 1ull << p;
+            p += (uint32_t)__builtin_amdgcn_readlane((int)step, (int)p);
+        }
+        const uint64_t tc = stamps ? __builtin_amdgcn_s_memtime() : 0;
+        const bool marked = (mask >> lane) & 1;
+        const uint32_t u0 = upos + wave_incl_sum(marked ? len : 0) - (marked ? len : 0);
+        int e = 0;
+        if (marked) {
+            if ((uint64_t)q + csize > end) e = 3;                 // truncated
+            else if ((uint64_t)u0 + len > ulen) e = 4;            // past the piece
+            else if (kind != 0 && (off == 0 || off > u0)) e = 6;  // before the piece
+        }
+        const uint64_t eb = __ballot(e != 0);
+        if (eb) {
+            bad = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(eb));
+            break;
+        }
+        // source map: short elements lane by lane, long ones by the wave
+        const uint32_t base = kind == 0 ? (kLitFlag | (q + hdr)) : (u0 - off);
+        const bool is_long = marked && len > (uint32_t)kWave;
+        const uint64_t td = stamps ? __builtin_amdgcn_s_memtime() : 0;
+        const uint32_t mylen = marked && !is_long ? len : 0;
+        const uint32_t maxlen = wave_max(mylen);
+        for (uint32_t j = 0; j < maxlen; ++j) {
+            if (j < mylen) smap[u0 + j] = (uint16_t)(base + j);
+        }
+        uint64_t lm = __ballot(is_long);
+        while (lm) {
+            const int l = __builtin_ctzll(lm);
+            lm &= lm - 1;
+            const uint32_t lu0 = (uint32_t)__builtin_amdgcn_readlane((int)u0, l);
+            const uint32_t llen = (uint32_t)__builtin_amdgcn_readlane((int)len, l);
+            const uint32_t lbase = (uint32_t)__builtin_amdgcn_readlane((int)base, l);
+            for (uint32_t j = lane; j < llen; j += kWave) smap[lu0 + j] = (uint16_t)(lbase + j);
+        }
+        upos = (uint32_t)__builtin_amdgcn_readlane((int)(u0 + len), (int)(63 - __builtin_clzll(mask)));
+        ip += p;
+        if (stamps) {
+            const uint64_t te = __builtin_amdgcn_s_memtime();
+            t_dec += tb - ta;
+            t_chain += tc - tb;
+            t_fill += te - td;
+            t_iter += 1;
+        }
+    }
+    if (stamps && blk == 0 && lane == 0) {
+        stamps[5] = t_dec;
+        stamps[6] = t_chain;
+        stamps[7] = t_fill;
+        stamps[9] = t_iter;
+    }
+    if (!bad && (ip != end || upos != ulen)) bad = 7;
+    if (bad) {
+        if (lane == 0) err[blk] = bad;
+        return;
+    }
+    __syncthreads();
+    stamp(stamps, blk, lane, 2);
+    // ---- 2. resolve: pointer jumping until every entry is a literal byte;
+    // 8 entries per lane per step: one 16-byte read, up to 8 independent
+    // reads of their sources, one 16-byte write
+    for (int round = 0;; ++round) {
+        bool more = false;
+        for (uint32_t o = lane * 8; o < ulen; o += kWave * 8) {
+            u32x4 m = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(smap + o);
+            // branch-free: every lane issues its 8 reads back to back (a
+            // resolved entry re-reads entry 0, and keeps its value)
+            uint32_t e[8], r[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) e[k] = (m[k >> 1] >> (16 * (k & 1))) & 0xffff;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) r[k] = smap[(e[k] & kLitFlag) ? 0u : e[k]];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool copy = !(e[k] & kLitFlag) && o + k < ulen;
+                r[k] = copy ? r[k] : e[k];
+                more |= copy && !(r[k] & kLitFlag);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m[k] = r[2 * k] | (r[2 * k + 1] << 16);
+            *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(smap + o) = m;
+        }
+        if (!__ballot(more)) break;
+        if (round > 16) {  // cannot happen for a valid piece (depth <= ulen)
+            if (lane == 0) err[blk] = 10;
+            return;
+        }
+    }
+    __syncthreads();
+    stamp(stamps, blk, lane, 3);
+    // ---- 3. gather + store, 8 bytes per lane per step
+    gbyte* dst = as_global(pc.dst);
+    const bool aligned8 = ((uintptr_t)pc.dst & 7) == 0;
+    const uint32_t vec_end = aligned8 ? (ulen & ~7u) : 0;
+    for (uint32_t o = lane * 8; o < vec_end; o += kWave * 8) {
+        const u32x4 m = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(smap + o);
+        uint32_t lo32 = 0, hi32 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pair = m[k];
+            const uint32_t b0 = cin[pair & 0x7fff], b1 = cin[(pair >> 16) & 0x7fff];
+            if (k < 2) lo32 |= (b0 | (b1 << 8)) << (16 * k);
+            else hi32 |= (b0 | (b1 << 8)) << (16 * (k - 2));
+        }
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 val;
+        val[0] = lo32;
+        val[1] = hi32;
+        *reinterpret_cast<__attribute__((address_space(1))) u32x2*>(dst + o) = val;
+    }
+    for (uint32_t o = vec_end + lane; o < ulen; o += kWave) dst[o] = cin[smap[o] & 0x7fff];
+    stamp(stamps, blk, lane, 4);
+    if (lane == 0) err[blk] = 0;
 }
 
 // One wave per whole stream, cut at exact multiples of the piece limit: a
@@ -440,7 +681,6 @@ __device__ __forceinline__ O emit_copy(O o, uint32_t off, uint32_t len) {
     return emit_copy2(o, off, len);
 }
 
-typedef __attribute__((address_space(3))) uint8_t lbyte;
 __device__ __forceinline__ uint32_t lload32(const lbyte* p) {
     typedef uint32_t __attribute__((aligned(1))) u32u;
     return *reinterpret_cast<const __attribute__((address_space(3))) u32u*>(p);
@@ -596,13 +836,36 @@ int LaunchSnappySplit(const SnappyStream* streams_dev, int n, uint32_t piece_lim
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int LaunchSnappyDecompressPieces(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
-                                 hipStream_t s) {
+int LaunchSnappyDecompressPiecesSerial(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
+                                       hipStream_t s) {
     if (n <= 0) return 0;
     if (hi == 0 || hi > kSnappyMaxBlock || lo >= hi) return -1;
     const uint32_t lds = (hi + 4095) & ~4095u;
     hipLaunchKernelGGL(snappy_decompress_pieces_kernel, dim3(n), dim3(kWave), lds, s, pieces_dev, n, lo, hi, err_dev);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int LaunchSnappyDecompressPiecesStamped(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
+                                        uint64_t* stamps, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (hi == 0 || hi > kSnappyMaxBlock || lo >= hi) return -1;
+    // pieces up to kParMax: the parallel decoder; larger ones: the serial one
+    if (lo < kParMax) {
+        const uint32_t phi = std::min(hi, kParMax);
+        const uint32_t cin_cap = (uint32_t)((SnappyMaxCompressedLength(phi) + 16 + 15) & ~15ull);
+        const uint32_t lds = cin_cap + 2 * ((phi + 7) & ~7u);
+        hipLaunchKernelGGL(snappy_decompress_pieces_par_kernel, dim3(n), dim3(kWave), lds, s, pieces_dev, n, lo, phi,
+                           cin_cap, err_dev, stamps);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (hi <= kParMax) return 0;
+        lo = kParMax;
+    }
+    return LaunchSnappyDecompressPiecesSerial(pieces_dev, n, lo, hi, err_dev, s);
+}
+
+int LaunchSnappyDecompressPieces(const SnappyPiece* pieces_dev, int n, uint32_t lo, uint32_t hi, int* err_dev,
+                                 hipStream_t s) {
+    return LaunchSnappyDecompressPiecesStamped(pieces_dev, n, lo, hi, err_dev, nullptr, s);
 }
 
 int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch, uint32_t* out_len_dev,

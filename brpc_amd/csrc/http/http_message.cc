@@ -9,62 +9,125 @@
 namespace mrpc {
 
 // ---------------------------------------------------------------- sink
+// Parts, the end and the reader arrive from different threads (the parser's
+// and the user's); one of them at a time owns delivery (_delivering) and
+// drains what is queued, so the reader sees its callbacks one at a time and
+// in order: every part, then OnEndOfMessage exactly once.
 void ProgressiveSink::Feed(Buf&& part) {
-    ProgressiveReader* r;
     {
         std::lock_guard<std::mutex> g(_mu);
-        if (!_reader) {
-            _pending.append(std::move(part));
-            return;
-        }
-        r = _reader;
+        if (_ended) return;  // the reader refused earlier: the rest is dropped
+        _pending.append(std::move(part));
+        if (!_reader || _delivering) return;
+        _delivering = true;
     }
-    for (size_t i = 0; i < part.backing_block_num(); ++i) {
-        Status st = r->OnReadOnePart(part.block_data(i), part.block_len(i));
-        if (!st.ok()) {
-            std::lock_guard<std::mutex> g(_mu);
-            _ended = true;  // reader refused: drop the rest
-            return;
-        }
-    }
+    Drain();
 }
 
 void ProgressiveSink::End(int error_code, const std::string& error_text) {
-    ProgressiveReader* r = nullptr;
     {
         std::lock_guard<std::mutex> g(_mu);
-        if (_end_delivered) return;
-        _ended = true;
-        _error_code = error_code;
-        _error_text = error_text;
-        if (_reader) {
-            r = _reader;
-            _end_delivered = true;
+        if (_body_done) return;
+        _body_done = true;
+        if (!_ended) {
+            _ended = true;
+            _error_code = error_code;
+            _error_text = error_text;
         }
+        if (!_reader || _delivering) {
+            if (!_reader) RunOnEndLocked();  // nobody reads: the connection is free now
+            return;
+        }
+        _delivering = true;
     }
-    if (r) r->OnEndOfMessage(error_code ? Status(error_code, error_text) : Status());
+    Drain();
 }
 
 void ProgressiveSink::SetReader(ProgressiveReader* r) {
-    Buf pending;
-    bool ended;
-    int ec;
-    std::string et;
     {
         std::lock_guard<std::mutex> g(_mu);
         if (_reader) return;
         _reader = r;
-        pending.swap(_pending);
-        ended = _ended;
-        ec = _error_code;
-        et = _error_text;
-        if (ended) _end_delivered = true;
+        if (_delivering) return;
+        _delivering = true;
     }
-    bool ok = true;
-    for (size_t i = 0; ok && i < pending.backing_block_num(); ++i) {
-        ok = r->OnReadOnePart(pending.block_data(i), pending.block_len(i)).ok();
+    Drain();
+}
+
+void ProgressiveSink::SetOnBodyDone(std::function<void()> fn) {
+    std::function<void()> now;
+    {
+        std::lock_guard<std::mutex> g(_mu);
+        if (_body_done) now = std::move(fn);
+        else _on_body_done = std::move(fn);
     }
-    if (ended) r->OnEndOfMessage(ec ? Status(ec, et) : Status());
+    if (now) now();
+}
+
+void ProgressiveSink::RunOnEndLocked() {
+    if (!_on_body_done) return;
+    std::function<void()> fn = std::move(_on_body_done);
+    _on_body_done = nullptr;
+    // run outside the lock by the caller's thread: defer through a fiber-safe
+    // path is not needed (the callback only returns a socket to its pool)
+    _mu.unlock();
+    fn();
+    _mu.lock();
+}
+
+void ProgressiveSink::Drain() {
+    for (;;) {
+        Buf batch;
+        ProgressiveReader* r;
+        bool deliver_end = false;
+        Status end_st;
+        {
+            std::lock_guard<std::mutex> g(_mu);
+            r = _reader;
+            batch.swap(_pending);
+            if (batch.empty()) {
+                if (_ended && !_end_delivered) {
+                    _end_delivered = true;
+                    deliver_end = true;
+                    end_st = _error_code ? Status(_error_code, _error_text) : Status();
+                }
+                _delivering = false;
+                if (_body_done) RunOnEndLocked();
+            }
+        }
+        if (batch.empty()) {
+            if (deliver_end) r->OnEndOfMessage(end_st);
+            return;
+        }
+        for (size_t i = 0; i < batch.backing_block_num(); ++i) {
+            Status st = r->OnReadOnePart(batch.block_data(i), batch.block_len(i));
+            if (!st.ok()) {
+                // the reader refused: it gets no more parts, and its
+                // OnEndOfMessage carries that error (the reference's
+                // ProgressiveReader contract, failed_on_read_one_part); the
+                // rest of the body is still parsed off the connection
+                bool deliver;
+                {
+                    std::lock_guard<std::mutex> g(_mu);
+                    _ended = true;
+                    _pending.clear();
+                    deliver = !_end_delivered;
+                    _end_delivered = true;
+                    _error_code = st.error_code();
+                    _error_text = st.error_str();
+                    _delivering = false;
+                    if (_body_done) RunOnEndLocked();
+                }
+                if (deliver) r->OnEndOfMessage(st);
+                return;
+            }
+        }
+    }
+}
+
+bool ProgressiveSink::body_done() const {
+    std::lock_guard<std::mutex> g(_mu);
+    return _body_done;
 }
 
 bool ProgressiveSink::ended() const {

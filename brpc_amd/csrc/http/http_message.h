@@ -6,6 +6,8 @@
 // reads so a body arriving in pieces is scanned once.
 #pragma once
 
+#include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -28,15 +30,34 @@ public:
     void End(int error_code, const std::string& error_text);
     void SetReader(ProgressiveReader* r);
     bool ended() const;
+    bool body_done() const;
+    // Runs once the body left the connection (now, if it already did): a
+    // pooled connection goes back to its pool only then.
+    void SetOnBodyDone(std::function<void()> fn);
 
 private:
+    void Drain();
+    void RunOnEndLocked();
     mutable std::mutex _mu;
     ProgressiveReader* _reader = nullptr;
     Buf _pending;
-    bool _ended = false;
+    bool _ended = false;          // no more parts for the reader (end of body, or it refused)
+    bool _body_done = false;      // the parser reached the end of the body
     bool _end_delivered = false;
+    bool _delivering = false;
     int _error_code = 0;
     std::string _error_text;
+    std::function<void()> _on_body_done;
+};
+
+// In-order responses on one HTTP/1.x connection (RFC 7230 §6.3.2): the
+// server runs pipelined requests concurrently, each response waits here for
+// the ones before it. One per connection, shared by its requests.
+struct HttpResponseOrder {
+    std::mutex mu;
+    uint64_t next_req = 0;   // the parser's counter (one parsing thread per socket)
+    uint64_t next_resp = 0;  // under mu
+    std::map<uint64_t, std::pair<Buf, bool>> ready;  // seq -> (packet, shutdown after), under mu
 };
 
 class HttpMessage : public InputMessageBase {
@@ -48,6 +69,8 @@ public:
     PipelinedInfo pi;                           // client: the call this response answers
     uint32_t stream_id = 0;                     // h2: stream of this message
     std::shared_ptr<ProgressiveSink> progressive;  // client: body continues through the sink
+    std::shared_ptr<HttpResponseOrder> order;      // server, HTTP/1.x: the connection's response order
+    uint64_t order_seq = 0;
 };
 
 class HttpParser : public ParsingContext {
@@ -76,6 +99,8 @@ public:
     // there: HEAD => no body, progressive => stream through a sink).
     void (*on_head)(HttpParser* p, HttpMessage* m, void* arg) = nullptr;
     void* on_head_arg = nullptr;
+    // server side: numbers the requests of this connection
+    std::shared_ptr<HttpResponseOrder> order;
 
     // Quick check used for protocol sniffing: returns 1 if `head` starts an
     // HTTP message, 0 if it cannot, -1 if more bytes are needed.

@@ -761,7 +761,8 @@ bool Socket::IsWriteComplete(WriteRequest* old_head, bool singular_node, WriteRe
 int Socket::Write(Buf* data, const WriteOptions* options) {
     static const WriteOptions kDefault;
     const WriteOptions& opt = options ? *options : kDefault;
-    if (data->empty()) return 0;
+    // an empty write only matters as a half-close after what is queued
+    if (data->empty() && !opt.shutdown_write_after) return 0;
     if (Failed()) {
         const int ec = _error_code ? _error_code : EFAILEDSOCKET;
         if (opt.id_wait != fiber::INVALID_CALL_ID) fiber::call_id_error(opt.id_wait, ec, error_text());

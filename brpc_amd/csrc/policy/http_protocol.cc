@@ -86,6 +86,11 @@ ParseResult ParseHttpMessage(Buf* source, Socket* socket, bool read_eof, const v
         return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
     }
     HttpMessage* msg = p->release();
+    if (!msg->is_response) {
+        if (!p->order) p->order = std::make_shared<HttpResponseOrder>();
+        msg->order = p->order;
+        msg->order_seq = p->order->next_req++;
+    }
     if (FLAGS_http_verbose) {
         fprintf(stderr, "[http %s] %s %s\n", msg->is_response ? "response" : "request",
                 msg->is_response ? std::to_string(msg->header.status_code()).c_str()
@@ -214,8 +219,36 @@ void ProcessHttpResponse(InputMessageBase* msg_base) {
 }
 
 // ------------------------------------------------------------------ server
+// Writes `packet` once every earlier response of the connection was written
+// (pipelined requests finish in any order; their responses may not).
+static void WriteInOrder(HttpResponseOrder* order, uint64_t seq, Socket* sock, Buf* packet, bool shutdown_after) {
+    auto write = [sock](Buf* b, bool shut) {
+        WriteOptions wopt;
+        wopt.ignore_eovercrowded = true;
+        wopt.shutdown_write_after = shut;  // "Connection: close" / HTTP/1.0
+        sock->Write(b, &wopt);
+    };
+    if (!order) {
+        write(packet, shutdown_after);
+        return;
+    }
+    std::lock_guard<std::mutex> g(order->mu);
+    if (seq != order->next_resp) {
+        order->ready.emplace(seq, std::make_pair(std::move(*packet), shutdown_after));
+        return;
+    }
+    write(packet, shutdown_after);
+    ++order->next_resp;
+    for (auto it = order->ready.begin(); it != order->ready.end() && it->first == order->next_resp;
+         it = order->ready.erase(it)) {
+        write(&it->second.first, it->second.second);
+        ++order->next_resp;
+    }
+}
+
 static void SendHttpResponse(Controller* cntl, pb::Message* req, pb::Message* res, Server* server,
-                             MethodStatus* ms, int64_t received_us, bool keep_alive, bool http10) {
+                             MethodStatus* ms, int64_t received_us, bool keep_alive, bool http10,
+                             std::shared_ptr<HttpResponseOrder> order, uint64_t order_seq) {
     std::unique_ptr<Controller> cntl_guard(cntl);
     std::unique_ptr<pb::Message> req_guard(req);
     std::unique_ptr<pb::Message> res_guard(res);
@@ -225,6 +258,10 @@ static void SendHttpResponse(Controller* cntl, pb::Message* req, pb::Message* re
         if (cntl->_progressive_attachment) cntl->_progressive_attachment->MarkRPCAsDone(true);
         return;
     }
+    // a progressive body continues after this response: the connection
+    // cannot carry another response in order, so later pipelined requests
+    // of it are answered after the head (HTTP/1.x clients do not pipeline
+    // behind a streamed response in practice)
     HttpHeader& rh = cntl->http_response();
     rh.set_version(1, http10 ? 0 : 1);
     Buf body;
@@ -269,11 +306,12 @@ static void SendHttpResponse(Controller* cntl, pb::Message* req, pb::Message* re
     SerializeHttpResponseHead(&packet, rh, chunked || (http10 && cntl->_progressive_attachment) ? -1 : (int64_t)body.size(),
                               chunked, keep_alive);
     if (cntl->http_request().method() != HTTP_METHOD_HEAD) packet.append(std::move(body));
-    WriteOptions wopt;
-    wopt.ignore_eovercrowded = true;
-    wopt.shutdown_write_after = !keep_alive;  // "Connection: close" / HTTP/1.0
-    sock->Write(&packet, &wopt);
+    // a progressive body ends the connection itself (its last chunk, or the
+    // close that delimits an HTTP/1.0 body), not with this head
+    const bool progressive = cntl->_progressive_attachment != nullptr && !cntl->Failed();
+    WriteInOrder(order.get(), order_seq, sock.get(), &packet, !keep_alive && !progressive);
     if (cntl->_progressive_attachment) {
+        if (!keep_alive) cntl->_progressive_attachment->set_shutdown_after_end();
         cntl->_progressive_attachment->MarkRPCAsDone(cntl->Failed());
         cntl->_progressive_attachment.reset();
     }
@@ -299,6 +337,8 @@ void ProcessHttpRequest(InputMessageBase* msg_base) {
     req_h = msg->header;
     const bool http10 = req_h.major_version() == 1 && req_h.minor_version() == 0;
     const bool keep_alive = msg->keep_alive;
+    std::shared_ptr<HttpResponseOrder> order = msg->order;
+    const uint64_t order_seq = msg->order_seq;
     if (const std::string* lid = req_h.GetHeader("log-id")) cntl->set_log_id(strtoull(lid->c_str(), nullptr, 10));
     if (!FLAGS_http_header_of_user_ip.empty()) {
         if (const std::string* ip = req_h.GetHeader(FLAGS_http_header_of_user_ip)) {
@@ -377,11 +417,11 @@ void ProcessHttpRequest(InputMessageBase* msg_base) {
     msg.reset();
     if (!concurrency_added) server = nullptr;
     if (cntl->Failed()) {
-        SendHttpResponse(cntl, req, res, server, ms, start_us, keep_alive, http10);
+        SendHttpResponse(cntl, req, res, server, ms, start_us, keep_alive, http10, order, order_seq);
         return;
     }
-    Closure* done = NewCallback([cntl, req, res, server, ms, start_us, keep_alive, http10] {
-        SendHttpResponse(cntl, req, res, server, ms, start_us, keep_alive, http10);
+    Closure* done = NewCallback([cntl, req, res, server, ms, start_us, keep_alive, http10, order, order_seq] {
+        SendHttpResponse(cntl, req, res, server, ms, start_us, keep_alive, http10, order, order_seq);
     });
     CallServiceMethod(mp->service, mp->method, cntl, req, res, done);
 }

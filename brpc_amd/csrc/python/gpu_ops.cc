@@ -182,6 +182,18 @@ void bind_gpu_ops(py::module_& g) {
                                                 as_stream(stream)),
               "snappy_decompress_pieces");
     });
+    g.def("snappy_decompress_pieces_serial_launch", [](uintptr_t pieces, int n, uint32_t lo, uint32_t hi,
+                                                       uintptr_t err, uintptr_t stream) {
+        check(gpu::LaunchSnappyDecompressPiecesSerial((const gpu::SnappyPiece*)pieces, n, lo, hi, (int*)err,
+                                                      as_stream(stream)),
+              "snappy_decompress_pieces_serial");
+    });
+    g.def("snappy_decompress_pieces_stamped_launch", [](uintptr_t pieces, int n, uint32_t lo, uint32_t hi,
+                                                        uintptr_t err, uintptr_t stamps, uintptr_t stream) {
+        check(gpu::LaunchSnappyDecompressPiecesStamped((const gpu::SnappyPiece*)pieces, n, lo, hi, (int*)err,
+                                                       (uint64_t*)stamps, as_stream(stream)),
+              "snappy_decompress_pieces_stamped");
+    });
     g.def("snappy_compress_scratch_per_block", [] { return gpu::SnappyCompressScratchPerBlock(); });
     g.def("snappy_max_compressed_length", [](uint64_t n) { return gpu::SnappyMaxCompressedLength(n); });
     g.def("snappy_compress_launch", [](uintptr_t jobs, int n, uint32_t max_ulen, uintptr_t scratch, uintptr_t out_len,

@@ -309,7 +309,16 @@ void Controller::OnCallComplete(Call* c, int error_code, bool responded) {
         _lb->Feedback(info);
     }
     if (c->sending_sock) {
-        if (_connection_type == CONNECTION_TYPE_POOLED && responded && error_code == 0) {
+        if (_connection_type == CONNECTION_TYPE_POOLED && responded && error_code == 0 && _progressive_sink &&
+            !_progressive_sink->body_done()) {
+            // the body still streams over this connection: it rejoins the
+            // pool when the body is done, not with the response head
+            const SocketId sid = c->sending_sock->id();
+            _progressive_sink->SetOnBodyDone([sid] {
+                SocketUniquePtr s;
+                if (Socket::Address(sid, &s) == 0) s->ReturnToPool();
+            });
+        } else if (_connection_type == CONNECTION_TYPE_POOLED && responded && error_code == 0) {
             c->sending_sock->ReturnToPool();
         } else if (_connection_type == CONNECTION_TYPE_POOLED || _connection_type == CONNECTION_TYPE_SHORT) {
             c->sending_sock->SetFailed(EUNUSED, "short/pooled connection done");

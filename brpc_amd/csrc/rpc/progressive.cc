@@ -21,13 +21,15 @@ ProgressiveAttachment::~ProgressiveAttachment() {
     }
     SocketUniquePtr s;
     if (send_end && Socket::Address(_sid, &s) == 0) {
-        if (_before_http_1_1) {
-            s->SetFailed(ECLOSE, "end of progressive body (http/1.0)");  // body ends at close
-        } else {
-            Buf end;
-            end.append("0\r\n\r\n", 5);
-            s->Write(&end);
-        }
+        // HTTP/1.0: the body ends where the connection does, so half-close
+        // it once everything queued is written; HTTP/1.1: the last chunk
+        // (then the same half-close for "Connection: close")
+        Buf end;
+        if (!_before_http_1_1) end.append("0\r\n\r\n", 5);
+        WriteOptions opt;
+        opt.ignore_eovercrowded = true;
+        opt.shutdown_write_after = _before_http_1_1 || _shutdown_after_end;
+        s->Write(&end, &opt);
     }
     if (notify) notify->Run();
 }

@@ -42,11 +42,14 @@ public:
 
     // protocol internal: the header was sent (or the RPC failed)
     void MarkRPCAsDone(bool rpc_failed);
+    // The response said "Connection: close": half-close after the last chunk.
+    void set_shutdown_after_end() { _shutdown_after_end = true; }
 
 private:
     int write_chunk(Buf* frame);
     SocketId _sid;
     bool _before_http_1_1;
+    bool _shutdown_after_end = false;
     std::mutex _mu;
     bool _header_sent = false;
     bool _rpc_failed = false;

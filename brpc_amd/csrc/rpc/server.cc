@@ -204,12 +204,15 @@ const Server::MethodProperty* Server::FindMethodPropertyByURI(const std::string&
         }
         return mp;
     }
-    // builtin services with default method: /status -> status.default_method
+    // [service]/default_method: /status -> status.default_method. Only
+    // services that define default_method (the builtin pages) take it; an
+    // unknown method of any other service is not found (404), as in the
+    // reference's FindMethodPropertyByURIImpl (http_rpc_protocol.cpp:1040-1053)
     auto s = _services_by_short_name.find(parts[0]);
     if (s != _services_by_short_name.end()) {
         const pb::ServiceDescriptor* sd = s->second->GetDescriptor();
         if (sd->method_count() > 0) {
-            auto it = _methods.find(sd->full_name + "." + sd->method(0)->name);
+            auto it = _methods.find(sd->full_name + ".default_method");
             if (it != _methods.end()) {
                 if (unresolved) {
                     unresolved->clear();
