@@ -275,6 +275,15 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
     return v;
 }
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));
+    return v;
+}
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
     v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
@@ -320,6 +329,9 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(con
     lbyte* const cin = (lbyte*)lds;
     __attribute__((address_space(3))) uint16_t* const smap =
         (__attribute__((address_space(3))) uint16_t*)(lds + cin_cap);
+    // 64 slots of per-pass element starts, after the map
+    __attribute__((address_space(3))) uint32_t* const strip =
+        (__attribute__((address_space(3))) uint32_t*)(lds + cin_cap + 2 * ((hi + 7) & ~7u));
     {
         gbyte_c* g = as_global(static_cast<const uint8_t*>(pc.src) - mis);
         for (uint32_t o = lane * 16; o < end; o += kWave * 16)
@@ -383,25 +395,34 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(con
             bad = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(eb));
             break;
         }
-        // source map: short elements lane by lane, long ones by the wave
+        // source map, one output byte per lane: the iteration's output span
+        // in passes of 64 positions. Element starts are scattered into a
+        // 64-slot LDS strip, an inclusive DPP max-scan hands every lane the
+        // latest element that started at or before its position (or the
+        // carry from the previous pass), and one bpermute fetches that
+        // element's (u0, base). Cost per 64 output bytes, whatever the
+        // element lengths.
         const uint32_t base = kind == 0 ? (kLitFlag | (q + hdr)) : (u0 - off);
-        const bool is_long = marked && len > (uint32_t)kWave;
         const uint64_t td = stamps ? __builtin_amdgcn_s_memtime() : 0;
-        const uint32_t mylen = marked && !is_long ? len : 0;
-        const uint32_t maxlen = wave_max(mylen);
-        for (uint32_t j = 0; j < maxlen; ++j) {
-            if (j < mylen) smap[u0 + j] = (uint16_t)(base + j);
+        const uint32_t info = (u0 & 0xffff) | (base << 16);
+        const uint32_t span_end =
+            (uint32_t)__builtin_amdgcn_readlane((int)(u0 + len), (int)(63 - __builtin_clzll(mask)));
+        uint32_t carry = 0;
+        for (uint32_t P = upos; P < span_end; P += kWave) {
+            strip[lane] = 0;
+            if (marked && u0 >= P && u0 < P + kWave) strip[u0 - P] = (uint32_t)lane + 1;
+            // other lanes' stores: without the barrier the compiler may
+            // forward this lane's own 0 (one wave: s_barrier is free, and DS
+            // operations of a wave complete in order)
+            __syncthreads();
+            const uint32_t m = wave_incl_max(strip[lane]);
+            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m ? m - 1 : 0) << 2), (int)info);
+            const uint32_t e = m ? got : carry;
+            const uint32_t pos = P + (uint32_t)lane;
+            if (pos < span_end) smap[pos] = (uint16_t)((e >> 16) + (pos - (e & 0xffff)));
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)e, 63);
         }
-        uint64_t lm = __ballot(is_long);
-        while (lm) {
-            const int l = __builtin_ctzll(lm);
-            lm &= lm - 1;
-            const uint32_t lu0 = (uint32_t)__builtin_amdgcn_readlane((int)u0, l);
-            const uint32_t llen = (uint32_t)__builtin_amdgcn_readlane((int)len, l);
-            const uint32_t lbase = (uint32_t)__builtin_amdgcn_readlane((int)base, l);
-            for (uint32_t j = lane; j < llen; j += kWave) smap[lu0 + j] = (uint16_t)(lbase + j);
-        }
-        upos = (uint32_t)__builtin_amdgcn_readlane((int)(u0 + len), (int)(63 - __builtin_clzll(mask)));
+        upos = span_end;
         ip += p;
         if (stamps) {
             const uint64_t te = __builtin_amdgcn_s_memtime();
@@ -649,7 +670,17 @@ __device__ __forceinline__ O emit_literal(O o, S src, uint32_t len) {
         *o++ = (uint8_t)n;
         *o++ = (uint8_t)(n >> 8);
     }
-    for (uint32_t k = 0; k < len; ++k) o[k] = src[k];
+    // 4 source bytes per LDS round trip (lload32), written byte by byte
+    // (the output slot has any alignment; stores need no wait)
+    uint32_t k = 0;
+    for (; k + 4 <= len; k += 4) {
+        const uint32_t v = lload32(src + k);
+        o[k] = (uint8_t)v;
+        o[k + 1] = (uint8_t)(v >> 8);
+        o[k + 2] = (uint8_t)(v >> 16);
+        o[k + 3] = (uint8_t)(v >> 24);
+    }
+    for (; k < len; ++k) o[k] = src[k];
     return o + len;
 }
 
@@ -681,13 +712,22 @@ __device__ __forceinline__ O emit_copy(O o, uint32_t off, uint32_t len) {
     return emit_copy2(o, off, len);
 }
 
+// Unaligned 4/8-byte LDS reads as aligned dword reads + v_alignbyte: an
+// (aligned(1)) dereference compiles to one ds_read_u8 per byte, and the
+// compressor's serial probe loop waits on every one of them. The reads may
+// touch up to 7 bytes past the staged block (the LDS layout leaves them
+// readable; callers never use those bytes).
+typedef const __attribute__((address_space(3))) uint32_t lword_c;
 __device__ __forceinline__ uint32_t lload32(const lbyte* p) {
-    typedef uint32_t __attribute__((aligned(1))) u32u;
-    return *reinterpret_cast<const __attribute__((address_space(3))) u32u*>(p);
+    const uintptr_t a = (uintptr_t)p;
+    lword_c* w = (lword_c*)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
 }
 __device__ __forceinline__ uint64_t lload64(const lbyte* p) {
-    typedef uint64_t __attribute__((aligned(1))) u64u;
-    return *reinterpret_cast<const __attribute__((address_space(3))) u64u*>(p);
+    const uintptr_t a = (uintptr_t)p;
+    lword_c* w = (lword_c*)(a & ~(uintptr_t)3);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (uint32_t)(a & 3);
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
 }
 
 // Dynamic LDS: the block's input (in_cap bytes), then — kOutLds — the 64
@@ -853,7 +893,7 @@ int LaunchSnappyDecompressPiecesStamped(const SnappyPiece* pieces_dev, int n, ui
     if (lo < kParMax) {
         const uint32_t phi = std::min(hi, kParMax);
         const uint32_t cin_cap = (uint32_t)((SnappyMaxCompressedLength(phi) + 16 + 15) & ~15ull);
-        const uint32_t lds = cin_cap + 2 * ((phi + 7) & ~7u);
+        const uint32_t lds = cin_cap + 2 * ((phi + 7) & ~7u) + 4 * kWave;
         hipLaunchKernelGGL(snappy_decompress_pieces_par_kernel, dim3(n), dim3(kWave), lds, s, pieces_dev, n, lo, phi,
                            cin_cap, err_dev, stamps);
         if (hipGetLastError() != hipSuccess) return -1;

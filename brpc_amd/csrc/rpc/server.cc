@@ -1,5 +1,7 @@
 #include "rpc/server.h"
 
+#include <sys/stat.h>
+
 #include <signal.h>
 #include <unistd.h>
 
@@ -38,6 +40,7 @@ Server::~Server() {
     Stop(0);
     Join();
     ClearServices();
+    if (!_options.pid_file.empty()) unlink(_options.pid_file.c_str());
     if (_keytable_pool) fiber::keytable_pool_destroy(_keytable_pool);
     if (_options.session_local_data_factory) {
         for (void* d : _session_pool) _options.session_local_data_factory->DestroyData(d);
@@ -65,6 +68,41 @@ int Server::AddServiceInternal(Service* s, bool is_builtin, ServiceOwnership own
         LOG(ERROR) << "Service " << sd->full_name << " already added";
         return -1;
     }
+    // the restful mappings are checked before anything is registered, so a
+    // bad mapping leaves no trace of the service (reference
+    // Server::AddServiceInternal + RestfulMap::AddMethod)
+    std::vector<std::pair<std::string, std::string>> maps;
+    parse_restful(restful, &maps);
+    std::vector<std::pair<std::string, std::string>> resolved;
+    for (auto& m : maps) {
+        std::string target = m.second;
+        if (target.find('.') == std::string::npos) target = sd->full_name + "." + target;
+        const pb::MethodDescriptor* found = nullptr;
+        for (int i = 0; i < sd->method_count(); ++i) {
+            if (sd->full_name + "." + sd->method(i)->name == target) found = sd->method(i);
+        }
+        if (!found) {
+            LOG(ERROR) << "restful mapping to unknown method " << target;
+            return -1;
+        }
+        if (m.first.empty() || m.first[0] != '/') {
+            LOG(ERROR) << "restful path `" << m.first << "' must start with '/'";
+            return -1;
+        }
+        for (auto& r : _restful) {
+            if (r.first == m.first) {
+                LOG(ERROR) << "restful path `" << m.first << "' is already mapped to " << r.second;
+                return -1;
+            }
+        }
+        for (auto& r : resolved) {
+            if (r.first == m.first) {
+                LOG(ERROR) << "restful path `" << m.first << "' is mapped twice";
+                return -1;
+            }
+        }
+        resolved.emplace_back(m.first, target);
+    }
     ServiceProperty sp;
     sp.is_builtin_service = is_builtin;
     sp.ownership = ownership;
@@ -82,18 +120,9 @@ int Server::AddServiceInternal(Service* s, bool is_builtin, ServiceOwnership own
         mp.status = std::make_shared<MethodStatus>();
         _methods[sd->full_name + "." + md->name] = mp;
     }
-    std::vector<std::pair<std::string, std::string>> maps;
-    parse_restful(restful, &maps);
-    for (auto& m : maps) {
-        std::string target = m.second;
-        if (target.find('.') == std::string::npos) target = sd->full_name + "." + target;
-        auto it = _methods.find(target);
-        if (it == _methods.end()) {
-            LOG(ERROR) << "restful mapping to unknown method " << target;
-            return -1;
-        }
-        it->second.http_url = m.first;
-        _restful.emplace_back(m.first, target);
+    for (auto& r : resolved) {
+        _methods[r.second].http_url = r.first;
+        _restful.push_back(r);
     }
     return 0;
 }
@@ -113,6 +142,10 @@ int Server::RemoveService(Service* service) {
     auto it = _services.find(sd->full_name);
     if (it == _services.end()) return -1;
     for (int i = 0; i < sd->method_count(); ++i) _methods.erase(sd->full_name + "." + sd->method(i)->name);
+    for (auto r = _restful.begin(); r != _restful.end();) {
+        if (r->second.compare(0, sd->full_name.size() + 1, sd->full_name + ".") == 0) r = _restful.erase(r);
+        else ++r;
+    }
     _services_by_short_name.erase(sd->name);
     if (_first_service == service) _first_service = nullptr;
     if (it->second.ownership == SERVER_OWNS_SERVICE) delete it->second.service;
@@ -252,6 +285,16 @@ std::unique_ptr<Acceptor> Server::BuildAcceptor(bool builtin_only) {
     if (!_options.enabled_protocols.empty()) enabled = split_string_any(_options.enabled_protocols, " ,;");
     std::vector<std::pair<ProtocolType, Protocol>> protocols;
     ListProtocols(&protocols);
+    // every enabled name must be a server protocol (the reference refuses to
+    // start with unknown ones, server.cpp:569-612)
+    for (auto& e : enabled) {
+        bool known = false;
+        for (auto& p : protocols) known |= p.second.support_server() && e == p.second.name;
+        if (!known) {
+            LOG(ERROR) << "ServerOptions.enabled_protocols has an unknown protocol `" << e << "'";
+            return nullptr;
+        }
+    }
     for (auto& p : protocols) {
         if (!p.second.support_server()) continue;
         if (builtin_only && p.first != PROTOCOL_HTTP && p.first != PROTOCOL_H2) continue;
@@ -379,7 +422,18 @@ int Server::StartInternal(const EndPoint& ep, const ServerOptions* opt) {
             if (_internal_am) _internal_am->StartAccept(ifd, _options.idle_timeout_sec);
         }
     }
-    if (!_options.pid_file.empty()) std::ofstream(_options.pid_file) << getpid();
+    if (!_options.pid_file.empty()) {
+        // parent directories first, like the reference's PutPidFileIfNeeded
+        for (size_t pos = _options.pid_file.find('/', 1); pos != std::string::npos;
+             pos = _options.pid_file.find('/', pos + 1)) {
+            const std::string dir = _options.pid_file.substr(0, pos);
+            if (mkdir(dir.c_str(), 0755) != 0 && errno != EEXIST) {
+                LOG(WARNING) << "Fail to create " << dir << " for the pid file";
+                break;
+            }
+        }
+        std::ofstream(_options.pid_file) << getpid();
+    }
     _start_us = realtime_us();
     _status = RUNNING;
     g_running_servers.fetch_add(1);

@@ -97,7 +97,7 @@ public:
     int RemoveService(Service* service);
     void ClearServices();
     Service* FindServiceByFullName(const std::string& full_name) const;
-    Service* FindServiceByName(const std::string& name) const;
+    Service* FindServiceByName(const std::string& name) const;            // short name: "EchoService"
     const MethodProperty* FindMethodPropertyByFullName(const std::string& service_full_name,
                                                        const std::string& method_name) const;
     const MethodProperty* FindMethodPropertyByFullName(const std::string& full_method_name) const;
