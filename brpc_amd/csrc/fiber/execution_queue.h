@@ -3,11 +3,16 @@
 // first producer on an idle queue starts the consumer fiber. High-priority
 // tasks run before normal ones. After stop(), the consumer is invoked once
 // more with iterator.is_queue_stopped() == true, then join() returns.
+// execute() can hand back a TaskHandle; cancel(handle) removes the task if
+// the consumer has not taken it yet (execution_queue_cancel, reference
+// bthread/execution_queue.h:206: 0 cancelled, 1 already running or done).
 // Used by Streaming RPC receivers (batched on_received_messages) and by the
 // GPU transfer engine.
 #pragma once
 
+#include <algorithm>
 #include <cerrno>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -37,6 +42,12 @@ public:
         bool _stopped;
     };
     typedef int (*ExecuteFn)(void* meta, Iterator& iter);
+    // Names a task for cancel(); default-constructed handles name nothing.
+    struct TaskHandle {
+        uint64_t seq = 0;
+        bool high = false;
+        std::weak_ptr<ExecutionQueue> queue;
+    };
     struct Options {
         Attr attr;
         size_t max_batch = 128;
@@ -48,8 +59,25 @@ public:
     }
     ~ExecutionQueue() {}
 
-    int execute(const T& t, bool high_priority = false) { return execute_impl(T(t), high_priority); }
-    int execute(T&& t, bool high_priority = false) { return execute_impl(std::move(t), high_priority); }
+    int execute(const T& t, bool high_priority = false, TaskHandle* handle = nullptr) {
+        return execute_impl(T(t), high_priority, handle);
+    }
+    int execute(T&& t, bool high_priority = false, TaskHandle* handle = nullptr) {
+        return execute_impl(std::move(t), high_priority, handle);
+    }
+    // 0: the task was removed before the consumer took it; 1: it is running
+    // or ran already; -1: the handle names no task of this queue.
+    int cancel(const TaskHandle& h) {
+        std::shared_ptr<ExecutionQueue> q = h.queue.lock();
+        if (q.get() != this || h.seq == 0) return -1;
+        std::lock_guard<std::mutex> g(_mu);
+        std::deque<Node>& d = h.high ? _high : _normal;
+        auto it = std::lower_bound(d.begin(), d.end(), h.seq,
+                                   [](const Node& n, uint64_t seq) { return n.seq < seq; });
+        if (it == d.end() || it->seq != h.seq) return 1;
+        d.erase(it);
+        return 0;
+    }
 
     void stop() {
         bool start_consumer = false;
@@ -81,12 +109,23 @@ private:
     ExecutionQueue(ExecuteFn fn, void* meta, const Options& opt)
         : _fn(fn), _meta(meta), _opt(opt), _running(false), _stopped(false), _stopped_delivered(false), _done(1) {}
 
-    int execute_impl(T&& t, bool high) {
+    struct Node {
+        T task;
+        uint64_t seq;
+    };
+
+    int execute_impl(T&& t, bool high, TaskHandle* handle) {
         bool start_consumer = false;
         {
             std::lock_guard<std::mutex> g(_mu);
             if (_stopped) return EINVAL;
-            (high ? _high : _normal).push_back(std::move(t));
+            const uint64_t seq = ++_next_seq;
+            (high ? _high : _normal).push_back(Node{std::move(t), seq});
+            if (handle) {
+                handle->seq = seq;
+                handle->high = high;
+                handle->queue = this->shared_from_this();
+            }
             if (!_running) {
                 _running = true;
                 start_consumer = true;
@@ -115,14 +154,14 @@ private:
                 batch.clear();
                 size_t take = 0;
                 while (!q->_high.empty() && take < q->_opt.max_batch) {
-                    batch.push_back(std::move(q->_high.front()));
-                    q->_high.erase(q->_high.begin());
+                    batch.push_back(std::move(q->_high.front().task));
+                    q->_high.pop_front();
                     ++take;
                 }
-                if (take < q->_opt.max_batch && !q->_normal.empty()) {
-                    size_t n = std::min(q->_normal.size(), q->_opt.max_batch - take);
-                    for (size_t i = 0; i < n; ++i) batch.push_back(std::move(q->_normal[i]));
-                    q->_normal.erase(q->_normal.begin(), q->_normal.begin() + n);
+                while (take < q->_opt.max_batch && !q->_normal.empty()) {
+                    batch.push_back(std::move(q->_normal.front().task));
+                    q->_normal.pop_front();
+                    ++take;
                 }
                 if (batch.empty()) {
                     if (q->_stopped && !q->_stopped_delivered) {
@@ -151,8 +190,9 @@ private:
     void* _meta;
     Options _opt;
     mutable std::mutex _mu;
-    std::vector<T> _high;
-    std::vector<T> _normal;
+    std::deque<Node> _high;
+    std::deque<Node> _normal;
+    uint64_t _next_seq = 0;
     bool _running;
     bool _stopped;
     bool _stopped_delivered;

@@ -657,6 +657,24 @@ __device__ __forceinline__ uint64_t load64(gbyte_c* p) {
     return *reinterpret_cast<const __attribute__((address_space(1))) u64_unaligned*>(p);
 }
 
+// Unaligned 4/8-byte LDS reads as aligned dword reads + v_alignbyte: an
+// (aligned(1)) dereference compiles to one ds_read_u8 per byte, and the
+// compressor's serial probe loop waits on every one of them. The reads may
+// touch up to 7 bytes past the staged block (the LDS layout leaves them
+// readable; callers never use those bytes).
+typedef const __attribute__((address_space(3))) uint32_t lword_c;
+__device__ __forceinline__ uint32_t lload32(const lbyte* p) {
+    const uintptr_t a = (uintptr_t)p;
+    lword_c* w = (lword_c*)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
+}
+__device__ __forceinline__ uint64_t lload64(const lbyte* p) {
+    const uintptr_t a = (uintptr_t)p;
+    lword_c* w = (lword_c*)(a & ~(uintptr_t)3);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (uint32_t)(a & 3);
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+}
+
 template <typename O, typename S>
 __device__ __forceinline__ O emit_literal(O o, S src, uint32_t len) {
     const uint32_t n = len - 1;
@@ -712,23 +730,6 @@ __device__ __forceinline__ O emit_copy(O o, uint32_t off, uint32_t len) {
     return emit_copy2(o, off, len);
 }
 
-// Unaligned 4/8-byte LDS reads as aligned dword reads + v_alignbyte: an
-// (aligned(1)) dereference compiles to one ds_read_u8 per byte, and the
-// compressor's serial probe loop waits on every one of them. The reads may
-// touch up to 7 bytes past the staged block (the LDS layout leaves them
-// readable; callers never use those bytes).
-typedef const __attribute__((address_space(3))) uint32_t lword_c;
-__device__ __forceinline__ uint32_t lload32(const lbyte* p) {
-    const uintptr_t a = (uintptr_t)p;
-    lword_c* w = (lword_c*)(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
-}
-__device__ __forceinline__ uint64_t lload64(const lbyte* p) {
-    const uintptr_t a = (uintptr_t)p;
-    lword_c* w = (lword_c*)(a & ~(uintptr_t)3);
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = (uint32_t)(a & 3);
-    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
-}
 
 // Dynamic LDS: the block's input (in_cap bytes), then — kOutLds — the 64
 // lanes' output slots of `slot` bytes each; otherwise the slots live in the

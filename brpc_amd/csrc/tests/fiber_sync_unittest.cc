@@ -338,6 +338,56 @@ TEST(FiberSync, execution_queue_high_priority_and_stop) {
     EXPECT_NE(q->execute(7), 0);  // stopped queues refuse work
 }
 
+TEST(FiberSync, execution_queue_cancel_before_the_consumer_takes_it) {
+    struct Meta {
+        std::vector<int> seen;
+    } meta;
+    Mutex gate;
+    gate.lock();
+    struct Ctx {
+        Meta* m;
+        Mutex* gate;
+    } ctx{&meta, &gate};
+    auto q = ExecutionQueue<int>::Create(
+        [](void* p, ExecutionQueue<int>::Iterator& it) -> int {
+            Ctx* c = static_cast<Ctx*>(p);
+            if (it.is_queue_stopped()) return 0;
+            for (; it; ++it) {
+                if (*it == 0) {
+                    c->gate->lock();
+                    c->gate->unlock();
+                }
+                c->m->seen.push_back(*it);
+            }
+            return 0;
+        },
+        &ctx);
+    ExecutionQueue<int>::TaskHandle h0, h1, h2, h3, hp;
+    ASSERT_EQ(q->execute(0, false, &h0), 0);
+    ::usleep(10000);  // the consumer holds task 0
+    q->execute(1, false, &h1);
+    q->execute(2, false, &h2);
+    q->execute(3, false, &h3);
+    q->execute(50, true, &hp);
+    EXPECT_EQ(q->cancel(h2), 0);    // queued: removed
+    EXPECT_EQ(q->cancel(h2), 1);    // not there any more
+    EXPECT_EQ(q->cancel(hp), 0);    // high-priority tasks cancel too
+    EXPECT_EQ(q->cancel(h0), 1);    // already running
+    EXPECT_EQ(q->cancel(ExecutionQueue<int>::TaskHandle()), -1);
+    auto other = ExecutionQueue<int>::Create([](void*, ExecutionQueue<int>::Iterator&) -> int { return 0; }, nullptr);
+    EXPECT_EQ(other->cancel(h1), -1);  // a handle of another queue
+    gate.unlock();
+    q->stop();
+    q->join();
+    ASSERT_EQ(meta.seen.size(), 3u);
+    EXPECT_EQ(meta.seen[0], 0);
+    EXPECT_EQ(meta.seen[1], 1);
+    EXPECT_EQ(meta.seen[2], 3);
+    EXPECT_EQ(q->cancel(h3), 1);  // ran
+    other->stop();
+    other->join();
+}
+
 TEST(FiberSync, timer_add_and_delete) {
     std::atomic<int> fired{0};
     TimerId a, b;
