@@ -225,15 +225,28 @@ def test_structurally_sparse_bodies_stay_on_the_host(dev):
         native.gpu.disable_json_index()
 
 
+def _jsonout_fixture(tmp_path):
+    """The reference's test/jsonout document and its schema (message.proto),
+    shipped with the tests as tests/fixtures/ref_jsonout.tar.gz so the GPU
+    parity check runs wherever the tests do (the reference tree is not on
+    the GPU box). Returns (directory, document bytes)."""
+    import tarfile
+    with tarfile.open(os.path.join(os.path.dirname(__file__), "fixtures", "ref_jsonout.tar.gz")) as t:
+        for name in ("jsonout", "message.proto"):
+            m = t.getmember(name)
+            assert m.isfile()
+            with open(os.path.join(tmp_path, name), "wb") as f:
+                f.write(t.extractfile(m).read())
+    with open(os.path.join(tmp_path, "jsonout"), "rb") as f:
+        return str(tmp_path), f.read()
+
+
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.path.isfile("/root/reference/test/jsonout"), reason="reference fixture not present")
-def test_reference_jsonout_fixture_through_device_index(dev):
+def test_reference_jsonout_fixture_through_device_index(dev, tmp_path):
     """The reference's 98 KB test/jsonout document (gss_us_res_t) parsed with
     the GPU structural index gives exactly the CPU parser's message."""
     from brpc_amd import native
-    ref = "/root/reference/test"
-    with open(os.path.join(ref, "jsonout"), "rb") as f:
-        text = f.read()
+    ref, text = _jsonout_fixture(tmp_path)
     cpu = native.json_proto_roundtrip(ref, "message.proto", "gss.message.gss_us_res_t", text, False)
     native.gpu.enable_json_index(0, 4096)
     try:
