@@ -741,9 +741,9 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
                                                                 int* __restrict__ err, uint32_t in_cap,
                                                                 uint32_t slot_bytes) {
     __shared__ uint16_t table[kWave * kHashEntries];
-    __shared__ uint32_t first_pos[kFirstEntries];
+    __shared__ __attribute__((aligned(16))) uint32_t first_pos[kFirstEntries];
     __shared__ uint32_t sizes[kWave];
-    extern __shared__ uint8_t dyn_lds[];
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
     const int blk = blockIdx.x;
     if (blk >= n) return;
     const int lane = threadIdx.x;
@@ -820,11 +820,14 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         sizes[lane] = match(as_global(gscratch + (size_t)lane * SnappyCompressSlot()));
     }
     __syncthreads();
-    // varint header + exclusive prefix sum of the 64 slot sizes
+    // varint header + prefix sum of the 64 slot sizes (DPP scan: lane k
+    // holds slot k's size)
     uint32_t hdr = 1;
     for (uint32_t u = ulen; u >= 0x80; u >>= 7) ++hdr;
-    uint32_t total = hdr;
-    for (int k = 0; k < kWave; ++k) total += sizes[k];
+    const uint32_t my_size = sizes[lane];
+    const uint32_t incl = wave_incl_sum(my_size);
+    const uint32_t total = hdr + (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+    const uint32_t my_off = hdr + incl - my_size;
     gbyte* dst = as_global(job.dst);
     if (total > job.dst_cap) {
         if (lane == 0) {
@@ -833,22 +836,51 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         }
         return;
     }
-    if (lane < (int)hdr) {
-        uint32_t u = ulen >> (7 * lane);
-        dst[lane] = (uint8_t)((u & 0x7f) | (lane + 1 < (int)hdr ? 0x80 : 0));
-    }
-    // coalesced copy-out: the wave moves one slot at a time
-    uint32_t at = hdr;
-    for (int k = 0; k < kWave; ++k) {
-        const uint32_t sz = sizes[k];
-        if (kOutLds) {
-            const lbyte* src = lds_slots + (size_t)k * slot_bytes;
-            for (uint32_t j = lane; j < sz; j += kWave) dst[at + j] = src[j];
-        } else {
-            gbyte_c* src = as_global(gscratch + (size_t)k * SnappyCompressSlot());
-            for (uint32_t j = lane; j < sz; j += kWave) dst[at + j] = src[j];
+    if (kOutLds && total <= (uint32_t)sizeof(first_pos) && ((uintptr_t)job.dst & 15) == 0) {
+        // assemble the stream in LDS (the earliest-position table is free
+        // now): every lane moves its own slot, 16 bytes per read, then the
+        // wave streams the whole block out with coalesced 16-byte stores
+        // instead of one wave step per slot
+        __syncthreads();
+        lbyte* const stage = (lbyte*)first_pos;
+        if (lane < (int)hdr) {
+            const uint32_t u = ulen >> (7 * lane);
+            stage[lane] = (uint8_t)((u & 0x7f) | (lane + 1 < (int)hdr ? 0x80 : 0));
         }
-        at += sz;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const lbyte* src = lds_slots + (size_t)lane * slot_bytes;  // 16-byte aligned
+        for (uint32_t j = 0; j < my_size; j += 16) {
+            const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(src + j);
+            const uint32_t n = min(16u, my_size - j);
+#pragma unroll
+            for (uint32_t b = 0; b < 16; ++b) {
+                if (b < n) stage[my_off + j + b] = (uint8_t)(v[b >> 2] >> (8 * (b & 3)));
+            }
+        }
+        __syncthreads();
+        const uint32_t vec_end = total & ~15u;
+        for (uint32_t o = (uint32_t)lane * 16; o < vec_end; o += kWave * 16)
+            *reinterpret_cast<__attribute__((address_space(1))) u32x4*>(dst + o) =
+                *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(stage + o);
+        for (uint32_t o = vec_end + lane; o < total; o += kWave) dst[o] = stage[o];
+    } else {
+        if (lane < (int)hdr) {
+            uint32_t u = ulen >> (7 * lane);
+            dst[lane] = (uint8_t)((u & 0x7f) | (lane + 1 < (int)hdr ? 0x80 : 0));
+        }
+        // coalesced copy-out: the wave moves one slot at a time
+        uint32_t at = hdr;
+        for (int k = 0; k < kWave; ++k) {
+            const uint32_t sz = (uint32_t)__builtin_amdgcn_readlane((int)my_size, k);
+            if (kOutLds) {
+                const lbyte* src = lds_slots + (size_t)k * slot_bytes;
+                for (uint32_t j = lane; j < sz; j += kWave) dst[at + j] = src[j];
+            } else {
+                gbyte_c* src = as_global(gscratch + (size_t)k * SnappyCompressSlot());
+                for (uint32_t j = lane; j < sz; j += kWave) dst[at + j] = src[j];
+            }
+            at += sz;
+        }
     }
     if (lane == 0) {
         out_len[blk] = total;

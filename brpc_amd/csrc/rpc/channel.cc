@@ -197,6 +197,12 @@ void Channel::CallMethod(const pb::MethodDescriptor* method, RpcController* cont
         if (done) done->Run();
         return;
     }
+    // canceled before the call (StartCancel on its call_id()): nothing is
+    // sent, the call ends with ECANCELED
+    if (cntl->Failed() && cntl->ErrorCode() == ECANCELED) {
+        if (done) done->Run();
+        return;
+    }
     // Controller-level settings override the channel's only if set.
     if (cntl->_timeout_ms == Controller::UNSET_MAGIC) cntl->_timeout_ms = _options.timeout_ms;
     if (cntl->_backup_request_ms == Controller::UNSET_MAGIC) cntl->_backup_request_ms = _options.backup_request_ms;

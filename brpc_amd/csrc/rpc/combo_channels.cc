@@ -42,7 +42,9 @@ struct PCall {
     int fail_limit = 0, success_limit = 0;
     bool gather = false;  // ParallelChannelOptions::gather_response_attachments
     bool finished = false;
+    bool canceled = false;  // the parent was canceled
     int first_error = 0;
+    int unified_error = 0;  // the failed sub calls' common code (ECANCELED aside), or ETOOMANYFAILS
     std::string first_error_text;
     std::atomic<int> refs{1};
 
@@ -72,6 +74,7 @@ void finish_parent(PCall* pc, int error_code, const std::string& text) {
     cntl->_end_us = monotonic_us();
     Closure* done = pc->done;
     const fiber::CallId cid = pc->cid;
+    cntl->_ended_id = cid;
     __atomic_store_n(&cntl->_correlation_id.value, 0, __ATOMIC_RELEASE);  // pairs with Controller::Join
     // cancel sub calls still in flight; their done closures only unref
     for (auto& s : pc->subs) {
@@ -114,15 +117,23 @@ void on_sub_done(SubState* s) {
                     ++pc->nsuccess;
                 } else {
                     ++pc->nfail;
+                    const int sec = s->cntl.ErrorCode();
                     if (!pc->first_error) {
-                        pc->first_error = s->cntl.ErrorCode();
+                        pc->first_error = sec;
                         pc->first_error_text = s->cntl.ErrorText();
                     }
+                    if (sec != ECANCELED) {
+                        if (pc->unified_error == 0) pc->unified_error = sec;
+                        else if (pc->unified_error != sec) pc->unified_error = ETOOMANYFAILS;
+                    }
                 }
-                if (pc->nfail >= pc->fail_limit) {
+                if (pc->nfail >= pc->fail_limit || (pc->canceled && pc->ndone == pc->nlaunched)) {
                     pc->finished = true;
                     complete = true;
-                    ec = pc->nfail == 1 && pc->nlaunched == 1 ? pc->first_error : ETOOMANYFAILS;
+                    // the reference's unified code (parallel_channel.cpp:352-366):
+                    // the failed sub calls' common error, ECANCELED when they
+                    // were all canceled, ETOOMANYFAILS when they differ
+                    ec = pc->canceled ? ECANCELED : (pc->unified_error ? pc->unified_error : ECANCELED);
                     et = std::to_string(pc->nfail) + "/" + std::to_string(pc->nlaunched) +
                          " sub calls failed (fail_limit=" + std::to_string(pc->fail_limit) +
                          "), first: [E" + std::to_string(pc->first_error) + "] " + pc->first_error_text;
@@ -140,13 +151,31 @@ void on_sub_done(SubState* s) {
 int OnParallelError(fiber::CallId id, void* data, int error_code, const std::string& text) {
     PCall* pc = static_cast<PCall*>(data);
     // cancellation / timeout of the parent: cancel the sub calls and let
-    // them complete the parent through the fail path
+    // them complete the parent through the fail path. The id is released
+    // first: a canceled sub call may complete inline, and the last one
+    // finishes the parent, which locks this id.
+    pc->refs.fetch_add(1);
+    if (error_code == ECANCELED) {
+        std::lock_guard<std::mutex> g(pc->mu);
+        pc->canceled = true;
+    }
+    fiber::call_id_unlock(id);
     for (auto& s : pc->subs) {
         if (s->launched) s->cntl.StartCancel();
     }
+    pc->unref();
     (void)error_code;
     (void)text;
-    return fiber::call_id_unlock(id);
+    return 0;
+}
+
+// A controller canceled before CallMethod (StartCancel on its call_id()):
+// the combo call ends at once with ECANCELED and issues no sub call, like a
+// plain Channel's.
+bool canceled_before_call(Controller* cntl, Closure* done) {
+    if (!cntl->Failed() || cntl->ErrorCode() != ECANCELED) return false;
+    if (done) done->Run();
+    return true;
 }
 
 }  // namespace
@@ -190,6 +219,7 @@ void ParallelChannel::CallMethod(const pb::MethodDescriptor* method, RpcControll
                                  const pb::Message* request, pb::Message* response, Closure* done) {
     Controller* cntl = static_cast<Controller*>(controller_base);
     cntl->_begin_us = monotonic_us();
+    if (canceled_before_call(cntl, done)) return;
     const int n = (int)_subs.size();
     PCall* pc = new PCall;
     pc->cntl = cntl;
@@ -519,6 +549,8 @@ struct SelectiveChannel::Call {
     int inflight = 0;
     fiber::TimerId backup_timer = 0;
     bool backup_cancelled = false;
+    bool canceled = false;            // under mu: the parent was canceled
+    std::vector<Controller*> live;    // under mu: attempts in flight
     std::atomic<int> refs{1};
     void unref() {
         if (refs.fetch_sub(1) == 1) delete this;
@@ -668,6 +700,7 @@ SelectiveChannel::Call::Attempt* SelectiveChannel::Call::prepare(int idx) {
     ++inflight;
     ++attempts;
     tried.push_back(idx);
+    live.push_back(&a->sub_cntl);
     return a;
 }
 
@@ -693,7 +726,13 @@ void SelectiveChannel::Call::on_attempt_done(Attempt* a) {
     {
         std::lock_guard<std::mutex> g(mu);
         --inflight;
-        if (!finished) {
+        live.erase(std::remove(live.begin(), live.end(), &a->sub_cntl), live.end());
+        if (!finished && canceled) {
+            if (inflight == 0) {  // the parent was canceled: no retry, no late success
+                finish(ECANCELED, "RPC canceled", nullptr);
+                complete = true;
+            }
+        } else if (!finished) {
             if (!a->sub_cntl.Failed()) {
                 cntl->response_attachment() = a->sub_cntl.response_attachment();
                 finish(0, "", res.get());
@@ -732,6 +771,7 @@ void SelectiveChannel::Call::on_attempt_done(Attempt* a) {
         Closure* d = done;
         const fiber::CallId id = cid;
         const bool drop_timer_ref = backup_cancelled;
+        cntl->_ended_id = id;
         __atomic_store_n(&cntl->_correlation_id.value, 0, __ATOMIC_RELEASE);  // pairs with Controller::Join
         if (fiber::call_id_lock(id, nullptr) == 0) fiber::call_id_unlock_and_destroy(id);
         if (d) d->Run();
@@ -760,14 +800,30 @@ static void selective_backup(void* arg) {
     });
 }
 
-static int OnSelectiveError(fiber::CallId id, void* data, int, const std::string&) {
-    return fiber::call_id_unlock(id);  // attempts carry their own timeouts
+static int OnSelectiveError(fiber::CallId id, void* data, int error_code, const std::string&) {
+    SelectiveChannel::Call* c = static_cast<SelectiveChannel::Call*>(data);
+    if (error_code != ECANCELED) return fiber::call_id_unlock(id);  // attempts carry their own timeouts
+    // canceled: cancel the attempts in flight; the last one to return
+    // finishes the call with ECANCELED (the id is released first, an
+    // attempt may complete inline)
+    std::vector<Controller*> live;
+    c->refs.fetch_add(1);
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        c->canceled = true;
+        live = c->live;
+    }
+    fiber::call_id_unlock(id);
+    for (Controller* sc : live) sc->StartCancel();
+    c->unref();
+    return 0;
 }
 
 void SelectiveChannel::CallMethod(const pb::MethodDescriptor* method, RpcController* controller,
                                   const pb::Message* request, pb::Message* response, Closure* done) {
     Controller* cntl = static_cast<Controller*>(controller);
     cntl->_begin_us = monotonic_us();
+    if (canceled_before_call(cntl, done)) return;
     if (cntl->timeout_ms() == Controller::UNSET_MAGIC) cntl->set_timeout_ms(_options.timeout_ms);
     Call* c = new Call{this, cntl, method, request, response, done};
     fiber::call_id_create(&c->cid, c, OnSelectiveError);

@@ -88,6 +88,7 @@ void Controller::Reset() {
     _has_request_code = false;
     _request_id.clear();
     _correlation_id = fiber::CallId{0};
+    _ended_id = fiber::CallId{0};
     _timeout_id = 0;
     _backup_id = 0;
     _begin_us = _begin_real_us = _end_us = 0;
@@ -145,6 +146,9 @@ void Controller::SetFailed(int error_code, const char* fmt, ...) {
 }
 
 fiber::CallId Controller::call_id() {
+    // after the call ended, the same (now destroyed) id: StartCancel on it
+    // does nothing, as in the reference, instead of failing a finished call
+    if (_correlation_id.value == 0 && _ended_id.value != 0) return _ended_id;
     if (_correlation_id.value == 0) {
         if (fiber::call_id_create(&_correlation_id, this, HandleError) != 0) {
             LOG(FATAL) << "Fail to create call id";
@@ -350,6 +354,7 @@ void Controller::EndRPC(fiber::CallId id) {
     Closure* done = _done;
     _done = nullptr;
     const fiber::CallId cid = _correlation_id;
+    _ended_id = cid;
     __atomic_store_n(&_correlation_id.value, 0, __ATOMIC_RELEASE);  // pairs with Join()
     // After this, a sync caller may destroy *this.
     fiber::call_id_unlock_and_destroy(cid);

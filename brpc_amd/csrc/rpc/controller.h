@@ -224,6 +224,7 @@ public:
     bool _has_request_code = false;
     std::string _request_id;
     fiber::CallId _correlation_id{0};
+    fiber::CallId _ended_id{0};  // the id of the finished call: call_id() keeps naming it (cancels are no-ops)
     fiber::TimerId _timeout_id = 0;
     fiber::TimerId _backup_id = 0;
     int64_t _begin_us = 0;
