@@ -364,20 +364,28 @@ int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, bool
             g_busy.fetch_add(1, std::memory_order_relaxed);
             return 1;
         }
+        // the copy-in folds the checksum while the bytes pass through
+        // registers: one pass over HBM instead of two
         Segment seg{src, p, len};
-        if (BatchedCopy(&seg, 1, g_device) != 0) return -1;
+        uint32_t crc = 0;
+        if (BatchedCopy(&seg, 1, g_device, with_crc ? &crc : nullptr) != 0) return -1;
         g_copied_in.fetch_add(1, std::memory_order_relaxed);
         src = static_cast<const char*>(p);
+        if (with_crc) {
+            d->set_crc32c(crc);
+            d->set_has_crc(true);
+        }
     } else {
         hold.append_block(block, offset, len);
-    }
-    if (with_crc) {
-        const void* p = src;
-        uint64_t l64 = len;
-        uint32_t crc = 0;
-        if (Crc32cDevice(&p, &l64, 1, &crc, g_device) != 0) return -1;
-        d->set_crc32c(crc);
-        d->set_has_crc(true);
+        if (with_crc) {
+            // checksum-only segment (null dst) through the copy engine, so
+            // concurrent senders' checksums share one launch and one event
+            Segment seg{src, nullptr, len};
+            uint32_t crc = 0;
+            if (BatchedCopy(&seg, 1, g_device, &crc) != 0) return -1;
+            d->set_crc32c(crc);
+            d->set_has_crc(true);
+        }
     }
     uint32_t slot = 0;
     uint64_t seq = 0;
