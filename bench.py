@@ -482,6 +482,41 @@ def main():
                 finally:
                     disable()
 
+    # Device-body codec legs (the HBM-resident body path): the
+    # 64 KiB payload is one serialized EchoRequest living in HBM. The sender
+    # snappy-encodes it on the device (the cross-RPC codec batch), lends the
+    # encoded block over xGMI; the receiver decodes it straight out of the
+    # lent region into its own HBM and pb_scan-indexes it there; the server
+    # echoes it back the same way (gpu/device_codec.h). The host touches the
+    # RpcMeta and the block table only. Incompressible bodies (random) are
+    # lent raw after the encode and still indexed on arrival. Every 64th
+    # reply is checked: bytes and the device field table.
+    rdb = {}
+    if dev_payload and not a.skip_64k and not a.skip_grpc:
+        for body in bodies:
+            wld = EchoWorkload("device_snappy_64KB_" + body, request_size=16, attachment_size=65536,
+                               device_attachment=True, requests_per_step=max(1, a.requests_per_step_grpc * 4))
+            od = wld.press_options(peer, gpu_device=topo.device)
+            od.update({"concurrency": a.concurrency, "attachment_body": body, "attachment_pb": True,
+                       "device_scan": True, "device_compress": 1, "check_echo": True, "check_every": 64})
+            c0, x0, b0 = native.gpu.device_codec_stats(), native.gpu.xgmi_stats(), native.gpu.codec_batch_stats()
+            r = timed_leg(wld, a.steps, a.warmup, od)
+            c1, x1, b1 = native.gpu.device_codec_stats(), native.gpu.xgmi_stats(), native.gpu.codec_batch_stats()
+            enc_in = c1["encoded_bytes"] - c0["encoded_bytes"]
+            enc_out = c1["encoded_out_bytes"] - c0["encoded_out_bytes"]
+            nl = b1["launches"] - b0["launches"]
+            r["device"] = {
+                "encodes": c1["encodes"] - c0["encodes"], "decodes": c1["decodes"] - c0["decodes"],
+                "scans": c1["scans"] - c0["scans"],
+                "lent_encoded": x1["compressed_sent"] - x0["compressed_sent"],
+                "lent_raw_incompressible": x1["compress_skipped_raw"] - x0["compress_skipped_raw"],
+                "device_ratio": round(enc_in / enc_out, 3) if enc_out else None,
+                "codec_requests_per_launch": round((b1["requests"] - b0["requests"]) / nl, 2) if nl else 0,
+                "bad_tables": c1["bad_tables"] - c0["bad_tables"],
+                "decode_errors": c1["decode_errors"] - c0["decode_errors"],
+            }
+            rdb[body] = r
+
     # Sweep (example/rdma_performance/client.cpp:35-48,221-300 analog):
     # payload size x queue depth, lending vs the RCCL plane, each point a
     # closed loop for --sweep-seconds; avg/p90/p99/p99.9 latency, GB/s and
@@ -759,6 +794,13 @@ def main():
                 out[name + "_requests_per_launch"] = r["gpu"]["requests_per_launch"]
                 errs += r["gpu"]["errors"]
             out[name + "_errors"] = errs
+        for body, r in rdb.items():
+            k = "device_snappy_64KB_" + body
+            out[k + "_qps"] = round(r["qps"], 1)
+            out[k + "_p99_us"] = r["p99_us"]
+            out[k + "_errors"] = r["errors"]
+            out[k + "_timed_s"] = round(r["elapsed_s"], 3)
+            out[k + "_device"] = r["device"]
         if rc:
             out["rccl_64KB_qps"] = round(rc["qps"], 1)
             out["rccl_64KB_p99_us"] = rc["p99_us"]
@@ -788,6 +830,8 @@ def main():
                 ("echo_1MB", r1m), ("rccl_1MB", r1mr), ("cpu_handler_64KB", rgc), ("gpu_handler_64KB", rg))
         for name, r in rx.items():
             legs += ((name + "_cpu", r["cpu"]), (name + "_gpu", r.get("gpu")))
+        for body, r in rdb.items():
+            legs += (("device_snappy_64KB_" + body, r),)
         # which transport carried each leg's payloads (summed over ranks)
         out["transport"] = {name: leg["transport"] for name, leg in legs if leg and name[:4] != "grpc"}
         # host CPU microseconds per RPC of each leg (whole rank: client,

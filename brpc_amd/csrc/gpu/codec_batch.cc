@@ -163,10 +163,10 @@ bool launch(CBatch* b, int device) {
         nstreams += r->streams.size();
         for (const SnappyStream& st : r->streams) npieces += st.max_pieces;
         if (!r->streams.empty()) piece_limit = std::max(piece_limit, r->stream_piece_limit);
-        b->scan_row.push_back(r->want_scan ? nscan : (size_t)-1);
+        b->scan_row.push_back(nscan);
         ncomp += r->comp.size();
         ndecomp += r->decomp.size();
-        nscan += r->want_scan ? 1 : 0;
+        nscan += r->scans.size();
         comp_max = std::max(comp_max, r->comp_max_ulen);
         decomp_max = std::max(decomp_max, r->decomp_max_ulen);
         h2d.insert(h2d.end(), r->h2d.begin(), r->h2d.end());
@@ -192,7 +192,7 @@ bool launch(CBatch* b, int device) {
         const CodecRequest* r = b->reqs[i];
         std::copy(r->comp.begin(), r->comp.end(), b->comp_jobs.p + b->comp_first[i]);
         std::copy(r->decomp.begin(), r->decomp.end(), b->decomp_jobs.p + b->decomp_first[i]);
-        if (r->want_scan) b->scan_jobs.p[b->scan_row[i]] = r->scan;
+        std::copy(r->scans.begin(), r->scans.end(), b->scan_jobs.p + b->scan_row[i]);
         std::copy(r->pieces.begin(), r->pieces.end(), b->piece_jobs.p + b->piece_first[i]);
         std::copy(r->runs.begin(), r->runs.end(), b->run_jobs.p + b->run_first[i]);
         for (size_t k = 0; k < r->dec_runs.size(); ++k) {
@@ -338,11 +338,11 @@ int RunCodecRequest(CodecRequest* r, int device) {
             for (uint32_t k = 0; code == 0 && k < st.max_pieces; ++k) code = mine->piece_err.p[st.first + k];
             r->stream_err[j] = code;
         }
-        if (r->want_scan) {
-            const size_t row = mine->scan_row[idx];
+        if (!r->scans.empty()) {
+            const size_t row = mine->scan_row[idx], ns = r->scans.size();
             const uint64_t* f = mine->scan_fields.p + row * 2 * kCodecScanFields;
-            r->scan_nfields = mine->scan_n.p[row];
-            r->scan_fields.assign(f, f + 2 * kCodecScanFields);
+            r->scan_nfields.assign(mine->scan_n.p + row, mine->scan_n.p + row + ns);
+            r->scan_fields.assign(f, f + ns * 2 * kCodecScanFields);
         }
     }
     release(e, mine);

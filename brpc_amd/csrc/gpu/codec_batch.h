@@ -34,9 +34,9 @@ struct CodecRequest {
     // headerless pieces cut on the host (pointers device-accessible)
     std::vector<SnappyPiece> pieces;
     uint32_t pieces_max_ulen = 0;
-    // optional wire scan of one decoded message (kCodecScanFields rows)
-    bool want_scan = false;
-    PbScanJob scan{nullptr, 0};
+    // wire scans of decoded messages (kCodecScanFields rows each), run after
+    // every decode of the batch
+    std::vector<PbScanJob> scans;
     // copies issued after the kernels (HBM -> pinned)
     std::vector<Segment> d2h;
     // packed varint runs decoded last (their bytes are final by then);
@@ -51,8 +51,8 @@ struct CodecRequest {
     std::vector<int32_t> run_err;  // per chunk: 0, or 1 when the device size disagreed (nothing written)
     std::vector<uint32_t> dec_counts;  // per decode chunk: varints ending in it
     std::vector<int32_t> dec_err;      // per decode chunk: 0, or 1 for a malformed varint
-    std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields
-    int32_t scan_nfields = -1;
+    std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields per scan
+    std::vector<int32_t> scan_nfields;  // per scan: field count or a negative code
 };
 
 constexpr uint32_t kCodecScanFields = 128;

@@ -519,8 +519,7 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
         req.stream_piece_limit = limit;
     }
     if (index) {
-        req.want_scan = true;
-        req.scan = PbScanJob{reinterpret_cast<const uint8_t*>(out_base), total};
+        req.scans.push_back(PbScanJob{reinterpret_cast<const uint8_t*>(out_base), total});
         if (out_base != dst.p) req.d2h.push_back(Segment{dbody.p, dst.p, total});
     }
     if (RunCodecRequest(&req, dev) != 0) return false;
@@ -531,7 +530,7 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
         if (e) return false;
     }
     if (index) {
-        index->nfields = req.scan_nfields;
+        index->nfields = req.scan_nfields.empty() ? -1 : req.scan_nfields[0];
         index->fields.swap(req.scan_fields);
     }
     Buf whole;

@@ -19,10 +19,12 @@
 #include "base/logging.h"
 #include "base/time.h"
 #include "gpu/copy_engine.h"
+#include "gpu/device_codec.h"
 #include "gpu/device_handler.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
+#include "mrpc/proto/options.pb.h"
 #include "mrpc/proto/rpc_meta.pb.h"
 #include "net/socket.h"
 #include "policy/device_payload.h"
@@ -34,6 +36,9 @@ DEFINE_int32(xgmi_reap_interval_ms, 5, "reap released lends this often while any
 DEFINE_int32(xgmi_reap_scan_mb, 256,
              "scan every outstanding lend for releases once they hold this many MiB (out-of-order releases "
              "of large payloads otherwise pin arena blocks until the 100 ms scan)");
+DEFINE_int32(device_payload_compress_min_bytes, 16384,
+             "device blocks of at least this many bytes are snappy-encoded on the device when the sender asked "
+             "for device payload compression (Controller::set_device_payload_compress_type)");
 DEFINE_int32(xgmi_dead_peer_reap_ms, 2000,
              "lent blocks whose connection failed are reclaimed after this long (the peer may still be pulling)");
 
@@ -67,7 +72,8 @@ std::string boot_id() {
 
 std::atomic<int64_t> g_sent_bytes{0}, g_recv_bytes{0}, g_sent_payloads{0}, g_recv_payloads{0}, g_busy{0},
     g_crc_fail{0}, g_copied_in{0}, g_released_unconsumed{0}, g_cross_bytes{0}, g_cross_payloads{0},
-    g_peer_fail{0}, g_peer_access{0}, g_attach_fail{0}, g_peer_maps{0};
+    g_peer_fail{0}, g_peer_access{0}, g_attach_fail{0}, g_peer_maps{0}, g_comp_sent{0}, g_comp_recv{0},
+    g_comp_raw{0}, g_comp_fail{0};
 
 // ------------------------------------------------------------------ lending
 // The process-wide table of blocks lent to peers. A slot holds a Buf that
@@ -347,12 +353,72 @@ PeerMap* peer_of(Socket* sock, std::shared_ptr<Transport>* keep) {
     return ep ? ep->peer.get() : nullptr;
 }
 
+// Encode the payload on the device into a fresh lendable block and lend
+// that (gpu/device_codec.h). 0: lent; 1: not worth it or not possible (the
+// caller lends the raw bytes); <0: error.
+int lend_compressed(Socket* sock, const char* src, uint32_t len, const DeviceLendOptions& opt,
+                    policy::DevicePayload* d) {
+    const DeviceSnappyLayout lay = DeviceSnappyLayoutFor(len);
+    Buf hold;
+    void* p = AppendNewDeviceBlock(&hold, lay.region(), g_device);
+    const int64_t aoff = p ? ArenaOffset(p, g_device) : -1;
+    if (aoff < 0) return 1;
+    std::vector<uint32_t> clen(lay.nblocks);
+    if (DeviceSnappyEncode(src, len, p, lay, clen.data(), g_device) != 0) {
+        g_comp_fail.fetch_add(1, std::memory_order_relaxed);
+        return 1;
+    }
+    uint64_t total = 0;
+    for (uint32_t c : clen) total += c;
+    if (total * 8 > (uint64_t)len * 7) {
+        // incompressible (random bytes, already-compressed data): decoding
+        // would cost the receiver more than the bytes it saves
+        g_comp_raw.fetch_add(1, std::memory_order_relaxed);
+        return 1;
+    }
+    if (opt.verify) {
+        // the receiver checks the DECODED bytes: checksum the source
+        Segment seg{src, nullptr, len};
+        uint32_t crc = 0;
+        if (BatchedCopy(&seg, 1, g_device, &crc) != 0) return -1;
+        d->set_crc32c(crc);
+        d->set_has_crc(true);
+    }
+    uint32_t slot = 0;
+    uint64_t seq = 0;
+    if (!g_lender->lend(std::move(hold), sock->id(), &slot, &seq)) {
+        g_busy.fetch_add(1, std::memory_order_relaxed);
+        d->clear_has_crc();
+        return 1;
+    }
+    d->set_ring_offset(aoff);
+    d->set_length((int64_t)len);
+    d->set_lent_length((int64_t)lay.region());
+    d->set_compress_type(COMPRESS_TYPE_SNAPPY);
+    d->set_block_stride(lay.stride);
+    d->set_block_ulen(lay.block_ulen);
+    for (uint32_t c : clen) d->add_block_clen(c);
+    d->set_pb_scan(opt.scan);
+    d->set_src_device(g_device);
+    d->set_slot(slot);
+    d->set_seq(seq);
+    g_sent_bytes.fetch_add((int64_t)total, std::memory_order_relaxed);
+    g_sent_payloads.fetch_add(1, std::memory_order_relaxed);
+    g_comp_sent.fetch_add(1, std::memory_order_relaxed);
+    return 0;
+}
+
 // ------------------------------------------------------------------ hooks
-int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, bool with_crc, policy::DevicePayload* d) {
+int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, const DeviceLendOptions& opt,
+              policy::DevicePayload* d) {
     Lender* l = g_lender;
     if (!l) return -1;
     if (block->device != g_device) return 1;  // another GPU's block: stage it
     const char* src = block->data + offset;
+    if (opt.compress == COMPRESS_TYPE_SNAPPY && len >= (uint32_t)std::max(1, FLAGS_device_payload_compress_min_bytes)) {
+        const int rc = lend_compressed(sock, src, len, opt, d);
+        if (rc <= 0) return rc;
+    }
     int64_t aoff = ArenaOffset(src, g_device);
     Buf hold;
     if (aoff < 0) {
@@ -368,16 +434,16 @@ int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, bool
         // registers: one pass over HBM instead of two
         Segment seg{src, p, len};
         uint32_t crc = 0;
-        if (BatchedCopy(&seg, 1, g_device, with_crc ? &crc : nullptr) != 0) return -1;
+        if (BatchedCopy(&seg, 1, g_device, opt.verify ? &crc : nullptr) != 0) return -1;
         g_copied_in.fetch_add(1, std::memory_order_relaxed);
         src = static_cast<const char*>(p);
-        if (with_crc) {
+        if (opt.verify) {
             d->set_crc32c(crc);
             d->set_has_crc(true);
         }
     } else {
         hold.append_block(block, offset, len);
-        if (with_crc) {
+        if (opt.verify) {
             // checksum-only segment (null dst) through the copy engine, so
             // concurrent senders' checksums share one launch and one event
             Segment seg{src, nullptr, len};
@@ -395,6 +461,7 @@ int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, bool
     }
     d->set_ring_offset(aoff);
     d->set_length((int64_t)len);
+    d->set_pb_scan(opt.scan);
     d->set_src_device(g_device);
     d->set_slot(slot);
     d->set_seq(seq);
@@ -407,21 +474,28 @@ void release_in(PeerMap* pm, const policy::DevicePayload& d) {
     if (pm && d.slot() < pm->nslots) pm->table->released[d.slot()].store(d.seq(), std::memory_order_release);
 }
 
-int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Buf* outs) {
+int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Buf* outs,
+              DevicePayloadIndex* index) {
     std::shared_ptr<Transport> keep;
     PeerMap* pm = peer_of(sock, &keep);
     if (!pm) {
         for (int i = 0; i < n; ++i) outs[i].clear();
         return -1;
     }
+    // raw payloads are pulled by one batched copy; device-compressed ones are
+    // decoded straight out of the lent region by one codec request
     std::vector<Segment> segs;
+    std::vector<int> seg_of;  // payload of each segment
+    std::vector<DeviceSnappyBlocks> jobs;
+    std::vector<int> job_of;
     segs.reserve(n);
     int rc = 0;
     for (int i = 0; i < n && rc == 0; ++i) {
         const policy::DevicePayload& d = *descs[i];
-        const int64_t off = d.ring_offset(), len = d.length();
-        if (off < 0 || len < 0 || (uint64_t)off > pm->size || (uint64_t)len > pm->size - (uint64_t)off ||
-            d.slot() >= pm->nslots) {
+        const bool comp = d.compress_type() != 0;
+        const int64_t off = d.ring_offset(), len = d.length(), region = comp ? d.lent_length() : len;
+        if (off < 0 || len < 0 || region < 0 || (uint64_t)off > pm->size || (uint64_t)region > pm->size - (uint64_t)off ||
+            d.slot() >= pm->nslots || (comp && (d.compress_type() != COMPRESS_TYPE_SNAPPY || len == 0))) {
             rc = -1;
             break;
         }
@@ -431,34 +505,96 @@ int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Bu
             rc = -1;
             break;
         }
-        segs.push_back(Segment{pm->base + off, dst, (uint64_t)len});
+        if (comp) {
+            DeviceSnappyBlocks j;
+            j.region = pm->base + off;
+            j.region_len = (uint64_t)region;
+            j.lay.block_ulen = d.block_ulen();
+            j.lay.stride = d.block_stride();
+            j.lay.nblocks = (uint32_t)d.block_clen_size();
+            j.clen = d.block_clen().data();
+            j.dst = dst;
+            j.len = (uint64_t)len;
+            j.scan = d.pb_scan() && index;
+            jobs.push_back(j);
+            job_of.push_back(i);
+        } else {
+            segs.push_back(Segment{pm->base + off, dst, (uint64_t)len});
+            seg_of.push_back(i);
+        }
     }
-    // one pull for every payload; when the sender asked for verification
+    // one pull for every raw payload; when the sender asked for verification
     // the pull kernel folds CRC32C while the bytes pass through registers
     bool want_crc = false;
-    for (int i = 0; i < n; ++i) want_crc |= descs[i]->has_crc();
+    for (int i : seg_of) want_crc |= descs[i]->has_crc();
     std::vector<uint32_t> crcs(want_crc ? segs.size() : 0);
     if (rc == 0 && !segs.empty())
         rc = BatchedCopy(segs.data(), (int)segs.size(), g_device, want_crc ? crcs.data() : nullptr);
+    std::vector<int> jerr(jobs.size(), 0);
+    std::vector<DevicePayloadIndex> jidx(jobs.size());
+    if (rc == 0 && !jobs.empty()) {
+        rc = DeviceSnappyDecode(jobs.data(), (int)jobs.size(), jerr.data(), jidx.data(), g_device);
+        for (int e : jerr) rc |= e ? -1 : 0;
+    }
     // the bytes are ours now (or never will be): give every region back
     for (int i = 0; i < n; ++i) release_in(pm, *descs[i]);
-    if (rc != 0) {
-        for (int i = 0; i < n; ++i) outs[i].clear();
+    auto fail = [&] {
+        for (int k = 0; k < n; ++k) outs[k].clear();
         if (pm->device != g_device) g_peer_fail.fetch_add(1, std::memory_order_relaxed);
         return -1;
+    };
+    if (rc != 0) return fail();
+    for (size_t k = 0; k < seg_of.size(); ++k) {
+        const policy::DevicePayload& d = *descs[seg_of[k]];
+        if (d.has_crc() && crcs[k] != d.crc32c()) {
+            g_crc_fail.fetch_add(1, std::memory_order_relaxed);
+            return fail();
+        }
     }
-    size_t si = 0;
+    // decoded payloads are verified on their output (the sender checksummed
+    // its source): checksum-only segments, one engine call for all of them
+    std::vector<Segment> vsegs;
+    std::vector<int> vof;
+    for (size_t k = 0; k < jobs.size(); ++k) {
+        if (!descs[job_of[k]]->has_crc()) continue;
+        vsegs.push_back(Segment{jobs[k].dst, nullptr, jobs[k].len});
+        vof.push_back(job_of[k]);
+    }
+    if (!vsegs.empty()) {
+        std::vector<uint32_t> v(vsegs.size());
+        if (BatchedCopy(vsegs.data(), (int)vsegs.size(), g_device, v.data()) != 0) return fail();
+        for (size_t k = 0; k < v.size(); ++k) {
+            if (v[k] != descs[vof[k]]->crc32c()) {
+                g_crc_fail.fetch_add(1, std::memory_order_relaxed);
+                return fail();
+            }
+        }
+    }
+    if (index) {
+        // raw payloads that asked for an index are scanned where they landed
+        std::vector<const void*> bufs;
+        std::vector<uint64_t> lens;
+        std::vector<int> of;
+        for (size_t k = 0; k < seg_of.size(); ++k) {
+            if (!descs[seg_of[k]]->pb_scan()) continue;
+            bufs.push_back(segs[k].dst);
+            lens.push_back(segs[k].len);
+            of.push_back(seg_of[k]);
+        }
+        if (!bufs.empty()) {
+            std::vector<DevicePayloadIndex> got(bufs.size());
+            if (DevicePbScan(bufs.data(), lens.data(), (int)bufs.size(), got.data(), g_device) != 0) return fail();
+            for (size_t k = 0; k < of.size(); ++k) index[of[k]] = std::move(got[k]);
+        }
+        for (size_t k = 0; k < jobs.size(); ++k) {
+            if (jobs[k].scan) index[job_of[k]] = std::move(jidx[k]);
+        }
+    }
     for (int i = 0; i < n; ++i) {
         const policy::DevicePayload& d = *descs[i];
-        if (d.length() == 0) continue;
-        if (d.has_crc() && crcs[si] != d.crc32c()) {
-            g_crc_fail.fetch_add(1, std::memory_order_relaxed);
-            for (int k = 0; k < n; ++k) outs[k].clear();
-            return -1;
-        }
-        ++si;
-        g_recv_bytes.fetch_add(d.length(), std::memory_order_relaxed);
+        g_recv_bytes.fetch_add(d.compress_type() ? d.lent_length() : d.length(), std::memory_order_relaxed);
         if (pm->device != g_device) g_cross_bytes.fetch_add(d.length(), std::memory_order_relaxed);
+        if (d.compress_type()) g_comp_recv.fetch_add(1, std::memory_order_relaxed);
     }
     g_recv_payloads.fetch_add(n, std::memory_order_relaxed);
     if (pm->device != g_device) g_cross_payloads.fetch_add(n, std::memory_order_relaxed);
@@ -586,6 +722,10 @@ XgmiStats GetXgmiStats() {
     s.peer_access_enabled = g_peer_access.load();
     s.attach_failures = g_attach_fail.load();
     s.peer_maps = g_peer_maps.load();
+    s.compressed_sent = g_comp_sent.load();
+    s.compressed_recv = g_comp_recv.load();
+    s.compress_skipped_raw = g_comp_raw.load();
+    s.compress_failures = g_comp_fail.load();
     return s;
 }
 

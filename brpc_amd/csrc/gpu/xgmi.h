@@ -58,6 +58,10 @@ struct XgmiStats {
     int64_t peer_access_enabled = 0;  // hipDeviceEnablePeerAccess successes
     int64_t attach_failures = 0;      // hellos that could not be mapped (fallback: staged over TCP)
     int64_t peer_maps = 0;            // peer arenas mapped
+    // device-compressed payloads (Controller::set_device_payload_compress_type):
+    // lent encoded, decoded on arrival, lent raw because incompressible, or
+    // lent raw because the device encode failed
+    int64_t compressed_sent = 0, compressed_recv = 0, compress_skipped_raw = 0, compress_failures = 0;
 };
 XgmiStats GetXgmiStats();
 

@@ -118,11 +118,11 @@ bool plane_send(int peer, const Buf& piece, int64_t pos, DevicePayloads* descs) 
 
 }  // namespace
 
-int LendDeviceBlocks(Socket* sock, const Buf& in, bool verify, Buf* host_out, DevicePayloads* descs,
-                     std::string* err) {
+int LendDeviceBlocks(Socket* sock, const Buf& in, const DeviceLendOptions& opt, Buf* host_out,
+                     DevicePayloads* descs, std::string* err) {
     // the RCCL plane takes large payloads to a rank of our plane (never the
     // verified ones: the integrity check rides on the lending pull)
-    const int prank = (!verify && sock && in.size() >= (size_t)FLAGS_rccl_min_bytes) ? sock->plane_rank() : -1;
+    const int prank = (!opt.verify && sock && in.size() >= (size_t)FLAGS_rccl_min_bytes) ? sock->plane_rank() : -1;
     const bool plane = prank >= 0 && gpu::rccl::Active();
     const bool host_plane = plane && gpu::rccl::HostMemory();
     if (in.all_host_accessible() && !host_plane) {
@@ -167,7 +167,7 @@ int LendDeviceBlocks(Socket* sock, const Buf& in, bool verify, Buf* host_out, De
         } else {
             DevicePayload* d = descs->Add();
             d->set_position((int64_t)pos);
-            const int rc = g_hooks.send(sock, r.block, r.offset, r.length, verify, d);
+            const int rc = g_hooks.send(sock, r.block, r.offset, r.length, opt, d);
             if (rc > 0) {  // transport busy: stage this block inline
                 descs->RemoveLast();
                 Buf one;
@@ -188,7 +188,8 @@ int LendDeviceBlocks(Socket* sock, const Buf& in, bool verify, Buf* host_out, De
 }
 
 int PullDeviceBlocksBatch(Socket* sock, const std::vector<std::pair<const DevicePayloads*, Buf*>>& items,
-                          std::string* err) {
+                          std::string* err, std::vector<DevicePayloadIndex>* indexes) {
+    if (indexes) indexes->assign(items.size(), DevicePayloadIndex());
     size_t total = 0;
     for (const auto& it : items) total += (size_t)it.first->size();
     if (total == 0) return 0;
@@ -252,13 +253,24 @@ int PullDeviceBlocksBatch(Socket* sock, const std::vector<std::pair<const Device
             return -1;
         }
         std::vector<Buf> got(lent.size());
-        if (g_hooks.recv(sock, lent.data(), (int)lent.size(), got.data()) != 0) {
+        bool any_scan = false;
+        for (const DevicePayload* x : lent) any_scan |= x->pb_scan();
+        std::vector<DevicePayloadIndex> idx(indexes && any_scan ? lent.size() : 0);
+        if (g_hooks.recv(sock, lent.data(), (int)lent.size(), got.data(), idx.empty() ? nullptr : idx.data()) != 0) {
             // the hook released every lent slot whatever happened
             discard_plane();
             if (err) *err = "fail to receive " + std::to_string(lent.size()) + " device payload(s)";
             return -1;
         }
         for (size_t k = 0; k < lent.size(); ++k) pulled[lent_at[k]] = std::move(got[k]);
+        if (!idx.empty()) {
+            // flat index -> item: the first scanned payload of each item
+            for (size_t k = 0, at = 0, item = 0; k < lent.size(); ++k) {
+                while (item + 1 < items.size() && lent_at[k] >= at + sorted[item].size()) at += sorted[item++].size();
+                if (lent[k]->pb_scan() && (*indexes)[item].nfields < 0 && idx[k].nfields >= 0)
+                    (*indexes)[item] = std::move(idx[k]);
+            }
+        }
     }
     if (!plane_at.empty()) {
         std::vector<int> src;
@@ -293,9 +305,14 @@ int PullDeviceBlocksBatch(Socket* sock, const std::vector<std::pair<const Device
     return 0;
 }
 
-int PullDeviceBlocks(Socket* sock, const DevicePayloads& descs, Buf* attachment, std::string* err) {
+int PullDeviceBlocks(Socket* sock, const DevicePayloads& descs, Buf* attachment, std::string* err,
+                     DevicePayloadIndex* index) {
     if (descs.size() == 0) return 0;
-    return PullDeviceBlocksBatch(sock, {{&descs, attachment}}, err);
+    if (!index) return PullDeviceBlocksBatch(sock, {{&descs, attachment}}, err);
+    std::vector<DevicePayloadIndex> idx;
+    const int rc = PullDeviceBlocksBatch(sock, {{&descs, attachment}}, err, &idx);
+    if (rc == 0 && !idx.empty()) *index = std::move(idx[0]);
+    return rc;
 }
 
 void ReleaseDeviceBlocks(Socket* sock, const DevicePayloads& descs) {
@@ -306,8 +323,11 @@ bool SplitDevicePayload(Controller* cntl, bool request, const Buf& attachment, B
                         Socket* sock) {
     if (!sock) sock = cntl->_pack_socket;
     std::string err;
-    if (LendDeviceBlocks(sock, attachment, cntl->verify_device_payload(), host_out, meta->mutable_device_payload(),
-                         &err) != 0) {
+    DeviceLendOptions opt;
+    opt.verify = cntl->verify_device_payload();
+    opt.compress = (int)cntl->device_payload_compress_type();
+    opt.scan = cntl->device_payload_scan();
+    if (LendDeviceBlocks(sock, attachment, opt, host_out, meta->mutable_device_payload(), &err) != 0) {
         cntl->SetFailed(EXGMI, "%s", err.c_str());
         return false;
     }
@@ -327,7 +347,17 @@ bool SplitDevicePayload(Controller* cntl, bool request, const Buf& attachment, B
 bool MergeDevicePayload(Controller* cntl, Socket* sock, const RpcMeta& meta, bool request, Buf* attachment) {
     (void)request;
     std::string err;
-    if (PullDeviceBlocks(sock, meta.device_payload(), attachment, &err) != 0) {
+    bool scanned = false;
+    CompressType got = COMPRESS_TYPE_NONE;
+    for (const DevicePayload& x : meta.device_payload()) {
+        scanned |= x.pb_scan();
+        if (x.compress_type()) got = (CompressType)x.compress_type();
+    }
+    cntl->_device_payload_index.nfields = -1;
+    cntl->_device_payload_index.fields.clear();
+    cntl->_received_device_compress = got;
+    if (PullDeviceBlocks(sock, meta.device_payload(), attachment, &err,
+                         scanned ? &cntl->_device_payload_index : nullptr) != 0) {
         cntl->SetFailed(EXGMI, "%s", err.c_str());
         return false;
     }

@@ -308,13 +308,27 @@ int PressSession::Init(const PressOptions& opt, std::string* error) {
             if ((q & 0xff) == 0) id = -id;
         }
         if (_opt.attachment_size > 0) {
-            _attachment.resize(_opt.attachment_size);
-            uint64_t r = 0x9E3779B97F4A7C15ull;
-            for (size_t i = 0; i < _attachment.size(); ++i) {
-                r ^= r << 13;
-                r ^= r >> 7;
-                r ^= r << 17;
-                _attachment[i] = (char)r;
+            if (!_opt.attachment_body.empty()) {
+                _attachment = EchoBody(_opt.attachment_body, (size_t)_opt.attachment_size);
+                if (_attachment.size() != (size_t)_opt.attachment_size) {
+                    *error = "unknown attachment body kind '" + _opt.attachment_body + "' (const, text or random)";
+                    return -1;
+                }
+            } else {
+                _attachment.resize(_opt.attachment_size);
+                uint64_t r = 0x9E3779B97F4A7C15ull;
+                for (size_t i = 0; i < _attachment.size(); ++i) {
+                    r ^= r << 13;
+                    r ^= r >> 7;
+                    r ^= r << 17;
+                    _attachment[i] = (char)r;
+                }
+            }
+            if (_opt.attachment_pb) {
+                example::EchoRequest m;
+                m.set_message(_attachment);
+                _attachment.clear();
+                m.SerializeToString(&_attachment);
             }
             char* blk = _attachment_buf.append_contiguous(_attachment.size());
             if (blk) memcpy(blk, _attachment.data(), _attachment.size());
@@ -378,6 +392,9 @@ void PressSession::issue(Worker* w, int64_t seq, PressCall* call, bool async) {
     if (call->echo_req.ids_size() != (int)_ids.size()) *call->echo_req.mutable_ids() = _ids;
     if (_device_attachment) {
         gpu::AppendDevice(&cntl.request_attachment(), _device_attachment, _attachment.size(), _opt.gpu_device);
+        if (_opt.device_compress) cntl.set_device_payload_compress_type((CompressType)_opt.device_compress);
+        if (_opt.device_scan) cntl.set_device_payload_scan(true);
+        if (_opt.verify_device_payload) cntl.set_verify_device_payload(true);
     } else if (!_attachment.empty()) {
         // one shared block, appended by reference like rpc_press's IOBuf
         // attachment (tools/rpc_press/rpc_press_impl.cpp): no per-call copy
@@ -410,9 +427,17 @@ void PressSession::finish(PressCall* call) {
             } else {
                 for (int k = 0; k < _fanout; ++k) want += _attachment;  // gathered in channel order
             }
+            const DevicePayloadIndex& ix = cntl.device_payload_index();
             if (gpu::CopyBufToHost(cntl.response_attachment(), &got) != 0 || got != want) {
                 ok = false;
                 cntl.SetFailed(ERESPONSE, "echoed attachment mismatch (%zu bytes)", got.size());
+            } else if (_device_attachment && _opt.device_scan && _fanout == 1 &&
+                       (ix.nfields != 1 || ix.fields.size() < 2 || ix.fields[0] != ((1u << 3) | 2) ||
+                        (ix.fields[1] & 0xffffffffu) != (uint64_t)(_attachment.size() - (ix.fields[1] >> 32)))) {
+                // the reply's device field table: one length-delimited field 1
+                // running to the end of the message
+                ok = false;
+                cntl.SetFailed(ERESPONSE, "device pb index of the echoed attachment is wrong (nfields %d)", ix.nfields);
             } else if ((_opt.gpu_process || _opt.cpu_process) &&
                        call->echo_res.crc32c() != crc32c::Value(want.data(), want.size())) {
                 ok = false;

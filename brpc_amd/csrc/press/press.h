@@ -57,6 +57,20 @@ struct PressOptions {
     int attachment_size = 0;   // bytes of attachment per request
     int packed_ids = 0;        // int64 ids per request (EchoRequest.ids, a packed varint run), echoed back
     bool device_attachment = false;  // attachment lives in HBM (needs GPU)
+    // attachment contents: "" (pseudo-random bytes), or an EchoBody kind
+    // ("const", "text", "random")
+    std::string attachment_body;
+    // the attachment is one serialized EchoRequest whose message is that
+    // body (a protobuf the receiver can index on the device: device_scan)
+    bool attachment_pb = false;
+    // device attachments: snappy-encode on the device before lending
+    // (Controller::set_device_payload_compress_type; the server mirrors it)
+    int device_compress = 0;
+    // device attachments: the receiver pb_scan-indexes the payload (the
+    // server mirrors it; check_echo verifies the reply's field table)
+    bool device_scan = false;
+    // device attachments: CRC32C-verified on the device by the receiver
+    bool verify_device_payload = false;
     int gpu_device = -1;
     bool check_echo = false;   // verify the echoed payload
     int check_every = 1;       // ... of every n-th call (bench legs sample; tests check all)

@@ -12,6 +12,8 @@
 #include "base/time.h"
 #include "fiber/fiber.h"
 #include "gpu/copy_engine.h"
+#include "gpu/device_codec.h"
+#include "policy/device_payload.h"
 #include "gpu/gpu.h"
 #include "gpu/kernels.h"
 
@@ -137,6 +139,47 @@ void bind_gpu_ops(py::module_& g) {
         return crcs;
     }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("device") = 0, py::arg("with_crc") = false,
        py::arg("fold") = false);
+    // Device-payload codec (gpu/device_codec.h), for numerics tests: encode
+    // `len` bytes at src into blocks at dst (layout of -device_payload_block_kb)
+    // -> (block_ulen, stride, [clen...]); decode such a table back -> per-job
+    // code (0 ok, 1 bad table, 2 malformed block) and the field table when scanned.
+    g.def("device_snappy_layout", [](uint64_t len) {
+        const gpu::DeviceSnappyLayout l = gpu::DeviceSnappyLayoutFor(len);
+        return py::make_tuple(l.block_ulen, l.stride, l.nblocks);
+    });
+    g.def("device_snappy_encode", [](uintptr_t src, uint64_t len, uintptr_t dst, int device) {
+        const gpu::DeviceSnappyLayout l = gpu::DeviceSnappyLayoutFor(len);
+        std::vector<uint32_t> clen(l.nblocks);
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::DeviceSnappyEncode((const void*)src, len, (void*)dst, l, clen.data(), device);
+        }
+        check(rc, "device_snappy_encode");
+        return clen;
+    });
+    g.def("device_snappy_decode", [](uintptr_t region, uint64_t region_len, uint32_t block_ulen, uint32_t stride,
+                                     const std::vector<uint32_t>& clen, uintptr_t dst, uint64_t len, bool scan,
+                                     int device) {
+        gpu::DeviceSnappyBlocks j;
+        j.region = (const char*)region;
+        j.region_len = region_len;
+        j.lay.block_ulen = block_ulen;
+        j.lay.stride = stride;
+        j.lay.nblocks = (uint32_t)clen.size();
+        j.clen = clen.data();
+        j.dst = (void*)dst;
+        j.len = len;
+        j.scan = scan;
+        int err = 0, rc;
+        DevicePayloadIndex idx;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::DeviceSnappyDecode(&j, 1, &err, &idx, device);
+        }
+        check(rc, "device_snappy_decode");
+        return py::make_tuple(err, idx.nfields, idx.fields);
+    });
     g.def("resident_stats", [] {
         const gpu::ResidentStats s = gpu::GetResidentStats();
         py::dict d;

@@ -19,6 +19,7 @@
 #include "gpu/snappy_offload.h"
 #include "gpu/json_offload.h"
 #include "gpu/codec_batch.h"
+#include "gpu/device_codec.h"
 #include "json/json2pb.h"
 #include "pb/descriptor.h"
 #include "pb/parser.h"
@@ -154,6 +155,11 @@ press::PressOptions press_options(const py::dict& d) {
         else if (k == "attachment_size") o.attachment_size = v.cast<int>();
         else if (k == "packed_ids") o.packed_ids = v.cast<int>();
         else if (k == "device_attachment") o.device_attachment = v.cast<bool>();
+        else if (k == "attachment_body") o.attachment_body = v.cast<std::string>();
+        else if (k == "attachment_pb") o.attachment_pb = v.cast<bool>();
+        else if (k == "device_compress") o.device_compress = v.cast<int>();
+        else if (k == "device_scan") o.device_scan = v.cast<bool>();
+        else if (k == "verify_device_payload") o.verify_device_payload = v.cast<bool>();
         else if (k == "gpu_device") o.gpu_device = v.cast<int>();
         else if (k == "check_echo") o.check_echo = v.cast<bool>();
         else if (k == "fanout_servers") o.fanout_servers = v.cast<std::string>();
@@ -561,6 +567,10 @@ PYBIND11_MODULE(_native, m) {
         d["peer_access_enabled"] = s.peer_access_enabled;
         d["attach_failures"] = s.attach_failures;
         d["peer_maps"] = s.peer_maps;
+        d["compressed_sent"] = s.compressed_sent;
+        d["compressed_recv"] = s.compressed_recv;
+        d["compress_skipped_raw"] = s.compress_skipped_raw;
+        d["compress_failures"] = s.compress_failures;
         int64_t staged = 0, staged_bytes = 0;
         GetStagedStats(&staged, &staged_bytes);
         d["staged_payloads"] = staged;
@@ -681,6 +691,19 @@ PYBIND11_MODULE(_native, m) {
         d["pack_run_chunks"] = s.pack_run_chunks;
         d["unpack_runs"] = s.unpack_runs;
         d["unpack_fallbacks"] = s.unpack_fallbacks;
+        return d;
+    });
+    g.def("device_codec_stats", [] {
+        const gpu::DeviceCodecStats s = gpu::GetDeviceCodecStats();
+        py::dict d;
+        d["encodes"] = s.encodes;
+        d["encoded_bytes"] = s.encoded_bytes;
+        d["encoded_out_bytes"] = s.encoded_out_bytes;
+        d["decodes"] = s.decodes;
+        d["decoded_bytes"] = s.decoded_bytes;
+        d["bad_tables"] = s.bad_tables;
+        d["decode_errors"] = s.decode_errors;
+        d["scans"] = s.scans;
         return d;
     });
     g.def("codec_batch_stats", [] {

@@ -102,6 +102,11 @@ void Controller::Reset() {
     _span_enabled = false;
     _trace_id = _span_id = _parent_span_id = 0;
     _verify_device_payload = false;
+    _device_payload_compress = COMPRESS_TYPE_NONE;
+    _device_payload_scan = false;
+    _received_device_compress = COMPRESS_TYPE_NONE;
+    _device_payload_index.nfields = -1;
+    _device_payload_index.fields.clear();
     _read_progressively = false;
     _progressive_reader = nullptr;
     _progressive_attachment.reset();

@@ -21,6 +21,7 @@
 #include "mrpc/proto/options.pb.h"
 #include "net/socket.h"
 #include "pb/service.h"
+#include "policy/device_payload.h"
 
 namespace mrpc {
 
@@ -175,6 +176,25 @@ public:
     // checksum verification.
     void set_verify_device_payload(bool on) { _verify_device_payload = on; }
     bool verify_device_payload() const { return _verify_device_payload; }
+    // Device-side compression of the device blocks this side sends (request
+    // attachment on a client, response attachment on a server): with
+    // COMPRESS_TYPE_SNAPPY each lent block of at least
+    // -device_payload_compress_min_bytes is snappy-encoded in HBM by the
+    // batched codec kernels and the receiver decodes it straight out of the
+    // lent region into its own HBM — the bytes never reach the host
+    // (reference analog: the body codec of src/brpc/compress.cpp:79-92,
+    // moved onto the device payload). Incompressible blocks are lent raw.
+    void set_device_payload_compress_type(CompressType t) { _device_payload_compress = t; }
+    CompressType device_payload_compress_type() const { return _device_payload_compress; }
+    // The device attachment this side sends is ONE serialized protobuf
+    // message: the receiver indexes its top-level fields on the device
+    // (pb_scan) and finds the table in device_payload_index().
+    void set_device_payload_scan(bool on) { _device_payload_scan = on; }
+    bool device_payload_scan() const { return _device_payload_scan; }
+    // What arrived: the field table of a received pb_scan payload, and the
+    // device compression the peer used (COMPRESS_TYPE_NONE: lent raw).
+    const DevicePayloadIndex& device_payload_index() const { return _device_payload_index; }
+    CompressType received_device_payload_compress_type() const { return _received_device_compress; }
 
     // ================= internal (protocols / channels) =================
     struct Call {
@@ -244,6 +264,10 @@ public:
     Span* _span = nullptr;
     uint64_t _trace_id = 0, _span_id = 0, _parent_span_id = 0;
     bool _verify_device_payload = false;
+    CompressType _device_payload_compress = COMPRESS_TYPE_NONE;
+    bool _device_payload_scan = false;
+    CompressType _received_device_compress = COMPRESS_TYPE_NONE;
+    DevicePayloadIndex _device_payload_index;
     // device payloads described in the request being written (lent blocks,
     // RCCL plane sequences): cancelled when the write is refused, since the
     // receiver will never see their meta

@@ -90,7 +90,7 @@ int send_frame(SocketId host, int64_t dest_stream, int64_t src_stream, FrameType
     Buf host_part;
     if (payload && !payload->all_host_accessible()) {
         std::string err;
-        if (policy::LendDeviceBlocks(sock.get(), *payload, false, &host_part, fm.mutable_device_payload(), &err) != 0) {
+        if (policy::LendDeviceBlocks(sock.get(), *payload, DeviceLendOptions(), &host_part, fm.mutable_device_payload(), &err) != 0) {
             LOG_EVERY_SECOND(WARNING) << "stream " << src_stream << ": " << err;
             return EINVAL;
         }

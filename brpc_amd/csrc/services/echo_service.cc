@@ -236,7 +236,12 @@ void EchoServiceImpl::Echo(RpcController* cntl_base, const example::EchoRequest*
         response->set_device(-1);
         response->set_crc32c(crc);
     }
-    // zero-copy echo of the attachment (host or device blocks alike)
+    // zero-copy echo of the attachment (host or device blocks alike); a
+    // device payload goes back the way it came: encoded on the device again
+    // if it arrived encoded, indexed by the client if it arrived indexed
+    if (cntl->received_device_payload_compress_type() != COMPRESS_TYPE_NONE)
+        cntl->set_device_payload_compress_type(cntl->received_device_payload_compress_type());
+    if (cntl->device_payload_index().nfields >= 0) cntl->set_device_payload_scan(true);
     cntl->response_attachment().append(cntl->request_attachment());
 }
 

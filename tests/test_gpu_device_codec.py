@@ -1,0 +1,221 @@
+"""Device-payload codec (gpu/device_codec.h): HBM attachments snappy-encoded
+on the device, lent encoded, decoded by the receiver straight out of the lent
+region, optionally pb_scan-indexed. Numerics against the host snappy codec
+and the host protobuf serializer; RPC legs against the echoed bytes."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from brpc_amd import native
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    assert native.gpu.device_count() > 0, "native runtime sees no HIP device"
+    return torch.device("cuda", 0)
+
+
+def _varint(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def _encode(native, data, dev):
+    src = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+    ulen, stride, nblocks = native.gpu.device_snappy_layout(len(data))
+    region = torch.zeros(stride * nblocks, dtype=torch.uint8, device=dev)
+    clen = native.gpu.device_snappy_encode(src.data_ptr(), len(data), region.data_ptr(), 0)
+    return region, ulen, stride, clen
+
+
+@pytest.mark.parametrize("kind,size", [("text", 65536), ("text", 100003), ("random", 65536), ("const", 4096),
+                                       ("text", 1), ("text", 1 << 20)])
+def test_device_snappy_blocks_are_standard_snappy_and_round_trip(dev, kind, size):
+    from brpc_amd import native
+    data = native.echo_body(kind, size)
+    region, ulen, stride, clen = _encode(native, data, dev)
+    assert len(clen) == (size + ulen - 1) // ulen
+    host = region.cpu().numpy().tobytes()
+    # every block is a complete raw snappy stream the host codec decodes
+    for i, c in enumerate(clen):
+        assert 0 < c <= stride
+        block = host[i * stride:i * stride + c]
+        assert native.snappy_uncompress(block) == data[i * ulen:(i + 1) * ulen]
+    # the device decoder rebuilds the payload from the table alone
+    out = torch.zeros(size, dtype=torch.uint8, device=dev)
+    err, nf, _ = native.gpu.device_snappy_decode(region.data_ptr(), region.numel(), ulen, stride, clen,
+                                                 out.data_ptr(), size, False, 0)
+    assert err == 0
+    assert out.cpu().numpy().tobytes() == data
+    if kind == "text":
+        assert sum(clen) < size * 0.6 or size < 4096
+
+
+def test_device_snappy_decode_refuses_bad_tables(dev):
+    from brpc_amd import native
+    data = native.echo_body("text", 20000)
+    region, ulen, stride, clen = _encode(native, data, dev)
+    out = torch.zeros(len(data), dtype=torch.uint8, device=dev)
+    before = native.gpu.device_codec_stats()["bad_tables"]
+    bad = [
+        (region.numel(), ulen, stride, clen[:-1]),                    # blocks do not cover the payload
+        (region.numel(), ulen, stride, [stride + 1] + clen[1:]),       # block longer than its slot
+        (stride * (len(clen) - 1), ulen, stride, clen),               # last block outside the region
+        (region.numel(), ulen, stride, [1] + clen[1:]),               # a block without elements
+        (region.numel(), 0, stride, clen),                            # no block size
+    ]
+    for rlen, u, st, cl in bad:
+        err, _, _ = native.gpu.device_snappy_decode(region.data_ptr(), rlen, u, st, cl, out.data_ptr(), len(data),
+                                                    False, 0)
+        assert err == 1, (rlen, u, st, cl[:3])
+    assert native.gpu.device_codec_stats()["bad_tables"] - before == len(bad)
+    # a corrupted block (valid table) is caught by the decoder, not trusted
+    host = bytearray(region.cpu().numpy().tobytes())
+    h = len(_varint(min(ulen, len(data))))
+    for k in range(h, clen[0]):
+        host[k] = 0xFF
+    region2 = torch.frombuffer(host, dtype=torch.uint8).to(dev)
+    err, _, _ = native.gpu.device_snappy_decode(region2.data_ptr(), region2.numel(), ulen, stride, clen,
+                                                out.data_ptr(), len(data), False, 0)
+    assert err == 2
+
+
+def test_device_snappy_decode_scans_the_message(dev):
+    """pb_scan on the decoded bytes: the field table matches the host's
+    serialization of the same message."""
+    from brpc_amd import native
+    body = native.echo_body("text", 50000)
+    # EchoRequest{message = body (field 1, bytes), gpu_process = true (field 3)}
+    msg = bytes([0x0A]) + _varint(len(body)) + body + bytes([0x18, 0x01])
+    region, ulen, stride, clen = _encode(native, msg, dev)
+    out = torch.zeros(len(msg), dtype=torch.uint8, device=dev)
+    err, nf, fields = native.gpu.device_snappy_decode(region.data_ptr(), region.numel(), ulen, stride, clen,
+                                                      out.data_ptr(), len(msg), True, 0)
+    assert err == 0 and nf == 2
+    off = 1 + len(_varint(len(body)))
+    assert fields[0] == (1 << 3) | 2 and fields[1] == (off << 32) | len(body)
+    assert fields[2] == (3 << 3) | 0 and fields[3] == 1
+
+
+def _echo(native, server, n, **extra):
+    o = {"server": server, "concurrency": 16, "attachment_size": 65536, "device_attachment": True,
+         "gpu_device": 0, "check_echo": True}
+    o.update(extra)
+    p = native.Press(o)
+    p.run_requests(n)
+    return p.stats()
+
+
+@pytest.mark.parametrize("body", ["text", "const"])
+def test_compressed_device_attachments_echo(dev, body):
+    """Both directions encoded on the device (the server mirrors the
+    client's choice), every echo checked byte for byte."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        x0, c0 = native.gpu.xgmi_stats(), native.gpu.device_codec_stats()
+        st = _echo(native, s.address, 2000, attachment_body=body, device_compress=1)
+        assert st["success"] == 2000 and st["error"] == 0, st
+        x1, c1 = native.gpu.xgmi_stats(), native.gpu.device_codec_stats()
+        # request and response of (almost) every call: the first calls of a
+        # connection are staged over TCP while the hello is in flight
+        assert x1["compressed_sent"] - x0["compressed_sent"] >= 3800, (x0, x1)
+        assert x1["compressed_recv"] - x0["compressed_recv"] >= 3800, (x0, x1)
+        assert c1["decodes"] - c0["decodes"] >= 3800, (c0, c1)
+        assert c1["bad_tables"] == c0["bad_tables"] and c1["decode_errors"] == c0["decode_errors"]
+        # what the lends carried: the encoded size, not the payload's
+        assert c1["encoded_out_bytes"] - c0["encoded_out_bytes"] < 0.7 * (c1["encoded_bytes"] - c0["encoded_bytes"])
+    finally:
+        s.stop()
+
+
+def test_incompressible_device_attachments_are_lent_raw(dev):
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        x0 = native.gpu.xgmi_stats()
+        st = _echo(native, s.address, 500, attachment_body="random", device_compress=1)
+        assert st["success"] == 500 and st["error"] == 0, st
+        x1 = native.gpu.xgmi_stats()
+        assert x1["compress_skipped_raw"] - x0["compress_skipped_raw"] >= 900, (x0, x1)
+        assert x1["compressed_sent"] == x0["compressed_sent"]
+    finally:
+        s.stop()
+
+
+@pytest.mark.parametrize("compress", [0, 1])
+def test_device_attachment_indexed_on_arrival(dev, compress):
+    """The attachment is one serialized EchoRequest: the server gets its
+    field table from the device, mirrors the scan, and the press checks the
+    table of every reply."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        c0 = native.gpu.device_codec_stats()
+        st = _echo(native, s.address, 1000, attachment_body="text", attachment_pb=True, device_scan=True,
+                   device_compress=compress)
+        assert st["success"] == 1000 and st["error"] == 0, st
+        c1 = native.gpu.device_codec_stats()
+        assert c1["scans"] - c0["scans"] >= 1900, (c0, c1)
+    finally:
+        s.stop()
+
+
+def test_compressed_device_attachments_verified(dev):
+    """CRC32C of the source on the sender, of the decoded bytes on the
+    receiver (both on the device)."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        x0 = native.gpu.xgmi_stats()
+        st = _echo(native, s.address, 1000, attachment_body="text", device_compress=1, verify_device_payload=True)
+        assert st["success"] == 1000 and st["error"] == 0, st
+        x1 = native.gpu.xgmi_stats()
+        assert x1["crc_failures"] == x0["crc_failures"]
+        assert x1["compressed_recv"] - x0["compressed_recv"] >= 1800
+    finally:
+        s.stop()
+
+
+_SERVER_SCRIPT = r"""
+import sys, torch
+from brpc_amd.models import start_echo_server
+s = start_echo_server("127.0.0.1:0", gpu_device=0)
+print(s.port, flush=True)
+sys.stdin.read()
+s.stop()
+"""
+
+
+def test_compressed_device_attachments_cross_process(dev):
+    """The receiver decodes out of ANOTHER process's arena (IPC-mapped)."""
+    from brpc_amd import native
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    srv = subprocess.Popen([sys.executable, "-c", _SERVER_SCRIPT], stdin=subprocess.PIPE,
+                           stdout=subprocess.PIPE, env=env, text=True)
+    try:
+        port = int(srv.stdout.readline())
+        x0 = native.gpu.xgmi_stats()
+        st = _echo(native, "127.0.0.1:%d" % port, 300, attachment_size=1 << 20, concurrency=4,
+                   attachment_body="text", device_compress=1)
+        assert st["success"] == 300 and st["error"] == 0, st
+        x1 = native.gpu.xgmi_stats()
+        assert x1["compressed_recv"] - x0["compressed_recv"] >= 250, (x0, x1)
+    finally:
+        srv.stdin.close()
+        srv.wait(timeout=60)
