@@ -36,7 +36,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", default="gpu_handler",
                     choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps", "grpc_cpu",
-                             "grpc_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu"])
+                             "grpc_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu", "dev_snappy",
+                             "dev_1m_verify"])
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--body", default="text", help="echo body kind of the codec legs: text, random, const")
     ap.add_argument("--concurrency", type=int, default=50)
@@ -75,6 +76,14 @@ def main():
         o["gpu_process"] = True
     if a.leg in ("dev_64k", "rccl_64k"):
         o["device_attachment"] = True
+    if a.leg == "dev_snappy":
+        # the bench's device_snappy_64KB_<body> leg: an HBM protobuf body
+        # encoded/decoded/indexed on the device both ways
+        o.update({"attachment_size": 65536, "device_attachment": True, "attachment_body": a.body,
+                  "attachment_pb": True, "device_scan": True, "device_compress": 1})
+    if a.leg == "dev_1m_verify":
+        # 1 MiB HBM attachments, CRC32C-verified on the device (fused into the pull)
+        o.update({"attachment_size": 1 << 20, "device_attachment": True, "verify_device_payload": True})
     if a.leg == "echo_32b":
         o["request_size"] = 32
     if a.leg == "lat_100qps":

@@ -124,14 +124,13 @@ def main():
                                                                            err.data_ptr(), stamps.data_ptr(), st)
                         torch.cuda.synchronize()
                         t = stamps.cpu().tolist()
-                        # shader clock at 100 MHz (s_memtime) -> us per phase of block 0
                         # shader-clock cycles per phase of block 0
                         phases = {k: t[i + 1] - t[i] for i, k in
                                   enumerate(("stage", "parse_map", "resolve", "gather"))}
                         phases.update({"parse_decode": t[5], "parse_chain": t[6], "parse_fill": t[7],
                                        "parse_iters": t[9]})
                     print(json.dumps({"kernel": "snappy_decompress_pieces", "impl": impl, "body": kind,
-                                      "block0_phase_us": phases,
+                                      "block0_phase_cycles": phases,
                                       "src": src_at, "dst": dst_at, "pieces": npieces, "bytes_out": total,
                                       "ratio": round(ratio, 3), "us_per_launch": round(us, 1),
                                       "GBps_out": round(total / us / 1e3, 2), "verified": ok,
@@ -158,7 +157,16 @@ def main():
                 ok = not any(errs) and all(
                     native.snappy_uncompress(sl[i * cap:i * cap + lens[i]]) == raw[i * blk:(i + 1) * blk]
                     for i in range(0, npieces, 7))
+                stamps = torch.zeros(8, dtype=torch.int64, device=dev)
+                native.gpu.snappy_compress_stamped_launch(cj_dev.data_ptr(), npieces, blk, scratch.data_ptr(),
+                                                          meta.data_ptr(), meta.data_ptr() + 4 * npieces,
+                                                          stamps.data_ptr(), st)
+                torch.cuda.synchronize()
+                t = stamps.cpu().tolist()
+                # shader-clock cycles per phase of block 0
+                phases = {k: t[i + 1] - t[i] for i, k in enumerate(("stage", "first_pos", "match", "write"))}
                 print(json.dumps({"kernel": "snappy_compress", "body": kind, "src": src_at, "dst": dst_at,
+                                  "block0_phase_cycles": phases,
                                   "blocks": npieces, "bytes_in": total,
                                   "ratio": round(total / max(1, sum(lens)), 3),
                                   "host_ratio": round(ratio, 3), "us_per_launch": round(us, 1),

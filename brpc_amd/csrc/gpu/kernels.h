@@ -133,6 +133,10 @@ constexpr uint64_t SnappyMaxCompressedLength(uint64_t n) { return 32 + n + n / 6
 // is then unused).
 int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch, uint32_t* out_len_dev,
                          int* err_dev, hipStream_t s);
+// Same, stamping block 0's phases (shader clock) into stamps[0..4]: start,
+// staged, earliest-position table built, matched, written.
+int LaunchSnappyCompressStamped(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch,
+                                uint32_t* out_len_dev, int* err_dev, uint64_t* stamps, hipStream_t s);
 // Whether a launch with this max_ulen writes the global scratch (blocks
 // above 16 KiB); otherwise scratch may be null.
 constexpr bool SnappyCompressUsesScratch(uint32_t max_ulen) { return max_ulen > 16384; }

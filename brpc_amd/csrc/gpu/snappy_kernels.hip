@@ -739,7 +739,8 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
                                                                 uint8_t* __restrict__ scratch,
                                                                 uint32_t* __restrict__ out_len,
                                                                 int* __restrict__ err, uint32_t in_cap,
-                                                                uint32_t slot_bytes) {
+                                                                uint32_t slot_bytes,
+                                                                uint64_t* __restrict__ stamps) {
     __shared__ uint16_t table[kWave * kHashEntries];
     __shared__ __attribute__((aligned(16))) uint32_t first_pos[kFirstEntries];
     __shared__ uint32_t sizes[kWave];
@@ -757,6 +758,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         return;
     }
     lbyte* const in = (lbyte*)dyn_lds;
+    stamp(stamps, blk, lane, 0);
     // stage the block in LDS: every match probe below is an LDS read, not an
     // HBM round trip on the lane's serial path
     {
@@ -776,6 +778,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         for (int i = lane; i < kFirstEntries; i += kWave) first_pos[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
+    stamp(stamps, blk, lane, 1);
     const uint32_t seg = (ulen + kWave - 1) / kWave;
     const uint32_t s = min(ulen, seg * (uint32_t)lane);
     const uint32_t e = min(ulen, s + seg);
@@ -783,6 +786,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         atomicMin(&first_pos[(lload32(in + q) * 0x1e35a7bdu) >> (32 - kFirstBits)], q);
     }
     __syncthreads();
+    stamp(stamps, blk, lane, 2);
     uint16_t* ht = table + lane * kHashEntries;
     auto match = [&](auto o0) {
         auto o = o0;
@@ -820,6 +824,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         sizes[lane] = match(as_global(gscratch + (size_t)lane * SnappyCompressSlot()));
     }
     __syncthreads();
+    stamp(stamps, blk, lane, 3);
     // varint header + prefix sum of the 64 slot sizes (DPP scan: lane k
     // holds slot k's size)
     uint32_t hdr = 1;
@@ -886,6 +891,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         out_len[blk] = total;
         err[blk] = 0;
     }
+    stamp(stamps, blk, lane, 4);
 }
 
 }  // namespace
@@ -941,8 +947,8 @@ int LaunchSnappyDecompressPieces(const SnappyPiece* pieces_dev, int n, uint32_t 
     return LaunchSnappyDecompressPiecesStamped(pieces_dev, n, lo, hi, err_dev, nullptr, s);
 }
 
-int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch, uint32_t* out_len_dev,
-                         int* err_dev, hipStream_t s) {
+int LaunchSnappyCompressStamped(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch, uint32_t* out_len_dev,
+                                int* err_dev, uint64_t* stamps, hipStream_t s) {
     if (n <= 0) return 0;
     if (max_ulen == 0) max_ulen = 1;
     if (max_ulen > kSnappyMaxBlock) return -1;
@@ -957,12 +963,17 @@ int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, vo
                   "16 KiB blocks keep their slots in LDS");
     if (!SnappyCompressUsesScratch(max_ulen)) {
         hipLaunchKernelGGL(snappy_compress_kernel<true>, dim3(n), dim3(kWave), in_cap + kWave * slot, s, jobs_dev, n,
-                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot);
+                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot, stamps);
     } else {
         hipLaunchKernelGGL(snappy_compress_kernel<false>, dim3(n), dim3(kWave), in_cap, s, jobs_dev, n,
-                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot);
+                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot, stamps);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int LaunchSnappyCompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, void* scratch, uint32_t* out_len_dev,
+                         int* err_dev, hipStream_t s) {
+    return LaunchSnappyCompressStamped(jobs_dev, n, max_ulen, scratch, out_len_dev, err_dev, nullptr, s);
 }
 
 }  // namespace gpu

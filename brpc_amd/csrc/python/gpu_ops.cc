@@ -231,6 +231,12 @@ void bind_gpu_ops(py::module_& g) {
                                                       as_stream(stream)),
               "snappy_decompress_pieces_serial");
     });
+    g.def("snappy_compress_stamped_launch", [](uintptr_t jobs, int n, uint32_t max_ulen, uintptr_t scratch,
+                                                  uintptr_t out_len, uintptr_t err, uintptr_t stamps, uintptr_t stream) {
+        check(gpu::LaunchSnappyCompressStamped((const gpu::SnappyJob*)jobs, n, max_ulen, (void*)scratch,
+                                               (uint32_t*)out_len, (int*)err, (uint64_t*)stamps, as_stream(stream)),
+              "snappy_compress_stamped");
+    });
     g.def("snappy_decompress_pieces_stamped_launch", [](uintptr_t pieces, int n, uint32_t lo, uint32_t hi,
                                                         uintptr_t err, uintptr_t stamps, uintptr_t stream) {
         check(gpu::LaunchSnappyDecompressPiecesStamped((const gpu::SnappyPiece*)pieces, n, lo, hi, (int*)err,
