@@ -782,8 +782,22 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
     const uint32_t seg = (ulen + kWave - 1) / kWave;
     const uint32_t s = min(ulen, seg * (uint32_t)lane);
     const uint32_t e = min(ulen, s + seg);
-    for (uint32_t q = s; q < e && q + 4 <= ulen; ++q) {
-        atomicMin(&first_pos[(lload32(in + q) * 0x1e35a7bdu) >> (32 - kFirstBits)], q);
+    {
+        // an 8-byte window of the segment in registers, refilled every 4
+        // positions: the atomics issue back to back instead of each waiting
+        // on its own LDS read
+        uint32_t wb = 0xFFFFFFFFu, w0 = 0, w1 = 0;
+        for (uint32_t q = s; q < e && q + 4 <= ulen; ++q) {
+            const uint32_t qb = q & ~3u;
+            if (qb != wb) {
+                lword_c* w = (lword_c*)(in + qb);
+                w0 = w[0];
+                w1 = w[1];
+                wb = qb;
+            }
+            const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, q & 3);
+            atomicMin(&first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)], q);
+        }
     }
     __syncthreads();
     stamp(stamps, blk, lane, 2);
@@ -791,16 +805,31 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
     auto match = [&](auto o0) {
         auto o = o0;
         uint32_t p = s, lit = s;
+        // the probe's serial chain is LDS round trips; per position: the
+        // 4 bytes at p come from a register window (refilled every 4 bytes),
+        // both candidates (the lane's recent table, the block's earliest
+        // table) are read in one round trip, and both are verified in one more
+        uint32_t wb = 0xFFFFFFFFu, w0 = 0, w1 = 0;
         while (p + 4 <= e) {
-            const uint32_t v = lload32(in + p);
-            const uint32_t h = (v * 0x1e35a7bdu) >> (32 - kHashBits);
-            uint32_t cand = ht[h];
-            ht[h] = (uint16_t)p;
-            bool hit = cand != kNoPos && lload32(in + cand) == v;
-            if (!hit) {
-                cand = first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)];
-                hit = cand < p && lload32(in + cand) == v;
+            const uint32_t pb = p & ~3u;
+            if (pb != wb) {
+                lword_c* w = (lword_c*)(in + pb);
+                w0 = w[0];
+                w1 = w[1];
+                wb = pb;
             }
+            const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, p & 3);
+            const uint32_t hm = v * 0x1e35a7bdu;
+            const uint32_t h = hm >> (32 - kHashBits);
+            const uint32_t c1 = ht[h];
+            const uint32_t c2 = first_pos[hm >> (32 - kFirstBits)];
+            ht[h] = (uint16_t)p;
+            const bool ok1 = c1 != kNoPos, ok2 = c2 < p;
+            const uint32_t v1 = lload32(in + (ok1 ? c1 : 0u));
+            const uint32_t v2 = lload32(in + (ok2 ? c2 : 0u));
+            const bool hit1 = ok1 && v1 == v;
+            const bool hit = hit1 || (ok2 && v2 == v);
+            const uint32_t cand = hit1 ? c1 : c2;
             if (hit) {
                 uint32_t len = 4;
                 while (p + len + 8 <= e && lload64(in + cand + len) == lload64(in + p + len)) len += 8;

@@ -592,7 +592,12 @@ int xgmi_recv(Socket* sock, const policy::DevicePayload* const* descs, int n, Bu
     }
     for (int i = 0; i < n; ++i) {
         const policy::DevicePayload& d = *descs[i];
-        g_recv_bytes.fetch_add(d.compress_type() ? d.lent_length() : d.length(), std::memory_order_relaxed);
+        int64_t moved = d.length();
+        if (d.compress_type()) {
+            moved = 0;
+            for (uint32_t c : d.block_clen()) moved += c;
+        }
+        g_recv_bytes.fetch_add(moved, std::memory_order_relaxed);
         if (pm->device != g_device) g_cross_bytes.fetch_add(d.length(), std::memory_order_relaxed);
         if (d.compress_type()) g_comp_recv.fetch_add(1, std::memory_order_relaxed);
     }
