@@ -510,6 +510,7 @@ def main():
                 "scans": c1["scans"] - c0["scans"],
                 "lent_encoded": x1["compressed_sent"] - x0["compressed_sent"],
                 "lent_raw_incompressible": x1["compress_skipped_raw"] - x0["compress_skipped_raw"],
+                "lent_raw_adaptive_skip": x1["compress_skipped_adaptive"] - x0["compress_skipped_adaptive"],
                 "device_ratio": round(enc_in / enc_out, 3) if enc_out else None,
                 "codec_requests_per_launch": round((b1["requests"] - b0["requests"]) / nl, 2) if nl else 0,
                 "bad_tables": c1["bad_tables"] - c0["bad_tables"],

@@ -73,7 +73,7 @@ std::string boot_id() {
 std::atomic<int64_t> g_sent_bytes{0}, g_recv_bytes{0}, g_sent_payloads{0}, g_recv_payloads{0}, g_busy{0},
     g_crc_fail{0}, g_copied_in{0}, g_released_unconsumed{0}, g_cross_bytes{0}, g_cross_payloads{0},
     g_peer_fail{0}, g_peer_access{0}, g_attach_fail{0}, g_peer_maps{0}, g_comp_sent{0}, g_comp_recv{0},
-    g_comp_raw{0}, g_comp_fail{0};
+    g_comp_raw{0}, g_comp_fail{0}, g_comp_skipped{0};
 
 // ------------------------------------------------------------------ lending
 // The process-wide table of blocks lent to peers. A slot holds a Buf that
@@ -353,6 +353,14 @@ PeerMap* peer_of(Socket* sock, std::shared_ptr<Transport>* keep) {
     return ep ? ep->peer.get() : nullptr;
 }
 
+// Adaptive skip (per connection, hashed): after kSkipAfter incompressible
+// payloads in a row a connection lends raw without encoding, probing again
+// every kProbeEvery payloads — a stream of random or already-compressed
+// tensors stops paying for an encode it throws away.
+constexpr int kSkipAfter = 4, kProbeEvery = 32;
+std::atomic<int32_t> g_incompressible[1024];
+std::atomic<int32_t>& streak_of(Socket* sock) { return g_incompressible[(sock->id() * 0x9E3779B97F4A7C15ull) >> 54]; }
+
 // Encode the payload on the device into a fresh lendable block and lend
 // that (gpu/device_codec.h). 0: lent; 1: not worth it or not possible (the
 // caller lends the raw bytes); <0: error.
@@ -374,8 +382,10 @@ int lend_compressed(Socket* sock, const char* src, uint32_t len, const DeviceLen
         // incompressible (random bytes, already-compressed data): decoding
         // would cost the receiver more than the bytes it saves
         g_comp_raw.fetch_add(1, std::memory_order_relaxed);
+        streak_of(sock).fetch_add(1, std::memory_order_relaxed);
         return 1;
     }
+    streak_of(sock).store(0, std::memory_order_relaxed);
     if (opt.verify) {
         // the receiver checks the DECODED bytes: checksum the source
         Segment seg{src, nullptr, len};
@@ -416,8 +426,14 @@ int xgmi_send(Socket* sock, BufBlock* block, uint32_t offset, uint32_t len, cons
     if (block->device != g_device) return 1;  // another GPU's block: stage it
     const char* src = block->data + offset;
     if (opt.compress == COMPRESS_TYPE_SNAPPY && len >= (uint32_t)std::max(1, FLAGS_device_payload_compress_min_bytes)) {
-        const int rc = lend_compressed(sock, src, len, opt, d);
-        if (rc <= 0) return rc;
+        const int32_t streak = streak_of(sock).load(std::memory_order_relaxed);
+        if (streak < kSkipAfter || streak % kProbeEvery == 0) {
+            const int rc = lend_compressed(sock, src, len, opt, d);
+            if (rc <= 0) return rc;
+        } else {
+            streak_of(sock).fetch_add(1, std::memory_order_relaxed);
+            g_comp_skipped.fetch_add(1, std::memory_order_relaxed);
+        }
     }
     int64_t aoff = ArenaOffset(src, g_device);
     Buf hold;
@@ -731,6 +747,7 @@ XgmiStats GetXgmiStats() {
     s.compressed_recv = g_comp_recv.load();
     s.compress_skipped_raw = g_comp_raw.load();
     s.compress_failures = g_comp_fail.load();
+    s.compress_skipped_adaptive = g_comp_skipped.load();
     return s;
 }
 

@@ -62,6 +62,8 @@ struct XgmiStats {
     // lent encoded, decoded on arrival, lent raw because incompressible, or
     // lent raw because the device encode failed
     int64_t compressed_sent = 0, compressed_recv = 0, compress_skipped_raw = 0, compress_failures = 0;
+    // lent raw without an encode: the connection's recent payloads were incompressible
+    int64_t compress_skipped_adaptive = 0;
 };
 XgmiStats GetXgmiStats();
 

@@ -571,6 +571,7 @@ PYBIND11_MODULE(_native, m) {
         d["compressed_recv"] = s.compressed_recv;
         d["compress_skipped_raw"] = s.compress_skipped_raw;
         d["compress_failures"] = s.compress_failures;
+        d["compress_skipped_adaptive"] = s.compress_skipped_adaptive;
         int64_t staged = 0, staged_bytes = 0;
         GetStagedStats(&staged, &staged_bytes);
         d["staged_payloads"] = staged;

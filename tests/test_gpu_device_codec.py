@@ -150,7 +150,12 @@ def test_incompressible_device_attachments_are_lent_raw(dev):
         st = _echo(native, s.address, 500, attachment_body="random", device_compress=1)
         assert st["success"] == 500 and st["error"] == 0, st
         x1 = native.gpu.xgmi_stats()
-        assert x1["compress_skipped_raw"] - x0["compress_skipped_raw"] >= 900, (x0, x1)
+        encoded_then_raw = x1["compress_skipped_raw"] - x0["compress_skipped_raw"]
+        never_encoded = x1["compress_skipped_adaptive"] - x0["compress_skipped_adaptive"]
+        # a few encodes per connection direction, then the adaptive skip
+        # (with a probe every 32 payloads) lends the rest raw unencoded
+        assert encoded_then_raw + never_encoded >= 900, (x0, x1)
+        assert never_encoded >= 700, (x0, x1)
         assert x1["compressed_sent"] == x0["compressed_sent"]
     finally:
         s.stop()
