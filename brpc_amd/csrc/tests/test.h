@@ -54,6 +54,10 @@ void report_failure(const char* file, int line, const std::string& msg);
 #define EXPECT_TRUE(c) MTEST_CHECK_((c), "EXPECT_TRUE(" #c ")", (void)0)
 #define EXPECT_FALSE(c) MTEST_CHECK_(!(c), "EXPECT_FALSE(" #c ")", (void)0)
 #define ASSERT_TRUE(c) MTEST_CHECK_((c), "ASSERT_TRUE(" #c ")", return)
+// with a context message (a std::string expression)
+#define EXPECT_TRUE_M(c, m) MTEST_CHECK_((c), std::string("EXPECT_TRUE(" #c ") ") + (m), (void)0)
+#define EXPECT_FALSE_M(c, m) MTEST_CHECK_(!(c), std::string("EXPECT_FALSE(" #c ") ") + (m), (void)0)
+#define ASSERT_TRUE_M(c, m) MTEST_CHECK_((c), std::string("ASSERT_TRUE(" #c ") ") + (m), return)
 #define ASSERT_FALSE(c) MTEST_CHECK_(!(c), "ASSERT_FALSE(" #c ")", return)
 #define MTEST_CMP_(a, b, op, on_fail) \
     MTEST_CHECK_(((a)op(b)), std::string(#a " " #op " " #b " : ") + mtest::fmt2((a), (b)), on_fail)
