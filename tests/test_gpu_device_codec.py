@@ -152,10 +152,12 @@ def test_incompressible_device_attachments_are_lent_raw(dev):
         x1 = native.gpu.xgmi_stats()
         encoded_then_raw = x1["compress_skipped_raw"] - x0["compress_skipped_raw"]
         never_encoded = x1["compress_skipped_adaptive"] - x0["compress_skipped_adaptive"]
-        # a few encodes per connection direction, then the adaptive skip
-        # (with a probe every 32 payloads) lends the rest raw unencoded
-        assert encoded_then_raw + never_encoded >= 900, (x0, x1)
-        assert never_encoded >= 700, (x0, x1)
+        # requests only: a request that arrived raw is echoed raw (the server
+        # mirrors what it received). A few encodes while the in-flight calls
+        # race the streak, then the adaptive skip (a probe every 32 payloads)
+        # lends the rest raw without encoding
+        assert encoded_then_raw + never_encoded >= 450, (x0, x1)
+        assert never_encoded >= 300, (x0, x1)
         assert x1["compressed_sent"] == x0["compressed_sent"]
     finally:
         s.stop()
