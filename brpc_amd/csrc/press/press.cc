@@ -432,6 +432,7 @@ void PressSession::finish(PressCall* call) {
                 ok = false;
                 cntl.SetFailed(ERESPONSE, "echoed attachment mismatch (%zu bytes)", got.size());
             } else if (_device_attachment && _opt.device_scan && _fanout == 1 &&
+                       !cntl.response_attachment().all_host_accessible() &&
                        (ix.nfields != 1 || ix.fields.size() < 2 || ix.fields[0] != ((1u << 3) | 2) ||
                         (ix.fields[1] & 0xffffffffu) != (uint64_t)(_attachment.size() - (ix.fields[1] >> 32)))) {
                 // the reply's device field table: one length-delimited field 1

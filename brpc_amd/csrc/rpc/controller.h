@@ -192,7 +192,10 @@ public:
     void set_device_payload_scan(bool on) { _device_payload_scan = on; }
     bool device_payload_scan() const { return _device_payload_scan; }
     // What arrived: the field table of a received pb_scan payload, and the
-    // device compression the peer used (COMPRESS_TYPE_NONE: lent raw).
+    // device compression the peer used (COMPRESS_TYPE_NONE: lent raw). The
+    // table exists only for payloads that came over the device transport: a
+    // payload staged inline over TCP (no transport yet, or a busy lender)
+    // arrives as host bytes with nfields = -1, for the host parser.
     const DevicePayloadIndex& device_payload_index() const { return _device_payload_index; }
     CompressType received_device_payload_compress_type() const { return _received_device_compress; }
 
