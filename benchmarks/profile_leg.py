@@ -130,6 +130,8 @@ def main():
     print("leg=%s qps=%.0f p50=%s p99=%s errors=%d samples=%d cpus_used=%.2f cgroup=%s" % (
         a.leg, st["qps"], st["p50_us"], st["p99_us"], st["error"], n, cpu, thr))
     x1 = native.gpu.xgmi_stats()
+    if a.leg == "dev_snappy":
+        print("device codec:", native.gpu.device_codec_stats(), "codec batch:", native.gpu.codec_batch_stats())
     if os.environ.get("RESIDENT"):
         print("resident:", native.gpu.resident_stats())
     subs = x1["copy_submits"] - x0["copy_submits"]

@@ -117,16 +117,19 @@ __device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch,
         out[m] = acc;
         return;
     }
-    unsigned long long* slot = reinterpret_cast<unsigned long long*>(scratch) + m;
-    unsigned long long old = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), assumed, nv;
-    do {
-        assumed = old;
-        nv = (((assumed >> 32) + 1ull) << 32) | (unsigned long long)((uint32_t)assumed ^ acc);
-        old = atomicCAS(slot, assumed, nv);
-    } while (old != assumed);
-    if ((uint32_t)(nv >> 32) == chunks) {
-        atomicExch(slot, 0ull);
-        out[m] = (uint32_t)nv;
+    // XOR is order-free: one atomic XOR into the message's CRC word, then one
+    // counter increment that releases it; the chunk that brings the count to
+    // `chunks` acquires every other chunk's XOR, takes the CRC and resets the
+    // slot. Two single-shot L2 atomics per chunk (a CAS loop on one 64-bit
+    // word serialized the 64 chunks of a 1 MiB message behind retries).
+    uint32_t* crc_word = scratch + 2 * m;
+    uint32_t* cnt_word = scratch + 2 * m + 1;
+    __hip_atomic_fetch_xor(crc_word, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t before = __hip_atomic_fetch_add(cnt_word, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (before + 1 == chunks) {
+        const uint32_t v = __hip_atomic_exchange(crc_word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cnt_word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        out[m] = v;
     }
 }
 

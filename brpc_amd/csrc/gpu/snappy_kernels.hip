@@ -316,6 +316,21 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(con
     if (pc.ulen <= lo || pc.ulen > hi) return;
     const uint32_t ulen = pc.ulen;
     stamp(stamps, blk, lane, 0);
+    // Incompressible pieces (one long literal, 1.14:1 or worse) and very
+    // compressible ones (a few long copies, 8:1 or better) decode faster one
+    // element per wave step: the source map costs one pass per 64 output
+    // bytes and the resolve one round per doubling of the copy-chain depth,
+    // whatever the element count (MI355X, 4 KiB pieces: random 18 vs 3.5 us,
+    // one repeated byte 41 vs 22 us per launch of 112; text stays here).
+    if ((uint64_t)pc.src_len * 8 >= (uint64_t)ulen * 7 || (uint64_t)pc.src_len * 8 <= ulen) {
+        const uint32_t mis4 = (uint32_t)((uintptr_t)pc.src & 3);
+        gbyte_c* in4 = as_global(static_cast<const uint8_t*>(pc.src) - mis4);
+        const uint32_t in_len = pc.src_len + mis4;
+        const uint32_t win = load_window(in4, in_len, 0, lane);
+        const int bad = decode_elements(in4, in_len, mis4, 0, win, ulen, lds, pc.dst, lane);
+        if (lane == 0) err[blk] = bad;
+        return;
+    }
     // stage: the piece from the 16-byte boundary below it (a 16-byte
     // aligned chunk never crosses a page, so reading its unused head and
     // tail stays inside mapped memory)
@@ -688,9 +703,17 @@ __device__ __forceinline__ O emit_literal(O o, S src, uint32_t len) {
         *o++ = (uint8_t)n;
         *o++ = (uint8_t)(n >> 8);
     }
-    // 4 source bytes per LDS round trip (lload32), written byte by byte
-    // (the output slot has any alignment; stores need no wait)
+    // 16 source bytes per LDS round trip (two lload64 issued together), then
+    // 4 (lload32), written byte by byte (the output slot has any alignment;
+    // stores need no wait)
     uint32_t k = 0;
+    for (; k + 16 <= len; k += 16) {
+        const uint64_t a = lload64(src + k), b = lload64(src + k + 8);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[k + i] = (uint8_t)(a >> (8 * i));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[k + 8 + i] = (uint8_t)(b >> (8 * i));
+    }
     for (; k + 4 <= len; k += 4) {
         const uint32_t v = lload32(src + k);
         o[k] = (uint8_t)v;
@@ -831,9 +854,19 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
             const bool hit = hit1 || (ok2 && v2 == v);
             const uint32_t cand = hit1 ? c1 : c2;
             if (hit) {
+                // 8 bytes per LDS round trip; the first differing byte comes
+                // from the XOR (reads may run up to 7 bytes past e: clamped)
                 uint32_t len = 4;
-                while (p + len + 8 <= e && lload64(in + cand + len) == lload64(in + p + len)) len += 8;
-                while (p + len < e && in[cand + len] == in[p + len]) ++len;
+                for (;;) {
+                    if (p + len >= e) break;
+                    const uint64_t x = lload64(in + cand + len) ^ lload64(in + p + len);
+                    if (x) {
+                        len += (uint32_t)__builtin_ctzll(x) >> 3;
+                        break;
+                    }
+                    len += 8;
+                }
+                len = min(len, e - p);
                 if (p > lit) o = emit_literal(o, in + lit, p - lit);
                 o = emit_copy(o, p - cand, len);
                 p += len;

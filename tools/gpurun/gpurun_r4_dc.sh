@@ -20,18 +20,22 @@ for spec in dev_snappy:text dev_snappy:random grpc_cpu:text grpc_cpu:random dev_
     head -1 $P/leg_${leg}_${body}.txt
 done
 cd /tmp
-timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$R/$P/kt_dev_snappy" -o run -- \
-    python3 "$R/benchmarks/profile_leg.py" --leg dev_snappy --body text --seconds 2 --no-profile \
-    > "$R/$P/kt_dev_snappy.log" 2>&1 || exit $?
+for leg in dev_snappy dev_1m_verify; do
+    timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$P/kt_$leg" -o run -- \
+        python3 "$R/benchmarks/profile_leg.py" --leg $leg --body text --seconds 2 --no-profile \
+        > "$R/$P/kt_$leg.log" 2>&1 || exit $?
+done
 for leg in dev_snappy dev_1m_verify; do
     for c in FETCH_SIZE WRITE_SIZE; do
-        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d "$R/$P/pmc_${c}_${leg}" -o run -- \
+        timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$R/$P/pmc_${c}_${leg}" -o run -- \
             python3 "$R/benchmarks/profile_leg.py" --leg $leg --body text --seconds 1 --no-profile \
             > "$R/$P/pmc_${c}_${leg}.log" 2>&1 || exit $?
     done
 done
 cd "$R"
-python3 benchmarks/rocprof_summary.py $P/kt_dev_snappy --prune > $P/kt_dev_snappy_summary.txt 2>&1
+for leg in dev_snappy dev_1m_verify; do
+    python3 benchmarks/rocprof_summary.py $P/kt_$leg --prune > $P/kt_${leg}_summary.txt 2>&1
+done
 for leg in dev_snappy dev_1m_verify; do
     python3 benchmarks/rocprof_summary.py $P/pmc_FETCH_SIZE_$leg $P/pmc_WRITE_SIZE_$leg --prune \
         > $P/pmc_${leg}_summary.txt 2>&1
