@@ -84,7 +84,24 @@ struct HbmTls {
         }
     }
 };
-thread_local HbmTls tls_hbm;
+// The per-thread caches live on the heap behind a 16-byte TLS holder: the
+// caches are 60+ KiB, and a TLS segment that small lets libmrpc use the
+// initial-exec TLS model (no __tls_get_addr call per thread-local access).
+template <typename T>
+struct TlsHolder {
+    T* p = nullptr;
+    bool dead = false;
+    ~TlsHolder() {
+        dead = true;
+        delete p;
+        p = nullptr;
+    }
+    T* get() {
+        if (!p && !dead) p = new T;
+        return p;
+    }
+};
+thread_local TlsHolder<HbmTls> tls_hbm;
 
 bool arena_init(int device, std::string* error) {
     Arena& a = g_arena[device];
@@ -144,7 +161,7 @@ struct PinnedTls {
         }
     }
 };
-thread_local PinnedTls tls_pinned;
+thread_local TlsHolder<PinnedTls> tls_pinned;
 const int kPinnedMaxClass = 22;  // 4 MiB; larger pinned buffers are dedicated allocations
 
 // Arena fully carved: cut the smallest free block of a larger class into
@@ -214,9 +231,9 @@ void* HbmAlloc(size_t n, int device) {
     Arena& a = g_arena[device];
     if (c <= kMaxClass && arena_init(device, nullptr)) {
         char* p = nullptr;
-        HbmTls& t = tls_hbm;
-        if (t.alive && t.c[device].n[c] > 0) {
-            p = t.c[device].items[c][--t.c[device].n[c]];
+        HbmTls* t = tls_hbm.get();
+        if (t && t->alive && t->c[device].n[c] > 0) {
+            p = t->c[device].items[c][--t->c[device].n[c]];
         } else {
             {
                 std::lock_guard<std::mutex> g(a.lists[c].mu);
@@ -285,9 +302,9 @@ void HbmFree(void* p, size_t n, int device) {
     Arena& a = g_arena[device];
     a.live_blocks.fetch_sub(1, std::memory_order_relaxed);
     a.live_bytes.fetch_sub((int64_t)1 << c, std::memory_order_relaxed);
-    HbmTls& t = tls_hbm;
-    if (t.alive && t.c[device].n[c] < tls_limit(c)) {
-        t.c[device].items[c][t.c[device].n[c]++] = static_cast<char*>(p);
+    HbmTls* t = tls_hbm.get();
+    if (t && t->alive && t->c[device].n[c] < tls_limit(c)) {
+        t->c[device].items[c][t->c[device].n[c]++] = static_cast<char*>(p);
         return;
     }
     std::lock_guard<std::mutex> g(a.lists[c].mu);
@@ -329,8 +346,8 @@ void* PinnedAlloc(size_t n) {
         if (p) ps.bytes.fetch_add((int64_t)n, std::memory_order_relaxed);
         return p;
     }
-    PinnedTls& t = tls_pinned;
-    if (t.alive && t.c.n[c] > 0) return t.c.items[c][--t.c.n[c]];
+    PinnedTls* t = tls_pinned.get();
+    if (t && t->alive && t->c.n[c] > 0) return t->c.items[c][--t->c.n[c]];
     {
         std::lock_guard<std::mutex> g(ps.lists[c].mu);
         if (!ps.lists[c].items.empty()) {
@@ -366,9 +383,9 @@ void PinnedFree(void* p, size_t n) {
         ps.bytes.fetch_sub((int64_t)n, std::memory_order_relaxed);
         return;
     }
-    PinnedTls& t = tls_pinned;
-    if (t.alive && t.c.n[c] < tls_limit(c)) {
-        t.c.items[c][t.c.n[c]++] = static_cast<char*>(p);
+    PinnedTls* t = tls_pinned.get();
+    if (t && t->alive && t->c.n[c] < tls_limit(c)) {
+        t->c.items[c][t->c.n[c]++] = static_cast<char*>(p);
         return;
     }
     std::lock_guard<std::mutex> g(ps.lists[c].mu);

@@ -89,7 +89,13 @@ def main():
     pybind_inc = pybind11.get_include()
     ext_suffix = sysconfig.get_config_var("EXT_SUFFIX")
 
-    cxxflags = (f"-std=c++17 {opt} {san} -fPIC -pthread -march=x86-64-v2 -mpclmul "
+    # TLS descriptors: thread-locals of the dlopen'ed libmrpc (fiber worker
+    # state, pool caches, var agents) resolve through _dl_tlsdesc_dynamic's
+    # register-preserving fast path instead of a PLT call into
+    # __tls_get_addr (17% of a device-codec leg's host samples). initial-exec
+    # is not an option: torch's libraries leave no static TLS surplus
+    tls = "" if san else "-mtls-dialect=gnu2"
+    cxxflags = (f"-std=c++17 {opt} {san} {tls} -fPIC -pthread -march=x86-64-v2 -mpclmul "
                 f"-Wall -Wno-unused-function -Wno-invalid-offsetof -Wno-unused-variable "
                 f"-Wno-sign-compare -Wno-class-memaccess -Wno-unused-but-set-variable -Wno-unused-result "
                 f"-D__HIP_PLATFORM_AMD__ -DMRPC_GPU_ARCH=\\\"{ARCH}\\\" "
