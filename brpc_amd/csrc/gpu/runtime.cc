@@ -26,6 +26,9 @@ DEFINE_bool(pinned_coherent, true,
             "(cached), which is only safe when kernels never re-read recycled pinned blocks");
 DEFINE_int32(gpu_streams_per_device, 4, "HIP streams per device in the pool (<= GPU_MAX_HW_QUEUES)");
 DEFINE_int32(gpu_poller_spin_us, 50, "event poller busy-polls this long after the last completion before backing off");
+DEFINE_int32(gpu_poller_wait_pct, 50,
+             "the event poller sleeps until the oldest in-flight event reached this share of the recent "
+             "hand-over-to-completion time before polling (0: poll continuously)");
 DEFINE_int32(gpu_poller_sleep_us, 2, "event poller sleep between polls once the spin budget is spent");
 DEFINE_int32(gpu_poller_idle_spin_us, 0,
              "with nothing in flight the event poller watches for new events this long before sleeping "
@@ -82,6 +85,7 @@ struct Waiter {
     ResidentRing* ring = nullptr;
     uint64_t first = 0, last = 0;
     int64_t since_us = 0;
+    int64_t added_us = 0;  // when the poller was handed the event
 };
 
 class EventPoller {
@@ -95,6 +99,7 @@ public:
                 pthread_create(&_th, nullptr, &EventPoller::run, this);
             }
             _incoming.push_back(w);
+            _incoming.back().added_us = now_us();
             _nincoming.store(1, std::memory_order_release);
             wake = _sleeping;
         }
@@ -169,7 +174,13 @@ private:
                     active[keep++] = active[i];
                     continue;
                 }
-                if (active[i].done_us) *active[i].done_us = now_us();
+                {
+                    const int64_t t = now_us();
+                    if (active[i].done_us) *active[i].done_us = t;
+                    // how long events take from hand-over to completion
+                    const int64_t took = t - active[i].added_us;
+                    if (took > 0 && took < 100000) _ema_us += (took - _ema_us) / 8;
+                }
                 active[i].butex->store(r == hipSuccess ? 1 : -1, std::memory_order_release);
                 // queue the woken fibers without signalling; one signal for
                 // the whole pass below (fewer futex wake-ups of idle workers)
@@ -182,8 +193,26 @@ private:
             if (!active.empty()) {
                 const int64_t t = now_us();
                 if (progressed) last_progress_us = t;
-                if (t - last_progress_us > FLAGS_gpu_poller_spin_us) {
-                    timespec ts{0, 1000L * std::max(1, FLAGS_gpu_poller_sleep_us)};
+                // nothing can be due before the oldest event reached a share
+                // of the typical completion time: sleep until then instead of
+                // calling hipEventQuery in a loop (each call walks the HIP
+                // runtime's thread-locals and locks; a spinning poller was a
+                // full host core under codec load)
+                int64_t oldest = t;
+                for (const Waiter& w : active) oldest = std::min(oldest, w.added_us);
+                const int64_t due = oldest + _ema_us * FLAGS_gpu_poller_wait_pct / 100;
+                int64_t sleep_us = 0;
+                if (FLAGS_gpu_poller_wait_pct > 0 && due - t >= 8) {
+                    sleep_us = std::min<int64_t>(due - t, 200);
+                } else if (!progressed && FLAGS_gpu_poller_wait_pct > 0 && _ema_us >= 20) {
+                    // long events (codec batches, large pulls): one pass per
+                    // ~tenth of their duration is enough
+                    sleep_us = std::max<int64_t>(2, std::min<int64_t>(_ema_us / 10, 10));
+                } else if (t - last_progress_us > FLAGS_gpu_poller_spin_us) {
+                    sleep_us = std::max(1, FLAGS_gpu_poller_sleep_us);
+                }
+                if (sleep_us) {
+                    timespec ts{0, 1000L * sleep_us};
                     nanosleep(&ts, nullptr);
                 }
             }
@@ -198,6 +227,7 @@ private:
     bool _started = false;
     pthread_t _th;
     std::atomic<int64_t> _polled{0};
+    int64_t _ema_us = 0;  // hand-over to completion, moving average (poller thread only)
 };
 
 EventPoller* poller() {
