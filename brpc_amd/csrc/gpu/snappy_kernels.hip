@@ -690,6 +690,24 @@ __device__ __forceinline__ uint64_t lload64(const lbyte* p) {
     return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
 }
 
+// A literal element's tag (1-3 bytes) for `len` bytes; the bytes follow.
+template <typename O>
+__device__ __forceinline__ O emit_literal_tag(O o, uint32_t len) {
+    const uint32_t n = len - 1;
+    if (n < 60) {
+        *o++ = (uint8_t)(n << 2);
+    } else if (n < 256) {
+        *o++ = (uint8_t)(60 << 2);
+        *o++ = (uint8_t)n;
+    } else {
+        *o++ = (uint8_t)(61 << 2);
+        *o++ = (uint8_t)n;
+        *o++ = (uint8_t)(n >> 8);
+    }
+    return o;
+}
+constexpr int kLitSpans = 16;  // deferred literal copies per lane (more are copied in place)
+
 template <typename O, typename S>
 __device__ __forceinline__ O emit_literal(O o, S src, uint32_t len) {
     const uint32_t n = len - 1;
@@ -757,16 +775,30 @@ __device__ __forceinline__ O emit_copy(O o, uint32_t off, uint32_t len) {
 // Dynamic LDS: the block's input (in_cap bytes), then — kOutLds — the 64
 // lanes' output slots of `slot` bytes each; otherwise the slots live in the
 // global scratch (blocks above 32 KiB, whose slots would not fit).
-template <bool kOutLds>
+// kCand (blocks up to kCandMax, the RPC path's 4 KiB blocks): no per-lane
+// recent table; after the earliest-position table is built, a candidate pass
+// gives every position its match candidate (the earliest earlier position
+// with the same 4 bytes, verified) in a u16 array after the slots, four
+// positions per three LDS round trips with no chain between positions. The
+// lane's walk then reads four candidates per round trip, so a run of misses
+// costs ALU only; the wave pays round trips where some lane extends a match.
+constexpr uint32_t kCandMax = 8192;
+// (Padding the staged input and the candidates so that lanes 64 bytes apart
+// hit distinct LDS banks was measured slower on MI355X: 56 vs 51 us per
+// 112-block launch of text; the layouts stay dense.)
+__host__ __device__ constexpr uint32_t CompressInBytes(uint32_t in_cap, bool) { return in_cap; }
+__host__ __device__ constexpr uint32_t CompressCandBytes(uint32_t in_cap) { return 2 * in_cap + 16; }
+template <bool kOutLds, bool kCand>
 __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob* __restrict__ jobs, int n,
                                                                 uint8_t* __restrict__ scratch,
                                                                 uint32_t* __restrict__ out_len,
                                                                 int* __restrict__ err, uint32_t in_cap,
                                                                 uint32_t slot_bytes,
                                                                 uint64_t* __restrict__ stamps) {
-    __shared__ uint16_t table[kWave * kHashEntries];
+    __shared__ uint16_t table[kCand ? 1 : kWave * kHashEntries];
     __shared__ __attribute__((aligned(16))) uint32_t first_pos[kFirstEntries];
     __shared__ uint32_t sizes[kWave];
+    __shared__ uint64_t spans[kWave * kLitSpans];  // deferred literal copies per lane
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
     const int blk = blockIdx.x;
     if (blk >= n) return;
@@ -781,6 +813,18 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         return;
     }
     lbyte* const in = (lbyte*)dyn_lds;
+    const uint32_t in_bytes = CompressInBytes(in_cap, kCand);
+    // input accessors over the (kCand: padded) staging
+    auto dw = [&](uint32_t d) -> uint32_t { return ((lword_c*)in)[d]; };
+    auto rd8 = [&](uint32_t x) -> uint8_t { return in[x]; };
+    auto rd32 = [&](uint32_t x) -> uint32_t {
+        const uint32_t d = x >> 2;
+        return __builtin_amdgcn_alignbyte(dw(d + 1), dw(d), x & 3);
+    };
+    auto rd64 = [&](uint32_t x) -> uint64_t {
+        const uint32_t d = x >> 2, w0 = dw(d), w1 = dw(d + 1), w2 = dw(d + 2), sh = x & 3;
+        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+    };
     stamp(stamps, blk, lane, 0);
     // stage the block in LDS: every match probe below is an LDS read, not an
     // HBM round trip on the lane's serial path
@@ -797,7 +841,8 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         }
         for (uint32_t o = done + lane; o < ulen; o += kWave) in[o] = src[o];
         uint32_t* t = reinterpret_cast<uint32_t*>(table);
-        for (int i = lane; i < kWave * kHashEntries / 2; i += kWave) t[i] = 0xFFFFFFFFu;
+        if (!kCand)
+            for (int i = lane; i < kWave * kHashEntries / 2; i += kWave) t[i] = 0xFFFFFFFFu;
         for (int i = lane; i < kFirstEntries; i += kWave) first_pos[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
@@ -813,9 +858,8 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         for (uint32_t q = s; q < e && q + 4 <= ulen; ++q) {
             const uint32_t qb = q & ~3u;
             if (qb != wb) {
-                lword_c* w = (lword_c*)(in + qb);
-                w0 = w[0];
-                w1 = w[1];
+                w0 = dw(qb >> 2);
+                w1 = dw((qb >> 2) + 1);
                 wb = qb;
             }
             const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, q & 3);
@@ -823,11 +867,79 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         }
     }
     __syncthreads();
+    // candidates (kCand): u16 per position after the output slots; a lane
+    // writes and reads only its own segment's entries (no barrier needed)
+    __attribute__((address_space(3))) uint16_t* const mc =
+        (__attribute__((address_space(3))) uint16_t*)(in + in_bytes + (kOutLds ? kWave * slot_bytes : 0));
+    if (kCand) {
+        for (uint32_t qb = s & ~3u; qb < e; qb += 4) {
+            const uint32_t w0 = dw(qb >> 2), w1 = dw((qb >> 2) + 1);
+            uint32_t c[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)i);
+                c[i] = first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t q = qb + (uint32_t)i;
+                const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)i);
+                const bool ok = c[i] < q && q + 4 <= ulen && rd32(c[i] < q ? c[i] : 0u) == v;
+                if (q >= s && q < e) mc[q] = ok ? (uint16_t)c[i] : kNoPos;
+            }
+        }
+    }
     stamp(stamps, blk, lane, 2);
-    uint16_t* ht = table + lane * kHashEntries;
+    uint16_t* ht = table + (kCand ? 0 : lane * kHashEntries);
     auto match = [&](auto o0) {
         auto o = o0;
+        // Literal bytes are not copied inside the walk: their tags are
+        // written and their bytes filled after it, so a lane that found a
+        // long literal does not hold the wave's other lanes (a divergent wave
+        // pays for every path any lane takes).
+        uint64_t* const sp = spans + lane * kLitSpans;
+        int nsp = 0;
+        auto literal = [&](auto out, uint32_t from, uint32_t n) {
+            if (nsp < kLitSpans) {
+                out = emit_literal_tag(out, n);
+                sp[nsp++] = (uint64_t)from | ((uint64_t)n << 24) | ((uint64_t)(uint32_t)(out - o0) << 44);
+                return out + n;
+            }
+            out = emit_literal_tag(out, n);
+            for (uint32_t k = 0; k < n; ++k) out[k] = rd8(from + k);
+            return out + n;
+        };
         uint32_t p = s, lit = s;
+        if (kCand) {
+            uint32_t cb = 0xFFFFFFFFu;
+            uint64_t cw = 0;
+            while (p + 4 <= e) {
+                if ((p >> 2) != cb) {  // four candidates per LDS read
+                    cb = p >> 2;
+                    cw = *(const __attribute__((address_space(3))) uint64_t*)(mc + (cb << 2));
+                }
+                const uint32_t cand = (uint32_t)(cw >> (16 * (p & 3))) & 0xFFFF;
+                if (cand != kNoPos) {
+                    uint32_t len = 4;
+                    for (;;) {
+                        if (p + len >= e) break;
+                        const uint64_t x = rd64(cand + len) ^ rd64(p + len);
+                        if (x) {
+                            len += (uint32_t)__builtin_ctzll(x) >> 3;
+                            break;
+                        }
+                        len += 8;
+                    }
+                    len = min(len, e - p);
+                    if (p > lit) o = literal(o, lit, p - lit);
+                    o = emit_copy(o, p - cand, len);
+                    p += len;
+                    lit = p;
+                } else {
+                    p += 1 + ((p - lit) >> 5);
+                }
+            }
+        } else {
         // the probe's serial chain is LDS round trips; per position: the
         // 4 bytes at p come from a register window (refilled every 4 bytes),
         // both candidates (the lane's recent table, the block's earliest
@@ -867,7 +979,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
                     len += 8;
                 }
                 len = min(len, e - p);
-                if (p > lit) o = emit_literal(o, in + lit, p - lit);
+                if (p > lit) o = literal(o, lit, p - lit);
                 o = emit_copy(o, p - cand, len);
                 p += len;
                 lit = p;
@@ -875,10 +987,33 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
                 p += 1 + ((p - lit) >> 5);
             }
         }
-        if (e > lit) o = emit_literal(o, in + lit, e - lit);
+        }
+        if (e > lit) o = literal(o, lit, e - lit);
+        // the deferred literal bytes: 16 per LDS round trip
+        for (int i = 0; i < nsp; ++i) {
+            const uint64_t d = sp[i];
+            const uint32_t from = (uint32_t)(d & 0xFFFFFF), n = (uint32_t)((d >> 24) & 0xFFFFF);
+            auto out = o0 + (uint32_t)(d >> 44);
+            uint32_t k = 0;
+            for (; k + 16 <= n; k += 16) {
+                const uint64_t x0 = rd64(from + k), x1 = rd64(from + k + 8);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) out[k + j] = (uint8_t)(x0 >> (8 * j));
+#pragma unroll
+                for (int j = 0; j < 8; ++j) out[k + 8 + j] = (uint8_t)(x1 >> (8 * j));
+            }
+            for (; k + 4 <= n; k += 4) {
+                const uint32_t x = rd32(from + k);
+                out[k] = (uint8_t)x;
+                out[k + 1] = (uint8_t)(x >> 8);
+                out[k + 2] = (uint8_t)(x >> 16);
+                out[k + 3] = (uint8_t)(x >> 24);
+            }
+            for (; k < n; ++k) out[k] = rd8(from + k);
+        }
         return (uint32_t)(o - o0);
     };
-    lbyte* const lds_slots = in + in_cap;
+    lbyte* const lds_slots = in + in_bytes;
     uint8_t* const gscratch = scratch + (size_t)blk * SnappyCompressScratchPerBlock();
     if (kOutLds) {
         sizes[lane] = match(lds_slots + (size_t)lane * slot_bytes);
@@ -915,9 +1050,11 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
             stage[lane] = (uint8_t)((u & 0x7f) | (lane + 1 < (int)hdr ? 0x80 : 0));
         }
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const lbyte* src = lds_slots + (size_t)lane * slot_bytes;  // 16-byte aligned
+        // (read as 4-byte-aligned vectors: any slot stride works)
+        typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+        const lbyte* src = lds_slots + (size_t)lane * slot_bytes;
         for (uint32_t j = 0; j < my_size; j += 16) {
-            const u32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(src + j);
+            const u32x4a4 v = *reinterpret_cast<const __attribute__((address_space(3))) u32x4a4*>(src + j);
             const uint32_t n = min(16u, my_size - j);
 #pragma unroll
             for (uint32_t b = 0; b < 16; ++b) {
@@ -1021,13 +1158,19 @@ int LaunchSnappyCompressStamped(const SnappyJob* jobs_dev, int n, uint32_t max_u
     // slots in LDS too while that keeps >= 2 waves per CU (blocks up to
     // 16 KiB: <= 67 KiB); a 32 KiB block with LDS slots would run alone on its CU
     static_assert(16384 + kWave * ((16384 / kWave + 16 + 15) & ~15u) + kWave * kHashEntries * 2 + kFirstEntries * 4 +
-                          kWave * 4 <= 80 * 1024,
+                          kWave * 4 + kWave * kLitSpans * 8 <= 80 * 1024,
                   "16 KiB blocks keep their slots in LDS");
-    if (!SnappyCompressUsesScratch(max_ulen)) {
-        hipLaunchKernelGGL(snappy_compress_kernel<true>, dim3(n), dim3(kWave), in_cap + kWave * slot, s, jobs_dev, n,
-                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot, stamps);
+    if (max_ulen <= kCandMax) {
+        // input, slots and the candidate array in LDS: <= 8 + 9 + 16 KiB
+        const uint32_t cslot = slot;
+        hipLaunchKernelGGL((snappy_compress_kernel<true, true>), dim3(n), dim3(kWave),
+                           CompressInBytes(in_cap, true) + kWave * cslot + CompressCandBytes(in_cap), s, jobs_dev, n,
+                           static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, cslot, stamps);
+    } else if (!SnappyCompressUsesScratch(max_ulen)) {
+        hipLaunchKernelGGL((snappy_compress_kernel<true, false>), dim3(n), dim3(kWave), in_cap + kWave * slot, s,
+                           jobs_dev, n, static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot, stamps);
     } else {
-        hipLaunchKernelGGL(snappy_compress_kernel<false>, dim3(n), dim3(kWave), in_cap, s, jobs_dev, n,
+        hipLaunchKernelGGL((snappy_compress_kernel<false, false>), dim3(n), dim3(kWave), in_cap, s, jobs_dev, n,
                            static_cast<uint8_t*>(scratch), out_len_dev, err_dev, in_cap, slot, stamps);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
