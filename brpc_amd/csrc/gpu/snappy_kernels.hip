@@ -706,7 +706,7 @@ __device__ __forceinline__ O emit_literal_tag(O o, uint32_t len) {
     }
     return o;
 }
-constexpr int kLitSpans = 16;  // deferred literal copies per lane (more are copied in place)
+constexpr int kLitSpans = 8;  // deferred literal copies per lane (more are copied in place)
 
 template <typename O, typename S>
 __device__ __forceinline__ O emit_literal(O o, S src, uint32_t len) {
@@ -796,7 +796,11 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
                                                                 uint32_t slot_bytes,
                                                                 uint64_t* __restrict__ stamps) {
     __shared__ uint16_t table[kCand ? 1 : kWave * kHashEntries];
-    __shared__ __attribute__((aligned(16))) uint32_t first_pos[kFirstEntries];
+    // kCand: an 11-bit earliest-position table (8 KiB): with the candidate
+    // array replacing the per-lane tables, a 4 KiB block's workgroup fits in
+    // 30 KiB of LDS, five per CU instead of three
+    constexpr int kFB = kCand ? 11 : kFirstBits;
+    __shared__ __attribute__((aligned(16))) uint32_t first_pos[1 << kFB];
     __shared__ uint32_t sizes[kWave];
     __shared__ uint64_t spans[kWave * kLitSpans];  // deferred literal copies per lane
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
@@ -843,7 +847,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
         uint32_t* t = reinterpret_cast<uint32_t*>(table);
         if (!kCand)
             for (int i = lane; i < kWave * kHashEntries / 2; i += kWave) t[i] = 0xFFFFFFFFu;
-        for (int i = lane; i < kFirstEntries; i += kWave) first_pos[i] = 0xFFFFFFFFu;
+        for (int i = lane; i < (1 << kFB); i += kWave) first_pos[i] = 0xFFFFFFFFu;
     }
     __syncthreads();
     stamp(stamps, blk, lane, 1);
@@ -863,7 +867,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
                 wb = qb;
             }
             const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, q & 3);
-            atomicMin(&first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)], q);
+            atomicMin(&first_pos[(v * 0x1e35a7bdu) >> (32 - kFB)], q);
         }
     }
     __syncthreads();
@@ -878,7 +882,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)i);
-                c[i] = first_pos[(v * 0x1e35a7bdu) >> (32 - kFirstBits)];
+                c[i] = first_pos[(v * 0x1e35a7bdu) >> (32 - kFB)];
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -957,7 +961,7 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
             const uint32_t hm = v * 0x1e35a7bdu;
             const uint32_t h = hm >> (32 - kHashBits);
             const uint32_t c1 = ht[h];
-            const uint32_t c2 = first_pos[hm >> (32 - kFirstBits)];
+            const uint32_t c2 = first_pos[hm >> (32 - kFB)];
             ht[h] = (uint16_t)p;
             const bool ok1 = c1 != kNoPos, ok2 = c2 < p;
             const uint32_t v1 = lload32(in + (ok1 ? c1 : 0u));
