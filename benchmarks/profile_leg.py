@@ -45,12 +45,16 @@ def main():
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--folded-out", default="")
     ap.add_argument("--no-profile", action="store_true", help="just run the leg (no SIGPROF sampling)")
+    ap.add_argument("--flags", default="", help="comma-separated name=value runtime flags to set first")
     a = ap.parse_args()
     import torch
     from brpc_amd import native, parallel
     from brpc_amd.models import start_echo_server
     cuda = torch.cuda.is_available()
     native.set_flag("fiber_concurrency", str(a.workers))
+    for kv in filter(None, a.flags.split(",")):
+        k, _, v = kv.partition("=")
+        native.set_flag(k, v)
     dev = 0 if cuda else -1
     if cuda:
         from brpc_amd.parallel.placement import choose_l3_domain

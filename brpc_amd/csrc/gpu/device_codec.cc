@@ -9,9 +9,10 @@
 #include "gpu/kernels.h"
 #include "policy/device_payload.h"
 
-DEFINE_int32(device_payload_block_kb, 4,
-             "uncompressed KiB per device snappy block of a compressed device payload (one wave each; 4 KiB "
-             "blocks take the parallel piece decoder); 1..64");
+DEFINE_int32(device_payload_block_kb, 2,
+             "uncompressed KiB per device snappy block of a compressed device payload (one wave each); 1..64. "
+             "Smaller blocks spread a payload over more waves: on MI355X the 64 KiB text leg runs 121k QPS at 2 KiB "
+             "(ratio 1.96) against 80k at 4 KiB (ratio 2.24)");
 
 namespace mrpc {
 namespace gpu {

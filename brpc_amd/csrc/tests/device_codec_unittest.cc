@@ -45,6 +45,8 @@ int decode_code(const gpu::DeviceSnappyBlocks& j) {
 }  // namespace
 
 TEST(DeviceCodec, layout_covers_the_payload_with_worst_case_strides) {
+    const int saved = FLAGS_device_payload_block_kb;
+    FLAGS_device_payload_block_kb = 4;
     const gpu::DeviceSnappyLayout l = gpu::DeviceSnappyLayoutFor(65536);
     EXPECT_EQ(l.block_ulen, 4096u);
     EXPECT_EQ(l.nblocks, 16u);
@@ -54,6 +56,8 @@ TEST(DeviceCodec, layout_covers_the_payload_with_worst_case_strides) {
     EXPECT_EQ(gpu::DeviceSnappyLayoutFor(1).nblocks, 1u);
     EXPECT_EQ(gpu::DeviceSnappyLayoutFor(4097).nblocks, 2u);
     EXPECT_EQ(gpu::DeviceSnappyLayoutFor(1 << 20).nblocks, 256u);
+    FLAGS_device_payload_block_kb = saved;
+    EXPECT_EQ(gpu::DeviceSnappyLayoutFor(65536).block_ulen, 2048u);  // the default
 }
 
 TEST(DeviceCodec, layout_follows_the_block_flag_within_bounds) {
