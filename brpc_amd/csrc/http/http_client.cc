@@ -51,7 +51,7 @@ int HttpFetch(const std::string& method, const std::string& url, const std::stri
         getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &len);
         if (err) return -1;
     }
-    std::string path = uri.path();
+    std::string path = uri.path().empty() ? "/" : uri.path();
     const std::string q = uri.query_string();
     if (!q.empty()) path += "?" + q;
     std::string req = method + " " + path + " HTTP/1.1\r\nHost: " + host + "\r\nConnection: close\r\nUser-Agent: mrpc\r\n";

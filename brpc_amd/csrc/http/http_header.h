@@ -53,29 +53,58 @@ struct CaseIgnoredLess {
     bool operator()(const std::string& a, const std::string& b) const;
 };
 
+// A request URL (role of src/brpc/uri.h). The query keeps its raw text:
+// lookups parse it lazily (empty segments and empty keys are skipped, a key
+// without '=' has an empty value, keys and values are percent-decoded), and
+// query()/GenerateH2Path() give back the original text until SetQuery or
+// RemoveQuery change it, after which the pairs are re-serialized in their
+// original order (percent-encoded).
 class URI {
 public:
     URI() : _port(-1) {}
-    // Parse "http://host:port/path?query#fragment" or "/path?query".
+    // Parse "[scheme://][user_info@]host[:port][/path][?query][#fragment]"
+    // or "/path[?query][#fragment]". Surrounding spaces are ignored; a space
+    // or control character inside, a bad port or an unclosed IPv6 bracket
+    // fail with -1 and status() names the problem. Without a scheme, text
+    // that does not start with '/' is a host (and optional port, path...).
     int SetHttpURL(const std::string& url);
+    // The h2 :path pseudo header: "/path[?query][#fragment]" (no host part).
+    void SetH2Path(const std::string& path);
+    void GenerateH2Path(std::string* out) const;
     std::string to_string() const;
+    const std::string& status() const { return _status; }
     const std::string& scheme() const { return _scheme; }
     const std::string& host() const { return _host; }
     int port() const { return _port; }
+    const std::string& user_info() const { return _user_info; }
     const std::string& path() const { return _path; }
     void set_path(const std::string& p) { _path = p; }
     const std::string& fragment() const { return _fragment; }
-    const std::string* GetQuery(const std::string& key) const;
-    void SetQuery(const std::string& key, const std::string& value) { _query[key] = value; }
-    void RemoveQuery(const std::string& key) { _query.erase(key); }
-    const std::map<std::string, std::string>& queries() const { return _query; }
-    std::string query_string() const;
     void set_host(const std::string& h) { _host = h; }
+    const std::string* GetQuery(const std::string& key) const;
+    void SetQuery(const std::string& key, const std::string& value);
+    // number of pairs removed (0 or 1)
+    size_t RemoveQuery(const std::string& key);
+    size_t QueryCount() const;
+    // the raw query text (or its re-serialization after a change)
+    const std::string& query() const;
+    std::string query_string() const { return query(); }
+    std::map<std::string, std::string> queries() const;
 
 private:
-    std::string _scheme, _host, _path, _fragment;
+    void parse_query() const;
+    void set_raw_query(const std::string& q) {
+        _query = q;
+        _qv.clear();
+        _parsed = false;
+        _dirty = false;
+    }
+    std::string _scheme, _user_info, _host, _path, _fragment, _status;
     int _port;
-    std::map<std::string, std::string> _query;
+    mutable std::string _query;
+    mutable std::vector<std::pair<std::string, std::string>> _qv;
+    mutable bool _parsed = false;
+    mutable bool _dirty = false;
 };
 
 class HttpHeader {

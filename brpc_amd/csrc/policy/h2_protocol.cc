@@ -439,7 +439,7 @@ int H2Context::on_headers_complete(Socket* s, Stream* st, bool end_stream, HttpM
                 HttpMethod m;
                 if (Str2HttpMethod(x.value, &m)) h.set_method(m);
             } else if (x.name == ":path") {
-                h.uri().SetHttpURL(x.value);
+                h.uri().SetH2Path(x.value);
             } else if (x.name == ":authority") {
                 h.SetHeader("host", x.value);
             } else if (x.name == ":status") {
