@@ -110,6 +110,18 @@ public:
     }
     iterator begin() { return iterator(_slots.data(), _slots.data() + _slots.size()); }
     iterator end() { return iterator(_slots.data() + _slots.size(), _slots.data() + _slots.size()); }
+    // read-only walk (the reference's const iteration)
+    template <typename Fn>
+    void for_each(Fn fn) const {
+        for (const Slot& s : _slots) {
+            if (s.used) fn(s.kv.first, s.kv.second);
+        }
+    }
+    void swap(FlatMap& o) {
+        _slots.swap(o._slots);
+        std::swap(_size, o._size);
+        std::swap(_lf, o._lf);
+    }
 
 private:
     static const size_t npos = (size_t)-1;
