@@ -36,7 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", default="gpu_handler",
                     choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps", "grpc_cpu",
-                             "grpc_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu", "dev_snappy",
+                             "grpc_gpu", "baidu_cpu", "baidu_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu", "dev_snappy",
                              "dev_1m_verify"])
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--body", default="text", help="echo body kind of the codec legs: text, random, const")
@@ -96,6 +96,11 @@ def main():
         # the bench's gRPC + snappy leg: 64 KiB protobuf body, snappy both ways
         o.update({"request_size": 65536, "protocol": "h2:grpc", "request_compress_type": 1})
         if a.leg == "grpc_gpu":
+            native.gpu.enable_snappy(dev, 16384)
+    if a.leg.startswith("baidu_"):
+        # the bench's baidu_std + snappy 64 KiB leg
+        o.update({"request_size": 65536, "protocol": "baidu_std", "request_compress_type": 1})
+        if a.leg == "baidu_gpu":
             native.gpu.enable_snappy(dev, 16384)
     if a.leg.startswith("ids_"):
         # the bench's 16k packed-ids legs: device pack/unpack with snappy
