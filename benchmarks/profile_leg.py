@@ -138,6 +138,8 @@ def main():
     thr = {k: c1.get(k, 0) - c0.get(k, 0) for k in ("nr_throttled", "throttled_usec", "nr_periods")}
     print("leg=%s qps=%.0f p50=%s p99=%s errors=%d samples=%d cpus_used=%.2f cgroup=%s" % (
         a.leg, st["qps"], st["p50_us"], st["p99_us"], st["error"], n, cpu, thr))
+    if st["error"]:
+        print("last_error:", st.get("last_error"), "codes:", st.get("error_codes"))
     x1 = native.gpu.xgmi_stats()
     if a.leg == "dev_snappy":
         print("device codec:", native.gpu.device_codec_stats(), "codec batch:", native.gpu.codec_batch_stats())
