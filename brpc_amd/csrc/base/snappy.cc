@@ -185,6 +185,40 @@ bool GetUncompressedLength(const char* in, size_t n, size_t* result) {
     return true;
 }
 
+// Copy len bytes from op - off to op inside out (the ranges may overlap).
+// With 16 bytes of room after the copy, whole 8-byte words are moved: a
+// short offset first widens its repeating pattern to at least 8 bytes (each
+// step doubles it), then every word is read before it is overwritten. The
+// last word may write up to 15 bytes past the copy; later elements or the
+// final length check make those bytes correct (they are always inside out).
+static inline void copy_match(char* out, size_t op, size_t off, size_t len, size_t out_len) {
+    char* d = out + op;
+    const char* s = d - off;
+    if (out_len - op >= len + 16) {
+        char* const stop = d + len;
+        while ((size_t)(d - s) < 8) {  // widen the pattern
+            uint64_t w;
+            memcpy(&w, s, 8);
+            memcpy(d, &w, 8);
+            d += d - s;
+            if (d >= stop) return;
+        }
+        // the pattern distance d - s is now a multiple of off and >= 8:
+        // out[x] = out[x - (d - s)], so s walks along with d
+        while (d < stop) {
+            uint64_t w;
+            memcpy(&w, s, 8);
+            memcpy(d, &w, 8);
+            memcpy(&w, s + 8, 8);
+            memcpy(d + 8, &w, 8);
+            d += 16;
+            s += 16;
+        }
+        return;
+    }
+    for (size_t i = 0; i < len; ++i) d[i] = s[i];
+}
+
 static bool decompress_impl(const char* in, size_t n, char* out, size_t out_len, bool validate_only) {
     const char* ip = in;
     const char* end = in + n;
@@ -205,7 +239,11 @@ static bool decompress_impl(const char* in, size_t n, char* out, size_t out_len,
             }
             ++len;
             if ((size_t)(end - ip) < len || out_len - op < len) return false;
-            if (!validate_only) memcpy(out + op, ip, len);
+            if (!validate_only) {
+                // short literals: one fixed 16-byte move when both sides have room
+                if (len <= 16 && end - ip >= 16 && out_len - op >= 16) memcpy(out + op, ip, 16);
+                else memcpy(out + op, ip, len);
+            }
             ip += len;
             op += len;
             break;
@@ -215,9 +253,7 @@ static bool decompress_impl(const char* in, size_t n, char* out, size_t out_len,
             const size_t len = 4 + ((tag >> 2) & 7);
             const size_t off = ((size_t)(tag >> 5) << 8) | (uint8_t)*ip++;
             if (off == 0 || off > op || out_len - op < len) return false;
-            if (!validate_only) {
-                for (size_t i = 0; i < len; ++i) out[op + i] = out[op - off + i];
-            }
+            if (!validate_only) copy_match(out, op, off, len, out_len);
             op += len;
             break;
         }
@@ -227,9 +263,7 @@ static bool decompress_impl(const char* in, size_t n, char* out, size_t out_len,
             const size_t off = (uint8_t)ip[0] | ((size_t)(uint8_t)ip[1] << 8);
             ip += 2;
             if (off == 0 || off > op || out_len - op < len) return false;
-            if (!validate_only) {
-                for (size_t i = 0; i < len; ++i) out[op + i] = out[op - off + i];
-            }
+            if (!validate_only) copy_match(out, op, off, len, out_len);
             op += len;
             break;
         }
@@ -239,9 +273,7 @@ static bool decompress_impl(const char* in, size_t n, char* out, size_t out_len,
             const size_t off = (size_t)load32(ip);
             ip += 4;
             if (off == 0 || off > op || out_len - op < len) return false;
-            if (!validate_only) {
-                for (size_t i = 0; i < len; ++i) out[op + i] = out[op - off + i];
-            }
+            if (!validate_only) copy_match(out, op, off, len, out_len);
             op += len;
             break;
         }
