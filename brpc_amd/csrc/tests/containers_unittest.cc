@@ -212,7 +212,9 @@ TEST(ContainersDepth, doubly_buffered_data_readers_see_whole_versions) {
             }
         });
     }
+    while (reads.load() < 8) std::this_thread::yield();  // readers are running
     for (int gen = 1; gen <= 300; ++gen) {
+        if (gen % 30 == 0) std::this_thread::yield();
         d.Modify([gen](std::vector<int>& v) {
             for (int& x : v) x = gen;
             return 1;
