@@ -356,6 +356,41 @@ TEST(SnappyUnit, roundtrip_many_shapes) {
     }
 }
 
+// Hand-built streams of every copy shape (offsets 1..70, lengths 1..64,
+// copies ending at the very end of the output where the word-at-a-time path
+// has no room) against a byte-by-byte reference decoder.
+TEST(SnappyUnit, copy_paths_match_a_naive_decoder) {
+    std::mt19937 rng(9);
+    for (int trial = 0; trial < 3000; ++trial) {
+        std::string stream, want;
+        // a literal first so every offset has history
+        const size_t lit = 1 + rng() % 60;  // one-byte literal tag
+        std::string l = RandomBytes(lit, trial);
+        std::string body;
+        body.push_back((char)((lit - 1) << 2));
+        body += l;
+        want += l;
+        const int ncopies = 1 + (int)(rng() % 12);
+        for (int c = 0; c < ncopies; ++c) {
+            const size_t off = 1 + rng() % std::min<size_t>(70, want.size());
+            const size_t len = 1 + rng() % 64;
+            body.push_back((char)(((len - 1) << 2) | 2));  // copy with a 2-byte offset
+            body.push_back((char)(off & 0xff));
+            body.push_back((char)(off >> 8));
+            for (size_t i = 0; i < len; ++i) want.push_back(want[want.size() - off]);
+        }
+        size_t n = want.size();
+        do {  // varint of the uncompressed length
+            stream.push_back((char)((n & 0x7f) | (n >= 0x80 ? 0x80 : 0)));
+            n >>= 7;
+        } while (n);
+        stream += body;
+        std::string got;
+        ASSERT_TRUE(snappy::Uncompress(stream.data(), stream.size(), &got));
+        ASSERT_TRUE(got == want);
+    }
+}
+
 TEST(SnappyUnit, compressible_input_shrinks) {
     const std::string in(1 << 20, 'q');
     std::string c;
