@@ -6,6 +6,7 @@
 
 #include "base/flags.h"
 #include "gpu/codec_batch.h"
+#include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
 #include "policy/device_payload.h"
 
@@ -20,7 +21,7 @@ namespace gpu {
 namespace {
 
 std::atomic<int64_t> g_encodes{0}, g_enc_bytes{0}, g_enc_out{0}, g_decodes{0}, g_dec_bytes{0}, g_bad_tables{0},
-    g_dec_err{0}, g_scans{0};
+    g_dec_err{0}, g_scans{0}, g_runs{0}, g_run_bytes{0}, g_run_elems{0}, g_run_err{0};
 
 uint32_t varint_len(uint64_t v) {
     uint32_t n = 1;
@@ -156,6 +157,83 @@ int DevicePbScan(const void* const* bufs, const uint64_t* lens, int n, DevicePay
     return 0;
 }
 
+bool DevicePayloadField(const DevicePayloadIndex& index, uint32_t number, uint64_t* off, uint64_t* len) {
+    const int n = std::min<int>(index.nfields, (int)(index.fields.size() / 2));
+    for (int k = 0; k < n; ++k) {
+        const uint64_t key = index.fields[2 * k];
+        if ((key >> 3) != number || (key & 7) != 2) continue;
+        const uint64_t v = index.fields[2 * k + 1];
+        *off = v >> 32;
+        *len = v & 0xFFFFFFFFull;
+        return true;
+    }
+    return false;
+}
+
+int DeviceDecodePackedRuns(DevicePackedRun* runs, int n, int device) {
+    if (n <= 0) return 0;
+    CodecRequest req;
+    std::vector<size_t> first(n + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        DevicePackedRun& r = runs[i];
+        first[i] = req.dec_runs.size();
+        r.count = 0;
+        r.err = 0;
+        if (!r.src || !r.dst || r.kind > PB_RUN_BOOL || r.len > 0xFFFFFFFFull) {
+            r.err = 2;
+            continue;
+        }
+        if (r.len == 0) continue;
+        const uint32_t head = (uint32_t)req.dec_runs.size();
+        for (uint64_t o = 0; o < r.len; o += kPbRunDecodeChunkBytes) {
+            PbRunDecodeChunk c;
+            c.run = static_cast<const uint8_t*>(r.src);
+            c.dst = r.dst;
+            c.offset = (uint32_t)o;
+            c.len = (uint32_t)std::min<uint64_t>(kPbRunDecodeChunkBytes, r.len - o);
+            c.first = head;
+            c.kind = r.kind;
+            req.dec_runs.push_back(c);
+        }
+    }
+    first[n] = req.dec_runs.size();
+    if (req.dec_runs.empty()) return 0;
+    // every run's final byte comes back with the batch (the host cannot read
+    // HBM): one still carrying a continuation bit ends inside a varint
+    uint8_t* tail = static_cast<uint8_t*>(PinnedAlloc((size_t)n));
+    if (!tail) return -1;
+    for (int i = 0; i < n; ++i) {
+        tail[i] = 0;
+        if (first[i + 1] > first[i]) {
+            req.d2h.push_back(Segment{static_cast<const uint8_t*>(runs[i].src) + runs[i].len - 1, tail + i, 1});
+        }
+    }
+    if (RunCodecRequest(&req, device) != 0) {
+        PinnedFree(tail, (size_t)n);
+        return -1;
+    }
+    for (int i = 0; i < n; ++i) {
+        DevicePackedRun& r = runs[i];
+        if (r.err || r.len == 0) continue;
+        uint64_t count = 0;
+        for (size_t k = first[i]; k < first[i + 1]; ++k) {
+            count += req.dec_counts[k];
+            if (req.dec_err[k]) r.err = 1;
+        }
+        if (tail[i] & 0x80) r.err = 1;
+        if (r.err) {
+            g_run_err.fetch_add(1, std::memory_order_relaxed);
+            continue;
+        }
+        r.count = count;
+        g_runs.fetch_add(1, std::memory_order_relaxed);
+        g_run_bytes.fetch_add((int64_t)r.len, std::memory_order_relaxed);
+        g_run_elems.fetch_add((int64_t)count, std::memory_order_relaxed);
+    }
+    PinnedFree(tail, (size_t)n);
+    return 0;
+}
+
 DeviceCodecStats GetDeviceCodecStats() {
     DeviceCodecStats s;
     s.encodes = g_encodes.load();
@@ -166,6 +244,10 @@ DeviceCodecStats GetDeviceCodecStats() {
     s.bad_tables = g_bad_tables.load();
     s.decode_errors = g_dec_err.load();
     s.scans = g_scans.load();
+    s.packed_runs = g_runs.load();
+    s.packed_bytes = g_run_bytes.load();
+    s.packed_elems = g_run_elems.load();
+    s.packed_errors = g_run_err.load();
     return s;
 }
 

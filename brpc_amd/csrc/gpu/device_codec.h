@@ -59,10 +59,36 @@ int DeviceSnappyDecode(const DeviceSnappyBlocks* jobs, int n, int* err, DevicePa
 // Index already-decoded device messages (one codec request). 0 on success.
 int DevicePbScan(const void* const* bufs, const uint64_t* lens, int n, DevicePayloadIndex* index, int device);
 
+// The field table entry of length-delimited field `number` (the first one
+// when repeated): its bytes are [*off, *off + *len) of the scanned payload.
+// False when the index holds no such field.
+bool DevicePayloadField(const DevicePayloadIndex& index, uint32_t number, uint64_t* off, uint64_t* len);
+
+// A packed repeated numeric field whose bytes are already in device memory
+// (a device payload located by its DevicePayloadIndex), decoded into a device
+// array in the field's vector layout (kind: gpu::PbRunKind; 4 bytes per
+// element for the 32-bit kinds, 8 for the 64-bit ones, 1 for bool). dst needs
+// room for every element of the run (never more than `len`). The reference
+// parses such fields element by element on the host
+// (src/brpc/protocol.cpp:349-360 ParsePbFromIOBuf); here the bytes never
+// leave HBM.
+struct DevicePackedRun {
+    const void* src = nullptr;
+    uint64_t len = 0;
+    uint32_t kind = 0;
+    void* dst = nullptr;
+    uint64_t count = 0;  // out: elements written
+    int err = 0;         // out: 0 ok, 1 malformed or truncated varint, 2 refused (bad arguments)
+};
+// All runs in one codec request (two launches: count, then place). Returns
+// -1 only on a device error; per-run codes in runs[i].err.
+int DeviceDecodePackedRuns(DevicePackedRun* runs, int n, int device);
+
 struct DeviceCodecStats {
     int64_t encodes = 0, encoded_bytes = 0, encoded_out_bytes = 0;
     int64_t decodes = 0, decoded_bytes = 0, bad_tables = 0, decode_errors = 0;
     int64_t scans = 0;
+    int64_t packed_runs = 0, packed_bytes = 0, packed_elems = 0, packed_errors = 0;
 };
 DeviceCodecStats GetDeviceCodecStats();
 

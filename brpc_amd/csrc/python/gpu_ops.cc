@@ -180,6 +180,39 @@ void bind_gpu_ops(py::module_& g) {
         check(rc, "device_snappy_decode");
         return py::make_tuple(err, idx.nfields, idx.fields);
     });
+    // Packed numeric fields already in HBM -> device arrays (one codec
+    // request for all runs): [(count, code)] per run, code 0 ok, 1 malformed
+    // or truncated, 2 refused.
+    g.def("device_decode_packed", [](const std::vector<uintptr_t>& srcs, const std::vector<uint64_t>& lens,
+                                     const std::vector<uint32_t>& kinds, const std::vector<uintptr_t>& dsts,
+                                     int device) {
+        if (srcs.size() != lens.size() || kinds.size() != lens.size() || dsts.size() != lens.size())
+            throw std::invalid_argument("size mismatch");
+        std::vector<gpu::DevicePackedRun> runs(lens.size());
+        for (size_t i = 0; i < lens.size(); ++i) {
+            runs[i].src = (const void*)srcs[i];
+            runs[i].len = lens[i];
+            runs[i].kind = kinds[i];
+            runs[i].dst = (void*)dsts[i];
+        }
+        int rc;
+        {
+            py::gil_scoped_release nogil;
+            rc = gpu::DeviceDecodePackedRuns(runs.data(), (int)runs.size(), device);
+        }
+        check(rc, "device_decode_packed");
+        py::list out;
+        for (const gpu::DevicePackedRun& r : runs) out.append(py::make_tuple(r.count, r.err));
+        return out;
+    }, py::arg("srcs"), py::arg("lens"), py::arg("kinds"), py::arg("dsts"), py::arg("device") = 0);
+    g.def("device_payload_field", [](int nfields, const std::vector<uint64_t>& fields, uint32_t number) -> py::object {
+        DevicePayloadIndex idx;
+        idx.nfields = nfields;
+        idx.fields = fields;
+        uint64_t off = 0, len = 0;
+        if (!gpu::DevicePayloadField(idx, number, &off, &len)) return py::none();
+        return py::make_tuple(off, len);
+    });
     g.def("resident_stats", [] {
         const gpu::ResidentStats s = gpu::GetResidentStats();
         py::dict d;

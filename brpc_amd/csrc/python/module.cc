@@ -705,6 +705,10 @@ PYBIND11_MODULE(_native, m) {
         d["bad_tables"] = s.bad_tables;
         d["decode_errors"] = s.decode_errors;
         d["scans"] = s.scans;
+        d["packed_runs"] = s.packed_runs;
+        d["packed_bytes"] = s.packed_bytes;
+        d["packed_elems"] = s.packed_elems;
+        d["packed_errors"] = s.packed_errors;
         return d;
     });
     g.def("codec_batch_stats", [] {

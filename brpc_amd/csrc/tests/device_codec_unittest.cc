@@ -139,3 +139,45 @@ TEST(DeviceCodec, descriptor_block_table_round_trips_on_the_wire) {
     EXPECT_EQ(b2.block_clen_size(), 0);
     EXPECT_FALSE(b2.pb_scan());
 }
+
+TEST(DeviceCodec, payload_field_lookup_reads_length_delimited_entries) {
+    DevicePayloadIndex idx;
+    idx.nfields = 3;
+    idx.fields = {(1u << 3) | 0, 42,                                  // varint field 1
+                  (2u << 3) | 2, (7ull << 32) | 1000,                 // bytes field 2
+                  (2u << 3) | 2, (2000ull << 32) | 5};                // a repeated second entry
+    uint64_t off = 0, len = 0;
+    EXPECT_FALSE(gpu::DevicePayloadField(idx, 1, &off, &len));  // not length-delimited
+    ASSERT_TRUE(gpu::DevicePayloadField(idx, 2, &off, &len));
+    EXPECT_EQ(off, 7u);
+    EXPECT_EQ(len, 1000u);
+    EXPECT_FALSE(gpu::DevicePayloadField(idx, 3, &off, &len));
+    idx.nfields = -1;  // not scanned
+    EXPECT_FALSE(gpu::DevicePayloadField(idx, 2, &off, &len));
+    idx.nfields = 5;  // more than the table holds: bounded by the table
+    EXPECT_TRUE(gpu::DevicePayloadField(idx, 2, &off, &len));
+}
+
+TEST(DeviceCodec, packed_runs_with_bad_arguments_are_refused_before_any_launch) {
+    static char buf[16];
+    gpu::DevicePackedRun runs[4];
+    runs[0].src = nullptr;  // no source
+    runs[0].dst = buf;
+    runs[0].len = 4;
+    runs[1].src = buf;  // no destination
+    runs[1].len = 4;
+    runs[2].src = buf;  // unknown kind
+    runs[2].dst = buf;
+    runs[2].len = 4;
+    runs[2].kind = 99;
+    runs[3].src = buf;  // empty: nothing to decode, not an error
+    runs[3].dst = buf;
+    runs[3].len = 0;
+    EXPECT_EQ(gpu::DeviceDecodePackedRuns(runs, 4, 0), 0);
+    EXPECT_EQ(runs[0].err, 2);
+    EXPECT_EQ(runs[1].err, 2);
+    EXPECT_EQ(runs[2].err, 2);
+    EXPECT_EQ(runs[3].err, 0);
+    EXPECT_EQ(runs[3].count, 0u);
+    EXPECT_EQ(gpu::DeviceDecodePackedRuns(runs, 0, 0), 0);
+}

@@ -226,3 +226,111 @@ def test_compressed_device_attachments_cross_process(dev):
     finally:
         srv.stdin.close()
         srv.wait(timeout=60)
+
+
+# ---------------------------------------------------------------- packed runs
+# kind -> (numpy dtype of the decoded array, wire value of each element)
+_PB_KINDS = {
+    0: ("int32", lambda a: a.astype("int64").view("uint64")),        # int32: sign-extended, 10 bytes if < 0
+    1: ("uint32", lambda a: a.astype("uint64")),
+    2: ("int32", lambda a: ((a.astype("int64") << 1) ^ (a.astype("int64") >> 63)).view("uint64") & 0xFFFFFFFF),
+    3: ("int64", lambda a: a.view("uint64")),
+    4: ("uint64", lambda a: a),
+    5: ("int64", lambda a: ((a << 1) ^ (a >> 63)).view("uint64")),
+    6: ("uint8", lambda a: a.astype("uint64")),
+}
+
+
+def _varints(np, wire):
+    """Vectorized protobuf varint encoding of a uint64 array."""
+    wire = wire.astype(np.uint64)
+    nbytes = np.ones(wire.shape, dtype=np.int64)
+    for k in range(1, 10):
+        nbytes += (wire >> np.uint64(7 * k)) > 0
+    start = np.cumsum(nbytes) - nbytes
+    out = np.zeros(int(nbytes.sum()), dtype=np.uint8)
+    for k in range(10):
+        m = nbytes > k
+        byte = ((wire[m] >> np.uint64(7 * k)) & np.uint64(0x7F)).astype(np.uint8)
+        byte |= np.where(nbytes[m] > k + 1, 0x80, 0).astype(np.uint8)
+        out[start[m] + k] = byte
+    return out.tobytes()
+
+
+def _values(np, kind, n, seed):
+    rng = np.random.default_rng(seed)
+    if kind == 6:
+        return rng.integers(0, 2, n).astype(np.uint8)
+    if kind in (0, 2):
+        v = rng.integers(-2**31, 2**31, n, dtype=np.int64).astype(np.int32)
+        v[::3] = rng.integers(-100, 100, len(v[::3]))  # short varints next to 5- and 10-byte ones
+        return v
+    if kind == 1:
+        return rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) >> rng.integers(0, 32, n).astype(np.uint32)
+    if kind in (3, 5):
+        return rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64) >> rng.integers(0, 63, n)
+    return rng.integers(0, 2**64 - 1, n, dtype=np.uint64) >> rng.integers(0, 64, n).astype(np.uint64)
+
+
+@pytest.mark.parametrize("kind", sorted(_PB_KINDS))
+def test_device_packed_runs_match_the_host(dev, kind):
+    """Runs in HBM of 1, a few hundred and ~100k elements (one and many
+    4 KiB chunks, varints straddling chunk edges) decoded in one request."""
+    import numpy as np
+    from brpc_amd import native
+    dtype, wire_of = _PB_KINDS[kind]
+    runs = [_values(np, kind, n, seed=kind * 10 + i) for i, n in enumerate((1, 333, 100003))]
+    wires = [_varints(np, wire_of(v)) for v in runs]
+    srcs = [torch.frombuffer(bytearray(w), dtype=torch.uint8).to(dev) for w in wires]
+    esize = np.dtype(dtype).itemsize
+    dsts = [torch.zeros(len(w) * esize, dtype=torch.uint8, device=dev) for w in wires]
+    res = native.gpu.device_decode_packed([s.data_ptr() for s in srcs], [len(w) for w in wires], [kind] * 3,
+                                          [d.data_ptr() for d in dsts], 0)
+    for v, w, d, (count, code) in zip(runs, wires, dsts, res):
+        assert code == 0 and count == len(v), (len(w), count, code)
+        got = np.frombuffer(d.cpu().numpy().tobytes()[:count * esize], dtype=dtype)
+        want = v.astype(dtype) if kind != 6 else (v != 0).astype(np.uint8)
+        assert np.array_equal(got, want)
+
+
+def test_device_packed_runs_refuse_malformed_input(dev):
+    from brpc_amd import native
+    import numpy as np
+    good = _varints(np, np.arange(1000, dtype=np.uint64) * 977)
+    cases = [
+        good[:-1] + bytes([good[-1] | 0x80]),    # ends inside a varint
+        good + bytes([0xFF] * 10 + [0x01]),      # an 11-byte varint
+        good[:5000] + bytes([0xFF] * 9 + [0x02]),  # a 10th byte above 1
+    ]
+    srcs = [torch.frombuffer(bytearray(c), dtype=torch.uint8).to(dev) for c in cases]
+    dst = torch.zeros(8 * 20000, dtype=torch.uint8, device=dev)
+    c0 = native.gpu.device_codec_stats()
+    res = native.gpu.device_decode_packed([s.data_ptr() for s in srcs] + [srcs[0].data_ptr()],
+                                          [len(c) for c in cases] + [len(cases[0])], [4, 4, 4, 9],
+                                          [dst.data_ptr()] * 4, 0)
+    assert [code for _, code in res] == [1, 1, 1, 2], res
+    assert native.gpu.device_codec_stats()["packed_errors"] - c0["packed_errors"] == 3
+
+
+def test_packed_field_of_a_received_payload_stays_in_hbm(dev):
+    """The whole HBM-resident path: a message with a packed int32 field and a
+    bytes field is snappy-encoded on the device, decoded and scanned from the
+    block table, and its packed field is located by the field table and
+    decoded into a device array; no byte of it is read on the host."""
+    import numpy as np
+    from brpc_amd import native
+    vals = _values(np, 0, 50000, seed=7)
+    packed = _varints(np, _PB_KINDS[0][1](vals))
+    blob = native.echo_body("text", 30000)
+    msg = (bytes([0x0A]) + _varint(len(packed)) + packed + bytes([0x12]) + _varint(len(blob)) + blob)
+    region, ulen, stride, clen = _encode(native, msg, dev)
+    out = torch.zeros(len(msg), dtype=torch.uint8, device=dev)
+    err, nf, fields = native.gpu.device_snappy_decode(region.data_ptr(), region.numel(), ulen, stride, clen,
+                                                      out.data_ptr(), len(msg), True, 0)
+    assert err == 0 and nf == 2
+    off, ln = native.gpu.device_payload_field(nf, fields, 1)
+    assert ln == len(packed) and native.gpu.device_payload_field(nf, fields, 5) is None
+    arr = torch.zeros(len(vals), dtype=torch.int32, device=dev)
+    [(count, code)] = native.gpu.device_decode_packed([out.data_ptr() + off], [ln], [0], [arr.data_ptr()], 0)
+    assert code == 0 and count == len(vals)
+    assert np.array_equal(arr.cpu().numpy(), vals)
