@@ -57,6 +57,8 @@ struct CBatch {
     PinnedArray<int> stream_err, piece_err;
     SnappyPiece* pieces = nullptr;  // HBM: written by the split kernel, read by the piece decoder
     size_t pieces_cap = 0;
+    uint32_t* dec_prefix = nullptr;  // HBM: per-chunk counts, scanned, of the packed-run decoder
+    size_t dec_prefix_cap = 0;
     PinnedArray<uint32_t> comp_len, decomp_len;
     PinnedArray<int> comp_err, decomp_err;
     PinnedArray<PbScanJob> scan_jobs;
@@ -209,6 +211,13 @@ bool launch(CBatch* b, int device) {
             first += st.max_pieces;
         }
     }
+    if (ndec > b->dec_prefix_cap) {
+        if (b->dec_prefix) HbmFree(b->dec_prefix, b->dec_prefix_cap * sizeof(uint32_t), device);
+        const size_t cap = std::max<size_t>(ndec, 1024);
+        b->dec_prefix = static_cast<uint32_t*>(HbmAlloc(cap * sizeof(uint32_t), device));
+        b->dec_prefix_cap = b->dec_prefix ? cap : 0;
+        if (!b->dec_prefix) return false;
+    }
     if (ncomp && SnappyCompressUsesScratch(comp_max)) {
         const size_t need = ncomp * SnappyCompressScratchPerBlock();
         if (need > b->scratch_bytes) {
@@ -251,7 +260,7 @@ bool launch(CBatch* b, int device) {
         rc = LaunchPbScanPtrs(b->scan_jobs.p, (int64_t)nscan, kCodecScanFields, b->scan_fields.p, b->scan_n.p, s);
     }
     if (rc == 0 && !d2h.empty()) rc = LaunchBatchedCopy(d2h.data(), (int)d2h.size(), s);
-    if (rc == 0 && ndec) rc = LaunchPbRunDecode(b->dec_jobs.p, (int)ndec, b->dec_counts.p, b->dec_err.p, s);
+    if (rc == 0 && ndec) rc = LaunchPbRunDecode(b->dec_jobs.p, (int)ndec, b->dec_counts.p, b->dec_prefix, b->dec_err.p, s);
     g_dec_chunks.fetch_add((int64_t)ndec, std::memory_order_relaxed);
     if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
     if (prev != device) hipSetDevice(prev);

@@ -193,9 +193,10 @@ int LaunchPbRunEncode(const PbRunChunk* chunks, int n, int32_t* err, hipStream_t
 
 // Batched decoder of packed varint runs (the parse half of K2: large packed
 // fields of a body the device already decoded): a run is cut into chunks of
-// <= kPbRunDecodeChunkBytes; pass 1 counts the varints ending in each chunk,
-// pass 2 gives every chunk its first element index (sum of the earlier
-// chunks' counts of the same run) and writes each varint ending in it,
+// <= kPbRunDecodeChunkBytes; pass 1 counts the varints ending in each chunk
+// (into counts, and into `prefix`, device memory of n entries, which one
+// workgroup then scans), pass 2 gives every chunk its first element index
+// (prefix[chunk] - prefix[run's first chunk]) and writes each varint ending in it,
 // converted to the field's vector layout, at dst[index]. A varint belongs
 // to the chunk its last byte is in, so one may start up to 9 bytes into the
 // previous chunk (read from there). Codes in err: 0 ok, 1 a varint longer
@@ -209,7 +210,8 @@ struct PbRunDecodeChunk {
     uint32_t first;      // table index of the run's first chunk
     uint32_t kind;       // PbRunKind
 };
-int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, int32_t* err, hipStream_t s);
+int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, uint32_t* prefix, int32_t* err,
+                      hipStream_t s);
 
 // JSON structural index (gpu/json_kernels.hip): out_pos receives, in order,
 // the byte offsets of every unescaped '"' and of every { } [ ] : , outside

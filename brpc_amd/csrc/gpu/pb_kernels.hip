@@ -347,7 +347,8 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t x, uint32_t* red) {
 }
 
 __global__ void __launch_bounds__(kRunThreads) pb_run_count_kernel(const PbRunDecodeChunk* __restrict__ chunks,
-                                                                   uint32_t* __restrict__ counts) {
+                                                                   uint32_t* __restrict__ counts,
+                                                                   uint32_t* __restrict__ prefix) {
     __shared__ uint8_t b[kHalo + kPbRunDecodeChunkBytes];
     __shared__ uint32_t red[kRunThreads / 64];
     const PbRunDecodeChunk c = chunks[blockIdx.x];
@@ -358,7 +359,52 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_count_kernel(const PbRunDe
     uint32_t n = 0;
     for (uint32_t j = threadIdx.x * 16; j < threadIdx.x * 16 + 16 && j < len; ++j) n += (b[kHalo + j] & 0x80) ? 0 : 1;
     n = block_sum(n, red);
-    if (threadIdx.x == 0) counts[blockIdx.x] = n;
+    if (threadIdx.x == 0) {
+        counts[blockIdx.x] = n;  // the host's copy (pinned)
+        prefix[blockIdx.x] = n;  // scanned in HBM by pb_run_prefix_kernel
+    }
+}
+
+// One workgroup turns the per-chunk counts into their exclusive prefix sum
+// over the whole table (mod 2^32), so every chunk of every run finds its
+// first element index as prefix[chunk] - prefix[run's first chunk] with two
+// loads: summing the earlier chunks' counts in each workgroup instead grows
+// with the square of a run's length (16 K chunks for a 64 MiB run).
+constexpr int kPrefixThreads = 1024, kPrefixPer = 4;
+__global__ void __launch_bounds__(kPrefixThreads) pb_run_prefix_kernel(uint32_t* __restrict__ prefix, int n) {
+    __shared__ uint32_t wave_tot[kPrefixThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t carry = 0;
+    for (int base = 0; base < n; base += kPrefixThreads * kPrefixPer) {
+        const int i0 = base + t * kPrefixPer;
+        uint32_t v[kPrefixPer], mine = 0;
+#pragma unroll
+        for (int j = 0; j < kPrefixPer; ++j) {
+            v[j] = i0 + j < n ? prefix[i0 + j] : 0;
+            mine += v[j];
+        }
+        uint32_t incl = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wave_tot[wave] = incl;
+        __syncthreads();
+        uint32_t run = carry + incl - mine, tile = 0;
+        for (int w = 0; w < kPrefixThreads / 64; ++w) {
+            const uint32_t x = wave_tot[w];
+            if (w < wave) run += x;
+            tile += x;
+        }
+#pragma unroll
+        for (int j = 0; j < kPrefixPer; ++j) {
+            if (i0 + j < n) prefix[i0 + j] = run;
+            run += v[j];
+        }
+        carry += tile;
+        __syncthreads();  // wave_tot is rewritten by the next tile
+    }
 }
 
 __device__ __forceinline__ void store_elem(uint8_t* o, uint32_t kind, uint64_t raw) {
@@ -377,11 +423,10 @@ __device__ __forceinline__ void store_elem(uint8_t* o, uint32_t kind, uint64_t r
 }
 
 __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunDecodeChunk* __restrict__ chunks,
-                                                                    const uint32_t* __restrict__ counts,
+                                                                    const uint32_t* __restrict__ prefix,
                                                                     int32_t* __restrict__ err) {
     __shared__ uint8_t b[kHalo + kPbRunDecodeChunkBytes];
     __shared__ __attribute__((aligned(16))) uint8_t image[kPbRunDecodeChunkBytes * 8];
-    __shared__ uint32_t red[kRunThreads / 64];
     __shared__ uint32_t wave_tot[kRunThreads / 64];
     __shared__ int bad;
     const PbRunDecodeChunk c = chunks[blockIdx.x];
@@ -392,9 +437,8 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunD
     if (t == 0) bad = 0;
     stage_chunk(cc, b, halo);
     // first element index: the earlier chunks of the run
-    uint32_t part = 0;
-    for (uint32_t k = c.first + t; k < blockIdx.x; k += kRunThreads) part += counts[k];
-    const uint32_t base = block_sum(part, red);  // (its barriers also order the staging)
+    const uint32_t base = prefix[blockIdx.x] - prefix[c.first];
+    __syncthreads();  // the staging is complete
     const uint32_t eb = c.kind == PB_RUN_BOOL ? 1 : (c.kind <= PB_RUN_SINT32 ? 4 : 8);
     const uint32_t j0 = (uint32_t)t * 16;
     uint32_t mine = 0;
@@ -436,11 +480,15 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunD
 
 }  // namespace
 
-int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, int32_t* err, hipStream_t s) {
+int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, uint32_t* prefix, int32_t* err,
+                      hipStream_t s) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, counts);
+    if (!prefix) return -1;
+    hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, counts, prefix);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(pb_run_decode_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, counts, err);
+    hipLaunchKernelGGL(pb_run_prefix_kernel, dim3(1), dim3(kPrefixThreads), 0, s, prefix, n);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(pb_run_decode_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, prefix, err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
