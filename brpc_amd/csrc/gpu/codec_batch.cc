@@ -15,8 +15,8 @@
 #include "gpu/hbm_pool.h"
 
 DEFINE_int32(codec_batch_max_inflight, 6,
-             "codec batches in flight per device before the next one waits for the oldest (0: no limit); while "
-             "it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches");
+             "codec batches in flight per device before the next one waits for a completion (0: no limit); "
+             "while it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches");
 
 namespace mrpc {
 namespace gpu {
@@ -101,25 +101,6 @@ void retire_done(Engine& e) {
             if (oldest->butex->load(std::memory_order_acquire) == 0) return;
             e.flying.pop_front();
         }
-        release(e, oldest);
-    }
-}
-
-// Leader only: retire completed batches; with the limit reached, wait for
-// the oldest (the open batch keeps collecting requests meanwhile).
-void throttle(Engine& e) {
-    const int limit = FLAGS_codec_batch_max_inflight;
-    for (;;) {
-        retire_done(e);
-        CBatch* oldest = nullptr;
-        {
-            std::lock_guard<std::mutex> g(e.mu);
-            if (limit <= 0 || (int)e.flying.size() < limit) return;
-            oldest = e.flying.front();
-            // our own ref: a requester may retire and recycle it meanwhile
-            oldest->refs.fetch_add(1, std::memory_order_relaxed);
-        }
-        while (oldest->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(oldest->butex, 0);
         release(e, oldest);
     }
 }
@@ -275,6 +256,42 @@ bool launch(CBatch* b, int device) {
     return true;
 }
 
+// Launch the open batch while fewer than -codec_batch_max_inflight batches
+// are in flight; one launcher at a time, and nobody waits here. With the
+// limit reached the open batch keeps collecting requests until a completion
+// frees a place: the requesters of every finished batch pump again, so an
+// open batch always has a completion coming that launches it. (A leader that
+// kept launching, blocking on the oldest batch, served the whole burst
+// while its own RPC, long finished, waited behind it: one call of every
+// run timed out at a limit of 1.)
+void pump(Engine& e, int device) {
+    const int limit = FLAGS_codec_batch_max_inflight;
+    for (;;) {
+        retire_done(e);
+        CBatch* cur;
+        {
+            std::lock_guard<std::mutex> g(e.mu);
+            if (e.launching || !e.open) return;
+            if (limit > 0 && (int)e.flying.size() >= limit) return;
+            e.launching = true;
+            cur = e.open;
+            e.open = nullptr;
+        }
+        const bool ok = launch(cur, device);
+        if (!ok) {
+            LOG_EVERY_SECOND(ERROR) << "codec batch of " << cur->reqs.size() << " requests failed on device " << device;
+            cur->butex->store(-1, std::memory_order_release);
+            fiber::butex_wake_all(cur->butex);
+        }
+        std::lock_guard<std::mutex> g(e.mu);
+        if (ok) {
+            cur->refs.fetch_add(1, std::memory_order_relaxed);
+            e.flying.push_back(cur);
+        }
+        e.launching = false;
+    }
+}
+
 }  // namespace
 
 int RunCodecRequest(CodecRequest* r, int device) {
@@ -283,7 +300,6 @@ int RunCodecRequest(CodecRequest* r, int device) {
     g_requests.fetch_add(1, std::memory_order_relaxed);
     CBatch* mine;
     size_t idx = 0;
-    bool leader = false;
     {
         std::lock_guard<std::mutex> g(e.mu);
         if (!e.open) {
@@ -294,36 +310,8 @@ int RunCodecRequest(CodecRequest* r, int device) {
         idx = mine->reqs.size();
         mine->reqs.push_back(r);
         mine->refs.fetch_add(1, std::memory_order_relaxed);
-        if (!e.launching) {
-            e.launching = true;
-            leader = true;
-        }
     }
-    if (leader) {
-        for (;;) {
-            throttle(e);
-            CBatch* cur;
-            {
-                std::lock_guard<std::mutex> g(e.mu);
-                cur = e.open;
-                e.open = nullptr;
-                if (!cur) {
-                    e.launching = false;
-                    break;
-                }
-            }
-            if (!launch(cur, device)) {
-                LOG_EVERY_SECOND(ERROR) << "codec batch of " << cur->reqs.size() << " requests failed on device "
-                                        << device;
-                cur->butex->store(-1, std::memory_order_release);
-                fiber::butex_wake_all(cur->butex);
-            } else {
-                cur->refs.fetch_add(1, std::memory_order_relaxed);
-                std::lock_guard<std::mutex> g(e.mu);
-                e.flying.push_back(cur);
-            }
-        }
-    }
+    pump(e, device);
     while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
     const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
     if (rc == 0) {
@@ -355,9 +343,10 @@ int RunCodecRequest(CodecRequest* r, int device) {
         }
     }
     release(e, mine);
-    // an idle engine must not keep finished batches (their events, pinned
-    // tables and HBM piece buffers) until the next codec request
-    retire_done(e);
+    // retire what finished (an idle engine must not keep events, pinned
+    // tables and HBM buffers until the next request) and launch the batch
+    // that waited for a place
+    pump(e, device);
     return rc;
 }
 
