@@ -9,4 +9,8 @@ for m in 1 1 2 6 6; do
   echo "m=$m $(grep -E '^leg=' $P/m$m.log | cut -c1-120)"; grep -E "last_error" $P/m$m.log | cut -c1-200 || true
 done
 timeout -k 10 400 python -u -m pytest tests/test_gpu_device_codec.py tests/test_gpu_pb_pack.py tests/test_gpu_snappy.py -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $P/pytest.log 2>&1; rc=$?
-tail -3 $P/pytest.log; exit $rc
+tail -3 $P/pytest.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u benchmarks/device_packed_bw.py > $P/bw.jsonl 2>&1 || exit $?
+cat $P/bw.jsonl
+(cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$P/kt -o kt -- python3 $GRAFT_REPO_ROOT/benchmarks/device_packed_bw.py --iters 5 > $GRAFT_REPO_ROOT/$P/kt.log 2>&1) || exit $?
+find $P/kt -name '*kernel_stats.csv' -exec cat {} \; | cut -c1-200 | head -8
