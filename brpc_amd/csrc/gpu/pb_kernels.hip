@@ -319,7 +319,10 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunC
 // [16t, 16t + 16) of the staged copy.
 constexpr int kHalo = 16;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kStage16 = (kHalo + kPbRunDecodeChunkBytes + 32) / 16;
+// staged at raw + kPad: every lane's 32-byte window (16 bytes before its
+// own 16) stays inside the array
+constexpr int kPad = 16;
+constexpr int kStage16 = (kPad + kHalo + kPbRunDecodeChunkBytes + 64) / 16;
 
 // Stages [p, p + n) into lds (n <= kHalo + chunk); returns the LDS byte
 // offset of p.
@@ -467,9 +470,8 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunD
     const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
     const uint32_t halo = c.offset < (uint32_t)kHalo ? c.offset : (uint32_t)kHalo;
     if (t == 0) bad = 0;
-    // cb[x]: chunk byte x, for x in [-halo, len)
-    const uint8_t* cb = reinterpret_cast<const uint8_t*>(raw) + stage_aligned(c.run + c.offset - halo, halo + len, raw) +
-                        halo;
+    // chunk byte x (x in [-halo, len)) is at LDS byte x + o
+    const uint32_t o = kPad + stage_aligned(c.run + c.offset - halo, halo + len, raw + kPad / 16) + halo;
     // first element index: the earlier chunks of the run
     const uint32_t base = prefix[blockIdx.x] - prefix[c.first];
     const uint32_t eb = c.kind == PB_RUN_BOOL ? 1 : (c.kind <= PB_RUN_SINT32 ? 4 : 8);
@@ -479,9 +481,38 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunD
     const uint32_t sh0 = (uint32_t)((uintptr_t)dst & 15);
     const uint32_t sh = sh0 % eb == 0 ? sh0 : 0;
     __syncthreads();  // the staging is complete
+    // lane t decodes the varints ending in chunk bytes [j0, j0 + 16), from a
+    // register window of bytes [j0 - 16, j0 + 16): 9 aligned LDS words
+    // funnel-shifted into 8, then fixed-position bit work only (no
+    // byte-serial LDS walks)
     const uint32_t j0 = (uint32_t)t * 16;
-    uint32_t mine = 0;
-    for (uint32_t j = j0; j < j0 + 16 && j < len; ++j) mine += (cb[j] & 0x80) ? 0 : 1;
+    const uint32_t wb = o + j0 - 16;  // >= 0: o >= kPad
+    const uint32_t* words = reinterpret_cast<const uint32_t*>(raw) + (wb >> 2);
+    const uint32_t fs = (wb & 3) * 8;
+    uint32_t W[8];
+    {
+        uint32_t w9[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) w9[k] = words[k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            W[k] = fs ? (uint32_t)((((uint64_t)w9[k + 1] << 32) | w9[k]) >> fs) : w9[k];
+        }
+    }
+    uint32_t cont = 0;  // bit i: window byte i carries a continuation bit
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t m = W[k] & 0x80808080u;
+        cont |= (((m >> 7) & 1) | ((m >> 14) & 2) | ((m >> 21) & 4) | ((m >> 28) & 8)) << (4 * k);
+    }
+    // bytes before the run's staged part end the lookback (the first lane of
+    // a run's first chunk)
+    const int first_valid = 16 - (int)j0 - (int)halo;  // window index of chunk byte -halo
+    if (first_valid > 0) cont &= ~((1u << first_valid) - 1);
+    const int mine_n = (int)len - (int)j0;
+    const uint32_t own = mine_n >= 16 ? 0xFFFFu : (mine_n <= 0 ? 0u : ((1u << mine_n) - 1));
+    const uint32_t term = (~cont >> 16) & own;
+    const uint32_t mine = __popc(term);
     uint32_t incl = mine;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -493,19 +524,22 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunD
     uint32_t rank = incl - mine;
     for (int w = 0; w < wave; ++w) rank += wave_tot[w];
     const uint32_t total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
-    const int lim = -(int)halo;
-    for (uint32_t j = j0; j < j0 + 16 && j < len; ++j) {
-        const uint8_t last = cb[j];
-        if (last & 0x80) continue;
-        int s = (int)j;
-        while (s > lim && (cb[s - 1] & 0x80) && (int)j - s < 9) --s;
-        const bool too_long = (int)j - s == 9 && ((s > lim && (cb[s - 1] & 0x80)) || last > 1);
-        if (too_long) bad = 1;
+#define WBYTE(i) ((W[(i) >> 2] >> (8 * ((i) & 3))) & 0xFFu)
+#pragma unroll
+    for (int p = 16; p < 32; ++p) {
+        if (!((term >> (p - 16)) & 1)) continue;
+        const uint32_t below = ~cont & ((1u << p) - 1);
+        const int n = p - (below ? 31 - __clz(below) : -1);  // varint bytes
+        if (n > 10 || (n == 10 && WBYTE(p) > 1)) bad = 1;
         uint64_t v = 0;
-        for (int k = s; k <= (int)j; ++k) v |= (uint64_t)(cb[k] & 0x7f) << (7 * (k - s));
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            if (k < n) v = (v << 7) | (WBYTE(p - k) & 0x7F);
+        }
         store_elem(image + sh + (size_t)rank * eb, c.kind, v);
         ++rank;
     }
+#undef WBYTE
     __syncthreads();
     if (bad) {
         if (t == 0) err[blockIdx.x] = 1;
