@@ -53,6 +53,7 @@ def main():
             dst = torch.empty(n * esize, dtype=torch.uint8, device=dev)
             call = lambda: native.gpu.device_decode_packed([src.data_ptr()], [len(wire)], [kind],
                                                            [dst.data_ptr()], 0)
+            torch.cuda.synchronize()  # the upload runs on torch's stream, the decoder on ours
             [(count, code)] = call()
             assert code == 0 and count == n, (count, code, n)
             got = dst.view(torch.int32 if kind == 0 else torch.int64)[:16].cpu().numpy()

@@ -276,18 +276,21 @@ void pump(Engine& e, int device) {
             e.launching = true;
             cur = e.open;
             e.open = nullptr;
+            // the in-flight list's ref, taken before the launch: the batch can
+            // complete, and its requesters drop their refs, before we get back
+            cur->refs.fetch_add(1, std::memory_order_relaxed);
         }
         const bool ok = launch(cur, device);
         if (!ok) {
             LOG_EVERY_SECOND(ERROR) << "codec batch of " << cur->reqs.size() << " requests failed on device " << device;
             cur->butex->store(-1, std::memory_order_release);
             fiber::butex_wake_all(cur->butex);
-        }
-        std::lock_guard<std::mutex> g(e.mu);
-        if (ok) {
-            cur->refs.fetch_add(1, std::memory_order_relaxed);
+        } else {
+            std::lock_guard<std::mutex> g(e.mu);
             e.flying.push_back(cur);
         }
+        if (!ok) release(e, cur);
+        std::lock_guard<std::mutex> g(e.mu);
         e.launching = false;
     }
 }

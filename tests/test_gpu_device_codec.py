@@ -35,6 +35,7 @@ def _encode(native, data, dev):
     src = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
     ulen, stride, nblocks = native.gpu.device_snappy_layout(len(data))
     region = torch.zeros(stride * nblocks, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     clen = native.gpu.device_snappy_encode(src.data_ptr(), len(data), region.data_ptr(), 0)
     return region, ulen, stride, clen
 
@@ -54,6 +55,7 @@ def test_device_snappy_blocks_are_standard_snappy_and_round_trip(dev, kind, size
         assert native.snappy_uncompress(block) == data[i * ulen:(i + 1) * ulen]
     # the device decoder rebuilds the payload from the table alone
     out = torch.zeros(size, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     err, nf, _ = native.gpu.device_snappy_decode(region.data_ptr(), region.numel(), ulen, stride, clen,
                                                  out.data_ptr(), size, False, 0)
     assert err == 0
@@ -76,6 +78,7 @@ def test_device_snappy_decode_refuses_bad_tables(dev):
         (region.numel(), 0, stride, clen),                            # no block size
     ]
     for rlen, u, st, cl in bad:
+        torch.cuda.synchronize()  # torch fills/copies run on its own stream
         err, _, _ = native.gpu.device_snappy_decode(region.data_ptr(), rlen, u, st, cl, out.data_ptr(), len(data),
                                                     False, 0)
         assert err == 1, (rlen, u, st, cl[:3])
@@ -86,6 +89,7 @@ def test_device_snappy_decode_refuses_bad_tables(dev):
     for k in range(h, clen[0]):
         host[k] = 0xFF
     region2 = torch.frombuffer(host, dtype=torch.uint8).to(dev)
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     err, _, _ = native.gpu.device_snappy_decode(region2.data_ptr(), region2.numel(), ulen, stride, clen,
                                                 out.data_ptr(), len(data), False, 0)
     assert err == 2
@@ -100,6 +104,7 @@ def test_device_snappy_decode_scans_the_message(dev):
     msg = bytes([0x0A]) + _varint(len(body)) + body + bytes([0x18, 0x01])
     region, ulen, stride, clen = _encode(native, msg, dev)
     out = torch.zeros(len(msg), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     err, nf, fields = native.gpu.device_snappy_decode(region.data_ptr(), region.numel(), ulen, stride, clen,
                                                       out.data_ptr(), len(msg), True, 0)
     assert err == 0 and nf == 2
@@ -284,6 +289,7 @@ def test_device_packed_runs_match_the_host(dev, kind):
     srcs = [torch.frombuffer(bytearray(w), dtype=torch.uint8).to(dev) for w in wires]
     esize = np.dtype(dtype).itemsize
     dsts = [torch.zeros(len(w) * esize, dtype=torch.uint8, device=dev) for w in wires]
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     res = native.gpu.device_decode_packed([s.data_ptr() for s in srcs], [len(w) for w in wires], [kind] * 3,
                                           [d.data_ptr() for d in dsts], 0)
     for v, w, d, (count, code) in zip(runs, wires, dsts, res):
@@ -305,6 +311,7 @@ def test_device_packed_runs_refuse_malformed_input(dev):
     srcs = [torch.frombuffer(bytearray(c), dtype=torch.uint8).to(dev) for c in cases]
     dst = torch.zeros(8 * 20000, dtype=torch.uint8, device=dev)
     c0 = native.gpu.device_codec_stats()
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     res = native.gpu.device_decode_packed([s.data_ptr() for s in srcs] + [srcs[0].data_ptr()],
                                           [len(c) for c in cases] + [len(cases[0])], [4, 4, 4, 9],
                                           [dst.data_ptr()] * 4, 0)
@@ -325,12 +332,14 @@ def test_packed_field_of_a_received_payload_stays_in_hbm(dev):
     msg = (bytes([0x0A]) + _varint(len(packed)) + packed + bytes([0x12]) + _varint(len(blob)) + blob)
     region, ulen, stride, clen = _encode(native, msg, dev)
     out = torch.zeros(len(msg), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     err, nf, fields = native.gpu.device_snappy_decode(region.data_ptr(), region.numel(), ulen, stride, clen,
                                                       out.data_ptr(), len(msg), True, 0)
     assert err == 0 and nf == 2
     off, ln = native.gpu.device_payload_field(nf, fields, 1)
     assert ln == len(packed) and native.gpu.device_payload_field(nf, fields, 5) is None
     arr = torch.zeros(len(vals), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # torch fills/copies run on its own stream
     [(count, code)] = native.gpu.device_decode_packed([out.data_ptr() + off], [ln], [0], [arr.data_ptr()], 0)
     assert code == 0 and count == len(vals)
     assert np.array_equal(arr.cpu().numpy(), vals)
