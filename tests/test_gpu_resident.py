@@ -29,6 +29,7 @@ rnd = random.Random(7)
 
 src = torch.randint(0, 256, (8 << 20,), dtype=torch.uint8, device=dev)
 pin = torch.randint(0, 256, (4 << 20,), dtype=torch.uint8).pin_memory()
+torch.cuda.synchronize()  # randint runs on torch's stream, the copy engine on its own
 errors = []
 
 def worker(seed, rounds):
