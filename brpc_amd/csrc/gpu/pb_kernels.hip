@@ -362,28 +362,33 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t x, uint32_t* red) {
 }
 
 __global__ void __launch_bounds__(kRunThreads) pb_run_count_kernel(const PbRunDecodeChunk* __restrict__ chunks,
-                                                                   uint32_t* __restrict__ counts,
+                                                                   int nchunks, uint32_t* __restrict__ counts,
                                                                    uint32_t* __restrict__ prefix) {
     // straight from the loads, no LDS: varint ends are bytes with the top
-    // bit clear, counted 16 at a time inside [0, len) of the chunk
+    // bit clear, counted 16 at a time inside [0, len) of the chunk. One
+    // 4 KiB chunk is a single 16-byte load per lane, so a workgroup strides
+    // over several: 16 K one-chunk workgroups (a 64 MiB run) were bound by
+    // workgroup dispatch at ~1 TB/s
     __shared__ uint32_t red[kRunThreads / 64];
-    const PbRunDecodeChunk c = chunks[blockIdx.x];
-    const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
-    const uint8_t* p = c.run + c.offset;
-    const int a = (int)((uintptr_t)p & 15);
-    const u32x4* src = reinterpret_cast<const u32x4*>(p - a);
-    const uint32_t n16 = ((uint32_t)a + len + 15) >> 4;
-    uint32_t n = 0;
-    for (uint32_t i = threadIdx.x; i < n16; i += kRunThreads) {
-        const u32x4 v = src[i];
-        const uint32_t bits = ends_of(v.x) | (ends_of(v.y) << 4) | (ends_of(v.z) << 8) | (ends_of(v.w) << 12);
-        const int lo = max(a - (int)(i * 16), 0), hi = min(a + (int)len - (int)(i * 16), 16);
-        if (hi > lo) n += __popc(bits & (((1u << hi) - 1) & ~((1u << lo) - 1)));
-    }
-    n = block_sum(n, red);
-    if (threadIdx.x == 0) {
-        counts[blockIdx.x] = n;  // the host's copy (pinned)
-        prefix[blockIdx.x] = n;  // scanned in HBM by pb_run_prefix_kernel
+    for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+        const PbRunDecodeChunk c = chunks[ci];
+        const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
+        const uint8_t* p = c.run + c.offset;
+        const int a = (int)((uintptr_t)p & 15);
+        const u32x4* src = reinterpret_cast<const u32x4*>(p - a);
+        const uint32_t n16 = ((uint32_t)a + len + 15) >> 4;
+        uint32_t n = 0;
+        for (uint32_t i = threadIdx.x; i < n16; i += kRunThreads) {
+            const u32x4 v = src[i];
+            const uint32_t bits = ends_of(v.x) | (ends_of(v.y) << 4) | (ends_of(v.z) << 8) | (ends_of(v.w) << 12);
+            const int lo = max(a - (int)(i * 16), 0), hi = min(a + (int)len - (int)(i * 16), 16);
+            if (hi > lo) n += __popc(bits & (((1u << hi) - 1) & ~((1u << lo) - 1)));
+        }
+        n = block_sum(n, red);
+        if (threadIdx.x == 0) {
+            counts[ci] = n;  // the host's copy (pinned)
+            prefix[ci] = n;  // scanned in HBM by pb_run_prefix_kernel
+        }
     }
 }
 
@@ -560,7 +565,10 @@ int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, u
                       hipStream_t s) {
     if (n <= 0) return 0;
     if (!prefix) return -1;
-    hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, counts, prefix);
+    // 8 workgroups per CU at most; each strides over the rest
+    const int count_grid = n < 2048 ? n : 2048;
+    hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)count_grid), dim3(kRunThreads), 0, s, chunks, n, counts,
+                       prefix);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(pb_run_prefix_kernel, dim3(1), dim3(kPrefixThreads), 0, s, prefix, n);
     if (hipGetLastError() != hipSuccess) return -1;
