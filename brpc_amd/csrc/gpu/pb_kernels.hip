@@ -370,8 +370,12 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_count_kernel(const PbRunDe
     // over several: 16 K one-chunk workgroups (a 64 MiB run) were bound by
     // workgroup dispatch at ~1 TB/s
     __shared__ uint32_t red[kRunThreads / 64];
+    PbRunDecodeChunk c = chunks[blockIdx.x];
     for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
-        const PbRunDecodeChunk c = chunks[ci];
+        // the table is pinned host memory: fetch the next descriptor now,
+        // its PCIe round trip overlaps this chunk
+        PbRunDecodeChunk next = c;
+        if (ci + (int)gridDim.x < nchunks) next = chunks[ci + gridDim.x];
         const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
         const uint8_t* p = c.run + c.offset;
         const int a = (int)((uintptr_t)p & 15);
@@ -389,6 +393,7 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_count_kernel(const PbRunDe
             counts[ci] = n;  // the host's copy (pinned)
             prefix[ci] = n;  // scanned in HBM by pb_run_prefix_kernel
         }
+        c = next;
     }
 }
 
@@ -464,99 +469,108 @@ __device__ __forceinline__ void copy_out_aligned(uint8_t* dst, const uint8_t* im
 }
 
 __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunDecodeChunk* __restrict__ chunks,
+                                                                    int nchunks,
                                                                     const uint32_t* __restrict__ prefix,
                                                                     int32_t* __restrict__ err) {
     __shared__ u32x4 raw[kStage16];
     __shared__ __attribute__((aligned(16))) uint8_t image[kPbRunDecodeChunkBytes * 8 + 16];
     __shared__ uint32_t wave_tot[kRunThreads / 64];
     __shared__ int bad;
-    const PbRunDecodeChunk c = chunks[blockIdx.x];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
-    const uint32_t halo = c.offset < (uint32_t)kHalo ? c.offset : (uint32_t)kHalo;
-    if (t == 0) bad = 0;
-    // chunk byte x (x in [-halo, len)) is at LDS byte x + o
-    const uint32_t o = kPad + stage_aligned(c.run + c.offset - halo, halo + len, raw + kPad / 16) + halo;
-    // first element index: the earlier chunks of the run
-    const uint32_t base = prefix[blockIdx.x] - prefix[c.first];
-    const uint32_t eb = c.kind == PB_RUN_BOOL ? 1 : (c.kind <= PB_RUN_SINT32 ? 4 : 8);
-    uint8_t* dst = static_cast<uint8_t*>(c.dst) + (size_t)base * eb;
-    // the image sits at dst's alignment so copy-out is 16-byte both sides;
-    // element stores stay naturally aligned only when dst is
-    const uint32_t sh0 = (uint32_t)((uintptr_t)dst & 15);
-    const uint32_t sh = sh0 % eb == 0 ? sh0 : 0;
-    __syncthreads();  // the staging is complete
-    // lane t decodes the varints ending in chunk bytes [j0, j0 + 16), from a
-    // register window of bytes [j0 - 16, j0 + 16): 9 aligned LDS words
-    // funnel-shifted into 8, then fixed-position bit work only (no
-    // byte-serial LDS walks)
-    const uint32_t j0 = (uint32_t)t * 16;
-    const uint32_t wb = o + j0 - 16;  // >= 0: o >= kPad
-    const uint32_t* words = reinterpret_cast<const uint32_t*>(raw) + (wb >> 2);
-    const uint32_t fs = (wb & 3) * 8;
-    uint32_t W[8];
-    {
-        uint32_t w9[9];
+    PbRunDecodeChunk c = chunks[blockIdx.x];
+    // grid-stride over the chunks; the next descriptor (pinned host memory)
+    // is fetched while this chunk decodes
+    for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+        PbRunDecodeChunk next = c;
+        if (ci + (int)gridDim.x < nchunks) next = chunks[ci + gridDim.x];
+        const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
+        const uint32_t halo = c.offset < (uint32_t)kHalo ? c.offset : (uint32_t)kHalo;
+        if (t == 0) bad = 0;
+        // chunk byte x (x in [-halo, len)) is at LDS byte x + o
+        const uint32_t o = kPad + stage_aligned(c.run + c.offset - halo, halo + len, raw + kPad / 16) + halo;
+        // first element index: the earlier chunks of the run
+        const uint32_t base = prefix[ci] - prefix[c.first];
+        const uint32_t eb = c.kind == PB_RUN_BOOL ? 1 : (c.kind <= PB_RUN_SINT32 ? 4 : 8);
+        uint8_t* dst = static_cast<uint8_t*>(c.dst) + (size_t)base * eb;
+        // the image sits at dst's alignment so copy-out is 16-byte both sides;
+        // element stores stay naturally aligned only when dst is
+        const uint32_t sh0 = (uint32_t)((uintptr_t)dst & 15);
+        const uint32_t sh = sh0 % eb == 0 ? sh0 : 0;
+        __syncthreads();  // the staging is complete
+        // lane t decodes the varints ending in chunk bytes [j0, j0 + 16), from a
+        // register window of bytes [j0 - 16, j0 + 16): 9 aligned LDS words
+        // funnel-shifted into 8, then fixed-position bit work only (no
+        // byte-serial LDS walks)
+        const uint32_t j0 = (uint32_t)t * 16;
+        const uint32_t wb = o + j0 - 16;  // >= 0: o >= kPad
+        const uint32_t* words = reinterpret_cast<const uint32_t*>(raw) + (wb >> 2);
+        const uint32_t fs = (wb & 3) * 8;
+        uint32_t W[8];
+        {
+            uint32_t w9[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) w9[k] = words[k];
+            for (int k = 0; k < 9; ++k) w9[k] = words[k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                W[k] = fs ? (uint32_t)((((uint64_t)w9[k + 1] << 32) | w9[k]) >> fs) : w9[k];
+            }
+        }
+        uint32_t cont = 0;  // bit i: window byte i carries a continuation bit
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            W[k] = fs ? (uint32_t)((((uint64_t)w9[k + 1] << 32) | w9[k]) >> fs) : w9[k];
+            const uint32_t m = W[k] & 0x80808080u;
+            cont |= (((m >> 7) & 1) | ((m >> 14) & 2) | ((m >> 21) & 4) | ((m >> 28) & 8)) << (4 * k);
         }
-    }
-    uint32_t cont = 0;  // bit i: window byte i carries a continuation bit
+        // bytes before the run's staged part end the lookback (the first lane of
+        // a run's first chunk)
+        const int first_valid = 16 - (int)j0 - (int)halo;  // window index of chunk byte -halo
+        if (first_valid > 0) cont &= ~((1u << first_valid) - 1);
+        const int mine_n = (int)len - (int)j0;
+        const uint32_t own = mine_n >= 16 ? 0xFFFFu : (mine_n <= 0 ? 0u : ((1u << mine_n) - 1));
+        const uint32_t term = (~cont >> 16) & own;
+        const uint32_t mine = __popc(term);
+        uint32_t incl = mine;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t m = W[k] & 0x80808080u;
-        cont |= (((m >> 7) & 1) | ((m >> 14) & 2) | ((m >> 21) & 4) | ((m >> 28) & 8)) << (4 * k);
-    }
-    // bytes before the run's staged part end the lookback (the first lane of
-    // a run's first chunk)
-    const int first_valid = 16 - (int)j0 - (int)halo;  // window index of chunk byte -halo
-    if (first_valid > 0) cont &= ~((1u << first_valid) - 1);
-    const int mine_n = (int)len - (int)j0;
-    const uint32_t own = mine_n >= 16 ? 0xFFFFu : (mine_n <= 0 ? 0u : ((1u << mine_n) - 1));
-    const uint32_t term = (~cont >> 16) & own;
-    const uint32_t mine = __popc(term);
-    uint32_t incl = mine;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-    }
-    if (lane == 63) wave_tot[wave] = incl;
-    __syncthreads();
-    uint32_t rank = incl - mine;
-    for (int w = 0; w < wave; ++w) rank += wave_tot[w];
-    const uint32_t total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += y;
+        }
+        if (lane == 63) wave_tot[wave] = incl;
+        __syncthreads();
+        uint32_t rank = incl - mine;
+        for (int w = 0; w < wave; ++w) rank += wave_tot[w];
+        const uint32_t total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
 #define WBYTE(i) ((W[(i) >> 2] >> (8 * ((i) & 3))) & 0xFFu)
 #pragma unroll
-    for (int p = 16; p < 32; ++p) {
-        if (!((term >> (p - 16)) & 1)) continue;
-        const uint32_t below = ~cont & ((1u << p) - 1);
-        const int n = p - (below ? 31 - __clz(below) : -1);  // varint bytes
-        if (n > 10 || (n == 10 && WBYTE(p) > 1)) bad = 1;
-        uint64_t v = 0;
+        for (int p = 16; p < 32; ++p) {
+            if (!((term >> (p - 16)) & 1)) continue;
+            const uint32_t below = ~cont & ((1u << p) - 1);
+            const int n = p - (below ? 31 - __clz(below) : -1);  // varint bytes
+            if (n > 10 || (n == 10 && WBYTE(p) > 1)) bad = 1;
+            uint64_t v = 0;
 #pragma unroll
-        for (int k = 0; k < 10; ++k) {
-            if (k < n) v = (v << 7) | (WBYTE(p - k) & 0x7F);
+            for (int k = 0; k < 10; ++k) {
+                if (k < n) v = (v << 7) | (WBYTE(p - k) & 0x7F);
+            }
+            store_elem(image + sh + (size_t)rank * eb, c.kind, v);
+            ++rank;
         }
-        store_elem(image + sh + (size_t)rank * eb, c.kind, v);
-        ++rank;
-    }
 #undef WBYTE
-    __syncthreads();
-    if (bad) {
-        if (t == 0) err[blockIdx.x] = 1;
-        return;
+        __syncthreads();
+        if (bad) {
+            if (t == 0) err[ci] = 1;
+        } else {
+            const uint32_t nbytes = total * eb;
+            if (sh == sh0) {
+                copy_out_aligned(dst, image, sh, nbytes);
+            } else {
+                copy_out(dst, image, nbytes);
+            }
+            if (t == 0) err[ci] = 0;
+        }
+        __syncthreads();  // raw, image, wave_tot and bad are reused
+        c = next;
     }
-    const uint32_t nbytes = total * eb;
-    if (sh == sh0) {
-        copy_out_aligned(dst, image, sh, nbytes);
-    } else {
-        copy_out(dst, image, nbytes);
-    }
-    if (t == 0) err[blockIdx.x] = 0;
 }
 
 }  // namespace
@@ -567,12 +581,14 @@ int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, u
     if (!prefix) return -1;
     // 8 workgroups per CU at most; each strides over the rest
     const int count_grid = n < 2048 ? n : 2048;
+    const int decode_grid = n < 1024 ? n : 1024;  // 4 resident per CU (37 KiB of LDS each)
     hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)count_grid), dim3(kRunThreads), 0, s, chunks, n, counts,
                        prefix);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(pb_run_prefix_kernel, dim3(1), dim3(kPrefixThreads), 0, s, prefix, n);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(pb_run_decode_kernel, dim3((unsigned)n), dim3(kRunThreads), 0, s, chunks, prefix, err);
+    hipLaunchKernelGGL(pb_run_decode_kernel, dim3((unsigned)decode_grid), dim3(kRunThreads), 0, s, chunks, n, prefix,
+                       err);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
