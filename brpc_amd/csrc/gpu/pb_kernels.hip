@@ -350,50 +350,47 @@ __device__ __forceinline__ uint32_t ends_of(uint32_t w) {
     return ((m >> 7) & 1) | ((m >> 14) & 2) | ((m >> 21) & 4) | ((m >> 28) & 8);
 }
 
-__device__ __forceinline__ uint32_t block_sum(uint32_t x, uint32_t* red) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-    if (lane == 0) red[wave] = x;
-    __syncthreads();
-    const uint32_t s = red[0] + red[1] + red[2] + red[3];
-    __syncthreads();
-    return s;
-}
-
 __global__ void __launch_bounds__(kRunThreads) pb_run_count_kernel(const PbRunDecodeChunk* __restrict__ chunks,
                                                                    int nchunks, uint32_t* __restrict__ counts,
                                                                    uint32_t* __restrict__ prefix) {
-    // straight from the loads, no LDS: varint ends are bytes with the top
-    // bit clear, counted 16 at a time inside [0, len) of the chunk. One
-    // 4 KiB chunk is a single 16-byte load per lane, so a workgroup strides
-    // over several: 16 K one-chunk workgroups (a 64 MiB run) were bound by
-    // workgroup dispatch at ~1 TB/s
-    __shared__ uint32_t red[kRunThreads / 64];
-    PbRunDecodeChunk c = chunks[blockIdx.x];
-    for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
-        // the table is pinned host memory: fetch the next descriptor now,
-        // its PCIe round trip overlaps this chunk
-        PbRunDecodeChunk next = c;
-        if (ci + (int)gridDim.x < nchunks) next = chunks[ci + gridDim.x];
+    // one wave per chunk, straight from the loads (no LDS, no barriers):
+    // varint ends are bytes with the top bit clear, counted 16 at a time
+    // inside [0, len). Every lane issues its (up to 5) 16-byte loads before
+    // using any, so a wave keeps a whole 4 KiB chunk in flight; one load per
+    // lane and a block-wide reduction per chunk held this pass to ~1 TB/s
+    constexpr int kUnits = (kPbRunDecodeChunkBytes + 16 + 63 * 16) / (64 * 16);  // 16 B units per lane
+    const int lane = threadIdx.x & 63;
+    const int nwaves = (int)gridDim.x * (kRunThreads / 64);
+    for (int ci = (int)blockIdx.x * (kRunThreads / 64) + (int)(threadIdx.x >> 6); ci < nchunks; ci += nwaves) {
+        const PbRunDecodeChunk c = chunks[ci];
         const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
         const uint8_t* p = c.run + c.offset;
         const int a = (int)((uintptr_t)p & 15);
         const u32x4* src = reinterpret_cast<const u32x4*>(p - a);
         const uint32_t n16 = ((uint32_t)a + len + 15) >> 4;
-        uint32_t n = 0;
-        for (uint32_t i = threadIdx.x; i < n16; i += kRunThreads) {
-            const u32x4 v = src[i];
-            const uint32_t bits = ends_of(v.x) | (ends_of(v.y) << 4) | (ends_of(v.z) << 8) | (ends_of(v.w) << 12);
-            const int lo = max(a - (int)(i * 16), 0), hi = min(a + (int)len - (int)(i * 16), 16);
-            if (hi > lo) n += __popc(bits & (((1u << hi) - 1) & ~((1u << lo) - 1)));
+        u32x4 v[kUnits];
+#pragma unroll
+        for (int k = 0; k < kUnits; ++k) {
+            const uint32_t i = (uint32_t)lane + 64u * k;
+            if (i < n16) v[k] = src[i];
         }
-        n = block_sum(n, red);
-        if (threadIdx.x == 0) {
+        uint32_t n = 0;
+#pragma unroll
+        for (int k = 0; k < kUnits; ++k) {
+            const uint32_t i = (uint32_t)lane + 64u * k;
+            if (i < n16) {
+                const uint32_t bits =
+                    ends_of(v[k].x) | (ends_of(v[k].y) << 4) | (ends_of(v[k].z) << 8) | (ends_of(v[k].w) << 12);
+                const int lo = max(a - (int)(i * 16), 0), hi = min(a + (int)len - (int)(i * 16), 16);
+                if (hi > lo) n += __popc(bits & (((1u << hi) - 1) & ~((1u << lo) - 1)));
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off, 64);
+        if (lane == 0) {
             counts[ci] = n;  // the host's copy (pinned)
             prefix[ci] = n;  // scanned in HBM by pb_run_prefix_kernel
         }
-        c = next;
     }
 }
 
@@ -579,8 +576,10 @@ int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, u
                       hipStream_t s) {
     if (n <= 0) return 0;
     if (!prefix) return -1;
-    // 8 workgroups per CU at most; each strides over the rest
-    const int count_grid = n < 2048 ? n : 2048;
+    // a wave per chunk, 8 workgroups (32 waves) per CU at most; the waves
+    // stride over the rest
+    const int count_wgs = (n + kRunThreads / 64 - 1) / (kRunThreads / 64);
+    const int count_grid = count_wgs < 2048 ? count_wgs : 2048;
     const int decode_grid = n < 1024 ? n : 1024;  // 4 resident per CU (37 KiB of LDS each)
     hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)count_grid), dim3(kRunThreads), 0, s, chunks, n, counts,
                        prefix);
