@@ -311,12 +311,39 @@ __global__ void __launch_bounds__(kRunThreads) pb_run_encode_kernel(const PbRunC
 // ------------------------------------------------------------ run decoder
 // Packed fields of a decoded body (the reference's ParsePbFromIOBuf walks
 // them element by element on the host, src/brpc/protocol.cpp).
-// Both passes give each chunk (plus up to 16 bytes of the run before it) to
-// one wave and read it with 16-byte loads of the aligned units around it (a
-// byte outside the run shares its aligned 16 bytes with a byte inside, so
-// with its page), straight into registers.
+// Both passes read the chunk (plus up to 16 bytes of the run before it)
+// with 16-byte loads of the aligned span around it (a byte outside the run
+// shares its aligned 16 bytes with a byte inside, so with its page): a
+// wave's load moves 1 KiB instead of the 64 bytes of per-lane byte loads,
+// which held the count pass to ~1 TB/s on HBM. Lane t then owns chunk bytes
+// [16t, 16t + 16) of the staged copy.
 constexpr int kHalo = 16;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// staged at raw + kPad: every lane's 32-byte window (16 bytes before its
+// own 16) stays inside the array
+constexpr int kPad = 16;
+constexpr int kStage16 = (kPad + kHalo + kPbRunDecodeChunkBytes + 64) / 16;
+
+// Stages [p, p + n) into lds (n <= kHalo + chunk); returns the LDS byte
+// offset of p.
+__device__ __forceinline__ uint32_t stage_aligned(const uint8_t* p, uint32_t n, u32x4* lds) {
+    const uint32_t a = (uint32_t)((uintptr_t)p & 15);
+    const u32x4* src = reinterpret_cast<const u32x4*>(p - a);
+    const uint32_t n16 = (a + n + 15) >> 4;
+    u32x4 v[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kRunThreads;
+        if (i < n16) v[k] = src[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kRunThreads;
+        if (i < n16) lds[i] = v[k];
+    }
+    return a;
+}
+
 // Bits 0..3 of each nibble k: byte k of w ends a varint (top bit clear).
 __device__ __forceinline__ uint32_t ends_of(uint32_t w) {
     const uint32_t m = ~w & 0x80808080u;
@@ -424,145 +451,122 @@ __device__ __forceinline__ void store_elem(uint8_t* o, uint32_t kind, uint64_t r
     }
 }
 
-// Lane-window decode of one 16-byte slice: bytes 16..31 of the 32-byte
-// window W (bytes 0..15 are the lookback) hold the slice. cont bit i: window
-// byte i carries a continuation bit; own: which of the 16 slice bytes belong
-// to the chunk. Writes the slice's elements from out + rank * eb; returns
-// whether a varint was malformed.
-__device__ __forceinline__ bool decode_slice(const uint32_t (&W)[8], uint32_t cont, uint32_t own, uint32_t kind,
-                                             uint32_t eb, uint8_t* out, uint32_t rank) {
-    const uint32_t term = (~cont >> 16) & own;
-    bool bad = false;
-#define WBYTE(i) ((W[(i) >> 2] >> (8 * ((i) & 3))) & 0xFFu)
-#pragma unroll
-    for (int p = 16; p < 32; ++p) {
-        if (!((term >> (p - 16)) & 1)) continue;
-        const uint32_t below = ~cont & ((1u << p) - 1);
-        const int n = p - (below ? 31 - __clz(below) : -1);  // varint bytes
-        bad |= n > 10 || (n == 10 && WBYTE(p) > 1);
-        uint64_t v = 0;
-#pragma unroll
-        for (int k = 0; k < 10; ++k) {
-            if (k < n) v = (v << 7) | (WBYTE(p - k) & 0x7F);
-        }
-        store_elem(out + (size_t)rank * eb, kind, v);
-        ++rank;
-    }
-#undef WBYTE
-    return bad;
+// dst gets image[sh, sh + total) where dst = sh (mod 16): the aligned body
+// moves as 16-byte LDS reads and 16-byte stores.
+__device__ __forceinline__ void copy_out_aligned(uint8_t* dst, const uint8_t* image, uint32_t sh, uint32_t total) {
+    const uint32_t t = threadIdx.x;
+    uint32_t head = (16 - sh) & 15;
+    if (head > total) head = total;
+    if (t < head) dst[t] = image[sh + t];
+    const uint32_t nv = (total - head) / 16;
+    const u32x4* from = reinterpret_cast<const u32x4*>(image + sh + head);
+    u32x4* body = reinterpret_cast<u32x4*>(dst + head);
+    for (uint32_t w = t; w < nv; w += kRunThreads) body[w] = from[w];
+    for (uint32_t j = head + 16 * nv + t; j < total; j += kRunThreads) dst[j] = image[sh + j];
 }
 
-__device__ __forceinline__ uint32_t cont_bits(const uint32_t (&W)[8]) {
-    uint32_t cont = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cont |= ends_of(~W[k]) << (4 * k);  // top bit set
-    return cont;
-}
-
-// One wave per chunk, grid-striding like the count pass: lane l owns chunk
-// bytes [64l, 64l + 64), loads the six 16-byte units around them (all issued
-// before any is used: a whole chunk in flight per wave), shifts them to the
-// chunk's alignment in registers and decodes four 16-byte slices, each from
-// a 32-byte register window (16 bytes of lookback). Ranks come from one wave
-// scan; elements are stored straight to the destination (a lane's are
-// contiguous, lanes in order). No LDS, no barriers. A malformed chunk
-// reports 1 and may leave partial output.
 __global__ void __launch_bounds__(kRunThreads) pb_run_decode_kernel(const PbRunDecodeChunk* __restrict__ chunks,
                                                                     int nchunks,
                                                                     const uint32_t* __restrict__ prefix,
                                                                     int32_t* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const int nwaves = (int)gridDim.x * (kRunThreads / 64);
-    for (int ci = (int)blockIdx.x * (kRunThreads / 64) + (int)(threadIdx.x >> 6); ci < nchunks; ci += nwaves) {
-        const PbRunDecodeChunk c = chunks[ci];
-        const int len = (int)(c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes);
-        const int halo = (int)(c.offset < (uint32_t)kHalo ? c.offset : (uint32_t)kHalo);
-        const uint8_t* p = c.run + c.offset;
-        const int a = (int)((uintptr_t)p & 15);
-        const u32x4* units = reinterpret_cast<const u32x4*>(p - a);
-        // unit u holds chunk bytes [16u - a, 16u - a + 16); lane l needs
-        // units 4l-1 .. 4l+4. A unit is read only when it holds a byte of
-        // the staged range [-halo, len), so with it its page
-        u32x4 U[6];
+    __shared__ u32x4 raw[kStage16];
+    __shared__ __attribute__((aligned(16))) uint8_t image[kPbRunDecodeChunkBytes * 8 + 16];
+    __shared__ uint32_t wave_tot[kRunThreads / 64];
+    __shared__ int bad;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    PbRunDecodeChunk c = chunks[blockIdx.x];
+    // grid-stride over the chunks; the next descriptor (pinned host memory)
+    // is fetched while this chunk decodes
+    for (int ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
+        PbRunDecodeChunk next = c;
+        if (ci + (int)gridDim.x < nchunks) next = chunks[ci + gridDim.x];
+        const uint32_t len = c.len < kPbRunDecodeChunkBytes ? c.len : kPbRunDecodeChunkBytes;
+        const uint32_t halo = c.offset < (uint32_t)kHalo ? c.offset : (uint32_t)kHalo;
+        if (t == 0) bad = 0;
+        // chunk byte x (x in [-halo, len)) is at LDS byte x + o
+        const uint32_t o = kPad + stage_aligned(c.run + c.offset - halo, halo + len, raw + kPad / 16) + halo;
+        // first element index: the earlier chunks of the run
+        const uint32_t base = prefix[ci] - prefix[c.first];
+        const uint32_t eb = c.kind == PB_RUN_BOOL ? 1 : (c.kind <= PB_RUN_SINT32 ? 4 : 8);
+        uint8_t* dst = static_cast<uint8_t*>(c.dst) + (size_t)base * eb;
+        // the image sits at dst's alignment so copy-out is 16-byte both sides;
+        // element stores stay naturally aligned only when dst is
+        const uint32_t sh0 = (uint32_t)((uintptr_t)dst & 15);
+        const uint32_t sh = sh0 % eb == 0 ? sh0 : 0;
+        __syncthreads();  // the staging is complete
+        // lane t decodes the varints ending in chunk bytes [j0, j0 + 16), from a
+        // register window of bytes [j0 - 16, j0 + 16): 9 aligned LDS words
+        // funnel-shifted into 8, then fixed-position bit work only (no
+        // byte-serial LDS walks)
+        const uint32_t j0 = (uint32_t)t * 16;
+        const uint32_t wb = o + j0 - 16;  // >= 0: o >= kPad
+        const uint32_t* words = reinterpret_cast<const uint32_t*>(raw) + (wb >> 2);
+        const uint32_t fs = (wb & 3) * 8;
+        uint32_t W[8];
+        {
+            uint32_t w9[9];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const int u = 4 * lane - 1 + k;
-            const int first = 16 * u - a;
-            if (first + 15 >= -halo && first < len) {
-                U[k] = units[u];
-            } else {
-                U[k] = u32x4{0, 0, 0, 0};
+            for (int k = 0; k < 9; ++k) w9[k] = words[k];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                W[k] = fs ? (uint32_t)((((uint64_t)w9[k + 1] << 32) | w9[k]) >> fs) : w9[k];
             }
         }
-        // T[i]: chunk bytes [64l - 16 + 4i, +4): the 96 loaded bytes shifted
-        // down by a (they start at chunk byte 64l - 16 - a)
-        uint32_t R[24];
+        uint32_t cont = 0;  // bit i: window byte i carries a continuation bit
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            R[4 * k] = U[k].x;
-            R[4 * k + 1] = U[k].y;
-            R[4 * k + 2] = U[k].z;
-            R[4 * k + 3] = U[k].w;
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t m = W[k] & 0x80808080u;
+            cont |= (((m >> 7) & 1) | ((m >> 14) & 2) | ((m >> 21) & 4) | ((m >> 28) & 8)) << (4 * k);
         }
-        // whole words first, in two wave-uniform steps with fixed indices
-        // (a select by a>>2 becomes an indexed access, i.e. scratch), then
-        // the byte remainder as a funnel shift
-        if (a & 4) {
-#pragma unroll
-            for (int i = 0; i < 23; ++i) R[i] = R[i + 1];
-        }
-        if (a & 8) {
-#pragma unroll
-            for (int i = 0; i < 22; ++i) R[i] = R[i + 2];
-        }
-        const int fs = (a & 3) * 8;
-        uint32_t T[20];
-#pragma unroll
-        for (int i = 0; i < 20; ++i) T[i] = fs ? (uint32_t)((((uint64_t)R[i + 1] << 32) | R[i]) >> fs) : R[i];
-        // slice k of this lane: chunk bytes [64l + 16k, +16), window = T[4k .. 4k+8)
-        uint32_t cont[4], own[4], mine = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t W[8] = {T[4 * k], T[4 * k + 1], T[4 * k + 2], T[4 * k + 3],
-                                   T[4 * k + 4], T[4 * k + 5], T[4 * k + 6], T[4 * k + 7]};
-            cont[k] = cont_bits(W);
-            const int j0 = 64 * lane + 16 * k;
-            // bytes before the staged range end the lookback
-            const int first_valid = 16 - j0 - halo;  // window index of chunk byte -halo
-            if (first_valid > 0) cont[k] &= ~((1u << first_valid) - 1);
-            const int n = len - j0;
-            own[k] = n >= 16 ? 0xFFFFu : (n <= 0 ? 0u : ((1u << n) - 1));
-            mine += __popc((~cont[k] >> 16) & own[k]);
-        }
+        // bytes before the run's staged part end the lookback (the first lane of
+        // a run's first chunk)
+        const int first_valid = 16 - (int)j0 - (int)halo;  // window index of chunk byte -halo
+        if (first_valid > 0) cont &= ~((1u << first_valid) - 1);
+        const int mine_n = (int)len - (int)j0;
+        const uint32_t own = mine_n >= 16 ? 0xFFFFu : (mine_n <= 0 ? 0u : ((1u << mine_n) - 1));
+        const uint32_t term = (~cont >> 16) & own;
+        const uint32_t mine = __popc(term);
         uint32_t incl = mine;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const uint32_t y = __shfl_up(incl, off, 64);
             if (lane >= off) incl += y;
         }
-        const uint32_t eb = c.kind == PB_RUN_BOOL ? 1 : (c.kind <= PB_RUN_SINT32 ? 4 : 8);
-        // first element index: the earlier chunks of the run
-        uint8_t* out = static_cast<uint8_t*>(c.dst) + (size_t)(prefix[ci] - prefix[c.first]) * eb;
+        if (lane == 63) wave_tot[wave] = incl;
+        __syncthreads();
         uint32_t rank = incl - mine;
-        bool bad = false;
-        // one slice body (160 fixed-position steps) run 4 times: the window,
-        // masks and slice state rotate down through registers each time
-        // (indexing them by k would put them in scratch)
-#pragma unroll 1
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t W[8] = {T[0], T[1], T[2], T[3], T[4], T[5], T[6], T[7]};
-            bad |= decode_slice(W, cont[0], own[0], c.kind, eb, out, rank);
-            rank += __popc((~cont[0] >> 16) & own[0]);
+        for (int w = 0; w < wave; ++w) rank += wave_tot[w];
+        const uint32_t total = wave_tot[0] + wave_tot[1] + wave_tot[2] + wave_tot[3];
+#define WBYTE(i) ((W[(i) >> 2] >> (8 * ((i) & 3))) & 0xFFu)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) T[i] = T[i + 4];
+        for (int p = 16; p < 32; ++p) {
+            if (!((term >> (p - 16)) & 1)) continue;
+            const uint32_t below = ~cont & ((1u << p) - 1);
+            const int n = p - (below ? 31 - __clz(below) : -1);  // varint bytes
+            if (n > 10 || (n == 10 && WBYTE(p) > 1)) bad = 1;
+            uint64_t v = 0;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                cont[i] = cont[i + 1];
-                own[i] = own[i + 1];
+            for (int k = 0; k < 10; ++k) {
+                if (k < n) v = (v << 7) | (WBYTE(p - k) & 0x7F);
             }
+            store_elem(image + sh + (size_t)rank * eb, c.kind, v);
+            ++rank;
         }
-        const bool any_bad = __any(bad);
-        if (lane == 0) err[ci] = any_bad ? 1 : 0;
+#undef WBYTE
+        __syncthreads();
+        if (bad) {
+            if (t == 0) err[ci] = 1;
+        } else {
+            const uint32_t nbytes = total * eb;
+            if (sh == sh0) {
+                copy_out_aligned(dst, image, sh, nbytes);
+            } else {
+                copy_out(dst, image, nbytes);
+            }
+            if (t == 0) err[ci] = 0;
+        }
+        __syncthreads();  // raw, image, wave_tot and bad are reused
+        c = next;
     }
 }
 
@@ -576,7 +580,7 @@ int LaunchPbRunDecode(const PbRunDecodeChunk* chunks, int n, uint32_t* counts, u
     // stride over the rest
     const int count_wgs = (n + kRunThreads / 64 - 1) / (kRunThreads / 64);
     const int count_grid = count_wgs < 2048 ? count_wgs : 2048;
-    const int decode_grid = count_grid;
+    const int decode_grid = n < 1024 ? n : 1024;  // 4 resident per CU (37 KiB of LDS each)
     hipLaunchKernelGGL(pb_run_count_kernel, dim3((unsigned)count_grid), dim3(kRunThreads), 0, s, chunks, n, counts,
                        prefix);
     if (hipGetLastError() != hipSuccess) return -1;
