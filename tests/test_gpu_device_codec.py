@@ -343,3 +343,24 @@ def test_packed_field_of_a_received_payload_stays_in_hbm(dev):
     [(count, code)] = native.gpu.device_decode_packed([out.data_ptr() + off], [ln], [0], [arr.data_ptr()], 0)
     assert code == 0 and count == len(vals)
     assert np.array_equal(arr.cpu().numpy(), vals)
+
+
+def test_codec_batch_limit_one_does_not_hold_a_requester(dev):
+    """-codec_batch_max_inflight=1 under 50 calls in flight: every call
+    finishes, and none waits for the whole burst. (A leader that launched
+    batches while waiting on the oldest one kept its own finished RPC until
+    the load stopped: a latency as long as the run.)"""
+    import time
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    native.set_flag("codec_batch_max_inflight", "1")
+    try:
+        t0 = time.perf_counter()
+        st = _echo(native, s.address, 6000, concurrency=50, attachment_body="text", device_compress=1)
+        elapsed_us = (time.perf_counter() - t0) * 1e6
+        assert st["success"] == 6000 and st["error"] == 0, st
+        assert st["max_us"] < 0.5 * elapsed_us, (st["max_us"], elapsed_us)
+    finally:
+        native.set_flag("codec_batch_max_inflight", "6")
+        s.stop()
