@@ -58,6 +58,7 @@ struct PressSession::Worker {
     std::map<int, std::pair<int64_t, std::string>> codes;  // error histogram
     std::atomic<int64_t>* remaining = nullptr;  // closed loop with a budget
     std::atomic<bool>* stop = nullptr;          // run-until-stopped
+    int64_t deadline_us = 0;                    // closed loop: stop issuing after this (0: none)
     int64_t pace_us = 0;                        // open loop interval per sender
     fiber::fiber_t tid = 0;
 
@@ -463,6 +464,7 @@ static void* closed_loop(void* arg) {
     int64_t seq = w->index;
     for (;;) {
         if (w->remaining) {
+            if (w->deadline_us && monotonic_us() >= w->deadline_us) break;
             if (w->remaining->fetch_sub(1, std::memory_order_relaxed) <= 0) break;
         } else if (w->stop->load(std::memory_order_relaxed)) {
             break;
@@ -521,7 +523,7 @@ void PressSession::collect(std::vector<std::unique_ptr<Worker>>& ws) {
     }
 }
 
-int PressSession::RunRequests(int64_t n) {
+int64_t PressSession::RunRequests(int64_t n, int64_t deadline_us) {
     if (_channels.empty() || n <= 0) return -1;
     std::atomic<int64_t> remaining{n};
     const int nw = (int)std::min<int64_t>(_opt.concurrency, n);
@@ -533,6 +535,7 @@ int PressSession::RunRequests(int64_t n) {
         w->s = this;
         w->index = i;
         w->remaining = &remaining;
+        w->deadline_us = deadline_us;
     }
     for (auto& w : ws) {
         fiber::Attr attr(fiber::STACK_NORMAL, fiber::ATTR_NOSIGNAL);
@@ -548,7 +551,7 @@ int PressSession::RunRequests(int64_t n) {
     collect(ws);
     std::lock_guard<std::mutex> g(_mu);
     _busy_s += (monotonic_us() - t0) / 1e6;
-    return 0;
+    return std::max<int64_t>(0, remaining.load(std::memory_order_relaxed));
 }
 
 int PressSession::RunFor(double seconds,

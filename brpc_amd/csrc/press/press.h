@@ -124,8 +124,11 @@ public:
     // Returns 0 on success, else fills *error.
     int Init(const PressOptions& opt, std::string* error);
     // Closed loop: issue exactly n calls over `concurrency` workers, return
-    // when all finished. Stats accumulate until ResetStats().
-    int RunRequests(int64_t n);
+    // when all finished. Stats accumulate until ResetStats(). With a
+    // deadline (monotonic us, 0: none) workers stop issuing once it passed
+    // and the calls in flight finish (each bounded by timeout_ms): returns
+    // the number of calls never issued (0 when all n ran), -1 on misuse.
+    int64_t RunRequests(int64_t n, int64_t deadline_us = 0);
     // Run for `seconds` (closed loop, or paced when qps>0); `tick` gets the
     // per-interval snapshot every second (rpc_press's info thread).
     int RunFor(double seconds, const std::function<void(const Snapshot& interval, const Snapshot& total)>& tick);

@@ -104,7 +104,8 @@ int StreamPress::write_chunk(Peer* p, std::string* err) {
     }
 }
 
-int StreamPress::RunSteps(int steps, std::string* err) {
+int StreamPress::RunSteps(int steps, std::string* err, int64_t deadline_us, int* done) {
+    if (done) *done = 0;
     const int64_t round = (int64_t)_opt.chunk_size * _opt.chunks_per_step;
     const int depth = std::max(1, _opt.pipeline_rounds);
     // every peer acknowledged `rounds` complete rounds (cumulative acks)
@@ -127,6 +128,10 @@ int StreamPress::RunSteps(int steps, std::string* err) {
     };
     const int64_t first = _steps;
     for (int s = 0; s < steps; ++s) {
+        if (deadline_us && monotonic_us() >= deadline_us) {
+            steps = s;  // no step starts after the deadline
+            break;
+        }
         for (int c = 0; c < _opt.chunks_per_step; ++c) {
             for (auto& p : _peers) {
                 if (write_chunk(p.get(), err) != 0) return -1;
@@ -137,8 +142,9 @@ int StreamPress::RunSteps(int steps, std::string* err) {
         const int64_t must = first + s + 1 - (depth - 1);
         if (must > first && wait_acked(must) != 0) return -1;
     }
-    if (wait_acked(first + steps) != 0) return -1;
+    if (steps > 0 && wait_acked(first + steps) != 0) return -1;
     _steps = first + steps;
+    if (done) *done = steps;
     return 0;
 }
 

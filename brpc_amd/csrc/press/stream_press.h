@@ -47,8 +47,10 @@ public:
     StreamPress() = default;
     ~StreamPress();
     int Init(const StreamPressOptions& opt, std::string* err);
-    // 0, or -1 with *err (timeout, stream failure).
-    int RunSteps(int steps, std::string* err);
+    // 0, or -1 with *err (timeout, stream failure). With a deadline
+    // (monotonic us, 0: none) no step starts after it; *done (optional)
+    // gets the steps completed by this call.
+    int RunSteps(int steps, std::string* err, int64_t deadline_us = 0, int* done = nullptr);
     int64_t bytes_sent() const { return _sent; }
     int64_t bytes_acked();
     int64_t steps_done() const { return _steps; }

@@ -217,9 +217,12 @@ public:
         }
         if (rc != 0) throw std::runtime_error("press init failed: " + err);
     }
-    void run_requests(int64_t n) {
+    // Returns the calls never issued because max_seconds (>0) ran out
+    // (0: all n ran).
+    int64_t run_requests(int64_t n, double max_seconds) {
         py::gil_scoped_release nogil;
-        _s.RunRequests(n);
+        const int64_t deadline = max_seconds > 0 ? monotonic_us() + (int64_t)(max_seconds * 1e6) : 0;
+        return _s.RunRequests(n, deadline);
     }
     void run_for(double seconds) {
         py::gil_scoped_release nogil;
@@ -261,14 +264,18 @@ public:
         }
         if (rc != 0) throw std::runtime_error("stream press init failed: " + err);
     }
-    void run_steps(int steps) {
+    // Steps completed; fewer than `steps` when max_seconds (>0) ran out
+    // before the rest started.
+    int run_steps(int steps, double max_seconds) {
         std::string err;
-        int rc;
+        int rc, done = 0;
         {
             py::gil_scoped_release nogil;
-            rc = _s->RunSteps(steps, &err);
+            const int64_t deadline = max_seconds > 0 ? monotonic_us() + (int64_t)(max_seconds * 1e6) : 0;
+            rc = _s->RunSteps(steps, &err, deadline, &done);
         }
         if (rc != 0) throw std::runtime_error(err);
+        return done;
     }
     py::dict stats() {
         py::dict d;
@@ -523,13 +530,13 @@ PYBIND11_MODULE(_native, m) {
 
     py::class_<PyStreamPress>(m, "StreamPress")
         .def(py::init<const py::dict&>())
-        .def("run_steps", &PyStreamPress::run_steps)
+        .def("run_steps", &PyStreamPress::run_steps, py::arg("steps"), py::arg("max_seconds") = 0.0)
         .def("stats", &PyStreamPress::stats)
         .def("close", &PyStreamPress::close);
 
     py::class_<PyPress>(m, "Press")
         .def(py::init<const py::dict&>())
-        .def("run_requests", &PyPress::run_requests)
+        .def("run_requests", &PyPress::run_requests, py::arg("n"), py::arg("max_seconds") = 0.0)
         .def("run_for", &PyPress::run_for)
         .def("stats", &PyPress::stats)
         .def("reset_stats", &PyPress::reset_stats);

@@ -75,3 +75,57 @@ def test_bench_multi_rank_gloo(nranks):
     assert j["p99_us_at_100qps_before_move"] > 0
     if nranks > 2:  # a relay chain needs at least two other ranks
         assert j["pipeline_hops"] == nranks - 1 and j["pipeline_gbytes_per_s"] > 0
+
+
+SMALL = ["--steps", "3", "--warmup", "1", "--requests-per-step", "2000", "--requests-per-step-64k", "500",
+         "--requests-per-step-grpc", "100", "--latency-sample-s", "0.3", "--skip-1m", "--skip-grpc"]
+
+
+def test_bench_leg_deadline_cuts_a_stalled_leg():
+    """A leg that overruns its deadline is cut, says so, and the run moves
+    on to the next legs: the JSON line is complete."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL +
+                       ["--leg-deadline-s", "3", "--stall-leg", "echo_64KB_host"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    assert j["timed_out_legs"] == ["echo_64KB_host"] and "incomplete" not in j
+    assert j["leg_wall_s"]["echo_64KB_host"] < 6.0
+    # the legs after the stalled one ran
+    assert j["qps_64KB_cpu_handler"] > 0 and j["stream_gbytes_per_s_64KB_chunks"] > 0 and j["p99_us_at_100qps"] > 0
+    assert j["value"] > 0 and j["errors"] == 0
+
+
+def test_bench_watchdog_prints_partial_json_on_hang():
+    """A leg that never returns (a hung native call or collective): the
+    watchdog prints what was measured, names the leg, and ends the rank."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL +
+                       ["--hard-deadline-s", "30", "--stall-leg", "cpu_handler_64KB:hang"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    j = lines[0]
+    assert j["incomplete"] is True and j["hung_leg"] == "cpu_handler_64KB"
+    assert KEYS <= set(j) and j["value"] > 0 and j["qps_64KB"] > 0
+    assert "qps_64KB_cpu_handler" not in j
+
+
+def test_bench_watchdog_two_ranks():
+    """The same at two ranks over gloo: every rank ends, torchrun returns,
+    rank 0's JSON holds the legs before the hang."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29541",
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL +
+                       ["--workers", "2", "--requests-per-step-fanout", "100", "--stream-min-s", "0.2",
+                        "--hard-deadline-s", "40", "--stall-leg", "scatter_64KB:hang"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    j = lines[0]
+    assert j["incomplete"] is True and j["hung_leg"] == "scatter_64KB"
+    assert j["n_gpus"] == 2 and j["fanout_errors"] == 0 and j["fanout_gbytes_per_s"] > 0
