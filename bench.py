@@ -408,6 +408,8 @@ def main(argv=None):
         limit = budget.leg_seconds()
         if limit <= 0:
             extra["skipped_legs"].append(name)
+            if topo.rank == 0:
+                print("bench: leg %s skipped (budget)" % name, file=sys.stderr, flush=True)
             return None
         dog.current = name
         t0 = time.monotonic()
@@ -416,6 +418,10 @@ def main(argv=None):
             r["leg_wall_s"] = round(time.monotonic() - t0, 3)
             legs[name] = r
         dog.current = None
+        if topo.rank == 0:  # progress (a long run must not look hung)
+            print("bench: leg %s %.1f s%s (wall %.0f s)" % (
+                name, time.monotonic() - t0, " TIMED OUT" if r and r.get("timed_out") else "",
+                time.monotonic() - T_START), file=sys.stderr, flush=True)
         return r
 
     def timed_leg(name, deadline, wl, steps, warmup, opts=None, min_s=0.0, transport_kind=None,
