@@ -252,7 +252,7 @@ bool launch(CBatch* b, int device) {
         if (s) SyncStream(s);
         return false;
     }
-    WatchEvent(b->ev, b->butex);
+    WatchEvent(b->ev, b->butex, nullptr, kEventCodec);
     return true;
 }
 

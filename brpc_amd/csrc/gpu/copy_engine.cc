@@ -144,7 +144,7 @@ void launch(Batch* b, int device) {
         fiber::butex_wake_all(b->butex);
         return;
     }
-    WatchEvent(b->ev, b->butex, &b->t_done);
+    WatchEvent(b->ev, b->butex, &b->t_done, kEventCopy);
 }
 
 }  // namespace

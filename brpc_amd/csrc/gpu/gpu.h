@@ -86,7 +86,12 @@ int SyncStream(hipStream_t s);
 // (or -1 on failure) into *butex and wakes every waiter parked on it. One
 // event can release a whole batch of fibers.
 // `done_us` (optional) receives the monotonic time the poller saw it done.
-void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us = nullptr);
+// `cls` groups events of similar duration (EventClass): the poller keeps a
+// completion-time average per class and sleeps until the earliest event
+// can be due, so a short copy handed over behind long codec batches is
+// polled on the copy's time scale, not the batches'.
+enum EventClass { kEventOther = 0, kEventCopy = 1, kEventCodec = 2, kEventClasses = 3 };
+void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us = nullptr, int cls = kEventOther);
 // Same for batches [first, last] of a resident copy worker ring (the
 // poller reads their pinned done words instead of querying an event).
 struct ResidentRing;

@@ -867,7 +867,12 @@ uint32_t* stream_scratch(int dev, hipStream_t s) {
     uint32_t* p = nullptr;
     const size_t bytes = 2 * kInlineSegments * sizeof(uint32_t);
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, bytes) != hipSuccess) return nullptr;
+    // hipMemset is asynchronous to the host and runs on the null stream,
+    // which non-blocking streams do not wait for: without the sync the first
+    // launch on `s` could fold into the allocation's old bytes (a wrong CRC
+    // once per stream; seen as one GPU-handler CRC mismatch with 8 ranks
+    // sharing a GPU, profiles/r5_rehearse8_one_gpu.json)
+    if (hipMemset(p, 0, bytes) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) return nullptr;
     (*m)[{dev, s}] = p;
     return p;
 }

@@ -537,6 +537,23 @@ public:
     // already committed to the matching group, never for a rank that is
     // busy elsewhere or slow: pairs with traffic move independently, idle
     // pairs exchange nothing.
+    //
+    // Why groups of different ranks cannot wait on each other in a cycle:
+    //  * a rank sets ready bits only while it has no group in flight, and
+    //    before it builds a group it clears every bit that did not fire (a
+    //    failed clear means the pair fired: it joins the group). So while a
+    //    group is in flight the rank has no bit set, nobody can fire a pair
+    //    with it, and every pair-round in ANY rank's in-flight group is in
+    //    the in-flight (or the next-built) group of its other endpoint too;
+    //  * each group issues its pairs in ascending peer order, which is the
+    //    same as ascending (low rank, high rank) pair order on every rank.
+    //    Even a library that ran a group's peers strictly one after another
+    //    then makes progress: the globally smallest pending pair is the
+    //    first pending one at both of its endpoints. (RCCL runs a group's
+    //    peers on parallel channels in its own delta-ordered schedule,
+    //    which is deadlock-free on consistent groups as well.)
+    // The stub library (one in-order queue per process, blocking sends) is
+    // the serial worst case, and runs the plane at 2, 3 and 8 ranks.
     void run() {
         if (!ops->host_memory()) hipSetDevice(device);
         for (;;) {
@@ -697,7 +714,14 @@ public:
                             return false;
                         }());
             if (!peer_ready && !have) continue;
+            // (not ready: nothing of ours may be listed; a stale list would
+            // be appended to and go out of step with the shm list)
+            if (!ps.listed.empty()) unlist_locked(p);
             write_list_locked(p, &stalled);
+            // what was actually listed decides: credit may have returned
+            // since `have` was computed, and a list we publish without our
+            // ready bit set would never be withdrawn
+            have = !ps.listed.empty();
             for (;;) {
                 if (w & other) {
                     // both ready: fire (the round moves on, both bits clear)
@@ -764,6 +788,17 @@ public:
             PeerState& ps = peers[p];
             PairSlot* s = slot(p);
             const PairList& theirs = s->list[ps.round % 2][1 - side_with(p)];
+            const PairList& ours = s->list[ps.round % 2][side_with(p)];
+            // the peer receives what the shm list says: our sends must be
+            // exactly that list, or the pair's sends and receives go out of
+            // step (a hang until -rccl_timeout_ms at best)
+            bool in_step = ours.n == ps.listed.size();
+            for (uint32_t i = 0; in_step && i < ours.n; ++i)
+                in_step = ours.e[i].seq == ps.listed[i].seq && ours.e[i].len == ps.listed[i].len;
+            if (!in_step && dead_reason.empty()) {
+                dead_reason = "pair list out of step with rank " + std::to_string(p) + " (" +
+                              std::to_string(ps.listed.size()) + " listed, shm says " + std::to_string(ours.n) + ")";
+            }
             moving_send[p].swap(ps.listed);
             const uint32_t n = std::min<uint32_t>(theirs.n, kListMax);
             for (uint32_t i = 0; i < n; ++i) {

@@ -86,6 +86,7 @@ struct Waiter {
     uint64_t first = 0, last = 0;
     int64_t since_us = 0;
     int64_t added_us = 0;  // when the poller was handed the event
+    int cls = kEventOther;  // EventClass: whose completion-time average applies
 };
 
 class EventPoller {
@@ -179,7 +180,8 @@ private:
                     if (active[i].done_us) *active[i].done_us = t;
                     // how long events take from hand-over to completion
                     const int64_t took = t - active[i].added_us;
-                    if (took > 0 && took < 100000) _ema_us += (took - _ema_us) / 8;
+                    int64_t& ema = _ema_us[active[i].cls];
+                    if (took > 0 && took < 100000) ema += (took - ema) / 8;
                 }
                 active[i].butex->store(r == hipSuccess ? 1 : -1, std::memory_order_release);
                 // queue the woken fibers without signalling; one signal for
@@ -198,16 +200,23 @@ private:
                 // calling hipEventQuery in a loop (each call walks the HIP
                 // runtime's thread-locals and locks; a spinning poller was a
                 // full host core under codec load)
-                int64_t oldest = t;
-                for (const Waiter& w : active) oldest = std::min(oldest, w.added_us);
-                const int64_t due = oldest + _ema_us * FLAGS_gpu_poller_wait_pct / 100;
+                // Each event is due at its hand-over plus a share of ITS
+                // class's typical completion time; the earliest due event
+                // sets the nap (one global average let a short
+                // copy behind long codec batches wait up to 200 us).
+                int64_t due = INT64_MAX, shortest = INT64_MAX;
+                for (const Waiter& w : active) {
+                    const int64_t ema = _ema_us[w.cls];
+                    due = std::min(due, w.added_us + ema * FLAGS_gpu_poller_wait_pct / 100);
+                    shortest = std::min(shortest, ema);
+                }
                 int64_t sleep_us = 0;
                 if (FLAGS_gpu_poller_wait_pct > 0 && due - t >= 8) {
                     sleep_us = std::min<int64_t>(due - t, 200);
-                } else if (!progressed && FLAGS_gpu_poller_wait_pct > 0 && _ema_us >= 20) {
-                    // long events (codec batches, large pulls): one pass per
-                    // ~tenth of their duration is enough
-                    sleep_us = std::max<int64_t>(2, std::min<int64_t>(_ema_us / 10, 10));
+                } else if (!progressed && FLAGS_gpu_poller_wait_pct > 0 && shortest >= 20) {
+                    // only long events pending (codec batches, large pulls):
+                    // one pass per ~tenth of the shortest class's duration
+                    sleep_us = std::max<int64_t>(2, std::min<int64_t>(shortest / 10, 10));
                 } else if (t - last_progress_us > FLAGS_gpu_poller_spin_us) {
                     sleep_us = std::max(1, FLAGS_gpu_poller_sleep_us);
                 }
@@ -227,7 +236,7 @@ private:
     bool _started = false;
     pthread_t _th;
     std::atomic<int64_t> _polled{0};
-    int64_t _ema_us = 0;  // hand-over to completion, moving average (poller thread only)
+    int64_t _ema_us[kEventClasses] = {};  // hand-over to completion per EventClass (poller thread only)
 };
 
 EventPoller* poller() {
@@ -356,8 +365,10 @@ int WaitEvent(hipEvent_t ev) {
     return v == 1 ? 0 : -1;
 }
 
-void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us) {
-    poller()->add(Waiter{ev, butex, done_us});
+void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us, int cls) {
+    Waiter w{ev, butex, done_us};
+    w.cls = cls >= 0 && cls < kEventClasses ? cls : kEventOther;
+    poller()->add(w);
 }
 
 void WatchResident(ResidentRing* ring, uint64_t first_seq, uint64_t last_seq, std::atomic<int>* butex,
@@ -367,6 +378,7 @@ void WatchResident(ResidentRing* ring, uint64_t first_seq, uint64_t last_seq, st
     w.first = first_seq;
     w.last = last_seq;
     w.since_us = monotonic_us();
+    w.cls = kEventCopy;
     poller()->add(w);
 }
 

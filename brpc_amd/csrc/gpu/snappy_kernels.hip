@@ -55,6 +55,16 @@ namespace gpu {
 
 namespace {
 
+// Length of a literal with nb (1..4) extra length bytes in `ext`. The
+// stored value is length - 1: 0xFFFFFFFF (a 4 GiB literal) would wrap to 0
+// in 32 bits and pass as an empty literal, so it saturates instead and fails
+// every bound check like any other literal longer than its piece.
+__device__ __forceinline__ uint32_t lit_len(uint32_t ext, uint32_t nb) {
+    const uint32_t raw = ext & (0xFFFFFFFFu >> (32 - 8 * nb));
+    return raw == 0xFFFFFFFFu ? raw : raw + 1;
+}
+
+
 constexpr int kWave = 64;
 constexpr uint32_t kWindow = 256;  // bytes of compressed stream held in VGPRs
 
@@ -118,7 +128,7 @@ __device__ __forceinline__ int decode_elements(gbyte_c* in, uint32_t in_len, uin
                     bad = 3;
                     break;
                 }
-                len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
+                len = lit_len(ext, nb);
                 ip += nb;
             }
             if (len > in_len - ip || len > ulen - op) {
@@ -374,7 +384,7 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(con
             hdr = 1;
             if (len > 60) {
                 const uint32_t nb = len - 60;
-                len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
+                len = lit_len(ext, nb);
                 hdr += nb;
             }
         } else if (kind == 1) {
@@ -587,7 +597,7 @@ __global__ void __launch_bounds__(kWave) snappy_split_kernel(const SnappyStream*
             uint32_t nb = 0;
             if (len > 60) {
                 nb = len - 60;
-                len = (ext & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
+                len = lit_len(ext, nb);
             }
             csize = 1ull + nb + len;
         } else if (kind == 1) {

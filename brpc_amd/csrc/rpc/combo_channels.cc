@@ -127,17 +127,20 @@ void on_sub_done(SubState* s) {
                         else if (pc->unified_error != sec) pc->unified_error = ETOOMANYFAILS;
                     }
                 }
-                if (pc->nfail >= pc->fail_limit || (pc->canceled && pc->ndone == pc->nlaunched)) {
+                if (pc->nfail >= pc->fail_limit) {
                     pc->finished = true;
                     complete = true;
                     // the reference's unified code (parallel_channel.cpp:352-366):
                     // the failed sub calls' common error, ECANCELED when they
                     // were all canceled, ETOOMANYFAILS when they differ
-                    ec = pc->canceled ? ECANCELED : (pc->unified_error ? pc->unified_error : ECANCELED);
+                    ec = pc->unified_error ? pc->unified_error : ECANCELED;
                     et = std::to_string(pc->nfail) + "/" + std::to_string(pc->nlaunched) +
                          " sub calls failed (fail_limit=" + std::to_string(pc->fail_limit) +
                          "), first: [E" + std::to_string(pc->first_error) + "] " + pc->first_error_text;
                 } else if (pc->nsuccess >= pc->success_limit || pc->ndone == pc->nlaunched) {
+                    // (a canceled call whose failures stayed under fail_limit
+                    // succeeds: enough sub calls succeeded before the cancel,
+                    // parallel_channel.cpp:375-381)
                     pc->finished = true;
                     complete = true;
                 }

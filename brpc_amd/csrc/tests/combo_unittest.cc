@@ -535,3 +535,39 @@ TEST(SelectiveChannel, remove_channel_moves_traffic) {
     sc.RemoveAndDestroyChannel(hb);
     EXPECT_EQ(call(&sc, "r", &out), EHOSTDOWN);
 }
+
+// A cancel that comes after enough sub calls succeeded: the call succeeds
+// with what was merged (parallel_channel.cpp:375-381); with a fail_limit the
+// canceled sub call reaches, it fails with ECANCELED.
+TEST(ParallelChannel, cancel_after_partial_success) {
+    TaggedServer fast("fast"), slow("slow");
+    slow.echo.delay_us = 1000000;
+    for (int limit : {2, 1}) {
+        ParallelChannelOptions po;
+        po.timeout_ms = 5000;
+        po.fail_limit = limit;
+        ParallelChannel pc;
+        pc.Init(&po);
+        pc.AddChannel(make_channel(fast.addr(), 5000), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+        pc.AddChannel(make_channel(slow.addr(), 5000), OWNS_CHANNEL, nullptr, std::make_shared<ConcatMerger>());
+        example::EchoService_Stub stub(&pc);
+        Controller cntl;
+        example::EchoRequest req;
+        example::EchoResponse res;
+        req.set_message("c");
+        std::atomic<int> done{0};
+        const int64_t t0 = monotonic_us();
+        stub.Echo(&cntl, &req, &res, NewCallback([&done] { done.fetch_add(1); }));
+        usleep(150000);  // the fast sub call is back, the slow one sleeps
+        StartCancel(cntl.call_id());
+        for (int i = 0; i < 400 && !done.load(); ++i) usleep(2000);
+        ASSERT_EQ(done.load(), 1);
+        EXPECT_LT(monotonic_us() - t0, 800000);  // did not wait for the slow server
+        if (limit == 2) {
+            EXPECT_FALSE(cntl.Failed());
+            EXPECT_EQ(res.message(), "c@fast");
+        } else {
+            EXPECT_EQ(cntl.ErrorCode(), ECANCELED);
+        }
+    }
+}

@@ -223,20 +223,27 @@ TEST(FiberDepth, key_destructors_run_per_fiber_with_their_values) {
 }
 
 TEST(FiberDepth, fiber_count_tracks_live_fibers) {
+    // Measured against the count while the 50 are alive, not against a
+    // sample taken before them: fibers of earlier cases may still be
+    // exiting when this starts, and exits only ever lower the count, so
+    // both checks hold whatever else is winding down.
     std::atomic<int> release{0};
-    const int64_t before = fiber::fiber_count();
+    std::atomic<int> started{0};
     std::vector<fiber::fiber_t> ts(50);
     for (auto& t : ts) {
         fiber::start(
             [&] {
+                started.fetch_add(1);
                 while (!release.load()) fiber::usleep(1000);
             },
             false, nullptr, &t);
     }
-    ::usleep(20000);
-    EXPECT_GE(fiber::fiber_count(), before + 50);
+    for (int i = 0; i < 2000 && started.load() < 50; ++i) ::usleep(1000);
+    ASSERT_EQ(started.load(), 50);
+    const int64_t during = fiber::fiber_count();
+    EXPECT_GE(during, 50);
     release = 1;
     for (auto t : ts) fiber::join(t, nullptr);
-    for (int i = 0; i < 100 && fiber::fiber_count() > before; ++i) ::usleep(1000);
-    EXPECT_LE(fiber::fiber_count(), before);
+    for (int i = 0; i < 100 && fiber::fiber_count() > during - 50; ++i) ::usleep(1000);
+    EXPECT_LE(fiber::fiber_count(), during - 50);
 }

@@ -80,6 +80,31 @@ def test_snappy_rejects_malformed(dev):
         snappy_decompress(d, [0], [len(bad)], [29])
 
 
+@pytest.mark.parametrize("ulen", [5, 64, 3000])
+def test_snappy_rejects_4_byte_literal_length_wrap(dev, ulen):
+    """A literal whose 4 length bytes are FF FF FF FF stores length-1 =
+    2^32-1: in 32 bits the length wraps to 0. It must be refused, not read
+    as an empty literal, by the serial and parallel decoders."""
+    from brpc_amd.ops import snappy_decompress
+    varint = bytearray()
+    v = ulen
+    while True:
+        varint.append((v & 0x7F) | (0x80 if v > 0x7F else 0))
+        v >>= 7
+        if not v:
+            break
+    # the wrapping literal, then a valid literal that would fill the piece
+    body = bytes([0xFC, 0xFF, 0xFF, 0xFF, 0xFF])
+    if ulen <= 60:
+        body += bytes([(ulen - 1) << 2]) + b"a" * ulen
+    else:
+        body += bytes([61 << 2, (ulen - 1) & 0xFF, (ulen - 1) >> 8]) + b"a" * ulen
+    bad = bytes(varint) + body
+    d = torch.frombuffer(bytearray(bad), dtype=torch.uint8).to(dev)
+    with pytest.raises(ValueError):
+        snappy_decompress(d, [0], [len(bad)], [ulen])
+
+
 @pytest.mark.parametrize("kind", ["random", "runs", "text", "mixed"])
 @pytest.mark.parametrize("n", [1, 3, 4, 63, 64, 65, 1000, 65536, 300001])
 def test_gpu_compress_round_trips_through_host_and_gpu(dev, kind, n):
