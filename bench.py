@@ -113,6 +113,7 @@ def parse(argv=None):
     ap.add_argument("--min-leg-s", type=float, default=3.0, help="a leg needs at least this much budget to start")
     ap.add_argument("--hard-deadline-s", type=float, default=540.0,
                     help="watchdog: print what was measured and end every rank at this many wall seconds")
+    ap.add_argument("--only", default="", help="comma-separated leg names: run only these (experiments)")
     ap.add_argument("--stall-leg", default="", help=argparse.SUPPRESS)  # test hook: NAME[:hang]
     return ap.parse_args(argv)
 
@@ -285,6 +286,7 @@ def main(argv=None):
     cuda = torch.cuda.is_available()
     n = topo.world_size
     stall_name, _, stall_mode = a.stall_leg.partition(":")
+    only = set(x for x in a.only.split(",") if x)
 
     def sync():
         if cuda:
@@ -405,6 +407,8 @@ def main(argv=None):
     def run_leg(name, fn, *args, **kw):
         """Run one leg under the budget. fn(deadline, *args) -> result dict
         (or None). Collective-safe: every rank takes the same branch."""
+        if only and name not in only:
+            return None
         limit = budget.leg_seconds()
         if limit <= 0:
             extra["skipped_legs"].append(name)
@@ -691,9 +695,7 @@ def main(argv=None):
             ox.update({"concurrency": a.concurrency})
             ox.update(extra_opts)
             rcpu = run_leg(name + "_cpu", timed_leg, wlx, a.steps, a.warmup, dict(ox), min_s=a.codec_min_s)
-            if rcpu is None:
-                continue
-            rx[name] = {"cpu": rcpu}
+            rx[name] = {"cpu": rcpu} if rcpu is not None else {}
             if "body" in extra_opts and extra_opts.get("request_compress_type"):
                 # what the compressor sees: the body's snappy ratio on the host
                 raw = native.echo_body(extra_opts["body"], ox["request_size"])

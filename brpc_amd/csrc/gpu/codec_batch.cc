@@ -14,6 +14,9 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 
+DEFINE_bool(codec_fused, true,
+            "run codec batches of compress blocks and decode pieces (<= 8 KiB) as one fused launch of the "
+            "workgroup-parallel codec (gpu/codec_fused.hip) instead of serial per-stage kernels");
 DEFINE_int32(codec_batch_max_inflight, 6,
              "codec batches in flight per device before the next one waits for a completion (0: no limit); "
              "while it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches");
@@ -62,6 +65,9 @@ struct CBatch {
     PinnedArray<uint32_t> comp_len, decomp_len;
     PinnedArray<int> comp_err, decomp_err;
     PinnedArray<PbScanJob> scan_jobs;
+    PinnedArray<uint32_t> piece_group, group_pieces;  // fused launches: piece -> scan group, pieces per group
+    uint32_t* group_done = nullptr;                   // HBM counters, zero between launches
+    size_t group_done_cap = 0;
     PinnedArray<uint64_t> scan_fields;
     PinnedArray<int32_t> scan_n;
     void* scratch = nullptr;  // compress slots of blocks above 16 KiB
@@ -106,7 +112,7 @@ void retire_done(Engine& e) {
 }
 
 Engine g_engine[kMaxDev];
-std::atomic<int64_t> g_requests{0}, g_launches{0}, g_run_chunks{0}, g_dec_chunks{0};
+std::atomic<int64_t> g_requests{0}, g_launches{0}, g_run_chunks{0}, g_dec_chunks{0}, g_fused_launches{0};
 
 CBatch* new_batch(Engine& e) {
     if (!e.spare.empty()) {
@@ -208,12 +214,70 @@ bool launch(CBatch* b, int device) {
         }
         if (!b->scratch) return false;
     }
+    // one fused launch when the batch is device-body work only: compress
+    // blocks and headerless pieces that fit the workgroup codec, and scans
+    // that each name the pieces forming their message
+    bool fused = FLAGS_codec_fused && nruns == 0 && ndec == 0 && h2d.empty() && d2h.empty() && ndecomp == 0 &&
+                 nstreams == 0 && (ncomp || nhpieces) && comp_max <= kFusedMaxBlock && hpiece_max <= kFusedMaxBlock;
+    for (size_t i = 0; fused && i < b->reqs.size(); ++i) {
+        const CodecRequest* r = b->reqs[i];
+        if (r->scans.empty()) continue;
+        if (r->scan_piece_first.size() != r->scans.size() || r->scan_piece_count.size() != r->scans.size()) {
+            fused = false;
+            break;
+        }
+        for (size_t k = 0; k < r->scans.size(); ++k) {
+            if (r->scan_piece_count[k] == 0 || r->scan_piece_first[k] + r->scan_piece_count[k] > r->pieces.size()) {
+                fused = false;
+            }
+        }
+    }
+    if (fused && (!b->piece_group.reserve(nhpieces) || !b->group_pieces.reserve(nscan))) return false;
     int prev = 0;
     hipGetDevice(&prev);
     if (prev != device) hipSetDevice(device);
     hipStream_t s = PoolStream(device);
     b->ev = AcquireEvent();
     int rc = (s && b->ev) ? 0 : -1;
+    if (rc == 0 && fused) {
+        if (nscan > b->group_done_cap) {
+            if (b->group_done) HbmFree(b->group_done, b->group_done_cap * sizeof(uint32_t), device);
+            const size_t cap = std::max<size_t>(nscan, 256);
+            b->group_done = static_cast<uint32_t*>(HbmAlloc(cap * sizeof(uint32_t), device));
+            b->group_done_cap = b->group_done ? cap : 0;
+            // ordered before the launch on the same stream
+            if (!b->group_done || hipMemsetAsync(b->group_done, 0, cap * sizeof(uint32_t), s) != hipSuccess) rc = -1;
+        }
+        for (size_t p = 0; p < nhpieces; ++p) b->piece_group.p[p] = kFusedNoGroup;
+        for (size_t i = 0; i < b->reqs.size(); ++i) {
+            const CodecRequest* r = b->reqs[i];
+            for (size_t k = 0; k < r->scans.size(); ++k) {
+                const size_t g = b->scan_row[i] + k;
+                b->group_pieces.p[g] = r->scan_piece_count[k];
+                for (uint32_t q = 0; q < r->scan_piece_count[k]; ++q)
+                    b->piece_group.p[b->piece_first[i] + r->scan_piece_first[k] + q] = (uint32_t)g;
+            }
+        }
+        FusedCodecArgs fa;
+        fa.comp = b->comp_jobs.p;
+        fa.ncomp = (int)ncomp;
+        fa.comp_len = b->comp_len.p;
+        fa.comp_err = b->comp_err.p;
+        fa.pieces = b->piece_jobs.p;
+        fa.npieces = (int)nhpieces;
+        fa.piece_err = b->piece_job_err.p;
+        fa.piece_group = nscan ? b->piece_group.p : nullptr;
+        fa.scans = b->scan_jobs.p;
+        fa.group_pieces = b->group_pieces.p;
+        fa.group_done = b->group_done;
+        fa.scan_fields = b->scan_fields.p;
+        fa.scan_n = b->scan_n.p;
+        fa.max_fields = kCodecScanFields;
+        fa.max_ulen = std::max(ncomp ? comp_max : 1u, nhpieces ? hpiece_max : 1u);
+        if (rc == 0) rc = LaunchFusedCodec(fa, s);
+        g_fused_launches.fetch_add(1, std::memory_order_relaxed);
+        ncomp = nhpieces = nscan = 0;  // nothing left for the per-stage sequence below
+    }
     if (rc == 0 && nruns) rc = LaunchPbRunEncode(b->run_jobs.p, (int)nruns, b->run_err.p, s);
     g_run_chunks.fetch_add((int64_t)nruns, std::memory_order_relaxed);
     if (rc == 0 && !h2d.empty()) rc = LaunchBatchedCopy(h2d.data(), (int)h2d.size(), s);
@@ -359,6 +423,7 @@ CodecBatchStats GetCodecBatchStats() {
     s.launches = g_launches.load(std::memory_order_relaxed);
     s.run_chunks = g_run_chunks.load(std::memory_order_relaxed);
     s.decode_chunks = g_dec_chunks.load(std::memory_order_relaxed);
+    s.fused_launches = g_fused_launches.load(std::memory_order_relaxed);
     return s;
 }
 

@@ -37,6 +37,12 @@ struct CodecRequest {
     // wire scans of decoded messages (kCodecScanFields rows each), run after
     // every decode of the batch
     std::vector<PbScanJob> scans;
+    // optional, per scan: the range of `pieces` that decode into its message.
+    // When every scan of a batch names its pieces (and the batch holds only
+    // compress jobs and pieces of <= kFusedMaxBlock), the batch is ONE fused
+    // launch (gpu/codec_fused.hip) and the scan runs as soon as the
+    // message's last piece is decoded.
+    std::vector<uint32_t> scan_piece_first, scan_piece_count;
     // copies issued after the kernels (HBM -> pinned)
     std::vector<Segment> d2h;
     // packed varint runs decoded last (their bytes are final by then);
@@ -62,7 +68,7 @@ constexpr uint32_t kCodecScanFields = 128;
 int RunCodecRequest(CodecRequest* r, int device);
 
 struct CodecBatchStats {
-    int64_t requests = 0, launches = 0, run_chunks = 0, decode_chunks = 0;
+    int64_t requests = 0, launches = 0, run_chunks = 0, decode_chunks = 0, fused_launches = 0;
 };
 CodecBatchStats GetCodecBatchStats();
 

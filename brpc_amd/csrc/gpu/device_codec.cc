@@ -123,6 +123,8 @@ int DeviceSnappyDecode(const DeviceSnappyBlocks* jobs, int n, int* err, DevicePa
         if (j.scan && index) {
             scan_row[k] = req.scans.size();
             req.scans.push_back(PbScanJob{static_cast<const uint8_t*>(j.dst), j.len});
+            req.scan_piece_first.push_back((uint32_t)first[k]);
+            req.scan_piece_count.push_back(j.lay.nblocks);
         }
     }
     if (req.pieces.empty()) return 0;

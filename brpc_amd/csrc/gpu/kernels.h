@@ -157,6 +157,39 @@ struct PbScanJob {
 int LaunchPbScanPtrs(const PbScanJob* jobs, int64_t n, uint32_t max_fields, uint64_t* fields, int32_t* nfields,
                      hipStream_t s);
 
+// Fused device-body codec launch (gpu/codec_fused.hip): ONE launch runs a
+// codec batch's compress blocks and headerless decode pieces, each at most
+// kFusedMaxBlock uncompressed bytes, one 256-thread workgroup per block or
+// piece, all concurrently; a message whose pieces all decoded is pb-scanned
+// by the workgroup that finished its last piece (no further launch).
+//  * compress: a block-wide parse — every position's match candidate and
+//    length in parallel, the greedy element chain found by speculative
+//    per-segment walks that are re-walked until their entries agree — into
+//    one raw snappy stream with its varint header (matches span the block);
+//  * decode: the element chain found the same way over the compressed
+//    bytes, then a source map resolved by pointer jumping.
+constexpr uint32_t kFusedMaxBlock = 8192;
+constexpr uint32_t kFusedNoGroup = 0xFFFFFFFFu;
+struct FusedCodecArgs {
+    const SnappyJob* comp = nullptr;  // compress jobs (device-readable table)
+    int ncomp = 0;
+    uint32_t* comp_len = nullptr;
+    int* comp_err = nullptr;          // 0, 1 (block too large), 2 (output exceeds dst_cap)
+    const SnappyPiece* pieces = nullptr;
+    int npieces = 0;
+    int* piece_err = nullptr;         // 0, 1 (too large), 3 (element chain leaves the piece), 4 (size), 6 (offset)
+    const uint32_t* piece_group = nullptr;  // per piece: scan group, or kFusedNoGroup
+    const PbScanJob* scans = nullptr;       // per group: the message its pieces form
+    const uint32_t* group_pieces = nullptr; // per group: how many pieces decode into it
+    uint32_t* group_done = nullptr;         // per group: HBM counter, zero between launches
+    uint64_t* scan_fields = nullptr;        // per group: max_fields {tag, value} rows
+    int32_t* scan_n = nullptr;
+    uint32_t max_fields = 0;
+    uint32_t max_ulen = 0;                  // >= every block's and piece's size
+};
+int LaunchFusedCodec(const FusedCodecArgs& a, hipStream_t s);
+
+
 // Batched encoder of repeated numeric runs (SURVEY K2, and the number
 // arrays of pb2json, K6): one workgroup per chunk of <= kPbRunChunkElems
 // elements, read in the std::vector layout of the field (1/4/8 bytes per

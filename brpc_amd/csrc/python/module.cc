@@ -725,6 +725,7 @@ PYBIND11_MODULE(_native, m) {
         d["launches"] = s.launches;
         d["run_chunks"] = s.run_chunks;
         d["decode_chunks"] = s.decode_chunks;
+        d["fused_launches"] = s.fused_launches;
         return d;
     });
     // numeric run (vector layout bytes) -> varints / JSON numbers on the device (tests)

@@ -6,12 +6,15 @@
 #   bench1       bench.py at N=1 (the driver's BENCH shape)
 #   rehearse:K   K ranks on the box's one GPU (torchrun, --skip-rccl: RCCL
 #                refuses ranks that share a GPU), every N>1 leg, small steps
+#   pytest:FILE  one GPU test file (tests/FILE.py)
+#   bench:ARGS   bench.py ARGS (comma-separated), one JSON + a leg summary
 #   kt:ARGS      rocprofv3 kernel trace of bench.py ARGS (comma-separated)
 # Output lands in gpurun_out/<tag>/ (tag = $TAG, default "run").
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 T=gpurun_out/${TAG:-run}; mkdir -p $T
+nb=0
 for st in "$@"; do
   case $st in
     tests)
@@ -32,6 +35,15 @@ for st in "$@"; do
         --requests-per-step-fanout 200 --latency-sample-s 2 --sweep-seconds 0.2 \
         > $T/rehearse$k.log 2>&1 || { tail -20 $T/rehearse$k.log; exit 1; }
       grep '^{"metric"' $T/rehearse$k.log > $T/rehearse$k.json; cut -c1-400 $T/rehearse$k.json ;;
+    pytest:*)
+      f=${st#pytest:}
+      timeout -k 10 600 python -u -m pytest tests/${f%%::*}.py -m gpu -x -q --timeout 120 --timeout-method thread \
+        > $T/pytest_${f%%::*}.txt 2>&1 || { tail -40 $T/pytest_${f%%::*}.txt; exit 1; }
+      tail -2 $T/pytest_${f%%::*}.txt ;;
+    bench:*)
+      args=${st#bench:}; nb=$((nb+1))
+      timeout -k 10 600 python -u bench.py ${args//,/ } > $T/bench_$nb.log 2>&1 || { tail -20 $T/bench_$nb.log; exit 1; }
+      grep '^{"metric"' $T/bench_$nb.log > $T/bench_$nb.json; echo "bench_$nb: $args"; python benchmarks/leg_summary.py $T/bench_$nb.json ;;
     kt:*)
       args=${st#kt:}
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $T/kt -o kt -- python3 bench.py ${args//,/ } \
