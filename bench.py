@@ -286,7 +286,7 @@ def main(argv=None):
     cuda = torch.cuda.is_available()
     n = topo.world_size
     stall_name, _, stall_mode = a.stall_leg.partition(":")
-    only = set(x for x in a.only.split(",") if x)
+    only = set(x for x in a.only.replace("+", ",").split(",") if x)
 
     def sync():
         if cuda:

@@ -520,6 +520,12 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     }
     if (index) {
         req.scans.push_back(PbScanJob{reinterpret_cast<const uint8_t*>(out_base), total});
+        if (host_cut) {
+            // every piece decodes into this message: a fused batch scans it
+            // as soon as its last piece is done
+            req.scan_piece_first.push_back(0);
+            req.scan_piece_count.push_back((uint32_t)req.pieces.size());
+        }
         if (out_base != dst.p) req.d2h.push_back(Segment{dbody.p, dst.p, total});
     }
     if (RunCodecRequest(&req, dev) != 0) return false;

@@ -484,6 +484,14 @@ ssize_t Socket::RdmaRead(int fd, size_t size_hint) {
         }
         InstallRdmaEndpoint(std::move(ep));
         _rdma_state.store(RDMA_ON, std::memory_order_release);
+        if (!_read_buf.empty()) {
+            // bytes behind the hello on TCP: once verbs carry the traffic,
+            // the TCP stream must stay silent (reference: FALLBACK_TCP /
+            // EPROTO, test/brpc_rdma_unittest.cpp:577,1126)
+            LOG(WARNING) << "data on TCP after the RDMA hello from " << _remote_side;
+            errno = EPROTO;
+            return -1;
+        }
         errno = EAGAIN;
         return -1;
     }
@@ -495,10 +503,15 @@ ssize_t Socket::RdmaRead(int fd, size_t size_hint) {
         return n;
     }
     // Nothing from the verbs side: the idle TCP connection tells us whether
-    // the peer went away.
+    // the peer went away, or broke the protocol by writing on it.
     char c;
     const ssize_t r = ::recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
     if (r == 0) return 0;
+    if (r > 0) {
+        LOG(WARNING) << "data on TCP after the RDMA hello from " << _remote_side;
+        errno = EPROTO;
+        return -1;
+    }
     if (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK) return -1;
     errno = EAGAIN;
     return -1;
