@@ -66,6 +66,9 @@ constexpr int kT = 256;  // threads per workgroup
 constexpr int kWaves = kT / 64;
 constexpr int kTableBits = 12;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint32_t kWalkSeg = 64;                            // positions (or compressed bytes) per walk segment
+constexpr uint32_t kCompSegs = kFusedMaxBlock / kWalkSeg;    // 128
+static_assert(kCompSegs <= (uint32_t)kT, "one walker thread per segment");
 
 typedef const __attribute__((address_space(1))) uint8_t gbyte_c;
 typedef __attribute__((address_space(1))) uint8_t gbyte;
@@ -190,9 +193,10 @@ __device__ __forceinline__ void store_out(void* dst, const uint8_t* stage, uint3
 // ---------------------------------------------------------------- compress
 // LDS: in (C + 96, 16 B of alignment slack + 80 B of zero pad) | L (C) |
 // cand (2C) | NC (2C + 16) | table (16 KiB, later the output stage) |
-// wtot (kWaves) | xch (kT) | ex (kT)
+// wtot (kWaves) | xch (kT) | ex (kT) | segruns (u64 x kCompSegs) | segcarry
 __host__ __device__ constexpr uint32_t CompressLds(uint32_t C) {
-    return (C + 96) + C + 2 * C + (2 * C + 16) + (4u << kTableBits) + 4 * (kWaves + 2 * kT) + 64;
+    return (C + 96) + C + 2 * C + (2 * C + 16) + (4u << kTableBits) + 4 * (kWaves + 2 * kT) + 8 + 12 * kCompSegs +
+           64;
 }
 
 __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
@@ -216,6 +220,8 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     uint32_t* wtot = table + (1u << kTableBits);
     uint32_t* xch = wtot + kWaves;
     uint32_t* ex = xch + kT;
+    uint64_t* segruns = reinterpret_cast<uint64_t*>(ex + kT + 2);  // 8-byte aligned: 6C + 112 + 16 KiB + 4 * (516 + 2)
+    uint32_t* segcarry = reinterpret_cast<uint32_t*>(segruns + kCompSegs);
 
     for (uint32_t i = t; i < (1u << kTableBits); i += kT) table[i] = kNone;
     const uint32_t mis = stage_in(jb.src, n, raw, 80);
@@ -262,23 +268,31 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         if (t == 0) NC[n] = (uint16_t)n;
     }
     __syncthreads();
-    // 3. the greedy parse: speculative segment walks, re-walked until every
-    //    segment's entry is its predecessor's exit
-    uint32_t entry = lo, mask = 0;
+    // 3. the greedy parse: speculative walks over 64-position segments (one
+    //    thread each), re-walked until every segment's entry is its
+    //    predecessor's exit. A segment this long holds several elements, so
+    //    walks from different entries meet inside it and the corrections
+    //    stop after a few rounds instead of crawling one segment per round.
+    const uint32_t S = (n + kWalkSeg - 1) / kWalkSeg;
+    const bool walker = (uint32_t)t < S;
+    const uint32_t wlo = walker ? (uint32_t)t * kWalkSeg : n, whi = walker ? min(n, wlo + kWalkSeg) : n;
+    uint32_t entry = wlo;
+    uint64_t mask = 0;
     auto walk = [&](uint32_t e) -> uint32_t {
         mask = 0;
-        while (e < hi) {
-            mask |= 1u << (e - lo);
+        while (e < whi) {
+            mask |= 1ull << (e - wlo);
             const uint32_t l = L[e];
             e = l >= 4 ? e + l : NC[e + 1];
         }
         return e;
     };
-    uint32_t exitp = walk(entry);
-    ex[t] = exitp;
+    uint32_t exitp = walker ? walk(entry) : n;
+    if (walker) ex[t] = exitp;
+    uint32_t rounds = 0;
     for (;;) {
         __syncthreads();
-        const uint32_t want = t ? ex[t - 1] : 0u;
+        const uint32_t want = walker ? (t ? ex[t - 1] : 0u) : entry;
         __syncthreads();
         bool moved = false;
         if (want != entry) {
@@ -288,12 +302,17 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
             exitp = e;
             ex[t] = e;
         }
+        ++rounds;
         if (!__syncthreads_or(moved)) break;
     }
-    // 4. sizes, offsets, tags
+    if (a.stats && t == 0) {
+        atomicAdd(&a.stats[0], rounds);
+        atomicMax(&a.stats[1], rounds);
+    }
+    // 4. sizes, offsets, tags (the walkers); literal bytes (everyone)
     uint32_t out = 0;
-    for (uint32_t m = mask; m; m &= m - 1) {
-        const uint32_t p = lo + (uint32_t)__builtin_ctz(m);
+    for (uint64_t m = mask; m; m &= m - 1) {
+        const uint32_t p = wlo + (uint32_t)__builtin_ctzll(m);
         const uint32_t l = L[p];
         if (l >= 4) {
             out += (l < 12 && p - cand[p] < 2048) ? 2 : 3;
@@ -314,10 +333,11 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         return;
     }
     // (the table is free: the last reads of it were before the barriers above)
-    uint32_t o = hdr + base, runs = 0;
-    for (uint32_t m = mask; m; m &= m - 1) {
-        const uint32_t b = (uint32_t)__builtin_ctz(m);
-        const uint32_t p = lo + b;
+    uint32_t o = hdr + base;
+    uint64_t runs = 0;
+    for (uint64_t m = mask; m; m &= m - 1) {
+        const uint32_t b = (uint32_t)__builtin_ctzll(m);
+        const uint32_t p = wlo + b;
         const uint32_t l = L[p];
         if (l >= 4) {
             const uint32_t off = p - cand[p];
@@ -347,18 +367,24 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
             }
             cand[p] = (uint16_t)o;  // where the run's bytes go (cand is unused at literals)
             o += ll;
-            runs |= 1u << b;
+            runs |= 1ull << b;
         }
     }
     if (t < (int)hdr) stage[t] = (uint8_t)(((n >> (7 * t)) & 0x7f) | (t + 1 < (int)hdr ? 0x80 : 0));
-    // literal bytes: every thread places its own positions; the run in force
-    // at p is the latest run start <= p (a block max-scan of run starts + 1)
+    // the run in force at p: the latest run start <= p (segment masks, and
+    // a block max-scan of each segment's last run start + 1 for the carry)
     uint32_t tot;
-    const uint32_t carry = block_excl_scan(runs ? lo + 32 - (uint32_t)__builtin_clz(runs) : 0u, 0u, OpMax(), wtot, &tot);
+    const uint32_t carry =
+        block_excl_scan(runs ? wlo + 64 - (uint32_t)__builtin_clzll(runs) : 0u, 0u, OpMax(), wtot, &tot);
+    if (walker) {
+        segruns[t] = runs;
+        segcarry[t] = carry;
+    }
+    __syncthreads();
     for (uint32_t p = lo; p < hi; ++p) {
-        const uint32_t b = p - lo;
-        const uint32_t mine = runs & (b == 31 ? 0xFFFFFFFFu : ((2u << b) - 1));
-        const uint32_t r1 = mine ? lo + 32 - (uint32_t)__builtin_clz(mine) : carry;
+        const uint32_t w = p / kWalkSeg, b = p % kWalkSeg;
+        const uint64_t mine = segruns[w] & (b == 63 ? ~0ull : ((2ull << b) - 1));
+        const uint32_t r1 = mine ? w * kWalkSeg + 64 - (uint32_t)__builtin_clzll(mine) : segcarry[w];
         if (r1 == 0) continue;
         const uint32_t r = r1 - 1;
         if (p < NC[r + 1]) stage[cand[r] + (p - r)] = in[p];
@@ -401,9 +427,11 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
         const uint32_t mis = stage_in(pc.src, m, raw, 16);
         const uint8_t* cin = raw + mis;
         __syncthreads();
-        // 1. the element chain over the compressed bytes
-        const uint32_t G = (m + kT - 1) / kT;  // <= 38 for 8 KiB pieces
-        const uint32_t lo = min(m, G * (uint32_t)t), hi = min(m, lo + G);
+        // 1. the element chain over the compressed bytes: speculative walks
+        //    over 64-byte segments, re-walked until the entries agree
+        const uint32_t S = (m + kWalkSeg - 1) / kWalkSeg;  // <= 150 for 8 KiB pieces
+        const bool walker = (uint32_t)t < S;
+        const uint32_t lo = walker ? (uint32_t)t * kWalkSeg : m, hi = walker ? min(m, lo + kWalkSeg) : m;
         auto csize = [&](uint32_t i) -> uint32_t {
             const uint32_t tag = cin[i];
             const uint32_t kind = tag & 3;
@@ -430,11 +458,12 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
             }
             return e;
         };
-        uint32_t exitp = walk(entry);
-        ex[t] = exitp;
+        uint32_t exitp = walker ? walk(entry) : m;
+        if (walker) ex[t] = exitp;
+        uint32_t rounds = 0;
         for (;;) {
             __syncthreads();
-            const uint32_t want = t ? ex[t - 1] : 0u;
+            const uint32_t want = walker ? (t ? ex[t - 1] : 0u) : entry;
             __syncthreads();
             bool moved = false;
             if (want != entry) {
@@ -444,9 +473,14 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
                 exitp = e;
                 ex[t] = e;
             }
+            ++rounds;
             if (!__syncthreads_or(moved)) break;
         }
-        if (t == kT - 1 && exitp != m) bad = 3;  // the chain must end exactly at the piece's end
+        if (a.stats && t == 0) {
+            atomicAdd(&a.stats[2], rounds);
+            atomicMax(&a.stats[3], rounds);
+        }
+        if ((uint32_t)t == S - 1 && exitp != m) bad = 3;  // the chain must end exactly at the piece's end
         // 2. output sizes -> positions; descriptors at element starts
         auto elem = [&](uint32_t i, uint32_t* len, uint32_t* off, uint32_t* lsrc) {
             const uint32_t tag = cin[i];
@@ -480,8 +514,10 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
         }
         uint32_t total;
         uint32_t o = block_excl_scan(outb, 0u, OpSum(), wtot, &total);
-        if (total != n) {
-            if (t == 0) bad = bad ? bad : 4;
+        // (the scan's barriers publish `bad`: a broken chain's sizes are
+        // garbage, so nothing below is written unless the chain is sound)
+        if (bad || total != n) {
+            if (t == 0 && !bad) bad = 4;
         } else {
             for (uint64_t k = mask; k; k &= k - 1) {
                 uint32_t len, off, ls = 0;

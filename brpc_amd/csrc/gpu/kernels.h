@@ -186,6 +186,7 @@ struct FusedCodecArgs {
     int32_t* scan_n = nullptr;
     uint32_t max_fields = 0;
     uint32_t max_ulen = 0;                  // >= every block's and piece's size
+    uint32_t* stats = nullptr;  // optional, 4 device words: compress parse rounds (sum, max), decode (sum, max)
 };
 int LaunchFusedCodec(const FusedCodecArgs& a, hipStream_t s);
 

@@ -8,6 +8,7 @@
 #                refuses ranks that share a GPU), every N>1 leg, small steps
 #   pytest:FILE  one GPU test file (tests/FILE.py)
 #   bench:ARGS   bench.py ARGS (comma-separated), one JSON + a leg summary
+#   run:ARGS     python ARGS (comma-separated), output in run_N.txt
 #   kt:ARGS      rocprofv3 kernel trace of bench.py ARGS (comma-separated)
 # Output lands in gpurun_out/<tag>/ (tag = $TAG, default "run").
 set -u
@@ -15,6 +16,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 T=gpurun_out/${TAG:-run}; mkdir -p $T
 nb=0
+nr=0
 for st in "$@"; do
   case $st in
     tests)
@@ -44,6 +46,10 @@ for st in "$@"; do
       args=${st#bench:}; nb=$((nb+1))
       timeout -k 10 600 python -u bench.py ${args//,/ } > $T/bench_$nb.log 2>&1 || { tail -20 $T/bench_$nb.log; exit 1; }
       grep '^{"metric"' $T/bench_$nb.log > $T/bench_$nb.json; echo "bench_$nb: $args"; python benchmarks/leg_summary.py $T/bench_$nb.json ;;
+    run:*)
+      args=${st#run:}; nr=$((nr+1))
+      timeout -k 10 600 python -u ${args//,/ } > $T/run_$nr.txt 2>&1 || { tail -30 $T/run_$nr.txt; exit 1; }
+      echo "run_$nr: $args"; tail -40 $T/run_$nr.txt ;;
     kt:*)
       args=${st#kt:}
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $T/kt -o kt -- python3 bench.py ${args//,/ } \
