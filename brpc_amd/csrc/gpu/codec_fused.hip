@@ -66,9 +66,7 @@ constexpr int kT = 256;  // threads per workgroup
 constexpr int kWaves = kT / 64;
 constexpr int kTableBits = 12;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr uint32_t kWalkSeg = 64;                            // positions (or compressed bytes) per walk segment
-constexpr uint32_t kCompSegs = kFusedMaxBlock / kWalkSeg;    // 128
-static_assert(kCompSegs <= (uint32_t)kT, "one walker thread per segment");
+
 
 typedef const __attribute__((address_space(1))) uint8_t gbyte_c;
 typedef __attribute__((address_space(1))) uint8_t gbyte;
@@ -190,17 +188,80 @@ __device__ __forceinline__ void store_out(void* dst, const uint8_t* stage, uint3
     }
 }
 
+// ---------------------------------------------------------------- chains
+// The element chain of a block (compress: the greedy parse's element
+// starts; decode: the element boundaries of the compressed bytes) is the
+// orbit of `first` under nx[] (nx[i] > i). Each of the 4 waves walks a
+// contiguous quarter of the positions, window by window: the lanes load
+// nx[] of a 64-position window in one LDS read, and the wave follows the
+// chain through it with v_readlane hops (a scalar dependency of a few
+// cycles, no LDS round trip per element), writing the window's 64-bit mask
+// of element starts. A wave starts at its quarter's first position
+// (speculative); rounds then give every wave its predecessor's exit and
+// re-walk the waves whose entry changed, so after round r the first r + 1
+// quarters are exact (at most 4 rounds; walks from different entries merge
+// within a few elements, so one re-walk is the usual case).
+// marks: one u64 per window; ex: kWaves words. Returns the chain's end (the
+// last wave's exit). rounds (optional) gets the number of rounds.
+__device__ __forceinline__ uint32_t chain_marks(const uint16_t* nx, uint32_t npos, uint64_t* marks, uint32_t* ex,
+                                                uint32_t* rounds_out) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t W = (npos + 63) / 64;
+    const uint32_t per = (W + kWaves - 1) / kWaves;
+    const uint32_t w0 = min(W, per * (uint32_t)wv), w1 = min(W, w0 + per);
+    const uint32_t lo = w0 * 64, hi = min(npos, w1 * 64);
+    auto walk = [&](uint32_t e) -> uint32_t {
+        for (uint32_t w = w0 + (uint32_t)lane; w < w1; w += 64) marks[w] = 0;
+        while (e < hi) {
+            const uint32_t win = e & ~63u;
+            const uint32_t nxl = win + (uint32_t)lane < npos ? nx[win + lane] : npos;
+            uint64_t bits = 0;
+            uint32_t r = e - win;
+            while (r < 64 && win + r < hi) {
+                bits |= 1ull << r;
+                e = (uint32_t)__builtin_amdgcn_readlane((int)nxl, (int)r);
+                r = e - win;  // wraps to a huge value when e left the window
+            }
+            if (lane == 0) marks[win >> 6] = bits;
+        }
+        return e;
+    };
+    uint32_t entry = wv == 0 ? 0u : lo;
+    uint32_t exitp = lo < hi || wv == 0 ? walk(entry) : entry;
+    if (lane == 0) ex[wv] = exitp;
+    uint32_t rounds = 1;
+    for (;;) {
+        __syncthreads();
+        const uint32_t want = wv ? ex[wv - 1] : 0u;
+        __syncthreads();
+        bool moved = false;
+        if (want != entry) {
+            entry = want;
+            const uint32_t e = walk(entry);
+            moved = e != exitp;
+            exitp = e;
+            if (lane == 0) ex[wv] = e;
+        }
+        if (!__syncthreads_or(moved)) break;
+        ++rounds;
+    }
+    if (rounds_out) *rounds_out = rounds;
+    return ex[kWaves - 1];
+}
+
 // ---------------------------------------------------------------- compress
-// LDS: in (C + 96, 16 B of alignment slack + 80 B of zero pad) | L (C) |
-// cand (2C) | NC (2C + 16) | table (16 KiB, later the output stage) |
-// wtot (kWaves) | xch (kT) | ex (kT) | segruns (u64 x kCompSegs) | segcarry
+constexpr uint32_t kCompWins = kFusedMaxBlock / 64;  // 128
+// LDS: in (C + 96: 16 B of alignment slack, 80 B of zero pad) | L (C) |
+// cand (2C) | NX (2C + 16) | table (16 KiB, later the output stage) |
+// mb, wm (u64 x kCompWins) | nz, wsz, wbase, carry (u32 x (kCompWins + 1)) |
+// wtot | xch | ex
 __host__ __device__ constexpr uint32_t CompressLds(uint32_t C) {
-    return (C + 96) + C + 2 * C + (2 * C + 16) + (4u << kTableBits) + 4 * (kWaves + 2 * kT) + 8 + 12 * kCompSegs +
-           64;
+    return (C + 96) + C + 2 * C + (2 * C + 16) + (4u << kTableBits) + 16 * kCompWins + 16 * (kCompWins + 1) +
+           4 * (kWaves + kT + kWaves) + 64;
 }
 
 __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const SnappyJob jb = a.comp[job];
     const uint32_t n = (uint32_t)jb.src_len;
     const uint32_t C = (a.max_ulen + 15) & ~15u;
@@ -214,27 +275,36 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     uint8_t* raw = lds;
     uint8_t* L = raw + C + 96;
     uint16_t* cand = reinterpret_cast<uint16_t*>(L + C);
-    uint16_t* NC = cand + C;
-    uint32_t* table = reinterpret_cast<uint32_t*>(NC + C + 8);
+    uint16_t* NX = cand + C;
+    uint32_t* table = reinterpret_cast<uint32_t*>(NX + C + 8);
     uint8_t* stage = reinterpret_cast<uint8_t*>(table);
-    uint32_t* wtot = table + (1u << kTableBits);
+    uint64_t* mb = reinterpret_cast<uint64_t*>(table + (1u << kTableBits));  // match-position bits per window
+    uint64_t* wm = mb + kCompWins;                                            // element starts per window
+    uint32_t* nz = reinterpret_cast<uint32_t*>(wm + kCompWins);               // next window with a match
+    uint32_t* wsz = nz + kCompWins + 1;
+    uint32_t* wbase = wsz + kCompWins + 1;
+    uint32_t* carry = wbase + kCompWins + 1;
+    uint32_t* wtot = carry + kCompWins + 1;
     uint32_t* xch = wtot + kWaves;
     uint32_t* ex = xch + kT;
-    uint64_t* segruns = reinterpret_cast<uint64_t*>(ex + kT + 2);  // 8-byte aligned: 6C + 112 + 16 KiB + 4 * (516 + 2)
-    uint32_t* segcarry = reinterpret_cast<uint32_t*>(segruns + kCompSegs);
+    const uint32_t W = (n + 63) / 64;
 
     for (uint32_t i = t; i < (1u << kTableBits); i += kT) table[i] = kNone;
     const uint32_t mis = stage_in(jb.src, n, raw, 80);
     const uint8_t* in = raw + mis;
-    const uint32_t G = (n + kT - 1) / kT;  // segment = the thread's positions, <= 32
-    const uint32_t lo = min(n, G * (uint32_t)t), hi = min(n, lo + G);
     __syncthreads();
-    // 1. earliest position of every hash
-    for (uint32_t p = lo; p < hi && p + 4 <= n; ++p) atomicMin(&table[hash4(rd32(raw, mis + p))], p);
+    // 1. earliest position of every hash (interleaved positions; a hash
+    //    already holding an earlier position skips its atomic, so a long run
+    //    of one repeated key costs one round of contended atomics, not n)
+    for (uint32_t p = t; p + 4 <= n; p += kT) {
+        uint32_t* e = &table[hash4(rd32(raw, mis + p))];
+        if (*e > p) atomicMin(e, p);
+    }
     __syncthreads();
-    // 2. candidates and match lengths (<= 64, one copy element)
-    uint32_t first = n;
-    for (uint32_t p = lo; p < hi; ++p) {
+    // 2. candidate and match length (<= 64: one copy element) per position;
+    //    the wave's ballot is the window's match mask
+    for (uint32_t base = 0; base < W * 64; base += kT) {
+        const uint32_t p = base + (uint32_t)t;
         uint32_t l = 0, c = 0;
         if (p + 4 <= n) {
             const uint32_t key = rd32(raw, mis + p);
@@ -254,76 +324,63 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
                 c = cp;
             }
         }
-        L[p] = (uint8_t)l;
-        cand[p] = (uint16_t)c;
-        if (l >= 4 && first == n) first = p;
-    }
-    // NC[p]: the first match position >= p (n: none)
-    {
-        uint32_t carry = block_excl_suffix(first, n, OpMin(), wtot, xch);
-        for (uint32_t p = hi; p-- > lo;) {
-            if (L[p] >= 4) carry = p;
-            NC[p] = (uint16_t)carry;
+        if (p < n) {
+            L[p] = (uint8_t)l;
+            cand[p] = (uint16_t)c;
         }
-        if (t == 0) NC[n] = (uint16_t)n;
+        const uint64_t m = __ballot(l >= 4);
+        const uint32_t w = (base >> 6) + (uint32_t)wv;
+        if (lane == 0 && w < W) mb[w] = m;
     }
     __syncthreads();
-    // 3. the greedy parse: speculative walks over 64-position segments (one
-    //    thread each), re-walked until every segment's entry is its
-    //    predecessor's exit. A segment this long holds several elements, so
-    //    walks from different entries meet inside it and the corrections
-    //    stop after a few rounds instead of crawling one segment per round.
-    const uint32_t S = (n + kWalkSeg - 1) / kWalkSeg;
-    const bool walker = (uint32_t)t < S;
-    const uint32_t wlo = walker ? (uint32_t)t * kWalkSeg : n, whi = walker ? min(n, wlo + kWalkSeg) : n;
-    uint32_t entry = wlo;
-    uint64_t mask = 0;
-    auto walk = [&](uint32_t e) -> uint32_t {
-        mask = 0;
-        while (e < whi) {
-            mask |= 1ull << (e - wlo);
-            const uint32_t l = L[e];
-            e = l >= 4 ? e + l : NC[e + 1];
-        }
-        return e;
-    };
-    uint32_t exitp = walker ? walk(entry) : n;
-    if (walker) ex[t] = exitp;
-    uint32_t rounds = 0;
-    for (;;) {
-        __syncthreads();
-        const uint32_t want = walker ? (t ? ex[t - 1] : 0u) : entry;
-        __syncthreads();
-        bool moved = false;
-        if (want != entry) {
-            entry = want;
-            const uint32_t e = walk(entry);
-            moved = e != exitp;
-            exitp = e;
-            ex[t] = e;
-        }
-        ++rounds;
-        if (!__syncthreads_or(moved)) break;
+    // nz[w]: the first window >= w with a match (W: none)
+    {
+        const uint32_t v = (uint32_t)t < W ? (mb[t] ? (uint32_t)t : W) : W;
+        const uint32_t r = min(v, block_excl_suffix(v, W, OpMin(), wtot, xch));
+        if ((uint32_t)t <= W) nz[t] = (uint32_t)t < W ? r : W;
     }
+    __syncthreads();
+    // the parse's successor: a copy jumps over its match, a literal runs to
+    // the next match position (NC)
+    auto next_match = [&](uint32_t q) -> uint32_t {
+        if (q >= n) return n;
+        const uint32_t w = q >> 6;
+        const uint64_t m = mb[w] >> (q & 63);
+        if (m) return q + (uint32_t)__builtin_ctzll(m);
+        const uint32_t w2 = nz[w + 1];
+        return w2 < W ? w2 * 64 + (uint32_t)__builtin_ctzll(mb[w2]) : n;
+    };
+    for (uint32_t p = t; p < n; p += kT) {
+        const uint32_t l = L[p];
+        NX[p] = (uint16_t)(l >= 4 ? p + l : next_match(p + 1));
+    }
+    __syncthreads();
+    // 3. the greedy parse
+    uint32_t rounds = 0;
+    chain_marks(NX, n, wm, ex, &rounds);
     if (a.stats && t == 0) {
         atomicAdd(&a.stats[0], rounds);
         atomicMax(&a.stats[1], rounds);
     }
-    // 4. sizes, offsets, tags (the walkers); literal bytes (everyone)
-    uint32_t out = 0;
-    for (uint64_t m = mask; m; m &= m - 1) {
-        const uint32_t p = wlo + (uint32_t)__builtin_ctzll(m);
+    // 4. element sizes per window (lane = position), window offsets
+    auto elem_size = [&](uint32_t p, bool st) -> uint32_t {
+        if (!st) return 0;
         const uint32_t l = L[p];
-        if (l >= 4) {
-            out += (l < 12 && p - cand[p] < 2048) ? 2 : 3;
-        } else {
-            const uint32_t ll = NC[p + 1] - p;
-            out += lit_tag_bytes(ll) + ll;
-        }
+        if (l >= 4) return (l < 12 && p - cand[p] < 2048) ? 2 : 3;
+        const uint32_t ll = NX[p] - p;
+        return lit_tag_bytes(ll) + ll;
+    };
+    for (uint32_t k = (uint32_t)wv; k < W; k += kWaves) {
+        const uint32_t p = k * 64 + (uint32_t)lane;
+        const bool st = p < n && ((wm[k] >> lane) & 1);
+        const uint32_t incl = wave_incl_scan(elem_size(p, st), OpSum());
+        if (lane == 63) wsz[k] = incl;
     }
+    __syncthreads();
     uint32_t body;
-    const uint32_t base = block_excl_scan(out, 0u, OpSum(), wtot, &body);
     const uint32_t hdr = varint_len(n);
+    const uint32_t wb = block_excl_scan((uint32_t)t < W ? wsz[t] : 0u, 0u, OpSum(), wtot, &body);
+    if ((uint32_t)t < W) wbase[t] = hdr + wb;
     const uint32_t total = hdr + body;
     if (total > jb.dst_cap || total > (4u << kTableBits)) {  // block-uniform
         if (t == 0) {
@@ -332,62 +389,62 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         }
         return;
     }
-    // (the table is free: the last reads of it were before the barriers above)
-    uint32_t o = hdr + base;
-    uint64_t runs = 0;
-    for (uint64_t m = mask; m; m &= m - 1) {
-        const uint32_t b = (uint32_t)__builtin_ctzll(m);
-        const uint32_t p = wlo + b;
+    // (the table is free: its last reads were before the barriers above)
+    {
+        // latest literal-run start + 1 before each window (0: none)
+        const uint64_t rb = (uint32_t)t < W ? wm[t] & ~mb[t] : 0;
+        const uint32_t v = rb ? (uint32_t)t * 64 + 64 - (uint32_t)__builtin_clzll(rb) : 0u;
+        uint32_t tot;
+        const uint32_t c = block_excl_scan(v, 0u, OpMax(), wtot, &tot);
+        if ((uint32_t)t < W) carry[t] = c;
+    }
+    // 5. tags: every element start's lane writes its tag at its offset
+    for (uint32_t k = (uint32_t)wv; k < W; k += kWaves) {
+        const uint32_t p = k * 64 + (uint32_t)lane;
+        const bool st = p < n && ((wm[k] >> lane) & 1);
+        const uint32_t sz = elem_size(p, st);
+        const uint32_t o = wbase[k] + wave_incl_scan(sz, OpSum()) - sz;
+        if (!st) continue;
         const uint32_t l = L[p];
         if (l >= 4) {
             const uint32_t off = p - cand[p];
             if (l < 12 && off < 2048) {
                 stage[o] = (uint8_t)(((off >> 8) << 5) | ((l - 4) << 2) | 1);
                 stage[o + 1] = (uint8_t)off;
-                o += 2;
             } else {
                 stage[o] = (uint8_t)(((l - 1) << 2) | 2);
                 stage[o + 1] = (uint8_t)off;
                 stage[o + 2] = (uint8_t)(off >> 8);
-                o += 3;
             }
         } else {
-            const uint32_t ll = NC[p + 1] - p, v = ll - 1;
+            const uint32_t ll = NX[p] - p, v = ll - 1;
+            uint32_t h = 1;
             if (ll <= 60) {
-                stage[o++] = (uint8_t)(v << 2);
+                stage[o] = (uint8_t)(v << 2);
             } else if (ll <= 256) {
                 stage[o] = 60 << 2;
                 stage[o + 1] = (uint8_t)v;
-                o += 2;
+                h = 2;
             } else {
                 stage[o] = 61 << 2;
                 stage[o + 1] = (uint8_t)v;
                 stage[o + 2] = (uint8_t)(v >> 8);
-                o += 3;
+                h = 3;
             }
-            cand[p] = (uint16_t)o;  // where the run's bytes go (cand is unused at literals)
-            o += ll;
-            runs |= 1ull << b;
+            cand[p] = (uint16_t)(o + h);  // where the run's bytes go (cand is unused at literals)
         }
     }
     if (t < (int)hdr) stage[t] = (uint8_t)(((n >> (7 * t)) & 0x7f) | (t + 1 < (int)hdr ? 0x80 : 0));
-    // the run in force at p: the latest run start <= p (segment masks, and
-    // a block max-scan of each segment's last run start + 1 for the carry)
-    uint32_t tot;
-    const uint32_t carry =
-        block_excl_scan(runs ? wlo + 64 - (uint32_t)__builtin_clzll(runs) : 0u, 0u, OpMax(), wtot, &tot);
-    if (walker) {
-        segruns[t] = runs;
-        segcarry[t] = carry;
-    }
     __syncthreads();
-    for (uint32_t p = lo; p < hi; ++p) {
-        const uint32_t w = p / kWalkSeg, b = p % kWalkSeg;
-        const uint64_t mine = segruns[w] & (b == 63 ? ~0ull : ((2ull << b) - 1));
-        const uint32_t r1 = mine ? w * kWalkSeg + 64 - (uint32_t)__builtin_clzll(mine) : segcarry[w];
+    // 6. literal bytes, one position per lane: the run in force at p is the
+    //    latest literal-run start <= p
+    for (uint32_t p = t; p < n; p += kT) {
+        const uint32_t w = p >> 6, b = p & 63;
+        const uint64_t rb = wm[w] & ~mb[w] & (b == 63 ? ~0ull : ((2ull << b) - 1));
+        const uint32_t r1 = rb ? w * 64 + 64 - (uint32_t)__builtin_clzll(rb) : carry[w];
         if (r1 == 0) continue;
         const uint32_t r = r1 - 1;
-        if (p < NC[r + 1]) stage[cand[r] + (p - r)] = in[p];
+        if (p < NX[r]) stage[cand[r] + (p - r)] = in[p];
     }
     __syncthreads();
     store_out(jb.dst, stage, total);
@@ -398,191 +455,181 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
 }
 
 // ---------------------------------------------------------------- decode
-// LDS: cin (cap + 32 + 96) | desc (2C) | src (2C) | sbits (C/8 + 16) |
-// wtot | xch | ex (u32 x kT, exits as u32) | flag
+constexpr uint32_t kDecWins = (uint32_t)((SnappyMaxCompressedLength(kFusedMaxBlock) + 63) / 64);  // 150
 __host__ __device__ constexpr uint32_t DecodeCinCap(uint32_t C) {
     return (uint32_t)((SnappyMaxCompressedLength(C) + 15) & ~15ull);
 }
+// LDS: cin (cap + 128) | NX (2 x (cap + 16)) | desc (2C) | src (2C) |
+// cm (u64 x kDecWins) | sb (u64 x kCompWins) | wsz, wbase (u32 x kDecWins) |
+// ocarry (u32 x kCompWins) | wtot | xch | ex
 __host__ __device__ constexpr uint32_t DecodeLds(uint32_t C) {
-    return DecodeCinCap(C) + 128 + 2 * C + 2 * C + (C / 8 + 16) + 4 * (kWaves + 2 * kT) + 64;
+    return DecodeCinCap(C) + 128 + 2 * (DecodeCinCap(C) + 16) + 2 * C + 2 * C + 8 * kDecWins + 8 * kCompWins +
+           8 * kDecWins + 4 * kCompWins + 4 * (kWaves + kT + kWaves) + 64;
 }
 
 __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const SnappyPiece pc = a.pieces[job];
     const uint32_t C = (a.max_ulen + 15) & ~15u;
+    const uint32_t cap = DecodeCinCap(C);
     const uint32_t m = pc.src_len, n = pc.ulen;
     uint8_t* raw = lds;
-    uint16_t* desc = reinterpret_cast<uint16_t*>(raw + DecodeCinCap(C) + 128);
+    uint16_t* NX = reinterpret_cast<uint16_t*>(raw + cap + 128);
+    uint16_t* desc = NX + cap + 16;
     uint16_t* src = desc + C;
-    uint32_t* sbits = reinterpret_cast<uint32_t*>(src + C);
-    uint32_t* wtot = sbits + C / 32 + 4;
+    uint64_t* cm = reinterpret_cast<uint64_t*>(src + C);  // element starts per compressed window
+    uint64_t* sb = cm + kDecWins;                          // element starts per output window
+    uint32_t* wsz = reinterpret_cast<uint32_t*>(sb + kCompWins);
+    uint32_t* wbase = wsz + kDecWins;
+    uint32_t* ocarry = wbase + kDecWins;
+    uint32_t* wtot = ocarry + kCompWins;
     uint32_t* xch = wtot + kWaves;
     uint32_t* ex = xch + kT;
     __shared__ int bad;
     if (t == 0) bad = 0;
-    const bool fits = n <= a.max_ulen && m <= DecodeCinCap(C) && n > 0 && m > 0;
+    const bool fits = n <= a.max_ulen && m <= cap && n > 0 && m > 0;
     if (fits) {
-        for (uint32_t i = t; i < C / 32 + 1; i += kT) sbits[i] = 0;
+        const uint32_t Wc = (m + 63) / 64, Wo = (n + 63) / 64;
+        for (uint32_t i = t; i < Wo; i += kT) sb[i] = 0;
         const uint32_t mis = stage_in(pc.src, m, raw, 16);
         const uint8_t* cin = raw + mis;
         __syncthreads();
-        // 1. the element chain over the compressed bytes: speculative walks
-        //    over 64-byte segments, re-walked until the entries agree
-        const uint32_t S = (m + kWalkSeg - 1) / kWalkSeg;  // <= 150 for 8 KiB pieces
-        const bool walker = (uint32_t)t < S;
-        const uint32_t lo = walker ? (uint32_t)t * kWalkSeg : m, hi = walker ? min(m, lo + kWalkSeg) : m;
-        auto csize = [&](uint32_t i) -> uint32_t {
+        // 1. every compressed position's element size as if an element
+        //    started there; the chain from position 0 keeps the true ones
+        //    (a size running past the piece saturates at m + 1)
+        auto elem = [&](uint32_t i, uint32_t* len, uint32_t* off, uint32_t* lsrc) -> uint32_t {
             const uint32_t tag = cin[i];
             const uint32_t kind = tag & 3;
-            if (kind == 1) return 2;
-            if (kind == 2) return 3;
-            if (kind == 3) return 5;
-            uint32_t len = (tag >> 2) + 1, h = 1;
-            if (len > 60) {
-                const uint32_t nb = len - 60;
-                const uint32_t raw_len = rd32(raw, mis + i + 1) & (0xFFFFFFFFu >> (32 - 8 * nb));
-                if (raw_len >= 0x7FFF0000u) return 0x7FFF0000u;  // far past any piece
-                len = raw_len + 1;
-                h += nb;
-            }
-            return h + len;
-        };
-        uint64_t mask = 0;
-        uint32_t entry = lo;
-        auto walk = [&](uint32_t e) -> uint32_t {
-            mask = 0;
-            while (e < hi) {
-                mask |= 1ull << (e - lo);
-                e = min(e + csize(e), 0x7FFF0000u);
-            }
-            return e;
-        };
-        uint32_t exitp = walker ? walk(entry) : m;
-        if (walker) ex[t] = exitp;
-        uint32_t rounds = 0;
-        for (;;) {
-            __syncthreads();
-            const uint32_t want = walker ? (t ? ex[t - 1] : 0u) : entry;
-            __syncthreads();
-            bool moved = false;
-            if (want != entry) {
-                entry = want;
-                const uint32_t e = walk(entry);
-                moved = e != exitp;
-                exitp = e;
-                ex[t] = e;
-            }
-            ++rounds;
-            if (!__syncthreads_or(moved)) break;
-        }
-        if (a.stats && t == 0) {
-            atomicAdd(&a.stats[2], rounds);
-            atomicMax(&a.stats[3], rounds);
-        }
-        if ((uint32_t)t == S - 1 && exitp != m) bad = 3;  // the chain must end exactly at the piece's end
-        // 2. output sizes -> positions; descriptors at element starts
-        auto elem = [&](uint32_t i, uint32_t* len, uint32_t* off, uint32_t* lsrc) {
-            const uint32_t tag = cin[i];
-            const uint32_t kind = tag & 3;
+            *off = 0;
+            *lsrc = 0;
             if (kind == 0) {
                 uint32_t l = (tag >> 2) + 1, h = 1;
                 if (l > 60) {
                     const uint32_t nb = l - 60;
-                    l = (rd32(raw, mis + i + 1) & (0xFFFFFFFFu >> (32 - 8 * nb))) + 1;
+                    const uint32_t r = rd32(raw, mis + i + 1) & (0xFFFFFFFFu >> (32 - 8 * nb));
+                    l = r >= 0x7FFF0000u ? 0x7FFF0000u : r + 1;
                     h += nb;
                 }
                 *len = l;
-                *off = 0;
                 *lsrc = i + h;
-            } else if (kind == 1) {
+                return h + l;
+            }
+            if (kind == 1) {
                 *len = ((tag >> 2) & 7) + 4;
                 *off = ((tag >> 5) << 8) | cin[i + 1];
-            } else if (kind == 2) {
-                *len = (tag >> 2) + 1;
-                *off = cin[i + 1] | ((uint32_t)cin[i + 2] << 8);
-            } else {
-                *len = (tag >> 2) + 1;
-                *off = rd32(raw, mis + i + 1);
+                return 2;
             }
+            *len = (tag >> 2) + 1;
+            if (kind == 2) {
+                *off = cin[i + 1] | ((uint32_t)cin[i + 2] << 8);
+                return 3;
+            }
+            *off = rd32(raw, mis + i + 1);
+            return 5;
         };
-        uint32_t outb = 0;
-        for (uint64_t k = mask; k; k &= k - 1) {
-            uint32_t len, off, ls = 0;
-            elem(lo + (uint32_t)__builtin_ctzll(k), &len, &off, &ls);
-            outb = min(outb + len, 0x7FFF0000u);
+        for (uint32_t i = t; i < m; i += kT) {
+            uint32_t len, off, ls;
+            const uint32_t cs = elem(i, &len, &off, &ls);
+            NX[i] = (uint16_t)min(i + cs, m + 1);
         }
-        uint32_t total;
-        uint32_t o = block_excl_scan(outb, 0u, OpSum(), wtot, &total);
-        // (the scan's barriers publish `bad`: a broken chain's sizes are
-        // garbage, so nothing below is written unless the chain is sound)
-        if (bad || total != n) {
-            if (t == 0 && !bad) bad = 4;
+        __syncthreads();
+        uint32_t rounds = 0;
+        const uint32_t end = chain_marks(NX, m, cm, ex, &rounds);
+        if (a.stats && t == 0) {
+            atomicAdd(&a.stats[2], rounds);
+            atomicMax(&a.stats[3], rounds);
+        }
+        if (end != m) {
+            if (t == 0) bad = 3;  // the chain does not end at the piece's end
         } else {
-            for (uint64_t k = mask; k; k &= k - 1) {
-                uint32_t len, off, ls = 0;
-                const uint32_t i = lo + (uint32_t)__builtin_ctzll(k);
-                elem(i, &len, &off, &ls);
-                if (off == 0 && (cin[i] & 3) == 0) {
-                    desc[o] = (uint16_t)(0x8000u | ls);
-                } else if (off == 0 || off > o) {
-                    atomicOr(&bad, 6);  // a copy from before the piece
-                    desc[o] = 0x8000u;
-                } else {
-                    desc[o] = (uint16_t)off;
+            // 2. output lengths per compressed window (lane = position)
+            for (uint32_t k = (uint32_t)wv; k < Wc; k += kWaves) {
+                const uint32_t i = k * 64 + (uint32_t)lane;
+                uint32_t len = 0, off, ls;
+                if (i < m && ((cm[k] >> lane) & 1)) elem(i, &len, &off, &ls);
+                const uint32_t incl = wave_incl_scan(len, OpSum());  // a sound chain's lengths fit
+                if (lane == 63) wsz[k] = incl;
+            }
+        }
+        __syncthreads();  // (publishes `bad`)
+        if (!bad) {
+            uint32_t total;
+            const uint32_t wb = block_excl_scan((uint32_t)t < Wc ? wsz[t] : 0u, 0u, OpSum(), wtot, &total);
+            if ((uint32_t)t < Wc) wbase[t] = wb;
+            if (total != n) {
+                if (t == 0) bad = 4;
+            } else {
+                __syncthreads();
+                // descriptors at element starts: a literal's source in the
+                // piece, or a copy's offset
+                for (uint32_t k = (uint32_t)wv; k < Wc; k += kWaves) {
+                    const uint32_t i = k * 64 + (uint32_t)lane;
+                    uint32_t len = 0, off = 0, ls = 0;
+                    const bool st = i < m && ((cm[k] >> lane) & 1);
+                    if (st) elem(i, &len, &off, &ls);
+                    const uint32_t o = wbase[k] + wave_incl_scan(len, OpSum()) - len;
+                    if (!st) continue;
+                    if ((cin[i] & 3) == 0) {
+                        desc[o] = (uint16_t)(0x8000u | ls);
+                    } else if (off == 0 || off > o) {
+                        atomicOr(&bad, 6);  // a copy from before the piece
+                        desc[o] = 0x8000u;
+                    } else {
+                        desc[o] = (uint16_t)off;
+                    }
+                    atomicOr(reinterpret_cast<uint32_t*>(sb) + (o >> 5), 1u << (o & 31));
                 }
-                atomicOr(&sbits[o >> 5], 1u << (o & 31));
-                o += len;
             }
         }
         __syncthreads();
-        if (bad == 0) {
-            // every output byte's element: the latest start <= it (thread t
-            // owns output word t: bytes [32t, 32t + 32))
-            const uint32_t ob = 32u * (uint32_t)t, oe = min(n, ob + 32);
-            const uint32_t bits = ob < n ? sbits[t] : 0u;
-            uint32_t tot;
-            const uint32_t carry =
-                block_excl_scan(bits ? ob + 32 - (uint32_t)__builtin_clz(bits) : 0u, 0u, OpMax(), wtot, &tot);
-            for (uint32_t q = ob; q < oe; ++q) {
-                const uint32_t b = q - ob;
-                const uint32_t mine = bits & (b == 31 ? 0xFFFFFFFFu : ((2u << b) - 1));
-                const uint32_t s = (mine ? ob + 32 - (uint32_t)__builtin_clz(mine) : carry) - 1;
-                const uint32_t d = desc[s];
-                src[q] = (uint16_t)((d & 0x8000u) ? (0x8000u | ((d & 0x7FFFu) + (q - s))) : (q - d));
+        if (!bad) {
+            {
+                // latest element start + 1 before each output window
+                const uint64_t bits = (uint32_t)t < Wo ? sb[t] : 0;
+                const uint32_t v = bits ? (uint32_t)t * 64 + 64 - (uint32_t)__builtin_clzll(bits) : 0u;
+                uint32_t tot;
+                const uint32_t c = block_excl_scan(v, 0u, OpMax(), wtot, &tot);
+                if ((uint32_t)t < Wo) ocarry[t] = c;
             }
             __syncthreads();
-            // 3. pointer jumping: every copy byte ends at a literal byte
+            // 3. source map: every output byte's literal byte, or an earlier
+            //    output byte (4 consecutive bytes per thread, interleaved)
+            for (uint32_t q0 = (uint32_t)t * 4; q0 < n; q0 += kT * 4) {
+                for (uint32_t q = q0; q < q0 + 4 && q < n; ++q) {
+                    const uint32_t w = q >> 6, b = q & 63;
+                    const uint64_t mine = sb[w] & (b == 63 ? ~0ull : ((2ull << b) - 1));
+                    const uint32_t s = (mine ? w * 64 + 64 - (uint32_t)__builtin_clzll(mine) : ocarry[w]) - 1;
+                    const uint32_t d = desc[s];
+                    src[q] = (uint16_t)((d & 0x8000u) ? (0x8000u | ((d & 0x7FFFu) + (q - s))) : (q - d));
+                }
+            }
+            __syncthreads();
+            // pointer jumping: every copy byte ends at a literal byte
             for (;;) {
                 bool more = false;
-                for (uint32_t q = ob; q < oe; ++q) {
-                    const uint32_t v = src[q];
-                    if (!(v & 0x8000u)) {
-                        const uint32_t w = src[v];
-                        src[q] = (uint16_t)w;
-                        more |= !(w & 0x8000u);
+                for (uint32_t q0 = (uint32_t)t * 4; q0 < n; q0 += kT * 4) {
+                    for (uint32_t q = q0; q < q0 + 4 && q < n; ++q) {
+                        const uint32_t v = src[q];
+                        if (!(v & 0x8000u)) {
+                            const uint32_t w = src[v];
+                            src[q] = (uint16_t)w;
+                            more |= !(w & 0x8000u);
+                        }
                     }
                 }
                 if (!__syncthreads_or(more)) break;
             }
-            // gather: one 32-byte run of the output per thread
-            if (ob < n) {
-                gbyte* d = (gbyte*)pc.dst + ob;
-                const uint32_t cnt = oe - ob;
-                if (cnt == 32 && (reinterpret_cast<uintptr_t>(pc.dst) & 15) == 0) {
-                    uint32_t w[8];
+            // gather + store, 4 bytes per thread and store
+            gbyte* d = (gbyte*)pc.dst;
+            const bool al = (reinterpret_cast<uintptr_t>(pc.dst) & 3) == 0;
+            for (uint32_t q0 = (uint32_t)t * 4; q0 < n; q0 += kT * 4) {
+                if (al && q0 + 4 <= n) {
+                    uint32_t x = 0;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        uint32_t x = 0;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) x |= (uint32_t)cin[src[ob + 4 * k + j] & 0x7FFFu] << (8 * j);
-                        w[k] = x;
-                    }
-                    auto* dv = reinterpret_cast<__attribute__((address_space(1))) u32x4*>(d);
-                    dv[0] = u32x4{w[0], w[1], w[2], w[3]};
-                    dv[1] = u32x4{w[4], w[5], w[6], w[7]};
+                    for (int j = 0; j < 4; ++j) x |= (uint32_t)cin[src[q0 + j] & 0x7FFFu] << (8 * j);
+                    *reinterpret_cast<__attribute__((address_space(1))) uint32_t*>(d + q0) = x;
                 } else {
-                    for (uint32_t q = 0; q < cnt; ++q) d[q] = cin[src[ob + q] & 0x7FFFu];
+                    for (uint32_t q = q0; q < q0 + 4 && q < n; ++q) d[q] = cin[src[q] & 0x7FFFu];
                 }
             }
         }
