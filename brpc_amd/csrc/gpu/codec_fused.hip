@@ -188,6 +188,23 @@ __device__ __forceinline__ void store_out(void* dst, const uint8_t* stage, uint3
     }
 }
 
+// Phase stamps (shader clock, cumulative since the workgroup started) of
+// the first compress block and the first decode piece, into stats[4..] and
+// stats[16..] (benchmarks/fused_codec_ab.py prints them per phase).
+struct Stamper {
+    uint32_t* st = nullptr;
+    uint64_t t0 = 0;
+    __device__ Stamper(uint32_t* stats, bool first, int base) {
+        if (stats && first && threadIdx.x == 0) {
+            st = stats + base;
+            t0 = __builtin_amdgcn_s_memtime();
+        }
+    }
+    __device__ void operator()(int k) const {
+        if (st) st[k] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
+    }
+};
+
 // ---------------------------------------------------------------- chains
 // The element chain of a block (compress: the greedy parse's element
 // starts; decode: the element boundaries of the compressed bytes) is the
@@ -289,10 +306,12 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     uint32_t* ex = xch + kT;
     const uint32_t W = (n + 63) / 64;
 
+    const Stamper stamp(a.stats, job == 0, 4);
     for (uint32_t i = t; i < (1u << kTableBits); i += kT) table[i] = kNone;
     const uint32_t mis = stage_in(jb.src, n, raw, 80);
     const uint8_t* in = raw + mis;
     __syncthreads();
+    stamp(0);
     // 1. earliest position of every hash (interleaved positions; a hash
     //    already holding an earlier position skips its atomic, so a long run
     //    of one repeated key costs one round of contended atomics, not n)
@@ -301,6 +320,7 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         if (*e > p) atomicMin(e, p);
     }
     __syncthreads();
+    stamp(1);
     // 2. candidate and match length (<= 64: one copy element) per position;
     //    the wave's ballot is the window's match mask
     for (uint32_t base = 0; base < W * 64; base += kT) {
@@ -333,6 +353,7 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         if (lane == 0 && w < W) mb[w] = m;
     }
     __syncthreads();
+    stamp(2);
     // nz[w]: the first window >= w with a match (W: none)
     {
         const uint32_t v = (uint32_t)t < W ? (mb[t] ? (uint32_t)t : W) : W;
@@ -355,9 +376,11 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         NX[p] = (uint16_t)(l >= 4 ? p + l : next_match(p + 1));
     }
     __syncthreads();
+    stamp(3);
     // 3. the greedy parse
     uint32_t rounds = 0;
     chain_marks(NX, n, wm, ex, &rounds);
+    stamp(4);
     if (a.stats && t == 0) {
         atomicAdd(&a.stats[0], rounds);
         atomicMax(&a.stats[1], rounds);
@@ -382,6 +405,7 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     const uint32_t wb = block_excl_scan((uint32_t)t < W ? wsz[t] : 0u, 0u, OpSum(), wtot, &body);
     if ((uint32_t)t < W) wbase[t] = hdr + wb;
     const uint32_t total = hdr + body;
+    stamp(5);
     if (total > jb.dst_cap || total > (4u << kTableBits)) {  // block-uniform
         if (t == 0) {
             a.comp_err[job] = 2;
@@ -436,6 +460,7 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     }
     if (t < (int)hdr) stage[t] = (uint8_t)(((n >> (7 * t)) & 0x7f) | (t + 1 < (int)hdr ? 0x80 : 0));
     __syncthreads();
+    stamp(6);
     // 6. literal bytes, one position per lane: the run in force at p is the
     //    latest literal-run start <= p
     for (uint32_t p = t; p < n; p += kT) {
@@ -447,7 +472,9 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         if (p < NX[r]) stage[cand[r] + (p - r)] = in[p];
     }
     __syncthreads();
+    stamp(7);
     store_out(jb.dst, stage, total);
+    stamp(8);
     if (t == 0) {
         a.comp_len[job] = total;
         a.comp_err[job] = 0;
@@ -491,9 +518,11 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
     if (fits) {
         const uint32_t Wc = (m + 63) / 64, Wo = (n + 63) / 64;
         for (uint32_t i = t; i < Wo; i += kT) sb[i] = 0;
+        const Stamper stamp(a.stats, job == 0, 16);
         const uint32_t mis = stage_in(pc.src, m, raw, 16);
         const uint8_t* cin = raw + mis;
         __syncthreads();
+        stamp(0);
         // 1. every compressed position's element size as if an element
         //    started there; the chain from position 0 keeps the true ones
         //    (a size running past the piece saturates at m + 1)
@@ -533,8 +562,10 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
             NX[i] = (uint16_t)min(i + cs, m + 1);
         }
         __syncthreads();
+        stamp(1);
         uint32_t rounds = 0;
         const uint32_t end = chain_marks(NX, m, cm, ex, &rounds);
+        stamp(2);
         if (a.stats && t == 0) {
             atomicAdd(&a.stats[2], rounds);
             atomicMax(&a.stats[3], rounds);
@@ -552,6 +583,7 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
             }
         }
         __syncthreads();  // (publishes `bad`)
+        stamp(3);
         if (!bad) {
             uint32_t total;
             const uint32_t wb = block_excl_scan((uint32_t)t < Wc ? wsz[t] : 0u, 0u, OpSum(), wtot, &total);
@@ -592,6 +624,7 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
                 if ((uint32_t)t < Wo) ocarry[t] = c;
             }
             __syncthreads();
+            stamp(5);
             // 3. source map: every output byte's literal byte, or an earlier
             //    output byte (4 consecutive bytes per thread, interleaved)
             for (uint32_t q0 = (uint32_t)t * 4; q0 < n; q0 += kT * 4) {
@@ -604,6 +637,7 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
                 }
             }
             __syncthreads();
+            stamp(6);
             // pointer jumping: every copy byte ends at a literal byte
             for (;;) {
                 bool more = false;
@@ -619,6 +653,7 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
                 }
                 if (!__syncthreads_or(more)) break;
             }
+            stamp(7);
             // gather + store, 4 bytes per thread and store
             gbyte* d = (gbyte*)pc.dst;
             const bool al = (reinterpret_cast<uintptr_t>(pc.dst) & 3) == 0;
@@ -632,6 +667,7 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
                     for (uint32_t q = q0; q < q0 + 4 && q < n; ++q) d[q] = cin[src[q] & 0x7FFFu];
                 }
             }
+            stamp(8);
         }
     }
     __syncthreads();

@@ -210,7 +210,7 @@ void bind_gpu_ops(py::module_& g) {
             hipStream_t s = nullptr;
             hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
             const size_t cap = (gpu::SnappyMaxCompressedLength(block) + 15) & ~(size_t)15;
-            DevBuf src(all.size()), dst(all.size() + 16), cmp(cap * n), cmp2(cap * n), stats(16), scratch(16);
+            DevBuf src(all.size()), dst(all.size() + 16), cmp(cap * n), cmp2(cap * n), stats(128), scratch(16);
             DevBuf jobs(sizeof(gpu::SnappyJob) * n), pieces(sizeof(gpu::SnappyPiece) * n), lens(4 * n), errs(4 * n),
                 perr(4 * n), lens2(4 * n), errs2(4 * n);
             hipMemcpy(src.p, all.data(), all.size(), hipMemcpyHostToDevice);
@@ -220,7 +220,7 @@ void bind_gpu_ops(py::module_& g) {
                 hj2[i] = gpu::SnappyJob{src.as<char>() + blocks[i].first, cmp2.as<char>() + cap * i, blocks[i].second, cap};
             }
             hipMemcpy(jobs.p, hj.data(), sizeof(gpu::SnappyJob) * n, hipMemcpyHostToDevice);
-            hipMemset(stats.p, 0, 16);
+            hipMemset(stats.p, 0, 128);
             gpu::FusedCodecArgs fc;
             fc.comp = jobs.as<gpu::SnappyJob>();
             fc.ncomp = n;
@@ -264,8 +264,8 @@ void bind_gpu_ops(py::module_& g) {
             fm.npieces = n;
             fm.piece_err = fd.piece_err;
             const double mixed_us = time_launches([&] { gpu::LaunchFusedCodec(fm, s); }, iters, s);
-            uint32_t st[4];
-            hipMemcpy(st, stats.p, 16, hipMemcpyDeviceToHost);
+            uint32_t st[32];
+            hipMemcpy(st, stats.p, 128, hipMemcpyDeviceToHost);
             // the per-lane-segment kernels on the same blocks
             hipMemcpy(jobs.p, hj2.data(), sizeof(gpu::SnappyJob) * n, hipMemcpyHostToDevice);
             const double old_comp_us = time_launches(
@@ -295,6 +295,13 @@ void bind_gpu_ops(py::module_& g) {
             out["compress_rounds_max"] = st[1];
             out["decode_rounds_avg"] = (double)st[2] / (double)(n * (launches * 2));
             out["decode_rounds_max"] = st[3];
+            // cumulative shader-clock stamps of the first block / piece (the
+            // mixed launch ran last)
+            py::list cs, ds;
+            for (int k = 0; k < 9; ++k) cs.append(st[4 + k]);
+            for (int k = 0; k < 9; ++k) ds.append(st[16 + k]);
+            out["compress_phase_cycles"] = cs;
+            out["decode_phase_cycles"] = ds;
         }
         return out;
     }, py::arg("bodies"), py::arg("block") = 4096, py::arg("iters") = 50, py::arg("device") = 0);
