@@ -62,7 +62,7 @@ namespace gpu {
 
 namespace {
 
-constexpr int kT = 256;  // threads per workgroup
+constexpr int kT = 1024;  // threads per workgroup: 16 waves, 4 per SIMD to hide LDS latency
 constexpr int kWaves = kT / 64;
 constexpr int kTableBits = 12;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -83,14 +83,18 @@ struct OpMin {
     __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; }
 };
 
+// Inclusive wave64 scan on DPP (row shifts, then row broadcasts 15 and 31):
+// VALU cross-lane moves, no LDS round trip. `identity` fills lanes with no
+// source.
 template <typename Op>
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, Op op) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)v, (unsigned)o, 64);
-        if (lane >= o) v = op(y, v);
-    }
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, Op op, uint32_t identity = 0) {
+    const int id = (int)identity;
+    v = op((uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x111, 0xf, 0xf, false), v);
+    v = op((uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x112, 0xf, 0xf, false), v);
+    v = op((uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x114, 0xf, 0xf, false), v);
+    v = op((uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x118, 0xf, 0xf, false), v);
+    v = op((uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x142, 0xa, 0xf, false), v);
+    v = op((uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x143, 0xc, 0xf, false), v);
     return v;
 }
 
@@ -100,7 +104,7 @@ template <typename Op>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t identity, Op op, uint32_t* wtot,
                                                     uint32_t* total) {
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-    const uint32_t incl = wave_incl_scan(v, op);
+    const uint32_t incl = wave_incl_scan(v, op, identity);
     if (lane == 63) wtot[w] = incl;
     __syncthreads();
     uint32_t pre = identity, tot = identity;
