@@ -22,10 +22,10 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     a = ap.parse_args()
     from brpc_amd import native
-    for kind in a.kinds.split(","):
-        for nb in [int(x) for x in a.bodies.split(",")]:
+    for kind in a.kinds.replace("+", ",").split(","):
+        for nb in [int(x) for x in a.bodies.replace("+", ",").split(",")]:
             bodies = [native.echo_body(kind, 65536) for _ in range(nb)]
-            for blk in [int(x) for x in a.blocks.split(",")]:
+            for blk in [int(x) for x in a.blocks.replace("+", ",").split(",")]:
                 r = native.gpu.fused_codec_bench(bodies, blk, a.iters, 0)
                 r.update({"kind": kind, "bodies": nb, "block": blk})
                 print(json.dumps(r), flush=True)
