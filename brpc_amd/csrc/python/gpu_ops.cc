@@ -298,8 +298,8 @@ void bind_gpu_ops(py::module_& g) {
             // cumulative shader-clock stamps of the first block / piece (the
             // mixed launch ran last)
             py::list cs, ds;
-            for (int k = 0; k < 9; ++k) cs.append(st[4 + k]);
-            for (int k = 0; k < 9; ++k) ds.append(st[16 + k]);
+            for (int k = 0; k < 10; ++k) cs.append(st[4 + k]);
+            for (int k = 0; k < 10; ++k) ds.append(st[16 + k]);
             out["compress_phase_cycles"] = cs;
             out["decode_phase_cycles"] = ds;
         }
