@@ -212,80 +212,48 @@ struct Stamper {
 // ---------------------------------------------------------------- chains
 // The element chain of a block (compress: the greedy parse's element
 // starts; decode: the element boundaries of the compressed bytes) is the
-// orbit of 0 under nx[] (nx[i] > i). Each wave walks a contiguous 1/16 of
-// the positions, window by window: the lanes load nx[] of a 64-position
-// window in one LDS read, and the wave follows the chain through it with
-// v_readlane hops (a scalar dependency of a few cycles, no LDS round trip
-// per element), writing the window's 64-bit mask of element starts. A wave
-// starts at its segment's first position (speculative); each round then
-// hands every wave its predecessor's exit (one barrier per round, exits
-// double-buffered) and re-walks the waves whose entry changed. A re-walk
-// stops as soon as it lands on a start of its previous walk: from there on
-// the two walks coincide, so the old marks and exit stand. After round r
-// the first r + 1 segments are exact.
-// marks: one u64 per window; xb: 2 x kWaves exits + kWaves + 1 round flags.
-// Returns the chain's end (the last segment's exit).
-__device__ __forceinline__ uint32_t chain_marks(const uint16_t* nx, uint32_t npos, uint64_t* marks, uint32_t* xb,
-                                                uint32_t* rounds_out, const Stamper& stamp, int sk) {
+// orbit of 0 under nx[] (nx[i] > i). It is found by pointer jumping over
+// every position at once: J_0 = nx, J_{k+1} = J_k o J_k (double-buffered),
+// and in round k every position already on the chain marks J_k of itself,
+// so after round k every chain element within 2^(k+1) steps of 0 is marked.
+// The rounds end once J_{k+1}(0) has left the block (the chain is shorter
+// than 2^(k+1)): ceil(log2(elements)) + 1 rounds of a few independent LDS
+// ops per position, with no serial walk and no data-dependent worst case
+// (a speculative per-segment walk needed 15 rounds on periodic input).
+// on: npos + 64 bytes; j0, j1: npos u16 each. marks: one u64 per 64
+// positions (the ballot of on[]). Returns where the chain ends (>= npos).
+__device__ __forceinline__ uint32_t chain_marks(const uint16_t* nx, uint32_t npos, uint64_t* marks, uint8_t* on,
+                                                uint16_t* j0, uint16_t* j1, uint32_t* rounds_out) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t W = (npos + 63) / 64;
-    const uint32_t per = (W + kWaves - 1) / kWaves;
-    const uint32_t w0 = min(W, per * (uint32_t)wv), w1 = min(W, w0 + per);
-    const uint32_t lo = w0 * 64, hi = min(npos, w1 * 64);
-    uint32_t* ex0 = xb;
-    uint32_t* ex1 = xb + kWaves;
-    uint32_t* chg = xb + 2 * kWaves;
-    // walk from e; with `merge`, stop where the previous walk's marks resume
-    auto walk = [&](uint32_t e, bool merge, uint32_t old_exit) -> uint32_t {
-        uint32_t last = w0;  // windows [last, win) the walk jumped over are cleared
-        while (e < hi) {
-            const uint32_t win = e & ~63u, wi = win >> 6;
-            for (uint32_t w = last + (uint32_t)lane; w < wi; w += 64) marks[w] = 0;
-            const uint32_t nxl = win + (uint32_t)lane < npos ? nx[win + lane] : npos;
-            const uint64_t old = merge ? marks[wi] : 0;
-            uint64_t bits = 0;
-            uint32_t r = e - win;
-            while (r < 64 && win + r < hi) {
-                if ((old >> r) & 1) {  // the previous walk passed here: same path from now on
-                    bits |= old & (~0ull << r);
-                    if (lane == 0) marks[wi] = bits;
-                    return old_exit;
-                }
-                bits |= 1ull << r;
-                e = (uint32_t)__builtin_amdgcn_readlane((int)nxl, (int)r);
-                r = e - win;  // wraps to a huge value when e left the window
-            }
-            if (lane == 0) marks[wi] = bits;
-            last = wi + 1;
-        }
-        for (uint32_t w = last + (uint32_t)lane; w < w1; w += 64) marks[w] = 0;
-        return e;
-    };
-    for (uint32_t i = t; i <= (uint32_t)kWaves; i += kT) chg[i] = 0;
-    uint32_t entry = wv == 0 ? 0u : lo;
-    uint32_t exitp = walk(entry, false, 0);
-    if (lane == 0) ex0[wv] = exitp;
-    __syncthreads();
-    stamp(sk);
-    uint32_t rounds = 1;
-    for (int r = 0; r < kWaves; ++r) {
-        const uint32_t* cur = (r & 1) ? ex1 : ex0;
-        uint32_t* nxt = (r & 1) ? ex0 : ex1;
-        const uint32_t want = wv ? cur[wv - 1] : 0u;
-        if (want != entry) {
-            entry = want;
-            const uint32_t e = walk(entry, true, exitp);
-            if (e != exitp && lane == 0) chg[r] = 1;
-            exitp = e;
-        }
-        if (lane == 0) nxt[wv] = exitp;
-        __syncthreads();
-        if (!chg[r]) break;
-        ++rounds;
+    for (uint32_t i = t; i < W * 64; i += kT) {
+        if (i < npos) j0[i] = nx[i];
+        on[i] = i == 0;
     }
+    __syncthreads();
+    uint32_t rounds = 0, end;
+    for (int k = 0;; ++k) {
+        const uint16_t* src = (k & 1) ? j1 : j0;
+        uint16_t* dst = (k & 1) ? j0 : j1;
+        for (uint32_t i = t; i < npos; i += kT) {
+            const uint32_t j = src[i];
+            const uint32_t jj = j < npos ? src[j] : j;
+            if (j < npos && on[i]) on[j] = 1;
+            dst[i] = (uint16_t)jj;
+        }
+        ++rounds;
+        __syncthreads();
+        end = dst[0];
+        if (end >= npos) break;  // (block-uniform: read after the barrier)
+        __syncthreads();         // dst[0] read before the next round overwrites its source
+    }
+    for (uint32_t w = (uint32_t)wv; w < W; w += kWaves) {
+        const uint64_t m = __ballot(on[w * 64 + lane] != 0);
+        if (lane == 0) marks[w] = m;
+    }
+    __syncthreads();
     if (rounds_out) *rounds_out = rounds;
-    // the last round wrote its exits into the buffer it called nxt
-    return (((rounds - 1) & 1) ? ex0 : ex1)[kWaves - 1];
+    return end;
 }
 
 // ---------------------------------------------------------------- compress
@@ -296,7 +264,7 @@ constexpr uint32_t kCompWins = kFusedMaxBlock / 64;  // 128
 // wtot | xch | ex
 __host__ __device__ constexpr uint32_t CompressLds(uint32_t C) {
     return (C + 96) + C + 2 * C + (2 * C + 16) + (4u << kTableBits) + 16 * kCompWins + 16 * (kCompWins + 1) +
-           4 * (kWaves + kT + 4 * kWaves) + 64;
+           4 * (kWaves + kT + 4 * kWaves) + (C + 64) + 4 * C + 64;
 }
 
 __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
@@ -326,6 +294,9 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     uint32_t* wtot = carry + kCompWins + 1;
     uint32_t* xch = wtot + kWaves;
     uint32_t* ex = xch + kT;
+    uint8_t* on = reinterpret_cast<uint8_t*>(ex + 4 * kWaves);  // chain: C + 64 bytes, then two u16 jump arrays
+    uint16_t* j0 = reinterpret_cast<uint16_t*>(on + C + 64);
+    uint16_t* j1 = j0 + C;
     const uint32_t W = (n + 63) / 64;
 
     const Stamper stamp(a.stats, job == 0, 4);
@@ -401,7 +372,7 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     stamp(3);
     // 3. the greedy parse
     uint32_t rounds = 0;
-    chain_marks(NX, n, wm, ex, &rounds, stamp, 9);
+    chain_marks(NX, n, wm, on, j0, j1, &rounds);
     stamp(4);
     if (a.stats && t == 0) {
         atomicAdd(&a.stats[0], rounds);
@@ -513,7 +484,8 @@ __host__ __device__ constexpr uint32_t DecodeCinCap(uint32_t C) {
 // ocarry (u32 x kCompWins) | wtot | xch | ex
 __host__ __device__ constexpr uint32_t DecodeLds(uint32_t C) {
     return DecodeCinCap(C) + 128 + 2 * (DecodeCinCap(C) + 16) + 2 * C + 2 * C + 8 * kDecWins + 8 * kCompWins +
-           8 * kDecWins + 4 * kCompWins + 4 * (kWaves + kT + 4 * kWaves) + 64;
+           8 * kDecWins + 4 * kCompWins + 4 * (kWaves + kT + 4 * kWaves) + (DecodeCinCap(C) + 64) +
+           4 * DecodeCinCap(C) + 64;
 }
 
 __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
@@ -534,6 +506,9 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
     uint32_t* wtot = ocarry + kCompWins;
     uint32_t* xch = wtot + kWaves;
     uint32_t* ex = xch + kT;
+    uint8_t* on = reinterpret_cast<uint8_t*>(ex + 4 * kWaves);  // chain: cap + 64 bytes, then two u16 jump arrays
+    uint16_t* j0 = reinterpret_cast<uint16_t*>(on + cap + 64);
+    uint16_t* j1 = j0 + cap;
     __shared__ int bad;
     if (t == 0) bad = 0;
     const bool fits = n <= a.max_ulen && m <= cap && n > 0 && m > 0;
@@ -586,7 +561,7 @@ __device__ void decode_piece(const FusedCodecArgs& a, int job, uint8_t* lds) {
         __syncthreads();
         stamp(1);
         uint32_t rounds = 0;
-        const uint32_t end = chain_marks(NX, m, cm, ex, &rounds, stamp, 9);
+        const uint32_t end = chain_marks(NX, m, cm, on, j0, j1, &rounds);
         stamp(2);
         if (a.stats && t == 0) {
             atomicAdd(&a.stats[2], rounds);
