@@ -210,6 +210,8 @@ struct Stamper {
 };
 
 // ---------------------------------------------------------------- chains
+constexpr int kChainPer = 10;  // positions per thread: covers a compressed 8 KiB piece (<= 9589 bytes)
+static_assert(SnappyMaxCompressedLength(kFusedMaxBlock) <= (uint64_t)kChainPer * kT, "chain positions per thread");
 // The element chain of a block (compress: the greedy parse's element
 // starts; decode: the element boundaries of the compressed bytes) is the
 // orbit of 0 under nx[] (nx[i] > i). It is found by pointer jumping over
@@ -235,17 +237,28 @@ __device__ __forceinline__ uint32_t chain_marks(const uint16_t* nx, uint32_t npo
     for (int k = 0;; ++k) {
         const uint16_t* src = (k & 1) ? j1 : j0;
         uint16_t* dst = (k & 1) ? j0 : j1;
-        for (uint32_t i = t; i < npos; i += kT) {
-            const uint32_t j = src[i];
-            const uint32_t jj = j < npos ? src[j] : j;
-            if (j < npos && on[i]) on[j] = 1;
+        // up to kChainPer positions per thread: every load is issued before
+        // any result is used
+        uint32_t j[kChainPer];
+#pragma unroll
+        for (int u = 0; u < kChainPer; ++u) {
+            const uint32_t i = (uint32_t)t + (uint32_t)u * kT;
+            j[u] = i < npos ? src[i] : npos;
+        }
+#pragma unroll
+        for (int u = 0; u < kChainPer; ++u) {
+            const uint32_t i = (uint32_t)t + (uint32_t)u * kT;
+            if (i >= npos) break;
+            const uint32_t jj = j[u] < npos ? src[j[u]] : j[u];
+            if (j[u] < npos && on[i]) on[j[u]] = 1;
             dst[i] = (uint16_t)jj;
         }
         ++rounds;
         __syncthreads();
+        // (dst is the next round's source, never written by it: no second
+        // barrier before the next round)
         end = dst[0];
-        if (end >= npos) break;  // (block-uniform: read after the barrier)
-        __syncthreads();         // dst[0] read before the next round overwrites its source
+        if (end >= npos) break;  // block-uniform: read after the barrier
     }
     for (uint32_t w = (uint32_t)wv; w < W; w += kWaves) {
         const uint64_t m = __ballot(on[w * 64 + lane] != 0);
@@ -264,7 +277,7 @@ constexpr uint32_t kCompWins = kFusedMaxBlock / 64;  // 128
 // wtot | xch | ex
 __host__ __device__ constexpr uint32_t CompressLds(uint32_t C) {
     return (C + 96) + C + 2 * C + (2 * C + 16) + (4u << kTableBits) + 16 * kCompWins + 16 * (kCompWins + 1) +
-           4 * (kWaves + kT + 4 * kWaves) + (C + 64) + 4 * C + 64;
+           4 * (kWaves + kT + 4 * kWaves) + (C + 64) + 6 * C + 64;
 }
 
 __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
@@ -297,6 +310,7 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     uint8_t* on = reinterpret_cast<uint8_t*>(ex + 4 * kWaves);  // chain: C + 64 bytes, then two u16 jump arrays
     uint16_t* j0 = reinterpret_cast<uint16_t*>(on + C + 64);
     uint16_t* j1 = j0 + C;
+    uint16_t* ES = j1 + C;  // output bytes of the element starting at p, if one does
     const uint32_t W = (n + 63) / 64;
 
     const Stamper stamp(a.stats, job == 0, 4);
@@ -366,7 +380,9 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
     };
     for (uint32_t p = t; p < n; p += kT) {
         const uint32_t l = L[p];
-        NX[p] = (uint16_t)(l >= 4 ? p + l : next_match(p + 1));
+        const uint32_t nx = l >= 4 ? p + l : next_match(p + 1);
+        NX[p] = (uint16_t)nx;
+        ES[p] = (uint16_t)(l >= 4 ? ((l < 12 && p - cand[p] < 2048) ? 2 : 3) : lit_tag_bytes(nx - p) + (nx - p));
     }
     __syncthreads();
     stamp(3);
@@ -379,13 +395,7 @@ __device__ void compress_block(const FusedCodecArgs& a, int job, uint8_t* lds) {
         atomicMax(&a.stats[1], rounds);
     }
     // 4. element sizes per window (lane = position), window offsets
-    auto elem_size = [&](uint32_t p, bool st) -> uint32_t {
-        if (!st) return 0;
-        const uint32_t l = L[p];
-        if (l >= 4) return (l < 12 && p - cand[p] < 2048) ? 2 : 3;
-        const uint32_t ll = NX[p] - p;
-        return lit_tag_bytes(ll) + ll;
-    };
+    auto elem_size = [&](uint32_t p, bool st) -> uint32_t { return st ? ES[p] : 0u; };
     for (uint32_t k = (uint32_t)wv; k < W; k += kWaves) {
         const uint32_t p = k * 64 + (uint32_t)lane;
         const bool st = p < n && ((wm[k] >> lane) & 1);
