@@ -34,8 +34,13 @@ class RedisServerContext : public ParsingContext {
 public:
     static const int kTag = 0x52454453;  // "REDS"
     int protocol_tag() const override { return kTag; }
-    RedisCommandHandler* transaction = nullptr;  // inside MULTI
-    std::vector<std::vector<std::string>> queued;
+    ~RedisServerContext() override { delete transaction; }
+    // commands go here while a handler's transaction is open (it returned
+    // CONTINUE) until the transaction handler returns OK
+    RedisCommandHandler* transaction = nullptr;
+    // replies deferred by handlers that returned BATCHED, owed in the next
+    // OK reply (an array of batched + 1 replies)
+    int batched = 0;
     // incremental command parser: a command's arguments are consumed from
     // the socket buffer as each one completes, and the state survives
     // across reads (a large SET spanning many reads is parsed once, not
@@ -138,47 +143,64 @@ int parse_command(RedisServerContext* ctx, Buf* in, std::vector<std::string>* ar
     return 1;
 }
 
-void run_command(Server* server, RedisServerContext* ctx, std::vector<std::string>& args, RedisReply* out) {
+// One command under the handler protocol of the reference
+// (src/brpc/policy/redis_protocol.cpp:79-131, redis.h RedisCommandHandler):
+//  * OK: the reply goes out now; after BATCHED commands it is an array with
+//    one reply per batched command plus this one, sent element by element;
+//  * CONTINUE: the reply goes out and the handler's transaction handler
+//    takes the connection's next commands until it returns OK (MULTI/EXEC);
+//  * BATCHED: the reply is owed; flush_batched tells the handler whether
+//    this is the last command of what arrived, i.e. whether to settle now.
+// Returns -1 on a protocol violation by the handler (the connection fails).
+int run_command(Server* server, RedisServerContext* ctx, std::vector<std::string>& args, bool flush_batched,
+                Buf* out_buf) {
     RedisService* svc = server->options().redis_service;
-    const std::string name = to_lower(args[0]);
-    args[0] = name;
+    args[0] = to_lower(args[0]);
+    RedisReply out;
+    RedisCommandHandler::Result r = RedisCommandHandler::OK;
     if (ctx->transaction) {
-        if (name == "exec") {
-            RedisCommandHandler* th = ctx->transaction;
-            ctx->transaction = nullptr;
-            out->SetArray(ctx->queued.size());
-            for (size_t i = 0; i < ctx->queued.size(); ++i) th->Run(ctx->queued[i], &(*out)[i], true);
-            ctx->queued.clear();
-            delete th;
-            return;
-        }
-        if (name == "discard") {
+        r = ctx->transaction->Run(args, &out, flush_batched);
+        if (r == RedisCommandHandler::OK) {
             delete ctx->transaction;
             ctx->transaction = nullptr;
-            ctx->queued.clear();
-            out->SetStatus("OK");
-            return;
+        } else if (r == RedisCommandHandler::BATCHED) {
+            LOG(ERROR) << "a redis transaction handler returned BATCHED";
+            return -1;
         }
-        ctx->queued.push_back(args);
-        out->SetStatus("QUEUED");
-        return;
-    }
-    RedisCommandHandler* h = svc->FindCommandHandler(name);
-    if (!h) {
-        out->SetError("ERR unknown command '" + name + "'");
-        return;
-    }
-    if (name == "multi") {
-        RedisCommandHandler* th = h->NewTransactionHandler();
-        if (!th) {
-            out->SetError("ERR MULTI is not supported");
-            return;
+    } else {
+        RedisCommandHandler* h = svc->FindCommandHandler(args[0]);
+        if (!h) {
+            out.SetError("ERR unknown command '" + args[0] + "'");
+        } else {
+            r = h->Run(args, &out, flush_batched);
+            if (r == RedisCommandHandler::CONTINUE) {
+                if (ctx->batched) {
+                    LOG(ERROR) << "a redis handler returned CONTINUE inside a batch";
+                    return -1;
+                }
+                ctx->transaction = h->NewTransactionHandler();
+                if (!ctx->transaction) {
+                    out.SetError("ERR '" + args[0] + "' opened a transaction its handler cannot run");
+                    r = RedisCommandHandler::OK;
+                }
+            } else if (r == RedisCommandHandler::BATCHED) {
+                ++ctx->batched;
+            }
         }
-        ctx->transaction = th;
-        out->SetStatus("OK");
-        return;
     }
-    h->Run(args, out, true);
+    if (r == RedisCommandHandler::BATCHED) return 0;  // owed
+    if (r == RedisCommandHandler::OK && ctx->batched) {
+        if (!out.is_array() || (int)out.size() != ctx->batched + 1) {
+            LOG(ERROR) << "a redis handler settled " << ctx->batched << " batched commands with "
+                       << (out.is_array() ? (int)out.size() : -1) << " replies";
+            return -1;
+        }
+        for (size_t i = 0; i < out.size(); ++i) out[i].SerializeTo(out_buf);
+        ctx->batched = 0;
+        return 0;
+    }
+    out.SerializeTo(out_buf);
+    return 0;
 }
 
 }  // namespace
@@ -253,19 +275,27 @@ ParseResult ParseRedisMessage(Buf* source, Socket* socket, bool read_eof, const 
             return MakeParseError(PARSE_ERROR_TRY_OTHERS);
         }
     }
-    // execute every complete command now, in order; one write per batch
+    // execute every complete command now, in order; one write per batch.
+    // A command is run once the next one was parsed (or none is left), so
+    // the last command of what arrived runs with flush_batched.
     Buf out;
     int rc;
+    std::vector<std::string> cur, next;
+    bool have = false, broken = false;
     for (;;) {
-        std::vector<std::string> args;
-        rc = parse_command(ctx, source, &args);
+        rc = parse_command(ctx, source, &next);
         if (rc <= 0) break;
-        RedisReply reply;
-        run_command(const_cast<Server*>(server), ctx, args, &reply);
-        reply.SerializeTo(&out);
+        if (have && run_command(const_cast<Server*>(server), ctx, cur, false, &out) != 0) {
+            broken = true;
+            break;
+        }
+        cur.swap(next);
+        next.clear();
+        have = true;
     }
+    if (have && !broken && run_command(const_cast<Server*>(server), ctx, cur, true, &out) != 0) broken = true;
     if (!out.empty()) socket->Write(&out);
-    if (rc < 0) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+    if (rc < 0 || broken) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
     // every complete command ran inside parse; what is left is the start
     // of the next one: read more (reference: redis_protocol.cpp:167-194)
     return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);

@@ -191,18 +191,50 @@ bool RedisRequest::AddCommandByComponents(const std::vector<std::string>& args) 
 }
 
 bool RedisRequest::AddCommand(const char* fmt, ...) {
-    // split the format on spaces; each %s / %d / %lld / %b consumes an arg
-    // and becomes (part of) one component, so %s values may hold spaces
+    // Split the format into components the way redis-cli does (reference:
+    // src/brpc/redis_command.cpp, RedisCommandFormatV): spaces separate
+    // components; a '...' or "..." string is one component (spaces kept,
+    // possibly empty) and also ends the component before it, so
+    // "get ''key" is {get, "", key}. Inside quotes a backslash escapes only
+    // the quote character itself ('\'' -> ', "\"" -> "); any other
+    // backslash stays. Each %s / %d / %u / %lld / %b consumes an argument
+    // and becomes part of the current component, so %s values may hold
+    // spaces or quotes.
     std::vector<std::string> comps;
     std::string cur;
     bool in_comp = false;
+    char quote = 0;
     va_list ap;
     va_start(ap, fmt);
+    auto fail = [&] {
+        va_end(ap);
+        _has_error = true;
+        return false;
+    };
     for (const char* p = fmt; *p; ++p) {
-        if (*p == ' ') {
+        if (quote) {
+            if (*p == '\\' && p[1] == quote) {
+                cur.push_back(quote);
+                ++p;
+                continue;
+            }
+            if (*p == quote) {  // the quoted component ends here
+                comps.push_back(cur);
+                cur.clear();
+                quote = 0;
+                in_comp = false;
+                continue;
+            }
+        } else if (*p == ' ') {
             if (in_comp) comps.push_back(cur);
             cur.clear();
             in_comp = false;
+            continue;
+        } else if (*p == '\'' || *p == '"') {
+            if (in_comp) comps.push_back(cur);
+            cur.clear();
+            in_comp = false;
+            quote = *p;
             continue;
         }
         in_comp = true;
@@ -227,11 +259,10 @@ bool RedisRequest::AddCommand(const char* fmt, ...) {
         } else if (*p == '%') {
             cur.push_back('%');
         } else {
-            va_end(ap);
-            _has_error = true;
-            return false;
+            return fail();
         }
     }
+    if (quote) return fail();  // unterminated quote
     va_end(ap);
     if (in_comp) comps.push_back(cur);
     return AddCommandByComponents(comps);

@@ -77,23 +77,38 @@ private:
     KV* _kv;
 };
 
+// MULTI the reference's way (test/brpc_redis_unittest.cpp MultiCommandHandler):
+// "multi" answers +OK and returns CONTINUE; its transaction handler answers
+// +QUEUED (CONTINUE) for every command, a nested MULTI with an error, and
+// runs the queue at EXEC, returning OK with one reply per queued command.
 class MultiHandler : public RedisCommandHandler {
 public:
     explicit MultiHandler(RedisService* svc) : _svc(svc) {}
     Result Run(const std::vector<std::string>&, RedisReply* out, bool) override {
         out->SetStatus("OK");
-        return OK;
+        return CONTINUE;
     }
     RedisCommandHandler* NewTransactionHandler() override {
         struct Tx : public RedisCommandHandler {
             RedisService* svc;
-            Result Run(const std::vector<std::string>& args, RedisReply* out, bool b) override {
-                RedisCommandHandler* h = svc->FindCommandHandler(args[0]);
-                if (!h) {
-                    out->SetError("ERR unknown command");
+            std::vector<std::vector<std::string>> queued;
+            Result Run(const std::vector<std::string>& args, RedisReply* out, bool) override {
+                if (args[0] == "multi") {
+                    out->SetError("ERR MULTI calls can not be nested");
+                    return CONTINUE;
+                }
+                if (args[0] == "exec") {
+                    out->SetArray(queued.size());
+                    for (size_t i = 0; i < queued.size(); ++i) {
+                        RedisCommandHandler* h = svc->FindCommandHandler(queued[i][0]);
+                        if (h) h->Run(queued[i], &(*out)[i], true);
+                        else (*out)[i].SetError("ERR unknown command");
+                    }
                     return OK;
                 }
-                return h->Run(args, out, b);
+                queued.push_back(args);
+                out->SetStatus("QUEUED");
+                return CONTINUE;
             }
         };
         Tx* t = new Tx;
@@ -506,4 +521,321 @@ TEST(Redis, split_value_with_foreign_magic_stays_redis) {
     close(fd);
     server.Stop(0);
     server.Join();
+}
+
+namespace {
+
+// A server with the test's handlers, and a redis channel to it.
+struct RedisFixture {
+    KV kv;
+    RedisService svc;
+    SetHandler set{&kv};
+    GetHandler get{&kv};
+    IncrHandler incr{&kv};
+    MultiHandler multi{&svc};
+    Server server;
+    Channel ch;
+    bool ok = false;
+    RedisFixture() {
+        svc.AddCommandHandler("set", &set);
+        svc.AddCommandHandler("get", &get);
+        svc.AddCommandHandler("incr", &incr);
+        svc.AddCommandHandler("multi", &multi);
+    }
+    bool Start() {
+        ServerOptions so;
+        so.redis_service = &svc;
+        so.has_builtin_services = false;
+        if (server.Start("127.0.0.1:0", &so) != 0) return false;
+        ChannelOptions co;
+        co.protocol = "redis";
+        co.timeout_ms = 3000;
+        return ch.Init(("127.0.0.1:" + std::to_string(server.listen_port())).c_str(), &co) == 0;
+    }
+};
+
+std::string wire(const RedisRequest& r) { return r.ToString(); }
+
+// INCRBY/DECR/DECRBY over the shared KV (the reference runs them against a
+// real redis-server; here the server side is ours)
+class AddHandler : public RedisCommandHandler {
+public:
+    AddHandler(KV* kv, int sign, bool by) : _kv(kv), _sign(sign), _by(by) {}
+    Result Run(const std::vector<std::string>& args, RedisReply* out, bool) override {
+        if (args.size() != (_by ? 3u : 2u)) {
+            out->SetError("ERR wrong number of arguments");
+            return OK;
+        }
+        const int64_t d = _by ? atoll(args[2].c_str()) : 1;
+        std::lock_guard<std::mutex> g(_kv->mu);
+        const int64_t v = atoll(_kv->m[args[1]].c_str()) + _sign * d;
+        _kv->m[args[1]] = std::to_string(v);
+        out->SetInteger(v);
+        return OK;
+    }
+
+private:
+    KV* _kv;
+    int _sign;
+    bool _by;
+};
+
+}  // namespace
+
+TEST(Redis, keys_with_spaces) {
+    RedisFixture f;
+    ASSERT_TRUE(f.Start());
+    RedisRequest req;
+    RedisResponse res;
+    Controller cntl;
+    ASSERT_TRUE(req.AddCommand("set %s 'he1 he1 da1'", "hello world"));
+    ASSERT_TRUE(req.AddCommand("set 'hello2 world2' 'he2 he2 da2'"));
+    ASSERT_TRUE(req.AddCommand("set \"hello3 world3\" \"he3 he3 da3\""));
+    ASSERT_TRUE(req.AddCommand("get \"hello world\""));
+    ASSERT_TRUE(req.AddCommand("get 'hello world'"));
+    ASSERT_TRUE(req.AddCommand("get 'hello2 world2'"));
+    ASSERT_TRUE(req.AddCommand("get 'hello3 world3'"));
+    f.ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+    ASSERT_FALSE(cntl.Failed());
+    ASSERT_EQ(res.reply_size(), 7);
+    for (int i = 0; i < 3; ++i) EXPECT_EQ(res.reply(i).data(), "OK");
+    EXPECT_EQ(res.reply(3).data(), "he1 he1 da1");
+    EXPECT_EQ(res.reply(4).data(), "he1 he1 da1");
+    EXPECT_EQ(res.reply(5).data(), "he2 he2 da2");
+    EXPECT_EQ(res.reply(6).data(), "he3 he3 da3");
+}
+
+TEST(Redis, incr_and_decr) {
+    RedisFixture f;
+    AddHandler decr(&f.kv, -1, false), incrby(&f.kv, 1, true), decrby(&f.kv, -1, true);
+    f.svc.AddCommandHandler("decr", &decr);
+    f.svc.AddCommandHandler("incrby", &incrby);
+    f.svc.AddCommandHandler("decrby", &decrby);
+    ASSERT_TRUE(f.Start());
+    RedisRequest req;
+    RedisResponse res;
+    Controller cntl;
+    req.AddCommand("incr counter1");
+    req.AddCommand("decr counter1");
+    req.AddCommand("incrby counter1 %d", 10);
+    req.AddCommand("decrby counter1 %d", 20);
+    f.ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+    ASSERT_FALSE(cntl.Failed());
+    ASSERT_EQ(res.reply_size(), 4);
+    for (int i = 0; i < 4; ++i) EXPECT_EQ(res.reply(i).type(), REDIS_REPLY_INTEGER);
+    EXPECT_EQ(res.reply(0).integer(), 1);
+    EXPECT_EQ(res.reply(1).integer(), 0);
+    EXPECT_EQ(res.reply(2).integer(), 10);
+    EXPECT_EQ(res.reply(3).integer(), -10);
+}
+
+TEST(Redis, cmd_format_empty_and_adjacent_quotes) {
+    struct Case {
+        const char* fmt;
+        const char* want;
+    } cases[] = {
+        {"set a ''", "*3\r\n$3\r\nset\r\n$1\r\na\r\n$0\r\n\r\n"},
+        {"mset b '' c ''", "*5\r\n$4\r\nmset\r\n$1\r\nb\r\n$0\r\n\r\n$1\r\nc\r\n$0\r\n\r\n"},
+        {"set a 123", "*3\r\n$3\r\nset\r\n$1\r\na\r\n$3\r\n123\r\n"},
+        {"mset b '' c ccc", "*5\r\n$4\r\nmset\r\n$1\r\nb\r\n$0\r\n\r\n$1\r\nc\r\n$3\r\nccc\r\n"},
+        {"get ''key value", "*4\r\n$3\r\nget\r\n$0\r\n\r\n$3\r\nkey\r\n$5\r\nvalue\r\n"},
+        {"get key'' value", "*4\r\n$3\r\nget\r\n$3\r\nkey\r\n$0\r\n\r\n$5\r\nvalue\r\n"},
+        {"get 'ext'key   value  ", "*4\r\n$3\r\nget\r\n$3\r\next\r\n$3\r\nkey\r\n$5\r\nvalue\r\n"},
+        {"  get   key'ext'   value  ", "*4\r\n$3\r\nget\r\n$3\r\nkey\r\n$3\r\next\r\n$5\r\nvalue\r\n"},
+    };
+    for (const Case& c : cases) {
+        RedisRequest req;
+        ASSERT_TRUE(req.AddCommand(c.fmt));
+        EXPECT_TRUE_M(wire(req) == c.want, std::string(c.fmt));
+    }
+    RedisRequest bad;
+    EXPECT_FALSE(bad.AddCommand("set a 'unterminated"));
+    EXPECT_TRUE(bad.has_error());
+}
+
+TEST(Redis, quote_and_escape) {
+    struct Case {
+        const char* fmt;
+        const char* value;
+    } cases[] = {
+        {"set a 'foo bar'", "foo bar"},      {"set a 'foo \\'bar'", "foo 'bar"},
+        {"set a 'foo \"bar'", "foo \"bar"},  {"set a 'foo \\\"bar'", "foo \\\"bar"},
+        {"set a \"foo 'bar\"", "foo 'bar"},  {"set a \"foo \\'bar\"", "foo \\'bar"},
+        {"set a \"foo \\\"bar\"", "foo \"bar"},
+    };
+    for (const Case& c : cases) {
+        RedisRequest req;
+        ASSERT_TRUE(req.AddCommand(c.fmt));
+        const std::string v = c.value;
+        const std::string want = "*3\r\n$3\r\nset\r\n$1\r\na\r\n$" + std::to_string(v.size()) + "\r\n" + v + "\r\n";
+        EXPECT_TRUE_M(wire(req) == want, std::string(c.fmt));
+    }
+}
+
+// The server's incremental command parser: a command delivered one byte
+// at a time, then a command with a non-bulk argument (refused), and
+// connections opening with a non-array (not redis).
+TEST(Redis, command_parser_incremental_and_refusals) {
+    RedisFixture f;
+    ASSERT_TRUE(f.Start());
+    {
+        const int fd = raw_connect(f.server.listen_port());
+        ASSERT_GE(fd, 0);
+        const std::string cmd = "*3\r\n$3\r\nset\r\n$3\r\nabc\r\n$3\r\ndef\r\n";
+        for (int round = 0; round < 20; ++round) {
+            for (char c : cmd) ASSERT_TRUE(send_all(fd, std::string(1, c)));
+            EXPECT_EQ(recv_n(fd, 5), "+OK\r\n");
+        }
+        ASSERT_TRUE(send_all(fd, "*2\r\n$3\r\nget\r\n$3\r\nabc\r\n"));
+        EXPECT_EQ(recv_n(fd, 9), "$3\r\ndef\r\n");
+        // an integer where a bulk argument must be: the connection is dropped
+        ASSERT_TRUE(send_all(fd, "*3\r\n$3\r\nset\r\n:123\r\n$3\r\ndef\r\n"));
+        EXPECT_EQ(recv_n(fd, 1), "");
+        close(fd);
+    }
+    for (const char* first : {":123456\r\n", "+OK\r\n", "$5\r\nhello\r\n"}) {
+        const int fd = raw_connect(f.server.listen_port());
+        ASSERT_GE(fd, 0);
+        ASSERT_TRUE(send_all(fd, first));
+        EXPECT_EQ(recv_n(fd, 1), "");  // no protocol claims it: closed
+        close(fd);
+    }
+}
+
+TEST(Redis, server_command_continue) {
+    RedisFixture f;
+    ASSERT_TRUE(f.Start());
+    {
+        RedisRequest req;
+        RedisResponse res;
+        Controller cntl;
+        ASSERT_TRUE(req.AddCommand("set hello world"));
+        ASSERT_TRUE(req.AddCommand("get hello"));
+        f.ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        ASSERT_EQ(res.reply_size(), 2);
+        EXPECT_EQ(res.reply(1).data(), "world");
+    }
+    {
+        RedisRequest req;
+        RedisResponse res;
+        Controller cntl;
+        ASSERT_TRUE(req.AddCommand("multi"));
+        ASSERT_TRUE(req.AddCommand("mUltI"));
+        const int count = 10;
+        for (int i = 0; i < count; ++i) ASSERT_TRUE(req.AddCommand("incr hello2"));
+        ASSERT_TRUE(req.AddCommand("exec"));
+        f.ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        ASSERT_EQ(res.reply_size(), count + 3);
+        EXPECT_EQ(res.reply(0).data(), "OK");
+        EXPECT_TRUE(res.reply(1).is_error());
+        for (int i = 2; i < count + 2; ++i) EXPECT_EQ(res.reply(i).data(), "QUEUED");
+        const RedisReply& m = res.reply(count + 2);
+        ASSERT_TRUE(m.is_array());
+        ASSERT_EQ((int)m.size(), count);
+        for (int i = 0; i < count; ++i) EXPECT_EQ(m[i].integer(), i + 1);
+    }
+    {
+        // after EXEC the connection is back to plain commands
+        RedisRequest req;
+        RedisResponse res;
+        Controller cntl;
+        ASSERT_TRUE(req.AddCommand("get hello"));
+        ASSERT_TRUE(req.AddCommand("get nothere"));
+        ASSERT_TRUE(req.AddCommand("set key1 value1"));
+        ASSERT_TRUE(req.AddCommand("get key1"));
+        f.ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+        ASSERT_FALSE(cntl.Failed());
+        EXPECT_EQ(res.reply(0).data(), "world");
+        EXPECT_TRUE(res.reply(1).is_nil());
+        EXPECT_EQ(res.reply(2).data(), "OK");
+        EXPECT_EQ(res.reply(3).data(), "value1");
+    }
+}
+
+namespace {
+// Batched handlers (reference: RedisServiceImpl::OnBatched): commands that
+// arrive together are deferred (BATCHED) and settled by the last one of the
+// read (flush_batched) with one reply per command, in one array.
+struct BatchKV {
+    KV kv;
+    std::vector<std::vector<std::string>> pending;
+    int batches = 0;
+    void Do(const std::vector<std::string>& a, RedisReply* out) {
+        std::lock_guard<std::mutex> g(kv.mu);
+        if (a[0] == "set") {
+            kv.m[a[1]] = a[2];
+            out->SetStatus("OK");
+        } else {
+            auto it = kv.m.find(a[1]);
+            if (it == kv.m.end()) out->SetNil();
+            else out->SetString(it->second);
+        }
+    }
+    RedisCommandHandler::Result OnBatched(const std::vector<std::string>& a, RedisReply* out, bool flush) {
+        if (pending.empty() && flush) {
+            Do(a, out);
+            return RedisCommandHandler::OK;
+        }
+        pending.push_back(a);
+        if (!flush) return RedisCommandHandler::BATCHED;
+        out->SetArray(pending.size());
+        for (size_t i = 0; i < pending.size(); ++i) Do(pending[i], &(*out)[i]);
+        pending.clear();
+        ++batches;
+        return RedisCommandHandler::OK;
+    }
+};
+class BatchedHandler : public RedisCommandHandler {
+public:
+    explicit BatchedHandler(BatchKV* b) : _b(b) {}
+    Result Run(const std::vector<std::string>& args, RedisReply* out, bool flush) override {
+        if (args.size() < 2) {
+            out->SetError("ERR wrong number of arguments");
+            return OK;
+        }
+        return _b->OnBatched(args, out, flush);
+    }
+
+private:
+    BatchKV* _b;
+};
+}  // namespace
+
+TEST(Redis, server_handle_pipeline_batched) {
+    BatchKV b;
+    BatchedHandler h(&b);
+    RedisService svc;
+    svc.AddCommandHandler("set", &h);
+    svc.AddCommandHandler("get", &h);
+    Server server;
+    ServerOptions so;
+    so.redis_service = &svc;
+    so.has_builtin_services = false;
+    ASSERT_EQ(server.Start("127.0.0.1:0", &so), 0);
+    // one write, so all eight commands arrive in one read
+    const int fd = raw_connect(server.listen_port());
+    ASSERT_GE(fd, 0);
+    RedisRequest req;
+    for (const char* c : {"set key1 v1", "set key2 v2", "set key3 v3", "get hello", "get hello", "set key1 world",
+                          "set key2 world", "get key2"})
+        ASSERT_TRUE(req.AddCommand(c));
+    ASSERT_TRUE(send_all(fd, wire(req)));
+    const std::string want = "+OK\r\n+OK\r\n+OK\r\n$-1\r\n$-1\r\n+OK\r\n+OK\r\n$5\r\nworld\r\n";
+    EXPECT_EQ(recv_n(fd, want.size()), want);
+    EXPECT_EQ(b.batches, 1);
+    close(fd);
+    // through a channel, too
+    Channel ch;
+    ChannelOptions co;
+    co.protocol = "redis";
+    co.timeout_ms = 3000;
+    ASSERT_EQ(ch.Init(("127.0.0.1:" + std::to_string(server.listen_port())).c_str(), &co), 0);
+    RedisResponse res;
+    Controller cntl;
+    ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+    ASSERT_FALSE(cntl.Failed());
+    ASSERT_EQ(res.reply_size(), 8);
+    EXPECT_EQ(res.reply(7).data(), "world");
 }
