@@ -52,7 +52,7 @@ for st in "$@"; do
       echo "run_$nr: $args"; tail -40 $T/run_$nr.txt ;;
     kt:*)
       args=${st#kt:}
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $T/kt -o kt -- python3 bench.py ${args//,/ } \
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $T/kt -o kt -- python3 bench.py ${args//,/ } \
         > $T/kt.log 2>&1 || { tail -20 $T/kt.log; exit 1; }
       python benchmarks/rocprof_summary.py $T/kt > $T/kt_summary.txt 2>&1; head -40 $T/kt_summary.txt ;;
     *) echo "unknown stage $st"; exit 2 ;;
