@@ -17,9 +17,14 @@
 #include <vector>
 
 #include "base/macros.h"
+#include "base/tsan.h"
 
 namespace mrpc {
 
+// The per-thread free lists hand an object from the fiber that returned it
+// to the next fiber that takes it on the same worker with no atomic in
+// between (program order of the worker orders them); TSan tracks fibers as
+// separate threads, so put()/get() carry explicit release/acquire marks.
 template <typename T>
 class ResourcePool {
 public:
@@ -36,17 +41,13 @@ public:
 
     T* get(uint32_t* id) {
         Local& l = local();
-        if (!l.free_ids.empty()) {
+        if (!l.free_ids.empty() || refill_from_global(l)) {
             uint32_t i = l.free_ids.back();
             l.free_ids.pop_back();
             *id = i;
-            return address(i);
-        }
-        if (refill_from_global(l)) {
-            uint32_t i = l.free_ids.back();
-            l.free_ids.pop_back();
-            *id = i;
-            return address(i);
+            T* t = address(i);
+            MRPC_TSAN_ACQUIRE(t);
+            return t;
         }
         if (l.cur_block == kInvalid || l.cur_index >= kBlockItems) {
             uint32_t b = _nblock.fetch_add(1, std::memory_order_relaxed);
@@ -62,6 +63,7 @@ public:
     }
 
     void put(uint32_t id) {
+        MRPC_TSAN_RELEASE(address(id));
         Local& l = local();
         if (l.free_ids.size() >= kLocalMax) {
             std::lock_guard<std::mutex> g(_mu);
@@ -147,6 +149,7 @@ public:
         if (!l.items.empty()) {
             T* t = l.items.back();
             l.items.pop_back();
+            MRPC_TSAN_ACQUIRE(t);
             return t;
         }
         {
@@ -160,6 +163,7 @@ public:
         return new T;
     }
     void put(T* t) {
+        MRPC_TSAN_RELEASE(t);
         Local& l = local();
         if (l.items.size() < kLocalMax) {
             l.items.push_back(t);

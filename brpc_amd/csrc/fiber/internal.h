@@ -30,6 +30,10 @@ inline int futex_wake_private(void* addr, int nwake) {
 }
 
 // Chase-Lev work stealing deque. Owner push/pop at bottom, thieves steal top.
+// Slots are relaxed atomics: a thief reads slot `top` before its CAS decides
+// whether the read counted, and the owner may be rewriting that slot after a
+// wrap-around; the value of a failed steal is discarded, but the read must
+// still not be a data race (TSan flags it otherwise).
 template <typename T>
 class WorkStealingQueue {
 public:
@@ -37,13 +41,13 @@ public:
     ~WorkStealingQueue() { delete[] _buf; }
     void init(size_t cap) {
         _cap = cap;
-        _buf = new T[cap];
+        _buf = new std::atomic<T>[cap];
     }
     bool push(const T& x) {
         const size_t b = _bottom.load(std::memory_order_relaxed);
         const size_t t = _top.load(std::memory_order_acquire);
         if (b >= t + _cap) return false;
-        _buf[b & (_cap - 1)] = x;
+        _buf[b & (_cap - 1)].store(x, std::memory_order_relaxed);
         _bottom.store(b + 1, std::memory_order_release);
         return true;
     }
@@ -59,7 +63,7 @@ public:
             _bottom.store(b, std::memory_order_relaxed);
             return false;
         }
-        *val = _buf[nb & (_cap - 1)];
+        *val = _buf[nb & (_cap - 1)].load(std::memory_order_relaxed);
         if (t != nb) return true;
         const bool popped = _top.compare_exchange_strong(t, t + 1, std::memory_order_seq_cst, std::memory_order_relaxed);
         _bottom.store(b, std::memory_order_relaxed);
@@ -73,7 +77,7 @@ public:
             std::atomic_thread_fence(std::memory_order_seq_cst);
             b = _bottom.load(std::memory_order_acquire);
             if (t >= b) return false;
-            *val = _buf[t & (_cap - 1)];
+            *val = _buf[t & (_cap - 1)].load(std::memory_order_relaxed);
         } while (!_top.compare_exchange_strong(t, t + 1, std::memory_order_seq_cst, std::memory_order_relaxed));
         return true;
     }
@@ -86,7 +90,7 @@ public:
 private:
     std::atomic<size_t> _bottom;
     size_t _cap;
-    T* _buf;
+    std::atomic<T>* _buf;
     MRPC_CACHELINE_ALIGNED std::atomic<size_t> _top;
 };
 
@@ -129,8 +133,9 @@ struct TaskMeta {
     // so a late publish of an old sleep can never hide a newer timer.
     std::mutex sleep_mu;
     uint64_t sleep_gen = 0;
-    bool stop = false;
-    bool interrupted = false;
+    // set by other threads (stop/interrupt), read by the fiber's worker
+    std::atomic<bool> stop{false};
+    std::atomic<bool> interrupted{false};
     bool is_main = false;
     std::atomic<int>* version_butex = nullptr;  // current version of this slot
     fiber_t tid = 0;
@@ -217,7 +222,7 @@ public:
     bool is_current_main_task() const { return _cur_meta == _main_meta; }
     TaskControl* control() const { return _control; }
     int index() const { return _index; }
-    int64_t nswitch() const { return _nswitch; }
+    int64_t nswitch() const { return _nswitch.load(std::memory_order_relaxed); }
     int64_t idle_ns() const { return _idle_ns.load(std::memory_order_relaxed); }
 
     // public for the runtime's free functions
@@ -240,7 +245,7 @@ private:
     void* _last_arg = nullptr;
     int _num_nosignal = 0;
     int _remote_num_nosignal = 0;
-    int64_t _nswitch = 0;
+    std::atomic<int64_t> _nswitch{0};  // written by the owner, read by stats
     uint64_t _steal_seed;
     size_t _steal_offset;
     std::atomic<int64_t> _idle_ns{0};

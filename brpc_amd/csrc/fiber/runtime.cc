@@ -230,8 +230,8 @@ int TaskGroup::init(size_t rq_cap) {
         m->version_butex->store(1, std::memory_order_relaxed);
     }
     m->is_main = true;
-    m->stop = false;
-    m->interrupted = false;
+    m->stop.store(false, std::memory_order_relaxed);
+    m->interrupted.store(false, std::memory_order_relaxed);
     m->fn = nullptr;
     m->arg = nullptr;
     m->stack = nullptr;
@@ -324,7 +324,7 @@ void TaskGroup::sched_to_impl(TaskGroup** pg, TaskMeta* next, bool handover) {
         MRPC_TSAN_NEW_CONTEXT(next);
     }
     if (next != cur) {
-        ++g->_nswitch;
+        g->_nswitch.store(g->_nswitch.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
         g->_cur_meta = next;
         if (!handover) {
             void* fake_stack = nullptr;
@@ -660,8 +660,8 @@ int TaskGroup::start_background(fiber_t* th, const Attr* attr, FiberFn fn, void*
     }
     m->current_waiter.store(nullptr, std::memory_order_relaxed);
     m->current_sleep.store(0, std::memory_order_relaxed);
-    m->stop = false;
-    m->interrupted = false;
+    m->stop.store(false, std::memory_order_relaxed);
+    m->interrupted.store(false, std::memory_order_relaxed);
     m->is_main = false;
     m->fn = fn;
     m->arg = arg;
@@ -706,8 +706,8 @@ int TaskGroup::start_foreground(TaskGroup** pg, fiber_t* th, const Attr* attr, F
     }
     m->current_waiter.store(nullptr, std::memory_order_relaxed);
     m->current_sleep.store(0, std::memory_order_relaxed);
-    m->stop = false;
-    m->interrupted = false;
+    m->stop.store(false, std::memory_order_relaxed);
+    m->interrupted.store(false, std::memory_order_relaxed);
     m->is_main = false;
     m->fn = fn;
     m->arg = arg;

@@ -15,8 +15,11 @@
 #include "gpu/hbm_pool.h"
 
 DEFINE_bool(codec_fused, true,
-            "run codec batches of compress blocks and decode pieces (<= 8 KiB) as one fused launch of the "
-            "workgroup-parallel codec (gpu/codec_fused.hip) instead of serial per-stage kernels");
+            "run codec batches of compress blocks and decode pieces (<= 8 KiB) as one launch (compress, "
+            "decode and the last-piece pb scan together) instead of serial per-stage kernels");
+DEFINE_string(codec_fused_kernel, "waves",
+              "kernel of the one-launch codec batch: 'waves' (one wave per block/piece, snappy_kernels.hip) or "
+              "'workgroup' (one 1024-thread workgroup per block/piece, codec_fused.hip)");
 DEFINE_int32(codec_batch_max_inflight, 6,
              "codec batches in flight per device before the next one waits for a completion (0: no limit); "
              "while it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches");
@@ -274,7 +277,7 @@ bool launch(CBatch* b, int device) {
         fa.scan_n = b->scan_n.p;
         fa.max_fields = kCodecScanFields;
         fa.max_ulen = std::max(ncomp ? comp_max : 1u, nhpieces ? hpiece_max : 1u);
-        if (rc == 0) rc = LaunchFusedCodec(fa, s);
+        if (rc == 0) rc = FLAGS_codec_fused_kernel == "workgroup" ? LaunchFusedCodec(fa, s) : LaunchCodecWaves(fa, s);
         g_fused_launches.fetch_add(1, std::memory_order_relaxed);
         ncomp = nhpieces = nscan = 0;  // nothing left for the per-stage sequence below
     }

@@ -188,6 +188,10 @@ struct FusedCodecArgs {
     uint32_t max_ulen = 0;                  // >= every block's and piece's size
     uint32_t* stats = nullptr;  // optional, 4 device words: compress parse rounds (sum, max), decode (sum, max)
 };
+// The same batch as LaunchFusedCodec on one wave per block / piece (the
+// per-lane-segment compressor and the wave decoder of snappy_kernels.hip),
+// one launch; blocks and pieces up to kFusedMaxBlock.
+int LaunchCodecWaves(const FusedCodecArgs& a, hipStream_t s);
 int LaunchFusedCodec(const FusedCodecArgs& a, hipStream_t s);
 
 

@@ -48,6 +48,7 @@
 
 #include <algorithm>
 
+#include "gpu/device_pb.h"
 #include "gpu/kernels.h"
 
 namespace mrpc {
@@ -309,14 +310,12 @@ __device__ __forceinline__ void stamp(uint64_t* stamps, int blk, int lane, int i
     if (stamps && blk == 0 && lane == 0) stamps[i] = __builtin_amdgcn_s_memtime();
 }
 
-__global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(const SnappyPiece* __restrict__ pieces,
-                                                                             int n, uint32_t lo, uint32_t hi,
-                                                                             uint32_t cin_cap,
-                                                                             int* __restrict__ err,
-                                                                             uint64_t* __restrict__ stamps) {
+// One piece per wave; the body of snappy_decompress_pieces_par_kernel and of
+// the decode role of codec_waves_kernel (every exit is wave-uniform).
+__device__ __forceinline__ void decode_piece_wave(const SnappyPiece* __restrict__ pieces, int blk, uint32_t lo,
+                                                  uint32_t hi, uint32_t cin_cap, int* __restrict__ err,
+                                                  uint64_t* __restrict__ stamps) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int blk = blockIdx.x;
-    if (blk >= n) return;
     const int lane = threadIdx.x;
     const SnappyPiece pc = pieces[blk];
     if (pc.ulen == 0) {
@@ -525,6 +524,15 @@ __global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(con
     for (uint32_t o = vec_end + lane; o < ulen; o += kWave) dst[o] = cin[smap[o] & 0x7fff];
     stamp(stamps, blk, lane, 4);
     if (lane == 0) err[blk] = 0;
+}
+
+__global__ void __launch_bounds__(kWave) snappy_decompress_pieces_par_kernel(const SnappyPiece* __restrict__ pieces,
+                                                                             int n, uint32_t lo, uint32_t hi,
+                                                                             uint32_t cin_cap,
+                                                                             int* __restrict__ err,
+                                                                             uint64_t* __restrict__ stamps) {
+    if ((int)blockIdx.x >= n) return;
+    decode_piece_wave(pieces, (int)blockIdx.x, lo, hi, cin_cap, err, stamps);
 }
 
 // One wave per whole stream, cut at exact multiples of the piece limit: a
@@ -798,13 +806,13 @@ constexpr uint32_t kCandMax = 8192;
 // 112-block launch of text; the layouts stay dense.)
 __host__ __device__ constexpr uint32_t CompressInBytes(uint32_t in_cap, bool) { return in_cap; }
 __host__ __device__ constexpr uint32_t CompressCandBytes(uint32_t in_cap) { return 2 * in_cap + 16; }
+// One block per wave; the body of snappy_compress_kernel and of the
+// compress role of codec_waves_kernel.
 template <bool kOutLds, bool kCand>
-__global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob* __restrict__ jobs, int n,
-                                                                uint8_t* __restrict__ scratch,
-                                                                uint32_t* __restrict__ out_len,
-                                                                int* __restrict__ err, uint32_t in_cap,
-                                                                uint32_t slot_bytes,
-                                                                uint64_t* __restrict__ stamps) {
+__device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs, int blk,
+                                              uint8_t* __restrict__ scratch, uint32_t* __restrict__ out_len,
+                                              int* __restrict__ err, uint32_t in_cap, uint32_t slot_bytes,
+                                              uint64_t* __restrict__ stamps) {
     __shared__ uint16_t table[kCand ? 1 : kWave * kHashEntries];
     // kCand: an 11-bit earliest-position table (8 KiB): with the candidate
     // array replacing the per-lane tables, a 4 KiB block's workgroup fits in
@@ -814,8 +822,6 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
     __shared__ uint32_t sizes[kWave];
     __shared__ uint64_t spans[kWave * kLitSpans];  // deferred literal copies per lane
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    const int blk = blockIdx.x;
-    if (blk >= n) return;
     const int lane = threadIdx.x;
     const SnappyJob job = jobs[blk];
     const uint32_t ulen = (uint32_t)job.src_len;
@@ -1107,7 +1113,72 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
     stamp(stamps, blk, lane, 4);
 }
 
+template <bool kOutLds, bool kCand>
+__global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob* __restrict__ jobs, int n,
+                                                                uint8_t* __restrict__ scratch,
+                                                                uint32_t* __restrict__ out_len,
+                                                                int* __restrict__ err, uint32_t in_cap,
+                                                                uint32_t slot_bytes,
+                                                                uint64_t* __restrict__ stamps) {
+    if ((int)blockIdx.x >= n) return;
+    compress_wave<kOutLds, kCand>(jobs, (int)blockIdx.x, scratch, out_len, err, in_cap, slot_bytes, stamps);
+}
+
+// One launch per device-body codec batch, one wave per unit of work:
+// workgroups [0, ncomp) compress a block each, the rest decode a headerless
+// piece each, and the wave that finishes the last piece of a message scans
+// its protobuf fields (the group counter is reset for the batch's next
+// launch). The per-stage sequence it replaces ran compress, decompress and
+// pb-scan launches back to back on the batch's stream: ~31 + 33 + 5 us of
+// latency-bound kernels per batch, each wave far from filling its CU, so
+// sharing one dispatch halves the batch's device time while keeping the
+// small-footprint waves that pack 5 per CU (many batches in flight share
+// the chip; the 1024-thread workgroup codec of codec_fused.hip is faster
+// alone but holds a CU per block and loses when batches overlap).
+__global__ void __launch_bounds__(kWave) codec_waves_kernel(FusedCodecArgs a, uint32_t in_cap, uint32_t slot,
+                                                            uint32_t cin_cap, uint32_t phi) {
+    const int b = blockIdx.x;
+    if (b < a.ncomp) {
+        compress_wave<true, true>(a.comp, b, nullptr, a.comp_len, a.comp_err, in_cap, slot, nullptr);
+        return;
+    }
+    const int j = b - a.ncomp;
+    if (j >= a.npieces) return;
+    decode_piece_wave(a.pieces, j, 0, phi, cin_cap, a.piece_err, nullptr);
+    const uint32_t g = a.piece_group ? a.piece_group[j] : kFusedNoGroup;
+    if (g == kFusedNoGroup) return;
+    __shared__ int last;
+    __threadfence();  // this piece's bytes before the count
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&a.group_done[g], 1u) + 1 == a.group_pieces[g];
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // every other piece's bytes after the count
+    if (threadIdx.x == 0) {
+        a.group_done[g] = 0;
+        const PbScanJob sj = a.scans[g];
+        a.scan_n[g] = devpb::scan_message((devpb::gbyte_c*)sj.buf, 0, sj.len,
+                                          a.scan_fields + (uint64_t)g * a.max_fields * 2, a.max_fields);
+    }
+}
+
 }  // namespace
+
+int LaunchCodecWaves(const FusedCodecArgs& a, hipStream_t s) {
+    const int n = a.ncomp + a.npieces;
+    if (n <= 0) return 0;
+    const uint32_t mu = a.max_ulen ? a.max_ulen : 1;
+    if (mu > kCandMax || mu > kParMax) return -1;
+    const uint32_t in_cap = (mu + 15) & ~15u;
+    const uint32_t seg = (mu + kWave - 1) / kWave;
+    const uint32_t slot = (seg + 16 + 15) & ~15u;
+    const uint32_t comp_lds = CompressInBytes(in_cap, true) + kWave * slot + CompressCandBytes(in_cap);
+    const uint32_t cin_cap = (uint32_t)((SnappyMaxCompressedLength(mu) + 16 + 15) & ~15ull);
+    const uint32_t dec_lds = cin_cap + 2 * ((mu + 7) & ~7u) + 4 * kWave;
+    const uint32_t lds = std::max(a.ncomp ? comp_lds : 0u, a.npieces ? dec_lds : 0u);
+    hipLaunchKernelGGL(codec_waves_kernel, dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot, cin_cap, mu);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int LaunchSnappyDecompress(const SnappyJob* jobs_dev, int n, uint32_t max_ulen, uint32_t* out_len_dev, int* err_dev,
                            hipStream_t s) {

@@ -12,6 +12,7 @@
 #include "base/flags.h"
 #include "base/logging.h"
 #include "base/time.h"
+#include "base/tsan.h"
 #include "fiber/fiber.h"
 
 DEFINE_int32(event_dispatcher_num, 1, "Number of event dispatchers");
@@ -74,7 +75,12 @@ int EventDispatcher::AddConsumer(SocketId socket_id, int fd) {
     epoll_event evt;
     evt.events = EPOLLIN | EPOLLET | EPOLLRDHUP;
     evt.data.u64 = socket_id;
-    return epoll_ctl(_epfd, EPOLL_CTL_ADD, fd, &evt);
+    // epoll_ctl/epoll_pwait2 order the socket's setup before its first
+    // event; tell TSan (it does not intercept epoll_pwait2)
+    MRPC_TSAN_RELEASE(&_epfd);
+    const int rc = epoll_ctl(_epfd, EPOLL_CTL_ADD, fd, &evt);
+    MRPC_TSAN_RELEASE(&_epfd);  // and the fd access of epoll_ctl before a close after the first event
+    return rc;
 }
 
 int EventDispatcher::RemoveConsumer(int fd) {
@@ -86,6 +92,7 @@ int EventDispatcher::AddEpollOut(SocketId socket_id, int fd, bool pollin) {
     epoll_event evt;
     evt.data.u64 = socket_id;
     evt.events = EPOLLOUT | EPOLLET;
+    MRPC_TSAN_RELEASE(&_epfd);
     if (pollin) {
         evt.events |= EPOLLIN | EPOLLRDHUP;
         return epoll_ctl(_epfd, EPOLL_CTL_MOD, fd, &evt);
@@ -146,7 +153,10 @@ void EventDispatcher::Run() {
             n = epoll_wait(_epfd, e, 32, -1);
         }
         if (_stop) break;
-        if (n > 0) last_event_ns = monotonic_ns();
+        if (n > 0) {
+            last_event_ns = monotonic_ns();
+            MRPC_TSAN_ACQUIRE(&_epfd);
+        }
         if (n < 0) {
             if (errno == EINTR) continue;
             PLOG(ERROR) << "epoll_wait";

@@ -5,6 +5,8 @@
 // keeping the read on the core that took the interrupt.
 #pragma once
 
+#include <atomic>
+
 #include <cstdint>
 
 #include "net/socket.h"
@@ -31,7 +33,7 @@ private:
     void Run();
     int _epfd;
     int _wakeup_fds[2];
-    bool _stop;
+    std::atomic<bool> _stop;
     fiber::fiber_t _tid;
 };
 

@@ -172,7 +172,7 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
     m->_write_head.store(nullptr, std::memory_order_relaxed);
     m->_unwritten_bytes.store(0, std::memory_order_relaxed);
     m->_last_active_us.store(monotonic_us(), std::memory_order_relaxed);
-    m->_error_code = 0;
+    m->_error_code.store(0, std::memory_order_relaxed);
     m->_error_text.clear();
     m->_preferred_index = -1;
     m->_parsing_context.store(nullptr, std::memory_order_relaxed);
@@ -193,6 +193,7 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
         m->_transport.reset();
     }
     // One reference held until SetFailed().
+    const SocketId sid = m->_this_id;  // once registered, the socket may fail and be reused before we return
     m->_versioned_ref.store(make_vref(ver, 1), std::memory_order_release);
     if (m->ResetFileDescriptor(opt.fd) != 0) {
         const int saved = errno;
@@ -200,7 +201,7 @@ int Socket::Create(const SocketOptions& opt, SocketId* id) {
         return -1;
     }
     g_nsocket.fetch_add(1, std::memory_order_relaxed);
-    *id = m->_this_id;
+    *id = sid;
     return 0;
 }
 
@@ -314,7 +315,7 @@ int Socket::SetFailed(int error_code, const char* fmt, ...) {
     std::shared_ptr<Transport> tr;
     {
         std::lock_guard<std::mutex> g(_mu);
-        _error_code = error_code;
+        _error_code.store(error_code, std::memory_order_relaxed);
         _error_text = text.empty() ? ErrorText(error_code) : text;
         tr = _transport;
     }
@@ -725,7 +726,8 @@ void Socket::ReturnFailedWriteRequest(WriteRequest* req, int error_code, const s
 }
 
 void Socket::ReleaseAllFailedWriteRequests(WriteRequest* req) {
-    const int error_code = _error_code ? _error_code : EFAILEDSOCKET;
+    const int saved_ec = _error_code.load(std::memory_order_relaxed);
+    const int error_code = saved_ec ? saved_ec : EFAILEDSOCKET;
     const std::string text = error_text();
     do {
         // release all but the last connected request
@@ -777,7 +779,8 @@ int Socket::Write(Buf* data, const WriteOptions* options) {
     // an empty write only matters as a half-close after what is queued
     if (data->empty() && !opt.shutdown_write_after) return 0;
     if (Failed()) {
-        const int ec = _error_code ? _error_code : EFAILEDSOCKET;
+        const int saved_ec = _error_code.load(std::memory_order_relaxed);
+        const int ec = saved_ec ? saved_ec : EFAILEDSOCKET;
         if (opt.id_wait != fiber::INVALID_CALL_ID) fiber::call_id_error(opt.id_wait, ec, error_text());
         errno = ec;
         if (opt.auth_winner) SetAuthentication(ec);
@@ -1110,7 +1113,7 @@ int Socket::Revive(int new_fd) {
     }
     {
         std::lock_guard<std::mutex> g(_mu);
-        _error_code = 0;
+        _error_code.store(0, std::memory_order_relaxed);
         _error_text.clear();
     }
     if (new_fd >= 0) ResetFileDescriptor(new_fd);

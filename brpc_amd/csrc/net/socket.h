@@ -156,7 +156,7 @@ public:
     int SetFailed(int error_code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
     int SetFailed();
     bool Failed() const;
-    int error_code() const { return _error_code; }
+    int error_code() const { return _error_code.load(std::memory_order_relaxed); }
     std::string error_text() const;
     // Ask the socket to be recycled once no one references it (for sockets
     // created with health checking; see ReleaseAdditionalReference in ref).
@@ -287,7 +287,9 @@ private:
     std::atomic<int64_t> _unwritten_bytes;
     std::atomic<int>* _epollout_butex;
     std::atomic<int64_t> _last_active_us;
-    int _error_code;
+    // set after the version bump that marks the socket failed: a reader that
+    // sees Failed() before it lands falls back to EFAILEDSOCKET
+    std::atomic<int> _error_code;
     std::string _error_text;
     mutable std::mutex _mu;  // protects transport, error text, pool
     std::shared_ptr<Transport> _transport;

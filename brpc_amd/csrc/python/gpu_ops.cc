@@ -279,8 +279,37 @@ void bind_gpu_ops(py::module_& g) {
             const double old_dec_us = time_launches(
                 [&] { gpu::LaunchSnappyDecompressPieces(pieces.as<gpu::SnappyPiece>(), n, 0, block, perr.as<int>(), s); },
                 iters, s);
+            // the one-launch wave codec on the same batch (its compress half
+            // writes cmp2, its decode half reads the workgroup codec's cmp)
+            gpu::FusedCodecArgs fw = fm;
+            fw.comp_len = lens2.as<uint32_t>();
+            fw.comp_err = errs2.as<int>();
+            fw.stats = nullptr;
+            const double waves_mixed_us = time_launches([&] { gpu::LaunchCodecWaves(fw, s); }, iters, s);
+            // throughput when batches overlap, as on the RPC path (several
+            // batches in flight on the pool's streams): 4 streams, one mixed
+            // launch each per round
+            hipStream_t ss[4];
+            for (auto& x : ss) hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
+            auto overlapped = [&](auto launch) {
+                for (auto& x : ss) launch(x);
+                for (auto& x : ss) hipStreamSynchronize(x);
+                const int64_t t0 = monotonic_us();
+                for (int it = 0; it < iters; ++it)
+                    for (auto& x : ss) launch(x);
+                for (auto& x : ss) hipStreamSynchronize(x);
+                return (double)(monotonic_us() - t0) / iters;
+            };
+            gpu::FusedCodecArgs fm2 = fm;
+            fm2.stats = nullptr;
+            const double fused_x4_us = overlapped([&](hipStream_t x) { gpu::LaunchFusedCodec(fm2, x); });
+            const double waves_x4_us = overlapped([&](hipStream_t x) { gpu::LaunchCodecWaves(fw, x); });
+            for (auto& x : ss) hipStreamDestroy(x);
             hipStreamDestroy(s);
             py::gil_scoped_acquire gil;
+            out["waves_mixed_us"] = waves_mixed_us;
+            out["fused_mixed_x4_us"] = fused_x4_us;
+            out["waves_mixed_x4_us"] = waves_x4_us;
             const uint64_t launches = (uint64_t)iters + 1;
             out["blocks"] = n;
             out["fused_compress_us"] = comp_us;

@@ -703,6 +703,7 @@ SelectiveChannel::Call::Attempt* SelectiveChannel::Call::prepare(int idx) {
     ++inflight;
     ++attempts;
     tried.push_back(idx);
+    a->sub_cntl.call_id();  // created now, so a cancel between here and issue() reaches it
     live.push_back(&a->sub_cntl);
     return a;
 }
@@ -809,15 +810,20 @@ static int OnSelectiveError(fiber::CallId id, void* data, int error_code, const 
     // canceled: cancel the attempts in flight; the last one to return
     // finishes the call with ECANCELED (the id is released first, an
     // attempt may complete inline)
-    std::vector<Controller*> live;
+    // an attempt may end (and free its controller) as soon as `mu` is
+    // released: take the ids of the calls in flight, not the controllers,
+    // and cancel by id (a stale id is a no-op)
+    std::vector<fiber::CallId> live;
     c->refs.fetch_add(1);
     {
         std::lock_guard<std::mutex> g(c->mu);
         c->canceled = true;
-        live = c->live;
+        for (Controller* sc : c->live) live.push_back(sc->inflight_call_id());
     }
     fiber::call_id_unlock(id);
-    for (Controller* sc : live) sc->StartCancel();
+    for (fiber::CallId sid : live) {
+        if (sid.value) StartCancel(sid);
+    }
     c->unref();
     return 0;
 }

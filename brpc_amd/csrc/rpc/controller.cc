@@ -1,4 +1,5 @@
 #include "rpc/controller.h"
+#include "rpc/stream_internal.h"
 
 #include <cerrno>
 #include <cstdarg>
@@ -354,6 +355,7 @@ void Controller::EndRPC(fiber::CallId id) {
         OnCallComplete(&_current_call, ECANCELED, false);
     }
     _end_us = monotonic_us();
+    if (_request_stream != INVALID_STREAM_ID) OnRequestStreamCallEnded(_request_stream);
     if (_span) Span::EndClientSpan(_span, this);
     if (_on_end) _on_end(this);
     Closure* done = _done;

@@ -117,6 +117,11 @@ public:
     bool is_server_side() const { return _server != nullptr; }
     void Reset() override;
     fiber::CallId call_id();  // correlation id (creates it on first use)
+    // the id of the call in flight, 0 once it ended; safe to read while the
+    // call ends on another thread (no id is created)
+    fiber::CallId inflight_call_id() const {
+        return fiber::CallId{__atomic_load_n(&_correlation_id.value, __ATOMIC_ACQUIRE)};
+    }
     void Join();              // wait for an async RPC to finish
 
     // ---------------- cancellation

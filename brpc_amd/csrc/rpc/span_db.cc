@@ -69,7 +69,8 @@ public:
         std::unique_lock<std::mutex> g(_qmu);
         if (!_started) return;
         const uint64_t target = _enqueued_seq + _queue.size();
-        _flush_cv.wait_for(g, std::chrono::seconds(5), [&] { return _done_seq >= target; });
+        _flush_cv.wait_until(g, std::chrono::system_clock::now() + std::chrono::seconds(5),
+                             [&] { return _done_seq >= target; });
     }
 
     std::vector<std::string> find_trace(uint64_t trace, size_t max) {
@@ -227,7 +228,13 @@ private:
             std::deque<SpanRecord*> batch;
             {
                 std::unique_lock<std::mutex> g(_qmu);
-                _qcv.wait_for(g, std::chrono::seconds(1), [&] { return !_queue.empty(); });
+                // system_clock deadlines: steady-clock waits go through
+                // pthread_cond_clockwait, which the toolchain's TSan runtime
+                // does not intercept (it then sees _qmu held for good and
+                // reports every later lock as a double lock); a clock step
+                // only stretches or shortens one poll
+                _qcv.wait_until(g, std::chrono::system_clock::now() + std::chrono::seconds(1),
+                                [&] { return !_queue.empty(); });
                 batch.swap(_queue);
                 _enqueued_seq += batch.size();
             }

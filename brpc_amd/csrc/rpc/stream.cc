@@ -423,6 +423,18 @@ void OnResponseStreamSettings(Controller* cntl, Socket* host, const StreamSettin
     if (!s->connected) mark_connected(s, host->id(), st.stream_id(), st.need_feedback());
 }
 
+void OnRequestStreamCallEnded(StreamId sid) {
+    {
+        std::unique_lock<std::mutex> lk;
+        StreamObj* s = lock_stream(sid, &lk);
+        if (!s || s->connected || s->closed) return;
+    }
+    // the call ended (failed, or the server never accepted the stream): a
+    // stream no peer will ever connect to is closed, so its writer and its
+    // handler's on_closed learn now instead of never
+    StreamClose(sid);
+}
+
 int StreamCreate(StreamId* request_stream, Controller& cntl, const StreamOptions* options) {
     if (cntl._request_stream != INVALID_STREAM_ID) {
         LOG(ERROR) << "Can't create more than one stream on a controller";

@@ -16,6 +16,8 @@ void OnRequestStreamSettings(Controller* cntl, Socket* host, const StreamSetting
 void OnServerStreamCreated(StreamId sid, SocketId host);
 // client: response carried server stream settings -> connect
 void OnResponseStreamSettings(Controller* cntl, Socket* host, const StreamSettings& s);
+// client: the call carrying the stream ended; close it if it never connected
+void OnRequestStreamCallEnded(StreamId sid);
 void RegisterStreamingProtocol();
 
 }  // namespace mrpc

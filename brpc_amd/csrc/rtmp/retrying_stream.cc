@@ -43,6 +43,10 @@ namespace {
 class SubStream : public RtmpClientStream {
 public:
     explicit SubStream(std::weak_ptr<RtmpRetryingClientStream::Impl> i) : _impl(std::move(i)) {}
+    // detach from the connection before this class's part is destroyed: a
+    // status or stop callback racing with ~RtmpClientStream would otherwise
+    // dispatch through a half-destroyed object
+    ~SubStream() override { Destroy(); }
     std::atomic<bool> by_owner{false};
 
     void OnMetaData(RtmpMetaData* md, const std::string& name) override {
@@ -145,8 +149,11 @@ void RtmpRetryingClientStream::Impl::Collect() {
         subs.swap(retired);
         clients.swap(retired_clients);
     }
-    for (auto& s : subs) s->by_owner.store(true);
-    subs.clear();  // ~RtmpClientStream -> Destroy (deleteStream if still open)
+    for (auto& s : subs) {
+        s->by_owner.store(true);
+        s->Destroy();  // deleteStream if still open; no callback runs once it returns
+    }
+    subs.clear();
     clients.clear();
 }
 

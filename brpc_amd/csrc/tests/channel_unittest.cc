@@ -71,8 +71,10 @@ private:
 
 // Three servers (optionally requiring authentication).
 struct Cluster {
-    std::vector<std::unique_ptr<Server>> servers;
+    // services outlive the servers: handlers still sleeping in Echo when a
+    // test ends are joined by ~Cluster before their service goes away
     std::vector<std::unique_ptr<TaggedEcho>> services;
+    std::vector<std::unique_ptr<Server>> servers;
     std::vector<int> ports;
     Auth auth;
     explicit Cluster(bool with_auth = false, int n = 3) {
@@ -85,6 +87,12 @@ struct Cluster {
             if (with_auth) o.auth = &auth;
             servers.back()->Start("127.0.0.1:0", &o);
             ports.push_back(servers.back()->listen_port());
+        }
+    }
+    ~Cluster() {
+        for (auto& s : servers) {
+            s->Stop(0);
+            s->Join();
         }
     }
     std::string addr(int i) const { return "127.0.0.1:" + std::to_string(ports[i]); }

@@ -172,8 +172,8 @@ TEST(FiberDepth, many_sleepers_never_wake_early) {
     std::vector<int64_t> sorted = late;
     std::sort(sorted.begin(), sorted.end());
     EXPECT_GE(sorted.front(), 0);             // never early
-    EXPECT_LT(sorted[n / 2], 5000);           // median lateness well under the 100 us .. ms range
-    EXPECT_LT(sorted.back(), 500000);
+    EXPECT_LT(sorted[n / 2], 5000 * mtest::kSlowdown);  // median lateness well under the 100 us .. ms range
+    EXPECT_LT(sorted.back(), 500000 * mtest::kSlowdown);
 }
 
 TEST(FiberDepth, fd_timedwait_times_out_then_sees_data) {

@@ -169,7 +169,7 @@ rdma::QpAddress BogusAddress() {
     return a;
 }
 
-std::string g_last_error;
+thread_local std::string g_last_error;  // the calling thread's last failure (tests call from many threads)
 
 bool Echo(ChannelBase* ch, const std::string& msg, int* code = nullptr, int64_t sleep_us = 0) {
     example::EchoService_Stub stub(ch);

@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -34,11 +35,14 @@ public:
         ClosureGuard g(done);
         Controller* cntl = static_cast<Controller*>(c);
         ++calls;
-        last_log_id = cntl->log_id();
-        last_remote = cntl->remote_side().to_string();
-        last_local = cntl->local_side().to_string();
-        last_req_compress = (int)cntl->request_compress_type();
-        server_side = cntl->is_server_side();
+        {
+            std::lock_guard<std::mutex> lk(mu);  // concurrent calls land here together
+            last_log_id = cntl->log_id();
+            last_remote = cntl->remote_side().to_string();
+            last_local = cntl->local_side().to_string();
+            last_req_compress = (int)cntl->request_compress_type();
+            server_side = cntl->is_server_side();
+        }
         if (req->sleep_us() > 0) fiber::usleep((uint64_t)req->sleep_us());
         if (req->server_fail()) {
             cntl->SetFailed(req->code() ? req->code() : EINTERNAL, "asked to fail");
@@ -49,6 +53,7 @@ public:
         if (req->code() > 0) cntl->set_response_compress_type((CompressType)req->code());
     }
     std::atomic<int> calls{0};
+    std::mutex mu;
     uint64_t last_log_id = 0;
     std::string last_remote, last_local;
     int last_req_compress = -1;
@@ -56,13 +61,17 @@ public:
 };
 
 struct Fixture {
+    InspectEcho echo;  // outlives the server
     Server server;
-    InspectEcho echo;
     int port = 0;
     explicit Fixture(ServerOptions o = ServerOptions()) {
         server.AddService(&echo, SERVER_DOESNT_OWN_SERVICE);
         o.has_builtin_services = false;
         if (server.Start("127.0.0.1:0", &o) == 0) port = server.listen_port();
+    }
+    ~Fixture() {
+        server.Stop(0);
+        server.Join();
     }
     std::string addr() const { return "127.0.0.1:" + std::to_string(port); }
 };

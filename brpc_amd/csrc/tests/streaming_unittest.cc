@@ -1,7 +1,10 @@
 // Streaming RPC behaviour (spirit of the reference's
 // test/brpc_streaming_rpc_unittest.cpp): bidirectional ping-pong, writer
 // backpressure with the async StreamWait, idle timeouts, close from either
-// side, and streams ending with their host connection.
+// side, streams ending with their host connection, an offer the server never
+// accepts, order across many sizes, and data the server writes before its
+// response leaves (reference test/brpc_streaming_rpc_unittest.cpp: sanity,
+// received_in_order, server_send_data_before_run_done).
 #include <unistd.h>
 
 #include <atomic>
@@ -66,6 +69,10 @@ public:
         StreamOptions so;
         so.handler = r.get();
         const std::string& mode = req->message();
+        if (mode == "noaccept") {  // the stream the client offered is never accepted
+            res->set_message(mode);
+            return;
+        }
         if (mode == "pong") r->pong = true;
         if (mode == "slow") {  // a reader that consumes one message per 20 ms
             r->sleep_per_batch_us = 20000;
@@ -81,6 +88,15 @@ public:
             std::lock_guard<std::mutex> lk(mu);
             recorders.push_back(r);
             sids.push_back(sid);
+        }
+        if (mode == "early") {
+            // data written before the response (done->Run) leaves: it must
+            // reach the client after the stream is established, in order
+            for (int i = 0; i < 3; ++i) {
+                Buf b;
+                b.append("early-" + std::to_string(i));
+                if (StreamWrite(sid, b) != 0) r->write_errors.fetch_add(1);
+            }
         }
         if (mode == "close") {
             fiber::start([sid] {
@@ -289,4 +305,72 @@ TEST(StreamingRpc, streams_end_with_their_connection) {
     b.append("after");
     EXPECT_NE(StreamWrite(sid, b), 0);
     StreamClose(sid);  // closing twice is harmless
+}
+
+TEST(StreamingRpc, sanity_stream_the_server_never_accepts_closes) {
+    Fixture f;
+    ASSERT_TRUE(f.ok);
+    Recorder client;
+    const StreamId sid = f.open("noaccept", &client);
+    ASSERT_NE(sid, INVALID_STREAM_ID);  // the RPC itself succeeded
+    EXPECT_TRUE(wait_until([&] { return client.closed.load(); }));
+    EXPECT_FALSE(StreamIsConnected(sid));
+    Buf b;
+    b.append("nobody listens");
+    EXPECT_NE(StreamWrite(sid, b), 0);
+    StreamClose(sid);
+}
+
+TEST(StreamingRpc, received_in_order_across_sizes) {
+    Fixture f;
+    ASSERT_TRUE(f.ok);
+    Recorder client;
+    const StreamId sid = f.open("plain", &client);
+    ASSERT_NE(sid, INVALID_STREAM_ID);
+    // 600 messages of 1 B .. 20 KiB, written back to back (small ones get
+    // batched, large ones span several Buf blocks): the reader sees exactly
+    // the written sequence
+    std::vector<std::string> sent;
+    uint32_t x = 12345;
+    for (int i = 0; i < 600; ++i) {
+        x = x * 1103515245u + 12345u;
+        const size_t len = 1 + (x >> 8) % (i % 50 == 0 ? 20000 : 300);
+        std::string m = std::to_string(i) + ":" + std::string(len, (char)('a' + i % 26));
+        Buf b;
+        b.append(m);
+        while (StreamWrite(sid, b) == EAGAIN) {
+            timespec due = realtime_after_us(1000000);
+            StreamWait(sid, &due);
+        }
+        sent.push_back(std::move(m));
+    }
+    auto srv = f.svc.last();
+    ASSERT_TRUE(wait_until([&] { return srv->count() == sent.size(); }, 10000000));
+    {
+        std::lock_guard<std::mutex> g(srv->mu);
+        for (size_t i = 0; i < sent.size(); ++i) {
+            if (srv->got[i] != sent[i]) {
+                EXPECT_EQ(srv->got[i].substr(0, 16), sent[i].substr(0, 16));
+                break;
+            }
+        }
+    }
+    StreamClose(sid);
+    EXPECT_TRUE(wait_until([&] { return client.closed.load(); }));
+}
+
+TEST(StreamingRpc, server_sends_data_before_its_response) {
+    Fixture f;
+    ASSERT_TRUE(f.ok);
+    Recorder client;
+    const StreamId sid = f.open("early", &client);
+    ASSERT_NE(sid, INVALID_STREAM_ID);
+    ASSERT_TRUE(wait_until([&] { return client.count() == 3; }));
+    {
+        std::lock_guard<std::mutex> g(client.mu);
+        for (int i = 0; i < 3; ++i) EXPECT_EQ(client.got[i], "early-" + std::to_string(i));
+    }
+    EXPECT_EQ(f.svc.last()->write_errors.load(), 0);
+    StreamClose(sid);
+    EXPECT_TRUE(wait_until([&] { return client.closed.load(); }));
 }

@@ -14,6 +14,14 @@
 
 namespace mtest {
 
+// Wall-clock bounds of timing tests are multiplied by this under the
+// sanitizers (TSan runs code 5-15x slower and serialises on its shadow)
+#if defined(__SANITIZE_THREAD__) || defined(__SANITIZE_ADDRESS__)
+constexpr int kSlowdown = 20;
+#else
+constexpr int kSlowdown = 1;
+#endif
+
 struct TestCase {
     const char* suite;
     const char* name;

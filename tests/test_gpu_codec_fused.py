@@ -1,9 +1,12 @@
-"""Fused workgroup-parallel codec (gpu/codec_fused.hip) behind the device
-payload codec: every block it writes is a standard raw snappy stream (the
-host codec decodes it), the device decoder rebuilds the payload from it,
-its ratio is at least the per-lane-segment compressor's, and malformed
-pieces are refused without hanging. Numerics against the host snappy codec
-(base/snappy.cc) and numpy byte equality."""
+"""One-launch codec batches behind the device payload codec, both kernels:
+'waves' (codec_waves_kernel, snappy_kernels.hip: one wave per block/piece)
+and 'workgroup' (codec_fused.hip: one 1024-thread workgroup per block/piece).
+Every block either writes is a standard raw snappy stream (the host codec
+decodes it), the device decoder rebuilds the payload from it, the workgroup
+codec's ratio is at least the per-lane-segment compressor's, the last piece
+of a message scans its fields, and malformed pieces are refused without
+hanging. Numerics against the host snappy codec (base/snappy.cc) and numpy
+byte equality."""
 import random
 
 import pytest
@@ -25,6 +28,10 @@ def _restore_flags(native):
     yield
     native.set_flag("device_payload_block_kb", "2")
     native.set_flag("codec_fused", "true")
+    native.set_flag("codec_fused_kernel", "waves")
+
+
+KERNELS = ["waves", "workgroup"]
 
 
 def _corpus(kind, n, seed):
@@ -80,10 +87,12 @@ def _roundtrip(native, data, scan=False):
     return sum(clen), nf, fields
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("kb", [1, 2, 4, 8])
 @pytest.mark.parametrize("kind", ["text", "random", "runs", "mixed", "const"])
 @pytest.mark.parametrize("size", [1, 5, 63, 64, 65, 4095, 4096, 4097, 65536, 100003])
-def test_fused_blocks_round_trip(native, kb, kind, size):
+def test_fused_blocks_round_trip(native, kernel, kb, kind, size):
+    native.set_flag("codec_fused_kernel", kernel)
     native.set_flag("device_payload_block_kb", str(kb))
     before = native.gpu.codec_batch_stats()["fused_launches"]
     _roundtrip(native, _corpus(kind, size, size * 31 + kb))
@@ -95,6 +104,7 @@ def test_fused_ratio_not_worse_than_lane_segments(native, kb):
     """The block-wide parse finds matches across the old per-lane segment
     ends: on text its output is at most the lane-segment compressor's."""
     native.set_flag("device_payload_block_kb", str(kb))
+    native.set_flag("codec_fused_kernel", "workgroup")
     data = _corpus("text", 1 << 18, 7)
     fused, _, _ = _roundtrip(native, data)
     native.set_flag("codec_fused", "false")
@@ -103,7 +113,9 @@ def test_fused_ratio_not_worse_than_lane_segments(native, kb):
     assert len(data) / fused > 2.0
 
 
-def test_fused_scan_runs_after_the_last_piece(native):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_fused_scan_runs_after_the_last_piece(native, kernel):
+    native.set_flag("codec_fused_kernel", kernel)
     native.set_flag("device_payload_block_kb", "4")
     body = native.echo_body("text", 50000)
     msg = bytes([0x0A]) + _varint(len(body)) + body + bytes([0x18, 0x01])
@@ -115,11 +127,13 @@ def test_fused_scan_runs_after_the_last_piece(native):
         assert fields[2] == (3 << 3) | 0 and fields[3] == 1
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("seed", range(6))
-def test_fused_decoder_refuses_corrupt_pieces(native, seed):
+def test_fused_decoder_refuses_corrupt_pieces(native, kernel, seed):
     """Random byte damage in a compressed block: the decode reports an
     error or (if the damage left a valid stream) returns bytes; it never
     hangs or writes outside its block."""
+    native.set_flag("codec_fused_kernel", kernel)
     native.set_flag("device_payload_block_kb", "4")
     dev = torch.device("cuda", 0)
     data = _corpus("mixed", 40000, seed)

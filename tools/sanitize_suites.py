@@ -16,6 +16,8 @@ import subprocess
 import sys
 import tempfile
 
+SUPP = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tsan.supp")
+
 
 def suites(binary):
     out = subprocess.run([binary, "--list"], capture_output=True, text=True, timeout=120).stdout
@@ -30,7 +32,7 @@ def suites(binary):
 def run_suite(binary, suite, kind, timeout):
     env = dict(os.environ)
     if kind == "tsan":
-        env["TSAN_OPTIONS"] = "halt_on_error=0 report_signal_unsafe=0 second_deadlock_stack=1"
+        env["TSAN_OPTIONS"] = "halt_on_error=0 report_signal_unsafe=0 second_deadlock_stack=1 suppressions=" + SUPP
         pat = "WARNING: ThreadSanitizer"
     else:
         env["ASAN_OPTIONS"] = "detect_leaks=0"
@@ -57,7 +59,7 @@ def run_planes(tree, kind):
     out = []
     for nranks, extra in ((2, []), (3, []), (8, ["--calls", "40,4"])):
         env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", LD_PRELOAD=lib,
-                   TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0", ASAN_OPTIONS="detect_leaks=0")
+                   TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 suppressions=" + SUPP, ASAN_OPTIONS="detect_leaks=0")
         with tempfile.TemporaryDirectory() as d:
             try:
                 r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
