@@ -348,11 +348,17 @@ bool base64_decode(const std::string& in, std::string* out) {
     out->clear();
     uint32_t acc = 0;
     int bits = 0;
+    size_t n = 0, pad = 0;
     for (char c : in) {
-        if (c == '=') break;
         if (c == '\n' || c == '\r' || c == ' ') continue;
+        if (c == '=') {
+            ++pad;
+            continue;
+        }
+        if (pad) return false;  // data after padding
         int v = rev[(uint8_t)c];
         if (v < 0) return false;
+        ++n;
         acc = (acc << 6) | (uint32_t)v;
         bits += 6;
         if (bits >= 8) {
@@ -360,6 +366,9 @@ bool base64_decode(const std::string& in, std::string* out) {
             out->push_back((char)((acc >> bits) & 0xff));
         }
     }
+    // a lone trailing symbol carries no whole byte; padding, when present,
+    // completes a 4-symbol group (unpadded input is accepted)
+    if (n % 4 == 1 || pad > 2 || (pad && (n + pad) % 4 != 0)) return false;
     return true;
 }
 

@@ -280,3 +280,141 @@ TEST(Json2pbDepth, enums_by_name_and_number) {
     EXPECT_EQ(n.color(), test::BLUE);
     EXPECT_TRUE(has(to_json(n), "\"color\":\"BLUE\""));
 }
+
+TEST(Json2pbDepth, bytes_are_base64_both_ways_by_default) {
+    test::Rich r;
+    r.set_must("m");
+    r.set_raw(std::string("\x00\xff\x10" "binary" "\x80", 10));
+    const std::string j = to_json(r);
+    EXPECT_TRUE_M(has(j, "\"raw\":\"AP8QYmluYXJ5gA==\""), std::string(j));
+    test::Rich back;
+    ASSERT_TRUE(to_pb(j, &back));
+    EXPECT_EQ(back.raw(), r.raw());
+    // both directions switched off: the bytes travel as a JSON string
+    json2pb::Pb2JsonOptions po;
+    po.bytes_to_base64 = false;
+    test::Rich t;
+    t.set_must("m");
+    t.set_raw("plain text");
+    const std::string jt = to_json(t, po);
+    EXPECT_TRUE_M(has(jt, "\"raw\":\"plain text\""), std::string(jt));
+    json2pb::Json2PbOptions jo;
+    jo.base64_to_bytes = false;
+    test::Rich tb;
+    ASSERT_TRUE(to_pb(jt, &tb, nullptr, jo));
+    EXPECT_EQ(tb.raw(), "plain text");
+}
+
+TEST(Json2pbDepth, invalid_base64_is_refused) {
+    const char* bad[] = {"{\"must\":\"m\",\"raw\":\"@@@@\"}", "{\"must\":\"m\",\"raw\":\"QUJD=\"}",
+                         "{\"must\":\"m\",\"raw\":12}"};
+    for (const char* j : bad) {
+        test::Rich r;
+        std::string err;
+        const bool ok = to_pb(j, &r, &err);
+        EXPECT_FALSE_M(err.empty(), std::string(j));
+        if (ok) EXPECT_FALSE_M(r.has_raw(), std::string(j));
+    }
+}
+
+TEST(Json2pbDepth, always_print_primitive_fields) {
+    test::Rich r;
+    r.set_must("m");
+    json2pb::Pb2JsonOptions o;
+    EXPECT_FALSE(has(to_json(r, o), "\"i32\""));
+    o.always_print_primitive_fields = true;
+    const std::string j = to_json(r, o);
+    EXPECT_TRUE_M(has(j, "\"i32\":0"), std::string(j));
+    EXPECT_TRUE_M(has(j, "\"flag\":false"), std::string(j));
+    EXPECT_TRUE_M(has(j, "\"s\":\"\""), std::string(j));
+    // the defaults parse back to equal values
+    test::Rich back;
+    ASSERT_TRUE(to_pb(j, &back));
+    EXPECT_EQ(back.i32(), 0);
+    EXPECT_EQ(back.s(), "");
+}
+
+TEST(Json2pbDepth, empty_repeated_fields_on_request) {
+    test::Rich r;
+    r.set_must("m");
+    EXPECT_FALSE(has(to_json(r), "\"nums\""));
+    json2pb::Pb2JsonOptions o;
+    o.jsonify_empty_array = true;
+    const std::string j = to_json(r, o);
+    EXPECT_TRUE_M(has(j, "\"nums\":[]"), std::string(j));
+    EXPECT_TRUE_M(has(j, "\"inners\":[]"), std::string(j));
+    test::Rich back;
+    ASSERT_TRUE(to_pb(j, &back));
+    EXPECT_EQ(back.nums_size(), 0);
+}
+
+TEST(Json2pbDepth, enums_printed_as_numbers_on_request) {
+    test::Rich r;
+    r.set_must("m");
+    r.set_color(test::BLUE);
+    EXPECT_TRUE(has(to_json(r), "\"color\":\"BLUE\""));
+    json2pb::Pb2JsonOptions o;
+    o.enum_option_as_string = false;
+    const std::string j = to_json(r, o);
+    EXPECT_TRUE_M(has(j, "\"color\":2"), std::string(j));
+    test::Rich back;
+    ASSERT_TRUE(to_pb(j, &back));
+    EXPECT_EQ(back.color(), test::BLUE);
+}
+
+TEST(Json2pbDepth, repeated_messages_and_strings_round_trip) {
+    test::Rich r;
+    r.set_must("m");
+    for (int i = 0; i < 40; ++i) {
+        test::Inner* in = r.add_inners();
+        in->set_x(i * i - 7);
+        for (int k = 0; k < i % 4; ++k) in->add_tags("t" + std::to_string(i) + "\"q\\" + std::to_string(k));
+    }
+    const std::string j = to_json(r);
+    test::Rich back;
+    ASSERT_TRUE(to_pb(j, &back));
+    ASSERT_EQ(back.inners_size(), 40);
+    for (int i = 0; i < 40; ++i) {
+        EXPECT_EQ(back.inners(i).x(), i * i - 7);
+        ASSERT_EQ(back.inners(i).tags_size(), i % 4);
+        for (int k = 0; k < i % 4; ++k) EXPECT_EQ(back.inners(i).tags(k), r.inners(i).tags(k));
+    }
+}
+
+TEST(Json2pbDepth, infinities_both_ways) {
+    test::Rich r;
+    r.set_must("m");
+    r.set_d(std::numeric_limits<double>::infinity());
+    const std::string j = to_json(r);
+    test::Rich back;
+    ASSERT_TRUE_M(to_pb(j, &back), std::string(j));
+    EXPECT_TRUE(std::isinf(back.d()) && back.d() > 0);
+    test::Rich neg;
+    ASSERT_TRUE(to_pb("{\"must\":\"m\",\"d\":\"-Infinity\"}", &neg));
+    EXPECT_TRUE(std::isinf(neg.d()) && neg.d() < 0);
+}
+
+TEST(Json2pbDepth, missing_required_field_on_output_is_reported) {
+    test::Rich r;  // `must` unset
+    r.set_i32(3);
+    std::string out, err;
+    const bool ok = json2pb::ProtoMessageToJson(r, &out, json2pb::Pb2JsonOptions(), &err);
+    // refused, or printed with the problem named (either keeps the caller
+    // from shipping a message its peer cannot parse without knowing)
+    EXPECT_TRUE_M(!ok || has(err, "must"), std::string(out) + " / " + std::string(err));
+}
+
+TEST(Json2pbDepth, unknown_nested_keys_of_every_kind_are_skipped) {
+    test::Rich r;
+    ASSERT_TRUE(to_pb("{\"zz0\":null,\"must\":\"m\",\"zz1\":[{},[],null,true,-1.5e3,\"s\"],"
+                      "\"inner\":{\"x\":5,\"unknown\":{\"deep\":[{\"a\":{\"b\":[1]}}]}},\"zz2\":false}", &r));
+    EXPECT_EQ(r.must(), "m");
+    EXPECT_EQ(r.inner().x(), 5);
+    // the same document is refused by a strict parser, naming the key
+    json2pb::Json2PbOptions strict;
+    strict.allow_unknown_fields = false;
+    test::Rich s2;
+    std::string err;
+    EXPECT_FALSE(to_pb("{\"must\":\"m\",\"inner\":{\"x\":5,\"unknown\":1}}", &s2, &err, strict));
+    EXPECT_TRUE_M(has(err, "unknown"), std::string(err));
+}
