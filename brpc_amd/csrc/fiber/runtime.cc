@@ -99,7 +99,8 @@ struct StackPool {
     std::mutex mu;
     std::vector<Stack*> free;
 };
-StackPool g_stack_pools[5];
+// never destroyed: workers still return stacks while static destructors run at exit
+StackPool* const g_stack_pools = new StackPool[5];
 std::atomic<int64_t> g_nstack{0};
 
 size_t stack_size_of(StackType t) {

@@ -42,6 +42,13 @@ DEFINE_int32(rccl_round_payloads, 64, "most payloads moved to one peer per pair 
 DEFINE_int64(rccl_round_bytes, int64_t(64) << 20, "most payload bytes moved to one peer per pair round");
 DEFINE_int32(rccl_stash_ttl_ms, 30000, "received payloads nobody claims are dropped after this long");
 DEFINE_int32(rccl_idle_spin_us, 0, "an idle plane poster watches its wake word this long before sleeping");
+DEFINE_bool(rccl_defer_busy_peers, true,
+            "do not offer a new pair round to a peer whose group is in flight (it could not fire before its "
+            "group ends; the offer would mostly be withdrawn); offer when it rings back after the group");
+DEFINE_int32(rccl_fire_grace_us, 40,
+             "once a pair round fired, wait up to this long for the other pairs this rank is ready with to fire "
+             "too before building the group (each ready bit cleared unfired is a withdrawal: its payloads go "
+             "back to the queue for a later round)");
 DEFINE_int32(rccl_test_poster_delay_us, 0,
              "test only: the poster sleeps this long after every group (a slow or preempted rank)");
 
@@ -249,7 +256,7 @@ struct alignas(64) PairSlot {
 };
 const int kMaxPairs = kMaxRanks * (kMaxRanks - 1) / 2;
 
-const uint64_t kBellMagic = 0x4d52504342454c32ull;  // "MRPCBEL2"
+const uint64_t kBellMagic = 0x4d52504342454c33ull;  // "MRPCBEL3"
 struct Doorbell {
     uint64_t magic;
     std::atomic<uint32_t> seq;     // bumped on abort (futex word of no one in particular)
@@ -258,6 +265,7 @@ struct Doorbell {
     char reason[200];
     std::atomic<int32_t> pid[kMaxRanks];
     std::atomic<uint32_t> wake[kMaxRanks];  // futex word per rank: bumped by whoever has news for it
+    std::atomic<uint32_t> busy[kMaxRanks];  // 1 while the rank has a group in flight
     PairSlot pairs[kMaxPairs];
 };
 
@@ -339,6 +347,7 @@ public:
 
     std::mutex mu;
     std::vector<PeerState> peers;
+    std::vector<char> in_last_group;  // [peer]: a pair round with it was in our latest group
     std::deque<Payload> self_q;
     std::map<Key, Stashed> stash;
     std::map<Key, WaitSlot> waiting;
@@ -591,6 +600,7 @@ public:
                     if (check_liveness()) break;
                 }
                 idle = false;
+                if (!leave && !stop && !fired.empty()) grace_locked(lk, &fired);
                 if (!leave && !dead && !bell->abort.load(std::memory_order_acquire)) {
                     withdraw_all_locked(&fired);
                     build_group_locked(fired, /*with_self=*/!stop);
@@ -602,7 +612,15 @@ public:
                 break;
             }
             if (dead) break;
-            if (run_group() != 0) break;
+            bell->busy[rank].store(1, std::memory_order_release);
+            const int grc = run_group();
+            bell->busy[rank].store(0, std::memory_order_release);
+            if (FLAGS_rccl_defer_busy_peers) {
+                for (int p = 0; p < world; ++p) {
+                    if (p != rank) ring(p);  // peers that deferred offers to us
+                }
+            }
+            if (grc != 0) break;
             if (!stop && FLAGS_rccl_test_poster_delay_us > 0) usleep((useconds_t)FLAGS_rccl_test_poster_delay_us);
         }
         if (!dead) abort("rank shut down", true, /*is_error=*/false);
@@ -707,6 +725,16 @@ public:
             }
             if (!offer_new) continue;
             const bool peer_ready = (w & other) != 0;
+            // a peer with a group in flight cannot fire a round before that
+            // group ends, and our bit would most likely be withdrawn (its
+            // payloads re-queued) once some other pair fires first: offer to
+            // it when it is back (it rings every peer after each group)
+            // (a peer that shared our latest group is only finishing that
+            // same group: announce now, it fires as soon as it is back)
+            if (!peer_ready && FLAGS_rccl_defer_busy_peers && bell->busy[p].load(std::memory_order_acquire) &&
+                !((size_t)p < in_last_group.size() && in_last_group[p])) {
+                continue;
+            }
             bool have = !ps.queued.empty() && (fits_credit_locked(p, ps.queued.front().len) || [&] {
                             s->stalled[dir(rank, p)].store(1, std::memory_order_release);
                             if (fits_credit_locked(p, ps.queued.front().len)) return true;
@@ -741,6 +769,34 @@ public:
             }
         }
         if (stalled) g_credit_stalls.fetch_add(1, std::memory_order_relaxed);
+    }
+
+    // (mu held, may drop it) a round fired: give the other pairs we are
+    // ready with a short while to fire as well, so one group carries them
+    // instead of withdrawing them now and offering them again next pass.
+    // No group is in flight meanwhile, exactly as in the idle wait, so the
+    // deadlock argument above is unchanged.
+    void grace_locked(std::unique_lock<std::mutex>& lk, std::vector<int>* fired) {
+        if (FLAGS_rccl_fire_grace_us <= 0) return;
+        const int64_t until = monotonic_us() + FLAGS_rccl_fire_grace_us;
+        for (;;) {
+            int pending = 0;
+            for (int p = 0; p < world; ++p) {
+                if (p == rank || !peers[p].ready) continue;
+                if (std::find(fired->begin(), fired->end(), p) != fired->end()) continue;
+                if ((slot(p)->word.load(std::memory_order_acquire) >> 2) != peers[p].round) {
+                    fired->push_back(p);  // the peer fired it
+                } else {
+                    ++pending;
+                }
+            }
+            if (pending == 0 || monotonic_us() >= until || dead || bell->abort.load(std::memory_order_acquire)) {
+                return;
+            }
+            lk.unlock();
+            for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+            lk.lock();
+        }
     }
 
     // (mu held) clear our ready bit everywhere nothing fired; a failed clear
@@ -782,6 +838,8 @@ public:
     void build_group_locked(const std::vector<int>& fired, bool with_self) {
         moving_send.assign(world, {});
         moving_recv.assign(world, {});
+        in_last_group.assign(world, 0);
+        for (int p : fired) in_last_group[p] = 1;
         self_send.clear();
         self_recv.clear();
         for (int p : fired) {

@@ -34,12 +34,16 @@ def main():
     ap.add_argument("--abort-test", action="store_true",
                     help="after the legs, rank 1 aborts the plane under traffic; every rank must notice "
                          "within a second and keep serving through the fallback")
+    ap.add_argument("--flags", default="", help="extra native flags, name=value[,name=value...]")
     a = ap.parse_args()
     from brpc_amd import native, parallel
     from brpc_amd.models import start_echo_server
     topo = parallel.init_distributed(prefer_gpu=False)
     native.set_flag("fiber_concurrency", "3")
     native.set_flag("rccl_timeout_ms", "30000")
+    for kv in [x for x in a.flags.split(",") if x]:
+        k, v = kv.split("=", 1)
+        native.set_flag(k, v)
     if a.window:
         native.set_flag("rccl_window_bytes", str(a.window))
     up = parallel.init_rccl_plane(topo, library=parallel.stub_library())

@@ -57,16 +57,21 @@ def run_suite(binary, suite, kind, timeout):
 def run_planes(tree, kind):
     lib = subprocess.run(["g++", "-print-file-name=lib%s.so" % kind], capture_output=True, text=True).stdout.strip()
     out = []
-    for nranks, extra in ((2, []), (3, []), (8, ["--calls", "40,4"])):
-        env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", LD_PRELOAD=lib,
+    for nranks, extra in ((2, ["--calls", "80,8"]), (3, ["--calls", "80,8"]), (8, ["--calls", "40,4"])):
+        # the sanitizer runtime is preloaded into the ranks only (through
+        # `env`), not into the launcher
+        env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
                    TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 suppressions=" + SUPP, ASAN_OPTIONS="detect_leaks=0")
         with tempfile.TemporaryDirectory() as d:
             try:
                 r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
                                     str(nranks), "--master-addr", "127.0.0.1", "--master-port", str(29700 + nranks),
+                                    "--no-python", "env", "LD_PRELOAD=" + lib, sys.executable,
                                     os.path.join(tree, "tests", "plane_ranks.py"), "--out-dir", d] + extra,
-                                   capture_output=True, text=True, timeout=1800, cwd="/tmp", env=env)
+                                   capture_output=True, text=True, timeout=900, cwd=tree, env=env)
                 text, rc = r.stdout + r.stderr, r.returncode
+                ranks = len([f for f in os.listdir(d) if f.startswith("rank")])
+                text += "\n# rank reports: %d of %d\n" % (ranks, nranks)
             except subprocess.TimeoutExpired:
                 text, rc = "", "timeout"
         pat = "WARNING: ThreadSanitizer" if kind == "tsan" else "ERROR: AddressSanitizer"
@@ -75,7 +80,8 @@ def run_planes(tree, kind):
         if n:
             i = text.find(pat)
             first = text[i:i + 1500]
-        out.append(("RcclPlaneStub%dRanks" % nranks, rc, n, "", first))
+        summary = [l for l in text.splitlines() if l.startswith("# rank reports")]
+        out.append(("RcclPlaneStub%dRanks" % nranks, rc, n, summary[-1] if summary else "", first))
     return out
 
 
@@ -98,7 +104,7 @@ def main():
     if a.planes:
         for res in run_planes(a.tree, a.kind):
             results.append(res)
-            print("%s rc=%s %s=%d" % (res[0], res[1], a.kind, res[2]), flush=True)
+            print("%s rc=%s %s=%d %s" % (res[0], res[1], a.kind, res[2], res[3]), flush=True)
     total = sum(r[2] for r in results)
     print("# total %s reports: %d over %d runs" % (a.kind, total, len(results)))
     for r in results:
