@@ -37,6 +37,7 @@
 
 #include <atomic>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "base/logging.h"
@@ -44,6 +45,7 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
+#include "pb/descriptor.h"
 #include "pb/message.h"
 #include "rpc/compress.h"
 #include "var/var.h"
@@ -65,6 +67,10 @@ DEFINE_int32(gpu_pb_pack_min_elems, 4096,
 DEFINE_int32(gpu_pb_unpack_min_bytes, 16384,
              "packed varint fields of at least this many bytes in a body the GPU codec decoded are decoded on the "
              "device too (pb_run_count/decode kernels, one more codec batch per message); 0: never");
+DEFINE_bool(gpu_snappy_packed_only, true,
+            "with the GPU snappy codec enabled, route only messages with large packed numeric fields to it (their "
+            "varints are packed/unpacked on the device in the same batch); plain host bodies (strings, bytes) go to "
+            "the CPU codec, which beats a host-memory GPU round trip on them (bench: the *_snappy_64KB_* legs)");
 DEFINE_int32(gpu_snappy_block_kb, 4,
              "uncompressed bytes per device snappy block (one wave each): smaller blocks spread one body over more "
              "waves (lower latency) at some cost in ratio; <= 64");
@@ -279,8 +285,10 @@ bool decode_runs(std::vector<pb::PackedRunIn>* runs, PinnedBuf* out, int device)
 
 struct DeviceRunDecoder : public pb::PackedRunDecoder {
     PinnedBuf out{1};
+    int calls = 0;  // runs handed to the device by this parse
     size_t min_bytes() const override { return (size_t)std::max(1, FLAGS_gpu_pb_unpack_min_bytes); }
     void Decode(std::vector<pb::PackedRunIn>* runs) override {
+        calls += (int)runs->size();
         if (g_device < 0 || !decode_runs(runs, &out, g_device)) {
             g_unpack_fallbacks.fetch_add(1, std::memory_order_relaxed);
             return;
@@ -545,15 +553,50 @@ bool gpu_decompress(const Buf& in, Buf* out, PbIndex* index = nullptr) {
     return true;
 }
 
-std::atomic<int64_t> g_indexed_parses{0}, g_index_fallbacks{0}, g_packs{0}, g_pack_runs{0}, g_pack_run_chunks{0};
+std::atomic<int64_t> g_indexed_parses{0}, g_index_fallbacks{0}, g_packs{0}, g_pack_runs{0}, g_pack_run_chunks{0},
+    g_plain_routed{0};
 
 
+
+// -gpu_snappy_packed_only on the receive side: whether a body carries a
+// large packed run is only known once it is decoded, so the route adapts per
+// message type (and worker). Types without packed numeric fields never go to
+// the device; for the others, a device decode that found no run to unpack
+// sends the next kPlainSkip bodies of the type to the CPU codec before the
+// device probes again (the same adaptive skip as incompressible device
+// payloads).
+const uint32_t kPlainSkip = 31;
+struct TypeRoute {
+    bool packable = false;
+    uint32_t skip = 0;
+};
+TypeRoute& route_of(const pb::Descriptor* d) {
+    static thread_local std::unordered_map<const pb::Descriptor*, TypeRoute> routes;
+    auto it = routes.find(d);
+    if (it != routes.end()) return it->second;
+    TypeRoute r;
+    for (int i = 0; i < d->field_count() && !r.packable; ++i) {
+        const pb::FieldDescriptor* f = d->field(i);
+        r.packable = f->is_repeated() && f->packed && f->is_packable();
+    }
+    return routes.emplace(d, r).first->second;
+}
 
 // SetPbParseOffload hook: snappy decode + pb_scan in one device pass; the
 // host merges the top-level fields from the table (bytes fields become one
 // assign each, nested messages parse from their ranges).
 int parse_offload(const Buf& in, CompressType type, pb::Message* msg) {
     if (type != COMPRESS_TYPE_SNAPPY || g_device < 0 || device_blocks_elsewhere(in, g_device)) return 0;
+    TypeRoute* route = nullptr;
+    if (FLAGS_gpu_snappy_packed_only) {
+        route = &route_of(msg->GetDescriptor());
+        if (!route->packable) return 0;
+        if (route->skip > 0) {
+            --route->skip;
+            g_plain_routed.fetch_add(1, std::memory_order_relaxed);
+            return 0;
+        }
+    }
     Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
     const int64_t t0 = span ? monotonic_us() : 0;
     PbIndex index;
@@ -573,6 +616,7 @@ int parse_offload(const Buf& in, CompressType type, pb::Message* msg) {
                                  FLAGS_gpu_pb_unpack_min_bytes > 0 ? &decoder : nullptr)) {
         ok = msg->IsInitialized();
         g_indexed_parses.fetch_add(1, std::memory_order_relaxed);
+        if (route && decoder.calls == 0) route->skip = kPlainSkip;  // a plain body: CPU for a while
     } else {
         // too many fields for the table, unknown fields, ...: the bytes are
         // already decoded, so only the parse runs on the host
@@ -588,7 +632,7 @@ int parse_offload(const Buf& in, CompressType type, pb::Message* msg) {
 }
 
 bool offload(const Buf& in, Buf* out, bool compress) {
-    if (g_device < 0 || device_blocks_elsewhere(in, g_device)) return false;
+    if (g_device < 0 || FLAGS_gpu_snappy_packed_only || device_blocks_elsewhere(in, g_device)) return false;
     Buf result;
     Span* span = IsRpczEnabled() ? Span::tls_parent() : nullptr;
     const int64_t t0 = span ? monotonic_us() : 0;
@@ -632,6 +676,12 @@ bool pack_offload(const pb::Message& msg, size_t n, Buf* out) {
     }
     Buf raw;
     body.give_to(&raw);
+    if (FLAGS_gpu_snappy_packed_only && !device_runs) {
+        // no packed run large enough for the device: the CPU codec compresses
+        // the body we already serialized
+        g_plain_routed.fetch_add(1, std::memory_order_relaxed);
+        return CompressBuf(COMPRESS_TYPE_SNAPPY, raw, out);
+    }
     Buf result;
     bool ok;
     {
@@ -807,6 +857,7 @@ GpuSnappyStats GetGpuSnappyStats() {
     s.index_fallbacks = g_index_fallbacks.load();
     s.packs = g_packs.load();
     s.pack_runs = g_pack_runs.load();
+    s.plain_routed = g_plain_routed.load();
     s.pack_run_chunks = g_pack_run_chunks.load();
     s.unpack_runs = g_unpack_runs.load();
     s.unpack_fallbacks = g_unpack_fallbacks.load();

@@ -21,6 +21,7 @@ struct GpuSnappyStats {
     int64_t packs = 0;  // bodies serialized straight into pinned memory and compressed there
     int64_t pack_runs = 0, pack_run_chunks = 0;  // packed fields those bodies left to pb_run_encode_kernel
     int64_t unpack_runs = 0, unpack_fallbacks = 0;  // packed fields of decoded bodies parsed on the device
+    int64_t plain_routed = 0;  // -gpu_snappy_packed_only: plain bodies left to the CPU codec
 };
 GpuSnappyStats GetGpuSnappyStats();
 

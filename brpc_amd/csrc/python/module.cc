@@ -681,10 +681,14 @@ PYBIND11_MODULE(_native, m) {
         d["host_memory"] = s.host_memory;
         return d;
     });
-    g.def("enable_snappy", [](int dev, size_t min_bytes) {
+    // packed_only (-gpu_snappy_packed_only): the device codec takes only
+    // messages with large packed numeric fields; False forces every snappy
+    // body of at least min_bytes onto the device (the A/B and the tests)
+    g.def("enable_snappy", [](int dev, size_t min_bytes, bool packed_only) {
         std::string err;
+        SetFlag("gpu_snappy_packed_only", packed_only ? "true" : "false");
         if (gpu::EnableGpuSnappy(dev, min_bytes, &err) != 0) throw std::runtime_error(err);
-    }, py::arg("device") = 0, py::arg("min_bytes") = 32768);
+    }, py::arg("device") = 0, py::arg("min_bytes") = 32768, py::arg("packed_only") = true);
     g.def("disable_snappy", [] { gpu::DisableGpuSnappy(); });
     g.def("snappy_stats", [] {
         const gpu::GpuSnappyStats s = gpu::GetGpuSnappyStats();
@@ -693,6 +697,7 @@ PYBIND11_MODULE(_native, m) {
         d["decompress_calls"] = s.decompress_calls;
         d["fallbacks"] = s.fallbacks;
         d["indexed_parses"] = s.indexed_parses;
+        d["plain_routed"] = s.plain_routed;
         d["index_fallbacks"] = s.index_fallbacks;
         d["packs"] = s.packs;
         d["pack_runs"] = s.pack_runs;

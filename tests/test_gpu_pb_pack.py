@@ -164,6 +164,33 @@ def test_packed_ids_encoded_on_device_in_the_codec_batch(native, protocol):
         s.stop()
 
 
+def test_plain_bodies_go_to_the_cpu_codec_by_default(native):
+    """-gpu_snappy_packed_only (the default of enable_snappy): 64 KiB text
+    bodies without packed ids are compressed by the CPU codec on the send
+    side (plain_routed counts them) and, after one probing device decode
+    per type and worker, decoded by the CPU codec too."""
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    native.gpu.enable_snappy(0, 16384)
+    try:
+        b0 = native.gpu.snappy_stats()
+        p = native.Press({"server": s.address, "protocol": "baidu_std", "concurrency": 8, "request_size": 65536,
+                          "body": "text", "request_compress_type": 1, "check_echo": True})
+        p.run_requests(400)
+        st = p.stats()
+        assert st["success"] == 400 and st["error"] == 0, st
+        b1 = native.gpu.snappy_stats()
+        assert b1["pack_runs"] == b0["pack_runs"]
+        assert b1["compress_calls"] == b0["compress_calls"], (b0, b1)
+        assert b1["plain_routed"] - b0["plain_routed"] >= 400, (b0, b1)
+        # device decodes only as probes: at most one per 32 bodies per worker
+        # (requests on the server, responses on the client; a worker probes each type once before it skips)
+        assert b1["indexed_parses"] - b0["indexed_parses"] <= 2 * (400 // 32) + 32, (b0, b1)
+    finally:
+        native.gpu.disable_snappy()
+        s.stop()
+
+
 def test_packed_ids_below_threshold_stay_on_host(native):
     from brpc_amd.models import start_echo_server
     s = start_echo_server("127.0.0.1:0", gpu_device=0)

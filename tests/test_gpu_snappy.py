@@ -228,7 +228,7 @@ def test_gpu_snappy_offload_is_standard_snappy(mode):
     from brpc_amd import native
     native.set_flag("gpu_snappy_device_split", "true" if mode == "device_split" else "false")
     native.set_flag("gpu_snappy_direct_host", "false" if mode == "staged" else "true")
-    native.gpu.enable_snappy(0, 1024)
+    native.gpu.enable_snappy(0, 1024, packed_only=False)
     try:
         rnd = os.urandom(200000)
         cases = [rnd, b"abcdefgh" * 40000, rnd[:70000] + b"\0" * 100000 + rnd[:5000], b"q" * 65536, b"r" * 65537]
@@ -253,7 +253,7 @@ def test_grpc_snappy_bodies_on_gpu():
     from brpc_amd import native
     from brpc_amd.models import start_echo_server
     s = start_echo_server("127.0.0.1:0", gpu_device=0)
-    native.gpu.enable_snappy(0, 16384)
+    native.gpu.enable_snappy(0, 16384, packed_only=False)
     try:
         before = native.gpu.snappy_stats()
         p = native.Press({"server": s.address, "protocol": "h2:grpc", "concurrency": 8, "request_size": 65536,
@@ -282,7 +282,7 @@ def test_baidu_std_snappy_bodies_parsed_from_device_index():
     from brpc_amd import native
     from brpc_amd.models import start_echo_server
     s = start_echo_server("127.0.0.1:0", gpu_device=0)
-    native.gpu.enable_snappy(0, 16384)
+    native.gpu.enable_snappy(0, 16384, packed_only=False)
     try:
         before = native.gpu.snappy_stats()
         p = native.Press({"server": s.address, "protocol": "baidu_std", "concurrency": 8, "request_size": 40000,
@@ -310,7 +310,7 @@ def test_concurrent_codec_requests_share_launches():
     from brpc_amd import native
     from brpc_amd.models import start_echo_server
     s = start_echo_server("127.0.0.1:0", gpu_device=0)
-    native.gpu.enable_snappy(0, 16384)
+    native.gpu.enable_snappy(0, 16384, packed_only=False)
     try:
         b0 = native.gpu.codec_batch_stats()
         p = native.Press({"server": s.address, "protocol": "h2:grpc", "concurrency": 50, "request_size": 65536,
