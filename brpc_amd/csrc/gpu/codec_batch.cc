@@ -14,9 +14,11 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 
-DEFINE_bool(codec_fused, true,
+DEFINE_bool(codec_fused, false,
             "run codec batches of compress blocks and decode pieces (<= 8 KiB) as one launch (compress, "
-            "decode and the last-piece pb scan together) instead of serial per-stage kernels");
+            "decode and the last-piece pb scan together) instead of serial per-stage kernels (off: on the "
+            "device-body RPC leg the per-stage sequence measured faster, 114 k vs 74 k QPS with the wave kernel "
+            "and 46 k with the workgroup kernel, although one launch halves a batch's device time alone)");
 DEFINE_string(codec_fused_kernel, "waves",
               "kernel of the one-launch codec batch: 'waves' (one wave per block/piece, snappy_kernels.hip) or "
               "'workgroup' (one 1024-thread workgroup per block/piece, codec_fused.hip)");

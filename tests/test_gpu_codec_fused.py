@@ -25,9 +25,10 @@ def native():
 
 @pytest.fixture(autouse=True)
 def _restore_flags(native):
+    native.set_flag("codec_fused", "true")
     yield
     native.set_flag("device_payload_block_kb", "2")
-    native.set_flag("codec_fused", "true")
+    native.set_flag("codec_fused", "false")
     native.set_flag("codec_fused_kernel", "waves")
 
 
