@@ -1060,6 +1060,7 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
             "placement_rank0": placement,
             "control_plane": topo.backend or "none",
             "devices_by_rank": extra.get("devices"),
+            "flags": list(a.flag),  # --flag NAME=VALUE overrides of this run
         },
     }
     if r32:

@@ -14,11 +14,15 @@
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
 
-DEFINE_bool(codec_fused, false,
-            "run codec batches of compress blocks and decode pieces (<= 8 KiB) as one launch (compress, "
-            "decode and the last-piece pb scan together) instead of serial per-stage kernels (off: on the "
-            "device-body RPC leg the per-stage sequence measured faster, 114 k vs 74 k QPS with the wave kernel "
-            "and 46 k with the workgroup kernel, although one launch halves a batch's device time alone)");
+DEFINE_bool(codec_fused, true,
+            "run codec batches of compress blocks and decode pieces (<= 8 KiB) as one launch (then the pb scans, "
+            "if any, as a second one) instead of one launch per stage: 158-161 k vs 115 k QPS on the device-body "
+            "text leg (profiles/r5_device_codec_ab.txt)");
+DEFINE_bool(codec_fused_scan_in_kernel, false,
+            "fused batches: the wave that finishes a message's last piece scans its fields in the same launch "
+            "(else the pb scan is a second launch). Off: the hand-off needs a device-scope fence per piece, "
+            "which on gfx950 compiles to buffer_wbl2 + buffer_inv (an L2 write-back of the XCD) in every wave; "
+            "in the RPC leg, with batches overlapping, that made the one-launch kernels 1.5-4x slower per launch");
 DEFINE_string(codec_fused_kernel, "waves",
               "kernel of the one-launch codec batch: 'waves' (one wave per block/piece, snappy_kernels.hip) or "
               "'workgroup' (one 1024-thread workgroup per block/piece, codec_fused.hip)");
@@ -271,7 +275,8 @@ bool launch(CBatch* b, int device) {
         fa.pieces = b->piece_jobs.p;
         fa.npieces = (int)nhpieces;
         fa.piece_err = b->piece_job_err.p;
-        fa.piece_group = nscan ? b->piece_group.p : nullptr;
+        const bool scan_in_kernel = FLAGS_codec_fused_scan_in_kernel && nscan;
+        fa.piece_group = scan_in_kernel ? b->piece_group.p : nullptr;
         fa.scans = b->scan_jobs.p;
         fa.group_pieces = b->group_pieces.p;
         fa.group_done = b->group_done;
@@ -281,7 +286,8 @@ bool launch(CBatch* b, int device) {
         fa.max_ulen = std::max(ncomp ? comp_max : 1u, nhpieces ? hpiece_max : 1u);
         if (rc == 0) rc = FLAGS_codec_fused_kernel == "workgroup" ? LaunchFusedCodec(fa, s) : LaunchCodecWaves(fa, s);
         g_fused_launches.fetch_add(1, std::memory_order_relaxed);
-        ncomp = nhpieces = nscan = 0;  // nothing left for the per-stage sequence below
+        ncomp = nhpieces = 0;  // nothing left for the per-stage sequence below but (maybe) the scans
+        if (scan_in_kernel) nscan = 0;
     }
     if (rc == 0 && nruns) rc = LaunchPbRunEncode(b->run_jobs.p, (int)nruns, b->run_err.p, s);
     g_run_chunks.fetch_add((int64_t)nruns, std::memory_order_relaxed);

@@ -1135,13 +1135,18 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
 // small-footprint waves that pack 5 per CU (many batches in flight share
 // the chip; the 1024-thread workgroup codec of codec_fused.hip is faster
 // alone but holds a CU per block and loses when batches overlap).
+// Instantiated per role set: a batch of only decode pieces gets a kernel
+// without the compressor's registers and static LDS (the per-wave footprint
+// decides how many waves of concurrent batches share a CU).
+template <bool kComp, bool kDec>
 __global__ void __launch_bounds__(kWave) codec_waves_kernel(FusedCodecArgs a, uint32_t in_cap, uint32_t slot,
                                                             uint32_t cin_cap, uint32_t phi) {
     const int b = blockIdx.x;
-    if (b < a.ncomp) {
+    if (kComp && b < a.ncomp) {
         compress_wave<true, true>(a.comp, b, nullptr, a.comp_len, a.comp_err, in_cap, slot, nullptr);
         return;
     }
+    if (!kDec) return;
     const int j = b - a.ncomp;
     if (j >= a.npieces) return;
     decode_piece_wave(a.pieces, j, 0, phi, cin_cap, a.piece_err, nullptr);
@@ -1176,7 +1181,16 @@ int LaunchCodecWaves(const FusedCodecArgs& a, hipStream_t s) {
     const uint32_t cin_cap = (uint32_t)((SnappyMaxCompressedLength(mu) + 16 + 15) & ~15ull);
     const uint32_t dec_lds = cin_cap + 2 * ((mu + 7) & ~7u) + 4 * kWave;
     const uint32_t lds = std::max(a.ncomp ? comp_lds : 0u, a.npieces ? dec_lds : 0u);
-    hipLaunchKernelGGL(codec_waves_kernel, dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot, cin_cap, mu);
+    if (a.ncomp && a.npieces) {
+        hipLaunchKernelGGL((codec_waves_kernel<true, true>), dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot,
+                           cin_cap, mu);
+    } else if (a.ncomp) {
+        hipLaunchKernelGGL((codec_waves_kernel<true, false>), dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot,
+                           cin_cap, mu);
+    } else {
+        hipLaunchKernelGGL((codec_waves_kernel<false, true>), dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot,
+                           cin_cap, mu);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -28,8 +28,9 @@ def _restore_flags(native):
     native.set_flag("codec_fused", "true")
     yield
     native.set_flag("device_payload_block_kb", "2")
-    native.set_flag("codec_fused", "false")
+    native.set_flag("codec_fused", "true")
     native.set_flag("codec_fused_kernel", "waves")
+    native.set_flag("codec_fused_scan_in_kernel", "false")
 
 
 KERNELS = ["waves", "workgroup"]
@@ -114,9 +115,13 @@ def test_fused_ratio_not_worse_than_lane_segments(native, kb):
     assert len(data) / fused > 2.0
 
 
+@pytest.mark.parametrize("in_kernel", [False, True])
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_fused_scan_runs_after_the_last_piece(native, kernel):
+def test_fused_scan_runs_after_the_last_piece(native, kernel, in_kernel):
+    """The message's field table: by the wave/workgroup that finished its
+    last piece (in_kernel) or by the pb-scan launch after the batch."""
     native.set_flag("codec_fused_kernel", kernel)
+    native.set_flag("codec_fused_scan_in_kernel", "true" if in_kernel else "false")
     native.set_flag("device_payload_block_kb", "4")
     body = native.echo_body("text", 50000)
     msg = bytes([0x0A]) + _varint(len(body)) + body + bytes([0x18, 0x01])
