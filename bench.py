@@ -1139,6 +1139,10 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
         out["rccl_payloads_per_round"] = round(tr.get("rccl_payloads", 0) / max(1, tr.get("rccl_rounds", 0)), 2)
         out["rccl_aborts"] = extra.get("plane_aborts", tr.get("rccl_aborts", 0))
         out["rccl_world"] = tr["rccl_world"]
+        if tr["rccl_world"] == 1:
+            out["rccl_note"] = ("one-rank plane: every payload goes from the rank to itself, which the plane moves "
+                                "with one batched copy kernel per group on its stream (-rccl_self_copy); between "
+                                "ranks its groups are ncclSend/ncclRecv")
     r1m = legs.get("echo_1MB")
     if r1m:
         out["qps_1MB"] = round(r1m["qps"], 1)

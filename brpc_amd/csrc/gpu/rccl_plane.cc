@@ -28,6 +28,7 @@
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
 #include "gpu/hbm_pool.h"
+#include "gpu/kernels.h"
 #include "mrpc/proto/device_payload.pb.h"
 #include "var/var.h"
 
@@ -42,6 +43,9 @@ DEFINE_int32(rccl_round_payloads, 64, "most payloads moved to one peer per pair 
 DEFINE_int64(rccl_round_bytes, int64_t(64) << 20, "most payload bytes moved to one peer per pair round");
 DEFINE_int32(rccl_stash_ttl_ms, 30000, "received payloads nobody claims are dropped after this long");
 DEFINE_int32(rccl_idle_spin_us, 0, "an idle plane poster watches its wake word this long before sleeping");
+DEFINE_bool(rccl_self_copy, true,
+            "payloads a rank sends to itself move with one batched copy kernel on the plane stream instead of "
+            "ncclSend/ncclRecv pairs to self (RCCL's per-op overhead for what is a device-local copy)");
 DEFINE_bool(rccl_defer_busy_peers, true,
             "do not offer a new pair round to a peer whose group is in flight (it could not fire before its "
             "group ends; the offer would mostly be withdrawn); offer when it rings back after the group");
@@ -143,6 +147,8 @@ public:
     virtual void* alloc(size_t len, Buf* out) = 0;
     virtual bool accepts(const BufBlock* b) const = 0;
     virtual bool host_memory() const = 0;
+    // queue copies on the stream (self payloads: rank to itself)
+    virtual int copy(const std::vector<Segment>& segs) = 0;
 };
 
 class HipOps : public StreamOps {
@@ -176,6 +182,13 @@ public:
     void* alloc(size_t len, Buf* out) override { return AppendNewDeviceBlock(out, len, _device); }
     bool accepts(const BufBlock* b) const override { return b->kind == MemKind::DEVICE && b->device == _device; }
     bool host_memory() const override { return false; }
+    int copy(const std::vector<Segment>& segs) override {
+        for (size_t i = 0; i < segs.size(); i += kInlineSegments) {
+            const int n = (int)std::min<size_t>(kInlineSegments, segs.size() - i);
+            if (LaunchBatchedCopy(segs.data() + i, n, _stream) != 0) return -1;
+        }
+        return 0;
+    }
 
 private:
     int _device = -1;
@@ -210,6 +223,12 @@ public:
     }
     bool accepts(const BufBlock* b) const override { return IsHostAccessible(b->kind); }
     bool host_memory() const override { return true; }
+    int copy(const std::vector<Segment>& segs) override {
+        // the stub's stream runs groups synchronously at group end, and the
+        // marker recorded after this completes after it
+        for (const Segment& g : segs) memcpy(g.dst, g.src, g.len);
+        return 0;
+    }
 
 private:
     const Api& _api;
@@ -986,7 +1005,25 @@ public:
         void* st = ops->stream();
         const int64_t t0 = monotonic_us();
         int rc = 0;
-        ncclResult_t r = api.group_start();
+        // self payloads: one batched copy on the plane stream (a send/recv
+        // pair to oneself costs RCCL ~16 us of per-op overhead each for
+        // what is a device-local copy: the N=1 leg ran ~25 of them per
+        // group, 950 us p99)
+        const bool self_copy = FLAGS_rccl_self_copy && !self_send.empty();
+        if (self_copy) {
+            std::vector<Segment> segs;
+            segs.reserve(self_send.size());
+            for (size_t i = 0; i < self_send.size(); ++i)
+                segs.push_back(Segment{self_send[i].ptr, self_recv[i].ptr, (uint64_t)self_send[i].len});
+            if (ops->copy(segs) != 0) {
+                abort("self payload copy failed", true);
+                return -1;
+            }
+        }
+        bool peers_move = false;
+        for (int p = 0; p < world; ++p) peers_move |= !moving_send[p].empty() || !moving_recv[p].empty();
+        ncclResult_t r = ncclSuccess;
+        if (peers_move || !self_copy) r = api.group_start();
         for (int p = 0; p < world && r == ncclSuccess; ++p) {
             if (p == rank) continue;
             for (size_t i = 0; i < moving_send[p].size() && r == ncclSuccess; ++i)
@@ -994,13 +1031,15 @@ public:
             for (size_t i = 0; i < moving_recv[p].size() && r == ncclSuccess; ++i)
                 r = api.recv(moving_recv[p][i].ptr, moving_recv[p][i].len, ncclUint8, p, comm, (hipStream_t)st);
         }
-        for (size_t i = 0; i < self_send.size() && r == ncclSuccess; ++i) {
+        for (size_t i = 0; !self_copy && i < self_send.size() && r == ncclSuccess; ++i) {
             r = api.send(self_send[i].ptr, self_send[i].len, ncclUint8, rank, comm, (hipStream_t)st);
             if (r == ncclSuccess)
                 r = api.recv(self_recv[i].ptr, self_recv[i].len, ncclUint8, rank, comm, (hipStream_t)st);
         }
-        const ncclResult_t e = api.group_end();
-        if (r == ncclSuccess) r = e;
+        if (peers_move || !self_copy) {
+            const ncclResult_t e = api.group_end();
+            if (r == ncclSuccess) r = e;
+        }
         if (r == ncclSuccess) rc = ops->record(&marker);
         marker_live = r == ncclSuccess && rc == 0;
         g_rounds.fetch_add(1, std::memory_order_relaxed);
