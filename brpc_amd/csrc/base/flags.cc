@@ -279,11 +279,14 @@ int LoadFlagsFromFile(const std::string& path) {
     std::string line;
     int n = 0;
     while (std::getline(in, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();  // CRLF files
         size_t b = line.find_first_not_of(" \t-");
         if (b == std::string::npos || line[b] == '#') continue;
         size_t eq = line.find('=', b);
         if (eq == std::string::npos) continue;
-        if (SetFlag(line.substr(b, eq - b), line.substr(eq + 1))) ++n;
+        size_t ne = eq;  // "name = value": the name without trailing blanks
+        while (ne > b && (line[ne - 1] == ' ' || line[ne - 1] == '\t')) --ne;
+        if (SetFlag(line.substr(b, ne - b), line.substr(eq + 1))) ++n;
     }
     return n;
 }
