@@ -353,7 +353,7 @@ __device__ __forceinline__ void decode_piece_wave(const SnappyPiece* __restrict_
     lbyte* const cin = (lbyte*)lds;
     __attribute__((address_space(3))) uint16_t* const smap =
         (__attribute__((address_space(3))) uint16_t*)(lds + cin_cap);
-    // 64 slots of per-pass element starts, after the map
+    // 256 slots of per-pass element starts, after the map
     __attribute__((address_space(3))) uint32_t* const strip =
         (__attribute__((address_space(3))) uint32_t*)(lds + cin_cap + 2 * ((hi + 7) & ~7u));
     {
@@ -432,19 +432,40 @@ __device__ __forceinline__ void decode_piece_wave(const SnappyPiece* __restrict_
         const uint32_t span_end =
             (uint32_t)__builtin_amdgcn_readlane((int)(u0 + len), (int)(63 - __builtin_clzll(mask)));
         uint32_t carry = 0;
-        for (uint32_t P = upos; P < span_end; P += kWave) {
-            strip[lane] = 0;
-            if (marked && u0 >= P && u0 < P + kWave) strip[u0 - P] = (uint32_t)lane + 1;
+        // 256 positions per pass, four consecutive ones per lane: one
+        // barrier and one wave max-scan per pass, and the lane's four
+        // bpermutes issue back to back (one position per lane per pass was
+        // ~600 cycles of LDS round trips per 64 output bytes, a third of a
+        // 2 KiB piece's decode)
+        typedef unsigned int u32x4s __attribute__((ext_vector_type(4)));
+        for (uint32_t P = upos; P < span_end; P += 4 * kWave) {
+            *reinterpret_cast<__attribute__((address_space(3))) u32x4s*>(strip + 4 * lane) = u32x4s{0, 0, 0, 0};
+            if (marked && u0 >= P && u0 < P + 4 * kWave) strip[u0 - P] = (uint32_t)lane + 1;
             // other lanes' stores: without the barrier the compiler may
-            // forward this lane's own 0 (one wave: s_barrier is free, and DS
-            // operations of a wave complete in order)
+            // forward this lane's own zeros (one wave: s_barrier is free, and
+            // DS operations of a wave complete in order)
             __syncthreads();
-            const uint32_t m = wave_incl_max(strip[lane]);
-            const uint32_t got = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m ? m - 1 : 0) << 2), (int)info);
-            const uint32_t e = m ? got : carry;
-            const uint32_t pos = P + (uint32_t)lane;
-            if (pos < span_end) smap[pos] = (uint16_t)((e >> 16) + (pos - (e & 0xffff)));
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)e, 63);
+            const u32x4s sv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4s*>(strip + 4 * lane);
+            uint32_t m0 = sv.x, m1 = max(m0, sv.y), m2 = max(m1, sv.z), m3 = max(m2, sv.w);
+            const uint32_t incl = wave_incl_max(m3);
+            // the latest element start of the lanes before this one
+            const uint32_t before = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ? lane - 1 : 0) << 2), (int)incl);
+            const uint32_t bm = lane ? before : 0u;
+            m0 = max(m0, bm);
+            m1 = max(m1, bm);
+            m2 = max(m2, bm);
+            m3 = max(m3, bm);
+            const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m0 ? m0 - 1 : 0) << 2), (int)info);
+            const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m1 ? m1 - 1 : 0) << 2), (int)info);
+            const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m2 ? m2 - 1 : 0) << 2), (int)info);
+            const uint32_t g3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m3 ? m3 - 1 : 0) << 2), (int)info);
+            const uint32_t e0 = m0 ? g0 : carry, e1 = m1 ? g1 : carry, e2 = m2 ? g2 : carry, e3 = m3 ? g3 : carry;
+            const uint32_t pos = P + 4u * (uint32_t)lane;
+            if (pos < span_end) smap[pos] = (uint16_t)((e0 >> 16) + (pos - (e0 & 0xffff)));
+            if (pos + 1 < span_end) smap[pos + 1] = (uint16_t)((e1 >> 16) + (pos + 1 - (e1 & 0xffff)));
+            if (pos + 2 < span_end) smap[pos + 2] = (uint16_t)((e2 >> 16) + (pos + 2 - (e2 & 0xffff)));
+            if (pos + 3 < span_end) smap[pos + 3] = (uint16_t)((e3 >> 16) + (pos + 3 - (e3 & 0xffff)));
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)e3, 63);
         }
         upos = span_end;
         ip += p;
@@ -1179,7 +1200,7 @@ int LaunchCodecWaves(const FusedCodecArgs& a, hipStream_t s) {
     const uint32_t slot = (seg + 16 + 15) & ~15u;
     const uint32_t comp_lds = CompressInBytes(in_cap, true) + kWave * slot + CompressCandBytes(in_cap);
     const uint32_t cin_cap = (uint32_t)((SnappyMaxCompressedLength(mu) + 16 + 15) & ~15ull);
-    const uint32_t dec_lds = cin_cap + 2 * ((mu + 7) & ~7u) + 4 * kWave;
+    const uint32_t dec_lds = cin_cap + 2 * ((mu + 7) & ~7u) + 16 * kWave;
     const uint32_t lds = std::max(a.ncomp ? comp_lds : 0u, a.npieces ? dec_lds : 0u);
     if (a.ncomp && a.npieces) {
         hipLaunchKernelGGL((codec_waves_kernel<true, true>), dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot,
@@ -1230,7 +1251,7 @@ int LaunchSnappyDecompressPiecesStamped(const SnappyPiece* pieces_dev, int n, ui
     if (lo < kParMax) {
         const uint32_t phi = std::min(hi, kParMax);
         const uint32_t cin_cap = (uint32_t)((SnappyMaxCompressedLength(phi) + 16 + 15) & ~15ull);
-        const uint32_t lds = cin_cap + 2 * ((phi + 7) & ~7u) + 4 * kWave;
+        const uint32_t lds = cin_cap + 2 * ((phi + 7) & ~7u) + 16 * kWave;
         hipLaunchKernelGGL(snappy_decompress_pieces_par_kernel, dim3(n), dim3(kWave), lds, s, pieces_dev, n, lo, phi,
                            cin_cap, err_dev, stamps);
         if (hipGetLastError() != hipSuccess) return -1;
