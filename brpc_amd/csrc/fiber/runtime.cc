@@ -443,8 +443,19 @@ static void add_sleep_event(void* arg) {
     // pooled memory, valid even if the fiber already woke). If this worker
     // was delayed until the fiber woke, returned and maybe slept again, the
     // generation no longer matches and the stale id is dropped.
-    std::lock_guard<std::mutex> g(e.meta->sleep_mu);
-    if (e.meta->sleep_gen == e.gen) e.meta->current_sleep.store(id, std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> g(e.meta->sleep_mu);
+        if (e.meta->sleep_gen != e.gen) return;
+        e.meta->current_sleep.store(id, std::memory_order_seq_cst);
+    }
+    // interrupt() sets `interrupted` and then takes current_sleep; we publish
+    // current_sleep and then look at `interrupted` (both seq_cst): one of the
+    // two sees the other, so an interrupt that raced with this publish still
+    // ends the sleep (whoever takes the id wakes the fiber)
+    if (e.meta->interrupted.load(std::memory_order_seq_cst)) {
+        const uint64_t taken = e.meta->current_sleep.exchange(0, std::memory_order_acq_rel);
+        if (taken && get_global_timer_thread()->unschedule(taken) == 0) tls_group()->ready_to_run(e.tid);
+    }
 }
 
 int TaskGroup::usleep(TaskGroup** pg, uint64_t us) {
@@ -454,6 +465,11 @@ int TaskGroup::usleep(TaskGroup** pg, uint64_t us) {
     }
     TaskGroup* g = *pg;
     TaskMeta* m = g->_cur_meta;
+    if (m->interrupted.load(std::memory_order_acquire)) {  // interrupted before it slept
+        m->interrupted.store(false, std::memory_order_relaxed);
+        errno = m->stop ? ESTOP : EINTR;
+        return -1;
+    }
     uint64_t gen;
     {
         std::lock_guard<std::mutex> lk(m->sleep_mu);
@@ -494,7 +510,7 @@ int TaskGroup::interrupt(fiber_t tid, TaskControl* c) {
     {
         std::lock_guard<std::mutex> lk(m->version_lock);
         if ((uint32_t)m->version_butex->load(std::memory_order_relaxed) != tid_version(tid)) return EINVAL;
-        m->interrupted = true;
+        m->interrupted.store(true, std::memory_order_seq_cst);
     }
     ButexWaiter* w = m->current_waiter.exchange(nullptr, std::memory_order_acquire);
     if (w) {
@@ -502,7 +518,7 @@ int TaskGroup::interrupt(fiber_t tid, TaskControl* c) {
         m->current_waiter.store(w, std::memory_order_release);
         return 0;
     }
-    uint64_t sleep_id = m->current_sleep.exchange(0, std::memory_order_acquire);
+    uint64_t sleep_id = m->current_sleep.exchange(0, std::memory_order_seq_cst);
     if (sleep_id) {
         if (get_global_timer_thread()->unschedule(sleep_id) == 0) ready_to_run_general(tid);
     }

@@ -223,25 +223,27 @@ bool launch(CBatch* b, int device) {
         }
         if (!b->scratch) return false;
     }
-    // one fused launch when the batch is device-body work only: compress
-    // blocks and headerless pieces that fit the workgroup codec, and scans
-    // that each name the pieces forming their message
-    bool fused = FLAGS_codec_fused && nruns == 0 && ndec == 0 && h2d.empty() && d2h.empty() && ndecomp == 0 &&
-                 nstreams == 0 && (ncomp || nhpieces) && comp_max <= kFusedMaxBlock && hpiece_max <= kFusedMaxBlock;
-    for (size_t i = 0; fused && i < b->reqs.size(); ++i) {
+    // one fused launch when the batch is codec work only: compress blocks
+    // and headerless pieces that fit the one-launch kernels (the pb scans
+    // follow as a second launch unless -codec_fused_scan_in_kernel, which
+    // needs every scan to name the pieces forming its message)
+    const bool fused = FLAGS_codec_fused && nruns == 0 && ndec == 0 && h2d.empty() && d2h.empty() && ndecomp == 0 &&
+                       nstreams == 0 && (ncomp || nhpieces) && comp_max <= kFusedMaxBlock && hpiece_max <= kFusedMaxBlock;
+    bool scan_in_kernel = fused && FLAGS_codec_fused_scan_in_kernel && nscan > 0;
+    for (size_t i = 0; scan_in_kernel && i < b->reqs.size(); ++i) {
         const CodecRequest* r = b->reqs[i];
         if (r->scans.empty()) continue;
         if (r->scan_piece_first.size() != r->scans.size() || r->scan_piece_count.size() != r->scans.size()) {
-            fused = false;
+            scan_in_kernel = false;
             break;
         }
         for (size_t k = 0; k < r->scans.size(); ++k) {
             if (r->scan_piece_count[k] == 0 || r->scan_piece_first[k] + r->scan_piece_count[k] > r->pieces.size()) {
-                fused = false;
+                scan_in_kernel = false;
             }
         }
     }
-    if (fused && (!b->piece_group.reserve(nhpieces) || !b->group_pieces.reserve(nscan))) return false;
+    if (scan_in_kernel && (!b->piece_group.reserve(nhpieces) || !b->group_pieces.reserve(nscan))) return false;
     int prev = 0;
     hipGetDevice(&prev);
     if (prev != device) hipSetDevice(device);
@@ -249,22 +251,26 @@ bool launch(CBatch* b, int device) {
     b->ev = AcquireEvent();
     int rc = (s && b->ev) ? 0 : -1;
     if (rc == 0 && fused) {
-        if (nscan > b->group_done_cap) {
-            if (b->group_done) HbmFree(b->group_done, b->group_done_cap * sizeof(uint32_t), device);
-            const size_t cap = std::max<size_t>(nscan, 256);
-            b->group_done = static_cast<uint32_t*>(HbmAlloc(cap * sizeof(uint32_t), device));
-            b->group_done_cap = b->group_done ? cap : 0;
-            // ordered before the launch on the same stream
-            if (!b->group_done || hipMemsetAsync(b->group_done, 0, cap * sizeof(uint32_t), s) != hipSuccess) rc = -1;
-        }
-        for (size_t p = 0; p < nhpieces; ++p) b->piece_group.p[p] = kFusedNoGroup;
-        for (size_t i = 0; i < b->reqs.size(); ++i) {
-            const CodecRequest* r = b->reqs[i];
-            for (size_t k = 0; k < r->scans.size(); ++k) {
-                const size_t g = b->scan_row[i] + k;
-                b->group_pieces.p[g] = r->scan_piece_count[k];
-                for (uint32_t q = 0; q < r->scan_piece_count[k]; ++q)
-                    b->piece_group.p[b->piece_first[i] + r->scan_piece_first[k] + q] = (uint32_t)g;
+        if (scan_in_kernel) {
+            if (nscan > b->group_done_cap) {
+                if (b->group_done) HbmFree(b->group_done, b->group_done_cap * sizeof(uint32_t), device);
+                const size_t cap = std::max<size_t>(nscan, 256);
+                b->group_done = static_cast<uint32_t*>(HbmAlloc(cap * sizeof(uint32_t), device));
+                b->group_done_cap = b->group_done ? cap : 0;
+                // ordered before the launch on the same stream
+                if (!b->group_done || hipMemsetAsync(b->group_done, 0, cap * sizeof(uint32_t), s) != hipSuccess) {
+                    rc = -1;
+                }
+            }
+            for (size_t p = 0; p < nhpieces; ++p) b->piece_group.p[p] = kFusedNoGroup;
+            for (size_t i = 0; i < b->reqs.size(); ++i) {
+                const CodecRequest* r = b->reqs[i];
+                for (size_t k = 0; k < r->scans.size(); ++k) {
+                    const size_t g = b->scan_row[i] + k;
+                    b->group_pieces.p[g] = r->scan_piece_count[k];
+                    for (uint32_t q = 0; q < r->scan_piece_count[k]; ++q)
+                        b->piece_group.p[b->piece_first[i] + r->scan_piece_first[k] + q] = (uint32_t)g;
+                }
             }
         }
         FusedCodecArgs fa;
@@ -275,7 +281,6 @@ bool launch(CBatch* b, int device) {
         fa.pieces = b->piece_jobs.p;
         fa.npieces = (int)nhpieces;
         fa.piece_err = b->piece_job_err.p;
-        const bool scan_in_kernel = FLAGS_codec_fused_scan_in_kernel && nscan;
         fa.piece_group = scan_in_kernel ? b->piece_group.p : nullptr;
         fa.scans = b->scan_jobs.p;
         fa.group_pieces = b->group_pieces.p;

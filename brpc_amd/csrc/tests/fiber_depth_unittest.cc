@@ -247,3 +247,29 @@ TEST(FiberDepth, fiber_count_tracks_live_fibers) {
     for (int i = 0; i < 100 && fiber::fiber_count() > during - 50; ++i) ::usleep(1000);
     EXPECT_LE(fiber::fiber_count(), during - 50);
 }
+
+TEST(FiberDepth, interrupt_racing_a_sleep_never_loses_the_wake) {
+    // interrupt() issued while the target is still getting to, or just
+    // entering, its sleep: the sleep must end at once with EINTR (the
+    // publish of the sleep's timer and the interrupt used to race, and the
+    // fiber then slept its full time)
+    const int n = 200;
+    std::vector<fiber::fiber_t> ts(n);
+    std::vector<int> rcs(n, 0), errs(n, 0);
+    const int64_t t0 = monotonic_us();
+    for (int i = 0; i < n; ++i) {
+        fiber::start(
+            [&rcs, &errs, i] {
+                rcs[i] = fiber::usleep(3000000);
+                errs[i] = errno;
+            },
+            false, nullptr, &ts[i]);
+        if (i % 3 == 1) fiber::yield();
+        fiber::interrupt(ts[i]);
+    }
+    for (auto t : ts) fiber::join(t, nullptr);
+    EXPECT_LT(monotonic_us() - t0, 2000000);
+    int eintr = 0;
+    for (int i = 0; i < n; ++i) eintr += rcs[i] == -1 && errs[i] == EINTR;
+    EXPECT_EQ(eintr, n);
+}
