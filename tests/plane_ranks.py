@@ -49,7 +49,8 @@ def main():
     up = parallel.init_rccl_plane(topo, library=parallel.stub_library())
     server = start_echo_server("127.0.0.1:0", num_threads=3)
     addrs = parallel.exchange_addresses(server.address, topo)
-    others = [x for i, x in enumerate(addrs) if i != topo.rank]
+    # one rank: it presses its own server, so every payload goes to itself
+    others = [x for i, x in enumerate(addrs) if i != topo.rank] or [server.address]
     parallel.set_rccl_min_bytes(32768)
     out = {"rank": topo.rank, "world": topo.world_size, "plane_up": bool(up), "legs": []}
     import time

@@ -120,3 +120,17 @@ def test_plane_slow_rank_stalls_only_its_own_pairs():
     for r, (full, slow) in rates.items():
         if r not in slow_clients:
             assert slow > 0.5 * full, (r, rates)
+
+
+@pytest.mark.parametrize("pipeline", [0, 2])
+def test_plane_one_rank_self_payloads(pipeline):
+    """A one-rank plane: every payload goes from the rank to itself, moved
+    by one batched copy per group (-rccl_self_copy), with up to
+    -rccl_self_pipeline such groups in flight; every echoed byte checked."""
+    outs = _run(1, 29760 + pipeline, "--calls", "300,30",
+                "--flags", "rccl_self_pipeline=%d" % pipeline)
+    _check_legs(outs)
+    o = outs[0]
+    for leg in o["legs"]:
+        assert leg["sent_payloads"] >= leg["calls"], leg  # request and response both over the plane
+        assert leg["sent_payloads"] == leg["recv_payloads"], leg
