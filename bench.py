@@ -348,6 +348,7 @@ def main(argv=None):
                 "copy_launches": x["copy_launches"],
                 "rccl_payloads": r["recv_payloads"], "rccl_rounds": r["rounds"], "rccl_aborts": r["aborts"],
                 "rccl_credit_stalls": r["credit_stalls"], "rccl_recv_timeouts": r["recv_timeouts"],
+                "rccl_group_us": r["group_us"],
                 "hbm_fallback_allocs": hbm["fallback_allocs"], "hbm_block_splits": hbm["splits"]}
 
     def transport_delta(s0):
@@ -1137,6 +1138,8 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
         tr = rc["transport"]
         out["rccl_payloads"] = tr.get("rccl_payloads", 0)
         out["rccl_payloads_per_round"] = round(tr.get("rccl_payloads", 0) / max(1, tr.get("rccl_rounds", 0)), 2)
+        # issue-to-completion wall time of a group on the plane stream
+        out["rccl_group_us_per_round"] = round(tr.get("rccl_group_us", 0) / max(1, tr.get("rccl_rounds", 0)), 2)
         out["rccl_aborts"] = extra.get("plane_aborts", tr.get("rccl_aborts", 0))
         out["rccl_world"] = tr["rccl_world"]
         if tr["rccl_world"] == 1:

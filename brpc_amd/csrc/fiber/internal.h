@@ -16,8 +16,11 @@
 #include <mutex>
 #include <vector>
 
+#include "base/flags.h"
 #include "base/macros.h"
 #include "fiber/fiber.h"
+
+DECLARE_bool(fiber_signal_parked_only);
 
 namespace mrpc {
 namespace fiber {
@@ -95,6 +98,15 @@ private:
 };
 
 // Idle workers sleep here. Value = signal count << 1 | stopped bit.
+//
+// A signal only enters the kernel when a worker is parked: under load every
+// worker is running or spinning, and an unconditional FUTEX_WAKE costs a
+// syscall per lot tried (signal_task walks up to kParkingLots of them) on
+// every ready fiber. Dekker pair, both sides seq_cst: the signaler bumps
+// _pending then reads _waiters; a parker bumps _waiters then lets the
+// kernel compare _pending. A signaler that saw no waiter is ordered before
+// the parker's increment, so the parker's compare sees the new _pending and
+// does not sleep.
 class MRPC_CACHELINE_ALIGNED ParkingLot {
 public:
     struct State {
@@ -103,14 +115,21 @@ public:
     };
     ParkingLot() : _pending(0) {}
     int signal(int n) {
-        _pending.fetch_add(n << 1, std::memory_order_release);
+        _pending.fetch_add(n << 1, std::memory_order_seq_cst);
+        if (_waiters.load(std::memory_order_seq_cst) == 0 && FLAGS_fiber_signal_parked_only) return 0;
         return futex_wake_private(&_pending, n);
     }
     State get_state() { return State{_pending.load(std::memory_order_acquire)}; }
-    void wait(const State& expected) { futex_wait_private(&_pending, expected.val, nullptr); }
+    void wait(const State& expected) {
+        _waiters.fetch_add(1, std::memory_order_seq_cst);
+        futex_wait_private(&_pending, expected.val, nullptr);
+        _waiters.fetch_sub(1, std::memory_order_relaxed);
+    }
     void wait_for(const State& expected, int64_t timeout_ns) {
         const timespec ts{(time_t)(timeout_ns / 1000000000), (long)(timeout_ns % 1000000000)};
+        _waiters.fetch_add(1, std::memory_order_seq_cst);
         futex_wait_private(&_pending, expected.val, &ts);
+        _waiters.fetch_sub(1, std::memory_order_relaxed);
     }
     void stop() {
         _pending.fetch_or(1);
@@ -119,6 +138,7 @@ public:
 
 private:
     std::atomic<int> _pending;
+    std::atomic<int> _waiters{0};  // workers inside wait()/wait_for()
 };
 
 struct KeyTable;

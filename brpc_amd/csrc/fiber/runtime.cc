@@ -68,6 +68,9 @@ DEFINE_int32(fiber_worker_cpu_offset, -1,
              "one process per GPU passes local_rank * cpus_per_rank");
 // Off by default: on the MI355X box (16-CPU quota) idle spinning cost more
 // throughput than it saved latency (profiles/bench_r1_spin_ab.txt).
+DEFINE_bool(fiber_signal_parked_only, true,
+            "a ready fiber enters the kernel (FUTEX_WAKE) only when a worker is parked; false: every signal "
+            "wakes unconditionally, one syscall per parking lot tried");
 DEFINE_int32(fiber_idle_spin_us, 0,
              "an idle worker polls for new fibers this long before sleeping on its parking lot "
              "(trades CPU for futex-wakeup latency on the RPC round trip; 0 disables)");

@@ -57,6 +57,9 @@ DEFINE_int32(rccl_fire_grace_us, 40,
              "once a pair round fired, wait up to this long for the other pairs this rank is ready with to fire "
              "too before building the group (each ready bit cleared unfired is a withdrawal: its payloads go "
              "back to the queue for a later round)");
+DEFINE_int32(rccl_poll_spin_us, 0,
+             "the poster polls its in-flight group's completion with pause loops this long before it yields "
+             "the core between polls");
 DEFINE_int32(rccl_test_poster_delay_us, 0,
              "test only: the poster sleeps this long after every group (a slow or preempted rank)");
 
@@ -1058,11 +1061,16 @@ public:
             }
             if (q == 0) {
                 if (!block) return 0;
-                if (monotonic_us() - t0 > (int64_t)FLAGS_rccl_timeout_ms * 1000) {
+                const int64_t waited = monotonic_us() - t0;
+                if (waited > (int64_t)FLAGS_rccl_timeout_ms * 1000) {
                     abort("a self payload copy made no progress within -rccl_timeout_ms", true);
                     return -1;
                 }
-                std::this_thread::yield();
+                if (waited < FLAGS_rccl_poll_spin_us) {
+                    for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+                } else {
+                    std::this_thread::yield();
+                }
                 continue;
             }
             ops->release(f.marker);
@@ -1168,8 +1176,13 @@ public:
                 abort(std::string(bell->reason), false);
                 return -1;
             }
-            if (++spins < 200) std::this_thread::yield();
-            else usleep(20);
+            if (now - t0 < FLAGS_rccl_poll_spin_us) {
+                for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+            } else if (++spins < 200) {
+                std::this_thread::yield();
+            } else {
+                usleep(20);
+            }
         }
         ops->release(marker);
         marker_live = false;

@@ -273,3 +273,56 @@ TEST(FiberDepth, interrupt_racing_a_sleep_never_loses_the_wake) {
     for (int i = 0; i < n; ++i) eintr += rcs[i] == -1 && errs[i] == EINTR;
     EXPECT_EQ(eintr, n);
 }
+
+TEST(FiberDepth, parked_workers_never_miss_a_signal) {
+    // A signal skips FUTEX_WAKE when no worker sits in its parking lot
+    // (-fiber_signal_parked_only). Four plain pthreads start fibers and
+    // wake butex waiters at irregular gaps, so workers park, nap and spin
+    // while signals arrive: every fiber must run, none may wait for an
+    // unrelated event to be noticed.
+    std::atomic<int> failures{0};
+    std::vector<pthread_t> th(4);
+    for (auto& t : th) {
+        pthread_create(
+            &t, nullptr,
+            [](void* arg) -> void* {
+                auto* fails = static_cast<std::atomic<int>*>(arg);
+                for (int i = 0; i < 150; ++i) {
+                    usleep(i % 25 == 0 ? 15000 : 50 + (i * 37) % 400);
+                    std::atomic<int> done{0};
+                    fiber::fiber_t f;
+                    if (fiber::start_background(&f, nullptr, set_flag, &done) != 0) {
+                        fails->fetch_add(1);
+                        continue;
+                    }
+                    const int64_t t0 = monotonic_us();
+                    while (done.load() == 0 && monotonic_us() - t0 < 2000000) usleep(20);
+                    if (done.load() == 0) fails->fetch_add(1);
+                    fiber::join(f, nullptr);
+                    // a fiber parked on a butex, woken from this pthread
+                    std::atomic<int>* b = fiber::butex_create();
+                    b->store(0);
+                    std::atomic<int> woke{0};
+                    fiber::fiber_t w;
+                    fiber::start(
+                        [b, &woke] {
+                            while (b->load() == 0) fiber::butex_wait(b, 0, nullptr);
+                            woke.store(1);
+                        },
+                        false, nullptr, &w);
+                    usleep(30 + i % 90);
+                    b->store(1);
+                    fiber::butex_wake_all(b);
+                    const int64_t t1 = monotonic_us();
+                    while (woke.load() == 0 && monotonic_us() - t1 < 2000000) usleep(20);
+                    if (woke.load() == 0) fails->fetch_add(1);
+                    fiber::join(w, nullptr);
+                    fiber::butex_destroy(b);
+                }
+                return nullptr;
+            },
+            &failures);
+    }
+    for (auto& t : th) pthread_join(t, nullptr);
+    EXPECT_EQ(failures.load(), 0);
+}
