@@ -51,8 +51,14 @@ def main():
     ap.add_argument("--block", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--kinds", default="text,random,const")
+    ap.add_argument("--flag", action="append", default=[], help="NAME=VALUE runtime flag (repeatable)")
+    ap.add_argument("--compress-only", action="store_true")
+    ap.add_argument("--places", default="hbm", help="input/output placements to run: hbm or hbm,pinned")
     a = ap.parse_args()
     from brpc_amd import native
+    for f in a.flag:
+        k, v = f.split("=", 1)
+        native.set_flag(k, v)
     from brpc_amd.ops._common import stream_handle
     dev = torch.device("cuda", 0)
     st = stream_handle(dev)
@@ -100,8 +106,8 @@ def main():
             comps.append(c[h:])
         packed = b"".join(comps)
         ratio = total / max(1, len(packed))
-        for src_at in ("hbm", "pinned"):
-            for dst_at in ("hbm", "pinned"):
+        for src_at in ([] if a.compress_only else a.places.split(",")):
+            for dst_at in a.places.split(","):
                 cin = place(packed, src_at)
                 out = empty(total, dst_at)
                 rec, pos = b"", 0
@@ -139,8 +145,8 @@ def main():
         scratch = torch.empty(npieces * int(native.gpu.snappy_compress_scratch_per_block()), dtype=torch.uint8,
                               device=dev)
         meta = torch.zeros(2 * npieces, dtype=torch.int32, device=dev)
-        for src_at in ("hbm", "pinned"):
-            for dst_at in ("hbm", "pinned"):
+        for src_at in a.places.split(","):
+            for dst_at in a.places.split(","):
                 rin = place(raw, src_at)
                 slots = empty(npieces * cap, dst_at)
                 cj = []
@@ -164,8 +170,12 @@ def main():
                 torch.cuda.synchronize()
                 t = stamps.cpu().tolist()
                 # shader-clock cycles per phase of block 0
-                phases = {k: t[i + 1] - t[i] for i, k in enumerate(("stage", "first_pos", "match", "write"))}
-                print(json.dumps({"kernel": "snappy_compress", "body": kind, "src": src_at, "dst": dst_at,
+                names = (("stage", "cand_len", "chain", "emit") if native.get_flag("gpu_snappy_compress_pj") == "true"
+                         else ("stage", "first_pos", "match", "write"))
+                phases = {k: t[i + 1] - t[i] for i, k in enumerate(names)}
+                if names[1] == "cand_len":
+                    phases["doubling_rounds"] = t[5]
+                print(json.dumps({"kernel": "snappy_compress", "body": kind, "flags": a.flag, "src": src_at, "dst": dst_at,
                                   "block0_phase_cycles": phases,
                                   "blocks": npieces, "bytes_in": total,
                                   "ratio": round(total / max(1, sum(lens)), 3),

@@ -23,6 +23,10 @@ DEFINE_bool(codec_fused_scan_in_kernel, false,
             "(else the pb scan is a second launch). Off: the hand-off needs a device-scope fence per piece, "
             "which on gfx950 compiles to buffer_wbl2 + buffer_inv (an L2 write-back of the XCD) in every wave; "
             "in the RPC leg, with batches overlapping, that made the one-launch kernels 1.5-4x slower per launch");
+DEFINE_bool(gpu_snappy_compress_pj, false,
+            "snappy blocks up to 4 KiB compress with the data-parallel parse (every position's candidate and "
+            "match length at once, the greedy element chain by pointer doubling; snappy_kernels.hip "
+            "compress_wave_pj) instead of per-lane slices whose matches stop at the slice end");
 DEFINE_string(codec_fused_kernel, "waves",
               "kernel of the one-launch codec batch: 'waves' (one wave per block/piece, snappy_kernels.hip) or "
               "'workgroup' (one 1024-thread workgroup per block/piece, codec_fused.hip)");
