@@ -25,14 +25,17 @@ DEFINE_bool(codec_fused_scan_in_kernel, false,
             "in the RPC leg, with batches overlapping, that made the one-launch kernels 1.5-4x slower per launch");
 DEFINE_bool(gpu_snappy_compress_pj, false,
             "snappy blocks up to 4 KiB compress with the data-parallel parse (every position's candidate and "
-            "match length at once, the greedy element chain by pointer doubling; snappy_kernels.hip "
-            "compress_wave_pj) instead of per-lane slices whose matches stop at the slice end");
+            "match length at once, the greedy element chain by speculative slice walks; snappy_kernels.hip "
+            "compress_wave_pj) instead of per-lane slices whose matches stop at the slice end: ratio 2.14 vs "
+            "1.96 on 2 KiB text blocks, but 47 vs 28 us per launch, so off");
 DEFINE_string(codec_fused_kernel, "waves",
               "kernel of the one-launch codec batch: 'waves' (one wave per block/piece, snappy_kernels.hip) or "
               "'workgroup' (one 1024-thread workgroup per block/piece, codec_fused.hip)");
-DEFINE_int32(codec_batch_max_inflight, 6,
+DEFINE_int32(codec_batch_max_inflight, 4,
              "codec batches in flight per device before the next one waits for a completion (0: no limit); "
-             "while it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches");
+             "while it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches "
+             "(device text leg, 50 RPCs in flight: 4 -> 171-174k QPS with the codec events polled "
+             "continuously, 6 -> 161-163k, 3 -> 161k, 8 -> 142k; profiles/r5_device_codec_ab.txt)");
 
 namespace mrpc {
 namespace gpu {

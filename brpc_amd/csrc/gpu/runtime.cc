@@ -30,6 +30,12 @@ DEFINE_int32(gpu_poller_wait_pct, 50,
              "the event poller sleeps until the oldest in-flight event reached this share of the recent "
              "hand-over-to-completion time before polling (0: poll continuously)");
 DEFINE_int32(gpu_poller_sleep_us, 2, "event poller sleep between polls once the spin budget is spent");
+DEFINE_int32(gpu_poller_codec_wait_pct, 0,
+             "-gpu_poller_wait_pct for codec-batch events (0: poll them continuously: a device-body RPC waits "
+             "on four codec batches in a row, and the nap before each completion was measured on its latency)");
+DEFINE_int32(gpu_poller_codec_idle_spin_us, 100,
+             "after a codec batch completed, an idle event poller watches for the next one this long before "
+             "sleeping on its condvar (codec streams hand over a batch every few tens of microseconds)");
 DEFINE_int32(gpu_poller_idle_spin_us, 0,
              "with nothing in flight the event poller watches for new events this long before sleeping "
              "(saves a condvar wake-up per batch on busy RPC streams; costs that much CPU per idle period)");
@@ -127,6 +133,7 @@ private:
     void loop() {
         std::vector<Waiter> active;
         int64_t last_progress_us = 0;
+        int64_t last_codec_done_us = INT64_MIN / 2;
         for (;;) {
             bool progressed = false;
             if (active.empty()) {
@@ -134,7 +141,10 @@ private:
                 // sleeping — the next batch of a busy RPC stream is usually
                 // microseconds away, and a condvar wake-up costs a kernel
                 // round trip (and a CPU idle exit) per batch
-                const int64_t until = now_us() + std::max(0, FLAGS_gpu_poller_idle_spin_us);
+                const int64_t t0 = now_us();
+                int spin = std::max(0, FLAGS_gpu_poller_idle_spin_us);
+                if (t0 - last_codec_done_us < 1000) spin = std::max(spin, FLAGS_gpu_poller_codec_idle_spin_us);
+                const int64_t until = t0 + spin;
                 while (!_nincoming.load(std::memory_order_acquire) && now_us() < until) {
                     for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
                 }
@@ -178,6 +188,7 @@ private:
                 {
                     const int64_t t = now_us();
                     if (active[i].done_us) *active[i].done_us = t;
+                    if (active[i].cls == kEventCodec) last_codec_done_us = t;
                     // how long events take from hand-over to completion
                     const int64_t took = t - active[i].added_us;
                     int64_t& ema = _ema_us[active[i].cls];
@@ -205,15 +216,18 @@ private:
                 // sets the nap (one global average let a short
                 // copy behind long codec batches wait up to 200 us).
                 int64_t due = INT64_MAX, shortest = INT64_MAX;
+                bool eager = false;  // an event whose class polls continuously (wait share 0)
                 for (const Waiter& w : active) {
                     const int64_t ema = _ema_us[w.cls];
-                    due = std::min(due, w.added_us + ema * FLAGS_gpu_poller_wait_pct / 100);
+                    const int pct = w.cls == kEventCodec ? FLAGS_gpu_poller_codec_wait_pct : FLAGS_gpu_poller_wait_pct;
+                    eager |= pct <= 0;
+                    due = std::min(due, w.added_us + ema * std::max(0, pct) / 100);
                     shortest = std::min(shortest, ema);
                 }
                 int64_t sleep_us = 0;
-                if (FLAGS_gpu_poller_wait_pct > 0 && due - t >= 8) {
+                if (!eager && due - t >= 8) {
                     sleep_us = std::min<int64_t>(due - t, 200);
-                } else if (!progressed && FLAGS_gpu_poller_wait_pct > 0 && shortest >= 20) {
+                } else if (!eager && !progressed && shortest >= 20) {
                     // only long events pending (codec batches, large pulls):
                     // one pass per ~tenth of the shortest class's duration
                     sleep_us = std::max<int64_t>(2, std::min<int64_t>(shortest / 10, 10));
