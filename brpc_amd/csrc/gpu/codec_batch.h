@@ -59,6 +59,36 @@ struct CodecRequest {
     std::vector<int32_t> dec_err;      // per decode chunk: 0, or 1 for a malformed varint
     std::vector<uint64_t> scan_fields;  // 2 * kCodecScanFields per scan
     std::vector<int32_t> scan_nfields;  // per scan: field count or a negative code
+
+    // Empty again, keeping every vector's capacity (pooled requests: the
+    // device codec path issued ~20 allocations per RPC building fresh ones).
+    void Reset() {
+        runs.clear();
+        h2d.clear();
+        comp.clear();
+        decomp.clear();
+        comp_max_ulen = decomp_max_ulen = 0;
+        streams.clear();
+        stream_piece_limit = 4096;
+        pieces.clear();
+        pieces_max_ulen = 0;
+        scans.clear();
+        scan_piece_first.clear();
+        scan_piece_count.clear();
+        d2h.clear();
+        dec_runs.clear();
+        comp_len.clear();
+        decomp_len.clear();
+        comp_err.clear();
+        decomp_err.clear();
+        stream_err.clear();
+        piece_err.clear();
+        run_err.clear();
+        dec_counts.clear();
+        dec_err.clear();
+        scan_fields.clear();
+        scan_nfields.clear();
+    }
 };
 
 constexpr uint32_t kCodecScanFields = 128;

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "base/flags.h"
+#include "base/pool.h"
 #include "gpu/codec_batch.h"
 #include "gpu/hbm_pool.h"
 #include "gpu/kernels.h"
@@ -62,6 +63,16 @@ void fill_index(const CodecRequest& req, size_t row, DevicePayloadIndex* out) {
     out->fields.assign(f, f + 2 * n);
 }
 
+// A CodecRequest from the object pool, emptied but with its vectors'
+// capacity (the encode and decode of every device-body RPC build one).
+struct PooledRequest {
+    CodecRequest* r;
+    PooledRequest() : r(get_object<CodecRequest>()) { r->Reset(); }
+    ~PooledRequest() { return_object(r); }
+    PooledRequest(const PooledRequest&) = delete;
+    PooledRequest& operator=(const PooledRequest&) = delete;
+};
+
 }  // namespace
 
 DeviceSnappyLayout DeviceSnappyLayoutFor(size_t len) {
@@ -77,7 +88,8 @@ int DeviceSnappyEncode(const void* src, size_t len, void* dst, const DeviceSnapp
     if (!src || !dst || len == 0 || lay.nblocks == 0) return -1;
     const char* s = static_cast<const char*>(src);
     char* d = static_cast<char*>(dst);
-    CodecRequest req;
+    PooledRequest pooled;
+    CodecRequest& req = *pooled.r;
     req.comp.resize(lay.nblocks);
     for (uint32_t i = 0; i < lay.nblocks; ++i) {
         req.comp[i] = SnappyJob{s + (size_t)i * lay.block_ulen, d + (size_t)i * lay.stride, block_len(lay, len, i),
@@ -98,7 +110,8 @@ int DeviceSnappyEncode(const void* src, size_t len, void* dst, const DeviceSnapp
 }
 
 int DeviceSnappyDecode(const DeviceSnappyBlocks* jobs, int n, int* err, DevicePayloadIndex* index, int device) {
-    CodecRequest req;
+    PooledRequest pooled;
+    CodecRequest& req = *pooled.r;
     std::vector<size_t> first(n, 0), count(n, 0), scan_row(n, (size_t)-1);
     for (int k = 0; k < n; ++k) {
         const DeviceSnappyBlocks& j = jobs[k];
