@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "base/flags.h"
+#include "gpu/codec_batch.h"
 #include "gpu/device_codec.h"
 #include "gpu/kernels.h"
 #include "mrpc/proto/device_payload.pb.h"
@@ -180,4 +181,55 @@ TEST(DeviceCodec, packed_runs_with_bad_arguments_are_refused_before_any_launch) 
     EXPECT_EQ(runs[3].err, 0);
     EXPECT_EQ(runs[3].count, 0u);
     EXPECT_EQ(gpu::DeviceDecodePackedRuns(runs, 0, 0), 0);
+}
+
+TEST(DeviceCodec, pooled_request_reset_matches_a_fresh_one) {
+    // the device codec reuses CodecRequests from a pool: Reset() must leave
+    // every job list and result empty and every limit at its default, or a
+    // pooled request would carry jobs of the previous RPC into the next batch
+    gpu::CodecRequest r;
+    const gpu::CodecRequest fresh;
+    r.runs.resize(2);
+    r.h2d.resize(3);
+    r.comp.resize(4);
+    r.decomp.resize(5);
+    r.comp_max_ulen = 77;
+    r.decomp_max_ulen = 88;
+    r.streams.resize(1);
+    r.stream_piece_limit = 123;
+    r.pieces.resize(6);
+    r.pieces_max_ulen = 99;
+    r.scans.resize(2);
+    r.scan_piece_first.resize(2);
+    r.scan_piece_count.resize(2);
+    r.d2h.resize(1);
+    r.dec_runs.resize(3);
+    r.comp_len.resize(4);
+    r.decomp_len.resize(5);
+    r.comp_err.resize(4);
+    r.decomp_err.resize(5);
+    r.stream_err.resize(1);
+    r.piece_err.resize(6);
+    r.run_err.resize(2);
+    r.dec_counts.resize(3);
+    r.dec_err.resize(3);
+    r.scan_fields.resize(8);
+    r.scan_nfields.resize(2);
+    const size_t cap = r.pieces.capacity();
+    r.Reset();
+    EXPECT_TRUE(r.runs.empty() && r.h2d.empty() && r.comp.empty() && r.decomp.empty() && r.streams.empty());
+    EXPECT_TRUE(r.pieces.empty() && r.scans.empty() && r.scan_piece_first.empty() && r.scan_piece_count.empty());
+    EXPECT_TRUE(r.d2h.empty() && r.dec_runs.empty() && r.comp_len.empty() && r.decomp_len.empty());
+    EXPECT_TRUE(r.comp_err.empty() && r.decomp_err.empty() && r.stream_err.empty() && r.piece_err.empty());
+    EXPECT_TRUE(r.run_err.empty() && r.dec_counts.empty() && r.dec_err.empty() && r.scan_fields.empty());
+    EXPECT_TRUE(r.scan_nfields.empty());
+    EXPECT_EQ(r.comp_max_ulen, fresh.comp_max_ulen);
+    EXPECT_EQ(r.decomp_max_ulen, fresh.decomp_max_ulen);
+    EXPECT_EQ(r.stream_piece_limit, fresh.stream_piece_limit);
+    EXPECT_EQ(r.pieces_max_ulen, fresh.pieces_max_ulen);
+    EXPECT_EQ(r.pieces.capacity(), cap);  // capacity kept: no allocation on the next use
+    // 22 lists and 4 limits (x86-64 layout, with the padding after the two
+    // lone limits): a member added later changes the size, and this test
+    // (and Reset()) must learn about it
+    EXPECT_EQ(sizeof(gpu::CodecRequest), 22 * sizeof(std::vector<int>) + 4 * sizeof(uint32_t) + 8);
 }
