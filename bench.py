@@ -115,7 +115,90 @@ def parse(argv=None):
                     help="watchdog: print what was measured and end every rank at this many wall seconds")
     ap.add_argument("--only", default="", help="comma-separated leg names: run only these (experiments)")
     ap.add_argument("--stall-leg", default="", help=argparse.SUPPRESS)  # test hook: NAME[:hang]
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # test hook: that rank exits 3
+    ap.add_argument("--spawn-grace-s", type=float, default=30.0,
+                    help="self-launched ranks: once one rank failed, the others get this long before they are killed")
     return ap.parse_args(argv)
+
+
+def spawn_ranks(a, argv):
+    """`python bench.py --gpus N` without a launcher: start N ranks here
+    (tools/rpc_press/rpc_press.cpp:27-46 honours -thread_num by itself; this
+    honours --gpus). Runs BEFORE torch is imported or any GPU call is made:
+    the parent only starts children (fork + exec of a fresh interpreter),
+    relays rank 0's JSON line to stdout (its other output to stderr) and returns the worst exit
+    status. Every rank gets torchrun's variables with a rendezvous on
+    127.0.0.1; other ranks' stdout goes to stderr, so exactly one JSON line
+    reaches the caller. When a rank fails the others get --spawn-grace-s to
+    finish (a rank stuck in a collective with a dead peer never would) and
+    are then killed, so a broken rank cannot hang the job."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    me = os.path.abspath(__file__)
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus),
+                   LOCAL_WORLD_SIZE=str(a.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   MRPC_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, me] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(),
+                                      start_new_session=True))
+
+    def relay():
+        for line in procs[0].stdout:
+            text = line.decode(errors="replace")
+            # the JSON line to stdout; library chatter (gloo) to stderr
+            out = sys.stdout if text.startswith("{") else sys.stderr
+            out.write(text)
+            out.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    worst, fail_at = 0, None
+    while True:
+        rcs = [p.poll() for p in procs]
+        for rc in rcs:
+            if rc is not None and rc != 0:
+                # a signal death (-N) ranks as its shell status 128+N
+                code = rc if rc > 0 else 128 - rc
+                worst = max(worst, code)
+                if fail_at is None:
+                    fail_at = time.monotonic()
+                    print("bench: a rank exited with status %d; the others get %.0f s" % (code, a.spawn_grace_s),
+                          file=sys.stderr, flush=True)
+        if all(rc is not None for rc in rcs):
+            break
+        if fail_at is not None and time.monotonic() - fail_at > a.spawn_grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except OSError:
+                        pass
+                    p.wait()
+                    worst = max(worst, 128 + signal.SIGKILL)
+            break
+        time.sleep(0.1)
+    t.join(timeout=5.0)
+    return worst
+
+
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters (nr_throttled, throttled_usec, ...)."""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
 
 
 def cpu_quota():
@@ -246,15 +329,25 @@ class Watchdog(threading.Thread):
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = parse(argv)
+    env_ws = os.environ.get("WORLD_SIZE")
+    if env_ws is None and a.gpus > 1:
+        return spawn_ranks(a, argv)
+    if int(env_ws or "1") != a.gpus:
+        # a launcher that started a different number of ranks than asked
+        # for would report a curve point for the wrong N
+        print("bench: --gpus %d but WORLD_SIZE %s: refusing to run" % (a.gpus, env_ws or "1"), file=sys.stderr)
+        return 2
+    if a.fail_rank >= 0 and int(os.environ.get("RANK", "0")) == a.fail_rank:
+        print("bench: --fail-rank %d: exiting" % a.fail_rank, file=sys.stderr, flush=True)
+        return 3
     import torch  # noqa: E402
     from brpc_amd import native  # noqa: E402
     from brpc_amd.models import ECHO_32B, ECHO_64KB, EchoWorkload, start_echo_server  # noqa: E402
     from brpc_amd import parallel  # noqa: E402
 
     topo = parallel.init_distributed()
-    if topo.world_size != a.gpus:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (a.gpus, topo.world_size), file=sys.stderr)
     workers = a.workers or auto_workers(topo.local_world_size)
     for f in a.flag:
         k, _, v = f.partition("=")
@@ -360,6 +453,39 @@ def main(argv=None):
         d["xgmi_peer_access_pairs_total"] = int(parallel.allreduce_sum(s1["xgmi_peer_access_pairs"], topo))
         return d
 
+    # Where a leg's time goes (summed over ranks): the copy engine's
+    # per-submission breakdown (waiting for the batch to be issued, the
+    # launch API calls, issue -> completion seen by the poller, completion
+    # -> the fiber resumed), segments per launch, and the CPU-quota
+    # throttling the leg suffered (cgroup cpu.stat).
+    def diag_snapshot():
+        x = native.gpu.xgmi_stats()
+        d = {k: x[k] for k in ("copy_submits", "copy_launches", "copy_segments", "copy_queue_us", "copy_api_us",
+                               "copy_gpu_us", "copy_wake_us")}
+        d["polled_events"] = native.gpu.polled_events() if cuda else 0
+        cg = cgroup_cpu_stat()
+        d["cg_nr_throttled"] = cg.get("nr_throttled", 0)
+        d["cg_throttled_usec"] = cg.get("throttled_usec", 0)
+        return d
+
+    def diag_delta(d0):
+        d1 = diag_snapshot()
+        d = {k: parallel.allreduce_sum(d1[k] - d0[k], topo) for k in d0}
+        out = {}
+        subs = d["copy_submits"]
+        if subs > 0:
+            out["copy_submits"] = int(subs)
+            out["copy_segments_per_launch"] = round(d["copy_segments"] / max(1, d["copy_launches"]), 2)
+            for k in ("queue", "api", "gpu", "wake"):
+                out["copy_%s_us_per_submit" % k] = round(d["copy_%s_us" % k] / subs, 1)
+        if d["polled_events"]:
+            out["polled_events"] = int(d["polled_events"])
+        # the box's quota is shared by every rank: take one rank's view
+        if d["cg_nr_throttled"]:
+            out["cgroup_throttled_periods"] = int(d["cg_nr_throttled"] / n)
+            out["cgroup_throttled_ms"] = round(d["cg_throttled_usec"] / n / 1000.0, 1)
+        return out
+
     def transport_check(tr, kind, cross_gpu):
         """Did the leg's payloads take the transport it is meant to
         measure? kind: "lend" (HBM attachments between ranks over xGMI),
@@ -460,11 +586,12 @@ def main(argv=None):
         if press is not None:
             press.reset_stats()
         tr0 = transport_snapshot()
+        dg0 = diag_snapshot()
         parallel.barrier(topo)
         sync()
         ru0 = resource.getrusage(resource.RUSAGE_SELF)
         t0 = time.perf_counter()
-        step_s = []
+        step_s, step_n = [], []
         k = 0
         while press is not None and not cut:
             if k >= steps and time.perf_counter() - t0 >= min_s:
@@ -474,9 +601,11 @@ def main(argv=None):
             if rem <= 0:
                 cut = True
                 break
-            if press.run_requests(nreq, rem) > 0:
+            unissued = press.run_requests(nreq, rem)
+            if unissued > 0:
                 cut = True
             step_s.append(time.perf_counter() - ts)
+            step_n.append(max(0, nreq - unissued))
             k += 1
             if k == 1:
                 stall_hook(name, deadline)
@@ -504,8 +633,9 @@ def main(argv=None):
         steps_done = int(-parallel.allreduce_max(-len(step_s), topo))
         del press
         tr = transport_delta(tr0)
+        dg = diag_delta(dg0)
         ok, why = transport_check(tr, transport_kind, cross_gpu)
-        step_seq = [nreq / x for x in step_s if x > 0]
+        step_seq = [c / x for c, x in zip(step_n, step_s) if x > 0]
         step_qps = sorted(step_seq)
         r = {
             "step_qps_seq": [int(q) for q in step_seq],
@@ -524,6 +654,7 @@ def main(argv=None):
             "step_qps_min": step_qps[0] if step_qps else 0.0,
             "step_qps_max": step_qps[-1] if step_qps else 0.0,
             "transport": tr,
+            "diag": dg,
             "cpu_us_per_rpc": round(cpu_us_per_rpc, 2),
         }
         if timed_out:
@@ -1171,6 +1302,10 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
     # host CPU microseconds per RPC of each leg (whole rank: client,
     # server, dispatcher, pollers)
     out["cpu_us_per_rpc"] = {k: v["cpu_us_per_rpc"] for k, v in timed.items() if "cpu_us_per_rpc" in v}
+    # where each leg's time went (copy-engine breakdown, CPU throttling)
+    dg = {k: v["diag"] for k, v in timed.items() if v.get("diag")}
+    if dg:
+        out["diag"] = dg
     # per-leg transport verdict (N > 1): a silent staging fallback shows here
     tok = {k: v["transport_ok"] for k, v in legs.items() if isinstance(v, dict) and "transport_ok" in v}
     if tok:
@@ -1262,4 +1397,4 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -20,6 +20,8 @@ def main(path):
     for k in ("timed_out_legs", "failed_legs", "skipped_legs", "error_detail", "transport_problems"):
         if k in j:
             print("  %s: %s" % (k, j[k]))
+    for k, v in sorted(j.get("diag", {}).items()):
+        print("  diag %-43s %s" % (k, v))
     for k, v in j.items():
         if k.endswith("_device") and isinstance(v, dict):
             print("  %s: %s" % (k, v))
