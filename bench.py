@@ -461,7 +461,7 @@ def main(argv=None):
     def diag_snapshot():
         x = native.gpu.xgmi_stats()
         d = {k: x[k] for k in ("copy_submits", "copy_launches", "copy_segments", "copy_queue_us", "copy_api_us",
-                               "copy_gpu_us", "copy_wake_us")}
+                               "copy_gpu_us", "copy_wake_us", "copy_kernel_ticks", "copy_kernel_timed")}
         d["polled_events"] = native.gpu.polled_events() if cuda else 0
         cg = cgroup_cpu_stat()
         d["cg_nr_throttled"] = cg.get("nr_throttled", 0)
@@ -478,6 +478,11 @@ def main(argv=None):
             out["copy_segments_per_launch"] = round(d["copy_segments"] / max(1, d["copy_launches"]), 2)
             for k in ("queue", "api", "gpu", "wake"):
                 out["copy_%s_us_per_submit" % k] = round(d["copy_%s_us" % k] / subs, 1)
+        if d["copy_kernel_timed"] > 0:
+            # kernel start -> end on the GPU's 100 MHz wall clock, per launch:
+            # against copy_gpu_us (launch -> completion seen) it splits the
+            # device time into queueing and running
+            out["copy_kernel_us_per_launch"] = round(d["copy_kernel_ticks"] / d["copy_kernel_timed"] / 100.0, 1)
         if d["polled_events"]:
             out["polled_events"] = int(d["polled_events"])
         # the box's quota is shared by every rank: take one rank's view

@@ -12,9 +12,15 @@ cd - > /dev/null
 export WORLD_SIZE=2 LOCAL_WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 GROUP_RANK=0
 ARGS="--gpus 2 --steps 2 --warmup 1 --requests-per-step-64k 4000 --only echo_64KB --skip-rccl --latency-sample-s 0
       --time-budget-s 100 --hard-deadline-s 140"
+# PROF=0: the same two ranks without the profiler
+ARGS="$ARGS ${EXTRA:-}"
 for r in 0 1; do
-    RANK=$r LOCAL_RANK=$r timeout -k 10 200 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv \
-        -d $OUT/r$r -o r$r -- python3 bench.py $ARGS > $OUT/r$r.out 2> $OUT/r$r.err &
+    if [ "${PROF:-1}" = 1 ]; then
+        RANK=$r LOCAL_RANK=$r timeout -k 10 200 rocprofv3 ${PROFARGS:---kernel-trace --hip-runtime-trace} --output-format csv \
+            -d $OUT/r$r -o r$r -- python3 bench.py $ARGS > $OUT/r$r.out 2> $OUT/r$r.err &
+    else
+        RANK=$r LOCAL_RANK=$r timeout -k 10 200 python3 bench.py $ARGS > $OUT/r$r.out 2> $OUT/r$r.err &
+    fi
     pids="$pids $!"
 done
 rc=0

@@ -286,7 +286,11 @@ int LoadFlagsFromFile(const std::string& path) {
         if (eq == std::string::npos) continue;
         size_t ne = eq;  // "name = value": the name without trailing blanks
         while (ne > b && (line[ne - 1] == ' ' || line[ne - 1] == '\t')) --ne;
-        if (SetFlag(line.substr(b, ne - b), line.substr(eq + 1))) ++n;
+        // ... and the value without blanks on either side ("x = true ")
+        size_t vb = eq + 1, ve = line.size();
+        while (vb < ve && (line[vb] == ' ' || line[vb] == '\t')) ++vb;
+        while (ve > vb && (line[ve - 1] == ' ' || line[ve - 1] == '\t')) --ve;
+        if (SetFlag(line.substr(b, ne - b), line.substr(vb, ve - vb))) ++n;
     }
     return n;
 }

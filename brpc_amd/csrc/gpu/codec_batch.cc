@@ -264,10 +264,12 @@ bool launch(CBatch* b, int device) {
                 const size_t cap = std::max<size_t>(nscan, 256);
                 b->group_done = static_cast<uint32_t*>(HbmAlloc(cap * sizeof(uint32_t), device));
                 b->group_done_cap = b->group_done ? cap : 0;
-                // ordered before the launch on the same stream
-                if (!b->group_done || hipMemsetAsync(b->group_done, 0, cap * sizeof(uint32_t), s) != hipSuccess) {
-                    rc = -1;
-                }
+            }
+            // zeroed before EVERY launch, ordered before it on the same
+            // stream: a launch that stopped partway (a fault) must not leave
+            // counters that start the next launch's scans early
+            if (!b->group_done || hipMemsetAsync(b->group_done, 0, nscan * sizeof(uint32_t), s) != hipSuccess) {
+                rc = -1;
             }
             for (size_t p = 0; p < nhpieces; ++p) b->piece_group.p[p] = kFusedNoGroup;
             for (size_t i = 0; i < b->reqs.size(); ++i) {

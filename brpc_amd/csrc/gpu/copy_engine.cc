@@ -27,6 +27,12 @@ DEFINE_int32(copy_engine_resident_max_us, 4000,
              "a resident instance exits after this long in any case (bounds how long work sharing its hardware "
              "queue can wait); the next batch relaunches it");
 
+DEFINE_bool(copy_engine_done_words, true,
+            "batches complete through a word the kernel's last workgroup stores into pinned memory (the poller "
+            "reads it) instead of a hipEvent query; the event stays as the fallback. Measured: with two processes "
+            "on a GPU, hipEventQuery reported copies done ~570 us after launch against ~12 us for the kernel "
+            "(profiles/r6_xproc_diagnosis.txt)");
+
 namespace mrpc {
 namespace gpu {
 
@@ -46,6 +52,11 @@ struct Batch {
     std::atomic<int>* butex = nullptr;
     hipEvent_t ev = nullptr;
     std::atomic<int> refs{0};
+    // completion word (FLAGS_copy_engine_done_words); fell_back: the event
+    // completed the batch, so the slot's counter is not known to be zero
+    bool has_word = false, fell_back = false;
+    uint32_t word_slot = 0;
+    const uint64_t* word = nullptr;  // the slot's pinned words (stamps at [1], [2])
     // latency breakdown (monotonic us): first submission, launch issued,
     // completion seen by the poller
     int64_t t_open = 0, t_issue_begin = 0, t_issued = 0, t_done = 0;
@@ -63,6 +74,13 @@ std::atomic<int64_t> g_submits{0}, g_launches{0}, g_segments{0}, g_bytes{0};
 // sums over submissions (us): waiting for the batch to be issued, the
 // launch API calls, launch-to-completion-seen, completion-to-resumed
 std::atomic<int64_t> g_t_queue{0}, g_t_api{0}, g_t_gpu{0}, g_t_wake{0};
+// completion-word launches: GPU wall-clock ticks from workgroup 0's start
+// to the last workgroup's end, and how many launches that covers
+std::atomic<int64_t> g_kernel_ticks{0}, g_kernel_timed{0};
+
+// One submitter per batch accounts the batch-wide stamps: the one whose
+// segments come first.
+inline bool leader_of_batch(const Batch*, size_t first) { return first == 0; }
 
 Batch* new_batch(Engine& e) {
     if (!e.spare.empty()) {
@@ -119,6 +137,11 @@ void launch(Batch* b, int device) {
     b->ev = AcquireEvent();
     int rc = (s && b->ev) ? 0 : -1;
     const size_t n = b->segs.size();
+    DoneWord dw;
+    b->fell_back = false;
+    b->has_word = rc == 0 && FLAGS_copy_engine_done_words && AcquireDoneWord(device, &dw, &b->word_slot);
+    const DoneWord* done = b->has_word ? &dw : nullptr;
+    b->word = b->has_word ? dw.word : nullptr;
     if (rc == 0 && b->want_crc) {
         // fused pull + checksum: the kernel stores the CRCs straight into
         // pinned host memory (one launch, no memset, no D2H copy)
@@ -128,11 +151,11 @@ void launch(Batch* b, int device) {
             b->crc_host = static_cast<uint32_t*>(PinnedAlloc(b->crc_cap * sizeof(uint32_t)));
         }
         if (!b->crc_host ||
-            LaunchBatchedCopyCrc32cMessages(b->segs.data(), b->msg_of.data(), (int)n, b->crc_host, s) != 0) {
+            LaunchBatchedCopyCrc32cMessages(b->segs.data(), b->msg_of.data(), (int)n, b->crc_host, s, done) != 0) {
             rc = -1;
         }
     } else if (rc == 0) {
-        rc = LaunchBatchedCopy(b->segs.data(), (int)n, s);
+        rc = LaunchBatchedCopy(b->segs.data(), (int)n, s, done);
     }
     if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
     b->t_issued = monotonic_us();
@@ -140,11 +163,16 @@ void launch(Batch* b, int device) {
     g_launches.fetch_add(1, std::memory_order_relaxed);
     if (rc != 0) {
         LOG_EVERY_SECOND(ERROR) << "batched copy launch of " << b->segs.size() << " segments failed on device " << device;
+        b->fell_back = true;  // part of it may have run: its word slot is not reused
         b->butex->store(-1, std::memory_order_release);
         fiber::butex_wake_all(b->butex);
         return;
     }
-    WatchEvent(b->ev, b->butex, &b->t_done, kEventCopy);
+    if (b->has_word) {
+        WatchWord(dw.word, dw.seq, b->ev, b->butex, &b->t_done, kEventCopy, &b->fell_back);
+    } else {
+        WatchEvent(b->ev, b->butex, &b->t_done, kEventCopy);
+    }
 }
 
 }  // namespace
@@ -219,6 +247,13 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs, bool fol
         g_t_gpu.fetch_add(std::max<int64_t>(0, mine->t_done - mine->t_issued), std::memory_order_relaxed);
         g_t_wake.fetch_add(std::max<int64_t>(0, now - mine->t_done), std::memory_order_relaxed);
     }
+    if (rc == 0 && leader_of_batch(mine, first) && mine->word && !mine->fell_back) {
+        const uint64_t t0 = mine->word[1], t1 = mine->word[2];
+        if (t1 >= t0 && t1 - t0 < 100000000ull) {
+            g_kernel_ticks.fetch_add((int64_t)(t1 - t0), std::memory_order_relaxed);
+            g_kernel_timed.fetch_add(1, std::memory_order_relaxed);
+        }
+    }
     if (rc == 0 && crcs) {
         if (fold) {
             crcs[0] = mine->crc_host[first_msg];
@@ -239,6 +274,10 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs, bool fol
                              (float)(monotonic_us() - t0) / 1000.0f);
     }
     if (mine->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        // a slot whose launch completed through the event (failed) keeps
+        // an unknown counter: it is never reused
+        if (mine->has_word && !mine->fell_back) ReleaseDoneWord(device, mine->word_slot);
+        mine->has_word = false;
         ReleaseEvent(mine->ev);
         mine->ev = nullptr;
         mine->t_done = 0;
@@ -262,6 +301,8 @@ CopyEngineStats GetCopyEngineStats() {
     s.api_us = g_t_api.load(std::memory_order_relaxed);
     s.gpu_us = g_t_gpu.load(std::memory_order_relaxed);
     s.wake_us = g_t_wake.load(std::memory_order_relaxed);
+    s.kernel_ticks = g_kernel_ticks.load(std::memory_order_relaxed);
+    s.kernel_timed = g_kernel_timed.load(std::memory_order_relaxed);
     return s;
 }
 

@@ -37,6 +37,9 @@ struct CopyEngineStats {
     // summed over submissions (us): until the batch's launch began, the
     // launch API calls, launch-to-completion-seen, completion-to-resumed
     int64_t queue_us = 0, api_us = 0, gpu_us = 0, wake_us = 0;
+    // launches with a completion word: summed kernel duration (GPU wall-clock
+    // ticks, workgroup 0 start -> last workgroup end) and how many
+    int64_t kernel_ticks = 0, kernel_timed = 0;
 };
 CopyEngineStats GetCopyEngineStats();
 

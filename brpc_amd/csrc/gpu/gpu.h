@@ -95,8 +95,20 @@ void WatchEvent(hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us = nullp
 // Same for batches [first, last] of a resident copy worker ring (the
 // poller reads their pinned done words instead of querying an event).
 struct ResidentRing;
+struct DoneWord;  // kernels.h
 void WatchResident(ResidentRing* ring, uint64_t first_seq, uint64_t last_seq, std::atomic<int>* butex,
                    int64_t* done_us = nullptr);
+// Same for a launch with a completion word (kernels.h DoneWord): done when
+// *word == seq (one read of pinned memory per poll). `ev`, recorded after the
+// launch, is the fallback: it is queried only once the word is overdue
+// (-gpu_done_word_fallback_ms), so a launch that never stores its word
+// (failed) still completes with the event's verdict; *fell_back is set then.
+void WatchWord(const uint64_t* word, uint64_t seq, hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us,
+               int cls, bool* fell_back);
+// Completion-word slots of a device: a device counter and a pinned host word
+// each. false: none free (the caller completes through its event alone).
+bool AcquireDoneWord(int device, DoneWord* out, uint32_t* slot);
+void ReleaseDoneWord(int device, uint32_t slot);
 // Pooled events (hipEventDisableTiming).
 hipEvent_t AcquireEvent();
 void ReleaseEvent(hipEvent_t e);

@@ -38,8 +38,22 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
 int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s);
 // One wave that sleeps `us` microseconds of GPU wall clock (capped at 10 s).
 int LaunchSleepKernel(uint64_t us, hipStream_t s);
+// Completion word of a launch: the kernel's last workgroup to finish
+// stores `seq` into *word (pinned host memory, system-scope release, after
+// every workgroup's stores were released at agent scope), so the host sees
+// the batch done by reading one word — no hipEvent in the completion path.
+// `counter` (device memory, zero between launches) counts finished
+// workgroups; the last one resets it. Launchers that split a batch into
+// several launches on one stream pass the word to the last launch only.
+// word[1] / word[2] receive the GPU wall clock (hipDeviceAttributeWallClockRate)
+// when workgroup 0 started and when the last workgroup finished.
+struct DoneWord {
+    uint32_t* counter = nullptr;
+    uint64_t* word = nullptr;
+    uint64_t seq = 0;
+};
 // Copy every segment src -> dst (one launch for many small copies).
-int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s);
+int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s, const DoneWord* done = nullptr);
 // Fused: copy every segment AND write its standard CRC32C to out[i]
 // (one read of the bytes; sources may be local/peer HBM or pinned host).
 // One launch per 32 segments and nothing else: no memset of `out`, which
@@ -50,7 +64,8 @@ int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStr
 // of the message's bytes (its segments concatenated), folded on the device.
 // A message may have at most kInlineSegments segments (else -2, nothing
 // launched for it).
-int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s);
+int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s,
+                                    const DoneWord* done = nullptr);
 
 // Packed-varint decode (protobuf wire type 0, packed repeated field):
 // `in` holds n bytes of concatenated varints; out receives the values

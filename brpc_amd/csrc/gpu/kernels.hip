@@ -84,7 +84,34 @@ struct SegBatch {
     uint32_t msg_chunks[kInlineSegments]; // by message slot: chunks of all its segments
     uint8_t msg[kInlineSegments];         // message slot of the segment
     uint8_t first_of_msg[kInlineSegments];
+    // completion word (DoneWord in kernels.h); null: the launch has none
+    uint32_t* done_ctr;
+    unsigned long long* done_word;
+    unsigned long long done_seq;
+    unsigned long long done_pad;  // keeps sizeof a multiple of 16 (LDS staging of the resident ring)
 };
+
+// End of a workgroup of a launch with a completion word: after every lane's
+// stores, release them at agent scope and count the workgroup; the last one
+// resets the counter for the next launch and publishes the sequence number
+// to the host (system scope). Uniform per launch: no divergence without a word.
+// Each workgroup's first lane does the agent-scope release (an L2
+// write-back of ITS XCD) after every wave's stores were acknowledged by L2
+// (s_waitcnt 0 before the barrier), so the word implies every XCD that ran
+// a workgroup wrote its part back.
+__device__ __forceinline__ void signal_done(const SegBatch& b) {
+    if (!b.done_word) return;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t before = __hip_atomic_fetch_add(b.done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (before + 1 == gridDim.x) {
+            __hip_atomic_store(b.done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            b.done_word[2] = wall_clock64();
+            __hip_atomic_store(b.done_word, b.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
 
 __device__ __forceinline__ int find_segment(const SegBatch& b, uint32_t chunk) {
     int lo = 0, hi = b.nseg - 1;
@@ -204,7 +231,12 @@ __global__ void __launch_bounds__(kThreads) crc32c_kernel(SegBatch b, const uint
     }
 }
 
+__device__ __forceinline__ void stamp_start(const SegBatch& b) {
+    if (b.done_word && blockIdx.x == 0 && threadIdx.x == 0) b.done_word[1] = wall_clock64();
+}
+
 __global__ void __launch_bounds__(kThreads) batched_copy_kernel(SegBatch b) {
+    stamp_start(b);
     const uint32_t chunk = blockIdx.x;
     const int seg = find_segment(b, chunk);
     const uint64_t len = b.len[seg];
@@ -238,6 +270,7 @@ __global__ void __launch_bounds__(kThreads) batched_copy_kernel(SegBatch b) {
     } else {
         for (uint64_t off = cbeg + threadIdx.x; off < cend; off += kThreads) dst[off] = src[off];
     }
+    signal_done(b);
 }
 
 // Fused pull + checksum: the batched copy and the LDS CRC32C in ONE pass
@@ -253,6 +286,7 @@ typedef uint32_t u32x4_unaligned __attribute__((ext_vector_type(4), aligned(1)))
 __global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const uint32_t* __restrict__ tables,
                                                                uint32_t* __restrict__ scratch,
                                                                uint32_t* __restrict__ out) {
+    stamp_start(b);
     __shared__ uint32_t t[8][256];
     __shared__ uint32_t wave_acc[kThreads / 64];
     {
@@ -308,6 +342,7 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_kernel(SegBatch b, const
         uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
         fold_chunk(b, seg, after, seg_chunks, acc, scratch, out);
     }
+    signal_done(b);
 }
 
 // ---------------------------------------------------------------- CRC32C on MFMA
@@ -910,6 +945,12 @@ uint32_t fill_batch(SegBatch* b, const Segment* segs, int n, const int* msg_of =
     return c;
 }
 
+void set_done(SegBatch* b, const DoneWord& d) {
+    b->done_ctr = d.counter;
+    b->done_word = reinterpret_cast<unsigned long long*>(d.word);
+    b->done_seq = d.seq;
+}
+
 // Split [0, nseg) into launch groups of <= kInlineSegments segments that
 // never split a message. Returns false when one message alone is larger.
 bool next_group(const int* msg_of, int nseg, int begin, int* end) {
@@ -986,7 +1027,8 @@ int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStr
     return 0;
 }
 
-int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s) {
+int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s,
+                                    const DoneWord* done) {
     if (nseg <= 0) return 0;
     if (ensure_tables() != 0) return -1;
     int dev = 0;
@@ -997,6 +1039,7 @@ int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int 
         if (!next_group(msg_of, nseg, i, &e)) return -2;
         SegBatch b;
         const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of + i);
+        if (done && e == nseg) set_done(&b, *done);
         hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch,
                            out + msg_of[i]);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -1022,11 +1065,12 @@ int LaunchSleepKernel(uint64_t us, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s) {
+int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s, const DoneWord* done) {
     for (int i = 0; i < nseg; i += kInlineSegments) {
         const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;
         SegBatch b;
         const uint32_t chunks = fill_batch(&b, segs + i, n);
+        if (done && i + n == nseg) set_done(&b, *done);
         hipLaunchKernelGGL(batched_copy_kernel, dim3(chunks), dim3(kThreads), 0, s, b);
         if (hipGetLastError() != hipSuccess) return -1;
     }

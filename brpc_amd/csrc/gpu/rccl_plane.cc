@@ -668,14 +668,15 @@ public:
             const int grc = run_group();
             // the stream is in order: self groups issued before this group
             // are done once it is
-            if (grc == 0 && reap_self(/*block=*/true) != 0) break;
+            const int src = grc == 0 ? reap_self(/*block=*/true) : 0;
+            // every exit path clears busy and rings the peers:
+            // a peer may have deferred offers to us whatever our own flag
+            // says, and a stale busy word would keep deferring them
             bell->busy[rank].store(0, std::memory_order_release);
-            if (FLAGS_rccl_defer_busy_peers) {
-                for (int p = 0; p < world; ++p) {
-                    if (p != rank) ring(p);  // peers that deferred offers to us
-                }
+            for (int p = 0; p < world; ++p) {
+                if (p != rank) ring(p);  // peers that deferred offers to us
             }
-            if (grc != 0) break;
+            if (grc != 0 || src != 0) break;
             if (!stop && FLAGS_rccl_test_poster_delay_us > 0) usleep((useconds_t)FLAGS_rccl_test_poster_delay_us);
         }
         if (!dead) abort("rank shut down", true, /*is_error=*/false);

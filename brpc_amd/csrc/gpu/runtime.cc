@@ -5,6 +5,7 @@
 #include <sys/prctl.h>
 #include <time.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cctype>
 #include <condition_variable>
@@ -36,6 +37,10 @@ DEFINE_int32(gpu_poller_codec_wait_pct, 0,
 DEFINE_int32(gpu_poller_codec_idle_spin_us, 100,
              "after a codec batch completed, an idle event poller watches for the next one this long before "
              "sleeping on its condvar (codec streams hand over a batch every few tens of microseconds)");
+DEFINE_int32(gpu_done_word_fallback_ms, 50,
+             "a launch whose completion word is this overdue is completed by its event instead (a failed launch "
+             "never stores the word)");
+DEFINE_int32(gpu_done_word_slots, 4096, "completion-word slots per device (launches in flight with a word)");
 DEFINE_int32(gpu_poller_idle_spin_us, 0,
              "with nothing in flight the event poller watches for new events this long before sleeping "
              "(saves a condvar wake-up per batch on busy RPC streams; costs that much CPU per idle period)");
@@ -90,6 +95,9 @@ struct Waiter {
     // resident-worker batches [first, last] instead of an event
     ResidentRing* ring = nullptr;
     uint64_t first = 0, last = 0;
+    // completion-word launches: done when *word == first
+    const uint64_t* word = nullptr;
+    bool* fell_back = nullptr;
     int64_t since_us = 0;
     int64_t added_us = 0;  // when the poller was handed the event
     int cls = kEventOther;  // EventClass: whose completion-time average applies
@@ -166,7 +174,23 @@ private:
             int64_t now_pass = 0;
             for (size_t i = 0; i < active.size(); ++i) {
                 hipError_t r;
-                if (active[i].ring) {
+                if (active[i].word) {
+                    if (__atomic_load_n(active[i].word, __ATOMIC_ACQUIRE) == active[i].first) {
+                        r = hipSuccess;
+                    } else {
+                        if (!now_pass) now_pass = monotonic_us();
+                        r = hipErrorNotReady;
+                        if (now_pass - active[i].added_us > (int64_t)FLAGS_gpu_done_word_fallback_ms * 1000) {
+                            // overdue: the event decides (a failed launch)
+                            r = hipEventQuery(active[i].ev);
+                            if (r != hipErrorNotReady && active[i].fell_back) *active[i].fell_back = true;
+                        }
+                    }
+                    if (r == hipErrorNotReady) {
+                        active[keep++] = active[i];
+                        continue;
+                    }
+                } else if (active[i].ring) {
                     // plain reads of the ring's pinned done words
                     if (!ResidentDone(active[i].ring, active[i].first, active[i].last)) {
                         if (!now_pass) now_pass = monotonic_us();
@@ -394,6 +418,71 @@ void WatchResident(ResidentRing* ring, uint64_t first_seq, uint64_t last_seq, st
     w.since_us = monotonic_us();
     w.cls = kEventCopy;
     poller()->add(w);
+}
+
+void WatchWord(const uint64_t* word, uint64_t seq, hipEvent_t ev, std::atomic<int>* butex, int64_t* done_us,
+               int cls, bool* fell_back) {
+    Waiter w{ev, butex, done_us};
+    w.word = word;
+    w.first = seq;
+    w.fell_back = fell_back;
+    w.cls = cls >= 0 && cls < kEventClasses ? cls : kEventOther;
+    poller()->add(w);
+}
+
+namespace {
+// Completion-word slots per device: counters in HBM (zero between
+// launches: every launch's last workgroup resets its own), words in pinned
+// coherent host memory. Sequence numbers only grow, so a word never
+// matches a later launch's seq by accident.
+struct DoneSlots {
+    std::mutex mu;
+    bool init = false, ok = false;
+    uint32_t* counters = nullptr;
+    uint64_t* words = nullptr;
+    std::vector<uint32_t> free;
+    uint64_t next_seq = 0;
+};
+DoneSlots g_done[kMaxDevices];
+}  // namespace
+
+bool AcquireDoneWord(int device, DoneWord* out, uint32_t* slot) {
+    if (device < 0 || device >= kMaxDevices) return false;
+    DoneSlots& d = g_done[device];
+    std::lock_guard<std::mutex> g(d.mu);
+    if (!d.init) {
+        d.init = true;
+        const uint32_t n = (uint32_t)std::max(64, FLAGS_gpu_done_word_slots);
+        int prev = 0;
+        hipGetDevice(&prev);
+        if (prev != device) hipSetDevice(device);
+        void* c = nullptr;
+        if (hipMalloc(&c, n * sizeof(uint32_t)) == hipSuccess && hipMemset(c, 0, n * sizeof(uint32_t)) == hipSuccess &&
+            hipDeviceSynchronize() == hipSuccess) {
+            d.counters = static_cast<uint32_t*>(c);
+            d.words = static_cast<uint64_t*>(HostMallocPinned(n * 4 * sizeof(uint64_t)));
+        }
+        if (prev != device) hipSetDevice(prev);
+        if (d.counters && d.words) {
+            memset(d.words, 0, n * 4 * sizeof(uint64_t));
+            for (uint32_t i = n; i > 0; --i) d.free.push_back(i - 1);
+            d.ok = true;
+        }
+    }
+    if (!d.ok || d.free.empty()) return false;
+    const uint32_t s = d.free.back();
+    d.free.pop_back();
+    *slot = s;
+    out->counter = d.counters + s;
+    out->word = d.words + 4 * (size_t)s;  // [word, kernel start, kernel end, -] (GPU wall clock)
+    out->seq = ++d.next_seq;
+    return true;
+}
+
+void ReleaseDoneWord(int device, uint32_t slot) {
+    DoneSlots& d = g_done[device];
+    std::lock_guard<std::mutex> g(d.mu);
+    d.free.push_back(slot);
 }
 
 hipEvent_t AcquireEvent() { return get_event(); }

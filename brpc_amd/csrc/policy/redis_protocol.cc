@@ -294,8 +294,12 @@ ParseResult ParseRedisMessage(Buf* source, Socket* socket, bool read_eof, const 
         have = true;
     }
     if (have && !broken && run_command(const_cast<Server*>(server), ctx, cur, true, &out) != 0) broken = true;
+    // a handler that broke the protocol drops the connection without the
+    // replies gathered so far (reference redis_protocol.cpp:177-185); a
+    // malformed command still gets the replies of the commands before it
+    if (broken) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
     if (!out.empty()) socket->Write(&out);
-    if (rc < 0 || broken) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
+    if (rc < 0) return MakeParseError(PARSE_ERROR_ABSOLUTELY_WRONG);
     // every complete command ran inside parse; what is left is the start
     // of the next one: read more (reference: redis_protocol.cpp:167-194)
     return MakeParseError(PARSE_ERROR_NOT_ENOUGH_DATA);

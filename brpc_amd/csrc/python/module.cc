@@ -592,6 +592,8 @@ PYBIND11_MODULE(_native, m) {
         d["copy_api_us"] = c.api_us;
         d["copy_gpu_us"] = c.gpu_us;
         d["copy_wake_us"] = c.wake_us;
+        d["copy_kernel_ticks"] = c.kernel_ticks;
+        d["copy_kernel_timed"] = c.kernel_timed;
         return d;
     });
     g.def("reap_lent", [] { gpu::ReapLentBlocks(); });

@@ -373,15 +373,19 @@ TEST(BaseDepth, flags_from_a_file) {
     char path[] = "/tmp/bd_flagsXXXXXX";
     const int fd = mkstemp(path);
     ASSERT_TRUE(fd >= 0);
-    const std::string body = "# comment\nbd_i32=11\n\nbd_str = spaced \nbd_double=0.5\n";
+    SetFlag("bd_bool", "false");
+    const std::string body =
+        "# comment\nbd_i32 = 11 \n\nbd_str = spaced \nbd_double=0.5\n\tbd_bool\t=\ttrue\t\nbd_i64 =  -8\n";
     ASSERT_EQ((size_t)write(fd, body.data(), body.size()), body.size());
     close(fd);
     const int n = LoadFlagsFromFile(path);
     unlink(path);
-    EXPECT_GE(n, 3);
+    EXPECT_EQ(n, 5);  // every line applied, blanks around '=' and at the end included
     EXPECT_EQ(FLAGS_bd_i32, 11);
     EXPECT_EQ(FLAGS_bd_double, 0.5);
-    EXPECT_TRUE(FLAGS_bd_str == "spaced" || FLAGS_bd_str == " spaced ");
+    EXPECT_EQ(FLAGS_bd_str, "spaced");
+    EXPECT_TRUE(FLAGS_bd_bool);
+    EXPECT_EQ(FLAGS_bd_i64, -8);
     SetFlag("bd_i32", "5");
 }
 
