@@ -115,6 +115,8 @@ def parse(argv=None):
                     help="watchdog: print what was measured and end every rank at this many wall seconds")
     ap.add_argument("--only", default="", help="comma-separated leg names: run only these (experiments)")
     ap.add_argument("--stall-leg", default="", help=argparse.SUPPRESS)  # test hook: NAME[:hang]
+    ap.add_argument("--ring-hop", type=int, default=1,
+                    help="rank r's client talks to the server of rank r+HOP (0: its own server; experiments)")
     ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # test hook: that rank exits 3
     ap.add_argument("--spawn-grace-s", type=float, default=30.0,
                     help="self-launched ranks: once one rank failed, the others get this long before they are killed")
@@ -420,7 +422,7 @@ def main(argv=None):
         rccl_up = parallel.allreduce_sum(1 if rccl_up else 0, topo) == topo.world_size
     dev_payload = cuda and not a.host_payload  # attachments in HBM (else host memory)
     devices = parallel.gather_objects(topo.device, topo)
-    ring_cross_gpu = n > 1 and devices[topo.rank] != devices[parallel.ring_peer(topo)]
+    ring_cross_gpu = n > 1 and devices[topo.rank] != devices[parallel.ring_peer(topo, a.ring_hop)]
     ring_cross_gpu = parallel.allreduce_max(1 if ring_cross_gpu else 0, topo) > 0
     any_cross_gpu = n > 1 and len(set(devices)) > 1
     extra["devices"] = devices
@@ -461,7 +463,8 @@ def main(argv=None):
     def diag_snapshot():
         x = native.gpu.xgmi_stats()
         d = {k: x[k] for k in ("copy_submits", "copy_launches", "copy_segments", "copy_queue_us", "copy_api_us",
-                               "copy_gpu_us", "copy_wake_us", "copy_kernel_ticks", "copy_kernel_timed")}
+                               "copy_gpu_us", "copy_wake_us", "copy_kernel_ticks", "copy_kernel_timed",
+                               "copy_start_delay_us", "copy_notice_us")}
         d["polled_events"] = native.gpu.polled_events() if cuda else 0
         cg = cgroup_cpu_stat()
         d["cg_nr_throttled"] = cg.get("nr_throttled", 0)
@@ -483,6 +486,8 @@ def main(argv=None):
             # against copy_gpu_us (launch -> completion seen) it splits the
             # device time into queueing and running
             out["copy_kernel_us_per_launch"] = round(d["copy_kernel_ticks"] / d["copy_kernel_timed"] / 100.0, 1)
+            out["copy_start_delay_us_per_launch"] = round(d["copy_start_delay_us"] / d["copy_kernel_timed"], 1)
+            out["copy_notice_us_per_launch"] = round(d["copy_notice_us"] / d["copy_kernel_timed"], 1)
         if d["polled_events"]:
             out["polled_events"] = int(d["polled_events"])
         # the box's quota is shared by every rank: take one rank's view
@@ -524,7 +529,7 @@ def main(argv=None):
 
     server = start_echo_server("127.0.0.1:0", num_threads=workers, gpu_device=topo.device)
     addrs = parallel.exchange_addresses(server.address, topo)
-    peer = addrs[parallel.ring_peer(topo)]
+    peer = addrs[parallel.ring_peer(topo, a.ring_hop)]
 
     def stall_hook(name, deadline):
         # test hook (--stall-leg NAME[:hang]): the leg overruns its deadline,
@@ -759,6 +764,20 @@ def main(argv=None):
     if rccl_up and not a.skip_64k:
         wlr = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=dev_payload, requests_per_step=half64))
         run_leg("rccl_64KB", plane_leg, wlr, a.steps, a.warmup)
+        if n == 1 and cuda:
+            # At N = 1 the plane's payloads go from the rank to itself, which
+            # it moves with one batched copy per group (-rccl_self_copy): the
+            # rccl_* legs are reported as rccl_self_copy_*. This leg keeps the
+            # real ncclSend/ncclRecv-to-self per-op cost measured every round.
+            def nccl_self_leg(name, deadline, wl, steps, warmup):
+                native.set_flag("rccl_self_copy", "false")
+                try:
+                    return plane_leg(name, deadline, wl, steps, warmup)
+                finally:
+                    native.set_flag("rccl_self_copy", "true")
+            wln = EchoWorkload(**dict(ECHO_64KB.asdict(), device_attachment=dev_payload,
+                                      requests_per_step=max(1, half64 // 4)))
+            run_leg("rccl_nccl_self_64KB", nccl_self_leg, wln, a.steps, a.warmup)
 
     # 1 MiB legs (BASELINE config 5 analog: rdma_performance with 1 MB
     # payloads): HBM attachments lent over xGMI, and over the RCCL plane.
@@ -868,14 +887,20 @@ def main(argv=None):
     # RpcMeta and the block table only. Incompressible bodies (random) are
     # lent raw after the encode and still indexed on arrival. Every 64th
     # reply is checked: bytes and the device field table.
+    # The gRPC twin (BASELINE config 4 on HBM bodies): the same device body
+    # over h2:grpc, the descriptors in the mrpc-meta-bin header of each
+    # message (policy/h2_protocol.cc), negotiated by a private SETTINGS
+    # parameter between brpc_amd peers.
+    device_legs = [(pfx + "device_snappy_64KB_" + body, body, proto)
+                   for pfx, proto in (("", "baidu_std"), ("grpc_", "h2:grpc")) for body in bodies]
     if dev_payload and not a.skip_64k and not a.skip_grpc:
-        for body in bodies:
-            name = "device_snappy_64KB_" + body
+        for name, body, proto in device_legs:
             wld = EchoWorkload(name, request_size=16, attachment_size=65536,
                                device_attachment=True, requests_per_step=max(1, a.requests_per_step_grpc * 4))
             od = wld.press_options(peer, gpu_device=topo.device)
             od.update({"concurrency": a.concurrency, "attachment_body": body, "attachment_pb": True,
-                       "device_scan": True, "device_compress": 1, "check_echo": True, "check_every": 64})
+                       "device_scan": True, "device_compress": 1, "check_echo": True, "check_every": 64,
+                       "protocol": proto})
             c0, x0, b0 = native.gpu.device_codec_stats(), native.gpu.xgmi_stats(), native.gpu.codec_batch_stats()
             r = run_leg(name, timed_leg, wld, a.steps, a.warmup, od, min_s=a.codec_min_s,
                         transport_kind=lend, cross_gpu=ring_cross_gpu)
@@ -1252,8 +1277,7 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
             "The *_snappy_64KB_*_gpu legs force it onto plain bodies to show the trade: the CPU codec is faster there")
         out["http_json_64KB_text_note"] = ("CPU only: the JSON offload's density gate leaves a long string field "
                                            "to the host, so no GPU run of this body is reported")
-    for body in ("text", "random", "const"):
-        k = "device_snappy_64KB_" + body
+    for k in ["%sdevice_snappy_64KB_%s" % (p, b) for p in ("", "grpc_") for b in ("text", "random", "const")]:
         r = legs.get(k)
         if not r:
             continue
@@ -1266,11 +1290,16 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
             out[k + "_encoded_fraction"] = r["device"]["encoded_fraction"]
             out[k + "_decoded_fraction"] = r["device"]["decoded_fraction"]
     rc = legs.get("rccl_64KB")
+    # one rank: the plane moves payloads to itself with a copy kernel, so
+    # those legs are labelled rccl_self_copy_* (RCCL runs only in the
+    # rccl_nccl_self_* leg); between ranks they are ncclSend/ncclRecv
+    self_plane = bool(rc) and rc["transport"]["rccl_world"] == 1
+    rp = "rccl_self_copy_" if self_plane else "rccl_"
     if rc:
-        out["rccl_64KB_qps"] = round(rc["qps"], 1)
-        out["rccl_64KB_p99_us"] = rc["p99_us"]
-        out["rccl_64KB_gbytes_per_s"] = round(rc["qps"] * 65536 * 2 / 1e9, 3)
-        out["rccl_64KB_errors"] = rc["errors"]
+        out[rp + "64KB_qps"] = round(rc["qps"], 1)
+        out[rp + "64KB_p99_us"] = rc["p99_us"]
+        out[rp + "64KB_gbytes_per_s"] = round(rc["qps"] * 65536 * 2 / 1e9, 3)
+        out[rp + "64KB_errors"] = rc["errors"]
         tr = rc["transport"]
         out["rccl_payloads"] = tr.get("rccl_payloads", 0)
         out["rccl_payloads_per_round"] = round(tr.get("rccl_payloads", 0) / max(1, tr.get("rccl_rounds", 0)), 2)
@@ -1278,10 +1307,19 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
         out["rccl_group_us_per_round"] = round(tr.get("rccl_group_us", 0) / max(1, tr.get("rccl_rounds", 0)), 2)
         out["rccl_aborts"] = extra.get("plane_aborts", tr.get("rccl_aborts", 0))
         out["rccl_world"] = tr["rccl_world"]
-        if tr["rccl_world"] == 1:
-            out["rccl_note"] = ("one-rank plane: every payload goes from the rank to itself, which the plane moves "
-                                "with one batched copy kernel per group on its stream (-rccl_self_copy); between "
-                                "ranks its groups are ncclSend/ncclRecv")
+        if self_plane:
+            out["rccl_note"] = ("one-rank plane: every payload goes from the rank to itself; the rccl_self_copy_* "
+                                "legs move them with one batched copy kernel per group on the plane's stream "
+                                "(-rccl_self_copy), NOT with RCCL. rccl_nccl_self_64KB_* is the same leg through "
+                                "ncclSend/ncclRecv to self. Between ranks every plane group is ncclSend/ncclRecv")
+    rn = legs.get("rccl_nccl_self_64KB")
+    if rn:
+        out["rccl_nccl_self_64KB_qps"] = round(rn["qps"], 1)
+        out["rccl_nccl_self_64KB_p99_us"] = rn["p99_us"]
+        out["rccl_nccl_self_64KB_errors"] = rn["errors"]
+        trn = rn["transport"]
+        out["rccl_nccl_self_group_us_per_round"] = round(
+            trn.get("rccl_group_us", 0) / max(1, trn.get("rccl_rounds", 0)), 2)
     r1m = legs.get("echo_1MB")
     if r1m:
         out["qps_1MB"] = round(r1m["qps"], 1)
@@ -1291,16 +1329,22 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
         out["timed_s_1MB"] = round(r1m["elapsed_s"], 3)
     r1mr = legs.get("rccl_1MB")
     if r1mr:
-        out["rccl_1MB_qps"] = round(r1mr["qps"], 1)
-        out["rccl_1MB_gbytes_per_s"] = round(r1mr["qps"] * (1 << 20) * 2 / 1e9, 3)
-        out["rccl_1MB_p99_us"] = r1mr["p99_us"]
-        out["rccl_1MB_errors"] = r1mr["errors"]
+        out[rp + "1MB_qps"] = round(r1mr["qps"], 1)
+        out[rp + "1MB_gbytes_per_s"] = round(r1mr["qps"] * (1 << 20) * 2 / 1e9, 3)
+        out[rp + "1MB_p99_us"] = r1mr["p99_us"]
+        out[rp + "1MB_errors"] = r1mr["errors"]
     sweep = legs.get("sweep")
     if sweep:
         out["sweep"] = sweep["points"]
         if "rccl_crossover_bytes" in sweep:
-            out["rccl_crossover_bytes"] = sweep["rccl_crossover_bytes"]
-            out["rccl_crossover_points"] = sweep["rccl_crossover_points"]
+            if self_plane or n == 1:
+                # both sides of the comparison are device-local copies at N = 1
+                out["rccl_crossover_bytes"] = None
+                out["rccl_crossover_note"] = ("N = 1: the sweep's rccl points are the plane's self-copy kernel, "
+                                              "not RCCL; no crossover is claimed")
+            else:
+                out["rccl_crossover_bytes"] = sweep["rccl_crossover_bytes"]
+                out["rccl_crossover_points"] = sweep["rccl_crossover_points"]
     timed = {k: v for k, v in legs.items() if k != "sweep" and isinstance(v, dict) and "transport" in v}
     # which transport carried each leg's payloads (summed over ranks)
     out["transport"] = {k: v["transport"] for k, v in timed.items() if k[:4] != "grpc"}

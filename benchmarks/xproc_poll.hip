@@ -5,8 +5,10 @@
 // host memory (system scope), so for every op we know when the kernel was
 // really done (the word) and when hipEventQuery first said so.
 //
-//   build/bin/xproc_poll NPROC [threads] [streams] [iters] [bytes] [ipc] [arena_mb] [bigargs]
+//   build/bin/xproc_poll NPROC [threads] [streams] [iters] [bytes] [ipc] [arena_mb] [bigargs] [mrpc]
 //
+// mrpc=1: the copies are the framework's own launches (gpu::LaunchBatchedCopy
+// with a DoneWord, libmrpc.so) instead of this file's kernel.
 // arena_mb > 0: sources are carved from ONE hipMalloc of that size per
 // process (the framework's IPC arena), and ipc imports the peer's whole
 // arena. bigargs=1: the kernel also takes a 1.6 KB by-value argument (the
@@ -30,6 +32,8 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include "gpu/kernels.h"
 
 #define CHECK(x)                                                                               \
     do {                                                                                       \
@@ -98,13 +102,13 @@ struct Mailbox {
 static Mailbox* g_box = nullptr;
 
 static void run(int threads, int nstreams, int iters, size_t bytes, int rank, int nproc, bool ipc, size_t arena_mb,
-                bool bigargs) {
+                bool bigargs, bool mrpc) {
     std::vector<hipStream_t> streams(nstreams);
     for (auto& s : streams) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     const int nslots = threads;
     unsigned long long* words = nullptr;
-    CHECK(hipHostMalloc((void**)&words, sizeof(unsigned long long) * nslots, hipHostMallocCoherent | hipHostMallocMapped));
-    memset(words, 0, sizeof(unsigned long long) * nslots);
+    CHECK(hipHostMalloc((void**)&words, sizeof(unsigned long long) * 4 * nslots, hipHostMallocCoherent | hipHostMallocMapped));
+    memset(words, 0, sizeof(unsigned long long) * 4 * nslots);  // [word, stamps...] per slot
     unsigned* counters = nullptr;
     CHECK(hipMalloc((void**)&counters, sizeof(unsigned) * nslots));
     CHECK(hipMemset(counters, 0, sizeof(unsigned) * nslots));
@@ -148,7 +152,7 @@ static void run(int threads, int nstreams, int iters, size_t bytes, int rank, in
             }
             size_t keep = 0;
             for (Op* o : act) {
-                if (!o->t_word && __atomic_load_n(&words[o->slot], __ATOMIC_ACQUIRE) == o->seq) o->t_word = now_us();
+                if (!o->t_word && __atomic_load_n(&words[4 * o->slot], __ATOMIC_ACQUIRE) == o->seq) o->t_word = now_us();
                 const hipError_t r = hipEventQuery(o->ev);
                 if (r == hipErrorNotReady) {
                     act[keep++] = o;
@@ -179,14 +183,21 @@ static void run(int threads, int nstreams, int iters, size_t bytes, int rank, in
                 o.done.store(0);
                 hipStream_t s = streams[(t + i) % nstreams];
                 o.t_launch = now_us();
-                if (bigargs) {
+                if (mrpc) {
+                    mrpc::gpu::Segment seg{src[t], dst[t], bytes};
+                    mrpc::gpu::DoneWord dw;
+                    dw.counter = counters + t;
+                    dw.word = reinterpret_cast<uint64_t*>(words + 4 * t);
+                    dw.seq = o.seq;
+                    if (mrpc::gpu::LaunchBatchedCopy(&seg, 1, s, &dw) != 0) _exit(5);
+                } else if (bigargs) {
                     BigArgs big;
                     memset(&big, 0, sizeof(big));
                     hipLaunchKernelGGL(copy_done_big, dim3(blocks), dim3(256), 0, s, (const uint4*)src[t], (uint4*)dst[t],
-                                       n16, counters + t, words + t, o.seq, big);
+                                       n16, counters + t, words + 4 * t, o.seq, big);
                 } else {
                     hipLaunchKernelGGL(copy_done, dim3(blocks), dim3(256), 0, s, (const uint4*)src[t], (uint4*)dst[t],
-                                       n16, counters + t, words + t, o.seq);
+                                       n16, counters + t, words + 4 * t, o.seq);
                 }
                 CHECK(hipEventRecord(o.ev, s));
                 {
@@ -226,6 +237,7 @@ int main(int argc, char** argv) {
     const bool ipc = argc > 6 && atoi(argv[6]) != 0;
     const size_t arena_mb = argc > 7 ? (size_t)atoll(argv[7]) : 0;
     const bool bigargs = argc > 8 && atoi(argv[8]) != 0;
+    const bool mrpc = argc > 9 && atoi(argv[9]) != 0;
     if (nproc > 16 || threads > 16) return 1;
     g_box = static_cast<Mailbox*>(mmap(nullptr, sizeof(Mailbox), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0));
     if (g_box == MAP_FAILED) return 1;
@@ -233,12 +245,12 @@ int main(int argc, char** argv) {
     for (int r = 1; r < nproc; ++r) {
         const pid_t p = fork();
         if (p == 0) {
-            run(threads, nstreams, iters, bytes, r, nproc, ipc, arena_mb, bigargs);
+            run(threads, nstreams, iters, bytes, r, nproc, ipc, arena_mb, bigargs, mrpc);
             _exit(0);
         }
         kids.push_back(p);
     }
-    run(threads, nstreams, iters, bytes, 0, nproc, ipc, arena_mb, bigargs);
+    run(threads, nstreams, iters, bytes, 0, nproc, ipc, arena_mb, bigargs, mrpc);
     int bad = 0;
     for (pid_t p : kids) {
         int st = 0;

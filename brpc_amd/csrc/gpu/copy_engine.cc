@@ -27,11 +27,22 @@ DEFINE_int32(copy_engine_resident_max_us, 4000,
              "a resident instance exits after this long in any case (bounds how long work sharing its hardware "
              "queue can wait); the next batch relaunches it");
 
-DEFINE_bool(copy_engine_done_words, true,
+DEFINE_bool(copy_engine_done_words, false,
             "batches complete through a word the kernel's last workgroup stores into pinned memory (the poller "
-            "reads it) instead of a hipEvent query; the event stays as the fallback. Measured: with two processes "
-            "on a GPU, hipEventQuery reported copies done ~570 us after launch against ~12 us for the kernel "
-            "(profiles/r6_xproc_diagnosis.txt)");
+            "reads it, the event stays as the fallback), with the kernel's start/end GPU clock: the diagnostic "
+            "split of launch -> kernel start -> end -> seen (bench.py diag). Off by default: every workgroup's "
+            "agent-scope release (an L2 write-back) halved 1 MiB pull bandwidth, and with the in-flight limit "
+            "event completion is as fast (profiles/r6_xproc_diagnosis.txt)");
+
+DEFINE_int32(copy_engine_max_inflight, 4,
+             "launches of one device's copy engine in flight at once (0: no limit). Submissions that find the "
+             "limit reached join the open batch, which the first waiter of the next completed batch launches: "
+             "with 50 RPCs in flight and a few workers per process, unlimited launches of ~1 segment each queued "
+             "up in the HIP streams (~600 us from launch to kernel start at 2 ranks per GPU, "
+             "profiles/r6_xproc_diagnosis.txt)");
+DEFINE_bool(copy_engine_word_event, true,
+            "launches with a completion word still record an event (the fallback verdict of a launch that "
+            "never stores its word)");
 
 namespace mrpc {
 namespace gpu {
@@ -54,6 +65,7 @@ struct Batch {
     std::atomic<int> refs{0};
     // completion word (FLAGS_copy_engine_done_words); fell_back: the event
     // completed the batch, so the slot's counter is not known to be zero
+    std::atomic<bool> retired{false};  // its in-flight slot was given back (first waiter to wake)
     bool has_word = false, fell_back = false;
     uint32_t word_slot = 0;
     const uint64_t* word = nullptr;  // the slot's pinned words (stamps at [1], [2])
@@ -66,6 +78,7 @@ struct Engine {
     std::mutex mu;
     Batch* open = nullptr;     // batch accepting submissions
     bool launching = false;    // a leader is draining `open`
+    int inflight = 0;          // launched, not yet retired (FLAGS_copy_engine_max_inflight)
     std::vector<Batch*> spare; // recycled batches
 };
 
@@ -77,6 +90,43 @@ std::atomic<int64_t> g_t_queue{0}, g_t_api{0}, g_t_gpu{0}, g_t_wake{0};
 // completion-word launches: GPU wall-clock ticks from workgroup 0's start
 // to the last workgroup's end, and how many launches that covers
 std::atomic<int64_t> g_kernel_ticks{0}, g_kernel_timed{0};
+// ... and, with the GPU clock correlated to the host's (calibrate_clock),
+// launch API return -> kernel start and kernel end -> the poller saw it
+std::atomic<int64_t> g_start_delay_us{0}, g_notice_us{0};
+std::atomic<int64_t> g_clock_offset_us{INT64_MIN};  // host monotonic us - GPU ticks / 100
+
+// Correlate the GPU wall clock with the host's monotonic clock: a one-lane
+// kernel stores its clock into pinned memory while the host spins on it;
+// of 20 probes the one seen soonest after its launch bounds the offset
+// within a few microseconds.
+void calibrate_clock(int device) {
+    static std::once_flag once;
+    std::call_once(once, [device] {
+        uint64_t* w = static_cast<uint64_t*>(HostMallocPinned(64));
+        hipStream_t s = PoolStream(device);
+        if (!w || !s) return;
+        int64_t best_win = INT64_MAX, best_off = INT64_MIN;
+        for (int i = 0; i < 20; ++i) {
+            __atomic_store_n(w, 0ull, __ATOMIC_RELEASE);
+            const int64_t t0 = monotonic_us();
+            if (LaunchClockProbe(w, s) != 0) break;
+            uint64_t v = 0;
+            int64_t t1 = t0;
+            while ((v = __atomic_load_n(w, __ATOMIC_ACQUIRE)) == 0) {
+                t1 = monotonic_us();
+                if (t1 - t0 > 100000) break;
+            }
+            t1 = monotonic_us();
+            if (v && t1 - t0 < best_win) {
+                best_win = t1 - t0;
+                best_off = t1 - (int64_t)(v / 100);
+            }
+        }
+        hipStreamSynchronize(s);
+        g_clock_offset_us.store(best_off, std::memory_order_relaxed);
+        HostFreePinned(w);
+    });
+}
 
 // One submitter per batch accounts the batch-wide stamps: the one whose
 // segments come first.
@@ -139,6 +189,7 @@ void launch(Batch* b, int device) {
     const size_t n = b->segs.size();
     DoneWord dw;
     b->fell_back = false;
+    if (FLAGS_copy_engine_done_words) calibrate_clock(device);
     b->has_word = rc == 0 && FLAGS_copy_engine_done_words && AcquireDoneWord(device, &dw, &b->word_slot);
     const DoneWord* done = b->has_word ? &dw : nullptr;
     b->word = b->has_word ? dw.word : nullptr;
@@ -157,7 +208,10 @@ void launch(Batch* b, int device) {
     } else if (rc == 0) {
         rc = LaunchBatchedCopy(b->segs.data(), (int)n, s, done);
     }
-    if (rc == 0 && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
+    // with a completion word the event is only the fallback of a launch
+    // that never stores its word; -copy_engine_word_event=false drops it
+    const bool record = !b->has_word || FLAGS_copy_engine_word_event;
+    if (rc == 0 && record && hipEventRecord(b->ev, s) != hipSuccess) rc = -1;
     b->t_issued = monotonic_us();
     if (prev != device) hipSetDevice(prev);
     g_launches.fetch_add(1, std::memory_order_relaxed);
@@ -169,9 +223,38 @@ void launch(Batch* b, int device) {
         return;
     }
     if (b->has_word) {
-        WatchWord(dw.word, dw.seq, b->ev, b->butex, &b->t_done, kEventCopy, &b->fell_back);
+        WatchWord(dw.word, dw.seq, record ? b->ev : nullptr, b->butex, &b->t_done, kEventCopy, &b->fell_back);
     } else {
         WatchEvent(b->ev, b->butex, &b->t_done, kEventCopy);
+    }
+}
+
+bool at_limit(const Engine& e) {
+    return FLAGS_copy_engine_max_inflight > 0 && e.inflight >= FLAGS_copy_engine_max_inflight;
+}
+
+// Launch the open batch, and whatever collects while launching, until
+// nothing is open or the in-flight limit is reached (the next retiring
+// waiter picks up from there). The caller set e.launching.
+void drain(Engine& e, int device) {
+    for (;;) {
+        Batch* cur;
+        {
+            std::lock_guard<std::mutex> g(e.mu);
+            cur = e.open;
+            if (!cur || at_limit(e)) {
+                e.launching = false;
+                return;
+            }
+            e.open = nullptr;
+            ++e.inflight;
+        }
+        uint64_t bytes = 0;
+        for (const Segment& s : cur->segs) bytes += s.len;
+        g_segments.fetch_add((int64_t)cur->segs.size(), std::memory_order_relaxed);
+        g_bytes.fetch_add((int64_t)bytes, std::memory_order_relaxed);
+        cur->t_issue_begin = monotonic_us();
+        launch(cur, device);
     }
 }
 
@@ -196,6 +279,7 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs, bool fol
         if (!e.open) {
             e.open = new_batch(e);
             e.open->butex->store(0, std::memory_order_relaxed);
+            e.open->retired.store(false, std::memory_order_relaxed);
             e.open->t_open = monotonic_us();
         }
         mine = e.open;
@@ -210,36 +294,26 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs, bool fol
         mine->nmsg += fold ? 1 : n;
         if (crcs) mine->want_crc = true;
         mine->refs.fetch_add(1, std::memory_order_relaxed);
-        if (!e.launching) {
+        if (!e.launching && !at_limit(e)) {
             e.launching = true;
             leader = true;
         }
     }
-    if (leader) {
-        // Drain: whatever accumulated while we were launching goes out as
-        // the next batch, until no submission is left open.
-        for (;;) {
-            Batch* cur;
-            {
-                std::lock_guard<std::mutex> g(e.mu);
-                cur = e.open;
-                e.open = nullptr;
-                if (!cur) {
-                    e.launching = false;
-                    break;
-                }
-            }
-            uint64_t bytes = 0;
-            for (const Segment& s : cur->segs) bytes += s.len;
-            g_segments.fetch_add((int64_t)cur->segs.size(), std::memory_order_relaxed);
-            g_bytes.fetch_add((int64_t)bytes, std::memory_order_relaxed);
-            cur->t_issue_begin = monotonic_us();
-            launch(cur, device);
-        }
-    }
+    if (leader) drain(e, device);
     const int64_t t_submit = monotonic_us();
     while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
     const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
+    // the first waiter of a finished batch gives its in-flight slot back and
+    // launches what collected meanwhile
+    if (!mine->retired.exchange(true, std::memory_order_acq_rel)) {
+        bool lead = false;
+        {
+            std::lock_guard<std::mutex> g(e.mu);
+            --e.inflight;
+            if (e.open && !e.launching) e.launching = lead = true;
+        }
+        if (lead) drain(e, device);
+    }
     if (rc == 0 && mine->t_done) {
         const int64_t now = monotonic_us();
         g_t_queue.fetch_add(std::max<int64_t>(0, mine->t_issue_begin - t_submit), std::memory_order_relaxed);
@@ -252,6 +326,11 @@ int BatchedCopy(const Segment* segs, int n, int device, uint32_t* crcs, bool fol
         if (t1 >= t0 && t1 - t0 < 100000000ull) {
             g_kernel_ticks.fetch_add((int64_t)(t1 - t0), std::memory_order_relaxed);
             g_kernel_timed.fetch_add(1, std::memory_order_relaxed);
+            const int64_t off = g_clock_offset_us.load(std::memory_order_relaxed);
+            if (off != INT64_MIN && mine->t_done) {
+                g_start_delay_us.fetch_add(off + (int64_t)(t0 / 100) - mine->t_issued, std::memory_order_relaxed);
+                g_notice_us.fetch_add(mine->t_done - (off + (int64_t)(t1 / 100)), std::memory_order_relaxed);
+            }
         }
     }
     if (rc == 0 && crcs) {
@@ -303,6 +382,8 @@ CopyEngineStats GetCopyEngineStats() {
     s.wake_us = g_t_wake.load(std::memory_order_relaxed);
     s.kernel_ticks = g_kernel_ticks.load(std::memory_order_relaxed);
     s.kernel_timed = g_kernel_timed.load(std::memory_order_relaxed);
+    s.start_delay_us = g_start_delay_us.load(std::memory_order_relaxed);
+    s.notice_us = g_notice_us.load(std::memory_order_relaxed);
     return s;
 }
 

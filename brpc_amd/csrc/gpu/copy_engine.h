@@ -40,6 +40,9 @@ struct CopyEngineStats {
     // launches with a completion word: summed kernel duration (GPU wall-clock
     // ticks, workgroup 0 start -> last workgroup end) and how many
     int64_t kernel_ticks = 0, kernel_timed = 0;
+    // over the same launches (GPU clock correlated to the host's): launch
+    // API return -> kernel start, kernel end -> completion seen (us, summed)
+    int64_t start_delay_us = 0, notice_us = 0;
 };
 CopyEngineStats GetCopyEngineStats();
 

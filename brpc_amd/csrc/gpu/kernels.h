@@ -36,6 +36,9 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
 // `out` needs no initialisation and may be pinned host memory (the kernel
 // stores each finished CRC; read it after the stream's event).
 int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s);
+// One lane stores the GPU wall clock (100 MHz) into *out_pinned (pinned host
+// memory, system scope): clock correlation for diagnostics.
+int LaunchClockProbe(uint64_t* out_pinned, hipStream_t s);
 // One wave that sleeps `us` microseconds of GPU wall clock (capped at 10 s).
 int LaunchSleepKernel(uint64_t us, hipStream_t s);
 // Completion word of a launch: the kernel's last workgroup to finish

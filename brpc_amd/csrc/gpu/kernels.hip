@@ -1056,6 +1056,15 @@ __global__ void sleep_kernel(uint64_t ticks) {
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+__global__ void clock_probe_kernel(unsigned long long* out) {
+    if (threadIdx.x == 0) __hip_atomic_store(out, wall_clock64(), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int LaunchClockProbe(uint64_t* out_pinned, hipStream_t s) {
+    hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, s, reinterpret_cast<unsigned long long*>(out_pinned));
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int LaunchSleepKernel(uint64_t us, hipStream_t s) {
     int dev = 0, khz = 0;
     hipGetDevice(&dev);

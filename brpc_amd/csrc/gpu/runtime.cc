@@ -180,7 +180,8 @@ private:
                     } else {
                         if (!now_pass) now_pass = monotonic_us();
                         r = hipErrorNotReady;
-                        if (now_pass - active[i].added_us > (int64_t)FLAGS_gpu_done_word_fallback_ms * 1000) {
+                        if (active[i].ev &&
+                            now_pass - active[i].added_us > (int64_t)FLAGS_gpu_done_word_fallback_ms * 1000) {
                             // overdue: the event decides (a failed launch)
                             r = hipEventQuery(active[i].ev);
                             if (r != hipErrorNotReady && active[i].fell_back) *active[i].fell_back = true;

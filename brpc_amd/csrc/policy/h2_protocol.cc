@@ -22,6 +22,7 @@
 #include "base/logging.h"
 #include "base/time.h"
 #include "base/util.h"
+#include "fiber/butex.h"
 #include "fiber/call_id.h"
 #include "fiber/sync.h"
 #include "http/hpack.h"
@@ -29,6 +30,9 @@
 #include "http/http_message.h"
 #include "json/json2pb.h"
 #include "net/input_messenger.h"
+#include "gpu/xgmi.h"
+#include "mrpc/proto/rpc_meta.pb.h"
+#include "policy/device_payload.h"
 #include "policy/policies.h"
 #include "rpc/authenticator.h"
 #include "rpc/controller.h"
@@ -44,6 +48,12 @@ DECLARE_uint64(max_body_size);
 DEFINE_int32(h2_client_stream_window_size, 256 * 1024, "initial receive window of each h2 stream");
 DEFINE_int32(h2_client_connection_window_size, 1024 * 1024, "receive window of each h2 connection");
 DEFINE_int32(h2_max_concurrent_streams, 100000, "SETTINGS_MAX_CONCURRENT_STREAMS we advertise");
+DEFINE_bool(h2_mrpc_extensions, false,
+            "announce the brpc_amd h2 extensions (attachments over gRPC) even without the device transport; by "
+            "default only a process with the xGMI transport announces them");
+DEFINE_int32(h2_device_settings_wait_ms, 200,
+             "a gRPC request with a device attachment on a connection whose peer SETTINGS have not arrived yet "
+             "waits this long to learn whether the peer takes device payloads");
 
 namespace mrpc {
 namespace policy {
@@ -65,6 +75,20 @@ enum : uint8_t {
 enum : uint8_t { F_END_STREAM = 1, F_ACK = 1, F_END_HEADERS = 4, F_PADDED = 8, F_PRIORITY = 0x20 };
 enum : uint32_t { H2_NO_ERROR = 0, H2_PROTOCOL_ERROR = 1, H2_INTERNAL_ERROR = 2, H2_FLOW_CONTROL_ERROR = 3,
                   H2_FRAME_SIZE_ERROR = 6, H2_REFUSED_STREAM = 7, H2_CANCEL = 8, H2_COMPRESSION_ERROR = 9 };
+
+// Device payloads over h2/gRPC (brpc_amd peers only):
+//  * a private SETTINGS parameter in the experimental range (RFC 7540
+//    §11.3: 0xf000-0xffff) announces that this end takes device payloads
+//    (its process has the xGMI transport). Peers that do not know it ignore
+//    it (§6.5.2), and it is only sent by processes with the transport, so a
+//    connection to a grpcio peer stays byte-identical;
+//  * the `mrpc-meta-bin` header (gRPC binary metadata: base64) carries an
+//    RpcMeta with the fields baidu_std puts in its meta: the xGMI hello, the
+//    lent DevicePayload descriptors and the size of the inline attachment
+//    bytes that follow the gRPC message in the DATA frames. It is only sent
+//    to a peer that announced the setting.
+const uint16_t kSettingsMrpcDevice = 0xF0A5;
+const char kMrpcMetaHeader[] = "mrpc-meta-bin";
 
 const char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
 const size_t kPrefaceLen = 24;
@@ -114,8 +138,11 @@ public:
     static const int kTag = 0x48324358;  // "H2CX"
     int protocol_tag() const override { return kTag; }
 
-    H2Context(bool server) : _server(server), _next_stream_id(1) {}
+    H2Context(bool server) : _server(server), _next_stream_id(1), _settings_seen(fiber::butex_create()) {
+        _settings_seen->store(0, std::memory_order_relaxed);
+    }
     ~H2Context() override {
+        fiber::butex_destroy(_settings_seen);
         for (auto& kv : _streams) {
             if (kv.second->cid != fiber::INVALID_CALL_ID) {
                 fiber::call_id_error(kv.second->cid, EFAILEDSOCKET, "h2 connection closed");
@@ -124,6 +151,28 @@ public:
         }
     }
     bool server() const { return _server; }
+    // The peer announced kSettingsMrpcDevice (takes device payloads and the
+    // mrpc-meta-bin header).
+    bool peer_takes_device_payloads() const { return _peer_device.load(std::memory_order_acquire); }
+    // Client: wait (bounded) until the peer's first SETTINGS arrived (our
+    // preface goes out first: a server answers it with its SETTINGS).
+    bool WaitPeerSettings(Socket* s, int64_t timeout_us) {
+        if (_settings_seen->load(std::memory_order_acquire)) return true;
+        {
+            std::lock_guard<fiber::Mutex> g(_mu);
+            Buf out;
+            send_local_settings_locked(&out);
+            write_locked(s, &out);
+        }
+        const int64_t deadline = monotonic_us() + timeout_us;
+        while (_settings_seen->load(std::memory_order_acquire) == 0) {
+            const int64_t left = deadline - monotonic_us();
+            if (left <= 0) return false;
+            timespec ts = realtime_after_us(std::min<int64_t>(left, 10000));
+            fiber::butex_wait(_settings_seen, 0, &ts);
+        }
+        return true;
+    }
 
     // ---------------------------------------------------------------- read
     ParseResult Consume(Buf* src, Socket* s);
@@ -175,6 +224,8 @@ private:
     int64_t _conn_recv_unacked = 0;
     bool _goaway = false;
     std::unordered_map<uint32_t, Stream*> _streams;
+    std::atomic<int>* _settings_seen;  // butex: 1 once the peer's first SETTINGS were applied
+    std::atomic<bool> _peer_device{false};
 };
 
 void H2Context::write_locked(Socket* s, Buf* frames, fiber::CallId id_wait) {
@@ -195,10 +246,13 @@ void H2Context::send_local_settings_locked(Buf* out) {
     } params[] = {{2, 0},
                   {3, (uint32_t)FLAGS_h2_max_concurrent_streams},
                   {4, (uint32_t)FLAGS_h2_client_stream_window_size},
-                  {5, kFrameSize}};
-    const int n = sizeof(params) / sizeof(params[0]);
+                  {5, kFrameSize},
+                  {kSettingsMrpcDevice, 1}};
+    int n = sizeof(params) / sizeof(params[0]);
+    if (!gpu::XgmiEnabled() && !FLAGS_h2_mrpc_extensions) --n;  // only with the device transport, by default
     frame_header(out, 6 * n, H2_SETTINGS, 0, 0);
-    for (auto& p : params) {
+    for (int i = 0; i < n; ++i) {
+        const auto& p = params[i];
         char b[6];
         const uint16_t id = htons(p.id);
         const uint32_t v = htonl(p.v);
@@ -411,9 +465,11 @@ int H2Context::on_settings(Socket* s, uint8_t flags, Buf& payload) {
         }
         case 5: _remote.max_frame_size = v; break;
         case 6: _remote.max_header_list_size = v; break;
+        case kSettingsMrpcDevice: _peer_device.store(v == 1, std::memory_order_release); break;
         default: break;  // unknown settings are ignored
         }
     }
+    if (_settings_seen->exchange(1, std::memory_order_acq_rel) == 0) fiber::butex_wake_all(_settings_seen);
     Buf out;
     send_local_settings_locked(&out);
     frame_header(&out, 0, H2_SETTINGS, F_ACK, 0);
@@ -737,6 +793,43 @@ ParseResult ParseH2Message(Buf* source, Socket* socket, bool read_eof, const voi
 }
 
 static bool is_grpc_content(const std::string& ct) { return starts_with(ct, "application/grpc"); }
+
+// mrpc-meta-bin (see kSettingsMrpcDevice): false on a malformed header.
+static bool parse_mrpc_meta(const HttpHeader& h, RpcMeta* m, bool* present) {
+    const std::string* v = h.GetHeader(kMrpcMetaHeader);
+    *present = v != nullptr;
+    if (!v) return true;
+    std::string raw;
+    return base64_decode(*v, &raw) && m->ParseFromString(raw);
+}
+
+static std::string encode_mrpc_meta(const RpcMeta& m) {
+    std::string raw;
+    m.SerializeToString(&raw);
+    return base64_encode(raw.data(), raw.size());
+}
+
+static bool cut_inline_attachment(Buf* body, const RpcMeta& m, Buf* out);
+
+// Client: a well-formed mrpc-meta-bin whose inline attachment (if any) was
+// moved from the body's tail into the response attachment.
+static bool take_inline_attachment(Controller* cntl, bool ok, const RpcMeta& m, Buf* body) {
+    cntl->response_attachment().clear();
+    return ok && cut_inline_attachment(body, m, &cntl->response_attachment());
+}
+
+// The inline attachment bytes a brpc_amd peer appended after the gRPC
+// message (RpcMeta.attachment_size): moved from the tail of `body` to *out.
+static bool cut_inline_attachment(Buf* body, const RpcMeta& m, Buf* out) {
+    const int64_t n = m.attachment_size();
+    if (n <= 0) return true;
+    if ((uint64_t)n > body->size()) return false;
+    Buf msg;
+    body->cutn(&msg, body->size() - (size_t)n);
+    out->append(std::move(*body));
+    body->swap(msg);
+    return true;
+}
 static bool has_fields(const pb::Message* m) { return m && m->GetDescriptor()->field_count() > 0; }
 
 // ------------------------------------------------------------------ client
@@ -839,8 +932,38 @@ void PackH2Request(Buf* packet, uint64_t correlation_id, const pb::MethodDescrip
     }
     hs.push_back({"user-agent", "mrpc/1.0"});
     Buf body(request_buf);
+    // Attachments over gRPC exist between brpc_amd peers only (the
+    // reference refuses them: http_rpc_protocol.cpp:511): device blocks are
+    // lent exactly as on baidu_std (SplitDevicePayload: xGMI or the RCCL
+    // plane, device snappy, pb_scan), host bytes follow the message inline,
+    // and mrpc-meta-bin describes both.
+    RpcMeta dmeta;
+    bool send_meta = false;
+    const Buf& att = cntl->request_attachment();
+    if (grpc && !att.empty()) {
+        if (!ctx->peer_takes_device_payloads()) ctx->WaitPeerSettings(s, (int64_t)FLAGS_h2_device_settings_wait_ms * 1000);
+        if (!ctx->peer_takes_device_payloads()) {
+            cntl->SetFailed(EREQUEST, "request_attachment must be empty for grpc unless the peer takes device payloads");
+            return;
+        }
+        Buf host;
+        if (!SplitDevicePayload(cntl, /*request=*/true, att, &host, &dmeta, s)) return;
+        if (!host.empty()) {
+            dmeta.set_attachment_size((int32_t)host.size());
+            body.append(std::move(host));
+        }
+        send_meta = true;
+    }
+    // xGMI hello, offered until the connection has a device transport
+    if (grpc && cntl->_use_device_transport && !s->transport() && ctx->peer_takes_device_payloads() &&
+        gpu::FillXgmiHello(dmeta.mutable_xgmi_hello())) {
+        send_meta = true;
+    }
+    if (send_meta) hs.push_back({kMrpcMetaHeader, encode_mrpc_meta(dmeta)});
     std::string err;
     if (ctx->StartRequest(s, fiber::CallId{correlation_id}, hs, &body, &err) != 0) {
+        CancelDevicePayload(dmeta);  // never sent: un-lend
+        if (cntl->_packed_payloads) cntl->_packed_payloads->descs.Clear();
         cntl->SetFailed(EFAILEDSOCKET, "%s", err.c_str());
     }
     // frames are already written in order under the context lock
@@ -849,7 +972,30 @@ void PackH2Request(Buf* packet, uint64_t correlation_id, const pb::MethodDescrip
 
 void ProcessH2Response(InputMessageBase* msg_base) {
     std::unique_ptr<HttpMessage> msg(static_cast<HttpMessage*>(msg_base));
+    Socket* sock = msg->socket();
+    RpcMeta dmeta;
+    bool has_dmeta = false;
+    const bool dmeta_ok = parse_mrpc_meta(msg->header, &dmeta, &has_dmeta);
+    if (has_dmeta && dmeta_ok && dmeta.has_xgmi_hello() && gpu::XgmiEnabled()) {
+        std::string err;
+        if (gpu::AttachXgmiPeer(sock, dmeta.xgmi_hello(), &err) != 0) {
+            LOG_EVERY_SECOND(WARNING) << "xGMI peer " << sock->remote_side() << " not attached: " << err;
+        }
+    }
+    // h2 connections never join the RCCL plane; requests waiting to learn
+    // the connection's transports go ahead
+    if (sock->plane_rank() == Socket::kPlaneUnknown) sock->set_plane_rank(-1);
+    sock->DeviceHelloAnswered();
     const fiber::CallId cid = msg->pi.id_wait;
+    bool device_payload_taken = false;
+    struct GiveBack {  // lent response payloads nobody pulls go back to the server
+        Socket* s;
+        const RpcMeta& m;
+        const bool& taken;
+        ~GiveBack() {
+            if (!taken) ReleaseDevicePayload(s, m);
+        }
+    } give_back{sock, dmeta, device_payload_taken};
     if (cid == fiber::INVALID_CALL_ID) return;
     Controller* cntl = nullptr;
     if (fiber::call_id_lock(cid, (void**)&cntl) != 0) return;
@@ -871,14 +1017,25 @@ void ProcessH2Response(InputMessageBase* msg_base) {
         if (body.size() > 512) body.resize(512);
         saved_error = EHTTP;
         cntl->SetFailed(EHTTP, "[HTTP %d] %s", status, body.c_str());
+    } else if (grpc && has_dmeta && !take_inline_attachment(cntl, dmeta_ok, dmeta, &msg->body)) {
+        saved_error = ERESPONSE;
+        cntl->SetFailed(ERESPONSE, "bad %s header", kMrpcMetaHeader);
     } else if (grpc) {
+        if (has_dmeta && dmeta.device_payload_size() > 0) {
+            device_payload_taken = true;
+            if (!MergeDevicePayload(cntl, sock, dmeta, /*request=*/false, &cntl->response_attachment())) {
+                saved_error = cntl->ErrorCode();
+            }
+        }
         Buf pbbuf;
         bool compressed = false;
-        const int r = RemoveGrpcPrefix(&msg->body, &pbbuf, &compressed);
+        const int r = saved_error ? 1 : RemoveGrpcPrefix(&msg->body, &pbbuf, &compressed);
         const std::string* enc = msg->header.GetHeader("grpc-encoding");
         const int ct = compressed ? GrpcEncodingToCompressType(enc ? *enc : std::string()) : COMPRESS_TYPE_NONE;
         Buf plain;
-        if (r != 1) {
+        if (saved_error) {
+            // the device payload failed (already reported)
+        } else if (r != 1) {
             saved_error = ERESPONSE;
             cntl->SetFailed(ERESPONSE, "bad grpc response framing");
         } else if (compressed && ct <= 0) {
@@ -927,6 +1084,7 @@ struct H2ServerCall {
     uint32_t sid;
     bool grpc;
     bool json_proto;  // h2 (non-grpc) with a proto content type
+    bool peer_device = false;  // the request came with mrpc-meta-bin: attachments may go back the same way
 };
 
 static void SendH2Response(H2ServerCall c) {
@@ -947,6 +1105,21 @@ static void SendH2Response(H2ServerCall c) {
         hs.push_back({":status", "200"});
         hs.push_back({"content-type", "application/grpc"});
         std::vector<HPackHeader> trailers;
+        // the response attachment of a brpc_amd peer: device blocks lent
+        // (descriptors in mrpc-meta-bin), host bytes after the message
+        RpcMeta dmeta;
+        Buf inline_att;
+        bool send_meta = cntl->_reply_xgmi_hello && gpu::FillXgmiHello(dmeta.mutable_xgmi_hello());
+        if (!cntl->Failed() && !cntl->response_attachment().empty()) {
+            if (!c.peer_device) {
+                LOG_EVERY_SECOND(WARNING) << "response_attachment (" << cntl->response_attachment().size()
+                                          << " bytes) dropped: a grpc peer without device payloads";
+            } else if (SplitDevicePayload(cntl, /*request=*/false, cntl->response_attachment(), &inline_att, &dmeta,
+                                          sock.get())) {
+                if (!inline_att.empty()) dmeta.set_attachment_size((int32_t)inline_att.size());
+                send_meta = true;
+            }
+        }
         if (!cntl->Failed() && c.res) {
             Buf pbbuf;
             const int ct = cntl->response_compress_type();
@@ -969,8 +1142,15 @@ static void SendH2Response(H2ServerCall c) {
         if (cntl->Failed()) {
             body.clear();
             trailers.push_back({"grpc-message", PercentEncode(cntl->ErrorText())});
+            // nothing of the attachment goes out: un-lend it
+            CancelDevicePayload(dmeta);
+            dmeta.clear_device_payload();
+            dmeta.clear_attachment_size();
+        } else if (!inline_att.empty()) {
+            body.append(std::move(inline_att));
         }
-        ctx->SendResponse(sock.get(), c.sid, hs, &body, &trailers);
+        if (send_meta) hs.push_back({kMrpcMetaHeader, encode_mrpc_meta(dmeta)});
+        if (ctx->SendResponse(sock.get(), c.sid, hs, &body, &trailers) != 0) CancelDevicePayload(dmeta);
         return;
     }
     int status = rh.status_code();
@@ -1019,10 +1199,23 @@ void ProcessH2Request(InputMessageBase* msg_base) {
     const bool grpc = is_grpc_content(req_h.content_type());
     H2ServerCall call{cntl, nullptr, nullptr, nullptr, nullptr, start_us, msg->stream_id, grpc,
                       req_h.content_type().find("proto") != std::string::npos};
+    RpcMeta dmeta;
+    bool has_dmeta = false;
+    const bool dmeta_ok = parse_mrpc_meta(req_h, &dmeta, &has_dmeta);
+    bool device_payload_taken = false;
     if (grpc) {
         if (const std::string* t = req_h.GetHeader("grpc-timeout")) {
             const int64_t us = ConvertGrpcTimeoutToUS(*t);
             if (us > 0) cntl->_deadline_us = msg->received_us() + us;
+        }
+        call.peer_device = has_dmeta && dmeta_ok;
+        if (call.peer_device && dmeta.has_xgmi_hello() && gpu::XgmiEnabled()) {
+            std::string err;
+            if (gpu::AttachXgmiPeer(socket, dmeta.xgmi_hello(), &err) == 0) {
+                cntl->_reply_xgmi_hello = true;
+            } else {
+                LOG_EVERY_SECOND(WARNING) << "xGMI peer " << socket->remote_side() << " not attached: " << err;
+            }
         }
     }
     const Server::MethodProperty* mp = nullptr;
@@ -1058,6 +1251,17 @@ void ProcessH2Request(InputMessageBase* msg_base) {
         call.req = mp->service->GetRequestPrototype(mp->method).New();
         call.res = mp->service->GetResponsePrototype(mp->method).New();
         if (grpc) {
+            if (has_dmeta) {
+                if (!dmeta_ok || !cut_inline_attachment(&msg->body, dmeta, &cntl->request_attachment())) {
+                    cntl->SetFailed(EREQUEST, "bad %s header", kMrpcMetaHeader);
+                    break;
+                }
+                device_payload_taken = true;
+                if (dmeta.device_payload_size() > 0 &&
+                    !MergeDevicePayload(cntl, socket, dmeta, /*request=*/true, &cntl->request_attachment())) {
+                    break;
+                }
+            }
             Buf pbbuf;
             bool compressed = false;
             const int r = RemoveGrpcPrefix(&msg->body, &pbbuf, &compressed);
@@ -1096,6 +1300,9 @@ void ProcessH2Request(InputMessageBase* msg_base) {
             cntl->request_attachment().swap(msg->body);
         }
     } while (false);
+    // rejected before the descriptors were looked at: the client's lent
+    // blocks still go back
+    if (has_dmeta && dmeta_ok && !device_payload_taken) ReleaseDevicePayload(socket, dmeta);
     msg.reset();
     if (concurrency_added) call.server = server;
     if (cntl->Failed()) {

@@ -594,6 +594,8 @@ PYBIND11_MODULE(_native, m) {
         d["copy_wake_us"] = c.wake_us;
         d["copy_kernel_ticks"] = c.kernel_ticks;
         d["copy_kernel_timed"] = c.kernel_timed;
+        d["copy_start_delay_us"] = c.start_delay_us;
+        d["copy_notice_us"] = c.notice_us;
         return d;
     });
     g.def("reap_lent", [] { gpu::ReapLentBlocks(); });

@@ -1,6 +1,10 @@
 // HTTP protocol + json2pb + builtin pages (spirit of the reference's
 // test/brpc_http_rpc_protocol_unittest.cpp, brpc_http_message_unittest.cpp,
 // test/brpc_builtin_service_unittest.cpp, json2pb unittests).
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include <cmath>
@@ -658,4 +662,115 @@ TEST(H2, json_and_grpc) {
     ch.CallMethod(nullptr, &cntl, nullptr, nullptr, nullptr);
     ASSERT_FALSE(cntl.Failed());
     EXPECT_EQ(cntl.response_attachment().to_string(), "OK\n");
+}
+
+// Attachments over gRPC (policy/h2_protocol.cc kSettingsMrpcDevice): the
+// reference refuses them (http_rpc_protocol.cpp:511); between brpc_amd peers
+// that announced the private SETTINGS parameter they travel in-band (host
+// bytes after the message, sized by the mrpc-meta-bin header) or lent (device
+// blocks, GPU tests). Without the announcement nothing of it is on the wire.
+DECLARE_bool(h2_mrpc_extensions);
+
+TEST(H2, grpc_attachment_needs_an_mrpc_peer) {
+    HttpServer s;
+    ASSERT_GT(s.port, 0);
+    Channel ch;
+    ChannelOptions opt;
+    opt.protocol = "h2:grpc";
+    opt.timeout_ms = 3000;
+    ASSERT_EQ(ch.Init(s.addr().c_str(), &opt), 0);
+    example::EchoService_Stub stub(&ch);
+    Controller cntl;
+    example::EchoRequest req;
+    example::EchoResponse res;
+    req.set_message("with attachment");
+    cntl.request_attachment().append("tail bytes");
+    stub.Echo(&cntl, &req, &res, nullptr);
+    ASSERT_TRUE(cntl.Failed());
+    EXPECT_EQ(cntl.ErrorCode(), EREQUEST);
+    EXPECT_NE(cntl.ErrorText().find("request_attachment must be empty"), std::string::npos);
+    // the same channel still serves plain gRPC calls
+    Controller c2;
+    example::EchoResponse r2;
+    stub.Echo(&c2, &req, &r2, nullptr);
+    ASSERT_TRUE_M(!c2.Failed(), c2.ErrorText());
+    EXPECT_EQ(r2.message(), "with attachment");
+}
+
+TEST(H2, grpc_attachments_between_mrpc_peers) {
+    FLAGS_h2_mrpc_extensions = true;
+    {
+        HttpServer s;
+        ASSERT_GT(s.port, 0);
+        Channel ch;
+        ChannelOptions opt;
+        opt.protocol = "h2:grpc";
+        opt.timeout_ms = 3000;
+        ASSERT_EQ(ch.Init(s.addr().c_str(), &opt), 0);
+        example::EchoService_Stub stub(&ch);
+        for (int i = 0; i < 40; ++i) {
+            Controller cntl;
+            example::EchoRequest req;
+            example::EchoResponse res;
+            req.set_message("m" + std::to_string(i));
+            // 0, small and multi-frame attachments (> the 16 KiB frame size)
+            const std::string att = i % 4 == 0 ? "" : std::string((size_t)(i % 4 == 3 ? 100000 : 37 * i), (char)('a' + i % 26));
+            cntl.request_attachment().append(att);
+            if (i % 5 == 1) cntl.set_request_compress_type(COMPRESS_TYPE_GZIP);  // the message compressed, not the attachment
+            stub.Echo(&cntl, &req, &res, nullptr);
+            ASSERT_TRUE_M(!cntl.Failed(), std::to_string(i) + ": " + cntl.ErrorText());
+            EXPECT_EQ(res.message(), req.message());
+            EXPECT_TRUE_M(cntl.response_attachment().to_string() == att, std::to_string(i));
+        }
+    }
+    FLAGS_h2_mrpc_extensions = false;
+}
+
+TEST(H2, mrpc_settings_parameter_only_when_announced) {
+    // a raw client reads the server's SETTINGS: 4 parameters by default
+    // (grpcio peers see the frames they always saw), 5 with the extensions
+    for (bool on : {false, true}) {
+        FLAGS_h2_mrpc_extensions = on;
+        HttpServer s;
+        ASSERT_GT(s.port, 0);
+        const int fd = socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_port = htons((uint16_t)s.port);
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        ASSERT_EQ(connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)), 0);
+        const std::string hello = std::string("PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n", 24) + std::string("\0\0\0\x04\0\0\0\0\0", 9);
+        ASSERT_EQ(write(fd, hello.data(), hello.size()), (ssize_t)hello.size());
+        std::string in;
+        bool found = false;
+        uint32_t settings_len = 0;
+        for (int tries = 0; tries < 100 && !found; ++tries) {
+            pollfd p{fd, POLLIN, 0};
+            if (poll(&p, 1, 100) <= 0) continue;
+            char buf[4096];
+            const ssize_t n = read(fd, buf, sizeof(buf));
+            if (n <= 0) break;
+            in.append(buf, (size_t)n);
+            for (size_t off = 0; off + 9 <= in.size();) {
+                const uint32_t len = ((uint32_t)(uint8_t)in[off] << 16) | ((uint32_t)(uint8_t)in[off + 1] << 8) |
+                                     (uint8_t)in[off + 2];
+                if (off + 9 + len > in.size()) break;
+                if (in[off + 3] == 4 && (in[off + 4] & 1) == 0) {
+                    settings_len = len;
+                    found = true;
+                    bool has = false;
+                    for (uint32_t k = 0; k + 6 <= len; k += 6) {
+                        const uint16_t id = (uint16_t)(((uint8_t)in[off + 9 + k] << 8) | (uint8_t)in[off + 10 + k]);
+                        has |= id == 0xF0A5;
+                    }
+                    EXPECT_EQ(has, on);
+                }
+                off += 9 + len;
+            }
+        }
+        close(fd);
+        ASSERT_TRUE(found);
+        EXPECT_EQ(settings_len, on ? 30u : 24u);
+    }
+    FLAGS_h2_mrpc_extensions = false;
 }

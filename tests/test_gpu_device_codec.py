@@ -204,6 +204,34 @@ def test_compressed_device_attachments_verified(dev):
         s.stop()
 
 
+@pytest.mark.parametrize("compress", [0, 1])
+def test_grpc_device_attachments_lent_encoded_and_indexed(dev, compress):
+    """BASELINE config 4 on HBM bodies: the same device body over h2:grpc.
+    The connection negotiates through the private SETTINGS parameter and the
+    xGMI hello in mrpc-meta-bin; after that every request and response body
+    is lent (device-snappy-encoded when asked), pb-scanned on arrival, and
+    every reply checked byte for byte and against its field table."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        x0, c0 = native.gpu.xgmi_stats(), native.gpu.device_codec_stats()
+        st = _echo(native, s.address, 1000, protocol="h2:grpc", attachment_body="text", attachment_pb=True,
+                   device_scan=True, device_compress=compress)
+        assert st["success"] == 1000 and st["error"] == 0, st
+        x1, c1 = native.gpu.xgmi_stats(), native.gpu.device_codec_stats()
+        # requests and responses, but for the first calls of the connection
+        # (staged in-band while the hello is in flight)
+        assert x1["recv_payloads"] - x0["recv_payloads"] >= 1900, (x0, x1)
+        assert c1["scans"] - c0["scans"] >= 1900, (c0, c1)
+        if compress:
+            assert x1["compressed_recv"] - x0["compressed_recv"] >= 1900, (x0, x1)
+            assert c1["decodes"] - c0["decodes"] >= 1900, (c0, c1)
+        assert c1["bad_tables"] == c0["bad_tables"] and c1["decode_errors"] == c0["decode_errors"]
+    finally:
+        s.stop()
+
+
 _SERVER_SCRIPT = r"""
 import sys, torch
 from brpc_amd.models import start_echo_server

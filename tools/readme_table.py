@@ -81,6 +81,19 @@ def rows(d):
         add("http + json, 64 KiB text string field (host only: the JSON offload's density gate leaves a long string "
             "field to the host)",
             "%s QPS" % k(d["http_json_64KB_text_qps_cpu"]), us(d, "http_json_64KB_text_cpu"))
+    if "rccl_self_copy_64KB_qps" in d:
+        add("Echo 64 KiB / 1 MiB through the one-rank RCCL plane: self payloads moved by the plane's copy kernel "
+            "(NOT RCCL; -rccl_self_copy)",
+            "%s QPS / %s QPS (%.0f GB/s), %s aborts" % (k(d["rccl_self_copy_64KB_qps"]),
+                                                        k(d.get("rccl_self_copy_1MB_qps", 0)),
+                                                        d.get("rccl_self_copy_1MB_gbytes_per_s", 0),
+                                                        d.get("rccl_aborts")),
+            us(d, "rccl_64KB"))
+    if "rccl_nccl_self_64KB_qps" in d:
+        add("Echo 64 KiB through ncclSend/ncclRecv to self (one-rank plane, -rccl_self_copy=false)",
+            "%s QPS, p99 %s µs, %s µs per group" % (k(d["rccl_nccl_self_64KB_qps"]), d.get("rccl_nccl_self_64KB_p99_us"),
+                                                    d.get("rccl_nccl_self_group_us_per_round")),
+            us(d, "rccl_nccl_self_64KB"))
     if "rccl_64KB_qps" in d:
         add("Echo 64 KiB / 1 MiB over the RCCL plane (%s-rank communicator)" % d.get("rccl_world"),
             "%s QPS / %s QPS (%.0f GB/s), %s aborts" % (k(d["rccl_64KB_qps"]), k(d.get("rccl_1MB_qps", 0)),
