@@ -36,7 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", default="gpu_handler",
                     choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps", "grpc_cpu",
-                             "grpc_gpu", "baidu_cpu", "baidu_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu", "dev_snappy",
+                             "grpc_gpu", "baidu_cpu", "baidu_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu", "dev_snappy", "grpc_dev_snappy", "grpc_dev_64k",
                              "dev_1m_verify"])
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--body", default="text", help="echo body kind of the codec legs: text, random, const")
@@ -80,11 +80,15 @@ def main():
         o["gpu_process"] = True
     if a.leg in ("dev_64k", "rccl_64k"):
         o["device_attachment"] = True
-    if a.leg == "dev_snappy":
-        # the bench's device_snappy_64KB_<body> leg: an HBM protobuf body
+    if a.leg == "grpc_dev_64k":
+        o.update({"attachment_size": 65536, "device_attachment": True, "protocol": "h2:grpc"})
+    if a.leg in ("dev_snappy", "grpc_dev_snappy"):
+        # the bench's [grpc_]device_snappy_64KB_<body> leg: an HBM protobuf body
         # encoded/decoded/indexed on the device both ways
         o.update({"attachment_size": 65536, "device_attachment": True, "attachment_body": a.body,
                   "attachment_pb": True, "device_scan": True, "device_compress": 1})
+        if a.leg == "grpc_dev_snappy":
+            o["protocol"] = "h2:grpc"
     if a.leg == "dev_1m_verify":
         # 1 MiB HBM attachments, CRC32C-verified on the device (fused into the pull)
         o.update({"attachment_size": 1 << 20, "device_attachment": True, "verify_device_payload": True})
@@ -92,7 +96,7 @@ def main():
         o["request_size"] = 32
     if a.leg == "lat_100qps":
         o.update({"qps": 100.0, "concurrency": 1, "request_size": 32})
-    if a.leg.startswith("grpc"):
+    if a.leg in ("grpc_cpu", "grpc_gpu"):
         # the bench's gRPC + snappy leg: 64 KiB protobuf body, snappy both ways
         o.update({"request_size": 65536, "protocol": "h2:grpc", "request_compress_type": 1})
         if a.leg == "grpc_gpu":
@@ -141,7 +145,7 @@ def main():
     if st["error"]:
         print("last_error:", st.get("last_error"), "codes:", st.get("error_codes"))
     x1 = native.gpu.xgmi_stats()
-    if a.leg == "dev_snappy":
+    if a.leg.endswith("dev_snappy"):
         print("device codec:", native.gpu.device_codec_stats(), "codec batch:", native.gpu.codec_batch_stats())
     if os.environ.get("RESIDENT"):
         print("resident:", native.gpu.resident_stats())

@@ -258,8 +258,8 @@ bool HuffmanDecode(const uint8_t* p, size_t n, std::string* out) {
 }  // namespace hpack
 
 // ------------------------------------------------------------------ encoder
-static void encode_string(std::string* out, const std::string& s) {
-    const size_t hl = hpack::HuffmanEncodedLength(s);
+static void encode_string(std::string* out, const std::string& s, bool huffman = true) {
+    const size_t hl = huffman ? hpack::HuffmanEncodedLength(s) : s.size();
     if (hl < s.size()) {
         hpack::EncodeInteger(out, 0x80, 7, hl);
         hpack::HuffmanEncode(out, s);
@@ -293,7 +293,7 @@ void HPackEncoder::Encode(Buf* out, const HPackHeader& h, HPackIndexPolicy polic
     } else {
         hpack::EncodeInteger(&s, policy == HPackIndexPolicy::NEVER_INDEXED ? 0x10 : 0x00, 4, name_only);
         if (!name_only) encode_string(&s, h.name);
-        encode_string(&s, h.value);
+        encode_string(&s, h.value, policy != HPackIndexPolicy::NOT_INDEXED_RAW);
     }
     out->append(s);
 }
