@@ -344,6 +344,13 @@ def main(argv=None):
     if a.fail_rank >= 0 and int(os.environ.get("RANK", "0")) == a.fail_rank:
         print("bench: --fail-rank %d: exiting" % a.fail_rank, file=sys.stderr, flush=True)
         return 3
+    # Several ranks on one GPU (a rehearsal on a smaller box): keep the
+    # hardware queues of all of them within what the GPU maps at once. Set
+    # before the HIP runtime starts (the first torch.cuda call).
+    from brpc_amd.parallel.topology import hw_queues_per_rank  # noqa: E402 (no HIP call)
+    hwq = hw_queues_per_rank(int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+    if "GPU_MAX_HW_QUEUES" not in os.environ and hwq < 4:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
     import torch  # noqa: E402
     from brpc_amd import native  # noqa: E402
     from brpc_amd.models import ECHO_32B, ECHO_64KB, EchoWorkload, start_echo_server  # noqa: E402
@@ -355,6 +362,10 @@ def main(argv=None):
         k, _, v = f.partition("=")
         native.set_flag(k, v)
     native.set_flag("fiber_concurrency", str(workers))
+    # the pool's streams map 1:1 onto the hardware queues the rank may use
+    hwq_now = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    if hwq_now < 4:
+        native.set_flag("gpu_streams_per_device", str(max(1, hwq_now)))
     placement = {}
     if a.cpu_l3_domain != -2:
         l3 = a.cpu_l3_domain
@@ -495,6 +506,25 @@ def main(argv=None):
             out["cgroup_throttled_periods"] = int(d["cg_nr_throttled"] / n)
             out["cgroup_throttled_ms"] = round(d["cg_throttled_usec"] / n / 1000.0, 1)
         return out
+
+    # Perf floor (N > 1): a device leg whose QPS per GPU in use is below
+    # perf_floor x its one-rank rate (benchmarks/n1_reference.json) is
+    # flagged: transport_ok only says WHICH path the payloads took.
+    try:
+        with open(os.path.join(ROOT, "benchmarks", "n1_reference.json")) as f:
+            n1_ref = json.load(f)
+    except (OSError, ValueError):
+        n1_ref = {}
+
+    def perf_check(name, qps):
+        ref = n1_ref.get("qps", {}).get(name)
+        if n <= 1 or not ref:
+            return None
+        gpus = max(1, len(set(devices))) if cuda else 1
+        per_gpu = qps / gpus
+        floor = float(n1_ref.get("perf_floor", 0.25)) * ref
+        return per_gpu >= floor, {"qps_per_gpu": round(per_gpu, 1), "gpus": gpus, "floor_qps": round(floor, 1),
+                                  "n1_qps": ref}
 
     def transport_check(tr, kind, cross_gpu):
         """Did the leg's payloads take the transport it is meant to
@@ -645,6 +675,7 @@ def main(argv=None):
         tr = transport_delta(tr0)
         dg = diag_delta(dg0)
         ok, why = transport_check(tr, transport_kind, cross_gpu)
+        perf = perf_check(name, ok_total / dt_max if dt_max > 0 else 0.0) if transport_kind else None
         step_seq = [c / x for c, x in zip(step_n, step_s) if x > 0]
         step_qps = sorted(step_seq)
         r = {
@@ -675,6 +706,8 @@ def main(argv=None):
             r["transport_ok"] = ok
             if why:
                 r["transport_problems"] = why
+        if perf is not None:
+            r["perf_ok"], r["perf_floor"] = perf
         return r
 
     def latency_sample(name, deadline):
@@ -1223,6 +1256,7 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
             "control_plane": topo.backend or "none",
             "devices_by_rank": extra.get("devices"),
             "flags": list(a.flag),  # --flag NAME=VALUE overrides of this run
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
         },
     }
     if r32:
@@ -1355,6 +1389,11 @@ def build_output(a, topo, legs, extra, workers, l3, placement):
     dg = {k: v["diag"] for k, v in timed.items() if v.get("diag")}
     if dg:
         out["diag"] = dg
+    # per-leg performance floor (N > 1): per-GPU QPS against the N = 1 rate
+    pok = {k: v["perf_ok"] for k, v in legs.items() if isinstance(v, dict) and "perf_ok" in v}
+    if pok:
+        out["perf_ok"] = pok
+        out["perf_floor"] = {k: v["perf_floor"] for k, v in legs.items() if isinstance(v, dict) and "perf_floor" in v}
     # per-leg transport verdict (N > 1): a silent staging fallback shows here
     tok = {k: v["transport_ok"] for k, v in legs.items() if isinstance(v, dict) and "transport_ok" in v}
     if tok:

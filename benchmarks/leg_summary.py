@@ -17,7 +17,7 @@ def main(path):
             print("  %-48s %12s" % (leg, v))
     for k, v in sorted(cpu.items()):
         print("  cpu_us %-41s %8s %s" % (k, v, "" if k not in tok else ("transport ok" if tok[k] else "TRANSPORT BAD")))
-    for k in ("timed_out_legs", "failed_legs", "skipped_legs", "error_detail", "transport_problems"):
+    for k in ("timed_out_legs", "failed_legs", "skipped_legs", "error_detail", "transport_problems", "perf_ok"):
         if k in j:
             print("  %s: %s" % (k, j[k]))
     for k, v in sorted(j.get("diag", {}).items()):

@@ -60,6 +60,45 @@ def init_distributed(prefer_gpu=True):
     return Topology(rank, ws, lrank, lws, device, backend)
 
 
+def _kfd_gpu_nodes():
+    """(simd_count, num_cp_queues) of every GPU node in the KFD topology,
+    read from sysfs: no HIP call, so it can run before the runtime starts."""
+    import glob
+    out = []
+    for path in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")):
+        props = {}
+        try:
+            with open(path) as f:
+                for line in f:
+                    k, _, v = line.strip().partition(" ")
+                    props[k] = v
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0") or 0) > 0:
+            out.append(int(props.get("num_cp_queues", "0") or 0))
+    return out
+
+
+def hw_queues_per_rank(local_world_size, default=4):
+    """Hardware queues each rank's HIP runtime may create (GPU_MAX_HW_QUEUES)
+    when several ranks share a GPU. The GPU maps at most num_cp_queues
+    compute queues of all its processes at once (24 on the MI355X boxes,
+    KFD topology); beyond that the scheduler time-slices the queues, and a
+    kernel waits hundreds of microseconds for its queue's turn. Measured, 8
+    ranks on one GPU (4 streams + 1 internal queue each = 40 queues):
+    echo_64KB 18k QPS; with 2 queues each: 569k (profiles/r6_xproc_diagnosis.txt).
+    One rank per GPU keeps the default."""
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    nodes = _kfd_gpu_nodes()
+    ngpu = len([x for x in vis.split(",") if x.strip()]) if vis else len(nodes)
+    if ngpu <= 0 or local_world_size <= ngpu:
+        return default
+    per_gpu = (local_world_size + ngpu - 1) // ngpu
+    cp = min(nodes) if nodes and min(nodes) > 0 else 24
+    # one queue per rank is HIP's own (null stream / internal copies)
+    return max(1, min(default, cp // per_gpu - 1))
+
+
 def _tensor(x, topo):
     dev = torch.device("cuda", topo.device) if topo.backend == "nccl" else torch.device("cpu")
     return torch.tensor([x], dtype=torch.float64, device=dev)

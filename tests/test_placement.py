@@ -101,3 +101,22 @@ print("ok", k)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code, root], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_hw_queues_per_rank_keeps_shared_gpus_within_the_queue_budget(monkeypatch):
+    """Ranks sharing a GPU split its mapped compute queues (num_cp_queues):
+    8 ranks on one 24-queue GPU get 2 each (+1 of HIP's own = 24); one rank
+    per GPU keeps HIP's default of 4."""
+    from brpc_amd.parallel import topology
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setattr(topology, "_kfd_gpu_nodes", lambda: [24])
+    assert topology.hw_queues_per_rank(1) == 4
+    assert topology.hw_queues_per_rank(2) == 4
+    assert topology.hw_queues_per_rank(4) == 4
+    assert topology.hw_queues_per_rank(8) == 2
+    assert topology.hw_queues_per_rank(16) == 1
+    monkeypatch.setattr(topology, "_kfd_gpu_nodes", lambda: [24] * 8)
+    assert topology.hw_queues_per_rank(8) == 4  # one rank per GPU
+    monkeypatch.setattr(topology, "_kfd_gpu_nodes", lambda: [])
+    assert topology.hw_queues_per_rank(8) == 4  # no KFD (CPU host): HIP's default
