@@ -95,10 +95,12 @@ def parse(argv=None):
     ap.add_argument("--cpu-l3-domain", type=int, default=-2,
                     help="confine the rank to the CPUs of this L3 domain (-2: auto, one domain per local rank "
                          "spread over the node; -1: no confinement)")
-    ap.add_argument("--dispatcher-poll-us", type=int, default=200,
+    ap.add_argument("--dispatcher-poll-us", type=int, default=-1,
                     help="event dispatcher busy-polls epoll for this long after the last event before "
                          "sleeping (-event_dispatcher_spin_us; 0: always sleep in epoll_wait). The GPU "
-                         "event poller and the RCCL plane poster watch for work as long before sleeping.")
+                         "event poller and the RCCL plane poster watch for work as long before sleeping. "
+                         "-1 (auto): 200, or 0 when the rank's share of the CPU quota is under 4 CPUs (ranks "
+                         "crowded onto one box: every spinning thread takes a CPU the workers need)")
     ap.add_argument("--latency-first", action="store_true",
                     help="take the 100-QPS latency sample before the throughput legs")
     ap.add_argument("--no-latency-replace", action="store_true",
@@ -383,6 +385,8 @@ def main(argv=None):
     # after the last event, then sleep. Under load that removes the kernel
     # wake-up from every hop; at 100 QPS they sleep between requests, and
     # the JSON reports the rank's CPU% during that sample.
+    if a.dispatcher_poll_us < 0:
+        a.dispatcher_poll_us = 200 if cpu_quota() // max(1, topo.local_world_size) >= 4 else 0
     native.set_flag("event_dispatcher_spin_us", str(max(0, a.dispatcher_poll_us)))
     native.set_flag("gpu_poller_idle_spin_us", str(max(0, a.dispatcher_poll_us)))
     native.set_flag("rccl_idle_spin_us", str(max(0, a.dispatcher_poll_us)))

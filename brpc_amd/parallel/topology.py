@@ -61,8 +61,10 @@ def init_distributed(prefer_gpu=True):
 
 
 def _kfd_gpu_nodes():
-    """(simd_count, num_cp_queues) of every GPU node in the KFD topology,
-    read from sysfs: no HIP call, so it can run before the runtime starts."""
+    """num_cp_queues of every GPU this process can open, from the KFD
+    topology in sysfs: no HIP call, so it can run before the runtime starts.
+    A container sees every GPU of the host in the topology but can open only
+    its own render nodes (/dev/dri/renderD<drm_render_minor>)."""
     import glob
     out = []
     for path in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")):
@@ -74,8 +76,12 @@ def _kfd_gpu_nodes():
                     props[k] = v
         except OSError:
             continue
-        if int(props.get("simd_count", "0") or 0) > 0:
-            out.append(int(props.get("num_cp_queues", "0") or 0))
+        if int(props.get("simd_count", "0") or 0) <= 0:
+            continue
+        minor = props.get("drm_render_minor")
+        if minor is not None and not os.access("/dev/dri/renderD%s" % minor, os.R_OK | os.W_OK):
+            continue
+        out.append(int(props.get("num_cp_queues", "0") or 0))
     return out
 
 
