@@ -69,6 +69,81 @@ std::string fmt_time(int64_t real_us) {
     return buf;
 }
 
+std::string html_escape(const std::string& in) {
+    std::string out;
+    out.reserve(in.size());
+    for (char c : in) {
+        switch (c) {
+        case '<': out += "&lt;"; break;
+        case '>': out += "&gt;"; break;
+        case '&': out += "&amp;"; break;
+        case '"': out += "&quot;"; break;
+        default: out += c;
+        }
+    }
+    return out;
+}
+
+// Values of a series_json() array ("[[i,v],[i,v],...]"), in order.
+std::vector<double> series_values(const std::string& json) {
+    std::vector<double> v;
+    const char* p = json.c_str();
+    while ((p = strchr(p, '[')) != nullptr) {
+        ++p;
+        if (*p == '[') continue;  // the outer bracket
+        const char* comma = strchr(p, ',');
+        if (!comma) break;
+        char* end = nullptr;
+        const double x = strtod(comma + 1, &end);
+        if (end == comma + 1) break;
+        v.push_back(x);
+        p = end;
+    }
+    return v;
+}
+
+// The series as an inline SVG line chart (no scripts, no downloads: the
+// role of the reference's flot views, builtin/vars_service.cpp:40-75 and
+// flot_min_js.cpp): the newest sample on the right, min/max/last labelled.
+std::string svg_chart(const std::vector<double>& v, int w, int h, bool labels) {
+    std::ostringstream os;
+    os << "<svg xmlns=\"http://www.w3.org/2000/svg\" width=\"" << w << "\" height=\"" << h << "\" viewBox=\"0 0 "
+       << w << " " << h << "\"><rect width=\"" << w << "\" height=\"" << h << "\" fill=\"#f8f8f8\" stroke=\"#ccc\"/>";
+    if (v.size() >= 2) {
+        double lo = v[0], hi = v[0];
+        for (double x : v) {
+            lo = std::min(lo, x);
+            hi = std::max(hi, x);
+        }
+        const double span = hi > lo ? hi - lo : 1.0;
+        const int pad = labels ? 16 : 2;
+        os << "<polyline fill=\"none\" stroke=\"#1f77b4\" stroke-width=\"1.5\" points=\"";
+        for (size_t i = 0; i < v.size(); ++i) {
+            const double x = pad + (double)(w - 2 * pad) * i / (v.size() - 1);
+            const double y = (h - pad) - (double)(h - 2 * pad) * (v[i] - lo) / span;
+            os << (i ? " " : "") << (int)x << "," << (int)y;
+        }
+        os << "\"/>";
+        if (labels) {
+            os << "<text x=\"2\" y=\"12\" font-size=\"11\">max " << hi << "</text>"
+               << "<text x=\"2\" y=\"" << h - 3 << "\" font-size=\"11\">min " << lo << "</text>"
+               << "<text x=\"" << w - 120 << "\" y=\"12\" font-size=\"11\">last " << v.back() << "</text>";
+        }
+    } else {
+        os << "<text x=\"4\" y=\"" << h / 2 << "\" font-size=\"11\">no samples yet</text>";
+    }
+    os << "</svg>";
+    return os.str();
+}
+
+void html(Controller* cntl, const std::string& title, const std::string& body) {
+    cntl->http_response().set_content_type("text/html; charset=utf-8");
+    cntl->response_attachment().append("<!DOCTYPE html><html><head><meta charset=\"utf-8\"><title>" + html_escape(title) +
+                                       "</title><style>body{font-family:monospace} td{padding:2px 8px;"
+                                       "vertical-align:top} tr:nth-child(even){background:#f4f4f4}</style></head>"
+                                       "<body>" + body + "</body></html>\n");
+}
+
 // ------------------------------------------------------------------ pages
 class IndexImpl : public index {
 public:
@@ -116,6 +191,20 @@ public:
         os << "concurrency: " << s->concurrency() << " (max " << s->max_concurrency() << ")\n\n";
         std::vector<const Server::MethodProperty*> mps;
         s->ListMethodProperties(&mps);
+        if (query(cntl, "html")) {
+            // the same, as a page: server facts, then one row per method
+            std::ostringstream h;
+            h << "<h3>" << html_escape(s->listen_address().to_string()) << "</h3><pre>" << html_escape(os.str()) << "</pre>"
+              << "<table><tr><th>method</th><th>status</th></tr>";
+            for (auto* mp : mps) {
+                if (mp->is_builtin_service) continue;
+                h << "<tr><td>" << html_escape(mp->method->full_name) << "</td><td><pre>"
+                  << html_escape(mp->status ? mp->status->Describe() : std::string()) << "</pre></td></tr>";
+            }
+            h << "</table><p><a href=\"/vars?html\">/vars</a> <a href=\"/\">index</a></p>";
+            html(cntl, "status", h.str());
+            return;
+        }
         for (auto* mp : mps) {
             if (mp->is_builtin_service) continue;
             os << mp->method->full_name << "\n";
@@ -132,6 +221,39 @@ public:
         Controller* cntl = C(c);
         const std::string& name = unresolved(cntl);
         std::ostringstream os;
+        if (!name.empty() && name.find_first_of("*?;") == std::string::npos && query(cntl, "chart")) {
+            // one variable's series as a chart page
+            if (var::Variable::describe_exposed(name, os) != 0) {
+                cntl->SetFailed(ENOMETHOD, "no variable named `%s'", name.c_str());
+                return;
+            }
+            const std::vector<double> v = series_values(var::Variable::series_exposed(name));
+            html(cntl, name,
+                 "<h3>" + html_escape(name) + " = " + html_escape(os.str()) + "</h3>" + svg_chart(v, 720, 240, true) +
+                     "<p>" + std::to_string(v.size()) + " samples, oldest on the left. <a href=\"/vars/" +
+                     html_escape(name) + "?series\">raw series</a> <a href=\"/vars?html\">all vars</a></p>");
+            return;
+        }
+        if (query(cntl, "html")) {
+            // every variable; those with a series get a sparkline linking to
+            // their chart page
+            std::vector<std::pair<std::string, std::string>> out;
+            var::Variable::dump_exposed(&out, name);
+            std::ostringstream h;
+            h << "<table><tr><th>name</th><th>value</th><th>trend</th></tr>";
+            for (auto& kv : out) {
+                const std::vector<double> v = series_values(var::Variable::series_exposed(kv.first));
+                h << "<tr><td>" << html_escape(kv.first) << "</td><td>" << html_escape(kv.second) << "</td><td>";
+                if (!v.empty()) {
+                    h << "<a href=\"/vars/" << html_escape(kv.first) << "?chart\">" << svg_chart(v, 160, 28, false)
+                      << "</a>";
+                }
+                h << "</td></tr>";
+            }
+            h << "</table>";
+            html(cntl, "vars", h.str());
+            return;
+        }
         if (!name.empty() && name.find_first_of("*?;") == std::string::npos) {
             if (query(cntl, "series")) {
                 os << var::Variable::series_exposed(name);

@@ -156,6 +156,9 @@ struct TaskMeta {
     // set by other threads (stop/interrupt), read by the fiber's worker
     std::atomic<bool> stop{false};
     std::atomic<bool> interrupted{false};
+    // the worker pthread running this fiber right now (0 while it is not
+    // running): interrupt() sends it SIGURG so a blocking syscall returns
+    std::atomic<pthread_t> running_on{0};
     bool is_main = false;
     std::atomic<int>* version_butex = nullptr;  // current version of this slot
     fiber_t tid = 0;

@@ -27,6 +27,7 @@
 #include "fiber/context.h"
 
 #include "fiber/internal.h"
+#include "fiber/interrupt_pthread.h"
 #include "fiber/key_internal.h"
 #include "fiber/timer.h"
 
@@ -330,6 +331,8 @@ void TaskGroup::sched_to_impl(TaskGroup** pg, TaskMeta* next, bool handover) {
     if (next != cur) {
         g->_nswitch.store(g->_nswitch.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
         g->_cur_meta = next;
+        cur->running_on.store(0, std::memory_order_relaxed);
+        next->running_on.store(pthread_self(), std::memory_order_release);
         if (!handover) {
             void* fake_stack = nullptr;
             (void)fake_stack;
@@ -524,7 +527,13 @@ int TaskGroup::interrupt(fiber_t tid, TaskControl* c) {
     uint64_t sleep_id = m->current_sleep.exchange(0, std::memory_order_seq_cst);
     if (sleep_id) {
         if (get_global_timer_thread()->unschedule(sleep_id) == 0) ready_to_run_general(tid);
+        return 0;
     }
+    // neither parked nor sleeping: running on a worker, maybe blocked in a
+    // system call the runtime cannot see — SIGURG makes that call return
+    // EINTR (interrupt_pthread.h); the fiber sees `interrupted` afterwards
+    const pthread_t th = m->running_on.load(std::memory_order_acquire);
+    if (th && !pthread_equal(th, pthread_self()) && !m->is_main) interrupt_pthread(th);
     (void)c;
     return 0;
 }
@@ -1055,6 +1064,9 @@ void TaskControl::stop_and_join() {
         _stop = true;
     }
     for (int i = 0; i < kParkingLots; ++i) _pl[i].stop();
+    // workers blocked in a system call of user code: EINTR, so they reach
+    // the stop check (reference task_control.cpp:244-247)
+    for (pthread_t t : _workers) interrupt_pthread(t);
     for (pthread_t t : _workers) pthread_join(t, nullptr);
 }
 

@@ -3,11 +3,16 @@
 // services, concurrency limiters, every protocol, the client-side response
 // handlers, and the runtime metrics.
 #include <signal.h>
+#include <sys/stat.h>
 
+#include <algorithm>
+#include <fstream>
 #include <mutex>
 
 #include "base/buf.h"
+#include "base/flags.h"
 #include "base/logging.h"
+#include "base/time.h"
 #include "cluster/load_balancer.h"
 #include "cluster/naming_service.h"
 #include "fiber/fiber.h"
@@ -18,9 +23,16 @@
 #include "rpc/compress.h"
 #include "rpc/concurrency_limiter.h"
 #include "rpc/errno.h"
+#include "rpc/periodic_task.h"
 #include "rpc/protocol.h"
+#include "rpc/server.h"
 #include "rpc/stream_internal.h"
 #include "var/var.h"
+
+DEFINE_string(dummy_server_port_file, "dummy_server.port",
+              "while no server runs in the process, creating (or touching) this file with a port number in it "
+              "starts a server of builtin services on that port (reference global.cpp DUMMY_SERVER_PORT_FILE)");
+DEFINE_int32(dummy_server_watch_ms, 1000, "how often the dummy server port file is checked");
 
 namespace mrpc {
 
@@ -46,6 +58,53 @@ static void expose_runtime_vars() {
     new var::PassiveStatus<int64_t>("buf_block_memory", [] { return Buf::block_memory(); });
     new var::PassiveStatus<int64_t>("socket_count", [] { return Socket::nsocket(); });
     new var::PassiveStatus<int64_t>("contention_count", [] { return fiber::ContentionCount(); });
+}
+
+namespace {
+// The dummy_server.port watcher (reference global.cpp:117,226-254 with
+// butil::FileWatcher::init_from_not_exist): a file that appears, or whose
+// modification time changes, is read once; its first integer is the port.
+class GlobalUpdate : public PeriodicTask {
+public:
+    bool OnTriggeringTask(timespec* next) override {
+        check();
+        *next = realtime_after_us((int64_t)std::max(10, FLAGS_dummy_server_watch_ms) * 1000);
+        return true;
+    }
+    void OnDestroyingTask() override { delete this; }
+
+private:
+    void check() {
+        struct stat st;
+        const std::string path = FLAGS_dummy_server_port_file;
+        if (path.empty() || stat(path.c_str(), &st) != 0) {
+            _seen = false;  // gone: a later creation counts again
+            return;
+        }
+        const int64_t mtime = (int64_t)st.st_mtim.tv_sec * 1000000000LL + st.st_mtim.tv_nsec;
+        if (_seen && mtime == _mtime) return;
+        if (IsDummyServerRunning() || RunningServerCount() > 0) return;  // consumed only when it can act
+        _seen = true;
+        _mtime = mtime;
+        std::ifstream in(path);
+        long port = -1;
+        if (!(in >> port) || port < 0 || port > 65535) {
+            LOG(WARNING) << "ignore " << path << ": no port in it";
+            return;
+        }
+        if (StartDummyServerAt((int)port) == 0) {
+            LOG(INFO) << "dummy server started on port " << port << " (" << path << ")";
+        } else {
+            LOG(WARNING) << "fail to start the dummy server on port " << port;
+        }
+    }
+    bool _seen = false;
+    int64_t _mtime = 0;
+};
+}  // namespace
+
+void StartGlobalUpdate() {
+    PeriodicTaskManager::StartTaskAt(new GlobalUpdate, realtime_after_us(1000));
 }
 
 void GlobalInitializeOrDie() {
@@ -88,6 +147,7 @@ void GlobalInitializeOrDie() {
         var::ExposeDefaultVariables();
         expose_runtime_vars();
         fiber::init_runtime();
+        StartGlobalUpdate();
     });
 }
 

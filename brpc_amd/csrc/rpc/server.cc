@@ -617,14 +617,29 @@ void* Controller::session_local_data() {
     return _session_local_data;
 }
 
+namespace {
+std::mutex g_dummy_mu;
+Server* g_dummy = nullptr;
+}  // namespace
+
 int StartDummyServerAt(int port) {
-    static Server* dummy = nullptr;
-    static std::mutex mu;
-    std::lock_guard<std::mutex> g(mu);
-    if (dummy) return -1;
-    dummy = new Server;
+    std::lock_guard<std::mutex> g(g_dummy_mu);
+    if (g_dummy) return -1;
+    Server* s = new Server;
     ServerOptions opt;
-    return dummy->Start(port, &opt);
+    if (s->Start(port, &opt) != 0) {
+        delete s;
+        return -1;
+    }
+    g_dummy = s;
+    return 0;
 }
+
+bool IsDummyServerRunning() {
+    std::lock_guard<std::mutex> g(g_dummy_mu);
+    return g_dummy != nullptr;
+}
+
+int RunningServerCount() { return g_running_servers.load(std::memory_order_relaxed); }
 
 }  // namespace mrpc

@@ -191,5 +191,13 @@ void SetAddBuiltinServicesHook(AddBuiltinServicesFn fn);
 
 // Start a server hosting only builtin services (tools, dummy server).
 int StartDummyServerAt(int port);
+bool IsDummyServerRunning();
+// Servers of this process that are running (var `rpc_server_count`).
+int RunningServerCount();
+// The housekeeping task every process with a channel or server runs (role of
+// the reference's GlobalUpdate, src/brpc/global.cpp:223-260): once a second,
+// while no server runs, a new or changed -dummy_server_port_file starts a
+// builtin-only server on the port it holds. Started by GlobalInitializeOrDie.
+void StartGlobalUpdate();
 
 }  // namespace mrpc

@@ -16,6 +16,8 @@
 #include "rpc/span.h"
 #include "services/echo_service.h"
 #include "tests/test.h"
+#include "var/var.h"
+#include <unistd.h>
 
 using namespace mrpc;
 
@@ -301,4 +303,34 @@ TEST(BuiltinPages, memory_and_gpu_pages_answer) {
     EXPECT_EQ(code, 0);
     s.get("/gpu", &code);  // no device here: the page still answers
     EXPECT_EQ(code, 0);
+}
+
+// Chart views (role of the reference's flot pages, builtin/vars_service.cpp
+// :40-75): a windowed variable's series as an inline SVG line, sparklines
+// on the HTML variable list, and an HTML /status.
+TEST(BuiltinPages, vars_series_chart_and_html_views) {
+    Site s;
+    var::Adder<int64_t> a;
+    var::PerSecond<var::Adder<int64_t>> ps("builtin_chart_per_second", &a, 10);
+    for (int i = 0; i < 3; ++i) {
+        a << (i + 1) * 100;
+        usleep(1100 * 1000);  // the sampler takes one point a second
+    }
+    int code = -1, status = 0;
+    const std::string page = s.get("/vars/builtin_chart_per_second?chart", &code, &status);
+    EXPECT_EQ(code, 0);
+    EXPECT_TRUE(has(page, "<svg"));
+    EXPECT_TRUE(has(page, "<polyline"));
+    EXPECT_TRUE(has(page, "builtin_chart_per_second"));
+    const std::string list = s.get("/vars/builtin_chart_*?html");
+    EXPECT_TRUE(has(list, "<table>"));
+    EXPECT_TRUE(has(list, "href=\"/vars/builtin_chart_per_second?chart\""));
+    s.get("/vars/not_a_var_at_all?chart", &code);
+    EXPECT_EQ(code, ENOMETHOD);
+    const std::string st = s.get("/status?html", &code);
+    EXPECT_EQ(code, 0);
+    EXPECT_TRUE(has(st, "<table>"));
+    EXPECT_TRUE(has(st, "example.EchoService.Echo"));
+    // the plain views are unchanged
+    EXPECT_FALSE(has(s.get("/status"), "<table>"));
 }

@@ -17,6 +17,7 @@
 #include "base/time.h"
 #include "fiber/butex.h"
 #include "fiber/fiber.h"
+#include "fiber/interrupt_pthread.h"
 #include "tests/test.h"
 
 using namespace mrpc;
@@ -328,4 +329,78 @@ TEST(FiberDepth, parked_workers_never_miss_a_signal) {
     }
     for (auto& t : th) pthread_join(t, nullptr);
     EXPECT_EQ(failures.load(), 0);
+}
+
+// interrupt_pthread (reference src/bthread/interrupt_pthread.cpp): a fiber
+// blocked in a system call on its worker — invisible to the runtime, no
+// butex or timer to cancel — gets EINTR from fiber::interrupt().
+namespace {
+struct BlockedRead {
+    int fd = -1;
+    std::atomic<int> started{0};
+    std::atomic<int> result{0};
+    std::atomic<int> err{0};
+};
+void* blocking_read(void* arg) {
+    BlockedRead* b = static_cast<BlockedRead*>(arg);
+    b->started.store(1);
+    char c;
+    const ssize_t n = ::read(b->fd, &c, 1);  // blocks the worker pthread
+    b->err.store(n < 0 ? errno : 0);
+    b->result.store(n < 0 ? -1 : 2);
+    return nullptr;
+}
+}  // namespace
+
+TEST(FiberDepth, interrupt_wakes_a_fiber_blocked_in_a_syscall) {
+    int p[2];
+    ASSERT_EQ(pipe(p), 0);
+    BlockedRead b;
+    b.fd = p[0];
+    fiber::fiber_t t = 0;
+    ASSERT_EQ(fiber::start_background(&t, nullptr, blocking_read, &b), 0);
+    for (int i = 0; i < 2000 && !b.started.load(); ++i) ::usleep(1000);
+    ASSERT_EQ(b.started.load(), 1);
+    ::usleep(20000);  // let it enter read()
+    EXPECT_EQ(b.result.load(), 0);
+    const long before = fiber::interrupt_pthread_signals();
+    ASSERT_EQ(fiber::interrupt(t), 0);
+    for (int i = 0; i < 2000 && b.result.load() == 0; ++i) ::usleep(1000);
+    EXPECT_EQ(b.result.load(), -1);
+    EXPECT_EQ(b.err.load(), EINTR);
+    EXPECT_GT(fiber::interrupt_pthread_signals(), before);
+    fiber::join(t, nullptr);
+    close(p[0]);
+    close(p[1]);
+}
+
+TEST(FiberDepth, interrupt_pthread_breaks_a_plain_blocking_call) {
+    int p[2];
+    ASSERT_EQ(pipe(p), 0);
+    std::atomic<int> err{0};
+    std::atomic<int> in{0};
+    pthread_t th;
+    struct Args {
+        int fd;
+        std::atomic<int>* err;
+        std::atomic<int>* in;
+    } a{p[0], &err, &in};
+    ASSERT_EQ(pthread_create(&th, nullptr,
+                             [](void* x) -> void* {
+                                 Args* a = static_cast<Args*>(x);
+                                 a->in->store(1);
+                                 char c;
+                                 const ssize_t n = ::read(a->fd, &c, 1);
+                                 a->err->store(n < 0 ? errno : -1);
+                                 return nullptr;
+                             },
+                             &a),
+              0);
+    for (int i = 0; i < 2000 && !in.load(); ++i) ::usleep(1000);
+    ::usleep(20000);
+    ASSERT_EQ(fiber::interrupt_pthread(th), 0);
+    pthread_join(th, nullptr);
+    EXPECT_EQ(err.load(), EINTR);
+    close(p[0]);
+    close(p[1]);
 }

@@ -5,6 +5,7 @@ fetching many urls concurrently."""
 import os
 import socket
 import subprocess
+import sys
 import time
 import urllib.request
 
@@ -148,3 +149,44 @@ def test_rpcz_pages_by_trace_and_time(procs, tmp_path):
     stamp = time.strftime("%Y/%m/%d-%H:%M:%S", time.localtime(time.time() + 5))
     _, by_date = _get("http://127.0.0.1:%d/rpcz?time=%s&max=500" % (port, stamp))
     assert sum(1 for l in by_date.splitlines() if l.startswith("S ")) == 25
+
+
+_DUMMY_SCRIPT = r"""
+import os, sys, time, urllib.request
+sys.path.insert(0, sys.argv[1])
+from brpc_amd import native
+path, port = sys.argv[2], int(sys.argv[3])
+native.set_flag("dummy_server_port_file", path)
+native.set_flag("dummy_server_watch_ms", "50")
+native.global_init()  # what every channel / server does first
+time.sleep(0.3)
+def health():
+    try:
+        return urllib.request.urlopen("http://127.0.0.1:%d/health" % port, timeout=1).read()
+    except OSError:
+        return None
+assert health() is None  # no file yet, no server
+with open(path, "w") as f:
+    f.write("%d\n" % port)
+for _ in range(100):
+    if health():
+        break
+    time.sleep(0.05)
+print("HEALTH", health())
+"""
+
+
+def test_dummy_server_port_file_starts_builtin_server(tmp_path):
+    """The dummy_server.port watcher (reference src/brpc/global.cpp:223-260):
+    while no server runs in the process, writing a port into the watched file
+    starts a server of builtin services on it."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    path = str(tmp_path / "dummy_server.port")
+    r = subprocess.run([sys.executable, "-c", _DUMMY_SCRIPT, ROOT, path, str(port)], capture_output=True, text=True,
+                       timeout=120, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "HEALTH b'OK\\n'" in r.stdout, (r.stdout, r.stderr[-2000:])
