@@ -109,7 +109,7 @@ int key_create2(FiberKey*key, void (*dtor)(void*, const void*), const void* dtor
         idx = r.next++;
     }
     KeyInfo& ki = r.infos[idx];
-    ki.used = true;
+    __atomic_store_n(&ki.used, true, __ATOMIC_RELEASE);  // read lock-free by setspecific
     ki.dtor = dtor;
     ki.dtor_arg = dtor_arg;
     *key = ((uint64_t)idx << 32) | ki.version;
@@ -125,10 +125,11 @@ int key_delete(FiberKey key) {
     std::lock_guard<std::mutex> g(r.mu);
     uint32_t idx = key_index(key);
     if (idx >= kMaxKeys || !r.infos[idx].used || r.infos[idx].version != key_version(key)) return EINVAL;
-    r.infos[idx].used = false;
+    __atomic_store_n(&r.infos[idx].used, false, __ATOMIC_RELEASE);
     r.infos[idx].dtor = nullptr;
-    ++r.infos[idx].version;
-    if (r.infos[idx].version == 0) r.infos[idx].version = 1;
+    uint32_t v = r.infos[idx].version + 1;
+    if (v == 0) v = 1;
+    __atomic_store_n(&r.infos[idx].version, v, __ATOMIC_RELEASE);
     r.free_idx.push_back(idx);
     return 0;
 }
@@ -153,6 +154,16 @@ static KeyTable** current_table_slot() {
 }
 
 int setspecific(FiberKey key, void* data) {
+    // a key that was never created, or was deleted (its slot's version moved
+    // on), is refused like the reference's bthread_setspecific (EINVAL)
+    {
+        KeyRegistry& r = registry();
+        const uint32_t idx = key_index(key);
+        if (idx >= kMaxKeys || !__atomic_load_n(&r.infos[idx].used, __ATOMIC_ACQUIRE) ||
+            __atomic_load_n(&r.infos[idx].version, __ATOMIC_ACQUIRE) != key_version(key)) {
+            return EINVAL;
+        }
+    }
     KeyTable** slot = current_table_slot();
     if (!*slot) {
         TaskGroup* g = tls_group();
