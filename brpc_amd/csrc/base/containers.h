@@ -283,7 +283,7 @@ private:
         tls.v.emplace_back(this, w);
         return w.get();
     }
-    T _data[2];
+    T _data[2]{};  // value-initialized: scalar T starts at zero in both copies
     std::atomic<int> _index;
     std::mutex _modify_mu;
     std::mutex _wrappers_mu;
