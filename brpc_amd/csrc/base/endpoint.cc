@@ -134,7 +134,13 @@ int hostname2endpoint(const char* host_and_port, EndPoint* ep) {
     if (str2endpoint(host_and_port, ep) == 0) return 0;
     const char* colon = strrchr(host_and_port, ':');
     std::string host = colon ? std::string(host_and_port, colon - host_and_port) : std::string(host_and_port);
-    int port = colon ? atoi(colon + 1) : 80;
+    int port = 80;
+    if (colon) {
+        char* end = nullptr;
+        const long p = strtol(colon + 1, &end, 10);
+        if (end == colon + 1 || (*end && *end != ' ') || p < 0 || p > 65535) return -1;
+        port = (int)p;
+    }
     addrinfo hints;
     memset(&hints, 0, sizeof(hints));
     hints.ai_family = AF_UNSPEC;  // an A record first, else AAAA
