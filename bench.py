@@ -346,6 +346,13 @@ def main(argv=None):
     if a.fail_rank >= 0 and int(os.environ.get("RANK", "0")) == a.fail_rank:
         print("bench: --fail-rank %d: exiting" % a.fail_rank, file=sys.stderr, flush=True)
         return 3
+    # The JSON line is the only thing this process may print on stdout:
+    # libraries write there too (RCCL's version banner on its first
+    # communicator), so fd 1 becomes stderr and the line goes to a private
+    # duplicate of the original stdout.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     # Several ranks on one GPU (a rehearsal on a smaller box): keep the
     # hardware queues of all of them within what the GPU maps at once. Set
     # before the HIP runtime starts (the first torch.cuda call).
@@ -419,7 +426,7 @@ def main(argv=None):
                 if incomplete:
                     out["incomplete"] = True
                     out["hung_leg"] = hung_leg
-                print(json.dumps(out), flush=True)
+                print(json.dumps(out), file=json_out, flush=True)
 
     dog = Watchdog(a.hard_deadline_s, emit)
     dog.start()

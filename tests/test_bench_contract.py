@@ -24,6 +24,8 @@ def test_bench_single_rank():
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
+    # nothing but the JSON line on stdout (library banners go to stderr)
+    assert r.stdout.strip().splitlines() == [r.stdout.strip()], r.stdout[:500]
     j = lines[0]
     assert KEYS <= set(j)
     assert j["n_gpus"] == 1 and j["steps"] == 3 and j["value"] > 0 and j["errors"] == 0
