@@ -216,9 +216,13 @@ CountdownEvent::CountdownEvent(int initial) : _b(butex_create()) { _b->store(ini
 CountdownEvent::~CountdownEvent() { butex_destroy(_b); }
 
 void CountdownEvent::signal(int n) {
-    // Keep the value a valid int while waking
-    const int prev = _b->fetch_sub(n, std::memory_order_release);
-    if (prev <= n) butex_wake_all(_b);
+    // The decrement can release a waiter that destroys this event at once:
+    // read the butex pointer first, never a member after the fetch_sub (the
+    // butex itself is pooled, so a late wake on a recycled one is only a
+    // spurious wake-up, as with bthread's countdown event).
+    std::atomic<int>* const b = _b;
+    const int prev = b->fetch_sub(n, std::memory_order_release);
+    if (prev <= n) butex_wake_all(b);
 }
 
 void CountdownEvent::add_count(int n) { _b->fetch_add(n, std::memory_order_release); }

@@ -258,6 +258,7 @@ TEST(ExecutionQueueMore, queue_outlives_its_owner_until_the_work_is_done) {
     gate.unlock();
     for (int i = 0; i < 2000 && !weak.expired(); ++i) ::usleep(1000);
     EXPECT_TRUE(weak.expired());
+    std::lock_guard<std::mutex> g(s.mu);  // expired() is a relaxed load: no ordering with the consumer's writes
     EXPECT_EQ(s.v.size(), 50u);
 }
 
