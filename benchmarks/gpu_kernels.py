@@ -50,10 +50,20 @@ def main():
                               "GBps": tot / t / 1e9}))
         dst = torch.empty_like(buf)
         from brpc_amd.ops import batched_copy_crc32c
-        ok = int(batched_copy_crc32c([small], [dst[: small.numel()]])[0]) == crc32c_host(small.cpu().numpy().tobytes())
-        t = timeit(lambda: batched_copy_crc32c([buf], [dst]))
-        print(json.dumps({"kernel": "copy_crc32c_fused", "bytes": n, "sec": t, "GBps_read": n / t / 1e9,
-                          "GBps_rw": 2 * n / t / 1e9, "verified": ok}))
+        for mfma, name in ((True, "copy_crc32c_fused"), (False, "copy_crc32c_fused_table")):
+            ok = int(batched_copy_crc32c([small], [dst[: small.numel()]], mfma=mfma)[0]) == crc32c_host(
+                small.cpu().numpy().tobytes())
+            t = timeit(lambda: batched_copy_crc32c([buf], [dst], mfma=mfma))
+            print(json.dumps({"kernel": name, "bytes": n, "sec": t, "GBps_read": n / t / 1e9,
+                              "GBps_rw": 2 * n / t / 1e9, "verified": ok}))
+            # the verified pull's launch shapes: 32 x 1 MiB and 32 x 64 KiB
+            for seg in (1 << 20, 65536):
+                k = min(32, n // seg)
+                ss = [buf[i * seg:(i + 1) * seg] for i in range(k)]
+                dd = [dst[i * seg:(i + 1) * seg] for i in range(k)]
+                t = timeit(lambda: batched_copy_crc32c(ss, dd, mfma=mfma))
+                print(json.dumps({"kernel": "%s_%dx%dKiB" % (name, k, seg >> 10), "bytes": k * seg, "sec": t,
+                                  "GBps_read": k * seg / t / 1e9}))
         # the transport's per-tick pull: 64 x 64 KiB payloads in one launch set
         nb = min(64, n // 65536)
         pulls_s = [buf[i * 65536:(i + 1) * 65536] for i in range(nb)]

@@ -170,11 +170,8 @@ def main():
                 torch.cuda.synchronize()
                 t = stamps.cpu().tolist()
                 # shader-clock cycles per phase of block 0
-                names = (("stage", "cand_len", "chain", "emit") if native.get_flag("gpu_snappy_compress_pj") == "true"
-                         else ("stage", "first_pos", "match", "write"))
+                names = ("stage", "first_pos", "match", "write")
                 phases = {k: t[i + 1] - t[i] for i, k in enumerate(names)}
-                if names[1] == "cand_len":
-                    phases["doubling_rounds"] = t[5]
                 print(json.dumps({"kernel": "snappy_compress", "body": kind, "flags": a.flag, "src": src_at, "dst": dst_at,
                                   "block0_phase_cycles": phases,
                                   "blocks": npieces, "bytes_in": total,

@@ -622,11 +622,13 @@ ssize_t BufPortal::append_from_fd(int fd, size_t max_count) {
     BufBlock* blocks[kMaxIov];
     int nb = 0;
     size_t space = 0;
+    // at most max_count bytes per call (the last region is cut short), as
+    // IOPortal::append_from_file_descriptor: callers bound one read with it
     if (_pending && !_pending->full()) {
         blocks[nb] = _pending;
         iov[nb].iov_base = _pending->data + _pending->size;
-        iov[nb].iov_len = _pending->left();
-        space += _pending->left();
+        iov[nb].iov_len = std::min<size_t>(_pending->left(), max_count);
+        space += iov[nb].iov_len;
         ++nb;
     } else if (_pending) {
         _pending->dec_ref();
@@ -637,8 +639,8 @@ ssize_t BufPortal::append_from_fd(int fd, size_t max_count) {
         if (!b) break;
         blocks[nb] = b;  // we own one ref
         iov[nb].iov_base = b->data;
-        iov[nb].iov_len = b->cap;
-        space += b->cap;
+        iov[nb].iov_len = std::min<size_t>(b->cap, max_count - space);
+        space += iov[nb].iov_len;
         ++nb;
     }
     ssize_t nr = ::readv(fd, iov, nb);

@@ -23,14 +23,6 @@ DEFINE_bool(codec_fused_scan_in_kernel, false,
             "(else the pb scan is a second launch). Off: the hand-off needs a device-scope fence per piece, "
             "which on gfx950 compiles to buffer_wbl2 + buffer_inv (an L2 write-back of the XCD) in every wave; "
             "in the RPC leg, with batches overlapping, that made the one-launch kernels 1.5-4x slower per launch");
-DEFINE_bool(gpu_snappy_compress_pj, false,
-            "snappy blocks up to 4 KiB compress with the data-parallel parse (every position's candidate and "
-            "match length at once, the greedy element chain by speculative slice walks; snappy_kernels.hip "
-            "compress_wave_pj) instead of per-lane slices whose matches stop at the slice end: ratio 2.14 vs "
-            "1.96 on 2 KiB text blocks, but 47 vs 28 us per launch, so off");
-DEFINE_string(codec_fused_kernel, "waves",
-              "kernel of the one-launch codec batch: 'waves' (one wave per block/piece, snappy_kernels.hip) or "
-              "'workgroup' (one 1024-thread workgroup per block/piece, codec_fused.hip)");
 DEFINE_int32(codec_batch_max_inflight, 4,
              "codec batches in flight per device before the next one waits for a completion (0: no limit); "
              "while it waits, the requests that arrive join it, so a busy GPU gets fewer, larger batches "
@@ -298,7 +290,7 @@ bool launch(CBatch* b, int device) {
         fa.scan_n = b->scan_n.p;
         fa.max_fields = kCodecScanFields;
         fa.max_ulen = std::max(ncomp ? comp_max : 1u, nhpieces ? hpiece_max : 1u);
-        if (rc == 0) rc = FLAGS_codec_fused_kernel == "workgroup" ? LaunchFusedCodec(fa, s) : LaunchCodecWaves(fa, s);
+        if (rc == 0) rc = LaunchCodecWaves(fa, s);
         g_fused_launches.fetch_add(1, std::memory_order_relaxed);
         ncomp = nhpieces = 0;  // nothing left for the per-stage sequence below but (maybe) the scans
         if (scan_in_kernel) nscan = 0;

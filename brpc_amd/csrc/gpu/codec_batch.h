@@ -40,8 +40,8 @@ struct CodecRequest {
     // optional, per scan: the range of `pieces` that decode into its message.
     // When every scan of a batch names its pieces (and the batch holds only
     // compress jobs and pieces of <= kFusedMaxBlock), the batch is ONE fused
-    // launch (gpu/codec_fused.hip) and the scan runs as soon as the
-    // message's last piece is decoded.
+    // launch (codec_waves_kernel) and, with -codec_fused_scan_in_kernel,
+    // the scan runs as soon as the message's last piece is decoded.
     std::vector<uint32_t> scan_piece_first, scan_piece_count;
     // copies issued after the kernels (HBM -> pinned)
     std::vector<Segment> d2h;

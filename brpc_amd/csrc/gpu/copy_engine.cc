@@ -34,6 +34,8 @@ DEFINE_bool(copy_engine_done_words, false,
             "agent-scope release (an L2 write-back) halved 1 MiB pull bandwidth, and with the in-flight limit "
             "event completion is as fast (profiles/r6_xproc_diagnosis.txt)");
 
+DEFINE_bool(copy_engine_crc_mfma, true,
+            "verified pulls fold their CRC32C on the matrix cores (copy_crc32c_mfma_kernel); false: byte tables");
 DEFINE_int32(copy_engine_max_inflight, 4,
              "launches of one device's copy engine in flight at once (0: no limit). Submissions that find the "
              "limit reached join the open batch, which the first waiter of the next completed batch launches: "
@@ -202,7 +204,8 @@ void launch(Batch* b, int device) {
             b->crc_host = static_cast<uint32_t*>(PinnedAlloc(b->crc_cap * sizeof(uint32_t)));
         }
         if (!b->crc_host ||
-            LaunchBatchedCopyCrc32cMessages(b->segs.data(), b->msg_of.data(), (int)n, b->crc_host, s, done) != 0) {
+            LaunchBatchedCopyCrc32cMessages(b->segs.data(), b->msg_of.data(), (int)n, b->crc_host, s, done,
+                                            FLAGS_copy_engine_crc_mfma) != 0) {
             rc = -1;
         }
     } else if (rc == 0) {

@@ -1,6 +1,6 @@
 // Device-side protobuf wire walk shared by the gfx950 kernels that index
-// messages (pb_kernels.hip: the batched scans; codec_fused.hip: the scan a
-// fused codec launch runs once the last piece of a message is decoded).
+// messages (pb_kernels.hip: the batched scans; snappy_kernels.hip: the scan
+// a fused codec launch runs once the last piece of a message is decoded).
 #pragma once
 
 #include <hip/hip_runtime.h>

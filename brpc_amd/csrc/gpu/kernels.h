@@ -61,14 +61,16 @@ int LaunchBatchedCopy(const Segment* segs, int nseg, hipStream_t s, const DoneWo
 // (one read of the bytes; sources may be local/peer HBM or pinned host).
 // One launch per 32 segments and nothing else: no memset of `out`, which
 // may be pinned host memory read after the stream's event.
-int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s);
+// mfma: the CRC runs on the matrix cores (copy_crc32c_mfma_kernel, the
+// default), else on the byte-table kernel.
+int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s, bool mfma = true);
 // Same copy, but consecutive segments with equal msg_of[] (non-decreasing,
 // starting anywhere) form a MESSAGE and out[msg_of[i]] receives the CRC32C
 // of the message's bytes (its segments concatenated), folded on the device.
 // A message may have at most kInlineSegments segments (else -2, nothing
 // launched for it).
 int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s,
-                                    const DoneWord* done = nullptr);
+                                    const DoneWord* done = nullptr, bool mfma = true);
 
 // Packed-varint decode (protobuf wire type 0, packed repeated field):
 // `in` holds n bytes of concatenated varints; out receives the values
@@ -175,17 +177,12 @@ struct PbScanJob {
 int LaunchPbScanPtrs(const PbScanJob* jobs, int64_t n, uint32_t max_fields, uint64_t* fields, int32_t* nfields,
                      hipStream_t s);
 
-// Fused device-body codec launch (gpu/codec_fused.hip): ONE launch runs a
-// codec batch's compress blocks and headerless decode pieces, each at most
-// kFusedMaxBlock uncompressed bytes, one 256-thread workgroup per block or
-// piece, all concurrently; a message whose pieces all decoded is pb-scanned
-// by the workgroup that finished its last piece (no further launch).
-//  * compress: a block-wide parse — every position's match candidate and
-//    length in parallel, the greedy element chain found by speculative
-//    per-segment walks that are re-walked until their entries agree — into
-//    one raw snappy stream with its varint header (matches span the block);
-//  * decode: the element chain found the same way over the compressed
-//    bytes, then a source map resolved by pointer jumping.
+// Fused device-body codec launch (codec_waves_kernel, snappy_kernels.hip):
+// ONE launch runs a codec batch's compress blocks and headerless decode
+// pieces, each at most kFusedMaxBlock uncompressed bytes, one wave per block
+// or piece (the per-lane-segment compressor and the wave decoder); a
+// message's field table follows as a pb-scan launch, or (opt-in) the wave
+// that finished its last piece scans it.
 constexpr uint32_t kFusedMaxBlock = 8192;
 constexpr uint32_t kFusedNoGroup = 0xFFFFFFFFu;
 struct FusedCodecArgs {
@@ -204,13 +201,8 @@ struct FusedCodecArgs {
     int32_t* scan_n = nullptr;
     uint32_t max_fields = 0;
     uint32_t max_ulen = 0;                  // >= every block's and piece's size
-    uint32_t* stats = nullptr;  // optional, 4 device words: compress parse rounds (sum, max), decode (sum, max)
 };
-// The same batch as LaunchFusedCodec on one wave per block / piece (the
-// per-lane-segment compressor and the wave decoder of snappy_kernels.hip),
-// one launch; blocks and pieces up to kFusedMaxBlock.
 int LaunchCodecWaves(const FusedCodecArgs& a, hipStream_t s);
-int LaunchFusedCodec(const FusedCodecArgs& a, hipStream_t s);
 
 
 // Batched encoder of repeated numeric runs (SURVEY K2, and the number

@@ -366,6 +366,7 @@ typedef signed char i8x16 __attribute__((ext_vector_type(16)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kGroupBytes = 2048;                       // 32 columns x 64 B
+static_assert(kChunkBytes == 2 * kGroupBytes * (kThreads / 64), "copy_crc32c_mfma_kernel: 2 groups per wave");
 constexpr int kGroupsPerChunk = 32;
 constexpr uint64_t kMfmaChunk = (uint64_t)kGroupBytes * kGroupsPerChunk;  // 64 KiB per wave
 
@@ -490,6 +491,123 @@ __global__ void __launch_bounds__(kThreads) crc32c_mfma_kernel(
             atomicXor(out + seg, v);
         }
     }
+}
+
+// Fused pull + checksum with the CRC on the matrix cores: the batched
+// copy's 16 KiB end-aligned chunks (fill_batch / fold_chunk geometry, so the
+// message folding is shared with copy_crc32c_kernel), 4 KiB per wave, two
+// 2 KiB MFMA groups per wave. Lane (c, h) of a wave loads the 32 bytes
+// [64c + 32h, +32) of each group — exactly the B-fragment bytes of the MFMA
+// CRC — stores them to dst, and expands them into the 16 MFMAs of the group.
+// Each column's 64-byte CRC is shifted straight to the chunk end with one
+// multiply by x^(8*64*j), j = 64-byte blocks after it in the chunk (the
+// c_lane_shift table), so no Horner chain links the groups. The byte-table
+// kernel's per-lane serial table lookups ran at ~230 GB/s (3% of HBM) and
+// held the 1 MiB verified leg GPU-bound; the A fragments come from LDS,
+// staged once per workgroup, and a workgroup walks several chunks so the
+// staging amortises.
+__device__ __noinline__ void copy_bytes_slow(const uint8_t* base, uint8_t* dbase, int64_t lbeg, uint32_t* w) {
+    for (int i = 0; i < 8; ++i) w[i] = 0;
+    for (int b = 0; b < 32; ++b) {
+        const int64_t off = lbeg + b;
+        if (off >= 0) {
+            const uint8_t c = base[off];
+            if (dbase) dbase[off] = c;
+            w[b >> 2] |= (uint32_t)c << (8 * (b & 3));
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) copy_crc32c_mfma_kernel(SegBatch b, const CrcMfmaConsts* __restrict__ K,
+                                                                    uint32_t* __restrict__ scratch,
+                                                                    uint32_t* __restrict__ out, uint32_t nchunks) {
+    stamp_start(b);
+    __shared__ i8x16 sa[16][64];
+    __shared__ uint32_t wave_acc[kThreads / 64];
+    for (int i = threadIdx.x; i < 16 * 64; i += kThreads) (&sa[0][0])[i] = (&K->afrag[0][0])[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int c = lane & 31;
+    const int h = lane >> 5;
+    for (uint32_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+        const int seg = find_segment(b, chunk);
+        const uint64_t len = b.len[seg];
+        const uint8_t* base = static_cast<const uint8_t*>(b.src[seg]);
+        uint8_t* dbase = static_cast<uint8_t*>(b.dst[seg]);
+        const uint32_t seg_chunks = b.chunk_start[seg + 1] - b.chunk_start[seg];
+        const uint32_t k = chunk - b.chunk_start[seg];
+        const uint32_t after = seg_chunks - 1 - k;
+        const int64_t chunk_end = (int64_t)len - (int64_t)after * (int64_t)kChunkBytes;
+        const int64_t wave_end = chunk_end - (int64_t)(kThreads / 64 - 1 - wave) * 4096;
+        // both groups' loads first: 64 B per lane in flight, as in the copy kernel
+        uint32_t w[2][8];
+        bool any[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int64_t lbeg = wave_end - (int64_t)(2 - g) * 2048 + 64 * c + 32 * h;
+            any[g] = lbeg + 32 > 0;
+            if (lbeg >= 0) {
+                const u32x4_unaligned* p = reinterpret_cast<const u32x4_unaligned*>(base + lbeg);
+                const u32x4_unaligned v0 = p[0], v1 = p[1];
+                w[g][0] = v0.x; w[g][1] = v0.y; w[g][2] = v0.z; w[g][3] = v0.w;
+                w[g][4] = v1.x; w[g][5] = v1.y; w[g][6] = v1.z; w[g][7] = v1.w;
+            } else if (any[g]) {
+                copy_bytes_slow(base, dbase, lbeg, w[g]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w[g][i] = 0;
+            }
+        }
+        if (dbase) {  // null destination: checksum only (uniform per segment)
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                const int64_t lbeg = wave_end - (int64_t)(2 - g) * 2048 + 64 * c + 32 * h;
+                if (lbeg >= 0) {
+                    u32x4_unaligned* q = reinterpret_cast<u32x4_unaligned*>(dbase + lbeg);
+                    u32x4_unaligned v0, v1;
+                    v0.x = w[g][0]; v0.y = w[g][1]; v0.z = w[g][2]; v0.w = w[g][3];
+                    v1.x = w[g][4]; v1.y = w[g][5]; v1.z = w[g][6]; v1.w = w[g][7];
+                    q[0] = v0;
+                    q[1] = v1;
+                }
+            }
+        }
+        uint32_t v = 0;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            // a group wholly before the segment adds nothing (wave-uniform)
+            if (!__ballot(any[g])) continue;
+            i32x16 d = {0};
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t bits = (w[g][j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+                d = __builtin_amdgcn_mfma_i32_32x32x32_i8(sa[j][lane], expand16(bits), d, 0, 0, 0);
+                if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+            }
+            uint32_t part = 0;
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                part |= ((uint32_t)d[reg] & 1u) << row;
+            }
+            const uint32_t crc_c = part | __shfl_xor(part, 32, 64);
+            // 64-byte blocks after column c of group g inside the chunk
+            const int blocks_after = 64 * (kThreads / 64 - 1 - wave) + 32 * (1 - g) + (31 - c);
+            v ^= mult_mod_p(c_lane_shift[blocks_after], crc_c);
+        }
+        // the 32 columns (each present twice, once per lane half)
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) v ^= __shfl_xor(v, off, 64);
+        if (lane == 0) wave_acc[wave] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
+            fold_chunk(b, seg, after, seg_chunks, acc, scratch, out);
+        }
+        __syncthreads();  // wave_acc is reused by the next chunk
+    }
+    signal_done(b);
 }
 
 __global__ void crc_chunk_count_kernel(const uint64_t* __restrict__ lens, int64_t nseg, uint64_t* __restrict__ cs) {
@@ -1009,7 +1127,21 @@ int LaunchCrc32cSegments(const uint64_t* starts_dev, const uint64_t* lens_dev, i
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s) {
+// One fused copy + CRC launch of a filled batch: the MFMA kernel (a
+// workgroup walks chunks, at most 8 workgroups per CU of the 256) or the
+// byte-table kernel (one workgroup per chunk).
+static void launch_copy_crc(const SegBatch& b, uint32_t chunks, int dev, uint32_t* scratch, uint32_t* out,
+                            hipStream_t s, bool mfma) {
+    if (mfma) {
+        const uint32_t grid = chunks < 2048u ? chunks : 2048u;
+        hipLaunchKernelGGL(copy_crc32c_mfma_kernel, dim3(grid), dim3(kThreads), 0, s, b,
+                           (const CrcMfmaConsts*)g_tables[dev].mfma, scratch, out, chunks);
+    } else {
+        hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch, out);
+    }
+}
+
+int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s, bool mfma) {
     if (nseg <= 0) return 0;
     if (ensure_tables() != 0) return -1;
     int dev = 0;
@@ -1020,15 +1152,14 @@ int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStr
         const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;
         SegBatch b;
         const uint32_t chunks = fill_batch(&b, segs + i, n);
-        hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch,
-                           out + i);
+        launch_copy_crc(b, chunks, dev, scratch, out + i, s, mfma);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;
 }
 
 int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int nseg, uint32_t* out, hipStream_t s,
-                                    const DoneWord* done) {
+                                    const DoneWord* done, bool mfma) {
     if (nseg <= 0) return 0;
     if (ensure_tables() != 0) return -1;
     int dev = 0;
@@ -1040,8 +1171,7 @@ int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int 
         SegBatch b;
         const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of + i);
         if (done && e == nseg) set_done(&b, *done);
-        hipLaunchKernelGGL(copy_crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch,
-                           out + msg_of[i]);
+        launch_copy_crc(b, chunks, dev, scratch, out + msg_of[i], s, mfma);
         if (hipGetLastError() != hipSuccess) return -1;
     }
     return 0;

@@ -52,8 +52,6 @@
 #include "gpu/device_pb.h"
 #include "gpu/kernels.h"
 
-DECLARE_bool(gpu_snappy_compress_pj);
-
 namespace mrpc {
 namespace gpu {
 
@@ -1137,453 +1135,6 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
     stamp(stamps, blk, lane, 4);
 }
 
-// ------------------------------------------------ data-parallel compressor
-// compress_wave's lanes each walk a 1/64 slice of the block: matches stop at
-// the slice end and every slice opens with a literal, so a 2 KiB block of
-// text reaches 1.96:1, and the wave waits for its slowest lane's serial walk
-// (~34k of its ~56k cycles). This variant makes every decision that does
-// not depend on the previous one for all positions at once and keeps the
-// one serial decision — which positions start an element — to a few short
-// walks:
-//   1. candidates: the earliest position with the same 4-byte hash
-//      (verified), for every position;
-//   2. L(q): the match length at q (up to 32), for every position (lane +
-//      64 i: a wave step probes 64 consecutive positions);
-//   3. f(q) = q + L(q) at a hit, else the next hit (or the block end): the
-//      greedy parse is the chain 0, f(0), f(f(0)), ...;
-//   4. the chain by speculative slice walks: every lane walks f through its
-//      slice from the slice start, then re-walks from the previous lane's
-//      exit where that differs, until no entry changes (greedy parses from
-//      nearby starts fall into step within an element or two);
-//   5. element sizes, a prefix sum for their offsets, then tags and literal
-//      bytes written by all lanes at once into LDS and streamed out.
-// Matches may cross what were slice ends, so text compresses close to the
-// single-threaded greedy parse (2 KiB blocks: ~2.14:1 with 32-byte copies).
-// (A first version found the chain by pointer doubling over all positions:
-// log2(n) full passes, ~74k cycles per 2 KiB block against ~3k for the
-// walks.)
-constexpr uint32_t kPjMax = 4096;
-__host__ __device__ constexpr uint32_t PjAlign(uint32_t x) { return (x + 15) & ~15u; }
-// dynamic LDS: input, then u16 candidate / f / J ping-pong arrays, then u8
-// lengths and marks (position n is the terminal). The per-position arrays
-// skip one dword after every 32 positions: a lane's slice of 32 positions
-// then starts 17 (u16) or 9 (u8) dwords after its neighbour's, so the
-// slice passes hit 32 distinct banks instead of 2 or 4, and the
-// interleaved passes (lane + 64 i) stay conflict-free.
-__host__ __device__ constexpr uint32_t PjIdx16(uint32_t q) { return q + ((q >> 5) << 1); }
-__host__ __device__ constexpr uint32_t PjIdx8(uint32_t q) { return q + ((q >> 5) << 2); }
-__host__ __device__ constexpr uint32_t PjLdsBytes(uint32_t in_cap) {
-    return PjAlign(in_cap + 16) + 3 * PjAlign(2 * (PjIdx16(in_cap) + 8)) + 2 * PjAlign(PjIdx8(in_cap) + 16);
-}
-
-__device__ __forceinline__ uint32_t lit_tag_bytes(uint32_t len) { return len <= 60 ? 1u : len <= 256 ? 2u : 3u; }
-
-__device__ __forceinline__ void compress_wave_pj(const SnappyJob* __restrict__ jobs, int blk,
-                                                 uint32_t* __restrict__ out_len, int* __restrict__ err,
-                                                 uint32_t in_cap, uint64_t* __restrict__ stamps) {
-    // One wave alone on its SIMD waits out every LDS round trip (~100+
-    // cycles), so each pass issues the reads of several positions before it
-    // uses any of them (kB positions per batch, independent by construction).
-    constexpr int kFB = 11;
-    constexpr int kB = 8;
-    // copies up to 32 bytes: a 2 KiB text block loses ~1.6% of its ratio to
-    // 64 (2.14 vs 2.17:1) and the probe loop of a batch, which runs as long
-    // as its longest match, halves
-    constexpr uint32_t kCap = 32;
-    __shared__ __attribute__((aligned(16))) uint32_t first_pos[1 << kFB];  // later: the output stage
-    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    typedef __attribute__((address_space(3))) uint16_t lu16;
-    const int lane = threadIdx.x;
-    const SnappyJob job = jobs[blk];
-    const uint32_t n = (uint32_t)job.src_len;
-    if (job.src_len > in_cap || n > kPjMax) {
-        if (lane == 0) {
-            err[blk] = 1;
-            out_len[blk] = 0;
-        }
-        return;
-    }
-    gbyte* dst = as_global(job.dst);
-    uint32_t hdr = 1;
-    for (uint32_t u = n; u >= 0x80; u >>= 7) ++hdr;
-    if (n < 5) {  // the header and at most one literal
-        const uint32_t total = hdr + (n ? 1 + n : 0);
-        if (total > job.dst_cap) {
-            if (lane == 0) {
-                err[blk] = 2;
-                out_len[blk] = 0;
-            }
-            return;
-        }
-        if (lane == 0) {
-            gbyte_c* src = as_global(job.src);
-            dst[0] = (uint8_t)n;
-            if (n) {
-                dst[1] = (uint8_t)((n - 1) << 2);
-                for (uint32_t k = 0; k < n; ++k) dst[2 + k] = src[k];
-            }
-            out_len[blk] = total;
-            err[blk] = 0;
-        }
-        return;
-    }
-    lbyte* const in = (lbyte*)dyn_lds;
-    const uint32_t a16 = PjAlign(2 * (PjIdx16(in_cap) + 8)), a8 = PjAlign(PjIdx8(in_cap) + 16);
-    uint32_t off = PjAlign(in_cap + 16);
-    lu16* const cand_ = (lu16*)(dyn_lds + off);
-    lu16* const fnext_ = (lu16*)(dyn_lds + off + a16);
-    lu16* const eoff_ = (lu16*)(dyn_lds + off + 2 * a16);
-    off += 3 * a16;
-    lbyte* const mlen_ = (lbyte*)(dyn_lds + off);
-    lbyte* const vis_ = (lbyte*)(dyn_lds + off + a8);
-    // padded views: X(q) is position q's entry
-    auto cand = [&](uint32_t q) -> auto& { return cand_[PjIdx16(q)]; };
-    auto fnext = [&](uint32_t q) -> auto& { return fnext_[PjIdx16(q)]; };
-    auto mlen = [&](uint32_t q) -> auto& { return mlen_[PjIdx8(q)]; };
-    auto vis = [&](uint32_t q) -> auto& { return vis_[PjIdx8(q)]; };
-    auto eoff = [&](uint32_t q) -> auto& { return eoff_[PjIdx16(q)]; };
-    auto dw = [&](uint32_t d) -> uint32_t { return ((lword_c*)in)[d]; };
-    auto rd32 = [&](uint32_t x) -> uint32_t {
-        const uint32_t d = x >> 2;
-        return __builtin_amdgcn_alignbyte(dw(d + 1), dw(d), x & 3);
-    };
-    auto rd64 = [&](uint32_t x) -> uint64_t {
-        const uint32_t d = x >> 2, w0 = dw(d), w1 = dw(d + 1), w2 = dw(d + 2), sh = x & 3;
-        return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
-    };
-    auto hash = [](uint32_t v) -> uint32_t { return (v * 0x1e35a7bdu) >> (32 - kFB); };
-    stamp(stamps, blk, lane, 0);
-    {
-        gbyte_c* src = as_global(job.src);
-        uint32_t done = 0;
-        if ((reinterpret_cast<uintptr_t>(job.src) & 15) == 0) {
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            done = n & ~15u;
-            for (uint32_t o = lane * 16; o < done; o += kWave * 16) {
-                *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(in + o) =
-                    *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(src + o);
-            }
-        }
-        for (uint32_t o = done + lane; o < n; o += kWave) in[o] = src[o];
-        if (lane < 16) in[n + lane] = 0;  // probes may read past the end (lengths are clamped)
-        for (int i = lane; i < (1 << kFB); i += kWave) first_pos[i] = 0xFFFFFFFFu;
-    }
-    __syncthreads();
-    const uint32_t qend = n - 3;  // positions with 4 bytes
-    // earliest position per hash (positions interleaved across lanes)
-    for (uint32_t b = lane; b < qend; b += kB * kWave) {
-        uint32_t v[kB];
-#pragma unroll
-        for (int i = 0; i < kB; ++i) {
-            const uint32_t q = b + i * kWave;
-            v[i] = rd32(q < qend ? q : 0u);
-        }
-#pragma unroll
-        for (int i = 0; i < kB; ++i) {
-            const uint32_t q = b + i * kWave;
-            if (q < qend) atomicMin(&first_pos[hash(v[i])], q);
-        }
-    }
-    __syncthreads();
-    stamp(stamps, blk, lane, 1);
-    // 1+2: candidate and match length of every position, 4 per lane at once.
-    // Positions past the end are clamped to n - 1 (a lane then recomputes
-    // and rewrites the last position's own values) instead of guarding the
-    // stores: hipcc (ROCm 7.2, gfx950) dropped the q < n guard of the middle
-    // stores of this unrolled loop, and those wrote 0xFFFF candidates over
-    // the length array of blocks whose in_cap left the arrays adjacent.
-    for (uint32_t b0 = lane; b0 < n; b0 += 4 * kWave) {
-        uint32_t v[4], f[4], fv[4], c[4], len[4], lim[4];
-        bool act[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t q = min(b0 + i * kWave, n - 1);
-            v[i] = rd32(q < qend ? q : 0u);
-        }
-        // (every read below is unconditional, its address clamped: a read
-        // under a lane condition makes the compiler wait for it at once)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t q = min(b0 + i * kWave, n - 1);
-            const uint32_t fp = first_pos[hash(v[i])];
-            f[i] = q < qend ? fp : 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t q = min(b0 + i * kWave, n - 1);
-            fv[i] = rd32(f[i] < q ? f[i] : 0u);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t q = min(b0 + i * kWave, n - 1);
-            const bool hit = q < qend && f[i] < q && fv[i] == v[i];
-            c[i] = hit ? f[i] : 0xFFFFu;
-            len[i] = hit ? 4u : 0u;
-            lim[i] = min(kCap, n - q);
-            act[i] = hit && len[i] < lim[i];
-        }
-        // extend the hits 8 bytes per step, all four probes in flight
-        for (int step = 0; step < (int)(kCap / 8); ++step) {
-            bool any = false;
-            uint64_t x[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t q = min(b0 + i * kWave, n - 1);
-                const uint64_t y = rd64(act[i] ? c[i] + len[i] : 0u) ^ rd64(act[i] ? q + len[i] : 0u);
-                x[i] = act[i] ? y : 0ull;
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (!act[i]) continue;
-                if (x[i]) {
-                    len[i] += (uint32_t)__builtin_ctzll(x[i]) >> 3;
-                    act[i] = false;
-                } else {
-                    len[i] += 8;
-                    act[i] = len[i] < lim[i];
-                }
-                any |= act[i];
-            }
-            if (!any) break;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t q = min(b0 + i * kWave, n - 1);
-            cand(q) = (uint16_t)c[i];
-            mlen(q) = (uint8_t)min(len[i], lim[i]);
-        }
-    }
-    __syncthreads();
-    stamp(stamps, blk, lane, 2);
-    // 3: f(q) over 32-position chunks (contiguous in the padded arrays): a
-    // lane owns whole chunks; f at a hit is q + L, else the next hit, which
-    // for the chunk tails after a slice's last hit comes from the later lanes
-    const uint32_t nchunks = (n + 31) >> 5;
-    const uint32_t cpl = (nchunks + kWave - 1) / kWave;  // chunks per lane: 1 (<= 2 KiB) or 2
-    const uint32_t s = min(n, (uint32_t)lane * cpl * 32);
-    const uint32_t e = min(n, s + cpl * 32);
-    {
-        uint32_t nxt = 0xFFFFu, tail = e;  // [tail, e): after the slice's last hit
-        for (uint32_t top = e; top > s;) {
-            const uint32_t k = min((uint32_t)kB, top - s);
-            uint32_t m[kB];
-#pragma unroll
-            for (int i = 0; i < kB; ++i) m[i] = mlen((uint32_t)i < k ? top - 1 - i : s);
-#pragma unroll
-            for (int i = 0; i < kB; ++i) {
-                if ((uint32_t)i >= k) break;
-                const uint32_t q = top - 1 - i;
-                uint32_t f;
-                if (m[i] >= 4) {
-                    f = q + m[i];
-                    if (nxt == 0xFFFFu) tail = q + 1;
-                    nxt = q;
-                } else {
-                    f = nxt;
-                }
-                fnext(q) = (uint16_t)f;
-                vis(q) = 0;
-            }
-            top -= k;
-        }
-        const uint32_t fh = nxt == 0xFFFFu ? n : nxt;  // first hit of the slice
-        if (nxt == 0xFFFFu) tail = s;
-        // suffix min over later lanes: reverse the lanes, prefix max of n - fh
-        const uint32_t g = n - fh;
-        const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((63 - lane) << 2, (int)g);
-        const uint32_t t = wave_incl_max(r);
-        // (bpermute with every lane active: lane 63 reads lane 63 and drops it)
-        const uint32_t exr = (uint32_t)__builtin_amdgcn_ds_bpermute(((62 - lane) & 63) << 2, (int)t);
-        const uint32_t later = n - (lane < 63 ? exr : 0u);
-        for (uint32_t q = tail; q < e; ++q) fnext(q) = (uint16_t)later;
-    }
-    __syncthreads();
-    // 4: the greedy chain. Each lane walks f through its slice from the
-    // slice start (a guess of where the chain enters it), then takes the
-    // previous lane's exit as its entry and walks again where that differs,
-    // until no entry changes. Lane 0's entry is exact, so round r fixes at
-    // least lane r; greedy parses from nearby starts fall into step within
-    // an element or two, so 2-3 rounds settle a block. Slices are ~3
-    // elements: a walk is a few dependent LDS reads, not log2(n) passes
-    // over every position.
-    {
-        auto walk = [&](uint32_t x) -> uint32_t {
-            uint32_t p = x;
-            while (p < e) {
-                vis(p) = 1;
-                p = fnext(p);
-            }
-            return p;
-        };
-        uint32_t entry = s;
-        uint32_t exit = walk(s);
-        int rounds = 1;
-        for (; rounds <= kWave + 1; ++rounds) {
-            const uint32_t pe = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane - 1) & 63) << 2, (int)exit);
-            const uint32_t want = lane == 0 ? 0u : pe;
-            const bool change = want != entry;
-            if (__builtin_amdgcn_ballot_w64(change) == 0) break;
-            if (change) {
-                for (uint32_t q = s; q < e; ++q) vis(q) = 0;
-                entry = want;
-                exit = walk(want);
-            }
-        }
-        if (stamps && blk == 0 && lane == 0) stamps[5] = (uint64_t)rounds;
-    }
-    __syncthreads();
-    stamp(stamps, blk, lane, 3);
-    // 5: element sizes and offsets over the slices, tags, then literal bytes
-    lbyte* const stage = (lbyte*)first_pos;
-    uint32_t mine = 0, lastv = 0;
-    for (uint32_t b = s; b < e; b += kB) {
-        uint32_t mv[kB], ml[kB], cd[kB], fx[kB];
-#pragma unroll
-        for (int i = 0; i < kB; ++i) {
-            const uint32_t q = min(b + i, e - 1);
-            mv[i] = vis(q) & (b + i < e ? 0xFFu : 0u);
-            ml[i] = mlen(q);
-            cd[i] = cand(q);
-            fx[i] = fnext(q);
-        }
-#pragma unroll
-        for (int i = 0; i < kB; ++i) {
-            if (!mv[i]) continue;
-            const uint32_t q = b + i;
-            if (ml[i] >= 4) {
-                mine += (ml[i] < 12 && q - cd[i] < 2048) ? 2u : 3u;
-            } else {
-                const uint32_t ll = fx[i] - q;
-                mine += lit_tag_bytes(ll) + ll;
-            }
-            lastv = q + 1;
-        }
-    }
-    const uint32_t incl = wave_incl_sum(mine);
-    const uint32_t total = hdr + (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-    const uint32_t lv_incl = wave_incl_max(lastv);
-    const uint32_t carry_r = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane - 1) & 63) << 2, (int)lv_incl);
-    const uint32_t carry = lane > 0 ? carry_r : 0u;
-    if (total > job.dst_cap || total > (uint32_t)sizeof(first_pos)) {
-        if (lane == 0) {
-            err[blk] = 2;
-            out_len[blk] = 0;
-        }
-        return;
-    }
-    {
-        uint32_t at = hdr + incl - mine;
-        for (uint32_t b = s; b < e; b += kB) {
-            uint32_t mv[kB], ml[kB], cd[kB], fx[kB];
-#pragma unroll
-            for (int i = 0; i < kB; ++i) {
-                const uint32_t q = min(b + i, e - 1);
-                mv[i] = vis(q) & (b + i < e ? 0xFFu : 0u);
-                ml[i] = mlen(q);
-                cd[i] = cand(q);
-                fx[i] = fnext(q);
-            }
-#pragma unroll
-            for (int i = 0; i < kB; ++i) {
-                if (!mv[i]) continue;
-                const uint32_t q = b + i;
-                eoff(q) = (uint16_t)at;
-                const uint32_t l = ml[i];
-                if (l >= 4) {
-                    const uint32_t o = q - cd[i];
-                    if (l < 12 && o < 2048) {
-                        stage[at] = (uint8_t)(((o >> 8) << 5) | ((l - 4) << 2) | 1);
-                        stage[at + 1] = (uint8_t)o;
-                        at += 2;
-                    } else {
-                        stage[at] = (uint8_t)(((l - 1) << 2) | 2);
-                        stage[at + 1] = (uint8_t)o;
-                        stage[at + 2] = (uint8_t)(o >> 8);
-                        at += 3;
-                    }
-                } else {
-                    const uint32_t ll = fx[i] - q, m = ll - 1;
-                    if (m < 60) {
-                        stage[at] = (uint8_t)(m << 2);
-                    } else if (m < 256) {
-                        stage[at] = (uint8_t)(60 << 2);
-                        stage[at + 1] = (uint8_t)m;
-                    } else {
-                        stage[at] = (uint8_t)(61 << 2);
-                        stage[at + 1] = (uint8_t)m;
-                        stage[at + 2] = (uint8_t)(m >> 8);
-                    }
-                    at += lit_tag_bytes(ll) + ll;
-                }
-            }
-        }
-        if (lane < (int)hdr) {
-            const uint32_t u = n >> (7 * lane);
-            stage[lane] = (uint8_t)((u & 0x7f) | (lane + 1 < (int)hdr ? 0x80 : 0));
-        }
-    }
-    __syncthreads();
-    {
-        // literal bytes: every position inside a literal element lands at
-        // its element's offset + tag + distance
-        uint32_t el = carry ? carry - 1 : 0, base = 0;
-        bool lit = false;
-        if (s < e) {
-            const uint32_t p = vis(s) ? s : el;
-            el = p;
-            lit = mlen(p) < 4;
-            base = eoff(p) + (lit ? lit_tag_bytes(fnext(p) - p) : 0u);
-        }
-        for (uint32_t b = s; b < e; b += kB) {
-            uint32_t mv[kB], ml[kB], eo[kB], fx[kB], by[kB];
-#pragma unroll
-            for (int i = 0; i < kB; ++i) {
-                const uint32_t q = min(b + i, e - 1);
-                mv[i] = vis(q) & (b + i < e ? 0xFFu : 0u);
-                ml[i] = mlen(q);
-                eo[i] = eoff(q);
-                fx[i] = fnext(q);
-                by[i] = in[q];
-            }
-#pragma unroll
-            for (int i = 0; i < kB; ++i) {
-                const uint32_t q = b + i;
-                if (q >= e) break;
-                if (q != el && mv[i]) {
-                    el = q;
-                    lit = ml[i] < 4;
-                    base = eo[i] + (lit ? lit_tag_bytes(fx[i] - q) : 0u);
-                }
-                if (lit) stage[base + (q - el)] = (uint8_t)by[i];
-            }
-        }
-    }
-    __syncthreads();
-    if (((uintptr_t)job.dst & 15) == 0) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const uint32_t vec_end = total & ~15u;
-        for (uint32_t o = (uint32_t)lane * 16; o < vec_end; o += kWave * 16)
-            *reinterpret_cast<__attribute__((address_space(1))) u32x4*>(dst + o) =
-                *reinterpret_cast<const __attribute__((address_space(3))) u32x4*>(stage + o);
-        for (uint32_t o = vec_end + lane; o < total; o += kWave) dst[o] = stage[o];
-    } else {
-        for (uint32_t o = lane; o < total; o += kWave) dst[o] = stage[o];
-    }
-    if (lane == 0) {
-        out_len[blk] = total;
-        err[blk] = 0;
-    }
-    stamp(stamps, blk, lane, 4);
-}
-
-__global__ void __launch_bounds__(kWave) snappy_compress_pj_kernel(const SnappyJob* __restrict__ jobs, int n,
-                                                                   uint32_t* __restrict__ out_len,
-                                                                   int* __restrict__ err, uint32_t in_cap,
-                                                                   uint64_t* __restrict__ stamps) {
-    if ((int)blockIdx.x >= n) return;
-    compress_wave_pj(jobs, (int)blockIdx.x, out_len, err, in_cap, stamps);
-}
-
 template <bool kOutLds, bool kCand>
 __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob* __restrict__ jobs, int n,
                                                                 uint8_t* __restrict__ scratch,
@@ -1604,21 +1155,21 @@ __global__ void __launch_bounds__(kWave) snappy_compress_kernel(const SnappyJob*
 // latency-bound kernels per batch, each wave far from filling its CU, so
 // sharing one dispatch halves the batch's device time while keeping the
 // small-footprint waves that pack 5 per CU (many batches in flight share
-// the chip; the 1024-thread workgroup codec of codec_fused.hip is faster
-// alone but holds a CU per block and loses when batches overlap).
+// the chip). Two alternatives were measured and removed in round 6
+// (profiles/r5_device_codec_ab.txt): a 1024-thread workgroup per block with
+// a block-wide parse (faster alone, 26 vs 29 us, but it holds a CU per
+// block: 139k vs 158-161k QPS on the device text leg with batches
+// overlapping) and a data-parallel compressor whose matches cross the lane
+// slices (ratio 2.14 vs 1.96, but 47 vs 28 us per launch: 116k QPS).
 // Instantiated per role set: a batch of only decode pieces gets a kernel
 // without the compressor's registers and static LDS (the per-wave footprint
 // decides how many waves of concurrent batches share a CU).
-template <bool kComp, bool kDec, bool kPj>
+template <bool kComp, bool kDec>
 __global__ void __launch_bounds__(kWave) codec_waves_kernel(FusedCodecArgs a, uint32_t in_cap, uint32_t slot,
                                                             uint32_t cin_cap, uint32_t phi) {
     const int b = blockIdx.x;
     if (kComp && b < a.ncomp) {
-        if (kPj) {
-            compress_wave_pj(a.comp, b, a.comp_len, a.comp_err, in_cap, nullptr);
-        } else {
-            compress_wave<true, true>(a.comp, b, nullptr, a.comp_len, a.comp_err, in_cap, slot, nullptr);
-        }
+        compress_wave<true, true>(a.comp, b, nullptr, a.comp_len, a.comp_err, in_cap, slot, nullptr);
         return;
     }
     if (!kDec) return;
@@ -1652,31 +1203,19 @@ int LaunchCodecWaves(const FusedCodecArgs& a, hipStream_t s) {
     const uint32_t in_cap = (mu + 15) & ~15u;
     const uint32_t seg = (mu + kWave - 1) / kWave;
     const uint32_t slot = (seg + 16 + 15) & ~15u;
-    const bool pj = FLAGS_gpu_snappy_compress_pj && mu <= kPjMax;
-    const uint32_t comp_lds =
-        pj ? PjLdsBytes(in_cap) : CompressInBytes(in_cap, true) + kWave * slot + CompressCandBytes(in_cap);
+    const uint32_t comp_lds = CompressInBytes(in_cap, true) + kWave * slot + CompressCandBytes(in_cap);
     const uint32_t cin_cap = (uint32_t)((SnappyMaxCompressedLength(mu) + 16 + 15) & ~15ull);
     const uint32_t dec_lds = cin_cap + 2 * ((mu + 7) & ~7u) + 16 * kWave;
     const uint32_t lds = std::max(a.ncomp ? comp_lds : 0u, a.npieces ? dec_lds : 0u);
     if (a.ncomp && a.npieces) {
-        if (pj) {
-            hipLaunchKernelGGL((codec_waves_kernel<true, true, true>), dim3((unsigned)n), dim3(kWave), lds, s, a,
-                               in_cap, slot, cin_cap, mu);
-        } else {
-            hipLaunchKernelGGL((codec_waves_kernel<true, true, false>), dim3((unsigned)n), dim3(kWave), lds, s, a,
-                               in_cap, slot, cin_cap, mu);
-        }
+        hipLaunchKernelGGL((codec_waves_kernel<true, true>), dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot,
+                           cin_cap, mu);
     } else if (a.ncomp) {
-        if (pj) {
-            hipLaunchKernelGGL((codec_waves_kernel<true, false, true>), dim3((unsigned)n), dim3(kWave), lds, s, a,
-                               in_cap, slot, cin_cap, mu);
-        } else {
-            hipLaunchKernelGGL((codec_waves_kernel<true, false, false>), dim3((unsigned)n), dim3(kWave), lds, s, a,
-                               in_cap, slot, cin_cap, mu);
-        }
+        hipLaunchKernelGGL((codec_waves_kernel<true, false>), dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot,
+                           cin_cap, mu);
     } else {
-        hipLaunchKernelGGL((codec_waves_kernel<false, true, false>), dim3((unsigned)n), dim3(kWave), lds, s, a,
-                           in_cap, slot, cin_cap, mu);
+        hipLaunchKernelGGL((codec_waves_kernel<false, true>), dim3((unsigned)n), dim3(kWave), lds, s, a, in_cap, slot,
+                           cin_cap, mu);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -1746,10 +1285,7 @@ int LaunchSnappyCompressStamped(const SnappyJob* jobs_dev, int n, uint32_t max_u
     static_assert(16384 + kWave * ((16384 / kWave + 16 + 15) & ~15u) + kWave * kHashEntries * 2 + kFirstEntries * 4 +
                           kWave * 4 + kWave * kLitSpans * 8 <= 80 * 1024,
                   "16 KiB blocks keep their slots in LDS");
-    if (FLAGS_gpu_snappy_compress_pj && max_ulen <= kPjMax) {
-        hipLaunchKernelGGL(snappy_compress_pj_kernel, dim3(n), dim3(kWave), PjLdsBytes(in_cap), s, jobs_dev, n,
-                           out_len_dev, err_dev, in_cap, stamps);
-    } else if (max_ulen <= kCandMax) {
+    if (max_ulen <= kCandMax) {
         // input, slots and the candidate array in LDS: <= 8 + 9 + 16 KiB
         const uint32_t cslot = slot;
         hipLaunchKernelGGL((snappy_compress_kernel<true, true>), dim3(n), dim3(kWave),

@@ -13,7 +13,7 @@ DEFINE_bool(log_unknown_protocol, false, "log bytes of connections speaking no k
 
 namespace mrpc {
 
-static const size_t kMinOnceRead = 4096;
+static const size_t kMinOnceRead = 8192;  // one default block: a burst of small messages in one read
 static const size_t kMaxOnceRead = 524288;
 
 InputMessenger::InputMessenger(size_t capacity) : _capacity(capacity) {}

@@ -72,32 +72,6 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(p); }
 };
 
-// Kernel time of `launch` (events around `iters` back-to-back launches).
-template <typename F>
-double time_launches(F launch, int iters, hipStream_t s) {
-    hipEvent_t a, b;
-    hipEventCreate(&a);
-    hipEventCreate(&b);
-    launch();  // warm-up
-    hipEventRecord(a, s);
-    for (int i = 0; i < iters; ++i) launch();
-    hipEventRecord(b, s);
-    hipEventSynchronize(b);
-    float ms = 0;
-    hipEventElapsedTime(&ms, a, b);
-    hipEventDestroy(a);
-    hipEventDestroy(b);
-    return 1000.0 * ms / std::max(1, iters);
-}
-
-int varint_bytes(uint32_t v) {
-    int k = 1;
-    while (v >= 0x80) {
-        v >>= 7;
-        ++k;
-    }
-    return k;
-}
 }  // namespace
 
 void bind_gpu_ops(py::module_& g) {
@@ -185,155 +159,6 @@ void bind_gpu_ops(py::module_& g) {
     // `len` bytes at src into blocks at dst (layout of -device_payload_block_kb)
     // -> (block_ulen, stride, [clen...]); decode such a table back -> per-job
     // code (0 ok, 1 bad table, 2 malformed block) and the field table when scanned.
-    // RPC-shaped A/B of the device-body codecs: `bodies` are cut into
-    // `block`-byte blocks; returns per-launch kernel microseconds of the
-    // fused workgroup codec (compress launch, decode launch, one mixed
-    // launch of both) and of the per-lane-segment kernels, the compressed
-    // size of each, the fused parse rounds, and whether every decode
-    // rebuilt the input (benchmarks/fused_codec_ab.py)
-    g.def("fused_codec_bench", [](const std::vector<py::bytes>& bodies, uint32_t block, int iters, int device) {
-        std::string all;
-        std::vector<std::pair<size_t, uint32_t>> blocks;  // (offset, len)
-        for (const py::bytes& b : bodies) {
-            std::string x = b;
-            for (size_t o = 0; o < x.size(); o += block)
-                blocks.push_back({all.size() + o, (uint32_t)std::min<size_t>(block, x.size() - o)});
-            all += x;
-            all.resize((all.size() + 15) & ~(size_t)15, '\0');
-        }
-        const int n = (int)blocks.size();
-        if (n == 0 || block == 0 || block > gpu::kFusedMaxBlock) throw std::invalid_argument("bad shape");
-        py::dict out;
-        {
-            py::gil_scoped_release nogil;
-            hipSetDevice(device);
-            hipStream_t s = nullptr;
-            hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
-            const size_t cap = (gpu::SnappyMaxCompressedLength(block) + 15) & ~(size_t)15;
-            DevBuf src(all.size()), dst(all.size() + 16), cmp(cap * n), cmp2(cap * n), stats(128), scratch(16);
-            DevBuf jobs(sizeof(gpu::SnappyJob) * n), pieces(sizeof(gpu::SnappyPiece) * n), lens(4 * n), errs(4 * n),
-                perr(4 * n), lens2(4 * n), errs2(4 * n);
-            hipMemcpy(src.p, all.data(), all.size(), hipMemcpyHostToDevice);
-            std::vector<gpu::SnappyJob> hj(n), hj2(n);
-            for (int i = 0; i < n; ++i) {
-                hj[i] = gpu::SnappyJob{src.as<char>() + blocks[i].first, cmp.as<char>() + cap * i, blocks[i].second, cap};
-                hj2[i] = gpu::SnappyJob{src.as<char>() + blocks[i].first, cmp2.as<char>() + cap * i, blocks[i].second, cap};
-            }
-            hipMemcpy(jobs.p, hj.data(), sizeof(gpu::SnappyJob) * n, hipMemcpyHostToDevice);
-            hipMemset(stats.p, 0, 128);
-            gpu::FusedCodecArgs fc;
-            fc.comp = jobs.as<gpu::SnappyJob>();
-            fc.ncomp = n;
-            fc.comp_len = lens.as<uint32_t>();
-            fc.comp_err = errs.as<int>();
-            fc.max_ulen = block;
-            fc.stats = stats.as<uint32_t>();
-            const double comp_us = time_launches([&] { gpu::LaunchFusedCodec(fc, s); }, iters, s);
-            std::vector<uint32_t> clen(n);
-            std::vector<int> cerr(n);
-            hipMemcpy(clen.data(), lens.p, 4 * n, hipMemcpyDeviceToHost);
-            hipMemcpy(cerr.data(), errs.p, 4 * n, hipMemcpyDeviceToHost);
-            std::vector<gpu::SnappyPiece> hp(n);
-            uint64_t csum = 0;
-            for (int i = 0; i < n; ++i) {
-                const int h = varint_bytes(blocks[i].second);
-                hp[i] = gpu::SnappyPiece{cmp.as<char>() + cap * i + h, dst.as<char>() + blocks[i].first,
-                                         clen[i] - (uint32_t)h, blocks[i].second};
-                csum += clen[i];
-            }
-            hipMemcpy(pieces.p, hp.data(), sizeof(gpu::SnappyPiece) * n, hipMemcpyHostToDevice);
-            gpu::FusedCodecArgs fd;
-            fd.pieces = pieces.as<gpu::SnappyPiece>();
-            fd.npieces = n;
-            fd.piece_err = perr.as<int>();
-            fd.max_ulen = block;
-            fd.stats = stats.as<uint32_t>();
-            const double dec_us = time_launches([&] { gpu::LaunchFusedCodec(fd, s); }, iters, s);
-            std::string back(all.size(), '\0');
-            std::vector<int> pe(n);
-            hipMemcpy(&back[0], dst.p, all.size(), hipMemcpyDeviceToHost);
-            hipMemcpy(pe.data(), perr.p, 4 * n, hipMemcpyDeviceToHost);
-            bool ok = true;
-            for (int i = 0; i < n; ++i) {
-                ok = ok && cerr[i] == 0 && pe[i] == 0 &&
-                     memcmp(&back[blocks[i].first], &all[blocks[i].first], blocks[i].second) == 0;
-            }
-            // one mixed launch: the batch's encodes and decodes together
-            gpu::FusedCodecArgs fm = fc;
-            fm.pieces = fd.pieces;
-            fm.npieces = n;
-            fm.piece_err = fd.piece_err;
-            const double mixed_us = time_launches([&] { gpu::LaunchFusedCodec(fm, s); }, iters, s);
-            uint32_t st[32];
-            hipMemcpy(st, stats.p, 128, hipMemcpyDeviceToHost);
-            // the per-lane-segment kernels on the same blocks
-            hipMemcpy(jobs.p, hj2.data(), sizeof(gpu::SnappyJob) * n, hipMemcpyHostToDevice);
-            const double old_comp_us = time_launches(
-                [&] { gpu::LaunchSnappyCompress(jobs.as<gpu::SnappyJob>(), n, block, nullptr, lens2.as<uint32_t>(),
-                                                errs2.as<int>(), s); },
-                iters, s);
-            std::vector<uint32_t> clen2(n);
-            hipMemcpy(clen2.data(), lens2.p, 4 * n, hipMemcpyDeviceToHost);
-            uint64_t csum2 = 0;
-            for (int i = 0; i < n; ++i) csum2 += clen2[i];
-            const double old_dec_us = time_launches(
-                [&] { gpu::LaunchSnappyDecompressPieces(pieces.as<gpu::SnappyPiece>(), n, 0, block, perr.as<int>(), s); },
-                iters, s);
-            // the one-launch wave codec on the same batch (its compress half
-            // writes cmp2, its decode half reads the workgroup codec's cmp)
-            gpu::FusedCodecArgs fw = fm;
-            fw.comp_len = lens2.as<uint32_t>();
-            fw.comp_err = errs2.as<int>();
-            fw.stats = nullptr;
-            const double waves_mixed_us = time_launches([&] { gpu::LaunchCodecWaves(fw, s); }, iters, s);
-            // throughput when batches overlap, as on the RPC path (several
-            // batches in flight on the pool's streams): 4 streams, one mixed
-            // launch each per round
-            hipStream_t ss[4];
-            for (auto& x : ss) hipStreamCreateWithFlags(&x, hipStreamNonBlocking);
-            auto overlapped = [&](auto launch) {
-                for (auto& x : ss) launch(x);
-                for (auto& x : ss) hipStreamSynchronize(x);
-                const int64_t t0 = monotonic_us();
-                for (int it = 0; it < iters; ++it)
-                    for (auto& x : ss) launch(x);
-                for (auto& x : ss) hipStreamSynchronize(x);
-                return (double)(monotonic_us() - t0) / iters;
-            };
-            gpu::FusedCodecArgs fm2 = fm;
-            fm2.stats = nullptr;
-            const double fused_x4_us = overlapped([&](hipStream_t x) { gpu::LaunchFusedCodec(fm2, x); });
-            const double waves_x4_us = overlapped([&](hipStream_t x) { gpu::LaunchCodecWaves(fw, x); });
-            for (auto& x : ss) hipStreamDestroy(x);
-            hipStreamDestroy(s);
-            py::gil_scoped_acquire gil;
-            out["waves_mixed_us"] = waves_mixed_us;
-            out["fused_mixed_x4_us"] = fused_x4_us;
-            out["waves_mixed_x4_us"] = waves_x4_us;
-            const uint64_t launches = (uint64_t)iters + 1;
-            out["blocks"] = n;
-            out["fused_compress_us"] = comp_us;
-            out["fused_decode_us"] = dec_us;
-            out["fused_mixed_us"] = mixed_us;
-            out["old_compress_us"] = old_comp_us;
-            out["old_decode_us"] = old_dec_us;
-            out["fused_ratio"] = (double)all.size() / (double)std::max<uint64_t>(1, csum);
-            out["old_ratio"] = (double)all.size() / (double)std::max<uint64_t>(1, csum2);
-            out["verified"] = ok;
-            out["compress_rounds_avg"] = (double)st[0] / (double)(n * (launches * 2));
-            out["compress_rounds_max"] = st[1];
-            out["decode_rounds_avg"] = (double)st[2] / (double)(n * (launches * 2));
-            out["decode_rounds_max"] = st[3];
-            // cumulative shader-clock stamps of the first block / piece (the
-            // mixed launch ran last)
-            py::list cs, ds;
-            for (int k = 0; k < 10; ++k) cs.append(st[4 + k]);
-            for (int k = 0; k < 10; ++k) ds.append(st[16 + k]);
-            out["compress_phase_cycles"] = cs;
-            out["decode_phase_cycles"] = ds;
-        }
-        return out;
-    }, py::arg("bodies"), py::arg("block") = 4096, py::arg("iters") = 50, py::arg("device") = 0);
     g.def("device_snappy_layout", [](uint64_t len) {
         const gpu::DeviceSnappyLayout l = gpu::DeviceSnappyLayoutFor(len);
         return py::make_tuple(l.block_ulen, l.stride, l.nblocks);
@@ -413,13 +238,15 @@ void bind_gpu_ops(py::module_& g) {
         return d;
     });
     g.def("batched_copy_crc32c_launch", [](const std::vector<uintptr_t>& srcs, const std::vector<uintptr_t>& dsts,
-                                           const std::vector<uint64_t>& lens, uintptr_t out, uintptr_t stream) {
+                                           const std::vector<uint64_t>& lens, uintptr_t out, uintptr_t stream,
+                                           bool mfma) {
         if (srcs.size() != lens.size() || dsts.size() != lens.size()) throw std::invalid_argument("size mismatch");
         std::vector<gpu::Segment> segs(lens.size());
         for (size_t i = 0; i < lens.size(); ++i) segs[i] = gpu::Segment{(const void*)srcs[i], (void*)dsts[i], lens[i]};
-        check(gpu::LaunchBatchedCopyCrc32c(segs.data(), (int)segs.size(), (uint32_t*)out, as_stream(stream)),
+        check(gpu::LaunchBatchedCopyCrc32c(segs.data(), (int)segs.size(), (uint32_t*)out, as_stream(stream), mfma),
               "batched_copy_crc32c");
-    }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("out"), py::arg("stream") = 0);
+    }, py::arg("srcs"), py::arg("dsts"), py::arg("lens"), py::arg("out"), py::arg("stream") = 0,
+       py::arg("mfma") = true);
     g.def("pb_scan_launch", [](uintptr_t buf, uint64_t buf_len, uintptr_t offsets, int64_t n, uint32_t max_fields,
                                uintptr_t fields, uintptr_t nfields, uintptr_t stream) {
         check(gpu::LaunchPbScan((const uint8_t*)buf, buf_len, (const int64_t*)offsets, n, max_fields,

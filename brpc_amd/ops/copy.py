@@ -19,10 +19,11 @@ def batched_copy(srcs, dsts):
                                    [nbytes(s) for s in srcs], stream_handle(dev))
 
 
-def batched_copy_crc32c(srcs, dsts):
+def batched_copy_crc32c(srcs, dsts, mfma=True):
     """Fused: dsts[i][:] = srcs[i][:] and returns the standard CRC32C of each
     source (int64 device tensor) — one read of the bytes (the pull kernel of
-    the xGMI transport's verified receives)."""
+    the xGMI transport's verified receives). mfma: the CRC runs on the matrix
+    cores (the default; False: the byte-table kernel)."""
     import torch
     if len(srcs) != len(dsts):
         raise ValueError("srcs/dsts length mismatch")
@@ -37,5 +38,5 @@ def batched_copy_crc32c(srcs, dsts):
     # no zeroing needed: the kernel stores each finished CRC (fold_segment_crc)
     out = torch.empty(len(srcs), dtype=torch.int32, device=dev)
     native.gpu.batched_copy_crc32c_launch([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts],
-                                          [nbytes(s) for s in srcs], out.data_ptr(), stream_handle(dev))
+                                          [nbytes(s) for s in srcs], out.data_ptr(), stream_handle(dev), mfma)
     return out.to(torch.int64) & 0xFFFFFFFF

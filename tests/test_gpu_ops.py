@@ -412,20 +412,44 @@ def test_gpu_process_echo_handler_bench_shape(dev, device_attachment):
         s.stop()
 
 
-def test_batched_copy_crc32c_fused(dev):
-    """The fused pull+checksum kernel: bytes copied exactly and CRC32C equal
-    to the host SSE4.2 value, aligned and misaligned segments alike."""
+@pytest.mark.parametrize("mfma", [True, False])
+def test_batched_copy_crc32c_fused(dev, mfma):
+    """The fused pull+checksum kernels (CRC on the matrix cores, and on byte
+    tables): bytes copied exactly, nothing written around the destination,
+    and CRC32C equal to the host SSE4.2 value, aligned and misaligned
+    segments alike."""
     from brpc_amd.ops import batched_copy_crc32c, crc32c_host
     big = torch.randint(0, 256, (1 << 21,), dtype=torch.uint8, device=dev)
-    cases = [(0, 1), (3, 15), (0, 16), (5, 4099), (1, 65521), (16, 1 << 20), (7, (1 << 20) + 333)]
+    cases = [(0, 1), (3, 15), (0, 16), (5, 4099), (1, 65521), (16, 1 << 20), (7, (1 << 20) + 333), (0, 0),
+             (9, 31), (2, 33), (0, 2048), (11, 4096 + 7), (0, 16384), (13, 16384 + 1), (0, 3 * 16384 - 5)]
     srcs = [big[o:o + n] for o, n in cases]
     outs = [torch.zeros(n + 32, dtype=torch.uint8, device=dev) for _, n in cases]
-    dsts = [outs[i][3 + i:3 + i + n] for i, (_, n) in enumerate(cases)]
-    crcs = batched_copy_crc32c(srcs, dsts).cpu().tolist()
+    dsts = [outs[i][3 + i % 8:3 + i % 8 + n] for i, (_, n) in enumerate(cases)]
+    crcs = batched_copy_crc32c(srcs, dsts, mfma=mfma).cpu().tolist()
     torch.cuda.synchronize()
-    for s, d, c in zip(srcs, dsts, crcs):
-        assert torch.equal(s, d)
-        assert c == crc32c_host(s.cpu().numpy().tobytes())
+    for i, (s, d, c) in enumerate(zip(srcs, dsts, crcs)):
+        assert torch.equal(s, d), i
+        assert c == crc32c_host(s.cpu().numpy().tobytes()), i
+        o = 3 + i % 8
+        assert int(outs[i][:o].sum()) == 0 and int(outs[i][o + s.numel():].sum()) == 0, i
+
+
+@pytest.mark.parametrize("mfma", [True, False])
+def test_copy_crc32c_checksum_only_segments(dev, mfma):
+    """A null destination is a checksum-only segment (the verify path of
+    payloads that stay where they are): the CRC is right and nothing is
+    written."""
+    from brpc_amd import native
+    from brpc_amd.ops import crc32c_host
+    from brpc_amd.ops._common import stream_handle
+    sizes = [5, 4096, 16384 + 77, 1 << 20]
+    srcs = [torch.randint(0, 256, (n + 3,), dtype=torch.uint8, device=dev)[3:] for n in sizes]
+    out = torch.zeros(len(sizes), dtype=torch.int32, device=dev)
+    native.gpu.batched_copy_crc32c_launch([s.data_ptr() for s in srcs], [0] * len(sizes), sizes, out.data_ptr(),
+                                          stream_handle(dev), mfma)
+    torch.cuda.synchronize()
+    got = [(int(x) & 0xFFFFFFFF) for x in out.cpu().tolist()]
+    assert got == [crc32c_host(s.cpu().numpy().tobytes()) for s in srcs]
 
 
 def test_rpcz_annotates_device_pulls(dev, tmp_path):
@@ -457,7 +481,8 @@ def test_rpcz_annotates_device_pulls(dev, tmp_path):
         s.stop()
 
 
-def test_crc_kernels_need_no_zeroed_output(dev):
+@pytest.mark.parametrize("mfma", [True, False])
+def test_crc_kernels_need_no_zeroed_output(dev, mfma):
     """The copy+CRC kernel folds chunk CRCs through a per-stream scratch that
     every launch leaves zeroed, and STORES each result: garbage in the output
     buffer, repeated launches on one stream and multi-chunk segments give the
@@ -472,7 +497,7 @@ def test_crc_kernels_need_no_zeroed_output(dev):
     for rep in range(3):
         out = torch.full((len(sizes),), 0x5A5A5A5A, dtype=torch.int32, device=dev)
         native.gpu.batched_copy_crc32c_launch([s.data_ptr() for s in srcs], [d.data_ptr() for d in dsts], sizes,
-                                              out.data_ptr(), stream_handle(dev))
+                                              out.data_ptr(), stream_handle(dev), mfma)
         torch.cuda.synchronize()
         got = [(int(x) & 0xFFFFFFFF) for x in out.cpu().tolist()]
         assert got == want, rep
