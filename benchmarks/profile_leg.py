@@ -36,7 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", default="gpu_handler",
                     choices=["gpu_handler", "host_64k", "dev_64k", "echo_32b", "rccl_64k", "lat_100qps", "grpc_cpu",
-                             "grpc_gpu", "baidu_cpu", "baidu_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu", "dev_snappy", "grpc_dev_snappy", "grpc_dev_64k",
+                             "grpc_gpu", "baidu_cpu", "baidu_gpu", "ids_baidu_cpu", "ids_baidu_gpu", "ids_json_cpu", "ids_json_gpu", "dev_snappy", "grpc_dev_snappy", "grpc_dev_64k", "dev_64k_verify",
                              "dev_1m_verify"])
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--body", default="text", help="echo body kind of the codec legs: text, random, const")
@@ -89,6 +89,8 @@ def main():
                   "attachment_pb": True, "device_scan": True, "device_compress": 1})
         if a.leg == "grpc_dev_snappy":
             o["protocol"] = "h2:grpc"
+    if a.leg == "dev_64k_verify":
+        o.update({"attachment_size": 65536, "device_attachment": True, "verify_device_payload": True})
     if a.leg == "dev_1m_verify":
         # 1 MiB HBM attachments, CRC32C-verified on the device (fused into the pull)
         o.update({"attachment_size": 1 << 20, "device_attachment": True, "verify_device_payload": True})
