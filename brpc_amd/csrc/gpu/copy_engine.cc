@@ -35,7 +35,13 @@ DEFINE_bool(copy_engine_done_words, false,
             "event completion is as fast (profiles/r6_xproc_diagnosis.txt)");
 
 DEFINE_bool(copy_engine_crc_mfma, true,
-            "verified pulls fold their CRC32C on the matrix cores (copy_crc32c_mfma_kernel); false: byte tables");
+            "verified pulls of at least -copy_engine_crc_mfma_min_bytes per launch fold their CRC32C on the matrix "
+            "cores (copy_crc32c_mfma_kernel); false: always the byte-table kernel");
+DEFINE_int64(copy_engine_crc_mfma_min_bytes, 2 << 20,
+             "launch size from which verified pulls take the MFMA CRC kernel: it won on 1 MiB payload batches "
+             "(135k vs 122k QPS, 57 vs 64 us per launch) and lost on 64 KiB ones (392k vs 421k, 9.9 vs 8.0 us), "
+             "where the A-fragment staging and MFMA chain add latency to one-chunk workgroups "
+             "(profiles/r6_crc_kernels.txt)");
 DEFINE_int32(copy_engine_max_inflight, 4,
              "launches of one device's copy engine in flight at once (0: no limit). Submissions that find the "
              "limit reached join the open batch, which the first waiter of the next completed batch launches: "
@@ -203,9 +209,11 @@ void launch(Batch* b, int device) {
             b->crc_cap = std::max<size_t>((size_t)b->nmsg, 64);
             b->crc_host = static_cast<uint32_t*>(PinnedAlloc(b->crc_cap * sizeof(uint32_t)));
         }
+        uint64_t launch_bytes = 0;
+        for (const Segment& g : b->segs) launch_bytes += g.len;
+        const bool mfma = FLAGS_copy_engine_crc_mfma && launch_bytes >= (uint64_t)FLAGS_copy_engine_crc_mfma_min_bytes;
         if (!b->crc_host ||
-            LaunchBatchedCopyCrc32cMessages(b->segs.data(), b->msg_of.data(), (int)n, b->crc_host, s, done,
-                                            FLAGS_copy_engine_crc_mfma) != 0) {
+            LaunchBatchedCopyCrc32cMessages(b->segs.data(), b->msg_of.data(), (int)n, b->crc_host, s, done, mfma) != 0) {
             rc = -1;
         }
     } else if (rc == 0) {

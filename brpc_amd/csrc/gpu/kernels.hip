@@ -25,6 +25,7 @@
 #include <mutex>
 #include <vector>
 
+#include "base/crc32c.h"
 #include "gpu/kernels.h"
 
 namespace mrpc {
@@ -44,6 +45,8 @@ struct CrcTables {
 
 __constant__ uint32_t c_lane_shift[256];
 __constant__ uint32_t c_x2n[64];
+constexpr int kChunkPows = 128;             // chunks after a chunk inside its segment (2 MiB)
+__constant__ uint32_t c_chunk_pow[kChunkPows];  // x^(8*kChunkBytes*a)
 
 __device__ __forceinline__ uint32_t mult_mod_p(uint32_t a, uint32_t b) {
     uint32_t p = 0;
@@ -84,6 +87,11 @@ struct SegBatch {
     uint32_t msg_chunks[kInlineSegments]; // by message slot: chunks of all its segments
     uint8_t msg[kInlineSegments];         // message slot of the segment
     uint8_t first_of_msg[kInlineSegments];
+    // CRC batches: x^(8*tail) per segment and each message's init/final term
+    // (x^(8*len)*~0 ^ ~0), computed on the host by fill_batch so the one
+    // lane that folds a chunk does two multiplies, not a log-time power
+    uint32_t tail_poly[kInlineSegments];
+    uint32_t msg_init[kInlineSegments];
     // completion word (DoneWord in kernels.h); null: the launch has none
     uint32_t* done_ctr;
     unsigned long long* done_word;
@@ -139,8 +147,8 @@ __device__ __forceinline__ uint32_t crc_word8(uint32_t crc, uint32_t lo, uint32_
 // (device memory, or pinned host memory the CPU reads after the batch's
 // event: no D2H copy).
 __device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch, int m, uint32_t chunks,
-                                                 uint32_t acc, uint32_t* __restrict__ out) {
-    if (chunks == 1) {
+                                                 uint32_t acc, uint32_t* __restrict__ out, uint32_t count = 1) {
+    if (chunks == count) {  // this fold carries every chunk of the message
         out[m] = acc;
         return;
     }
@@ -152,12 +160,18 @@ __device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch,
     uint32_t* crc_word = scratch + 2 * m;
     uint32_t* cnt_word = scratch + 2 * m + 1;
     __hip_atomic_fetch_xor(crc_word, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t before = __hip_atomic_fetch_add(cnt_word, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (before + 1 == chunks) {
+    const uint32_t before = __hip_atomic_fetch_add(cnt_word, count, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (before + count == chunks) {
         const uint32_t v = __hip_atomic_exchange(crc_word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(cnt_word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         out[m] = v;
     }
+}
+
+// x^(8*kChunkBytes*a): a table lookup for the chunk counts of segments up
+// to 2 MiB, the log-time power beyond.
+__device__ __forceinline__ uint32_t chunk_shift_poly(uint32_t a) {
+    return a < (uint32_t)kChunkPows ? c_chunk_pow[a] : shift_bytes_poly((uint64_t)a * kChunkBytes);
 }
 
 // One chunk's raw CRC: shift it by the bytes that follow the chunk inside its
@@ -167,12 +181,10 @@ __device__ __forceinline__ void fold_segment_crc(uint32_t* __restrict__ scratch,
 __device__ __forceinline__ void fold_chunk(const SegBatch& b, int seg, uint32_t after, uint32_t seg_chunks,
                                            uint32_t acc, uint32_t* __restrict__ scratch,
                                            uint32_t* __restrict__ out) {
-    const uint64_t shift = (uint64_t)after * kChunkBytes + b.tail[seg];
-    if (shift) acc = mult_mod_p(shift_bytes_poly(shift), acc);
+    if (after) acc = mult_mod_p(chunk_shift_poly(after), acc);
+    if (b.tail[seg]) acc = mult_mod_p(b.tail_poly[seg], acc);
     const int m = b.msg[seg];
-    if (after == seg_chunks - 1 && b.first_of_msg[seg]) {
-        acc ^= mult_mod_p(shift_bytes_poly(b.msg_len[m]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
-    }
+    if (after == seg_chunks - 1 && b.first_of_msg[seg]) acc ^= b.msg_init[m];
     fold_segment_crc(scratch, m, b.msg_chunks[m], acc, out);
 }
 
@@ -367,6 +379,7 @@ typedef int i32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kGroupBytes = 2048;                       // 32 columns x 64 B
 static_assert(kChunkBytes == 2 * kGroupBytes * (kThreads / 64), "copy_crc32c_mfma_kernel: 2 groups per wave");
+static_assert(kChunkBytes == (1u << 14), "copy_crc32c_mfma_kernel: Horner constant x^(8*kChunkBytes) = c_x2n[17]");
 constexpr int kGroupsPerChunk = 32;
 constexpr uint64_t kMfmaChunk = (uint64_t)kGroupBytes * kGroupsPerChunk;  // 64 KiB per wave
 
@@ -388,10 +401,13 @@ __device__ __forceinline__ i8x16 expand16(uint32_t bits) {
     return r.v;
 }
 
-// Rare path (leading partial group / unaligned segment end), kept out of
-// line so it does not inflate the hot loop's register allocation.
-__device__ __noinline__ void fetch_bytes_slow(const uint8_t* base, int64_t lbeg, uint32_t* w) {
+// Rare path (leading partial group / unaligned segment end). Inlined with
+// w[] by reference so the array stays in registers: an out-of-line helper
+// taking a pointer forced it into 80 bytes of per-lane scratch.
+__device__ __forceinline__ void fetch_bytes_slow(const uint8_t* base, int64_t lbeg, uint32_t (&w)[8]) {
+#pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = 0;
+#pragma unroll
     for (int b = 0; b < 32; ++b) {
         const int64_t off = lbeg + b;
         if (off >= 0) w[b >> 2] |= (uint32_t)base[off] << (8 * (b & 3));
@@ -433,7 +449,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_mfma_kernel(
         const bool aligned = ((reinterpret_cast<uintptr_t>(base) + len) & 15) == 0;
         // lane's 32 bytes of group gg; bytes before the segment read as zero
         // (a zero prefix leaves the CRC register unchanged)
-        auto fetch = [&](int gg, uint32_t* w) {
+        auto fetch = [&](int gg, uint32_t(&w)[8]) {
             const int64_t gend = chunk_end - (int64_t)(kGroupsPerChunk - 1 - gg) * kGroupBytes;
             const int64_t lbeg = gend - kGroupBytes + 64 * c + 32 * h;
             if (lbeg >= 0 && aligned) {
@@ -506,16 +522,44 @@ __global__ void __launch_bounds__(kThreads) crc32c_mfma_kernel(
 // held the 1 MiB verified leg GPU-bound; the A fragments come from LDS,
 // staged once per workgroup, and a workgroup walks several chunks so the
 // staging amortises.
-__device__ __noinline__ void copy_bytes_slow(const uint8_t* base, uint8_t* dbase, int64_t lbeg, uint32_t* w) {
+// A lane's 32 bytes that start before the segment: bytes at offsets < 0
+// read as zero and are not stored. Fully unrolled so w[] stays in registers
+// (an out-of-line helper taking w by pointer put every lane's w[] in
+// scratch memory: 80 bytes of private segment per lane, ~230 GB/s).
+__device__ __forceinline__ void copy_bytes_slow(const uint8_t* base, uint8_t* dbase, int64_t lbeg, uint32_t (&w)[8]) {
+#pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = 0;
+#pragma unroll
     for (int b = 0; b < 32; ++b) {
         const int64_t off = lbeg + b;
         if (off >= 0) {
-            const uint8_t c = base[off];
-            if (dbase) dbase[off] = c;
-            w[b >> 2] |= (uint32_t)c << (8 * (b & 3));
+            const uint32_t c = base[off];
+            if (dbase) dbase[off] = (uint8_t)c;
+            w[b >> 2] |= c << (8 * (b & 3));
         }
     }
+}
+
+// A run of consecutive chunks of one segment, folded by thread 0: Horner
+// over the run (each new chunk follows the previous one), then ONE shift to
+// the message end and ONE atomic fold for the run, instead of a log-time
+// shift and two contended L2 atomics per 16 KiB chunk.
+struct ChunkRun {
+    int seg = -1;
+    uint32_t acc = 0, n = 0, after_last = 0;
+    bool has_first = false;  // the run holds the segment's first chunk
+};
+
+__device__ __forceinline__ void flush_run(const SegBatch& b, ChunkRun& r, uint32_t* __restrict__ scratch,
+                                          uint32_t* __restrict__ out) {
+    if (r.seg < 0) return;
+    uint32_t acc = r.acc;
+    if (r.after_last) acc = mult_mod_p(chunk_shift_poly(r.after_last), acc);
+    if (b.tail[r.seg]) acc = mult_mod_p(b.tail_poly[r.seg], acc);
+    const int m = b.msg[r.seg];
+    if (r.has_first && b.first_of_msg[r.seg]) acc ^= b.msg_init[m];
+    fold_segment_crc(scratch, m, b.msg_chunks[m], acc, out, r.n);
+    r = ChunkRun();
 }
 
 __global__ void __launch_bounds__(kThreads) copy_crc32c_mfma_kernel(SegBatch b, const CrcMfmaConsts* __restrict__ K,
@@ -524,13 +568,17 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_mfma_kernel(SegBatch b, 
     stamp_start(b);
     __shared__ i8x16 sa[16][64];
     __shared__ uint32_t wave_acc[kThreads / 64];
-    for (int i = threadIdx.x; i < 16 * 64; i += kThreads) (&sa[0][0])[i] = (&K->afrag[0][0])[i];
-    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int c = lane & 31;
     const int h = lane >> 5;
-    for (uint32_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    // a contiguous range of chunks per workgroup (one per workgroup up to
+    // the grid cap), so runs of one segment fold locally
+    const uint32_t per = (nchunks + gridDim.x - 1) / gridDim.x;
+    const uint32_t c0 = blockIdx.x * per;
+    const uint32_t c1 = min(nchunks, c0 + per);
+    ChunkRun run;  // thread 0's
+    for (uint32_t chunk = c0; chunk < c1; ++chunk) {
         const int seg = find_segment(b, chunk);
         const uint64_t len = b.len[seg];
         const uint8_t* base = static_cast<const uint8_t*>(b.src[seg]);
@@ -558,6 +606,13 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_mfma_kernel(SegBatch b, 
 #pragma unroll
                 for (int i = 0; i < 8; ++i) w[g][i] = 0;
             }
+        }
+        if (chunk == c0) {
+            // stage the A fragments (16 KiB from L2) behind the first
+            // chunk's loads, so a one-chunk workgroup (the RPC batches)
+            // waits for both latencies at once, not one after the other
+            for (int i = threadIdx.x; i < 16 * 64; i += kThreads) (&sa[0][0])[i] = (&K->afrag[0][0])[i];
+            __syncthreads();
         }
         if (dbase) {  // null destination: checksum only (uniform per segment)
 #pragma unroll
@@ -603,10 +658,19 @@ __global__ void __launch_bounds__(kThreads) copy_crc32c_mfma_kernel(SegBatch b, 
         __syncthreads();
         if (threadIdx.x == 0) {
             const uint32_t acc = wave_acc[0] ^ wave_acc[1] ^ wave_acc[2] ^ wave_acc[3];
-            fold_chunk(b, seg, after, seg_chunks, acc, scratch, out);
+            if (run.seg != seg) {
+                flush_run(b, run, scratch, out);
+                run.seg = seg;
+                run.has_first = k == 0;
+            }
+            // Horner: everything folded so far precedes this chunk by 16 KiB
+            run.acc = run.n ? mult_mod_p(c_x2n[17], run.acc) ^ acc : acc;  // x^(8*16384) = x^(2^17)
+            run.n += 1;
+            run.after_last = after;
         }
         __syncthreads();  // wave_acc is reused by the next chunk
     }
+    if (threadIdx.x == 0) flush_run(b, run, scratch, out);
     signal_done(b);
 }
 
@@ -936,6 +1000,11 @@ int ensure_tables_locked(int dev) {
     if (hipMemcpy(dt.t8, h.t8, sizeof(h.t8), hipMemcpyHostToDevice) != hipSuccess) return -1;
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_lane_shift), h.lane_shift, sizeof(h.lane_shift)) != hipSuccess) return -1;
     if (hipMemcpyToSymbol(HIP_SYMBOL(c_x2n), h.x2n, sizeof(h.x2n)) != hipSuccess) return -1;
+    {
+        uint32_t pows[kChunkPows];
+        for (int a = 0; a < kChunkPows; ++a) pows[a] = host_xpow((uint64_t)8 * kChunkBytes * a);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_chunk_pow), pows, sizeof(pows)) != hipSuccess) return -1;
+    }
     // ---- MFMA constants
     static CrcMfmaConsts m;
     static std::once_flag once;
@@ -1033,7 +1102,23 @@ uint32_t* stream_scratch(int dev, hipStream_t s) {
 // Fill a SegBatch with up to kInlineSegments segments; returns chunk count.
 // msg_of (optional, non-decreasing): the message each segment belongs to;
 // without it every segment is its own message.
-uint32_t fill_batch(SegBatch* b, const Segment* segs, int n, const int* msg_of = nullptr) {
+// x^(8n) mod P on the host, memoised per thread: RPC batches repeat a few
+// lengths (whole payloads, the bytes after a payload's head block).
+uint32_t host_shift_poly(uint64_t n) {
+    struct Entry {
+        uint64_t n = ~0ull;
+        uint32_t p = 0;
+    };
+    static thread_local Entry cache[64];
+    Entry& e = cache[(n ^ (n >> 13) ^ (n >> 29)) & 63];
+    if (e.n != n) {
+        e.n = n;
+        e.p = crc32c::ShiftBytesPoly((size_t)n);
+    }
+    return e.p;
+}
+
+uint32_t fill_batch(SegBatch* b, const Segment* segs, int n, const int* msg_of = nullptr, bool crc = false) {
     memset(b, 0, sizeof(*b));
     b->nseg = n;
     uint32_t c = 0;
@@ -1059,6 +1144,15 @@ uint32_t fill_batch(SegBatch* b, const Segment* segs, int n, const int* msg_of =
         if (i == n - 1 || b->msg[i] != b->msg[i + 1]) after = 0;
         b->tail[i] = after;
         after += segs[i].len;
+    }
+    if (crc) {
+        for (int i = 0; i < n; ++i) {
+            if (b->tail[i]) b->tail_poly[i] = host_shift_poly(b->tail[i]);
+            if (b->first_of_msg[i]) {
+                const int m = b->msg[i];
+                b->msg_init[m] = crc32c::MultModP(host_shift_poly(b->msg_len[m]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+            }
+        }
     }
     return c;
 }
@@ -1096,7 +1190,7 @@ int LaunchCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStream_t s) {
     for (int i = 0; i < nseg; i += kInlineSegments) {
         const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;
         SegBatch b;
-        const uint32_t chunks = fill_batch(&b, segs + i, n);
+        const uint32_t chunks = fill_batch(&b, segs + i, n, nullptr, true);
         hipLaunchKernelGGL(crc32c_kernel, dim3(chunks), dim3(kThreads), 0, s, b, g_tables[dev].t8, scratch, out + i);
         if (hipGetLastError() != hipSuccess) return -1;
     }
@@ -1151,7 +1245,7 @@ int LaunchBatchedCopyCrc32c(const Segment* segs, int nseg, uint32_t* out, hipStr
     for (int i = 0; i < nseg; i += kInlineSegments) {
         const int n = nseg - i < kInlineSegments ? nseg - i : kInlineSegments;
         SegBatch b;
-        const uint32_t chunks = fill_batch(&b, segs + i, n);
+        const uint32_t chunks = fill_batch(&b, segs + i, n, nullptr, true);
         launch_copy_crc(b, chunks, dev, scratch, out + i, s, mfma);
         if (hipGetLastError() != hipSuccess) return -1;
     }
@@ -1169,7 +1263,7 @@ int LaunchBatchedCopyCrc32cMessages(const Segment* segs, const int* msg_of, int 
     for (int i = 0, e = 0; i < nseg; i = e) {
         if (!next_group(msg_of, nseg, i, &e)) return -2;
         SegBatch b;
-        const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of + i);
+        const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of + i, true);
         if (done && e == nseg) set_done(&b, *done);
         launch_copy_crc(b, chunks, dev, scratch, out + msg_of[i], s, mfma);
         if (hipGetLastError() != hipSuccess) return -1;
@@ -1583,7 +1677,7 @@ int ResidentSubmit(ResidentRing* r, const Segment* segs, const int* msg_of, int 
             }
         }
         SegBatch b;
-        const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of ? msg_of + i : nullptr);
+        const uint32_t chunks = fill_batch(&b, segs + i, e - i, msg_of ? msg_of + i : nullptr, crc_out != nullptr);
         memcpy(&sl.batch, &b, sizeof(b));
         sl.crc_out = crc_out ? crc_out + (msg_of ? msg_of[i] : i) : nullptr;
         sl.chunks = chunks;

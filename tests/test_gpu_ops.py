@@ -434,6 +434,32 @@ def test_batched_copy_crc32c_fused(dev, mfma):
         assert int(outs[i][:o].sum()) == 0 and int(outs[i][o + s.numel():].sum()) == 0, i
 
 
+@pytest.mark.parametrize("mfma", ["true", "false"])
+@pytest.mark.parametrize("size", [4096, 65536, 100003, 1 << 20])
+def test_verified_device_pulls_over_rpc(dev, mfma, size):
+    """-verify_device_payload on the RPC path with either CRC kernel: the
+    sender's device CRC and the receiver's fused pull+CRC agree on every
+    payload (no CRC failure), and the echoed bytes are right."""
+    from brpc_amd import native
+    from brpc_amd.models import start_echo_server
+    native.set_flag("copy_engine_crc_mfma", mfma)
+    native.set_flag("copy_engine_crc_mfma_min_bytes", "0")  # every launch takes the chosen kernel
+    s = start_echo_server("127.0.0.1:0", gpu_device=0)
+    try:
+        before = native.gpu.xgmi_stats()["crc_failures"]
+        p = native.Press({"server": s.address, "concurrency": 16, "attachment_size": size, "device_attachment": True,
+                          "verify_device_payload": True, "gpu_device": 0, "check_echo": True, "check_every": 1,
+                          "max_retry": 0})
+        p.run_requests(400)
+        st = p.stats()
+        assert st["success"] == 400 and st["error"] == 0, (st["error_codes"], st["last_error"])
+        assert native.gpu.xgmi_stats()["crc_failures"] == before
+    finally:
+        s.stop()
+        native.set_flag("copy_engine_crc_mfma", "true")
+        native.set_flag("copy_engine_crc_mfma_min_bytes", str(2 << 20))
+
+
 @pytest.mark.parametrize("mfma", [True, False])
 def test_copy_crc32c_checksum_only_segments(dev, mfma):
     """A null destination is a checksum-only segment (the verify path of
