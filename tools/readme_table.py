@@ -52,16 +52,19 @@ def rows(d):
                                                                                 d.get("gbytes_per_s_1MB", 0),
                                                                                 d.get("p99_us_1MB")),
             us(d, "echo_1MB"))
-    for body in ("text", "random"):
-        q = d.get("device_snappy_64KB_%s_qps" % body)
-        if q is None:
-            continue
-        dev = d.get("device_snappy_64KB_%s_device" % body) or {}
-        add("Device-body codec, 64 KiB protobuf in HBM, %s body (snappy on the device both ways, pb-indexed)" % body,
-            "%s QPS, ratio %s, encoded %.0f%% / decoded %.0f%% of payloads" % (
-                k(q), dev.get("device_ratio", "?"), 100 * d.get("device_snappy_64KB_%s_encoded_fraction" % body, 0),
-                100 * d.get("device_snappy_64KB_%s_decoded_fraction" % body, 0)),
-            us(d, "device_snappy_64KB_%s" % body))
+    for pre, proto in (("", "baidu_std"), ("grpc_", "h2/gRPC")):
+        for body in ("text", "random"):
+            leg = "%sdevice_snappy_64KB_%s" % (pre, body)
+            q = d.get(leg + "_qps")
+            if q is None:
+                continue
+            dev = d.get(leg + "_device") or {}
+            add("Device-body codec over %s, 64 KiB protobuf in HBM, %s body (snappy on the device both ways, "
+                "pb-indexed)" % (proto, body),
+                "%s QPS, ratio %s, encoded %.0f%% / decoded %.0f%% of payloads" % (
+                    k(q), dev.get("device_ratio", "?"), 100 * d.get(leg + "_encoded_fraction", 0),
+                    100 * d.get(leg + "_decoded_fraction", 0)),
+                us(d, leg))
     for proto in ("grpc", "baidu_std"):
         for body in ("text", "random"):
             base = "%s_snappy_64KB_%s" % (proto, body)
