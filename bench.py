@@ -969,6 +969,12 @@ def main(argv=None):
                 "bad_tables": c1["bad_tables"] - c0["bad_tables"],
                 "decode_errors": c1["decode_errors"] - c0["decode_errors"],
             }
+            # where a codec step's latency goes, per request (us): waiting
+            # for a launch, launch API, launch -> completion seen, wake-up
+            nt = b1.get("timed", 0) - b0.get("timed", 0)
+            if nt > 0:
+                r["device"]["codec_step_us"] = {
+                    k: round((b1[k + "_us"] - b0[k + "_us"]) / nt, 1) for k in ("queue", "api", "gpu", "wake")}
             # what fraction of the payloads actually went through the codec
             # (the random body is mostly lent raw by the adaptive skip)
             r["device"]["encoded_fraction"] = round(r["device"]["encodes"] / payloads, 4) if payloads else None

@@ -9,6 +9,7 @@
 #include <mutex>
 
 #include "base/flags.h"
+#include "base/time.h"
 #include "base/logging.h"
 #include "fiber/butex.h"
 #include "gpu/gpu.h"
@@ -83,6 +84,9 @@ struct CBatch {
     std::atomic<int>* butex = nullptr;
     hipEvent_t ev = nullptr;
     std::atomic<int> refs{0};
+    // latency breakdown (monotonic us): launch began, event recorded, the
+    // poller saw the completion
+    int64_t launch_us = 0, launched_us = 0, done_us = 0;
 };
 
 struct Engine {
@@ -121,6 +125,10 @@ void retire_done(Engine& e) {
 
 Engine g_engine[kMaxDev];
 std::atomic<int64_t> g_requests{0}, g_launches{0}, g_run_chunks{0}, g_dec_chunks{0}, g_fused_launches{0};
+// per request, summed: waiting for a launch, the batch's launch API time,
+// launch -> completion seen by the poller (device time + queueing + poll),
+// completion seen -> requester running again
+std::atomic<int64_t> g_queue_us{0}, g_api_us{0}, g_gpu_us{0}, g_wake_us{0}, g_timed{0};
 
 CBatch* new_batch(Engine& e) {
     if (!e.spare.empty()) {
@@ -333,7 +341,8 @@ bool launch(CBatch* b, int device) {
         if (s) SyncStream(s);
         return false;
     }
-    WatchEvent(b->ev, b->butex, nullptr, kEventCodec);
+    b->done_us = 0;
+    WatchEvent(b->ev, b->butex, &b->done_us, kEventCodec);
     return true;
 }
 
@@ -361,7 +370,9 @@ void pump(Engine& e, int device) {
             // complete, and its requesters drop their refs, before we get back
             cur->refs.fetch_add(1, std::memory_order_relaxed);
         }
+        cur->launch_us = monotonic_us();
         const bool ok = launch(cur, device);
+        cur->launched_us = monotonic_us();
         if (!ok) {
             LOG_EVERY_SECOND(ERROR) << "codec batch of " << cur->reqs.size() << " requests failed on device " << device;
             cur->butex->store(-1, std::memory_order_release);
@@ -382,6 +393,7 @@ int RunCodecRequest(CodecRequest* r, int device) {
     if (device < 0 || device >= kMaxDev || Init(device) != 0) return -1;
     Engine& e = g_engine[device];
     g_requests.fetch_add(1, std::memory_order_relaxed);
+    const int64_t submit_us = monotonic_us();
     CBatch* mine;
     size_t idx = 0;
     {
@@ -398,6 +410,14 @@ int RunCodecRequest(CodecRequest* r, int device) {
     pump(e, device);
     while (mine->butex->load(std::memory_order_acquire) == 0) fiber::butex_wait(mine->butex, 0);
     const int rc = mine->butex->load(std::memory_order_acquire) == 1 ? 0 : -1;
+    if (rc == 0 && mine->done_us > 0) {
+        const int64_t woke = monotonic_us();
+        g_queue_us.fetch_add(std::max<int64_t>(0, mine->launch_us - submit_us), std::memory_order_relaxed);
+        g_api_us.fetch_add(mine->launched_us - mine->launch_us, std::memory_order_relaxed);
+        g_gpu_us.fetch_add(std::max<int64_t>(0, mine->done_us - mine->launched_us), std::memory_order_relaxed);
+        g_wake_us.fetch_add(std::max<int64_t>(0, woke - mine->done_us), std::memory_order_relaxed);
+        g_timed.fetch_add(1, std::memory_order_relaxed);
+    }
     if (rc == 0) {
         const size_t c0 = mine->comp_first[idx], d0 = mine->decomp_first[idx];
         r->comp_len.assign(mine->comp_len.p + c0, mine->comp_len.p + c0 + r->comp.size());
@@ -441,6 +461,11 @@ CodecBatchStats GetCodecBatchStats() {
     s.run_chunks = g_run_chunks.load(std::memory_order_relaxed);
     s.decode_chunks = g_dec_chunks.load(std::memory_order_relaxed);
     s.fused_launches = g_fused_launches.load(std::memory_order_relaxed);
+    s.timed = g_timed.load(std::memory_order_relaxed);
+    s.queue_us = g_queue_us.load(std::memory_order_relaxed);
+    s.api_us = g_api_us.load(std::memory_order_relaxed);
+    s.gpu_us = g_gpu_us.load(std::memory_order_relaxed);
+    s.wake_us = g_wake_us.load(std::memory_order_relaxed);
     return s;
 }
 

@@ -99,6 +99,9 @@ int RunCodecRequest(CodecRequest* r, int device);
 
 struct CodecBatchStats {
     int64_t requests = 0, launches = 0, run_chunks = 0, decode_chunks = 0, fused_launches = 0;
+    // latency breakdown summed over `timed` requests (us): waiting for a
+    // launch, launch API, launch -> completion seen, completion -> resumed
+    int64_t timed = 0, queue_us = 0, api_us = 0, gpu_us = 0, wake_us = 0;
 };
 CodecBatchStats GetCodecBatchStats();
 

@@ -735,6 +735,11 @@ PYBIND11_MODULE(_native, m) {
         d["run_chunks"] = s.run_chunks;
         d["decode_chunks"] = s.decode_chunks;
         d["fused_launches"] = s.fused_launches;
+        d["timed"] = s.timed;
+        d["queue_us"] = s.queue_us;
+        d["api_us"] = s.api_us;
+        d["gpu_us"] = s.gpu_us;
+        d["wake_us"] = s.wake_us;
         return d;
     });
     // numeric run (vector layout bytes) -> varints / JSON numbers on the device (tests)
