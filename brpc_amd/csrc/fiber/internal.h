@@ -119,6 +119,9 @@ public:
         if (_waiters.load(std::memory_order_seq_cst) == 0 && FLAGS_fiber_signal_parked_only) return 0;
         return futex_wake_private(&_pending, n);
     }
+    // moves the state without waking anyone: a worker about to park on a
+    // snapshot older than this returns from wait() at once
+    void bump() { _pending.fetch_add(2, std::memory_order_seq_cst); }
     State get_state() { return State{_pending.load(std::memory_order_acquire)}; }
     void wait(const State& expected) {
         _waiters.fetch_add(1, std::memory_order_seq_cst);

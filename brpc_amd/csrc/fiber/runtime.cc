@@ -76,6 +76,8 @@ DEFINE_int32(fiber_idle_spin_us, 0,
              "an idle worker polls for new fibers this long before sleeping on its parking lot "
              "(trades CPU for futex-wakeup latency on the RPC round trip; 0 disables)");
 DEFINE_int32(fiber_max_spinning_workers, 2, "at most this many idle workers spin at once");
+DEFINE_bool(fiber_signal_skip_when_spinning, true,
+            "with -fiber_idle_spin_us > 0, a ready fiber wakes no parked worker while another worker spins");
 DEFINE_int32(fiber_worker_nap_us, 0,
              "an idle worker that ran a fiber within -fiber_worker_nap_window_ms sleeps on its parking lot with "
              "this timeout (us) and re-polls, so its core stays in shallow idle states (warm caches, us wakeups) "
@@ -613,8 +615,8 @@ static std::atomic<int> g_napping_workers{0};
 bool TaskGroup::spin_for_task(fiber_t* tid) {
     const int budget_us = FLAGS_fiber_idle_spin_us;
     if (budget_us <= 0) return false;
-    if (g_spinning_workers.fetch_add(1, std::memory_order_relaxed) >= FLAGS_fiber_max_spinning_workers) {
-        g_spinning_workers.fetch_sub(1, std::memory_order_relaxed);
+    if (g_spinning_workers.fetch_add(1, std::memory_order_seq_cst) >= FLAGS_fiber_max_spinning_workers) {
+        g_spinning_workers.fetch_sub(1, std::memory_order_seq_cst);
         return false;
     }
     const int64_t deadline = monotonic_ns() + (int64_t)budget_us * 1000;
@@ -629,7 +631,7 @@ bool TaskGroup::spin_for_task(fiber_t* tid) {
         if (_last_pl_state.stopped()) break;
         if ((++i & 7) == 0 && monotonic_ns() >= deadline) break;
     }
-    g_spinning_workers.fetch_sub(1, std::memory_order_relaxed);
+    g_spinning_workers.fetch_sub(1, std::memory_order_seq_cst);
     return got;
 }
 
@@ -1043,6 +1045,19 @@ bool TaskControl::steal_task(fiber_t* tid, uint64_t* seed, size_t offset) {
 void TaskControl::signal_task(int num_task) {
     if (num_task <= 0) return;
     if (num_task > 2) num_task = 2;
+    // A spinning worker will take the task: no FUTEX_WAKE. Without this
+    // every start_background() while any worker is parked paid a wake
+    // syscall (~1.5-2 us here, build/bin/mrpc_microbench fiber_create vs
+    // fiber_create_nosignal) and the woken worker parked again after one
+    // short fiber. Dekker pair, both sides seq_cst: bump every lot, then
+    // read the spinner count; a spinner drops out of the count, then parks
+    // on a snapshot taken before its last failed steal. Either we see it
+    // spinning (then the bump precedes its futex compare, which fails), or
+    // it had left the count and we wake as usual.
+    if (FLAGS_fiber_idle_spin_us > 0 && FLAGS_fiber_signal_skip_when_spinning) {
+        for (int i = 0; i < kParkingLots; ++i) _pl[i].bump();
+        if (g_spinning_workers.load(std::memory_order_seq_cst) > 0) return;
+    }
     int start = (int)(fast_rand_less_than(kParkingLots));
     for (int i = 0; i < kParkingLots && num_task > 0; ++i) {
         num_task -= _pl[(start + i) % kParkingLots].signal(1);
