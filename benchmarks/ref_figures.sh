@@ -1,0 +1,19 @@
+#!/bin/bash
+# The reference's other published echo figures (BASELINE.md rows besides the
+# headline), re-measured with build/bin/multi_threaded_echo_main on one host:
+# QPS vs client threads at 1 KB, pooled vs single connections at 16 B / 32 KB,
+# and 400 fiber senders at 32 B (the TimerThread figure).
+#   bash benchmarks/ref_figures.sh > gpurun_out/ref_figures.txt
+set -o pipefail
+B=build/bin/multi_threaded_echo_main
+run() {
+  echo -n "$1: "
+  shift
+  timeout -k 10 60 $B --duration_s 2 "$@" 2>/dev/null | grep "^qps=" || exit 1
+}
+for t in 1 8 64 256; do run "1KB single, $t pthreads" --thread_num $t --request_size 1024 --connection_type single; done
+run "16B single, 50 pthreads" --thread_num 50 --request_size 16 --connection_type single
+run "16B pooled, 50 pthreads" --thread_num 50 --request_size 16 --connection_type pooled
+run "32KB single, 50 pthreads" --thread_num 50 --request_size 32768 --connection_type single
+run "32KB pooled, 50 pthreads" --thread_num 50 --request_size 32768 --connection_type pooled
+run "32B single, 400 fibers" --thread_num 400 --use_fiber --request_size 32 --connection_type single

@@ -614,6 +614,8 @@ void BufPortal::return_cached_blocks() {
         _pending->dec_ref();
         _pending = nullptr;
     }
+    for (BufBlock* b : _spare) b->dec_ref();
+    _spare.clear();
 }
 
 ssize_t BufPortal::append_from_fd(int fd, size_t max_count) {
@@ -635,7 +637,13 @@ ssize_t BufPortal::append_from_fd(int fd, size_t max_count) {
         _pending = nullptr;
     }
     while (space < max_count && nb < kMaxIov) {
-        BufBlock* b = acquire_default_block();
+        BufBlock* b = nullptr;
+        if (!_spare.empty()) {
+            b = _spare.back();
+            _spare.pop_back();
+        } else {
+            b = acquire_default_block();
+        }
         if (!b) break;
         blocks[nb] = b;  // we own one ref
         iov[nb].iov_base = b->data;
@@ -660,6 +668,8 @@ ssize_t BufPortal::append_from_fd(int fd, size_t max_count) {
         // non-full block as the next pending block, release the others.
         if (!new_pending && !b->full()) {
             new_pending = b;
+        } else if (b->size == 0 && b->cap + kHeader == Buf::DEFAULT_BLOCK_SIZE && (size_t)kMaxIov > _spare.size()) {
+            _spare.push_back(b);  // untouched: the portal's ref moves to the spare list
         } else {
             b->dec_ref();
         }

@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "base/macros.h"
 
@@ -176,12 +177,19 @@ private:
 class BufPortal : public Buf {
 public:
     BufPortal() : _pending(nullptr) {}
+    BufPortal(const BufPortal&) = delete;  // owns refs of its pending and spare blocks
+    BufPortal& operator=(const BufPortal&) = delete;
     ~BufPortal();
     // readv up to max_count bytes. Returns bytes read (0 = EOF), -1 on error.
     ssize_t append_from_fd(int fd, size_t max_count);
     void return_cached_blocks();
 private:
-    BufBlock* _pending;  // chain of partially-filled blocks reused by the next read
+    BufBlock* _pending;  // the partially-filled block the next read continues
+    // Blocks a read sized for but did not fill, kept for the next read (as
+    // IOPortal keeps its block chain): a read of max_count bytes takes up to
+    // 64 blocks, and freeing the unused ones every call cost page faults and
+    // heap trims in the kernel (32 KiB echo: ~290 us of system time per RPC)
+    std::vector<BufBlock*> _spare;
 };
 
 // Block level helpers

@@ -280,3 +280,37 @@ TEST(BufMore, random_cuts_into_bufs_preserve_order) {
     for (auto& p : parts) joined.append(std::move(p));
     EXPECT_TRUE(joined.equals(want));
 }
+
+// A read sized for 512 KiB that finds 32 KiB keeps the untouched blocks for
+// the next read instead of freeing them (BufPortal::_spare): repeated reads
+// allocate no new blocks, and return_cached_blocks() gives them all back.
+TEST(BufMore, portal_keeps_unfilled_blocks_for_the_next_read) {
+    int fds[2];
+    ASSERT_EQ(pipe(fds), 0);
+    const std::string msg = pattern(32768, 21);
+    const int64_t blocks0 = Buf::block_count();
+    {
+        BufPortal portal;
+        int64_t after_first = 0;
+        for (int round = 0; round < 20; ++round) {
+            ASSERT_EQ(write(fds[1], msg.data(), msg.size()), (ssize_t)msg.size());
+            size_t got = 0;
+            while (got < msg.size()) {
+                const ssize_t r = portal.append_from_fd(fds[0], 524288);
+                ASSERT_TRUE(r > 0);
+                got += (size_t)r;
+            }
+            Buf out;
+            portal.cutn(&out, msg.size());
+            EXPECT_TRUE(out.equals(msg));
+            if (round == 0) after_first = Buf::block_count();
+            // later rounds reuse the spare blocks: no growth past the first
+            EXPECT_TRUE(Buf::block_count() <= after_first);
+        }
+        portal.return_cached_blocks();
+        EXPECT_TRUE(portal.empty());
+    }
+    close(fds[0]);
+    close(fds[1]);
+    EXPECT_TRUE(Buf::block_count() <= blocks0 + 8);  // at most the thread's block cache
+}
