@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "base/time.h"
+#include "builtin/cpu_profiler.h"
 #include "examples/common.h"
 
 DEFINE_int32(thread_num, 8, "concurrent senders");
@@ -19,6 +20,7 @@ DEFINE_double(duration_s, 1.0, "seconds to run");
 DEFINE_string(server, "", "ip:port of an external server (empty: start one in-process)");
 DEFINE_string(protocol, "baidu_std", "protocol");
 DEFINE_string(connection_type, "", "single / pooled / short");
+DEFINE_string(profile_folded, "", "write a CPU profile of the run (folded stacks) to this file");
 
 int main(int argc, char** argv) {
     mrpc::ParseCommandLineFlags(&argc, &argv);
@@ -71,7 +73,18 @@ int main(int argc, char** argv) {
         }
     }
     const int64_t t0 = mrpc::monotonic_us();
-    usleep((useconds_t)(FLAGS_duration_s * 1e6));
+    if (!FLAGS_profile_folded.empty()) {
+        std::string folded;
+        int64_t nsamples = 0;
+        mrpc::profiler::ProfileCpu(FLAGS_duration_s, 997, &folded, nullptr, &nsamples);
+        FILE* f = fopen(FLAGS_profile_folded.c_str(), "w");
+        if (f) {
+            fwrite(folded.data(), 1, folded.size(), f);
+            fclose(f);
+        }
+    } else {
+        usleep((useconds_t)(FLAGS_duration_s * 1e6));
+    }
     stop = true;
     for (auto& t : threads) t.join();
     for (auto t : fibers) mrpc::fiber::join(t);

@@ -95,9 +95,37 @@ Value& Value::operator[](const std::string& key) {
     return _obj.back().second;
 }
 
+namespace {
+// Bytes that need no escape are copied in runs: a word at a time while no
+// byte of it is a control character, '"' or '\\' (per-byte push_back was
+// 43% of an http echo of a 32 KiB string field).
+inline bool word_is_plain(uint64_t w) {
+    const uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
+    const uint64_t lt20 = (w - ones * 0x20) & ~w & highs;  // a byte < 0x20 (bytes >= 0x80 are plain)
+    const uint64_t q = w ^ (ones * '"'), b = w ^ (ones * '\\');
+    const uint64_t zq = (q - ones) & ~q & highs, zb = (b - ones) & ~b & highs;
+    return (lt20 | zq | zb) == 0;
+}
+inline bool byte_is_plain(unsigned char c) { return c >= 0x20 && c != '"' && c != '\\'; }
+}  // namespace
+
 void EscapeString(const std::string& s, std::string* out) {
+    out->reserve(out->size() + s.size() + 2);
     out->push_back('"');
-    for (unsigned char c : s) {
+    const char* p = s.data();
+    const char* const end = p + s.size();
+    while (p < end) {
+        const char* run = p;
+        while (end - p >= 8) {
+            uint64_t w;
+            memcpy(&w, p, 8);
+            if (!word_is_plain(w)) break;
+            p += 8;
+        }
+        while (p < end && byte_is_plain((unsigned char)*p)) ++p;
+        out->append(run, (size_t)(p - run));
+        if (p >= end) break;
+        const unsigned char c = (unsigned char)*p++;
         switch (c) {
         case '"': *out += "\\\""; break;
         case '\\': *out += "\\\\"; break;
@@ -106,14 +134,11 @@ void EscapeString(const std::string& s, std::string* out) {
         case '\t': *out += "\\t"; break;
         case '\b': *out += "\\b"; break;
         case '\f': *out += "\\f"; break;
-        default:
-            if (c < 0x20) {
-                char b[8];
-                snprintf(b, sizeof(b), "\\u%04x", c);
-                *out += b;
-            } else {
-                out->push_back((char)c);
-            }
+        default: {
+            char b[8];
+            snprintf(b, sizeof(b), "\\u%04x", c);
+            *out += b;
+        }
         }
     }
     out->push_back('"');
@@ -447,7 +472,11 @@ private:
         ++_p;  // opening quote
         for (;;) {  // runs without escapes or quotes go in one append
             const char* q = _p;
-            while (q < _end && *q != '"' && *q != '\\') ++q;
+            // the closing quote, then any backslash before it (both memchr)
+            const char* quote = (const char*)memchr(q, '"', (size_t)(_end - q));
+            if (!quote) quote = _end;
+            const char* bs = (const char*)memchr(q, '\\', (size_t)(quote - q));
+            q = bs ? bs : quote;
             s->append(_p, (size_t)(q - _p));
             _p = q;
             if (_p >= _end || *_p == '"') break;

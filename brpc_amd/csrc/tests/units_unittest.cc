@@ -602,6 +602,41 @@ TEST(JsonUnit, parse_types_and_serialize) {
     EXPECT_TRUE(v.find("missing") == nullptr);
 }
 
+// EscapeString copies plain runs a word at a time: every special byte at
+// every offset of an 8-byte word must still be escaped, and every string
+// must come back from the parser unchanged (runs split by the memchr scan).
+TEST(JsonUnit, escape_specials_at_every_word_offset_and_round_trip) {
+    const char specials[] = {'"', '\\', '\n', '\r', '\t', '\b', '\f', '\x01', '\x1f', '\x7f', (char)0x80, (char)0xff};
+    for (char sp : specials) {
+        for (size_t at = 0; at < 19; ++at) {
+            std::string raw(19, 'a');
+            raw[at] = sp;
+            std::string esc;
+            json::EscapeString(raw, &esc);
+            const unsigned char u = (unsigned char)sp;
+            if (u < 0x20 || sp == '"' || sp == '\\') {
+                EXPECT_TRUE(esc.size() > raw.size() + 2);  // escaped
+            } else {
+                EXPECT_EQ(esc, "\"" + raw + "\"");  // 0x7f and high bytes pass through
+            }
+            json::Value v;
+            ASSERT_TRUE(json::Parse(esc, &v));
+            EXPECT_EQ(v.as_string(), raw);
+        }
+    }
+    std::mt19937 rng(17);
+    for (int t = 0; t < 200; ++t) {
+        std::string raw(rng() % 300, '\0');
+        for (auto& c : raw) c = (rng() % 10 == 0) ? (char)(rng() % 0x22) : (char)('a' + rng() % 26);
+        std::string esc = "prefix";  // appends after existing content
+        json::EscapeString(raw, &esc);
+        ASSERT_EQ(esc.compare(0, 6, "prefix"), 0);
+        json::Value v;
+        ASSERT_TRUE(json::Parse(esc.substr(6), &v));
+        EXPECT_EQ(v.as_string(), raw);
+    }
+}
+
 // Host int arrays stay packed (no Value per element); anything that is not
 // a plain int64 turns the array into Values with the same contents.
 TEST(JsonUnit, packed_int_arrays_and_fallbacks) {
