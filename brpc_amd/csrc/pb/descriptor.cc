@@ -35,30 +35,6 @@ const char* FieldTypeName(FieldType t) {
     return "?";
 }
 
-CppType CppTypeOf(FieldType t) {
-    switch (t) {
-    case FieldType::DOUBLE: return CppType::DOUBLE;
-    case FieldType::FLOAT: return CppType::FLOAT;
-    case FieldType::INT64:
-    case FieldType::SFIXED64:
-    case FieldType::SINT64: return CppType::INT64;
-    case FieldType::UINT64:
-    case FieldType::FIXED64: return CppType::UINT64;
-    case FieldType::INT32:
-    case FieldType::SFIXED32:
-    case FieldType::SINT32: return CppType::INT32;
-    case FieldType::UINT32:
-    case FieldType::FIXED32: return CppType::UINT32;
-    case FieldType::BOOL: return CppType::BOOL;
-    case FieldType::ENUM: return CppType::ENUM;
-    case FieldType::STRING:
-    case FieldType::BYTES: return CppType::STRING;
-    case FieldType::GROUP:
-    case FieldType::MESSAGE: return CppType::MESSAGE;
-    }
-    return CppType::INT32;
-}
-
 size_t CppTypeSize(CppType t) {
     switch (t) {
     case CppType::INT32:

@@ -31,7 +31,18 @@ enum class Label : uint8_t { OPTIONAL = 1, REQUIRED = 2, REPEATED = 3 };
 enum class CppType : uint8_t { INT32, INT64, UINT32, UINT64, DOUBLE, FLOAT, BOOL, ENUM, STRING, MESSAGE };
 
 const char* FieldTypeName(FieldType t);
-CppType CppTypeOf(FieldType t);
+// inline: message.cc's reflective serialize / size / parse loops ask it per
+// field (2.6% of the 32 B echo's host samples as an out-of-line call)
+inline CppType CppTypeOf(FieldType t) {
+    static constexpr CppType kMap[19] = {
+        CppType::INT32,  CppType::DOUBLE, CppType::FLOAT,  CppType::INT64,   CppType::UINT64,
+        CppType::INT32,  CppType::UINT64, CppType::UINT32, CppType::BOOL,    CppType::STRING,
+        CppType::MESSAGE, CppType::MESSAGE, CppType::STRING, CppType::UINT32, CppType::ENUM,
+        CppType::INT32,  CppType::INT64,  CppType::INT32,  CppType::INT64,
+    };
+    const unsigned i = (unsigned)t;
+    return i < 19 ? kMap[i] : CppType::INT32;
+}
 size_t CppTypeSize(CppType t);   // storage size of a singular field
 size_t CppTypeAlign(CppType t);
 
