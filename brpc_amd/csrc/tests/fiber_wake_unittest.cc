@@ -268,10 +268,14 @@ TEST(FiberWake, many_fibers_wait_on_their_own_pipes) {
 }
 
 TEST(FiberWake, timers_fire_in_deadline_order_and_delete_semantics) {
-    static std::atomic<int> seq{0};
+    static std::atomic<int> seq{0}, done{0};
     static int order[3];
     seq = 0;
-    auto rec = [](void* a) { order[seq.fetch_add(1)] = (int)(intptr_t)a; };
+    done = 0;
+    auto rec = [](void* a) {
+        order[seq.fetch_add(1)] = (int)(intptr_t)a;
+        done.fetch_add(1, std::memory_order_release);  // the slot is written before it counts
+    };
     TimerId t30, t10, t20, never;
     (void)t30;
     (void)t20;
@@ -281,8 +285,8 @@ TEST(FiberWake, timers_fire_in_deadline_order_and_delete_semantics) {
     ASSERT_EQ(timer_add_us(&never, 5000000, rec, (void*)99), 0);
     EXPECT_EQ(timer_del(never), 0);  // removed before it ran
     const int64_t end = monotonic_us() + 2000000;
-    while (seq.load() < 3 && monotonic_us() < end) ::usleep(1000);
-    ASSERT_EQ(seq.load(), 3);
+    while (done.load(std::memory_order_acquire) < 3 && monotonic_us() < end) ::usleep(1000);
+    ASSERT_EQ(done.load(std::memory_order_acquire), 3);
     EXPECT_EQ(order[0], 10);
     EXPECT_EQ(order[1], 20);
     EXPECT_EQ(order[2], 30);
