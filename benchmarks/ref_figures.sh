@@ -17,3 +17,7 @@ run "16B pooled, 50 pthreads" --thread_num 50 --request_size 16 --connection_typ
 run "32KB single, 50 pthreads" --thread_num 50 --request_size 32768 --connection_type single
 run "32KB pooled, 50 pthreads" --thread_num 50 --request_size 32768 --connection_type pooled
 run "32B single, 400 fibers" --thread_num 400 --use_fiber --request_size 32 --connection_type single
+# memcache client against the example's in-process binary-protocol server
+# (the reference measured against memcached 1.4.15: 90k single connection)
+echo -n "memcache GETs, batches of 10, 1 thread: "; timeout -k 10 60 build/bin/memcache_main --thread_num 1 --duration_s 2 2>/dev/null | grep "^load:" || exit 1
+echo -n "memcache GETs, batches of 10, 4 threads: "; timeout -k 10 60 build/bin/memcache_main --thread_num 4 --duration_s 2 2>/dev/null | grep "^load:" || exit 1

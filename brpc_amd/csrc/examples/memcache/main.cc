@@ -7,6 +7,7 @@
 // empty.
 #include <arpa/inet.h>
 #include <netinet/in.h>
+#include <netinet/tcp.h>
 #include <sys/socket.h>
 
 #include <algorithm>
@@ -21,7 +22,7 @@
 #include "redis/memcache.h"
 
 DEFINE_string(server, "", "memcached ip:port (empty: start the in-process one)");
-DEFINE_int32(batch, 100, "operations per pipelined request");
+DEFINE_int32(batch, 100, "operations per pipelined request (>= 3: the checks append to key_1 and delete key_2)");
 DEFINE_int32(thread_num, 4, "threads of the load phase");
 DEFINE_double(duration_s, 0.5, "seconds of the load phase");
 
@@ -95,6 +96,11 @@ private:
         for (;;) {
             const int fd = accept(_lfd, nullptr, nullptr);
             if (fd < 0) return;
+            // one write per response: without NODELAY, Nagle holds every
+            // response after the first of a pipelined batch until the
+            // client's delayed ACK (~30 ms per batch of 10 GETs)
+            const int one = 1;
+            setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
             {
                 std::lock_guard<std::mutex> g(_mu);
                 _fds.push_back(fd);
