@@ -21,3 +21,10 @@ run "32B single, 400 fibers" --thread_num 400 --use_fiber --request_size 32 --co
 # (the reference measured against memcached 1.4.15: 90k single connection)
 echo -n "memcache GETs, batches of 10, 1 thread: "; timeout -k 10 60 build/bin/memcache_main --thread_num 1 --duration_s 2 2>/dev/null | grep "^load:" || exit 1
 echo -n "memcache GETs, batches of 10, 4 threads: "; timeout -k 10 60 build/bin/memcache_main --thread_num 4 --duration_s 2 2>/dev/null | grep "^load:" || exit 1
+# redis client against the framework's own RedisService (the reference
+# measured against redis-server: batches of 10 from 1 / 50 / 200 bthreads
+# ~16.9k / 38k / 29k QPS single connection, 75.6k pooled with 50)
+for t in 1 50 200; do
+  echo -n "redis GET batches of 10, $t fibers, single: "; timeout -k 10 60 build/bin/redis_kv_main --thread_num $t --duration_s 2 2>/dev/null | grep "^load:" || exit 1
+done
+echo -n "redis GET batches of 10, 50 fibers, pooled: "; timeout -k 10 60 build/bin/redis_kv_main --thread_num 50 --connection_type pooled --duration_s 2 2>/dev/null | grep "^load:" || exit 1
