@@ -16,11 +16,19 @@
 
 #include <atomic>
 #include <thread>
+#include <vector>
+
+#include "base/time.h"
+#include "fiber/fiber.h"
 
 #include "examples/common.h"
 #include "thrift/thrift.h"
 
 using mrpc::thrift::Value;
+
+DEFINE_int32(thread_num, 0, "load phase: fibers echoing \"hello\" through the framework client (0: none)");
+DEFINE_int32(repeat, 1, "load phase: the string is \"hello\" repeated this many times (the reference: 1 and 1000)");
+DEFINE_double(duration_s, 1.0, "load phase: seconds");
 
 namespace {
 
@@ -212,6 +220,42 @@ int main(int argc, char** argv) {
                     res.success()->find(1)->as_string() == "native:" + std::to_string(i);
     }
     printf("framework client -> native server: %s\n", to_native ? "ok" : "FAILED");
+
+    // 4) load: the reference's thrift figure (docs/en/thrift.md) echoes
+    // "hello" (and "hello" x 1000) from 60 threads
+    if (FLAGS_thread_num > 0 && ok) {
+        std::string hello;
+        for (int i = 0; i < FLAGS_repeat; ++i) hello += "hello";
+        std::atomic<bool> stop{false};
+        std::atomic<int64_t> n{0}, errors{0}, lat_sum{0};
+        std::vector<mrpc::fiber::fiber_t> fs(FLAGS_thread_num);
+        for (auto& f : fs) {
+            mrpc::fiber::start(
+                [&] {
+                    while (!stop.load(std::memory_order_relaxed)) {
+                        mrpc::ThriftFramedMessage req, res;
+                        mrpc::Controller cntl;
+                        req.method_name = "Echo";
+                        req.body = MakeArgs(hello);
+                        ch.CallMethod(nullptr, &cntl, &req, &res, nullptr);
+                        if (cntl.Failed() || !res.success()) {
+                            errors.fetch_add(1);
+                        } else {
+                            n.fetch_add(1);
+                            lat_sum.fetch_add(cntl.latency_us());
+                        }
+                    }
+                },
+                false, nullptr, &f);
+        }
+        mrpc::fiber::usleep((uint64_t)(FLAGS_duration_s * 1e6));
+        stop = true;
+        for (auto f : fs) mrpc::fiber::join(f);
+        printf("load: %lld QPS, avg %lld us, \"hello\" x %d, %d fibers, %lld failed calls\n",
+               (long long)(n.load() / FLAGS_duration_s), n.load() ? (long long)(lat_sum.load() / n.load()) : 0ll,
+               FLAGS_repeat, FLAGS_thread_num, (long long)errors.load());
+        ok = errors.load() == 0 && n.load() > 0;
+    }
     server.Stop(0);
     server.Join();
     return demo::Check(ok && native_ok && to_native, "framed thrift interop");
