@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "base/time.h"
+#include "builtin/cpu_profiler.h"
 #include "fiber/fiber.h"
 
 #include "examples/common.h"
@@ -29,6 +30,7 @@ using mrpc::thrift::Value;
 DEFINE_int32(thread_num, 0, "load phase: fibers echoing \"hello\" through the framework client (0: none)");
 DEFINE_int32(repeat, 1, "load phase: the string is \"hello\" repeated this many times (the reference: 1 and 1000)");
 DEFINE_double(duration_s, 1.0, "load phase: seconds");
+DEFINE_string(profile_folded, "", "load phase: write a CPU profile (folded stacks) to this file");
 
 namespace {
 
@@ -248,7 +250,17 @@ int main(int argc, char** argv) {
                 },
                 false, nullptr, &f);
         }
-        mrpc::fiber::usleep((uint64_t)(FLAGS_duration_s * 1e6));
+        if (!FLAGS_profile_folded.empty()) {
+            std::string folded;
+            int64_t nsamples = 0;
+            mrpc::profiler::ProfileCpu(FLAGS_duration_s, 997, &folded, nullptr, &nsamples);
+            if (FILE* pf = fopen(FLAGS_profile_folded.c_str(), "w")) {
+                fwrite(folded.data(), 1, folded.size(), pf);
+                fclose(pf);
+            }
+        } else {
+            mrpc::fiber::usleep((uint64_t)(FLAGS_duration_s * 1e6));
+        }
         stop = true;
         for (auto f : fs) mrpc::fiber::join(f);
         printf("load: %lld QPS, avg %lld us, \"hello\" x %d, %d fibers, %lld failed calls\n",
