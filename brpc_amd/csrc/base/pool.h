@@ -9,6 +9,7 @@
 // free-list allocator (butil::ObjectPool).
 #pragma once
 
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
@@ -144,33 +145,37 @@ public:
         static ObjectPool* p = new ObjectPool;
         return p;
     }
+    // Objects move between a thread's cache and the global list kBatch at
+    // a time: a thread that only gets (a socket's reader cutting messages)
+    // and threads that only put (the workers that ran them) would otherwise
+    // take the global mutex once per object each (~1% of the 32 B echo's
+    // host samples in MostCommonMessage::Get alone).
+    static constexpr size_t kBatch = kLocalMax / 2;
     T* get() {
         Local& l = local();
+        if (l.items.empty()) {
+            std::lock_guard<std::mutex> g(_mu);
+            const size_t n = std::min(kBatch, _global.size());
+            l.items.insert(l.items.end(), _global.end() - n, _global.end());
+            _global.resize(_global.size() - n);
+        }
         if (!l.items.empty()) {
             T* t = l.items.back();
             l.items.pop_back();
             MRPC_TSAN_ACQUIRE(t);
             return t;
         }
-        {
-            std::lock_guard<std::mutex> g(_mu);
-            if (!_global.empty()) {
-                T* t = _global.back();
-                _global.pop_back();
-                return t;
-            }
-        }
         return new T;
     }
     void put(T* t) {
         MRPC_TSAN_RELEASE(t);
         Local& l = local();
-        if (l.items.size() < kLocalMax) {
-            l.items.push_back(t);
-            return;
+        if (l.items.size() >= kLocalMax) {
+            std::lock_guard<std::mutex> g(_mu);
+            _global.insert(_global.end(), l.items.end() - kBatch, l.items.end());
+            l.items.resize(l.items.size() - kBatch);
         }
-        std::lock_guard<std::mutex> g(_mu);
-        _global.push_back(t);
+        l.items.push_back(t);
     }
 private:
     struct Local {

@@ -246,3 +246,54 @@ TEST(PoolObject, concurrent_threads_never_share_an_object) {
     for (auto& t : ts) t.join();
     EXPECT_EQ(conflicts.load(), 0);
 }
+
+// A thread that only gets and a thread that only puts (a socket reader and
+// the worker that ran its message): objects cross in batches through the
+// global list, none is handed out twice, and recycling keeps the number
+// ever constructed bounded by what is in flight plus the two caches.
+namespace {
+struct OpF {
+    static std::atomic<int> constructed;
+    std::atomic<int> live{0};
+    OpF() { constructed.fetch_add(1); }
+};
+std::atomic<int> OpF::constructed{0};
+}  // namespace
+
+TEST(PoolObject, getter_and_putter_threads_recycle_in_batches) {
+    const int kN = 20000, kInFlight = 100;
+    std::vector<std::atomic<OpF*>> slots(kInFlight);
+    for (auto& s : slots) s.store(nullptr);
+    std::atomic<int> dup{0}, got{0};
+    std::atomic<bool> done{false};
+    std::thread getter([&] {
+        for (int i = 0; i < kN; ++i) {
+            OpF* p = get_object<OpF>();
+            if (p->live.exchange(1) != 0) dup.fetch_add(1);
+            std::atomic<OpF*>& s = slots[i % kInFlight];
+            while (s.load(std::memory_order_acquire) != nullptr) std::this_thread::yield();
+            s.store(p, std::memory_order_release);
+            got.fetch_add(1);
+        }
+        done = true;
+    });
+    std::thread putter([&] {
+        int put = 0;
+        while (put < kN) {
+            for (auto& s : slots) {
+                OpF* p = s.load(std::memory_order_acquire);
+                if (!p) continue;
+                s.store(nullptr, std::memory_order_release);
+                p->live.store(0);
+                return_object<OpF>(p);
+                ++put;
+            }
+        }
+    });
+    getter.join();
+    putter.join();
+    EXPECT_EQ(got.load(), kN);
+    EXPECT_EQ(dup.load(), 0);
+    // in flight + the putter's cache + a batch on its way: far below kN
+    EXPECT_TRUE(OpF::constructed.load() <= kInFlight + 2 * (int)ObjectPool<OpF>::kLocalMax + 1);
+}
