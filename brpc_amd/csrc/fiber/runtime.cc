@@ -357,7 +357,7 @@ void TaskGroup::task_runner(void*) {
     g->run_remained();
     do {
         TaskMeta* m = g->_cur_meta;
-        m->start_ns = monotonic_ns();
+        m->start_ns = monotonic_coarse_ns();  // only the /fibers age (ms)
         if (!m->stop) {
             m->fn(m->arg);
         }

@@ -258,7 +258,7 @@ void Channel::CallMethod(const pb::MethodDescriptor* method, RpcController* cont
         fiber::timer_add_us(&cntl->_backup_id, cntl->_backup_request_ms * 1000, HandleBackupRequest,
                             (void*)(uintptr_t)cid.value);
     }
-    cntl->IssueRPC(start_real_us);
+    cntl->IssueRPC(cntl->_begin_us);  // the first try starts with the call
     if (!done) fiber::call_id_join(cid);
 }
 

@@ -259,7 +259,7 @@ int Controller::HandleError(fiber::CallId id, void* data, int error_code, const 
         c->_accessed->Add(c->_current_call.peer_id);
         ++c->_nretry;
         c->_has_backup = true;
-        c->IssueRPC(realtime_us());
+        c->IssueRPC(monotonic_us());
         return 0;
     }
     if (id != c->_current_call.id && id != c->_unfinished_call.id) {
@@ -299,7 +299,7 @@ void Controller::OnVersionedRPCReturned(fiber::CallId id, int error_code) {
         ++_nretry;
         _error_code = 0;
         _error_text.clear();
-        IssueRPC(realtime_us());
+        IssueRPC(monotonic_us());
         return;
     }
     EndRPC(id);
@@ -368,12 +368,11 @@ void Controller::EndRPC(fiber::CallId id) {
     if (done) done->Run();
 }
 
-void Controller::IssueRPC(int64_t start_realtime_us) {
-    (void)start_realtime_us;
+void Controller::IssueRPC(int64_t begin_us) {
     const fiber::CallId cid = fiber::call_id_with_version(_correlation_id, 1 + _nretry);
     _current_call.Reset();
     _current_call.id = cid;
-    _current_call.begin_us = monotonic_us();
+    _current_call.begin_us = begin_us;
     SocketUniquePtr tmp;
     if (_single_server_id != INVALID_SOCKET_ID) {
         if (Socket::Address(_single_server_id, &tmp) != 0) {

@@ -314,7 +314,7 @@ public:
     std::function<void(Controller*)> _on_end;
 
     // Engine
-    void IssueRPC(int64_t start_realtime_us);
+    void IssueRPC(int64_t begin_us);  // begin_us: monotonic start of this try
     // Called with the correlation id locked. error_code==0 means a response
     // for attempt `id` has been parsed into _response.
     void OnVersionedRPCReturned(fiber::CallId id, int error_code);
