@@ -892,7 +892,24 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
     const uint32_t seg = (ulen + kWave - 1) / kWave;
     const uint32_t s = min(ulen, seg * (uint32_t)lane);
     const uint32_t e = min(ulen, s + seg);
-    {
+    if (kCand) {
+        // 32 positions per LDS round trip: the chunk's 9 words are read
+        // together, then its atomics issue back to back (an LDS read between
+        // them would wait for every atomic issued before it: a round trip per
+        // 4 positions). Reads may run 35 bytes past the block (the slots
+        // follow it in LDS; those positions are masked).
+        for (uint32_t qb = s & ~3u; qb < e; qb += 32) {
+            uint32_t w[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) w[i] = dw((qb >> 2) + (uint32_t)i);
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                const uint32_t q = qb + (uint32_t)i;
+                const uint32_t v = __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], (uint32_t)(i & 3));
+                if (q >= s && q < e && q + 4 <= ulen) atomicMin(&first_pos[(v * 0x1e35a7bdu) >> (32 - kFB)], q);
+            }
+        }
+    } else {
         // an 8-byte window of the segment in registers, refilled every 4
         // positions: the atomics issue back to back instead of each waiting
         // on its own LDS read
@@ -914,19 +931,28 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
     __attribute__((address_space(3))) uint16_t* const mc =
         (__attribute__((address_space(3))) uint16_t*)(in + in_bytes + (kOutLds ? kWave * slot_bytes : 0));
     if (kCand) {
-        for (uint32_t qb = s & ~3u; qb < e; qb += 4) {
-            const uint32_t w0 = dw(qb >> 2), w1 = dw((qb >> 2) + 1);
-            uint32_t c[4];
+        // three round trips per 16 positions (words; table entries;
+        // candidate bytes), not three per 4 (16, not 32: register arrays of
+        // 32 took the kernel from 84 to 206 VGPRs)
+        for (uint32_t qb = s & ~3u; qb < e; qb += 16) {
+            uint32_t w[5], c[16], x[16];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)i);
+            for (int i = 0; i < 5; ++i) w[i] = dw((qb >> 2) + (uint32_t)i);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t v = __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], (uint32_t)(i & 3));
                 c[i] = first_pos[(v * 0x1e35a7bdu) >> (32 - kFB)];
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            for (int i = 0; i < 16; ++i) {
                 const uint32_t q = qb + (uint32_t)i;
-                const uint32_t v = __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)i);
-                const bool ok = c[i] < q && q + 4 <= ulen && rd32(c[i] < q ? c[i] : 0u) == v;
+                x[i] = rd32(c[i] < q ? c[i] : 0u);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint32_t q = qb + (uint32_t)i;
+                const uint32_t v = __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], (uint32_t)(i & 3));
+                const bool ok = c[i] < q && q + 4 <= ulen && x[i] == v;
                 if (q >= s && q < e) mc[q] = ok ? (uint16_t)c[i] : kNoPos;
             }
         }
