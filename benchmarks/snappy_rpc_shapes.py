@@ -172,6 +172,8 @@ def main():
                 # shader-clock cycles per phase of block 0
                 names = ("stage", "first_pos", "match", "write")
                 phases = {k: t[i + 1] - t[i] for i, k in enumerate(names)}
+                phases.update({"walk_iters_wave": t[5], "walk_iters_lane_mean": round(t[6] / 64, 1),
+                               "walk_matches_lane_mean": round(t[7] / 64, 1)})
                 print(json.dumps({"kernel": "snappy_compress", "body": kind, "flags": a.flag, "src": src_at, "dst": dst_at,
                                   "block0_phase_cycles": phases,
                                   "blocks": npieces, "bytes_in": total,

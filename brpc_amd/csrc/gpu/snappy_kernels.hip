@@ -997,6 +997,7 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
     }
     stamp(stamps, blk, lane, 2);
     uint16_t* ht = table + (kCand ? 0 : lane * kHashEntries);
+    uint32_t walk_iters = 0, walk_hits = 0;  // phase stamps only
     auto match = [&](auto o0) {
         auto o = o0;
         // Literal bytes are not copied inside the walk: their tags are
@@ -1020,6 +1021,7 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
             uint32_t cb = 0xFFFFFFFFu;
             uint64_t cw = 0;
             while (p + 4 <= e) {
+                ++walk_iters;
                 if ((p >> 2) != cb) {  // four candidates per LDS read
                     cb = p >> 2;
                     cw = *(const __attribute__((address_space(3))) uint64_t*)(mc + (cb << 2));
@@ -1037,6 +1039,7 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
                         len += 8;
                     }
                     len = min(len, e - p);
+                    ++walk_hits;
                     if (p > lit) o = literal(o, lit, p - lit);
                     o = emit_copy(o, p - cand, len);
                     p += len;
@@ -1128,6 +1131,17 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
     }
     __syncthreads();
     stamp(stamps, blk, lane, 3);
+    if (stamps && blk == 0) {
+        // walk iterations: the wave's (its slowest lane's) and the lanes'
+        // sum; matches: the lanes' sum
+        const uint32_t it_max = wave_max(walk_iters), it_sum = wave_incl_sum(walk_iters);
+        const uint32_t hit_sum = wave_incl_sum(walk_hits);
+        if (lane == kWave - 1) {
+            stamps[5] = it_max;
+            stamps[6] = it_sum;
+            stamps[7] = hit_sum;
+        }
+    }
     // varint header + prefix sum of the 64 slot sizes (DPP scan: lane k
     // holds slot k's size)
     uint32_t hdr = 1;
