@@ -861,6 +861,7 @@ __device__ __forceinline__ O emit_copy(O o, uint32_t off, uint32_t len) {
 // lane's walk then reads four candidates per round trip, so a run of misses
 // costs ALU only; the wave pays round trips where some lane extends a match.
 constexpr uint32_t kCandMax = 8192;
+static_assert(kCandMax / kWave <= 128, "match records hold a slice offset and length in 7 bits each");
 // (Padding the staged input and the candidates so that lanes 64 bytes apart
 // hit distinct LDS banks was measured slower on MI355X: 56 vs 51 us per
 // 112-block launch of text; the layouts stay dense.)
@@ -1018,7 +1019,15 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
         };
         uint32_t p = s, lit = s;
         if (kCand) {
-            uint32_t cb = 0xFFFFFFFFu;
+            // The walk only decides: each match is recorded as two u16 in the
+            // lane's own candidate entries it has already passed (record k at
+            // s + 2k, s + 2k + 1 < p: a match covers >= 4 positions), and a
+            // second loop emits the records. A wave runs every path any lane
+            // takes, so with the emission inside the walk each of the ~29
+            // iterations (the lane over unique bytes misses at every position)
+            // that some lane matched in paid the literal and copy emission
+            // too (~1.2k cycles per iteration, profiles/r6_codec_late.txt).
+            uint32_t cb = 0xFFFFFFFFu, nm = 0;
             uint64_t cw = 0;
             while (p + 4 <= e) {
                 ++walk_iters;
@@ -1040,13 +1049,23 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
                     }
                     len = min(len, e - p);
                     ++walk_hits;
-                    if (p > lit) o = literal(o, lit, p - lit);
-                    o = emit_copy(o, p - cand, len);
+                    // p - s < seg <= 128 and len - 4 < 128: 7 bits each
+                    mc[s + 2 * nm] = (uint16_t)((p - s) | ((len - 4) << 7));
+                    mc[s + 2 * nm + 1] = (uint16_t)(p - cand);
+                    ++nm;
                     p += len;
                     lit = p;
                 } else {
                     p += 1 + ((p - lit) >> 5);
                 }
+            }
+            lit = s;
+            for (uint32_t k = 0; k < nm; ++k) {
+                const uint32_t a = mc[s + 2 * k], off = mc[s + 2 * k + 1];
+                const uint32_t mp = s + (a & 127), mlen = (a >> 7) + 4;
+                if (mp > lit) o = literal(o, lit, mp - lit);
+                o = emit_copy(o, off, mlen);
+                lit = mp + mlen;
             }
         } else {
         // the probe's serial chain is LDS round trips; per position: the
