@@ -487,9 +487,9 @@ __device__ __forceinline__ void decode_piece_wave(const SnappyPiece* __restrict_
             const u32x4s sv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4s*>(strip + 4 * lane);
             uint32_t m0 = sv.x, m1 = max(m0, sv.y), m2 = max(m1, sv.z), m3 = max(m2, sv.w);
             const uint32_t incl = wave_incl_max(m3);
-            // the latest element start of the lanes before this one
-            const uint32_t before = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane ? lane - 1 : 0) << 2), (int)incl);
-            const uint32_t bm = lane ? before : 0u;
+            // the latest element start of the lanes before this one: DPP
+            // wave_shr:1 (lane 0 reads 0), no LDS round trip
+            const uint32_t bm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xf, 0xf, false);
             m0 = max(m0, bm);
             m1 = max(m1, bm);
             m2 = max(m2, bm);
