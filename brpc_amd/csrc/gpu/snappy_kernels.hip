@@ -372,14 +372,16 @@ __device__ __forceinline__ void decode_piece_wave(const SnappyPiece* __restrict_
     lbyte* const cin = (lbyte*)lds;
     __attribute__((address_space(3))) uint16_t* const smap =
         (__attribute__((address_space(3))) uint16_t*)(lds + cin_cap);
-    // 256 slots of per-pass element starts, after the map
-    __attribute__((address_space(3))) uint32_t* const strip =
+    // a bit per output position: an element starts there (256 words, up
+    // to kParMax positions), after the map
+    __attribute__((address_space(3))) uint32_t* const starts =
         (__attribute__((address_space(3))) uint32_t*)(lds + cin_cap + 2 * ((hi + 7) & ~7u));
     {
         gbyte_c* g = as_global(static_cast<const uint8_t*>(pc.src) - mis);
         for (uint32_t o = lane * 16; o < end; o += kWave * 16)
             *reinterpret_cast<__attribute__((address_space(3))) u32x4*>(cin + o) =
                 *reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(g + o);
+        for (uint32_t i = lane; i < (ulen + 31) / 32; i += kWave) starts[i] = 0;
     }
     __syncthreads();
     stamp(stamps, blk, lane, 1);
@@ -387,7 +389,7 @@ __device__ __forceinline__ void decode_piece_wave(const SnappyPiece* __restrict_
     // ---- 1. parse + source map
     uint32_t ip = mis, upos = 0;
     int bad = 0;
-    uint64_t t_dec = 0, t_chain = 0, t_fill = 0, t_iter = 0;  // phase stamps only
+    uint64_t t_dec = 0, t_chain = 0, t_iter = 0;  // phase stamps only
     while (ip < end) {
         const uint64_t ta = stamps ? __builtin_amdgcn_s_memtime() : 0;
         const uint32_t q = ip + (uint32_t)lane;
@@ -458,74 +460,77 @@ __device__ __forceinline__ void decode_piece_wave(const SnappyPiece* __restrict_
             bad = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(eb));
             break;
         }
-        // source map, one output byte per lane: the iteration's output span
-        // in passes of 64 positions. Element starts are scattered into a
-        // 64-slot LDS strip, an inclusive DPP max-scan hands every lane the
-        // latest element that started at or before its position (or the
-        // carry from the previous pass), and one bpermute fetches that
-        // element's (u0, base). Cost per 64 output bytes, whatever the
-        // element lengths.
+        // the element's source at its first output byte, and its start bit;
+        // the source map is filled in one pass after the parse
         const uint32_t base = kind == 0 ? (kLitFlag | (q + hdr)) : (u0 - off);
-        const uint64_t td = stamps ? __builtin_amdgcn_s_memtime() : 0;
-        const uint32_t info = (u0 & 0xffff) | (base << 16);
+        if (marked) {
+            smap[u0] = (uint16_t)base;
+            atomicOr((unsigned int*)(starts + (u0 >> 5)), 1u << (u0 & 31));
+        }
         const uint32_t span_end =
             (uint32_t)__builtin_amdgcn_readlane((int)(u0 + len), (int)(63 - __builtin_clzll(mask)));
-        uint32_t carry = 0;
-        // 256 positions per pass, four consecutive ones per lane: one
-        // barrier and one wave max-scan per pass, and the lane's four
-        // bpermutes issue back to back (one position per lane per pass was
-        // ~600 cycles of LDS round trips per 64 output bytes, a third of a
-        // 2 KiB piece's decode)
-        typedef unsigned int u32x4s __attribute__((ext_vector_type(4)));
-        for (uint32_t P = upos; P < span_end; P += 4 * kWave) {
-            *reinterpret_cast<__attribute__((address_space(3))) u32x4s*>(strip + 4 * lane) = u32x4s{0, 0, 0, 0};
-            if (marked && u0 >= P && u0 < P + 4 * kWave) strip[u0 - P] = (uint32_t)lane + 1;
-            // other lanes' stores: without the barrier the compiler may
-            // forward this lane's own zeros (one wave: s_barrier is free, and
-            // DS operations of a wave complete in order)
-            __syncthreads();
-            const u32x4s sv = *reinterpret_cast<const __attribute__((address_space(3))) u32x4s*>(strip + 4 * lane);
-            uint32_t m0 = sv.x, m1 = max(m0, sv.y), m2 = max(m1, sv.z), m3 = max(m2, sv.w);
-            const uint32_t incl = wave_incl_max(m3);
-            // the latest element start of the lanes before this one: DPP
-            // wave_shr:1 (lane 0 reads 0), no LDS round trip
-            const uint32_t bm = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xf, 0xf, false);
-            m0 = max(m0, bm);
-            m1 = max(m1, bm);
-            m2 = max(m2, bm);
-            m3 = max(m3, bm);
-            const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m0 ? m0 - 1 : 0) << 2), (int)info);
-            const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m1 ? m1 - 1 : 0) << 2), (int)info);
-            const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m2 ? m2 - 1 : 0) << 2), (int)info);
-            const uint32_t g3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((m3 ? m3 - 1 : 0) << 2), (int)info);
-            const uint32_t e0 = m0 ? g0 : carry, e1 = m1 ? g1 : carry, e2 = m2 ? g2 : carry, e3 = m3 ? g3 : carry;
-            const uint32_t pos = P + 4u * (uint32_t)lane;
-            if (pos < span_end) smap[pos] = (uint16_t)((e0 >> 16) + (pos - (e0 & 0xffff)));
-            if (pos + 1 < span_end) smap[pos + 1] = (uint16_t)((e1 >> 16) + (pos + 1 - (e1 & 0xffff)));
-            if (pos + 2 < span_end) smap[pos + 2] = (uint16_t)((e2 >> 16) + (pos + 2 - (e2 & 0xffff)));
-            if (pos + 3 < span_end) smap[pos + 3] = (uint16_t)((e3 >> 16) + (pos + 3 - (e3 & 0xffff)));
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)e3, 63);
-        }
         upos = span_end;
         ip += p;
         if (stamps) {
-            const uint64_t te = __builtin_amdgcn_s_memtime();
             t_dec += tb - ta;
             t_chain += tc - tb;
-            t_fill += te - td;
             t_iter += 1;
         }
     }
     if (stamps && blk == 0 && lane == 0) {
         stamps[5] = t_dec;
         stamps[6] = t_chain;
-        stamps[7] = t_fill;
         stamps[9] = t_iter;
     }
     if (!bad && (ip != end || upos != ulen)) bad = 7;
     if (bad) {
         if (lane == 0) err[blk] = bad;
         return;
+    }
+    __syncthreads();
+    // source map, four consecutive positions per lane, 256 per pass: a
+    // position's element is the latest start at or before it (the lane's own
+    // start bits, then a DPP max-scan over the lanes before it and the carry
+    // from the previous pass), its source the element's first-byte source
+    // plus the distance (start entries keep their value, so the pass reads
+    // and rewrites the map in place). One pass per 256 output bytes over the
+    // whole piece; it was one per parse iteration (~150 bytes each) with a
+    // scatter, a barrier and two bpermute round trips.
+    {
+        const uint64_t tf = stamps ? __builtin_amdgcn_s_memtime() : 0;
+        uint32_t carry = 0;
+        for (uint32_t P = 0; P < ulen; P += 4 * kWave) {
+            const uint32_t pos = P + 4u * (uint32_t)lane;
+            const uint32_t bits = pos < ulen ? (starts[pos >> 5] >> (pos & 31)) & 0xFu : 0u;
+            uint32_t l[4];
+            l[0] = (bits & 1) ? pos + 1 : 0u;
+            l[1] = (bits & 2) ? pos + 2 : l[0];
+            l[2] = (bits & 4) ? pos + 3 : l[1];
+            l[3] = (bits & 8) ? pos + 4 : l[2];
+            const uint32_t incl = wave_incl_max(l[3]);
+            const uint32_t before =
+                max(carry, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xf, 0xf, false));
+            uint32_t u[4], b[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) u[k] = max(before, l[k]) - 1;  // position 0 always starts an element
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[k] = smap[u[k]];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) b[k] = (b[k] + (pos + (uint32_t)k - u[k])) & 0xffff;
+            if (pos + 4 <= ulen) {
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                u32x2 v;
+                v[0] = b[0] | (b[1] << 16);
+                v[1] = b[2] | (b[3] << 16);
+                *reinterpret_cast<__attribute__((address_space(3))) u32x2*>(smap + pos) = v;
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (pos + (uint32_t)k < ulen) smap[pos + k] = (uint16_t)b[k];
+            }
+            carry = max(carry, (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1));
+        }
+        if (stamps && blk == 0 && lane == 0) stamps[7] = __builtin_amdgcn_s_memtime() - tf;
     }
     __syncthreads();
     stamp(stamps, blk, lane, 2);
