@@ -163,7 +163,7 @@ def main():
                 ok = not any(errs) and all(
                     native.snappy_uncompress(sl[i * cap:i * cap + lens[i]]) == raw[i * blk:(i + 1) * blk]
                     for i in range(0, npieces, 7))
-                stamps = torch.zeros(8, dtype=torch.int64, device=dev)
+                stamps = torch.zeros(16, dtype=torch.int64, device=dev)
                 native.gpu.snappy_compress_stamped_launch(cj_dev.data_ptr(), npieces, blk, scratch.data_ptr(),
                                                           meta.data_ptr(), meta.data_ptr() + 4 * npieces,
                                                           stamps.data_ptr(), st)
@@ -172,7 +172,7 @@ def main():
                 # shader-clock cycles per phase of block 0
                 names = ("stage", "first_pos", "match", "write")
                 phases = {k: t[i + 1] - t[i] for i, k in enumerate(names)}
-                phases.update({"walk_iters_wave": t[5], "walk_iters_lane_mean": round(t[6] / 64, 1),
+                phases.update({"first_pos_atomics": t[8] - t[1], "walk_iters_wave": t[5], "walk_iters_lane_mean": round(t[6] / 64, 1),
                                "walk_matches_lane_mean": round(t[7] / 64, 1)})
                 print(json.dumps({"kernel": "snappy_compress", "body": kind, "flags": a.flag, "src": src_at, "dst": dst_at,
                                   "block0_phase_cycles": phases,

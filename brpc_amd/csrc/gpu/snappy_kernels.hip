@@ -970,6 +970,7 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
         }
     }
     __syncthreads();
+    if (stamps && blk == 0 && lane == 0) stamps[8] = __builtin_amdgcn_s_memtime();  // atomics done
     // candidates (kCand): u16 per position after the output slots; a lane
     // writes and reads only its own segment's entries (no barrier needed)
     __attribute__((address_space(3))) uint16_t* const mc =
@@ -992,12 +993,28 @@ __device__ __forceinline__ void compress_wave(const SnappyJob* __restrict__ jobs
                 const uint32_t q = qb + (uint32_t)i;
                 x[i] = rd32(c[i] < q ? c[i] : 0u);
             }
+            uint32_t mv[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const uint32_t q = qb + (uint32_t)i;
                 const uint32_t v = __builtin_amdgcn_alignbyte(w[(i >> 2) + 1], w[i >> 2], (uint32_t)(i & 3));
                 const bool ok = c[i] < q && q + 4 <= ulen && x[i] == v;
-                if (q >= s && q < e) mc[q] = ok ? (uint16_t)c[i] : kNoPos;
+                mv[i] = ok ? c[i] : kNoPos;
+            }
+            if (qb >= s && qb + 16 <= e) {
+                // the whole chunk is the lane's: four 8-byte stores (qb is a
+                // multiple of 4), not 16 guarded 2-byte ones
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    *(__attribute__((address_space(3))) uint64_t*)(mc + qb + 4 * j) =
+                        (uint64_t)mv[4 * j] | ((uint64_t)mv[4 * j + 1] << 16) | ((uint64_t)mv[4 * j + 2] << 32) |
+                        ((uint64_t)mv[4 * j + 3] << 48);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t q = qb + (uint32_t)i;
+                    if (q >= s && q < e) mc[q] = (uint16_t)mv[i];
+                }
             }
         }
     }
